@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""bench.py — x264 motion-search / transform kernels on MI355X.
+
+Metric (BASELINE.json): SAD+SATD candidate-MVs/sec + DCT+quant blocks/sec, 1080p.
+Workload of the headline `value` (BASELINE.json configs[1]): 1080p synthetic luma,
+full-search integer ME with range 16 (33x33 = 1089 16x16 SAD candidates per MB,
+8160 MBs per frame), one step = one x264hip_8_me_search_full launch over
+`--frames` (fenc, ref) pairs already resident in HBM.  value = candidates/s over
+all ranks.  Side rates of configs[2] (SATD 8x8 candidates, fused 4x4 and 8x8
+DCT+quant blocks) are measured in the same run and reported under "extra".
+
+Multi-GPU: one process per GPU (torchrun), frames are sharded by rank (every
+rank owns its own frame pairs: weak scaling, no data-path collective); the
+barrier + max-over-ranks of the timed region use the default process group.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+from __graft_entry__ import load_package  # noqa: E402
+
+# MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): 256 CUs x 4 SIMD-32 at
+# 2.4 GHz -> 78.6 T VALU lane-ops/s; v_sad_u8 folds 4 byte absdiffs per lane-op.
+VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
+SAD_PEAK_ABSDIFF = 4 * VALU_LANE_OPS          # 314.6 T absdiff/s
+HBM_PEAK = 8.0e12
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=16, help="frame pairs per step per GPU")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--range", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    ap.add_argument("--no-extra", action="store_true", help="skip the configs[2] side rates")
+    ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall-clock bound of the CPU sample")
+    return ap.parse_args()
+
+
+def dist_setup():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(v, world):
+    if world == 1:
+        return v
+    import torch.distributed as dist
+    t = torch.tensor([v], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def timed(fn, steps, warmup, world):
+    """Run warmup, then `steps` timed calls bracketed by barrier + synchronize.
+    Returns (wall seconds max over ranks, mean per-launch event ms on this rank)."""
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for s, e in evs:
+        s.record()
+        fn()
+        e.record()
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    ev_ms = sum(s.elapsed_time(e) for s, e in evs) / steps
+    return max_over_ranks(t1 - t0, world), ev_ms
+
+
+def main():
+    a = parse()
+    world, rank, local = dist_setup()
+    x = load_package()
+    x.init(torch.cuda.current_device())
+    from x264hip import synth
+
+    W, H, R, F = a.width, a.height, a.range, a.frames
+    mbw, mbh = (W + 15) // 16, (H + 15) // 16
+    Hp = mbh * 16                                   # x264 pads the height to whole MBs
+    cand_per_mb = (2 * R + 1) ** 2
+    # F+1 synthetic frames per rank; pair k = (frame k+1, ref frame k); rank-seeded
+    planes, stride, origin = synth.make_sequence(F + 1, W, Hp, 8, seed=1 + rank)
+    dev = torch.from_numpy(planes).cuda()
+    fstride = planes[0].size
+    table = torch.empty((F, mbh, mbw, 2 * R + 1, 2 * R + 1), dtype=torch.int16, device="cuda")
+
+    def step():
+        x.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, table=table,
+                         fenc_frame_stride=fstride, ref_frame_stride=fstride)
+
+    wall, ev_ms = timed(step, a.steps, a.warmup, world)
+    cands = world * a.steps * F * mbw * mbh * cand_per_mb
+    value = cands / wall
+    ms_per_step = wall / a.steps * 1e3
+
+    # roofline of the dominant kernel (me_full_sad16): algorithmic absdiffs per launch
+    absdiff_per_launch = F * mbw * mbh * cand_per_mb * 256
+    achieved = absdiff_per_launch / (ev_ms * 1e-3)
+    roof = {
+        "kernel": "me_full_sad16_kernel<8,%d>" % R,
+        "bound": "valu",
+        "achieved": achieved / 1e12,
+        "peak": SAD_PEAK_ABSDIFF / 1e12,
+        "unit": "T absdiff/s (v_sad_u8 lane-op = 4 absdiff)",
+        "frac": achieved / SAD_PEAK_ABSDIFF,
+        "traffic": None,
+        "algorithmic_bytes_per_launch": F * (mbw * mbh * 256 + mbw * mbh * 256 + mbw * mbh * cand_per_mb * 2),
+        "launch_ms": ev_ms,
+    }
+    pmc = os.path.join(ROOT, "profiles", "pmc_me_full.json")
+    if os.path.exists(pmc):
+        with open(pmc) as fh:
+            d = json.load(fh)
+        if d.get("frames") == F and d.get("range") == R and d.get("width") == W:
+            roof["traffic"] = d.get("hbm_bytes_per_launch")
+
+    out = {
+        "metric": "SAD+SATD candidate-MVs/sec + DCT+quant blocks/sec, 1080p, 1/2/4/8 GPU",
+        "value": value,
+        "unit": "SAD16x16 candidates/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {"workload": "configs[1]: %dx%d luma, full-search ME range %d, sad_16x16 candidate tables, "
+                               "%d frame pairs per GPU per step" % (W, H, R, F),
+                   "frames_per_step_per_gpu": F, "mbs_per_frame": mbw * mbh, "candidates_per_mb": cand_per_mb,
+                   "parallelism": "frame-per-GPU x%d" % world},
+        "roofline": roof,
+    }
+
+    if not a.no_extra:
+        out["extra"] = extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F)
+    if rank == 0 and world == 1 and not a.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(planes, origin, stride, mbw, mbh, R, a.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
+    """configs[2] side rates on the same frames: SATD 8x8 candidates/s and fused
+    DCT+quant blocks/s (QP 26, flat16 CQM, inter-luma lists, zero-MV prediction)."""
+    res = {}
+    flat = [16] * 64
+    q4m, q4b, q8m, q8b = x.cqm_init(8, [flat] * 8)
+    mf4 = torch.from_numpy(q4m[1, 26].copy()).cuda()
+    bs4 = torch.from_numpy(q4b[1, 26].copy()).cuda()
+    mf8 = torch.from_numpy(q8m[1, 26].copy()).cuda()
+    bs8 = torch.from_numpy(q8b[1, 26].copy()).cuda()
+    nmb = F * mbw * mbh
+    dct = torch.empty((nmb, 256), dtype=torch.int16, device="cuda")
+    nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
+    for t, mf, bs in ((4, mf4, bs4), (8, mf8, bs8)):
+        def step(t=t, mf=mf, bs=bs):
+            x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, mf, bs, dct=dct, nz=nz,
+                           fenc_frame_stride=fstride, pred_frame_stride=fstride)
+        wall, ev_ms = timed(step, a.steps, a.warmup, world)
+        blocks = nmb * (16 if t == 4 else 4)
+        bpb = (16 + 16 + 32) if t == 4 else (64 + 64 + 128)     # fenc + pred in, int16 coefs out
+        res["dct%d_quant_blocks_per_s" % t] = world * a.steps * blocks / wall
+        res["dct%d_quant_hbm_frac" % t] = blocks * bpb / (ev_ms * 1e-3) / HBM_PEAK
+        res["dct%d_quant_launch_ms" % t] = ev_ms
+    # SATD 8x8: 9 qpel-neighbourhood-sized candidate sets around the zero MV per 8x8 block
+    # (integer offsets here; the subpel interpolation path is a later kernel)
+    nb = F * mbw * mbh * 4
+    ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
+    base = (ys.ravel() * 8 * stride + xs.ravel() * 8).astype(np.int64)
+    fo, ro = [], []
+    for f in range(F):
+        for dy in (-1, 0, 1):
+            for dx in (-1, 0, 1):
+                fo.append(base + origin + (f + 1) * fstride)
+                ro.append(base + origin + f * fstride + dy * stride + dx)
+    fo = torch.from_numpy(np.concatenate(fo)).cuda()
+    ro = torch.from_numpy(np.concatenate(ro)).cuda()
+    sc = torch.empty(fo.numel(), dtype=torch.int32, device="cuda")
+    flat_dev = dev.view(-1)
+
+    def sstep():
+        x.pixel_cmp_batch(x.CMP_SATD, x.PIXEL_8x8, flat_dev, stride, flat_dev, stride, fo, ro, scores=sc)
+    wall, ev_ms = timed(sstep, a.steps, a.warmup, world)
+    res["satd8x8_candidates_per_s"] = world * a.steps * fo.numel() / wall
+    res["satd8x8_launch_ms"] = ev_ms
+    del nb
+    return res
+
+
+def cpu_baseline(planes, origin, stride, mbw, mbh, R, seconds):
+    """The oracle (kind "port": reference C kernels restated, -O3 -march=x86-64-v3)
+    computing the same full-search tables on the host cores, time-bounded."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib as orc  # cpu_baseline leg only
+    threads = min(16, os.cpu_count() or 1)
+    cand_per_mb = (2 * R + 1) ** 2
+    done = 0
+    t0 = time.perf_counter()
+    k = 0
+    while True:
+        f = 1 + (k % (planes.shape[0] - 1))
+        _, used = orc.me_search_full_mt(planes[f].ravel(), origin, stride, planes[f - 1].ravel(), origin, stride,
+                                        mbw, mbh, R, threads)
+        done += mbw * mbh * cand_per_mb
+        k += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": done / dt, "unit": "SAD16x16 candidates/s", "cores": used, "kind": "port",
+            "sample": "%d full 1080p frames (%d candidates) of the same workload, %d threads, %.1f s wall"
+                      % (k, done, used, dt)}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,338 @@
+/*****************************************************************************
+ * x264hip.h: C ABI of the MI355X (gfx950) backend for x264's pixel / dct /
+ *            quant function tables.
+ *
+ * Two layers, both plain C (no HIP or torch types in any signature):
+ *
+ *  1. Drop-in table initialisers.  The three structs below are
+ *     layout-identical re-declarations of the reference tables
+ *       x264_pixel_function_t  (reference common/pixel.h:78-144)
+ *       x264_dct_function_t    (reference common/dct.h:29-59)
+ *       x264_quant_function_t  (reference common/quant.h:30-70)
+ *     for BIT_DEPTH 8 (pixel=uint8_t, dctcoef=int16_t, udctcoef=uint16_t) and
+ *     BIT_DEPTH 10 (pixel=uint16_t, dctcoef=int32_t, udctcoef=uint32_t),
+ *     reference common/common.h:93-109.  x264hip_{8,10}_*_init() replace
+ *     x264_{8,10}_*_init() (reference common/pixel.c:809, common/dct.c:477,
+ *     common/quant.c:414) for the entries this backend implements; the
+ *     *_init_hip() forms only override, like x264_pixel_init_altivec()
+ *     (reference common/pixel.c:1598-1603).  Every table entry is a
+ *     synchronous call that executes on the GPU (one dispatch per call).
+ *
+ *  2. Batched, device-resident entries (x264hip_{8,10}_*_batch, me_*, mb_*):
+ *     the same kernels over whole frames / block lists already in HBM, on a
+ *     caller-supplied hipStream_t passed as `void *stream` (NULL = default).
+ *     These are where the GPU pays; they return 0 or a negative X264HIP_E*.
+ *
+ * Threading: table entries are reentrant (one HIP stream + staging buffer
+ * per calling thread), as required by x264's frame/slice threads
+ * (reference encoder/encoder.c:1758-1772).
+ *****************************************************************************/
+#ifndef X264HIP_H
+#define X264HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* cpu flag selecting this backend; bits 26-31 are unused by x86
+ * (reference x264.h:139-170). */
+#define X264HIP_CPU_HIP (1U<<26)
+
+/* block-size indices, reference common/pixel.h:37-53 */
+enum
+{
+    X264HIP_PIXEL_16x16 = 0,
+    X264HIP_PIXEL_16x8  = 1,
+    X264HIP_PIXEL_8x16  = 2,
+    X264HIP_PIXEL_8x8   = 3,
+    X264HIP_PIXEL_8x4   = 4,
+    X264HIP_PIXEL_4x8   = 5,
+    X264HIP_PIXEL_4x4   = 6,
+    X264HIP_PIXEL_4x16  = 7,
+};
+
+/* implicit strides of the per-MB caches, reference common/common.h:570-571 */
+#define X264HIP_FENC_STRIDE 16
+#define X264HIP_FDEC_STRIDE 32
+
+/* error codes of the batched entries */
+#define X264HIP_OK          0
+#define X264HIP_EINVAL    (-1)  /* bad size / op / shape */
+#define X264HIP_EDEVICE   (-2)  /* HIP runtime error (see x264hip_last_error) */
+#define X264HIP_ENODEV    (-3)  /* no usable gfx950 device */
+
+/* metric selector of x264hip_*_pixel_cmp_batch */
+enum { X264HIP_CMP_SAD = 0, X264HIP_CMP_SSD = 1, X264HIP_CMP_SATD = 2 };
+
+/* transform selector of x264hip_*_sub_dct_batch (one "block" = one call of
+ * the named reference entry, fenc stride 16 / fdec stride 32 semantics are
+ * replaced by the explicit strides) */
+enum
+{
+    X264HIP_DCT_SUB4x4     = 0,  /* dct.c:145-189, 16 coefs  */
+    X264HIP_DCT_SUB8x8     = 1,  /* dct.c:191-197, 64 coefs  */
+    X264HIP_DCT_SUB16x16   = 2,  /* dct.c:199-205, 256 coefs */
+    X264HIP_DCT_SUB8x8_DC  = 3,  /* dct.c:216-232, 4 coefs   */
+    X264HIP_DCT_SUB8x16_DC = 4,  /* dct.c:234-270, 8 coefs   */
+    X264HIP_DCT_SUB8x8_8   = 5,  /* dct.c:358-377, 64 coefs  */
+    X264HIP_DCT_SUB16x16_8 = 6,  /* dct.c:379-385, 256 coefs */
+};
+
+/* coefficient-domain DC transforms of x264hip_*_dc_batch */
+enum { X264HIP_DC_4x4 = 0 /* dct.c:47-76 */, X264HIP_DC_2x4 = 1 /* dct.c:109-143 */ };
+
+/* quantiser selector of x264hip_*_quant_batch, quant.c:59-104 */
+enum
+{
+    X264HIP_QUANT_8x8   = 0,
+    X264HIP_QUANT_4x4   = 1,
+    X264HIP_QUANT_4x4x4 = 2,
+    X264HIP_QUANT_4x4_DC = 3,
+    X264HIP_QUANT_2x2_DC = 4,
+};
+
+struct x264hip_run_level_t;   /* opaque; only its pointer appears (quant.h:61-63) */
+
+/*----------------------------------------------------------------------------
+ * Table declarations, instantiated per bit depth.
+ *--------------------------------------------------------------------------*/
+#define X264HIP_DECLARE_TABLES( BD, pixel, dctcoef, udctcoef )                                   \
+typedef int  (*x264hip_##BD##_pixel_cmp_t)( pixel *, intptr_t, pixel *, intptr_t );              \
+typedef void (*x264hip_##BD##_pixel_cmp_x3_t)( pixel *, pixel *, pixel *, pixel *, intptr_t, int[3] ); \
+typedef void (*x264hip_##BD##_pixel_cmp_x4_t)( pixel *, pixel *, pixel *, pixel *, pixel *, intptr_t, int[4] ); \
+typedef struct                                                                                  \
+{                                                                                               \
+    x264hip_##BD##_pixel_cmp_t  sad[8];                                                         \
+    x264hip_##BD##_pixel_cmp_t  ssd[8];                                                         \
+    x264hip_##BD##_pixel_cmp_t satd[8];                                                         \
+    x264hip_##BD##_pixel_cmp_t ssim[7];                                                         \
+    x264hip_##BD##_pixel_cmp_t sa8d[4];                                                         \
+    x264hip_##BD##_pixel_cmp_t mbcmp[8];                                                        \
+    x264hip_##BD##_pixel_cmp_t mbcmp_unaligned[8];                                              \
+    x264hip_##BD##_pixel_cmp_t fpelcmp[8];                                                      \
+    x264hip_##BD##_pixel_cmp_x3_t fpelcmp_x3[7];                                                \
+    x264hip_##BD##_pixel_cmp_x4_t fpelcmp_x4[7];                                                \
+    x264hip_##BD##_pixel_cmp_t sad_aligned[8];                                                  \
+    int (*vsad)( pixel *, intptr_t, int );                                                      \
+    int (*asd8)( pixel *pix1, intptr_t stride1, pixel *pix2, intptr_t stride2, int height );    \
+    uint64_t (*sa8d_satd[1])( pixel *pix1, intptr_t stride1, pixel *pix2, intptr_t stride2 );   \
+    uint64_t (*var[4])( pixel *pix, intptr_t stride );                                          \
+    int (*var2[4])( pixel *fenc, pixel *fdec, int ssd[2] );                                     \
+    uint64_t (*hadamard_ac[4])( pixel *pix, intptr_t stride );                                  \
+    void (*ssd_nv12_core)( pixel *pixuv1, intptr_t stride1, pixel *pixuv2, intptr_t stride2,    \
+                           int width, int height, uint64_t *ssd_u, uint64_t *ssd_v );           \
+    void (*ssim_4x4x2_core)( const pixel *pix1, intptr_t stride1,                               \
+                             const pixel *pix2, intptr_t stride2, int sums[2][4] );             \
+    float (*ssim_end4)( int sum0[5][4], int sum1[5][4], int width );                            \
+    x264hip_##BD##_pixel_cmp_x3_t sad_x3[7];                                                    \
+    x264hip_##BD##_pixel_cmp_x4_t sad_x4[7];                                                    \
+    x264hip_##BD##_pixel_cmp_x3_t satd_x3[7];                                                   \
+    x264hip_##BD##_pixel_cmp_x4_t satd_x4[7];                                                   \
+    int (*ads[7])( int enc_dc[4], uint16_t *sums, int delta,                                    \
+                   uint16_t *cost_mvx, int16_t *mvs, int width, int thresh );                   \
+    void (*intra_mbcmp_x3_16x16)( pixel *fenc, pixel *fdec, int res[3] );                       \
+    void (*intra_satd_x3_16x16) ( pixel *fenc, pixel *fdec, int res[3] );                       \
+    void (*intra_sad_x3_16x16)  ( pixel *fenc, pixel *fdec, int res[3] );                       \
+    void (*intra_mbcmp_x3_4x4)  ( pixel *fenc, pixel *fdec, int res[3] );                       \
+    void (*intra_satd_x3_4x4)   ( pixel *fenc, pixel *fdec, int res[3] );                       \
+    void (*intra_sad_x3_4x4)    ( pixel *fenc, pixel *fdec, int res[3] );                       \
+    void (*intra_mbcmp_x3_chroma)( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_satd_x3_chroma) ( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_sad_x3_chroma)  ( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_mbcmp_x3_8x16c) ( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_satd_x3_8x16c)  ( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_sad_x3_8x16c)   ( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_mbcmp_x3_8x8c)  ( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_satd_x3_8x8c)   ( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_sad_x3_8x8c)    ( pixel *fenc, pixel *fdec, int res[3] );                      \
+    void (*intra_mbcmp_x3_8x8)  ( pixel *fenc, pixel edge[36], int res[3] );                    \
+    void (*intra_sa8d_x3_8x8)   ( pixel *fenc, pixel edge[36], int res[3] );                    \
+    void (*intra_sad_x3_8x8)    ( pixel *fenc, pixel edge[36], int res[3] );                    \
+    int (*intra_mbcmp_x9_4x4)( pixel *fenc, pixel *fdec, uint16_t *bitcosts );                  \
+    int (*intra_satd_x9_4x4) ( pixel *fenc, pixel *fdec, uint16_t *bitcosts );                  \
+    int (*intra_sad_x9_4x4)  ( pixel *fenc, pixel *fdec, uint16_t *bitcosts );                  \
+    int (*intra_mbcmp_x9_8x8)( pixel *fenc, pixel *fdec, pixel edge[36], uint16_t *bitcosts, uint16_t *satds ); \
+    int (*intra_sa8d_x9_8x8) ( pixel *fenc, pixel *fdec, pixel edge[36], uint16_t *bitcosts, uint16_t *satds ); \
+    int (*intra_sad_x9_8x8)  ( pixel *fenc, pixel *fdec, pixel edge[36], uint16_t *bitcosts, uint16_t *satds ); \
+} x264hip_##BD##_pixel_function_t;                                                              \
+                                                                                                \
+typedef struct                                                                                  \
+{                                                                                               \
+    void (*sub4x4_dct) ( dctcoef dct[16], pixel *pix1, pixel *pix2 );                           \
+    void (*add4x4_idct)( pixel *p_dst, dctcoef dct[16] );                                       \
+    void (*sub8x8_dct)    ( dctcoef dct[4][16], pixel *pix1, pixel *pix2 );                     \
+    void (*sub8x8_dct_dc) ( dctcoef dct[4], pixel *pix1, pixel *pix2 );                         \
+    void (*add8x8_idct)   ( pixel *p_dst, dctcoef dct[4][16] );                                 \
+    void (*add8x8_idct_dc)( pixel *p_dst, dctcoef dct[4] );                                     \
+    void (*sub8x16_dct_dc)( dctcoef dct[8], pixel *pix1, pixel *pix2 );                         \
+    void (*sub16x16_dct)    ( dctcoef dct[16][16], pixel *pix1, pixel *pix2 );                  \
+    void (*add16x16_idct)   ( pixel *p_dst, dctcoef dct[16][16] );                              \
+    void (*add16x16_idct_dc)( pixel *p_dst, dctcoef dct[16] );                                  \
+    void (*sub8x8_dct8) ( dctcoef dct[64], pixel *pix1, pixel *pix2 );                          \
+    void (*add8x8_idct8)( pixel *p_dst, dctcoef dct[64] );                                      \
+    void (*sub16x16_dct8) ( dctcoef dct[4][64], pixel *pix1, pixel *pix2 );                     \
+    void (*add16x16_idct8)( pixel *p_dst, dctcoef dct[4][64] );                                 \
+    void (*dct4x4dc) ( dctcoef d[16] );                                                         \
+    void (*idct4x4dc)( dctcoef d[16] );                                                         \
+    void (*dct2x4dc)( dctcoef dct[8], dctcoef dct4x4[8][16] );                                  \
+} x264hip_##BD##_dct_function_t;                                                                \
+                                                                                                \
+typedef struct                                                                                  \
+{                                                                                               \
+    int (*quant_8x8)  ( dctcoef dct[64], udctcoef mf[64], udctcoef bias[64] );                  \
+    int (*quant_4x4)  ( dctcoef dct[16], udctcoef mf[16], udctcoef bias[16] );                  \
+    int (*quant_4x4x4)( dctcoef dct[4][16], udctcoef mf[16], udctcoef bias[16] );               \
+    int (*quant_4x4_dc)( dctcoef dct[16], int mf, int bias );                                   \
+    int (*quant_2x2_dc)( dctcoef dct[4], int mf, int bias );                                    \
+    void (*dequant_8x8)( dctcoef dct[64], int dequant_mf[6][64], int i_qp );                    \
+    void (*dequant_4x4)( dctcoef dct[16], int dequant_mf[6][16], int i_qp );                    \
+    void (*dequant_4x4_dc)( dctcoef dct[16], int dequant_mf[6][16], int i_qp );                 \
+    void (*idct_dequant_2x4_dc)( dctcoef dct[8], dctcoef dct4x4[8][16], int dequant_mf[6][16], int i_qp ); \
+    void (*idct_dequant_2x4_dconly)( dctcoef dct[8], int dequant_mf[6][16], int i_qp );         \
+    int (*optimize_chroma_2x2_dc)( dctcoef dct[4], int dequant_mf );                            \
+    int (*optimize_chroma_2x4_dc)( dctcoef dct[8], int dequant_mf );                            \
+    void (*denoise_dct)( dctcoef *dct, uint32_t *sum, udctcoef *offset, int size );             \
+    int (*decimate_score15)( dctcoef *dct );                                                    \
+    int (*decimate_score16)( dctcoef *dct );                                                    \
+    int (*decimate_score64)( dctcoef *dct );                                                    \
+    int (*coeff_last[14])( dctcoef *dct );                                                      \
+    int (*coeff_last4)( dctcoef *dct );                                                         \
+    int (*coeff_last8)( dctcoef *dct );                                                         \
+    int (*coeff_level_run[13])( dctcoef *dct, struct x264hip_run_level_t *runlevel );           \
+    int (*coeff_level_run4)( dctcoef *dct, struct x264hip_run_level_t *runlevel );              \
+    int (*coeff_level_run8)( dctcoef *dct, struct x264hip_run_level_t *runlevel );              \
+    int (*trellis_cabac_4x4)( const int *unquant_mf, const uint8_t *zigzag, int lambda2,        \
+                              int last_nnz, dctcoef *coefs, dctcoef *quant_coefs, dctcoef *dct, \
+                              uint8_t *cabac_state_sig, uint8_t *cabac_state_last,              \
+                              uint64_t level_state0, uint16_t level_state1, int b_ac );         \
+    int (*trellis_cabac_8x8)( const int *unquant_mf, const uint8_t *zigzag, int lambda2,        \
+                              int last_nnz, dctcoef *coefs, dctcoef *quant_coefs, dctcoef *dct, \
+                              uint8_t *cabac_state_sig, uint8_t *cabac_state_last,              \
+                              uint64_t level_state0, uint16_t level_state1, int b_interlaced ); \
+    int (*trellis_cabac_4x4_psy)( const int *unquant_mf, const uint8_t *zigzag, int lambda2,    \
+                              int last_nnz, dctcoef *coefs, dctcoef *quant_coefs, dctcoef *dct, \
+                              uint8_t *cabac_state_sig, uint8_t *cabac_state_last,              \
+                              uint64_t level_state0, uint16_t level_state1, int b_ac,           \
+                              dctcoef *fenc_dct, int psy_trellis );                             \
+    int (*trellis_cabac_8x8_psy)( const int *unquant_mf, const uint8_t *zigzag, int lambda2,    \
+                              int last_nnz, dctcoef *coefs, dctcoef *quant_coefs, dctcoef *dct, \
+                              uint8_t *cabac_state_sig, uint8_t *cabac_state_last,              \
+                              uint64_t level_state0, uint16_t level_state1, int b_interlaced,   \
+                              dctcoef *fenc_dct, int psy_trellis );                             \
+    int (*trellis_cabac_dc)( const int *unquant_mf, const uint8_t *zigzag, int lambda2,         \
+                              int last_nnz, dctcoef *coefs, dctcoef *quant_coefs, dctcoef *dct, \
+                              uint8_t *cabac_state_sig, uint8_t *cabac_state_last,              \
+                              uint64_t level_state0, uint16_t level_state1, int num_coefs );    \
+    int (*trellis_cabac_chroma_422_dc)( const int *unquant_mf, const uint8_t *zigzag, int lambda2, \
+                              int last_nnz, dctcoef *coefs, dctcoef *quant_coefs, dctcoef *dct, \
+                              uint8_t *cabac_state_sig, uint8_t *cabac_state_last,              \
+                              uint64_t level_state0, uint16_t level_state1 );                   \
+} x264hip_##BD##_quant_function_t;
+
+X264HIP_DECLARE_TABLES( 8,  uint8_t,  int16_t, uint16_t )
+X264HIP_DECLARE_TABLES( 10, uint16_t, int32_t, uint32_t )
+
+/*----------------------------------------------------------------------------
+ * Runtime
+ *--------------------------------------------------------------------------*/
+/* Select and initialise a gfx950 device.  0 on success, X264HIP_ENODEV if no
+ * gfx950 device is present (the caller then keeps its own C entries, the
+ * convention of reference common/opencl.c:400-409). */
+int  x264hip_init( int device );
+/* last HIP error text of the calling thread ("" if none) */
+const char *x264hip_last_error( void );
+/* 1 if the library was built for gfx950 and a device is usable */
+int  x264hip_available( void );
+
+/*----------------------------------------------------------------------------
+ * Per-bit-depth entries.  BD = 8 or 10.
+ *--------------------------------------------------------------------------*/
+#define X264HIP_DECLARE_ENTRIES( BD, pixel, dctcoef, udctcoef, sadt )                            \
+/* drop-in table initialisers (see header comment) */                                           \
+void x264hip_##BD##_pixel_init( uint32_t cpu, x264hip_##BD##_pixel_function_t *pixf );          \
+void x264hip_##BD##_pixel_init_hip( x264hip_##BD##_pixel_function_t *pixf );                    \
+void x264hip_##BD##_dct_init( uint32_t cpu, x264hip_##BD##_dct_function_t *dctf );              \
+void x264hip_##BD##_dct_init_hip( x264hip_##BD##_dct_function_t *dctf );                        \
+void x264hip_##BD##_quant_init( void *h, uint32_t cpu, x264hip_##BD##_quant_function_t *pf );   \
+void x264hip_##BD##_quant_init_hip( x264hip_##BD##_quant_function_t *pf );                      \
+                                                                                                \
+/* quant tables: restates x264_cqm_init (reference common/set.c:73-206) for the                 \
+ * mf / bias arrays the quant entries consume.  scaling_list[8] as sps->scaling_list            \
+ * (4x4 lists 0..3 = CQM_4IY,4PY,4IC,4PC; 8x8 lists 4..7).  deadzone_inter/intra =              \
+ * param.analyse.i_luma_deadzone[0]/[1] (defaults 21/11, reference base.c:456-457).             \
+ * Output arrays are [4][qp_max_spec+1][16] and [4][qp_max_spec+1][64]; the 8x8                 \
+ * ones are written only when b_transform_8x8.  Returns qp_max_spec (51 / 63). */               \
+int x264hip_##BD##_cqm_init( const uint8_t *const scaling_list[8], int deadzone_inter,          \
+                             int deadzone_intra, int b_transform_8x8,                           \
+                             udctcoef *quant4_mf, udctcoef *quant4_bias,                        \
+                             udctcoef *quant8_mf, udctcoef *quant8_bias );                      \
+                                                                                                \
+/* generic block metrics over device-resident planes: for i < n,                               \
+ * scores[i] = op( fenc + fenc_off[i], fenc_stride, ref + ref_off[i], ref_stride )              \
+ * with op the reference sad/ssd/satd of size i_pixel (pixel.c:55-110, 265-332).                \
+ * Offsets and strides count pixels.  fenc_off/ref_off/scores are device arrays. */             \
+int x264hip_##BD##_pixel_cmp_batch( int op, int i_pixel,                                        \
+                                    const pixel *fenc, intptr_t fenc_stride,                    \
+                                    const pixel *ref, intptr_t ref_stride,                      \
+                                    const int64_t *fenc_off, const int64_t *ref_off,            \
+                                    int n, int32_t *scores, void *stream );                     \
+                                                                                                \
+/* exhaustive integer-pel search table (the candidate set of reference                          \
+ * encoder/me.c:618-631 before mv costs).  For every 16x16 macroblock of                        \
+ * n_frames (fenc, ref) pairs:                                                                  \
+ *   table[f][mb][j][i] = sad_16x16( fenc_f + 16*(mby*fenc_stride + mbx), fenc_stride,          \
+ *                                  ref_f + (16*mby + j - range)*ref_stride + 16*mbx + i - range, \
+ *                                  ref_stride ),   0 <= i,j <= 2*range                         \
+ * i.e. mx = i - range, my = j - range, raster order my-major.  ref must be a                   \
+ * padded plane (x264 PADH/PADV = 32, reference common/frame.h:32-35); every                    \
+ * window row is read from x-range-3 to x+15+range+3, so the caller keeps                      \
+ * range+3 <= the horizontal padding.  range is one of 4, 8, 16, 24. */                         \
+int x264hip_##BD##_me_search_full( const pixel *fenc, intptr_t fenc_stride,                     \
+                                   intptr_t fenc_frame_stride,                                  \
+                                   const pixel *ref, intptr_t ref_stride,                       \
+                                   intptr_t ref_frame_stride,                                   \
+                                   int mb_width, int mb_height, int n_frames, int range,        \
+                                   sadt *table, void *stream );                                 \
+                                                                                                \
+/* block lists of the reference transforms (dct.c), device arrays;                             \
+ * dct holds n consecutive outputs of the selected entry's size. */                             \
+int x264hip_##BD##_sub_dct_batch( int kind, const pixel *fenc, intptr_t fenc_stride,            \
+                                  const pixel *fdec, intptr_t fdec_stride,                      \
+                                  const int64_t *fenc_off, const int64_t *fdec_off,             \
+                                  int n, dctcoef *dct, void *stream );                          \
+/* in-place DC transforms: DC_4x4 on n arrays d[16]; DC_2x4 on n pairs                          \
+ * (dct[8] out, dct4x4[8][16] in/out) */                                                        \
+int x264hip_##BD##_dc_batch( int kind, dctcoef *dct, dctcoef *dct4x4, int n, void *stream );    \
+/* in-place quantisation of n blocks with one mf/bias set (device arrays of                     \
+ * 16 or 64 udctcoef for 4x4/4x4x4/8x8; for the DC kinds mf[0]/bias[0] are the                  \
+ * scalar int arguments of quant_4x4_dc / quant_2x2_dc).  nz[i] = the entry's                   \
+ * return value (quant.c:59-104). */                                                            \
+int x264hip_##BD##_quant_batch( int kind, dctcoef *dct, const udctcoef *mf,                     \
+                                const udctcoef *bias, int n, int32_t *nz, void *stream );       \
+int x264hip_##BD##_quant_dc_batch( int kind, dctcoef *dct, int mf, int bias,                    \
+                                   int n, int32_t *nz, void *stream );                          \
+                                                                                                \
+/* fused inter-luma residual path of reference encoder/macroblock.c:806-884:                    \
+ * per 16x16 macroblock, sub16x16_dct + 4x quant_4x4x4 (transform 4) or                         \
+ * sub16x16_dct8 + 4x quant_8x8 (transform 8) of fenc - pred.  dct gets 256                     \
+ * coefs per MB in the reference's dct4x4[16][16] / dct8x8[4][64] order; nz gets                \
+ * per MB the 16-bit mask (bit 4*i8+i4 = 4x4 block nonzero, transform 4) or                     \
+ * the 4-bit mask (bit i8, transform 8). */                                                     \
+int x264hip_##BD##_mb_dct_quant( int transform, const pixel *fenc, intptr_t fenc_stride,        \
+                                 intptr_t fenc_frame_stride,                                    \
+                                 const pixel *pred, intptr_t pred_stride,                       \
+                                 intptr_t pred_frame_stride,                                    \
+                                 int mb_width, int mb_height, int n_frames,                     \
+                                 const udctcoef *mf, const udctcoef *bias,                      \
+                                 dctcoef *dct, int32_t *nz, void *stream );
+
+X264HIP_DECLARE_ENTRIES( 8,  uint8_t,  int16_t, uint16_t, uint16_t )
+X264HIP_DECLARE_ENTRIES( 10, uint16_t, int32_t, uint32_t, uint32_t )
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* X264HIP_H */

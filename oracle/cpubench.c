@@ -1,0 +1,91 @@
+/*****************************************************************************
+ * cpubench.c — TEST INFRASTRUCTURE ONLY.  Multi-threaded drivers of the CPU
+ * oracle, used by bench.py's cpu_baseline leg (kind "port": the reference's
+ * C kernels restated in oracle.c, compiled -O3 -march=x86-64-v3).  Work is
+ * split by macroblock rows, one contiguous band per thread, like the
+ * per-row task split planned in BASELINE.md §3.
+ *****************************************************************************/
+#include <pthread.h>
+#include <stdint.h>
+#include <stddef.h>
+
+void oracle8_me_search_full( const uint8_t *fenc, intptr_t fs, const uint8_t *ref, intptr_t rs,
+                             int mb_width, int mb_height, int range, uint16_t *table );
+void oracle8_mb_dct_quant( int transform, const uint8_t *fenc, intptr_t fs, const uint8_t *pred, intptr_t ps,
+                           int mb_width, int mb_height, const uint16_t *mf, const uint16_t *bias,
+                           int16_t *dct, int32_t *nz );
+
+typedef struct
+{
+    const uint8_t *fenc, *ref;
+    intptr_t fs, rs;
+    int mb_width, row0, rows, range, transform;
+    const uint16_t *mf, *bias;
+    uint16_t *table;
+    int16_t *dct;
+    int32_t *nz;
+} job_t;
+
+static void *me_worker( void *arg )
+{
+    job_t *j = arg;
+    int w = 2 * j->range + 1;
+    oracle8_me_search_full( j->fenc + (intptr_t)16 * j->row0 * j->fs, j->fs,
+                            j->ref + (intptr_t)16 * j->row0 * j->rs, j->rs,
+                            j->mb_width, j->rows, j->range,
+                            j->table + (size_t)j->row0 * j->mb_width * w * w );
+    return NULL;
+}
+
+static void *dq_worker( void *arg )
+{
+    job_t *j = arg;
+    oracle8_mb_dct_quant( j->transform, j->fenc + (intptr_t)16 * j->row0 * j->fs, j->fs,
+                          j->ref + (intptr_t)16 * j->row0 * j->rs, j->rs, j->mb_width, j->rows,
+                          j->mf, j->bias, j->dct + (size_t)j->row0 * j->mb_width * 256,
+                          j->nz + (size_t)j->row0 * j->mb_width );
+    return NULL;
+}
+
+static int run( void *(*fn)( void * ), job_t base, int mb_height, int nthreads )
+{
+    pthread_t th[256];
+    job_t jobs[256];
+    if( nthreads < 1 )
+        nthreads = 1;
+    if( nthreads > 256 )
+        nthreads = 256;
+    if( nthreads > mb_height )
+        nthreads = mb_height;
+    int row = 0;
+    for( int t = 0; t < nthreads; t++ )
+    {
+        int rows = mb_height / nthreads + (t < mb_height % nthreads);
+        jobs[t] = base;
+        jobs[t].row0 = row;
+        jobs[t].rows = rows;
+        row += rows;
+        if( pthread_create( &th[t], NULL, fn, &jobs[t] ) )
+            return -1;
+    }
+    for( int t = 0; t < nthreads; t++ )
+        pthread_join( th[t], NULL );
+    return nthreads;
+}
+
+/* full-search SAD tables of mb rows [0, mb_height), 8-bit; returns threads used */
+int oracle8_me_search_full_mt( const uint8_t *fenc, intptr_t fs, const uint8_t *ref, intptr_t rs,
+                               int mb_width, int mb_height, int range, uint16_t *table, int nthreads )
+{
+    job_t b = { fenc, ref, fs, rs, mb_width, 0, 0, range, 0, NULL, NULL, table, NULL, NULL };
+    return run( me_worker, b, mb_height, nthreads );
+}
+
+/* fused dct+quant over mb rows [0, mb_height), 8-bit; returns threads used */
+int oracle8_mb_dct_quant_mt( int transform, const uint8_t *fenc, intptr_t fs, const uint8_t *pred, intptr_t ps,
+                             int mb_width, int mb_height, const uint16_t *mf, const uint16_t *bias,
+                             int16_t *dct, int32_t *nz, int nthreads )
+{
+    job_t b = { fenc, pred, fs, ps, mb_width, 0, 0, 0, transform, mf, bias, NULL, dct, nz };
+    return run( dq_worker, b, mb_height, nthreads );
+}

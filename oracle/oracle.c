@@ -1,0 +1,662 @@
+/*****************************************************************************
+ * oracle.c — TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference's
+ * portable C kernels on the north-star path, used as the parity checker for
+ * the HIP backend.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it; the product (x264-i386pic_amd/) never does.
+ *
+ * PARITY UNPINNED: the reference (xrgtn/x264-i386pic) ships no golden vectors
+ * for this path (checkasm is purely differential) and its C
+ * path cannot be compiled here under the round rules (common/osdep.h:39
+ * includes the configure-generated config.h).  This
+ * file restates the algorithm from the reference sources, line by line in
+ * semantics (never in text), and is cross-checked against an independent
+ * matrix-form restatement in tests/numpy_ref.py.
+ *
+ * Compiled twice (BIT_DEPTH=8 / 10) like the reference (Makefile:309-313);
+ * symbols are prefixed oracle8_ / oracle10_.
+ *****************************************************************************/
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifndef BIT_DEPTH
+#error "BIT_DEPTH must be 8 or 10"
+#endif
+
+#if BIT_DEPTH > 8
+typedef uint16_t pixel;
+typedef int32_t  dctcoef;
+typedef uint32_t udctcoef;
+typedef uint32_t sum_t;      /* reference common/pixel.c:233-239 */
+typedef uint64_t sum2_t;
+typedef uint32_t sadt;
+#else
+typedef uint8_t  pixel;
+typedef int16_t  dctcoef;
+typedef uint16_t udctcoef;
+typedef uint16_t sum_t;
+typedef uint32_t sum2_t;
+typedef uint16_t sadt;
+#endif
+#define PIXEL_MAX ((1 << BIT_DEPTH) - 1)
+#define BITS_PER_SUM (8 * sizeof(sum_t))
+#define QP_MAX_SPEC (51 + 6 * (BIT_DEPTH - 8))   /* reference common/common.h:58-59 */
+#define FENC_STRIDE 16                            /* reference common/common.h:570-571 */
+#define FDEC_STRIDE 32
+
+#define GLUE3_(a,b,c) a##b##c
+#define GLUE3(a,b,c) GLUE3_(a,b,c)
+#define FN(name) GLUE3(oracle, BIT_DEPTH, _##name)
+
+static const uint8_t pixel_w[8] = { 16, 16, 8, 8, 8, 4, 4, 4 };   /* reference common/pixel.h:55-59 */
+static const uint8_t pixel_h[8] = { 16, 8, 16, 8, 4, 8, 4, 16 };
+
+static inline pixel clip_pixel( int x )
+{
+    return x < 0 ? 0 : x > PIXEL_MAX ? PIXEL_MAX : x;
+}
+
+/*============================================================================
+ * pixel metrics — reference common/pixel.c
+ *==========================================================================*/
+
+/* PIXEL_SAD_C, reference common/pixel.c:55-70 */
+int FN(sad)( int i_pixel, const pixel *pix1, intptr_t s1, const pixel *pix2, intptr_t s2 )
+{
+    int lx = pixel_w[i_pixel], ly = pixel_h[i_pixel];
+    int sum = 0;
+    for( int y = 0; y < ly; y++, pix1 += s1, pix2 += s2 )
+        for( int x = 0; x < lx; x++ )
+            sum += abs( pix1[x] - pix2[x] );
+    return sum;
+}
+
+/* PIXEL_SSD_C, reference common/pixel.c:85-101 */
+int FN(ssd)( int i_pixel, const pixel *pix1, intptr_t s1, const pixel *pix2, intptr_t s2 )
+{
+    int lx = pixel_w[i_pixel], ly = pixel_h[i_pixel];
+    int sum = 0;
+    for( int y = 0; y < ly; y++, pix1 += s1, pix2 += s2 )
+        for( int x = 0; x < lx; x++ )
+        {
+            int d = pix1[x] - pix2[x];
+            sum += d * d;
+        }
+    return sum;
+}
+
+/* HADAMARD4 and the packed two-lane abs, reference common/pixel.c:242-259 */
+#define HADAMARD4( d0, d1, d2, d3, s0, s1, s2, s3 ) {\
+    sum2_t t0 = s0 + s1, t1 = s0 - s1, t2 = s2 + s3, t3 = s2 - s3;\
+    d0 = t0 + t2; d2 = t0 - t2; d1 = t1 + t3; d3 = t1 - t3; }
+
+static inline sum2_t abs2( sum2_t a )
+{
+    sum2_t s = ((a >> (BITS_PER_SUM - 1)) & (((sum2_t)1 << BITS_PER_SUM) + 1)) * ((sum_t)-1);
+    return (a + s) ^ s;
+}
+
+/* satd 4x4, packed horizontal pairs; reference common/pixel.c:265-288 */
+static int satd_4x4( const pixel *pix1, intptr_t i1, const pixel *pix2, intptr_t i2 )
+{
+    sum2_t tmp[4][2], a0, a1, a2, a3, b0, b1, sum = 0;
+    for( int i = 0; i < 4; i++, pix1 += i1, pix2 += i2 )
+    {
+        a0 = (sum2_t)(pix1[0] - pix2[0]);
+        a1 = (sum2_t)(pix1[1] - pix2[1]);
+        b0 = (a0 + a1) + ((a0 - a1) << BITS_PER_SUM);
+        a2 = (sum2_t)(pix1[2] - pix2[2]);
+        a3 = (sum2_t)(pix1[3] - pix2[3]);
+        b1 = (a2 + a3) + ((a2 - a3) << BITS_PER_SUM);
+        tmp[i][0] = b0 + b1;
+        tmp[i][1] = b0 - b1;
+    }
+    for( int i = 0; i < 2; i++ )
+    {
+        HADAMARD4( a0, a1, a2, a3, tmp[0][i], tmp[1][i], tmp[2][i], tmp[3][i] );
+        a0 = abs2( a0 ) + abs2( a1 ) + abs2( a2 ) + abs2( a3 );
+        sum += ((sum_t)a0) + (a0 >> BITS_PER_SUM);
+    }
+    return sum >> 1;
+}
+
+/* satd 8x4, two 4x4 blocks packed in the two halves; reference pixel.c:290-309 */
+static int satd_8x4( const pixel *pix1, intptr_t i1, const pixel *pix2, intptr_t i2 )
+{
+    sum2_t tmp[4][4], a0, a1, a2, a3, sum = 0;
+    for( int i = 0; i < 4; i++, pix1 += i1, pix2 += i2 )
+    {
+        a0 = (sum2_t)(pix1[0] - pix2[0]) + ((sum2_t)(pix1[4] - pix2[4]) << BITS_PER_SUM);
+        a1 = (sum2_t)(pix1[1] - pix2[1]) + ((sum2_t)(pix1[5] - pix2[5]) << BITS_PER_SUM);
+        a2 = (sum2_t)(pix1[2] - pix2[2]) + ((sum2_t)(pix1[6] - pix2[6]) << BITS_PER_SUM);
+        a3 = (sum2_t)(pix1[3] - pix2[3]) + ((sum2_t)(pix1[7] - pix2[7]) << BITS_PER_SUM);
+        HADAMARD4( tmp[i][0], tmp[i][1], tmp[i][2], tmp[i][3], a0, a1, a2, a3 );
+    }
+    for( int i = 0; i < 4; i++ )
+    {
+        HADAMARD4( a0, a1, a2, a3, tmp[0][i], tmp[1][i], tmp[2][i], tmp[3][i] );
+        sum += abs2( a0 ) + abs2( a1 ) + abs2( a2 ) + abs2( a3 );
+    }
+    return (((sum_t)sum) + (sum >> BITS_PER_SUM)) >> 1;
+}
+
+/* PIXEL_SATD_C tiling, reference common/pixel.c:311-332 (8-wide sizes use the
+ * 8x4 kernel, 4-wide sizes the 4x4 kernel) */
+int FN(satd)( int i_pixel, const pixel *pix1, intptr_t i1, const pixel *pix2, intptr_t i2 )
+{
+    int w = pixel_w[i_pixel], h = pixel_h[i_pixel];
+    int sum = 0;
+    if( w == 4 )
+    {
+        for( int y = 0; y < h; y += 4 )
+            sum += satd_4x4( pix1 + y*i1, i1, pix2 + y*i2, i2 );
+        return sum;
+    }
+    for( int x = 0; x < w; x += 8 )
+        for( int y = 0; y < h; y += 4 )
+            sum += satd_8x4( pix1 + y*i1 + x, i1, pix2 + y*i2 + x, i2 );
+    return sum;
+}
+
+/* SAD_X / SATD_X, fenc stride implicitly FENC_STRIDE; reference pixel.c:441-496 */
+void FN(sad_x3)( int i_pixel, const pixel *fenc, const pixel *p0, const pixel *p1, const pixel *p2,
+                 intptr_t stride, int scores[3] )
+{
+    scores[0] = FN(sad)( i_pixel, fenc, FENC_STRIDE, p0, stride );
+    scores[1] = FN(sad)( i_pixel, fenc, FENC_STRIDE, p1, stride );
+    scores[2] = FN(sad)( i_pixel, fenc, FENC_STRIDE, p2, stride );
+}
+
+void FN(sad_x4)( int i_pixel, const pixel *fenc, const pixel *p0, const pixel *p1, const pixel *p2,
+                 const pixel *p3, intptr_t stride, int scores[4] )
+{
+    FN(sad_x3)( i_pixel, fenc, p0, p1, p2, stride, scores );
+    scores[3] = FN(sad)( i_pixel, fenc, FENC_STRIDE, p3, stride );
+}
+
+void FN(satd_x3)( int i_pixel, const pixel *fenc, const pixel *p0, const pixel *p1, const pixel *p2,
+                  intptr_t stride, int scores[3] )
+{
+    scores[0] = FN(satd)( i_pixel, fenc, FENC_STRIDE, p0, stride );
+    scores[1] = FN(satd)( i_pixel, fenc, FENC_STRIDE, p1, stride );
+    scores[2] = FN(satd)( i_pixel, fenc, FENC_STRIDE, p2, stride );
+}
+
+void FN(satd_x4)( int i_pixel, const pixel *fenc, const pixel *p0, const pixel *p1, const pixel *p2,
+                  const pixel *p3, intptr_t stride, int scores[4] )
+{
+    FN(satd_x3)( i_pixel, fenc, p0, p1, p2, stride, scores );
+    scores[3] = FN(satd)( i_pixel, fenc, FENC_STRIDE, p3, stride );
+}
+
+/* generic list form used to check x264hip_*_pixel_cmp_batch */
+void FN(cmp_list)( int op, int i_pixel, const pixel *fenc, intptr_t fs, const pixel *ref, intptr_t rs,
+                   const int64_t *fenc_off, const int64_t *ref_off, int n, int32_t *scores )
+{
+    for( int i = 0; i < n; i++ )
+    {
+        const pixel *a = fenc + fenc_off[i], *b = ref + ref_off[i];
+        scores[i] = op == 0 ? FN(sad)( i_pixel, a, fs, b, rs )
+                  : op == 1 ? FN(ssd)( i_pixel, a, fs, b, rs )
+                  :           FN(satd)( i_pixel, a, fs, b, rs );
+    }
+}
+
+/*============================================================================
+ * forward transforms — reference common/dct.c
+ *==========================================================================*/
+
+/* pixel_sub_wxh, reference common/dct.c:145-155 (result stored as dctcoef) */
+static void pixel_sub_wxh( dctcoef *diff, int n, const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    for( int y = 0; y < n; y++, p1 += s1, p2 += s2 )
+        for( int x = 0; x < n; x++ )
+            diff[x + y*n] = p1[x] - p2[x];
+}
+
+/* sub4x4_dct, reference common/dct.c:157-189: rows then columns, int16 temps at
+ * 8 bit, transposed output dct[x*4+y]... (row i of the second pass writes dct[i*4+k]) */
+static void sub4x4_dct_s( dctcoef dct[16], const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    dctcoef d[16], tmp[16];
+    pixel_sub_wxh( d, 4, p1, s1, p2, s2 );
+    for( int i = 0; i < 4; i++ )
+    {
+        int s03 = d[i*4+0] + d[i*4+3], s12 = d[i*4+1] + d[i*4+2];
+        int d03 = d[i*4+0] - d[i*4+3], d12 = d[i*4+1] - d[i*4+2];
+        tmp[0*4+i] = s03 + s12;
+        tmp[1*4+i] = 2*d03 + d12;
+        tmp[2*4+i] = s03 - s12;
+        tmp[3*4+i] = d03 - 2*d12;
+    }
+    for( int i = 0; i < 4; i++ )
+    {
+        int s03 = tmp[i*4+0] + tmp[i*4+3], s12 = tmp[i*4+1] + tmp[i*4+2];
+        int d03 = tmp[i*4+0] - tmp[i*4+3], d12 = tmp[i*4+1] - tmp[i*4+2];
+        dct[i*4+0] = s03 + s12;
+        dct[i*4+1] = 2*d03 + d12;
+        dct[i*4+2] = s03 - s12;
+        dct[i*4+3] = d03 - 2*d12;
+    }
+}
+
+/* sub8x8_dct / sub16x16_dct block order, reference common/dct.c:191-205 */
+static void sub8x8_dct_s( dctcoef dct[4][16], const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    sub4x4_dct_s( dct[0], p1,          s1, p2,          s2 );
+    sub4x4_dct_s( dct[1], p1+4,        s1, p2+4,        s2 );
+    sub4x4_dct_s( dct[2], p1+4*s1,     s1, p2+4*s2,     s2 );
+    sub4x4_dct_s( dct[3], p1+4*s1+4,   s1, p2+4*s2+4,   s2 );
+}
+
+static void sub16x16_dct_s( dctcoef dct[16][16], const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    sub8x8_dct_s( &dct[ 0], p1,          s1, p2,          s2 );
+    sub8x8_dct_s( &dct[ 4], p1+8,        s1, p2+8,        s2 );
+    sub8x8_dct_s( &dct[ 8], p1+8*s1,     s1, p2+8*s2,     s2 );
+    sub8x8_dct_s( &dct[12], p1+8*s1+8,   s1, p2+8*s2+8,   s2 );
+}
+
+/* sub4x4_dct_dc, reference common/dct.c:207-214 */
+static int sub4x4_dct_dc_s( const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    int sum = 0;
+    for( int i = 0; i < 4; i++, p1 += s1, p2 += s2 )
+        sum += p1[0] + p1[1] + p1[2] + p1[3] - p2[0] - p2[1] - p2[2] - p2[3];
+    return sum;
+}
+
+/* sub8x8_dct_dc with its 2x2 DC transform, reference common/dct.c:216-232.
+ * The four sums are stored to dctcoef before the butterfly reads them back. */
+static void sub8x8_dct_dc_s( dctcoef dct[4], const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    dct[0] = sub4x4_dct_dc_s( p1,        s1, p2,        s2 );
+    dct[1] = sub4x4_dct_dc_s( p1+4,      s1, p2+4,      s2 );
+    dct[2] = sub4x4_dct_dc_s( p1+4*s1,   s1, p2+4*s2,   s2 );
+    dct[3] = sub4x4_dct_dc_s( p1+4*s1+4, s1, p2+4*s2+4, s2 );
+    int d0 = dct[0] + dct[1], d1 = dct[2] + dct[3];
+    int d2 = dct[0] - dct[1], d3 = dct[2] - dct[3];
+    dct[0] = d0 + d1;
+    dct[1] = d0 - d1;
+    dct[2] = d2 + d3;
+    dct[3] = d2 - d3;
+}
+
+/* sub8x16_dct_dc with its 2x4 DC transform, reference common/dct.c:234-270 */
+static void sub8x16_dct_dc_s( dctcoef dct[8], const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    int a[8];
+    for( int k = 0; k < 8; k++ )
+        a[k] = sub4x4_dct_dc_s( p1 + (k>>1)*4*s1 + (k&1)*4, s1, p2 + (k>>1)*4*s2 + (k&1)*4, s2 );
+    int b0 = a[0] + a[1], b1 = a[2] + a[3], b2 = a[4] + a[5], b3 = a[6] + a[7];
+    int b4 = a[0] - a[1], b5 = a[2] - a[3], b6 = a[4] - a[5], b7 = a[6] - a[7];
+    int c0 = b0 + b1, c1 = b2 + b3, c2 = b4 + b5, c3 = b6 + b7;
+    int c4 = b0 - b1, c5 = b2 - b3, c6 = b4 - b5, c7 = b6 - b7;
+    dct[0] = c0 + c1;
+    dct[1] = c2 + c3;
+    dct[2] = c0 - c1;
+    dct[3] = c2 - c3;
+    dct[4] = c4 - c5;
+    dct[5] = c6 - c7;
+    dct[6] = c4 + c5;
+    dct[7] = c6 + c7;
+}
+
+/* DCT8_1D, reference common/dct.c:332-356 */
+#define DCT8_1D {\
+    int s07 = SRC(0) + SRC(7), s16 = SRC(1) + SRC(6), s25 = SRC(2) + SRC(5), s34 = SRC(3) + SRC(4);\
+    int a0 = s07 + s34, a1 = s16 + s25, a2 = s07 - s34, a3 = s16 - s25;\
+    int d07 = SRC(0) - SRC(7), d16 = SRC(1) - SRC(6), d25 = SRC(2) - SRC(5), d34 = SRC(3) - SRC(4);\
+    int a4 = d16 + d25 + (d07 + (d07>>1));\
+    int a5 = d07 - d34 - (d25 + (d25>>1));\
+    int a6 = d07 + d34 - (d16 + (d16>>1));\
+    int a7 = d16 - d25 + (d34 + (d34>>1));\
+    DST(0) =  a0 + a1;\
+    DST(1) =  a4 + (a7>>2);\
+    DST(2) =  a2 + (a3>>1);\
+    DST(3) =  a5 + (a6>>2);\
+    DST(4) =  a0 - a1;\
+    DST(5) =  a6 - (a5>>2);\
+    DST(6) = (a2>>1) - a3;\
+    DST(7) = (a4>>2) - a7;\
+}
+
+/* sub8x8_dct8: column pass in place (dctcoef temps), then row pass writing the
+ * transposed output; reference common/dct.c:358-377 */
+static void sub8x8_dct8_s( dctcoef dct[64], const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    dctcoef tmp[64];
+    pixel_sub_wxh( tmp, 8, p1, s1, p2, s2 );
+#define SRC(x) tmp[(x)*8+i]
+#define DST(x) tmp[(x)*8+i]
+    for( int i = 0; i < 8; i++ )
+        DCT8_1D
+#undef SRC
+#undef DST
+#define SRC(x) tmp[i*8+(x)]
+#define DST(x) dct[(x)*8+i]
+    for( int i = 0; i < 8; i++ )
+        DCT8_1D
+#undef SRC
+#undef DST
+}
+
+static void sub16x16_dct8_s( dctcoef dct[4][64], const pixel *p1, intptr_t s1, const pixel *p2, intptr_t s2 )
+{
+    sub8x8_dct8_s( dct[0], p1,          s1, p2,          s2 );
+    sub8x8_dct8_s( dct[1], p1+8,        s1, p2+8,        s2 );
+    sub8x8_dct8_s( dct[2], p1+8*s1,     s1, p2+8*s2,     s2 );
+    sub8x8_dct8_s( dct[3], p1+8*s1+8,   s1, p2+8*s2+8,   s2 );
+}
+
+/* entry points with the reference's implicit strides (dct.h:31-33) */
+void FN(sub4x4_dct)( dctcoef dct[16], const pixel *p1, const pixel *p2 ) { sub4x4_dct_s( dct, p1, FENC_STRIDE, p2, FDEC_STRIDE ); }
+void FN(sub8x8_dct)( dctcoef dct[4][16], const pixel *p1, const pixel *p2 ) { sub8x8_dct_s( dct, p1, FENC_STRIDE, p2, FDEC_STRIDE ); }
+void FN(sub16x16_dct)( dctcoef dct[16][16], const pixel *p1, const pixel *p2 ) { sub16x16_dct_s( dct, p1, FENC_STRIDE, p2, FDEC_STRIDE ); }
+void FN(sub8x8_dct_dc)( dctcoef dct[4], const pixel *p1, const pixel *p2 ) { sub8x8_dct_dc_s( dct, p1, FENC_STRIDE, p2, FDEC_STRIDE ); }
+void FN(sub8x16_dct_dc)( dctcoef dct[8], const pixel *p1, const pixel *p2 ) { sub8x16_dct_dc_s( dct, p1, FENC_STRIDE, p2, FDEC_STRIDE ); }
+void FN(sub8x8_dct8)( dctcoef dct[64], const pixel *p1, const pixel *p2 ) { sub8x8_dct8_s( dct, p1, FENC_STRIDE, p2, FDEC_STRIDE ); }
+void FN(sub16x16_dct8)( dctcoef dct[4][64], const pixel *p1, const pixel *p2 ) { sub16x16_dct8_s( dct, p1, FENC_STRIDE, p2, FDEC_STRIDE ); }
+
+/* list form for x264hip_*_sub_dct_batch; kinds as X264HIP_DCT_* */
+static const int dct_kind_size[7] = { 16, 64, 256, 4, 8, 64, 256 };
+void FN(sub_dct_list)( int kind, const pixel *fenc, intptr_t fs, const pixel *fdec, intptr_t ds,
+                       const int64_t *fenc_off, const int64_t *fdec_off, int n, dctcoef *out )
+{
+    for( int i = 0; i < n; i++ )
+    {
+        const pixel *a = fenc + fenc_off[i], *b = fdec + fdec_off[i];
+        dctcoef *o = out + (size_t)i * dct_kind_size[kind];
+        switch( kind )
+        {
+            case 0: sub4x4_dct_s( o, a, fs, b, ds ); break;
+            case 1: sub8x8_dct_s( (dctcoef(*)[16])o, a, fs, b, ds ); break;
+            case 2: sub16x16_dct_s( (dctcoef(*)[16])o, a, fs, b, ds ); break;
+            case 3: sub8x8_dct_dc_s( o, a, fs, b, ds ); break;
+            case 4: sub8x16_dct_dc_s( o, a, fs, b, ds ); break;
+            case 5: sub8x8_dct8_s( o, a, fs, b, ds ); break;
+            case 6: sub16x16_dct8_s( (dctcoef(*)[64])o, a, fs, b, ds ); break;
+        }
+    }
+}
+
+/* dct4x4dc, reference common/dct.c:47-76 */
+void FN(dct4x4dc)( dctcoef d[16] )
+{
+    dctcoef tmp[16];
+    for( int i = 0; i < 4; i++ )
+    {
+        int s01 = d[i*4+0] + d[i*4+1], d01 = d[i*4+0] - d[i*4+1];
+        int s23 = d[i*4+2] + d[i*4+3], d23 = d[i*4+2] - d[i*4+3];
+        tmp[0*4+i] = s01 + s23;
+        tmp[1*4+i] = s01 - s23;
+        tmp[2*4+i] = d01 - d23;
+        tmp[3*4+i] = d01 + d23;
+    }
+    for( int i = 0; i < 4; i++ )
+    {
+        int s01 = tmp[i*4+0] + tmp[i*4+1], d01 = tmp[i*4+0] - tmp[i*4+1];
+        int s23 = tmp[i*4+2] + tmp[i*4+3], d23 = tmp[i*4+2] - tmp[i*4+3];
+        d[i*4+0] = ( s01 + s23 + 1 ) >> 1;
+        d[i*4+1] = ( s01 - s23 + 1 ) >> 1;
+        d[i*4+2] = ( d01 - d23 + 1 ) >> 1;
+        d[i*4+3] = ( d01 + d23 + 1 ) >> 1;
+    }
+}
+
+/* dct2x4dc, reference common/dct.c:109-143 (zeroes the gathered DCs) */
+void FN(dct2x4dc)( dctcoef dct[8], dctcoef dct4x4[8][16] )
+{
+    int a0 = dct4x4[0][0] + dct4x4[1][0], a1 = dct4x4[2][0] + dct4x4[3][0];
+    int a2 = dct4x4[4][0] + dct4x4[5][0], a3 = dct4x4[6][0] + dct4x4[7][0];
+    int a4 = dct4x4[0][0] - dct4x4[1][0], a5 = dct4x4[2][0] - dct4x4[3][0];
+    int a6 = dct4x4[4][0] - dct4x4[5][0], a7 = dct4x4[6][0] - dct4x4[7][0];
+    int b0 = a0 + a1, b1 = a2 + a3, b2 = a4 + a5, b3 = a6 + a7;
+    int b4 = a0 - a1, b5 = a2 - a3, b6 = a4 - a5, b7 = a6 - a7;
+    dct[0] = b0 + b1;
+    dct[1] = b2 + b3;
+    dct[2] = b0 - b1;
+    dct[3] = b2 - b3;
+    dct[4] = b4 - b5;
+    dct[5] = b6 - b7;
+    dct[6] = b4 + b5;
+    dct[7] = b6 + b7;
+    for( int k = 0; k < 8; k++ )
+        dct4x4[k][0] = 0;
+}
+
+/*============================================================================
+ * quantisation — reference common/quant.c:50-104
+ *==========================================================================*/
+#define QUANT_ONE( coef, mf, f ) \
+{ \
+    if( (coef) > 0 ) \
+        (coef) = ((f) + (uint32_t)(coef)) * (mf) >> 16; \
+    else \
+        (coef) = -(int32_t)(((f) + (uint32_t)(-(coef))) * (mf) >> 16); \
+    nz |= (coef); \
+}
+
+int FN(quant_8x8)( dctcoef dct[64], const udctcoef mf[64], const udctcoef bias[64] )
+{
+    int nz = 0;
+    for( int i = 0; i < 64; i++ )
+        QUANT_ONE( dct[i], mf[i], bias[i] );
+    return !!nz;
+}
+
+int FN(quant_4x4)( dctcoef dct[16], const udctcoef mf[16], const udctcoef bias[16] )
+{
+    int nz = 0;
+    for( int i = 0; i < 16; i++ )
+        QUANT_ONE( dct[i], mf[i], bias[i] );
+    return !!nz;
+}
+
+int FN(quant_4x4x4)( dctcoef dct[4][16], const udctcoef mf[16], const udctcoef bias[16] )
+{
+    int nza = 0;
+    for( int j = 0; j < 4; j++ )
+    {
+        int nz = 0;
+        for( int i = 0; i < 16; i++ )
+            QUANT_ONE( dct[j][i], mf[i], bias[i] );
+        nza |= (!!nz) << j;
+    }
+    return nza;
+}
+
+int FN(quant_4x4_dc)( dctcoef dct[16], int mf, int bias )
+{
+    int nz = 0;
+    for( int i = 0; i < 16; i++ )
+        QUANT_ONE( dct[i], mf, bias );
+    return !!nz;
+}
+
+int FN(quant_2x2_dc)( dctcoef dct[4], int mf, int bias )
+{
+    int nz = 0;
+    for( int i = 0; i < 4; i++ )
+        QUANT_ONE( dct[i], mf, bias );
+    return !!nz;
+}
+
+/*============================================================================
+ * CQM — reference common/set.c:28-206 (quant side only)
+ *==========================================================================*/
+#define SHIFT(x,s) ((s)<=0 ? (x)<<-(s) : ((x)+(1<<((s)-1)))>>(s))
+#define DIV(n,d) (((n) + ((d)>>1)) / (d))
+
+/* H.264 scaling constants, reference common/set.c:31-71 */
+static const uint16_t quant4_scale[6][3] =
+{
+    { 13107, 8066, 5243 }, { 11916, 7490, 4660 }, { 10082, 6554, 4194 },
+    {  9362, 5825, 3647 }, {  8192, 5243, 3355 }, {  7282, 4559, 2893 },
+};
+static const uint8_t quant8_scan[16] = { 0,3,4,3, 3,1,5,1, 4,5,2,5, 3,1,5,1 };
+static const uint16_t quant8_scale[6][6] =
+{
+    { 13107, 11428, 20972, 12222, 16777, 15481 },
+    { 11916, 10826, 19174, 11058, 14980, 14290 },
+    { 10082,  8943, 15978,  9675, 12710, 11985 },
+    {  9362,  8228, 14913,  8931, 11984, 11259 },
+    {  8192,  7346, 13159,  7740, 10486,  9777 },
+    {  7282,  6428, 11570,  6830,  9118,  8640 },
+};
+
+int FN(cqm_init)( const uint8_t *const scaling_list[8], int deadzone_inter, int deadzone_intra,
+                  int b_transform_8x8, udctcoef *q4_mf, udctcoef *q4_bias, udctcoef *q8_mf, udctcoef *q8_bias )
+{
+    /* deadzone per list: {32-dz[1], 32-dz[0], 32-11, 32-21}, reference set.c:81-83 */
+    int deadzone[4] = { 32 - deadzone_intra, 32 - deadzone_inter, 32 - 11, 32 - 21 };
+    int def_quant4[6][16], def_quant8[6][64];
+    int quant4_mf[4][6][16], quant8_mf[4][6][64];
+
+    for( int q = 0; q < 6; q++ )
+    {
+        for( int i = 0; i < 16; i++ )
+            def_quant4[q][i] = quant4_scale[q][(i&1) + ((i>>2)&1)];
+        for( int i = 0; i < 64; i++ )
+            def_quant8[q][i] = quant8_scale[q][quant8_scan[((i>>1)&12) | (i&3)]];
+    }
+    for( int q = 0; q < 6; q++ )
+    {
+        for( int l = 0; l < 4; l++ )
+            for( int i = 0; i < 16; i++ )
+                quant4_mf[l][q][i] = DIV( def_quant4[q][i] * 16, scaling_list[l][i] );
+        if( b_transform_8x8 )
+            for( int l = 0; l < 2; l++ )   /* num_8x8_lists for 4:2:0 with 8x8dct, set.c:87-88 */
+                for( int i = 0; i < 64; i++ )
+                    quant8_mf[l][q][i] = DIV( def_quant8[q][i] * 16, scaling_list[4+l][i] );
+    }
+    for( int q = 0; q <= QP_MAX_SPEC; q++ )
+    {
+        for( int l = 0; l < 4; l++ )
+            for( int i = 0; i < 16; i++ )
+            {
+                int j = SHIFT( quant4_mf[l][q%6][i], q/6 - 1 );
+                size_t o = ((size_t)l*(QP_MAX_SPEC+1) + q)*16 + i;
+                q4_mf[o] = (uint16_t)j;
+                if( !j )
+                    continue;   /* bias left untouched, as the reference does (set.c:171-175) */
+                int a = DIV( deadzone[l] << 10, j ), b = (1<<15) / j;
+                q4_bias[o] = a < b ? a : b;
+            }
+        if( b_transform_8x8 )
+            for( int l = 0; l < 2; l++ )
+                for( int i = 0; i < 64; i++ )
+                {
+                    int j = SHIFT( quant8_mf[l][q%6][i], q/6 );
+                    size_t o = ((size_t)l*(QP_MAX_SPEC+1) + q)*64 + i;
+                    q8_mf[o] = (uint16_t)j;
+                    if( !j )
+                        continue;
+                    int a = DIV( deadzone[l] << 10, j ), b = (1<<15) / j;
+                    q8_bias[o] = a < b ? a : b;
+                }
+    }
+    return QP_MAX_SPEC;
+}
+
+/*============================================================================
+ * frame-level helpers composed from the entries above (checkers for the
+ * batched HIP entries)
+ *==========================================================================*/
+
+/* exhaustive 16x16 SAD table, semantics of x264hip_*_me_search_full */
+void FN(me_search_full)( const pixel *fenc, intptr_t fs, const pixel *ref, intptr_t rs,
+                         int mb_width, int mb_height, int range, sadt *table )
+{
+    int w = 2*range + 1;
+    for( int mby = 0; mby < mb_height; mby++ )
+        for( int mbx = 0; mbx < mb_width; mbx++ )
+        {
+            const pixel *f = fenc + 16*(mby*fs + mbx);
+            sadt *t = table + ((size_t)mby*mb_width + mbx) * w * w;
+            for( int j = 0; j < w; j++ )
+                for( int i = 0; i < w; i++ )
+                    t[j*w+i] = (sadt)FN(sad)( 0, f, fs, ref + (16*mby + j - range)*rs + 16*mbx + i - range, rs );
+        }
+}
+
+/* fused inter-luma residual path, semantics of x264hip_*_mb_dct_quant
+ * (reference encoder/macroblock.c:806-884 without trellis/decimation) */
+void FN(mb_dct_quant)( int transform, const pixel *fenc, intptr_t fs, const pixel *pred, intptr_t ps,
+                       int mb_width, int mb_height, const udctcoef *mf, const udctcoef *bias,
+                       dctcoef *dct, int32_t *nz )
+{
+    for( int mby = 0; mby < mb_height; mby++ )
+        for( int mbx = 0; mbx < mb_width; mbx++ )
+        {
+            size_t mb = (size_t)mby*mb_width + mbx;
+            const pixel *f = fenc + 16*(mby*fs + mbx), *p = pred + 16*(mby*ps + mbx);
+            dctcoef *d = dct + mb*256;
+            int mask = 0;
+            if( transform == 8 )
+            {
+                sub16x16_dct8_s( (dctcoef(*)[64])d, f, fs, p, ps );
+                for( int i8 = 0; i8 < 4; i8++ )
+                    mask |= FN(quant_8x8)( d + 64*i8, mf, bias ) << i8;
+            }
+            else
+            {
+                sub16x16_dct_s( (dctcoef(*)[16])d, f, fs, p, ps );
+                for( int i8 = 0; i8 < 4; i8++ )
+                    mask |= FN(quant_4x4x4)( (dctcoef(*)[16])(d + 64*i8), mf, bias ) << (4*i8);
+            }
+            nz[mb] = mask;
+        }
+}
+
+/*============================================================================
+ * motion compensation inputs — reference common/mc.c
+ *==========================================================================*/
+
+/* hpel_filter, reference common/mc.c:173-196 (6-tap, clip, centre via int16
+ * intermediate with the 10-bit bias `pad`) */
+#define TAPFILTER(pix, d) ((pix)[x-2*d] + (pix)[x+3*d] - 5*((pix)[x-d] + (pix)[x+2*d]) + 20*((pix)[x] + (pix)[x+d]))
+void FN(hpel_filter)( pixel *dsth, pixel *dstv, pixel *dstc, const pixel *src,
+                      intptr_t stride, int width, int height, int16_t *buf )
+{
+    const int pad = (BIT_DEPTH > 9) ? (-10 * PIXEL_MAX) : 0;
+    for( int y = 0; y < height; y++ )
+    {
+        for( int x = -2; x < width + 3; x++ )
+        {
+            int v = TAPFILTER( src, stride );
+            dstv[x] = clip_pixel( (v + 16) >> 5 );
+            buf[x+2] = v + pad;
+        }
+        for( int x = 0; x < width; x++ )
+            dstc[x] = clip_pixel( (TAPFILTER( buf+2, 1 ) - 32*pad + 512) >> 10 );
+        for( int x = 0; x < width; x++ )
+            dsth[x] = clip_pixel( (TAPFILTER( src, 1 ) + 16) >> 5 );
+        dsth += stride;
+        dstv += stride;
+        dstc += stride;
+        src += stride;
+    }
+}
+
+/* get_ref without weighting: qpel from two hpel planes; reference common/mc.c:221-249
+ * with x264_hpel_ref0/1 of common/tables.c:183-184 */
+static const uint8_t hpel_ref0[16] = {0,1,1,1,0,1,1,1,2,3,3,3,0,1,1,1};
+static const uint8_t hpel_ref1[16] = {0,0,1,0,2,2,3,2,2,2,3,2,2,2,3,2};
+const pixel *FN(get_ref)( pixel *dst, intptr_t *dst_stride, const pixel *const src[4], intptr_t stride,
+                          int mvx, int mvy, int w, int h )
+{
+    int qpel_idx = ((mvy&3)<<2) + (mvx&3);
+    intptr_t offset = (mvy>>2)*stride + (mvx>>2);
+    const pixel *src1 = src[hpel_ref0[qpel_idx]] + offset + ((mvy&3) == 3) * stride;
+    if( qpel_idx & 5 )
+    {
+        const pixel *src2 = src[hpel_ref1[qpel_idx]] + offset + ((mvx&3) == 3);
+        for( int y = 0; y < h; y++ )
+            for( int x = 0; x < w; x++ )
+                dst[y * *dst_stride + x] = ( src1[y*stride + x] + src2[y*stride + x] + 1 ) >> 1;
+        return dst;
+    }
+    *dst_stride = stride;
+    return src1;
+}

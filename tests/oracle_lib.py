@@ -1,0 +1,191 @@
+"""ctypes front-end of the CPU oracle (oracle/liboracle.so) — TEST INFRASTRUCTURE.
+
+Every function takes numpy arrays and returns numpy arrays / ints; pointers
+into arrays are passed as (array, element offset).  Only tests/, the smoke
+check and bench.py's cpu_baseline leg use this module.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+_L = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+_P, _IP = C.c_void_p, C.c_ssize_t
+
+
+def pixel_dtype(bd):
+    return np.uint8 if bd == 8 else np.uint16
+
+
+def coef_dtype(bd):
+    return np.int16 if bd == 8 else np.int32
+
+
+def ucoef_dtype(bd):
+    return np.uint16 if bd == 8 else np.uint32
+
+
+def sad_dtype(bd):
+    return np.uint16 if bd == 8 else np.uint32
+
+
+def _addr(a, off=0):
+    return C.c_void_p(a.ctypes.data + int(off) * a.itemsize)
+
+
+def _f(bd, name, argtypes, restype=None):
+    fn = getattr(_L, f"oracle{bd}_{name}")
+    fn.argtypes = argtypes
+    fn.restype = restype
+    return fn
+
+
+for _bd in (8, 10):
+    for _n in ("sad", "ssd", "satd"):
+        _f(_bd, _n, [C.c_int, _P, _IP, _P, _IP], C.c_int)
+    for _n in ("sad_x3", "satd_x3"):
+        _f(_bd, _n, [C.c_int, _P, _P, _P, _P, _IP, _P])
+    for _n in ("sad_x4", "satd_x4"):
+        _f(_bd, _n, [C.c_int, _P, _P, _P, _P, _P, _IP, _P])
+    _f(_bd, "cmp_list", [C.c_int, C.c_int, _P, _IP, _P, _IP, _P, _P, C.c_int, _P])
+    for _n in ("sub4x4_dct", "sub8x8_dct", "sub16x16_dct", "sub8x8_dct_dc", "sub8x16_dct_dc",
+               "sub8x8_dct8", "sub16x16_dct8"):
+        _f(_bd, _n, [_P, _P, _P])
+    _f(_bd, "sub_dct_list", [C.c_int, _P, _IP, _P, _IP, _P, _P, C.c_int, _P])
+    _f(_bd, "dct4x4dc", [_P])
+    _f(_bd, "dct2x4dc", [_P, _P])
+    for _n in ("quant_8x8", "quant_4x4", "quant_4x4x4"):
+        _f(_bd, _n, [_P, _P, _P], C.c_int)
+    for _n in ("quant_4x4_dc", "quant_2x2_dc"):
+        _f(_bd, _n, [_P, C.c_int, C.c_int], C.c_int)
+    _f(_bd, "cqm_init", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P], C.c_int)
+    _f(_bd, "me_search_full", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P])
+    _f(_bd, "mb_dct_quant", [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P])
+    _f(_bd, "hpel_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int, _P])
+    _f(_bd, "get_ref", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int], _P)
+_L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
+_L.oracle8_me_search_full_mt.restype = C.c_int
+_L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
+_L.oracle8_mb_dct_quant_mt.restype = C.c_int
+
+_OPS = {"sad": 0, "ssd": 1, "satd": 2}
+
+
+def cmp(bd, op, i_pixel, a, a_off, sa, b, b_off, sb):
+    """reference sad/ssd/satd of size i_pixel at a[a_off] (stride sa) vs b[b_off] (stride sb)."""
+    return getattr(_L, f"oracle{bd}_{op}")(i_pixel, _addr(a, a_off), sa, _addr(b, b_off), sb)
+
+
+def cmp_x(bd, op, n, i_pixel, fenc, f_off, ref, offs, stride):
+    """sad_x3/x4, satd_x3/x4 (fenc stride 16)."""
+    out = np.zeros(4, np.int32)
+    args = [_addr(ref, o) for o in offs]
+    getattr(_L, f"oracle{bd}_{op}_x{n}")(i_pixel, _addr(fenc, f_off), *args, stride, _addr(out))
+    return out[:n].copy()
+
+
+def cmp_list(bd, op, i_pixel, fenc, fs, ref, rs, fenc_off, ref_off):
+    fo = np.ascontiguousarray(fenc_off, np.int64)
+    ro = np.ascontiguousarray(ref_off, np.int64)
+    out = np.zeros(len(fo), np.int32)
+    getattr(_L, f"oracle{bd}_cmp_list")(_OPS.get(op, op), i_pixel, _addr(fenc), fs, _addr(ref), rs,
+                                       _addr(fo), _addr(ro), len(fo), _addr(out))
+    return out
+
+
+DCT_OUT = {"sub4x4_dct": 16, "sub8x8_dct": 64, "sub16x16_dct": 256, "sub8x8_dct_dc": 4,
+           "sub8x16_dct_dc": 8, "sub8x8_dct8": 64, "sub16x16_dct8": 256}
+DCT_KINDS = ["sub4x4_dct", "sub8x8_dct", "sub16x16_dct", "sub8x8_dct_dc", "sub8x16_dct_dc",
+             "sub8x8_dct8", "sub16x16_dct8"]
+
+
+def sub_dct(bd, name, a, a_off, b, b_off):
+    """reference entry with implicit strides FENC_STRIDE=16 / FDEC_STRIDE=32."""
+    out = np.zeros(DCT_OUT[name], coef_dtype(bd))
+    getattr(_L, f"oracle{bd}_{name}")(_addr(out), _addr(a, a_off), _addr(b, b_off))
+    return out
+
+
+def sub_dct_list(bd, kind, fenc, fs, fdec, ds, fenc_off, fdec_off):
+    fo = np.ascontiguousarray(fenc_off, np.int64)
+    do = np.ascontiguousarray(fdec_off, np.int64)
+    out = np.zeros(len(fo) * DCT_OUT[DCT_KINDS[kind]], coef_dtype(bd))
+    getattr(_L, f"oracle{bd}_sub_dct_list")(kind, _addr(fenc), fs, _addr(fdec), ds, _addr(fo), _addr(do),
+                                           len(fo), _addr(out))
+    return out
+
+
+def dct4x4dc(bd, d):
+    d = np.array(d, coef_dtype(bd))
+    getattr(_L, f"oracle{bd}_dct4x4dc")(_addr(d))
+    return d
+
+
+def dct2x4dc(bd, dct4x4):
+    src = np.array(dct4x4, coef_dtype(bd)).reshape(8, 16).copy()
+    out = np.zeros(8, coef_dtype(bd))
+    getattr(_L, f"oracle{bd}_dct2x4dc")(_addr(out), _addr(src))
+    return out, src
+
+
+def quant(bd, name, dct, mf=None, bias=None):
+    """returns (quantised copy, nz)."""
+    d = np.array(dct, coef_dtype(bd))
+    fn = getattr(_L, f"oracle{bd}_{name}")
+    if name in ("quant_4x4_dc", "quant_2x2_dc"):
+        nz = fn(_addr(d), int(mf), int(bias))
+    else:
+        m = np.ascontiguousarray(mf, ucoef_dtype(bd))
+        b = np.ascontiguousarray(bias, ucoef_dtype(bd))
+        nz = fn(_addr(d), _addr(m), _addr(b))
+    return d, nz
+
+
+def cqm_init(bd, scaling_lists, dz_inter=21, dz_intra=11, transform_8x8=True):
+    qp1 = 52 + 6 * (bd - 8)
+    ut = ucoef_dtype(bd)
+    q4m, q4b = np.zeros((4, qp1, 16), ut), np.zeros((4, qp1, 16), ut)
+    q8m, q8b = np.zeros((4, qp1, 64), ut), np.zeros((4, qp1, 64), ut)
+    lists = [np.ascontiguousarray(np.asarray(s, np.uint8)) for s in scaling_lists]
+    ptrs = (_P * 8)(*[x.ctypes.data for x in lists])
+    getattr(_L, f"oracle{bd}_cqm_init")(ptrs, dz_inter, dz_intra, int(transform_8x8), _addr(q4m), _addr(q4b),
+                                       _addr(q8m), _addr(q8b))
+    return q4m, q4b, q8m, q8b
+
+
+def me_search_full(bd, fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, rng):
+    """one frame: table [mbh, mbw, 2r+1, 2r+1]."""
+    w = 2 * rng + 1
+    out = np.zeros((mbh, mbw, w, w), sad_dtype(bd))
+    getattr(_L, f"oracle{bd}_me_search_full")(_addr(fenc, f_origin), fs, _addr(ref, r_origin), rs, mbw, mbh,
+                                             rng, _addr(out))
+    return out
+
+
+def me_search_full_mt(fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, rng, nthreads):
+    w = 2 * rng + 1
+    out = np.zeros((mbh, mbw, w, w), np.uint16)
+    used = _L.oracle8_me_search_full_mt(_addr(fenc, f_origin), fs, _addr(ref, r_origin), rs, mbw, mbh, rng,
+                                        _addr(out), nthreads)
+    return out, used
+
+
+def mb_dct_quant(bd, transform, fenc, f_origin, fs, pred, p_origin, ps, mbw, mbh, mf, bias):
+    dct = np.zeros((mbh * mbw, 256), coef_dtype(bd))
+    nz = np.zeros(mbh * mbw, np.int32)
+    m = np.ascontiguousarray(mf, ucoef_dtype(bd))
+    b = np.ascontiguousarray(bias, ucoef_dtype(bd))
+    getattr(_L, f"oracle{bd}_mb_dct_quant")(transform, _addr(fenc, f_origin), fs, _addr(pred, p_origin), ps,
+                                           mbw, mbh, _addr(m), _addr(b), _addr(dct), _addr(nz))
+    return dct, nz
+
+
+def mb_dct_quant_mt(transform, fenc, f_origin, fs, pred, p_origin, ps, mbw, mbh, mf, bias, nthreads):
+    dct = np.zeros((mbh * mbw, 256), np.int16)
+    nz = np.zeros(mbh * mbw, np.int32)
+    m = np.ascontiguousarray(mf, np.uint16)
+    b = np.ascontiguousarray(bias, np.uint16)
+    used = _L.oracle8_mb_dct_quant_mt(transform, _addr(fenc, f_origin), fs, _addr(pred, p_origin), ps, mbw, mbh,
+                                      _addr(m), _addr(b), _addr(dct), _addr(nz), nthreads)
+    return dct, nz, used

@@ -1,0 +1,362 @@
+"""x264hip — host-side mirror of x264's pixel / dct / quant function tables,
+backed by the gfx950 HIP kernels in ``libx264hip.so`` (C ABI: include/x264hip.h).
+
+Two layers, mirroring the C ABI:
+
+* ``pixel_init(bitdepth)``, ``dct_init(bitdepth)``, ``quant_init(bitdepth)``
+  return ctypes structs laid out exactly like the reference's
+  ``x264_pixel_function_t`` / ``x264_dct_function_t`` / ``x264_quant_function_t``
+  (reference common/pixel.h:78-144, common/dct.h:29-59, common/quant.h:30-70),
+  filled by ``x264hip_{8,10}_*_init(X264HIP_CPU_HIP, ...)``.  Entries are called
+  like the reference's (``pixf.sad[PIXEL_16x16](pix1, 16, pix2, 64)``) and each
+  call runs one GPU dispatch.
+* Batched wrappers (``me_search_full``, ``pixel_cmp_batch``, ``sub_dct_batch``,
+  ``dc_batch``, ``quant_batch``, ``quant_dc_batch``, ``mb_dct_quant``) take
+  device-resident torch tensors and enqueue on the current torch stream.
+
+There is no CPU fallback: if the shared library is missing or no gfx950 device
+is usable, every entry point raises ``BackendUnavailable``.
+"""
+import ctypes
+import os
+
+__all__ = [
+    "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
+    "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
+    "quant_dc_batch", "mb_dct_quant", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
+    "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP",
+]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libx264hip.so")
+
+# reference common/pixel.h:37-59
+PIXEL_16x16, PIXEL_16x8, PIXEL_8x16, PIXEL_8x8, PIXEL_8x4, PIXEL_4x8, PIXEL_4x4, PIXEL_4x16 = range(8)
+PIXEL_SIZES = [(16, 16), (16, 8), (8, 16), (8, 8), (8, 4), (4, 8), (4, 4), (4, 16)]
+CMP_SAD, CMP_SSD, CMP_SATD = 0, 1, 2
+DCT_SUB4x4, DCT_SUB8x8, DCT_SUB16x16, DCT_SUB8x8_DC, DCT_SUB8x16_DC, DCT_SUB8x8_8, DCT_SUB16x16_8 = range(7)
+DCT_OUT_SIZE = [16, 64, 256, 4, 8, 64, 256]
+DC_4x4, DC_2x4 = 0, 1
+QUANT_8x8, QUANT_4x4, QUANT_4x4x4, QUANT_4x4_DC, QUANT_2x2_DC = range(5)
+CPU_HIP = 1 << 26
+FENC_STRIDE, FDEC_STRIDE = 16, 32
+PAD = 32  # x264 PADH / PADV, reference common/frame.h:32-33
+
+
+class BackendUnavailable(RuntimeError):
+    """The gfx950 backend (libx264hip.so or a gfx950 device) is not usable."""
+
+
+_lib = None
+
+
+def lib():
+    """Load libx264hip.so (no fallback: raises if it is missing)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BackendUnavailable(
+                f"{LIB_PATH} not built; run `make -C x264-i386pic_amd/csrc` (or __graft_entry__.build())")
+        # Bind the library to torch's HIP runtime: torch bundles libamdhip64.so with the
+        # same SONAME (libamdhip64.so.7), so loading torch first makes the dynamic loader
+        # reuse that copy instead of mapping a second HIP/HSA runtime from /opt/rocm
+        # (two runtimes in one process cannot share the GPU).
+        import torch  # noqa: F401
+        _lib = ctypes.CDLL(LIB_PATH)
+        _declare(_lib)
+    return _lib
+
+
+def init(device=0):
+    """x264hip_init(device); raises BackendUnavailable if no gfx950 device."""
+    rc = lib().x264hip_init(device)
+    if rc != 0:
+        raise BackendUnavailable(f"x264hip_init({device}) = {rc}: {lib().x264hip_last_error().decode()}")
+
+
+# ----------------------------------------------------------------- tables
+_c = ctypes
+_P = _c.c_void_p
+_IP = _c.c_ssize_t   # intptr_t
+
+CMP_T = _c.CFUNCTYPE(_c.c_int, _P, _IP, _P, _IP)
+CMP_X3_T = _c.CFUNCTYPE(None, _P, _P, _P, _P, _IP, _P)
+CMP_X4_T = _c.CFUNCTYPE(None, _P, _P, _P, _P, _P, _IP, _P)
+DCT_T = _c.CFUNCTYPE(None, _P, _P, _P)            # sub*_dct*(dct, pix1, pix2)
+DC_T = _c.CFUNCTYPE(None, _P)                     # dct4x4dc(d)
+DC2_T = _c.CFUNCTYPE(None, _P, _P)                # dct2x4dc(dct, dct4x4)
+QUANT_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P)      # quant_*(dct, mf, bias)
+QUANT_DC_T = _c.CFUNCTYPE(_c.c_int, _P, _c.c_int, _c.c_int)
+
+
+class PixelFunctions(_c.Structure):
+    """Layout of x264_pixel_function_t, reference common/pixel.h:78-144."""
+    _fields_ = [
+        ("sad", CMP_T * 8), ("ssd", CMP_T * 8), ("satd", CMP_T * 8), ("ssim", CMP_T * 7),
+        ("sa8d", CMP_T * 4), ("mbcmp", CMP_T * 8), ("mbcmp_unaligned", CMP_T * 8),
+        ("fpelcmp", CMP_T * 8), ("fpelcmp_x3", CMP_X3_T * 7), ("fpelcmp_x4", CMP_X4_T * 7),
+        ("sad_aligned", CMP_T * 8), ("vsad", _P), ("asd8", _P), ("sa8d_satd", _P * 1),
+        ("var", _P * 4), ("var2", _P * 4), ("hadamard_ac", _P * 4), ("ssd_nv12_core", _P),
+        ("ssim_4x4x2_core", _P), ("ssim_end4", _P),
+        ("sad_x3", CMP_X3_T * 7), ("sad_x4", CMP_X4_T * 7),
+        ("satd_x3", CMP_X3_T * 7), ("satd_x4", CMP_X4_T * 7), ("ads", _P * 7),
+    ] + [(n, _P) for n in (
+        "intra_mbcmp_x3_16x16", "intra_satd_x3_16x16", "intra_sad_x3_16x16",
+        "intra_mbcmp_x3_4x4", "intra_satd_x3_4x4", "intra_sad_x3_4x4",
+        "intra_mbcmp_x3_chroma", "intra_satd_x3_chroma", "intra_sad_x3_chroma",
+        "intra_mbcmp_x3_8x16c", "intra_satd_x3_8x16c", "intra_sad_x3_8x16c",
+        "intra_mbcmp_x3_8x8c", "intra_satd_x3_8x8c", "intra_sad_x3_8x8c",
+        "intra_mbcmp_x3_8x8", "intra_sa8d_x3_8x8", "intra_sad_x3_8x8",
+        "intra_mbcmp_x9_4x4", "intra_satd_x9_4x4", "intra_sad_x9_4x4",
+        "intra_mbcmp_x9_8x8", "intra_sa8d_x9_8x8", "intra_sad_x9_8x8")]
+
+
+class DctFunctions(_c.Structure):
+    """Layout of x264_dct_function_t, reference common/dct.h:29-59."""
+    _fields_ = [
+        ("sub4x4_dct", DCT_T), ("add4x4_idct", _P), ("sub8x8_dct", DCT_T), ("sub8x8_dct_dc", DCT_T),
+        ("add8x8_idct", _P), ("add8x8_idct_dc", _P), ("sub8x16_dct_dc", DCT_T), ("sub16x16_dct", DCT_T),
+        ("add16x16_idct", _P), ("add16x16_idct_dc", _P), ("sub8x8_dct8", DCT_T), ("add8x8_idct8", _P),
+        ("sub16x16_dct8", DCT_T), ("add16x16_idct8", _P), ("dct4x4dc", DC_T), ("idct4x4dc", _P),
+        ("dct2x4dc", DC2_T),
+    ]
+
+
+class QuantFunctions(_c.Structure):
+    """Layout of x264_quant_function_t, reference common/quant.h:30-70."""
+    _fields_ = [
+        ("quant_8x8", QUANT_T), ("quant_4x4", QUANT_T), ("quant_4x4x4", QUANT_T),
+        ("quant_4x4_dc", QUANT_DC_T), ("quant_2x2_dc", QUANT_DC_T),
+        ("dequant_8x8", _P), ("dequant_4x4", _P), ("dequant_4x4_dc", _P),
+        ("idct_dequant_2x4_dc", _P), ("idct_dequant_2x4_dconly", _P),
+        ("optimize_chroma_2x2_dc", _P), ("optimize_chroma_2x4_dc", _P), ("denoise_dct", _P),
+        ("decimate_score15", _P), ("decimate_score16", _P), ("decimate_score64", _P),
+        ("coeff_last", _P * 14), ("coeff_last4", _P), ("coeff_last8", _P),
+        ("coeff_level_run", _P * 13), ("coeff_level_run4", _P), ("coeff_level_run8", _P),
+        ("trellis_cabac_4x4", _P), ("trellis_cabac_8x8", _P), ("trellis_cabac_4x4_psy", _P),
+        ("trellis_cabac_8x8_psy", _P), ("trellis_cabac_dc", _P), ("trellis_cabac_chroma_422_dc", _P),
+    ]
+
+
+def _check_bd(bitdepth):
+    if bitdepth not in (8, 10):
+        raise ValueError("bitdepth must be 8 or 10")
+
+
+def _table(kind, struct, bitdepth, cpu):
+    _check_bd(bitdepth)
+    init()  # loud failure without a gfx950 device
+    tab = struct()
+    fn = getattr(lib(), f"x264hip_{bitdepth}_{kind}_init")
+    if kind == "quant":
+        fn(None, cpu, _c.byref(tab))
+    else:
+        fn(cpu, _c.byref(tab))
+    return tab
+
+
+def pixel_init(bitdepth=8, cpu=CPU_HIP):
+    """x264_pixel_init equivalent (reference common/pixel.c:809)."""
+    return _table("pixel", PixelFunctions, bitdepth, cpu)
+
+
+def dct_init(bitdepth=8, cpu=CPU_HIP):
+    """x264_dct_init equivalent (reference common/dct.c:477)."""
+    return _table("dct", DctFunctions, bitdepth, cpu)
+
+
+def quant_init(bitdepth=8, cpu=CPU_HIP):
+    """x264_quant_init equivalent (reference common/quant.c:414)."""
+    return _table("quant", QuantFunctions, bitdepth, cpu)
+
+
+# ----------------------------------------------------------------- declarations
+def _declare(L):
+    L.x264hip_init.argtypes = [_c.c_int]
+    L.x264hip_init.restype = _c.c_int
+    L.x264hip_last_error.restype = _c.c_char_p
+    L.x264hip_available.restype = _c.c_int
+    for bd in (8, 10):
+        f = lambda n: getattr(L, f"x264hip_{bd}_{n}")  # noqa: E731
+        f("pixel_init").argtypes = [_c.c_uint32, _P]
+        f("dct_init").argtypes = [_c.c_uint32, _P]
+        f("quant_init").argtypes = [_P, _c.c_uint32, _P]
+        f("pixel_init_hip").argtypes = [_P]
+        f("dct_init_hip").argtypes = [_P]
+        f("quant_init_hip").argtypes = [_P]
+        f("cqm_init").argtypes = [_P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P]
+        f("cqm_init").restype = _c.c_int
+        f("pixel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _IP, _P, _P, _c.c_int, _P, _P]
+        f("me_search_full").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P]
+        f("sub_dct_batch").argtypes = [_c.c_int, _P, _IP, _P, _IP, _P, _P, _c.c_int, _P, _P]
+        f("dc_batch").argtypes = [_c.c_int, _P, _P, _c.c_int, _P]
+        f("quant_batch").argtypes = [_c.c_int, _P, _P, _P, _c.c_int, _P, _P]
+        f("quant_dc_batch").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P]
+        f("mb_dct_quant").argtypes = [_c.c_int, _P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int,
+                                      _P, _P, _P, _P, _P]
+        for n in ("pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
+                  "quant_dc_batch", "mb_dct_quant"):
+            f(n).restype = _c.c_int
+
+
+# ----------------------------------------------------------------- CQM
+def cqm_init(bitdepth, scaling_lists, deadzone_inter=21, deadzone_intra=11, transform_8x8=True):
+    """Quant mf/bias tables (restated x264_cqm_init, reference common/set.c:73-206).
+
+    scaling_lists: 8 sequences (4 of 16, 4 of 64 entries) like sps->scaling_list.
+    Returns numpy arrays (quant4_mf, quant4_bias [4][QP+1][16], quant8_mf, quant8_bias [4][QP+1][64]).
+    """
+    import numpy as np
+    _check_bd(bitdepth)
+    qp1 = 52 + 6 * (bitdepth - 8)
+    ut = np.uint16 if bitdepth == 8 else np.uint32
+    q4m = np.zeros((4, qp1, 16), ut)
+    q4b = np.zeros((4, qp1, 16), ut)
+    q8m = np.zeros((4, qp1, 64), ut)
+    q8b = np.zeros((4, qp1, 64), ut)
+    lists = [np.ascontiguousarray(np.asarray(s, np.uint8)) for s in scaling_lists]
+    ptrs = (_P * 8)(*[x.ctypes.data for x in lists])
+    getattr(lib(), f"x264hip_{bitdepth}_cqm_init")(
+        ptrs, deadzone_inter, deadzone_intra, int(bool(transform_8x8)),
+        q4m.ctypes.data, q4b.ctypes.data, q8m.ctypes.data, q8b.ctypes.data)
+    return q4m, q4b, q8m, q8b
+
+
+# ----------------------------------------------------------------- batched (torch)
+def _stream():
+    import torch
+    return _c.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _ptr(t, offset_elems=0):
+    return _c.c_void_p(t.data_ptr() + offset_elems * t.element_size())
+
+
+def _rc(rc, name):
+    if rc != 0:
+        raise RuntimeError(f"x264hip {name} failed ({rc}): {lib().x264hip_last_error().decode()}")
+
+
+def _pix_bd(t):
+    import torch
+    if t.dtype == torch.uint8:
+        return 8
+    if t.dtype in (torch.int16, torch.uint16):
+        return 10
+    raise TypeError("pixel tensors are uint8 (8-bit) or int16/uint16 (10-bit)")
+
+
+def alloc_planes(nframes, width, height, bitdepth=8, device="cuda", pad=PAD):
+    """Padded plane stack like x264's frames (PADH/PADV = pad, reference common/frame.c:59-87).
+
+    Returns (tensor[nframes, height + 2*pad, stride], stride, origin) where origin is
+    the element offset of pixel (0,0) of frame 0 and stride is a multiple of 64 pixels.
+    """
+    import torch
+    stride = (width + 2 * pad + 63) // 64 * 64
+    dt = torch.uint8 if bitdepth == 8 else torch.int16
+    t = torch.zeros((nframes, height + 2 * pad, stride), dtype=dt, device=device)
+    return t, stride, pad * stride + pad
+
+
+def pixel_cmp_batch(op, i_pixel, fenc, fenc_stride, ref, ref_stride, fenc_off, ref_off, scores=None):
+    """scores[i] = op(fenc + fenc_off[i], ref + ref_off[i]) (device int64 offsets, pixels)."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = fenc_off.numel()
+    if scores is None:
+        scores = torch.empty(n, dtype=torch.int32, device=fenc.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_pixel_cmp_batch")(
+        op, i_pixel, _ptr(fenc), fenc_stride, _ptr(ref), ref_stride, _ptr(fenc_off), _ptr(ref_off), n,
+        _ptr(scores), _stream()), "pixel_cmp_batch")
+    return scores
+
+
+def me_search_full(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height,
+                   nframes, rng=16, table=None, fenc_frame_stride=None, ref_frame_stride=None):
+    """Exhaustive 16x16 SAD table [nframes, mb_height, mb_width, 2r+1, 2r+1] (x264hip_*_me_search_full)."""
+    import torch
+    bd = _pix_bd(fenc)
+    w = 2 * rng + 1
+    if table is None:
+        table = torch.empty((nframes, mb_height, mb_width, w, w),
+                            dtype=torch.int16 if bd == 8 else torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)
+    _rc(getattr(lib(), f"x264hip_{bd}_me_search_full")(
+        _ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs,
+        mb_width, mb_height, nframes, rng, _ptr(table), _stream()), "me_search_full")
+    return table
+
+
+def sub_dct_batch(kind, fenc, fenc_stride, fdec, fdec_stride, fenc_off, fdec_off, out=None):
+    import torch
+    bd = _pix_bd(fenc)
+    n = fenc_off.numel()
+    if out is None:
+        out = torch.empty(n * DCT_OUT_SIZE[kind], dtype=torch.int16 if bd == 8 else torch.int32,
+                          device=fenc.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_sub_dct_batch")(
+        kind, _ptr(fenc), fenc_stride, _ptr(fdec), fdec_stride, _ptr(fenc_off), _ptr(fdec_off), n,
+        _ptr(out), _stream()), "sub_dct_batch")
+    return out
+
+
+def _coef_bd(t):
+    import torch
+    if t.dtype == torch.int16:
+        return 8
+    if t.dtype == torch.int32:
+        return 10
+    raise TypeError("dctcoef tensors are int16 (8-bit) or int32 (10-bit)")
+
+
+def dc_batch(kind, dct, dct4x4=None, n=None):
+    bd = _coef_bd(dct)
+    if n is None:
+        n = dct.numel() // (16 if kind == DC_4x4 else 8)
+    _rc(getattr(lib(), f"x264hip_{bd}_dc_batch")(
+        kind, _ptr(dct), _ptr(dct4x4) if dct4x4 is not None else None, n, _stream()), "dc_batch")
+    return dct
+
+
+def quant_batch(kind, dct, mf, bias, nz=None):
+    import torch
+    bd = _coef_bd(dct)
+    n = dct.numel() // (64 if kind in (QUANT_8x8, QUANT_4x4x4) else 16)
+    if nz is None:
+        nz = torch.empty(n, dtype=torch.int32, device=dct.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_quant_batch")(
+        kind, _ptr(dct), _ptr(mf), _ptr(bias), n, _ptr(nz), _stream()), "quant_batch")
+    return nz
+
+
+def quant_dc_batch(kind, dct, mf, bias, nz=None):
+    import torch
+    bd = _coef_bd(dct)
+    n = dct.numel() // (16 if kind == QUANT_4x4_DC else 4)
+    if nz is None:
+        nz = torch.empty(n, dtype=torch.int32, device=dct.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_quant_dc_batch")(
+        kind, _ptr(dct), int(mf), int(bias), n, _ptr(nz), _stream()), "quant_dc_batch")
+    return nz
+
+
+def mb_dct_quant(transform, fenc, fenc_origin, fenc_stride, pred, pred_origin, pred_stride,
+                 mb_width, mb_height, nframes, mf, bias, dct=None, nz=None,
+                 fenc_frame_stride=None, pred_frame_stride=None):
+    """Fused residual transform + quant per MB (x264hip_*_mb_dct_quant)."""
+    import torch
+    bd = _pix_bd(fenc)
+    nmb = nframes * mb_height * mb_width
+    if dct is None:
+        dct = torch.empty((nmb, 256), dtype=torch.int16 if bd == 8 else torch.int32, device=fenc.device)
+    if nz is None:
+        nz = torch.empty(nmb, dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    pfs = pred_frame_stride if pred_frame_stride is not None else (pred[0].numel() if pred.dim() == 3 else 0)
+    _rc(getattr(lib(), f"x264hip_{bd}_mb_dct_quant")(
+        transform, _ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(pred, pred_origin), pred_stride, pfs,
+        mb_width, mb_height, nframes, _ptr(mf), _ptr(bias), _ptr(dct), _ptr(nz), _stream()), "mb_dct_quant")
+    return dct, nz

@@ -1,0 +1,490 @@
+// C ABI of the gfx950 backend: runtime, drop-in table initialisers, per-call
+// table entries and the batched device entries.  See include/x264hip.h.
+//
+// Per-call table entries keep the reference's synchronous, host-pointer
+// contract (reference common/pixel.h:31-35, dct.h:29-59, quant.h:30-36): the
+// caller's block is staged into a per-thread pinned buffer, ONE kernel of the
+// batched path runs on it (zero-copy reads over the host link) and the
+// result is read back after a stream synchronise.  No metric, transform or
+// quantisation is ever computed on the host here: if the GPU call fails the
+// process aborts with the HIP error (there is no CPU fallback).
+#include "hipcommon.h"
+#include "x264hip.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <mutex>
+
+using namespace x264hip;
+
+// ============================================================ runtime
+static int g_device = -1;
+static std::mutex g_init_mutex;
+static thread_local char t_err[256] = "";
+
+static int set_err( hipError_t e, const char *where )
+{
+    snprintf( t_err, sizeof(t_err), "%s: %s", where, hipGetErrorString( e ) );
+    return X264HIP_EDEVICE;
+}
+
+extern "C" const char *x264hip_last_error( void ) { return t_err; }
+
+extern "C" int x264hip_init( int device )
+{
+    std::lock_guard<std::mutex> lk( g_init_mutex );
+    int n = 0;
+    if( hipGetDeviceCount( &n ) != hipSuccess || n <= 0 )
+    {
+        snprintf( t_err, sizeof(t_err), "x264hip_init: no HIP device" );
+        return X264HIP_ENODEV;
+    }
+    if( device < 0 || device >= n )
+        return X264HIP_EINVAL;
+    hipDeviceProp_t prop;
+    hipError_t e = hipGetDeviceProperties( &prop, device );
+    if( e != hipSuccess )
+        return set_err( e, "hipGetDeviceProperties" );
+    if( strncmp( prop.gcnArchName, "gfx950", 6 ) )
+    {
+        snprintf( t_err, sizeof(t_err), "x264hip_init: device %d is %s, not gfx950", device, prop.gcnArchName );
+        return X264HIP_ENODEV;
+    }
+    e = hipSetDevice( device );
+    if( e != hipSuccess )
+        return set_err( e, "hipSetDevice" );
+    g_device = device;
+    return X264HIP_OK;
+}
+
+extern "C" int x264hip_available( void )
+{
+    if( g_device >= 0 )
+        return 1;
+    return x264hip_init( 0 ) == X264HIP_OK;
+}
+
+[[noreturn]] static void fatal( hipError_t e, const char *where )
+{
+    fprintf( stderr, "x264hip: fatal HIP error in %s: %s\n", where, hipGetErrorString( e ) );
+    abort();
+}
+
+#define CHECK_FATAL( call )                      \
+    do {                                         \
+        hipError_t e_ = ( call );                \
+        if( e_ != hipSuccess )                   \
+            fatal( e_, #call );                  \
+    } while( 0 )
+
+// per-thread stream + pinned staging buffer for the per-call table entries
+namespace {
+struct CallCtx
+{
+    hipStream_t stream = nullptr;
+    uint8_t *host = nullptr;   // host view
+    uint8_t *dev = nullptr;    // device view of the same pinned memory
+    static constexpr size_t SIZE = 64 << 10;
+    ~CallCtx()
+    {
+        // streams and pinned memory are reclaimed with the HIP context at exit
+    }
+};
+thread_local CallCtx t_call;
+
+CallCtx &call_ctx()
+{
+    if( !t_call.stream )
+    {
+        if( g_device < 0 && x264hip_init( 0 ) != X264HIP_OK )
+        {
+            fprintf( stderr, "x264hip: table entry called without a usable gfx950 device (%s)\n", t_err );
+            abort();
+        }
+        CHECK_FATAL( hipSetDevice( g_device ) );
+        CHECK_FATAL( hipStreamCreateWithFlags( &t_call.stream, hipStreamNonBlocking ) );
+        CHECK_FATAL( hipHostMalloc( (void **)&t_call.host, CallCtx::SIZE, hipHostMallocDefault ) );
+        CHECK_FATAL( hipHostGetDevicePointer( (void **)&t_call.dev, t_call.host, 0 ) );
+    }
+    return t_call;
+}
+
+// device view of a pointer into the staging buffer
+template <typename T> T *dview( CallCtx &c, T *h ) { return (T *)(c.dev + ((uint8_t *)h - c.host)); }
+
+// staging layout (bytes): [0,8K) block A, [8K,24K) blocks B, [24K,25K) offsets, [25K,26K) scores,
+// [26K,60K) coefficients / mf / bias
+constexpr size_t ST_A = 0, ST_B = 8 << 10, ST_OFF = 24 << 10, ST_SC = 25 << 10, ST_COEF = 26 << 10;
+
+template <typename P>
+void stage_block( P *dst, const P *src, intptr_t stride, int w, int h )
+{
+    for( int y = 0; y < h; y++ )
+        memcpy( dst + y * w, src + y * stride, w * sizeof(P) );
+}
+} // namespace
+
+// ============================================================ per-call pixel entries
+template <int BD, int OP, int IPIX>
+static int cmp_call( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::pixel *p2, intptr_t s2 )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    int32_t *sc = (int32_t *)(c.host + ST_SC);
+    stage_block( a, p1, s1, W, H );
+    stage_block( b, p2, s2, W, H );
+    off[0] = off[1] = 0;
+    CHECK_FATAL( launch_cmp_batch<BD>( OP, IPIX, dview( c, a ), W, dview( c, b ), W, dview( c, off ),
+                                       dview( c, off + 1 ), 1, dview( c, sc ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    return sc[0];
+}
+
+// x3 / x4: fenc has the implicit FENC_STRIDE (reference common/pixel.c:441-456)
+template <int BD, int OP, int IPIX, int N>
+static void cmpx_call( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *const *refs, intptr_t stride, int *scores )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    int32_t *sc = (int32_t *)(c.host + ST_SC);
+    stage_block( a, fenc, X264HIP_FENC_STRIDE, W, H );
+    for( int k = 0; k < N; k++ )
+    {
+        stage_block( b + k * W * H, refs[k], stride, W, H );
+        off[k] = 0;
+        off[N + k] = (int64_t)k * W * H;
+    }
+    CHECK_FATAL( launch_cmp_batch<BD>( OP, IPIX, dview( c, a ), W, dview( c, b ), W, dview( c, off ),
+                                       dview( c, off + N ), N, dview( c, sc ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    for( int k = 0; k < N; k++ )
+        scores[k] = sc[k];
+}
+
+template <int BD, int OP, int IPIX>
+static void cmp_x3( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *p0, typename PT<BD>::pixel *p1,
+                    typename PT<BD>::pixel *p2, intptr_t stride, int scores[3] )
+{
+    typename PT<BD>::pixel *r[3] = { p0, p1, p2 };
+    cmpx_call<BD, OP, IPIX, 3>( fenc, r, stride, scores );
+}
+
+template <int BD, int OP, int IPIX>
+static void cmp_x4( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *p0, typename PT<BD>::pixel *p1,
+                    typename PT<BD>::pixel *p2, typename PT<BD>::pixel *p3, intptr_t stride, int scores[4] )
+{
+    typename PT<BD>::pixel *r[4] = { p0, p1, p2, p3 };
+    cmpx_call<BD, OP, IPIX, 4>( fenc, r, stride, scores );
+}
+
+// ============================================================ per-call dct entries
+// kind as X264HIP_DCT_*; fenc stride 16, fdec stride 32 (reference dct.h:31-33)
+template <int BD, int KIND, int W, int H, int NOUT>
+static void sub_dct_call( typename PT<BD>::dctcoef *dct, typename PT<BD>::pixel *p1, typename PT<BD>::pixel *p2 )
+{
+    using pixel = typename PT<BD>::pixel;
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    stage_block( a, p1, X264HIP_FENC_STRIDE, W, H );
+    stage_block( b, p2, X264HIP_FDEC_STRIDE, W, H );
+    off[0] = off[1] = 0;
+    CHECK_FATAL( launch_sub_dct<BD>( KIND, dview( c, a ), W, dview( c, b ), W, dview( c, off ), dview( c, off + 1 ), 1,
+                                     dview( c, o ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( dct, o, NOUT * sizeof(dctcoef) );
+}
+
+template <int BD> static void c_sub4x4_dct( typename PT<BD>::dctcoef dct[16], typename PT<BD>::pixel *a, typename PT<BD>::pixel *b )
+{ sub_dct_call<BD, X264HIP_DCT_SUB4x4, 4, 4, 16>( dct, a, b ); }
+template <int BD> static void c_sub8x8_dct( typename PT<BD>::dctcoef dct[4][16], typename PT<BD>::pixel *a, typename PT<BD>::pixel *b )
+{ sub_dct_call<BD, X264HIP_DCT_SUB8x8, 8, 8, 64>( &dct[0][0], a, b ); }
+template <int BD> static void c_sub16x16_dct( typename PT<BD>::dctcoef dct[16][16], typename PT<BD>::pixel *a, typename PT<BD>::pixel *b )
+{ sub_dct_call<BD, X264HIP_DCT_SUB16x16, 16, 16, 256>( &dct[0][0], a, b ); }
+template <int BD> static void c_sub8x8_dct_dc( typename PT<BD>::dctcoef dct[4], typename PT<BD>::pixel *a, typename PT<BD>::pixel *b )
+{ sub_dct_call<BD, X264HIP_DCT_SUB8x8_DC, 8, 8, 4>( dct, a, b ); }
+template <int BD> static void c_sub8x16_dct_dc( typename PT<BD>::dctcoef dct[8], typename PT<BD>::pixel *a, typename PT<BD>::pixel *b )
+{ sub_dct_call<BD, X264HIP_DCT_SUB8x16_DC, 8, 16, 8>( dct, a, b ); }
+template <int BD> static void c_sub8x8_dct8( typename PT<BD>::dctcoef dct[64], typename PT<BD>::pixel *a, typename PT<BD>::pixel *b )
+{ sub_dct_call<BD, X264HIP_DCT_SUB8x8_8, 8, 8, 64>( dct, a, b ); }
+template <int BD> static void c_sub16x16_dct8( typename PT<BD>::dctcoef dct[4][64], typename PT<BD>::pixel *a, typename PT<BD>::pixel *b )
+{ sub_dct_call<BD, X264HIP_DCT_SUB16x16_8, 16, 16, 256>( &dct[0][0], a, b ); }
+
+template <int BD> static void c_dct4x4dc( typename PT<BD>::dctcoef d[16] )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    memcpy( o, d, 16 * sizeof(dctcoef) );
+    CHECK_FATAL( launch_dc<BD>( X264HIP_DC_4x4, dview( c, o ), nullptr, 1, c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( d, o, 16 * sizeof(dctcoef) );
+}
+
+template <int BD> static void c_dct2x4dc( typename PT<BD>::dctcoef dct[8], typename PT<BD>::dctcoef dct4x4[8][16] )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF), *s = o + 16;
+    memcpy( s, &dct4x4[0][0], 128 * sizeof(dctcoef) );
+    CHECK_FATAL( launch_dc<BD>( X264HIP_DC_2x4, dview( c, o ), dview( c, s ), 1, c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( dct, o, 8 * sizeof(dctcoef) );
+    memcpy( &dct4x4[0][0], s, 128 * sizeof(dctcoef) );
+}
+
+// ============================================================ per-call quant entries
+template <int BD, int KIND, int N, int NMF>
+static int quant_call( typename PT<BD>::dctcoef *dct, const typename PT<BD>::udctcoef *mf,
+                       const typename PT<BD>::udctcoef *bias, int mf_dc, int bias_dc )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    using udctcoef = typename PT<BD>::udctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    udctcoef *m = (udctcoef *)(c.host + ST_COEF + 1024), *f = m + 64;
+    int32_t *nz = (int32_t *)(c.host + ST_SC);
+    memcpy( o, dct, N * sizeof(dctcoef) );
+    if( NMF )
+    {
+        memcpy( m, mf, NMF * sizeof(udctcoef) );
+        memcpy( f, bias, NMF * sizeof(udctcoef) );
+    }
+    CHECK_FATAL( launch_quant<BD>( KIND, dview( c, o ), dview( c, m ), dview( c, f ), mf_dc, bias_dc, 1,
+                                   dview( c, nz ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( dct, o, N * sizeof(dctcoef) );
+    return nz[0];
+}
+
+template <int BD> static int c_quant_8x8( typename PT<BD>::dctcoef dct[64], typename PT<BD>::udctcoef mf[64], typename PT<BD>::udctcoef bias[64] )
+{ return quant_call<BD, X264HIP_QUANT_8x8, 64, 64>( dct, mf, bias, 0, 0 ); }
+template <int BD> static int c_quant_4x4( typename PT<BD>::dctcoef dct[16], typename PT<BD>::udctcoef mf[16], typename PT<BD>::udctcoef bias[16] )
+{ return quant_call<BD, X264HIP_QUANT_4x4, 16, 16>( dct, mf, bias, 0, 0 ); }
+template <int BD> static int c_quant_4x4x4( typename PT<BD>::dctcoef dct[4][16], typename PT<BD>::udctcoef mf[16], typename PT<BD>::udctcoef bias[16] )
+{ return quant_call<BD, X264HIP_QUANT_4x4x4, 64, 16>( &dct[0][0], mf, bias, 0, 0 ); }
+template <int BD> static int c_quant_4x4_dc( typename PT<BD>::dctcoef dct[16], int mf, int bias )
+{ return quant_call<BD, X264HIP_QUANT_4x4_DC, 16, 0>( dct, nullptr, nullptr, mf, bias ); }
+template <int BD> static int c_quant_2x2_dc( typename PT<BD>::dctcoef dct[4], int mf, int bias )
+{ return quant_call<BD, X264HIP_QUANT_2x2_DC, 4, 0>( dct, nullptr, nullptr, mf, bias ); }
+
+// ============================================================ table initialisers
+template <int BD, typename Tab>
+static void fill_pixel( Tab *pf )
+{
+#define SIZES8( field, OP )                                           \
+    pf->field[0] = cmp_call<BD, OP, 0>; pf->field[1] = cmp_call<BD, OP, 1>; \
+    pf->field[2] = cmp_call<BD, OP, 2>; pf->field[3] = cmp_call<BD, OP, 3>; \
+    pf->field[4] = cmp_call<BD, OP, 4>; pf->field[5] = cmp_call<BD, OP, 5>; \
+    pf->field[6] = cmp_call<BD, OP, 6>; pf->field[7] = cmp_call<BD, OP, 7>;
+#define SIZES7( field, FN, OP )                                       \
+    pf->field[0] = FN<BD, OP, 0>; pf->field[1] = FN<BD, OP, 1>;       \
+    pf->field[2] = FN<BD, OP, 2>; pf->field[3] = FN<BD, OP, 3>;       \
+    pf->field[4] = FN<BD, OP, 4>; pf->field[5] = FN<BD, OP, 5>;       \
+    pf->field[6] = FN<BD, OP, 6>;
+    // entries filled by the reference's C init, common/pixel.c:844-851
+    SIZES8( sad, 0 )
+    SIZES8( sad_aligned, 0 )
+    SIZES8( ssd, 1 )
+    SIZES8( satd, 2 )
+    SIZES7( sad_x3, cmp_x3, 0 )
+    SIZES7( sad_x4, cmp_x4, 0 )
+    SIZES7( satd_x3, cmp_x3, 2 )
+    SIZES7( satd_x4, cmp_x4, 2 )
+#undef SIZES8
+#undef SIZES7
+}
+
+template <int BD, typename Tab>
+static void fill_dct( Tab *d )
+{
+    d->sub4x4_dct = c_sub4x4_dct<BD>;
+    d->sub8x8_dct = c_sub8x8_dct<BD>;
+    d->sub8x8_dct_dc = c_sub8x8_dct_dc<BD>;
+    d->sub8x16_dct_dc = c_sub8x16_dct_dc<BD>;
+    d->sub16x16_dct = c_sub16x16_dct<BD>;
+    d->sub8x8_dct8 = c_sub8x8_dct8<BD>;
+    d->sub16x16_dct8 = c_sub16x16_dct8<BD>;
+    d->dct4x4dc = c_dct4x4dc<BD>;
+    d->dct2x4dc = c_dct2x4dc<BD>;
+}
+
+template <int BD, typename Tab>
+static void fill_quant( Tab *q )
+{
+    q->quant_8x8 = c_quant_8x8<BD>;
+    q->quant_4x4 = c_quant_4x4<BD>;
+    q->quant_4x4x4 = c_quant_4x4x4<BD>;
+    q->quant_4x4_dc = c_quant_4x4_dc<BD>;
+    q->quant_2x2_dc = c_quant_2x2_dc<BD>;
+}
+
+// ============================================================ CQM (quant side)
+// Restates x264_cqm_init, reference common/set.c:28-206, for the mf/bias
+// tables the quant entries take as inputs.
+static const uint16_t k_quant4_scale[6][3] = {
+    { 13107, 8066, 5243 }, { 11916, 7490, 4660 }, { 10082, 6554, 4194 },
+    { 9362, 5825, 3647 },  { 8192, 5243, 3355 },  { 7282, 4559, 2893 } };
+static const uint8_t k_quant8_scan[16] = { 0, 3, 4, 3, 3, 1, 5, 1, 4, 5, 2, 5, 3, 1, 5, 1 };
+static const uint16_t k_quant8_scale[6][6] = {
+    { 13107, 11428, 20972, 12222, 16777, 15481 }, { 11916, 10826, 19174, 11058, 14980, 14290 },
+    { 10082, 8943, 15978, 9675, 12710, 11985 },   { 9362, 8228, 14913, 8931, 11984, 11259 },
+    { 8192, 7346, 13159, 7740, 10486, 9777 },     { 7282, 6428, 11570, 6830, 9118, 8640 } };
+
+static inline int cqm_div( int n, int d ) { return (n + (d >> 1)) / d; }
+static inline int cqm_shift( int x, int s ) { return s <= 0 ? x << -s : (x + (1 << (s - 1))) >> s; }
+
+template <int BD>
+static int cqm_init( const uint8_t *const sl[8], int dz_inter, int dz_intra, int b8, typename PT<BD>::udctcoef *q4m,
+                     typename PT<BD>::udctcoef *q4b, typename PT<BD>::udctcoef *q8m, typename PT<BD>::udctcoef *q8b )
+{
+    const int qmax = 51 + 6 * (BD - 8);
+    const int dz[4] = { 32 - dz_intra, 32 - dz_inter, 32 - 11, 32 - 21 };
+    for( int q = 0; q <= qmax; q++ )
+    {
+        for( int l = 0; l < 4; l++ )
+            for( int i = 0; i < 16; i++ )
+            {
+                int base = cqm_div( k_quant4_scale[q % 6][(i & 1) + ((i >> 2) & 1)] * 16, sl[l][i] );
+                int j = cqm_shift( base, q / 6 - 1 );
+                size_t o = ((size_t)l * (qmax + 1) + q) * 16 + i;
+                q4m[o] = (uint16_t)j;
+                if( j )
+                {
+                    int a = cqm_div( dz[l] << 10, j ), b = (1 << 15) / j;
+                    q4b[o] = a < b ? a : b;
+                }
+            }
+        if( b8 )
+            for( int l = 0; l < 2; l++ )
+                for( int i = 0; i < 64; i++ )
+                {
+                    int base = cqm_div( k_quant8_scale[q % 6][k_quant8_scan[((i >> 1) & 12) | (i & 3)]] * 16, sl[4 + l][i] );
+                    int j = cqm_shift( base, q / 6 );
+                    size_t o = ((size_t)l * (qmax + 1) + q) * 64 + i;
+                    q8m[o] = (uint16_t)j;
+                    if( j )
+                    {
+                        int a = cqm_div( dz[l] << 10, j ), b = (1 << 15) / j;
+                        q8b[o] = a < b ? a : b;
+                    }
+                }
+    }
+    return qmax;
+}
+
+// ============================================================ exported entries
+static int map_err( hipError_t e, const char *where )
+{
+    if( e == hipSuccess )
+        return X264HIP_OK;
+    if( e == hipErrorInvalidValue )
+    {
+        snprintf( t_err, sizeof(t_err), "%s: invalid argument", where );
+        return X264HIP_EINVAL;
+    }
+    return set_err( e, where );
+}
+
+#define DEFINE_ENTRIES( BD )                                                                                         \
+    extern "C" void x264hip_##BD##_pixel_init_hip( x264hip_##BD##_pixel_function_t *pixf ) { fill_pixel<BD>( pixf ); } \
+    extern "C" void x264hip_##BD##_pixel_init( uint32_t cpu, x264hip_##BD##_pixel_function_t *pixf )                \
+    {                                                                                                                \
+        memset( pixf, 0, sizeof(*pixf) );                                                                            \
+        if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
+            fill_pixel<BD>( pixf );                                                                                  \
+    }                                                                                                                \
+    extern "C" void x264hip_##BD##_dct_init_hip( x264hip_##BD##_dct_function_t *d ) { fill_dct<BD>( d ); }          \
+    extern "C" void x264hip_##BD##_dct_init( uint32_t cpu, x264hip_##BD##_dct_function_t *d )                       \
+    {                                                                                                                \
+        memset( d, 0, sizeof(*d) );                                                                                  \
+        if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
+            fill_dct<BD>( d );                                                                                       \
+    }                                                                                                                \
+    extern "C" void x264hip_##BD##_quant_init_hip( x264hip_##BD##_quant_function_t *q ) { fill_quant<BD>( q ); }    \
+    extern "C" void x264hip_##BD##_quant_init( void *h, uint32_t cpu, x264hip_##BD##_quant_function_t *q )          \
+    {                                                                                                                \
+        (void)h;                                                                                                     \
+        memset( q, 0, sizeof(*q) );                                                                                  \
+        if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
+            fill_quant<BD>( q );                                                                                     \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_cqm_init( const uint8_t *const sl[8], int dz_inter, int dz_intra, int b8,         \
+                                            PT<BD>::udctcoef *q4m, PT<BD>::udctcoef *q4b, PT<BD>::udctcoef *q8m,     \
+                                            PT<BD>::udctcoef *q8b )                                                  \
+    {                                                                                                                \
+        return cqm_init<BD>( sl, dz_inter, dz_intra, b8, q4m, q4b, q8m, q8b );                                       \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_pixel_cmp_batch( int op, int i_pixel, const PT<BD>::pixel *fenc, intptr_t fs,     \
+                                                   const PT<BD>::pixel *ref, intptr_t rs, const int64_t *fo,         \
+                                                   const int64_t *ro, int n, int32_t *scores, void *stream )        \
+    {                                                                                                                \
+        if( op < 0 || op > 2 || i_pixel < 0 || i_pixel > 7 || n < 0 )                                                \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_cmp_batch<BD>( op, i_pixel, fenc, fs, ref, rs, fo, ro, n, scores,                     \
+                                              (hipStream_t)stream ), "pixel_cmp_batch" );                            \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_search_full( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,             \
+                                                  const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw,      \
+                                                  int mbh, int nframes, int range, PT<BD>::sadt *table,             \
+                                                  void *stream )                                                     \
+    {                                                                                                                \
+        if( mbw < 0 || mbh < 0 || nframes < 0 || !( range == 4 || range == 8 || range == 16 || range == 24 ) )        \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, table,           \
+                                            (hipStream_t)stream ), "me_search_full" );                               \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_sub_dct_batch( int kind, const PT<BD>::pixel *fenc, intptr_t fs,                  \
+                                                 const PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fo,          \
+                                                 const int64_t *dofs, int n, PT<BD>::dctcoef *dct, void *stream )    \
+    {                                                                                                                \
+        if( kind < 0 || kind > 6 || n < 0 )                                                                          \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_sub_dct<BD>( kind, fenc, fs, fdec, ds, fo, dofs, n, dct, (hipStream_t)stream ),      \
+                        "sub_dct_batch" );                                                                           \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_dc_batch( int kind, PT<BD>::dctcoef *dct, PT<BD>::dctcoef *dct4x4, int n,         \
+                                            void *stream )                                                           \
+    {                                                                                                                \
+        if( kind < 0 || kind > 1 || n < 0 || ( kind == 1 && !dct4x4 ) )                                              \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_dc<BD>( kind, dct, dct4x4, n, (hipStream_t)stream ), "dc_batch" );                  \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_quant_batch( int kind, PT<BD>::dctcoef *dct, const PT<BD>::udctcoef *mf,          \
+                                               const PT<BD>::udctcoef *bias, int n, int32_t *nz, void *stream )      \
+    {                                                                                                                \
+        if( kind < 0 || kind > 2 || n < 0 )                                                                          \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_quant<BD>( kind, dct, mf, bias, 0, 0, n, nz, (hipStream_t)stream ), "quant_batch" ); \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_quant_dc_batch( int kind, PT<BD>::dctcoef *dct, int mf, int bias, int n,          \
+                                                  int32_t *nz, void *stream )                                        \
+    {                                                                                                                \
+        if( kind < 3 || kind > 4 || n < 0 )                                                                          \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_quant<BD>( kind, dct, nullptr, nullptr, mf, bias, n, nz, (hipStream_t)stream ),      \
+                        "quant_dc_batch" );                                                                          \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_mb_dct_quant( int transform, const PT<BD>::pixel *fenc, intptr_t fs,              \
+                                                intptr_t ffs, const PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs,  \
+                                                int mbw, int mbh, int nframes, const PT<BD>::udctcoef *mf,          \
+                                                const PT<BD>::udctcoef *bias, PT<BD>::dctcoef *dct, int32_t *nz,     \
+                                                void *stream )                                                       \
+    {                                                                                                                \
+        if( ( transform != 4 && transform != 8 ) || mbw < 0 || mbh < 0 || nframes < 0 )                              \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_mb_dct_quant<BD>( transform, fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf,    \
+                                                 bias, dct, nz, (hipStream_t)stream ), "mb_dct_quant" );            \
+    }
+
+DEFINE_ENTRIES( 8 )
+DEFINE_ENTRIES( 10 )

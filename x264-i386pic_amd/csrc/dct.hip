@@ -1,0 +1,483 @@
+// Forward transforms and quantisation on gfx950.
+//
+// Semantics (all integer, bit-exact):
+//   sub4x4_dct     reference common/dct.c:157-189  (int16 temps at 8 bit)
+//   sub8x8/16x16   reference common/dct.c:191-205  (quadrant-major block order)
+//   *_dct_dc       reference common/dct.c:207-270
+//   sub8x8_dct8    reference common/dct.c:332-377  (column pass, int16 temps, row pass)
+//   dct4x4dc/2x4dc reference common/dct.c:47-76, 109-143
+//   QUANT_ONE      reference common/quant.c:50-57 (uint32 arithmetic), entries :59-104
+// Every block lives in one lane's registers; pixels arrive as aligned dwords
+// realigned with v_alignbyte_b32, coefficients leave as contiguous stores.
+#include "hipcommon.h"
+
+namespace x264hip {
+
+// ---------------------------------------------------------------- helpers
+template <int BD, int N>
+__device__ __forceinline__ void load_diff( int (&d)[N][N], const typename PT<BD>::pixel *a, intptr_t sa,
+                                           const typename PT<BD>::pixel *b, intptr_t sb )
+{
+    constexpr int NDW = N / PT<BD>::PPD;
+#pragma unroll
+    for( int y = 0; y < N; y++ )
+    {
+        uint32_t ra[NDW], rb[NDW];
+        load_packed<NDW>( a + y * sa, ra );
+        load_packed<NDW>( b + y * sb, rb );
+#pragma unroll
+        for( int x = 0; x < N; x++ )
+            d[y][x] = upix<BD>( ra[x / PT<BD>::PPD], x % PT<BD>::PPD ) - upix<BD>( rb[x / PT<BD>::PPD], x % PT<BD>::PPD );
+    }
+}
+
+// value stored to a dctcoef (int16 wrap at 8 bit), read back as int
+template <int BD> __device__ __forceinline__ int sto( int v ) { return (int)(typename PT<BD>::dctcoef)v; }
+
+// sub4x4_dct on a difference block: out[i*4+k] (reference order)
+template <int BD>
+__device__ __forceinline__ void dct4x4_core( int (&d)[4][4], int (&out)[16] )
+{
+    int tmp[4][4];   // tmp[k][i]: second index = source row
+#pragma unroll
+    for( int i = 0; i < 4; i++ )
+    {
+        int s03 = d[i][0] + d[i][3], s12 = d[i][1] + d[i][2];
+        int d03 = d[i][0] - d[i][3], d12 = d[i][1] - d[i][2];
+        tmp[0][i] = sto<BD>( s03 + s12 );
+        tmp[1][i] = sto<BD>( 2 * d03 + d12 );
+        tmp[2][i] = sto<BD>( s03 - s12 );
+        tmp[3][i] = sto<BD>( d03 - 2 * d12 );
+    }
+#pragma unroll
+    for( int i = 0; i < 4; i++ )
+    {
+        int s03 = tmp[i][0] + tmp[i][3], s12 = tmp[i][1] + tmp[i][2];
+        int d03 = tmp[i][0] - tmp[i][3], d12 = tmp[i][1] - tmp[i][2];
+        out[i * 4 + 0] = sto<BD>( s03 + s12 );
+        out[i * 4 + 1] = sto<BD>( 2 * d03 + d12 );
+        out[i * 4 + 2] = sto<BD>( s03 - s12 );
+        out[i * 4 + 3] = sto<BD>( d03 - 2 * d12 );
+    }
+}
+
+// DCT8_1D, reference common/dct.c:332-356 (src/dst via lambdas on indices)
+#define DCT8_1D_ARR( S, D )                                                             \
+    {                                                                                   \
+        int s07 = S( 0 ) + S( 7 ), s16 = S( 1 ) + S( 6 ), s25 = S( 2 ) + S( 5 ),        \
+            s34 = S( 3 ) + S( 4 );                                                      \
+        int a0 = s07 + s34, a1 = s16 + s25, a2 = s07 - s34, a3 = s16 - s25;             \
+        int d07 = S( 0 ) - S( 7 ), d16 = S( 1 ) - S( 6 ), d25 = S( 2 ) - S( 5 ),        \
+            d34 = S( 3 ) - S( 4 );                                                      \
+        int a4 = d16 + d25 + ( d07 + ( d07 >> 1 ) );                                    \
+        int a5 = d07 - d34 - ( d25 + ( d25 >> 1 ) );                                    \
+        int a6 = d07 + d34 - ( d16 + ( d16 >> 1 ) );                                    \
+        int a7 = d16 - d25 + ( d34 + ( d34 >> 1 ) );                                    \
+        D( 0, a0 + a1 );                                                                \
+        D( 1, a4 + ( a7 >> 2 ) );                                                       \
+        D( 2, a2 + ( a3 >> 1 ) );                                                       \
+        D( 3, a5 + ( a6 >> 2 ) );                                                       \
+        D( 4, a0 - a1 );                                                                \
+        D( 5, a6 - ( a5 >> 2 ) );                                                       \
+        D( 6, ( a2 >> 1 ) - a3 );                                                       \
+        D( 7, ( a4 >> 2 ) - a7 );                                                       \
+    }
+
+// sub8x8_dct8 on a difference block (d[y][x]); out[x*8+i] reference order
+template <int BD>
+__device__ __forceinline__ void dct8x8_core( int (&d)[8][8], int (&out)[64] )
+{
+    // column pass in place: column i, SRC(x) = d[x][i]
+#pragma unroll
+    for( int i = 0; i < 8; i++ )
+    {
+#define S( x ) d[x][i]
+#define D( x, v ) t[x] = sto<BD>( v )
+        int t[8];
+        DCT8_1D_ARR( S, D )
+#pragma unroll
+        for( int x = 0; x < 8; x++ )
+            d[x][i] = t[x];
+#undef S
+#undef D
+    }
+    // row pass: row i, SRC(x) = d[i][x], DST(x) = dct[x*8+i]
+#pragma unroll
+    for( int i = 0; i < 8; i++ )
+    {
+#define S( x ) d[i][x]
+#define D( x, v ) out[(x) * 8 + i] = sto<BD>( v )
+        DCT8_1D_ARR( S, D )
+#undef S
+#undef D
+    }
+}
+
+// QUANT_ONE, reference common/quant.c:50-57
+__device__ __forceinline__ int quant_one( int coef, uint32_t mf, uint32_t f )
+{
+    if( coef > 0 )
+        return (int)(((f + (uint32_t)coef) * mf) >> 16);
+    return -(int)(((f + (uint32_t)(-coef)) * mf) >> 16);
+}
+
+template <typename T, int N>
+__device__ __forceinline__ void store_coefs( T *dst, const int (&v)[N] )
+{
+#pragma unroll
+    for( int k = 0; k < N; k++ )
+        dst[k] = (T)v[k];
+}
+
+// ------------------------------------------------------- sub_dct_batch
+template <int BD, int KIND>
+__global__ __launch_bounds__( 256 ) void sub_dct_kernel( const typename PT<BD>::pixel *fenc, intptr_t fs,
+                                                         const typename PT<BD>::pixel *fdec, intptr_t ds,
+                                                         const int64_t *fo, const int64_t *dofs, int n,
+                                                         typename PT<BD>::dctcoef *out )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    constexpr int NSUB = KIND == 0 ? 1 : KIND == 1 ? 4 : KIND == 2 ? 16 : KIND == 5 ? 1 : KIND == 6 ? 4 : 1;
+    constexpr int OSZ = KIND == 0 ? 16 : KIND == 1 ? 64 : KIND == 2 ? 256 : KIND == 3 ? 4 : KIND == 4 ? 8 : KIND == 5 ? 64 : 256;
+    // one lane per (block, sub-block) for the multi-block kinds
+    const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = gi / NSUB;
+    const int sub = (int)(gi % NSUB);
+    if( i >= n )
+        return;
+    const typename PT<BD>::pixel *a = fenc + fo[i];
+    const typename PT<BD>::pixel *b = fdec + dofs[i];
+    dctcoef *o = out + i * OSZ;
+    if constexpr( KIND <= 2 )
+    {
+        // quadrant-major 4x4 order (dct.c:191-205)
+        int i8 = sub >> 2, i4 = sub & 3;
+        int x = (i8 & 1) * 8 + (i4 & 1) * 4, y = (i8 >> 1) * 8 + (i4 >> 1) * 4;
+        int d[4][4], c[16];
+        load_diff<BD, 4>( d, a + y * fs + x, fs, b + y * ds + x, ds );
+        dct4x4_core<BD>( d, c );
+        store_coefs( o + sub * 16, c );
+    }
+    else if constexpr( KIND == 3 || KIND == 4 )
+    {
+        // DC sums of 4x4 sub-blocks then the 2x2 / 2x4 butterflies
+        constexpr int NB = KIND == 3 ? 4 : 8;
+        int s[8];
+#pragma unroll
+        for( int k = 0; k < NB; k++ )
+        {
+            int d[4][4];
+            int x = (k & 1) * 4, y = (k >> 1) * 4;
+            load_diff<BD, 4>( d, a + y * fs + x, fs, b + y * ds + x, ds );
+            int t = 0;
+#pragma unroll
+            for( int yy = 0; yy < 4; yy++ )
+#pragma unroll
+                for( int xx = 0; xx < 4; xx++ )
+                    t += d[yy][xx];
+            s[k] = t;
+        }
+        if constexpr( KIND == 3 )
+        {
+            // sums are stored to dctcoef before the 2x2 transform (dct.c:218-231)
+            int e0 = sto<BD>( s[0] ), e1 = sto<BD>( s[1] ), e2 = sto<BD>( s[2] ), e3 = sto<BD>( s[3] );
+            int d0 = e0 + e1, d1 = e2 + e3, d2 = e0 - e1, d3 = e2 - e3;
+            o[0] = (dctcoef)(d0 + d1);
+            o[1] = (dctcoef)(d0 - d1);
+            o[2] = (dctcoef)(d2 + d3);
+            o[3] = (dctcoef)(d2 - d3);
+        }
+        else
+        {
+            int b0 = s[0] + s[1], b1 = s[2] + s[3], b2 = s[4] + s[5], b3 = s[6] + s[7];
+            int b4 = s[0] - s[1], b5 = s[2] - s[3], b6 = s[4] - s[5], b7 = s[6] - s[7];
+            int c0 = b0 + b1, c1 = b2 + b3, c2 = b4 + b5, c3 = b6 + b7;
+            int c4 = b0 - b1, c5 = b2 - b3, c6 = b4 - b5, c7 = b6 - b7;
+            o[0] = (dctcoef)(c0 + c1);
+            o[1] = (dctcoef)(c2 + c3);
+            o[2] = (dctcoef)(c0 - c1);
+            o[3] = (dctcoef)(c2 - c3);
+            o[4] = (dctcoef)(c4 - c5);
+            o[5] = (dctcoef)(c6 - c7);
+            o[6] = (dctcoef)(c4 + c5);
+            o[7] = (dctcoef)(c6 + c7);
+        }
+    }
+    else
+    {
+        int x = (sub & 1) * 8, y = (sub >> 1) * 8;
+        int d[8][8], c[64];
+        load_diff<BD, 8>( d, a + y * fs + x, fs, b + y * ds + x, ds );
+        dct8x8_core<BD>( d, c );
+        store_coefs( o + sub * 64, c );
+    }
+}
+
+template <int BD>
+hipError_t launch_sub_dct( int kind, const typename PT<BD>::pixel *fenc, intptr_t fs,
+                           const typename PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fo,
+                           const int64_t *dofs, int n, typename PT<BD>::dctcoef *dct, hipStream_t stream )
+{
+    static const int nsub[7] = { 1, 4, 16, 1, 1, 1, 4 };
+    if( kind < 0 || kind > 6 )
+        return hipErrorInvalidValue;
+    if( n <= 0 )
+        return hipSuccess;
+    int64_t lanes = (int64_t)n * nsub[kind];
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+    switch( kind )
+    {
+#define SD_CASE( K ) \
+        case K: hipLaunchKernelGGL( ( sub_dct_kernel<BD, K> ), g, blk, 0, stream, fenc, fs, fdec, ds, fo, dofs, n, dct ); break;
+        SD_CASE( 0 ) SD_CASE( 1 ) SD_CASE( 2 ) SD_CASE( 3 ) SD_CASE( 4 ) SD_CASE( 5 ) SD_CASE( 6 )
+#undef SD_CASE
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ dc_batch
+template <int BD>
+__global__ __launch_bounds__( 256 ) void dc4x4_kernel( typename PT<BD>::dctcoef *dct, int n )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    dctcoef *d = dct + i * 16;
+    int v[16], tmp[16];
+#pragma unroll
+    for( int k = 0; k < 16; k++ )
+        v[k] = d[k];
+#pragma unroll
+    for( int r = 0; r < 4; r++ )
+    {
+        int s01 = v[r * 4 + 0] + v[r * 4 + 1], d01 = v[r * 4 + 0] - v[r * 4 + 1];
+        int s23 = v[r * 4 + 2] + v[r * 4 + 3], d23 = v[r * 4 + 2] - v[r * 4 + 3];
+        tmp[0 * 4 + r] = sto<BD>( s01 + s23 );
+        tmp[1 * 4 + r] = sto<BD>( s01 - s23 );
+        tmp[2 * 4 + r] = sto<BD>( d01 - d23 );
+        tmp[3 * 4 + r] = sto<BD>( d01 + d23 );
+    }
+#pragma unroll
+    for( int r = 0; r < 4; r++ )
+    {
+        int s01 = tmp[r * 4 + 0] + tmp[r * 4 + 1], d01 = tmp[r * 4 + 0] - tmp[r * 4 + 1];
+        int s23 = tmp[r * 4 + 2] + tmp[r * 4 + 3], d23 = tmp[r * 4 + 2] - tmp[r * 4 + 3];
+        d[r * 4 + 0] = (dctcoef)((s01 + s23 + 1) >> 1);
+        d[r * 4 + 1] = (dctcoef)((s01 - s23 + 1) >> 1);
+        d[r * 4 + 2] = (dctcoef)((d01 - d23 + 1) >> 1);
+        d[r * 4 + 3] = (dctcoef)((d01 + d23 + 1) >> 1);
+    }
+}
+
+template <int BD>
+__global__ __launch_bounds__( 256 ) void dc2x4_kernel( typename PT<BD>::dctcoef *dct,
+                                                       typename PT<BD>::dctcoef *dct4x4, int n )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    dctcoef *o = dct + i * 8;
+    dctcoef *s = dct4x4 + i * 128;
+    int a[8];
+#pragma unroll
+    for( int k = 0; k < 8; k++ )
+        a[k] = s[k * 16];
+    int a0 = a[0] + a[1], a1 = a[2] + a[3], a2 = a[4] + a[5], a3 = a[6] + a[7];
+    int a4 = a[0] - a[1], a5 = a[2] - a[3], a6 = a[4] - a[5], a7 = a[6] - a[7];
+    int b0 = a0 + a1, b1 = a2 + a3, b2 = a4 + a5, b3 = a6 + a7;
+    int b4 = a0 - a1, b5 = a2 - a3, b6 = a4 - a5, b7 = a6 - a7;
+    o[0] = (dctcoef)(b0 + b1);
+    o[1] = (dctcoef)(b2 + b3);
+    o[2] = (dctcoef)(b0 - b1);
+    o[3] = (dctcoef)(b2 - b3);
+    o[4] = (dctcoef)(b4 - b5);
+    o[5] = (dctcoef)(b6 - b7);
+    o[6] = (dctcoef)(b4 + b5);
+    o[7] = (dctcoef)(b6 + b7);
+#pragma unroll
+    for( int k = 0; k < 8; k++ )
+        s[k * 16] = 0;
+}
+
+template <int BD>
+hipError_t launch_dc( int kind, typename PT<BD>::dctcoef *dct, typename PT<BD>::dctcoef *dct4x4, int n,
+                      hipStream_t stream )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (n + 255) / 256 );
+    if( kind == 0 )
+        hipLaunchKernelGGL( ( dc4x4_kernel<BD> ), g, blk, 0, stream, dct, n );
+    else if( kind == 1 )
+        hipLaunchKernelGGL( ( dc2x4_kernel<BD> ), g, blk, 0, stream, dct, dct4x4, n );
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// --------------------------------------------------------- quant_batch
+// KIND as X264HIP_QUANT_*: 0 8x8, 1 4x4, 2 4x4x4, 3 4x4_dc, 4 2x2_dc
+template <int BD, int KIND>
+__global__ __launch_bounds__( 256 ) void quant_kernel( typename PT<BD>::dctcoef *dct,
+                                                       const typename PT<BD>::udctcoef *__restrict__ mf,
+                                                       const typename PT<BD>::udctcoef *__restrict__ bias,
+                                                       int mf_dc, int bias_dc, int n, int32_t *nz )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    constexpr int N = KIND == 0 ? 64 : KIND == 2 ? 64 : KIND == 4 ? 4 : 16;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    dctcoef *d = dct + i * N;
+    int acc = 0, mask = 0;
+#pragma unroll
+    for( int k = 0; k < N; k++ )
+    {
+        uint32_t m, f;
+        if constexpr( KIND >= 3 )
+            m = (uint32_t)mf_dc, f = (uint32_t)bias_dc;
+        else
+            m = mf[k & (KIND == 0 ? 63 : 15)], f = bias[k & (KIND == 0 ? 63 : 15)];
+        int q = sto<BD>( quant_one( d[k], m, f ) );   // nz sees the stored value (quant.c:56)
+        d[k] = (dctcoef)q;
+        acc |= q;
+        if constexpr( KIND == 2 )
+            if( (k & 15) == 15 )
+            {
+                mask |= (acc != 0) << (k >> 4);
+                acc = 0;
+            }
+    }
+    if( nz )
+        nz[i] = KIND == 2 ? mask : (acc != 0);
+}
+
+template <int BD>
+hipError_t launch_quant( int kind, typename PT<BD>::dctcoef *dct, const typename PT<BD>::udctcoef *mf,
+                         const typename PT<BD>::udctcoef *bias, int mf_dc, int bias_dc, int n, int32_t *nz,
+                         hipStream_t stream )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (n + 255) / 256 );
+    switch( kind )
+    {
+#define Q_CASE( K ) \
+        case K: hipLaunchKernelGGL( ( quant_kernel<BD, K> ), g, blk, 0, stream, dct, mf, bias, mf_dc, bias_dc, n, nz ); break;
+        Q_CASE( 0 ) Q_CASE( 1 ) Q_CASE( 2 ) Q_CASE( 3 ) Q_CASE( 4 )
+#undef Q_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ------------------------------------------------- fused mb_dct_quant
+// transform 4: 16 lanes per macroblock, one 4x4 block per lane.
+// transform 8: 4 lanes per macroblock, one 8x8 block per lane.
+template <int BD, int T>
+__global__ __launch_bounds__( 256 ) void mb_dct_quant_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                              intptr_t fs, intptr_t ffs,
+                                                              const typename PT<BD>::pixel *__restrict__ pred,
+                                                              intptr_t ps, intptr_t pfs, int mbw, int mbh,
+                                                              int nframes,
+                                                              const typename PT<BD>::udctcoef *__restrict__ mf,
+                                                              const typename PT<BD>::udctcoef *__restrict__ bias,
+                                                              typename PT<BD>::dctcoef *__restrict__ dct,
+                                                              int32_t *__restrict__ nz )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    constexpr int LPM = T == 4 ? 16 : 4;      // lanes per macroblock
+    const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)nframes * mbh * mbw * LPM;
+    const bool live = gi < total;
+    const int64_t mb = live ? gi / LPM : 0;
+    const int blk = (int)(gi % LPM);
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+    const typename PT<BD>::pixel *a = fenc + f * ffs + (intptr_t)16 * mby * fs + 16 * mbx;
+    const typename PT<BD>::pixel *b = pred + f * pfs + (intptr_t)16 * mby * ps + 16 * mbx;
+    int nzbit = 0;
+    if( live )
+    {
+        if constexpr( T == 4 )
+        {
+            int i8 = blk >> 2, i4 = blk & 3;
+            int x = (i8 & 1) * 8 + (i4 & 1) * 4, y = (i8 >> 1) * 8 + (i4 >> 1) * 4;
+            int d[4][4], c[16];
+            load_diff<BD, 4>( d, a + y * fs + x, fs, b + y * ps + x, ps );
+            dct4x4_core<BD>( d, c );
+            int acc = 0;
+#pragma unroll
+            for( int k = 0; k < 16; k++ )
+            {
+                c[k] = sto<BD>( quant_one( c[k], mf[k], bias[k] ) );
+                acc |= c[k];
+            }
+            store_coefs( dct + mb * 256 + blk * 16, c );
+            nzbit = acc != 0;
+        }
+        else
+        {
+            int x = (blk & 1) * 8, y = (blk >> 1) * 8;
+            int d[8][8], c[64];
+            load_diff<BD, 8>( d, a + y * fs + x, fs, b + y * ps + x, ps );
+            dct8x8_core<BD>( d, c );
+            int acc = 0;
+#pragma unroll
+            for( int k = 0; k < 64; k++ )
+            {
+                c[k] = sto<BD>( quant_one( c[k], mf[k], bias[k] ) );
+                acc |= c[k];
+            }
+            store_coefs( dct + mb * 256 + blk * 64, c );
+            nzbit = acc != 0;
+        }
+    }
+    // gather the per-block nonzero flags of each macroblock (LPM divides 64)
+    uint64_t bal = __ballot( nzbit );
+    const int lane = threadIdx.x & 63;
+    if( live && blk == 0 )
+        nz[mb] = (int32_t)((bal >> (lane & ~(LPM - 1))) & ((1ull << LPM) - 1));
+}
+
+template <int BD>
+hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                const typename PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs, int mbw, int mbh,
+                                int nframes, const typename PT<BD>::udctcoef *mf,
+                                const typename PT<BD>::udctcoef *bias, typename PT<BD>::dctcoef *dct, int32_t *nz,
+                                hipStream_t stream )
+{
+    int lpm = transform == 4 ? 16 : transform == 8 ? 4 : 0;
+    if( !lpm )
+        return hipErrorInvalidValue;
+    int64_t lanes = (int64_t)nframes * mbh * mbw * lpm;
+    if( lanes <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+    if( transform == 4 )
+        hipLaunchKernelGGL( ( mb_dct_quant_kernel<BD, 4> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh,
+                            nframes, mf, bias, dct, nz );
+    else
+        hipLaunchKernelGGL( ( mb_dct_quant_kernel<BD, 8> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh,
+                            nframes, mf, bias, dct, nz );
+    return hipGetLastError();
+}
+
+#define INST( BD )                                                                                                 \
+    template hipError_t launch_sub_dct<BD>( int, const PT<BD>::pixel *, intptr_t, const PT<BD>::pixel *, intptr_t, \
+                                            const int64_t *, const int64_t *, int, PT<BD>::dctcoef *, hipStream_t ); \
+    template hipError_t launch_dc<BD>( int, PT<BD>::dctcoef *, PT<BD>::dctcoef *, int, hipStream_t );             \
+    template hipError_t launch_quant<BD>( int, PT<BD>::dctcoef *, const PT<BD>::udctcoef *,                        \
+                                          const PT<BD>::udctcoef *, int, int, int, int32_t *, hipStream_t );        \
+    template hipError_t launch_mb_dct_quant<BD>( int, const PT<BD>::pixel *, intptr_t, intptr_t,                   \
+                                                 const PT<BD>::pixel *, intptr_t, intptr_t, int, int, int,        \
+                                                 const PT<BD>::udctcoef *, const PT<BD>::udctcoef *,              \
+                                                 PT<BD>::dctcoef *, int32_t *, hipStream_t );
+INST( 8 )
+INST( 10 )
+
+} // namespace x264hip

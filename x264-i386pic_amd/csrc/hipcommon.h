@@ -1,0 +1,102 @@
+// Internal header shared by the gfx950 kernels and the C-ABI layer.
+// Pixel/coefficient types per bit depth follow reference common/common.h:93-109.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace x264hip {
+
+template <int BD> struct PT;
+template <> struct PT<8>
+{
+    using pixel = uint8_t;
+    using dctcoef = int16_t;
+    using udctcoef = uint16_t;
+    using sadt = uint16_t;               // 16x16 SAD <= 65280 fits
+    static constexpr int PIXEL_MAX = 255;
+    static constexpr int PPD = 4;        // pixels per dword
+};
+template <> struct PT<10>
+{
+    using pixel = uint16_t;
+    using dctcoef = int32_t;
+    using udctcoef = uint32_t;
+    using sadt = uint32_t;               // 16x16 SAD <= 261888
+    static constexpr int PIXEL_MAX = 1023;
+    static constexpr int PPD = 2;
+};
+
+// block sizes, reference common/pixel.h:55-59
+__host__ __device__ constexpr int pix_w( int i ) { return i == 0 || i == 1 ? 16 : i <= 4 ? 8 : 4; }
+__host__ __device__ constexpr int pix_h( int i )
+{
+    return i == 0 || i == 2 ? 16 : i == 1 || i == 3 || i == 5 ? 8 : i == 4 || i == 6 ? 4 : 16;
+}
+
+// Load NDW packed dwords (NDW*PPD pixels) starting at an arbitrary pixel address.
+// Reads dword-aligned words only; the extra word needed for a misaligned start
+// is fetched only when the start is misaligned (otherwise the last word is
+// re-read), so no byte outside the dwords holding requested pixels is touched.
+template <int NDW>
+__device__ __forceinline__ void load_packed( const void *p, uint32_t (&out)[NDW] )
+{
+    uintptr_t a = (uintptr_t)p;
+    const uint32_t *base = (const uint32_t *)(a & ~(uintptr_t)3);
+    uint32_t sh = (uint32_t)(a & 3);
+    uint32_t w[NDW + 1];
+#pragma unroll
+    for( int i = 0; i < NDW; i++ )
+        w[i] = base[i];
+    w[NDW] = base[sh ? NDW : NDW - 1];
+#pragma unroll
+    for( int i = 0; i < NDW; i++ )
+        out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
+}
+
+// packed sum of absolute differences: v_sad_u8 (4 x u8) / v_sad_u16 (2 x u16)
+template <int BD> __device__ __forceinline__ uint32_t sadp( uint32_t a, uint32_t b, uint32_t acc );
+template <> __device__ __forceinline__ uint32_t sadp<8>( uint32_t a, uint32_t b, uint32_t acc )
+{
+    return __builtin_amdgcn_sad_u8( a, b, acc );
+}
+template <> __device__ __forceinline__ uint32_t sadp<10>( uint32_t a, uint32_t b, uint32_t acc )
+{
+    return __builtin_amdgcn_sad_u16( a, b, acc );
+}
+
+// k-th pixel of a packed dword
+template <int BD> __device__ __forceinline__ int upix( uint32_t w, int k )
+{
+    return BD == 8 ? (int)((w >> (8 * k)) & 0xff) : (int)((w >> (16 * k)) & 0xffff);
+}
+
+} // namespace x264hip
+
+// ---- launchers implemented in the .hip files (all enqueue on `stream`) ----
+namespace x264hip {
+template <int BD>
+hipError_t launch_cmp_batch( int op, int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs,
+                             const typename PT<BD>::pixel *ref, intptr_t rs, const int64_t *fenc_off,
+                             const int64_t *ref_off, int n, int32_t *scores, hipStream_t stream );
+template <int BD>
+hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                           const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                           int nframes, int range, typename PT<BD>::sadt *table, hipStream_t stream );
+template <int BD>
+hipError_t launch_sub_dct( int kind, const typename PT<BD>::pixel *fenc, intptr_t fs,
+                           const typename PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fenc_off,
+                           const int64_t *fdec_off, int n, typename PT<BD>::dctcoef *dct, hipStream_t stream );
+template <int BD>
+hipError_t launch_dc( int kind, typename PT<BD>::dctcoef *dct, typename PT<BD>::dctcoef *dct4x4, int n,
+                      hipStream_t stream );
+template <int BD>
+hipError_t launch_quant( int kind, typename PT<BD>::dctcoef *dct, const typename PT<BD>::udctcoef *mf,
+                         const typename PT<BD>::udctcoef *bias, int mf_dc, int bias_dc, int n, int32_t *nz,
+                         hipStream_t stream );
+template <int BD>
+hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                const typename PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs, int mbw, int mbh,
+                                int nframes, const typename PT<BD>::udctcoef *mf,
+                                const typename PT<BD>::udctcoef *bias, typename PT<BD>::dctcoef *dct, int32_t *nz,
+                                hipStream_t stream );
+} // namespace x264hip
