@@ -27,9 +27,12 @@ sys.path.insert(0, ROOT)
 from __graft_entry__ import load_package  # noqa: E402
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md): 256 CUs x 4 SIMD-32 at
-# 2.4 GHz -> 78.6 T VALU lane-ops/s; v_sad_u8 folds 4 byte absdiffs per lane-op.
+# 2.4 GHz -> 78.6 T full-rate VALU lane-ops/s.  The byte-SAD instructions are not
+# full rate (measured, profiles/r01_sad_peak.txt, r01_qsad_probe.txt): v_sad_u8
+# (4 absdiffs) issues at 1/2 and v_qsad_pk_u16_u8 (16 absdiffs) at 1/8 of it, so
+# both top out at 78.6e12 * 2 = 157.3 T byte-absdiffs/s — the SAD roofline.
 VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
-SAD_PEAK_ABSDIFF = 4 * VALU_LANE_OPS          # 314.6 T absdiff/s
+SAD_PEAK_ABSDIFF = 2 * VALU_LANE_OPS          # 157.3 T absdiff/s
 HBM_PEAK = 8.0e12
 
 
@@ -112,7 +115,7 @@ def main():
     planes, stride, origin = synth.make_sequence(F + 1, W, Hp, 8, seed=1 + rank)
     dev = torch.from_numpy(planes).cuda()
     fstride = planes[0].size
-    table = torch.empty((F, mbh, mbw, 2 * R + 1, 2 * R + 1), dtype=torch.int16, device="cuda")
+    table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
 
     def step():
         x.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, table=table,
@@ -127,11 +130,11 @@ def main():
     absdiff_per_launch = F * mbw * mbh * cand_per_mb * 256
     achieved = absdiff_per_launch / (ev_ms * 1e-3)
     roof = {
-        "kernel": "me_full_sad16_kernel<8,%d>" % R,
+        "kernel": "me_full_sad16_v3_kernel<%d>" % R,
         "bound": "valu",
         "achieved": achieved / 1e12,
         "peak": SAD_PEAK_ABSDIFF / 1e12,
-        "unit": "T absdiff/s (v_sad_u8 lane-op = 4 absdiff)",
+        "unit": "T byte-absdiff/s (algorithmic: 256 per 16x16 candidate)",
         "frac": achieved / SAD_PEAK_ABSDIFF,
         "traffic": None,
         "algorithmic_bytes_per_launch": F * (mbw * mbh * 256 + mbw * mbh * 256 + mbw * mbh * cand_per_mb * 2),

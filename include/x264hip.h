@@ -282,13 +282,15 @@ int x264hip_##BD##_pixel_cmp_batch( int op, int i_pixel,                        
 /* exhaustive integer-pel search table (the candidate set of reference                          \
  * encoder/me.c:618-631 before mv costs).  For every 16x16 macroblock of                        \
  * n_frames (fenc, ref) pairs:                                                                  \
- *   table[f][mb][j][i] = sad_16x16( fenc_f + 16*(mby*fenc_stride + mbx), fenc_stride,          \
- *                                  ref_f + (16*mby + j - range)*ref_stride + 16*mbx + i - range, \
- *                                  ref_stride ),   0 <= i,j <= 2*range                         \
- * i.e. mx = i - range, my = j - range, raster order my-major.  ref must be a                   \
+ *   table[((f*mb_height + mby)*mb_width + mbx)*(2*range+1)*P + j*P + i]                          \
+ *     = sad_16x16( fenc_f + 16*(mby*fenc_stride + mbx), fenc_stride,                           \
+ *                  ref_f + (16*mby + j - range)*ref_stride + 16*mbx + i - range, ref_stride )   \
+ * for 0 <= i,j <= 2*range, i.e. mx = i - range, my = j - range, raster order                   \
+ * my-major, row pitch P = (2*range+1 + 3) & ~3 (entries i > 2*range are padding;              \
+ * the 8-bit kernel stores the SADs of mx = range+1.. there).  ref must be a                    \
  * padded plane (x264 PADH/PADV = 32, reference common/frame.h:32-35); every                    \
- * window row is read from x-range-3 to x+15+range+3, so the caller keeps                      \
- * range+3 <= the horizontal padding.  range is one of 4, 8, 16, 24. */                         \
+ * window row is read from x-range to x+15+range+8, so the caller keeps                        \
+ * range+8 <= the horizontal padding (PADH = 32).  range is one of 4, 8, 16, 24. */             \
 int x264hip_##BD##_me_search_full( const pixel *fenc, intptr_t fenc_stride,                     \
                                    intptr_t fenc_frame_stride,                                  \
                                    const pixel *ref, intptr_t ref_stride,                       \

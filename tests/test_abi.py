@@ -1,0 +1,131 @@
+"""CPU: the C ABI boundary.
+
+* libx264hip.so loads and exports every function include/x264hip.h declares;
+* the re-declared tables have the reference's field order and layout (checked
+  by compiling the header with gcc and comparing with the ctypes mirror);
+* the host-side CQM restatement in the product equals the oracle's.
+No kernel is launched (no GPU in this container)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, ensure_built, load_package
+
+HEADER = os.path.join(ROOT, "include", "x264hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    names = set()
+    # per-bit-depth entries inside X264HIP_DECLARE_ENTRIES
+    m = re.search(r"#define X264HIP_DECLARE_ENTRIES(.*?)\n\n", src, re.S)
+    for n in re.findall(r"\bx264hip_##BD##_(\w+)\s*\(", m.group(1)):
+        for bd in (8, 10):
+            names.add(f"x264hip_{bd}_{n}")
+    # plain prototypes outside the macros
+    body = re.sub(r"#define X264HIP_DECLARE_\w+.*?\n\n", "", src, flags=re.S)
+    for n in re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(x264hip_\w+)\s*\(", body, re.M):
+        names.add(n)
+    return sorted(names)
+
+
+def test_header_declares_entries():
+    names = declared_functions()
+    assert "x264hip_init" in names and "x264hip_8_me_search_full" in names
+    assert "x264hip_10_pixel_init" in names and "x264hip_8_quant_init_hip" in names
+    assert len(names) >= 30
+
+
+def test_library_exports_every_declared_symbol():
+    so = ensure_built("hip")
+    out = subprocess.run(["nm", "-D", "--defined-only", so], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [n for n in declared_functions() if n not in exported]
+    assert not missing, missing
+
+
+def test_library_loads_and_resolves():
+    x = load_package()
+    L = x.lib()
+    for n in declared_functions():
+        assert getattr(L, n) is not None
+
+
+def test_library_is_gfx950_code():
+    so = ensure_built("hip")
+    out = subprocess.run(["strings", so], capture_output=True, text=True).stdout
+    assert "gfx950" in out
+
+
+_PROBE = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "x264hip.h"
+#define P(T, F) printf(#T " " #F " %zu\n", offsetof(T, F));
+int main(void) {
+    printf("pixel8 %zu\npixel10 %zu\ndct8 %zu\ndct10 %zu\nquant8 %zu\nquant10 %zu\n",
+           sizeof(x264hip_8_pixel_function_t), sizeof(x264hip_10_pixel_function_t),
+           sizeof(x264hip_8_dct_function_t), sizeof(x264hip_10_dct_function_t),
+           sizeof(x264hip_8_quant_function_t), sizeof(x264hip_10_quant_function_t));
+    P(x264hip_8_pixel_function_t, sad_x3) P(x264hip_8_pixel_function_t, satd_x4)
+    P(x264hip_8_pixel_function_t, ads) P(x264hip_8_pixel_function_t, intra_sad_x9_8x8)
+    P(x264hip_8_dct_function_t, sub16x16_dct8) P(x264hip_8_dct_function_t, dct2x4dc)
+    P(x264hip_8_quant_function_t, quant_2x2_dc) P(x264hip_8_quant_function_t, coeff_level_run)
+    P(x264hip_8_quant_function_t, trellis_cabac_chroma_422_dc)
+    return 0;
+}
+"""
+
+
+def test_table_layout_matches_ctypes(tmp_path):
+    c = tmp_path / "probe.c"
+    c.write_text(_PROBE)
+    exe = tmp_path / "probe"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(c), "-o", str(exe)], check=True)
+    lines = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    vals = {}
+    for ln in lines:
+        if ln:
+            *k, v = ln.split()
+            vals[" ".join(k)] = int(v)
+    x = load_package()
+    assert vals["pixel8"] == vals["pixel10"] == ctypes.sizeof(x.PixelFunctions)
+    assert vals["dct8"] == vals["dct10"] == ctypes.sizeof(x.DctFunctions)
+    assert vals["quant8"] == vals["quant10"] == ctypes.sizeof(x.QuantFunctions)
+    assert vals["x264hip_8_pixel_function_t sad_x3"] == x.PixelFunctions.sad_x3.offset
+    assert vals["x264hip_8_pixel_function_t satd_x4"] == x.PixelFunctions.satd_x4.offset
+    assert vals["x264hip_8_pixel_function_t ads"] == x.PixelFunctions.ads.offset
+    assert vals["x264hip_8_pixel_function_t intra_sad_x9_8x8"] == x.PixelFunctions.intra_sad_x9_8x8.offset
+    assert vals["x264hip_8_dct_function_t sub16x16_dct8"] == x.DctFunctions.sub16x16_dct8.offset
+    assert vals["x264hip_8_dct_function_t dct2x4dc"] == x.DctFunctions.dct2x4dc.offset
+    assert vals["x264hip_8_quant_function_t quant_2x2_dc"] == x.QuantFunctions.quant_2x2_dc.offset
+    assert vals["x264hip_8_quant_function_t coeff_level_run"] == x.QuantFunctions.coeff_level_run.offset
+    # reference field counts: pixel.h:78-144 has 8*8+7+4+2*7+... pointers
+    n_ptr = vals["pixel8"] // 8
+    assert n_ptr == 8 * 7 + 7 + 4 + 7 * 2 + 1 + 1 + 1 + 4 + 4 + 4 + 3 + 7 * 4 + 7 + 15 + 3 + 6
+
+
+def test_init_without_hip_flag_leaves_table_empty():
+    """x264hip_*_init(cpu without X264HIP_CPU_HIP) fills nothing (no CPU entries)."""
+    x = load_package()
+    tab = x.PixelFunctions()
+    x.lib().x264hip_8_pixel_init(0, ctypes.byref(tab))
+    assert not any(bool(tab.sad[i]) for i in range(8))
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_product_cqm_equals_oracle(oracle, bd):
+    import checkasm_bufs as cb
+    x = load_package()
+    cb.srand(cb.SEED)
+    for i_cqm in range(6):
+        lists = cb.cqm_lists(i_cqm, bd)
+        for dz in ((21, 11), (0, 0), (5, 30)):
+            got = x.cqm_init(bd, lists, dz[0], dz[1])
+            want = oracle.cqm_init(bd, lists, dz[0], dz[1])
+            for g, w in zip(got, want):
+                assert np.array_equal(g, w), (i_cqm, dz)

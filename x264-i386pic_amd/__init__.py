@@ -273,14 +273,20 @@ def pixel_cmp_batch(op, i_pixel, fenc, fenc_stride, ref, ref_stride, fenc_off, r
     return scores
 
 
+def me_table_pitch(rng):
+    """row pitch of a full-search table: 2*range+1 rounded up to a multiple of 4"""
+    return (2 * rng + 1 + 3) // 4 * 4
+
+
 def me_search_full(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height,
                    nframes, rng=16, table=None, fenc_frame_stride=None, ref_frame_stride=None):
-    """Exhaustive 16x16 SAD table [nframes, mb_height, mb_width, 2r+1, 2r+1] (x264hip_*_me_search_full)."""
+    """Exhaustive 16x16 SAD table [nframes, mb_height, mb_width, 2r+1, pitch] (x264hip_*_me_search_full);
+    pitch = align4(2r+1), entries [..., 2r+1:] are padding."""
     import torch
     bd = _pix_bd(fenc)
     w = 2 * rng + 1
     if table is None:
-        table = torch.empty((nframes, mb_height, mb_width, w, w),
+        table = torch.empty((nframes, mb_height, mb_width, w, me_table_pitch(rng)),
                             dtype=torch.int16 if bd == 8 else torch.int32, device=fenc.device)
     ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
     rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)

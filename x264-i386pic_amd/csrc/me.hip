@@ -13,6 +13,7 @@
 // amortised over 16 candidates.  fenc (16 rows) stays in VGPRs for the whole
 // lane lifetime.  Candidate my finishes at row my+15 and is stored then.
 #include "hipcommon.h"
+#include <stdlib.h>
 #include <utility>
 
 namespace x264hip {
@@ -39,7 +40,7 @@ __device__ __forceinline__ void me_row( const typename PT<BD>::pixel *rb, intptr
         for( int k = 0; k < NDW; k++ )
             a = sadp<BD>( F[r][k], rr[k], a );
         if( r == 15 )
-            out[c * W] = (typename PT<BD>::sadt)a;
+            out[c * ((W + 3) & ~3)] = (typename PT<BD>::sadt)a;
         else
             acc[c & 15] = a;
     }
@@ -81,10 +82,209 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_kernel( const typename PT
         load_packed<NDW>( fe + r * fs, F[r] );
 
     const typename PT<BD>::pixel *rb = ref + f * rfs + (intptr_t)(16 * mby - R) * rs + 16 * mbx - R + col;
-    typename PT<BD>::sadt *out = table + mb * (W * W) + col;
+    typename PT<BD>::sadt *out = table + mb * (W * ((W + 3) & ~3)) + col;
 
     uint32_t acc[16];
     me_rows<BD, R>( rb, rs, F, acc, out, std::make_integer_sequence<int, 2 * R + 16>{} );
+}
+
+
+// ---------------------------------------------------------------------------
+// Variant 2: two lanes per candidate column.  Lane h (0/1) keeps only fenc rows
+// 8h..8h+7 in VGPRs and walks ref rows 8h + (0 .. 2R+7), so both lanes of a
+// column finish candidate my at the same step; their partial sums meet through
+// one DPP quad-perm add.  Halving the resident fenc halves the VGPR footprint
+// and lets the 10-bit path keep its fenc rows in registers too.
+// Requirements (checked by the launcher, else variant 1 runs): fenc base and
+// both strides are dword multiples, so a lane's byte shift is the same on
+// every row and rows are plain dword loads (the 5th dword of a row is read
+// unconditionally: it lies inside the plane padding, range + 4 <= PAD).
+template <int BD, int R, int Y>
+__device__ __forceinline__ void me_row2( const uint32_t *__restrict__ rbase, int rs_dw, uint32_t sh,
+                                         const uint32_t (&F)[8][16 / PT<BD>::PPD], uint32_t (&acc)[8],
+                                         typename PT<BD>::sadt *out )
+{
+    constexpr int NDW = 16 / PT<BD>::PPD;
+    constexpr int W = 2 * R + 1;
+    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    const uint32_t *row = rbase + Y * rs_dw;
+    uint32_t w[NDW + 1], rr[NDW];
+#pragma unroll
+    for( int k = 0; k <= NDW; k++ )
+        w[k] = row[k];
+#pragma unroll
+    for( int k = 0; k < NDW; k++ )
+        rr[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], sh );
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint32_t a = r == 0 ? 0u : acc[c & 7];
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            a = sadp<BD>( F[r][k], rr[k], a );
+        if( r == 7 )
+        {
+            // partner lane (lane ^ 1) holds the other 8 rows: quad_perm [1,0,3,2];
+            // both lanes store the same total to the same address (no branch)
+            uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a, 0xB1, 0xF, 0xF, false );
+            out[c * ((W + 3) & ~3)] = (typename PT<BD>::sadt)(a + other);
+        }
+        else
+            acc[c & 7] = a;
+    }
+}
+
+template <int BD, int R, int... Ys>
+__device__ __forceinline__ void me_rows2( const uint32_t *__restrict__ rbase, int rs_dw, uint32_t sh,
+                                          const uint32_t (&F)[8][16 / PT<BD>::PPD], uint32_t (&acc)[8],
+                                          typename PT<BD>::sadt *out, std::integer_sequence<int, Ys...> )
+{
+    ( me_row2<BD, R, Ys>( rbase, rs_dw, sh, F, acc, out ), ... );
+}
+
+template <int BD, int R>
+__global__ __launch_bounds__( 256 ) void me_full_sad16_v2_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                                  intptr_t fs, intptr_t ffs,
+                                                                  const typename PT<BD>::pixel *__restrict__ ref,
+                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                  int nframes, typename PT<BD>::sadt *__restrict__ table )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int W = 2 * R + 1;
+    constexpr int NDW = 16 / PT<BD>::PPD;
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * W);
+    if( slot >= total )
+        return;                                 // pairs never straddle: 2W is even
+    const int h = (int)(slot & 1);
+    const int col = (int)((slot >> 1) % W);
+    const int64_t mb = slot / (2 * W);
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+
+    uint32_t F[8][NDW];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs * sizeof(pixel) / 4);
+#pragma unroll
+    for( int r = 0; r < 8; r++ )
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+
+    const pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + 8 * h - R) * rs + 16 * mbx - R + col;
+    const uint32_t sh = (uint32_t)((uintptr_t)rb & 3);
+    const uint32_t *rbase = (const uint32_t *)((const char *)rb - sh);
+    typename PT<BD>::sadt *out = table + mb * (W * ((W + 3) & ~3)) + col;
+    uint32_t acc[8];
+    me_rows2<BD, R>( rbase, (int)(rs * sizeof(pixel) / 4), sh, F, acc, out,
+                     std::make_integer_sequence<int, 2 * R + 8>{} );
+}
+
+// ---------------------------------------------------------------------------
+// Variant 3 (8 bit): four candidate columns per lane with v_qsad_pk_u16_u8.
+// One qsad compares a fenc dword with the four byte-shifted dwords of an 8-byte
+// ref window and accumulates four packed u16 SADs, so a lane covers columns
+// 4j..4j+3 with no realignment at all; as in variant 2 the lane pair (h = 0/1)
+// splits the 16 fenc rows and meets through a DPP add (u16 halves cannot carry:
+// each half-sum <= 8*16*255 = 32640).  Per ref row a lane issues 2 loads for
+// 4 columns x 8 candidates, 4x fewer than variant 1.  Rows of the table have
+// pitch align4(2R+1); the 0..3 trailing entries hold the SADs of mx = R+1..
+typedef uint64_t u64x2a4 __attribute__( ( ext_vector_type( 2 ), aligned( 4 ) ) );
+
+template <int R, int Y>
+__device__ __forceinline__ void me_row3( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
+                                         uint64_t (&acc)[8], uint64_t *out )
+{
+    constexpr int P4 = (2 * R + 1 + 3) / 4;     // row pitch in u64 units
+    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    const uint32_t *row = rbase + Y * rs_dw;
+    // two overlapping 16-byte loads give the four 8-byte windows as aligned
+    // register pairs (w0w1, w2w3 | w1w2, w3w4): no register shuffling
+    const u64x2a4 e = *(const u64x2a4 *)row;
+    const u64x2a4 o = *(const u64x2a4 *)(row + 1);
+    const uint64_t win[4] = { e[0], o[0], e[1], o[1] };
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint64_t a = r == 0 ? 0ull : acc[c & 7];
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            a = __builtin_amdgcn_qsad_pk_u16_u8( win[k], F[r][k], a );
+        if( r == 7 )
+        {
+            uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+            lo += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)lo, 0xB1, 0xF, 0xF, false );
+            hi += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)hi, 0xB1, 0xF, 0xF, false );
+            out[c * P4] = ((uint64_t)hi << 32) | lo;
+        }
+        else
+            acc[c & 7] = a;
+    }
+}
+
+template <int R, int... Ys>
+__device__ __forceinline__ void me_rows3( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
+                                          uint64_t (&acc)[8], uint64_t *out, std::integer_sequence<int, Ys...> )
+{
+    ( me_row3<R, Ys>( rbase, rs_dw, F, acc, out ), ... );
+}
+
+template <int R>
+__global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
+                                                                  intptr_t ffs, const uint8_t *__restrict__ ref,
+                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                  int nframes, uint16_t *__restrict__ table )
+{
+    constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
+    constexpr int P = 4 * G;                    // table row pitch
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
+    if( slot >= total )
+        return;
+    const int h = (int)(slot & 1);
+    const int grp = (int)((slot >> 1) % G);
+    const int64_t mb = slot / (2 * G);
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+
+    uint32_t F[8][4];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs / 4);
+#pragma unroll
+    for( int r = 0; r < 8; r++ )
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+    const uint32_t *rbase =
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h - R) * rs + 16 * mbx - R + 4 * grp);
+    uint64_t *out = (uint64_t *)(table + mb * ((2 * R + 1) * P) + 4 * grp);
+    uint64_t acc[8];
+    me_rows3<R>( rbase, (int)(rs / 4), F, acc, out, std::make_integer_sequence<int, 2 * R + 8>{} );
+}
+
+// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT=1 forces the
+// single-lane-per-column kernel, default 2
+static int me_variant()
+{
+    const char *e = getenv( "X264HIP_ME_VARIANT" );
+    return e ? atoi( e ) : 0;
+}
+
+template <int R, typename P, typename T>
+static void launch_v3( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
+                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table )
+{
+    if constexpr( sizeof( P ) == 1 )
+        hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
+                            nframes, table );
 }
 
 template <int BD>
@@ -92,15 +292,35 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
                            int nframes, int range, typename PT<BD>::sadt *table, hipStream_t stream )
 {
-    const int64_t lanes = (int64_t)nframes * mbh * mbw * (2 * range + 1);
+    int variant = me_variant();
+    if( !variant )
+        variant = BD == 8 ? 3 : 1;
+    if( BD != 8 && variant == 3 )
+        variant = 1;
+    // variants 2/3 need dword-aligned fenc rows, dword-multiple strides and (3) a
+    // dword-aligned ref plane
+    if( (((uintptr_t)fenc | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
+          (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant == 3 ? (uintptr_t)ref : 0)) & 3) )
+        variant = 1;
+    const int64_t groups = variant == 3 ? 2 * ((2 * range + 1 + 3) / 4) : variant == 2 ? 2 * (2 * range + 1)
+                                                                                      : (2 * range + 1);
+    const int64_t lanes = (int64_t)nframes * mbh * mbw * groups;
     if( lanes <= 0 )
         return hipSuccess;
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
     switch( range )
     {
 #define ME_CASE( R ) \
-        case R: hipLaunchKernelGGL( ( me_full_sad16_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
-                                    mbw, mbh, nframes, table ); break;
+        case R:                                                                                                   \
+            if( variant == 3 )                                                                                    \
+                launch_v3<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table );           \
+            else if( variant == 2 )                                                                               \
+                hipLaunchKernelGGL( ( me_full_sad16_v2_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, \
+                                    rfs, mbw, mbh, nframes, table );                                              \
+            else                                                                                                  \
+                hipLaunchKernelGGL( ( me_full_sad16_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs,   \
+                                    rfs, mbw, mbh, nframes, table );                                              \
+            break;
         ME_CASE( 4 ) ME_CASE( 8 ) ME_CASE( 16 ) ME_CASE( 24 )
 #undef ME_CASE
         default: return hipErrorInvalidValue;
