@@ -65,18 +65,13 @@ def dist_setup():
 
 
 def barrier(world):
-    if world > 1:
-        import torch.distributed as dist
-        dist.barrier()
+    from x264hip import dist as xd
+    xd.barrier()
 
 
 def max_over_ranks(v, world):
-    if world == 1:
-        return v
-    import torch.distributed as dist
-    t = torch.tensor([v], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    from x264hip import dist as xd
+    return xd.reduce_max(v, device="cuda")
 
 
 def timed(fn, steps, warmup, world):
@@ -111,8 +106,11 @@ def main():
     mbw, mbh = (W + 15) // 16, (H + 15) // 16
     Hp = mbh * 16                                   # x264 pads the height to whole MBs
     cand_per_mb = (2 * R + 1) ** 2
-    # F+1 synthetic frames per rank; pair k = (frame k+1, ref frame k); rank-seeded
-    planes, stride, origin = synth.make_sequence(F + 1, W, Hp, 8, seed=1 + rank)
+    # one synthetic sequence of world*F pairs; pair k = (frame k+1, ref frame k);
+    # rank r owns pairs [r*F, (r+1)*F) and builds only frames r*F .. r*F+F
+    from x264hip import dist as xd
+    p0, p1 = xd.frame_shard(world * F, world, rank)
+    planes, stride, origin = synth.make_sequence(p1 - p0 + 1, W, Hp, 8, start=p0)
     dev = torch.from_numpy(planes).cuda()
     fstride = planes[0].size
     table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")

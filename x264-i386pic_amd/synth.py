@@ -1,7 +1,9 @@
 """Synthetic luma sequences for parity tests and bench.py.
 
 Frame 0 is seeded uniform noise (numpy PCG64) box-smoothed 5x5; frame k is
-frame 0 displaced by (3k, 2k) pixels plus +-2 noise (seed k).  Each frame is
+frame 0 displaced by (3k', 2k') pixels, k' = k mod 32, plus +-2 noise (seed k)
+(the motion wraps every 32 frames so every frame is a window of one fixed-size
+texture).  Each frame is
 stored like an x264 plane: PAD (=32, reference common/frame.h:32-33) pixels of
 edge replication on every side (x264_frame_expand_border semantics), rows of
 ``stride`` pixels.
@@ -9,6 +11,7 @@ edge replication on every side (x264_frame_expand_border semantics), rows of
 import numpy as np
 
 PAD = 32
+PERIOD = 32
 
 
 def plane_stride(width, pad=PAD):
@@ -25,24 +28,28 @@ def _texture(h, w, bitdepth, seed=1):
     return (box + 12) // 25
 
 
-def make_sequence(nframes, width, height, bitdepth=8, pad=PAD, seed=1):
-    """Returns (planes[nframes, height + 2*pad, stride] numpy, stride, origin).
+def make_sequence(nframes, width, height, bitdepth=8, pad=PAD, seed=1, start=0):
+    """Frames start .. start+nframes-1 of the sequence.
 
-    origin = element offset of pixel (0, 0) inside one frame."""
+    Returns (planes[nframes, height + 2*pad, stride] numpy, stride, origin);
+    origin = element offset of pixel (0, 0) inside one frame.  Any slice of the
+    sequence is identical to the same frames of a longer generation, so ranks
+    can each build their own shard (x264hip.dist.frame_shard)."""
     pmax = (1 << bitdepth) - 1
-    maxdx, maxdy = 3 * nframes, 2 * nframes
-    tex = _texture(height + maxdy, width + maxdx, bitdepth, seed)
+    tex = _texture(height + 2 * PERIOD, width + 3 * PERIOD, bitdepth, seed)
     stride = plane_stride(width, pad)
     dt = np.uint8 if bitdepth == 8 else np.uint16
     out = np.zeros((nframes, height + 2 * pad, stride), dt)
-    for k in range(nframes):
+    for i in range(nframes):
+        k = start + i
         rng = np.random.Generator(np.random.PCG64(1000 + k))
-        win = tex[2 * k:2 * k + height, 3 * k:3 * k + width]
+        kk = k % PERIOD
+        win = tex[2 * kk:2 * kk + height, 3 * kk:3 * kk + width]
         if k:
             win = win + rng.integers(-2, 3, size=win.shape)
         win = np.clip(win, 0, pmax)
         full = np.pad(win, ((pad, pad), (pad, stride - width - pad)), mode="edge")
-        out[k] = full.astype(dt)
+        out[i] = full.astype(dt)
     return out, stride, pad * stride + pad
 
 
