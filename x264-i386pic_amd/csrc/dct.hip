@@ -10,6 +10,7 @@
 // Every block lives in one lane's registers; pixels arrive as aligned dwords
 // realigned with v_alignbyte_b32, coefficients leave as contiguous stores.
 #include "hipcommon.h"
+#include <stdlib.h>
 
 namespace x264hip {
 
@@ -113,12 +114,29 @@ __device__ __forceinline__ void dct8x8_core( int (&d)[8][8], int (&out)[64] )
     }
 }
 
-// QUANT_ONE, reference common/quant.c:50-57
+// QUANT_ONE, reference common/quant.c:50-57, branch-free: s = 0 for coef > 0,
+// -1 otherwise (coef == 0 takes the reference's negative branch too), so
+// |coef| = (coef ^ s) - s and the result is (q ^ s) - s.
 __device__ __forceinline__ int quant_one( int coef, uint32_t mf, uint32_t f )
 {
-    if( coef > 0 )
-        return (int)(((f + (uint32_t)coef) * mf) >> 16);
-    return -(int)(((f + (uint32_t)(-coef)) * mf) >> 16);
+    const int s = (coef > 0) - 1;
+    const uint32_t mag = (uint32_t)((coef ^ s) - s);
+    const int q = (int)(((f + mag) * mf) >> 16);
+    return (q ^ s) - s;
+}
+
+// k-th entry of a uniform mf / bias row, read as dwords so the loads are
+// scalar (s_load) even for the 16-bit tables of 8-bit depth
+template <typename U>
+__device__ __forceinline__ uint32_t urow( const U *__restrict__ p, int k )
+{
+    if constexpr( sizeof( U ) == 2 )
+    {
+        const uint32_t w = ((const uint32_t *)p)[k >> 1];
+        return (k & 1) ? w >> 16 : w & 0xffff;
+    }
+    else
+        return p[k];
 }
 
 template <typename T, int N>
@@ -414,7 +432,7 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_kernel( const typename PT<
 #pragma unroll
             for( int k = 0; k < 16; k++ )
             {
-                c[k] = sto<BD>( quant_one( c[k], mf[k], bias[k] ) );
+                c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
                 acc |= c[k];
             }
             store_coefs( dct + mb * 256 + blk * 16, c );
@@ -430,7 +448,7 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_kernel( const typename PT<
 #pragma unroll
             for( int k = 0; k < 64; k++ )
             {
-                c[k] = sto<BD>( quant_one( c[k], mf[k], bias[k] ) );
+                c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
                 acc |= c[k];
             }
             store_coefs( dct + mb * 256 + blk * 64, c );
@@ -444,6 +462,115 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_kernel( const typename PT<
         nz[mb] = (int32_t)((bal >> (lane & ~(LPM - 1))) & ((1ull << LPM) - 1));
 }
 
+// Strip mapping (default): one wave = one 256-pixel-wide strip of one MB row
+// (16 macroblocks).  For T=4 lane l owns the 4-pixel column l of the strip and
+// walks its 4 block rows, so every row load is 64 contiguous dwords (fully
+// coalesced); for T=8 lane l owns 8x8 column l%32 of block row l/32 (two
+// 256-byte row segments per load).  The per-MB nz mask is OR-combined across
+// the MB's lanes with DPP / lane swaps.
+template <int BD, int T, bool STAGE>
+__global__ __launch_bounds__( 256 ) void mb_dct_quant_strip_kernel(
+    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
+    const typename PT<BD>::pixel *__restrict__ pred, intptr_t ps, intptr_t pfs, int mbw, int mbh, int nframes,
+    const typename PT<BD>::udctcoef *__restrict__ mf, const typename PT<BD>::udctcoef *__restrict__ bias,
+    typename PT<BD>::dctcoef *__restrict__ dct, int32_t *__restrict__ nz )
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int spr = (mbw + 15) >> 4;
+    if( wave >= (int64_t)nframes * mbh * spr )
+        return;                                               // wave-uniform
+    const int strip = (int)(wave % spr);
+    const int64_t t = wave / spr;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+    const typename PT<BD>::pixel *a0 = fenc + f * ffs + (intptr_t)16 * mby * fs + 256 * strip;
+    const typename PT<BD>::pixel *b0 = pred + f * pfs + (intptr_t)16 * mby * ps + 256 * strip;
+    const int64_t mbrow = (f * mbh + mby) * (int64_t)mbw;
+    // STAGE: the wave's 16 MBs of coefficients are assembled in LDS and leave as
+    // one contiguous run of 16 B per lane stores
+    using dctcoef = typename PT<BD>::dctcoef;
+    __shared__ dctcoef lds[STAGE ? 4 * 16 * 256 : 1];
+    dctcoef *stage = lds + (threadIdx.x >> 6) * (16 * 256);
+    if constexpr( T == 4 )
+    {
+        const int mbx = strip * 16 + (lane >> 2);
+        const bool live = mbx < mbw;
+        const int cx = lane & 3;                              // 4-px column inside the MB
+        int mask = 0;
+#pragma unroll
+        for( int by = 0; by < 4; by++ )
+        {
+            if( live )
+            {
+                int d[4][4], c[16];
+                load_diff<BD, 4>( d, a0 + 4 * by * fs + 4 * lane, fs, b0 + 4 * by * ps + 4 * lane, ps );
+                dct4x4_core<BD>( d, c );
+                int acc = 0;
+#pragma unroll
+                for( int k = 0; k < 16; k++ )
+                {
+                    c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
+                    acc |= c[k];
+                }
+                const int i8 = (by >> 1) * 2 + (cx >> 1), i4 = (by & 1) * 2 + (cx & 1);
+                if constexpr( STAGE )
+                    store_coefs( stage + (lane >> 2) * 256 + (i8 * 4 + i4) * 16, c );
+                else
+                    store_coefs( dct + (mbrow + mbx) * 256 + (i8 * 4 + i4) * 16, c );
+                mask |= (acc != 0) << (4 * i8 + i4);
+            }
+        }
+        // OR over the four lanes of the MB: quad_perm [1,0,3,2] then [2,3,0,1]
+        mask |= __builtin_amdgcn_update_dpp( 0, mask, 0xB1, 0xF, 0xF, false );
+        mask |= __builtin_amdgcn_update_dpp( 0, mask, 0x4E, 0xF, 0xF, false );
+        if( live && cx == 0 )
+            nz[mbrow + mbx] = mask;
+    }
+    else
+    {
+        const int bx = lane & 31, by = lane >> 5;             // 8x8 block column / row in the strip
+        const int mbx = strip * 16 + (bx >> 1);
+        const bool live = mbx < mbw;
+        int mask = 0;
+        if( live )
+        {
+            int d[8][8], c[64];
+            load_diff<BD, 8>( d, a0 + 8 * by * fs + 8 * bx, fs, b0 + 8 * by * ps + 8 * bx, ps );
+            dct8x8_core<BD>( d, c );
+            int acc = 0;
+#pragma unroll
+            for( int k = 0; k < 64; k++ )
+            {
+                c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
+                acc |= c[k];
+            }
+            const int i8 = by * 2 + (bx & 1);
+            if constexpr( STAGE )
+                store_coefs( stage + (bx >> 1) * 256 + i8 * 64, c );
+            else
+                store_coefs( dct + (mbrow + mbx) * 256 + i8 * 64, c );
+            mask = (acc != 0) << i8;
+        }
+        mask |= __builtin_amdgcn_update_dpp( 0, mask, 0xB1, 0xF, 0xF, false );   // lane ^ 1
+        mask |= __shfl_xor( mask, 32 );                                           // other block row
+        if( live && by == 0 && !(bx & 1) )
+            nz[mbrow + mbx] = mask;
+    }
+    if constexpr( STAGE )
+    {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
+        // the wave's MBs are consecutive in the table: copy n*256 coefficients
+        const int nmb = min( 16, mbw - strip * 16 );
+        const int nvec = nmb * 256 * (int)sizeof( dctcoef ) / 16;
+        const uint4 *src = (const uint4 *)stage;
+        uint4 *dst = (uint4 *)(dct + (mbrow + strip * 16) * 256);
+        for( int i = lane; i < nvec; i += 64 )
+            dst[i] = src[i];
+    }
+}
+
 template <int BD>
 hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                                 const typename PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs, int mbw, int mbh,
@@ -454,6 +581,28 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
     int lpm = transform == 4 ? 16 : transform == 8 ? 4 : 0;
     if( !lpm )
         return hipErrorInvalidValue;
+    const char *ev = getenv( "X264HIP_DQ_VARIANT" );
+    if( !ev || atoi( ev ) != 1 )
+    {
+        // default: strip kernel, one wave per 16 MBs of a row
+        int64_t waves = (int64_t)nframes * mbh * ((mbw + 15) / 16);
+        if( waves <= 0 )
+            return hipSuccess;
+        dim3 blk( 256 ), g( (unsigned)((waves + 3) / 4) );
+        const bool stage = !ev || atoi( ev ) != 2;
+#define DQ_STRIP( T, S ) hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, S> ), g, blk, 0, stream, fenc, fs, ffs, \
+                                             pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz )
+        if( transform == 4 )
+        {
+            if( stage ) DQ_STRIP( 4, true ); else DQ_STRIP( 4, false );
+        }
+        else
+        {
+            if( stage ) DQ_STRIP( 8, true ); else DQ_STRIP( 8, false );
+        }
+#undef DQ_STRIP
+        return hipGetLastError();
+    }
     int64_t lanes = (int64_t)nframes * mbh * mbw * lpm;
     if( lanes <= 0 )
         return hipSuccess;

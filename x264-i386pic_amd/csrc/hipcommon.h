@@ -40,9 +40,9 @@ __host__ __device__ constexpr int pix_h( int i )
 template <int NDW>
 __device__ __forceinline__ void load_packed( const void *p, uint32_t (&out)[NDW] )
 {
-    uintptr_t a = (uintptr_t)p;
-    const uint32_t *base = (const uint32_t *)(a & ~(uintptr_t)3);
-    uint32_t sh = (uint32_t)(a & 3);
+    // keep the pointer's provenance (global) so hipcc emits global_load, not flat_load
+    uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    const uint32_t *base = (const uint32_t *)((const char *)p - sh);
     uint32_t w[NDW + 1];
 #pragma unroll
     for( int i = 0; i < NDW; i++ )
