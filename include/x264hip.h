@@ -298,6 +298,28 @@ int x264hip_##BD##_me_search_full( const pixel *fenc, intptr_t fenc_stride,     
                                    int mb_width, int mb_height, int n_frames, int range,        \
                                    sadt *table, void *stream );                                 \
                                                                                                 \
+/* half-pel planes (reference x264_frame_filter common/mc.c:704-726 over the                 \
+ * whole frame, hpel_filter mc.c:173-196, then x264_frame_expand_border_filtered               \
+ * common/frame.c:599-625): for n_frames padded planes (PAD = 32, pointers at                   \
+ * pixel (0,0) of frame 0, common stride and frame stride) writes the H, V and                  \
+ * centre planes over [-32, width+32) x [-32, height+32).  width, height: whole MBs. */          \
+int x264hip_##BD##_hpel_filter( const pixel *src, pixel *dst_h, pixel *dst_v, pixel *dst_c,     \
+                                intptr_t stride, intptr_t frame_stride, int width, int height,  \
+                                int n_frames, void *stream );                                   \
+                                                                                                \
+/* quarter-pel candidate costs of refine_subpel (reference encoder/me.c:865-992):               \
+ * scores[i] = op( fenc + fenc_off[i], fenc_stride, get_ref(qx, qy) ) with op                   \
+ * X264HIP_CMP_SAD or X264HIP_CMP_SATD of size i_pixel and get_ref the unweighted               \
+ * reference MC (mc.c:221-249, pixel_avg of two half-pel planes): (qx, qy) =                   \
+ * qpel_xy[2i], qpel_xy[2i+1] is the block's top-left in quarter pixels of the                  \
+ * plane (4*x + mvx).  planes: full-pel, H, V, centre, all with ref_stride. */                  \
+int x264hip_##BD##_subpel_cmp_batch( int op, int i_pixel, const pixel *fenc,                    \
+                                     intptr_t fenc_stride, const pixel *fpel,                   \
+                                     const pixel *hpel_h, const pixel *hpel_v,                  \
+                                     const pixel *hpel_c, intptr_t ref_stride,                  \
+                                     const int64_t *fenc_off, const int32_t *qpel_xy,           \
+                                     int n, int32_t *scores, void *stream );                    \
+                                                                                                \
 /* block lists of the reference transforms (dct.c), device arrays;                             \
  * dct holds n consecutive outputs of the selected entry's size. */                             \
 int x264hip_##BD##_sub_dct_batch( int kind, const pixel *fenc, intptr_t fenc_stride,            \

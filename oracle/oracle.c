@@ -660,3 +660,53 @@ const pixel *FN(get_ref)( pixel *dst, intptr_t *dst_stride, const pixel *const s
     *dst_stride = stride;
     return src1;
 }
+
+/* whole-frame half-pel planes: x264_frame_filter (reference common/mc.c:704-726)
+ * over every MB row (rows [-8, H+8), columns [-8, W+8) of hpel_filter) followed by
+ * x264_frame_expand_border_filtered (common/frame.c:599-625: edges taken from
+ * x = -4 / W+3 and y = -8 / H+7, padh 28, padv 24).  Pointers at pixel (0,0),
+ * planes padded by 32. */
+void FN(frame_filter)( const pixel *src, pixel *dh, pixel *dv, pixel *dc, intptr_t stride, int width, int height )
+{
+    int16_t *buf = malloc( (width + 48) * sizeof(int16_t) );
+    intptr_t offs = -8 * stride - 8;
+    FN(hpel_filter)( dh + offs, dv + offs, dc + offs, src + offs, stride, width + 16, height + 16, buf );
+    free( buf );
+    pixel *planes[3] = { dh, dv, dc };
+    for( int p = 0; p < 3; p++ )
+    {
+        pixel *pl = planes[p];
+        for( int y = -8; y < height + 8; y++ )
+        {
+            pixel *row = pl + y * stride;
+            for( int x = -32; x < -4; x++ )
+                row[x] = row[-4];
+            for( int x = width + 4; x < width + 32; x++ )
+                row[x] = row[width + 3];
+        }
+        for( int y = -32; y < -8; y++ )
+            memcpy( pl + y * stride - 32, pl - 8 * stride - 32, (width + 64) * sizeof(pixel) );
+        for( int y = height + 8; y < height + 32; y++ )
+            memcpy( pl + y * stride - 32, pl + (height + 7) * stride - 32, (width + 64) * sizeof(pixel) );
+    }
+}
+
+/* list form of the qpel candidate costs (get_ref then sad / satd), semantics of
+ * x264hip_*_subpel_cmp_batch */
+void FN(subpel_list)( int op, int i_pixel, const pixel *fenc, intptr_t fs, const pixel *p0, const pixel *p1,
+                      const pixel *p2, const pixel *p3, intptr_t rs, const int64_t *fenc_off, const int32_t *qxy,
+                      int n, int32_t *scores )
+{
+    const pixel *planes[4] = { p0, p1, p2, p3 };
+    pixel tmp[16 * 16];
+    for( int i = 0; i < n; i++ )
+    {
+        intptr_t ts = 16;
+        int qx = qxy[2*i], qy = qxy[2*i+1];
+        /* get_ref takes the mv relative to a block origin: use origin (0,0) and the
+         * absolute qpel position as the mv */
+        const pixel *r = FN(get_ref)( tmp, &ts, planes, rs, qx, qy, pixel_w[i_pixel], pixel_h[i_pixel] );
+        const pixel *a = fenc + fenc_off[i];
+        scores[i] = op == 0 ? FN(sad)( i_pixel, a, fs, r, ts ) : FN(satd)( i_pixel, a, fs, r, ts );
+    }
+}

@@ -176,3 +176,49 @@ def cqm_init(bd, lists, dz_inter=21, dz_intra=11, transform_8x8=True):
     if transform_8x8:
         q8m, q8b = tables(def8, lists[4:], 2, 0, 64)
     return q4m, q4b, q8m, q8b
+
+
+def hpel_planes(plane2d, pad, width, height, bd):
+    """H, V, C half-pel planes of a padded plane [h+2pad, stride] (reference
+    hpel_filter mc.c:173-196 + border re-expansion frame.c:599-625), computed by
+    vectorised 6-tap filtering on the interior x in [-4, W+4), y in [-8, H+8),
+    then edge clamping over the padding."""
+    p = plane2d.astype(np.int64)
+    pm = (1 << bd) - 1
+    padv = -10 * pm if bd > 9 else 0
+    ys = np.arange(-8, height + 8) + pad
+    xs = np.arange(-4, width + 4) + pad
+    taps = np.array([1, -5, 20, 20, -5, 1])
+
+    def vt(yy, xx):          # vertical tap at rows yy (centre rows y..y+1 as in TAPFILTER(src, stride))
+        return sum(t * p[np.ix_(yy + k - 2, xx)] for k, t in enumerate(taps))
+
+    v = vt(ys, xs)
+    hsum = sum(t * p[np.ix_(ys, xs + k - 2)] for k, t in enumerate(taps))
+    vwide = vt(ys, np.arange(-6, width + 7) + pad)            # intermediates for the centre filter
+    b = wrap(vwide + padv, 8)                                  # int16 storage (mc.c:181)
+    csum = sum(t * b[:, k:k + width + 8] for k, t in enumerate(taps))
+    out = []
+    for val in (np.clip((hsum + 16) >> 5, 0, pm), np.clip((v + 16) >> 5, 0, pm),
+                np.clip((csum - 32 * padv + 512) >> 10, 0, pm)):
+        full = np.zeros_like(p)
+        yy = np.clip(np.arange(-pad, height + pad), -8, height + 7) + 8
+        xx = np.clip(np.arange(-pad, width + pad), -4, width + 3) + 4
+        full[pad - pad:height + 2 * pad, 0:width + 2 * pad] = val[np.ix_(yy, xx)]
+        out.append(full.astype(plane2d.dtype))
+    return out
+
+
+HPEL_REF0 = [0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1]
+HPEL_REF1 = [0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2]
+
+
+def get_ref(planes_flat, origin, stride, qx, qy, w, h):
+    """unweighted get_ref (mc.c:221-249) at absolute quarter-pel position (qx, qy)."""
+    idx = ((qy & 3) << 2) + (qx & 3)
+    off = origin + (qy >> 2) * stride + (qx >> 2)
+    a = block(planes_flat[HPEL_REF0[idx]], off + ((qy & 3) == 3) * stride, stride, w, h)
+    if idx & 5:
+        b = block(planes_flat[HPEL_REF1[idx]], off + ((qx & 3) == 3), stride, w, h)
+        return (a + b + 1) >> 1
+    return a

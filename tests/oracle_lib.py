@@ -64,6 +64,8 @@ for _bd in (8, 10):
     _f(_bd, "mb_dct_quant", [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "hpel_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int, _P])
     _f(_bd, "get_ref", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int], _P)
+    _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
+    _f(_bd, "subpel_list", [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
@@ -189,3 +191,21 @@ def mb_dct_quant_mt(transform, fenc, f_origin, fs, pred, p_origin, ps, mbw, mbh,
     used = _L.oracle8_mb_dct_quant_mt(transform, _addr(fenc, f_origin), fs, _addr(pred, p_origin), ps, mbw, mbh,
                                       _addr(m), _addr(b), _addr(dct), _addr(nz), nthreads)
     return dct, nz, used
+
+
+def frame_filter(bd, plane, origin, stride, width, height):
+    """half-pel planes (H, V, C) of one padded plane (flat numpy), same layout."""
+    outs = [np.zeros_like(plane) for _ in range(3)]
+    getattr(_L, f"oracle{bd}_frame_filter")(_addr(plane, origin), _addr(outs[0], origin), _addr(outs[1], origin),
+                                           _addr(outs[2], origin), stride, width, height)
+    return outs
+
+
+def subpel_list(bd, op, i_pixel, fenc, fs, planes, p_origin, rs, fenc_off, qxy):
+    fo = np.ascontiguousarray(fenc_off, np.int64)
+    q = np.ascontiguousarray(qxy, np.int32)
+    out = np.zeros(len(fo), np.int32)
+    getattr(_L, f"oracle{bd}_subpel_list")(_OPS.get(op, op), i_pixel, _addr(fenc), fs,
+                                          *[_addr(p, p_origin) for p in planes], rs, _addr(fo), _addr(q),
+                                          len(fo), _addr(out))
+    return out

@@ -223,3 +223,41 @@ def test_mb_dct_quant_small(oracle, bd, transform):
                 mask = sum(int(v) << k for k, v in enumerate(z))
             mb = mby * 3 + mbx
             assert np.array_equal(dct[mb].astype(np.int64), q.ravel()) and nz[mb] == mask, (mby, mbx)
+
+
+def _synth():
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "synth", os.path.join(os.path.dirname(__file__), "..", "x264-i386pic_amd", "synth.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_frame_filter_and_subpel(oracle, bd):
+    """half-pel planes (oracle loops vs vectorised numpy) and qpel get_ref costs."""
+    synth = _synth()
+    W, H = 48, 32
+    planes, stride, origin = synth.random_planes(2, W, H, bd, seed=bd)
+    p = planes[0]
+    hvc = oracle.frame_filter(bd, p.ravel().copy(), origin, stride, W, H)
+    want = nr.hpel_planes(p, 32, W, H, bd)
+    for a, b in zip(hvc, want):
+        assert np.array_equal(a.reshape(p.shape)[:, :W + 64], b[:, :W + 64])
+    flat = [p.ravel()] + [x for x in hvc]
+    rs = np.random.default_rng(bd)
+    for i_pixel in (0, 3, 6):
+        w, h = nr.SIZES[i_pixel]
+        qxy, fo = [], []
+        for _ in range(200):
+            bx, by = int(rs.integers(0, W - w + 1)), int(rs.integers(0, H - h + 1))
+            qxy.append((4 * bx + int(rs.integers(-40, 41)), 4 * by + int(rs.integers(-40, 41))))
+            fo.append(p.size + origin + by * stride + bx)
+        for op in ("sad", "satd"):
+            got = oracle.subpel_list(bd, op, i_pixel, planes.ravel(), stride, flat, origin, stride, fo, qxy)
+            for k, ((qx, qy), f) in enumerate(zip(qxy, fo)):
+                r = nr.get_ref(flat, origin, stride, qx, qy, w, h)
+                a = nr.block(planes.ravel(), f, stride, w, h)
+                assert got[k] == (nr.sad(a, r) if op == "sad" else nr.satd(a, r))

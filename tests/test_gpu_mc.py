@@ -1,0 +1,61 @@
+"""GPU parity of the subpel-search inputs: half-pel planes (x264hip_*_hpel_filter,
+reference x264_frame_filter + x264_frame_expand_border_filtered) and quarter-pel
+SAD / SATD candidates through get_ref (x264hip_*_subpel_cmp_batch, reference
+refine_subpel encoder/me.c:865-992)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a, bd):
+    return torch.from_numpy(a.view(np.int16) if bd == 10 else a).cuda()
+
+
+def _host(t, bd):
+    a = t.cpu().numpy()
+    return a.view(np.uint16) if bd == 10 else a
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("size", [(1920, 1088), (80, 48)])
+def test_hpel_filter(hip, oracle, bd, size):
+    from x264hip import synth
+    W, H = size
+    gen = synth.make_sequence if W > 100 else synth.random_planes
+    planes, stride, origin = gen(2, W, H, bd)
+    dev = _dev(planes, bd)
+    outs = hip.hpel_filter(dev, origin, stride, W, H)
+    for f in range(2):
+        want = oracle.frame_filter(bd, planes[f].ravel().copy(), origin, stride, W, H)
+        for o, w, name in zip(outs, want, "hvc"):
+            got = _host(o, bd)[f][:, :W + 64]
+            w2 = w.reshape(planes[f].shape)[:, :W + 64]
+            assert np.array_equal(got, w2), (f, name, np.argwhere(got != w2)[:4])
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("op", [0, 2])
+def test_subpel_cmp_random(hip, oracle, bd, op):
+    from x264hip import synth
+    W, H = 160, 96
+    planes, stride, origin = synth.random_planes(2, W, H, bd, seed=11)
+    dev = _dev(planes, bd)
+    hv = hip.hpel_filter(dev[:1], origin, stride, W, H)
+    ref_planes = [dev[0]] + [o[0] for o in hv]
+    host_planes = [planes[0].ravel()] + [_host(o, bd)[0].ravel() for o in hv]
+    rs = np.random.default_rng(op + bd)
+    for i_pixel in range(8):
+        n = 3000
+        bw, bh = hip.PIXEL_SIZES[i_pixel]
+        bx = rs.integers(0, W - bw + 1, n)
+        by = rs.integers(0, H - bh + 1, n)
+        mvx = rs.integers(-4 * 20, 4 * 20 + 1, n)                # +-20 px incl. every qpel phase
+        mvy = rs.integers(-4 * 20, 4 * 20 + 1, n)
+        qxy = np.stack([4 * bx + mvx, 4 * by + mvy], 1).astype(np.int32)
+        fo = (planes[0].size + origin + by * stride + bx).astype(np.int64)   # fenc = frame 1
+        got = hip.subpel_cmp_batch(op, i_pixel, dev.view(-1), stride, ref_planes, origin, stride,
+                                   torch.from_numpy(fo).cuda(), torch.from_numpy(qxy).cuda()).cpu().numpy()
+        want = oracle.subpel_list(bd, op, i_pixel, planes.ravel(), stride, host_planes, origin, stride, fo, qxy)
+        assert np.array_equal(got, want), (i_pixel, np.argwhere(got != want)[:3])

@@ -23,7 +23,7 @@ import os
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "me_table_pitch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP",
 ]
@@ -193,9 +193,11 @@ def _declare(L):
         f("dc_batch").argtypes = [_c.c_int, _P, _P, _c.c_int, _P]
         f("quant_batch").argtypes = [_c.c_int, _P, _P, _P, _c.c_int, _P, _P]
         f("quant_dc_batch").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P]
+        f("hpel_filter").argtypes = [_P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P]
+        f("subpel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, _c.c_int, _P, _P]
         f("mb_dct_quant").argtypes = [_c.c_int, _P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int,
                                       _P, _P, _P, _P, _P]
-        for n in ("pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
+        for n in ("pixel_cmp_batch", "me_search_full", "hpel_filter", "subpel_cmp_batch", "sub_dct_batch", "dc_batch", "quant_batch",
                   "quant_dc_batch", "mb_dct_quant"):
             f(n).restype = _c.c_int
 
@@ -366,3 +368,32 @@ def mb_dct_quant(transform, fenc, fenc_origin, fenc_stride, pred, pred_origin, p
         transform, _ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(pred, pred_origin), pred_stride, pfs,
         mb_width, mb_height, nframes, _ptr(mf), _ptr(bias), _ptr(dct), _ptr(nz), _stream()), "mb_dct_quant")
     return dct, nz
+
+
+def hpel_filter(planes, origin, stride, width, height, outs=None):
+    """Half-pel planes (H, V, centre) of a stack of padded planes [n, height+64, stride]
+    (x264hip_*_hpel_filter); returns three tensors of the same shape."""
+    import torch
+    bd = _pix_bd(planes)
+    n = planes.shape[0] if planes.dim() == 3 else 1
+    if outs is None:
+        outs = [torch.zeros_like(planes) for _ in range(3)]
+    fs = planes[0].numel() if planes.dim() == 3 else 0
+    _rc(getattr(lib(), f"x264hip_{bd}_hpel_filter")(
+        _ptr(planes, origin), _ptr(outs[0], origin), _ptr(outs[1], origin), _ptr(outs[2], origin), stride, fs,
+        width, height, n, _stream()), "hpel_filter")
+    return outs
+
+
+def subpel_cmp_batch(op, i_pixel, fenc, fenc_stride, planes, ref_origin, ref_stride, fenc_off, qpel_xy, scores=None):
+    """Quarter-pel candidate costs (x264hip_*_subpel_cmp_batch): planes = [fpel, H, V, C]
+    tensors (same layout), qpel_xy int32 [n, 2] absolute quarter-pel positions."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = fenc_off.numel()
+    if scores is None:
+        scores = torch.empty(n, dtype=torch.int32, device=fenc.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_subpel_cmp_batch")(
+        op, i_pixel, _ptr(fenc), fenc_stride, *[_ptr(p, ref_origin) for p in planes], ref_stride,
+        _ptr(fenc_off), _ptr(qpel_xy), n, _ptr(scores), _stream()), "subpel_cmp_batch")
+    return scores

@@ -443,6 +443,27 @@ static int map_err( hipError_t e, const char *where )
         return map_err( launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, table,           \
                                             (hipStream_t)stream ), "me_search_full" );                               \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_hpel_filter( const PT<BD>::pixel *src, PT<BD>::pixel *dh, PT<BD>::pixel *dv,       \
+                                               PT<BD>::pixel *dc, intptr_t stride, intptr_t fstride, int width,     \
+                                               int height, int nframes, void *stream )                              \
+    {                                                                                                                \
+        if( width <= 0 || height <= 0 || nframes < 0 || (width | height) & 15 )                                      \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_hpel_filter<BD>( src, dh, dv, dc, stride, fstride, width, height, nframes,            \
+                                                (hipStream_t)stream ), "hpel_filter" );                              \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_subpel_cmp_batch( int op, int i_pixel, const PT<BD>::pixel *fenc, intptr_t fs,    \
+                                                    const PT<BD>::pixel *p0, const PT<BD>::pixel *p1,                \
+                                                    const PT<BD>::pixel *p2, const PT<BD>::pixel *p3, intptr_t rs,   \
+                                                    const int64_t *fo, const int32_t *qxy, int n, int32_t *scores,   \
+                                                    void *stream )                                                   \
+    {                                                                                                                \
+        if( ( op != X264HIP_CMP_SAD && op != X264HIP_CMP_SATD ) || i_pixel < 0 || i_pixel > 7 || n < 0 )             \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
+        return map_err( launch_subpel_cmp<BD>( op, i_pixel, fenc, fs, planes, rs, fo, qxy, n, scores,                \
+                                               (hipStream_t)stream ), "subpel_cmp_batch" );                          \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_sub_dct_batch( int kind, const PT<BD>::pixel *fenc, intptr_t fs,                  \
                                                  const PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fo,          \
                                                  const int64_t *dofs, int n, PT<BD>::dctcoef *dct, void *stream )    \

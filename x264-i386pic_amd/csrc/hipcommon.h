@@ -99,4 +99,12 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
                                 int nframes, const typename PT<BD>::udctcoef *mf,
                                 const typename PT<BD>::udctcoef *bias, typename PT<BD>::dctcoef *dct, int32_t *nz,
                                 hipStream_t stream );
+template <int BD>
+hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD>::pixel *dh,
+                               typename PT<BD>::pixel *dv, typename PT<BD>::pixel *dc, intptr_t stride,
+                               intptr_t fstride, int width, int height, int nframes, hipStream_t stream );
+template <int BD>
+hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs,
+                              const typename PT<BD>::pixel *const planes[4], intptr_t rs, const int64_t *fenc_off,
+                              const int32_t *qxy, int n, int32_t *scores, hipStream_t stream );
 } // namespace x264hip

@@ -1,0 +1,268 @@
+// Motion-compensation inputs of the subpel search on gfx950:
+//  * half-pel planes (reference x264_frame_filter common/mc.c:704-726, hpel_filter
+//    mc.c:173-196, x264_frame_expand_border_filtered common/frame.c:599-625);
+//  * SAD / SATD of blocks fetched at quarter-pel positions (get_ref, mc.c:221-249,
+//    with x264_hpel_ref0/1 of common/tables.c:183-184 and pixel_avg mc.c:49-61),
+//    i.e. the candidate costs of refine_subpel (encoder/me.c:865-992).
+#include "hipcommon.h"
+
+namespace x264hip {
+
+// ------------------------------------------------------------ hpel filter
+// The reference filters x in [-8, W+8) and y in [-8, H+8) of each plane, then
+// re-expands the border from the last trusted column/row (x = -4 / W+3,
+// y = -8 / H+7) over the 32-pixel padding.  Interior kernel: one 64x16 tile per
+// workgroup staged through LDS (source with a 2/3-pixel halo, then the
+// vertical 6-tap intermediates that feed the centre plane).
+constexpr int HT_W = 64, HT_H = 16;
+constexpr int HS_W = HT_W + 5, HS_H = HT_H + 5;
+
+template <int BD>
+__device__ __forceinline__ int clip_px( int v )
+{
+    return v < 0 ? 0 : v > PT<BD>::PIXEL_MAX ? PT<BD>::PIXEL_MAX : v;
+}
+
+__device__ __forceinline__ int tap6( int a, int b, int c, int d, int e, int f )
+{
+    return a + f - 5 * (b + e) + 20 * (c + d);   // TAPFILTER, mc.c:172
+}
+
+template <int BD>
+__global__ __launch_bounds__( 256 ) void hpel_interior_kernel( const typename PT<BD>::pixel *__restrict__ src,
+                                                               typename PT<BD>::pixel *__restrict__ dh,
+                                                               typename PT<BD>::pixel *__restrict__ dv,
+                                                               typename PT<BD>::pixel *__restrict__ dc,
+                                                               intptr_t stride, intptr_t fstride, int width,
+                                                               int height )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int pad = BD > 9 ? -10 * PT<BD>::PIXEL_MAX : 0;    // mc.c:176
+    __shared__ int s_src[HS_H][HS_W];
+    __shared__ int s_v[HT_H][HS_W];
+    const int x0 = -4 + HT_W * blockIdx.x;      // interior region: x in [-4, W+4)
+    const int y0 = -8 + HT_H * blockIdx.y;      //                  y in [-8, H+8)
+    const intptr_t fo = (intptr_t)blockIdx.z * fstride;
+    const pixel *s = src + fo;
+    for( int i = threadIdx.x; i < HS_H * HS_W; i += 256 )
+    {
+        int r = i / HS_W, c = i % HS_W;
+        // columns past the right padding are never needed by a written pixel
+        s_src[r][c] = x0 - 2 + c < width + 32 ? (int)s[(intptr_t)(y0 - 2 + r) * stride + (x0 - 2 + c)] : 0;
+    }
+    __syncthreads();
+    // vertical intermediates for rows y0..y0+15, columns x0-2 .. x0+66
+    for( int i = threadIdx.x; i < HT_H * HS_W; i += 256 )
+    {
+        int r = i / HS_W, c = i % HS_W;
+        s_v[r][c] = tap6( s_src[r][c], s_src[r + 1][c], s_src[r + 2][c], s_src[r + 3][c], s_src[r + 4][c],
+                          s_src[r + 5][c] );
+    }
+    __syncthreads();
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int x = x0 + tx;
+    if( x >= width + 4 )
+        return;
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+    {
+        const int r = ty * 4 + k, y = y0 + r;
+        if( y >= height + 8 )
+            break;
+        const intptr_t o = fo + (intptr_t)y * stride + x;
+        const int v = s_v[r][tx + 2];
+        dv[o] = (pixel)clip_px<BD>( (v + 16) >> 5 );
+        const int hsum = tap6( s_src[r + 2][tx], s_src[r + 2][tx + 1], s_src[r + 2][tx + 2], s_src[r + 2][tx + 3],
+                               s_src[r + 2][tx + 4], s_src[r + 2][tx + 5] );
+        dh[o] = (pixel)clip_px<BD>( (hsum + 16) >> 5 );
+        // centre: the intermediates pass through int16 storage with the 10-bit bias (mc.c:179-181)
+        int b[6];
+#pragma unroll
+        for( int j = 0; j < 6; j++ )
+            b[j] = (int16_t)(s_v[r][tx + j] + pad);
+        const int csum = tap6( b[0], b[1], b[2], b[3], b[4], b[5] );
+        dc[o] = (pixel)clip_px<BD>( (csum - 32 * pad + 512) >> 10 );
+    }
+}
+
+// border re-expansion of the three planes: every padded pixel outside the
+// interior takes the interior pixel at the clamped coordinate (plane_expand_border,
+// frame.c:612-623 with padh = 28, padv = 24 from the last filtered pixels)
+template <int BD>
+__global__ __launch_bounds__( 256 ) void hpel_expand_kernel( typename PT<BD>::pixel *__restrict__ dh,
+                                                             typename PT<BD>::pixel *__restrict__ dv,
+                                                             typename PT<BD>::pixel *__restrict__ dc,
+                                                             intptr_t stride, intptr_t fstride, int width, int height,
+                                                             int pad )
+{
+    const int pw = width + 2 * pad, ph = height + 2 * pad;
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= (int64_t)pw * ph )
+        return;
+    const int x = (int)(i % pw) - pad, y = (int)(i / pw) - pad;
+    if( x >= -4 && x < width + 4 && y >= -8 && y < height + 8 )
+        return;
+    const int cx = x < -4 ? -4 : x >= width + 4 ? width + 3 : x;
+    const int cy = y < -8 ? -8 : y >= height + 8 ? height + 7 : y;
+    const intptr_t fo = (intptr_t)blockIdx.y * fstride;
+    const intptr_t d = fo + (intptr_t)y * stride + x, sidx = fo + (intptr_t)cy * stride + cx;
+    dh[d] = dh[sidx];
+    dv[d] = dv[sidx];
+    dc[d] = dc[sidx];
+}
+
+template <int BD>
+hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD>::pixel *dh,
+                               typename PT<BD>::pixel *dv, typename PT<BD>::pixel *dc, intptr_t stride,
+                               intptr_t fstride, int width, int height, int nframes, hipStream_t stream )
+{
+    if( nframes <= 0 || width <= 0 || height <= 0 )
+        return hipSuccess;
+    dim3 g1( (width + 8 + HT_W - 1) / HT_W, (height + 16 + HT_H - 1) / HT_H, nframes );
+    hipLaunchKernelGGL( ( hpel_interior_kernel<BD> ), g1, dim3( 256 ), 0, stream, src, dh, dv, dc, stride, fstride,
+                        width, height );
+    const int pad = 32;
+    const int64_t npx = (int64_t)(width + 2 * pad) * (height + 2 * pad);
+    dim3 g2( (unsigned)((npx + 255) / 256), nframes );
+    hipLaunchKernelGGL( ( hpel_expand_kernel<BD> ), g2, dim3( 256 ), 0, stream, dh, dv, dc, stride, fstride, width,
+                        height, pad );
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------ qpel candidates
+__constant__ uint8_t c_hpel_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };
+__constant__ uint8_t c_hpel_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };
+
+// rounding-up average of packed pixels, (a + b + 1) >> 1 per pixel (pixel_avg, mc.c:57)
+template <int BD> __device__ __forceinline__ uint32_t avg_packed( uint32_t a, uint32_t b )
+{
+    constexpr uint32_t keep = BD == 8 ? 0x7F7F7F7Fu : 0x7FFF7FFFu;
+    return (a | b) - (((a ^ b) >> 1) & keep);
+}
+
+template <int BD, int OP, int IPIX>
+__global__ __launch_bounds__( 256 ) void subpel_cmp_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                            intptr_t fs, const typename PT<BD>::pixel *p0,
+                                                            const typename PT<BD>::pixel *p1,
+                                                            const typename PT<BD>::pixel *p2,
+                                                            const typename PT<BD>::pixel *p3, intptr_t rs,
+                                                            const int64_t *__restrict__ fenc_off,
+                                                            const int32_t *__restrict__ qxy, int n,
+                                                            int32_t *__restrict__ scores )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    constexpr int NDW = W / PT<BD>::PPD;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    const int qx = qxy[2 * i], qy = qxy[2 * i + 1];
+    const int idx = ((qy & 3) << 2) + (qx & 3);
+    const intptr_t off = (intptr_t)(qy >> 2) * rs + (qx >> 2);
+    const pixel *planes[4] = { p0, p1, p2, p3 };
+    const pixel *s1 = planes[c_hpel_ref0[idx]] + off + ((qy & 3) == 3) * rs;
+    const bool two = idx & 5;
+    const pixel *s2 = planes[c_hpel_ref1[idx]] + off + ((qx & 3) == 3);
+    const pixel *a = fenc + fenc_off[i];
+    int sum = 0;
+    uint32_t acc = 0;
+    // 4-row bands keep the register footprint at 2 x 4 x NDW dwords
+#pragma unroll
+    for( int ty = 0; ty < H; ty += 4 )
+    {
+        uint32_t fr[4][NDW], rr[4][NDW];
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+        {
+            load_packed<NDW>( a + (ty + y) * fs, fr[y] );
+            load_packed<NDW>( s1 + (ty + y) * rs, rr[y] );
+            if( two )
+            {
+                uint32_t t[NDW];
+                load_packed<NDW>( s2 + (ty + y) * rs, t );
+#pragma unroll
+                for( int k = 0; k < NDW; k++ )
+                    rr[y][k] = avg_packed<BD>( rr[y][k], t[k] );
+            }
+        }
+        if constexpr( OP == 0 )
+        {
+#pragma unroll
+            for( int y = 0; y < 4; y++ )
+#pragma unroll
+                for( int k = 0; k < NDW; k++ )
+                    acc = sadp<BD>( fr[y][k], rr[y][k], acc );
+        }
+        else
+        {
+            // SATD: (sum |H4 D H4^T|) >> 1 per 4x4 tile (pixel.c:265-332)
+#pragma unroll
+            for( int tx = 0; tx < W; tx += 4 )
+            {
+                int d[4][4];
+#pragma unroll
+                for( int y = 0; y < 4; y++ )
+                {
+#pragma unroll
+                    for( int x = 0; x < 4; x++ )
+                    {
+                        const int px = tx + x;
+                        d[y][x] = upix<BD>( fr[y][px / PT<BD>::PPD], px % PT<BD>::PPD ) -
+                                  upix<BD>( rr[y][px / PT<BD>::PPD], px % PT<BD>::PPD );
+                    }
+                    int t0 = d[y][0] + d[y][1], t1 = d[y][0] - d[y][1], t2 = d[y][2] + d[y][3], t3 = d[y][2] - d[y][3];
+                    d[y][0] = t0 + t2; d[y][2] = t0 - t2; d[y][1] = t1 + t3; d[y][3] = t1 - t3;
+                }
+                int s4 = 0;
+#pragma unroll
+                for( int x = 0; x < 4; x++ )
+                {
+                    int t0 = d[0][x] + d[1][x], t1 = d[0][x] - d[1][x], t2 = d[2][x] + d[3][x], t3 = d[2][x] - d[3][x];
+                    s4 += abs( t0 + t2 ) + abs( t0 - t2 ) + abs( t1 + t3 ) + abs( t1 - t3 );
+                }
+                sum += s4 >> 1;
+            }
+        }
+    }
+    if constexpr( OP == 0 )
+        sum = (int)acc;
+    scores[i] = sum;
+}
+
+template <int BD>
+hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs,
+                              const typename PT<BD>::pixel *const planes[4], intptr_t rs, const int64_t *fenc_off,
+                              const int32_t *qxy, int n, int32_t *scores, hipStream_t stream )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (n + 255) / 256 );
+#define SP_CASE( OP, I )                                                                                      \
+    case I: hipLaunchKernelGGL( ( subpel_cmp_kernel<BD, OP, I> ), g, blk, 0, stream, fenc, fs, planes[0],       \
+                                planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores ); break;
+    if( op == 0 )
+    {
+        switch( i_pixel ) { SP_CASE( 0, 0 ) SP_CASE( 0, 1 ) SP_CASE( 0, 2 ) SP_CASE( 0, 3 ) SP_CASE( 0, 4 )
+                            SP_CASE( 0, 5 ) SP_CASE( 0, 6 ) SP_CASE( 0, 7 ) default: return hipErrorInvalidValue; }
+    }
+    else if( op == 2 )
+    {
+        switch( i_pixel ) { SP_CASE( 2, 0 ) SP_CASE( 2, 1 ) SP_CASE( 2, 2 ) SP_CASE( 2, 3 ) SP_CASE( 2, 4 )
+                            SP_CASE( 2, 5 ) SP_CASE( 2, 6 ) SP_CASE( 2, 7 ) default: return hipErrorInvalidValue; }
+    }
+    else
+        return hipErrorInvalidValue;
+#undef SP_CASE
+    return hipGetLastError();
+}
+
+#define INST( BD )                                                                                              \
+    template hipError_t launch_hpel_filter<BD>( const PT<BD>::pixel *, PT<BD>::pixel *, PT<BD>::pixel *,       \
+                                                PT<BD>::pixel *, intptr_t, intptr_t, int, int, int, hipStream_t ); \
+    template hipError_t launch_subpel_cmp<BD>( int, int, const PT<BD>::pixel *, intptr_t,                      \
+                                               const PT<BD>::pixel *const[4], intptr_t, const int64_t *,       \
+                                               const int32_t *, int, int32_t *, hipStream_t );
+INST( 8 )
+INST( 10 )
+
+} // namespace x264hip
