@@ -199,28 +199,41 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
         res["dct%d_quant_blocks_per_s" % t] = world * a.steps * blocks / wall
         res["dct%d_quant_hbm_frac" % t] = blocks * bpb / (ev_ms * 1e-3) / HBM_PEAK
         res["dct%d_quant_launch_ms" % t] = ev_ms
-    # SATD 8x8: 9 qpel-neighbourhood-sized candidate sets around the zero MV per 8x8 block
-    # (integer offsets here; the subpel interpolation path is a later kernel)
-    nb = F * mbw * mbh * 4
+    # SATD 8x8 subpel refine (configs[2]): half-pel planes of the F refs, then for every
+    # 8x8 block 9 quarter-pel candidates (+-1 qpel) around a half-pel MV next to the true
+    # motion (3, 2) px, each an unweighted get_ref + satd_8x8 (reference me.c:950-963)
+    hv = [torch.zeros_like(dev) for _ in range(3)]
+
+    def hstep():
+        x.hpel_filter(dev[:-1], origin, stride, mbw * 16, mbh * 16, outs=[h[:-1] for h in hv])
+    wall, ev_ms = timed(hstep, a.steps, a.warmup, world)
+    res["hpel_filter_frames_per_s"] = world * a.steps * F / wall
+    res["hpel_filter_launch_ms"] = ev_ms
+    nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
-    base = (ys.ravel() * 8 * stride + xs.ravel() * 8).astype(np.int64)
-    fo, ro = [], []
+    bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)
+    fo, qxy = [], []
     for f in range(F):
         for dy in (-1, 0, 1):
             for dx in (-1, 0, 1):
-                fo.append(base + origin + (f + 1) * fstride)
-                ro.append(base + origin + f * fstride + dy * stride + dx)
+                fo.append((f + 1) * fstride + origin + by * stride + bx)
+                q = np.stack([4 * bx + 12 + 2 + dx, 4 * by + 8 + dy], 1)
+                # frame f's planes: fold the frame offset into the quarter-pel row coordinate
+                q[:, 1] += 4 * f * (fstride // stride)
+                qxy.append(q.astype(np.int32))
     fo = torch.from_numpy(np.concatenate(fo)).cuda()
-    ro = torch.from_numpy(np.concatenate(ro)).cuda()
+    qxy = torch.from_numpy(np.concatenate(qxy)).cuda()
     sc = torch.empty(fo.numel(), dtype=torch.int32, device="cuda")
-    flat_dev = dev.view(-1)
+    flat = dev.view(-1)
+    ref_planes = [dev.view(-1)] + [h.view(-1) for h in hv]
 
     def sstep():
-        x.pixel_cmp_batch(x.CMP_SATD, x.PIXEL_8x8, flat_dev, stride, flat_dev, stride, fo, ro, scores=sc)
+        x.subpel_cmp_batch(x.CMP_SATD, x.PIXEL_8x8, flat, stride, ref_planes, origin, stride, fo, qxy, scores=sc)
     wall, ev_ms = timed(sstep, a.steps, a.warmup, world)
-    res["satd8x8_candidates_per_s"] = world * a.steps * fo.numel() / wall
-    res["satd8x8_launch_ms"] = ev_ms
-    del nb
+    res["satd8x8_subpel_candidates_per_s"] = world * a.steps * fo.numel() / wall
+    res["satd8x8_subpel_launch_ms"] = ev_ms
+    res["satd8x8_candidates_per_launch"] = int(fo.numel())
+    del nb8
     return res
 
 

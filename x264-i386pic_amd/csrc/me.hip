@@ -270,8 +270,11 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t 
     me_rows3<R>( rbase, (int)(rs / 4), F, acc, out, std::make_integer_sequence<int, 2 * R + 8>{} );
 }
 
-// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT=1 forces the
-// single-lane-per-column kernel, default 2
+// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2 or 3;
+// default 3 at 8 bit, 1 at 10 bit.  (A variant that dropped the padded column
+// group and finished the last column in separate waves ran 13-20% slower: the
+// table rows were then written by different waves at different times, so
+// nearly every 128-B line left L2 partially written.)
 static int me_variant()
 {
     const char *e = getenv( "X264HIP_ME_VARIANT" );
@@ -295,12 +298,12 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     int variant = me_variant();
     if( !variant )
         variant = BD == 8 ? 3 : 1;
-    if( BD != 8 && variant == 3 )
+    if( BD != 8 && variant >= 3 )
         variant = 1;
     // variants 2/3 need dword-aligned fenc rows, dword-multiple strides and (3) a
     // dword-aligned ref plane
     if( (((uintptr_t)fenc | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
-          (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant == 3 ? (uintptr_t)ref : 0)) & 3) )
+          (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant >= 3 ? (uintptr_t)ref : 0)) & 3) )
         variant = 1;
     const int64_t groups = variant == 3 ? 2 * ((2 * range + 1 + 3) / 4) : variant == 2 ? 2 * (2 * range + 1)
                                                                                       : (2 * range + 1);
