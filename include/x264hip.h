@@ -298,6 +298,19 @@ int x264hip_##BD##_me_search_full( const pixel *fenc, intptr_t fenc_stride,     
                                    int mb_width, int mb_height, int n_frames, int range,        \
                                    sadt *table, void *stream );                                 \
                                                                                                 \
+/* integer-pel ESA decision per macroblock over a me_search_full table (reference            \
+ * encoder/me.c:618-631, the plain exhaustive form its ads path :632-771 reproduces):           \
+ * par[8*i] = { bmx, bmy (fullpel centre = best predictor), mvp_x, mvp_y (qpel),                \
+ *              mv_x_min, mv_y_min, mv_x_max, mv_y_max (mv_limit_fpel, analyse.c:330-349) };    \
+ * the window is [max(bmx-me_range, mv_x_min), ..] with width rounded as                        \
+ * (max_x - min_x + 3) & ~3, cost = sad + cost_mv[4*mx - mvp_x] + cost_mv[4*my - mvp_y]         \
+ * (cost_mv: x264's h->cost_mv[qp], pointer at mvd 0), strict-< update from                     \
+ * (init_cost[i], bmx, bmy) in my-major raster order.  out[3*i] = {cost, mx, my}.               \
+ * The window must lie inside the table's [-range, range + 3] square.  n = #MBs. */             \
+int x264hip_##BD##_me_esa_argmin( const sadt *table, int range, int n, int me_range,            \
+                                  const int16_t *par, const int32_t *init_cost,                 \
+                                  const uint16_t *cost_mv, int32_t *out, void *stream );        \
+                                                                                                \
 /* half-pel planes (reference x264_frame_filter common/mc.c:704-726 over the                 \
  * whole frame, hpel_filter mc.c:173-196, then x264_frame_expand_border_filtered               \
  * common/frame.c:599-625): for n_frames padded planes (PAD = 32, pointers at                   \

@@ -710,3 +710,45 @@ void FN(subpel_list)( int op, int i_pixel, const pixel *fenc, intptr_t fs, const
         scores[i] = op == 0 ? FN(sad)( i_pixel, a, fs, r, ts ) : FN(satd)( i_pixel, a, fs, r, ts );
     }
 }
+
+/* exhaustive integer-pel search decision over a full-search table, restating the
+ * plain exhaustive form of the ESA case of x264_me_search_ref (reference
+ * encoder/me.c:618-631, which the ads successive-elimination path :632-771
+ * reproduces exactly): window clipped by the mv limits, width rounded as
+ * (max_x - min_x + 3) & ~3, cost = sad + p_cost_mvx[mx*4] + p_cost_mvy[my*4]
+ * with p_cost_mv* = cost_mv - mvp (me.c:60-70, 230-231), strict-< update from
+ * the predictor result (COPY3_IF_LT, me.h:87-93), my-major raster order.
+ * par[8*i] = { bmx, bmy, mvp_x, mvp_y, mv_x_min, mv_y_min, mv_x_max, mv_y_max };
+ * table rows have pitch align4(2R+1) and are centred on mv (0,0). */
+void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const int16_t *par, const int32_t *init_cost,
+                        const uint16_t *cost_mv, int32_t *out )
+{
+    const int W = 2 * R + 1, P = (W + 3) & ~3;
+    for( int i = 0; i < nmb; i++ )
+    {
+        const int16_t *p = par + 8 * i;
+        int bmx = p[0], bmy = p[1];
+        const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
+        int min_x = bmx - me_range > p[4] ? bmx - me_range : p[4];
+        int min_y = bmy - me_range > p[5] ? bmy - me_range : p[5];
+        int max_x = bmx + me_range < p[6] ? bmx + me_range : p[6];
+        int max_y = bmy + me_range < p[7] ? bmy + me_range : p[7];
+        int width = (max_x - min_x + 3) & ~3;
+        int bcost = init_cost[i];
+        const sadt *t = table + (size_t)i * W * P;
+        for( int my = min_y; my <= max_y; my++ )
+            for( int mx = min_x; mx < min_x + width; mx++ )
+            {
+                int cost = t[(my + R) * P + mx + R] + cx[mx * 4] + cy[my * 4];
+                if( cost < bcost )
+                {
+                    bcost = cost;
+                    bmx = mx;
+                    bmy = my;
+                }
+            }
+        out[3 * i] = bcost;
+        out[3 * i + 1] = bmx;
+        out[3 * i + 2] = bmy;
+    }
+}

@@ -64,6 +64,7 @@ for _bd in (8, 10):
     _f(_bd, "mb_dct_quant", [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "hpel_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int, _P])
     _f(_bd, "get_ref", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int], _P)
+    _f(_bd, "me_esa_argmin", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
     _f(_bd, "subpel_list", [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
@@ -208,4 +209,15 @@ def subpel_list(bd, op, i_pixel, fenc, fs, planes, p_origin, rs, fenc_off, qxy):
     getattr(_L, f"oracle{bd}_subpel_list")(_OPS.get(op, op), i_pixel, _addr(fenc), fs,
                                           *[_addr(p, p_origin) for p in planes], rs, _addr(fo), _addr(q),
                                           len(fo), _addr(out))
+    return out
+
+
+def me_esa_argmin(bd, table, rng, me_range, par, init_cost, cost_mv, c0):
+    """table: numpy [nmb, 2r+1, pitch]; cost_mv numpy uint16 with mvd 0 at index c0."""
+    t = np.ascontiguousarray(table)
+    p = np.ascontiguousarray(par, np.int16)
+    ic = np.ascontiguousarray(init_cost, np.int32)
+    out = np.zeros((len(p), 3), np.int32)
+    getattr(_L, f"oracle{bd}_me_esa_argmin")(_addr(t), rng, len(p), me_range, _addr(p), _addr(ic),
+                                            _addr(cost_mv, c0), _addr(out))
     return out

@@ -261,3 +261,33 @@ def test_frame_filter_and_subpel(oracle, bd):
                 r = nr.get_ref(flat, origin, stride, qx, qy, w, h)
                 a = nr.block(planes.ravel(), f, stride, w, h)
                 assert got[k] == (nr.sad(a, r) if op == "sad" else nr.satd(a, r))
+
+
+def test_me_esa_argmin_vs_numpy(oracle):
+    """oracle ESA decision vs a vectorised numpy restatement (argmin with first-index ties)."""
+    rs = np.random.default_rng(3)
+    R, me_range, nmb = 16, 12, 200
+    W, P = 2 * R + 1, 36
+    tab = rs.integers(0, 3000, size=(nmb, W, P)).astype(np.uint16)
+    tab[::5] //= 64                                              # many ties
+    i = np.arange(-4096, 4097)
+    cost_mv = np.minimum(40 * (2 * np.log2(np.abs(i) + 1) + 1.718) + 0.5, 65535).astype(np.uint16)
+    par = np.zeros((nmb, 8), np.int16)
+    par[:, :2] = rs.integers(-1, 2, (nmb, 2))
+    par[:, 2:4] = rs.integers(-40, 41, (nmb, 2))
+    par[:, 4:6] = par[:, :2] - me_range + rs.integers(0, 3, (nmb, 2))
+    par[:, 6:8] = par[:, :2] + me_range - rs.integers(0, 3, (nmb, 2))
+    init = rs.integers(0, 3000, nmb).astype(np.int32)
+    got = oracle.me_esa_argmin(8, tab, R, me_range, par, init, cost_mv, 4096)
+    for k in range(nmb):
+        bmx, bmy, px, py, x0, y0, x1, y1 = [int(v) for v in par[k]]
+        mnx, mny = max(bmx - me_range, x0), max(bmy - me_range, y0)
+        mxx, mxy = min(bmx + me_range, x1), min(bmy + me_range, y1)
+        width = (mxx - mnx + 3) & ~3
+        ys, xs = np.meshgrid(np.arange(mny, mxy + 1), np.arange(mnx, mnx + width), indexing="ij")
+        cost = (tab[k][ys + R, xs + R].astype(np.int64) + cost_mv[4096 + 4 * xs - px] + cost_mv[4096 + 4 * ys - py])
+        j = int(np.argmin(cost.ravel()))
+        want = (init[k], bmx, bmy)
+        if cost.ravel()[j] < init[k]:
+            want = (int(cost.ravel()[j]), int(xs.ravel()[j]), int(ys.ravel()[j]))
+        assert tuple(got[k]) == want, k

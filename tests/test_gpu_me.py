@@ -98,3 +98,51 @@ def test_me_full_1080p_properties(hip, oracle, variant):
     assert np.array_equal(sc.cpu().numpy(), got[:, :, R, R].ravel().astype(np.int32))
     # the minimum of every window is no larger than the zero-MV cost (sanity of argmin use)
     assert (got.reshape(mbh * mbw, -1).min(1) <= got[:, :, R, R].ravel()).all()
+
+
+def _cost_mv(lam=40, span=4096):
+    """an x264-shaped mv cost table (analyse.c:143-157): symmetric, lambda * bits."""
+    i = np.arange(-span, span + 1)
+    logs = np.where(i == 0, 0.718, 2.0 * np.log2(np.abs(i) + 1) + 1.718)
+    return np.minimum((lam * logs + 0.5).astype(np.int64), 65535).astype(np.uint16), span
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("rng,me_range", [(16, 16), (24, 16), (8, 4)])
+def test_me_esa_argmin(hip, oracle, bd, rng, me_range):
+    """ESA decision (encoder/me.c:618-631) over the GPU table: clipped windows, the
+    width rounding, mvp-dependent costs, ties and predictor-wins cases."""
+    from x264hip import synth
+    W, H = 160, 96
+    planes, stride, origin = synth.make_sequence(2, W, H, bd, seed=5)
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
+    fs = planes[0].size
+    mbw, mbh = W // 16, H // 16
+    table = hip.me_search_full(dev[1:], origin, stride, dev[:1], origin, stride, mbw, mbh, 1, rng,
+                               fenc_frame_stride=fs, ref_frame_stride=fs)
+    nmb = mbw * mbh
+    rs = np.random.default_rng(rng * 100 + bd)
+    slack = rng - me_range - 3 if rng >= me_range + 3 else 0
+    par = np.zeros((nmb, 8), np.int16)
+    par[:, 0] = rs.integers(-slack, slack + 1, nmb)               # bmx
+    par[:, 1] = rs.integers(-slack, slack + 1, nmb)               # bmy
+    par[:, 2] = rs.integers(-64, 65, nmb)                         # mvp qpel
+    par[:, 3] = rs.integers(-64, 65, nmb)
+    lim = rs.integers(0, me_range + 1, (nmb, 4))                  # some windows clipped
+    par[:, 4] = np.maximum(par[:, 0] - me_range, -rng + 0) + np.where(rs.random(nmb) < 0.3, lim[:, 0], 0)
+    par[:, 5] = np.maximum(par[:, 1] - me_range, -rng) + np.where(rs.random(nmb) < 0.3, lim[:, 1], 0)
+    par[:, 6] = np.minimum(par[:, 0] + me_range, rng - 3) - np.where(rs.random(nmb) < 0.3, lim[:, 2], 0)
+    par[:, 7] = np.minimum(par[:, 1] + me_range, rng) - np.where(rs.random(nmb) < 0.3, lim[:, 3], 0)
+    par[:, 6] = np.maximum(par[:, 6], par[:, 4])
+    par[:, 7] = np.maximum(par[:, 7], par[:, 5])
+    init = rs.integers(0, 20000, nmb).astype(np.int32)
+    init[::7] = 0                                                 # predictor unbeatable
+    cost_mv, c0 = _cost_mv()
+    cm_dev = torch.from_numpy(cost_mv.view(np.int16)).cuda()
+    got = hip.me_esa_argmin(table, rng, me_range, torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda(),
+                            (cm_dev, c0)).cpu().numpy()
+    tab = table.cpu().numpy()
+    tab = (tab.view(np.uint16) if bd == 8 else tab.view(np.uint32))[0].reshape(nmb, 2 * rng + 1, -1)
+    want = oracle.me_esa_argmin(bd, tab, rng, me_range, par, init, cost_mv, c0)
+    assert np.array_equal(got, want), np.argwhere((got != want).any(1))[:5]
+    assert (got[::7, 0] == 0).all() and (got[:, 0] <= init).all()

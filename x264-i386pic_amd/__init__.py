@@ -23,7 +23,7 @@ import os
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "me_table_pitch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "me_table_pitch", "me_esa_argmin", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP",
 ]
@@ -193,11 +193,12 @@ def _declare(L):
         f("dc_batch").argtypes = [_c.c_int, _P, _P, _c.c_int, _P]
         f("quant_batch").argtypes = [_c.c_int, _P, _P, _P, _c.c_int, _P, _P]
         f("quant_dc_batch").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P]
+        f("me_esa_argmin").argtypes = [_P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P]
         f("hpel_filter").argtypes = [_P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P]
         f("subpel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, _c.c_int, _P, _P]
         f("mb_dct_quant").argtypes = [_c.c_int, _P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int,
                                       _P, _P, _P, _P, _P]
-        for n in ("pixel_cmp_batch", "me_search_full", "hpel_filter", "subpel_cmp_batch", "sub_dct_batch", "dc_batch", "quant_batch",
+        for n in ("pixel_cmp_batch", "me_search_full", "me_esa_argmin", "hpel_filter", "subpel_cmp_batch", "sub_dct_batch", "dc_batch", "quant_batch",
                   "quant_dc_batch", "mb_dct_quant"):
             f(n).restype = _c.c_int
 
@@ -397,3 +398,19 @@ def subpel_cmp_batch(op, i_pixel, fenc, fenc_stride, planes, ref_origin, ref_str
         op, i_pixel, _ptr(fenc), fenc_stride, *[_ptr(p, ref_origin) for p in planes], ref_stride,
         _ptr(fenc_off), _ptr(qpel_xy), n, _ptr(scores), _stream()), "subpel_cmp_batch")
     return scores
+
+
+def me_esa_argmin(table, rng, me_range, par, init_cost, cost_mv_center, out=None):
+    """ESA decision per MB over a full-search table (x264hip_*_me_esa_argmin).
+    par int16 [n, 8], init_cost int32 [n], cost_mv_center: (uint16-as-int16 tensor, element
+    offset of mvd 0).  Returns int32 [n, 3] = (cost, mx, my)."""
+    import torch
+    bd = 8 if table.dtype == torch.int16 else 10
+    n = par.shape[0]
+    if out is None:
+        out = torch.empty((n, 3), dtype=torch.int32, device=table.device)
+    cm, c0 = cost_mv_center
+    _rc(getattr(lib(), f"x264hip_{bd}_me_esa_argmin")(
+        _ptr(table), rng, n, me_range, _ptr(par), _ptr(init_cost), _ptr(cm, c0), _ptr(out), _stream()),
+        "me_esa_argmin")
+    return out

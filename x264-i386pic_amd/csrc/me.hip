@@ -337,3 +337,78 @@ template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, co
                                         int, int, int, int, uint32_t *, hipStream_t );
 
 } // namespace x264hip
+
+namespace x264hip {
+
+// ---------------------------------------------------------------------------
+// ESA decision over a full-search table (reference encoder/me.c:618-631 plain
+// exhaustive form, equal to its ads path :632-771): one wave per macroblock.
+// Each lane scans every 64th candidate of the clipped window in my-major raster
+// order and keeps the packed key (cost << 12 | raster index); a wave min over
+// the keys returns the lowest cost and, among equal costs, the first in
+// raster order — what the strict-< scan of the reference keeps — which then
+// replaces the predictor result only if strictly better (COPY3_IF_LT).
+template <int BD>
+__global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT<BD>::sadt *__restrict__ table, int R,
+                                                               int nmb, int me_range, const int16_t *__restrict__ par,
+                                                               const int32_t *__restrict__ init_cost,
+                                                               const uint16_t *__restrict__ cost_mv,
+                                                               int32_t *__restrict__ out )
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t mb = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if( mb >= nmb )
+        return;                                                    // wave-uniform
+    const int W = 2 * R + 1, P = (W + 3) & ~3;
+    const int16_t *p = par + 8 * mb;
+    const int bmx = p[0], bmy = p[1], mvpx = p[2], mvpy = p[3];
+    const int min_x = max( bmx - me_range, (int)p[4] ), min_y = max( bmy - me_range, (int)p[5] );
+    const int max_x = min( bmx + me_range, (int)p[6] ), max_y = min( bmy + me_range, (int)p[7] );
+    const int width = (max_x - min_x + 3) & ~3;
+    const int n = width > 0 && max_y >= min_y ? width * (max_y - min_y + 1) : 0;
+    const typename PT<BD>::sadt *t = table + mb * (int64_t)(W * P) + (min_y + R) * P + (min_x + R);
+    uint32_t key = 0xFFFFFFFFu;
+    for( int i = lane; i < n; i += 64 )
+    {
+        const int dy = i / width, dx = i - dy * width;
+        const int mx = min_x + dx, my = min_y + dy;
+        const uint32_t cost = (uint32_t)t[dy * P + dx] + cost_mv[mx * 4 - mvpx] + cost_mv[my * 4 - mvpy];
+        key = min( key, (cost << 12) | (uint32_t)i );
+    }
+#pragma unroll
+    for( int off = 32; off >= 1; off >>= 1 )
+        key = min( key, (uint32_t)__shfl_xor( (int)key, off ) );
+    if( lane == 0 )
+    {
+        int32_t bcost = init_cost[mb], rx = bmx, ry = bmy;
+        if( key != 0xFFFFFFFFu && (int32_t)(key >> 12) < bcost )
+        {
+            const int i = (int)(key & 4095);
+            bcost = (int32_t)(key >> 12);
+            ry = min_y + i / width;
+            rx = min_x + i % width;
+        }
+        out[3 * mb] = bcost;
+        out[3 * mb + 1] = rx;
+        out[3 * mb + 2] = ry;
+    }
+}
+
+template <int BD>
+hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int nmb, int me_range,
+                                 const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,
+                                 hipStream_t stream )
+{
+    if( nmb <= 0 )
+        return hipSuccess;
+    hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD> ), dim3( (nmb + 3) / 4 ), dim3( 256 ), 0, stream, table, R, nmb,
+                        me_range, par, init_cost, cost_mv, out );
+    return hipGetLastError();
+}
+
+template hipError_t launch_me_esa_argmin<8>( const uint16_t *, int, int, int, const int16_t *, const int32_t *,
+                                             const uint16_t *, int32_t *, hipStream_t );
+template hipError_t launch_me_esa_argmin<10>( const uint32_t *, int, int, int, const int16_t *, const int32_t *,
+                                              const uint16_t *, int32_t *, hipStream_t );
+
+} // namespace x264hip
