@@ -14,7 +14,7 @@ def _frames(synth, bd, w, h, kind, seed=3):
     return synth.random_planes(3, w, h, bd, seed=seed)
 
 
-@pytest.fixture(params=["default", "1", "2", "3"])
+@pytest.fixture(params=["default", "1", "2", "3", "5"])
 def variant(request, monkeypatch):
     """every kernel variant (X264HIP_ME_VARIANT, read per launch) must be exact"""
     if request.param != "default":

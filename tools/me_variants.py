@@ -14,7 +14,7 @@ for bd in (8, 10):
     planes, stride, origin = synth.make_sequence(F + 1, W, H, bd)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
-    vs = (1, 2, 3) if bd == 8 else (1, 2)
+    vs = (1, 2, 3) if bd == 8 else (1, 2, 5)
     tab = {}
     for v in vs:
         os.environ["X264HIP_ME_VARIANT"] = str(v)

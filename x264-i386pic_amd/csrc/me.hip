@@ -270,8 +270,105 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t 
     me_rows3<R>( rbase, (int)(rs / 4), F, acc, out, std::make_integer_sequence<int, 2 * R + 8>{} );
 }
 
-// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2 or 3;
-// default 3 at 8 bit, 1 at 10 bit.  (A variant that dropped the padded column
+// ---------------------------------------------------------------------------
+// Variant 5 (10 bit, default): the variant-3 layout for 16-bit pixels.  A lane
+// owns two adjacent candidate columns (2g, 2g+1; the first is dword aligned for
+// even R) and half of the fenc rows; per ref row it loads 9 dwords once, forms
+// the odd column's dwords with one v_alignbyte_b32 each, and folds the row into
+// <= 8 candidates x 2 columns with v_sad_u16.  Two u32 SADs leave per store.
+template <int R, int Y>
+__device__ __forceinline__ void me_row5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
+                                         uint32_t (&acc)[8][2], uint32_t *out )
+{
+    constexpr int P = (2 * R + 1 + 3) / 4 * 4;
+    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    const uint32_t *row = rbase + Y * rs_dw;
+    uint32_t w[9], o[8];
+#pragma unroll
+    for( int k = 0; k < 9; k++ )
+        w[k] = row[k];
+#pragma unroll
+    for( int k = 0; k < 8; k++ )
+        o[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], 2 );
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint32_t a0 = r == 0 ? 0u : acc[c & 7][0], a1 = r == 0 ? 0u : acc[c & 7][1];
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+        {
+            a0 = __builtin_amdgcn_sad_u16( F[r][k], w[k], a0 );
+            a1 = __builtin_amdgcn_sad_u16( F[r][k], o[k], a1 );
+        }
+        if( r == 7 )
+        {
+            a0 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a0, 0xB1, 0xF, 0xF, false );
+            a1 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a1, 0xB1, 0xF, 0xF, false );
+            *(uint2 *)(out + c * P) = make_uint2( a0, a1 );
+        }
+        else
+        {
+            acc[c & 7][0] = a0;
+            acc[c & 7][1] = a1;
+        }
+    }
+}
+
+template <int R, int... Ys>
+__device__ __forceinline__ void me_rows5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
+                                          uint32_t (&acc)[8][2], uint32_t *out, std::integer_sequence<int, Ys...> )
+{
+    ( me_row5<R, Ys>( rbase, rs_dw, F, acc, out ), ... );
+}
+
+template <int R>
+__global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
+                                                                  intptr_t ffs, const uint16_t *__restrict__ ref,
+                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                  int nframes, uint32_t *__restrict__ table )
+{
+    constexpr int G = (2 * R + 1 + 1) / 2;      // column pairs per MB
+    constexpr int P = (2 * R + 1 + 3) / 4 * 4;
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
+    if( slot >= total )
+        return;
+    const int h = (int)(slot & 1);
+    const int grp = (int)((slot >> 1) % G);
+    const int64_t mb = slot / (2 * G);
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+
+    uint32_t F[8][8];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs / 2);
+#pragma unroll
+    for( int r = 0; r < 8; r++ )
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+    const uint32_t *rbase =
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h - R) * rs + 16 * mbx - R + 2 * grp);
+    uint32_t *out = table + mb * ((2 * R + 1) * P) + 2 * grp;
+    uint32_t acc[8][2];
+    me_rows5<R>( rbase, (int)(rs / 2), F, acc, out, std::make_integer_sequence<int, 2 * R + 8>{} );
+}
+
+template <int R, typename P, typename T>
+static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
+                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table )
+{
+    if constexpr( sizeof( P ) == 2 )
+        hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
+                            nframes, table );
+}
+
+// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2, 3 (8 bit)
+// or 5 (10 bit); default 3 at 8 bit, 5 at 10 bit.  (A variant that dropped the padded column
 // group and finished the last column in separate waves ran 13-20% slower: the
 // table rows were then written by different waves at different times, so
 // nearly every 128-B line left L2 partially written.)
@@ -297,16 +394,18 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
 {
     int variant = me_variant();
     if( !variant )
-        variant = BD == 8 ? 3 : 1;
-    if( BD != 8 && variant >= 3 )
+        variant = BD == 8 ? 3 : 5;
+    if( (BD != 8 && variant == 3) || (BD == 8 && variant == 5) )
         variant = 1;
     // variants 2/3 need dword-aligned fenc rows, dword-multiple strides and (3) a
     // dword-aligned ref plane
     if( (((uintptr_t)fenc | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
           (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant >= 3 ? (uintptr_t)ref : 0)) & 3) )
         variant = 1;
-    const int64_t groups = variant == 3 ? 2 * ((2 * range + 1 + 3) / 4) : variant == 2 ? 2 * (2 * range + 1)
-                                                                                      : (2 * range + 1);
+    const int64_t groups = variant == 3   ? 2 * ((2 * range + 1 + 3) / 4)
+                           : variant == 5 ? 2 * ((2 * range + 2) / 2)
+                           : variant == 2 ? 2 * (2 * range + 1)
+                                          : (2 * range + 1);
     const int64_t lanes = (int64_t)nframes * mbh * mbw * groups;
     if( lanes <= 0 )
         return hipSuccess;
@@ -315,7 +414,9 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     {
 #define ME_CASE( R ) \
         case R:                                                                                                   \
-            if( variant == 3 )                                                                                    \
+            if( variant == 5 )                                                                                    \
+                launch_v5<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table );           \
+            else if( variant == 3 )                                                                               \
                 launch_v3<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table );           \
             else if( variant == 2 )                                                                               \
                 hipLaunchKernelGGL( ( me_full_sad16_v2_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, \
