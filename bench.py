@@ -39,8 +39,11 @@ HBM_PEAK = 8.0e12
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # the GPU's clocks settle only after ~100 back-to-back launches (~35 ms of load,
+    # tools/me_sustain.py: 0.35-0.40 ms per launch at first, 0.306 ms steady), so the
+    # default warmup covers the ramp; every step is still a full launch over F pairs
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=150)
     ap.add_argument("--frames", type=int, default=16, help="frame pairs per step per GPU")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -233,7 +236,46 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     res["satd8x8_subpel_candidates_per_s"] = world * a.steps * fo.numel() / wall
     res["satd8x8_subpel_launch_ms"] = ev_ms
     res["satd8x8_candidates_per_launch"] = int(fo.numel())
-    del nb8
+    del nb8, hv, ref_planes, fo, qxy, sc
+    res.update(rates_10bit(x, a, world, mbw, mbh, F))
+    return res
+
+
+def rates_10bit(x, a, world, mbw, mbh, F):
+    """configs[4] side rates: 10-bit full search (v_sad_u16 path) and 10-bit fused
+    8x8 DCT + quant_8x8 (int32 coefficients) over F frame pairs of the same motion."""
+    from x264hip import synth, dist as xd
+    R = a.range
+    p0, p1 = xd.frame_shard(world * F, world, int(os.environ.get("RANK", "0")))
+    planes, stride, origin = synth.make_sequence(p1 - p0 + 1, mbw * 16, mbh * 16, 10, start=p0)
+    dev = torch.from_numpy(planes.view(np.int16)).cuda()
+    fstride = planes[0].size
+    table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int32, device="cuda")
+
+    def mstep():
+        x.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, table=table,
+                         fenc_frame_stride=fstride, ref_frame_stride=fstride)
+    wall, ev_ms = timed(mstep, a.steps, a.warmup, world)
+    cands = F * mbw * mbh * (2 * R + 1) ** 2
+    res = {"me10_candidates_per_s": world * a.steps * cands / wall, "me10_launch_ms": ev_ms,
+           "me10_absdiff_frac_of_v_sad_u16_peak": cands * 256 / (ev_ms * 1e-3) / VALU_LANE_OPS}
+    del table
+    flat = [16] * 64
+    _, _, q8m, q8b = x.cqm_init(10, [flat] * 8)
+    mf8 = torch.from_numpy(q8m[1, 26 + 12].copy()).cuda()
+    bs8 = torch.from_numpy(q8b[1, 26 + 12].copy()).cuda()
+    nmb = F * mbw * mbh
+    dct = torch.empty((nmb, 256), dtype=torch.int32, device="cuda")
+    nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
+
+    def dstep():
+        x.mb_dct_quant(8, dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, mf8, bs8, dct=dct, nz=nz,
+                       fenc_frame_stride=fstride, pred_frame_stride=fstride)
+    wall, ev_ms = timed(dstep, a.steps, a.warmup, world)
+    blocks = nmb * 4
+    res["dct8_quant10_blocks_per_s"] = world * a.steps * blocks / wall
+    res["dct8_quant10_hbm_frac"] = blocks * (128 + 128 + 256) / (ev_ms * 1e-3) / HBM_PEAK
+    res["dct8_quant10_launch_ms"] = ev_ms
     return res
 
 
