@@ -63,8 +63,18 @@ enum
 #define X264HIP_EDEVICE   (-2)  /* HIP runtime error (see x264hip_last_error) */
 #define X264HIP_ENODEV    (-3)  /* no usable gfx950 device */
 
-/* metric selector of x264hip_*_pixel_cmp_batch */
-enum { X264HIP_CMP_SAD = 0, X264HIP_CMP_SSD = 1, X264HIP_CMP_SATD = 2 };
+/* metric selector of x264hip_*_pixel_cmp_batch (SA8D: i_pixel 16x16 or 8x8) */
+enum { X264HIP_CMP_SAD = 0, X264HIP_CMP_SSD = 1, X264HIP_CMP_SATD = 2, X264HIP_CMP_SA8D = 3 };
+
+/* statistic selector of x264hip_*_pixel_stat_batch (uint64_t results) */
+enum
+{
+    X264HIP_STAT_VAR         = 0,  /* var[i_pixel] (16x16, 8x16, 8x8), pixel.c:181-198      */
+    X264HIP_STAT_HADAMARD_AC = 1,  /* hadamard_ac[i_pixel] (16x16..8x8), pixel.c:383-435    */
+    X264HIP_STAT_SA8D_SATD   = 2,  /* sa8d_satd[16x16]: sa8d | satd << 32, checkasm.c:424-460 */
+    X264HIP_STAT_VSAD        = 3,  /* vsad( pix1, stride1, height ), pixel.c:716-723          */
+    X264HIP_STAT_ASD8        = 4,  /* asd8( pix1, s1, pix2, s2, height ), pixel.c:747-754     */
+};
 
 /* transform selector of x264hip_*_sub_dct_batch (one "block" = one call of
  * the named reference entry, fenc stride 16 / fdec stride 32 semantics are
@@ -278,6 +288,46 @@ int x264hip_##BD##_pixel_cmp_batch( int op, int i_pixel,                        
                                     const pixel *ref, intptr_t ref_stride,                      \
                                     const int64_t *fenc_off, const int64_t *ref_off,            \
                                     int n, int32_t *scores, void *stream );                     \
+                                                                                                \
+/* 64-bit block statistics (X264HIP_STAT_*): out[i] = the reference entry on                   \
+ * pix1 + off1[i] (and pix2 + off2[i] for SA8D_SATD / ASD8; pix2/off2 unused                    \
+ * otherwise), `height` used by VSAD / ASD8 only.  Device arrays. */                            \
+int x264hip_##BD##_pixel_stat_batch( int op, int i_pixel,                                       \
+                                     const pixel *pix1, intptr_t stride1,                       \
+                                     const pixel *pix2, intptr_t stride2,                       \
+                                     const int64_t *off1, const int64_t *off2,                  \
+                                     int height, int n, uint64_t *out, void *stream );          \
+                                                                                                \
+/* var2[i_pixel] (8x16 or 8x8, pixel.c:203-227) with explicit strides: the U                    \
+ * blocks at fenc + fenc_off[i] / fdec + fdec_off[i], the V blocks at +fenc_vdelta /            \
+ * +fdec_vdelta (the table entry uses FENC_STRIDE/2, FDEC_STRIDE/2);                            \
+ * out[3i] = return value, out[3i+1..2] = ssd[0..1]. */                                         \
+int x264hip_##BD##_var2_batch( int i_pixel, const pixel *fenc, intptr_t fenc_stride,            \
+                               intptr_t fenc_vdelta, const pixel *fdec, intptr_t fdec_stride,   \
+                               intptr_t fdec_vdelta, const int64_t *fenc_off,                   \
+                               const int64_t *fdec_off, int n, int32_t *out, void *stream );    \
+                                                                                                \
+/* successive elimination, n independent calls of ads[i_pixel] (pixel.c:759-803,               \
+ * slots aliased as :1605-1608): call i reads enc_dc[4i..4i+3], sums +                          \
+ * sums_off[i] (with the common `delta`), cost_mvx + cost_off[i], width[i] and                  \
+ * thresh[i]; writes the passing candidate indices in order to                                  \
+ * mvs[i*mvs_pitch ..] and their count to nmv[i].  Device arrays. */                            \
+int x264hip_##BD##_ads_batch( int i_pixel, const int32_t *enc_dc, const uint16_t *sums,         \
+                              int delta, const int64_t *sums_off, const uint16_t *cost_mvx,     \
+                              const int64_t *cost_off, const int32_t *width,                    \
+                              const int32_t *thresh, int n, int16_t *mvs, int mvs_pitch,        \
+                              int32_t *nmv, void *stream );                                     \
+                                                                                                \
+/* ESA integral image of n_frames luma planes (x264_frame_filter, mc.c:748-782;                 \
+ * integral_init* mc.c:424-456): plane / integral point at (0,0), rows                          \
+ * [-32, lines+32) with common stride; row starts at x = -padh (PADH_ALIGN,                     \
+ * frame.h:34).  Writes the 8x8 box sums of rows [1-32, lines+32-8) and columns                 \
+ * [-padh, stride-padh-8) -- the values the reference leaves there -- and, when                 \
+ * sub8x8, the 4x4 box sums in the second plane at +stride*(lines+64). */                        \
+int x264hip_##BD##_frame_integral( const pixel *plane, intptr_t stride, intptr_t frame_stride,  \
+                                   int lines, int padh, int sub8x8, int n_frames,               \
+                                   uint16_t *integral, intptr_t integral_frame_stride,          \
+                                   void *stream );                                              \
                                                                                                 \
 /* exhaustive integer-pel search table (the candidate set of reference                          \
  * encoder/me.c:618-631 before mv costs).  For every 16x16 macroblock of                        \

@@ -203,6 +203,256 @@ void FN(cmp_list)( int op, int i_pixel, const pixel *fenc, intptr_t fs, const pi
 }
 
 /*============================================================================
+ * further pixel_function_t entries — reference common/pixel.c
+ *==========================================================================*/
+
+/* sa8d_8x8 (unnormalised), packed pairs; reference common/pixel.c:334-366 */
+static int sa8d_8x8_raw( const pixel *pix1, intptr_t i1, const pixel *pix2, intptr_t i2 )
+{
+    sum2_t tmp[8][4], a0, a1, a2, a3, a4, a5, a6, a7, b0, b1, b2, b3, sum = 0;
+    for( int i = 0; i < 8; i++, pix1 += i1, pix2 += i2 )
+    {
+        a0 = (sum2_t)(pix1[0] - pix2[0]); a1 = (sum2_t)(pix1[1] - pix2[1]);
+        b0 = (a0 + a1) + ((a0 - a1) << BITS_PER_SUM);
+        a2 = (sum2_t)(pix1[2] - pix2[2]); a3 = (sum2_t)(pix1[3] - pix2[3]);
+        b1 = (a2 + a3) + ((a2 - a3) << BITS_PER_SUM);
+        a4 = (sum2_t)(pix1[4] - pix2[4]); a5 = (sum2_t)(pix1[5] - pix2[5]);
+        b2 = (a4 + a5) + ((a4 - a5) << BITS_PER_SUM);
+        a6 = (sum2_t)(pix1[6] - pix2[6]); a7 = (sum2_t)(pix1[7] - pix2[7]);
+        b3 = (a6 + a7) + ((a6 - a7) << BITS_PER_SUM);
+        HADAMARD4( tmp[i][0], tmp[i][1], tmp[i][2], tmp[i][3], b0, b1, b2, b3 );
+    }
+    for( int i = 0; i < 4; i++ )
+    {
+        HADAMARD4( a0, a1, a2, a3, tmp[0][i], tmp[1][i], tmp[2][i], tmp[3][i] );
+        HADAMARD4( a4, a5, a6, a7, tmp[4][i], tmp[5][i], tmp[6][i], tmp[7][i] );
+        b0  = abs2( a0 + a4 ) + abs2( a0 - a4 );
+        b0 += abs2( a1 + a5 ) + abs2( a1 - a5 );
+        b0 += abs2( a2 + a6 ) + abs2( a2 - a6 );
+        b0 += abs2( a3 + a7 ) + abs2( a3 - a7 );
+        sum += (sum_t)b0 + (b0 >> BITS_PER_SUM);
+    }
+    return (int)sum;
+}
+
+/* sa8d[PIXEL_8x8] / sa8d[PIXEL_16x16], (sum+2)>>2; reference pixel.c:368-381 */
+int FN(sa8d)( int i_pixel, const pixel *pix1, intptr_t i1, const pixel *pix2, intptr_t i2 )
+{
+    int sum = sa8d_8x8_raw( pix1, i1, pix2, i2 );
+    if( i_pixel == 0 )
+        sum += sa8d_8x8_raw( pix1 + 8, i1, pix2 + 8, i2 )
+             + sa8d_8x8_raw( pix1 + 8*i1, i1, pix2 + 8*i2, i2 )
+             + sa8d_8x8_raw( pix1 + 8 + 8*i1, i1, pix2 + 8 + 8*i2, i2 );
+    return (sum + 2) >> 2;
+}
+
+/* sa8d_satd[PIXEL_16x16]: asm-only in the reference (pixel.c:922, x86/pixel-a.asm
+ * SA8D_SATD); its contract is the checkasm test (tools/checkasm.c:424-460):
+ * low 32 bits = sa8d_16x16, high 32 bits = satd_16x16. */
+uint64_t FN(sa8d_satd)( const pixel *pix1, intptr_t i1, const pixel *pix2, intptr_t i2 )
+{
+    return (uint32_t)FN(sa8d)( 0, pix1, i1, pix2, i2 ) | ((uint64_t)(uint32_t)FN(satd)( 0, pix1, i1, pix2, i2 ) << 32);
+}
+
+/* pixel_hadamard_ac, reference common/pixel.c:383-418 */
+static uint64_t hadamard_ac_raw( const pixel *pix, intptr_t stride )
+{
+    sum2_t tmp[32], a0, a1, a2, a3, dc, sum4 = 0, sum8 = 0;
+    for( int i = 0; i < 8; i++, pix += stride )
+    {
+        sum2_t *t = tmp + (i & 3) + (i & 4) * 4;
+        a0 = (pix[0] + pix[1]) + ((sum2_t)(pix[0] - pix[1]) << BITS_PER_SUM);
+        a1 = (pix[2] + pix[3]) + ((sum2_t)(pix[2] - pix[3]) << BITS_PER_SUM);
+        t[0] = a0 + a1;
+        t[4] = a0 - a1;
+        a2 = (pix[4] + pix[5]) + ((sum2_t)(pix[4] - pix[5]) << BITS_PER_SUM);
+        a3 = (pix[6] + pix[7]) + ((sum2_t)(pix[6] - pix[7]) << BITS_PER_SUM);
+        t[8] = a2 + a3;
+        t[12] = a2 - a3;
+    }
+    for( int i = 0; i < 8; i++ )
+    {
+        HADAMARD4( a0, a1, a2, a3, tmp[i*4+0], tmp[i*4+1], tmp[i*4+2], tmp[i*4+3] );
+        tmp[i*4+0] = a0; tmp[i*4+1] = a1; tmp[i*4+2] = a2; tmp[i*4+3] = a3;
+        sum4 += abs2( a0 ) + abs2( a1 ) + abs2( a2 ) + abs2( a3 );
+    }
+    for( int i = 0; i < 8; i++ )
+    {
+        HADAMARD4( a0, a1, a2, a3, tmp[i], tmp[8+i], tmp[16+i], tmp[24+i] );
+        sum8 += abs2( a0 ) + abs2( a1 ) + abs2( a2 ) + abs2( a3 );
+    }
+    dc = (sum_t)(tmp[0] + tmp[8] + tmp[16] + tmp[24]);
+    sum4 = (sum_t)sum4 + (sum4 >> BITS_PER_SUM) - dc;
+    sum8 = (sum_t)sum8 + (sum8 >> BITS_PER_SUM) - dc;
+    return ((uint64_t)sum8 << 32) + sum4;
+}
+
+/* HADAMARD_AC(w,h), reference common/pixel.c:420-435; i_pixel 0..3 */
+uint64_t FN(hadamard_ac)( int i_pixel, const pixel *pix, intptr_t stride )
+{
+    int w = pixel_w[i_pixel], h = pixel_h[i_pixel];
+    uint64_t sum = hadamard_ac_raw( pix, stride );
+    if( w == 16 )
+        sum += hadamard_ac_raw( pix + 8, stride );
+    if( h == 16 )
+        sum += hadamard_ac_raw( pix + 8*stride, stride );
+    if( w == 16 && h == 16 )
+        sum += hadamard_ac_raw( pix + 8*stride + 8, stride );
+    return ((sum >> 34) << 32) + ((uint32_t)sum >> 1);
+}
+
+/* PIXEL_VAR_C, reference common/pixel.c:181-198; i_pixel 0 (16x16), 2 (8x16), 3 (8x8) */
+uint64_t FN(var)( int i_pixel, const pixel *pix, intptr_t stride )
+{
+    int w = pixel_w[i_pixel], h = pixel_h[i_pixel];
+    uint32_t sum = 0, sqr = 0;
+    for( int y = 0; y < h; y++, pix += stride )
+        for( int x = 0; x < w; x++ )
+        {
+            sum += pix[x];
+            sqr += pix[x] * pix[x];
+        }
+    return sum + ((uint64_t)sqr << 32);
+}
+
+/* PIXEL_VAR2_C with explicit strides and U->V offsets, reference
+ * common/pixel.c:203-227 (the table form uses FENC_STRIDE / FDEC_STRIDE and
+ * V at +FENC_STRIDE/2, +FDEC_STRIDE/2); h 16 (shift 7) or 8 (shift 6) */
+int FN(var2_s)( int h, const pixel *fenc, intptr_t fs, intptr_t fvd, const pixel *fdec, intptr_t ds,
+                intptr_t dvd, int ssd[2] )
+{
+    int shift = h == 16 ? 7 : 6;
+    int sum_u = 0, sum_v = 0, sqr_u = 0, sqr_v = 0;
+    for( int y = 0; y < h; y++, fenc += fs, fdec += ds )
+        for( int x = 0; x < 8; x++ )
+        {
+            int du = fenc[x] - fdec[x];
+            int dv = fenc[x + fvd] - fdec[x + dvd];
+            sum_u += du; sum_v += dv;
+            sqr_u += du * du; sqr_v += dv * dv;
+        }
+    ssd[0] = sqr_u;
+    ssd[1] = sqr_v;
+    return (int)(sqr_u - ((int64_t)sum_u * sum_u >> shift) + sqr_v - ((int64_t)sum_v * sum_v >> shift));
+}
+
+int FN(var2)( int i_pixel, const pixel *fenc, const pixel *fdec, int ssd[2] )
+{
+    return FN(var2_s)( pixel_h[i_pixel], fenc, FENC_STRIDE, FENC_STRIDE / 2, fdec, FDEC_STRIDE, FDEC_STRIDE / 2, ssd );
+}
+
+/* pixel_vsad, reference common/pixel.c:716-723 */
+int FN(vsad)( const pixel *src, intptr_t stride, int height )
+{
+    int score = 0;
+    for( int i = 1; i < height; i++, src += stride )
+        for( int j = 0; j < 16; j++ )
+            score += abs( src[j] - src[j + stride] );
+    return score;
+}
+
+/* pixel_asd8, reference common/pixel.c:747-754 */
+int FN(asd8)( const pixel *pix1, intptr_t s1, const pixel *pix2, intptr_t s2, int height )
+{
+    int sum = 0;
+    for( int y = 0; y < height; y++, pix1 += s1, pix2 += s2 )
+        for( int x = 0; x < 8; x++ )
+            sum += pix1[x] - pix2[x];
+    return abs( sum );
+}
+
+/* x264_pixel_ads4/2/1 (successive elimination), reference common/pixel.c:759-803;
+ * nsums selects ads4 (4), ads2 (2) or ads1 (1) */
+int FN(ads)( int nsums, const int enc_dc[4], const uint16_t *sums, int delta, const uint16_t *cost_mvx,
+             int16_t *mvs, int width, int thresh )
+{
+    int nmv = 0;
+    for( int i = 0; i < width; i++, sums++ )
+    {
+        int ads;
+        if( nsums == 4 )
+            ads = abs( enc_dc[0] - sums[0] ) + abs( enc_dc[1] - sums[8] )
+                + abs( enc_dc[2] - sums[delta] ) + abs( enc_dc[3] - sums[delta + 8] );
+        else if( nsums == 2 )
+            ads = abs( enc_dc[0] - sums[0] ) + abs( enc_dc[1] - sums[delta] );
+        else
+            ads = abs( enc_dc[0] - sums[0] );
+        ads += cost_mvx[i];
+        if( ads < thresh )
+            mvs[nmv++] = (int16_t)i;
+    }
+    return nmv;
+}
+
+/* integral_init4h/8h/4v/8v, reference common/mc.c:424-456 */
+static void integral_init4h( uint16_t *sum, const pixel *pix, intptr_t stride )
+{
+    int v = pix[0] + pix[1] + pix[2] + pix[3];
+    for( int x = 0; x < stride - 4; x++ )
+    {
+        sum[x] = (uint16_t)(v + sum[x - stride]);
+        v += pix[x + 4] - pix[x];
+    }
+}
+
+static void integral_init8h( uint16_t *sum, const pixel *pix, intptr_t stride )
+{
+    int v = pix[0] + pix[1] + pix[2] + pix[3] + pix[4] + pix[5] + pix[6] + pix[7];
+    for( int x = 0; x < stride - 8; x++ )
+    {
+        sum[x] = (uint16_t)(v + sum[x - stride]);
+        v += pix[x + 8] - pix[x];
+    }
+}
+
+static void integral_init4v( uint16_t *sum8, uint16_t *sum4, intptr_t stride )
+{
+    for( int x = 0; x < stride - 8; x++ )
+        sum4[x] = (uint16_t)(sum8[x + 4*stride] - sum8[x]);
+    for( int x = 0; x < stride - 8; x++ )
+        sum8[x] = (uint16_t)(sum8[x + 8*stride] + sum8[x + 8*stride + 4] - sum8[x] - sum8[x + 4]);
+}
+
+static void integral_init8v( uint16_t *sum8, intptr_t stride )
+{
+    for( int x = 0; x < stride - 8; x++ )
+        sum8[x] = (uint16_t)(sum8[x + 8*stride] - sum8[x]);
+}
+
+/* the integral-image part of x264_frame_filter over a whole progressive frame
+ * (mb_y = 0 .. b_end in one pass), reference common/mc.c:748-782.  plane and
+ * integral point at (0,0); both have stride `stride`, rows [-PADV, lines+PADV)
+ * (the 4x4 plane follows at +stride*(lines+2*PADV) when sub8x8), and the row
+ * starts at x = -padh (PADH_ALIGN, frame.h:34; 32 for this repo's frames). */
+void FN(frame_integral)( const pixel *plane, intptr_t stride, int lines, int padh, int sub8x8,
+                         uint16_t *integral )
+{
+    const int padv = 32;
+    int start = -8, height = lines + 8 + padv - 9;
+    memset( integral - padv*stride - padh, 0, stride * sizeof(uint16_t) );
+    start = -padv;
+    for( int y = start; y < height; y++ )
+    {
+        const pixel *pix = plane + y*stride - padh;
+        uint16_t *sum8 = integral + (y + 1)*stride - padh;
+        if( sub8x8 )
+        {
+            integral_init4h( sum8, pix, stride );
+            sum8 -= 8*stride;
+            uint16_t *sum4 = sum8 + stride*(lines + padv*2);
+            if( y >= 8 - padv )
+                integral_init4v( sum8, sum4, stride );
+        }
+        else
+        {
+            integral_init8h( sum8, pix, stride );
+            if( y >= 8 - padv )
+                integral_init8v( sum8 - 8*stride, stride );
+        }
+    }
+}
+
+/*============================================================================
  * forward transforms — reference common/dct.c
  *==========================================================================*/
 

@@ -222,3 +222,58 @@ def get_ref(planes_flat, origin, stride, qx, qy, w, h):
         b = block(planes_flat[HPEL_REF1[idx]], off + ((qx & 3) == 3), stride, w, h)
         return (a + b + 1) >> 1
     return a
+
+
+# ---------------------------------------------------------------- further pixel entries
+def _hadamard(n):
+    h = np.array([[1]], np.int64)
+    while h.shape[0] < n:
+        h = np.block([[h, h], [h, -h]])
+    return h
+
+
+H8 = _hadamard(8)
+
+
+def sa8d(a, b):
+    """sa8d 8x8 / 16x16: (sum over 8x8 tiles of sum |H8 . D . H8^T| + 2) >> 2 (pixel.c:334-381)."""
+    d = a - b
+    h, w = d.shape
+    t = d.reshape(h // 8, 8, w // 8, 8).transpose(0, 2, 1, 3)
+    coef = np.einsum("ij,abjk,lk->abil", H8, t, H8)
+    return int((np.abs(coef).sum() + 2) >> 2)
+
+
+def hadamard_ac(p):
+    """(sum8 >> 2) << 32 | (sum4 >> 1) over 8x8 tiles, where sum4 = sum |H4 coefs| of the four 4x4
+    sub-blocks minus their DCs and sum8 = sum |H8 coefs| minus the DC (pixel.c:383-435)."""
+    h, w = p.shape
+    s4 = s8 = 0
+    for y in range(0, h, 8):
+        for x in range(0, w, 8):
+            t = p[y:y + 8, x:x + 8]
+            c8 = H8 @ t @ H8.T
+            s8 += int(np.abs(c8).sum() - abs(c8[0, 0]))
+            for yy in (0, 4):
+                for xx in (0, 4):
+                    c4 = H4 @ t[yy:yy + 4, xx:xx + 4] @ H4.T
+                    s4 += int(np.abs(c4).sum() - abs(c4[0, 0]))
+    return ((s8 >> 2) << 32) + (s4 >> 1)
+
+
+def var(p):
+    return int(p.sum()) + (int((p * p).sum()) << 32)
+
+
+def var2(u, du, v, dv, h):
+    """var2 over 8-wide U/V blocks (fenc - fdec differences); returns (res, ssd_u, ssd_v)."""
+    shift = 7 if h == 16 else 6
+    a, b = u - du, v - dv
+    su, sv, qu, qv = int(a.sum()), int(b.sum()), int((a * a).sum()), int((b * b).sum())
+    return qu - ((su * su) >> shift) + qv - ((sv * sv) >> shift), qu, qv
+
+
+def box_sums(plane2d, k):
+    """k x k box sums at every top-left position (valid region), int64."""
+    c = np.pad(plane2d.astype(np.int64), ((1, 0), (1, 0))).cumsum(0).cumsum(1)
+    return c[k:, k:] - c[:-k, k:] - c[k:, :-k] + c[:-k, :-k]

@@ -67,6 +67,16 @@ for _bd in (8, 10):
     _f(_bd, "me_esa_argmin", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
     _f(_bd, "subpel_list", [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P])
+    _f(_bd, "sa8d", [C.c_int, _P, _IP, _P, _IP], C.c_int)
+    _f(_bd, "sa8d_satd", [_P, _IP, _P, _IP], C.c_uint64)
+    _f(_bd, "hadamard_ac", [C.c_int, _P, _IP], C.c_uint64)
+    _f(_bd, "var", [C.c_int, _P, _IP], C.c_uint64)
+    _f(_bd, "var2", [C.c_int, _P, _P, _P], C.c_int)
+    _f(_bd, "var2_s", [C.c_int, _P, _IP, _IP, _P, _IP, _IP, _P], C.c_int)
+    _f(_bd, "vsad", [_P, _IP, C.c_int], C.c_int)
+    _f(_bd, "asd8", [_P, _IP, _P, _IP, C.c_int], C.c_int)
+    _f(_bd, "ads", [C.c_int, _P, _P, C.c_int, _P, _P, C.c_int, C.c_int], C.c_int)
+    _f(_bd, "frame_integral", [_P, _IP, C.c_int, C.c_int, C.c_int, _P])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
@@ -221,3 +231,60 @@ def me_esa_argmin(bd, table, rng, me_range, par, init_cost, cost_mv, c0):
     getattr(_L, f"oracle{bd}_me_esa_argmin")(_addr(t), rng, len(p), me_range, _addr(p), _addr(ic),
                                             _addr(cost_mv, c0), _addr(out))
     return out
+
+
+# ---------------------------------------------------------------- further pixel entries
+def sa8d(bd, i_pixel, a, a_off, sa, b, b_off, sb):
+    return getattr(_L, f"oracle{bd}_sa8d")(i_pixel, _addr(a, a_off), sa, _addr(b, b_off), sb)
+
+
+def sa8d_satd(bd, a, a_off, sa, b, b_off, sb):
+    return getattr(_L, f"oracle{bd}_sa8d_satd")(_addr(a, a_off), sa, _addr(b, b_off), sb)
+
+
+def hadamard_ac(bd, i_pixel, a, a_off, sa):
+    return getattr(_L, f"oracle{bd}_hadamard_ac")(i_pixel, _addr(a, a_off), sa)
+
+
+def var(bd, i_pixel, a, a_off, sa):
+    return getattr(_L, f"oracle{bd}_var")(i_pixel, _addr(a, a_off), sa)
+
+
+def var2(bd, i_pixel, fenc, f_off, fdec, d_off):
+    """table form: fenc stride 16 (V at +8), fdec stride 32 (V at +16); returns (res, ssd_u, ssd_v)."""
+    ssd = np.zeros(2, np.int32)
+    r = getattr(_L, f"oracle{bd}_var2")(i_pixel, _addr(fenc, f_off), _addr(fdec, d_off), _addr(ssd))
+    return r, int(ssd[0]), int(ssd[1])
+
+
+def var2_s(bd, h, fenc, f_off, fs, fvd, fdec, d_off, ds, dvd):
+    ssd = np.zeros(2, np.int32)
+    r = getattr(_L, f"oracle{bd}_var2_s")(h, _addr(fenc, f_off), fs, fvd, _addr(fdec, d_off), ds, dvd, _addr(ssd))
+    return r, int(ssd[0]), int(ssd[1])
+
+
+def vsad(bd, a, a_off, stride, height):
+    return getattr(_L, f"oracle{bd}_vsad")(_addr(a, a_off), stride, height)
+
+
+def asd8(bd, a, a_off, sa, b, b_off, sb, height):
+    return getattr(_L, f"oracle{bd}_asd8")(_addr(a, a_off), sa, _addr(b, b_off), sb, height)
+
+
+def ads(bd, nsums, enc_dc, sums, s_off, delta, cost_mvx, c_off, width, thresh):
+    """x264_pixel_ads{4,2,1}; returns the candidate index list (int16)."""
+    dc = np.ascontiguousarray(enc_dc, np.int32)
+    mvs = np.zeros(max(width, 1), np.int16)
+    n = getattr(_L, f"oracle{bd}_ads")(nsums, _addr(dc), _addr(sums, s_off), delta, _addr(cost_mvx, c_off),
+                                       _addr(mvs), width, thresh)
+    return mvs[:n].copy()
+
+
+def frame_integral(bd, plane, origin, stride, lines, padh, sub8x8):
+    """integral part of x264_frame_filter; returns the uint16 buffer [(2 if sub8x8 else 1)*(lines+64), stride]
+    whose element (32*stride + padh) is the integral's (0, 0)."""
+    rows = (lines + 64) * (2 if sub8x8 else 1)
+    buf = np.zeros(rows * stride, np.uint16)
+    getattr(_L, f"oracle{bd}_frame_integral")(_addr(plane, origin), stride, lines, padh, sub8x8,
+                                             _addr(buf, 32 * stride + padh))
+    return buf.reshape(rows, stride)

@@ -87,7 +87,11 @@ def test_cmp_batch_empty_and_bad_args(hip):
     p = ctypes.c_void_p(dev.data_ptr())
     assert L.x264hip_8_pixel_cmp_batch(0, 0, p, 16, p, 16, ctypes.c_void_p(off.data_ptr()),
                                        ctypes.c_void_p(off.data_ptr()), 0, ctypes.c_void_p(sc.data_ptr()), None) == 0
-    assert L.x264hip_8_pixel_cmp_batch(3, 0, p, 16, p, 16, None, None, 1, None, None) == -1   # bad op
+    assert L.x264hip_8_pixel_cmp_batch(7, 0, p, 16, p, 16, None, None, 1, None, None) == -1   # bad op
+    assert L.x264hip_8_pixel_cmp_batch(3, 1, p, 16, p, 16, None, None, 1, None, None) == -1   # sa8d 16x8
+    assert L.x264hip_8_pixel_stat_batch(5, 0, p, 16, p, 16, None, None, 0, 1, None, None) == -1  # bad op
+    assert L.x264hip_8_pixel_stat_batch(0, 1, p, 16, p, 16, None, None, 0, 1, None, None) == -1  # var 16x8
+    assert L.x264hip_8_var2_batch(0, p, 16, 8, p, 32, 16, None, None, 1, None, None) == -1       # var2 16x16
     assert L.x264hip_8_pixel_cmp_batch(0, 8, p, 16, p, 16, None, None, 1, None, None) == -1   # bad size
     assert L.x264hip_8_me_search_full(p, 16, 0, p, 16, 0, 1, 1, 1, 5, None, None) == -1      # bad range
 

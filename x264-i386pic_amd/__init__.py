@@ -34,7 +34,8 @@ LIB_PATH = os.path.join(_HERE, "libx264hip.so")
 # reference common/pixel.h:37-59
 PIXEL_16x16, PIXEL_16x8, PIXEL_8x16, PIXEL_8x8, PIXEL_8x4, PIXEL_4x8, PIXEL_4x4, PIXEL_4x16 = range(8)
 PIXEL_SIZES = [(16, 16), (16, 8), (8, 16), (8, 8), (8, 4), (4, 8), (4, 4), (4, 16)]
-CMP_SAD, CMP_SSD, CMP_SATD = 0, 1, 2
+CMP_SAD, CMP_SSD, CMP_SATD, CMP_SA8D = 0, 1, 2, 3
+STAT_VAR, STAT_HADAMARD_AC, STAT_SA8D_SATD, STAT_VSAD, STAT_ASD8 = 0, 1, 2, 3, 4
 DCT_SUB4x4, DCT_SUB8x8, DCT_SUB16x16, DCT_SUB8x8_DC, DCT_SUB8x16_DC, DCT_SUB8x8_8, DCT_SUB16x16_8 = range(7)
 DCT_OUT_SIZE = [16, 64, 256, 4, 8, 64, 256]
 DC_4x4, DC_2x4 = 0, 1
@@ -88,6 +89,12 @@ DC_T = _c.CFUNCTYPE(None, _P)                     # dct4x4dc(d)
 DC2_T = _c.CFUNCTYPE(None, _P, _P)                # dct2x4dc(dct, dct4x4)
 QUANT_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P)      # quant_*(dct, mf, bias)
 QUANT_DC_T = _c.CFUNCTYPE(_c.c_int, _P, _c.c_int, _c.c_int)
+VSAD_T = _c.CFUNCTYPE(_c.c_int, _P, _IP, _c.c_int)                 # vsad(pix, stride, height)
+ASD8_T = _c.CFUNCTYPE(_c.c_int, _P, _IP, _P, _IP, _c.c_int)        # asd8(p1, s1, p2, s2, height)
+CMP64_T = _c.CFUNCTYPE(_c.c_uint64, _P, _IP, _P, _IP)              # sa8d_satd
+VAR_T = _c.CFUNCTYPE(_c.c_uint64, _P, _IP)                         # var / hadamard_ac
+VAR2_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P)                        # var2(fenc, fdec, ssd[2])
+ADS_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _c.c_int, _P, _P, _c.c_int, _c.c_int)
 
 
 class PixelFunctions(_c.Structure):
@@ -96,11 +103,11 @@ class PixelFunctions(_c.Structure):
         ("sad", CMP_T * 8), ("ssd", CMP_T * 8), ("satd", CMP_T * 8), ("ssim", CMP_T * 7),
         ("sa8d", CMP_T * 4), ("mbcmp", CMP_T * 8), ("mbcmp_unaligned", CMP_T * 8),
         ("fpelcmp", CMP_T * 8), ("fpelcmp_x3", CMP_X3_T * 7), ("fpelcmp_x4", CMP_X4_T * 7),
-        ("sad_aligned", CMP_T * 8), ("vsad", _P), ("asd8", _P), ("sa8d_satd", _P * 1),
-        ("var", _P * 4), ("var2", _P * 4), ("hadamard_ac", _P * 4), ("ssd_nv12_core", _P),
+        ("sad_aligned", CMP_T * 8), ("vsad", VSAD_T), ("asd8", ASD8_T), ("sa8d_satd", CMP64_T * 1),
+        ("var", VAR_T * 4), ("var2", VAR2_T * 4), ("hadamard_ac", VAR_T * 4), ("ssd_nv12_core", _P),
         ("ssim_4x4x2_core", _P), ("ssim_end4", _P),
         ("sad_x3", CMP_X3_T * 7), ("sad_x4", CMP_X4_T * 7),
-        ("satd_x3", CMP_X3_T * 7), ("satd_x4", CMP_X4_T * 7), ("ads", _P * 7),
+        ("satd_x3", CMP_X3_T * 7), ("satd_x4", CMP_X4_T * 7), ("ads", ADS_T * 7),
     ] + [(n, _P) for n in (
         "intra_mbcmp_x3_16x16", "intra_satd_x3_16x16", "intra_sad_x3_16x16",
         "intra_mbcmp_x3_4x4", "intra_satd_x3_4x4", "intra_sad_x3_4x4",
@@ -198,7 +205,11 @@ def _declare(L):
         f("subpel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, _c.c_int, _P, _P]
         f("mb_dct_quant").argtypes = [_c.c_int, _P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int,
                                       _P, _P, _P, _P, _P]
-        for n in ("pixel_cmp_batch", "me_search_full", "me_esa_argmin", "hpel_filter", "subpel_cmp_batch", "sub_dct_batch", "dc_batch", "quant_batch",
+        f("pixel_stat_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _IP, _P, _P, _c.c_int, _c.c_int, _P, _P]
+        f("var2_batch").argtypes = [_c.c_int, _P, _IP, _IP, _P, _IP, _IP, _P, _P, _c.c_int, _P, _P]
+        f("ads_batch").argtypes = [_c.c_int, _P, _P, _c.c_int, _P, _P, _P, _P, _P, _c.c_int, _P, _c.c_int, _P, _P]
+        f("frame_integral").argtypes = [_P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _IP, _P]
+        for n in ("pixel_stat_batch", "var2_batch", "ads_batch", "frame_integral", "pixel_cmp_batch", "me_search_full", "me_esa_argmin", "hpel_filter", "subpel_cmp_batch", "sub_dct_batch", "dc_batch", "quant_batch",
                   "quant_dc_batch", "mb_dct_quant"):
             f(n).restype = _c.c_int
 
@@ -274,6 +285,64 @@ def pixel_cmp_batch(op, i_pixel, fenc, fenc_stride, ref, ref_stride, fenc_off, r
         op, i_pixel, _ptr(fenc), fenc_stride, _ptr(ref), ref_stride, _ptr(fenc_off), _ptr(ref_off), n,
         _ptr(scores), _stream()), "pixel_cmp_batch")
     return scores
+
+
+def pixel_stat_batch(op, i_pixel, pix1, stride1, off1, pix2=None, stride2=0, off2=None, height=0, out=None):
+    """out[i] (uint64 as int64 tensor) = STAT_* entry at pix1 + off1[i] (and pix2 + off2[i])."""
+    import torch
+    bd = _pix_bd(pix1)
+    n = off1.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.int64, device=pix1.device)
+    p2 = pix2 if pix2 is not None else pix1
+    o2 = off2 if off2 is not None else off1
+    _rc(getattr(lib(), f"x264hip_{bd}_pixel_stat_batch")(
+        op, i_pixel, _ptr(pix1), stride1, _ptr(p2), stride2 or stride1, _ptr(off1), _ptr(o2), height, n,
+        _ptr(out), _stream()), "pixel_stat_batch")
+    return out
+
+
+def var2_batch(i_pixel, fenc, fenc_stride, fenc_vdelta, fdec, fdec_stride, fdec_vdelta, fenc_off, fdec_off,
+               out=None):
+    """int32 [n, 3] = (var2 result, ssd_u, ssd_v) per U/V block pair."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = fenc_off.numel()
+    if out is None:
+        out = torch.empty((n, 3), dtype=torch.int32, device=fenc.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_var2_batch")(
+        i_pixel, _ptr(fenc), fenc_stride, fenc_vdelta, _ptr(fdec), fdec_stride, fdec_vdelta, _ptr(fenc_off),
+        _ptr(fdec_off), n, _ptr(out), _stream()), "var2_batch")
+    return out
+
+
+def ads_batch(bitdepth, i_pixel, enc_dc, sums, delta, sums_off, cost_mvx, cost_off, width, thresh, mvs_pitch=None):
+    """n calls of ads[i_pixel]; returns (mvs int16 [n, pitch], nmv int32 [n])."""
+    import torch
+    _check_bd(bitdepth)
+    n = sums_off.numel()
+    pitch = mvs_pitch if mvs_pitch is not None else max(1, int(width.max().item()) if n else 1)
+    mvs = torch.full((n, pitch), -1, dtype=torch.int16, device=sums.device)
+    nmv = torch.empty(n, dtype=torch.int32, device=sums.device)
+    _rc(getattr(lib(), f"x264hip_{bitdepth}_ads_batch")(
+        i_pixel, _ptr(enc_dc), _ptr(sums), delta, _ptr(sums_off), _ptr(cost_mvx), _ptr(cost_off), _ptr(width),
+        _ptr(thresh), n, _ptr(mvs), pitch, _ptr(nmv), _stream()), "ads_batch")
+    return mvs, nmv
+
+
+def frame_integral(planes, origin, stride, lines, padh=PAD, sub8x8=False, out=None):
+    """ESA integral image per frame: uint16 (as int16) [n, (2 if sub8x8 else 1) * (lines + 2*PAD), stride];
+    element [f, PAD + y, padh + x] is (x, y).  planes: [n, rows, stride] padded planes."""
+    import torch
+    bd = _pix_bd(planes)
+    n = planes.shape[0]
+    rows = (lines + 2 * PAD) * (2 if sub8x8 else 1)
+    if out is None:
+        out = torch.zeros((n, rows, stride), dtype=torch.int16, device=planes.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_frame_integral")(
+        _ptr(planes, origin), stride, planes[0].numel(), lines, padh, int(bool(sub8x8)), n,
+        _ptr(out, PAD * stride + padh), out[0].numel(), _stream()), "frame_integral")
+    return out
 
 
 def me_table_pitch(rng):

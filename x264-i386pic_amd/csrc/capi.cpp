@@ -184,6 +184,107 @@ static void cmp_x4( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *p0, ty
     cmpx_call<BD, OP, IPIX, 4>( fenc, r, stride, scores );
 }
 
+// sa8d_satd / var / hadamard_ac / vsad / asd8: one lane of the u64 statistics kernel
+template <int BD, int OP, int IPIX>
+static uint64_t stat_call( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::pixel *p2, intptr_t s2,
+                           int w, int h, int height )
+{
+    using pixel = typename PT<BD>::pixel;
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    uint64_t *out = (uint64_t *)(c.host + ST_SC);
+    if( (size_t)w * h * sizeof(pixel) > ST_B - ST_A )
+    {
+        fprintf( stderr, "x264hip: block of %dx%d exceeds the per-call staging buffer\n", w, h );
+        abort();
+    }
+    stage_block( a, p1, s1, w, h );
+    if( p2 )
+        stage_block( b, p2, s2, w, h );
+    off[0] = off[1] = 0;
+    CHECK_FATAL( launch_stat_batch<BD>( OP, IPIX, dview( c, a ), w, dview( c, b ), w, dview( c, off ),
+                                        dview( c, off + 1 ), height, 1, dview( c, out ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    return out[0];
+}
+
+template <int BD>
+static uint64_t c_sa8d_satd( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::pixel *p2, intptr_t s2 )
+{ return stat_call<BD, X264HIP_STAT_SA8D_SATD, 0>( p1, s1, p2, s2, 16, 16, 0 ); }
+template <int BD, int IPIX>
+static uint64_t c_var( typename PT<BD>::pixel *p, intptr_t s )
+{ return stat_call<BD, X264HIP_STAT_VAR, IPIX>( p, s, nullptr, 0, pix_w( IPIX ), pix_h( IPIX ), 0 ); }
+template <int BD, int IPIX>
+static uint64_t c_hadamard_ac( typename PT<BD>::pixel *p, intptr_t s )
+{ return stat_call<BD, X264HIP_STAT_HADAMARD_AC, IPIX>( p, s, nullptr, 0, pix_w( IPIX ), pix_h( IPIX ), 0 ); }
+template <int BD>
+static int c_vsad( typename PT<BD>::pixel *p, intptr_t s, int height )
+{ return height < 2 ? 0 : (int)stat_call<BD, X264HIP_STAT_VSAD, 0>( p, s, nullptr, 0, 16, height, height ); }
+template <int BD>
+static int c_asd8( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::pixel *p2, intptr_t s2, int height )
+{ return height < 1 ? 0 : (int)stat_call<BD, X264HIP_STAT_ASD8, 3>( p1, s1, p2, s2, 8, height, height ); }
+
+// var2: U at fenc[x], V at fenc[x + FENC_STRIDE/2]; fdec stride FDEC_STRIDE (pixel.c:203-227)
+template <int BD, int IPIX>
+static int c_var2( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *fdec, int ssd[2] )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int H = pix_h( IPIX );
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    int32_t *out = (int32_t *)(c.host + ST_SC);
+    stage_block( a, fenc, X264HIP_FENC_STRIDE, 16, H );
+    stage_block( b, fdec, X264HIP_FDEC_STRIDE, 24, H );
+    off[0] = off[1] = 0;
+    CHECK_FATAL( launch_var2_batch<BD>( IPIX, dview( c, a ), 16, 8, dview( c, b ), 24, 16, dview( c, off ),
+                                        dview( c, off + 1 ), 1, dview( c, out ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    ssd[0] = out[1];
+    ssd[1] = out[2];
+    return out[0];
+}
+
+// ads: the rows the reference reads (sums[0..], sums[delta..], +8 for ads4) are staged
+// back to back with a compact delta (pixel.c:759-803)
+template <int IPIX>
+static int c_ads( int enc_dc[4], uint16_t *sums, int delta, uint16_t *cost_mvx, int16_t *mvs, int width, int thresh )
+{
+    constexpr int NS = ads_nsums( IPIX );
+    if( width <= 0 )
+        return 0;
+    CallCtx &c = call_ctx();
+    const int len = width + (NS == 4 ? 8 : 0);
+    const int dstage = (len + 7) & ~7;
+    uint16_t *sm = (uint16_t *)(c.host + ST_B);
+    uint16_t *cm = (uint16_t *)(c.host + ST_COEF);
+    int16_t *mv = (int16_t *)(c.host + ST_COEF + (12 << 10));
+    int32_t *par = (int32_t *)(c.host + ST_SC);          // enc_dc[4], width, thresh, nmv
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    if( 2 * dstage * sizeof(uint16_t) > ST_OFF - ST_B || width * sizeof(uint16_t) > (12 << 10) )
+    {
+        fprintf( stderr, "x264hip: ads width %d exceeds the per-call staging buffer\n", width );
+        abort();
+    }
+    memcpy( sm, sums, len * sizeof(uint16_t) );
+    if( NS > 1 )
+        memcpy( sm + dstage, sums + delta, len * sizeof(uint16_t) );
+    memcpy( cm, cost_mvx, width * sizeof(uint16_t) );
+    for( int k = 0; k < 4; k++ )
+        par[k] = k < NS ? enc_dc[k] : 0;
+    par[4] = width;
+    par[5] = thresh;
+    off[0] = off[1] = 0;
+    CHECK_FATAL( launch_ads_batch( IPIX, dview( c, par ), dview( c, sm ), dstage, dview( c, off ), dview( c, cm ),
+                                   dview( c, off + 1 ), dview( c, par + 4 ), dview( c, par + 5 ), 1, dview( c, mv ),
+                                   width, dview( c, par + 6 ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    const int n = par[6];
+    memcpy( mvs, mv, n * sizeof(int16_t) );
+    return n;
+}
+
 // ============================================================ per-call dct entries
 // kind as X264HIP_DCT_*; fenc stride 16, fdec stride 32 (reference dct.h:31-33)
 template <int BD, int KIND, int W, int H, int NOUT>
@@ -300,6 +401,30 @@ static void fill_pixel( Tab *pf )
     SIZES7( sad_x4, cmp_x4, 0 )
     SIZES7( satd_x3, cmp_x3, 2 )
     SIZES7( satd_x4, cmp_x4, 2 )
+    // pixel.c:852-867 (sa8d, var, var2, hadamard_ac, vsad, asd8, ads) and the
+    // asm-only merged sa8d_satd (pixel.c:922)
+    pf->sa8d[0] = cmp_call<BD, X264HIP_CMP_SA8D, 0>;
+    pf->sa8d[3] = cmp_call<BD, X264HIP_CMP_SA8D, 3>;
+    pf->sa8d_satd[0] = c_sa8d_satd<BD>;
+    pf->var[0] = c_var<BD, 0>;
+    pf->var[2] = c_var<BD, 2>;
+    pf->var[3] = c_var<BD, 3>;
+    pf->var2[2] = c_var2<BD, 2>;
+    pf->var2[3] = c_var2<BD, 3>;
+    pf->hadamard_ac[0] = c_hadamard_ac<BD, 0>;
+    pf->hadamard_ac[1] = c_hadamard_ac<BD, 1>;
+    pf->hadamard_ac[2] = c_hadamard_ac<BD, 2>;
+    pf->hadamard_ac[3] = c_hadamard_ac<BD, 3>;
+    pf->vsad = c_vsad<BD>;
+    pf->asd8 = c_asd8<BD>;
+    // ads slots with the reference's aliasing (pixel.c:835-838, 1605-1608)
+    pf->ads[0] = c_ads<0>;
+    pf->ads[1] = c_ads<1>;
+    pf->ads[2] = c_ads<2>;
+    pf->ads[3] = c_ads<3>;
+    pf->ads[4] = c_ads<4>;
+    pf->ads[5] = c_ads<5>;
+    pf->ads[6] = c_ads<6>;
 #undef SIZES8
 #undef SIZES7
 }
@@ -428,10 +553,49 @@ static int map_err( hipError_t e, const char *where )
                                                    const PT<BD>::pixel *ref, intptr_t rs, const int64_t *fo,         \
                                                    const int64_t *ro, int n, int32_t *scores, void *stream )        \
     {                                                                                                                \
-        if( op < 0 || op > 2 || i_pixel < 0 || i_pixel > 7 || n < 0 )                                                \
+        if( op < 0 || op > 3 || i_pixel < 0 || i_pixel > 7 || n < 0 )                                                \
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_cmp_batch<BD>( op, i_pixel, fenc, fs, ref, rs, fo, ro, n, scores,                     \
                                               (hipStream_t)stream ), "pixel_cmp_batch" );                            \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_pixel_stat_batch( int op, int i_pixel, const PT<BD>::pixel *p1, intptr_t s1,      \
+                                                    const PT<BD>::pixel *p2, intptr_t s2, const int64_t *o1,        \
+                                                    const int64_t *o2, int height, int n, uint64_t *out,            \
+                                                    void *stream )                                                   \
+    {                                                                                                                \
+        if( op < 0 || op > 4 || n < 0 || ( (op == 3 || op == 4) && height < 0 ) )                                    \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_stat_batch<BD>( op, i_pixel, p1, s1, p2, s2, o1, o2, height, n, out,                  \
+                                               (hipStream_t)stream ), "pixel_stat_batch" );                          \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_var2_batch( int i_pixel, const PT<BD>::pixel *fenc, intptr_t fs, intptr_t fvd,    \
+                                              const PT<BD>::pixel *fdec, intptr_t ds, intptr_t dvd,                  \
+                                              const int64_t *fo, const int64_t *dof, int n, int32_t *out,            \
+                                              void *stream )                                                         \
+    {                                                                                                                \
+        if( n < 0 )                                                                                                  \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_var2_batch<BD>( i_pixel, fenc, fs, fvd, fdec, ds, dvd, fo, dof, n, out,               \
+                                               (hipStream_t)stream ), "var2_batch" );                                \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_ads_batch( int i_pixel, const int32_t *enc_dc, const uint16_t *sums, int delta,   \
+                                             const int64_t *sums_off, const uint16_t *cost, const int64_t *cost_off, \
+                                             const int32_t *width, const int32_t *thresh, int n, int16_t *mvs,       \
+                                             int mvs_pitch, int32_t *nmv, void *stream )                             \
+    {                                                                                                                \
+        if( i_pixel < 0 || i_pixel > 6 || n < 0 || mvs_pitch < 0 )                                                   \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_ads_batch( i_pixel, enc_dc, sums, delta, sums_off, cost, cost_off, width, thresh, n,  \
+                                          mvs, mvs_pitch, nmv, (hipStream_t)stream ), "ads_batch" );                 \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_frame_integral( const PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride,    \
+                                                  int lines, int padh, int sub8x8, int nframes, uint16_t *integral,  \
+                                                  intptr_t ifstride, void *stream )                                  \
+    {                                                                                                                \
+        if( lines <= 0 || nframes < 0 || padh < 0 || stride < padh + 16 )                                            \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_frame_integral<BD>( plane, stride, fstride, lines, padh, sub8x8, nframes, integral,   \
+                                                   ifstride, (hipStream_t)stream ), "frame_integral" );              \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_me_search_full( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,             \
                                                   const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw,      \

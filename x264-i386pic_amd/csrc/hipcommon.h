@@ -33,6 +33,12 @@ __host__ __device__ constexpr int pix_h( int i )
     return i == 0 || i == 2 ? 16 : i == 1 || i == 3 || i == 5 ? 8 : i == 4 || i == 6 ? 4 : 16;
 }
 
+// ads slot -> number of DC sums (reference pixel.c:835-838 and the aliasing at :1605-1608)
+__host__ __device__ constexpr int ads_nsums( int i_pixel )
+{
+    return i_pixel == 0 ? 4 : (i_pixel == 3 || i_pixel == 6) ? 1 : 2;
+}
+
 // Load NDW packed dwords (NDW*PPD pixels) starting at an arbitrary pixel address.
 // Reads dword-aligned words only; the extra word needed for a misaligned start
 // is fetched only when the start is misaligned (otherwise the last word is
@@ -111,4 +117,20 @@ template <int BD>
 hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int nmb, int me_range,
                                  const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,
                                  hipStream_t stream );
+template <int BD>
+hipError_t launch_stat_batch( int op, int i_pixel, const typename PT<BD>::pixel *p1, intptr_t s1,
+                              const typename PT<BD>::pixel *p2, intptr_t s2, const int64_t *off1,
+                              const int64_t *off2, int height, int n, uint64_t *out, hipStream_t stream );
+template <int BD>
+hipError_t launch_var2_batch( int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t fvd,
+                              const typename PT<BD>::pixel *fdec, intptr_t ds, intptr_t dvd, const int64_t *fo,
+                              const int64_t *dof, int n, int32_t *out, hipStream_t stream );
+hipError_t launch_ads_batch( int i_pixel, const int32_t *enc_dc, const uint16_t *sums, int delta,
+                             const int64_t *sums_off, const uint16_t *cost, const int64_t *cost_off,
+                             const int32_t *width, const int32_t *thresh, int n, int16_t *mvs, int mvs_pitch,
+                             int32_t *nmv, hipStream_t stream );
+template <int BD>
+hipError_t launch_frame_integral( const typename PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride, int lines,
+                                  int padh, int sub8x8, int nframes, uint16_t *integral, intptr_t ifstride,
+                                  hipStream_t stream );
 } // namespace x264hip

@@ -1,7 +1,12 @@
-// Block metrics (SAD / SSD / SATD) over block lists in device memory.
+// Block metrics over block lists in device memory: SAD / SSD / SATD / SA8D
+// (int scores), var / hadamard_ac / sa8d_satd / vsad / asd8 (u64 statistics),
+// var2, successive-elimination ads and the ESA integral image.
 //
 // Semantics: reference common/pixel.c — PIXEL_SAD_C :55-70, PIXEL_SSD_C :85-101,
-// satd 4x4 / 8x4 and the PIXEL_SATD_C tiling :265-332.  SATD is computed in
+// satd 4x4 / 8x4 and the PIXEL_SATD_C tiling :265-332, sa8d :334-381,
+// hadamard_ac :383-435, var / var2 :181-227, vsad :716-723, asd8 :747-754,
+// ads :759-803; integral_init* common/mc.c:424-456 as used by
+// x264_frame_filter mc.c:748-782.  SATD is computed in
 // plain (unpacked) Hadamard form: every coefficient of a 4x4 Hadamard has the
 // parity of the block's difference sum, so the per-4x4 |coef| sum is even and
 // the reference's ">>1 per 8x4 pair" equals ">>1 per 4x4" (checked against the
@@ -57,6 +62,68 @@ __device__ __forceinline__ int satd4x4( const typename PT<BD>::pixel *a, intptr_
     return s >> 1;
 }
 
+// 8-point Hadamard (Sylvester order; only sums of |coef| are taken, so the
+// order is irrelevant)
+__device__ __forceinline__ void had8( int (&v)[8] )
+{
+#pragma unroll
+    for( int h = 1; h < 8; h <<= 1 )
+#pragma unroll
+        for( int i = 0; i < 8; i++ )
+            if( !(i & h) )
+            {
+                int a = v[i], b = v[i + h];
+                v[i] = a + b;
+                v[i + h] = a - b;
+            }
+}
+
+// load 8 pixels of a row as ints
+template <int BD>
+__device__ __forceinline__ void row8( const typename PT<BD>::pixel *p, int (&v)[8] )
+{
+    constexpr int PPD = PT<BD>::PPD;
+    uint32_t r[8 / PPD];
+    load_packed<8 / PPD>( p, r );
+#pragma unroll
+    for( int x = 0; x < 8; x++ )
+        v[x] = upix<BD>( r[x / PPD], x % PPD );
+}
+
+// unnormalised sa8d of one 8x8 tile: sum |H8 . D . H8^T| (equals the packed
+// sa8d_8x8 of pixel.c:334-366; cross-checked in tests/test_cpu_pixel_ext.py)
+template <int BD>
+__device__ __forceinline__ int sa8d8x8( const typename PT<BD>::pixel *a, intptr_t sa,
+                                        const typename PT<BD>::pixel *b, intptr_t sb )
+{
+    int d[8][8];
+#pragma unroll
+    for( int y = 0; y < 8; y++ )
+    {
+        int va[8], vb[8];
+        row8<BD>( a + y * sa, va );
+        row8<BD>( b + y * sb, vb );
+#pragma unroll
+        for( int x = 0; x < 8; x++ )
+            d[y][x] = va[x] - vb[x];
+        had8( d[y] );
+    }
+    int s = 0;
+#pragma unroll
+    for( int x = 0; x < 8; x++ )
+    {
+        int c[8];
+#pragma unroll
+        for( int y = 0; y < 8; y++ )
+            c[y] = d[y][x];
+        had8( c );
+#pragma unroll
+        for( int y = 0; y < 8; y++ )
+            s += abs( c[y] );
+    }
+    return s;
+}
+
 template <int BD, int OP, int IPIX>
 __global__ __launch_bounds__( 256 ) void cmp_batch_kernel( const typename PT<BD>::pixel *fenc, intptr_t fs,
                                                            const typename PT<BD>::pixel *ref, intptr_t rs,
@@ -104,6 +171,15 @@ __global__ __launch_bounds__( 256 ) void cmp_batch_kernel( const typename PT<BD>
                 }
         }
     }
+    else if constexpr( OP == 3 )     // SA8D (16x16, 8x8): (sum + 2) >> 2
+    {
+#pragma unroll
+        for( int y = 0; y < H; y += 8 )
+#pragma unroll
+            for( int x = 0; x < W; x += 8 )
+                sum += sa8d8x8<BD>( a + y * fs + x, fs, b + y * rs + x, rs );
+        sum = (sum + 2) >> 2;
+    }
     else                             // SATD
     {
 #pragma unroll
@@ -145,6 +221,16 @@ hipError_t launch_cmp_batch( int op, int i_pixel, const typename PT<BD>::pixel *
         case 0: return cmp_dispatch<BD, 0>( i_pixel, g, blk, stream, fenc, fs, ref, rs, fenc_off, ref_off, n, scores );
         case 1: return cmp_dispatch<BD, 1>( i_pixel, g, blk, stream, fenc, fs, ref, rs, fenc_off, ref_off, n, scores );
         case 2: return cmp_dispatch<BD, 2>( i_pixel, g, blk, stream, fenc, fs, ref, rs, fenc_off, ref_off, n, scores );
+        case 3:
+            if( i_pixel == 0 )
+                hipLaunchKernelGGL( ( cmp_batch_kernel<BD, 3, 0> ), g, blk, 0, stream, fenc, fs, ref, rs, fenc_off,
+                                    ref_off, n, scores );
+            else if( i_pixel == 3 )
+                hipLaunchKernelGGL( ( cmp_batch_kernel<BD, 3, 3> ), g, blk, 0, stream, fenc, fs, ref, rs, fenc_off,
+                                    ref_off, n, scores );
+            else
+                return hipErrorInvalidValue;
+            return hipGetLastError();
     }
     return hipErrorInvalidValue;
 }
@@ -153,5 +239,393 @@ template hipError_t launch_cmp_batch<8>( int, int, const uint8_t *, intptr_t, co
                                          const int64_t *, const int64_t *, int, int32_t *, hipStream_t );
 template hipError_t launch_cmp_batch<10>( int, int, const uint16_t *, intptr_t, const uint16_t *, intptr_t,
                                           const int64_t *, const int64_t *, int, int32_t *, hipStream_t );
+
+
+// ---------------------------------------------------------------------------
+// u64 statistics, one lane per item:
+//   OP 0 var (pixel.c:181-198)          OP 1 hadamard_ac (pixel.c:383-435)
+//   OP 2 sa8d_satd (16x16; low = sa8d, high = satd: checkasm.c:424-460)
+//   OP 3 vsad (16 wide, `height` rows)  OP 4 asd8 (8 wide, `height` rows)
+template <int BD>
+__device__ __forceinline__ void hadac8x8( const typename PT<BD>::pixel *p, intptr_t s, uint32_t &s4, uint32_t &s8 )
+{
+    // 4x4 Hadamards of the four quadrants, then the 2x2 Hadamard across the
+    // quadrants gives the 8x8 Hadamard coefficients (H8 = [[H4,H4],[H4,-H4]]
+    // up to row order)
+    int q[4][4][4];
+#pragma unroll
+    for( int y = 0; y < 8; y++ )
+    {
+        int v[8];
+        row8<BD>( p + y * s, v );
+#pragma unroll
+        for( int h = 0; h < 2; h++ )
+        {
+            int a0 = v[4 * h], a1 = v[4 * h + 1], a2 = v[4 * h + 2], a3 = v[4 * h + 3];
+            had4( a0, a1, a2, a3 );
+            int *r = q[(y >> 2) * 2 + h][y & 3];
+            r[0] = a0; r[1] = a1; r[2] = a2; r[3] = a3;
+        }
+    }
+    int sum4 = 0, sum8 = 0;
+#pragma unroll
+    for( int x = 0; x < 4; x++ )
+    {
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            had4( q[k][0][x], q[k][1][x], q[k][2][x], q[k][3][x] );
+#pragma unroll
+            for( int y = 0; y < 4; y++ )
+                sum4 += abs( q[k][y][x] );
+        }
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+        {
+            int a = q[0][y][x], b = q[1][y][x], c = q[2][y][x], d = q[3][y][x];
+            int e = a + b, f = a - b, g = c + d, h = c - d;
+            sum8 += abs( e + g ) + abs( e - g ) + abs( f + h ) + abs( f - h );
+        }
+    }
+    const int dc = q[0][0][0] + q[1][0][0] + q[2][0][0] + q[3][0][0];   // sum of the 64 pixels
+    s4 += (uint32_t)(sum4 - dc);
+    s8 += (uint32_t)(sum8 - dc);
+}
+
+template <int BD, int OP, int IPIX>
+__global__ __launch_bounds__( 256 ) void stat_batch_kernel( const typename PT<BD>::pixel *p1, intptr_t s1,
+                                                            const typename PT<BD>::pixel *p2, intptr_t s2,
+                                                            const int64_t *off1, const int64_t *off2, int height,
+                                                            int n, uint64_t *out )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    constexpr int PPD = PT<BD>::PPD;
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    const pixel *a = p1 + off1[i];
+    uint64_t r = 0;
+    if constexpr( OP == 0 )
+    {
+        uint32_t sum = 0, sqr = 0;
+#pragma unroll
+        for( int y = 0; y < H; y++ )
+        {
+            uint32_t w[W / PPD];
+            load_packed<W / PPD>( a + y * s1, w );
+#pragma unroll
+            for( int k = 0; k < W; k++ )
+            {
+                uint32_t v = (uint32_t)upix<BD>( w[k / PPD], k % PPD );
+                sum += v;
+                sqr += v * v;
+            }
+        }
+        r = sum + ((uint64_t)sqr << 32);
+    }
+    else if constexpr( OP == 1 )
+    {
+        uint32_t s4 = 0, s8 = 0;
+#pragma unroll
+        for( int y = 0; y < H; y += 8 )
+#pragma unroll
+            for( int x = 0; x < W; x += 8 )
+                hadac8x8<BD>( a + y * s1 + x, s1, s4, s8 );
+        r = ((uint64_t)(s8 >> 2) << 32) + (s4 >> 1);
+    }
+    else if constexpr( OP == 2 )
+    {
+        const pixel *b = p2 + off2[i];
+        int sa = 0, st = 0;
+#pragma unroll 1
+        for( int t = 0; t < 4; t++ )
+            sa += sa8d8x8<BD>( a + (t >> 1) * 8 * s1 + (t & 1) * 8, s1, b + (t >> 1) * 8 * s2 + (t & 1) * 8, s2 );
+#pragma unroll 1
+        for( int y = 0; y < 16; y += 4 )
+#pragma unroll
+            for( int x = 0; x < 16; x += 4 )
+                st += satd4x4<BD>( a + y * s1 + x, s1, b + y * s2 + x, s2 );
+        r = (uint32_t)((sa + 2) >> 2) | ((uint64_t)(uint32_t)st << 32);
+    }
+    else if constexpr( OP == 3 )
+    {
+        uint32_t acc = 0, prev[16 / PPD];
+        load_packed<16 / PPD>( a, prev );
+        for( int y = 1; y < height; y++ )
+        {
+            uint32_t cur[16 / PPD];
+            load_packed<16 / PPD>( a + y * s1, cur );
+#pragma unroll
+            for( int k = 0; k < 16 / PPD; k++ )
+            {
+                acc = sadp<BD>( prev[k], cur[k], acc );
+                prev[k] = cur[k];
+            }
+        }
+        r = acc;
+    }
+    else
+    {
+        const pixel *b = p2 + off2[i];
+        int sum = 0;
+        for( int y = 0; y < height; y++ )
+        {
+            int va[8], vb[8];
+            row8<BD>( a + y * s1, va );
+            row8<BD>( b + y * s2, vb );
+#pragma unroll
+            for( int x = 0; x < 8; x++ )
+                sum += va[x] - vb[x];
+        }
+        r = (uint32_t)abs( sum );
+    }
+    out[i] = r;
+}
+
+template <int BD>
+hipError_t launch_stat_batch( int op, int i_pixel, const typename PT<BD>::pixel *p1, intptr_t s1,
+                              const typename PT<BD>::pixel *p2, intptr_t s2, const int64_t *off1,
+                              const int64_t *off2, int height, int n, uint64_t *out, hipStream_t st )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (n + 255) / 256 );
+#define STAT( OP, I ) \
+    hipLaunchKernelGGL( ( stat_batch_kernel<BD, OP, I> ), g, blk, 0, st, p1, s1, p2, s2, off1, off2, height, n, out )
+    switch( op )
+    {
+        case 0:
+            if( i_pixel == 0 ) STAT( 0, 0 ); else if( i_pixel == 2 ) STAT( 0, 2 ); else if( i_pixel == 3 ) STAT( 0, 3 );
+            else return hipErrorInvalidValue;
+            break;
+        case 1:
+            if( i_pixel == 0 ) STAT( 1, 0 ); else if( i_pixel == 1 ) STAT( 1, 1 ); else if( i_pixel == 2 ) STAT( 1, 2 );
+            else if( i_pixel == 3 ) STAT( 1, 3 ); else return hipErrorInvalidValue;
+            break;
+        case 2:
+            if( i_pixel != 0 ) return hipErrorInvalidValue;
+            STAT( 2, 0 );
+            break;
+        case 3: STAT( 3, 0 ); break;
+        case 4: STAT( 4, 3 ); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef STAT
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// var2 (pixel.c:203-227), one lane per (U,V) block pair: out[3i] = result,
+// out[3i+1] = ssd_u, out[3i+2] = ssd_v.  V blocks sit at +vd from the U blocks.
+template <int BD, int H>
+__global__ __launch_bounds__( 256 ) void var2_batch_kernel( const typename PT<BD>::pixel *fenc, intptr_t fs,
+                                                            intptr_t fvd, const typename PT<BD>::pixel *fdec,
+                                                            intptr_t ds, intptr_t dvd, const int64_t *fo,
+                                                            const int64_t *dof, int n, int32_t *out )
+{
+    int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    const typename PT<BD>::pixel *a = fenc + fo[i], *b = fdec + dof[i];
+    int su = 0, sv = 0, qu = 0, qv = 0;
+#pragma unroll
+    for( int y = 0; y < H; y++ )
+    {
+        int au[8], bu[8], av[8], bv[8];
+        row8<BD>( a + y * fs, au );
+        row8<BD>( b + y * ds, bu );
+        row8<BD>( a + y * fs + fvd, av );
+        row8<BD>( b + y * ds + dvd, bv );
+#pragma unroll
+        for( int x = 0; x < 8; x++ )
+        {
+            int du = au[x] - bu[x], dv = av[x] - bv[x];
+            su += du; sv += dv;
+            qu += du * du; qv += dv * dv;
+        }
+    }
+    constexpr int SHIFT = H == 16 ? 7 : 6;
+    out[3 * i] = (int)(qu - ((int64_t)su * su >> SHIFT) + qv - ((int64_t)sv * sv >> SHIFT));
+    out[3 * i + 1] = qu;
+    out[3 * i + 2] = qv;
+}
+
+template <int BD>
+hipError_t launch_var2_batch( int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t fvd,
+                              const typename PT<BD>::pixel *fdec, intptr_t ds, intptr_t dvd, const int64_t *fo,
+                              const int64_t *dof, int n, int32_t *out, hipStream_t st )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (n + 255) / 256 );
+    if( i_pixel == 2 )
+        hipLaunchKernelGGL( ( var2_batch_kernel<BD, 16> ), g, blk, 0, st, fenc, fs, fvd, fdec, ds, dvd, fo, dof, n, out );
+    else if( i_pixel == 3 )
+        hipLaunchKernelGGL( ( var2_batch_kernel<BD, 8> ), g, blk, 0, st, fenc, fs, fvd, fdec, ds, dvd, fo, dof, n, out );
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// successive elimination (x264_pixel_ads4/2/1, pixel.c:759-803), one wave per
+// call: each lane scores one candidate, the passing indices are compacted in
+// candidate order with a ballot + mbcnt prefix, as the reference's mvs[nmv++].
+template <int NS>
+__global__ __launch_bounds__( 256 ) void ads_batch_kernel( const int32_t *enc_dc, const uint16_t *sums, int delta,
+                                                           const int64_t *sums_off, const uint16_t *cost,
+                                                           const int64_t *cost_off, const int32_t *width,
+                                                           const int32_t *thresh, int n, int16_t *mvs,
+                                                           int mvs_pitch, int32_t *nmv )
+{
+    const int job = blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if( job >= n )
+        return;
+    const uint16_t *sm = sums + sums_off[job];
+    const uint16_t *cm = cost + cost_off[job];
+    const int w = width[job], th = thresh[job];
+    const int d0 = enc_dc[4 * job], d1 = enc_dc[4 * job + 1], d2 = enc_dc[4 * job + 2], d3 = enc_dc[4 * job + 3];
+    int16_t *o = mvs + (int64_t)job * mvs_pitch;
+    int cnt = 0;
+    for( int base = 0; base < w; base += 64 )
+    {
+        const int i = base + lane;
+        bool pass = false;
+        if( i < w )
+        {
+            int a = abs( d0 - (int)sm[i] );
+            if constexpr( NS == 4 )
+                a += abs( d1 - (int)sm[i + 8] ) + abs( d2 - (int)sm[i + delta] ) + abs( d3 - (int)sm[i + delta + 8] );
+            else if constexpr( NS == 2 )
+                a += abs( d1 - (int)sm[i + delta] );
+            a += cm[i];
+            pass = a < th;
+        }
+        const uint64_t m = __ballot( pass );
+        const int pos = cnt + (int)__builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32),
+                                                              __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) );
+        if( pass )
+            o[pos] = (int16_t)i;
+        cnt += __popcll( m );
+    }
+    if( lane == 0 )
+        nmv[job] = cnt;
+}
+
+hipError_t launch_ads_batch( int i_pixel, const int32_t *enc_dc, const uint16_t *sums, int delta,
+                             const int64_t *sums_off, const uint16_t *cost, const int64_t *cost_off,
+                             const int32_t *width, const int32_t *thresh, int n, int16_t *mvs, int mvs_pitch,
+                             int32_t *nmv, hipStream_t st )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (n + 3) / 4 );
+    switch( ads_nsums( i_pixel ) )
+    {
+        case 4: hipLaunchKernelGGL( ads_batch_kernel<4>, g, blk, 0, st, enc_dc, sums, delta, sums_off, cost, cost_off,
+                                    width, thresh, n, mvs, mvs_pitch, nmv ); break;
+        case 2: hipLaunchKernelGGL( ads_batch_kernel<2>, g, blk, 0, st, enc_dc, sums, delta, sums_off, cost, cost_off,
+                                    width, thresh, n, mvs, mvs_pitch, nmv ); break;
+        default: hipLaunchKernelGGL( ads_batch_kernel<1>, g, blk, 0, st, enc_dc, sums, delta, sums_off, cost,
+                                     cost_off, width, thresh, n, mvs, mvs_pitch, nmv ); break;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// ESA integral image (x264_frame_filter, mc.c:748-782): the reference builds a
+// running 2-D prefix in uint16 and differences it (integral_init8h/8v or
+// 4h/4v, mc.c:424-456); every value it leaves in rows [1-PADV, lines+PADV-8)
+// and columns [-padh, stride-padh-8) is an exact 8x8 (and, with sub8x8, 4x4)
+// box sum with that top-left, which is what this kernel writes directly: one
+// lane per column walks a strip of rows with a sliding window of horizontal
+// sums (coalesced row loads and stores).
+constexpr int INTEGRAL_STRIP = 64;
+
+template <int BD, bool SUB8>
+__global__ __launch_bounds__( 256 ) void integral_kernel( const typename PT<BD>::pixel *plane, intptr_t stride,
+                                                          intptr_t fstride, int lines, int padh, uint16_t *integral,
+                                                          intptr_t ifstride )
+{
+    constexpr int PADV = 32;
+    constexpr int PPD = PT<BD>::PPD;
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;     // column, 0 = x -padh
+    if( c >= stride - 8 )
+        return;
+    const int rows_end = lines + 2 * PADV - 8;               // buffer rows [1, rows_end) are box rows
+    const int t0 = 1 + blockIdx.y * INTEGRAL_STRIP;
+    if( t0 >= rows_end )
+        return;
+    const int t1 = min( t0 + INTEGRAL_STRIP, rows_end );
+    const typename PT<BD>::pixel *src = plane + blockIdx.z * fstride - PADV * stride - padh + c;
+    uint16_t *o8 = integral + blockIdx.z * ifstride - PADV * stride - padh + c;
+    uint16_t *o4 = o8 + stride * (lines + 2 * PADV);
+    uint32_t ring8[8] = {}, ring4[4] = {};
+    uint32_t acc8 = 0, acc4 = 0;
+    // input rows t0 .. t1+6; after adding row r, acc8 holds rows r-7..r, acc4 rows r-3..r
+    for( int r0 = t0; r0 < t1 + 7; r0 += 8 )
+    {
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+        {
+            const int r = r0 + k;
+            if( r < t1 + 7 )
+            {
+                uint32_t w[8 / PPD];
+                load_packed<8 / PPD>( src + (intptr_t)r * stride, w );
+                uint32_t h4 = 0, h8 = 0;
+#pragma unroll
+                for( int x = 0; x < 4; x++ )
+                    h4 += (uint32_t)upix<BD>( w[x / PPD], x % PPD );
+                h8 = h4;
+#pragma unroll
+                for( int x = 4; x < 8; x++ )
+                    h8 += (uint32_t)upix<BD>( w[x / PPD], x % PPD );
+                acc8 += h8 - ring8[k];
+                ring8[k] = h8;
+                acc4 += h4 - ring4[k & 3];
+                ring4[k & 3] = h4;
+                if( r - 7 >= t0 )
+                    o8[(intptr_t)(r - 7) * stride] = (uint16_t)acc8;
+                if( SUB8 && r - 3 >= t0 && r - 3 < t1 )
+                    o4[(intptr_t)(r - 3) * stride] = (uint16_t)acc4;
+            }
+        }
+    }
+}
+
+template <int BD>
+hipError_t launch_frame_integral( const typename PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride, int lines,
+                                  int padh, int sub8x8, int nframes, uint16_t *integral, intptr_t ifstride,
+                                  hipStream_t st )
+{
+    if( nframes <= 0 )
+        return hipSuccess;
+    const int rows = lines + 64 - 9;
+    dim3 blk( 256 ), g( (unsigned)((stride - 8 + 255) / 256), (unsigned)((rows + INTEGRAL_STRIP - 1) / INTEGRAL_STRIP),
+                        (unsigned)nframes );
+    if( sub8x8 )
+        hipLaunchKernelGGL( ( integral_kernel<BD, true> ), g, blk, 0, st, plane, stride, fstride, lines, padh,
+                            integral, ifstride );
+    else
+        hipLaunchKernelGGL( ( integral_kernel<BD, false> ), g, blk, 0, st, plane, stride, fstride, lines, padh,
+                            integral, ifstride );
+    return hipGetLastError();
+}
+
+#define INST( BD )                                                                                                     \
+    template hipError_t launch_stat_batch<BD>( int, int, const PT<BD>::pixel *, intptr_t, const PT<BD>::pixel *,       \
+                                               intptr_t, const int64_t *, const int64_t *, int, int, uint64_t *,       \
+                                               hipStream_t );                                                          \
+    template hipError_t launch_var2_batch<BD>( int, const PT<BD>::pixel *, intptr_t, intptr_t, const PT<BD>::pixel *,  \
+                                               intptr_t, intptr_t, const int64_t *, const int64_t *, int, int32_t *,   \
+                                               hipStream_t );                                                          \
+    template hipError_t launch_frame_integral<BD>( const PT<BD>::pixel *, intptr_t, intptr_t, int, int, int, int,      \
+                                                   uint16_t *, intptr_t, hipStream_t );
+INST( 8 )
+INST( 10 )
+#undef INST
 
 } // namespace x264hip
