@@ -810,6 +810,471 @@ int FN(cqm_init)( const uint8_t *const scaling_list[8], int deadzone_inter, int 
 }
 
 /*============================================================================
+ * inverse path — reference common/dct.c, common/quant.c
+ *==========================================================================*/
+
+/* idct4x4dc, reference common/dct.c:78-107 (tmp as dctcoef) */
+void FN(idct4x4dc)( dctcoef d[16] )
+{
+    dctcoef tmp[16];
+    for( int i = 0; i < 4; i++ )
+    {
+        int s01 = d[i*4+0] + d[i*4+1], d01 = d[i*4+0] - d[i*4+1];
+        int s23 = d[i*4+2] + d[i*4+3], d23 = d[i*4+2] - d[i*4+3];
+        tmp[0*4+i] = s01 + s23; tmp[1*4+i] = s01 - s23;
+        tmp[2*4+i] = d01 - d23; tmp[3*4+i] = d01 + d23;
+    }
+    for( int i = 0; i < 4; i++ )
+    {
+        int s01 = tmp[i*4+0] + tmp[i*4+1], d01 = tmp[i*4+0] - tmp[i*4+1];
+        int s23 = tmp[i*4+2] + tmp[i*4+3], d23 = tmp[i*4+2] - tmp[i*4+3];
+        d[i*4+0] = s01 + s23; d[i*4+1] = s01 - s23;
+        d[i*4+2] = d01 - d23; d[i*4+3] = d01 + d23;
+    }
+}
+
+/* add4x4_idct with explicit dst stride, reference common/dct.c:272-309 */
+static void add4x4_idct_s( pixel *p_dst, intptr_t ds, const dctcoef dct[16] )
+{
+    dctcoef d[16], tmp[16];
+    for( int i = 0; i < 4; i++ )
+    {
+        int s02 = dct[0*4+i] + dct[2*4+i], d02 = dct[0*4+i] - dct[2*4+i];
+        int s13 = dct[1*4+i] + (dct[3*4+i] >> 1), d13 = (dct[1*4+i] >> 1) - dct[3*4+i];
+        tmp[i*4+0] = s02 + s13; tmp[i*4+1] = d02 + d13;
+        tmp[i*4+2] = d02 - d13; tmp[i*4+3] = s02 - s13;
+    }
+    for( int i = 0; i < 4; i++ )
+    {
+        int s02 = tmp[0*4+i] + tmp[2*4+i], d02 = tmp[0*4+i] - tmp[2*4+i];
+        int s13 = tmp[1*4+i] + (tmp[3*4+i] >> 1), d13 = (tmp[1*4+i] >> 1) - tmp[3*4+i];
+        d[0*4+i] = (s02 + s13 + 32) >> 6; d[1*4+i] = (d02 + d13 + 32) >> 6;
+        d[2*4+i] = (d02 - d13 + 32) >> 6; d[3*4+i] = (s02 - s13 + 32) >> 6;
+    }
+    for( int y = 0; y < 4; y++, p_dst += ds )
+        for( int x = 0; x < 4; x++ )
+            p_dst[x] = clip_pixel( p_dst[x] + d[y*4+x] );
+}
+
+static void add8x8_idct_s( pixel *p, intptr_t ds, const dctcoef dct[4][16] )
+{
+    add4x4_idct_s( p, ds, dct[0] );
+    add4x4_idct_s( p + 4, ds, dct[1] );
+    add4x4_idct_s( p + 4*ds, ds, dct[2] );
+    add4x4_idct_s( p + 4*ds + 4, ds, dct[3] );
+}
+
+static void add16x16_idct_s( pixel *p, intptr_t ds, const dctcoef dct[16][16] )
+{
+    add8x8_idct_s( p, ds, &dct[0] );
+    add8x8_idct_s( p + 8, ds, &dct[4] );
+    add8x8_idct_s( p + 8*ds, ds, &dct[8] );
+    add8x8_idct_s( p + 8*ds + 8, ds, &dct[12] );
+}
+
+/* IDCT8_1D and add8x8_idct8, reference common/dct.c:388-446; the reference
+ * works in place on dct (dctcoef stores), so this copy does too */
+#define IDCT8_1D {\
+    int a0 = SRC(0) + SRC(4), a2 = SRC(0) - SRC(4);\
+    int a4 = (SRC(2) >> 1) - SRC(6), a6 = (SRC(6) >> 1) + SRC(2);\
+    int b0 = a0 + a6, b2 = a2 + a4, b4 = a2 - a4, b6 = a0 - a6;\
+    int a1 = -SRC(3) + SRC(5) - SRC(7) - (SRC(7) >> 1);\
+    int a3 =  SRC(1) + SRC(7) - SRC(3) - (SRC(3) >> 1);\
+    int a5 = -SRC(1) + SRC(7) + SRC(5) + (SRC(5) >> 1);\
+    int a7 =  SRC(3) + SRC(5) + SRC(1) + (SRC(1) >> 1);\
+    int b1 = (a7 >> 2) + a1, b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5, b7 = a7 - (a1 >> 2);\
+    DST(0, b0 + b7); DST(1, b2 + b5); DST(2, b4 + b3); DST(3, b6 + b1);\
+    DST(4, b6 - b1); DST(5, b4 - b3); DST(6, b2 - b5); DST(7, b0 - b7);\
+}
+
+static void add8x8_idct8_s( pixel *dst, intptr_t ds, dctcoef dct[64] )
+{
+    dct[0] += 32;
+#define SRC(x) dct[(x)*8+i]
+#define DST(x, rhs) dct[(x)*8+i] = (rhs)
+    for( int i = 0; i < 8; i++ )
+        IDCT8_1D
+#undef SRC
+#undef DST
+#define SRC(x) dct[i*8+(x)]
+#define DST(x, rhs) dst[i + (x)*ds] = clip_pixel( dst[i + (x)*ds] + ((rhs) >> 6) )
+    for( int i = 0; i < 8; i++ )
+        IDCT8_1D
+#undef SRC
+#undef DST
+}
+
+static void add16x16_idct8_s( pixel *p, intptr_t ds, dctcoef dct[4][64] )
+{
+    add8x8_idct8_s( p, ds, dct[0] );
+    add8x8_idct8_s( p + 8, ds, dct[1] );
+    add8x8_idct8_s( p + 8*ds, ds, dct[2] );
+    add8x8_idct8_s( p + 8*ds + 8, ds, dct[3] );
+}
+
+/* add4x4_idct_dc / add8x8_idct_dc / add16x16_idct_dc, reference dct.c:448-476 */
+static void add4x4_idct_dc_s( pixel *p, intptr_t ds, dctcoef dc )
+{
+    dc = (dc + 32) >> 6;
+    for( int i = 0; i < 4; i++, p += ds )
+        for( int x = 0; x < 4; x++ )
+            p[x] = clip_pixel( p[x] + dc );
+}
+
+static void add8x8_idct_dc_s( pixel *p, intptr_t ds, const dctcoef dct[4] )
+{
+    add4x4_idct_dc_s( p, ds, dct[0] );
+    add4x4_idct_dc_s( p + 4, ds, dct[1] );
+    add4x4_idct_dc_s( p + 4*ds, ds, dct[2] );
+    add4x4_idct_dc_s( p + 4*ds + 4, ds, dct[3] );
+}
+
+static void add16x16_idct_dc_s( pixel *p, intptr_t ds, const dctcoef dct[16] )
+{
+    for( int i = 0; i < 4; i++, dct += 4, p += 4*ds )
+        for( int k = 0; k < 4; k++ )
+            add4x4_idct_dc_s( p + 4*k, ds, dct[k] );
+}
+
+/* table forms (p_dst stride FDEC_STRIDE) */
+void FN(add4x4_idct)( pixel *p, dctcoef dct[16] ) { add4x4_idct_s( p, FDEC_STRIDE, dct ); }
+void FN(add8x8_idct)( pixel *p, dctcoef dct[4][16] ) { add8x8_idct_s( p, FDEC_STRIDE, dct ); }
+void FN(add16x16_idct)( pixel *p, dctcoef dct[16][16] ) { add16x16_idct_s( p, FDEC_STRIDE, dct ); }
+void FN(add8x8_idct_dc)( pixel *p, dctcoef dct[4] ) { add8x8_idct_dc_s( p, FDEC_STRIDE, dct ); }
+void FN(add16x16_idct_dc)( pixel *p, dctcoef dct[16] ) { add16x16_idct_dc_s( p, FDEC_STRIDE, dct ); }
+void FN(add8x8_idct8)( pixel *p, dctcoef dct[64] ) { add8x8_idct8_s( p, FDEC_STRIDE, dct ); }
+void FN(add16x16_idct8)( pixel *p, dctcoef dct[4][64] ) { add16x16_idct8_s( p, FDEC_STRIDE, dct ); }
+
+/* list form of the batched add_idct entry: kind as X264HIP_IDCT_* (0 add4x4,
+ * 1 add8x8, 2 add16x16, 3 add8x8_dc, 4 add16x16_dc, 5 add8x8_8, 6 add16x16_8);
+ * block i reads dct + i*size (a private copy: the input is not modified) */
+static const int idct_kind_size[7] = { 16, 64, 256, 4, 16, 64, 256 };
+void FN(add_idct_list)( int kind, pixel *dst, intptr_t ds, const int64_t *dst_off, const dctcoef *dct, int n )
+{
+    dctcoef tmp[256];
+    for( int i = 0; i < n; i++ )
+    {
+        int sz = idct_kind_size[kind];
+        memcpy( tmp, dct + (size_t)i*sz, sz * sizeof(dctcoef) );
+        pixel *p = dst + dst_off[i];
+        switch( kind )
+        {
+            case 0: add4x4_idct_s( p, ds, tmp ); break;
+            case 1: add8x8_idct_s( p, ds, (dctcoef(*)[16])tmp ); break;
+            case 2: add16x16_idct_s( p, ds, (dctcoef(*)[16])tmp ); break;
+            case 3: add8x8_idct_dc_s( p, ds, tmp ); break;
+            case 4: add16x16_idct_dc_s( p, ds, tmp ); break;
+            case 5: add8x8_idct8_s( p, ds, tmp ); break;
+            default: add16x16_idct8_s( p, ds, (dctcoef(*)[64])tmp ); break;
+        }
+    }
+}
+
+/* dequant_4x4 / dequant_8x8 / dequant_4x4_dc, reference common/quant.c:106-162 */
+void FN(dequant_4x4)( dctcoef dct[16], int dequant_mf[6][16], int i_qp )
+{
+    const int i_mf = i_qp % 6, i_qbits = i_qp / 6 - 4;
+    if( i_qbits >= 0 )
+        for( int i = 0; i < 16; i++ )
+            dct[i] = (dct[i] * dequant_mf[i_mf][i]) * (1 << i_qbits);
+    else
+    {
+        const int f = 1 << (-i_qbits - 1);
+        for( int i = 0; i < 16; i++ )
+            dct[i] = (dct[i] * dequant_mf[i_mf][i] + f) >> (-i_qbits);
+    }
+}
+
+void FN(dequant_8x8)( dctcoef dct[64], int dequant_mf[6][64], int i_qp )
+{
+    const int i_mf = i_qp % 6, i_qbits = i_qp / 6 - 6;
+    if( i_qbits >= 0 )
+        for( int i = 0; i < 64; i++ )
+            dct[i] = (dct[i] * dequant_mf[i_mf][i]) * (1 << i_qbits);
+    else
+    {
+        const int f = 1 << (-i_qbits - 1);
+        for( int i = 0; i < 64; i++ )
+            dct[i] = (dct[i] * dequant_mf[i_mf][i] + f) >> (-i_qbits);
+    }
+}
+
+void FN(dequant_4x4_dc)( dctcoef dct[16], int dequant_mf[6][16], int i_qp )
+{
+    const int i_qbits = i_qp / 6 - 6;
+    if( i_qbits >= 0 )
+    {
+        const int i_dmf = dequant_mf[i_qp % 6][0] << i_qbits;
+        for( int i = 0; i < 16; i++ )
+            dct[i] *= i_dmf;
+    }
+    else
+    {
+        const int i_dmf = dequant_mf[i_qp % 6][0], f = 1 << (-i_qbits - 1);
+        for( int i = 0; i < 16; i++ )
+            dct[i] = (dct[i] * i_dmf + f) >> (-i_qbits);
+    }
+}
+
+/* idct_dequant_2x4_dc / _dconly, reference common/quant.c:164-208 */
+#define IDQ_2X4_START \
+    int a0 = dct[0] + dct[1], a1 = dct[2] + dct[3], a2 = dct[4] + dct[5], a3 = dct[6] + dct[7]; \
+    int a4 = dct[0] - dct[1], a5 = dct[2] - dct[3], a6 = dct[4] - dct[5], a7 = dct[6] - dct[7]; \
+    int b0 = a0 + a1, b1 = a2 + a3, b2 = a4 + a5, b3 = a6 + a7; \
+    int b4 = a0 - a1, b5 = a2 - a3, b6 = a4 - a5, b7 = a6 - a7;
+
+void FN(idct_dequant_2x4_dc)( dctcoef dct[8], dctcoef dct4x4[8][16], int dequant_mf[6][16], int i_qp )
+{
+    IDQ_2X4_START
+    int dmf = dequant_mf[i_qp % 6][0] << i_qp / 6;
+    dct4x4[0][0] = ((b0 + b1) * dmf + 32) >> 6;
+    dct4x4[1][0] = ((b2 + b3) * dmf + 32) >> 6;
+    dct4x4[2][0] = ((b0 - b1) * dmf + 32) >> 6;
+    dct4x4[3][0] = ((b2 - b3) * dmf + 32) >> 6;
+    dct4x4[4][0] = ((b4 - b5) * dmf + 32) >> 6;
+    dct4x4[5][0] = ((b6 - b7) * dmf + 32) >> 6;
+    dct4x4[6][0] = ((b4 + b5) * dmf + 32) >> 6;
+    dct4x4[7][0] = ((b6 + b7) * dmf + 32) >> 6;
+}
+
+void FN(idct_dequant_2x4_dconly)( dctcoef dct[8], int dequant_mf[6][16], int i_qp )
+{
+    IDQ_2X4_START
+    int dmf = dequant_mf[i_qp % 6][0] << i_qp / 6;
+    dct[0] = ((b0 + b1) * dmf + 32) >> 6;
+    dct[1] = ((b2 + b3) * dmf + 32) >> 6;
+    dct[2] = ((b0 - b1) * dmf + 32) >> 6;
+    dct[3] = ((b2 - b3) * dmf + 32) >> 6;
+    dct[4] = ((b4 - b5) * dmf + 32) >> 6;
+    dct[5] = ((b6 - b7) * dmf + 32) >> 6;
+    dct[6] = ((b4 + b5) * dmf + 32) >> 6;
+    dct[7] = ((b6 + b7) * dmf + 32) >> 6;
+}
+
+/* optimize_chroma_2x2_dc / 2x4_dc, reference common/quant.c:210-293 */
+static void oc_idq_2x4( dctcoef out[8], const dctcoef dct[8], int dmf )
+{
+    IDQ_2X4_START
+    out[0] = ((b0 + b1) * dmf + 2080) >> 6;
+    out[1] = ((b2 + b3) * dmf + 2080) >> 6;
+    out[2] = ((b0 - b1) * dmf + 2080) >> 6;
+    out[3] = ((b2 - b3) * dmf + 2080) >> 6;
+    out[4] = ((b4 - b5) * dmf + 2080) >> 6;
+    out[5] = ((b6 - b7) * dmf + 2080) >> 6;
+    out[6] = ((b4 + b5) * dmf + 2080) >> 6;
+    out[7] = ((b6 + b7) * dmf + 2080) >> 6;
+}
+#undef IDQ_2X4_START
+
+static void oc_idq_2x2( dctcoef out[4], const dctcoef dct[4], int dmf )
+{
+    int d0 = dct[0] + dct[1], d1 = dct[2] + dct[3], d2 = dct[0] - dct[1], d3 = dct[2] - dct[3];
+    out[0] = ((d0 + d1) * dmf >> 5) + 32;
+    out[1] = ((d0 - d1) * dmf >> 5) + 32;
+    out[2] = ((d2 + d3) * dmf >> 5) + 32;
+    out[3] = ((d2 - d3) * dmf >> 5) + 32;
+}
+
+static int optimize_chroma_dc( dctcoef *dct, int dmf, int c422 )
+{
+    dctcoef orig[8], out[8];
+    int n = c422 ? 8 : 4, nz = 0, sum = 0;
+    if( c422 ) oc_idq_2x4( orig, dct, dmf ); else oc_idq_2x2( orig, dct, dmf );
+    for( int i = 0; i < n; i++ )
+        sum |= orig[i];
+    if( !(sum >> 6) )
+        return 0;
+    for( int coeff = n - 1; coeff >= 0; coeff-- )
+    {
+        int level = dct[coeff];
+        int sign = level >> 31 | 1;
+        while( level )
+        {
+            dct[coeff] = level - sign;
+            if( c422 ) oc_idq_2x4( out, dct, dmf ); else oc_idq_2x2( out, dct, dmf );
+            int diff = 0;
+            for( int i = 0; i < n; i++ )
+                diff |= orig[i] ^ out[i];
+            if( diff >> 6 )
+            {
+                nz = 1;
+                dct[coeff] = level;
+                break;
+            }
+            level -= sign;
+        }
+    }
+    return nz;
+}
+
+int FN(optimize_chroma_2x2_dc)( dctcoef dct[4], int dmf ) { return optimize_chroma_dc( dct, dmf, 0 ); }
+int FN(optimize_chroma_2x4_dc)( dctcoef dct[8], int dmf ) { return optimize_chroma_dc( dct, dmf, 1 ); }
+
+/* denoise_dct, reference common/quant.c:295-306 */
+void FN(denoise_dct)( dctcoef *dct, uint32_t *sum, const udctcoef *offset, int size )
+{
+    for( int i = 0; i < size; i++ )
+    {
+        int level = dct[i];
+        int sign = level >> 31;
+        level = (level + sign) ^ sign;
+        sum[i] += level;
+        level -= offset[i];
+        dct[i] = level < 0 ? 0 : (level ^ sign) - sign;
+    }
+}
+
+/* decimate_score15/16/64, reference common/quant.c:318-363, tables common/tables.c:373-383 */
+static const uint8_t decimate_table4[16] = { 3,2,2,1,1,1,0,0,0,0,0,0,0,0,0,0 };
+static const uint8_t decimate_table8[64] = {
+    3,3,3,3,2,2,2,2,2,2,2,2,1,1,1,1, 1,1,1,1,1,1,1,1,0,0,0,0,0,0,0,0,
+    0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0, 0,0,0,0,0,0,0,0,0,0,0,0,0,0,0,0 };
+
+static int decimate_score( const dctcoef *dct, int i_max )
+{
+    const uint8_t *ds = i_max == 64 ? decimate_table8 : decimate_table4;
+    int score = 0, idx = i_max - 1;
+    while( idx >= 0 && dct[idx] == 0 )
+        idx--;
+    while( idx >= 0 )
+    {
+        if( (unsigned)(dct[idx--] + 1) > 2 )
+            return 9;
+        int run = 0;
+        while( idx >= 0 && dct[idx] == 0 )
+        {
+            idx--;
+            run++;
+        }
+        score += ds[run];
+    }
+    return score;
+}
+
+int FN(decimate_score15)( dctcoef *dct ) { return decimate_score( dct + 1, 15 ); }
+int FN(decimate_score16)( dctcoef *dct ) { return decimate_score( dct, 16 ); }
+int FN(decimate_score64)( dctcoef *dct ) { return decimate_score( dct, 64 ); }
+
+/* coeff_last4/8/15/16/64 (the 15 form is called with dct+1 by its users via
+ * coeff_last[DCT_LUMA_AC]), reference common/quant.c:365-378 */
+int FN(coeff_last)( const dctcoef *l, int num )
+{
+    int i = num - 1;
+    while( i >= 0 && l[i] == 0 )
+        i--;
+    return i;
+}
+
+/* coeff_level_run4/8/15/16, reference common/quant.c:380-398; out = {last, mask,
+ * level[0..total)} as x264_run_level_t (common/bitstream.h:50-55) */
+int FN(coeff_level_run)( const dctcoef *dct, int num, int32_t *last, int32_t *mask, dctcoef *level )
+{
+    int i_last = *last = FN(coeff_last)( dct, num );
+    int total = 0, m = 0;
+    do
+    {
+        level[total++] = dct[i_last];
+        m |= 1 << i_last;
+        while( --i_last >= 0 && dct[i_last] == 0 );
+    } while( i_last >= 0 );
+    *mask = m;
+    return total;
+}
+
+/* zigzag scans and zigzag_sub, reference common/dct.c:768-925 */
+static const uint8_t zz8_frame[64][2] = {   /* (y, x): level[i] = dct[x*8+y] */
+    {0,0},{0,1},{1,0},{2,0},{1,1},{0,2},{0,3},{1,2},{2,1},{3,0},{4,0},{3,1},{2,2},{1,3},{0,4},{0,5},
+    {1,4},{2,3},{3,2},{4,1},{5,0},{6,0},{5,1},{4,2},{3,3},{2,4},{1,5},{0,6},{0,7},{1,6},{2,5},{3,4},
+    {4,3},{5,2},{6,1},{7,0},{7,1},{6,2},{5,3},{4,4},{3,5},{2,6},{1,7},{2,7},{3,6},{4,5},{5,4},{6,3},
+    {7,2},{7,3},{6,4},{5,5},{4,6},{3,7},{4,7},{5,6},{6,5},{7,4},{7,5},{6,6},{5,7},{6,7},{7,6},{7,7} };
+static const uint8_t zz8_field[64][2] = {
+    {0,0},{1,0},{2,0},{0,1},{1,1},{3,0},{4,0},{2,1},{0,2},{3,1},{5,0},{6,0},{7,0},{4,1},{1,2},{0,3},
+    {2,2},{5,1},{6,1},{7,1},{3,2},{1,3},{0,4},{2,3},{4,2},{5,2},{6,2},{7,2},{3,3},{1,4},{0,5},{2,4},
+    {4,3},{5,3},{6,3},{7,3},{3,4},{1,5},{0,6},{2,5},{4,4},{5,4},{6,4},{7,4},{3,5},{1,6},{2,6},{4,5},
+    {5,5},{6,5},{7,5},{3,6},{0,7},{1,7},{4,6},{5,6},{6,6},{7,6},{2,7},{3,7},{4,7},{5,7},{6,7},{7,7} };
+static const uint8_t zz4_frame[16][2] = {
+    {0,0},{0,1},{1,0},{2,0},{1,1},{0,2},{0,3},{1,2},{2,1},{3,0},{3,1},{2,2},{1,3},{2,3},{3,2},{3,3} };
+static const uint8_t zz4_field[16][2] = {
+    {0,0},{1,0},{0,1},{2,0},{3,0},{1,1},{2,1},{3,1},{0,2},{1,2},{2,2},{3,2},{0,3},{1,3},{2,3},{3,3} };
+
+void FN(zigzag_scan_8x8)( int field, dctcoef level[64], const dctcoef dct[64] )
+{
+    const uint8_t (*t)[2] = field ? zz8_field : zz8_frame;
+    for( int i = 0; i < 64; i++ )
+        level[i] = dct[t[i][1]*8 + t[i][0]];
+}
+
+void FN(zigzag_scan_4x4)( int field, dctcoef level[16], const dctcoef dct[16] )
+{
+    const uint8_t (*t)[2] = field ? zz4_field : zz4_frame;
+    for( int i = 0; i < 16; i++ )
+        level[i] = dct[t[i][1]*4 + t[i][0]];
+}
+
+/* zigzag_sub_{4x4,4x4ac,8x8}: level = zigzag(src - dst), then dst = src (the
+ * reference's COPY4x4 / COPY8x8); src stride FENC_STRIDE, dst FDEC_STRIDE.
+ * kind 0 = 4x4, 1 = 4x4ac (dc out, level[0] = 0), 2 = 8x8 */
+int FN(zigzag_sub_s)( int kind, int field, dctcoef *level, const pixel *src, intptr_t ss, pixel *dst, intptr_t ds,
+                      dctcoef *dc )
+{
+    int n = kind == 2 ? 64 : 16, w = kind == 2 ? 8 : 4, nz = 0;
+    const uint8_t (*t)[2] = kind == 2 ? (field ? zz8_field : zz8_frame) : (field ? zz4_field : zz4_frame);
+    for( int i = 0; i < n; i++ )
+    {
+        int y = t[i][0], x = t[i][1];
+        int v = src[x + y*ss] - dst[x + y*ds];
+        if( kind == 1 && i == 0 )
+        {
+            *dc = v;
+            level[0] = 0;
+            continue;
+        }
+        level[i] = v;
+        nz |= level[i];
+    }
+    for( int y = 0; y < w; y++ )
+        for( int x = 0; x < w; x++ )
+            dst[x + y*ds] = src[x + y*ss];
+    return !!nz;
+}
+
+/* zigzag_interleave_8x8_cavlc, reference common/dct.c:927-940 */
+void FN(zigzag_interleave_8x8_cavlc)( dctcoef *dst, const dctcoef *src, uint8_t *nnz )
+{
+    for( int i = 0; i < 4; i++ )
+    {
+        int nz = 0;
+        for( int j = 0; j < 16; j++ )
+        {
+            nz |= src[i + j*4];
+            dst[i*16 + j] = src[i + j*4];
+        }
+        nnz[(i & 1) + (i >> 1)*8] = !!nz;
+    }
+}
+
+/* dequant4_mf / dequant8_mf of x264_cqm_init, reference common/set.c:31-39, 52-61, 124-159 */
+static const uint8_t dequant4_scale[6][3] = {
+    { 10, 13, 16 }, { 11, 14, 18 }, { 13, 16, 20 }, { 14, 18, 23 }, { 16, 20, 25 }, { 18, 23, 29 } };
+static const uint8_t dequant8_scale[6][6] = {
+    { 20, 18, 32, 19, 25, 24 }, { 22, 19, 35, 21, 28, 26 }, { 26, 23, 42, 24, 33, 31 },
+    { 28, 25, 45, 26, 35, 33 }, { 32, 28, 51, 30, 40, 38 }, { 36, 32, 58, 34, 46, 43 } };
+
+void FN(cqm_dequant)( const uint8_t *const scaling_list[8], int b_transform_8x8, int *dq4, int *dq8 )
+{
+    for( int q = 0; q < 6; q++ )
+    {
+        for( int l = 0; l < 4; l++ )
+            for( int i = 0; i < 16; i++ )
+                dq4[(l*6 + q)*16 + i] = dequant4_scale[q][(i&1) + ((i>>2)&1)] * scaling_list[l][i];
+        if( b_transform_8x8 )
+            for( int l = 0; l < 2; l++ )
+                for( int i = 0; i < 64; i++ )
+                    dq8[(l*6 + q)*64 + i] = dequant8_scale[q][quant8_scan[((i>>1)&12) | (i&3)]] * scaling_list[4+l][i];
+    }
+}
+
+/*============================================================================
  * frame-level helpers composed from the entries above (checkers for the
  * batched HIP entries)
  *==========================================================================*/

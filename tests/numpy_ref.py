@@ -277,3 +277,74 @@ def box_sums(plane2d, k):
     """k x k box sums at every top-left position (valid region), int64."""
     c = np.pad(plane2d.astype(np.int64), ((1, 0), (1, 0))).cumsum(0).cumsum(1)
     return c[k:, k:] - c[:-k, k:] - c[k:, :-k] + c[:-k, :-k]
+
+
+# ---------------------------------------------------------------- inverse path
+def _idct4_1d(c0, c1, c2, c3):
+    """H.264 inverse core transform butterfly on arrays (dct.c:272-297 row/column pass)."""
+    s02, d02 = c0 + c2, c0 - c2
+    s13, d13 = c1 + (c3 >> 1), (c1 >> 1) - c3
+    return s02 + s13, d02 + d13, d02 - d13, s02 - s13
+
+
+def add4x4_idct(pred, dct, bd):
+    """pred (4x4 int) + idct of dct[16] (reference transposed layout); int16 temps at 8 bit."""
+    d = np.asarray(dct, np.int64).reshape(4, 4)        # d[r][c] = dct[r*4+c]
+    # first pass over i: uses dct[k*4+i] (column i of d^T ...) -> tmp[i][*]
+    t = np.stack(_idct4_1d(d[0], d[1], d[2], d[3]), axis=1)   # t[i][k]
+    t = wrap(t, bd)
+    o = np.stack(_idct4_1d(t[0], t[1], t[2], t[3]), axis=0)   # o[k][i] = d_out[k*4+i]
+    o = wrap((o + 32) >> 6, bd)
+    return np.clip(pred + o, 0, (1 << bd) - 1)
+
+
+def _idct8_1d(s):
+    a0, a2 = s[0] + s[4], s[0] - s[4]
+    a4, a6 = (s[2] >> 1) - s[6], (s[6] >> 1) + s[2]
+    b0, b2, b4, b6 = a0 + a6, a2 + a4, a2 - a4, a0 - a6
+    a1 = -s[3] + s[5] - s[7] - (s[7] >> 1)
+    a3 = s[1] + s[7] - s[3] - (s[3] >> 1)
+    a5 = -s[1] + s[7] + s[5] + (s[5] >> 1)
+    a7 = s[3] + s[5] + s[1] + (s[1] >> 1)
+    b1, b3, b5, b7 = (a7 >> 2) + a1, a3 + (a5 >> 2), (a3 >> 2) - a5, a7 - (a1 >> 2)
+    return [b0 + b7, b2 + b5, b4 + b3, b6 + b1, b6 - b1, b4 - b3, b2 - b5, b0 - b7]
+
+
+def add8x8_idct8(pred, dct, bd):
+    d = np.asarray(dct, np.int64).reshape(8, 8).copy()     # d[x][i] = dct[x*8+i]
+    d[0, 0] = wrap(d[0, 0] + 32, bd)
+    d = wrap(np.stack(_idct8_1d([d[x] for x in range(8)]), 0), bd)     # column pass, stored
+    o = np.stack(_idct8_1d([d[:, x] for x in range(8)]), 1)             # o[i][x] -> dst[i + x*stride]
+    return np.clip(pred + (o.T >> 6), 0, (1 << bd) - 1)
+
+
+def dequant(dct, dmf6, qp, shift_base):
+    """dequant_4x4 (shift_base 4) / dequant_8x8 (6): dmf6 [6][n]."""
+    c = np.asarray(dct, np.int64)
+    mf = np.asarray(dmf6, np.int64)[qp % 6]
+    q = qp // 6 - shift_base
+    if q >= 0:
+        return c * mf << q
+    return (c * mf + (1 << (-q - 1))) >> (-q)
+
+
+def decimate_score(c):
+    c = list(int(v) for v in c)
+    table = [3, 2, 2, 1, 1, 1] + [0] * 10 if len(c) < 64 else [3] * 4 + [2] * 8 + [1] * 12 + [0] * 40
+    nzi = [i for i, v in enumerate(c) if v]
+    if any(abs(c[i]) > 1 for i in nzi):
+        return 9
+    score = 0
+    for k, i in enumerate(reversed(nzi)):
+        nxt = nzi[len(nzi) - 2 - k] if k + 1 < len(nzi) else -1
+        score += table[i - nxt - 1]
+    return score
+
+
+def zigzag_frame(n):
+    """standard frame zigzag order as (row, col) of an n x n block (dct.c ZIGZAG*_FRAME)."""
+    order = []
+    for s in range(2 * n - 1):
+        cells = [(r, s - r) for r in range(n) if 0 <= s - r < n]
+        order += cells if s % 2 else cells[::-1]
+    return order

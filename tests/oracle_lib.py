@@ -77,6 +77,27 @@ for _bd in (8, 10):
     _f(_bd, "asd8", [_P, _IP, _P, _IP, C.c_int], C.c_int)
     _f(_bd, "ads", [C.c_int, _P, _P, C.c_int, _P, _P, C.c_int, C.c_int], C.c_int)
     _f(_bd, "frame_integral", [_P, _IP, C.c_int, C.c_int, C.c_int, _P])
+    _f(_bd, "idct4x4dc", [_P])
+    for _n in ("add4x4_idct", "add8x8_idct", "add16x16_idct", "add8x8_idct_dc", "add16x16_idct_dc",
+               "add8x8_idct8", "add16x16_idct8"):
+        _f(_bd, _n, [_P, _P])
+    _f(_bd, "add_idct_list", [C.c_int, _P, _IP, _P, _P, C.c_int])
+    for _n in ("dequant_4x4", "dequant_8x8", "dequant_4x4_dc"):
+        _f(_bd, _n, [_P, _P, C.c_int])
+    _f(_bd, "idct_dequant_2x4_dc", [_P, _P, _P, C.c_int])
+    _f(_bd, "idct_dequant_2x4_dconly", [_P, _P, C.c_int])
+    _f(_bd, "optimize_chroma_2x2_dc", [_P, C.c_int], C.c_int)
+    _f(_bd, "optimize_chroma_2x4_dc", [_P, C.c_int], C.c_int)
+    _f(_bd, "denoise_dct", [_P, _P, _P, C.c_int])
+    for _n in ("decimate_score15", "decimate_score16", "decimate_score64"):
+        _f(_bd, _n, [_P], C.c_int)
+    _f(_bd, "coeff_last", [_P, C.c_int], C.c_int)
+    _f(_bd, "coeff_level_run", [_P, C.c_int, _P, _P, _P], C.c_int)
+    _f(_bd, "zigzag_scan_8x8", [C.c_int, _P, _P])
+    _f(_bd, "zigzag_scan_4x4", [C.c_int, _P, _P])
+    _f(_bd, "zigzag_sub_s", [C.c_int, C.c_int, _P, _P, _IP, _P, _IP, _P], C.c_int)
+    _f(_bd, "zigzag_interleave_8x8_cavlc", [_P, _P, _P])
+    _f(_bd, "cqm_dequant", [_P, C.c_int, _P, _P])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
@@ -288,3 +309,70 @@ def frame_integral(bd, plane, origin, stride, lines, padh, sub8x8):
     getattr(_L, f"oracle{bd}_frame_integral")(_addr(plane, origin), stride, lines, padh, sub8x8,
                                              _addr(buf, 32 * stride + padh))
     return buf.reshape(rows, stride)
+
+
+# ---------------------------------------------------------------- inverse path
+IDCT_KINDS = ["add4x4_idct", "add8x8_idct", "add16x16_idct", "add8x8_idct_dc", "add16x16_idct_dc",
+              "add8x8_idct8", "add16x16_idct8"]
+IDCT_IN = [16, 64, 256, 4, 16, 64, 256]
+IDCT_W = [4, 8, 16, 8, 16, 8, 16]
+
+
+def fn(bd, name):
+    return getattr(_L, f"oracle{bd}_{name}")
+
+
+def add_idct(bd, name, dst, d_off, dct):
+    """table form (dst stride 32) on copies; returns (dst', dct') since the C path mutates dct."""
+    dst = dst.copy()
+    d = np.ascontiguousarray(dct, coef_dtype(bd)).copy()
+    fn(bd, name)(_addr(dst, d_off), _addr(d))
+    return dst, d
+
+
+def add_idct_list(bd, kind, dst, ds, dst_off, dct):
+    dst = dst.copy()
+    do = np.ascontiguousarray(dst_off, np.int64)
+    d = np.ascontiguousarray(dct, coef_dtype(bd))
+    fn(bd, "add_idct_list")(kind, _addr(dst), ds, _addr(do), _addr(d), len(do))
+    return dst
+
+
+def cqm_dequant(scaling_lists, transform_8x8=True):
+    lists = [np.ascontiguousarray(np.asarray(x, np.uint8)) for x in scaling_lists]
+    ptrs = (C.c_void_p * 8)(*[x.ctypes.data for x in lists])
+    dq4 = np.zeros((4, 6, 16), np.int32)
+    dq8 = np.zeros((2, 6, 64), np.int32)
+    _L.oracle8_cqm_dequant(ptrs, int(bool(transform_8x8)), _addr(dq4), _addr(dq8))
+    return dq4, dq8
+
+
+def inplace(bd, name, dct, *args):
+    d = np.ascontiguousarray(dct, coef_dtype(bd)).copy()
+    r = fn(bd, name)(_addr(d), *args)
+    return d, r
+
+
+def coeff_level_run(bd, dct, num):
+    d = np.ascontiguousarray(dct, coef_dtype(bd))
+    last, mask = C.c_int32(), C.c_int32()
+    level = np.zeros(18, coef_dtype(bd))
+    n = fn(bd, "coeff_level_run")(_addr(d), num, C.byref(last), C.byref(mask), _addr(level))
+    return n, last.value, mask.value, level[:n].copy()
+
+
+def zigzag_scan(bd, n, field, dct):
+    d = np.ascontiguousarray(dct, coef_dtype(bd))
+    level = np.zeros(n, coef_dtype(bd))
+    fn(bd, f"zigzag_scan_{'8x8' if n == 64 else '4x4'}")(int(field), _addr(level), _addr(d))
+    return level
+
+
+def zigzag_sub(bd, kind, field, src, s_off, ss, dst, d_off, ds):
+    """returns (nz, level, dc, dst')"""
+    dst = dst.copy()
+    level = np.zeros(64 if kind == 2 else 16, coef_dtype(bd))
+    dc = np.zeros(1, coef_dtype(bd))
+    nz = fn(bd, "zigzag_sub_s")(kind, int(field), _addr(level), _addr(src, s_off), ss, _addr(dst, d_off), ds,
+                               _addr(dc))
+    return nz, level, int(dc[0]), dst
