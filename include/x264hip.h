@@ -91,7 +91,37 @@ enum
 };
 
 /* coefficient-domain DC transforms of x264hip_*_dc_batch */
-enum { X264HIP_DC_4x4 = 0 /* dct.c:47-76 */, X264HIP_DC_2x4 = 1 /* dct.c:109-143 */ };
+enum { X264HIP_DC_4x4 = 0 /* dct.c:47-76 */, X264HIP_DC_2x4 = 1 /* dct.c:109-143 */,
+       X264HIP_DC_I4x4 = 2 /* idct4x4dc, dct.c:78-107 */ };
+
+/* inverse transforms + reconstruction of x264hip_*_add_idct_batch: one "call"
+ * = one call of the named reference entry (dct.c:272-476) with an explicit
+ * destination stride; dct block i at dct + i*{16,64,256,4,16,64,256}. */
+enum
+{
+    X264HIP_IDCT_ADD4x4      = 0,
+    X264HIP_IDCT_ADD8x8      = 1,
+    X264HIP_IDCT_ADD16x16    = 2,
+    X264HIP_IDCT_ADD8x8_DC   = 3,
+    X264HIP_IDCT_ADD16x16_DC = 4,
+    X264HIP_IDCT_ADD8x8_8    = 5,
+    X264HIP_IDCT_ADD16x16_8  = 6,
+};
+
+/* dequantisers of x264hip_*_dequant_batch, quant.c:106-162 */
+enum { X264HIP_DEQUANT_4x4 = 0, X264HIP_DEQUANT_8x8 = 1, X264HIP_DEQUANT_4x4_DC = 2 };
+
+/* coefficient statistics of x264hip_*_coef_stat_batch, quant.c:318-378
+ * (DECIMATE15 reads dct+1 like decimate_score15; LASTn read dct[0..n)) */
+enum
+{
+    X264HIP_COEF_DECIMATE15 = 0, X264HIP_COEF_DECIMATE16 = 1, X264HIP_COEF_DECIMATE64 = 2,
+    X264HIP_COEF_LAST4 = 3, X264HIP_COEF_LAST8 = 4, X264HIP_COEF_LAST15 = 5,
+    X264HIP_COEF_LAST16 = 6, X264HIP_COEF_LAST64 = 7,
+};
+
+/* zigzag_sub kinds of x264hip_*_zigzag_sub_batch, dct.c:856-925 */
+enum { X264HIP_ZIGZAG_SUB_4x4 = 0, X264HIP_ZIGZAG_SUB_4x4AC = 1, X264HIP_ZIGZAG_SUB_8x8 = 2 };
 
 /* quantiser selector of x264hip_*_quant_batch, quant.c:59-104 */
 enum
@@ -239,7 +269,26 @@ typedef struct                                                                  
                               int last_nnz, dctcoef *coefs, dctcoef *quant_coefs, dctcoef *dct, \
                               uint8_t *cabac_state_sig, uint8_t *cabac_state_last,              \
                               uint64_t level_state0, uint16_t level_state1 );                   \
-} x264hip_##BD##_quant_function_t;
+} x264hip_##BD##_quant_function_t;                                                             \
+                                                                                                \
+/* x264_zigzag_function_t, reference common/dct.h:61-70 */                                      \
+typedef struct                                                                                  \
+{                                                                                               \
+    void (*scan_8x8)( dctcoef level[64], dctcoef dct[64] );                                     \
+    void (*scan_4x4)( dctcoef level[16], dctcoef dct[16] );                                     \
+    int  (*sub_8x8)  ( dctcoef level[64], const pixel *p_src, pixel *p_dst );                   \
+    int  (*sub_4x4)  ( dctcoef level[16], const pixel *p_src, pixel *p_dst );                   \
+    int  (*sub_4x4ac)( dctcoef level[16], const pixel *p_src, pixel *p_dst, dctcoef *dc );      \
+    void (*interleave_8x8_cavlc)( dctcoef *dst, dctcoef *src, uint8_t *nnz );                   \
+} x264hip_##BD##_zigzag_function_t;                                                             \
+                                                                                                \
+/* x264_run_level_t, reference common/bitstream.h:50-55 (level 16-byte aligned) */             \
+typedef struct                                                                                  \
+{                                                                                               \
+    int32_t last;                                                                               \
+    int32_t mask;                                                                               \
+    dctcoef level[18] __attribute__((aligned(16)));                                             \
+} x264hip_##BD##_run_level_t;
 
 X264HIP_DECLARE_TABLES( 8,  uint8_t,  int16_t, uint16_t )
 X264HIP_DECLARE_TABLES( 10, uint16_t, int32_t, uint32_t )
@@ -267,6 +316,10 @@ void x264hip_##BD##_dct_init( uint32_t cpu, x264hip_##BD##_dct_function_t *dctf 
 void x264hip_##BD##_dct_init_hip( x264hip_##BD##_dct_function_t *dctf );                        \
 void x264hip_##BD##_quant_init( void *h, uint32_t cpu, x264hip_##BD##_quant_function_t *pf );   \
 void x264hip_##BD##_quant_init_hip( x264hip_##BD##_quant_function_t *pf );                      \
+void x264hip_##BD##_zigzag_init( uint32_t cpu, x264hip_##BD##_zigzag_function_t *pf_progressive, \
+                                 x264hip_##BD##_zigzag_function_t *pf_interlaced );             \
+void x264hip_##BD##_zigzag_init_hip( x264hip_##BD##_zigzag_function_t *pf_progressive,          \
+                                     x264hip_##BD##_zigzag_function_t *pf_interlaced );                      \
                                                                                                 \
 /* quant tables: restates x264_cqm_init (reference common/set.c:73-206) for the                 \
  * mf / bias arrays the quant entries consume.  scaling_list[8] as sps->scaling_list            \
@@ -413,7 +466,65 @@ int x264hip_##BD##_mb_dct_quant( int transform, const pixel *fenc, intptr_t fenc
                                  intptr_t pred_frame_stride,                                    \
                                  int mb_width, int mb_height, int n_frames,                     \
                                  const udctcoef *mf, const udctcoef *bias,                      \
-                                 dctcoef *dct, int32_t *nz, void *stream );
+                                 dctcoef *dct, int32_t *nz, void *stream );                     \
+                                                                                                \
+/* ---- inverse path (reference common/dct.c, common/quant.c), device arrays ---- */            \
+/* n calls of the add*_idct* entry `kind` (X264HIP_IDCT_*) on dst + dst_off[i]                  \
+ * (stride dst_stride); call i's coefficients at dct + i*size; dct is not modified. */          \
+int x264hip_##BD##_add_idct_batch( int kind, pixel *dst, intptr_t dst_stride,                   \
+                                   const int64_t *dst_off, const dctcoef *dct, int n,           \
+                                   void *stream );                                              \
+/* in-place dequant_4x4 / 8x8 / 4x4_dc (X264HIP_DEQUANT_*) of n blocks; dequant_mf is           \
+ * one list's int [6][16] or [6][64] (x264hip_cqm_dequant), qp[i] per block. */                 \
+int x264hip_##BD##_dequant_batch( int kind, dctcoef *dct, const int32_t *dequant_mf,            \
+                                  const int32_t *qp, int n, void *stream );                     \
+/* idct_dequant_2x4_dc (dconly = 0: writes dct4x4[8][16] per call, 128 coefs apart)             \
+ * or _dconly (dconly = 1: in place on dct[8]) for n calls, qp[i] per call. */                   \
+int x264hip_##BD##_idct_dequant_2x4_batch( int dconly, dctcoef *dct, dctcoef *dct4x4,           \
+                                           const int32_t *dequant_mf, const int32_t *qp,        \
+                                           int n, void *stream );                               \
+/* optimize_chroma_2x2_dc (c422 = 0, 4 coefs per call) / 2x4_dc (c422 = 1, 8 coefs):            \
+ * in place, dequant_mf[i] per call, nz[i] = return value. */                                   \
+int x264hip_##BD##_optimize_chroma_dc_batch( int c422, dctcoef *dct, const int32_t *dequant_mf, \
+                                             int n, int32_t *nz, void *stream );                \
+/* denoise_dct over n consecutive blocks of `size` coefficients sharing sum[size]               \
+ * (accumulated) and offset[size]. */                                                           \
+int x264hip_##BD##_denoise_dct_batch( dctcoef *dct, int size, int n, uint32_t *sum,             \
+                                      const udctcoef *offset, void *stream );                   \
+/* decimate_score / coeff_last (X264HIP_COEF_*) of n blocks `pitch` coefs apart. */             \
+int x264hip_##BD##_coef_stat_batch( int kind, const dctcoef *dct, int64_t pitch, int n,         \
+                                    int32_t *out, void *stream );                               \
+/* coeff_level_run4/8/15/16 (num) of n blocks `pitch` coefs apart: last[i], mask[i],             \
+ * count[i] (the return value) and level[18*i ..]. */                                           \
+int x264hip_##BD##_coeff_level_run_batch( int num, const dctcoef *dct, int64_t pitch, int n,    \
+                                          int32_t *last, int32_t *mask, int32_t *count,         \
+                                          dctcoef *level, void *stream );                       \
+/* zigzag_scan_4x4 (size 4) / 8x8 (size 8), frame or field order, n blocks. */                  \
+int x264hip_##BD##_zigzag_scan_batch( int size, int field, dctcoef *level, const dctcoef *dct,  \
+                                      int n, void *stream );                                    \
+/* zigzag_sub_4x4 / 4x4ac / 8x8 (X264HIP_ZIGZAG_SUB_*): level (16 or 64 per call),              \
+ * dc[i] (4x4ac only), nz[i]; dst block is overwritten with the src block. */                   \
+int x264hip_##BD##_zigzag_sub_batch( int kind, int field, dctcoef *level, dctcoef *dc,          \
+                                     const pixel *src, intptr_t src_stride, pixel *dst,         \
+                                     intptr_t dst_stride, const int64_t *src_off,               \
+                                     const int64_t *dst_off, int n, int32_t *nz, void *stream );\
+/* zigzag_interleave_8x8_cavlc of n blocks (64 coefs in/out, 16 nnz bytes per call). */         \
+int x264hip_##BD##_zigzag_interleave_batch( dctcoef *dst, const dctcoef *src, uint8_t *nnz,     \
+                                            int n, void *stream );                              \
+/* fused reconstruction of the inter luma residual (macroblock.c dequant + add16x16_idct /     \
+ * add16x16_idct8): recon = clip( pred + idct( dequant( dct ) ) ) per MB, dct[mb][256] as      \
+ * written by mb_dct_quant (unchanged), qp[mb] per MB, dequant_mf the list's [6][16|64]. */     \
+int x264hip_##BD##_mb_dequant_idct_add( int transform, const dctcoef *dct, int mb_width,        \
+                                        int mb_height, int n_frames, const int32_t *dequant_mf, \
+                                        const int32_t *qp, const pixel *pred,                   \
+                                        intptr_t pred_stride, intptr_t pred_frame_stride,       \
+                                        pixel *recon, intptr_t recon_stride,                    \
+                                        intptr_t recon_frame_stride, void *stream );
+
+/* dequant4_mf [4][6][16] and dequant8_mf [2][6][64] of x264_cqm_init (reference
+ * common/set.c:124-159) for the 8 scaling lists; bit-depth independent. */
+void x264hip_cqm_dequant( const uint8_t *const scaling_list[8], int b_transform_8x8,
+                          int32_t *dequant4_mf, int32_t *dequant8_mf );
 
 X264HIP_DECLARE_ENTRIES( 8,  uint8_t,  int16_t, uint16_t, uint16_t )
 X264HIP_DECLARE_ENTRIES( 10, uint16_t, int32_t, uint32_t, uint32_t )

@@ -1324,6 +1324,37 @@ void FN(mb_dct_quant)( int transform, const pixel *fenc, intptr_t fs, const pixe
         }
 }
 
+/* frame-level reconstruction, semantics of x264hip_*_mb_dequant_idct_add:
+ * per MB dequant_4x4 x16 + add16x16_idct, or dequant_8x8 x4 + add16x16_idct8,
+ * of a copy of dct[mb][256] onto recon = pred (one frame) */
+void FN(mb_dequant_idct_add)( int transform, const dctcoef *dct, int mb_width, int mb_height, const int *dmf,
+                              const int32_t *qp, const pixel *pred, intptr_t ps, pixel *recon, intptr_t rs )
+{
+    dctcoef tmp[256];
+    for( int mby = 0; mby < mb_height; mby++ )
+        for( int mbx = 0; mbx < mb_width; mbx++ )
+        {
+            size_t mb = (size_t)mby*mb_width + mbx;
+            memcpy( tmp, dct + mb*256, sizeof(tmp) );
+            pixel *r = recon + 16*(mby*rs + mbx);
+            const pixel *p = pred + 16*(mby*ps + mbx);
+            for( int y = 0; y < 16; y++ )
+                memcpy( r + y*rs, p + y*ps, 16 * sizeof(pixel) );
+            if( transform == 8 )
+            {
+                for( int i = 0; i < 4; i++ )
+                    FN(dequant_8x8)( tmp + 64*i, (int(*)[64])dmf, qp[mb] );
+                add16x16_idct8_s( r, rs, (dctcoef(*)[64])tmp );
+            }
+            else
+            {
+                for( int i = 0; i < 16; i++ )
+                    FN(dequant_4x4)( tmp + 16*i, (int(*)[16])dmf, qp[mb] );
+                add16x16_idct_s( r, rs, (dctcoef(*)[16])tmp );
+            }
+        }
+}
+
 /*============================================================================
  * motion compensation inputs — reference common/mc.c
  *==========================================================================*/

@@ -98,6 +98,7 @@ for _bd in (8, 10):
     _f(_bd, "zigzag_sub_s", [C.c_int, C.c_int, _P, _P, _IP, _P, _IP, _P], C.c_int)
     _f(_bd, "zigzag_interleave_8x8_cavlc", [_P, _P, _P])
     _f(_bd, "cqm_dequant", [_P, C.c_int, _P, _P])
+    _f(_bd, "mb_dequant_idct_add", [C.c_int, _P, C.c_int, C.c_int, _P, _P, _P, _IP, _P, _IP])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
@@ -376,3 +377,13 @@ def zigzag_sub(bd, kind, field, src, s_off, ss, dst, d_off, ds):
     nz = fn(bd, "zigzag_sub_s")(kind, int(field), _addr(level), _addr(src, s_off), ss, _addr(dst, d_off), ds,
                                _addr(dc))
     return nz, level, int(dc[0]), dst
+
+
+def mb_dequant_idct_add(bd, transform, dct, mbw, mbh, dmf, qp, pred, p_origin, ps, recon, r_origin, rs):
+    """one frame; recon is modified in place and returned."""
+    d = np.ascontiguousarray(dct, coef_dtype(bd))
+    m = np.ascontiguousarray(dmf, np.int32)
+    q = np.ascontiguousarray(qp, np.int32)
+    fn(bd, "mb_dequant_idct_add")(transform, _addr(d), mbw, mbh, _addr(m), _addr(q), _addr(pred, p_origin), ps,
+                                  _addr(recon, r_origin), rs)
+    return recon

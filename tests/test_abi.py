@@ -76,6 +76,10 @@ int main(void) {
     P(x264hip_8_dct_function_t, sub16x16_dct8) P(x264hip_8_dct_function_t, dct2x4dc)
     P(x264hip_8_quant_function_t, quant_2x2_dc) P(x264hip_8_quant_function_t, coeff_level_run)
     P(x264hip_8_quant_function_t, trellis_cabac_chroma_422_dc)
+    printf("zigzag8 %zu\nzigzag10 %zu\nrunlevel8 %zu\nrunlevel10 %zu\n",
+           sizeof(x264hip_8_zigzag_function_t), sizeof(x264hip_10_zigzag_function_t),
+           sizeof(x264hip_8_run_level_t), sizeof(x264hip_10_run_level_t));
+    P(x264hip_8_zigzag_function_t, sub_4x4ac) P(x264hip_8_run_level_t, level) P(x264hip_10_run_level_t, level)
     return 0;
 }
 """
@@ -104,6 +108,11 @@ def test_table_layout_matches_ctypes(tmp_path):
     assert vals["x264hip_8_dct_function_t dct2x4dc"] == x.DctFunctions.dct2x4dc.offset
     assert vals["x264hip_8_quant_function_t quant_2x2_dc"] == x.QuantFunctions.quant_2x2_dc.offset
     assert vals["x264hip_8_quant_function_t coeff_level_run"] == x.QuantFunctions.coeff_level_run.offset
+    assert vals["zigzag8"] == vals["zigzag10"] == ctypes.sizeof(x.ZigzagFunctions) == 6 * 8
+    assert vals["x264hip_8_zigzag_function_t sub_4x4ac"] == x.ZigzagFunctions.sub_4x4ac.offset
+    # x264_run_level_t (bitstream.h:50-55): level 16-byte aligned after last / mask
+    assert vals["x264hip_8_run_level_t level"] == vals["x264hip_10_run_level_t level"] == 16
+    assert vals["runlevel8"] == 64 and vals["runlevel10"] == 96
     # reference field counts: pixel.h:78-144 has 8*8+7+4+2*7+... pointers
     n_ptr = vals["pixel8"] // 8
     assert n_ptr == 8 * 7 + 7 + 4 + 7 * 2 + 1 + 1 + 1 + 4 + 4 + 4 + 3 + 7 * 4 + 7 + 15 + 3 + 6

@@ -36,6 +36,12 @@ PIXEL_16x16, PIXEL_16x8, PIXEL_8x16, PIXEL_8x8, PIXEL_8x4, PIXEL_4x8, PIXEL_4x4,
 PIXEL_SIZES = [(16, 16), (16, 8), (8, 16), (8, 8), (8, 4), (4, 8), (4, 4), (4, 16)]
 CMP_SAD, CMP_SSD, CMP_SATD, CMP_SA8D = 0, 1, 2, 3
 STAT_VAR, STAT_HADAMARD_AC, STAT_SA8D_SATD, STAT_VSAD, STAT_ASD8 = 0, 1, 2, 3, 4
+IDCT_ADD4x4, IDCT_ADD8x8, IDCT_ADD16x16, IDCT_ADD8x8_DC, IDCT_ADD16x16_DC, IDCT_ADD8x8_8, IDCT_ADD16x16_8 = range(7)
+IDCT_IN_SIZE = [16, 64, 256, 4, 16, 64, 256]
+DEQUANT_4x4, DEQUANT_8x8, DEQUANT_4x4_DC = 0, 1, 2
+COEF_DECIMATE15, COEF_DECIMATE16, COEF_DECIMATE64, COEF_LAST4, COEF_LAST8, COEF_LAST15, COEF_LAST16, COEF_LAST64 = range(8)
+ZIGZAG_SUB_4x4, ZIGZAG_SUB_4x4AC, ZIGZAG_SUB_8x8 = 0, 1, 2
+DC_I4x4 = 2
 DCT_SUB4x4, DCT_SUB8x8, DCT_SUB16x16, DCT_SUB8x8_DC, DCT_SUB8x16_DC, DCT_SUB8x8_8, DCT_SUB16x16_8 = range(7)
 DCT_OUT_SIZE = [16, 64, 256, 4, 8, 64, 256]
 DC_4x4, DC_2x4 = 0, 1
@@ -95,6 +101,18 @@ CMP64_T = _c.CFUNCTYPE(_c.c_uint64, _P, _IP, _P, _IP)              # sa8d_satd
 VAR_T = _c.CFUNCTYPE(_c.c_uint64, _P, _IP)                         # var / hadamard_ac
 VAR2_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P)                        # var2(fenc, fdec, ssd[2])
 ADS_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _c.c_int, _P, _P, _c.c_int, _c.c_int)
+IDCT_T = _c.CFUNCTYPE(None, _P, _P)                                # add*_idct*(p_dst, dct)
+DEQ_T = _c.CFUNCTYPE(None, _P, _P, _c.c_int)                       # dequant_*(dct, dmf, qp)
+IDQ24_T = _c.CFUNCTYPE(None, _P, _P, _P, _c.c_int)                 # idct_dequant_2x4_dc
+IDQ24O_T = _c.CFUNCTYPE(None, _P, _P, _c.c_int)                    # idct_dequant_2x4_dconly
+OPTC_T = _c.CFUNCTYPE(_c.c_int, _P, _c.c_int)                      # optimize_chroma_*_dc
+DENOISE_T = _c.CFUNCTYPE(None, _P, _P, _P, _c.c_int)
+COEF_T = _c.CFUNCTYPE(_c.c_int, _P)                                # decimate / coeff_last
+RUNLEVEL_T = _c.CFUNCTYPE(_c.c_int, _P, _P)
+ZSCAN_T = _c.CFUNCTYPE(None, _P, _P)
+ZSUB_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P)
+ZSUBAC_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P, _P)
+ZINTER_T = _c.CFUNCTYPE(None, _P, _P, _P)
 
 
 class PixelFunctions(_c.Structure):
@@ -122,10 +140,10 @@ class PixelFunctions(_c.Structure):
 class DctFunctions(_c.Structure):
     """Layout of x264_dct_function_t, reference common/dct.h:29-59."""
     _fields_ = [
-        ("sub4x4_dct", DCT_T), ("add4x4_idct", _P), ("sub8x8_dct", DCT_T), ("sub8x8_dct_dc", DCT_T),
-        ("add8x8_idct", _P), ("add8x8_idct_dc", _P), ("sub8x16_dct_dc", DCT_T), ("sub16x16_dct", DCT_T),
-        ("add16x16_idct", _P), ("add16x16_idct_dc", _P), ("sub8x8_dct8", DCT_T), ("add8x8_idct8", _P),
-        ("sub16x16_dct8", DCT_T), ("add16x16_idct8", _P), ("dct4x4dc", DC_T), ("idct4x4dc", _P),
+        ("sub4x4_dct", DCT_T), ("add4x4_idct", IDCT_T), ("sub8x8_dct", DCT_T), ("sub8x8_dct_dc", DCT_T),
+        ("add8x8_idct", IDCT_T), ("add8x8_idct_dc", IDCT_T), ("sub8x16_dct_dc", DCT_T), ("sub16x16_dct", DCT_T),
+        ("add16x16_idct", IDCT_T), ("add16x16_idct_dc", IDCT_T), ("sub8x8_dct8", DCT_T), ("add8x8_idct8", IDCT_T),
+        ("sub16x16_dct8", DCT_T), ("add16x16_idct8", IDCT_T), ("dct4x4dc", DC_T), ("idct4x4dc", DC_T),
         ("dct2x4dc", DC2_T),
     ]
 
@@ -135,15 +153,21 @@ class QuantFunctions(_c.Structure):
     _fields_ = [
         ("quant_8x8", QUANT_T), ("quant_4x4", QUANT_T), ("quant_4x4x4", QUANT_T),
         ("quant_4x4_dc", QUANT_DC_T), ("quant_2x2_dc", QUANT_DC_T),
-        ("dequant_8x8", _P), ("dequant_4x4", _P), ("dequant_4x4_dc", _P),
-        ("idct_dequant_2x4_dc", _P), ("idct_dequant_2x4_dconly", _P),
-        ("optimize_chroma_2x2_dc", _P), ("optimize_chroma_2x4_dc", _P), ("denoise_dct", _P),
-        ("decimate_score15", _P), ("decimate_score16", _P), ("decimate_score64", _P),
-        ("coeff_last", _P * 14), ("coeff_last4", _P), ("coeff_last8", _P),
-        ("coeff_level_run", _P * 13), ("coeff_level_run4", _P), ("coeff_level_run8", _P),
+        ("dequant_8x8", DEQ_T), ("dequant_4x4", DEQ_T), ("dequant_4x4_dc", DEQ_T),
+        ("idct_dequant_2x4_dc", IDQ24_T), ("idct_dequant_2x4_dconly", IDQ24O_T),
+        ("optimize_chroma_2x2_dc", OPTC_T), ("optimize_chroma_2x4_dc", OPTC_T), ("denoise_dct", DENOISE_T),
+        ("decimate_score15", COEF_T), ("decimate_score16", COEF_T), ("decimate_score64", COEF_T),
+        ("coeff_last", COEF_T * 14), ("coeff_last4", COEF_T), ("coeff_last8", COEF_T),
+        ("coeff_level_run", RUNLEVEL_T * 13), ("coeff_level_run4", RUNLEVEL_T), ("coeff_level_run8", RUNLEVEL_T),
         ("trellis_cabac_4x4", _P), ("trellis_cabac_8x8", _P), ("trellis_cabac_4x4_psy", _P),
         ("trellis_cabac_8x8_psy", _P), ("trellis_cabac_dc", _P), ("trellis_cabac_chroma_422_dc", _P),
     ]
+
+
+class ZigzagFunctions(_c.Structure):
+    """Layout of x264_zigzag_function_t, reference common/dct.h:61-70."""
+    _fields_ = [("scan_8x8", ZSCAN_T), ("scan_4x4", ZSCAN_T), ("sub_8x8", ZSUB_T), ("sub_4x4", ZSUB_T),
+                ("sub_4x4ac", ZSUBAC_T), ("interleave_8x8_cavlc", ZINTER_T)]
 
 
 def _check_bd(bitdepth):
@@ -178,12 +202,33 @@ def quant_init(bitdepth=8, cpu=CPU_HIP):
     return _table("quant", QuantFunctions, bitdepth, cpu)
 
 
+def zigzag_init(bitdepth=8, cpu=CPU_HIP):
+    """x264_zigzag_init equivalent (reference common/dct.c:938): (progressive, interlaced)."""
+    _check_bd(bitdepth)
+    init()
+    p, i = ZigzagFunctions(), ZigzagFunctions()
+    getattr(lib(), f"x264hip_{bitdepth}_zigzag_init")(cpu, _c.byref(p), _c.byref(i))
+    return p, i
+
+
+def cqm_dequant(scaling_lists, transform_8x8=True):
+    """dequant4_mf [4][6][16], dequant8_mf [2][6][64] (int32) of x264_cqm_init (reference common/set.c:124-159)."""
+    import numpy as np
+    lists = [np.ascontiguousarray(np.asarray(x, np.uint8)) for x in scaling_lists]
+    ptrs = (_P * 8)(*[x.ctypes.data for x in lists])
+    dq4 = np.zeros((4, 6, 16), np.int32)
+    dq8 = np.zeros((2, 6, 64), np.int32)
+    lib().x264hip_cqm_dequant(ptrs, int(bool(transform_8x8)), dq4.ctypes.data, dq8.ctypes.data)
+    return dq4, dq8
+
+
 # ----------------------------------------------------------------- declarations
 def _declare(L):
     L.x264hip_init.argtypes = [_c.c_int]
     L.x264hip_init.restype = _c.c_int
     L.x264hip_last_error.restype = _c.c_char_p
     L.x264hip_available.restype = _c.c_int
+    L.x264hip_cqm_dequant.argtypes = [_P, _c.c_int, _P, _P]
     for bd in (8, 10):
         f = lambda n: getattr(L, f"x264hip_{bd}_{n}")  # noqa: E731
         f("pixel_init").argtypes = [_c.c_uint32, _P]
@@ -209,6 +254,24 @@ def _declare(L):
         f("var2_batch").argtypes = [_c.c_int, _P, _IP, _IP, _P, _IP, _IP, _P, _P, _c.c_int, _P, _P]
         f("ads_batch").argtypes = [_c.c_int, _P, _P, _c.c_int, _P, _P, _P, _P, _P, _c.c_int, _P, _c.c_int, _P, _P]
         f("frame_integral").argtypes = [_P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _IP, _P]
+        f("zigzag_init").argtypes = [_c.c_uint32, _P, _P]
+        f("zigzag_init_hip").argtypes = [_P, _P]
+        f("add_idct_batch").argtypes = [_c.c_int, _P, _IP, _P, _P, _c.c_int, _P]
+        f("dequant_batch").argtypes = [_c.c_int, _P, _P, _P, _c.c_int, _P]
+        f("idct_dequant_2x4_batch").argtypes = [_c.c_int, _P, _P, _P, _P, _c.c_int, _P]
+        f("optimize_chroma_dc_batch").argtypes = [_c.c_int, _P, _P, _c.c_int, _P, _P]
+        f("denoise_dct_batch").argtypes = [_P, _c.c_int, _c.c_int, _P, _P, _P]
+        f("coef_stat_batch").argtypes = [_c.c_int, _P, _c.c_int64, _c.c_int, _P, _P]
+        f("coeff_level_run_batch").argtypes = [_c.c_int, _P, _c.c_int64, _c.c_int, _P, _P, _P, _P, _P]
+        f("zigzag_scan_batch").argtypes = [_c.c_int, _c.c_int, _P, _P, _c.c_int, _P]
+        f("zigzag_sub_batch").argtypes = [_c.c_int, _c.c_int, _P, _P, _P, _IP, _P, _IP, _P, _P, _c.c_int, _P, _P]
+        f("zigzag_interleave_batch").argtypes = [_P, _P, _P, _c.c_int, _P]
+        f("mb_dequant_idct_add").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _IP, _IP,
+                                             _P, _IP, _IP, _P]
+        for n in ("add_idct_batch", "dequant_batch", "idct_dequant_2x4_batch", "optimize_chroma_dc_batch",
+                  "denoise_dct_batch", "coef_stat_batch", "coeff_level_run_batch", "zigzag_scan_batch",
+                  "zigzag_sub_batch", "zigzag_interleave_batch", "mb_dequant_idct_add"):
+            f(n).restype = _c.c_int
         for n in ("pixel_stat_batch", "var2_batch", "ads_batch", "frame_integral", "pixel_cmp_batch", "me_search_full", "me_esa_argmin", "hpel_filter", "subpel_cmp_batch", "sub_dct_batch", "dc_batch", "quant_batch",
                   "quant_dc_batch", "mb_dct_quant"):
             f(n).restype = _c.c_int
@@ -345,6 +408,118 @@ def frame_integral(planes, origin, stride, lines, padh=PAD, sub8x8=False, out=No
     return out
 
 
+def add_idct_batch(kind, dst, dst_stride, dst_off, dct):
+    """in-place add*_idct* (IDCT_*) on dst + dst_off[i]; dct [n, size] (not modified)."""
+    bd = _pix_bd(dst)
+    _rc(getattr(lib(), f"x264hip_{bd}_add_idct_batch")(kind, _ptr(dst), dst_stride, _ptr(dst_off), _ptr(dct),
+                                                        dst_off.numel(), _stream()), "add_idct_batch")
+    return dst
+
+
+def dequant_batch(kind, dct, dequant_mf, qp):
+    """in-place dequant (DEQUANT_*) of dct [n, 16|64] with one list's int32 [6][16|64] and qp[n]."""
+    bd = _coef_bd(dct)
+    _rc(getattr(lib(), f"x264hip_{bd}_dequant_batch")(kind, _ptr(dct), _ptr(dequant_mf), _ptr(qp), qp.numel(),
+                                                       _stream()), "dequant_batch")
+    return dct
+
+
+def idct_dequant_2x4_batch(dconly, dct, dequant_mf, qp, dct4x4=None):
+    bd = _coef_bd(dct)
+    _rc(getattr(lib(), f"x264hip_{bd}_idct_dequant_2x4_batch")(
+        int(dconly), _ptr(dct), _ptr(dct4x4) if dct4x4 is not None else None, _ptr(dequant_mf), _ptr(qp),
+        qp.numel(), _stream()), "idct_dequant_2x4_batch")
+    return dct4x4 if dct4x4 is not None else dct
+
+
+def optimize_chroma_dc_batch(c422, dct, dequant_mf):
+    import torch
+    bd = _coef_bd(dct)
+    n = dequant_mf.numel()
+    nz = torch.empty(n, dtype=torch.int32, device=dct.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_optimize_chroma_dc_batch")(int(c422), _ptr(dct), _ptr(dequant_mf), n,
+                                                                  _ptr(nz), _stream()), "optimize_chroma_dc_batch")
+    return nz
+
+
+def denoise_dct_batch(dct, size, sums, offset):
+    bd = _coef_bd(dct)
+    _rc(getattr(lib(), f"x264hip_{bd}_denoise_dct_batch")(_ptr(dct), size, dct.numel() // size, _ptr(sums),
+                                                           _ptr(offset), _stream()), "denoise_dct_batch")
+    return dct
+
+
+def coef_stat_batch(kind, dct, pitch, n):
+    import torch
+    bd = _coef_bd(dct)
+    out = torch.empty(n, dtype=torch.int32, device=dct.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_coef_stat_batch")(kind, _ptr(dct), pitch, n, _ptr(out), _stream()),
+        "coef_stat_batch")
+    return out
+
+
+def coeff_level_run_batch(num, dct, pitch, n):
+    """returns (last, mask, count, level [n, 18])"""
+    import torch
+    bd = _coef_bd(dct)
+    last, mask, count = (torch.empty(n, dtype=torch.int32, device=dct.device) for _ in range(3))
+    level = torch.zeros((n, 18), dtype=dct.dtype, device=dct.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_coeff_level_run_batch")(num, _ptr(dct), pitch, n, _ptr(last), _ptr(mask),
+                                                               _ptr(count), _ptr(level), _stream()),
+        "coeff_level_run_batch")
+    return last, mask, count, level
+
+
+def zigzag_scan_batch(size, field, dct):
+    import torch
+    bd = _coef_bd(dct)
+    n = dct.numel() // (size * size)
+    level = torch.empty_like(dct)
+    _rc(getattr(lib(), f"x264hip_{bd}_zigzag_scan_batch")(size, int(field), _ptr(level), _ptr(dct), n, _stream()),
+        "zigzag_scan_batch")
+    return level
+
+
+def zigzag_sub_batch(kind, field, src, src_stride, dst, dst_stride, src_off, dst_off):
+    """returns (level [n, 16|64], dc [n], nz [n]); dst blocks become the src blocks."""
+    import torch
+    bd = _pix_bd(src)
+    n = src_off.numel()
+    w = 8 if kind == 2 else 4
+    ct = torch.int16 if bd == 8 else torch.int32
+    level = torch.empty((n, w * w), dtype=ct, device=src.device)
+    dc = torch.zeros(n, dtype=ct, device=src.device)
+    nz = torch.empty(n, dtype=torch.int32, device=src.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_zigzag_sub_batch")(kind, int(field), _ptr(level), _ptr(dc), _ptr(src),
+                                                          src_stride, _ptr(dst), dst_stride, _ptr(src_off),
+                                                          _ptr(dst_off), n, _ptr(nz), _stream()), "zigzag_sub_batch")
+    return level, dc, nz
+
+
+def zigzag_interleave_batch(src):
+    import torch
+    bd = _coef_bd(src)
+    n = src.numel() // 64
+    dst = torch.empty_like(src)
+    nnz = torch.zeros((n, 16), dtype=torch.uint8, device=src.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_zigzag_interleave_batch")(_ptr(dst), _ptr(src), _ptr(nnz), n, _stream()),
+        "zigzag_interleave_batch")
+    return dst, nnz
+
+
+def mb_dequant_idct_add(transform, dct, mb_width, mb_height, nframes, dequant_mf, qp, pred, pred_origin,
+                        pred_stride, recon, recon_origin, recon_stride, pred_frame_stride=None,
+                        recon_frame_stride=None):
+    """recon = clip(pred + idct(dequant(dct))) per MB (x264hip_*_mb_dequant_idct_add)."""
+    bd = _pix_bd(pred)
+    pfs = pred_frame_stride if pred_frame_stride is not None else (pred[0].numel() if pred.dim() == 3 else 0)
+    rfs = recon_frame_stride if recon_frame_stride is not None else (recon[0].numel() if recon.dim() == 3 else 0)
+    _rc(getattr(lib(), f"x264hip_{bd}_mb_dequant_idct_add")(
+        transform, _ptr(dct), mb_width, mb_height, nframes, _ptr(dequant_mf), _ptr(qp), _ptr(pred, pred_origin),
+        pred_stride, pfs, _ptr(recon, recon_origin), recon_stride, rfs, _stream()), "mb_dequant_idct_add")
+    return recon
+
+
 def me_table_pitch(rng):
     """row pitch of a full-search table: 2*range+1 rounded up to a multiple of 4"""
     return (2 * rng + 1 + 3) // 4 * 4
@@ -393,7 +568,7 @@ def _coef_bd(t):
 def dc_batch(kind, dct, dct4x4=None, n=None):
     bd = _coef_bd(dct)
     if n is None:
-        n = dct.numel() // (16 if kind == DC_4x4 else 8)
+        n = dct.numel() // (16 if kind in (DC_4x4, DC_I4x4) else 8)
     _rc(getattr(lib(), f"x264hip_{bd}_dc_batch")(
         kind, _ptr(dct), _ptr(dct4x4) if dct4x4 is not None else None, n, _stream()), "dc_batch")
     return dct

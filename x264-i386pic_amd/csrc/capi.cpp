@@ -343,6 +343,262 @@ template <int BD> static void c_dct2x4dc( typename PT<BD>::dctcoef dct[8], typen
     memcpy( &dct4x4[0][0], s, 128 * sizeof(dctcoef) );
 }
 
+// ============================================================ per-call inverse dct entries
+// add*_idct*: p_dst has the implicit FDEC_STRIDE (reference dct.h:31-33); the W x W
+// destination block is staged, updated by one kernel and copied back.  Unlike the
+// reference C add8x8_idct8 the caller's dct[] is left unmodified (checkasm compares
+// only the pixels, tools/checkasm.c:995-1013).
+template <int BD, int KIND, int W, int NC>
+static void idct_call( typename PT<BD>::pixel *p_dst, const typename PT<BD>::dctcoef *dct )
+{
+    using pixel = typename PT<BD>::pixel;
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A);
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    stage_block( a, p_dst, X264HIP_FDEC_STRIDE, W, W );
+    memcpy( o, dct, NC * sizeof(dctcoef) );
+    off[0] = 0;
+    CHECK_FATAL( launch_add_idct<BD>( KIND, dview( c, a ), W, dview( c, off ), dview( c, o ), 1, c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    for( int y = 0; y < W; y++ )
+        memcpy( p_dst + y * X264HIP_FDEC_STRIDE, a + y * W, W * sizeof(pixel) );
+}
+
+template <int BD> static void c_add4x4_idct( typename PT<BD>::pixel *p, typename PT<BD>::dctcoef dct[16] )
+{ idct_call<BD, X264HIP_IDCT_ADD4x4, 4, 16>( p, dct ); }
+template <int BD> static void c_add8x8_idct( typename PT<BD>::pixel *p, typename PT<BD>::dctcoef dct[4][16] )
+{ idct_call<BD, X264HIP_IDCT_ADD8x8, 8, 64>( p, &dct[0][0] ); }
+template <int BD> static void c_add16x16_idct( typename PT<BD>::pixel *p, typename PT<BD>::dctcoef dct[16][16] )
+{ idct_call<BD, X264HIP_IDCT_ADD16x16, 16, 256>( p, &dct[0][0] ); }
+template <int BD> static void c_add8x8_idct_dc( typename PT<BD>::pixel *p, typename PT<BD>::dctcoef dct[4] )
+{ idct_call<BD, X264HIP_IDCT_ADD8x8_DC, 8, 4>( p, dct ); }
+template <int BD> static void c_add16x16_idct_dc( typename PT<BD>::pixel *p, typename PT<BD>::dctcoef dct[16] )
+{ idct_call<BD, X264HIP_IDCT_ADD16x16_DC, 16, 16>( p, dct ); }
+template <int BD> static void c_add8x8_idct8( typename PT<BD>::pixel *p, typename PT<BD>::dctcoef dct[64] )
+{ idct_call<BD, X264HIP_IDCT_ADD8x8_8, 8, 64>( p, dct ); }
+template <int BD> static void c_add16x16_idct8( typename PT<BD>::pixel *p, typename PT<BD>::dctcoef dct[4][64] )
+{ idct_call<BD, X264HIP_IDCT_ADD16x16_8, 16, 256>( p, &dct[0][0] ); }
+
+template <int BD> static void c_idct4x4dc( typename PT<BD>::dctcoef d[16] )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    memcpy( o, d, 16 * sizeof(dctcoef) );
+    CHECK_FATAL( launch_idct4x4dc<BD>( dview( c, o ), 1, c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( d, o, 16 * sizeof(dctcoef) );
+}
+
+// ============================================================ per-call inverse quant entries
+// staging: coefficients at ST_COEF, dequant_mf at ST_COEF+4K, scalars at ST_SC
+constexpr size_t ST_DMF = ST_COEF + (4 << 10);
+
+template <int BD, int KIND, int N>
+static void dequant_call( typename PT<BD>::dctcoef *dct, const int *dmf, int qp )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    int32_t *m = (int32_t *)(c.host + ST_DMF);
+    int32_t *q = (int32_t *)(c.host + ST_SC);
+    memcpy( o, dct, N * sizeof(dctcoef) );
+    memcpy( m, dmf, 6 * (KIND == X264HIP_DEQUANT_8x8 ? 64 : 16) * sizeof(int32_t) );
+    q[0] = qp;
+    CHECK_FATAL( launch_dequant<BD>( KIND, dview( c, o ), dview( c, m ), dview( c, q ), 1, c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( dct, o, N * sizeof(dctcoef) );
+}
+template <int BD> static void c_dequant_4x4( typename PT<BD>::dctcoef dct[16], int dmf[6][16], int qp )
+{ dequant_call<BD, X264HIP_DEQUANT_4x4, 16>( dct, &dmf[0][0], qp ); }
+template <int BD> static void c_dequant_8x8( typename PT<BD>::dctcoef dct[64], int dmf[6][64], int qp )
+{ dequant_call<BD, X264HIP_DEQUANT_8x8, 64>( dct, &dmf[0][0], qp ); }
+template <int BD> static void c_dequant_4x4_dc( typename PT<BD>::dctcoef dct[16], int dmf[6][16], int qp )
+{ dequant_call<BD, X264HIP_DEQUANT_4x4_DC, 16>( dct, &dmf[0][0], qp ); }
+
+template <int BD>
+static void c_idct_dequant_2x4_dc( typename PT<BD>::dctcoef dct[8], typename PT<BD>::dctcoef dct4x4[8][16],
+                                   int dmf[6][16], int qp )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF), *s = o + 16;
+    int32_t *m = (int32_t *)(c.host + ST_DMF), *q = (int32_t *)(c.host + ST_SC);
+    memcpy( o, dct, 8 * sizeof(dctcoef) );
+    memcpy( m, &dmf[0][0], 96 * sizeof(int32_t) );
+    q[0] = qp;
+    CHECK_FATAL( launch_idct_dequant_2x4<BD>( 0, dview( c, o ), dview( c, s ), dview( c, m ), dview( c, q ), 1,
+                                              c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    for( int k = 0; k < 8; k++ )     // the reference writes only dct4x4[k][0]
+        dct4x4[k][0] = s[k * 16];
+}
+
+template <int BD>
+static void c_idct_dequant_2x4_dconly( typename PT<BD>::dctcoef dct[8], int dmf[6][16], int qp )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    int32_t *m = (int32_t *)(c.host + ST_DMF), *q = (int32_t *)(c.host + ST_SC);
+    memcpy( o, dct, 8 * sizeof(dctcoef) );
+    memcpy( m, &dmf[0][0], 96 * sizeof(int32_t) );
+    q[0] = qp;
+    CHECK_FATAL( launch_idct_dequant_2x4<BD>( 1, dview( c, o ), nullptr, dview( c, m ), dview( c, q ), 1, c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( dct, o, 8 * sizeof(dctcoef) );
+}
+
+template <int BD, int C422>
+static int c_optimize_chroma( typename PT<BD>::dctcoef *dct, int dmf )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    constexpr int N = C422 ? 8 : 4;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    int32_t *q = (int32_t *)(c.host + ST_SC);
+    memcpy( o, dct, N * sizeof(dctcoef) );
+    q[0] = dmf;
+    CHECK_FATAL( launch_optimize_chroma<BD>( C422, dview( c, o ), dview( c, q ), 1, dview( c, q + 1 ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( dct, o, N * sizeof(dctcoef) );
+    return q[1];
+}
+template <int BD> static int c_optimize_chroma_2x2_dc( typename PT<BD>::dctcoef dct[4], int dmf )
+{ return c_optimize_chroma<BD, 0>( dct, dmf ); }
+template <int BD> static int c_optimize_chroma_2x4_dc( typename PT<BD>::dctcoef dct[8], int dmf )
+{ return c_optimize_chroma<BD, 1>( dct, dmf ); }
+
+template <int BD>
+static void c_denoise_dct( typename PT<BD>::dctcoef *dct, uint32_t *sum, typename PT<BD>::udctcoef *offset, int size )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    using udctcoef = typename PT<BD>::udctcoef;
+    if( size <= 0 )
+        return;
+    if( size > 64 )
+    {
+        fprintf( stderr, "x264hip: denoise_dct size %d exceeds the per-call staging buffer\n", size );
+        abort();
+    }
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    uint32_t *sm = (uint32_t *)(c.host + ST_DMF);
+    udctcoef *of = (udctcoef *)(c.host + ST_DMF + 1024);
+    memcpy( o, dct, size * sizeof(dctcoef) );
+    memcpy( sm, sum, size * sizeof(uint32_t) );
+    memcpy( of, offset, size * sizeof(udctcoef) );
+    CHECK_FATAL( launch_denoise<BD>( dview( c, o ), size, 1, dview( c, sm ), dview( c, of ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( dct, o, size * sizeof(dctcoef) );
+    memcpy( sum, sm, size * sizeof(uint32_t) );
+}
+
+template <int BD, int KIND, int N>
+static int coef_stat_call( typename PT<BD>::dctcoef *dct )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    int32_t *r = (int32_t *)(c.host + ST_SC);
+    memcpy( o, dct, N * sizeof(dctcoef) );
+    CHECK_FATAL( launch_coef_stat<BD>( KIND, dview( c, o ), N, 1, dview( c, r ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    return r[0];
+}
+
+template <int BD, int NUM>
+static int c_level_run( typename PT<BD>::dctcoef *dct, struct x264hip_run_level_t *rl )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF);
+    dctcoef *lv = o + 64;
+    int32_t *r = (int32_t *)(c.host + ST_SC);
+    memcpy( o, dct, NUM * sizeof(dctcoef) );
+    CHECK_FATAL( launch_level_run<BD>( NUM, dview( c, o ), NUM, 1, dview( c, r ), dview( c, r + 1 ), dview( c, r + 2 ),
+                                       dview( c, lv ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    // x264_run_level_t: int32 last, int32 mask, 16-byte aligned dctcoef level[18]
+    // (reference common/bitstream.h:50-55)
+    uint8_t *base = (uint8_t *)rl;
+    memcpy( base, &r[0], 4 );
+    memcpy( base + 4, &r[1], 4 );
+    memcpy( base + 16, lv, r[2] * sizeof(dctcoef) );
+    return r[2];
+}
+
+// ============================================================ per-call zigzag entries
+template <int BD, int N>
+static void c_zigzag_scan( int field, typename PT<BD>::dctcoef *level, const typename PT<BD>::dctcoef *dct )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *o = (dctcoef *)(c.host + ST_COEF), *l = o + 64;
+    memcpy( o, dct, N * N * sizeof(dctcoef) );
+    CHECK_FATAL( launch_zigzag_scan<BD>( N, field, dview( c, l ), dview( c, o ), 1, c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( level, l, N * N * sizeof(dctcoef) );
+}
+template <int BD, int FIELD> static void c_scan_8x8( typename PT<BD>::dctcoef level[64], typename PT<BD>::dctcoef dct[64] )
+{ c_zigzag_scan<BD, 8>( FIELD, level, dct ); }
+template <int BD, int FIELD> static void c_scan_4x4( typename PT<BD>::dctcoef level[16], typename PT<BD>::dctcoef dct[16] )
+{ c_zigzag_scan<BD, 4>( FIELD, level, dct ); }
+
+// zigzag_sub: p_src stride FENC_STRIDE, p_dst stride FDEC_STRIDE (reference dct.c:828-840)
+template <int BD, int KIND, int FIELD>
+static int zigzag_sub_call( typename PT<BD>::dctcoef *level, const typename PT<BD>::pixel *src,
+                            typename PT<BD>::pixel *dst, typename PT<BD>::dctcoef *dc )
+{
+    using pixel = typename PT<BD>::pixel;
+    using dctcoef = typename PT<BD>::dctcoef;
+    constexpr int W = KIND == X264HIP_ZIGZAG_SUB_8x8 ? 8 : 4;
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    dctcoef *l = (dctcoef *)(c.host + ST_COEF), *d = l + 64;
+    int32_t *nz = (int32_t *)(c.host + ST_SC);
+    stage_block( a, src, X264HIP_FENC_STRIDE, W, W );
+    stage_block( b, (const pixel *)dst, X264HIP_FDEC_STRIDE, W, W );
+    off[0] = 0;
+    CHECK_FATAL( launch_zigzag_sub<BD>( KIND, FIELD, dview( c, l ), dview( c, d ), dview( c, a ), W, dview( c, b ), W,
+                                        dview( c, off ), dview( c, off ), 1, dview( c, nz ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( level, l, W * W * sizeof(dctcoef) );
+    for( int y = 0; y < W; y++ )
+        memcpy( dst + y * X264HIP_FDEC_STRIDE, b + y * W, W * sizeof(pixel) );
+    if( dc )
+        *dc = d[0];
+    return nz[0];
+}
+template <int BD, int FIELD>
+static int c_sub_8x8( typename PT<BD>::dctcoef level[64], const typename PT<BD>::pixel *s, typename PT<BD>::pixel *d )
+{ return zigzag_sub_call<BD, X264HIP_ZIGZAG_SUB_8x8, FIELD>( level, s, d, nullptr ); }
+template <int BD, int FIELD>
+static int c_sub_4x4( typename PT<BD>::dctcoef level[16], const typename PT<BD>::pixel *s, typename PT<BD>::pixel *d )
+{ return zigzag_sub_call<BD, X264HIP_ZIGZAG_SUB_4x4, FIELD>( level, s, d, nullptr ); }
+template <int BD, int FIELD>
+static int c_sub_4x4ac( typename PT<BD>::dctcoef level[16], const typename PT<BD>::pixel *s, typename PT<BD>::pixel *d,
+                        typename PT<BD>::dctcoef *dc )
+{ return zigzag_sub_call<BD, X264HIP_ZIGZAG_SUB_4x4AC, FIELD>( level, s, d, dc ); }
+
+template <int BD>
+static void c_interleave_8x8_cavlc( typename PT<BD>::dctcoef *dst, typename PT<BD>::dctcoef *src, uint8_t *nnz )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    CallCtx &c = call_ctx();
+    dctcoef *s = (dctcoef *)(c.host + ST_COEF), *d = s + 64;
+    uint8_t *nn = (uint8_t *)(c.host + ST_SC);
+    memcpy( s, src, 64 * sizeof(dctcoef) );
+    CHECK_FATAL( launch_interleave<BD>( dview( c, d ), dview( c, s ), dview( c, nn ), 1, c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( dst, d, 64 * sizeof(dctcoef) );
+    // the reference writes nnz[0], nnz[1], nnz[8], nnz[9] only (dct.c:927-940)
+    nnz[0] = nn[0]; nnz[1] = nn[1]; nnz[8] = nn[8]; nnz[9] = nn[9];
+}
+
 // ============================================================ per-call quant entries
 template <int BD, int KIND, int N, int NMF>
 static int quant_call( typename PT<BD>::dctcoef *dct, const typename PT<BD>::udctcoef *mf,
@@ -441,6 +697,32 @@ static void fill_dct( Tab *d )
     d->sub16x16_dct8 = c_sub16x16_dct8<BD>;
     d->dct4x4dc = c_dct4x4dc<BD>;
     d->dct2x4dc = c_dct2x4dc<BD>;
+    // inverse entries, reference dct.c:479-502
+    d->add4x4_idct = c_add4x4_idct<BD>;
+    d->add8x8_idct = c_add8x8_idct<BD>;
+    d->add8x8_idct_dc = c_add8x8_idct_dc<BD>;
+    d->add16x16_idct = c_add16x16_idct<BD>;
+    d->add16x16_idct_dc = c_add16x16_idct_dc<BD>;
+    d->add8x8_idct8 = c_add8x8_idct8<BD>;
+    d->add16x16_idct8 = c_add16x16_idct8<BD>;
+    d->idct4x4dc = c_idct4x4dc<BD>;
+}
+
+// zigzag tables, reference dct.c:938-951 (field scans for the interlaced table)
+template <int BD, typename Tab>
+static void fill_zigzag( Tab *p, Tab *i )
+{
+    p->scan_8x8 = c_scan_8x8<BD, 0>;
+    i->scan_8x8 = c_scan_8x8<BD, 1>;
+    p->scan_4x4 = c_scan_4x4<BD, 0>;
+    i->scan_4x4 = c_scan_4x4<BD, 1>;
+    p->sub_8x8 = c_sub_8x8<BD, 0>;
+    i->sub_8x8 = c_sub_8x8<BD, 1>;
+    p->sub_4x4 = c_sub_4x4<BD, 0>;
+    i->sub_4x4 = c_sub_4x4<BD, 1>;
+    p->sub_4x4ac = c_sub_4x4ac<BD, 0>;
+    i->sub_4x4ac = c_sub_4x4ac<BD, 1>;
+    p->interleave_8x8_cavlc = i->interleave_8x8_cavlc = c_interleave_8x8_cavlc<BD>;
 }
 
 template <int BD, typename Tab>
@@ -451,6 +733,35 @@ static void fill_quant( Tab *q )
     q->quant_4x4x4 = c_quant_4x4x4<BD>;
     q->quant_4x4_dc = c_quant_4x4_dc<BD>;
     q->quant_2x2_dc = c_quant_2x2_dc<BD>;
+    // reference quant.c:422-445 and the category aliasing at the end of x264_quant_init
+    q->dequant_4x4 = c_dequant_4x4<BD>;
+    q->dequant_4x4_dc = c_dequant_4x4_dc<BD>;
+    q->dequant_8x8 = c_dequant_8x8<BD>;
+    q->idct_dequant_2x4_dc = c_idct_dequant_2x4_dc<BD>;
+    q->idct_dequant_2x4_dconly = c_idct_dequant_2x4_dconly<BD>;
+    q->optimize_chroma_2x2_dc = c_optimize_chroma_2x2_dc<BD>;
+    q->optimize_chroma_2x4_dc = c_optimize_chroma_2x4_dc<BD>;
+    q->denoise_dct = c_denoise_dct<BD>;
+    q->decimate_score15 = coef_stat_call<BD, X264HIP_COEF_DECIMATE15, 16>;
+    q->decimate_score16 = coef_stat_call<BD, X264HIP_COEF_DECIMATE16, 16>;
+    q->decimate_score64 = coef_stat_call<BD, X264HIP_COEF_DECIMATE64, 64>;
+    q->coeff_last4 = coef_stat_call<BD, X264HIP_COEF_LAST4, 4>;
+    q->coeff_last8 = coef_stat_call<BD, X264HIP_COEF_LAST8, 8>;
+    // block categories, reference common/macroblock.h:273-289
+    for( int cat : { 1, 4, 7, 11 } )
+    {
+        q->coeff_last[cat] = coef_stat_call<BD, X264HIP_COEF_LAST15, 15>;
+        q->coeff_level_run[cat] = c_level_run<BD, 15>;
+    }
+    for( int cat : { 0, 2, 6, 8, 10, 12 } )
+    {
+        q->coeff_last[cat] = coef_stat_call<BD, X264HIP_COEF_LAST16, 16>;
+        q->coeff_level_run[cat] = c_level_run<BD, 16>;
+    }
+    for( int cat : { 5, 9, 13 } )
+        q->coeff_last[cat] = coef_stat_call<BD, X264HIP_COEF_LAST64, 64>;
+    q->coeff_level_run4 = c_level_run<BD, 4>;
+    q->coeff_level_run8 = c_level_run<BD, 8>;
 }
 
 // ============================================================ CQM (quant side)
@@ -542,6 +853,19 @@ static int map_err( hipError_t e, const char *where )
         memset( q, 0, sizeof(*q) );                                                                                  \
         if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
             fill_quant<BD>( q );                                                                                     \
+    }                                                                                                                \
+    extern "C" void x264hip_##BD##_zigzag_init_hip( x264hip_##BD##_zigzag_function_t *p,                            \
+                                                    x264hip_##BD##_zigzag_function_t *i )                            \
+    {                                                                                                                \
+        fill_zigzag<BD>( p, i );                                                                                     \
+    }                                                                                                                \
+    extern "C" void x264hip_##BD##_zigzag_init( uint32_t cpu, x264hip_##BD##_zigzag_function_t *p,                  \
+                                                x264hip_##BD##_zigzag_function_t *i )                                \
+    {                                                                                                                \
+        memset( p, 0, sizeof(*p) );                                                                                  \
+        memset( i, 0, sizeof(*i) );                                                                                  \
+        if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
+            fill_zigzag<BD>( p, i );                                                                                 \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_cqm_init( const uint8_t *const sl[8], int dz_inter, int dz_intra, int b8,         \
                                             PT<BD>::udctcoef *q4m, PT<BD>::udctcoef *q4b, PT<BD>::udctcoef *q8m,     \
@@ -649,9 +973,101 @@ static int map_err( hipError_t e, const char *where )
     extern "C" int x264hip_##BD##_dc_batch( int kind, PT<BD>::dctcoef *dct, PT<BD>::dctcoef *dct4x4, int n,         \
                                             void *stream )                                                           \
     {                                                                                                                \
-        if( kind < 0 || kind > 1 || n < 0 || ( kind == 1 && !dct4x4 ) )                                              \
+        if( kind < 0 || kind > 2 || n < 0 || ( kind == 1 && !dct4x4 ) )                                              \
             return X264HIP_EINVAL;                                                                                   \
+        if( kind == X264HIP_DC_I4x4 )                                                                                \
+            return map_err( launch_idct4x4dc<BD>( dct, n, (hipStream_t)stream ), "dc_batch" );                       \
         return map_err( launch_dc<BD>( kind, dct, dct4x4, n, (hipStream_t)stream ), "dc_batch" );                  \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_add_idct_batch( int kind, PT<BD>::pixel *dst, intptr_t ds, const int64_t *doff,    \
+                                                  const PT<BD>::dctcoef *dct, int n, void *stream )                  \
+    {                                                                                                                \
+        if( kind < 0 || kind > 6 || n < 0 )                                                                          \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_add_idct<BD>( kind, dst, ds, doff, dct, n, (hipStream_t)stream ), "add_idct_batch" ); \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_dequant_batch( int kind, PT<BD>::dctcoef *dct, const int32_t *dmf,                 \
+                                                 const int32_t *qp, int n, void *stream )                            \
+    {                                                                                                                \
+        if( kind < 0 || kind > 2 || n < 0 )                                                                          \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_dequant<BD>( kind, dct, dmf, qp, n, (hipStream_t)stream ), "dequant_batch" );         \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_idct_dequant_2x4_batch( int dconly, PT<BD>::dctcoef *dct,                           \
+                                                          PT<BD>::dctcoef *dct4x4, const int32_t *dmf,               \
+                                                          const int32_t *qp, int n, void *stream )                   \
+    {                                                                                                                \
+        if( n < 0 || ( !dconly && !dct4x4 ) )                                                                        \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_idct_dequant_2x4<BD>( dconly, dct, dct4x4, dmf, qp, n, (hipStream_t)stream ),         \
+                        "idct_dequant_2x4_batch" );                                                                  \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_optimize_chroma_dc_batch( int c422, PT<BD>::dctcoef *dct, const int32_t *dmf,      \
+                                                            int n, int32_t *nz, void *stream )                       \
+    {                                                                                                                \
+        if( n < 0 )                                                                                                  \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_optimize_chroma<BD>( c422, dct, dmf, n, nz, (hipStream_t)stream ),                    \
+                        "optimize_chroma_dc_batch" );                                                                \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_denoise_dct_batch( PT<BD>::dctcoef *dct, int size, int n, uint32_t *sum,           \
+                                                     const PT<BD>::udctcoef *offset, void *stream )                  \
+    {                                                                                                                \
+        if( n < 0 || size < 0 )                                                                                      \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_denoise<BD>( dct, size, n, sum, offset, (hipStream_t)stream ), "denoise_dct_batch" ); \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_coef_stat_batch( int kind, const PT<BD>::dctcoef *dct, int64_t pitch, int n,       \
+                                                   int32_t *out, void *stream )                                      \
+    {                                                                                                                \
+        if( kind < 0 || kind > 7 || n < 0 )                                                                          \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_coef_stat<BD>( kind, dct, pitch, n, out, (hipStream_t)stream ), "coef_stat_batch" );  \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_coeff_level_run_batch( int num, const PT<BD>::dctcoef *dct, int64_t pitch, int n,  \
+                                                         int32_t *last, int32_t *mask, int32_t *count,               \
+                                                         PT<BD>::dctcoef *level, void *stream )                      \
+    {                                                                                                                \
+        if( !( num == 4 || num == 8 || num == 15 || num == 16 ) || n < 0 )                                           \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_level_run<BD>( num, dct, pitch, n, last, mask, count, level, (hipStream_t)stream ),    \
+                        "coeff_level_run_batch" );                                                                   \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_zigzag_scan_batch( int size, int field, PT<BD>::dctcoef *level,                    \
+                                                     const PT<BD>::dctcoef *dct, int n, void *stream )               \
+    {                                                                                                                \
+        if( !( size == 4 || size == 8 ) || n < 0 )                                                                   \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_zigzag_scan<BD>( size, field ? 1 : 0, level, dct, n, (hipStream_t)stream ),          \
+                        "zigzag_scan_batch" );                                                                       \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_zigzag_sub_batch( int kind, int field, PT<BD>::dctcoef *level,                     \
+                                                    PT<BD>::dctcoef *dc, const PT<BD>::pixel *src, intptr_t ss,      \
+                                                    PT<BD>::pixel *dst, intptr_t ds, const int64_t *so,              \
+                                                    const int64_t *dso, int n, int32_t *nz, void *stream )           \
+    {                                                                                                                \
+        if( kind < 0 || kind > 2 || n < 0 || ( kind == 1 && !dc ) )                                                  \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_zigzag_sub<BD>( kind, field ? 1 : 0, level, dc, src, ss, dst, ds, so, dso, n, nz,      \
+                                               (hipStream_t)stream ), "zigzag_sub_batch" );                          \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_zigzag_interleave_batch( PT<BD>::dctcoef *dst, const PT<BD>::dctcoef *src,         \
+                                                           uint8_t *nnz, int n, void *stream )                       \
+    {                                                                                                                \
+        if( n < 0 )                                                                                                  \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_interleave<BD>( dst, src, nnz, n, (hipStream_t)stream ), "zigzag_interleave_batch" ); \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_mb_dequant_idct_add( int transform, const PT<BD>::dctcoef *dct, int mbw, int mbh,  \
+                                                       int nframes, const int32_t *dmf, const int32_t *qp,           \
+                                                       const PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs,         \
+                                                       PT<BD>::pixel *recon, intptr_t rs, intptr_t rfs,              \
+                                                       void *stream )                                                \
+    {                                                                                                                \
+        if( !( transform == 4 || transform == 8 ) || mbw < 0 || mbh < 0 || nframes < 0 )                             \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_mb_recon<BD>( transform, dct, mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs,   \
+                                             rfs, (hipStream_t)stream ), "mb_dequant_idct_add" );                    \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_quant_batch( int kind, PT<BD>::dctcoef *dct, const PT<BD>::udctcoef *mf,          \
                                                const PT<BD>::udctcoef *bias, int n, int32_t *nz, void *stream )      \
@@ -682,3 +1098,27 @@ static int map_err( hipError_t e, const char *where )
 
 DEFINE_ENTRIES( 8 )
 DEFINE_ENTRIES( 10 )
+
+// dequant4_mf / dequant8_mf of x264_cqm_init, reference common/set.c:31-39,
+// 52-61, 124-159 (host-side table set-up, the input of the dequant entries)
+static const uint8_t k_dequant4_scale[6][3] = {
+    { 10, 13, 16 }, { 11, 14, 18 }, { 13, 16, 20 }, { 14, 18, 23 }, { 16, 20, 25 }, { 18, 23, 29 } };
+static const uint8_t k_dequant8_scale[6][6] = {
+    { 20, 18, 32, 19, 25, 24 }, { 22, 19, 35, 21, 28, 26 }, { 26, 23, 42, 24, 33, 31 },
+    { 28, 25, 45, 26, 35, 33 }, { 32, 28, 51, 30, 40, 38 }, { 36, 32, 58, 34, 46, 43 } };
+static const uint8_t k_quant8_scan16[16] = { 0, 3, 4, 3, 3, 1, 5, 1, 4, 5, 2, 5, 3, 1, 5, 1 };
+
+extern "C" void x264hip_cqm_dequant( const uint8_t *const sl[8], int b8, int32_t *dq4, int32_t *dq8 )
+{
+    for( int q = 0; q < 6; q++ )
+    {
+        for( int l = 0; l < 4; l++ )
+            for( int i = 0; i < 16; i++ )
+                dq4[(l * 6 + q) * 16 + i] = k_dequant4_scale[q][(i & 1) + ((i >> 2) & 1)] * sl[l][i];
+        if( b8 )
+            for( int l = 0; l < 2; l++ )
+                for( int i = 0; i < 64; i++ )
+                    dq8[(l * 6 + q) * 64 + i] =
+                        k_dequant8_scale[q][k_quant8_scan16[((i >> 1) & 12) | (i & 3)]] * sl[4 + l][i];
+    }
+}

@@ -32,8 +32,6 @@ __device__ __forceinline__ void load_diff( int (&d)[N][N], const typename PT<BD>
     }
 }
 
-// value stored to a dctcoef (int16 wrap at 8 bit), read back as int
-template <int BD> __device__ __forceinline__ int sto( int v ) { return (int)(typename PT<BD>::dctcoef)v; }
 
 // sub4x4_dct on a difference block: out[i*4+k] (reference order)
 template <int BD>

@@ -70,6 +70,15 @@ template <> __device__ __forceinline__ uint32_t sadp<10>( uint32_t a, uint32_t b
     return __builtin_amdgcn_sad_u16( a, b, acc );
 }
 
+// value stored to a dctcoef (int16 wrap at 8 bit), read back as int
+template <int BD> __device__ __forceinline__ int sto( int v ) { return (int)(typename PT<BD>::dctcoef)v; }
+
+// x264_clip_pixel (reference common/common.h)
+template <int BD> __device__ __forceinline__ int clip_pix( int v )
+{
+    return v < 0 ? 0 : v > PT<BD>::PIXEL_MAX ? PT<BD>::PIXEL_MAX : v;
+}
+
 // k-th pixel of a packed dword
 template <int BD> __device__ __forceinline__ int upix( uint32_t w, int k )
 {
@@ -133,4 +142,43 @@ template <int BD>
 hipError_t launch_frame_integral( const typename PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride, int lines,
                                   int padh, int sub8x8, int nframes, uint16_t *integral, intptr_t ifstride,
                                   hipStream_t stream );
+template <int BD>
+hipError_t launch_add_idct( int kind, typename PT<BD>::pixel *dst, intptr_t ds, const int64_t *dst_off,
+                            const typename PT<BD>::dctcoef *dct, int n, hipStream_t stream );
+template <int BD>
+hipError_t launch_dequant( int kind, typename PT<BD>::dctcoef *dct, const int32_t *dmf, const int32_t *qp, int n,
+                           hipStream_t stream );
+template <int BD>
+hipError_t launch_idct4x4dc( typename PT<BD>::dctcoef *dct, int n, hipStream_t stream );
+template <int BD>
+hipError_t launch_idct_dequant_2x4( int dconly, typename PT<BD>::dctcoef *dct, typename PT<BD>::dctcoef *dct4x4,
+                                    const int32_t *dmf, const int32_t *qp, int n, hipStream_t stream );
+template <int BD>
+hipError_t launch_optimize_chroma( int c422, typename PT<BD>::dctcoef *dct, const int32_t *dmf, int n, int32_t *nz,
+                                   hipStream_t stream );
+template <int BD>
+hipError_t launch_denoise( typename PT<BD>::dctcoef *dct, int size, int n, uint32_t *sum,
+                           const typename PT<BD>::udctcoef *offset, hipStream_t stream );
+template <int BD>
+hipError_t launch_coef_stat( int kind, const typename PT<BD>::dctcoef *dct, int64_t pitch, int n, int32_t *out,
+                             hipStream_t stream );
+template <int BD>
+hipError_t launch_level_run( int num, const typename PT<BD>::dctcoef *dct, int64_t pitch, int n, int32_t *last,
+                             int32_t *mask, int32_t *count, typename PT<BD>::dctcoef *level, hipStream_t stream );
+template <int BD>
+hipError_t launch_zigzag_scan( int size, int field, typename PT<BD>::dctcoef *level,
+                               const typename PT<BD>::dctcoef *dct, int n, hipStream_t stream );
+template <int BD>
+hipError_t launch_zigzag_sub( int kind, int field, typename PT<BD>::dctcoef *level, typename PT<BD>::dctcoef *dc,
+                              const typename PT<BD>::pixel *src, intptr_t ss, typename PT<BD>::pixel *dst,
+                              intptr_t ds, const int64_t *so, const int64_t *dso, int n, int32_t *nz,
+                              hipStream_t stream );
+template <int BD>
+hipError_t launch_interleave( typename PT<BD>::dctcoef *dst, const typename PT<BD>::dctcoef *src, uint8_t *nnz, int n,
+                              hipStream_t stream );
+template <int BD>
+hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, int mbw, int mbh, int nframes,
+                            const int32_t *dmf, const int32_t *qp, const typename PT<BD>::pixel *pred, intptr_t ps,
+                            intptr_t pfs, typename PT<BD>::pixel *recon, intptr_t rs, intptr_t rfs,
+                            hipStream_t stream );
 } // namespace x264hip
