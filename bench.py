@@ -212,6 +212,36 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     wall, ev_ms = timed(hstep, a.steps, a.warmup, world)
     res["hpel_filter_frames_per_s"] = world * a.steps * F / wall
     res["hpel_filter_launch_ms"] = ev_ms
+    # fused reconstruction (dequant + idct + add, per-MB qp) on the coefficients of the last
+    # DCT+quant step, and the lookahead's half-resolution planes
+    dq4, dq8 = x.cqm_dequant([flat] * 8)
+    qp_mb = torch.full((nmb,), 26, dtype=torch.int32, device="cuda")
+    recon = torch.empty_like(dev[:-1])
+    for t, dq in ((4, dq4[1]), (8, dq8[1])):
+        x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F,
+                       mf4 if t == 4 else mf8, bs4 if t == 4 else bs8, dct=dct, nz=nz,
+                       fenc_frame_stride=fstride, pred_frame_stride=fstride)
+        dqd = torch.from_numpy(dq.copy()).cuda()
+
+        def rstep(t=t, dqd=dqd):
+            x.mb_dequant_idct_add(t, dct, mbw, mbh, F, dqd, qp_mb, dev[:-1], origin, stride, recon, origin, stride,
+                                  pred_frame_stride=fstride, recon_frame_stride=fstride)
+        wall, ev_ms = timed(rstep, a.steps, a.warmup, world)
+        blocks = nmb * (16 if t == 4 else 4)
+        bpb = (32 + 16 + 16) if t == 4 else (128 + 64 + 64)      # int16 coefs + pred in, recon out
+        res["recon%d_blocks_per_s" % t] = world * a.steps * blocks / wall
+        res["recon%d_hbm_frac" % t] = blocks * bpb / (ev_ms * 1e-3) / HBM_PEAK
+        res["recon%d_launch_ms" % t] = ev_ms
+    del recon
+    lw, lh = mbw * 16, mbh * 16
+    louts, _ = x.frame_init_lowres(dev[:-1], origin, stride, lw, lh)
+
+    def lstep():
+        x.frame_init_lowres(dev[:-1], origin, stride, lw, lh, outs=louts)
+    wall, ev_ms = timed(lstep, a.steps, a.warmup, world)
+    res["lowres_frames_per_s"] = world * a.steps * F / wall
+    res["lowres_launch_ms"] = ev_ms
+    del louts
     nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
     bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)

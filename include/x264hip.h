@@ -519,7 +519,17 @@ int x264hip_##BD##_mb_dequant_idct_add( int transform, const dctcoef *dct, int m
                                         const int32_t *qp, const pixel *pred,                   \
                                         intptr_t pred_stride, intptr_t pred_frame_stride,       \
                                         pixel *recon, intptr_t recon_stride,                    \
-                                        intptr_t recon_frame_stride, void *stream );
+                                        intptr_t recon_frame_stride, void *stream );               \
+                                                                                                \
+/* lookahead input: x264_frame_init_lowres (mc.c:458-507, frame.c:627-631) of n_frames          \
+ * luma planes of width x height (i_width[0] x i_lines[0]; src at (0,0)): the four              \
+ * half-resolution planes dst[0..3] (full-pel, H, V, centre) over [-32, width/2+32) x           \
+ * [-32, height/2+32) with the reference's border replication; dst points at (0,0),            \
+ * dst_stride a multiple of 4 bytes, (width/2+64) a multiple of 4/sizeof(pixel). */             \
+int x264hip_##BD##_frame_init_lowres( const pixel *src, intptr_t stride, intptr_t frame_stride, \
+                                      int width, int height, int n_frames, pixel *const dst[4], \
+                                      intptr_t dst_stride, intptr_t dst_frame_stride,           \
+                                      void *stream );
 
 /* dequant4_mf [4][6][16] and dequant8_mf [2][6][64] of x264_cqm_init (reference
  * common/set.c:124-159) for the 8 scaling lists; bit-depth independent. */

@@ -1498,3 +1498,56 @@ void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const i
         out[3 * i + 2] = bmy;
     }
 }
+
+/*============================================================================
+ * lookahead input — reference common/mc.c:458-507, common/frame.c:535-631
+ *==========================================================================*/
+
+/* x264_frame_init_lowres on a private copy of the luma plane: duplicate the
+ * last column / row (mc.c:465-468), frame_init_lowres_core (mc.c:484-507) into
+ * the four half-resolution planes, then plane_expand_border with PADH = PADV =
+ * 32 (frame.c:627-631).  src / dst point at (0,0); src has >= 1 pixel of
+ * writable padding right and below (the copy is taken from rows [0, height]
+ * and columns [0, width]). */
+void FN(frame_init_lowres)( const pixel *src_in, intptr_t stride, int width, int height,
+                            pixel *dst[4], intptr_t dst_stride )
+{
+    const int pad = 32, wl = width / 2, hl = height / 2;
+    pixel *src = malloc( (size_t)(height + 1) * stride * sizeof(pixel) );
+    for( int y = 0; y < height; y++ )
+        memcpy( src + y*stride, src_in + y*stride, (width + 1) * sizeof(pixel) );
+    for( int y = 0; y < height; y++ )
+        src[width + y*stride] = src[width - 1 + y*stride];
+    memcpy( src + stride*height, src + stride*(height - 1), (width + 1) * sizeof(pixel) );
+#define FILTER(a,b,c,d) ((((a+b+1)>>1)+((c+d+1)>>1)+1)>>1)
+    for( int y = 0; y < hl; y++ )
+    {
+        const pixel *s0 = src + 2*y*stride, *s1 = s0 + stride, *s2 = s1 + stride;
+        pixel *d0 = dst[0] + y*dst_stride, *dh = dst[1] + y*dst_stride;
+        pixel *dv = dst[2] + y*dst_stride, *dc = dst[3] + y*dst_stride;
+        for( int x = 0; x < wl; x++ )
+        {
+            d0[x] = FILTER( s0[2*x], s1[2*x], s0[2*x+1], s1[2*x+1] );
+            dh[x] = FILTER( s0[2*x+1], s1[2*x+1], s0[2*x+2], s1[2*x+2] );
+            dv[x] = FILTER( s1[2*x], s2[2*x], s1[2*x+1], s2[2*x+1] );
+            dc[x] = FILTER( s1[2*x+1], s2[2*x+1], s1[2*x+2], s2[2*x+2] );
+        }
+    }
+#undef FILTER
+    free( src );
+    for( int i = 0; i < 4; i++ )
+    {
+        pixel *pix = dst[i];
+        for( int y = 0; y < hl; y++ )
+            for( int k = 0; k < pad; k++ )
+            {
+                pix[y*dst_stride - pad + k] = pix[y*dst_stride];
+                pix[y*dst_stride + wl + k] = pix[y*dst_stride + wl - 1];
+            }
+        for( int y = 0; y < pad; y++ )
+        {
+            memcpy( pix + (-y-1)*dst_stride - pad, pix - pad, (wl + 2*pad) * sizeof(pixel) );
+            memcpy( pix + (hl + y)*dst_stride - pad, pix + (hl - 1)*dst_stride - pad, (wl + 2*pad) * sizeof(pixel) );
+        }
+    }
+}

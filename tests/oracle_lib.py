@@ -98,6 +98,7 @@ for _bd in (8, 10):
     _f(_bd, "zigzag_sub_s", [C.c_int, C.c_int, _P, _P, _IP, _P, _IP, _P], C.c_int)
     _f(_bd, "zigzag_interleave_8x8_cavlc", [_P, _P, _P])
     _f(_bd, "cqm_dequant", [_P, C.c_int, _P, _P])
+    _f(_bd, "frame_init_lowres", [_P, _IP, C.c_int, C.c_int, _P, _IP])
     _f(_bd, "mb_dequant_idct_add", [C.c_int, _P, C.c_int, C.c_int, _P, _P, _P, _IP, _P, _IP])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
@@ -387,3 +388,12 @@ def mb_dequant_idct_add(bd, transform, dct, mbw, mbh, dmf, qp, pred, p_origin, p
     fn(bd, "mb_dequant_idct_add")(transform, _addr(d), mbw, mbh, _addr(m), _addr(q), _addr(pred, p_origin), ps,
                                   _addr(recon, r_origin), rs)
     return recon
+
+
+def frame_init_lowres(bd, plane, origin, stride, width, height, dst_stride):
+    """returns 4 lowres planes [(height/2 + 64), dst_stride] with (0,0) at (32, 32)."""
+    hl = height // 2
+    outs = [np.zeros((hl + 64) * dst_stride, pixel_dtype(bd)) for _ in range(4)]
+    ptrs = (C.c_void_p * 4)(*[o.ctypes.data + (32 * dst_stride + 32) * o.itemsize for o in outs])
+    fn(bd, "frame_init_lowres")(_addr(plane, origin), stride, width, height, ptrs, dst_stride)
+    return [o.reshape(hl + 64, dst_stride) for o in outs]

@@ -59,3 +59,24 @@ def test_subpel_cmp_random(hip, oracle, bd, op):
                                    torch.from_numpy(fo).cuda(), torch.from_numpy(qxy).cuda()).cpu().numpy()
         want = oracle.subpel_list(bd, op, i_pixel, planes.ravel(), stride, host_planes, origin, stride, fo, qxy)
         assert np.array_equal(got, want), (i_pixel, np.argwhere(got != want)[:3])
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("size", [(1920, 1088), (176, 144), (72, 40)])
+def test_frame_init_lowres(hip, oracle, bd, size):
+    """x264_frame_init_lowres of 3 frames per call vs the oracle; the source padding holds
+    unrelated values (the reference duplicates column W / row H itself)."""
+    W, H = size
+    n = 3
+    rs = np.random.default_rng(bd * 7 + W)
+    stride = (W + 64 + 63) // 64 * 64
+    pdt = np.uint8 if bd == 8 else np.uint16
+    planes = rs.integers(0, 1 << bd, size=(n, H + 64, stride)).astype(pdt)
+    planes[1, 32:40, 32:32 + W] = (1 << bd) - 1
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
+    outs, ls = hip.frame_init_lowres(dev, 32 * stride + 32, stride, W, H)
+    for f in range(n):
+        want = oracle.frame_init_lowres(bd, planes[f].ravel(), 32 * stride + 32, stride, W, H, ls)
+        for k in range(4):
+            got = outs[k][f].cpu().numpy().view(pdt)
+            assert np.array_equal(got[:, :W // 2 + 64], want[k][:, :W // 2 + 64]), (f, k)

@@ -266,6 +266,8 @@ def _declare(L):
         f("zigzag_scan_batch").argtypes = [_c.c_int, _c.c_int, _P, _P, _c.c_int, _P]
         f("zigzag_sub_batch").argtypes = [_c.c_int, _c.c_int, _P, _P, _P, _IP, _P, _IP, _P, _P, _c.c_int, _P, _P]
         f("zigzag_interleave_batch").argtypes = [_P, _P, _P, _c.c_int, _P]
+        f("frame_init_lowres").argtypes = [_P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P, _IP, _IP, _P]
+        f("frame_init_lowres").restype = _c.c_int
         f("mb_dequant_idct_add").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _IP, _IP,
                                              _P, _IP, _IP, _P]
         for n in ("add_idct_batch", "dequant_batch", "idct_dequant_2x4_batch", "optimize_chroma_dc_batch",
@@ -518,6 +520,28 @@ def mb_dequant_idct_add(transform, dct, mb_width, mb_height, nframes, dequant_mf
         transform, _ptr(dct), mb_width, mb_height, nframes, _ptr(dequant_mf), _ptr(qp), _ptr(pred, pred_origin),
         pred_stride, pfs, _ptr(recon, recon_origin), recon_stride, rfs, _stream()), "mb_dequant_idct_add")
     return recon
+
+
+def frame_init_lowres(planes, origin, stride, width, height, outs=None):
+    """x264_frame_init_lowres of every frame of `planes` [n, rows, stride]: four half-resolution
+    planes [n, height/2 + 2*PAD, lowres_stride] with (0,0) at (PAD, PAD); returns (outs, lowres_stride)."""
+    import torch
+    bd = _pix_bd(planes)
+    n = planes.shape[0]
+    wl, hl = width // 2, height // 2
+    ls = plane_stride(wl)
+    if outs is None:
+        outs = [torch.zeros((n, hl + 2 * PAD, ls), dtype=planes.dtype, device=planes.device) for _ in range(4)]
+    ptrs = (_P * 4)(*[o.data_ptr() + (PAD * ls + PAD) * o.element_size() for o in outs])
+    _rc(getattr(lib(), f"x264hip_{bd}_frame_init_lowres")(
+        _ptr(planes, origin), stride, planes[0].numel(), width, height, n, ptrs, ls, outs[0][0].numel(), _stream()),
+        "frame_init_lowres")
+    return outs, ls
+
+
+def plane_stride(width, pad=PAD):
+    """x264-style stride of a padded plane: width + 2*pad rounded up to 64 pixels."""
+    return (width + 2 * pad + 63) // 64 * 64
 
 
 def me_table_pitch(rng):

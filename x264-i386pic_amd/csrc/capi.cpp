@@ -1058,6 +1058,18 @@ static int map_err( hipError_t e, const char *where )
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_interleave<BD>( dst, src, nnz, n, (hipStream_t)stream ), "zigzag_interleave_batch" ); \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_frame_init_lowres( const PT<BD>::pixel *src, intptr_t stride, intptr_t fstride,   \
+                                                     int width, int height, int nframes,                             \
+                                                     PT<BD>::pixel *const dst[4], intptr_t ds, intptr_t dfs,         \
+                                                     void *stream )                                                  \
+    {                                                                                                                \
+        if( width < 2 || height < 2 || nframes < 0 || !dst || ( (width / 2 + 64) % PT<BD>::PPD ) ||                 \
+            ( (ds * (intptr_t)sizeof(PT<BD>::pixel)) & 3 ) || ( ( (uintptr_t)dst[0] | (uintptr_t)dst[1] |             \
+                                                                    (uintptr_t)dst[2] | (uintptr_t)dst[3] ) & 3 ) )  \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_frame_init_lowres<BD>( src, stride, fstride, width, height, nframes, dst, ds, dfs,     \
+                                                      (hipStream_t)stream ), "frame_init_lowres" );                  \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_mb_dequant_idct_add( int transform, const PT<BD>::dctcoef *dct, int mbw, int mbh,  \
                                                        int nframes, const int32_t *dmf, const int32_t *qp,           \
                                                        const PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs,         \

@@ -181,4 +181,8 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
                             const int32_t *dmf, const int32_t *qp, const typename PT<BD>::pixel *pred, intptr_t ps,
                             intptr_t pfs, typename PT<BD>::pixel *recon, intptr_t rs, intptr_t rfs,
                             hipStream_t stream );
+template <int BD>
+hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t stride, intptr_t fstride, int width,
+                                     int height, int nframes, typename PT<BD>::pixel *const dst[4], intptr_t ds,
+                                     intptr_t dfs, hipStream_t stream );
 } // namespace x264hip

@@ -256,12 +256,84 @@ hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel 
     return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// x264_frame_init_lowres (mc.c:458-482): frame_init_lowres_core's four
+// half-resolution planes (mc.c:484-507, FILTER = nested rounding averages)
+// over the core [0, W/2) x [0, H/2) plus the 32-pixel border replication of
+// x264_frame_expand_border_lowres (frame.c:627-631), in one pass: a border
+// pixel takes the value of the clamped core pixel.  The source column W and
+// row H, which the reference duplicates from W-1 / H-1 before filtering, are
+// read through the same clamp.  One lane per PPD output pixels (one dword of
+// each plane).
+template <int BD>
+__global__ __launch_bounds__( 256 ) void lowres_kernel( const typename PT<BD>::pixel *src, intptr_t stride,
+                                                        intptr_t fstride, int width, int height,
+                                                        typename PT<BD>::pixel *d0, typename PT<BD>::pixel *dh,
+                                                        typename PT<BD>::pixel *dv, typename PT<BD>::pixel *dc,
+                                                        intptr_t ds, intptr_t dfs )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int PPD = PT<BD>::PPD, PAD = 32;
+    const int wl = width / 2, hl = height / 2;
+    const int gw = (wl + 2 * PAD) / PPD;                   // dword groups per output row
+    const int g = blockIdx.x * blockDim.x + threadIdx.x;
+    const int y = (int)blockIdx.y - PAD;
+    if( g >= gw )
+        return;
+    const int f = blockIdx.z;
+    const pixel *s = src + f * fstride;
+    const int yc = min( max( y, 0 ), hl - 1 );
+    const pixel *r0 = s + (intptr_t)(2 * yc) * stride;
+    const pixel *r1 = s + (intptr_t)min( 2 * yc + 1, height - 1 ) * stride;
+    const pixel *r2 = s + (intptr_t)min( 2 * yc + 2, height - 1 ) * stride;
+    uint32_t w0 = 0, wh = 0, wv = 0, wc = 0;
+#pragma unroll
+    for( int j = 0; j < PPD; j++ )
+    {
+        const int x = g * PPD + j - PAD;
+        const int xc = min( max( x, 0 ), wl - 1 );
+        const int c0 = 2 * xc, c1 = min( 2 * xc + 1, width - 1 ), c2 = min( 2 * xc + 2, width - 1 );
+        const int a0 = r0[c0], a1 = r0[c1], a2 = r0[c2];
+        const int b0 = r1[c0], b1 = r1[c1], b2 = r1[c2];
+        const int e0 = r2[c0], e1 = r2[c1], e2 = r2[c2];
+#define FILTER( a, b, c, d ) ((((a + b + 1) >> 1) + ((c + d + 1) >> 1) + 1) >> 1)
+        const int sh = j * (32 / PPD);
+        w0 |= (uint32_t)FILTER( a0, b0, a1, b1 ) << sh;
+        wh |= (uint32_t)FILTER( a1, b1, a2, b2 ) << sh;
+        wv |= (uint32_t)FILTER( b0, e0, b1, e1 ) << sh;
+        wc |= (uint32_t)FILTER( b1, e1, b2, e2 ) << sh;
+#undef FILTER
+    }
+    const intptr_t o = f * dfs + (intptr_t)y * ds + g * PPD - PAD;
+    *(uint32_t *)(d0 + o) = w0;
+    *(uint32_t *)(dh + o) = wh;
+    *(uint32_t *)(dv + o) = wv;
+    *(uint32_t *)(dc + o) = wc;
+}
+
+template <int BD>
+hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t stride, intptr_t fstride, int width,
+                                     int height, int nframes, typename PT<BD>::pixel *const dst[4], intptr_t ds,
+                                     intptr_t dfs, hipStream_t st )
+{
+    if( nframes <= 0 )
+        return hipSuccess;
+    const int wl = width / 2, hl = height / 2;
+    const int gw = (wl + 64) / PT<BD>::PPD;
+    dim3 blk( 256 ), g( (unsigned)((gw + 255) / 256), (unsigned)(hl + 64), (unsigned)nframes );
+    hipLaunchKernelGGL( lowres_kernel<BD>, g, blk, 0, st, src, stride, fstride, width, height, dst[0], dst[1], dst[2],
+                        dst[3], ds, dfs );
+    return hipGetLastError();
+}
+
 #define INST( BD )                                                                                              \
     template hipError_t launch_hpel_filter<BD>( const PT<BD>::pixel *, PT<BD>::pixel *, PT<BD>::pixel *,       \
                                                 PT<BD>::pixel *, intptr_t, intptr_t, int, int, int, hipStream_t ); \
     template hipError_t launch_subpel_cmp<BD>( int, int, const PT<BD>::pixel *, intptr_t,                      \
                                                const PT<BD>::pixel *const[4], intptr_t, const int64_t *,       \
-                                               const int32_t *, int, int32_t *, hipStream_t );
+                                               const int32_t *, int, int32_t *, hipStream_t );      \
+    template hipError_t launch_frame_init_lowres<BD>( const PT<BD>::pixel *, intptr_t, intptr_t, int, int, int,  \
+                                                      PT<BD>::pixel *const[4], intptr_t, intptr_t, hipStream_t );
 INST( 8 )
 INST( 10 )
 
