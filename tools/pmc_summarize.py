@@ -30,6 +30,21 @@ for k, d in out["kernels"].items():
         d["hbm_bytes_corrected"] = 2 * d["FETCH_SIZE"] * 1024 + d["WRITE_SIZE"] * 1024
     if "me_full_sad16" in k and "hbm_bytes_corrected" in d:
         out["hbm_bytes_per_launch"] = d["hbm_bytes_corrected"]
+# per-dispatch durations of the headline kernel from the kernel trace: all
+# dispatches, and the last `steps` ones (the bench's timed region follows its
+# warmup launches of the same kernel; the GPU clock ramps during the first ~100)
+durs = []
+for r in csv.DictReader(open(os.path.join(src, "prof_trace", "run_kernel_trace.csv"))):
+    if "me_full_sad16_v3_kernel" in r["Kernel_Name"]:
+        durs.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3))
+durs.sort()
+steps = b["steps"]
+trace = {"kernel": "me_full_sad16_v3_kernel", "dispatches": len(durs),
+         "avg_us_all": sum(d for _, d in durs) / max(1, len(durs)),
+         "avg_us_timed_region": sum(d for _, d in durs[-steps:]) / max(1, len(durs[-steps:])),
+         "bench_event_launch_us": b["roofline"]["launch_ms"] * 1e3}
+out["trace"] = trace
+json.dump(trace, open(os.path.join(dst, f"{tag}_me_trace_summary.json"), "w"), indent=1)
 json.dump(out, open(os.path.join(dst, "pmc_me_full.json"), "w"), indent=1)
 shutil.copy(os.path.join(src, "bench.log"), os.path.join(dst, f"{tag}_bench.log"))
 print(json.dumps(out, indent=1))
