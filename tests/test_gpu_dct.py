@@ -174,9 +174,19 @@ def test_dc_and_quant_dc_batch(hip, oracle, bd):
             assert np.array_equal(g[i], want) and nz[i] == wnz, (name, i)
 
 
+@pytest.fixture(params=["default", "1", "2", "3", "4", "5"])
+def dq_variant(request, monkeypatch):
+    """X264HIP_DQ_VARIANT: 1 block-major, 2 unstaged strip, 3 / 4 band layout staged / direct (transform 4)."""
+    if request.param != "default":
+        monkeypatch.setenv("X264HIP_DQ_VARIANT", request.param)
+    else:
+        monkeypatch.delenv("X264HIP_DQ_VARIANT", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("transform", [4, 8])
-def test_mb_dct_quant_1080p(hip, oracle, bd, transform):
+def test_mb_dct_quant_1080p(hip, oracle, bd, transform, dq_variant):
     """fused residual transform + quant over a whole 1080p frame pair (plus a
     second frame in the same launch) vs the oracle, QP 26 flat16, inter lists.
     The prediction is the reference displaced by the sequence's true motion

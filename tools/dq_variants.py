@@ -24,16 +24,20 @@ for bd in (8, 10):
         mf, bias = torch.from_numpy(mf.copy()).cuda(), torch.from_numpy(bias.copy()).cuda()
         outs = {}
         times = {}
-        for v in ("1", "2", "3"):
+        for v in ("1", "2", "3", "4", "5", "0"):
             os.environ["X264HIP_DQ_VARIANT"] = v
             outs[v] = x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin + 2 * stride + 3, stride, W // 16,
                                      H // 16, F, mf, bias, fenc_frame_stride=fsz, pred_frame_stride=fsz)
             times[v] = []
         torch.cuda.synchronize()
-        for v in ("2", "3"):
+        for _ in range(150):        # settle the clocks (tools/me_sustain.py)
+            x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin + 2 * stride + 3, stride, W // 16,
+                           H // 16, F, mf, bias, dct=outs["1"][0], nz=outs["1"][1], fenc_frame_stride=fsz,
+                           pred_frame_stride=fsz)
+        for v in ("2", "3", "4", "5", "0"):
             assert torch.equal(outs["1"][0], outs[v][0]) and torch.equal(outs["1"][1], outs[v][1]), v
         for rnd in range(5):
-            for v in ("1", "2", "3"):
+            for v in ("1", "2", "3", "4", "5", "0"):
                 os.environ["X264HIP_DQ_VARIANT"] = v
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -46,7 +50,7 @@ for bd in (8, 10):
         ps = 1 if bd == 8 else 2
         cs = 2 if bd == 8 else 4
         alg = nmb * 256 * (2 * ps + cs) + nmb * 4
-        for v in ("1", "2", "3"):
+        for v in ("1", "2", "3", "4", "5", "0"):
             ms = float(np.median(times[v]))
             res[f"bd{bd}_t{t}_v{v}"] = {"ms": ms, "Gblocks_s": nmb * (16 if t == 4 else 4) / ms / 1e6,
                                        "GBps": alg / ms / 1e6, "hbm_frac": alg / ms / 1e6 / 8000}

@@ -569,6 +569,177 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_strip_kernel(
     }
 }
 
+// Variant 3 (transform 4): one lane per (MB, 4-row band) of a 16-MB strip, so
+// every row of a band is a single 16-pixel vector load per plane (lanes of a
+// band read 256 contiguous pixels); the lane transforms and quantises the four
+// 4x4 blocks of its band and stages them in LDS like variant 0.
+template <int BD>
+__device__ __forceinline__ void load16( const typename PT<BD>::pixel *p, uint32_t (&w)[16 / PT<BD>::PPD] )
+{
+    constexpr int N = 16 / PT<BD>::PPD;
+    if( ((uintptr_t)p & 15) == 0 )
+    {
+#pragma unroll
+        for( int k = 0; k < N / 4; k++ )
+        {
+            const uint4 v = ((const uint4 *)p)[k];
+            w[4 * k] = v.x; w[4 * k + 1] = v.y; w[4 * k + 2] = v.z; w[4 * k + 3] = v.w;
+        }
+    }
+    else
+        load_packed<N>( p, w );
+}
+
+template <int BD, bool STAGE>
+__global__ __launch_bounds__( 256 ) void mb_dct_quant_band_kernel(
+    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
+    const typename PT<BD>::pixel *__restrict__ pred, intptr_t ps, intptr_t pfs, int mbw, int mbh, int nframes,
+    const typename PT<BD>::udctcoef *__restrict__ mf, const typename PT<BD>::udctcoef *__restrict__ bias,
+    typename PT<BD>::dctcoef *__restrict__ dct, int32_t *__restrict__ nz )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    constexpr int PPD = PT<BD>::PPD;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int spr = (mbw + 15) >> 4;
+    if( wave >= (int64_t)nframes * mbh * spr )
+        return;                                               // wave-uniform
+    const int strip = (int)(wave % spr);
+    const int64_t t = wave / spr;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+    const int m = lane & 15, by = lane >> 4;                  // MB in the strip, 4-row band
+    const int mbx = strip * 16 + m;
+    const bool live = mbx < mbw;
+    const int64_t mbrow = (f * mbh + mby) * (int64_t)mbw;
+    __shared__ dctcoef lds[STAGE ? 4 * 16 * 256 : 1];
+    dctcoef *stage = STAGE ? lds + (threadIdx.x >> 6) * (16 * 256) : dct + (mbrow + strip * 16) * 256;
+    int mask = 0;
+    if( live )
+    {
+        const typename PT<BD>::pixel *a = fenc + f * ffs + (intptr_t)(16 * mby + 4 * by) * fs + 16 * mbx;
+        const typename PT<BD>::pixel *b = pred + f * pfs + (intptr_t)(16 * mby + 4 * by) * ps + 16 * mbx;
+        int d[4][4][4];                                       // [block][y][x]
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+        {
+            uint32_t wa[16 / PPD], wb[16 / PPD];
+            load16<BD>( a + y * fs, wa );
+            load16<BD>( b + y * ps, wb );
+#pragma unroll
+            for( int x = 0; x < 16; x++ )
+                d[x >> 2][y][x & 3] = upix<BD>( wa[x / PPD], x % PPD ) - upix<BD>( wb[x / PPD], x % PPD );
+        }
+#pragma unroll
+        for( int bx = 0; bx < 4; bx++ )
+        {
+            int c[16];
+            dct4x4_core<BD>( d[bx], c );
+            int acc = 0;
+#pragma unroll
+            for( int k = 0; k < 16; k++ )
+            {
+                c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
+                acc |= c[k];
+            }
+            const int i8 = (by >> 1) * 2 + (bx >> 1), i4 = (by & 1) * 2 + (bx & 1);
+            store_coefs( stage + m * 256 + (i8 * 4 + i4) * 16, c );
+            mask |= (acc != 0) << (4 * i8 + i4);
+        }
+    }
+    // OR over the MB's four band lanes (lane ^ 16, lane ^ 32)
+    mask |= __shfl_xor( mask, 16 );
+    mask |= __shfl_xor( mask, 32 );
+    if( live && by == 0 )
+        nz[mbrow + mbx] = mask;
+    if constexpr( STAGE )
+    {
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
+        const int nmb = min( 16, mbw - strip * 16 );
+        const int nvec = nmb * 256 * (int)sizeof( dctcoef ) / 16;
+        const uint4 *src = (const uint4 *)stage;
+        uint4 *dst = (uint4 *)(dct + (mbrow + strip * 16) * 256);
+        for( int i = lane; i < nvec; i += 64 )
+            dst[i] = src[i];
+    }
+}
+
+// Variant 5 (transform 4): as variant 3 with 8 MBs per wave: lane = (band, MB,
+// half) reads 8 pixels per row and transforms two 4x4 blocks; half the LDS per
+// wave (more resident waves) and twice the waves (a shorter tail).
+template <int BD>
+__global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
+    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
+    const typename PT<BD>::pixel *__restrict__ pred, intptr_t ps, intptr_t pfs, int mbw, int mbh, int nframes,
+    const typename PT<BD>::udctcoef *__restrict__ mf, const typename PT<BD>::udctcoef *__restrict__ bias,
+    typename PT<BD>::dctcoef *__restrict__ dct, int32_t *__restrict__ nz )
+{
+    using dctcoef = typename PT<BD>::dctcoef;
+    constexpr int PPD = PT<BD>::PPD;
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int spr = (mbw + 7) >> 3;
+    if( wave >= (int64_t)nframes * mbh * spr )
+        return;                                               // wave-uniform
+    const int strip = (int)(wave % spr);
+    const int64_t t = wave / spr;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+    const int m = (lane & 15) >> 1, half = lane & 1, by = lane >> 4;
+    const int mbx = strip * 8 + m;
+    const bool live = mbx < mbw;
+    const int64_t mbrow = (f * mbh + mby) * (int64_t)mbw;
+    __shared__ dctcoef lds[4 * 8 * 256];
+    dctcoef *stage = lds + (threadIdx.x >> 6) * (8 * 256);
+    int mask = 0;
+    if( live )
+    {
+        const typename PT<BD>::pixel *a = fenc + f * ffs + (intptr_t)(16 * mby + 4 * by) * fs + 16 * mbx + 8 * half;
+        const typename PT<BD>::pixel *b = pred + f * pfs + (intptr_t)(16 * mby + 4 * by) * ps + 16 * mbx + 8 * half;
+        int d[2][4][4];
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+        {
+            uint32_t wa[8 / PPD], wb[8 / PPD];
+            load_packed<8 / PPD>( a + y * fs, wa );
+            load_packed<8 / PPD>( b + y * ps, wb );
+#pragma unroll
+            for( int x = 0; x < 8; x++ )
+                d[x >> 2][y][x & 3] = upix<BD>( wa[x / PPD], x % PPD ) - upix<BD>( wb[x / PPD], x % PPD );
+        }
+#pragma unroll
+        for( int k2 = 0; k2 < 2; k2++ )
+        {
+            int c[16];
+            dct4x4_core<BD>( d[k2], c );
+            int acc = 0;
+#pragma unroll
+            for( int k = 0; k < 16; k++ )
+            {
+                c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
+                acc |= c[k];
+            }
+            const int i8 = (by >> 1) * 2 + half, i4 = (by & 1) * 2 + k2;
+            store_coefs( stage + m * 256 + (i8 * 4 + i4) * 16, c );
+            mask |= (acc != 0) << (4 * i8 + i4);
+        }
+    }
+    mask |= __builtin_amdgcn_update_dpp( 0, mask, 0xB1, 0xF, 0xF, false );   // lane ^ 1
+    mask |= __shfl_xor( mask, 16 );
+    mask |= __shfl_xor( mask, 32 );
+    if( live && by == 0 && half == 0 )
+        nz[mbrow + mbx] = mask;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
+    const int nmb = min( 8, mbw - strip * 8 );
+    const int nvec = nmb * 256 * (int)sizeof( dctcoef ) / 16;
+    const uint4 *src = (const uint4 *)stage;
+    uint4 *dst = (uint4 *)(dct + (mbrow + strip * 8) * 256);
+    for( int i = lane; i < nvec; i += 64 )
+        dst[i] = src[i];
+}
+
 template <int BD>
 hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                                 const typename PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs, int mbw, int mbh,
@@ -587,6 +758,25 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
         if( waves <= 0 )
             return hipSuccess;
         dim3 blk( 256 ), g( (unsigned)((waves + 3) / 4) );
+        // transform 4 default: variant 5 (0.62-0.71 of HBM vs 0.50-0.52 for variant 0,
+        // tools/dq_variants.py); X264HIP_DQ_VARIANT=0 selects the 16-MB staged strip
+        if( transform == 4 && (!ev || atoi( ev ) == 5) )
+        {
+            const int64_t hw = (int64_t)nframes * mbh * ((mbw + 7) / 8);
+            hipLaunchKernelGGL( mb_dct_quant_halfband_kernel<BD>, dim3( (unsigned)((hw + 3) / 4) ), blk, 0, stream, fenc,
+                                fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+            return hipGetLastError();
+        }
+        if( transform == 4 && ev && (atoi( ev ) == 3 || atoi( ev ) == 4) )
+        {
+            if( atoi( ev ) == 3 )
+                hipLaunchKernelGGL( ( mb_dct_quant_band_kernel<BD, true> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps,
+                                    pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+            else
+                hipLaunchKernelGGL( ( mb_dct_quant_band_kernel<BD, false> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps,
+                                    pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+            return hipGetLastError();
+        }
         const bool stage = !ev || atoi( ev ) != 2;
 #define DQ_STRIP( T, S ) hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, S> ), g, blk, 0, stream, fenc, fs, ffs, \
                                              pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz )
