@@ -358,9 +358,19 @@ def test_zigzag_sub_batch_random(hip, oracle, bd):
             assert np.array_equal(dd.cpu().numpy().view(pdt), want_dst)
 
 
+@pytest.fixture(params=["default", "0", "1"])
+def recon_variant(request, monkeypatch):
+    """X264HIP_RECON_VARIANT: 0 = block-pair lanes for transform 4, 1 = one lane per block."""
+    if request.param == "default":
+        monkeypatch.delenv("X264HIP_RECON_VARIANT", raising=False)
+    else:
+        monkeypatch.setenv("X264HIP_RECON_VARIANT", request.param)
+    return request.param
+
+
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("transform", [4, 8])
-def test_mb_dequant_idct_add_frames(hip, oracle, bd, transform):
+def test_mb_dequant_idct_add_frames(hip, oracle, bd, transform, recon_variant):
     """forward (mb_dct_quant) then inverse (mb_dequant_idct_add) over 3 frames of 1080p-width
     synthetic video with per-MB qp; recon compared with the oracle's per-MB dequant + add16x16_idct(8)."""
     from x264hip import synth

@@ -16,6 +16,8 @@
 // Every dctcoef store of the reference (int16 at 8 bit) is reproduced with sto<BD>.
 #include "hipcommon.h"
 
+#include <stdlib.h>
+
 namespace x264hip {
 
 // ------------------------------------------------------------------ helpers
@@ -869,6 +871,69 @@ __global__ __launch_bounds__( 256 ) void mb_recon_kernel( const typename PT<BD>:
     }
 }
 
+// transform 4, 8-pixel variant: one lane per pair of horizontally adjacent
+// 4x4 blocks (their 32 coefficients are contiguous in the dct4x4 order), so
+// pixel rows move as 8-pixel pieces and a wave covers 8 MBs of one MB row
+template <int BD>
+__global__ __launch_bounds__( 256 ) void mb_recon_pair_kernel( const typename PT<BD>::dctcoef *dct, int mbw, int mbh,
+                                                               int nframes, const int32_t *dmf, const int32_t *qp,
+                                                               const typename PT<BD>::pixel *pred, intptr_t ps,
+                                                               intptr_t pfs, typename PT<BD>::pixel *recon,
+                                                               intptr_t rs, intptr_t rfs )
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int spr = (mbw + 7) >> 3;
+    if( wave >= (int64_t)nframes * mbh * spr )
+        return;
+    const int strip = (int)(wave % spr);
+    const int64_t t = wave / spr;
+    const int mby = (int)(t % mbh);
+    const int f = (int)(t / mbh);
+    const int m = (lane & 15) >> 1, half = lane & 1, by = lane >> 4;
+    const int mbx = strip * 8 + m;
+    if( mbx >= mbw )
+        return;
+    const int64_t mb = ((int64_t)f * mbh + mby) * mbw + mbx;
+    const int q = qp[mb];
+    const int qb = q / 6 - 4;
+    const int32_t *mq = dmf + (q % 6) * 16;
+    const int i8 = (by >> 1) * 2 + half, i4 = (by & 1) * 2;
+    int c[32];
+    load_coefs<BD, 32>( dct + mb * 256 + (i8 * 4 + i4) * 16, c );
+    int res[4][8];
+#pragma unroll
+    for( int k = 0; k < 2; k++ )
+    {
+        int cc[16], r[4][4];
+#pragma unroll
+        for( int j = 0; j < 16; j++ )
+        {
+            const int v = c[k * 16 + j], mm = mq[j];
+            cc[j] = sto<BD>( qb >= 0 ? (v * mm) * (1 << qb) : (v * mm + (1 << (-qb - 1))) >> (-qb) );
+        }
+        idct4_residual<BD>( cc, r );
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+#pragma unroll
+            for( int x = 0; x < 4; x++ )
+                res[y][4 * k + x] = r[y][x];
+    }
+    const intptr_t px = 16 * mbx + 8 * half;
+    const typename PT<BD>::pixel *pp = pred + (intptr_t)f * pfs + (intptr_t)(16 * mby + 4 * by) * ps + px;
+    typename PT<BD>::pixel *rp = recon + (intptr_t)f * rfs + (intptr_t)(16 * mby + 4 * by) * rs + px;
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+    {
+        int v[8];
+        read_row<BD, 8>( pp + y * ps, v );
+#pragma unroll
+        for( int x = 0; x < 8; x++ )
+            v[x] = clip_pix<BD>( v[x] + res[y][x] );
+        write_row<BD, 8>( rp + y * rs, v );
+    }
+}
+
 template <int BD>
 hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, int mbw, int mbh, int nframes,
                             const int32_t *dmf, const int32_t *qp, const typename PT<BD>::pixel *pred, intptr_t ps,
@@ -876,6 +941,17 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
 {
     if( mbw <= 0 || mbh <= 0 || nframes <= 0 )
         return hipSuccess;
+    const char *ev = getenv( "X264HIP_RECON_VARIANT" );
+    // 8 bit: block pairs (0.55 vs 0.43 of HBM, tools/recon_variants.py); 10 bit: one lane
+    // per block is faster (0.68 vs 0.58); X264HIP_RECON_VARIANT = 0 / 1 forces either
+    const bool pair = ev ? atoi( ev ) != 1 : BD == 8;
+    if( transform == 4 && pair )
+    {
+        const int64_t waves = (int64_t)nframes * mbh * ((mbw + 7) / 8);
+        hipLaunchKernelGGL( mb_recon_pair_kernel<BD>, dim3( (unsigned)((waves + 3) / 4) ), dim3( 256 ), 0, st, dct,
+                            mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs, rfs );
+        return hipGetLastError();
+    }
     const int bpm = transform == 8 ? 4 : 16;
     const int64_t total = (int64_t)nframes * mbw * mbh * bpm;
     dim3 blk( 256 ), g( (unsigned)((total + 255) / 256) );
