@@ -19,8 +19,14 @@ def _host(t, bd):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("size", [(1920, 1088), (80, 48)])
-def test_hpel_filter(hip, oracle, bd, size):
+@pytest.mark.parametrize("size", [(1920, 1088), (80, 48), (176, 144)])
+@pytest.mark.parametrize("variant", ["default", "1"])
+def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
+    """X264HIP_HPEL_VARIANT: default = fused single pass, 1 = interior tiles + border expand."""
+    if variant == "default":
+        monkeypatch.delenv("X264HIP_HPEL_VARIANT", raising=False)
+    else:
+        monkeypatch.setenv("X264HIP_HPEL_VARIANT", variant)
     from x264hip import synth
     W, H = size
     gen = synth.make_sequence if W > 100 else synth.random_planes

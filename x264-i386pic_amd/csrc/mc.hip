@@ -6,6 +6,8 @@
 //    i.e. the candidate costs of refine_subpel (encoder/me.c:865-992).
 #include "hipcommon.h"
 
+#include <stdlib.h>
+
 namespace x264hip {
 
 // ------------------------------------------------------------ hpel filter
@@ -111,6 +113,150 @@ __global__ __launch_bounds__( 256 ) void hpel_expand_kernel( typename PT<BD>::pi
     dc[d] = dc[sidx];
 }
 
+// Fused variant (default): one pass over the whole padded plane.  A pixel of
+// the border takes the value the reference copies into it, i.e. the filter at
+// the clamped coordinate (x in [-4, W+3], y in [-8, H+7]); since the clamp is
+// monotonic, a 64x16 output tile needs at most a 76x21 source tile around its
+// clamped coordinates (plus alignment).  The source tile is fetched as aligned dwords, each
+// thread produces 4 horizontally adjacent pixels of each plane (dword stores
+// at 8 bit), and the expand pass with its read-back disappears.
+constexpr int HF_W = 64, HF_H = 16, HF_SW = 76, HF_SH = HF_H + 5;   // SW: 4..7 px of alignment + 64 + 2 + 3 halo
+
+// clip( v >> S ) to a pixel, written as a clamp before the shift.  The form
+// clip( v >> S ) packed into bytes is lowered by this ROCm's compiler to
+// v_ashr_pk_u8_i32, whose packed result came back with the high half not
+// cleared on the box (bytes 2-3 of every stored dword corrupted); the
+// clamp-first form computes the same value and avoids that lowering.
+template <int BD, int S>
+__device__ __forceinline__ int shr_clip( int v )
+{
+    constexpr int HI = (PT<BD>::PIXEL_MAX << S) | ((1 << S) - 1);
+    return (v < 0 ? 0 : v > HI ? HI : v) >> S;
+}
+
+template <int BD>
+__global__ __launch_bounds__( 256 ) void hpel_fused_kernel( const typename PT<BD>::pixel *__restrict__ src,
+                                                            typename PT<BD>::pixel *__restrict__ dh,
+                                                            typename PT<BD>::pixel *__restrict__ dv,
+                                                            typename PT<BD>::pixel *__restrict__ dc,
+                                                            intptr_t stride, intptr_t fstride, int width, int height )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int PPD = PT<BD>::PPD;
+    constexpr int pad = BD > 9 ? -10 * PT<BD>::PIXEL_MAX : 0;    // mc.c:176
+    __shared__ __align__( 16 ) int s_src[HF_SH][HF_SW];
+    __shared__ __align__( 16 ) int s_v[HF_H][HF_SW];
+    const int x0 = -32 + HF_W * blockIdx.x, y0 = -32 + HF_H * blockIdx.y;
+    const int cx0 = min( max( x0, -4 ), width + 3 ), cy0 = min( max( y0, -8 ), height + 7 );
+    const int sx0 = ((cx0 - 4) & ~3);                       // dword-aligned source origin (4 px)
+    const int sy0 = cy0 - 2;
+    const intptr_t fo = (intptr_t)blockIdx.z * fstride;
+    const pixel *s = src + fo;
+    // source tile: HF_SH rows x HF_SW pixels from aligned dwords, unpacked to
+    // ints with 16-byte LDS stores; columns past the right padding are never
+    // read by a written pixel and are not fetched
+    constexpr int QPR = HF_SW / 4;                           // 4-pixel groups per tile row
+    for( int i = threadIdx.x; i < HF_SH * QPR; i += 256 )
+    {
+        const int r = i / QPR, k = i % QPR;
+        const int col = sx0 + 4 * k;
+        uint32_t w[4 / PPD] = {};
+        if( col + 4 <= width + 32 )
+#pragma unroll
+            for( int q = 0; q < 4 / PPD; q++ )
+                w[q] = *(const uint32_t *)(s + (intptr_t)(sy0 + r) * stride + col + q * PPD);
+        int4 v;
+        v.x = upix<BD>( w[0], 0 );
+        v.y = upix<BD>( w[1 / PPD], 1 % PPD );
+        v.z = upix<BD>( w[2 / PPD], 2 % PPD );
+        v.w = upix<BD>( w[3 / PPD], 3 % PPD );
+        *(int4 *)&s_src[r][4 * k] = v;
+    }
+    __syncthreads();
+    // vertical 6-tap intermediates, four columns per thread
+    for( int i = threadIdx.x; i < HF_H * QPR; i += 256 )
+    {
+        const int r = i / QPR, c = 4 * (i % QPR);
+        int4 a[6];
+#pragma unroll
+        for( int k = 0; k < 6; k++ )
+            a[k] = *(const int4 *)&s_src[r + k][c];
+        int4 v;
+        v.x = tap6( a[0].x, a[1].x, a[2].x, a[3].x, a[4].x, a[5].x );
+        v.y = tap6( a[0].y, a[1].y, a[2].y, a[3].y, a[4].y, a[5].y );
+        v.z = tap6( a[0].z, a[1].z, a[2].z, a[3].z, a[4].z, a[5].z );
+        v.w = tap6( a[0].w, a[1].w, a[2].w, a[3].w, a[4].w, a[5].w );
+        *(int4 *)&s_v[r][c] = v;
+    }
+    __syncthreads();
+    const int ty = threadIdx.x >> 4, xq = (threadIdx.x & 15) * 4;
+    const int y = y0 + ty;
+    const int xs = x0 + xq;
+    if( y >= height + 32 || xs >= width + 32 )
+        return;
+    const int ry = min( max( y, -8 ), height + 7 ) - sy0 - 2;      // row of s_v / centre row of s_src is ry+2
+    int vh[4], vv[4], vc[4];
+    if( xs >= -4 && xs + 3 <= width + 3 )
+    {
+        // unclamped columns: the 12-value windows [c-4, c+8) of the two rows are aligned
+        const int c = xs - sx0;                                    // multiple of 4
+        int hs_[12], vs_[12];
+#pragma unroll
+        for( int k = 0; k < 3; k++ )
+        {
+            const int4 a = *(const int4 *)&s_src[ry + 2][c - 4 + 4 * k];
+            const int4 b = *(const int4 *)&s_v[ry][c - 4 + 4 * k];
+            hs_[4 * k] = a.x; hs_[4 * k + 1] = a.y; hs_[4 * k + 2] = a.z; hs_[4 * k + 3] = a.w;
+            vs_[4 * k] = b.x; vs_[4 * k + 1] = b.y; vs_[4 * k + 2] = b.z; vs_[4 * k + 3] = b.w;
+        }
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+        {
+            vv[j] = shr_clip<BD, 5>( vs_[4 + j] + 16 );
+            vh[j] = shr_clip<BD, 5>( tap6( hs_[j + 2], hs_[j + 3], hs_[j + 4], hs_[j + 5], hs_[j + 6], hs_[j + 7] ) + 16 );
+            int b[6];
+#pragma unroll
+            for( int q = 0; q < 6; q++ )
+                b[q] = (int16_t)(vs_[j + 2 + q] + pad);
+            vc[j] = shr_clip<BD, 10>( tap6( b[0], b[1], b[2], b[3], b[4], b[5] ) - 32 * pad + 512 );
+        }
+    }
+    else
+    {
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+        {
+            const int cxl = min( max( xs + j, -4 ), width + 3 ) - sx0;   // column of the pixel in the tile
+            vv[j] = shr_clip<BD, 5>( s_v[ry][cxl] + 16 );
+            const int hs = tap6( s_src[ry + 2][cxl - 2], s_src[ry + 2][cxl - 1], s_src[ry + 2][cxl],
+                                 s_src[ry + 2][cxl + 1], s_src[ry + 2][cxl + 2], s_src[ry + 2][cxl + 3] );
+            vh[j] = shr_clip<BD, 5>( hs + 16 );
+            int b[6];
+#pragma unroll
+            for( int q = 0; q < 6; q++ )
+                b[q] = (int16_t)(s_v[ry][cxl - 2 + q] + pad);
+            vc[j] = shr_clip<BD, 10>( tap6( b[0], b[1], b[2], b[3], b[4], b[5] ) - 32 * pad + 512 );
+        }
+    }
+    const intptr_t o = fo + (intptr_t)y * stride + xs;
+#pragma unroll
+    for( int k = 0; k < 4 / PPD; k++ )
+    {
+        uint32_t wh = 0, wv = 0, wc = 0;
+#pragma unroll
+        for( int j = 0; j < PPD; j++ )
+        {
+            const int sh = j * (32 / PPD);
+            wh |= (uint32_t)vh[k * PPD + j] << sh;
+            wv |= (uint32_t)vv[k * PPD + j] << sh;
+            wc |= (uint32_t)vc[k * PPD + j] << sh;
+        }
+        *(uint32_t *)(dh + o + k * PPD) = wh;
+        *(uint32_t *)(dv + o + k * PPD) = wv;
+        *(uint32_t *)(dc + o + k * PPD) = wc;
+    }
+}
+
 template <int BD>
 hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD>::pixel *dh,
                                typename PT<BD>::pixel *dv, typename PT<BD>::pixel *dc, intptr_t stride,
@@ -118,6 +264,15 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
 {
     if( nframes <= 0 || width <= 0 || height <= 0 )
         return hipSuccess;
+    const char *ev = getenv( "X264HIP_HPEL_VARIANT" );
+    if( !ev || atoi( ev ) != 1 )
+    {
+        // fused single pass; needs 4-pixel aligned rows (width + 64 covered by whole tiles of 4)
+        dim3 g( (width + 64 + HF_W - 1) / HF_W, (height + 64 + HF_H - 1) / HF_H, nframes );
+        hipLaunchKernelGGL( ( hpel_fused_kernel<BD> ), g, dim3( 256 ), 0, stream, src, dh, dv, dc, stride, fstride,
+                            width, height );
+        return hipGetLastError();
+    }
     dim3 g1( (width + 8 + HT_W - 1) / HT_W, (height + 16 + HT_H - 1) / HT_H, nframes );
     hipLaunchKernelGGL( ( hpel_interior_kernel<BD> ), g1, dim3( 256 ), 0, stream, src, dh, dv, dc, stride, fstride,
                         width, height );
