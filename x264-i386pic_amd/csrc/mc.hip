@@ -442,23 +442,56 @@ __global__ __launch_bounds__( 256 ) void lowres_kernel( const typename PT<BD>::p
     const pixel *r1 = s + (intptr_t)min( 2 * yc + 1, height - 1 ) * stride;
     const pixel *r2 = s + (intptr_t)min( 2 * yc + 2, height - 1 ) * stride;
     uint32_t w0 = 0, wh = 0, wv = 0, wc = 0;
-#pragma unroll
-    for( int j = 0; j < PPD; j++ )
-    {
-        const int x = g * PPD + j - PAD;
-        const int xc = min( max( x, 0 ), wl - 1 );
-        const int c0 = 2 * xc, c1 = min( 2 * xc + 1, width - 1 ), c2 = min( 2 * xc + 2, width - 1 );
-        const int a0 = r0[c0], a1 = r0[c1], a2 = r0[c2];
-        const int b0 = r1[c0], b1 = r1[c1], b2 = r1[c2];
-        const int e0 = r2[c0], e1 = r2[c1], e2 = r2[c2];
 #define FILTER( a, b, c, d ) ((((a + b + 1) >> 1) + ((c + d + 1) >> 1) + 1) >> 1)
-        const int sh = j * (32 / PPD);
-        w0 |= (uint32_t)FILTER( a0, b0, a1, b1 ) << sh;
-        wh |= (uint32_t)FILTER( a1, b1, a2, b2 ) << sh;
-        wv |= (uint32_t)FILTER( b0, e0, b1, e1 ) << sh;
-        wc |= (uint32_t)FILTER( b1, e1, b2, e2 ) << sh;
-#undef FILTER
+    const int xg = g * PPD - PAD;                            // first output column of the lane
+    if( xg >= 0 && xg + PPD <= wl - 1 && 2 * yc + 2 <= height - 1 )
+    {
+        // unclamped: source columns 2*xg .. 2*xg + 2*PPD as aligned dwords of three rows
+        constexpr int ND = 2 * PPD / PPD + 1;                // dwords covering 2*PPD + 1 pixels
+        uint32_t q0[ND], q1[ND], q2[ND];
+#pragma unroll
+        for( int k = 0; k < ND; k++ )
+        {
+            q0[k] = ((const uint32_t *)(r0 + 2 * xg))[k];
+            q1[k] = ((const uint32_t *)(r1 + 2 * xg))[k];
+            q2[k] = ((const uint32_t *)(r2 + 2 * xg))[k];
+        }
+#pragma unroll
+        for( int j = 0; j < PPD; j++ )
+        {
+            const int i0 = 2 * j, i1 = 2 * j + 1, i2 = 2 * j + 2;
+            const int a0 = upix<BD>( q0[i0 / PPD], i0 % PPD ), a1 = upix<BD>( q0[i1 / PPD], i1 % PPD ),
+                      a2 = upix<BD>( q0[i2 / PPD], i2 % PPD );
+            const int b0 = upix<BD>( q1[i0 / PPD], i0 % PPD ), b1 = upix<BD>( q1[i1 / PPD], i1 % PPD ),
+                      b2 = upix<BD>( q1[i2 / PPD], i2 % PPD );
+            const int e0 = upix<BD>( q2[i0 / PPD], i0 % PPD ), e1 = upix<BD>( q2[i1 / PPD], i1 % PPD ),
+                      e2 = upix<BD>( q2[i2 / PPD], i2 % PPD );
+            const int sh = j * (32 / PPD);
+            w0 |= (uint32_t)FILTER( a0, b0, a1, b1 ) << sh;
+            wh |= (uint32_t)FILTER( a1, b1, a2, b2 ) << sh;
+            wv |= (uint32_t)FILTER( b0, e0, b1, e1 ) << sh;
+            wc |= (uint32_t)FILTER( b1, e1, b2, e2 ) << sh;
+        }
     }
+    else
+    {
+#pragma unroll
+        for( int j = 0; j < PPD; j++ )
+        {
+            const int x = xg + j;
+            const int xc = min( max( x, 0 ), wl - 1 );
+            const int c0 = 2 * xc, c1 = min( 2 * xc + 1, width - 1 ), c2 = min( 2 * xc + 2, width - 1 );
+            const int a0 = r0[c0], a1 = r0[c1], a2 = r0[c2];
+            const int b0 = r1[c0], b1 = r1[c1], b2 = r1[c2];
+            const int e0 = r2[c0], e1 = r2[c1], e2 = r2[c2];
+            const int sh = j * (32 / PPD);
+            w0 |= (uint32_t)FILTER( a0, b0, a1, b1 ) << sh;
+            wh |= (uint32_t)FILTER( a1, b1, a2, b2 ) << sh;
+            wv |= (uint32_t)FILTER( b0, e0, b1, e1 ) << sh;
+            wc |= (uint32_t)FILTER( b1, e1, b2, e2 ) << sh;
+        }
+    }
+#undef FILTER
     const intptr_t o = f * dfs + (intptr_t)y * ds + g * PPD - PAD;
     *(uint32_t *)(d0 + o) = w0;
     *(uint32_t *)(dh + o) = wh;
