@@ -43,7 +43,13 @@ def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("op", [0, 2])
-def test_subpel_cmp_random(hip, oracle, bd, op):
+@pytest.mark.parametrize("variant", ["default", "2"])
+def test_subpel_cmp_random(hip, oracle, bd, op, variant, monkeypatch):
+    """X264HIP_SUBPEL_VARIANT: default = lane per candidate, 2 = row-per-lane SATD for 8/16-wide blocks."""
+    if variant == "default":
+        monkeypatch.delenv("X264HIP_SUBPEL_VARIANT", raising=False)
+    else:
+        monkeypatch.setenv("X264HIP_SUBPEL_VARIANT", variant)
     from x264hip import synth
     W, H = 160, 96
     planes, stride, origin = synth.random_planes(2, W, H, bd, seed=11)

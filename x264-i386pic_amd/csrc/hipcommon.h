@@ -70,6 +70,56 @@ template <> __device__ __forceinline__ uint32_t sadp<10>( uint32_t a, uint32_t b
     return __builtin_amdgcn_sad_u16( a, b, acc );
 }
 
+// SATD of an 8x4 band as two 4x4 Hadamards in packed 16-bit lanes (the
+// reference's satd_8x4 "two tiles in one sum2_t" trick of pixel.c:290-309, done
+// with v_pk_add/sub_i16): pair x = (column x, column x+4) of each row.  Returns
+// sum |coef| of both tiles (even, the caller halves it once).  Differences and
+// all Hadamard stages fit int16 for 8 and 10 bit (|coef| <= 16 * 1023).
+typedef short x264hip_short2 __attribute__( ( ext_vector_type( 2 ) ) );
+template <int BD>
+__device__ __forceinline__ x264hip_short2 pair_px( const uint32_t (&r)[8 / PT<BD>::PPD], int x )
+{
+    uint32_t v;
+    if constexpr( BD == 8 )   // bytes x of r[0] and r[1] -> 16-bit lanes
+        v = __builtin_amdgcn_perm( r[1], r[0], (uint32_t)x | 0x0c00u | ((uint32_t)(4 + x) << 16) | 0x0c000000u );
+    else                      // 16-bit pixel x of r[0..1] and pixel x of r[2..3]
+        v = __builtin_amdgcn_perm( r[2 + (x >> 1)], r[x >> 1], (x & 1) ? 0x07060302u : 0x05040100u );
+    return __builtin_bit_cast( x264hip_short2, v );
+}
+
+template <int BD>
+__device__ __forceinline__ uint32_t satd8x4_packed( const uint32_t (&a)[4][8 / PT<BD>::PPD],
+                                                    const uint32_t (&b)[4][8 / PT<BD>::PPD] )
+{
+    x264hip_short2 d[4][4];
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+    {
+        x264hip_short2 p[4];
+#pragma unroll
+        for( int x = 0; x < 4; x++ )
+            p[x] = pair_px<BD>( a[y], x ) - pair_px<BD>( b[y], x );
+        const x264hip_short2 t0 = p[0] + p[1], t1 = p[0] - p[1], t2 = p[2] + p[3], t3 = p[2] - p[3];
+        d[y][0] = t0 + t2; d[y][2] = t0 - t2; d[y][1] = t1 + t3; d[y][3] = t1 - t3;
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for( int x = 0; x < 4; x++ )
+    {
+        const x264hip_short2 t0 = d[0][x] + d[1][x], t1 = d[0][x] - d[1][x];
+        const x264hip_short2 t2 = d[2][x] + d[3][x], t3 = d[2][x] - d[3][x];
+        const x264hip_short2 c[4] = { t0 + t2, t0 - t2, t1 + t3, t1 - t3 };
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            const x264hip_short2 m = __builtin_elementwise_max( c[k], (x264hip_short2)0 - c[k] );
+            s = __builtin_amdgcn_udot2( __builtin_bit_cast( unsigned short __attribute__( ( ext_vector_type( 2 ) ) ), m ),
+                                        (unsigned short __attribute__( ( ext_vector_type( 2 ) ) ))1, s, false );
+        }
+    }
+    return s;
+}
+
 // value stored to a dctcoef (int16 wrap at 8 bit), read back as int
 template <int BD> __device__ __forceinline__ int sto( int v ) { return (int)(typename PT<BD>::dctcoef)v; }
 

@@ -314,10 +314,12 @@ __global__ __launch_bounds__( 256 ) void subpel_cmp_kernel( const typename PT<BD
     const int qx = qxy[2 * i], qy = qxy[2 * i + 1];
     const int idx = ((qy & 3) << 2) + (qx & 3);
     const intptr_t off = (intptr_t)(qy >> 2) * rs + (qx >> 2);
-    const pixel *planes[4] = { p0, p1, p2, p3 };
-    const pixel *s1 = planes[c_hpel_ref0[idx]] + off + ((qy & 3) == 3) * rs;
+    // plane selection by value keeps the pointers in the global address space
+    // (an indexed local array of pointers would turn every load into a flat load)
+    const int i0 = c_hpel_ref0[idx], i1 = c_hpel_ref1[idx];
+    const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((qy & 3) == 3) * rs;
     const bool two = idx & 5;
-    const pixel *s2 = planes[c_hpel_ref1[idx]] + off + ((qx & 3) == 3);
+    const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((qx & 3) == 3);
     const pixel *a = fenc + fenc_off[i];
     int sum = 0;
     uint32_t acc = 0;
@@ -347,6 +349,24 @@ __global__ __launch_bounds__( 256 ) void subpel_cmp_kernel( const typename PT<BD
 #pragma unroll
                 for( int k = 0; k < NDW; k++ )
                     acc = sadp<BD>( fr[y][k], rr[y][k], acc );
+        }
+        else if constexpr( W >= 8 )
+        {
+            // SATD in 8x4 packed pairs; every tile sum is even, so one final >> 1
+#pragma unroll
+            for( int tx = 0; tx < W; tx += 8 )
+            {
+                uint32_t fa[4][8 / PT<BD>::PPD], ra[4][8 / PT<BD>::PPD];
+#pragma unroll
+                for( int y = 0; y < 4; y++ )
+#pragma unroll
+                    for( int k = 0; k < 8 / PT<BD>::PPD; k++ )
+                    {
+                        fa[y][k] = fr[y][tx / PT<BD>::PPD + k];
+                        ra[y][k] = rr[y][tx / PT<BD>::PPD + k];
+                    }
+                acc += satd8x4_packed<BD>( fa, ra );
+            }
         }
         else
         {
@@ -381,7 +401,99 @@ __global__ __launch_bounds__( 256 ) void subpel_cmp_kernel( const typename PT<BD
     }
     if constexpr( OP == 0 )
         sum = (int)acc;
+    else if constexpr( W >= 8 )
+        sum = (int)(acc >> 1);
     scores[i] = sum;
+}
+
+// Variant 2: SATD candidates with one lane per block row (W 8 / 16, H 8 / 16): the H lanes
+// of a candidate hold its rows, so a wave's row loads of horizontally adjacent
+// candidates (the usual list order: consecutive blocks at one qpel phase) touch
+// few cache lines; the horizontal 4-point Hadamards run in packed 16-bit pairs
+// inside the lane, the vertical ones are DPP quad butterflies across the four
+// lanes of a 4-row band.  Same result as the per-lane kernel (sum of |coef| is
+// invariant to the coefficient order).
+template <int BD>
+__device__ __forceinline__ x264hip_short2 dpp_quad( x264hip_short2 v, int ctrl_sel )
+{
+    const int iv = __builtin_bit_cast( int, v );
+    const int r = ctrl_sel == 0 ? __builtin_amdgcn_update_dpp( 0, iv, 0xB1, 0xF, 0xF, false )    // lane ^ 1
+                                : __builtin_amdgcn_update_dpp( 0, iv, 0x4E, 0xF, 0xF, false );   // lane ^ 2
+    return __builtin_bit_cast( x264hip_short2, r );
+}
+
+template <int BD, int IPIX>
+__global__ __launch_bounds__( 256 ) void subpel_satd_rows_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                                  intptr_t fs, const typename PT<BD>::pixel *p0,
+                                                                  const typename PT<BD>::pixel *p1,
+                                                                  const typename PT<BD>::pixel *p2,
+                                                                  const typename PT<BD>::pixel *p3, intptr_t rs,
+                                                                  const int64_t *__restrict__ fenc_off,
+                                                                  const int32_t *__restrict__ qxy, int n,
+                                                                  int32_t *__restrict__ scores )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    constexpr int NDW = W / PT<BD>::PPD;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = t / H;
+    const int r = (int)(t % H);
+    if( i >= n )
+        return;                                   // whole candidates only (H divides 64)
+    const int qx = qxy[2 * i], qy = qxy[2 * i + 1];
+    const int idx = ((qy & 3) << 2) + (qx & 3);
+    const intptr_t off = (intptr_t)(qy >> 2) * rs + (qx >> 2) + (intptr_t)r * rs;
+    const int i0 = c_hpel_ref0[idx], i1 = c_hpel_ref1[idx];
+    const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((qy & 3) == 3) * rs;
+    const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((qx & 3) == 3);
+    uint32_t fr[NDW], rr[NDW];
+    load_packed<NDW>( fenc + fenc_off[i] + (intptr_t)r * fs, fr );
+    load_packed<NDW>( s1, rr );
+    if( idx & 5 )
+    {
+        uint32_t tt[NDW];
+        load_packed<NDW>( s2, tt );
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            rr[k] = avg_packed<BD>( rr[k], tt[k] );
+    }
+    uint32_t acc = 0;
+#pragma unroll
+    for( int tx = 0; tx < W; tx += 8 )
+    {
+        uint32_t fa[8 / PT<BD>::PPD], ra[8 / PT<BD>::PPD];
+#pragma unroll
+        for( int k = 0; k < 8 / PT<BD>::PPD; k++ )
+        {
+            fa[k] = fr[tx / PT<BD>::PPD + k];
+            ra[k] = rr[tx / PT<BD>::PPD + k];
+        }
+        x264hip_short2 p[4];
+#pragma unroll
+        for( int x = 0; x < 4; x++ )
+            p[x] = pair_px<BD>( fa, x ) - pair_px<BD>( ra, x );
+        const x264hip_short2 t0 = p[0] + p[1], t1 = p[0] - p[1], t2 = p[2] + p[3], t3 = p[2] - p[3];
+        x264hip_short2 h[4] = { t0 + t2, t0 - t2, t1 + t3, t1 - t3 };
+        // vertical butterflies over the quad of rows: stage 1 lanes (0,1), stage 2 lanes (0,2)
+        const bool odd = r & 1, hi2 = r & 2;
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            x264hip_short2 o = dpp_quad<BD>( h[k], 0 );
+            h[k] = odd ? o - h[k] : h[k] + o;
+            o = dpp_quad<BD>( h[k], 1 );
+            h[k] = hi2 ? o - h[k] : h[k] + o;
+            const x264hip_short2 m = __builtin_elementwise_max( h[k], (x264hip_short2)0 - h[k] );
+            acc = __builtin_amdgcn_udot2( __builtin_bit_cast( unsigned short __attribute__( ( ext_vector_type( 2 ) ) ), m ),
+                                          (unsigned short __attribute__( ( ext_vector_type( 2 ) ) ))1, acc, false );
+        }
+    }
+    // sum over the candidate's H lanes
+#pragma unroll
+    for( int m = 1; m < H; m <<= 1 )
+        acc += (uint32_t)__shfl_xor( (int)acc, m, H );
+    if( r == 0 )
+        scores[i] = (int)(acc >> 1);
 }
 
 template <int BD>
@@ -391,6 +503,19 @@ hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel 
 {
     if( n <= 0 )
         return hipSuccess;
+    const char *ev = getenv( "X264HIP_SUBPEL_VARIANT" );
+    // variant 2: one lane per block row (slower on the bench list: 0.25 vs 0.13 ms for
+    // 4.7 M 8x8 candidates, the per-candidate set-up is repeated in every row lane)
+    if( op == 2 && i_pixel <= 3 && ev && atoi( ev ) == 2 )
+    {
+        const int h = pix_h( i_pixel );
+        const int64_t lanes = (int64_t)n * h;
+        dim3 g( (unsigned)((lanes + 255) / 256) );
+#define SR_CASE( I )                                                                                              case I: hipLaunchKernelGGL( ( subpel_satd_rows_kernel<BD, I> ), g, dim3( 256 ), 0, stream, fenc, fs,                                      planes[0], planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores ); break;
+        switch( i_pixel ) { SR_CASE( 0 ) SR_CASE( 1 ) SR_CASE( 2 ) SR_CASE( 3 ) }
+#undef SR_CASE
+        return hipGetLastError();
+    }
     dim3 blk( 256 ), g( (n + 255) / 256 );
 #define SP_CASE( OP, I )                                                                                      \
     case I: hipLaunchKernelGGL( ( subpel_cmp_kernel<BD, OP, I> ), g, blk, 0, stream, fenc, fs, planes[0],       \
