@@ -180,7 +180,26 @@ __global__ __launch_bounds__( 256 ) void cmp_batch_kernel( const typename PT<BD>
                 sum += sa8d8x8<BD>( a + y * fs + x, fs, b + y * rs + x, rs );
         sum = (sum + 2) >> 2;
     }
-    else                             // SATD
+    else if constexpr( W >= 8 )      // SATD, 8x4 bands in packed 16-bit pairs (one >> 1 at the end)
+    {
+        uint32_t acc = 0;
+#pragma unroll
+        for( int y = 0; y < H; y += 4 )
+#pragma unroll
+            for( int x = 0; x < W; x += 8 )
+            {
+                uint32_t ra[4][8 / PT<BD>::PPD], rb[4][8 / PT<BD>::PPD];
+#pragma unroll
+                for( int k = 0; k < 4; k++ )
+                {
+                    load_packed<8 / PT<BD>::PPD>( a + (y + k) * fs + x, ra[k] );
+                    load_packed<8 / PT<BD>::PPD>( b + (y + k) * rs + x, rb[k] );
+                }
+                acc += satd8x4_packed<BD>( ra, rb );
+            }
+        sum = (int)(acc >> 1);
+    }
+    else                             // SATD, 4-wide blocks
     {
 #pragma unroll
         for( int y = 0; y < H; y += 4 )
