@@ -127,6 +127,96 @@ def compute(bd):
                               q8m[1, qp], q8b[1, qp])
     out["mb_dct4_quant"], out["mb_dct4_nz"] = d4, n4
     out["mb_dct8_quant"], out["mb_dct8_nz"] = d8, n8
+    out.update(compute_ext(bd, planes, stride, origin, d4, d8))
+    return out
+
+
+def compute_ext(bd, planes, stride, origin, d4, d8):
+    """Fixtures of the further pixel entries, the inverse path and the lookahead /
+    motion-compensation inputs (§8f), cross-checked against numpy where a
+    restatement exists (tests/test_cpu_pixel_ext.py, test_cpu_inverse.py)."""
+    out = {}
+    b = cb.Bufs(bd)
+    b.fill_pixel_overflow()
+    p1 = b.pbuf1
+    # sa8d / sa8d_satd (TEST_PIXEL inputs), hadamard_ac, var, var2
+    sa = np.zeros((2, 80), np.int64)
+    ss = np.zeros(80, np.uint64)
+    for k, i in enumerate((0, 3)):
+        w, h = nr.SIZES[i]
+        for j in range(64):
+            s1 = 32 if (j & 31) == 31 else 16
+            sa[k, j] = orc.sa8d(bd, i, p1, 0, s1, p1, b.pbuf2_off + j, 64)
+            assert sa[k, j] == nr.sa8d(nr.block(p1, 0, s1, w, h), nr.block(p1, b.pbuf2_off + j, 64, w, h))
+        for t, j in enumerate(range(0, 0x1000, 256)):
+            sa[k, 64 + t] = orc.sa8d(bd, i, b.pbuf3, j, 16, b.pbuf4, j, 16)
+    for j in range(64):
+        ss[j] = orc.sa8d_satd(bd, p1, 0, 16, p1, b.pbuf2_off + j, 64)
+    for t, j in enumerate(range(0, 0x1000, 256)):
+        ss[64 + t] = orc.sa8d_satd(bd, b.pbuf3, j, 16, b.pbuf4, j, 16)
+    out["sa8d"], out["sa8d_satd"] = sa, ss
+    hac = np.zeros((4, 32), np.uint64)
+    for i in range(4):
+        w, h = nr.SIZES[i]
+        for j in range(32):
+            buf = p1 if j & 16 else b.pbuf3
+            off = (j & 15) * 256
+            if off + 16 * (h - 1) + w <= buf.size:
+                hac[i, j] = orc.hadamard_ac(bd, i, buf, off, 16)
+                assert hac[i, j] == nr.hadamard_ac(nr.block(buf, off, 16, w, h))
+    out["hadamard_ac"] = hac
+    out["var"] = np.array([[orc.var(bd, i, buf, off, 16) for buf, off in ((p1, 0), (p1, 77), (b.pbuf3, 256))]
+                           for i in (0, 2, 3)], np.uint64)
+    out["var2"] = np.array([orc.var2(bd, i, p1, fo, p1, do) for i in (2, 3)
+                            for fo, do in ((0, b.pbuf2_off), (64, b.pbuf2_off + 5))], np.int64)
+    # ads over the checkasm distributions (glibc rand, seed 4321)
+    pm = (1 << bd) - 1
+    cb.srand(4321)
+    cost = np.array([cb.rand30() & 0xFFFF for _ in range(32)], np.uint16)
+    ads = np.full((100, 29), -1, np.int16)
+    for i in range(100):
+        ns = (4, 2, 2, 1)[i & 3]
+        thresh = (cb.rand() % 257) * pm + (cb.rand30() & 0xFFFF)
+        if i < 40:
+            sums = np.array([(cb.rand() % 9) * 8 * pm for _ in range(72)], np.int64).astype(np.uint16)
+            dc = np.array([(cb.rand() % 9) * 8 * pm for _ in range(4)], np.int32)
+        else:
+            r = cb.rand30 if bd + 6 > 15 else cb.rand
+            sums = np.array([r() & ((1 << (bd + 6)) - 1) for _ in range(72)], np.uint16)
+            dc = np.array([r() & ((1 << (bd + 6)) - 1) for _ in range(4)], np.int32)
+        mv = orc.ads(bd, ns, dc, sums, 0, 32, cost, 0, 28, thresh)
+        ads[i, 0] = len(mv)
+        ads[i, 1:1 + len(mv)] = mv
+    out["ads"] = ads
+    # inverse path on the forward fixtures above: dequant at qp 26 (flat lists) and
+    # reconstruction of the 64x48 pair; coefficient statistics / scans of the MB coefs
+    dq4, dq8 = orc.cqm_dequant([cb.FLAT16] * 8)
+    qp = 26 + 6 * (bd - 8)
+    nmb = d4.shape[0]
+    qpm = np.full(nmb, qp, np.int32)
+    for t, d, dq in ((4, d4, dq4[1]), (8, d8, dq8[1])):
+        rec = np.zeros_like(planes[0]).ravel()
+        orc.mb_dequant_idct_add(bd, t, d, 4, 3, dq, qpm, planes[0].ravel(), origin, stride, rec, origin, stride)
+        out[f"recon{t}"] = rec.reshape(planes[0].shape)[32:32 + 48, 32:32 + 64].copy()
+    blocks = d4.reshape(-1, 16)
+    out["decimate16"] = np.array([orc.inplace(bd, "decimate_score16", x)[1] for x in blocks], np.int32)
+    out["coeff_last16"] = np.array([orc.fn(bd, "coeff_last")(orc._addr(np.ascontiguousarray(x)), 16) for x in blocks],
+                                   np.int32)
+    out["zigzag4_frame"] = np.stack([orc.zigzag_scan(bd, 16, 0, x) for x in blocks])
+    out["zigzag8_field"] = np.stack([orc.zigzag_scan(bd, 64, 1, x) for x in d8.reshape(-1, 64)])
+    rs = np.random.default_rng(99)
+    c16 = rs.integers(-(1 << (bd + 1)), 1 << (bd + 1), (12, 16))
+    out["dequant4"] = np.stack([orc.inplace(bd, "dequant_4x4", c16[q % 12], orc._addr(dq4[0]), q)[0]
+                                for q in range(0, 52 + 6 * (bd - 8), 4)])
+    # motion-compensation / lookahead inputs on the same synthetic frame
+    hp = orc.frame_filter(bd, planes[0].ravel().copy(), origin, stride, 64, 48)
+    out["hpel"] = np.stack([x.reshape(planes[0].shape) for x in hp])
+    ls = (32 + 64 + 63) // 64 * 64
+    out["lowres"] = np.stack(orc.frame_init_lowres(bd, planes[0].ravel(), origin, stride, 64, 48, ls))
+    integ = orc.frame_integral(bd, planes[0].ravel(), origin, stride, 48, 32, 1)
+    out["integral"] = integ
+    box = nr.box_sums(planes[0].astype(np.int64), 8)
+    assert np.array_equal(integ[1:48 + 56, :stride - 8], box[1:48 + 56, :stride - 8])
     return out
 
 
