@@ -268,6 +268,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     res["satd8x8_candidates_per_launch"] = int(fo.numel())
     del nb8, hv, ref_planes, fo, qxy, sc
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
+    res.update(rates_2160p(x, a, world))
     return res
 
 
@@ -306,6 +307,76 @@ def rates_10bit(x, a, world, mbw, mbh, F):
     res["dct8_quant10_blocks_per_s"] = world * a.steps * blocks / wall
     res["dct8_quant10_hbm_frac"] = blocks * (128 + 128 + 256) / (ev_ms * 1e-3) / HBM_PEAK
     res["dct8_quant10_launch_ms"] = ev_ms
+    return res
+
+
+def rates_2160p(x, a, world):
+    """configs[3] per GPU (frame-per-GPU across the node): 2160p, full search range 16
+    + fused 4x4 DCT+quant of each new frame against its predecessor.  Two rates:
+    frames resident in HBM, and the streaming form where every new frame is uploaded
+    from pinned host memory (the reference frame is the previous upload, already on
+    the device) on a copy stream overlapped with the previous frame's kernels."""
+    from x264hip import synth, dist as xd
+    W, H, R = 3840, 2176, a.range                     # 2160 padded to whole MBs
+    mbw, mbh = W // 16, H // 16
+    nf = 8
+    p0, _ = xd.frame_shard(world * nf, world, int(os.environ.get("RANK", "0")))
+    planes, stride, origin = synth.make_sequence(nf + 1, W, H, 8, start=p0)
+    fsz = planes[0].size
+    host = torch.from_numpy(planes).pin_memory()
+    ring = torch.empty((3,) + planes.shape[1:], dtype=torch.uint8, device="cuda")
+    table = torch.empty((1, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
+    flat = [16] * 64
+    q4m, q4b, _, _ = x.cqm_init(8, [flat] * 8)
+    mf4 = torch.from_numpy(q4m[1, 26].copy()).cuda()
+    bs4 = torch.from_numpy(q4b[1, 26].copy()).cuda()
+    dct = torch.empty((mbw * mbh, 256), dtype=torch.int16, device="cuda")
+    nz = torch.empty(mbw * mbh, dtype=torch.int32, device="cuda")
+    dev_all = host.cuda()
+    cand = mbw * mbh * (2 * R + 1) ** 2
+
+    def work(cur, ref, c_fs=fsz, r_fs=fsz):
+        x.me_search_full(cur, origin, stride, ref, origin, stride, mbw, mbh, 1, R, table=table,
+                         fenc_frame_stride=c_fs, ref_frame_stride=r_fs)
+        x.mb_dct_quant(4, cur, origin, stride, ref, origin, stride, mbw, mbh, 1, mf4, bs4, dct=dct, nz=nz,
+                       fenc_frame_stride=c_fs, pred_frame_stride=r_fs)
+
+    k = [0]
+
+    def resident():
+        i = k[0] % nf
+        work(dev_all[i + 1:i + 2], dev_all[i:i + 1])
+        k[0] += 1
+    wall, ev_ms = timed(resident, a.steps, min(a.warmup, 50), world)
+    res = {"2160p_resident_candidates_per_s": world * a.steps * cand / wall,
+           "2160p_resident_frame_ms": wall / a.steps * 1e3}
+    copy = torch.cuda.Stream()
+    done = [torch.cuda.Event() for _ in range(3)]
+    ready = [torch.cuda.Event() for _ in range(3)]
+    ring[0].copy_(host[0])
+    ready[0].record()
+    state = {"n": 0}
+
+    def streaming():
+        n = state["n"]
+        cur, ref = (n + 1) % 3, n % 3
+        with torch.cuda.stream(copy):                 # upload frame n+1 while frame n-1's kernels may still run
+            copy.wait_event(done[cur])
+            ring[cur].copy_(host[(n + 1) % (nf + 1)], non_blocking=True)
+            ready[cur].record(copy)
+        torch.cuda.current_stream().wait_event(ready[cur])
+        torch.cuda.current_stream().wait_event(ready[ref])
+        work(ring[cur:cur + 1], ring[ref:ref + 1], c_fs=0, r_fs=0)
+        done[ref].record()
+        state["n"] = n + 1
+    for ev in done:
+        ev.record()
+    wall, _ = timed(streaming, a.steps, min(a.warmup, 50), world)
+    torch.cuda.synchronize()
+    res["2160p_pcie_inclusive_candidates_per_s"] = world * a.steps * cand / wall
+    res["2160p_pcie_inclusive_frame_ms"] = wall / a.steps * 1e3
+    res["2160p_upload_bytes_per_frame"] = int(fsz)
+    del dev_all, ring, table, host
     return res
 
 
