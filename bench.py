@@ -60,8 +60,15 @@ def dist_setup():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # one rank per GPU; X264HIP_DIST_BACKEND=gloo lets several ranks share one GPU
+        # to exercise the N > 1 path functionally on a single-GPU box (not a measurement)
+        backend = os.environ.get("X264HIP_DIST_BACKEND", "nccl")
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, local
