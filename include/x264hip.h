@@ -401,6 +401,30 @@ int x264hip_##BD##_me_search_full( const pixel *fenc, intptr_t fenc_stride,     
                                    int mb_width, int mb_height, int n_frames, int range,        \
                                    sadt *table, void *stream );                                 \
                                                                                                 \
+/* full search around a per-MB centre (me.c centres its ESA window on the best                   \
+ * predictor, encoder/me.c:618-624): centre[2*mb..] = (cx, cy) full-pel, MBs in frame-major     \
+ * raster order.  The window origin (cx - range, cy - range) is clamped so every fetched        \
+ * pixel stays inside the 32-pixel padding (PADH = PADV = 32, frame.h:32-33) and aligned        \
+ * down to 4 (8 bit) / 2 (10 bit) pixels; origin[2*mb..] receives it (mv of table column 0      \
+ * and row 0).  table[mb][j][i] = SAD at mv (origin + (i, j)), i, j < 2*range+1, same layout    \
+ * as me_search_full (which is this entry with every centre (0, 0)). */                         \
+int x264hip_##BD##_me_search_centred( const pixel *fenc, intptr_t fenc_stride,                  \
+                                      intptr_t fenc_frame_stride,                               \
+                                      const pixel *ref, intptr_t ref_stride,                    \
+                                      intptr_t ref_frame_stride,                                \
+                                      int mb_width, int mb_height, int n_frames, int range,     \
+                                      const int16_t *centre, sadt *table, int16_t *origin,      \
+                                      void *stream );                                           \
+                                                                                                \
+/* me_esa_argmin over a me_search_centred table: origin[2*i..] as written by it.                \
+ * Window candidates outside the table's (2*range+1)^2 square are not evaluated, so             \
+ * to reproduce me.c's rounded window (up to 3 columns past bmx + me_range) around a            \
+ * centre (bmx, bmy) pick range >= me_range + 6 (8 bit; + 4 at 10 bit: alignment). */          \
+int x264hip_##BD##_me_esa_argmin_at( const sadt *table, int range, int n, int me_range,         \
+                                     const int16_t *origin, const int16_t *par,                 \
+                                     const int32_t *init_cost, const uint16_t *cost_mv,         \
+                                     int32_t *out, void *stream );                              \
+                                                                                                \
 /* integer-pel ESA decision per macroblock over a me_search_full table (reference            \
  * encoder/me.c:618-631, the plain exhaustive form its ads path :632-771 reproduces):           \
  * par[8*i] = { bmx, bmy (fullpel centre = best predictor), mvp_x, mvp_y (qpel),                \

@@ -1295,6 +1295,43 @@ void FN(me_search_full)( const pixel *fenc, intptr_t fs, const pixel *ref, intpt
         }
 }
 
+/* window origin of x264hip_*_me_search_centred for one MB: (cx, cy) - range,
+ * clamped so every pixel the kernels fetch lies in the 32-pixel padded plane,
+ * then aligned down to 4 (8 bit) / 2 (10 bit) pixels; returned relative to the MB */
+static void me_window( int mbx, int mby, int mb_width, int mb_height, int range, int cx, int cy, int *ox, int *oy )
+{
+    const int P = (2*range + 1 + 3) & ~3, al = BIT_DEPTH == 8 ? 4 : 2;
+    int ax = 16*mbx + cx - range, ay = 16*mby + cy - range;
+    int hx = 16*mb_width + 12 - P, hy = 16*mb_height + 16 - 2*range;
+    ax = ax < -32 ? -32 : ax > hx ? hx : ax;
+    ay = ay < -32 ? -32 : ay > hy ? hy : ay;
+    ax &= ~(al - 1);
+    *ox = ax - 16*mbx;
+    *oy = ay - 16*mby;
+}
+
+/* semantics of x264hip_*_me_search_centred: table[mb][j][i] = SAD at mv
+ * (ox + i, oy + j), i, j < 2*range+1, with (ox, oy) = origin[mb] from me_window */
+void FN(me_search_centred)( const pixel *fenc, intptr_t fs, const pixel *ref, intptr_t rs, int mb_width,
+                            int mb_height, int range, const int16_t *centre, sadt *table, int16_t *origin )
+{
+    int w = 2*range + 1;
+    for( int mby = 0; mby < mb_height; mby++ )
+        for( int mbx = 0; mbx < mb_width; mbx++ )
+        {
+            size_t mb = (size_t)mby*mb_width + mbx;
+            int ox, oy;
+            me_window( mbx, mby, mb_width, mb_height, range, centre[2*mb], centre[2*mb+1], &ox, &oy );
+            origin[2*mb] = (int16_t)ox;
+            origin[2*mb+1] = (int16_t)oy;
+            const pixel *f = fenc + 16*(mby*fs + mbx);
+            sadt *t = table + mb * w * w;
+            for( int j = 0; j < w; j++ )
+                for( int i = 0; i < w; i++ )
+                    t[j*w+i] = (sadt)FN(sad)( 0, f, fs, ref + (16*mby + oy + j)*rs + 16*mbx + ox + i, rs );
+        }
+}
+
 /* fused inter-luma residual path, semantics of x264hip_*_mb_dct_quant
  * (reference encoder/macroblock.c:806-884 without trellis/decimation) */
 void FN(mb_dct_quant)( int transform, const pixel *fenc, intptr_t fs, const pixel *pred, intptr_t ps,
@@ -1466,8 +1503,8 @@ void FN(subpel_list)( int op, int i_pixel, const pixel *fenc, intptr_t fs, const
  * the predictor result (COPY3_IF_LT, me.h:87-93), my-major raster order.
  * par[8*i] = { bmx, bmy, mvp_x, mvp_y, mv_x_min, mv_y_min, mv_x_max, mv_y_max };
  * table rows have pitch align4(2R+1) and are centred on mv (0,0). */
-void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const int16_t *par, const int32_t *init_cost,
-                        const uint16_t *cost_mv, int32_t *out )
+void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const int16_t *origin, const int16_t *par,
+                        const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out )
 {
     const int W = 2 * R + 1, P = (W + 3) & ~3;
     for( int i = 0; i < nmb; i++ )
@@ -1482,10 +1519,13 @@ void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const i
         int width = (max_x - min_x + 3) & ~3;
         int bcost = init_cost[i];
         const sadt *t = table + (size_t)i * W * P;
+        const int ox = origin ? origin[2*i] : -R, oy = origin ? origin[2*i+1] : -R;
         for( int my = min_y; my <= max_y; my++ )
             for( int mx = min_x; mx < min_x + width; mx++ )
             {
-                int cost = t[(my + R) * P + mx + R] + cx[mx * 4] + cy[my * 4];
+                if( mx - ox < 0 || mx - ox >= W || my - oy < 0 || my - oy >= W )
+                    continue;           /* outside the table: not evaluated */
+                int cost = t[(my - oy) * P + mx - ox] + cx[mx * 4] + cy[my * 4];
                 if( cost < bcost )
                 {
                     bcost = cost;

@@ -64,7 +64,8 @@ for _bd in (8, 10):
     _f(_bd, "mb_dct_quant", [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "hpel_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int, _P])
     _f(_bd, "get_ref", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int], _P)
-    _f(_bd, "me_esa_argmin", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
+    _f(_bd, "me_esa_argmin", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P])
+    _f(_bd, "me_search_centred", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
     _f(_bd, "subpel_list", [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P])
     _f(_bd, "sa8d", [C.c_int, _P, _IP, _P, _IP], C.c_int)
@@ -245,15 +246,28 @@ def subpel_list(bd, op, i_pixel, fenc, fs, planes, p_origin, rs, fenc_off, qxy):
     return out
 
 
-def me_esa_argmin(bd, table, rng, me_range, par, init_cost, cost_mv, c0):
-    """table: numpy [nmb, 2r+1, pitch]; cost_mv numpy uint16 with mvd 0 at index c0."""
+def me_esa_argmin(bd, table, rng, me_range, par, init_cost, cost_mv, c0, origin=None):
+    """table: numpy [nmb, 2r+1, pitch]; cost_mv numpy uint16 with mvd 0 at index c0;
+    origin: int16 [nmb, 2] table origins (None = centred on mv 0)."""
     t = np.ascontiguousarray(table)
     p = np.ascontiguousarray(par, np.int16)
     ic = np.ascontiguousarray(init_cost, np.int32)
     out = np.zeros((len(p), 3), np.int32)
-    getattr(_L, f"oracle{bd}_me_esa_argmin")(_addr(t), rng, len(p), me_range, _addr(p), _addr(ic),
+    o = None if origin is None else _addr(np.ascontiguousarray(origin, np.int16))
+    getattr(_L, f"oracle{bd}_me_esa_argmin")(_addr(t), rng, len(p), me_range, o, _addr(p), _addr(ic),
                                             _addr(cost_mv, c0), _addr(out))
     return out
+
+
+def me_search_centred(bd, fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, rng, centre):
+    """one frame: (table [mbh, mbw, 2r+1, 2r+1], origin int16 [mbh*mbw, 2])."""
+    w = 2 * rng + 1
+    out = np.zeros((mbh, mbw, w, w), sad_dtype(bd))
+    org = np.zeros((mbh * mbw, 2), np.int16)
+    c = np.ascontiguousarray(centre, np.int16)
+    getattr(_L, f"oracle{bd}_me_search_centred")(_addr(fenc, f_origin), fs, _addr(ref, r_origin), rs, mbw, mbh,
+                                                rng, _addr(c), _addr(out), _addr(org))
+    return out, org
 
 
 # ---------------------------------------------------------------- further pixel entries

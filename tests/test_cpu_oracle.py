@@ -291,3 +291,35 @@ def test_me_esa_argmin_vs_numpy(oracle):
         if cost.ravel()[j] < init[k]:
             want = (int(cost.ravel()[j]), int(xs.ravel()[j]), int(ys.ravel()[j]))
         assert tuple(got[k]) == want, k
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_me_search_centred_oracle(oracle, bd):
+    from conftest import load_package
+    """centred tables: centre (0,0) equals the plain table; shifted centres equal the SADs at
+    origin + (i, j) (numpy), with the origin clamped into the 32-pixel padding and aligned."""
+    load_package()
+    from x264hip import synth
+    W, H, R = 96, 64, 8
+    planes, stride, origin = synth.make_sequence(2, W, H, bd)
+    mbw, mbh = W // 16, H // 16
+    f, r = planes[1].ravel(), planes[0].ravel()
+    plain = oracle.me_search_full(bd, f, origin, stride, r, origin, stride, mbw, mbh, R)
+    tab, org = oracle.me_search_centred(bd, f, origin, stride, r, origin, stride, mbw, mbh, R,
+                                        np.zeros((mbw * mbh, 2), np.int16))
+    assert np.array_equal(tab, plain) and (org == -R).all()
+    rs = np.random.default_rng(bd)
+    cen = rs.integers(-40, 41, (mbw * mbh, 2)).astype(np.int16)
+    tab, org = oracle.me_search_centred(bd, f, origin, stride, r, origin, stride, mbw, mbh, R, cen)
+    al = 4 if bd == 8 else 2
+    P = (2 * R + 1 + 3) & ~3
+    for mb in range(mbw * mbh):
+        mbx, mby = mb % mbw, mb // mbw
+        ax = min(max(16 * mbx + cen[mb, 0] - R, -32), 16 * mbw + 12 - P) & ~(al - 1)
+        ay = min(max(16 * mby + cen[mb, 1] - R, -32), 16 * mbh + 16 - 2 * R)
+        assert (org[mb, 0], org[mb, 1]) == (ax - 16 * mbx, ay - 16 * mby)
+        fb = nr.block(f, origin + 16 * mby * stride + 16 * mbx, stride, 16, 16)
+        for j in (0, R, 2 * R):
+            for i in (0, 3, 2 * R):
+                rb = nr.block(r, origin + (ay + j) * stride + ax + i, stride, 16, 16)
+                assert tab[mby, mbx, j, i] == nr.sad(fb, rb), (mb, i, j)

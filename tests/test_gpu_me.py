@@ -146,3 +146,85 @@ def test_me_esa_argmin(hip, oracle, bd, rng, me_range):
     want = oracle.me_esa_argmin(bd, tab, rng, me_range, par, init, cost_mv, c0)
     assert np.array_equal(got, want), np.argwhere((got != want).any(1))[:5]
     assert (got[::7, 0] == 0).all() and (got[:, 0] <= init).all()
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("rng", [8, 16, 24])
+def test_me_search_centred(hip, oracle, bd, rng, variant):
+    """per-MB centres, including ones far enough out that the window is clamped into the
+    padding; table and origin equal the oracle's (all variants)."""
+    from x264hip import synth
+    W, H = 96, 64
+    planes, stride, origin = synth.make_sequence(3, W, H, bd, seed=7)
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
+    fs = planes[0].size
+    mbw, mbh, nf = W // 16, H // 16, 2
+    rs = np.random.default_rng(bd * 31 + rng)
+    cen = rs.integers(-48, 49, (nf * mbw * mbh, 2)).astype(np.int16)
+    cen[::5] = 0
+    table, org = hip.me_search_centred(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, nf, rng,
+                                       torch.from_numpy(cen).cuda(), fenc_frame_stride=fs, ref_frame_stride=fs)
+    got = table.cpu().numpy()
+    got = (got.view(np.uint16) if bd == 8 else got.view(np.uint32))[..., :2 * rng + 1]
+    org = org.cpu().numpy()
+    n1 = mbw * mbh
+    for f in range(nf):
+        want, worg = oracle.me_search_centred(bd, planes[f + 1].ravel(), origin, stride, planes[f].ravel(), origin,
+                                              stride, mbw, mbh, rng, cen[f * n1:(f + 1) * n1])
+        assert np.array_equal(org[f * n1:(f + 1) * n1], worg), f
+        assert np.array_equal(got[f], want), f
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_me_esa_argmin_centred(hip, oracle, bd):
+    """ESA decision around predictor centres (me.c:618-624 centres the window on bmx, bmy):
+    centred table with range = me_range + 8 and origin-aware argmin, vs the oracle."""
+    from x264hip import synth
+    W, H = 160, 96
+    rng, me_range = 24, 16
+    planes, stride, origin = synth.make_sequence(2, W, H, bd, seed=9)
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
+    mbw, mbh = W // 16, H // 16
+    nmb = mbw * mbh
+    rs = np.random.default_rng(bd + 77)
+    par = np.zeros((nmb, 8), np.int16)
+    par[:, 0] = rs.integers(-12, 13, nmb)
+    par[:, 1] = rs.integers(-12, 13, nmb)
+    par[:, 2] = rs.integers(-64, 65, nmb)
+    par[:, 3] = rs.integers(-64, 65, nmb)
+    mbx, mby = np.arange(nmb) % mbw, np.arange(nmb) // mbw
+    par[:, 4] = -16 * mbx - 24                                      # mv_limit_fpel-like (analyse.c:330-349)
+    par[:, 5] = -16 * mby - 24
+    par[:, 6] = 16 * (mbw - 1 - mbx) + 24 - 4
+    par[:, 7] = 16 * (mbh - 1 - mby) + 24
+    cen = np.ascontiguousarray(par[:, :2])
+    table, org = hip.me_search_centred(dev[1:], origin, stride, dev[:1], origin, stride, mbw, mbh, 1, rng,
+                                       torch.from_numpy(cen).cuda())
+    init = rs.integers(0, 20000, nmb).astype(np.int32)
+    cost_mv, c0 = _cost_mv()
+    cm_dev = torch.from_numpy(cost_mv.view(np.int16)).cuda()
+    got = hip.me_esa_argmin(table, rng, me_range, torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda(),
+                            (cm_dev, c0), origin=org).cpu().numpy()
+    tab = table.cpu().numpy()
+    tab = (tab.view(np.uint16) if bd == 8 else tab.view(np.uint32))[0].reshape(nmb, 2 * rng + 1, -1)
+    want = oracle.me_esa_argmin(bd, tab, rng, me_range, par, init, cost_mv, c0, origin=org.cpu().numpy())
+    assert np.array_equal(got, want), np.argwhere((got != want).any(1))[:5]
+    # every candidate of the rounded, clipped window lay inside the table: the decision equals the
+    # plain exhaustive scan over direct SADs (me.c:627-631)
+    f1, f0 = planes[1].ravel(), planes[0].ravel()
+    for mb in range(0, nmb, 9):
+        bmx, bmy = int(par[mb, 0]), int(par[mb, 1])
+        x0 = max(bmx - me_range, int(par[mb, 4]))
+        y0 = max(bmy - me_range, int(par[mb, 5]))
+        x1 = min(bmx + me_range, int(par[mb, 6]))
+        y1 = min(bmy + me_range, int(par[mb, 7]))
+        wdt = (x1 - x0 + 3) & ~3
+        best = (int(init[mb]), bmx, bmy)
+        fo = origin + 16 * mby[mb] * stride + 16 * mbx[mb]
+        for my in range(y0, y1 + 1):
+            for mx in range(x0, x0 + wdt):
+                c = oracle.cmp(bd, "sad", 0, f1, fo, stride, f0, fo + my * stride + mx, stride) \
+                    + int(cost_mv[c0 + mx * 4 - par[mb, 2]]) + int(cost_mv[c0 + my * 4 - par[mb, 3]])
+                if c < best[0]:
+                    best = (c, mx, my)
+        assert tuple(got[mb]) == best, mb

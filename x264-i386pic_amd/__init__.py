@@ -246,6 +246,11 @@ def _declare(L):
         f("quant_batch").argtypes = [_c.c_int, _P, _P, _P, _c.c_int, _P, _P]
         f("quant_dc_batch").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P]
         f("me_esa_argmin").argtypes = [_P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P]
+        f("me_esa_argmin_at").argtypes = [_P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P, _P]
+        f("me_search_centred").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                           _P, _P, _P, _P]
+        f("me_esa_argmin_at").restype = _c.c_int
+        f("me_search_centred").restype = _c.c_int
         f("hpel_filter").argtypes = [_P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P]
         f("subpel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, _c.c_int, _P, _P]
         f("mb_dct_quant").argtypes = [_c.c_int, _P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int,
@@ -668,8 +673,9 @@ def subpel_cmp_batch(op, i_pixel, fenc, fenc_stride, planes, ref_origin, ref_str
     return scores
 
 
-def me_esa_argmin(table, rng, me_range, par, init_cost, cost_mv_center, out=None):
-    """ESA decision per MB over a full-search table (x264hip_*_me_esa_argmin).
+def me_esa_argmin(table, rng, me_range, par, init_cost, cost_mv_center, out=None, origin=None):
+    """ESA decision per MB over a full-search table (x264hip_*_me_esa_argmin, or
+    x264hip_*_me_esa_argmin_at when `origin` [n, 2] int16 from me_search_centred is given).
     par int16 [n, 8], init_cost int32 [n], cost_mv_center: (uint16-as-int16 tensor, element
     offset of mvd 0).  Returns int32 [n, 3] = (cost, mx, my)."""
     import torch
@@ -678,7 +684,32 @@ def me_esa_argmin(table, rng, me_range, par, init_cost, cost_mv_center, out=None
     if out is None:
         out = torch.empty((n, 3), dtype=torch.int32, device=table.device)
     cm, c0 = cost_mv_center
-    _rc(getattr(lib(), f"x264hip_{bd}_me_esa_argmin")(
-        _ptr(table), rng, n, me_range, _ptr(par), _ptr(init_cost), _ptr(cm, c0), _ptr(out), _stream()),
-        "me_esa_argmin")
+    if origin is None:
+        _rc(getattr(lib(), f"x264hip_{bd}_me_esa_argmin")(
+            _ptr(table), rng, n, me_range, _ptr(par), _ptr(init_cost), _ptr(cm, c0), _ptr(out), _stream()),
+            "me_esa_argmin")
+    else:
+        _rc(getattr(lib(), f"x264hip_{bd}_me_esa_argmin_at")(
+            _ptr(table), rng, n, me_range, _ptr(origin), _ptr(par), _ptr(init_cost), _ptr(cm, c0), _ptr(out),
+            _stream()), "me_esa_argmin_at")
     return out
+
+
+def me_search_centred(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height, nframes,
+                      rng, centre, table=None, origin=None, fenc_frame_stride=None, ref_frame_stride=None):
+    """Full search around per-MB centres (x264hip_*_me_search_centred): centre int16 [n_mbs, 2];
+    returns (table [nframes, mbh, mbw, 2r+1, pitch], origin int16 [n_mbs, 2])."""
+    import torch
+    bd = _pix_bd(fenc)
+    w = 2 * rng + 1
+    if table is None:
+        table = torch.empty((nframes, mb_height, mb_width, w, me_table_pitch(rng)),
+                            dtype=torch.int16 if bd == 8 else torch.int32, device=fenc.device)
+    if origin is None:
+        origin = torch.empty((nframes * mb_height * mb_width, 2), dtype=torch.int16, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)
+    _rc(getattr(lib(), f"x264hip_{bd}_me_search_centred")(
+        _ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs, mb_width, mb_height,
+        nframes, rng, _ptr(centre), _ptr(table), _ptr(origin), _stream()), "me_search_centred")
+    return table, origin

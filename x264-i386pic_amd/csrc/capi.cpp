@@ -928,8 +928,19 @@ static int map_err( hipError_t e, const char *where )
     {                                                                                                                \
         if( mbw < 0 || mbh < 0 || nframes < 0 || !( range == 4 || range == 8 || range == 16 || range == 24 ) )        \
             return X264HIP_EINVAL;                                                                                   \
-        return map_err( launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, table,           \
-                                            (hipStream_t)stream ), "me_search_full" );                               \
+        return map_err( launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, table, nullptr,  \
+                                            nullptr, (hipStream_t)stream ), "me_search_full" );                      \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_search_centred( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,          \
+                                                     const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw,   \
+                                                     int mbh, int nframes, int range, const int16_t *centre,         \
+                                                     PT<BD>::sadt *table, int16_t *origin, void *stream )            \
+    {                                                                                                                \
+        if( mbw < 0 || mbh < 0 || nframes < 0 || !centre || !origin ||                                               \
+            !( range == 4 || range == 8 || range == 16 || range == 24 ) )                                            \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, table, centre,   \
+                                            origin, (hipStream_t)stream ), "me_search_centred" );                    \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_me_esa_argmin( const PT<BD>::sadt *table, int range, int n, int me_range,         \
                                                  const int16_t *par, const int32_t *init_cost,                       \
@@ -937,8 +948,18 @@ static int map_err( hipError_t e, const char *where )
     {                                                                                                                \
         if( range < 1 || range > 29 || n < 0 || me_range < 0 || 2 * me_range + 4 > 64 )                              \
             return X264HIP_EINVAL;                                                                                   \
-        return map_err( launch_me_esa_argmin<BD>( table, range, n, me_range, par, init_cost, cost_mv, out,           \
+        return map_err( launch_me_esa_argmin<BD>( table, range, n, me_range, nullptr, par, init_cost, cost_mv, out,  \
                                                   (hipStream_t)stream ), "me_esa_argmin" );                          \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_esa_argmin_at( const PT<BD>::sadt *table, int range, int n, int me_range,      \
+                                                    const int16_t *origin, const int16_t *par,                       \
+                                                    const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out, \
+                                                    void *stream )                                                   \
+    {                                                                                                                \
+        if( range < 1 || range > 29 || n < 0 || me_range < 0 || 2 * me_range + 4 > 64 || !origin )                   \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_me_esa_argmin<BD>( table, range, n, me_range, origin, par, init_cost, cost_mv, out,   \
+                                                  (hipStream_t)stream ), "me_esa_argmin_at" );                       \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_hpel_filter( const PT<BD>::pixel *src, PT<BD>::pixel *dh, PT<BD>::pixel *dv,       \
                                                PT<BD>::pixel *dc, intptr_t stride, intptr_t fstride, int width,     \

@@ -146,7 +146,8 @@ hipError_t launch_cmp_batch( int op, int i_pixel, const typename PT<BD>::pixel *
 template <int BD>
 hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                           int nframes, int range, typename PT<BD>::sadt *table, hipStream_t stream );
+                           int nframes, int range, typename PT<BD>::sadt *table, const int16_t *centre,
+                           int16_t *origin, hipStream_t stream );
 template <int BD>
 hipError_t launch_sub_dct( int kind, const typename PT<BD>::pixel *fenc, intptr_t fs,
                            const typename PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fenc_off,
@@ -174,8 +175,8 @@ hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel 
                               const int32_t *qxy, int n, int32_t *scores, hipStream_t stream );
 template <int BD>
 hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int nmb, int me_range,
-                                 const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,
-                                 hipStream_t stream );
+                                 const int16_t *origin, const int16_t *par, const int32_t *init_cost,
+                                 const uint16_t *cost_mv, int32_t *out, hipStream_t stream );
 template <int BD>
 hipError_t launch_stat_batch( int op, int i_pixel, const typename PT<BD>::pixel *p1, intptr_t s1,
                               const typename PT<BD>::pixel *p2, intptr_t s2, const int64_t *off1,

@@ -54,12 +54,38 @@ __device__ __forceinline__ void me_rows( const typename PT<BD>::pixel *rb, intpt
     ( me_row<BD, R, Ys>( rb, rs, F, acc, out ), ... );
 }
 
+// Window origin of one MB (me_search_centred; the plain search is the
+// special case centre = (0, 0)): (cx, cy) - R, clamped so that every pixel
+// any variant fetches lies in the 32-pixel padded plane (x264's PADH = PADV =
+// 32, common/frame.h:32-33), then aligned down to 4 (8 bit) / 2 (10 bit)
+// pixels so the grouped variants keep dword-aligned rows.  For centre (0, 0)
+// and R <= 24 neither step changes anything.  Returned relative to the MB.
+template <int BD, int R>
+__device__ __forceinline__ void me_window( const int16_t *__restrict__ centre, int64_t mb, int mbx, int mby, int mbw,
+                                           int mbh, int &ox, int &oy )
+{
+    constexpr int P = (2 * R + 1 + 3) & ~3, AL = BD == 8 ? 4 : 2;
+    int ax = 16 * mbx - R, ay = 16 * mby - R;
+    if( centre )
+    {
+        ax += centre[2 * mb];
+        ay += centre[2 * mb + 1];
+    }
+    ax = min( max( ax, -32 ), 16 * mbw + 12 - P );
+    ay = min( max( ay, -32 ), 16 * mbh + 16 - 2 * R );
+    ax &= ~(AL - 1);
+    ox = ax - 16 * mbx;
+    oy = ay - 16 * mby;
+}
+
 template <int BD, int R>
 __global__ __launch_bounds__( 256 ) void me_full_sad16_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
                                                                intptr_t fs, intptr_t ffs,
                                                                const typename PT<BD>::pixel *__restrict__ ref,
                                                                intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                                                               int nframes, typename PT<BD>::sadt *__restrict__ table )
+                                                               int nframes, typename PT<BD>::sadt *__restrict__ table,
+                                                               const int16_t *__restrict__ centre,
+                                                               int16_t *__restrict__ origin )
 {
     constexpr int W = 2 * R + 1;
     constexpr int NDW = 16 / PT<BD>::PPD;   // dwords per 16-pixel row
@@ -81,7 +107,14 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_kernel( const typename PT
     for( int r = 0; r < 16; r++ )
         load_packed<NDW>( fe + r * fs, F[r] );
 
-    const typename PT<BD>::pixel *rb = ref + f * rfs + (intptr_t)(16 * mby - R) * rs + 16 * mbx - R + col;
+    int ox, oy;
+    me_window<BD, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    if( origin && col == 0 )
+    {
+        origin[2 * mb] = (int16_t)ox;
+        origin[2 * mb + 1] = (int16_t)oy;
+    }
+    const typename PT<BD>::pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox + col;
     typename PT<BD>::sadt *out = table + mb * (W * ((W + 3) & ~3)) + col;
 
     uint32_t acc[16];
@@ -149,7 +182,9 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v2_kernel( const typename
                                                                   intptr_t fs, intptr_t ffs,
                                                                   const typename PT<BD>::pixel *__restrict__ ref,
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                                                                  int nframes, typename PT<BD>::sadt *__restrict__ table )
+                                                                  int nframes, typename PT<BD>::sadt *__restrict__ table,
+                                                                  const int16_t *__restrict__ centre,
+                                                                  int16_t *__restrict__ origin )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int W = 2 * R + 1;
@@ -175,7 +210,14 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v2_kernel( const typename
         for( int k = 0; k < NDW; k++ )
             F[r][k] = fe[r * fs_dw + k];
 
-    const pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + 8 * h - R) * rs + 16 * mbx - R + col;
+    int ox, oy;
+    me_window<BD, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    if( origin && col == 0 && h == 0 )
+    {
+        origin[2 * mb] = (int16_t)ox;
+        origin[2 * mb + 1] = (int16_t)oy;
+    }
+    const pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + col;
     const uint32_t sh = (uint32_t)((uintptr_t)rb & 3);
     const uint32_t *rbase = (const uint32_t *)((const char *)rb - sh);
     typename PT<BD>::sadt *out = table + mb * (W * ((W + 3) & ~3)) + col;
@@ -239,7 +281,9 @@ template <int R>
 __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                   intptr_t ffs, const uint8_t *__restrict__ ref,
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                                                                  int nframes, uint16_t *__restrict__ table )
+                                                                  int nframes, uint16_t *__restrict__ table,
+                                                                  const int16_t *__restrict__ centre,
+                                                                  int16_t *__restrict__ origin )
 {
     constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
     constexpr int P = 4 * G;                    // table row pitch
@@ -263,8 +307,15 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t 
 #pragma unroll
         for( int k = 0; k < 4; k++ )
             F[r][k] = fe[r * fs_dw + k];
+    int ox, oy;
+    me_window<8, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    if( origin && grp == 0 && h == 0 )
+    {
+        origin[2 * mb] = (int16_t)ox;
+        origin[2 * mb + 1] = (int16_t)oy;
+    }
     const uint32_t *rbase =
-        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h - R) * rs + 16 * mbx - R + 4 * grp);
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 4 * grp);
     uint64_t *out = (uint64_t *)(table + mb * ((2 * R + 1) * P) + 4 * grp);
     uint64_t acc[8];
     me_rows3<R>( rbase, (int)(rs / 4), F, acc, out, std::make_integer_sequence<int, 2 * R + 8>{} );
@@ -327,7 +378,9 @@ template <int R>
 __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
                                                                   intptr_t ffs, const uint16_t *__restrict__ ref,
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                                                                  int nframes, uint32_t *__restrict__ table )
+                                                                  int nframes, uint32_t *__restrict__ table,
+                                                                  const int16_t *__restrict__ centre,
+                                                                  int16_t *__restrict__ origin )
 {
     constexpr int G = (2 * R + 1 + 1) / 2;      // column pairs per MB
     constexpr int P = (2 * R + 1 + 3) / 4 * 4;
@@ -351,8 +404,15 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
 #pragma unroll
         for( int k = 0; k < 8; k++ )
             F[r][k] = fe[r * fs_dw + k];
+    int ox, oy;
+    me_window<10, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    if( origin && grp == 0 && h == 0 )
+    {
+        origin[2 * mb] = (int16_t)ox;
+        origin[2 * mb + 1] = (int16_t)oy;
+    }
     const uint32_t *rbase =
-        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h - R) * rs + 16 * mbx - R + 2 * grp);
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 2 * grp);
     uint32_t *out = table + mb * ((2 * R + 1) * P) + 2 * grp;
     uint32_t acc[8][2];
     me_rows5<R>( rbase, (int)(rs / 2), F, acc, out, std::make_integer_sequence<int, 2 * R + 8>{} );
@@ -360,11 +420,12 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
 
 template <int R, typename P, typename T>
 static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
-                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table )
+                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
+                       int16_t *origin )
 {
     if constexpr( sizeof( P ) == 2 )
         hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
-                            nframes, table );
+                            nframes, table, centre, origin );
 }
 
 // kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2, 3 (8 bit)
@@ -380,17 +441,19 @@ static int me_variant()
 
 template <int R, typename P, typename T>
 static void launch_v3( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
-                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table )
+                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
+                       int16_t *origin )
 {
     if constexpr( sizeof( P ) == 1 )
         hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
-                            nframes, table );
+                            nframes, table, centre, origin );
 }
 
 template <int BD>
 hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                           int nframes, int range, typename PT<BD>::sadt *table, hipStream_t stream )
+                           int nframes, int range, typename PT<BD>::sadt *table, const int16_t *centre,
+                           int16_t *origin, hipStream_t stream )
 {
     int variant = me_variant();
     if( !variant )
@@ -415,15 +478,15 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
 #define ME_CASE( R ) \
         case R:                                                                                                   \
             if( variant == 5 )                                                                                    \
-                launch_v5<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table );           \
+                launch_v5<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
             else if( variant == 3 )                                                                               \
-                launch_v3<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table );           \
+                launch_v3<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
             else if( variant == 2 )                                                                               \
                 hipLaunchKernelGGL( ( me_full_sad16_v2_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, \
-                                    rfs, mbw, mbh, nframes, table );                                              \
+                                    rfs, mbw, mbh, nframes, table, centre, origin );                              \
             else                                                                                                  \
                 hipLaunchKernelGGL( ( me_full_sad16_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs,   \
-                                    rfs, mbw, mbh, nframes, table );                                              \
+                                    rfs, mbw, mbh, nframes, table, centre, origin );                              \
             break;
         ME_CASE( 4 ) ME_CASE( 8 ) ME_CASE( 16 ) ME_CASE( 24 )
 #undef ME_CASE
@@ -433,9 +496,9 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
 }
 
 template hipError_t launch_me_full<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
-                                       int, int, int, uint16_t *, hipStream_t );
+                                       int, int, int, uint16_t *, const int16_t *, int16_t *, hipStream_t );
 template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
-                                        int, int, int, int, uint32_t *, hipStream_t );
+                                        int, int, int, int, uint32_t *, const int16_t *, int16_t *, hipStream_t );
 
 } // namespace x264hip
 
@@ -451,7 +514,9 @@ namespace x264hip {
 // replaces the predictor result only if strictly better (COPY3_IF_LT).
 template <int BD>
 __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT<BD>::sadt *__restrict__ table, int R,
-                                                               int nmb, int me_range, const int16_t *__restrict__ par,
+                                                               int nmb, int me_range,
+                                                               const int16_t *__restrict__ origin,
+                                                               const int16_t *__restrict__ par,
                                                                const int32_t *__restrict__ init_cost,
                                                                const uint16_t *__restrict__ cost_mv,
                                                                int32_t *__restrict__ out )
@@ -467,13 +532,17 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
     const int max_x = min( bmx + me_range, (int)p[6] ), max_y = min( bmy + me_range, (int)p[7] );
     const int width = (max_x - min_x + 3) & ~3;
     const int n = width > 0 && max_y >= min_y ? width * (max_y - min_y + 1) : 0;
-    const typename PT<BD>::sadt *t = table + mb * (int64_t)(W * P) + (min_y + R) * P + (min_x + R);
+    const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
+    const typename PT<BD>::sadt *t = table + mb * (int64_t)(W * P);
     uint32_t key = 0xFFFFFFFFu;
     for( int i = lane; i < n; i += 64 )
     {
         const int dy = i / width, dx = i - dy * width;
         const int mx = min_x + dx, my = min_y + dy;
-        const uint32_t cost = (uint32_t)t[dy * P + dx] + cost_mv[mx * 4 - mvpx] + cost_mv[my * 4 - mvpy];
+        const int tx = mx - ox, ty = my - oy;
+        if( tx < 0 || tx >= W || ty < 0 || ty >= W )
+            continue;                                   // outside the table: not evaluated
+        const uint32_t cost = (uint32_t)t[ty * P + tx] + cost_mv[mx * 4 - mvpx] + cost_mv[my * 4 - mvpy];
         key = min( key, (cost << 12) | (uint32_t)i );
     }
 #pragma unroll
@@ -497,19 +566,19 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
 
 template <int BD>
 hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int nmb, int me_range,
-                                 const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,
-                                 hipStream_t stream )
+                                 const int16_t *origin, const int16_t *par, const int32_t *init_cost,
+                                 const uint16_t *cost_mv, int32_t *out, hipStream_t stream )
 {
     if( nmb <= 0 )
         return hipSuccess;
     hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD> ), dim3( (nmb + 3) / 4 ), dim3( 256 ), 0, stream, table, R, nmb,
-                        me_range, par, init_cost, cost_mv, out );
+                        me_range, origin, par, init_cost, cost_mv, out );
     return hipGetLastError();
 }
 
-template hipError_t launch_me_esa_argmin<8>( const uint16_t *, int, int, int, const int16_t *, const int32_t *,
-                                             const uint16_t *, int32_t *, hipStream_t );
-template hipError_t launch_me_esa_argmin<10>( const uint32_t *, int, int, int, const int16_t *, const int32_t *,
-                                              const uint16_t *, int32_t *, hipStream_t );
+template hipError_t launch_me_esa_argmin<8>( const uint16_t *, int, int, int, const int16_t *, const int16_t *,
+                                             const int32_t *, const uint16_t *, int32_t *, hipStream_t );
+template hipError_t launch_me_esa_argmin<10>( const uint32_t *, int, int, int, const int16_t *, const int16_t *,
+                                              const int32_t *, const uint16_t *, int32_t *, hipStream_t );
 
 } // namespace x264hip
