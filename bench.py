@@ -248,7 +248,16 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     wall, ev_ms = timed(lstep, a.steps, a.warmup, world)
     res["lowres_frames_per_s"] = world * a.steps * F / wall
     res["lowres_launch_ms"] = ev_ms
-    del louts
+    # the lookahead's intra estimate on those lowres planes (slicetype.c:714-757, subme > 1:
+    # 10 predictions + satd_8x8 per 8x8 block, lambda of X264_LOOKAHEAD_QP = 12 -> 1, slicetype.c:47-48)
+    iouts = x.lowres_intra_cost(louts[0], x.plane_stride(lw // 2), mbw, mbh, True, True, 1)
+
+    def istep():
+        x.lowres_intra_cost(louts[0], x.plane_stride(lw // 2), mbw, mbh, True, True, 1, outs=iouts)
+    wall, ev_ms = timed(istep, a.steps, a.warmup, world)
+    res["lowres_intra_mbs_per_s"] = world * a.steps * F * mbw * mbh / wall
+    res["lowres_intra_launch_ms"] = ev_ms
+    del louts, iouts
     nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
     bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)

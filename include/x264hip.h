@@ -120,6 +120,18 @@ enum
     X264HIP_COEF_LAST16 = 6, X264HIP_COEF_LAST64 = 7,
 };
 
+/* block kinds of x264hip_*_intra_cmp_x3_batch: the pixel table's intra_*_x3
+ * entries (pixel.c:518-560).  Mode order of res[3]: V,H,DC for 4x4 / 16x16 /
+ * 8x8; DC,H,V for the chroma kinds. */
+enum
+{
+    X264HIP_INTRA_4x4   = 0,   /* intra_{sad,satd}_x3_4x4   (predict.c:495-511)   */
+    X264HIP_INTRA_8x8C  = 1,   /* intra_{sad,satd}_x3_8x8c  (predict.c:221-281)   */
+    X264HIP_INTRA_8x16C = 2,   /* intra_{sad,satd}_x3_8x16c (predict.c:361-441)   */
+    X264HIP_INTRA_16x16 = 3,   /* intra_{sad,satd}_x3_16x16 (predict.c:67-130)    */
+    X264HIP_INTRA_8x8   = 4,   /* intra_{sad,sa8d}_x3_8x8 from edge[36] (predict.c:716-739) */
+};
+
 /* zigzag_sub kinds of x264hip_*_zigzag_sub_batch, dct.c:856-925 */
 enum { X264HIP_ZIGZAG_SUB_4x4 = 0, X264HIP_ZIGZAG_SUB_4x4AC = 1, X264HIP_ZIGZAG_SUB_8x8 = 2 };
 
@@ -370,6 +382,37 @@ int x264hip_##BD##_ads_batch( int i_pixel, const int32_t *enc_dc, const uint16_t
                               const int64_t *cost_off, const int32_t *width,                    \
                               const int32_t *thresh, int n, int16_t *mvs, int mvs_pitch,        \
                               int32_t *nmv, void *stream );                                     \
+                                                                                                \
+/* n independent intra_*_x3 calls of X264HIP_INTRA_* kind: block i has fenc at                 \
+ * fenc + fenc_off[i] (stride fenc_stride) and its reconstructed neighbours at                  \
+ * fdec + fdec_off[i] (the block's (0,0); row -1 and column -1 are read, stride                 \
+ * fdec_stride), or for X264HIP_INTRA_8x8 the 36-entry filtered edge at                          \
+ * fdec + fdec_off[i].  op: X264HIP_CMP_SAD or X264HIP_CMP_SATD (X264HIP_CMP_SA8D                 \
+ * for the 8x8 kind).  scores[3i..3i+2] = the reference's res[3].  The                           \
+ * reference C also leaves its last prediction in fdec; this entry does not                      \
+ * write fdec (as the asm versions).  Device arrays. */                                          \
+int x264hip_##BD##_intra_cmp_x3_batch( int kind, int op, const pixel *fenc, intptr_t fenc_stride, \
+                                       const pixel *fdec, intptr_t fdec_stride,                  \
+                                       const int64_t *fenc_off, const int64_t *fdec_off, int n,  \
+                                       int32_t *scores, void *stream );                          \
+                                                                                                \
+/* the lookahead's intra estimate (slicetype_mb_cost's lowres_intra_mb leg,                     \
+ * encoder/slicetype.c:714-757) for every 8x8 block of n_frames lowres planes                    \
+ * (lowres[0] of x264hip_*_frame_init_lowres; plane at (0,0), 32 pixels of border,              \
+ * plane and stride 4-byte aligned).  satd = !lossless && subme > 1 (the mbcmp                   \
+ * choice of encoder.c:1409-1416), all_modes = subme > 1 (planar + the six                        \
+ * directional 8x8 modes over the filtered edge), lambda = x264_lambda_tab[qp].                   \
+ * Outputs per frame f: intra_cost[f*mbw*mbh + mb] (fenc->i_intra_cost),                         \
+ * row_satd[f*mbh + y] (i_row_satds[0][0], AQ-scaled), cost_est[2f] / [2f+1]                      \
+ * (i_cost_est[0][0] / i_cost_est_aq[0][0] over the frame-score MBs).  inv_qscale                 \
+ * [f*mbw*mbh + mb] (i_inv_qscale_factor) or NULL when AQ is off; row_satd and                    \
+ * cost_est may be NULL.  Every MB is computed (the do_edges case of                              \
+ * slicetype.c:823-828).  Device arrays. */                                                       \
+int x264hip_##BD##_lowres_intra_cost( const pixel *lowres, intptr_t stride,                     \
+                                      intptr_t frame_stride, int mb_width, int mb_height,        \
+                                      int n_frames, int satd, int all_modes, int lambda,         \
+                                      const uint16_t *inv_qscale, uint16_t *intra_cost,          \
+                                      int32_t *row_satd, int32_t *cost_est, void *stream );      \
                                                                                                 \
 /* ESA integral image of n_frames luma planes (x264_frame_filter, mc.c:748-782;                 \
  * integral_init* mc.c:424-456): plane / integral point at (0,0), rows                          \

@@ -1591,3 +1591,285 @@ void FN(frame_init_lowres)( const pixel *src_in, intptr_t stride, int width, int
         }
     }
 }
+
+/*============================================================================
+ * intra prediction and the pixel table's intra_*_x3 entries — reference
+ * common/predict.c, common/pixel.c:518-560; the lookahead's intra estimate of
+ * encoder/slicetype.c:714-757.  Predictors work on an FDEC-layout buffer (src
+ * at the block's (0,0), neighbours at x = -1 / y = -1) like the reference.
+ *==========================================================================*/
+#define F1(a,b)   (((a)+(b)+1)>>1)
+#define F2(a,b,c) (((a)+2*(b)+(c)+2)>>2)
+#define PX(x,y) src[(x) + (y)*FDEC_STRIDE]
+
+static void fill_rect( pixel *src, int x0, int y0, int w, int h, int v )
+{
+    for( int y = y0; y < y0 + h; y++ )
+        for( int x = x0; x < x0 + w; x++ )
+            PX(x,y) = v;
+}
+
+/* predict_4x4_{v,h,dc} (predict.c:495-511), predict_16x16_{dc,h,v} (:67-130):
+ * a square block of n pixels */
+static void pred_sq_v( pixel *src, int n )
+{
+    for( int y = 0; y < n; y++ )
+        for( int x = 0; x < n; x++ )
+            PX(x,y) = PX(x,-1);
+}
+static void pred_sq_h( pixel *src, int n )
+{
+    for( int y = 0; y < n; y++ )
+        fill_rect( src, 0, y, n, 1, PX(-1,y) );
+}
+static void pred_sq_dc( pixel *src, int n )
+{
+    int s = 0;
+    for( int i = 0; i < n; i++ )
+        s += PX(-1,i) + PX(i,-1);
+    fill_rect( src, 0, 0, n, n, (s + n) >> (n == 4 ? 3 : 5) );
+}
+
+/* predict_8x8c_dc (predict.c:221-258) and predict_8x16c_dc (:361-419):
+ * h = 8 or 16 rows of 4x4 DC quadrants */
+static void pred_chroma_dc( pixel *src, int h )
+{
+    int s0 = 0, s1 = 0, sl[4] = { 0 };
+    for( int i = 0; i < 4; i++ )
+    {
+        s0 += PX(i,-1);
+        s1 += PX(i+4,-1);
+        for( int k = 0; k < h / 4; k++ )
+            sl[k] += PX(-1,i + 4*k);
+    }
+    fill_rect( src, 0, 0, 4, 4, (s0 + sl[0] + 4) >> 3 );
+    fill_rect( src, 4, 0, 4, 4, (s1 + 2) >> 2 );
+    for( int k = 1; k < h / 4; k++ )
+    {
+        fill_rect( src, 0, 4*k, 4, 4, (sl[k] + 2) >> 2 );
+        fill_rect( src, 4, 4*k, 4, 4, (s1 + sl[k] + 4) >> 3 );
+    }
+}
+static void pred_chroma_h( pixel *src, int h ) { for( int y = 0; y < h; y++ ) fill_rect( src, 0, y, 8, 1, PX(-1,y) ); }
+static void pred_chroma_v( pixel *src, int h )
+{
+    for( int y = 0; y < h; y++ )
+        for( int x = 0; x < 8; x++ )
+            PX(x,y) = PX(x,-1);
+}
+/* predict_8x8c_p, predict.c:282-308 */
+static void pred_8x8c_p( pixel *src )
+{
+    int H = 0, V = 0;
+    for( int i = 0; i < 4; i++ )
+    {
+        H += (i + 1) * (PX(4+i,-1) - PX(2-i,-1));
+        V += (i + 1) * (PX(-1,4+i) - PX(-1,2-i));
+    }
+    const int a = 16 * (PX(-1,7) + PX(7,-1));
+    const int b = (17*H + 16) >> 5, c = (17*V + 16) >> 5;
+    for( int y = 0; y < 8; y++ )
+        for( int x = 0; x < 8; x++ )
+            PX(x,y) = clip_pixel( (a - 3*b - 3*c + 16 + b*x + c*y) >> 5 );
+}
+
+/* predict_8x8_filter (predict.c:632-676): edge[7..14] = l7..l0, edge[15] = lt,
+ * edge[16..31] = t0..t15, edge[32] = t15, low-pass filtered.  MB_LEFT = 1,
+ * MB_TOP = 2, MB_TOPRIGHT = 4, MB_TOPLEFT = 8 (reference common/macroblock.h). */
+void FN(predict_8x8_filter)( const pixel *src, pixel edge[36], int i_neighbor, int i_filters )
+{
+    const int have_lt = i_neighbor & 8;
+    if( i_filters & 1 )
+    {
+        edge[15] = F2( PX(0,-1), PX(-1,-1), PX(-1,0) );
+        edge[14] = F2( have_lt ? PX(-1,-1) : PX(-1,0), PX(-1,0), PX(-1,1) );
+        for( int y = 1; y < 7; y++ )
+            edge[14-y] = F2( PX(-1,y-1), PX(-1,y), PX(-1,y+1) );
+        edge[6] = edge[7] = (PX(-1,6) + 3*PX(-1,7) + 2) >> 2;
+    }
+    if( i_filters & 2 )
+    {
+        const int have_tr = i_neighbor & 4;
+        edge[16] = F2( have_lt ? PX(-1,-1) : PX(0,-1), PX(0,-1), PX(1,-1) );
+        for( int x = 1; x < 7; x++ )
+            edge[16+x] = F2( PX(x-1,-1), PX(x,-1), PX(x+1,-1) );
+        edge[23] = F2( PX(6,-1), PX(7,-1), have_tr ? PX(8,-1) : PX(7,-1) );
+        if( i_filters & 4 )
+        {
+            if( have_tr )
+            {
+                for( int x = 8; x < 15; x++ )
+                    edge[16+x] = F2( PX(x-1,-1), PX(x,-1), PX(x+1,-1) );
+                edge[31] = edge[32] = (PX(14,-1) + 3*PX(15,-1) + 2) >> 2;
+            }
+            else
+                for( int i = 24; i < 33; i++ )
+                    edge[i] = PX(7,-1);
+        }
+    }
+}
+
+/* predict_8x8_{v,h,dc,ddl,ddr,vr,hd,vl,hu} (predict.c:716-883) in the
+ * H.264 8.3.2.2 form: with l_y = edge[14-y], lt = edge[15], t_x = edge[16+x],
+ * each mode is a function of zVR = 2x-y, zHD = 2y-x or x+y walking along
+ * the edge array; tests/golden/intra8x8_golden.npz pins every mode against
+ * the reference's own per-pixel assignment lists. */
+static int pred8x8_px( int mode, const pixel *e, int x, int y )
+{
+    int z, c;
+    switch( mode )
+    {
+        case 0: return e[16+x];                                           /* V   */
+        case 1: return e[14-y];                                           /* H   */
+        case 3: z = x + y;                                                /* DDL */
+            return F2( e[16+z], e[17+z], e[16 + (z + 2 < 15 ? z + 2 : 15)] );
+        case 4:                                                           /* DDR */
+            c = x > y ? 15 + x - y : 15 - (y - x);
+            return F2( e[c-1], e[c], e[c+1] );
+        case 5: z = 2*x - y;                                              /* VR  */
+            if( z < 0 ) { c = 16 + z; return F2( e[c-1], e[c], e[c+1] ); }
+            if( !(z & 1) ) return F1( e[15 + z/2], e[16 + z/2] );
+            c = 15 + (z + 1)/2; return F2( e[c-1], e[c], e[c+1] );
+        case 6: z = 2*y - x;                                              /* HD  */
+            if( z < 0 ) { c = 14 - z; return F2( e[c-1], e[c], e[c+1] ); }
+            if( !(z & 1) ) return F1( e[15 - z/2], e[14 - z/2] );
+            c = 15 - (z + 1)/2; return F2( e[c-1], e[c], e[c+1] );
+        case 7: c = 16 + x + (y >> 1);                                    /* VL  */
+            return (y & 1) ? F2( e[c], e[c+1], e[c+2] ) : F1( e[c], e[c+1] );
+        case 8: z = x + 2*y;                                              /* HU  */
+            if( z > 13 ) return e[7];
+            if( z == 13 ) return F2( e[8], e[7], e[7] );
+            c = 14 - (z >> 1);
+            return (z & 1) ? F2( e[c], e[c-1], e[c-2] ) : F1( e[c], e[c-1] );
+    }
+    return 0;
+}
+void FN(predict_8x8)( int mode, pixel *src, const pixel edge[36] )
+{
+    if( mode == 2 )
+    {
+        int s = 8;
+        for( int i = 0; i < 8; i++ )
+            s += edge[14-i] + edge[16+i];
+        fill_rect( src, 0, 0, 8, 8, s >> 4 );
+        return;
+    }
+    for( int y = 0; y < 8; y++ )
+        for( int x = 0; x < 8; x++ )
+            PX(x,y) = pred8x8_px( mode, edge, x, y );
+}
+
+/* the non-8x8 predictors by (size kind, mode); kind X264HIP_INTRA_*:
+ * 0 = 4x4, 1 = 8x8c, 2 = 8x16c, 3 = 16x16; modes in the reference's I_PRED_*
+ * numbering (16x16 / 4x4: 0 V, 1 H, 2 DC; chroma: 0 DC, 1 H, 2 V, 3 P) */
+void FN(predict)( int kind, int mode, pixel *src )
+{
+    const int n = kind == 0 ? 4 : 16;
+    if( kind == 0 || kind == 3 )
+    {
+        if( mode == 0 ) pred_sq_v( src, n );
+        else if( mode == 1 ) pred_sq_h( src, n );
+        else pred_sq_dc( src, n );
+        return;
+    }
+    const int h = kind == 1 ? 8 : 16;
+    if( mode == 0 ) pred_chroma_dc( src, h );
+    else if( mode == 1 ) pred_chroma_h( src, h );
+    else if( mode == 2 ) pred_chroma_v( src, h );
+    else pred_8x8c_p( src );
+}
+
+/* intra_{sad,satd}_x3_{4x4,8x8c,8x16c,16x16} and intra_{sad,sa8d}_x3_8x8
+ * (pixel.c:518-560): res[k] = cmp( prediction k, fenc ) with the mode order
+ * v,h,dc (4x4, 16x16, 8x8 from edge[]) or dc,h,v (chroma).  kind 4 = 8x8 luma:
+ * fdec is then the 36-entry edge array.  The reference C writes its last
+ * prediction into fdec; this restatement works on a private copy. */
+void FN(intra_x3)( int kind, int op, const pixel *fenc, const pixel *fdec, int res[3] )
+{
+    static const uint8_t ipix[5] = { 6, 3, 2, 0, 3 };
+    pixel buf[17 * FDEC_STRIDE];
+    pixel *src = buf + FDEC_STRIDE + 8;
+    const int bw = kind == 0 ? 4 : kind == 3 ? 16 : 8, bh = kind == 0 ? 4 : kind == 1 || kind == 4 ? 8 : 16;
+    if( kind != 4 )
+        for( int y = -1; y < bh; y++ )
+            for( int x = -1; x < bw; x++ )
+                PX(x,y) = fdec[x + y*FDEC_STRIDE];
+    for( int k = 0; k < 3; k++ )
+    {
+        if( kind == 4 )
+            FN(predict_8x8)( k, src, fdec );
+        else
+            FN(predict)( kind, k, src );
+        const int i_pixel = ipix[kind];
+        res[k] = op == 0 ? FN(sad)( i_pixel, src, FDEC_STRIDE, fenc, FENC_STRIDE )
+               : op == 3 ? FN(sa8d)( i_pixel, src, FDEC_STRIDE, fenc, FENC_STRIDE )
+               :           FN(satd)( i_pixel, src, FDEC_STRIDE, fenc, FENC_STRIDE );
+    }
+}
+
+/* slicetype_mb_cost's intra leg (encoder/slicetype.c:714-757) for every 8x8
+ * block of one lowres plane (plane at (0,0), 32 pixels of border).  satd = the
+ * mbcmp choice of encoder.c:1411 (!lossless && subme > 1), all_modes =
+ * subme > 1: DC/H/V chroma-style, then planar and the six directional 8x8
+ * modes over the filtered edge.  Costs: ((min + 5*lambda) >> (BIT_DEPTH-8)) + 4
+ * into intra_cost[mb]; row_satd[y] sums the AQ-scaled cost of row y (inv_qscale
+ * NULL = AQ off) and est[0] / est[1] the plain / AQ costs of the frame-score
+ * MBs (slicetype.c:532-534, 751-756), every MB computed (do_edges). */
+void FN(lowres_intra_cost)( const pixel *plane, intptr_t stride, int mb_width, int mb_height, int satd,
+                            int all_modes, int lambda, const uint16_t *inv_qscale, uint16_t *intra_cost,
+                            int32_t *row_satd, int32_t est[2] )
+{
+    pixel fenc[8 * FENC_STRIDE], buf[9 * FDEC_STRIDE], edge[36];
+    pixel *src = buf + FDEC_STRIDE + 8;
+    est[0] = est[1] = 0;
+    for( int mby = 0; mby < mb_height; mby++ )
+    {
+        row_satd[mby] = 0;
+        for( int mbx = 0; mbx < mb_width; mbx++ )
+        {
+            const pixel *s = plane + 8*mbx + 8*mby*stride;
+            for( int y = 0; y < 8; y++ )
+                memcpy( fenc + y*FENC_STRIDE, s + y*stride, 8 * sizeof(pixel) );
+            for( int x = 0; x < 16; x++ )
+                PX(x,-1) = s[x - stride];
+            for( int y = -1; y < 8; y++ )
+                PX(-1,y) = s[y*stride - 1];
+            int cost = 1 << 30;
+            for( int k = 0; k < 3; k++ )
+            {
+                FN(predict)( 1, k, src );
+                const int c = satd ? FN(satd)( 3, src, FDEC_STRIDE, fenc, FENC_STRIDE )
+                                   : FN(sad)( 3, src, FDEC_STRIDE, fenc, FENC_STRIDE );
+                cost = c < cost ? c : cost;
+            }
+            if( all_modes )
+            {
+                pred_8x8c_p( src );
+                int c = satd ? FN(satd)( 3, fenc, FENC_STRIDE, src, FDEC_STRIDE )
+                             : FN(sad)( 3, fenc, FENC_STRIDE, src, FDEC_STRIDE );
+                cost = c < cost ? c : cost;
+                FN(predict_8x8_filter)( src, edge, 15, 15 );
+                for( int m = 3; m < 9; m++ )
+                {
+                    FN(predict_8x8)( m, src, edge );
+                    c = satd ? FN(satd)( 3, fenc, FENC_STRIDE, src, FDEC_STRIDE )
+                             : FN(sad)( 3, fenc, FENC_STRIDE, src, FDEC_STRIDE );
+                    cost = c < cost ? c : cost;
+                }
+            }
+            cost = ((cost + 5 * lambda) >> (BIT_DEPTH - 8)) + 4;
+            const int mb = mbx + mby * mb_width;
+            intra_cost[mb] = cost;
+            const int aq = inv_qscale ? (cost * inv_qscale[mb] + 128) >> 8 : cost;
+            row_satd[mby] += aq;
+            if( (mbx > 0 && mbx < mb_width - 1 && mby > 0 && mby < mb_height - 1) || mb_width <= 2 || mb_height <= 2 )
+            {
+                est[0] += cost;
+                est[1] += aq;
+            }
+        }
+    }
+}
+#undef PX
+#undef F1
+#undef F2

@@ -101,6 +101,11 @@ for _bd in (8, 10):
     _f(_bd, "cqm_dequant", [_P, C.c_int, _P, _P])
     _f(_bd, "frame_init_lowres", [_P, _IP, C.c_int, C.c_int, _P, _IP])
     _f(_bd, "mb_dequant_idct_add", [C.c_int, _P, C.c_int, C.c_int, _P, _P, _P, _IP, _P, _IP])
+    _f(_bd, "predict_8x8_filter", [_P, _P, C.c_int, C.c_int])
+    _f(_bd, "predict_8x8", [C.c_int, _P, _P])
+    _f(_bd, "predict", [C.c_int, C.c_int, _P])
+    _f(_bd, "intra_x3", [C.c_int, C.c_int, _P, _P, _P])
+    _f(_bd, "lowres_intra_cost", [_P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
@@ -411,3 +416,40 @@ def frame_init_lowres(bd, plane, origin, stride, width, height, dst_stride):
     ptrs = (C.c_void_p * 4)(*[o.ctypes.data + (32 * dst_stride + 32) * o.itemsize for o in outs])
     fn(bd, "frame_init_lowres")(_addr(plane, origin), stride, width, height, ptrs, dst_stride)
     return [o.reshape(hl + 64, dst_stride) for o in outs]
+
+
+FDEC_STRIDE, FENC_STRIDE = 32, 16
+INTRA_SIZES = {0: (4, 4), 1: (8, 8), 2: (8, 16), 3: (16, 16), 4: (8, 8)}   # X264HIP_INTRA_* -> (w, h)
+
+
+def predict_8x8(bd, mode, edge):
+    """predict_8x8[mode] from a 36-entry edge; returns the 8x8 block"""
+    e = np.ascontiguousarray(edge, pixel_dtype(bd))
+    buf = np.zeros(9 * FDEC_STRIDE, pixel_dtype(bd))
+    fn(bd, "predict_8x8")(mode, _addr(buf, FDEC_STRIDE + 8), _addr(e))
+    return buf[FDEC_STRIDE:].reshape(8, FDEC_STRIDE)[:, 8:16].copy()
+
+
+def predict_8x8_filter(bd, fdec, off, i_neighbor=15, i_filters=15, edge=None):
+    """predict_8x8_filter on an FDEC-layout buffer at element offset off; returns edge[36]"""
+    e = np.zeros(36, pixel_dtype(bd)) if edge is None else np.ascontiguousarray(edge, pixel_dtype(bd)).copy()
+    fn(bd, "predict_8x8_filter")(_addr(fdec, off), _addr(e), i_neighbor, i_filters)
+    return e
+
+
+def intra_x3(bd, kind, op, fenc, f_off, fdec, d_off):
+    """intra_*_x3 of kind X264HIP_INTRA_* (fenc stride 16, fdec stride 32 or edge[36] for kind 4)"""
+    out = np.zeros(3, np.int32)
+    fn(bd, "intra_x3")(kind, op, _addr(fenc, f_off), _addr(fdec, d_off), _addr(out))
+    return out
+
+
+def lowres_intra_cost(bd, plane, origin, stride, mbw, mbh, satd=True, all_modes=True, lam=4, inv_qscale=None):
+    """slicetype_mb_cost's intra leg over one lowres plane: (intra_cost u16 [mbh*mbw], row_satd, est[2])"""
+    cost = np.zeros(mbw * mbh, np.uint16)
+    rows = np.zeros(mbh, np.int32)
+    est = np.zeros(2, np.int32)
+    iq = None if inv_qscale is None else np.ascontiguousarray(inv_qscale, np.uint16)
+    fn(bd, "lowres_intra_cost")(_addr(plane, origin), stride, mbw, mbh, int(satd), int(all_modes), lam,
+                                None if iq is None else _addr(iq), _addr(cost), _addr(rows), _addr(est))
+    return cost, rows, est

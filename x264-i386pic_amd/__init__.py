@@ -41,6 +41,8 @@ IDCT_IN_SIZE = [16, 64, 256, 4, 16, 64, 256]
 DEQUANT_4x4, DEQUANT_8x8, DEQUANT_4x4_DC = 0, 1, 2
 COEF_DECIMATE15, COEF_DECIMATE16, COEF_DECIMATE64, COEF_LAST4, COEF_LAST8, COEF_LAST15, COEF_LAST16, COEF_LAST64 = range(8)
 ZIGZAG_SUB_4x4, ZIGZAG_SUB_4x4AC, ZIGZAG_SUB_8x8 = 0, 1, 2
+INTRA_4x4, INTRA_8x8C, INTRA_8x16C, INTRA_16x16, INTRA_8x8 = range(5)
+INTRA_SIZES = [(4, 4), (8, 8), (8, 16), (16, 16), (8, 8)]
 DC_I4x4 = 2
 DCT_SUB4x4, DCT_SUB8x8, DCT_SUB16x16, DCT_SUB8x8_DC, DCT_SUB8x16_DC, DCT_SUB8x8_8, DCT_SUB16x16_8 = range(7)
 DCT_OUT_SIZE = [16, 64, 256, 4, 8, 64, 256]
@@ -113,6 +115,7 @@ ZSCAN_T = _c.CFUNCTYPE(None, _P, _P)
 ZSUB_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P)
 ZSUBAC_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P, _P)
 ZINTER_T = _c.CFUNCTYPE(None, _P, _P, _P)
+INTRA_X3_T = _c.CFUNCTYPE(None, _P, _P, _P)                        # intra_*_x3(fenc, fdec|edge, res[3])
 
 
 class PixelFunctions(_c.Structure):
@@ -126,13 +129,13 @@ class PixelFunctions(_c.Structure):
         ("ssim_4x4x2_core", _P), ("ssim_end4", _P),
         ("sad_x3", CMP_X3_T * 7), ("sad_x4", CMP_X4_T * 7),
         ("satd_x3", CMP_X3_T * 7), ("satd_x4", CMP_X4_T * 7), ("ads", ADS_T * 7),
-    ] + [(n, _P) for n in (
+    ] + [(n, INTRA_X3_T) for n in (
         "intra_mbcmp_x3_16x16", "intra_satd_x3_16x16", "intra_sad_x3_16x16",
         "intra_mbcmp_x3_4x4", "intra_satd_x3_4x4", "intra_sad_x3_4x4",
         "intra_mbcmp_x3_chroma", "intra_satd_x3_chroma", "intra_sad_x3_chroma",
         "intra_mbcmp_x3_8x16c", "intra_satd_x3_8x16c", "intra_sad_x3_8x16c",
         "intra_mbcmp_x3_8x8c", "intra_satd_x3_8x8c", "intra_sad_x3_8x8c",
-        "intra_mbcmp_x3_8x8", "intra_sa8d_x3_8x8", "intra_sad_x3_8x8",
+        "intra_mbcmp_x3_8x8", "intra_sa8d_x3_8x8", "intra_sad_x3_8x8")] + [(n, _P) for n in (
         "intra_mbcmp_x9_4x4", "intra_satd_x9_4x4", "intra_sad_x9_4x4",
         "intra_mbcmp_x9_8x8", "intra_sa8d_x9_8x8", "intra_sad_x9_8x8")]
 
@@ -273,6 +276,11 @@ def _declare(L):
         f("zigzag_interleave_batch").argtypes = [_P, _P, _P, _c.c_int, _P]
         f("frame_init_lowres").argtypes = [_P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P, _IP, _IP, _P]
         f("frame_init_lowres").restype = _c.c_int
+        f("intra_cmp_x3_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _IP, _P, _P, _c.c_int, _P, _P]
+        f("intra_cmp_x3_batch").restype = _c.c_int
+        f("lowres_intra_cost").argtypes = [_P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                           _c.c_int, _P, _P, _P, _P, _P]
+        f("lowres_intra_cost").restype = _c.c_int
         f("mb_dequant_idct_add").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _IP, _IP,
                                              _P, _IP, _IP, _P]
         for n in ("add_idct_batch", "dequant_batch", "idct_dequant_2x4_batch", "optimize_chroma_dc_batch",
@@ -542,6 +550,43 @@ def frame_init_lowres(planes, origin, stride, width, height, outs=None):
         _ptr(planes, origin), stride, planes[0].numel(), width, height, n, ptrs, ls, outs[0][0].numel(), _stream()),
         "frame_init_lowres")
     return outs, ls
+
+
+def intra_cmp_x3_batch(kind, op, fenc, fenc_stride, fdec, fdec_stride, fenc_off, fdec_off, out=None):
+    """int32 [n, 3] = intra_*_x3 of kind INTRA_* per block (fdec_off: the block's (0,0) in fdec, or the
+    start of its 36-entry edge for INTRA_8x8)."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = fenc_off.numel()
+    if out is None:
+        out = torch.empty((n, 3), dtype=torch.int32, device=fenc.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_intra_cmp_x3_batch")(
+        kind, op, _ptr(fenc), fenc_stride, _ptr(fdec), fdec_stride, _ptr(fenc_off), _ptr(fdec_off), n,
+        _ptr(out), _stream()), "intra_cmp_x3_batch")
+    return out
+
+
+def lowres_intra_cost(lowres, lowres_stride, mb_width, mb_height, satd=True, all_modes=True, lam=4,
+                      inv_qscale=None, with_rows=True, outs=None):
+    """The lookahead's intra estimate of every lowres plane in `lowres` [n, rows, stride] (lowres[0] of
+    frame_init_lowres, (0,0) at (PAD, PAD)): (intra_cost uint16-as-int16 [n, mbh*mbw],
+    row_satd int32 [n, mbh], cost_est int32 [n, 2])."""
+    import torch
+    bd = _pix_bd(lowres)
+    n = lowres.shape[0]
+    dev = lowres.device
+    if outs is not None:
+        cost, rows, est = outs
+    else:
+        cost = torch.empty((n, mb_width * mb_height), dtype=torch.int16, device=dev)
+        rows = torch.empty((n, mb_height), dtype=torch.int32, device=dev) if with_rows else None
+        est = torch.empty((n, 2), dtype=torch.int32, device=dev) if with_rows else None
+    _rc(getattr(lib(), f"x264hip_{bd}_lowres_intra_cost")(
+        _ptr(lowres, PAD * lowres_stride + PAD), lowres_stride, lowres[0].numel(), mb_width, mb_height, n,
+        int(bool(satd)), int(bool(all_modes)), lam, _ptr(inv_qscale) if inv_qscale is not None else None,
+        _ptr(cost), _ptr(rows) if rows is not None else None, _ptr(est) if est is not None else None,
+        _stream()), "lowres_intra_cost")
+    return cost, rows, est
 
 
 def plane_stride(width, pad=PAD):

@@ -635,6 +635,39 @@ template <int BD> static int c_quant_2x2_dc( typename PT<BD>::dctcoef dct[4], in
 { return quant_call<BD, X264HIP_QUANT_2x2_DC, 4, 0>( dct, nullptr, nullptr, mf, bias ); }
 
 // ============================================================ table initialisers
+// intra_*_x3 (pixel.c:518-560): fenc (FENC_STRIDE) and the block's row -1 /
+// column -1 neighbours (FDEC_STRIDE) staged into one (W+1)x(H+1) tile, or the
+// 36-entry edge for the 8x8 luma kind
+template <int BD, int KIND, int OP>
+static void c_intra_x3( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *fdec, int res[3] )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int W = KIND == 0 ? 4 : KIND == 3 ? 16 : 8, H = KIND == 0 ? 4 : KIND == 1 || KIND == 4 ? 8 : 16;
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
+    int64_t *off = (int64_t *)(c.host + ST_OFF);
+    int32_t *sc = (int32_t *)(c.host + ST_SC);
+    stage_block( a, fenc, X264HIP_FENC_STRIDE, W, H );
+    const intptr_t ds = W + 1;
+    if( KIND == 4 )
+    {
+        memcpy( b, fdec, 36 * sizeof(pixel) );
+        off[1] = 0;
+    }
+    else
+    {
+        stage_block( b, fdec - X264HIP_FDEC_STRIDE - 1, X264HIP_FDEC_STRIDE, W + 1, H + 1 );
+        off[1] = ds + 1;
+    }
+    off[0] = 0;
+    CHECK_FATAL( launch_intra_x3<BD>( KIND, OP, dview( c, a ), W, dview( c, b ), ds, dview( c, off ),
+                                      dview( c, off + 1 ), 1, dview( c, sc ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    res[0] = sc[0];
+    res[1] = sc[1];
+    res[2] = sc[2];
+}
+
 template <int BD, typename Tab>
 static void fill_pixel( Tab *pf )
 {
@@ -681,6 +714,17 @@ static void fill_pixel( Tab *pf )
     pf->ads[4] = c_ads<4>;
     pf->ads[5] = c_ads<5>;
     pf->ads[6] = c_ads<6>;
+    // intra_*_x3, pixel.c:869-878 (the intra_mbcmp_* aliases are the encoder's, encoder.c:1409-1420)
+    pf->intra_sad_x3_4x4 = c_intra_x3<BD, X264HIP_INTRA_4x4, X264HIP_CMP_SAD>;
+    pf->intra_satd_x3_4x4 = c_intra_x3<BD, X264HIP_INTRA_4x4, X264HIP_CMP_SATD>;
+    pf->intra_sad_x3_8x8 = c_intra_x3<BD, X264HIP_INTRA_8x8, X264HIP_CMP_SAD>;
+    pf->intra_sa8d_x3_8x8 = c_intra_x3<BD, X264HIP_INTRA_8x8, X264HIP_CMP_SA8D>;
+    pf->intra_sad_x3_8x8c = c_intra_x3<BD, X264HIP_INTRA_8x8C, X264HIP_CMP_SAD>;
+    pf->intra_satd_x3_8x8c = c_intra_x3<BD, X264HIP_INTRA_8x8C, X264HIP_CMP_SATD>;
+    pf->intra_sad_x3_8x16c = c_intra_x3<BD, X264HIP_INTRA_8x16C, X264HIP_CMP_SAD>;
+    pf->intra_satd_x3_8x16c = c_intra_x3<BD, X264HIP_INTRA_8x16C, X264HIP_CMP_SATD>;
+    pf->intra_sad_x3_16x16 = c_intra_x3<BD, X264HIP_INTRA_16x16, X264HIP_CMP_SAD>;
+    pf->intra_satd_x3_16x16 = c_intra_x3<BD, X264HIP_INTRA_16x16, X264HIP_CMP_SATD>;
 #undef SIZES8
 #undef SIZES7
 }
@@ -911,6 +955,31 @@ static int map_err( hipError_t e, const char *where )
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_ads_batch( i_pixel, enc_dc, sums, delta, sums_off, cost, cost_off, width, thresh, n,  \
                                           mvs, mvs_pitch, nmv, (hipStream_t)stream ), "ads_batch" );                 \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_intra_cmp_x3_batch( int kind, int op, const PT<BD>::pixel *fenc, intptr_t fs,     \
+                                                      const PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fo,    \
+                                                      const int64_t *dof, int n, int32_t *scores, void *stream )    \
+    {                                                                                                                \
+        const bool ok = kind >= 0 && kind <= 4 &&                                                                    \
+                        ( op == X264HIP_CMP_SAD || ( kind == 4 ? op == X264HIP_CMP_SA8D : op == X264HIP_CMP_SATD ) ); \
+        if( !ok || n < 0 || ( n > 0 && ( !fenc || !fdec || !fo || !dof || !scores ) ) )                             \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_intra_x3<BD>( kind, op, fenc, fs, fdec, ds, fo, dof, n, scores,                       \
+                                             (hipStream_t)stream ), "intra_cmp_x3_batch" );                          \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_lowres_intra_cost( const PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride, \
+                                                     int mbw, int mbh, int nframes, int satd, int all_modes,        \
+                                                     int lambda, const uint16_t *invq, uint16_t *cost,              \
+                                                     int32_t *row_satd, int32_t *est, void *stream )                \
+    {                                                                                                                \
+        if( mbw < 0 || mbh < 0 || nframes < 0 || lambda < 0 || ( (uintptr_t)plane & 3 ) ||                          \
+            ( ( stride * (intptr_t)sizeof(PT<BD>::pixel) ) & 3 ) ||                                                 \
+            ( ( fstride * (intptr_t)sizeof(PT<BD>::pixel) ) & 3 ) || stride < 8 * mbw + 64 ||                      \
+            ( (int64_t)mbw * mbh * nframes > 0 && ( !plane || !cost ) ) )                                            \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_lowres_intra<BD>( plane, stride, fstride, mbw, mbh, nframes, satd, all_modes, lambda, \
+                                                 invq, cost, row_satd, est, (hipStream_t)stream ),                   \
+                        "lowres_intra_cost" );                                                                       \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_frame_integral( const PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride,    \
                                                   int lines, int padh, int sub8x8, int nframes, uint16_t *integral,  \

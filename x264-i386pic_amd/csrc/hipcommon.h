@@ -87,22 +87,22 @@ __device__ __forceinline__ x264hip_short2 pair_px( const uint32_t (&r)[8 / PT<BD
     return __builtin_bit_cast( x264hip_short2, v );
 }
 
-template <int BD>
-__device__ __forceinline__ uint32_t satd8x4_packed( const uint32_t (&a)[4][8 / PT<BD>::PPD],
-                                                    const uint32_t (&b)[4][8 / PT<BD>::PPD] )
+// SATD of two 4x4 tiles held in paired columns (x, x+4) of four rows of
+// differences p[y][x], accumulated onto acc.  The caller adds 0x8000 to p[0][0]
+// (both halves): every Hadamard coefficient has +-1 weight on that element, so
+// each coefficient then carries the same 0x8000 bias mod 2^16 and one
+// v_sad_u16 against 0x8000 adds |coef| of two coefficients -- no negate / max /
+// dot per output.  Exact while |coef| < 2^15 (<= 16 * 1023 here).
+__device__ __forceinline__ uint32_t had_sad_pairs( const x264hip_short2 (&p)[4][4], uint32_t acc )
 {
     x264hip_short2 d[4][4];
 #pragma unroll
     for( int y = 0; y < 4; y++ )
     {
-        x264hip_short2 p[4];
-#pragma unroll
-        for( int x = 0; x < 4; x++ )
-            p[x] = pair_px<BD>( a[y], x ) - pair_px<BD>( b[y], x );
-        const x264hip_short2 t0 = p[0] + p[1], t1 = p[0] - p[1], t2 = p[2] + p[3], t3 = p[2] - p[3];
+        const x264hip_short2 t0 = p[y][0] + p[y][1], t1 = p[y][0] - p[y][1];
+        const x264hip_short2 t2 = p[y][2] + p[y][3], t3 = p[y][2] - p[y][3];
         d[y][0] = t0 + t2; d[y][2] = t0 - t2; d[y][1] = t1 + t3; d[y][3] = t1 - t3;
     }
-    uint32_t s = 0;
 #pragma unroll
     for( int x = 0; x < 4; x++ )
     {
@@ -111,13 +111,28 @@ __device__ __forceinline__ uint32_t satd8x4_packed( const uint32_t (&a)[4][8 / P
         const x264hip_short2 c[4] = { t0 + t2, t0 - t2, t1 + t3, t1 - t3 };
 #pragma unroll
         for( int k = 0; k < 4; k++ )
-        {
-            const x264hip_short2 m = __builtin_elementwise_max( c[k], (x264hip_short2)0 - c[k] );
-            s = __builtin_amdgcn_udot2( __builtin_bit_cast( unsigned short __attribute__( ( ext_vector_type( 2 ) ) ), m ),
-                                        (unsigned short __attribute__( ( ext_vector_type( 2 ) ) ))1, s, false );
-        }
+            acc = __builtin_amdgcn_sad_u16( __builtin_bit_cast( uint32_t, c[k] ), 0x80008000u, acc );
     }
-    return s;
+    return acc;
+}
+
+__device__ __forceinline__ x264hip_short2 sat_bias( x264hip_short2 v )
+{
+    return __builtin_bit_cast( x264hip_short2, __builtin_bit_cast( uint32_t, v ) ^ 0x80008000u );
+}
+
+template <int BD>
+__device__ __forceinline__ uint32_t satd8x4_packed( const uint32_t (&a)[4][8 / PT<BD>::PPD],
+                                                    const uint32_t (&b)[4][8 / PT<BD>::PPD] )
+{
+    x264hip_short2 p[4][4];
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+#pragma unroll
+        for( int x = 0; x < 4; x++ )
+            p[y][x] = pair_px<BD>( a[y], x ) - pair_px<BD>( b[y], x );
+    p[0][0] = sat_bias( p[0][0] );
+    return had_sad_pairs( p, 0 );
 }
 
 // value stored to a dctcoef (int16 wrap at 8 bit), read back as int
@@ -236,4 +251,12 @@ template <int BD>
 hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t stride, intptr_t fstride, int width,
                                      int height, int nframes, typename PT<BD>::pixel *const dst[4], intptr_t ds,
                                      intptr_t dfs, hipStream_t stream );
+template <int BD>
+hipError_t launch_intra_x3( int kind, int op, const typename PT<BD>::pixel *fenc, intptr_t fs,
+                            const typename PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fo,
+                            const int64_t *dof, int n, int32_t *scores, hipStream_t stream );
+template <int BD>
+hipError_t launch_lowres_intra( const typename PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride, int mbw,
+                                int mbh, int nframes, int satd, int all_modes, int lambda, const uint16_t *invq,
+                                uint16_t *cost, int32_t *row_satd, int32_t *est, hipStream_t stream );
 } // namespace x264hip
