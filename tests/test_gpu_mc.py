@@ -43,9 +43,11 @@ def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("op", [0, 2])
-@pytest.mark.parametrize("variant", ["default", "2"])
+@pytest.mark.parametrize("variant", ["default", "1", "2", "3", "5"])
 def test_subpel_cmp_random(hip, oracle, bd, op, variant, monkeypatch):
-    """X264HIP_SUBPEL_VARIANT: default = lane per candidate, 2 = row-per-lane SATD for 8/16-wide blocks."""
+    """X264HIP_SUBPEL_VARIANT (lane per candidate unless noted): 1 = dwordx2 + dword loads
+    with a per-row branch, 2 = row-per-lane SATD for 8/16-wide blocks, 3 = unaligned
+    multi-dword row loads (8-bit default), 5 = dword-aligned loads + alignbyte (10-bit default)."""
     if variant == "default":
         monkeypatch.delenv("X264HIP_SUBPEL_VARIANT", raising=False)
     else:

@@ -403,7 +403,6 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_kernel( const typename PT<
                                                               typename PT<BD>::dctcoef *__restrict__ dct,
                                                               int32_t *__restrict__ nz )
 {
-    using dctcoef = typename PT<BD>::dctcoef;
     constexpr int LPM = T == 4 ? 16 : 4;      // lanes per macroblock
     const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)nframes * mbh * mbw * LPM;

@@ -496,6 +496,184 @@ __global__ __launch_bounds__( 256 ) void subpel_satd_rows_kernel( const typename
         scores[i] = (int)(acc >> 1);
 }
 
+// Variant 3 (default): lane per candidate like variant 1, without its per-row
+// branch and realignment.  The second plane pointer equals the first when the
+// qpel phase needs one plane (avg(a, a) = a), so every band's rows are issued
+// as one burst of loads; rows are fetched with unaligned 4/8/16-byte global
+// loads (amdhsa runs with unaligned access enabled: no alignbyte); the 8-bit
+// rounding average is one v_lerp_u8 per dword (pixel_avg, mc.c:57).
+template <int BD> __device__ __forceinline__ uint32_t avg_round( uint32_t a, uint32_t b )
+{
+    if constexpr( BD == 8 )
+        return __builtin_amdgcn_lerp( a, b, 0x01010101u );
+    else
+    {
+        // 10-bit pixels: a + b <= 2046 never carries out of a 16-bit lane
+        typedef unsigned short us2 __attribute__( ( ext_vector_type( 2 ) ) );
+        const us2 s = __builtin_bit_cast( us2, a ) + __builtin_bit_cast( us2, b ) + (us2)1;
+        return __builtin_bit_cast( uint32_t, s >> (us2)1 );
+    }
+}
+
+template <int NDW> __device__ __forceinline__ void load_row_u( const void *p, uint32_t (&out)[NDW] )
+{
+    if constexpr( NDW == 1 )
+        __builtin_memcpy( &out[0], p, 4 );
+    else if constexpr( NDW == 2 )
+    {
+        uint2 v;
+        __builtin_memcpy( &v, p, 8 );
+        out[0] = v.x; out[1] = v.y;
+    }
+    else
+    {
+#pragma unroll
+        for( int k = 0; k < NDW; k += 4 )
+        {
+            uint4 v;
+            __builtin_memcpy( &v, (const char *)p + 4 * k, 16 );
+            out[k] = v.x; out[k + 1] = v.y; out[k + 2] = v.z; out[k + 3] = v.w;
+        }
+    }
+}
+
+// Row of NDW packed dwords at an arbitrary pixel address from dword-aligned loads:
+// the NDW words of an aligned row, else the NDW + 1 words holding it realigned with
+// v_alignbyte (no byte outside the row's dwords is touched).  On gfx950 the address
+// path takes ~14.6 cycles per CU for a wave's dword-aligned dwordx2 / x3 / x4 load of
+// 8-16 bytes per lane against 28.5 (x2) and 56.8 (x4) when the lanes' addresses are
+// byte-misaligned (tools/ta_probe.hip, profiles/r01d_ta_probe.txt).
+template <int NDW>
+__device__ __forceinline__ void load_row_al( const void *p, uint32_t (&out)[NDW] )
+{
+    typedef const __attribute__( ( address_space( 1 ) ) ) uint32_t gword;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    gword *base = (gword *)((uintptr_t)p & ~(uintptr_t)3);
+    uint32_t w[NDW + 1];
+#pragma unroll
+    for( int i = 0; i < NDW; i++ )
+        w[i] = base[i];
+    w[NDW] = base[sh ? NDW : NDW - 1];      // branch-free: re-reads word NDW-1 when aligned
+#pragma unroll
+    for( int i = 0; i < NDW; i++ )
+        out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
+}
+
+template <int BD, int OP, int IPIX, int LD>
+__global__ __launch_bounds__( 256 ) void subpel_cmp3_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                             intptr_t fs, const typename PT<BD>::pixel *p0,
+                                                             const typename PT<BD>::pixel *p1,
+                                                             const typename PT<BD>::pixel *p2,
+                                                             const typename PT<BD>::pixel *p3, intptr_t rs,
+                                                             const int64_t *__restrict__ fenc_off,
+                                                             const int32_t *__restrict__ qxy, int n,
+                                                             int32_t *__restrict__ scores )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int PPD = PT<BD>::PPD;
+    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    constexpr int NDW = W / PPD;
+    constexpr int BAND = (16 / NDW) < 4 ? 4 : (16 / NDW) > H ? H : (16 / NDW);   // rows per load burst
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    const int2 q = *(const int2 *)(qxy + 2 * i);
+    const int qx = q.x, qy = q.y;
+    const int idx = ((qy & 3) << 2) + (qx & 3);
+    const intptr_t off = (intptr_t)(qy >> 2) * rs + (qx >> 2);
+    const int i0 = c_hpel_ref0[idx], i1 = c_hpel_ref1[idx];
+    const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((qy & 3) == 3) * rs;
+    const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((qx & 3) == 3);
+    if( !(idx & 5) )
+        s2 = s1;
+    const pixel *a = fenc + fenc_off[i];
+    uint32_t acc = 0;
+    int sum = 0;
+#pragma unroll
+    for( int ty = 0; ty < H; ty += BAND )
+    {
+        uint32_t fr[BAND][NDW], rr[BAND][NDW], r2[BAND][NDW];
+#pragma unroll
+        for( int y = 0; y < BAND; y++ )
+        {
+            if constexpr( LD == 0 )
+            {
+                load_row_u<NDW>( a + (ty + y) * fs, fr[y] );
+                load_row_u<NDW>( s1 + (ty + y) * rs, rr[y] );
+                load_row_u<NDW>( s2 + (ty + y) * rs, r2[y] );
+            }
+            else
+            {
+                load_row_al<NDW>( a + (ty + y) * fs, fr[y] );
+                load_row_al<NDW>( s1 + (ty + y) * rs, rr[y] );
+                load_row_al<NDW>( s2 + (ty + y) * rs, r2[y] );
+            }
+        }
+#pragma unroll
+        for( int y = 0; y < BAND; y++ )
+#pragma unroll
+            for( int k = 0; k < NDW; k++ )
+                rr[y][k] = avg_round<BD>( rr[y][k], r2[y][k] );
+        if constexpr( OP == 0 )
+        {
+#pragma unroll
+            for( int y = 0; y < BAND; y++ )
+#pragma unroll
+                for( int k = 0; k < NDW; k++ )
+                    acc = sadp<BD>( fr[y][k], rr[y][k], acc );
+        }
+        else if constexpr( W >= 8 )
+        {
+#pragma unroll
+            for( int by = 0; by < BAND; by += 4 )
+#pragma unroll
+                for( int tx = 0; tx < W; tx += 8 )
+                {
+                    uint32_t fa[4][8 / PPD], ra[4][8 / PPD];
+#pragma unroll
+                    for( int y = 0; y < 4; y++ )
+#pragma unroll
+                        for( int k = 0; k < 8 / PPD; k++ )
+                        {
+                            fa[y][k] = fr[by + y][tx / PPD + k];
+                            ra[y][k] = rr[by + y][tx / PPD + k];
+                        }
+                    acc += satd8x4_packed<BD>( fa, ra );
+                }
+        }
+        else
+        {
+#pragma unroll
+            for( int by = 0; by < BAND; by += 4 )
+            {
+                int d[4][4];
+#pragma unroll
+                for( int y = 0; y < 4; y++ )
+                {
+#pragma unroll
+                    for( int x = 0; x < 4; x++ )
+                        d[y][x] = upix<BD>( fr[by + y][x / PPD], x % PPD ) - upix<BD>( rr[by + y][x / PPD], x % PPD );
+                    int t0 = d[y][0] + d[y][1], t1 = d[y][0] - d[y][1], t2 = d[y][2] + d[y][3], t3 = d[y][2] - d[y][3];
+                    d[y][0] = t0 + t2; d[y][2] = t0 - t2; d[y][1] = t1 + t3; d[y][3] = t1 - t3;
+                }
+                int s4 = 0;
+#pragma unroll
+                for( int x = 0; x < 4; x++ )
+                {
+                    int t0 = d[0][x] + d[1][x], t1 = d[0][x] - d[1][x], t2 = d[2][x] + d[3][x], t3 = d[2][x] - d[3][x];
+                    s4 += abs( t0 + t2 ) + abs( t0 - t2 ) + abs( t1 + t3 ) + abs( t1 - t3 );
+                }
+                sum += s4 >> 1;
+            }
+        }
+    }
+    if constexpr( OP == 0 )
+        sum = (int)acc;
+    else if constexpr( W >= 8 )
+        sum = (int)(acc >> 1);
+    scores[i] = sum;
+}
+
 template <int BD>
 hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs,
                               const typename PT<BD>::pixel *const planes[4], intptr_t rs, const int64_t *fenc_off,
@@ -517,9 +695,26 @@ hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel 
         return hipGetLastError();
     }
     dim3 blk( 256 ), g( (n + 255) / 256 );
+    // variants (tools/subpel_variants.py, 4.7 M 8x8 SATD candidates of bench.py's list):
+    // 1 = the first lane-per-candidate kernel (dwordx2 + dword loads, a per-row branch for
+    // the second plane; 0.129 ms 8 bit / 0.215 ms 10 bit), 3 = unaligned multi-dword row
+    // loads (0.101 / 0.193; default at 8 bit), 5 = dword-aligned row loads + alignbyte
+    // (0.115 / 0.186; default at 10 bit, and 0.178 against 0.276 for variant 3 when the
+    // list is block-major)
+    const int var = ev ? atoi( ev ) : BD == 8 ? 3 : 5;
+    const bool v1 = var == 1;
 #define SP_CASE( OP, I )                                                                                      \
-    case I: hipLaunchKernelGGL( ( subpel_cmp_kernel<BD, OP, I> ), g, blk, 0, stream, fenc, fs, planes[0],       \
-                                planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores ); break;
+    case I:                                                                                                   \
+        if( v1 )                                                                                              \
+            hipLaunchKernelGGL( ( subpel_cmp_kernel<BD, OP, I> ), g, blk, 0, stream, fenc, fs, planes[0],     \
+                                planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores );              \
+        else if( var == 3 )                                                                                   \
+            hipLaunchKernelGGL( ( subpel_cmp3_kernel<BD, OP, I, 0> ), g, blk, 0, stream, fenc, fs, planes[0], \
+                                planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores );              \
+        else                                                                                                  \
+            hipLaunchKernelGGL( ( subpel_cmp3_kernel<BD, OP, I, 1> ), g, blk, 0, stream, fenc, fs, planes[0], \
+                                planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores );              \
+        break;
     if( op == 0 )
     {
         switch( i_pixel ) { SP_CASE( 0, 0 ) SP_CASE( 0, 1 ) SP_CASE( 0, 2 ) SP_CASE( 0, 3 ) SP_CASE( 0, 4 )
