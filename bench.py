@@ -45,6 +45,10 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=150)
     ap.add_argument("--frames", type=int, default=16, help="frame pairs per step per GPU")
+    # the streaming transform kernels (DCT+quant, reconstruction) move ~8.5 MB per 1080p
+    # frame; SURVEY.md §8d (configs[3]) asks for >= 64 frames per launch so the launch
+    # is not dominated by its ramp and tail
+    ap.add_argument("--tframes", type=int, default=64, help="frame pairs per transform launch per GPU")
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--range", type=int, default=16)
@@ -196,13 +200,20 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     bs4 = torch.from_numpy(q4b[1, 26].copy()).cuda()
     mf8 = torch.from_numpy(q8m[1, 26].copy()).cuda()
     bs8 = torch.from_numpy(q8b[1, 26].copy()).cuda()
-    nmb = F * mbw * mbh
+    # transform legs: their own TF-pair shard of the same sequence (>= 64 frames per launch)
+    from x264hip import synth, dist as xd
+    TF = a.tframes
+    t0, t1 = xd.frame_shard(world * TF, world, int(os.environ.get("RANK", "0")))
+    tplanes, _, _ = synth.make_sequence(t1 - t0 + 1, mbw * 16, mbh * 16, 8, start=t0)
+    tdev = torch.from_numpy(tplanes).cuda()
+    del tplanes
+    nmb = TF * mbw * mbh
     dct = torch.empty((nmb, 256), dtype=torch.int16, device="cuda")
     nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
     for t, mf, bs in ((4, mf4, bs4), (8, mf8, bs8)):
         def step(t=t, mf=mf, bs=bs):
-            x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, mf, bs, dct=dct, nz=nz,
-                           fenc_frame_stride=fstride, pred_frame_stride=fstride)
+            x.mb_dct_quant(t, tdev[1:], origin, stride, tdev[:-1], origin, stride, mbw, mbh, TF, mf, bs, dct=dct,
+                           nz=nz, fenc_frame_stride=fstride, pred_frame_stride=fstride)
         wall, ev_ms = timed(step, a.steps, a.warmup, world)
         blocks = nmb * (16 if t == 4 else 4)
         bpb = (16 + 16 + 32) if t == 4 else (64 + 64 + 128)     # fenc + pred in, int16 coefs out
@@ -223,23 +234,23 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     # DCT+quant step, and the lookahead's half-resolution planes
     dq4, dq8 = x.cqm_dequant([flat] * 8)
     qp_mb = torch.full((nmb,), 26, dtype=torch.int32, device="cuda")
-    recon = torch.empty_like(dev[:-1])
+    recon = torch.empty_like(tdev[:-1])
     for t, dq in ((4, dq4[1]), (8, dq8[1])):
-        x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F,
+        x.mb_dct_quant(t, tdev[1:], origin, stride, tdev[:-1], origin, stride, mbw, mbh, TF,
                        mf4 if t == 4 else mf8, bs4 if t == 4 else bs8, dct=dct, nz=nz,
                        fenc_frame_stride=fstride, pred_frame_stride=fstride)
         dqd = torch.from_numpy(dq.copy()).cuda()
 
         def rstep(t=t, dqd=dqd):
-            x.mb_dequant_idct_add(t, dct, mbw, mbh, F, dqd, qp_mb, dev[:-1], origin, stride, recon, origin, stride,
-                                  pred_frame_stride=fstride, recon_frame_stride=fstride)
+            x.mb_dequant_idct_add(t, dct, mbw, mbh, TF, dqd, qp_mb, tdev[:-1], origin, stride, recon, origin,
+                                  stride, pred_frame_stride=fstride, recon_frame_stride=fstride)
         wall, ev_ms = timed(rstep, a.steps, a.warmup, world)
         blocks = nmb * (16 if t == 4 else 4)
         bpb = (32 + 16 + 16) if t == 4 else (128 + 64 + 64)      # int16 coefs + pred in, recon out
         res["recon%d_blocks_per_s" % t] = world * a.steps * blocks / wall
         res["recon%d_hbm_frac" % t] = blocks * bpb / (ev_ms * 1e-3) / HBM_PEAK
         res["recon%d_launch_ms" % t] = ev_ms
-    del recon
+    del recon, tdev, dct, nz
     lw, lh = mbw * 16, mbh * 16
     louts, _ = x.frame_init_lowres(dev[:-1], origin, stride, lw, lh)
 
@@ -289,8 +300,9 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
 
 def rates_10bit(x, a, world, mbw, mbh, F):
-    """configs[4] side rates: 10-bit full search (v_sad_u16 path) and 10-bit fused
-    8x8 DCT + quant_8x8 (int32 coefficients) over F frame pairs of the same motion."""
+    """configs[4] side rates: 10-bit full search (v_sad_u16 path) over F frame pairs and
+    10-bit fused 8x8 DCT + quant_8x8 (int32 coefficients) over --tframes pairs of the
+    same motion."""
     from x264hip import synth, dist as xd
     R = a.range
     p0, p1 = xd.frame_shard(world * F, world, int(os.environ.get("RANK", "0")))
@@ -306,18 +318,23 @@ def rates_10bit(x, a, world, mbw, mbh, F):
     cands = F * mbw * mbh * (2 * R + 1) ** 2
     res = {"me10_candidates_per_s": world * a.steps * cands / wall, "me10_launch_ms": ev_ms,
            "me10_absdiff_frac_of_v_sad_u16_peak": cands * 256 / (ev_ms * 1e-3) / VALU_LANE_OPS}
-    del table
+    del table, dev
     flat = [16] * 64
     _, _, q8m, q8b = x.cqm_init(10, [flat] * 8)
     mf8 = torch.from_numpy(q8m[1, 26 + 12].copy()).cuda()
     bs8 = torch.from_numpy(q8b[1, 26 + 12].copy()).cuda()
-    nmb = F * mbw * mbh
+    TF = a.tframes                                  # >= 64 frames per transform launch
+    t0, t1 = xd.frame_shard(world * TF, world, int(os.environ.get("RANK", "0")))
+    tplanes, _, _ = synth.make_sequence(t1 - t0 + 1, mbw * 16, mbh * 16, 10, start=t0)
+    dev = torch.from_numpy(tplanes.view(np.int16)).cuda()
+    del tplanes
+    nmb = TF * mbw * mbh
     dct = torch.empty((nmb, 256), dtype=torch.int32, device="cuda")
     nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
 
     def dstep():
-        x.mb_dct_quant(8, dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, mf8, bs8, dct=dct, nz=nz,
-                       fenc_frame_stride=fstride, pred_frame_stride=fstride)
+        x.mb_dct_quant(8, dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, TF, mf8, bs8, dct=dct,
+                       nz=nz, fenc_frame_stride=fstride, pred_frame_stride=fstride)
     wall, ev_ms = timed(dstep, a.steps, a.warmup, world)
     blocks = nmb * 4
     res["dct8_quant10_blocks_per_s"] = world * a.steps * blocks / wall
