@@ -20,9 +20,10 @@ def _host(t, bd):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("size", [(1920, 1088), (80, 48), (176, 144)])
-@pytest.mark.parametrize("variant", ["default", "1"])
+@pytest.mark.parametrize("variant", ["default", "0", "1"])
 def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
-    """X264HIP_HPEL_VARIANT: default = fused single pass, 1 = interior tiles + border expand."""
+    """X264HIP_HPEL_VARIANT: default = streaming lanes at 8 bit (2) / fused tiles at 10 bit,
+    0 = fused single pass over LDS tiles, 1 = interior tiles + border expand."""
     if variant == "default":
         monkeypatch.delenv("X264HIP_HPEL_VARIANT", raising=False)
     else:

@@ -257,6 +257,197 @@ __global__ __launch_bounds__( 256 ) void hpel_fused_kernel( const typename PT<BD
     }
 }
 
+// Streaming variant (default at 8 bit): a lane owns 16 adjacent output columns
+// (16 bytes of each plane) of a strip of HS_ROWS rows and walks it top to bottom
+// with the 6-row source window in registers as 16-bit pixel pairs; the columns
+// beside its 16 come from the adjacent lanes through DPP wave shifts (a wave
+// covers 62 column quads plus a halo lane on each side), so a lane loads one
+// aligned 16-byte row piece per source row, stores 16-byte pieces, and no LDS is
+// used.  The vertical 6-tap runs on packed pairs (v_pk_mad: the 8-bit
+// intermediates -2550..10710 fit int16), the horizontal ones (H from pixels,
+// centre from the int16 intermediates, both mc.c:173-196) as v_dot2_i32_i16
+// chains over even-aligned pairs.  Border pixels are the filter at the clamped
+// coordinate (x in [-4, W+3], y in [-8, H+7]) as in the fused kernel: lanes are
+// laid on x = -16 + 16q, so the first / last quad replicate pixel -4 / W+3 into
+// their outer 12 columns and store one more piece for x in [-32, -16) /
+// [W+16, W+32); the first / last strip repeat rows -8 / H+7.
+typedef short hs2 __attribute__( ( ext_vector_type( 2 ) ) );
+
+__device__ __forceinline__ hs2 as_s2( uint32_t v ) { return __builtin_bit_cast( hs2, v ); }
+__device__ __forceinline__ uint32_t as_u( hs2 v ) { return __builtin_bit_cast( uint32_t, v ); }
+
+// the four outputs x..x+3 of a horizontal 6-tap over the even pairs P[J..J+4] =
+// (x-2, x-1), (x, x+1), (x+2, x+3), (x+4, x+5), (x+6, x+7), scaled by M (so the
+// clipped result lands on a byte boundary) plus bias
+template <int J, int M, int N>
+__device__ __forceinline__ void tap6_h4( const hs2 (&P)[N], int bias, int (&o)[4] )
+{
+    constexpr short A = M, B = -5 * M, C = 20 * M;
+    o[0] = __builtin_amdgcn_sdot2( P[J], (hs2){ A, B }, bias, false );
+    o[0] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ C, C }, o[0], false );
+    o[0] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ B, A }, o[0], false );
+    o[1] = __builtin_amdgcn_sdot2( P[J], (hs2){ 0, A }, bias, false );
+    o[1] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ B, C }, o[1], false );
+    o[1] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ C, B }, o[1], false );
+    o[1] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ A, 0 }, o[1], false );
+    o[2] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ A, B }, bias, false );
+    o[2] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ C, C }, o[2], false );
+    o[2] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ B, A }, o[2], false );
+    o[3] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ 0, A }, bias, false );
+    o[3] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ B, C }, o[3], false );
+    o[3] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ C, B }, o[3], false );
+    o[3] = __builtin_amdgcn_sdot2( P[J + 4], (hs2){ A, 0 }, o[3], false );
+}
+
+// four scaled filter sums clamped to [0, HI] whose byte BY is the pixel, packed
+// into the bytes of a dword with two v_perm (+ one merge)
+template <int HI, int BY> __device__ __forceinline__ uint32_t pack_clip4( const int (&o)[4] )
+{
+    uint32_t b[4];
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+        b[k] = (uint32_t)min( max( o[k], 0 ), HI );
+    // perm selector bytes 0-3 pick from the second operand, 4-7 from the first
+    constexpr uint32_t lo = (uint32_t)BY | ((uint32_t)(BY + 4) << 8) | 0x0c0c0000u;
+    constexpr uint32_t hi = 0x0c0c | ((uint32_t)BY << 16) | ((uint32_t)(BY + 4) << 24);
+    return __builtin_amdgcn_perm( b[1], b[0], lo ) | __builtin_amdgcn_perm( b[3], b[2], hi );
+}
+
+template <int HS_ROWS>
+__global__ __launch_bounds__( 256 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
+                                                             uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                             intptr_t stride, intptr_t fstride, int width,
+                                                             int height, int hbias, int cbias )
+{
+    const int lane = threadIdx.x & 63;
+    const int nq = (width + 32) >> 4;                       // column quads over x in [-16, W+16)
+    const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if( chunk * 62 >= nq )
+        return;                                              // wave-uniform
+    const int q = chunk * 62 - 1 + lane;
+    const bool st = lane >= 1 && lane <= 62 && q < nq;
+    const int x0 = -16 + 16 * min( max( q, -1 ), nq );       // halo lanes load clamped columns
+    const int r0 = -8 + (int)blockIdx.y * HS_ROWS;
+    const int r1 = min( r0 + HS_ROWS, height + 8 );
+    const intptr_t fo = (intptr_t)blockIdx.z * fstride + x0;
+    const uint8_t *sp = src + fo;
+    auto ld = [&]( int row ) { return *(const uint4 *)(sp + (intptr_t)row * stride); };
+    auto unpack = [&]( uint4 d, hs2 (&P)[11] ) {
+        const uint32_t dl = (uint32_t)__builtin_amdgcn_mov_dpp( (int)d.w, 0x138, 0xF, 0xF, true );   // lane - 1
+        const uint32_t dr = (uint32_t)__builtin_amdgcn_mov_dpp( (int)d.x, 0x130, 0xF, 0xF, true );   // lane + 1
+        P[0] = as_s2( __builtin_amdgcn_perm( 0u, dl, 0x0c030c02u ) );
+        const uint32_t w[4] = { d.x, d.y, d.z, d.w };
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+        {
+            P[1 + 2 * j] = as_s2( __builtin_amdgcn_perm( 0u, w[j], 0x0c010c00u ) );
+            P[2 + 2 * j] = as_s2( __builtin_amdgcn_perm( 0u, w[j], 0x0c030c02u ) );
+        }
+        P[9] = as_s2( __builtin_amdgcn_perm( 0u, dr, 0x0c010c00u ) );
+        P[10] = as_s2( __builtin_amdgcn_perm( 0u, dr, 0x0c030c02u ) );
+    };
+    hs2 win[6][11];                                          // source rows as even pairs, ring of 6
+    uint4 raw[6];                                            // next block's source rows, in flight
+#pragma unroll
+    for( int k = 0; k < 5; k++ )
+        raw[k] = ld( r0 - 2 + k );
+#pragma unroll
+    for( int k = 0; k < 5; k++ )
+        unpack( raw[k], win[k] );
+#pragma unroll
+    for( int k = 0; k < 6; k++ )
+        raw[k] = ld( r0 + 3 + k );
+    for( int cy = r0; cy < r1; cy += 6 )
+    {
+        uint4 cur[6];
+#pragma unroll
+        for( int k = 0; k < 6; k++ )
+        {
+            cur[k] = raw[k];
+            raw[k] = ld( cy + 9 + k );                       // rows of the next block (<= H + 16 + 8)
+        }
+#pragma unroll
+        for( int k = 0; k < 6; k++ )
+        {
+            const int y = cy + k;
+            if( y >= r1 )
+                break;                                       // wave-uniform
+            unpack( cur[k], win[(k + 5) % 6] );              // source row y + 3
+            // vertical 6-tap intermediates at columns x-2 .. x+19 (int16, exact at 8 bit)
+            hs2 vi[11];
+#pragma unroll
+            for( int p = 0; p < 11; p++ )
+            {
+                const hs2 a = win[k % 6][p], b = win[(k + 1) % 6][p], c = win[(k + 2) % 6][p];
+                const hs2 d = win[(k + 3) % 6][p], e = win[(k + 4) % 6][p], f = win[(k + 5) % 6][p];
+                vi[p] = (a + f) + (c + d) * (hs2)20 - (b + e) * (hs2)5;
+            }
+            uint32_t oh[4], ov[4], oc[4];
+#pragma unroll
+            for( int j = 0; j < 4; j++ )
+            {
+                // V: clip( (v + 16) >> 5 ), clamp before the shift
+                hs2 va = vi[1 + 2 * j] + (hs2)16, vb = vi[2 + 2 * j] + (hs2)16;
+                va = __builtin_elementwise_min( __builtin_elementwise_max( va, (hs2)0 ), (hs2)8191 );
+                vb = __builtin_elementwise_min( __builtin_elementwise_max( vb, (hs2)0 ), (hs2)8191 );
+                ov[j] = __builtin_amdgcn_perm( as_u( vb >> (hs2)5 ), as_u( va >> (hs2)5 ), 0x06040200u );
+            }
+            // H: clip( (t + 16) >> 5 ) computed as clamp( 8t + 128, 0, 0xffff ), byte 1;
+            // centre: clip( (t + 512) >> 10 ) as clamp( 64t + 32768, 0, 0xffffff ), byte 2
+            int o[4];
+            tap6_h4<0, 8>( win[(k + 2) % 6], hbias, o ); oh[0] = pack_clip4<0xffff, 1>( o );
+            tap6_h4<2, 8>( win[(k + 2) % 6], hbias, o ); oh[1] = pack_clip4<0xffff, 1>( o );
+            tap6_h4<4, 8>( win[(k + 2) % 6], hbias, o ); oh[2] = pack_clip4<0xffff, 1>( o );
+            tap6_h4<6, 8>( win[(k + 2) % 6], hbias, o ); oh[3] = pack_clip4<0xffff, 1>( o );
+            tap6_h4<0, 64>( vi, cbias, o ); oc[0] = pack_clip4<0xffffff, 2>( o );
+            tap6_h4<2, 64>( vi, cbias, o ); oc[1] = pack_clip4<0xffffff, 2>( o );
+            tap6_h4<4, 64>( vi, cbias, o ); oc[2] = pack_clip4<0xffffff, 2>( o );
+            tap6_h4<6, 64>( vi, cbias, o ); oc[3] = pack_clip4<0xffffff, 2>( o );
+            if( st )
+            {
+                intptr_t ox = 0;                             // extra piece: x in [-32, -16) / [W+16, W+32)
+                if( q == 0 )
+                {
+                    // x -16..-5 take pixel -4 (byte 0 of the last dword)
+                    oh[0] = oh[1] = oh[2] = __builtin_amdgcn_perm( 0u, oh[3], 0 );
+                    ov[0] = ov[1] = ov[2] = __builtin_amdgcn_perm( 0u, ov[3], 0 );
+                    oc[0] = oc[1] = oc[2] = __builtin_amdgcn_perm( 0u, oc[3], 0 );
+                    ox = -16;
+                }
+                else if( q == nq - 1 )
+                {
+                    // x W+4..W+15 take pixel W+3 (byte 3 of the first dword)
+                    oh[1] = oh[2] = oh[3] = __builtin_amdgcn_perm( 0u, oh[0], 0x03030303u );
+                    ov[1] = ov[2] = ov[3] = __builtin_amdgcn_perm( 0u, ov[0], 0x03030303u );
+                    oc[1] = oc[2] = oc[3] = __builtin_amdgcn_perm( 0u, oc[0], 0x03030303u );
+                    ox = 16;
+                }
+                const uint4 vh = make_uint4( oh[0], oh[1], oh[2], oh[3] );
+                const uint4 vv = make_uint4( ov[0], ov[1], ov[2], ov[3] );
+                const uint4 vc = make_uint4( oc[0], oc[1], oc[2], oc[3] );
+                const uint4 eh = ox < 0 ? make_uint4( oh[0], oh[0], oh[0], oh[0] ) : make_uint4( oh[3], oh[3], oh[3], oh[3] );
+                const uint4 ev = ox < 0 ? make_uint4( ov[0], ov[0], ov[0], ov[0] ) : make_uint4( ov[3], ov[3], ov[3], ov[3] );
+                const uint4 ec = ox < 0 ? make_uint4( oc[0], oc[0], oc[0], oc[0] ) : make_uint4( oc[3], oc[3], oc[3], oc[3] );
+                // rows: y, or the replicated border rows -32..-8 / H+7..H+31
+                const int ya = y == -8 ? -32 : y, yb = y == height + 7 ? height + 31 : y;
+                for( int yy = ya; yy <= yb; yy++ )
+                {
+                    const intptr_t o0 = fo + (intptr_t)yy * stride;
+                    *(uint4 *)(dh + o0) = vh;
+                    *(uint4 *)(dv + o0) = vv;
+                    *(uint4 *)(dc + o0) = vc;
+                    if( ox )
+                    {
+                        *(uint4 *)(dh + o0 + ox) = eh;
+                        *(uint4 *)(dv + o0 + ox) = ev;
+                        *(uint4 *)(dc + o0 + ox) = ec;
+                    }
+                }
+            }
+        }
+    }
+}
+
 template <int BD>
 hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD>::pixel *dh,
                                typename PT<BD>::pixel *dv, typename PT<BD>::pixel *dc, intptr_t stride,
@@ -265,7 +456,23 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
     if( nframes <= 0 || width <= 0 || height <= 0 )
         return hipSuccess;
     const char *ev = getenv( "X264HIP_HPEL_VARIANT" );
-    if( !ev || atoi( ev ) != 1 )
+    const int var = ev ? atoi( ev ) : BD == 8 ? 2 : 0;
+    if constexpr( BD == 8 )
+    {
+        // streaming kernel: needs 16-byte aligned rows (pixel (0,0) and the strides)
+        if( var == 2 && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
+                           (uintptr_t)fstride) & 15) )
+        {
+            const int nq = (width + 32) / 16, nchunk = (nq + 61) / 62;
+            // 24-row strips (12: same time, 36 / 48: fewer waves than SIMDs, 0.058 / 0.074 ms)
+            constexpr int R = 24;
+            dim3 g( (nchunk + 3) / 4, (height + 16 + R - 1) / R, nframes );
+            hipLaunchKernelGGL( hpel_stream_kernel<R>, g, dim3( 256 ), 0, stream, src, dh, dv, dc, stride, fstride,
+                                width, height, 8 * 16, 64 * 512 );
+            return hipGetLastError();
+        }
+    }
+    if( var != 1 )
     {
         // fused single pass; needs 4-pixel aligned rows (width + 64 covered by whole tiles of 4)
         dim3 g( (width + 64 + HF_W - 1) / HF_W, (height + 64 + HF_H - 1) / HF_H, nframes );
