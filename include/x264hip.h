@@ -414,6 +414,35 @@ int x264hip_##BD##_lowres_intra_cost( const pixel *lowres, intptr_t stride,     
                                       const uint16_t *inv_qscale, uint16_t *intra_cost,          \
                                       int32_t *row_satd, int32_t *cost_est, void *stream );      \
                                                                                                 \
+/* the lookahead's lowres motion search for P frames: slicetype_mb_cost's inter                  \
+ * leg (encoder/slicetype.c:514-713, 758-791 with b == p1, one list, no weights,                 \
+ * a fresh search, the do_edges scan of slicetype.c:818-833 as one lookahead                     \
+ * slice) with x264_me_search_ref / refine_subpel as the lookahead runs them                     \
+ * (encoder/me.c:182-420, 774-790, 865-992; lowres_context_init                                  \
+ * slicetype.c:45-61): me_method 0 = DIA, 1 = HEX; subme 2 or 4 (the lookahead's                 \
+ * h->mb.i_subpel_refine); satd = the mbcmp choice (!lossless && param subme > 1);               \
+ * me_range = param i_me_range; mv_range = param i_mv_range; lambda =                            \
+ * x264_lambda_tab[X264_LOOKAHEAD_QP]; cost_mv = device pointer at mvd 0 of                      \
+ * h->cost_mv[X264_LOOKAHEAD_QP] (analyse.c:143-157, valid over +-8*mv_range).                   \
+ * For n_pairs (fenc, ref) pairs of lowres frames -- fenc = lowres[0] of frame b,                \
+ * ref = lowres[0..3] (F, H, V, C) of frame p0, pointers at pixel (0,0), frame                   \
+ * strides apart, common stride, 32 pixels of border, (0,0) and stride 4-byte                    \
+ * aligned -- and intra_cost[f*mbs + mb] from lowres_intra_cost, writes                          \
+ * fenc->lowres_mvs (mvs[2*(f*mbs + mb)]), lowres_mv_costs (mv_costs), lowres_costs               \
+ * ((list_used << 14) + cost), the AQ-scaled inter row sums row_satd[f*mbh + y]                  \
+ * (i_row_satds[b-p0][0]) and est[3f..3f+2] = cost_est, cost_est_aq, intra_mbs.                  \
+ * inv_qscale NULL = AQ off; row_satd / est may be NULL. */                                       \
+int x264hip_##BD##_lowres_inter_cost( const pixel *fenc, intptr_t fenc_frame_stride,             \
+                                      const pixel *ref_f, const pixel *ref_h,                     \
+                                      const pixel *ref_v, const pixel *ref_c, intptr_t stride,   \
+                                      intptr_t ref_frame_stride, int mb_width, int mb_height,    \
+                                      int n_pairs, int me_method, int subme, int satd,           \
+                                      int me_range, int mv_range, int lambda,                    \
+                                      const uint16_t *cost_mv, const uint16_t *intra_cost,       \
+                                      const uint16_t *inv_qscale, int16_t *mvs,                  \
+                                      int32_t *mv_costs, uint16_t *lowres_costs,                 \
+                                      int32_t *row_satd, int32_t *est, void *stream );           \
+                                                                                                \
 /* ESA integral image of n_frames luma planes (x264_frame_filter, mc.c:748-782;                 \
  * integral_init* mc.c:424-456): plane / integral point at (0,0), rows                          \
  * [-32, lines+32) with common stride; row starts at x = -padh (PADH_ALIGN,                     \

@@ -1873,3 +1873,435 @@ void FN(lowres_intra_cost)( const pixel *plane, intptr_t stride, int mb_width, i
 #undef PX
 #undef F1
 #undef F2
+
+/*============================================================================
+ * the lookahead's lowres motion search: slicetype_mb_cost's inter leg for a
+ * P frame (reference encoder/slicetype.c:514-713, 758-791 with b == p1, one
+ * list, no weights, a fresh search) and the x264_me_search_ref /
+ * refine_subpel paths the lookahead runs (encoder/me.c:182-420, 774-790,
+ * 865-992 with me = DIA or HEX, subme = 2 or 4, no chroma, no thresholds).
+ *==========================================================================*/
+#define LR_COST_MAX (1 << 28)
+static const uint8_t lr_subpel_iters[5][4] = { {0,0,0,0}, {1,1,0,0}, {0,1,1,0}, {0,2,1,0}, {0,2,1,1} };  /* me.c:38-50 */
+static const uint8_t lr_mod6m1[8] = { 5,0,1,2,3,4,5,0 };                                                /* me.c:53 */
+static const int8_t lr_hex2[8][2] = { {-1,-2}, {-2,0}, {-1,2}, {1,2}, {2,0}, {1,-2}, {-1,-2}, {-2,0} }; /* me.c:55 */
+static const int8_t lr_square1[9][2] = { {0,0}, {0,-1}, {0,1}, {-1,0}, {1,0}, {-1,-1}, {-1,1}, {1,-1}, {1,1} };
+
+static inline uint32_t lr_pack( int a, int b ) { return (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)b << 16); }
+static inline int lr_clip3( int v, int lo, int hi ) { return v < lo ? lo : v > hi ? hi : v; }
+static inline int lr_median( int a, int b, int c )
+{
+    int mn = a < b ? a : b, mx = a < b ? b : a;
+    return c < mn ? mn : c > mx ? mx : c;
+}
+
+typedef struct
+{
+    const pixel *fenc;               /* 8x8 block, FENC_STRIDE */
+    const pixel *planes[4];          /* F, H, V, C of the reference at the block */
+    intptr_t stride;
+    const uint16_t *cmx, *cmy;       /* p_cost_mvx / p_cost_mvy = cost_mv - mvp */
+    int satd;                        /* mbcmp: satd (else sad) */
+    int spel_min[2], spel_max[2];    /* h->mb.mv_min_spel / mv_max_spel */
+    int fpel_min[2], fpel_max[2];    /* mv_limit_fpel */
+} lrme_t;
+
+static int lr_fpel( const lrme_t *m, int mx, int my )          /* fpelcmp on the full-pel plane */
+{
+    return FN(sad)( 3, m->fenc, FENC_STRIDE, m->planes[0] + my * m->stride + mx, m->stride );
+}
+
+static int lr_qpel( const lrme_t *m, int mx, int my, int satd ) /* get_ref (mc.c:221-249) then cmp */
+{
+    pixel tmp[8 * 16];
+    intptr_t ts = 16;
+    const pixel *r = FN(get_ref)( tmp, &ts, m->planes, m->stride, mx, my, 8, 8 );
+    return satd ? FN(satd)( 3, m->fenc, FENC_STRIDE, r, ts ) : FN(sad)( 3, m->fenc, FENC_STRIDE, r, ts );
+}
+
+#define LR_BITS_MVD( mx, my ) (m->cmx[(mx) * 4] + m->cmy[(my) * 4])
+#define LR_COST_MV( mx, my ) do { int c_ = lr_fpel( m, mx, my ) + LR_BITS_MVD( mx, my ); \
+                                  if( c_ < bcost ) { bcost = c_; bmx = (mx); bmy = (my); } } while( 0 )
+#define LR_CHECK_MVRANGE( mx, my ) ( (mx) >= m->fpel_min[0] && (mx) <= m->fpel_max[0] && \
+                                     (my) >= m->fpel_min[1] && (my) <= m->fpel_max[1] )
+
+/* x264_me_search_ref (me.c:182-420, 774-790) then refine_subpel (me.c:912-992) */
+static void lr_me_search( const lrme_t *m, const int mvp[2], int16_t (*mvc)[2], int i_mvc, int me_method,
+                          int subme, int me_range, int mv[2], int *cost )
+{
+    int bmx, bmy, bcost = LR_COST_MAX, bpred_cost = LR_COST_MAX;
+    uint32_t pmv, bpred_mv = 0;
+    int16_t tmp[16][2];
+    if( subme >= 3 )
+    {
+        int bpx = lr_clip3( mvp[0], 4 * m->fpel_min[0], 4 * m->fpel_max[0] );
+        int bpy = lr_clip3( mvp[1], 4 * m->fpel_min[1], 4 * m->fpel_max[1] );
+        pmv = lr_pack( bpx, bpy );
+        bpred_cost = lr_qpel( m, bpx, bpy, 0 ) + m->cmx[bpx] + m->cmy[bpy];      /* COST_MV_HPEL */
+        const int pmv_cost = bpred_cost;
+        if( i_mvc > 0 )
+        {
+            /* x264_predictor_clip (common/common.h:790-805) */
+            int valid = 0;
+            for( int i = 0; i < i_mvc; i++ )
+            {
+                uint32_t v = lr_pack( mvc[i][0], mvc[i][1] );
+                if( !v || v == pmv )
+                    continue;
+                tmp[2 + valid][0] = lr_clip3( mvc[i][0], 4 * m->fpel_min[0], 4 * m->fpel_max[0] );
+                tmp[2 + valid][1] = lr_clip3( mvc[i][1], 4 * m->fpel_min[1], 4 * m->fpel_max[1] );
+                valid++;
+            }
+            if( valid > 0 )
+            {
+                tmp[1][0] = bpx; tmp[1][1] = bpy;
+                bpred_cost <<= 4;
+                for( int i = 1; i <= valid; i++ )
+                {
+                    int mx = tmp[i + 1][0], my = tmp[i + 1][1];
+                    int c = lr_qpel( m, mx, my, 0 ) + m->cmx[mx] + m->cmy[my];
+                    if( (c << 4) + i < bpred_cost )
+                        bpred_cost = (c << 4) + i;
+                }
+                bpx = tmp[(bpred_cost & 15) + 1][0];
+                bpy = tmp[(bpred_cost & 15) + 1][1];
+                bpred_cost >>= 4;
+            }
+        }
+        bmx = (bpx + 2) >> 2;
+        bmy = (bpy + 2) >> 2;
+        bpred_mv = lr_pack( bpx, bpy );
+        if( bpred_mv & 0x00030003 )
+            LR_COST_MV( bmx, bmy );
+        else
+            bcost = bpred_cost;
+        if( pmv )
+        {
+            if( bmx | bmy )
+                LR_COST_MV( 0, 0 );
+        }
+        else if( pmv_cost < bcost )
+        {
+            bcost = pmv_cost;
+            bmx = bmy = 0;
+        }
+    }
+    else
+    {
+        bmx = lr_clip3( (mvp[0] + 2) >> 2, m->fpel_min[0], m->fpel_max[0] );
+        bmy = lr_clip3( (mvp[1] + 2) >> 2, m->fpel_min[1], m->fpel_max[1] );
+        pmv = lr_pack( bmx, bmy );
+        bcost = lr_fpel( m, bmx, bmy );
+        if( i_mvc > 0 )
+        {
+            /* x264_predictor_roundclip (common/common.h:774-788) */
+            int valid = 0;
+            for( int i = 0; i < i_mvc; i++ )
+            {
+                int mx = (mvc[i][0] + 2) >> 2, my = (mvc[i][1] + 2) >> 2;
+                uint32_t v = lr_pack( mx, my );
+                if( !v || v == pmv )
+                    continue;
+                tmp[2 + valid][0] = lr_clip3( mx, m->fpel_min[0], m->fpel_max[0] );
+                tmp[2 + valid][1] = lr_clip3( my, m->fpel_min[1], m->fpel_max[1] );
+                valid++;
+            }
+            if( valid > 0 )
+            {
+                tmp[1][0] = bmx; tmp[1][1] = bmy;
+                bcost <<= 4;
+                for( int i = 1; i <= valid; i++ )
+                {
+                    int mx = tmp[i + 1][0], my = tmp[i + 1][1];
+                    int c = lr_fpel( m, mx, my ) + LR_BITS_MVD( mx, my );
+                    if( (c << 4) + i < bcost )
+                        bcost = (c << 4) + i;
+                }
+                bmx = tmp[(bcost & 15) + 1][0];
+                bmy = tmp[(bcost & 15) + 1][1];
+                bcost >>= 4;
+            }
+        }
+        if( pmv )
+            LR_COST_MV( 0, 0 );
+    }
+
+    int costs[8];
+    if( me_method == 0 )
+    {
+        /* diamond search, radius 1 (me.c:322-342) */
+        bcost <<= 4;
+        int i = me_range;
+        do
+        {
+            costs[0] = lr_fpel( m, bmx, bmy - 1 ) + LR_BITS_MVD( bmx, bmy - 1 );
+            costs[1] = lr_fpel( m, bmx, bmy + 1 ) + LR_BITS_MVD( bmx, bmy + 1 );
+            costs[2] = lr_fpel( m, bmx - 1, bmy ) + LR_BITS_MVD( bmx - 1, bmy );
+            costs[3] = lr_fpel( m, bmx + 1, bmy ) + LR_BITS_MVD( bmx + 1, bmy );
+            if( (costs[0] << 4) + 1 < bcost ) bcost = (costs[0] << 4) + 1;
+            if( (costs[1] << 4) + 3 < bcost ) bcost = (costs[1] << 4) + 3;
+            if( (costs[2] << 4) + 4 < bcost ) bcost = (costs[2] << 4) + 4;
+            if( (costs[3] << 4) + 12 < bcost ) bcost = (costs[3] << 4) + 12;
+            if( !(bcost & 15) )
+                break;
+            bmx -= (int32_t)((uint32_t)bcost << 28) >> 30;
+            bmy -= (int32_t)((uint32_t)bcost << 30) >> 30;
+            bcost &= ~15;
+        } while( --i && LR_CHECK_MVRANGE( bmx, bmy ) );
+        bcost >>= 4;
+    }
+    else
+    {
+        /* hexagon search, radius 2, then the square refine (me.c:344-420) */
+#define LR_X3( a, b, c, d, e, f, o ) do { \
+        (o)[0] = lr_fpel( m, bmx + (a), bmy + (b) ) + LR_BITS_MVD( bmx + (a), bmy + (b) ); \
+        (o)[1] = lr_fpel( m, bmx + (c), bmy + (d) ) + LR_BITS_MVD( bmx + (c), bmy + (d) ); \
+        (o)[2] = lr_fpel( m, bmx + (e), bmy + (f) ) + LR_BITS_MVD( bmx + (e), bmy + (f) ); } while( 0 )
+        LR_X3( -2, 0, -1, 2, 1, 2, costs );
+        LR_X3( 2, 0, 1, -2, -1, -2, costs + 4 );
+        bcost <<= 3;
+        if( (costs[0] << 3) + 2 < bcost ) bcost = (costs[0] << 3) + 2;
+        if( (costs[1] << 3) + 3 < bcost ) bcost = (costs[1] << 3) + 3;
+        if( (costs[2] << 3) + 4 < bcost ) bcost = (costs[2] << 3) + 4;
+        if( (costs[4] << 3) + 5 < bcost ) bcost = (costs[4] << 3) + 5;
+        if( (costs[5] << 3) + 6 < bcost ) bcost = (costs[5] << 3) + 6;
+        if( (costs[6] << 3) + 7 < bcost ) bcost = (costs[6] << 3) + 7;
+        if( bcost & 7 )
+        {
+            int dir = (bcost & 7) - 2;
+            bmx += lr_hex2[dir + 1][0];
+            bmy += lr_hex2[dir + 1][1];
+            for( int i = (me_range >> 1) - 1; i > 0 && LR_CHECK_MVRANGE( bmx, bmy ); i-- )
+            {
+                LR_X3( lr_hex2[dir][0], lr_hex2[dir][1], lr_hex2[dir + 1][0], lr_hex2[dir + 1][1],
+                       lr_hex2[dir + 2][0], lr_hex2[dir + 2][1], costs );
+                bcost &= ~7;
+                if( (costs[0] << 3) + 1 < bcost ) bcost = (costs[0] << 3) + 1;
+                if( (costs[1] << 3) + 2 < bcost ) bcost = (costs[1] << 3) + 2;
+                if( (costs[2] << 3) + 3 < bcost ) bcost = (costs[2] << 3) + 3;
+                if( !(bcost & 7) )
+                    break;
+                dir += (bcost & 7) - 2;
+                dir = lr_mod6m1[dir + 1];
+                bmx += lr_hex2[dir + 1][0];
+                bmy += lr_hex2[dir + 1][1];
+            }
+        }
+        bcost >>= 3;
+#undef LR_X3
+        bcost <<= 4;
+        static const int8_t sq[8][2] = { {0,-1}, {0,1}, {-1,0}, {1,0}, {-1,-1}, {-1,1}, {1,-1}, {1,1} };
+        for( int k = 0; k < 8; k++ )
+        {
+            int c = lr_fpel( m, bmx + sq[k][0], bmy + sq[k][1] ) + LR_BITS_MVD( bmx + sq[k][0], bmy + sq[k][1] );
+            if( (c << 4) + k + 1 < bcost )
+                bcost = (c << 4) + k + 1;
+        }
+        bmx += lr_square1[bcost & 15][0];
+        bmy += lr_square1[bcost & 15][1];
+        bcost >>= 4;
+    }
+
+    /* -> qpel mv (me.c:774-790) */
+    int mx, my, c;
+    if( subme < 3 )
+    {
+        c = bcost;
+        if( lr_pack( bmx, bmy ) == pmv )
+            c += LR_BITS_MVD( bmx, bmy );
+        mx = 4 * bmx;
+        my = 4 * bmy;
+    }
+    else if( bpred_cost < bcost )
+    {
+        mx = (int16_t)(bpred_mv & 0xffff);
+        my = (int16_t)(bpred_mv >> 16);
+        c = bpred_cost;
+    }
+    else
+    {
+        mx = 4 * bmx;
+        my = 4 * bmy;
+        c = bcost;
+    }
+
+    /* refine_subpel( hpel, qpel, NULL, 0 ) (me.c:912-992) */
+    const int hpel = lr_subpel_iters[subme][2], qpel = lr_subpel_iters[subme][3];
+    bmx = mx; bmy = my; bcost = c;
+    if( hpel )
+    {
+        if( subme < 3 )
+        {
+            int px = lr_clip3( mvp[0], m->spel_min[0] + 2, m->spel_max[0] - 2 );
+            int py = lr_clip3( mvp[1], m->spel_min[1] + 2, m->spel_max[1] - 2 );
+            if( (px - bmx) | (py - bmy) )
+            {
+                int cc = lr_qpel( m, px, py, 0 ) + m->cmx[px] + m->cmy[py];
+                if( cc < bcost ) { bcost = cc; bmx = px; bmy = py; }
+            }
+        }
+        bcost <<= 6;
+        for( int i = hpel; i > 0; i-- )
+        {
+            int omx = bmx, omy = bmy;
+            costs[0] = lr_qpel( m, omx, omy - 2, 0 ) + m->cmx[omx] + m->cmy[omy - 2];
+            costs[1] = lr_qpel( m, omx, omy + 2, 0 ) + m->cmx[omx] + m->cmy[omy + 2];
+            costs[2] = lr_qpel( m, omx - 2, omy, 0 ) + m->cmx[omx - 2] + m->cmy[omy];
+            costs[3] = lr_qpel( m, omx + 2, omy, 0 ) + m->cmx[omx + 2] + m->cmy[omy];
+            if( (costs[0] << 6) + 2 < bcost ) bcost = (costs[0] << 6) + 2;
+            if( (costs[1] << 6) + 6 < bcost ) bcost = (costs[1] << 6) + 6;
+            if( (costs[2] << 6) + 16 < bcost ) bcost = (costs[2] << 6) + 16;
+            if( (costs[3] << 6) + 48 < bcost ) bcost = (costs[3] << 6) + 48;
+            if( !(bcost & 63) )
+                break;
+            bmx -= (int32_t)((uint32_t)bcost << 26) >> 29;
+            bmy -= (int32_t)((uint32_t)bcost << 29) >> 29;
+            bcost &= ~63;
+        }
+        bcost >>= 6;
+    }
+    if( m->satd )
+        bcost = lr_qpel( m, bmx, bmy, 1 ) + m->cmx[bmx] + m->cmy[bmy];   /* COST_MV_SATD( bmx, bmy, -1 ) */
+    if( subme != 1 )
+    {
+        int bdir = -1, odir;
+        for( int i = qpel; i > 0; i-- )
+        {
+            if( bmy <= m->spel_min[1] || bmy >= m->spel_max[1] || bmx <= m->spel_min[0] || bmx >= m->spel_max[0] )
+                break;
+            odir = bdir;
+            int omx = bmx, omy = bmy;
+            static const int8_t qd[4][2] = { {0,-1}, {0,1}, {-1,0}, {1,0} };
+            for( int dir = 0; dir < 4; dir++ )
+            {
+                if( (dir ^ 1) == odir )
+                    continue;
+                int qx = omx + qd[dir][0], qy = omy + qd[dir][1];
+                int cc = lr_qpel( m, qx, qy, m->satd ) + m->cmx[qx] + m->cmy[qy];
+                if( cc < bcost ) { bcost = cc; bmx = qx; bmy = qy; bdir = dir; }
+            }
+            if( bmx == omx && bmy == omy )
+                break;
+        }
+    }
+    mv[0] = bmx;
+    mv[1] = bmy;
+    *cost = bcost;
+}
+#undef LR_COST_MV
+#undef LR_BITS_MVD
+#undef LR_CHECK_MVRANGE
+
+/* One P-frame pair: fenc = lowres[0] of frame b, ref = the four lowres planes of
+ * frame p0 (all at pixel (0,0), common stride, 32 pixels of border); every MB
+ * in the reverse raster order of slicetype_slice_cost (slicetype.c:818-833, the
+ * do_edges case, one lookahead slice).  cost_mv = a->p_cost_mv (cost_mv[qp] of
+ * analyse.c:143-157, indexable over +-4*mv_range*2) at mvd 0; intra_cost =
+ * fenc->i_intra_cost (x264hip lowres_intra_cost).  Outputs lowres_mvs[mb][2],
+ * lowres_mv_costs[mb], lowres_costs[mb] ((list_used << 14) + cost), row_satd[y]
+ * (AQ-scaled inter row sums) and est = { cost_est, cost_est_aq, intra_mbs }. */
+void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
+                            const pixel *ref3, intptr_t stride, int mb_width, int mb_height, int me_method,
+                            int subme, int satd, int me_range, int mv_range, int lambda, const uint16_t *cost_mv,
+                            const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs, int32_t *mv_costs,
+                            uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] )
+{
+    pixel fbuf[8 * FENC_STRIDE];
+    int spel_min1 = 0, spel_max1 = 0;
+    est[0] = est[1] = est[2] = 0;
+    for( int y = 0; y < mb_height; y++ )
+        row_satd[y] = 0;
+    for( int mby = mb_height - 1; mby >= 0; mby-- )
+        for( int mbx = mb_width - 1; mbx >= 0; mbx-- )
+        {
+            const int mb = mbx + mby * mb_width;
+            const intptr_t off = 8 * mbx + 8 * mby * stride;
+            for( int y = 0; y < 8; y++ )
+                memcpy( fbuf + y * FENC_STRIDE, fenc + off + y * stride, 8 * sizeof(pixel) );
+            lrme_t m;
+            m.fenc = fbuf;
+            m.planes[0] = ref0 + off; m.planes[1] = ref1 + off; m.planes[2] = ref2 + off; m.planes[3] = ref3 + off;
+            m.stride = stride;
+            m.satd = satd;
+            const int mvr = 2 * mv_range;
+            m.spel_min[0] = 4 * (-8 * mbx - 12) > -mvr ? 4 * (-8 * mbx - 12) : -mvr;
+            m.spel_max[0] = 4 * (8 * (mb_width - mbx - 1) + 12) < mvr - 1 ? 4 * (8 * (mb_width - mbx - 1) + 12) : mvr - 1;
+            if( mbx >= mb_width - 2 )
+            {
+                spel_min1 = 4 * (-8 * mby - 12) > -mvr ? 4 * (-8 * mby - 12) : -mvr;
+                spel_max1 = 4 * (8 * (mb_height - mby - 1) + 12) < mvr - 1 ? 4 * (8 * (mb_height - mby - 1) + 12) : mvr - 1;
+            }
+            m.spel_min[1] = spel_min1; m.spel_max[1] = spel_max1;
+            for( int k = 0; k < 2; k++ )
+            {
+                m.fpel_min[k] = m.spel_min[k] >> 2;
+                m.fpel_max[k] = m.spel_max[k] >> 2;
+            }
+            /* reverse-order MV prediction (slicetype.c:654-672) */
+            int16_t mvc[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } };
+            int i_mvc = 0;
+#define LR_MVC( i ) do { mvc[i_mvc][0] = mvs[2 * (i)]; mvc[i_mvc][1] = mvs[2 * (i) + 1]; i_mvc++; } while( 0 )
+            if( mbx < mb_width - 1 )
+                LR_MVC( mb + 1 );
+            if( mby < mb_height - 1 )
+            {
+                LR_MVC( mb + mb_width );
+                if( mbx > 0 )
+                    LR_MVC( mb + mb_width - 1 );
+                if( mbx < mb_width - 1 )
+                    LR_MVC( mb + mb_width + 1 );
+            }
+#undef LR_MVC
+            int mvp[2];
+            if( i_mvc <= 1 )
+            {
+                mvp[0] = mvc[0][0];
+                mvp[1] = mvc[0][1];
+            }
+            else
+            {
+                mvp[0] = lr_median( mvc[0][0], mvc[1][0], mvc[2][0] );
+                mvp[1] = lr_median( mvc[0][1], mvc[1][1], mvc[2][1] );
+            }
+            m.cmx = cost_mv - mvp[0];
+            m.cmy = cost_mv - mvp[1];
+            int mv[2] = { 0, 0 }, cost;
+            int skip = 0;
+            if( !mvp[0] && !mvp[1] )
+            {
+                cost = satd ? FN(satd)( 3, fbuf, FENC_STRIDE, m.planes[0], stride )
+                            : FN(sad)( 3, fbuf, FENC_STRIDE, m.planes[0], stride );
+                skip = cost < 64;
+            }
+            if( !skip )
+            {
+                lr_me_search( &m, mvp, mvc, i_mvc, me_method, subme, me_range, mv, &cost );
+                cost -= cost_mv[0];
+                if( mv[0] | mv[1] )
+                    cost += 5 * lambda;
+            }
+            mvs[2 * mb] = mv[0];
+            mvs[2 * mb + 1] = mv[1];
+            mv_costs[mb] = cost;
+            /* slicetype.c:758-790 */
+            int bcost = (cost >> (BIT_DEPTH - 8)) + 4, list_used = 1;
+            const int fsm = (mbx > 0 && mbx < mb_width - 1 && mby > 0 && mby < mb_height - 1) || mb_width <= 2 ||
+                            mb_height <= 2;
+            const int b_intra = intra_cost[mb] < bcost;
+            if( b_intra )
+            {
+                bcost = intra_cost[mb];
+                list_used = 0;
+            }
+            if( fsm )
+                est[2] += b_intra;
+            const int aq = inv_qscale ? (bcost * inv_qscale[mb] + 128) >> 8 : bcost;
+            row_satd[mby] += aq;
+            if( fsm )
+            {
+                est[0] += bcost;
+                est[1] += aq;
+            }
+            lowres_costs[mb] = (uint16_t)((bcost < 16383 ? bcost : 16383) + (list_used << 14));
+        }
+}

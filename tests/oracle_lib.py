@@ -106,6 +106,8 @@ for _bd in (8, 10):
     _f(_bd, "predict", [C.c_int, C.c_int, _P])
     _f(_bd, "intra_x3", [C.c_int, C.c_int, _P, _P, _P])
     _f(_bd, "lowres_intra_cost", [_P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
+    _f(_bd, "lowres_inter_cost", [_P, _P, _P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
@@ -453,3 +455,37 @@ def lowres_intra_cost(bd, plane, origin, stride, mbw, mbh, satd=True, all_modes=
     fn(bd, "lowres_intra_cost")(_addr(plane, origin), stride, mbw, mbh, int(satd), int(all_modes), lam,
                                 None if iq is None else _addr(iq), _addr(cost), _addr(rows), _addr(est))
     return cost, rows, est
+
+
+def cost_mv_table(lam=1, mv_range=512):
+    """h->cost_mv[qp] of analyse.c:143-157 for lambda `lam` (X264_LOOKAHEAD_QP = 12 -> 1):
+    uint16 over mvd in [-8*mv_range, 8*mv_range]; returns (table, index of mvd 0).  logs
+    are evaluated in float32 like the reference's log2f."""
+    span = 2 * 4 * mv_range
+    i = np.arange(span + 1, dtype=np.float32)
+    logs = np.where(i == 0, np.float32(0.718), np.log2(i + np.float32(1)).astype(np.float32) * np.float32(2)
+                    + np.float32(1.718)).astype(np.float32)
+    half = np.minimum((np.float32(lam) * logs + np.float32(0.5)).astype(np.int64), 65535).astype(np.uint16)
+    return np.concatenate([half[:0:-1], half]).astype(np.uint16), span
+
+
+def lowres_inter_cost(bd, fenc, ref_planes, origin, stride, mbw, mbh, intra_cost, me_method=1, subme=4, satd=True,
+                      me_range=16, mv_range=512, lam=1, cost_mv=None, inv_qscale=None):
+    """slicetype_mb_cost's P-frame inter leg over one lowres pair (numpy planes, (0,0) at origin):
+    (mvs int16 [mbs, 2], mv_costs int32 [mbs], lowres_costs uint16 [mbs], row_satd int32 [mbh], est int32 [3])"""
+    if cost_mv is None:
+        cost_mv = cost_mv_table(lam, mv_range)
+    cm, c0 = cost_mv
+    n = mbw * mbh
+    mvs = np.zeros((n, 2), np.int16)
+    mvc = np.zeros(n, np.int32)
+    lc = np.zeros(n, np.uint16)
+    rows = np.zeros(mbh, np.int32)
+    est = np.zeros(3, np.int32)
+    ic = np.ascontiguousarray(intra_cost, np.uint16)
+    iq = None if inv_qscale is None else np.ascontiguousarray(inv_qscale, np.uint16)
+    fn(bd, "lowres_inter_cost")(_addr(fenc, origin), *[_addr(p, origin) for p in ref_planes], stride, mbw, mbh,
+                                me_method, subme, int(satd), me_range, mv_range, lam, _addr(cm, c0), _addr(ic),
+                                None if iq is None else _addr(iq), _addr(mvs), _addr(mvc), _addr(lc), _addr(rows),
+                                _addr(est))
+    return mvs, mvc, lc, rows, est

@@ -281,6 +281,10 @@ def _declare(L):
         f("lowres_intra_cost").argtypes = [_P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                            _c.c_int, _P, _P, _P, _P, _P]
         f("lowres_intra_cost").restype = _c.c_int
+        f("lowres_inter_cost").argtypes = [_P, _IP, _P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                           _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P, _P,
+                                           _P, _P, _P]
+        f("lowres_inter_cost").restype = _c.c_int
         f("mb_dequant_idct_add").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _IP, _IP,
                                              _P, _IP, _IP, _P]
         for n in ("add_idct_batch", "dequant_batch", "idct_dequant_2x4_batch", "optimize_chroma_dc_batch",
@@ -587,6 +591,36 @@ def lowres_intra_cost(lowres, lowres_stride, mb_width, mb_height, satd=True, all
         _ptr(cost), _ptr(rows) if rows is not None else None, _ptr(est) if est is not None else None,
         _stream()), "lowres_intra_cost")
     return cost, rows, est
+
+
+def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost, cost_mv_center, me_method=1,
+                      subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None, outs=None):
+    """The lookahead's P-frame lowres motion search (x264hip_*_lowres_inter_cost) for the pairs
+    (fenc[i], refs[*][i]): fenc = lowres[0] planes [n, rows, stride], refs = the four lowres planes
+    (F, H, V, C) of the references, same shape; (0,0) at (PAD, PAD).  intra_cost [n, mbs] from
+    lowres_intra_cost; cost_mv_center = (uint16-as-int16 tensor, element offset of mvd 0).  Returns
+    (mvs int16 [n, mbs, 2], mv_costs int32 [n, mbs], lowres_costs uint16-as-int16 [n, mbs],
+    row_satd int32 [n, mbh], est int32 [n, 3])."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = fenc.shape[0]
+    nmb = mb_width * mb_height
+    dev = fenc.device
+    if outs is None:
+        outs = (torch.empty((n, nmb, 2), dtype=torch.int16, device=dev),
+                torch.empty((n, nmb), dtype=torch.int32, device=dev),
+                torch.empty((n, nmb), dtype=torch.int16, device=dev),
+                torch.empty((n, mb_height), dtype=torch.int32, device=dev),
+                torch.empty((n, 3), dtype=torch.int32, device=dev))
+    mvs, mvc, lc, rows, est = outs
+    cm, c0 = cost_mv_center
+    o = PAD * lowres_stride + PAD
+    _rc(getattr(lib(), f"x264hip_{bd}_lowres_inter_cost")(
+        _ptr(fenc, o), fenc[0].numel(), *[_ptr(r, o) for r in refs], lowres_stride, refs[0][0].numel(),
+        mb_width, mb_height, n, me_method, subme, int(bool(satd)), me_range, mv_range, lam, _ptr(cm, c0),
+        _ptr(intra_cost), _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(mvs), _ptr(mvc), _ptr(lc),
+        _ptr(rows), _ptr(est), _stream()), "lowres_inter_cost")
+    return mvs, mvc, lc, rows, est
 
 
 def plane_stride(width, pad=PAD):

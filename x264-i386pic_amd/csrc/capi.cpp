@@ -981,6 +981,28 @@ static int map_err( hipError_t e, const char *where )
                                                  invq, cost, row_satd, est, (hipStream_t)stream ),                   \
                         "lowres_intra_cost" );                                                                       \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_lowres_inter_cost(                                                               \
+        const PT<BD>::pixel *fenc, intptr_t ffs, const PT<BD>::pixel *rf, const PT<BD>::pixel *rh,                  \
+        const PT<BD>::pixel *rv, const PT<BD>::pixel *rc, intptr_t stride, intptr_t rfs, int mbw, int mbh,          \
+        int npairs, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,                     \
+        const uint16_t *cost_mv, const uint16_t *intra_cost, const uint16_t *invq, int16_t *mvs, int32_t *mv_costs,   \
+        uint16_t *lowres_costs, int32_t *row_satd, int32_t *est, void *stream )                                      \
+    {                                                                                                                \
+        const intptr_t pb = (intptr_t)sizeof( PT<BD>::pixel );                                                       \
+        if( mbw < 0 || mbh < 0 || npairs < 0 || ( me_method != 0 && me_method != 1 ) ||                              \
+            ( subme != 2 && subme != 4 ) || me_range < 1 || mv_range < 1 || lambda < 0 ||                            \
+            ( (uintptr_t)fenc & 3 ) || ( ( stride * pb ) & 3 ) || ( ( ffs * pb ) & 3 ) ||                            \
+            stride < 8 * mbw + 64 ||                                                                                 \
+            ( (int64_t)mbw * mbh * npairs > 0 &&                                                                     \
+              ( !fenc || !rf || !rh || !rv || !rc || !cost_mv || !intra_cost || !mvs || !mv_costs ||                 \
+                !lowres_costs ) ) )                                                                                  \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *ref[4] = { rf, rh, rv, rc };                                                            \
+        return map_err( launch_lowres_inter<BD>( fenc, ffs, ref, stride, rfs, mbw, mbh, npairs, me_method, subme,    \
+                                                 satd, me_range, mv_range, lambda, cost_mv, intra_cost, invq, mvs,   \
+                                                 mv_costs, lowres_costs, row_satd, est, (hipStream_t)stream ),       \
+                        "lowres_inter_cost" );                                                                       \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_frame_integral( const PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride,    \
                                                   int lines, int padh, int sub8x8, int nframes, uint16_t *integral,  \
                                                   intptr_t ifstride, void *stream )                                  \

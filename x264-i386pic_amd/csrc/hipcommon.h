@@ -59,6 +59,43 @@ __device__ __forceinline__ void load_packed( const void *p, uint32_t (&out)[NDW]
         out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
 }
 
+// rounding-up average of packed pixels (pixel_avg, reference common/mc.c:57): one
+// v_lerp_u8 per dword at 8 bit
+template <int BD> __device__ __forceinline__ uint32_t avg_round( uint32_t a, uint32_t b )
+{
+    if constexpr( BD == 8 )
+        return __builtin_amdgcn_lerp( a, b, 0x01010101u );
+    else
+    {
+        // 10-bit pixels: a + b <= 2046 never carries out of a 16-bit lane
+        typedef unsigned short us2 __attribute__( ( ext_vector_type( 2 ) ) );
+        const us2 s = __builtin_bit_cast( us2, a ) + __builtin_bit_cast( us2, b ) + (us2)1;
+        return __builtin_bit_cast( uint32_t, s >> (us2)1 );
+    }
+}
+
+template <int NDW> __device__ __forceinline__ void load_row_u( const void *p, uint32_t (&out)[NDW] )
+{
+    if constexpr( NDW == 1 )
+        __builtin_memcpy( &out[0], p, 4 );
+    else if constexpr( NDW == 2 )
+    {
+        uint2 v;
+        __builtin_memcpy( &v, p, 8 );
+        out[0] = v.x; out[1] = v.y;
+    }
+    else
+    {
+#pragma unroll
+        for( int k = 0; k < NDW; k += 4 )
+        {
+            uint4 v;
+            __builtin_memcpy( &v, (const char *)p + 4 * k, 16 );
+            out[k] = v.x; out[k + 1] = v.y; out[k + 2] = v.z; out[k + 3] = v.w;
+        }
+    }
+}
+
 // packed sum of absolute differences: v_sad_u8 (4 x u8) / v_sad_u16 (2 x u16)
 template <int BD> __device__ __forceinline__ uint32_t sadp( uint32_t a, uint32_t b, uint32_t acc );
 template <> __device__ __forceinline__ uint32_t sadp<8>( uint32_t a, uint32_t b, uint32_t acc )
@@ -259,4 +296,11 @@ template <int BD>
 hipError_t launch_lowres_intra( const typename PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride, int mbw,
                                 int mbh, int nframes, int satd, int all_modes, int lambda, const uint16_t *invq,
                                 uint16_t *cost, int32_t *row_satd, int32_t *est, hipStream_t stream );
+template <int BD>
+hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs,
+                                const typename PT<BD>::pixel *const ref[4], intptr_t stride, intptr_t rfs, int mbw,
+                                int mbh, int npairs, int me_method, int subme, int satd, int me_range, int mv_range,
+                                int lambda, const uint16_t *cost_mv, const uint16_t *intra_cost,
+                                const uint16_t *invq, int16_t *mvs, int32_t *mv_costs, uint16_t *lowres_costs,
+                                int32_t *row_satd, int32_t *est, hipStream_t stream );
 } // namespace x264hip

@@ -703,47 +703,6 @@ __global__ __launch_bounds__( 256 ) void subpel_satd_rows_kernel( const typename
         scores[i] = (int)(acc >> 1);
 }
 
-// Variant 3 (default): lane per candidate like variant 1, without its per-row
-// branch and realignment.  The second plane pointer equals the first when the
-// qpel phase needs one plane (avg(a, a) = a), so every band's rows are issued
-// as one burst of loads; rows are fetched with unaligned 4/8/16-byte global
-// loads (amdhsa runs with unaligned access enabled: no alignbyte); the 8-bit
-// rounding average is one v_lerp_u8 per dword (pixel_avg, mc.c:57).
-template <int BD> __device__ __forceinline__ uint32_t avg_round( uint32_t a, uint32_t b )
-{
-    if constexpr( BD == 8 )
-        return __builtin_amdgcn_lerp( a, b, 0x01010101u );
-    else
-    {
-        // 10-bit pixels: a + b <= 2046 never carries out of a 16-bit lane
-        typedef unsigned short us2 __attribute__( ( ext_vector_type( 2 ) ) );
-        const us2 s = __builtin_bit_cast( us2, a ) + __builtin_bit_cast( us2, b ) + (us2)1;
-        return __builtin_bit_cast( uint32_t, s >> (us2)1 );
-    }
-}
-
-template <int NDW> __device__ __forceinline__ void load_row_u( const void *p, uint32_t (&out)[NDW] )
-{
-    if constexpr( NDW == 1 )
-        __builtin_memcpy( &out[0], p, 4 );
-    else if constexpr( NDW == 2 )
-    {
-        uint2 v;
-        __builtin_memcpy( &v, p, 8 );
-        out[0] = v.x; out[1] = v.y;
-    }
-    else
-    {
-#pragma unroll
-        for( int k = 0; k < NDW; k += 4 )
-        {
-            uint4 v;
-            __builtin_memcpy( &v, (const char *)p + 4 * k, 16 );
-            out[k] = v.x; out[k + 1] = v.y; out[k + 2] = v.z; out[k + 3] = v.w;
-        }
-    }
-}
-
 // Row of NDW packed dwords at an arbitrary pixel address from dword-aligned loads:
 // the NDW words of an aligned row, else the NDW + 1 words holding it realigned with
 // v_alignbyte (no byte outside the row's dwords is touched).  On gfx950 the address
@@ -766,6 +725,13 @@ __device__ __forceinline__ void load_row_al( const void *p, uint32_t (&out)[NDW]
         out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
 }
 
+// Variants 3 / 5 (LD = 0 / 1): lane per candidate like variant 1, without its per-row
+// branch and realignment.  The second plane pointer equals the first when the
+// qpel phase needs one plane (avg(a, a) = a), so every band's rows are issued
+// as one burst of loads; rows are fetched with unaligned 4/8/16-byte global
+// loads (amdhsa runs with unaligned access enabled: no alignbyte) or, LD = 1,
+// dword-aligned loads + alignbyte (load_row_al); the 8-bit
+// rounding average is one v_lerp_u8 per dword (pixel_avg, mc.c:57).
 template <int BD, int OP, int IPIX, int LD>
 __global__ __launch_bounds__( 256 ) void subpel_cmp3_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
                                                              intptr_t fs, const typename PT<BD>::pixel *p0,
