@@ -268,7 +268,25 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     wall, ev_ms = timed(istep, a.steps, a.warmup, world)
     res["lowres_intra_mbs_per_s"] = world * a.steps * F * mbw * mbh / wall
     res["lowres_intra_launch_ms"] = ev_ms
-    del louts, iouts
+    # the lookahead's P-frame lowres motion search on the same planes: frame k+1 against
+    # frame k for the F-1 pairs, HEX + subme 4 (lowres_context_init for subme > 1), range 16,
+    # lambda 1, cost_mv[X264_LOOKAHEAD_QP] over +-8*512 (analyse.c:143-157)
+    span = 8 * 512
+    ii = np.arange(span + 1, dtype=np.float32)
+    logs = np.where(ii == 0, np.float32(0.718), np.log2(ii + np.float32(1)) * np.float32(2) + np.float32(1.718))
+    half = np.minimum((logs.astype(np.float32) + np.float32(0.5)).astype(np.int64), 65535).astype(np.uint16)
+    cm = torch.from_numpy(np.concatenate([half[:0:-1], half]).view(np.int16)).cuda()
+    lref = [p[:-1] for p in louts]
+    lint = iouts[0][1:]
+    louts2 = x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span))
+
+    def lastep():
+        x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2)
+    wall, ev_ms = timed(lastep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+    res["lowres_me_pairs_per_s"] = world * max(1, a.steps // 5) * (F - 1) / wall
+    res["lowres_me_launch_ms"] = ev_ms
+    res["lowres_me_pairs_per_launch"] = F - 1
+    del louts, iouts, louts2, lref, lint
     nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
     bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)
