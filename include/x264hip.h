@@ -443,6 +443,32 @@ int x264hip_##BD##_lowres_inter_cost( const pixel *fenc, intptr_t fenc_frame_str
                                       int32_t *mv_costs, uint16_t *lowres_costs,                 \
                                       int32_t *row_satd, int32_t *est, void *stream );           \
                                                                                                 \
+/* the lookahead's B-frame costs: slicetype_mb_cost with b_bidir (p0 < b < p1,                    \
+ * slicetype.c:514-713, 758-791) for n triplets: fenc = lowres[0] of frame b, ref_a /            \
+ * ref_b = the four lowres planes (F, H, V, C) of p0 / p1, each with its own frame stride         \
+ * (0 = one reference for the whole batch).  List l (0 = p0, 1 = p1) is searched as in          \
+ * lowres_inter_cost when search & (1 << l) -- writing mvs_l / costs_l                           \
+ * (fenc->lowres_mvs[l] / lowres_mv_costs[l]) -- else read from them.  p1_mvs =                   \
+ * fref1->lowres_mvs[0][p1-p0-1] (NULL when p1 was not searched against p0: dmv = 0);            \
+ * dist_scale_factor and bipred_weight (i_bipred_weight in [0, 64]) as slicetype.c:529,868.       \
+ * Writes lowres_costs ((list_used << 14) + cost, fenc->lowres_costs[b-p0][p1-b]),               \
+ * row_satd[f*mbh + y] and est[2f..2f+1] = cost_est, cost_est_aq.  Other parameters as           \
+ * lowres_inter_cost. */                                                                         \
+int x264hip_##BD##_lowres_bidir_cost( const pixel *fenc, intptr_t fenc_frame_stride,             \
+                                      const pixel *ref_a_f, const pixel *ref_a_h,                 \
+                                      const pixel *ref_a_v, const pixel *ref_a_c,                 \
+                                      intptr_t ref_a_frame_stride, const pixel *ref_b_f,          \
+                                      const pixel *ref_b_h, const pixel *ref_b_v,                 \
+                                      const pixel *ref_b_c, intptr_t ref_b_frame_stride,          \
+                                      intptr_t stride, int mb_width, int mb_height, int n,        \
+                                      int me_method, int subme, int satd, int me_range,          \
+                                      int mv_range, int lambda, const uint16_t *cost_mv,          \
+                                      int search, int16_t *mvs0, int32_t *costs0, int16_t *mvs1,  \
+                                      int32_t *costs1, const int16_t *p1_mvs,                    \
+                                      int dist_scale_factor, int bipred_weight,                   \
+                                      const uint16_t *inv_qscale, uint16_t *lowres_costs,         \
+                                      int32_t *row_satd, int32_t *est, void *stream );           \
+                                                                                                \
 /* ESA integral image of n_frames luma planes (x264_frame_filter, mc.c:748-782;                 \
  * integral_init* mc.c:424-456): plane / integral point at (0,0), rows                          \
  * [-32, lines+32) with common stride; row starts at x = -padh (PADH_ALIGN,                     \

@@ -2192,6 +2192,86 @@ static void lr_me_search( const lrme_t *m, const int mvp[2], int16_t (*mvc)[2], 
 #undef LR_BITS_MVD
 #undef LR_CHECK_MVRANGE
 
+/* per-block setup of slicetype_mb_cost (slicetype.c:539-557): the 8x8 fenc copy and
+ * the lowres mv limits (the vertical ones are set at the first block of each row of the
+ * do_edges scan, x = W-1, and depend on the row only) */
+static void lr_setup( lrme_t *m, pixel *fbuf, const pixel *fenc, const pixel *const ref[4], intptr_t stride,
+                      int mbx, int mby, int mb_width, int mb_height, int mv_range, int satd )
+{
+    const intptr_t off = 8 * mbx + 8 * mby * stride;
+    for( int y = 0; y < 8; y++ )
+        memcpy( fbuf + y * FENC_STRIDE, fenc + off + y * stride, 8 * sizeof(pixel) );
+    m->fenc = fbuf;
+    for( int k = 0; k < 4; k++ )
+        m->planes[k] = ref[k] + off;
+    m->stride = stride;
+    m->satd = satd;
+    const int mvr = 2 * mv_range;
+    const int lo0 = 4 * (-8 * mbx - 12), hi0 = 4 * (8 * (mb_width - mbx - 1) + 12);
+    const int lo1 = 4 * (-8 * mby - 12), hi1 = 4 * (8 * (mb_height - mby - 1) + 12);
+    m->spel_min[0] = lo0 > -mvr ? lo0 : -mvr;
+    m->spel_max[0] = hi0 < mvr - 1 ? hi0 : mvr - 1;
+    m->spel_min[1] = lo1 > -mvr ? lo1 : -mvr;
+    m->spel_max[1] = hi1 < mvr - 1 ? hi1 : mvr - 1;
+    for( int k = 0; k < 2; k++ )
+    {
+        m->fpel_min[k] = m->spel_min[k] >> 2;
+        m->fpel_max[k] = m->spel_max[k] >> 2;
+    }
+}
+
+/* one list of slicetype_mb_cost (slicetype.c:645-702): reverse-order predictors from
+ * this pass's mvs of the list, the near-zero fast skip, x264_me_search, the cost
+ * adjustments; writes mvs[mb] and returns the list cost */
+static int lr_list( lrme_t *m, int16_t *mvs, int mb, int mbx, int mby, int mb_width, int mb_height, int me_method,
+                    int subme, int me_range, int lambda, const uint16_t *cost_mv )
+{
+    int16_t mvc[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } };
+    int i_mvc = 0;
+#define LR_MVC( i ) do { mvc[i_mvc][0] = mvs[2 * (i)]; mvc[i_mvc][1] = mvs[2 * (i) + 1]; i_mvc++; } while( 0 )
+    if( mbx < mb_width - 1 )
+        LR_MVC( mb + 1 );
+    if( mby < mb_height - 1 )
+    {
+        LR_MVC( mb + mb_width );
+        if( mbx > 0 )
+            LR_MVC( mb + mb_width - 1 );
+        if( mbx < mb_width - 1 )
+            LR_MVC( mb + mb_width + 1 );
+    }
+#undef LR_MVC
+    int mvp[2];
+    if( i_mvc <= 1 )
+    {
+        mvp[0] = mvc[0][0];
+        mvp[1] = mvc[0][1];
+    }
+    else
+    {
+        mvp[0] = lr_median( mvc[0][0], mvc[1][0], mvc[2][0] );
+        mvp[1] = lr_median( mvc[0][1], mvc[1][1], mvc[2][1] );
+    }
+    m->cmx = cost_mv - mvp[0];
+    m->cmy = cost_mv - mvp[1];
+    int mv[2] = { 0, 0 }, cost = 0, skip = 0;
+    if( !mvp[0] && !mvp[1] )
+    {
+        cost = m->satd ? FN(satd)( 3, m->fenc, FENC_STRIDE, m->planes[0], m->stride )
+                       : FN(sad)( 3, m->fenc, FENC_STRIDE, m->planes[0], m->stride );
+        skip = cost < 64;
+    }
+    if( !skip )
+    {
+        lr_me_search( m, mvp, mvc, i_mvc, me_method, subme, me_range, mv, &cost );
+        cost -= cost_mv[0];
+        if( mv[0] | mv[1] )
+            cost += 5 * lambda;
+    }
+    mvs[2 * mb] = mv[0];
+    mvs[2 * mb + 1] = mv[1];
+    return cost;
+}
+
 /* One P-frame pair: fenc = lowres[0] of frame b, ref = the four lowres planes of
  * frame p0 (all at pixel (0,0), common stride, 32 pixels of border); every MB
  * in the reverse raster order of slicetype_slice_cost (slicetype.c:818-833, the
@@ -2207,7 +2287,7 @@ void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *r
                             uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] )
 {
     pixel fbuf[8 * FENC_STRIDE];
-    int spel_min1 = 0, spel_max1 = 0;
+    const pixel *ref[4] = { ref0, ref1, ref2, ref3 };
     est[0] = est[1] = est[2] = 0;
     for( int y = 0; y < mb_height; y++ )
         row_satd[y] = 0;
@@ -2215,73 +2295,10 @@ void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *r
         for( int mbx = mb_width - 1; mbx >= 0; mbx-- )
         {
             const int mb = mbx + mby * mb_width;
-            const intptr_t off = 8 * mbx + 8 * mby * stride;
-            for( int y = 0; y < 8; y++ )
-                memcpy( fbuf + y * FENC_STRIDE, fenc + off + y * stride, 8 * sizeof(pixel) );
             lrme_t m;
-            m.fenc = fbuf;
-            m.planes[0] = ref0 + off; m.planes[1] = ref1 + off; m.planes[2] = ref2 + off; m.planes[3] = ref3 + off;
-            m.stride = stride;
-            m.satd = satd;
-            const int mvr = 2 * mv_range;
-            m.spel_min[0] = 4 * (-8 * mbx - 12) > -mvr ? 4 * (-8 * mbx - 12) : -mvr;
-            m.spel_max[0] = 4 * (8 * (mb_width - mbx - 1) + 12) < mvr - 1 ? 4 * (8 * (mb_width - mbx - 1) + 12) : mvr - 1;
-            if( mbx >= mb_width - 2 )
-            {
-                spel_min1 = 4 * (-8 * mby - 12) > -mvr ? 4 * (-8 * mby - 12) : -mvr;
-                spel_max1 = 4 * (8 * (mb_height - mby - 1) + 12) < mvr - 1 ? 4 * (8 * (mb_height - mby - 1) + 12) : mvr - 1;
-            }
-            m.spel_min[1] = spel_min1; m.spel_max[1] = spel_max1;
-            for( int k = 0; k < 2; k++ )
-            {
-                m.fpel_min[k] = m.spel_min[k] >> 2;
-                m.fpel_max[k] = m.spel_max[k] >> 2;
-            }
-            /* reverse-order MV prediction (slicetype.c:654-672) */
-            int16_t mvc[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } };
-            int i_mvc = 0;
-#define LR_MVC( i ) do { mvc[i_mvc][0] = mvs[2 * (i)]; mvc[i_mvc][1] = mvs[2 * (i) + 1]; i_mvc++; } while( 0 )
-            if( mbx < mb_width - 1 )
-                LR_MVC( mb + 1 );
-            if( mby < mb_height - 1 )
-            {
-                LR_MVC( mb + mb_width );
-                if( mbx > 0 )
-                    LR_MVC( mb + mb_width - 1 );
-                if( mbx < mb_width - 1 )
-                    LR_MVC( mb + mb_width + 1 );
-            }
-#undef LR_MVC
-            int mvp[2];
-            if( i_mvc <= 1 )
-            {
-                mvp[0] = mvc[0][0];
-                mvp[1] = mvc[0][1];
-            }
-            else
-            {
-                mvp[0] = lr_median( mvc[0][0], mvc[1][0], mvc[2][0] );
-                mvp[1] = lr_median( mvc[0][1], mvc[1][1], mvc[2][1] );
-            }
-            m.cmx = cost_mv - mvp[0];
-            m.cmy = cost_mv - mvp[1];
-            int mv[2] = { 0, 0 }, cost;
-            int skip = 0;
-            if( !mvp[0] && !mvp[1] )
-            {
-                cost = satd ? FN(satd)( 3, fbuf, FENC_STRIDE, m.planes[0], stride )
-                            : FN(sad)( 3, fbuf, FENC_STRIDE, m.planes[0], stride );
-                skip = cost < 64;
-            }
-            if( !skip )
-            {
-                lr_me_search( &m, mvp, mvc, i_mvc, me_method, subme, me_range, mv, &cost );
-                cost -= cost_mv[0];
-                if( mv[0] | mv[1] )
-                    cost += 5 * lambda;
-            }
-            mvs[2 * mb] = mv[0];
-            mvs[2 * mb + 1] = mv[1];
+            lr_setup( &m, fbuf, fenc, ref, stride, mbx, mby, mb_width, mb_height, mv_range, satd );
+            const int cost = lr_list( &m, mvs, mb, mbx, mby, mb_width, mb_height, me_method, subme, me_range, lambda,
+                                      cost_mv );
             mv_costs[mb] = cost;
             /* slicetype.c:758-790 */
             int bcost = (cost >> (BIT_DEPTH - 8)) + 4, list_used = 1;
@@ -2295,6 +2312,124 @@ void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *r
             }
             if( fsm )
                 est[2] += b_intra;
+            const int aq = inv_qscale ? (bcost * inv_qscale[mb] + 128) >> 8 : bcost;
+            row_satd[mby] += aq;
+            if( fsm )
+            {
+                est[0] += bcost;
+                est[1] += aq;
+            }
+            lowres_costs[mb] = (uint16_t)((bcost < 16383 ? bcost : 16383) + (list_used << 14));
+        }
+}
+
+/* TRY_BIDIR (slicetype.c:589-612): the weighted average of the two lists' predictions
+ * (pixel_avg / pixel_avg_weight_wxh, mc.c:49-87) scored with mbcmp.  subme2 = the
+ * lookahead runs subme 2 (param subme <= 1): hpel planes addressed directly. */
+static int lr_bidir( const lrme_t *m0, const lrme_t *m1, const int mv0[2], const int mv1[2], int subme2, int weight )
+{
+    pixel a[8 * 16], b[8 * 16], avg[8 * 16];
+    const pixel *s1, *s2;
+    intptr_t st1 = 16, st2 = 16;
+    if( subme2 )
+    {
+        const int i1 = ((mv0[0] & 2) >> 1) + (mv0[1] & 2), i2 = ((mv1[0] & 2) >> 1) + (mv1[1] & 2);
+        s1 = m0->planes[i1] + (mv0[0] >> 2) + (mv0[1] >> 2) * m0->stride;
+        s2 = m1->planes[i2] + (mv1[0] >> 2) + (mv1[1] >> 2) * m1->stride;
+        st1 = m0->stride;
+        st2 = m1->stride;
+    }
+    else
+    {
+        s1 = FN(get_ref)( a, &st1, m0->planes, m0->stride, mv0[0], mv0[1], 8, 8 );
+        s2 = FN(get_ref)( b, &st2, m1->planes, m1->stride, mv1[0], mv1[1], 8, 8 );
+    }
+    for( int y = 0; y < 8; y++ )
+        for( int x = 0; x < 8; x++ )
+            avg[y * 16 + x] = weight == 32 ? (s1[y * st1 + x] + s2[y * st2 + x] + 1) >> 1
+                                           : clip_pixel( (s1[y * st1 + x] * weight + s2[y * st2 + x] * (64 - weight) + 32) >> 6 );
+    return m0->satd ? FN(satd)( 3, m0->fenc, FENC_STRIDE, avg, 16 ) : FN(sad)( 3, m0->fenc, FENC_STRIDE, avg, 16 );
+}
+
+/* One B-frame triplet p0 < b < p1: slicetype_mb_cost with b_bidir (slicetype.c:514-713,
+ * 758-791): fenc = lowres[0] of frame b, ref_a / ref_b = the lowres planes of p0 / p1.
+ * List l is searched when search[l] (its mvs / costs are written) or read from mvs_l /
+ * costs_l (fenc->lowres_mvs[l] / lowres_mv_costs[l] of an earlier pass).  p1mvs =
+ * fref1->lowres_mvs[0][p1-p0-1] (NULL: not searched, dmv = 0), dsf = dist_scale_factor,
+ * weight = i_bipred_weight.  No intra in B frames.  Outputs lowres_costs[mb]
+ * (fenc->lowres_costs[b-p0][p1-b]), row_satd[y] and est = { cost_est, cost_est_aq }. */
+void FN(lowres_bidir_cost)( const pixel *fenc, const pixel *const ref_a[4], const pixel *const ref_b[4],
+                            intptr_t stride, int mb_width, int mb_height, int me_method, int subme, int satd,
+                            int me_range, int mv_range, int lambda, const uint16_t *cost_mv, const int search[2],
+                            int16_t *mvs0, int32_t *costs0, int16_t *mvs1, int32_t *costs1, const int16_t *p1mvs,
+                            int dsf, int weight, const uint16_t *inv_qscale, uint16_t *lowres_costs,
+                            int32_t *row_satd, int32_t est[2] )
+{
+    pixel fbuf[8 * FENC_STRIDE];
+    est[0] = est[1] = 0;
+    for( int y = 0; y < mb_height; y++ )
+        row_satd[y] = 0;
+    for( int mby = mb_height - 1; mby >= 0; mby-- )
+        for( int mbx = mb_width - 1; mbx >= 0; mbx-- )
+        {
+            const int mb = mbx + mby * mb_width;
+            lrme_t m0, m1;
+            lr_setup( &m0, fbuf, fenc, ref_a, stride, mbx, mby, mb_width, mb_height, mv_range, satd );
+            lr_setup( &m1, fbuf, fenc, ref_b, stride, mbx, mby, mb_width, mb_height, mv_range, satd );
+            int bcost = LR_COST_MAX, list_used = 0;
+            int dmv[2][2] = { { 0, 0 }, { 0, 0 } };
+            if( p1mvs )
+            {
+                const int mvr[2] = { p1mvs[2 * mb], p1mvs[2 * mb + 1] };
+                for( int k = 0; k < 2; k++ )
+                {
+                    dmv[0][k] = (mvr[k] * dsf + 128) >> 8;
+                    dmv[1][k] = dmv[0][k] - mvr[k];
+                    dmv[0][k] = lr_clip3( dmv[0][k], m0.spel_min[k], m0.spel_max[k] );
+                    dmv[1][k] = lr_clip3( dmv[1][k], m0.spel_min[k], m0.spel_max[k] );
+                    if( subme == 2 )
+                    {
+                        dmv[0][k] &= ~1;
+                        dmv[1][k] &= ~1;
+                    }
+                }
+            }
+            int c = lr_bidir( &m0, &m1, dmv[0], dmv[1], subme == 2, weight );
+            if( c < bcost ) { bcost = c; list_used = 3; }
+            if( dmv[0][0] | dmv[0][1] | dmv[1][0] | dmv[1][1] )
+            {
+                const int z[2] = { 0, 0 };
+                /* h->mc.avg of the two full-pel planes at mv 0 (slicetype.c:641-645) */
+                c = lr_bidir( &m0, &m1, z, z, 1, weight );
+                if( c < bcost ) { bcost = c; list_used = 3; }
+            }
+            int mv[2][2];
+            int16_t *lm[2] = { mvs0, mvs1 };
+            int32_t *lc[2] = { costs0, costs1 };
+            lrme_t *lmm[2] = { &m0, &m1 };
+            for( int l = 0; l < 2; l++ )
+            {
+                int cost;
+                if( search[l] )
+                {
+                    cost = lr_list( lmm[l], lm[l], mb, mbx, mby, mb_width, mb_height, me_method, subme, me_range,
+                                    lambda, cost_mv );
+                    lc[l][mb] = cost;
+                }
+                else
+                    cost = lc[l][mb];
+                mv[l][0] = lm[l][2 * mb];
+                mv[l][1] = lm[l][2 * mb + 1];
+                if( cost < bcost ) { bcost = cost; list_used = l + 1; }
+            }
+            if( mv[0][0] | mv[0][1] | mv[1][0] | mv[1][1] )
+            {
+                c = 5 * lambda + lr_bidir( &m0, &m1, mv[0], mv[1], subme == 2, weight );
+                if( c < bcost ) { bcost = c; list_used = 3; }
+            }
+            bcost = (bcost >> (BIT_DEPTH - 8)) + 4;
+            const int fsm = (mbx > 0 && mbx < mb_width - 1 && mby > 0 && mby < mb_height - 1) || mb_width <= 2 ||
+                            mb_height <= 2;
             const int aq = inv_qscale ? (bcost * inv_qscale[mb] + 128) >> 8 : bcost;
             row_satd[mby] += aq;
             if( fsm )

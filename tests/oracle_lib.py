@@ -108,6 +108,8 @@ for _bd in (8, 10):
     _f(_bd, "lowres_intra_cost", [_P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "lowres_inter_cost", [_P, _P, _P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P])
+    _f(_bd, "lowres_bidir_cost", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, _P, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P, _P, _P, _P])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
@@ -489,3 +491,30 @@ def lowres_inter_cost(bd, fenc, ref_planes, origin, stride, mbw, mbh, intra_cost
                                 None if iq is None else _addr(iq), _addr(mvs), _addr(mvc), _addr(lc), _addr(rows),
                                 _addr(est))
     return mvs, mvc, lc, rows, est
+
+
+def lowres_bidir_cost(bd, fenc, ref_a, ref_b, origin, stride, mbw, mbh, search, mvs0, costs0, mvs1, costs1,
+                      p1mvs=None, dsf=128, weight=32, me_method=1, subme=4, satd=True, me_range=16, mv_range=512,
+                      lam=1, cost_mv=None, inv_qscale=None):
+    """slicetype_mb_cost's B-frame leg over one lowres triplet.  mvs_l int16 [mbs, 2] / costs_l
+    int32 [mbs] are read (search bit clear) or written (set); copies are returned:
+    (mvs0, costs0, mvs1, costs1, lowres_costs uint16 [mbs], row_satd int32 [mbh], est int32 [2])"""
+    if cost_mv is None:
+        cost_mv = cost_mv_table(lam, mv_range)
+    cm, c0 = cost_mv
+    n = mbw * mbh
+    m0, k0 = np.array(mvs0, np.int16).reshape(n, 2).copy(), np.array(costs0, np.int32).reshape(n).copy()
+    m1, k1 = np.array(mvs1, np.int16).reshape(n, 2).copy(), np.array(costs1, np.int32).reshape(n).copy()
+    lc = np.zeros(n, np.uint16)
+    rows = np.zeros(mbh, np.int32)
+    est = np.zeros(2, np.int32)
+    srch = (C.c_int * 2)(search & 1, (search >> 1) & 1)
+    pa = (C.c_void_p * 4)(*[p.ctypes.data + origin * p.itemsize for p in ref_a])
+    pb = (C.c_void_p * 4)(*[p.ctypes.data + origin * p.itemsize for p in ref_b])
+    p1 = None if p1mvs is None else np.ascontiguousarray(p1mvs, np.int16)
+    iq = None if inv_qscale is None else np.ascontiguousarray(inv_qscale, np.uint16)
+    fn(bd, "lowres_bidir_cost")(_addr(fenc, origin), pa, pb, stride, mbw, mbh, me_method, subme, int(satd),
+                                me_range, mv_range, lam, _addr(cm, c0), srch, _addr(m0), _addr(k0), _addr(m1),
+                                _addr(k1), None if p1 is None else _addr(p1), dsf, weight,
+                                None if iq is None else _addr(iq), _addr(lc), _addr(rows), _addr(est))
+    return m0, k0, m1, k1, lc, rows, est

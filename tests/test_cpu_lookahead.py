@@ -119,3 +119,57 @@ def test_aq_scaling(oracle, bd):
     cost = (a[2] & 0x3fff).astype(np.int64)
     aq = (cost * iq + 128) >> 8
     assert np.array_equal(b[3], aq.reshape(mbh, mbw).sum(1))
+
+
+def _triplet(oracle, bd, W, H, seed=5):
+    """p0, b, p1 = frames 0, 1, 2 of a synthetic sequence through frame_init_lowres"""
+    frames, stride, origin = synth.make_sequence(3, W, H, bd, seed=seed)
+    ls = synth.plane_stride(W // 2)
+    lows = [oracle.frame_init_lowres(bd, frames[f].ravel(), origin, stride, W, H, ls) for f in range(3)]
+    return lows, 32 * ls + 32, ls
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("me_method,subme,satd", [(1, 4, True), (0, 2, False)])
+def test_bidir_lists_match_p_search(oracle, bd, me_method, subme, satd):
+    """the B leg's list searches are the P leg's searches against p0 and p1 (same predictors,
+    same me_search_ref), a cached second pass gives the same costs, and the block cost is at
+    most the better list's (slicetype.c:645-713)."""
+    W, H = 192, 128
+    lows, lo, ls = _triplet(oracle, bd, W, H)
+    mbw, mbh = W // 16, H // 16
+    n = mbw * mbh
+    z16, z32 = np.zeros((n, 2), np.int16), np.zeros(n, np.int32)
+    ic = np.full(n, 16383, np.uint16)
+    f = [p.ravel() for p in lows[1]]
+    a = [p.ravel() for p in lows[0]]
+    b = [p.ravel() for p in lows[2]]
+    kw = dict(me_method=me_method, subme=subme, satd=satd)
+    p0 = oracle.lowres_inter_cost(bd, f[0], a, lo, ls, mbw, mbh, ic, **kw)
+    p1 = oracle.lowres_inter_cost(bd, f[0], b, lo, ls, mbw, mbh, ic, **kw)
+    p1mvs = oracle.lowres_inter_cost(bd, b[0], a, lo, ls, mbw, mbh, ic, **kw)[0]
+    m0, k0, m1, k1, lc, rows, est = oracle.lowres_bidir_cost(bd, f[0], a, b, lo, ls, mbw, mbh, 3, z16, z32, z16, z32,
+                                                              p1mvs=p1mvs, dsf=128, weight=32, **kw)
+    assert np.array_equal(m0, p0[0]) and np.array_equal(k0, p0[1])
+    assert np.array_equal(m1, p1[0]) and np.array_equal(k1, p1[1])
+    again = oracle.lowres_bidir_cost(bd, f[0], a, b, lo, ls, mbw, mbh, 0, m0, k0, m1, k1, p1mvs=p1mvs, dsf=128,
+                                     weight=32, **kw)
+    assert np.array_equal(again[4], lc) and np.array_equal(again[5], rows)
+    cost = (lc & 0x3fff).astype(np.int64)
+    used = lc >> 14
+    assert set(np.unique(used)) <= {1, 2, 3}
+    assert (cost <= (np.minimum(k0, k1) >> (bd - 8)) + 4).all()
+    assert np.array_equal(rows, cost.reshape(mbh, mbw).sum(1))
+
+
+def test_bidir_identical_refs(oracle):
+    """p0 == b == p1: the predicted bidir average reproduces fenc, cost 0 + penalty, list 3."""
+    W, H = 128, 96
+    frames, stride, origin = synth.make_sequence(1, W, H, 8)
+    ls = synth.plane_stride(W // 2)
+    p = [q.ravel() for q in oracle.frame_init_lowres(8, frames[0].ravel(), origin, stride, W, H, ls)]
+    mbw, mbh = W // 16, H // 16
+    n = mbw * mbh
+    z16, z32 = np.zeros((n, 2), np.int16), np.zeros(n, np.int32)
+    r = oracle.lowres_bidir_cost(8, p[0], p, p, 32 * ls + 32, ls, mbw, mbh, 3, z16, z32, z16, z32, weight=43)
+    assert (r[4] == (3 << 14) + 4).all()

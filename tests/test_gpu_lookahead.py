@@ -79,3 +79,80 @@ def test_lowres_inter_identical(hip, oracle):
                                                     (torch.from_numpy(cm.view(np.int16)).cuda(), c0))
     assert not mvs.any().item() and not mvc.any().item()
     assert (lc.cpu().numpy().view(np.uint16) == (1 << 14) + 4).all()
+
+
+def _bidir_case(hip, oracle, bd, W, H, n, search, me_method, subme, satd, dsf, weight, with_p1=True, random=False,
+                aq=False, me_range=16):
+    """n B triplets (p0, b, p1) = (3i, 3i+1, 3i+2) of one sequence; the list searches (or the
+    cached mvs of a first pass) and every output against the oracle."""
+    from x264hip import synth
+    gen = synth.random_planes if random else synth.make_sequence
+    frames, stride, origin = gen(3 * n, W, H, bd)
+    dev = torch.from_numpy(frames.view(np.int16) if bd == 10 else frames).cuda()
+    lows, ls = hip.frame_init_lowres(dev, origin, stride, W, H)
+    mbw, mbh = W // 16, H // 16
+    nmb = mbw * mbh
+    cm, c0 = oracle.cost_mv_table(1, 512)
+    cmd = (torch.from_numpy(cm.view(np.int16)).cuda(), c0)
+    kw = dict(me_method=me_method, subme=subme, satd=satd, me_range=me_range)
+    fenc = lows[0][1::3]
+    ra = [p[0::3] for p in lows]
+    rb = [p[2::3] for p in lows]
+    ic = torch.full((n, nmb), 16383, dtype=torch.int16, device="cuda")
+    p1mvs = None
+    if with_p1:
+        p1mvs = hip.lowres_inter_cost(lows[0][2::3], ra, ls, mbw, mbh, ic, cmd, **kw)[0]
+    mvs = [torch.zeros((n, nmb, 2), dtype=torch.int16, device="cuda") for _ in range(2)]
+    costs = [torch.zeros((n, nmb), dtype=torch.int32, device="cuda") for _ in range(2)]
+    iq = None
+    if aq:
+        iq_np = np.random.default_rng(W + bd).integers(100, 700, (n, nmb)).astype(np.uint16)
+        iq = torch.from_numpy(iq_np.view(np.int16)).cuda()
+    fs = lows[0][0].numel()
+    if search != 3:
+        # a first pass searches both lists; the tested pass reads the lists search leaves clear
+        hip.lowres_bidir_cost(fenc, ra, rb, ls, mbw, mbh, cmd, 3, mvs[0], costs[0], mvs[1], costs[1], p1_mvs=p1mvs,
+                              dist_scale_factor=dsf, bipred_weight=weight, a_frame_stride=3 * fs,
+                              b_frame_stride=3 * fs, **kw)
+    before = [t.cpu().numpy() for t in mvs + costs]
+    lc, rows, est = hip.lowres_bidir_cost(fenc, ra, rb, ls, mbw, mbh, cmd, search, mvs[0], costs[0], mvs[1], costs[1],
+                                          p1_mvs=p1mvs, dist_scale_factor=dsf, bipred_weight=weight,
+                                          inv_qscale=iq, a_frame_stride=3 * fs, b_frame_stride=3 * fs, **kw)
+    torch.cuda.synchronize()
+    hl = [_host(p, bd) for p in lows]
+    p1h = None if p1mvs is None else p1mvs.cpu().numpy()
+    lo = 32 * ls + 32
+    got = [t.cpu().numpy() for t in mvs + costs] + [lc.cpu().numpy().view(np.uint16), rows.cpu().numpy(),
+                                                   est.cpu().numpy()]
+    for i in range(n):
+        want = oracle.lowres_bidir_cost(bd, hl[0][3 * i + 1].ravel(), [p[3 * i].ravel() for p in hl],
+                                        [p[3 * i + 2].ravel() for p in hl], lo, ls, mbw, mbh, search,
+                                        before[0][i], before[2][i], before[1][i], before[3][i],
+                                        p1mvs=None if p1h is None else p1h[i], dsf=dsf, weight=weight,
+                                        inv_qscale=None if iq is None else iq_np[i], **kw)
+        order = (0, 2, 1, 3, 4, 5, 6)            # oracle returns m0, k0, m1, k1, lc, rows, est
+        for name, k, w in zip(("mvs0", "costs0", "mvs1", "costs1", "lowres_costs", "row_satd", "est"), order, want):
+            g = got[k][i].reshape(w.shape)
+            assert np.array_equal(g, w), (i, name, np.argwhere(g != w)[:4])
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("me_method,subme,satd,weight", [(1, 4, True, 32), (1, 4, True, 43), (0, 2, False, 21)])
+def test_lowres_bidir_1080p(hip, oracle, bd, me_method, subme, satd, weight):
+    """two 1080p B triplets, both lists searched, p1's mvs as the bidir predictor."""
+    _bidir_case(hip, oracle, bd, 1920, 1088, 2, 3, me_method, subme, satd, 128 if weight == 32 else 85, weight)
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("search", [0, 1, 2])
+def test_lowres_bidir_cached(hip, oracle, bd, search):
+    """lists read from a first pass (search bits clear) or partly re-searched; no p1 mvs."""
+    _bidir_case(hip, oracle, bd, 176, 144, 3, search, 1, 4, True, 171, 22, with_p1=(search != 0))
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("size", [(176, 144), (64, 48), (32, 32)])
+def test_lowres_bidir_random(hip, oracle, bd, size):
+    """random planes (mvs at the limits), AQ, short range, small and degenerate frames."""
+    W, H = size
+    _bidir_case(hip, oracle, bd, W, H, 2, 3, 1, 4, True, 100, 39, random=True, aq=True, me_range=8)

@@ -285,6 +285,11 @@ def _declare(L):
                                            _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P, _P,
                                            _P, _P, _P]
         f("lowres_inter_cost").restype = _c.c_int
+        f("lowres_bidir_cost").argtypes = [_P, _IP, _P, _P, _P, _P, _IP, _P, _P, _P, _P, _IP, _IP, _c.c_int,
+                                           _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                           _c.c_int, _P, _c.c_int, _P, _P, _P, _P, _P, _c.c_int, _c.c_int, _P, _P,
+                                           _P, _P, _P]
+        f("lowres_bidir_cost").restype = _c.c_int
         f("mb_dequant_idct_add").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _IP, _IP,
                                              _P, _IP, _IP, _P]
         for n in ("add_idct_batch", "dequant_batch", "idct_dequant_2x4_batch", "optimize_chroma_dc_batch",
@@ -593,6 +598,18 @@ def lowres_intra_cost(lowres, lowres_stride, mb_width, mb_height, satd=True, all
     return cost, rows, est
 
 
+def _frame_stride(*planes):
+    """element distance between consecutive frames of [n, rows, stride] plane tensors (views such
+    as lowres[0][1::3] included); every plane of one reference must share it."""
+    fs = {p.stride(0) if p.shape[0] > 1 else p[0].numel() for p in planes}
+    if len(fs) != 1:
+        raise ValueError(f"planes disagree on the frame stride: {sorted(fs)}")
+    for p in planes:
+        if p.stride(1) != p.shape[2] or p.stride(2) != 1:
+            raise ValueError("each frame's plane must be row-contiguous")
+    return fs.pop()
+
+
 def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost, cost_mv_center, me_method=1,
                       subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None, outs=None):
     """The lookahead's P-frame lowres motion search (x264hip_*_lowres_inter_cost) for the pairs
@@ -616,11 +633,44 @@ def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost
     cm, c0 = cost_mv_center
     o = PAD * lowres_stride + PAD
     _rc(getattr(lib(), f"x264hip_{bd}_lowres_inter_cost")(
-        _ptr(fenc, o), fenc[0].numel(), *[_ptr(r, o) for r in refs], lowres_stride, refs[0][0].numel(),
+        _ptr(fenc, o), _frame_stride(fenc), *[_ptr(r, o) for r in refs], lowres_stride, _frame_stride(*refs),
         mb_width, mb_height, n, me_method, subme, int(bool(satd)), me_range, mv_range, lam, _ptr(cm, c0),
         _ptr(intra_cost), _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(mvs), _ptr(mvc), _ptr(lc),
         _ptr(rows), _ptr(est), _stream()), "lowres_inter_cost")
     return mvs, mvc, lc, rows, est
+
+
+def lowres_bidir_cost(fenc, refs_a, refs_b, lowres_stride, mb_width, mb_height, cost_mv_center, search,
+                      mvs0, costs0, mvs1, costs1, p1_mvs=None, dist_scale_factor=128, bipred_weight=32,
+                      me_method=1, subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None,
+                      outs=None, a_frame_stride=None, b_frame_stride=None):
+    """The lookahead's B-frame costs (x264hip_*_lowres_bidir_cost) for the triplets (fenc[i],
+    refs_a[*][i], refs_b[*][i]); a reference tensor with one frame and a frame stride of 0 serves
+    the whole batch.  mvs_l int16 [n, mbs, 2] / costs_l int32 [n, mbs] are searched into (search
+    bit l set) or read.  Returns (lowres_costs uint16-as-int16 [n, mbs], row_satd int32 [n, mbh],
+    est int32 [n, 2])."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = fenc.shape[0]
+    nmb = mb_width * mb_height
+    dev = fenc.device
+    if outs is None:
+        outs = (torch.empty((n, nmb), dtype=torch.int16, device=dev),
+                torch.empty((n, mb_height), dtype=torch.int32, device=dev),
+                torch.empty((n, 2), dtype=torch.int32, device=dev))
+    lc, rows, est = outs
+    cm, c0 = cost_mv_center
+    o = PAD * lowres_stride + PAD
+    afs = _frame_stride(*refs_a) if a_frame_stride is None else a_frame_stride
+    bfs = _frame_stride(*refs_b) if b_frame_stride is None else b_frame_stride
+    _rc(getattr(lib(), f"x264hip_{bd}_lowres_bidir_cost")(
+        _ptr(fenc, o), _frame_stride(fenc), *[_ptr(r, o) for r in refs_a], afs, *[_ptr(r, o) for r in refs_b], bfs,
+        lowres_stride, mb_width, mb_height, n, me_method, subme, int(bool(satd)), me_range, mv_range, lam,
+        _ptr(cm, c0), search, _ptr(mvs0), _ptr(costs0), _ptr(mvs1), _ptr(costs1),
+        _ptr(p1_mvs) if p1_mvs is not None else None, dist_scale_factor, bipred_weight,
+        _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(lc), _ptr(rows), _ptr(est), _stream()),
+        "lowres_bidir_cost")
+    return lc, rows, est
 
 
 def plane_stride(width, pad=PAD):

@@ -1003,6 +1003,29 @@ static int map_err( hipError_t e, const char *where )
                                                  mv_costs, lowres_costs, row_satd, est, (hipStream_t)stream ),       \
                         "lowres_inter_cost" );                                                                       \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_lowres_bidir_cost(                                                               \
+        const PT<BD>::pixel *fenc, intptr_t ffs, const PT<BD>::pixel *af, const PT<BD>::pixel *ah,                  \
+        const PT<BD>::pixel *av, const PT<BD>::pixel *ac, intptr_t afs, const PT<BD>::pixel *bf,                    \
+        const PT<BD>::pixel *bh, const PT<BD>::pixel *bv, const PT<BD>::pixel *bc, intptr_t bfs, intptr_t stride,   \
+        int mbw, int mbh, int n, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,        \
+        const uint16_t *cost_mv, int search, int16_t *mvs0, int32_t *costs0, int16_t *mvs1, int32_t *costs1,       \
+        const int16_t *p1mvs, int dsf, int weight, const uint16_t *invq, uint16_t *lowres_costs, int32_t *row_satd,  \
+        int32_t *est, void *stream )                                                                                 \
+    {                                                                                                                \
+        const intptr_t pb = (intptr_t)sizeof( PT<BD>::pixel );                                                       \
+        if( mbw < 0 || mbh < 0 || n < 0 || ( me_method != 0 && me_method != 1 ) || ( subme != 2 && subme != 4 ) ||   \
+            me_range < 1 || mv_range < 1 || lambda < 0 || search < 0 || search > 3 || weight < 0 || weight > 64 ||   \
+            ( (uintptr_t)fenc & 3 ) || ( ( stride * pb ) & 3 ) || ( ( ffs * pb ) & 3 ) || stride < 8 * mbw + 64 ||   \
+            ( (int64_t)mbw * mbh * n > 0 && ( !fenc || !af || !ah || !av || !ac || !bf || !bh || !bv || !bc ||       \
+                                              !cost_mv || !mvs0 || !costs0 || !mvs1 || !costs1 || !lowres_costs ) ) ) \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *ra[4] = { af, ah, av, ac }, *rb[4] = { bf, bh, bv, bc };                                \
+        return map_err( launch_lowres_bidir<BD>( fenc, ffs, ra, afs, rb, bfs, stride, mbw, mbh, n, me_method, subme, \
+                                                 satd, me_range, mv_range, lambda, cost_mv, search, mvs0, costs0,    \
+                                                 mvs1, costs1, p1mvs, dsf, weight, invq, lowres_costs, row_satd,     \
+                                                 est, (hipStream_t)stream ),                                         \
+                        "lowres_bidir_cost" );                                                                       \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_frame_integral( const PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride,    \
                                                   int lines, int padh, int sub8x8, int nframes, uint16_t *integral,  \
                                                   intptr_t ifstride, void *stream )                                  \

@@ -303,4 +303,13 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                 int lambda, const uint16_t *cost_mv, const uint16_t *intra_cost,
                                 const uint16_t *invq, int16_t *mvs, int32_t *mv_costs, uint16_t *lowres_costs,
                                 int32_t *row_satd, int32_t *est, hipStream_t stream );
+template <int BD>
+hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs,
+                                const typename PT<BD>::pixel *const ra[4], intptr_t afs,
+                                const typename PT<BD>::pixel *const rb[4], intptr_t bfs, intptr_t stride, int mbw,
+                                int mbh, int n, int me_method, int subme, int satd, int me_range, int mv_range,
+                                int lambda, const uint16_t *cost_mv, int search, int16_t *mvs0, int32_t *costs0,
+                                int16_t *mvs1, int32_t *costs1, const int16_t *p1mvs, int dsf, int weight,
+                                const uint16_t *invq, uint16_t *lowres_costs, int32_t *row_satd, int32_t *est,
+                                hipStream_t stream );
 } // namespace x264hip

@@ -1,6 +1,7 @@
 // The lookahead's lowres motion search on gfx950: slicetype_mb_cost's inter leg
 // for P frames (reference encoder/slicetype.c:514-713, 758-791 with b == p1, one
-// list, no weights, a fresh search) with the x264_me_search_ref /
+// list, no weights, a fresh search) and for B frames (both lists, searched or
+// cached, and the TRY_BIDIR weighted averages), with the x264_me_search_ref /
 // refine_subpel paths the lookahead runs (encoder/me.c:182-420, 774-790,
 // 865-992: me = DIA or HEX, lookahead subme 2 or 4, no chroma ME).
 //
@@ -36,17 +37,75 @@ __device__ __forceinline__ int lr_median( int a, int b, int c )
     return c < mn ? mn : c > mx ? mx : c;
 }
 
+// 8x8 SAD or packed SATD of fenc rows against predicted rows
+template <int BD>
+__device__ __forceinline__ int lr_cmp_rows( const uint32_t (&fe)[8][8 / PT<BD>::PPD],
+                                            const uint32_t (&r)[8][8 / PT<BD>::PPD], bool use_satd )
+{
+    constexpr int NDW = 8 / PT<BD>::PPD;
+    uint32_t acc = 0;
+    if( use_satd )
+    {
+#pragma unroll
+        for( int band = 0; band < 2; band++ )
+        {
+            uint32_t fa[4][NDW], ra[4][NDW];
+#pragma unroll
+            for( int y = 0; y < 4; y++ )
+#pragma unroll
+                for( int k = 0; k < NDW; k++ )
+                {
+                    fa[y][k] = fe[4 * band + y][k];
+                    ra[y][k] = r[4 * band + y][k];
+                }
+            acc += satd8x4_packed<BD>( fa, ra );
+        }
+        return (int)(acc >> 1);
+    }
+#pragma unroll
+    for( int y = 0; y < 8; y++ )
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            acc = sadp<BD>( fe[y][k], r[y][k], acc );
+    return (int)acc;
+}
+
 template <int BD> struct LrCtx
 {
     using pixel = typename PT<BD>::pixel;
     static constexpr int NDW = 8 / PT<BD>::PPD;
-    uint32_t fe[8][NDW];                    // fenc block rows (packed pixels)
+    const uint32_t (&fe)[8][NDW];           // fenc block rows (packed pixels), shared by the lists
     const pixel *p0, *p1, *p2, *p3;         // reference F, H, V, C at the block
     intptr_t stride;
     const uint16_t *cmx, *cmy;              // p_cost_mvx / p_cost_mvy (cost_mv - mvp)
     int satd;
     int smin0, smax0, smin1, smax1;         // h->mb.mv_min_spel / mv_max_spel
     int fmin0, fmax0, fmin1, fmax1;         // mv_limit_fpel
+
+    __device__ __forceinline__ LrCtx( const uint32_t (&f)[8][NDW] ) : fe( f ) {}
+
+    // per-block setup of slicetype_mb_cost (slicetype.c:539-557): the lowres mv limits
+    // (the vertical ones, set at the first block of each row of the scan, depend on
+    // the row only) and the reference planes at the block
+    __device__ __forceinline__ void setup( const pixel *r0, const pixel *r1, const pixel *r2, const pixel *r3,
+                                           intptr_t off, intptr_t s, int x, int y, int mbw, int mbh, int mvr,
+                                           int use_satd )
+    {
+        p0 = r0 + off;
+        p1 = r1 + off;
+        p2 = r2 + off;
+        p3 = r3 + off;
+        stride = s;
+        satd = use_satd;
+        smin0 = max( 4 * (-8 * x - 12), -mvr );
+        smax0 = min( 4 * (8 * (mbw - x - 1) + 12), mvr - 1 );
+        smin1 = max( 4 * (-8 * y - 12), -mvr );
+        smax1 = min( 4 * (8 * (mbh - y - 1) + 12), mvr - 1 );
+        fmin0 = smin0 >> 2;
+        fmax0 = smax0 >> 2;
+        fmin1 = smin1 >> 2;
+        fmax1 = smax1 >> 2;
+    }
 
     // fpelcmp (SAD) at a full-pel offset of the F plane
     __device__ __forceinline__ int fpel( int mx, int my ) const
@@ -65,15 +124,14 @@ template <int BD> struct LrCtx
         return (int)acc;
     }
 
-    // get_ref (mc.c:221-249) at a quarter-pel mv, then SAD or SATD 8x8
-    __device__ __forceinline__ int qpel( int mx, int my, bool use_satd ) const
+    // get_ref (mc.c:221-249) rows at a quarter-pel mv
+    __device__ __forceinline__ void ref_rows( int mx, int my, uint32_t (&r)[8][NDW] ) const
     {
         const int idx = ((my & 3) << 2) + (mx & 3);
         const intptr_t off = (intptr_t)(my >> 2) * stride + (mx >> 2);
         const int i0 = c_lr_ref0[idx], i1 = c_lr_ref1[idx];
         const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((my & 3) == 3) * stride;
         const pixel *s2 = (idx & 5) ? (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((mx & 3) == 3) : s1;
-        uint32_t r[8][NDW];
 #pragma unroll
         for( int y = 0; y < 8; y++ )
         {
@@ -84,31 +142,24 @@ template <int BD> struct LrCtx
             for( int k = 0; k < NDW; k++ )
                 r[y][k] = avg_round<BD>( a[k], b[k] );
         }
-        uint32_t acc = 0;
-        if( use_satd )
-        {
-#pragma unroll
-            for( int band = 0; band < 2; band++ )
-            {
-                uint32_t fa[4][NDW], ra[4][NDW];
-#pragma unroll
-                for( int y = 0; y < 4; y++ )
-#pragma unroll
-                    for( int k = 0; k < NDW; k++ )
-                    {
-                        fa[y][k] = fe[4 * band + y][k];
-                        ra[y][k] = r[4 * band + y][k];
-                    }
-                acc += satd8x4_packed<BD>( fa, ra );
-            }
-            return (int)(acc >> 1);
-        }
+    }
+
+    // hpel plane rows addressed directly (TRY_BIDIR for subme <= 1, slicetype.c:594-600)
+    __device__ __forceinline__ void hpel_rows( int mx, int my, uint32_t (&r)[8][NDW] ) const
+    {
+        const int i = ((mx & 2) >> 1) + (my & 2);
+        const pixel *s = (i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : p3) + (mx >> 2) + (intptr_t)(my >> 2) * stride;
 #pragma unroll
         for( int y = 0; y < 8; y++ )
-#pragma unroll
-            for( int k = 0; k < NDW; k++ )
-                acc = sadp<BD>( fe[y][k], r[y][k], acc );
-        return (int)acc;
+            load_row_u<NDW>( s + (intptr_t)y * stride, r[y] );
+    }
+
+    // get_ref at a quarter-pel mv, then SAD or SATD 8x8
+    __device__ __forceinline__ int qpel( int mx, int my, bool use_satd ) const
+    {
+        uint32_t r[8][NDW];
+        ref_rows( mx, my, r );
+        return lr_cmp_rows<BD>( fe, r, use_satd );
     }
 
     __device__ __forceinline__ int bits_mvd( int mx, int my ) const { return cmx[mx * 4] + cmy[my * 4]; }
@@ -400,6 +451,77 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
     ocost = bcost;
 }
 
+// one list of slicetype_mb_cost (slicetype.c:645-702): reverse-order predictors from the
+// row ring of this pass, the near-zero fast skip, x264_me_search and the cost
+// adjustments.  Returns the list cost; mvx / mvy the list's mv.
+template <int BD>
+__device__ __forceinline__ int lr_list( LrCtx<BD> &m, const int *ring, int x, int y, int mbw, int mbh,
+                                        int me_method, int subme, int me_range, int lambda,
+                                        const uint16_t *cost_mv, int &mvx, int &mvy )
+{
+    int mvc[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } };
+    int i_mvc = 0;
+    auto add = [&]( int v ) {
+        mvc[i_mvc][0] = (int16_t)(v & 0xffff);
+        mvc[i_mvc][1] = (int16_t)((uint32_t)v >> 16);
+        i_mvc++;
+    };
+    if( x < mbw - 1 )
+        add( ring[4 * y + ((x + 1) & 3)] );
+    if( y < mbh - 1 )
+    {
+        add( ring[4 * (y + 1) + (x & 3)] );
+        if( x > 0 )
+            add( ring[4 * (y + 1) + ((x - 1) & 3)] );
+        if( x < mbw - 1 )
+            add( ring[4 * (y + 1) + ((x + 1) & 3)] );
+    }
+    int mvpx, mvpy;
+    if( i_mvc <= 1 )
+    {
+        mvpx = mvc[0][0];
+        mvpy = mvc[0][1];
+    }
+    else
+    {
+        mvpx = lr_median( mvc[0][0], mvc[1][0], mvc[2][0] );
+        mvpy = lr_median( mvc[0][1], mvc[1][1], mvc[2][1] );
+    }
+    m.cmx = cost_mv - mvpx;
+    m.cmy = cost_mv - mvpy;
+    int cost = 0;
+    mvx = mvy = 0;
+    bool skip = false;
+    if( !mvpx && !mvpy )
+    {
+        // fast skip of near-zero residual blocks (slicetype.c:677-686)
+        cost = m.qpel( 0, 0, m.satd );
+        skip = cost < 64;
+    }
+    if( !skip )
+    {
+        lr_me_search<BD>( m, mvpx, mvpy, mvc, i_mvc, me_method, subme, me_range, mvx, mvy, cost );
+        cost -= cost_mv[0];
+        if( mvx | mvy )
+            cost += 5 * lambda;
+    }
+    return cost;
+}
+
+template <int BD>
+__device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, intptr_t stride,
+                                              uint32_t (&fe)[8][8 / PT<BD>::PPD] )
+{
+#pragma unroll
+    for( int r = 0; r < 8; r++ )
+    {
+        const uint32_t *row = (const uint32_t *)(fb + (intptr_t)r * stride);
+#pragma unroll
+        for( int k = 0; k < 8 / PT<BD>::PPD; k++ )
+            fe[r][k] = row[k];
+    }
+}
+
 template <int BD>
 __global__ __launch_bounds__( 256 ) void lowres_inter_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *r0,
@@ -409,7 +531,6 @@ __global__ __launch_bounds__( 256 ) void lowres_inter_kernel(
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
     uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est )
 {
-    using pixel = typename PT<BD>::pixel;
     constexpr int NDW = LrCtx<BD>::NDW;
     extern __shared__ int lr_smem[];
     int *ring = lr_smem;                         // [mbh][4] packed MVs of the row's 4 latest blocks
@@ -445,76 +566,13 @@ __global__ __launch_bounds__( 256 ) void lowres_inter_kernel(
                 continue;
             const int mb = x + y * mbw;
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
-            LrCtx<BD> m;
-            const pixel *fb = fenc + off;
-#pragma unroll
-            for( int r = 0; r < 8; r++ )
-            {
-                const uint32_t *row = (const uint32_t *)(fb + (intptr_t)r * stride);
-#pragma unroll
-                for( int k = 0; k < NDW; k++ )
-                    m.fe[r][k] = row[k];
-            }
-            m.p0 = r0 + off;
-            m.p1 = r1 + off;
-            m.p2 = r2 + off;
-            m.p3 = r3 + off;
-            m.stride = stride;
-            m.satd = satd;
-            m.smin0 = max( 4 * (-8 * x - 12), -mvr );
-            m.smax0 = min( 4 * (8 * (mbw - x - 1) + 12), mvr - 1 );
-            m.smin1 = max( 4 * (-8 * y - 12), -mvr );
-            m.smax1 = min( 4 * (8 * (mbh - y - 1) + 12), mvr - 1 );
-            m.fmin0 = m.smin0 >> 2;
-            m.fmax0 = m.smax0 >> 2;
-            m.fmin1 = m.smin1 >> 2;
-            m.fmax1 = m.smax1 >> 2;
-            // reverse-order MV prediction (slicetype.c:654-672)
-            int mvc[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } };
-            int i_mvc = 0;
-            auto add = [&]( int v ) {
-                mvc[i_mvc][0] = (int16_t)(v & 0xffff);
-                mvc[i_mvc][1] = (int16_t)((uint32_t)v >> 16);
-                i_mvc++;
-            };
-            if( x < mbw - 1 )
-                add( ring[4 * y + ((x + 1) & 3)] );
-            if( y < mbh - 1 )
-            {
-                add( ring[4 * (y + 1) + (x & 3)] );
-                if( x > 0 )
-                    add( ring[4 * (y + 1) + ((x - 1) & 3)] );
-                if( x < mbw - 1 )
-                    add( ring[4 * (y + 1) + ((x + 1) & 3)] );
-            }
-            int mvpx, mvpy;
-            if( i_mvc <= 1 )
-            {
-                mvpx = mvc[0][0];
-                mvpy = mvc[0][1];
-            }
-            else
-            {
-                mvpx = lr_median( mvc[0][0], mvc[1][0], mvc[2][0] );
-                mvpy = lr_median( mvc[0][1], mvc[1][1], mvc[2][1] );
-            }
-            m.cmx = cost_mv - mvpx;
-            m.cmy = cost_mv - mvpy;
-            int mvx = 0, mvy = 0, cost = 0;
-            bool skip = false;
-            if( !mvpx && !mvpy )
-            {
-                // fast skip of near-zero residual blocks (slicetype.c:677-686)
-                cost = m.qpel( 0, 0, satd );
-                skip = cost < 64;
-            }
-            if( !skip )
-            {
-                lr_me_search<BD>( m, mvpx, mvpy, mvc, i_mvc, me_method, subme, me_range, mvx, mvy, cost );
-                cost -= cost_mv[0];
-                if( mvx | mvy )
-                    cost += 5 * lambda;
-            }
+            uint32_t fe[8][NDW];
+            lr_load_fenc<BD>( fenc + off, stride, fe );
+            LrCtx<BD> m( fe );
+            m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd );
+            int mvx, mvy;
+            const int cost = lr_list<BD>( m, ring, x, y, mbw, mbh, me_method, subme, me_range, lambda, cost_mv, mvx,
+                                          mvy );
             ring[4 * y + (x & 3)] = (int)lr_pack( mvx, mvy );
             mvs[2 * mb] = (int16_t)mvx;
             mvs[2 * mb + 1] = (int16_t)mvy;
@@ -555,6 +613,240 @@ __global__ __launch_bounds__( 256 ) void lowres_inter_kernel(
         est[3 * f + threadIdx.x] = eacc[threadIdx.x];
 }
 
+// pixel_avg / pixel_avg_weight_wxh (mc.c:49-87) of two packed dwords: the rounding
+// average at weight 32, else (a*w + b*(64-w) + 32) >> 6 in 16-bit lanes (w in [0, 64]:
+// no clipping needed, 1023*64 + 32 < 2^16)
+template <int BD> __device__ __forceinline__ uint32_t lr_wavg( uint32_t a, uint32_t b, int w )
+{
+    if( w == 32 )
+        return avg_round<BD>( a, b );
+    typedef unsigned short us2 __attribute__( ( ext_vector_type( 2 ) ) );
+    const us2 wa = (us2)(unsigned short)w, wb = (us2)(unsigned short)(64 - w);
+    auto f = [&]( uint32_t x, uint32_t y ) {
+        const us2 r = (__builtin_bit_cast( us2, x ) * wa + __builtin_bit_cast( us2, y ) * wb + (us2)32) >> (us2)6;
+        return __builtin_bit_cast( uint32_t, r );
+    };
+    if constexpr( BD == 8 )
+    {
+        const uint32_t lo = f( __builtin_amdgcn_perm( 0u, a, 0x0c020c00u ), __builtin_amdgcn_perm( 0u, b, 0x0c020c00u ) );
+        const uint32_t hi = f( __builtin_amdgcn_perm( 0u, a, 0x0c030c01u ), __builtin_amdgcn_perm( 0u, b, 0x0c030c01u ) );
+        return __builtin_amdgcn_perm( hi, lo, 0x06020400u );
+    }
+    else
+        return f( a, b );
+}
+
+// TRY_BIDIR (slicetype.c:589-612): the weighted average of the two lists' predictions
+// scored with mbcmp; hpel = the subme <= 1 form (hpel planes addressed directly)
+template <int BD>
+__device__ __forceinline__ int lr_bidir( const LrCtx<BD> &m0, const LrCtx<BD> &m1, int ax, int ay, int bx, int by,
+                                         bool hpel, int w )
+{
+    constexpr int NDW = LrCtx<BD>::NDW;
+    uint32_t ra[8][NDW], rb[8][NDW];
+    if( hpel )
+    {
+        m0.hpel_rows( ax, ay, ra );
+        m1.hpel_rows( bx, by, rb );
+    }
+    else
+    {
+        m0.ref_rows( ax, ay, ra );
+        m1.ref_rows( bx, by, rb );
+    }
+#pragma unroll
+    for( int y = 0; y < 8; y++ )
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            ra[y][k] = lr_wavg<BD>( ra[y][k], rb[y][k], w );
+    return lr_cmp_rows<BD>( m0.fe, ra, m0.satd );
+}
+
+// B frames (p0 < b < p1): slicetype_mb_cost with b_bidir (slicetype.c:514-713, 758-791).
+// A list is searched on the wavefront when search & (1 << l), else its mv / cost are read.
+template <int BD>
+__global__ __launch_bounds__( 256 ) void lowres_bidir_kernel(
+    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *a0,
+    const typename PT<BD>::pixel *a1, const typename PT<BD>::pixel *a2, const typename PT<BD>::pixel *a3,
+    intptr_t afs, const typename PT<BD>::pixel *b0, const typename PT<BD>::pixel *b1,
+    const typename PT<BD>::pixel *b2, const typename PT<BD>::pixel *b3, intptr_t bfs, intptr_t stride, int mbw,
+    int mbh, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,
+    const uint16_t *__restrict__ cost_mv, int search, int16_t *__restrict__ mvs0, int32_t *__restrict__ costs0,
+    int16_t *__restrict__ mvs1, int32_t *__restrict__ costs1, const int16_t *__restrict__ p1mvs, int dsf, int weight,
+    const uint16_t *__restrict__ invq, uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd,
+    int32_t *__restrict__ est )
+{
+    constexpr int NDW = LrCtx<BD>::NDW;
+    extern __shared__ int lr_smem[];
+    int *ring0 = lr_smem;                        // [mbh][4] per list
+    int *ring1 = lr_smem + 4 * mbh;
+    int *rowacc = lr_smem + 8 * mbh;
+    int *eacc = rowacc + mbh;
+    const int f = blockIdx.x;
+    const int nmb = mbw * mbh;
+    fenc += (intptr_t)f * ffs;
+    a0 += (intptr_t)f * afs; a1 += (intptr_t)f * afs; a2 += (intptr_t)f * afs; a3 += (intptr_t)f * afs;
+    b0 += (intptr_t)f * bfs; b1 += (intptr_t)f * bfs; b2 += (intptr_t)f * bfs; b3 += (intptr_t)f * bfs;
+    if( invq )
+        invq += (intptr_t)f * nmb;
+    if( p1mvs )
+        p1mvs += 2 * (intptr_t)f * nmb;
+    mvs0 += 2 * (intptr_t)f * nmb;
+    mvs1 += 2 * (intptr_t)f * nmb;
+    costs0 += (intptr_t)f * nmb;
+    costs1 += (intptr_t)f * nmb;
+    lcosts += (intptr_t)f * nmb;
+    for( int i = threadIdx.x; i < mbh; i += blockDim.x )
+        rowacc[i] = 0;
+    if( threadIdx.x < 2 )
+        eacc[threadIdx.x] = 0;
+    int e0 = 0, e1 = 0;
+    const int mvr = 2 * mv_range;
+    const bool hp = subme == 2;                  // h->param.analyse.i_subpel_refine <= 1
+    __syncthreads();
+    const int steps = (mbw - 1) + 2 * (mbh - 1) + 1;
+    for( int t = 0; t < steps; t++ )
+    {
+        for( int y = threadIdx.x; y < mbh; y += blockDim.x )
+        {
+            const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
+            if( x < 0 || x >= mbw )
+                continue;
+            const int mb = x + y * mbw;
+            const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
+            uint32_t fe[8][NDW];
+            lr_load_fenc<BD>( fenc + off, stride, fe );
+            LrCtx<BD> m0( fe ), m1( fe );
+            m0.setup( a0, a1, a2, a3, off, stride, x, y, mbw, mbh, mvr, satd );
+            m1.setup( b0, b1, b2, b3, off, stride, x, y, mbw, mbh, mvr, satd );
+            int bcost = LR_COST_MAX, list_used = 0;
+            // the predicted bidir mvs from p1's list-0 mvs (slicetype.c:623-645)
+            int d0x = 0, d0y = 0, d1x = 0, d1y = 0;
+            if( p1mvs )
+            {
+                const int rx = p1mvs[2 * mb], ry = p1mvs[2 * mb + 1];
+                d0x = (rx * dsf + 128) >> 8;
+                d0y = (ry * dsf + 128) >> 8;
+                d1x = lr_clip3( d0x - rx, m0.smin0, m0.smax0 );
+                d1y = lr_clip3( d0y - ry, m0.smin1, m0.smax1 );
+                d0x = lr_clip3( d0x, m0.smin0, m0.smax0 );
+                d0y = lr_clip3( d0y, m0.smin1, m0.smax1 );
+                if( hp )
+                {
+                    d0x &= ~1; d0y &= ~1; d1x &= ~1; d1y &= ~1;
+                }
+            }
+            int c = lr_bidir<BD>( m0, m1, d0x, d0y, d1x, d1y, hp, weight );
+            if( c < bcost )
+            {
+                bcost = c;
+                list_used = 3;
+            }
+            if( d0x | d0y | d1x | d1y )
+            {
+                c = lr_bidir<BD>( m0, m1, 0, 0, 0, 0, true, weight );
+                if( c < bcost )
+                {
+                    bcost = c;
+                    list_used = 3;
+                }
+            }
+            int mv0x, mv0y, mv1x, mv1y, lc;
+            if( search & 1 )
+            {
+                lc = lr_list<BD>( m0, ring0, x, y, mbw, mbh, me_method, subme, me_range, lambda, cost_mv, mv0x, mv0y );
+                ring0[4 * y + (x & 3)] = (int)lr_pack( mv0x, mv0y );
+                mvs0[2 * mb] = (int16_t)mv0x;
+                mvs0[2 * mb + 1] = (int16_t)mv0y;
+                costs0[mb] = lc;
+            }
+            else
+            {
+                mv0x = mvs0[2 * mb];
+                mv0y = mvs0[2 * mb + 1];
+                lc = costs0[mb];
+            }
+            if( lc < bcost )
+            {
+                bcost = lc;
+                list_used = 1;
+            }
+            if( search & 2 )
+            {
+                lc = lr_list<BD>( m1, ring1, x, y, mbw, mbh, me_method, subme, me_range, lambda, cost_mv, mv1x, mv1y );
+                ring1[4 * y + (x & 3)] = (int)lr_pack( mv1x, mv1y );
+                mvs1[2 * mb] = (int16_t)mv1x;
+                mvs1[2 * mb + 1] = (int16_t)mv1y;
+                costs1[mb] = lc;
+            }
+            else
+            {
+                mv1x = mvs1[2 * mb];
+                mv1y = mvs1[2 * mb + 1];
+                lc = costs1[mb];
+            }
+            if( lc < bcost )
+            {
+                bcost = lc;
+                list_used = 2;
+            }
+            if( mv0x | mv0y | mv1x | mv1y )
+            {
+                c = 5 * lambda + lr_bidir<BD>( m0, m1, mv0x, mv0y, mv1x, mv1y, hp, weight );
+                if( c < bcost )
+                {
+                    bcost = c;
+                    list_used = 3;
+                }
+            }
+            // slicetype.c:758-790 (no intra in B frames)
+            bcost = (bcost >> (BD - 8)) + 4;
+            const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
+            const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
+            rowacc[y] += aq;
+            if( fsm )
+            {
+                e0 += bcost;
+                e1 += aq;
+            }
+            lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
+        }
+        __syncthreads();
+    }
+    if( e0 | e1 )
+    {
+        atomicAdd( &eacc[0], e0 );
+        atomicAdd( &eacc[1], e1 );
+    }
+    __syncthreads();
+    if( row_satd )
+        for( int i = threadIdx.x; i < mbh; i += blockDim.x )
+            row_satd[(intptr_t)f * mbh + i] = rowacc[i];
+    if( est && threadIdx.x < 2 )
+        est[2 * f + threadIdx.x] = eacc[threadIdx.x];
+}
+
+template <int BD>
+hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs,
+                                const typename PT<BD>::pixel *const ra[4], intptr_t afs,
+                                const typename PT<BD>::pixel *const rb[4], intptr_t bfs, intptr_t stride, int mbw,
+                                int mbh, int n, int me_method, int subme, int satd, int me_range, int mv_range,
+                                int lambda, const uint16_t *cost_mv, int search, int16_t *mvs0, int32_t *costs0,
+                                int16_t *mvs1, int32_t *costs1, const int16_t *p1mvs, int dsf, int weight,
+                                const uint16_t *invq, uint16_t *lowres_costs, int32_t *row_satd, int32_t *est,
+                                hipStream_t stream )
+{
+    if( n <= 0 || mbw <= 0 || mbh <= 0 )
+        return hipSuccess;
+    const int threads = min( 256, (mbh + 63) / 64 * 64 );
+    const size_t lds = (size_t)(9 * mbh + 2) * sizeof( int );
+    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n ), dim3( threads ), lds, stream, fenc, ffs, ra[0], ra[1],
+                        ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method, subme, satd,
+                        me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, weight,
+                        invq, lowres_costs, row_satd, est );
+    return hipGetLastError();
+}
+
 template <int BD>
 hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs,
                                 const typename PT<BD>::pixel *const ref[4], intptr_t stride, intptr_t rfs, int mbw,
@@ -578,6 +870,16 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                                  intptr_t, intptr_t, int, int, int, int, int, int, int, int, int, \
                                                  const uint16_t *, const uint16_t *, const uint16_t *, int16_t *, \
                                                  int32_t *, uint16_t *, int32_t *, int32_t *, hipStream_t );
+INST( 8 )
+INST( 10 )
+#undef INST
+#define INST( BD )                                                                                              \
+    template hipError_t launch_lowres_bidir<BD>( const PT<BD>::pixel *, intptr_t, const PT<BD>::pixel *const[4], \
+                                                 intptr_t, const PT<BD>::pixel *const[4], intptr_t, intptr_t, int,  \
+                                                 int, int, int, int, int, int, int, int, const uint16_t *, int,     \
+                                                 int16_t *, int32_t *, int16_t *, int32_t *, const int16_t *, int,  \
+                                                 int, const uint16_t *, uint16_t *, int32_t *, int32_t *,           \
+                                                 hipStream_t );
 INST( 8 )
 INST( 10 )
 #undef INST
