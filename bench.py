@@ -286,7 +286,26 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     res["lowres_me_pairs_per_s"] = world * max(1, a.steps // 5) * (F - 1) / wall
     res["lowres_me_launch_ms"] = ev_ms
     res["lowres_me_pairs_per_launch"] = F - 1
-    del louts, iouts, louts2, lref, lint
+    # the B-frame leg on the same planes: (p0, b, p1) = (k, k+1, k+2) for the F-2 triplets, both
+    # lists searched (a fresh slicetype_frame_cost with b_bidir), p1's list-0 mvs against p0 from
+    # one untimed P search as the bidir predictor, equal weights (i_bipred_weight 32, dsf 128)
+    ls_ = x.plane_stride(lw // 2)
+    nt = F - 2
+    nmb_ = mbw * mbh
+    p1m = x.lowres_inter_cost(louts[0][2:], [p[:-2] for p in louts], ls_, mbw, mbh, iouts[0][2:], (cm, span))[0]
+    bm = [torch.empty((nt, nmb_, 2), dtype=torch.int16, device="cuda") for _ in range(2)]
+    bk = [torch.empty((nt, nmb_), dtype=torch.int32, device="cuda") for _ in range(2)]
+    bargs = (louts[0][1:-1], [p[:-2] for p in louts], [p[2:] for p in louts], ls_, mbw, mbh, (cm, span), 3,
+             bm[0], bk[0], bm[1], bk[1])
+    bouts = x.lowres_bidir_cost(*bargs, p1_mvs=p1m)
+
+    def bstep():
+        x.lowres_bidir_cost(*bargs, p1_mvs=p1m, outs=bouts)
+    wall, ev_ms = timed(bstep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+    res["lowres_bidir_triplets_per_s"] = world * max(1, a.steps // 5) * nt / wall
+    res["lowres_bidir_launch_ms"] = ev_ms
+    res["lowres_bidir_triplets_per_launch"] = nt
+    del louts, iouts, louts2, lref, lint, p1m, bm, bk, bouts, bargs
     nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
     bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)

@@ -174,9 +174,10 @@ def test_dc_and_quant_dc_batch(hip, oracle, bd):
             assert np.array_equal(g[i], want) and nz[i] == wnz, (name, i)
 
 
-@pytest.fixture(params=["default", "1", "2", "3", "4", "5"])
+@pytest.fixture(params=["default", "0", "1", "2", "3", "4", "5", "6", "7"])
 def dq_variant(request, monkeypatch):
-    """X264HIP_DQ_VARIANT: 1 block-major, 2 unstaged strip, 3 / 4 band layout staged / direct (transform 4)."""
+    """X264HIP_DQ_VARIANT: 0 / 2 staged / unstaged strip, 1 block-major, 3 / 4 band layout staged /
+    direct, 5 half band (transform 4), 6 / 7 packed 16-bit staged / direct (8 bit, transform 8)."""
     if request.param != "default":
         monkeypatch.setenv("X264HIP_DQ_VARIANT", request.param)
     else:
@@ -211,3 +212,45 @@ def test_mb_dct_quant_1080p(hip, oracle, bd, transform, dq_variant):
         assert np.array_equal(dct[f * nmb:(f + 1) * nmb], wd), f
         assert np.array_equal(nz[f * nmb:(f + 1) * nmb], wn), f
     assert nz.any() and (nz == 0).any()
+
+
+@pytest.mark.parametrize("variant", ["default", "0", "7"])
+@pytest.mark.parametrize("cqm", [0, 3, 5])
+def test_mb_dct8_quant_extremes(hip, oracle, monkeypatch, variant, cqm):
+    """8-bit transform 8 at the residual extremes the packed 16-bit kernel's range argument
+    covers (checkerboards of +-255, constant +-255, uniform noise) with the largest mf of
+    every CQM family (all-ones lists: the uint32 (f + |c|) * mf wraps) at QP 0, 26 and 51;
+    20 MBs wide so the last 16-MB strip is partial."""
+    if variant != "default":
+        monkeypatch.setenv("X264HIP_DQ_VARIANT", variant)
+    else:
+        monkeypatch.delenv("X264HIP_DQ_VARIANT", raising=False)
+    mbw, mbh = 20, 3
+    W, H = 16 * mbw, 16 * mbh
+    stride = W + 64
+    origin = 32 * stride + 32
+    rng = np.random.default_rng(cqm)
+    yy, xx = np.mgrid[0:H + 64, 0:stride]
+    cb1 = (((xx + yy) & 1) * 255).astype(np.uint8)
+    cb2 = ((((xx >> 1) + (yy >> 2)) & 1) * 255).astype(np.uint8)
+    fr = [cb1, 255 - cb1, cb2, np.zeros_like(cb1), np.full_like(cb1, 255),
+          rng.integers(0, 256, cb1.shape, dtype=np.uint8), rng.integers(0, 256, cb1.shape, dtype=np.uint8)]
+    pairs = [(0, 1), (1, 0), (2, 3), (4, 3), (3, 4), (5, 6), (4, 2)]
+    fenc = np.stack([fr[a] for a, _ in pairs])
+    pred = np.stack([fr[b] for _, b in pairs])
+    q4m, q4b, q8m, q8b = hip.cqm_init(8, cb.cqm_lists(cqm, 8))
+    fd, pd = torch.from_numpy(fenc).cuda(), torch.from_numpy(pred).cuda()
+    fsz = fenc[0].size
+    nmb = mbw * mbh
+    for qp in (0, 26, 51):
+        for lst in (1, 3):
+            mf, bias = q8m[lst, qp], q8b[lst, qp]
+            dct, nz = hip.mb_dct_quant(8, fd, origin, stride, pd, origin, stride, mbw, mbh, len(pairs),
+                                       torch.from_numpy(mf.copy()).cuda(), torch.from_numpy(bias.copy()).cuda(),
+                                       fenc_frame_stride=fsz, pred_frame_stride=fsz)
+            dct, nz = dct.cpu().numpy(), nz.cpu().numpy()
+            for f in range(len(pairs)):
+                wd, wn = oracle.mb_dct_quant(8, 8, fenc[f].ravel(), origin, stride, pred[f].ravel(), origin, stride,
+                                             mbw, mbh, mf, bias)
+                assert np.array_equal(dct[f * nmb:(f + 1) * nmb], wd), (qp, lst, f)
+                assert np.array_equal(nz[f * nmb:(f + 1) * nmb], wn), (qp, lst, f)

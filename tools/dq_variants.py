@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B of the fused DCT+quant kernels (X264HIP_DQ_VARIANT 1 = block-major, default =
-strip) in one process; 1080p, F frame pairs (default 64: working set > 256 MiB MALL)."""
+strip, 6/7 = packed 8-bit transform 8) in one process; 1080p, F frame pairs (default 64: working set > 256 MiB MALL)."""
 import os, sys, json
 import numpy as np
 import torch
@@ -10,6 +10,7 @@ x = load_package(); x.init(0)
 from x264hip import synth
 F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
 res = {}
+VS = ("1", "2", "3", "4", "5", "6", "7", "0")
 for bd in (8, 10):
     W, H = 1920, 1088
     base, stride, origin = synth.make_sequence(17, W, H, bd)
@@ -24,7 +25,7 @@ for bd in (8, 10):
         mf, bias = torch.from_numpy(mf.copy()).cuda(), torch.from_numpy(bias.copy()).cuda()
         outs = {}
         times = {}
-        for v in ("1", "2", "3", "4", "5", "0"):
+        for v in VS:
             os.environ["X264HIP_DQ_VARIANT"] = v
             outs[v] = x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin + 2 * stride + 3, stride, W // 16,
                                      H // 16, F, mf, bias, fenc_frame_stride=fsz, pred_frame_stride=fsz)
@@ -34,10 +35,10 @@ for bd in (8, 10):
             x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin + 2 * stride + 3, stride, W // 16,
                            H // 16, F, mf, bias, dct=outs["1"][0], nz=outs["1"][1], fenc_frame_stride=fsz,
                            pred_frame_stride=fsz)
-        for v in ("2", "3", "4", "5", "0"):
+        for v in VS[1:]:
             assert torch.equal(outs["1"][0], outs[v][0]) and torch.equal(outs["1"][1], outs[v][1]), v
         for rnd in range(5):
-            for v in ("1", "2", "3", "4", "5", "0"):
+            for v in VS:
                 os.environ["X264HIP_DQ_VARIANT"] = v
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -50,7 +51,7 @@ for bd in (8, 10):
         ps = 1 if bd == 8 else 2
         cs = 2 if bd == 8 else 4
         alg = nmb * 256 * (2 * ps + cs) + nmb * 4
-        for v in ("1", "2", "3", "4", "5", "0"):
+        for v in VS:
             ms = float(np.median(times[v]))
             res[f"bd{bd}_t{t}_v{v}"] = {"ms": ms, "Gblocks_s": nmb * (16 if t == 4 else 4) / ms / 1e6,
                                        "GBps": alg / ms / 1e6, "hbm_frac": alg / ms / 1e6 / 8000}

@@ -739,6 +739,174 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
         dst[i] = src[i];
 }
 
+// Variant 6 (8 bit, transform 8, the default there): sub8x8_dct8 + quant_8x8 on
+// packed 16-bit pairs.  For 8-bit residuals the reference's int16 intermediates
+// (dct.c:332-377) never leave int16 range -- column-pass outputs are at most
+// 8*255 = 2040 in magnitude and every row-pass partial sum at most ~17.9k -- so
+// v_pk_* arithmetic on pairs gives the reference's values bit for bit: the
+// column pass runs on pairs of adjacent columns as the pixels arrive, one
+// v_perm per register regroups them into pairs of rows, and the row pass then
+// yields the reference's out[x*8+i], out[x*8+i+1] already paired in memory
+// order.  QUANT_ONE runs on pairs too: |c| and the sign with v_pk ops, the
+// uint32 (f + |c|) * mf as |c| * mf + f*mf (f*mf from the scalar unit, wrap
+// preserved) in 24-bit multiply-adds, and one v_perm takes both >> 16 results.
+// Same strip mapping as mb_dct_quant_strip_kernel; the LDS stage is
+// XOR-swizzled per 16-B chunk so the eight lanes of a ds_write_b128 group hit
+// distinct banks.
+typedef short dq_s2 __attribute__( ( ext_vector_type( 2 ) ) );
+
+__device__ __forceinline__ dq_s2 dq_as2( uint32_t v ) { return __builtin_bit_cast( dq_s2, v ); }
+__device__ __forceinline__ uint32_t dq_asu( dq_s2 v ) { return __builtin_bit_cast( uint32_t, v ); }
+
+#define DCT8_1D_PK( S, D )                                                              \
+    {                                                                                   \
+        const dq_s2 s07 = S( 0 ) + S( 7 ), s16 = S( 1 ) + S( 6 ), s25 = S( 2 ) + S( 5 ), \
+                    s34 = S( 3 ) + S( 4 );                                              \
+        const dq_s2 a0 = s07 + s34, a1 = s16 + s25, a2 = s07 - s34, a3 = s16 - s25;     \
+        const dq_s2 d07 = S( 0 ) - S( 7 ), d16 = S( 1 ) - S( 6 ), d25 = S( 2 ) - S( 5 ), \
+                    d34 = S( 3 ) - S( 4 );                                              \
+        const dq_s2 a4 = d16 + d25 + ( d07 + ( d07 >> 1 ) );                            \
+        const dq_s2 a5 = d07 - d34 - ( d25 + ( d25 >> 1 ) );                            \
+        const dq_s2 a6 = d07 + d34 - ( d16 + ( d16 >> 1 ) );                            \
+        const dq_s2 a7 = d16 - d25 + ( d34 + ( d34 >> 1 ) );                            \
+        D( 0, a0 + a1 );                                                                \
+        D( 1, a4 + ( a7 >> 2 ) );                                                       \
+        D( 2, a2 + ( a3 >> 1 ) );                                                       \
+        D( 3, a5 + ( a6 >> 2 ) );                                                       \
+        D( 4, a0 - a1 );                                                                \
+        D( 5, a6 - ( a5 >> 2 ) );                                                       \
+        D( 6, ( a2 >> 1 ) - a3 );                                                       \
+        D( 7, ( a4 >> 2 ) - a7 );                                                       \
+    }
+
+template <bool STAGE>
+__global__ __launch_bounds__( 256 ) void mb_dct8_quant_pk_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
+                                                                  intptr_t ffs, const uint8_t *__restrict__ pred,
+                                                                  intptr_t ps, intptr_t pfs, int mbw, int mbh,
+                                                                  int nframes, const uint16_t *__restrict__ mf,
+                                                                  const uint16_t *__restrict__ bias,
+                                                                  int16_t *__restrict__ dct, int32_t *__restrict__ nz )
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const int spr = (mbw + 15) >> 4;
+    if( wave >= (int64_t)nframes * mbh * spr )
+        return;                                               // wave-uniform
+    const int strip = (int)(wave % spr);
+    const int64_t t = wave / spr;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+    const int64_t mbrow = (f * mbh + mby) * (int64_t)mbw;
+    __shared__ uint4 lds[STAGE ? 4 * 64 * 8 : 1];             // per wave: 64 blocks x 8 chunks of 16 B
+    uint4 *stage = lds + (threadIdx.x >> 6) * 512;
+    uint4 *dst = (uint4 *)(dct + (mbrow + strip * 16) * 256);
+    const int bx = lane & 31, by = lane >> 5;                 // 8x8 block column / row in the strip
+    const int mbx = strip * 16 + (bx >> 1);
+    const bool live = mbx < mbw;
+    const int slot = (bx >> 1) * 4 + by * 2 + (bx & 1);      // block of the wave's 16 MBs, table order
+    const int key = bx & 7;
+    int mask = 0;
+    if( live )
+    {
+        const uint8_t *a = fenc + f * ffs + (intptr_t)(16 * mby + 8 * by) * fs + 256 * strip + 8 * bx;
+        const uint8_t *b = pred + f * pfs + (intptr_t)(16 * mby + 8 * by) * ps + 256 * strip + 8 * bx;
+        dq_s2 P[8][4];                                        // P[row][k] = (d[row][2k], d[row][2k+1])
+#pragma unroll
+        for( int y = 0; y < 8; y++ )
+        {
+            uint32_t wa[2], wb[2];
+            load_packed<2>( a + y * fs, wa );
+            load_packed<2>( b + y * ps, wb );
+#pragma unroll
+            for( int k = 0; k < 2; k++ )
+            {
+                P[y][2 * k] = dq_as2( __builtin_amdgcn_perm( 0u, wa[k], 0x0c010c00u ) ) -
+                              dq_as2( __builtin_amdgcn_perm( 0u, wb[k], 0x0c010c00u ) );
+                P[y][2 * k + 1] = dq_as2( __builtin_amdgcn_perm( 0u, wa[k], 0x0c030c02u ) ) -
+                                  dq_as2( __builtin_amdgcn_perm( 0u, wb[k], 0x0c030c02u ) );
+            }
+        }
+        // column pass on column pairs: SRC(x) = d[x][i]
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            dq_s2 o[8];
+#define S( x ) P[x][k]
+#define D( x, v ) o[x] = ( v )
+            DCT8_1D_PK( S, D )
+#undef S
+#undef D
+#pragma unroll
+            for( int x = 0; x < 8; x++ )
+                P[x][k] = o[x];
+        }
+        // row pass on row pairs (2j, 2j+1): out[x*8+2j], out[x*8+2j+1] = dword x*4+j
+        uint32_t out[8][4];
+        uint32_t acc = 0;
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+        {
+            dq_s2 q[8];
+#pragma unroll
+            for( int k = 0; k < 4; k++ )
+            {
+                q[2 * k] = dq_as2( __builtin_amdgcn_perm( dq_asu( P[2 * j + 1][k] ), dq_asu( P[2 * j][k] ), 0x05040100u ) );
+                q[2 * k + 1] =
+                    dq_as2( __builtin_amdgcn_perm( dq_asu( P[2 * j + 1][k] ), dq_asu( P[2 * j][k] ), 0x07060302u ) );
+            }
+            dq_s2 r[8];
+#define S( x ) q[x]
+#define D( x, v ) r[x] = ( v )
+            DCT8_1D_PK( S, D )
+#undef S
+#undef D
+#pragma unroll
+            for( int x = 0; x < 8; x++ )
+            {
+                const uint32_t mfw = ((const uint32_t *)mf)[x * 4 + j];
+                const uint32_t bw = ((const uint32_t *)bias)[x * 4 + j];
+                const uint32_t fml = (mfw & 0xffff) * (bw & 0xffff), fmh = (mfw >> 16) * (bw >> 16);
+                const dq_s2 c = r[x];
+                const dq_s2 ng = (dq_s2)0 - c;
+                const uint32_t mg = dq_asu( __builtin_elementwise_max( c, ng ) );
+                const uint32_t ql = (mg & 0xffff) * (mfw & 0xffff) + fml;
+                const uint32_t qh = (mg >> 16) * (mfw >> 16) + fmh;
+                const dq_s2 qv = dq_as2( __builtin_amdgcn_perm( qh, ql, 0x07060302u ) );
+                const dq_s2 sg = ng >> 15;                    // -1 where c > 0, else 0 (QUANT_ONE's branches)
+                const uint32_t v = dq_asu( sg - (qv ^ sg) );
+                out[x][j] = v;
+                acc |= v;
+            }
+        }
+        mask = (acc != 0) << (by * 2 + (bx & 1));
+#pragma unroll
+        for( int x = 0; x < 8; x++ )
+        {
+            const uint4 v = make_uint4( out[x][0], out[x][1], out[x][2], out[x][3] );
+            if constexpr( STAGE )
+                stage[slot * 8 + (x ^ key)] = v;
+            else
+                dst[slot * 8 + x] = v;
+        }
+    }
+    mask |= __builtin_amdgcn_update_dpp( 0, mask, 0xB1, 0xF, 0xF, false );   // lane ^ 1
+    mask |= __shfl_xor( mask, 32 );                                           // other block row
+    if( live && by == 0 && !(bx & 1) )
+        nz[mbrow + mbx] = mask;
+    if constexpr( !STAGE )
+        return;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
+    const int nmb = min( 16, mbw - strip * 16 );
+    for( int i = lane; i < nmb * 32; i += 64 )
+    {
+        const int s = i >> 3;
+        const int k = (((s >> 2) * 2 + (s & 1)) & 7);        // the writer's key
+        dst[i] = stage[s * 8 + ((i & 7) ^ k)];
+    }
+}
+#undef DCT8_1D_PK
+
 template <int BD>
 hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                                 const typename PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs, int mbw, int mbh,
@@ -776,6 +944,19 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
                                     pfs, mbw, mbh, nframes, mf, bias, dct, nz );
             return hipGetLastError();
         }
+        // transform 8 at 8 bit default: variant 6 (packed 16-bit pairs, 7 = its unstaged stores); 0 / 2
+        // select the strip kernel
+        if constexpr( BD == 8 )
+            if( transform == 8 && (!ev || atoi( ev ) == 6 || atoi( ev ) == 7) )
+            {
+                if( !ev || atoi( ev ) == 6 )
+                    hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<true>, g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs,
+                                        mbw, mbh, nframes, mf, bias, dct, nz );
+                else
+                    hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<false>, g, blk, 0, stream, fenc, fs, ffs, pred, ps,
+                                        pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+                return hipGetLastError();
+            }
         const bool stage = !ev || atoi( ev ) != 2;
 #define DQ_STRIP( T, S ) hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, S> ), g, blk, 0, stream, fenc, fs, ffs, \
                                              pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz )

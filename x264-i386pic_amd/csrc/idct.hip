@@ -934,6 +934,161 @@ __global__ __launch_bounds__( 256 ) void mb_recon_pair_kernel( const typename PT
     }
 }
 
+// 8 bit, transform 8 (the default there): the coefficients stay packed as the
+// int16 pairs they are stored as -- (c[x*8+2k], c[x*8+2k+1]) in one dword --
+// and only the eight values one IDCT8_1D consumes are widened to int32, so a
+// lane holds a block in 32 registers instead of 64 and the int16 stores of
+// add8x8_idct8 (dct.c:420-440) become the v_perm that packs each result pair.
+// The column pass works on column pairs straight from that layout; the row
+// pass reads row i's pairs and yields residual columns i, which are packed
+// per pixel row and added to the prediction in 16-bit pairs (clip by
+// v_pk_max / v_pk_min).  dequant_8x8 (quant.c:106-146) multiplies in 24 bits
+// when every dequant_mf entry fits (checked per workgroup while the table is
+// staged in LDS; the 24-bit product keeps the low 32 bits the int32 product
+// wraps to), else with the full 32-bit multiply.
+typedef short rc_s2 __attribute__( ( ext_vector_type( 2 ) ) );
+
+__device__ __forceinline__ rc_s2 rc_as2( uint32_t v ) { return __builtin_bit_cast( rc_s2, v ); }
+__device__ __forceinline__ uint32_t rc_asu( rc_s2 v ) { return __builtin_bit_cast( uint32_t, v ); }
+__device__ __forceinline__ uint32_t rc_pack( int lo, int hi )
+{
+    return __builtin_amdgcn_perm( (uint32_t)hi, (uint32_t)lo, 0x05040100u );
+}
+
+template <bool M24>
+__device__ __forceinline__ void recon8_pk_block( const int16_t *__restrict__ dct, const int32_t *m, int q,
+                                                 const uint8_t *pp, intptr_t ps, uint8_t *rp, intptr_t rs )
+{
+    uint32_t C[8][4];                                     // C[x][k] = (c[x*8+2k], c[x*8+2k+1])
+#pragma unroll
+    for( int x = 0; x < 8; x++ )
+    {
+        const uint4 w = ((const uint4 *)dct)[x];
+        C[x][0] = w.x; C[x][1] = w.y; C[x][2] = w.z; C[x][3] = w.w;
+    }
+    const int qb = q / 6 - 6;
+    // dequant fused into the column pass on column pairs (2k, 2k+1): SRC(x) = c[x*8+i],
+    // results stored back as dctcoef
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+    {
+        asm volatile( "" ::: "memory" );                  // keep each pair's table reads with its pass
+#pragma unroll
+        for( int x = 0; x < 8; x++ )
+        {
+            const int2 mm = ((const int2 *)(m + x * 8 + 2 * k))[0];
+            int v[2];
+#pragma unroll
+            for( int h = 0; h < 2; h++ )
+            {
+                const int c = h ? (int)(int16_t)(C[x][k] >> 16) : (int)(int16_t)C[x][k];
+                const int mv = h ? mm.y : mm.x;
+                const int p = M24 ? __mul24( c, mv ) : c * mv;
+                v[h] = qb >= 0 ? (int)((uint32_t)p << qb) : (p + (1 << (-qb - 1))) >> (-qb);
+            }
+            C[x][k] = rc_pack( v[0], v[1] );
+        }
+        if( k == 0 )
+            C[0][0] = rc_asu( rc_as2( C[0][0] ) + (rc_s2){ 32, 0 } );   // dct[0] += 32, stored as dctcoef
+        int o[2][8];
+#pragma unroll
+        for( int h = 0; h < 2; h++ )
+        {
+#define SRC( x ) (h ? (int)(int16_t)(C[x][k] >> 16) : (int)(int16_t)C[x][k])
+#define DST( x, v ) o[h][x] = ( v )
+            IDCT8_1D( SRC, DST )
+#undef SRC
+#undef DST
+        }
+#pragma unroll
+        for( int x = 0; x < 8; x++ )
+            C[x][k] = rc_pack( o[0][x], o[1][x] );
+    }
+    // row pass on row pairs (i, i+1): SRC(x) = c[i*8+x]; residual r[y][i] = v >> 6 is added
+    // to the prediction pixel pair (y; i, i+1) in place (16-bit pairs, clip by v_pk_max/min)
+    uint32_t P[8][2];
+#pragma unroll
+    for( int y = 0; y < 8; y++ )
+        load_packed<2>( pp + y * ps, P[y] );
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+    {
+        int o[2][8];
+#pragma unroll
+        for( int h = 0; h < 2; h++ )
+        {
+            const int i = 2 * k + h;
+#define SRC( x ) (((x) & 1) ? (int)(int16_t)(C[i][(x) >> 1] >> 16) : (int)(int16_t)C[i][(x) >> 1])
+#define DST( x, v ) o[h][x] = ( v ) >> 6
+            IDCT8_1D( SRC, DST )
+#undef SRC
+#undef DST
+        }
+        const uint32_t SEL = (k & 1) ? 0x0c030c02u : 0x0c010c00u;   // pixels 2k, 2k+1 of the dword
+#pragma unroll
+        for( int y = 0; y < 8; y++ )
+        {
+            rc_s2 v = rc_as2( __builtin_amdgcn_perm( 0u, P[y][k >> 1], SEL ) ) + rc_as2( rc_pack( o[0][y], o[1][y] ) );
+            v = __builtin_elementwise_min( __builtin_elementwise_max( v, (rc_s2)0 ), (rc_s2)255 );
+            // put the two result bytes back in place of the two prediction bytes
+            P[y][k >> 1] = (k & 1) ? __builtin_amdgcn_perm( rc_asu( v ), P[y][k >> 1], 0x06040100u )
+                                   : __builtin_amdgcn_perm( P[y][k >> 1], rc_asu( v ), 0x07060200u );
+        }
+    }
+#pragma unroll
+    for( int y = 0; y < 8; y++ )
+    {
+        if( ((uintptr_t)(rp + y * rs) & 3) == 0 )
+        {
+            ((uint32_t *)(rp + y * rs))[0] = P[y][0];
+            ((uint32_t *)(rp + y * rs))[1] = P[y][1];
+        }
+        else
+        {
+#pragma unroll
+            for( int x = 0; x < 8; x++ )
+                rp[y * rs + x] = (uint8_t)(P[y][x >> 2] >> (8 * (x & 3)));
+        }
+    }
+}
+
+__global__ __launch_bounds__( 256 ) void mb_recon8_pk_kernel( const int16_t *__restrict__ dct, int mbw, int mbh,
+                                                              int nframes, const int32_t *__restrict__ dmf,
+                                                              const int32_t *__restrict__ qp,
+                                                              const uint8_t *pred, intptr_t ps, intptr_t pfs,
+                                                              uint8_t *recon, intptr_t rs, intptr_t rfs )
+{
+    // the 6 x 64 dequant_mf table in LDS, rows 68 dwords apart (lanes on different qp%6
+    // rows read different 16-B slots of a bank row)
+    __shared__ int32_t tab[6 * 68];
+    int ok = 1;
+    for( int i = threadIdx.x; i < 6 * 64; i += blockDim.x )
+    {
+        const int v = dmf[i];
+        tab[(i >> 6) * 68 + (i & 63)] = v;
+        ok &= v >= -(1 << 23) && v < (1 << 23);
+    }
+    const bool m24 = __syncthreads_and( ok );
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int bw = mbw * 2, bh = mbh * 2;
+    if( t >= (int64_t)nframes * bw * bh )
+        return;
+    const int bx = (int)(t % bw);
+    const int64_t r = t / bw;
+    const int by = (int)(r % bh);
+    const int f = (int)(r / bh);
+    const int64_t mb = ((int64_t)f * mbh + (by >> 1)) * mbw + (bx >> 1);
+    const int q = qp[mb];
+    const int16_t *c = dct + mb * 256 + ((by & 1) * 2 + (bx & 1)) * 64;
+    const uint8_t *pp = pred + f * pfs + (intptr_t)(by * 8) * ps + bx * 8;
+    uint8_t *rp = recon + f * rfs + (intptr_t)(by * 8) * rs + bx * 8;
+    const int32_t *m = tab + (q % 6) * 68;
+    if( m24 )
+        recon8_pk_block<true>( c, m, q, pp, ps, rp, rs );
+    else
+        recon8_pk_block<false>( c, m, q, pp, ps, rp, rs );
+}
+
 template <int BD>
 hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, int mbw, int mbh, int nframes,
                             const int32_t *dmf, const int32_t *qp, const typename PT<BD>::pixel *pred, intptr_t ps,
@@ -945,6 +1100,15 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
     // 8 bit: block pairs (0.55 vs 0.43 of HBM, tools/recon_variants.py); 10 bit: one lane
     // per block is faster (0.68 vs 0.58); X264HIP_RECON_VARIANT = 0 / 1 forces either
     const bool pair = ev ? atoi( ev ) != 1 : BD == 8;
+    // transform 8 at 8 bit: the packed kernel unless X264HIP_RECON_VARIANT = 1 (lane per block, int32)
+    if constexpr( BD == 8 )
+        if( transform == 8 && (!ev || atoi( ev ) != 1) )
+        {
+            const int64_t total = (int64_t)nframes * mbw * mbh * 4;
+            hipLaunchKernelGGL( mb_recon8_pk_kernel, dim3( (unsigned)((total + 255) / 256) ), dim3( 256 ), 0, st, dct,
+                                mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs, rfs );
+            return hipGetLastError();
+        }
     if( transform == 4 && pair )
     {
         const int64_t waves = (int64_t)nframes * mbh * ((mbw + 7) / 8);
