@@ -403,3 +403,46 @@ def test_mb_dequant_idct_add_frames(hip, oracle, bd, transform, recon_variant):
                                    want, origin, stride)
         w2, g2 = want.reshape(planes[0].shape), got[f]
         assert np.array_equal(g2[32:32 + H, 32:32 + W], w2[32:32 + H, 32:32 + W]), f
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("transform", [4, 8])
+@pytest.mark.parametrize("dmf_kind,crange", [("cqm", "full"), ("huge", "full"), ("cqm", "mid"), ("cqm", "small")])
+def test_mb_dequant_idct_add_extremes(hip, oracle, bd, transform, dmf_kind, crange, recon_variant):
+    """uniform random coefficients over the whole dctcoef range and per-MB qp 0..max, so the
+    dequant products and IDCT intermediates wrap as the reference's int16 / int32 stores do;
+    'huge' dequant_mf entries (>= 2^23) take the kernels' full 32-bit multiply, the CQM ones
+    the 24-bit one; 'mid' / 'small' levels at qp <= 30 land on both sides of the 8-bit 8x8
+    kernel's +-4096 int16-pair bound (column pass packed and row pass int32, or both packed);
+    unaligned recon rows (origin + 1)."""
+    mbw, mbh, F = 20, 3, 2
+    W, H = 16 * mbw, 16 * mbh
+    stride = W + 64
+    origin = 32 * stride + 32
+    rs = np.random.default_rng(bd * 100 + transform * 10 + (dmf_kind == "huge"))
+    pdt = np.uint8 if bd == 8 else np.uint16
+    pmax = (1 << bd) - 1
+    planes = rs.integers(0, pmax + 1, (F, H + 64, stride)).astype(pdt)
+    cdt = np.int16 if bd == 8 else np.int32
+    lim = {"full": 1 << 15 if bd == 8 else 1 << 20, "mid": 40, "small": 12}[crange]
+    dc = rs.integers(-lim, lim, (F * mbw * mbh, 256)).astype(cdt)
+    dc[rs.random(dc.shape) < 0.5] = 0
+    qmax = 51 + 6 * (bd - 8) if crange == "full" else 30
+    qp = rs.integers(0, qmax + 1, F * mbw * mbh).astype(np.int32)
+    dq4, dq8 = hip.cqm_dequant(cb.cqm_lists(4, bd))
+    dmf = np.ascontiguousarray((dq8[1] if transform == 8 else dq4[1]).astype(np.int32))
+    if dmf_kind == "huge":
+        dmf = dmf * 4099 + (1 << 23)
+    pred = _T(planes)
+    recon = torch.zeros_like(pred)
+    ro = origin + 1
+    hip.mb_dequant_idct_add(transform, _T(dc), mbw, mbh, F, _T(dmf), _T(qp), pred, origin, stride, recon, ro,
+                            stride, pred_frame_stride=planes[0].size, recon_frame_stride=planes[0].size)
+    got = recon.cpu().numpy().view(pdt)
+    for f in range(F):
+        want = np.zeros_like(planes[0]).ravel()
+        sl = slice(f * mbw * mbh, (f + 1) * mbw * mbh)
+        oracle.mb_dequant_idct_add(bd, transform, dc[sl], mbw, mbh, dmf, qp[sl], planes[f].ravel(), origin, stride,
+                                   want, ro, stride)
+        w2 = want.reshape(planes[0].shape)
+        assert np.array_equal(got[f][32:32 + H, 33:33 + W], w2[32:32 + H, 33:33 + W]), f

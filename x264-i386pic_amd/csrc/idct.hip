@@ -955,6 +955,33 @@ __device__ __forceinline__ uint32_t rc_pack( int lo, int hi )
     return __builtin_amdgcn_perm( (uint32_t)hi, (uint32_t)lo, 0x05040100u );
 }
 
+#define IDCT8_1D_PK( SRC, DST )                                                                \
+    {                                                                                          \
+        const rc_s2 a0 = SRC( 0 ) + SRC( 4 ), a2 = SRC( 0 ) - SRC( 4 );                        \
+        const rc_s2 a4 = (SRC( 2 ) >> 1) - SRC( 6 ), a6 = (SRC( 6 ) >> 1) + SRC( 2 );          \
+        const rc_s2 b0 = a0 + a6, b2 = a2 + a4, b4 = a2 - a4, b6 = a0 - a6;                    \
+        const rc_s2 a1 = -SRC( 3 ) + SRC( 5 ) - SRC( 7 ) - (SRC( 7 ) >> 1);                    \
+        const rc_s2 a3 = SRC( 1 ) + SRC( 7 ) - SRC( 3 ) - (SRC( 3 ) >> 1);                     \
+        const rc_s2 a5 = -SRC( 1 ) + SRC( 7 ) + SRC( 5 ) + (SRC( 5 ) >> 1);                    \
+        const rc_s2 a7 = SRC( 3 ) + SRC( 5 ) + SRC( 1 ) + (SRC( 1 ) >> 1);                     \
+        const rc_s2 b1 = (a7 >> 2) + a1, b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5, b7 = a7 - (a1 >> 2); \
+        DST( 0, b0 + b7 ); DST( 1, b2 + b5 ); DST( 2, b4 + b3 ); DST( 3, b6 + b1 );            \
+        DST( 4, b6 - b1 ); DST( 5, b4 - b3 ); DST( 6, b2 - b5 ); DST( 7, b0 - b7 );            \
+    }
+
+// max over the pairs of C of |v| + 4096 as unsigned 16-bit (<= 8192 iff every |v| <= 4096)
+__device__ __forceinline__ bool recon8_small( const uint32_t (&C)[8][4] )
+{
+    typedef unsigned short u2 __attribute__( ( ext_vector_type( 2 ) ) );
+    u2 mx = (u2)0;
+#pragma unroll
+    for( int x = 0; x < 8; x++ )
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            mx = __builtin_elementwise_max( mx, __builtin_bit_cast( u2, C[x][k] ) + (u2)4096 );
+    return mx.x <= 8192 && mx.y <= 8192;
+}
+
 template <bool M24>
 __device__ __forceinline__ void recon8_pk_block( const int16_t *__restrict__ dct, const int32_t *m, int q,
                                                  const uint8_t *pp, intptr_t ps, uint8_t *rp, intptr_t rs )
@@ -967,70 +994,114 @@ __device__ __forceinline__ void recon8_pk_block( const int16_t *__restrict__ dct
         C[x][0] = w.x; C[x][1] = w.y; C[x][2] = w.z; C[x][3] = w.w;
     }
     const int qb = q / 6 - 6;
-    // dequant fused into the column pass on column pairs (2k, 2k+1): SRC(x) = c[x*8+i],
-    // results stored back as dctcoef
 #pragma unroll
-    for( int k = 0; k < 4; k++ )
+    for( int x = 0; x < 8; x++ )
     {
-        asm volatile( "" ::: "memory" );                  // keep each pair's table reads with its pass
+        const int4 m0 = ((const int4 *)(m + x * 8))[0], m1 = ((const int4 *)(m + x * 8))[1];
+        const int mm[8] = { m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w };
 #pragma unroll
-        for( int x = 0; x < 8; x++ )
+        for( int k = 0; k < 4; k++ )
         {
-            const int2 mm = ((const int2 *)(m + x * 8 + 2 * k))[0];
             int v[2];
 #pragma unroll
             for( int h = 0; h < 2; h++ )
             {
                 const int c = h ? (int)(int16_t)(C[x][k] >> 16) : (int)(int16_t)C[x][k];
-                const int mv = h ? mm.y : mm.x;
+                const int mv = mm[2 * k + h];
                 const int p = M24 ? __mul24( c, mv ) : c * mv;
                 v[h] = qb >= 0 ? (int)((uint32_t)p << qb) : (p + (1 << (-qb - 1))) >> (-qb);
             }
             C[x][k] = rc_pack( v[0], v[1] );
         }
-        if( k == 0 )
-            C[0][0] = rc_asu( rc_as2( C[0][0] ) + (rc_s2){ 32, 0 } );   // dct[0] += 32, stored as dctcoef
-        int o[2][8];
+    }
+    C[0][0] = rc_asu( rc_as2( C[0][0] ) + (rc_s2){ 32, 0 } );   // dct[0] += 32, stored as dctcoef
+    // column pass (SRC(x) = c[x*8+i], stored back as dctcoef) on column pairs.  Every partial
+    // sum of IDCT8_1D is at most 7.875 max|input| (+ the floor shifts' units), so with all
+    // inputs within +-4096 the int16 pair arithmetic is exact; otherwise int32 per column.
+    if( recon8_small( C ) )
+    {
 #pragma unroll
-        for( int h = 0; h < 2; h++ )
+        for( int k = 0; k < 4; k++ )
         {
-#define SRC( x ) (h ? (int)(int16_t)(C[x][k] >> 16) : (int)(int16_t)C[x][k])
-#define DST( x, v ) o[h][x] = ( v )
-            IDCT8_1D( SRC, DST )
+            rc_s2 o[8];
+#define SRC( x ) rc_as2( C[x][k] )
+#define DST( x, v ) o[x] = ( v )
+            IDCT8_1D_PK( SRC, DST )
 #undef SRC
 #undef DST
-        }
 #pragma unroll
-        for( int x = 0; x < 8; x++ )
-            C[x][k] = rc_pack( o[0][x], o[1][x] );
+            for( int x = 0; x < 8; x++ )
+                C[x][k] = rc_asu( o[x] );
+        }
     }
-    // row pass on row pairs (i, i+1): SRC(x) = c[i*8+x]; residual r[y][i] = v >> 6 is added
-    // to the prediction pixel pair (y; i, i+1) in place (16-bit pairs, clip by v_pk_max/min)
+    else
+    {
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            int o[2][8];
+#pragma unroll
+            for( int h = 0; h < 2; h++ )
+            {
+#define SRC( x ) (h ? (int)(int16_t)(C[x][k] >> 16) : (int)(int16_t)C[x][k])
+#define DST( x, v ) o[h][x] = ( v )
+                IDCT8_1D( SRC, DST )
+#undef SRC
+#undef DST
+            }
+#pragma unroll
+            for( int x = 0; x < 8; x++ )
+                C[x][k] = rc_pack( o[0][x], o[1][x] );
+        }
+    }
+    // row pass on row pairs (i, i+1): SRC(x) = c[i*8+x]; residual r[y][i] = v >> 6 goes onto
+    // the prediction pixel pair (y; i, i+1) in place (16-bit pairs, clip by v_pk_max/min)
     uint32_t P[8][2];
 #pragma unroll
     for( int y = 0; y < 8; y++ )
         load_packed<2>( pp + y * ps, P[y] );
+    const bool small = recon8_small( C );
 #pragma unroll
     for( int k = 0; k < 4; k++ )
     {
-        int o[2][8];
-#pragma unroll
-        for( int h = 0; h < 2; h++ )
+        rc_s2 r[8];
+        if( small )
         {
-            const int i = 2 * k + h;
-#define SRC( x ) (((x) & 1) ? (int)(int16_t)(C[i][(x) >> 1] >> 16) : (int)(int16_t)C[i][(x) >> 1])
-#define DST( x, v ) o[h][x] = ( v ) >> 6
-            IDCT8_1D( SRC, DST )
+            rc_s2 sv[8];
+#pragma unroll
+            for( int x = 0; x < 8; x++ )
+                sv[x] = rc_as2( __builtin_amdgcn_perm( C[2 * k + 1][x >> 1], C[2 * k][x >> 1],
+                                                       (x & 1) ? 0x07060302u : 0x05040100u ) );
+#define SRC( x ) sv[x]
+#define DST( x, v ) r[x] = ( v ) >> 6
+            IDCT8_1D_PK( SRC, DST )
 #undef SRC
 #undef DST
+        }
+        else
+        {
+            int o[2][8];
+#pragma unroll
+            for( int h = 0; h < 2; h++ )
+            {
+                const int i = 2 * k + h;
+#define SRC( x ) (((x) & 1) ? (int)(int16_t)(C[i][(x) >> 1] >> 16) : (int)(int16_t)C[i][(x) >> 1])
+#define DST( x, v ) o[h][x] = ( v ) >> 6
+                IDCT8_1D( SRC, DST )
+#undef SRC
+#undef DST
+            }
+#pragma unroll
+            for( int y = 0; y < 8; y++ )
+                r[y] = rc_as2( rc_pack( o[0][y], o[1][y] ) );
         }
         const uint32_t SEL = (k & 1) ? 0x0c030c02u : 0x0c010c00u;   // pixels 2k, 2k+1 of the dword
 #pragma unroll
         for( int y = 0; y < 8; y++ )
         {
-            rc_s2 v = rc_as2( __builtin_amdgcn_perm( 0u, P[y][k >> 1], SEL ) ) + rc_as2( rc_pack( o[0][y], o[1][y] ) );
+            rc_s2 v = rc_as2( __builtin_amdgcn_perm( 0u, P[y][k >> 1], SEL ) ) + r[y];
             v = __builtin_elementwise_min( __builtin_elementwise_max( v, (rc_s2)0 ), (rc_s2)255 );
-            // put the two result bytes back in place of the two prediction bytes
+            // the two result bytes replace the two prediction bytes
             P[y][k >> 1] = (k & 1) ? __builtin_amdgcn_perm( rc_asu( v ), P[y][k >> 1], 0x06040100u )
                                    : __builtin_amdgcn_perm( P[y][k >> 1], rc_asu( v ), 0x07060200u );
         }
@@ -1051,6 +1122,7 @@ __device__ __forceinline__ void recon8_pk_block( const int16_t *__restrict__ dct
         }
     }
 }
+#undef IDCT8_1D_PK
 
 __global__ __launch_bounds__( 256 ) void mb_recon8_pk_kernel( const int16_t *__restrict__ dct, int mbw, int mbh,
                                                               int nframes, const int32_t *__restrict__ dmf,
