@@ -11,11 +11,13 @@
 // bit-exact schedule is a wavefront: block (x, y) runs at step
 // t = (W-1-x) + 2(H-1-y), after all four of its predictors.  One workgroup
 // walks one frame pair's W + 2H - 2 steps with a barrier between steps, one
-// lane per block row; the four most recent MVs of every row sit in an LDS
-// ring (the predictors of a step are at most three steps old).  Each lane
-// runs the block's whole search (HEX / DIA, the hpel and qpel refinement) with
-// the 8x8 SAD / SATD on fenc rows held in registers and get_ref rebuilt from
-// the four lowres planes; the frame pairs of a batch run in parallel.
+// lane quad per block row (each lane two of the block's eight pixel rows, the
+// metrics finished by DPP quad reductions); the four most recent MVs of every
+// row sit in an LDS ring (the predictors of a step are at most three steps
+// old).  Each quad runs the block's whole search (HEX / DIA, the hpel and qpel
+// refinement) with fenc rows held in registers, integer patterns scored from a
+// register window of the F plane and get_ref rebuilt from the four lowres
+// planes; the frame pairs of a batch run in parallel.
 #include "hipcommon.h"
 
 namespace x264hip {
@@ -37,60 +39,94 @@ __device__ __forceinline__ int lr_median( int a, int b, int c )
     return c < mn ? mn : c > mx ? mx : c;
 }
 
-// 8x8 SAD or packed SATD of fenc rows against predicted rows
+// Lanes 4y .. 4y+3 of a workgroup share block row y: lane q = lane & 3 holds rows
+// 2q and 2q+1 of the 8x8 block, so every metric costs a quarter of its pixel work
+// per lane and is finished by a reduction over the quad (all four lanes end with
+// the same value and run the same search path).
+constexpr int LR_NR = 2;
+
+__device__ __forceinline__ uint32_t lr_swap1( uint32_t v )      // lane q ^ 1
+{
+    return (uint32_t)__builtin_amdgcn_mov_dpp( (int)v, 0xB1, 0xF, 0xF, true );   // quad_perm [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t lr_quad_sum( uint32_t v )
+{
+    v += lr_swap1( v );
+    v += (uint32_t)__builtin_amdgcn_mov_dpp( (int)v, 0x4E, 0xF, 0xF, true );      // quad_perm [2,3,0,1]
+    return v;
+}
+
+// 8x8 SAD or packed SATD of fenc rows against predicted rows (this lane's two rows).
+// SATD: lanes 2b and 2b+1 hold rows 0-1 and 2-3 of band b; each takes the horizontal
+// Hadamard of its rows and the first vertical stage, the partner's half arrives by
+// DPP and the even lane forms t0+t2 / t1+t3, the odd lane t2-t0 / t3-t1 (the
+// negated t0-t2 / t1-t3: same magnitude, and the 0x8000 bias on element (0,0),
+// applied by the even lane, stays 0x8000 mod 2^16 under negation).
 template <int BD>
-__device__ __forceinline__ int lr_cmp_rows( const uint32_t (&fe)[8][8 / PT<BD>::PPD],
-                                            const uint32_t (&r)[8][8 / PT<BD>::PPD], bool use_satd )
+__device__ __forceinline__ int lr_cmp_rows( const uint32_t (&fe)[LR_NR][8 / PT<BD>::PPD],
+                                            const uint32_t (&r)[LR_NR][8 / PT<BD>::PPD], bool use_satd, int q )
 {
     constexpr int NDW = 8 / PT<BD>::PPD;
     uint32_t acc = 0;
     if( use_satd )
     {
+        const bool odd = q & 1;
+        x264hip_short2 d[LR_NR][4];
 #pragma unroll
-        for( int band = 0; band < 2; band++ )
+        for( int j = 0; j < LR_NR; j++ )
         {
-            uint32_t fa[4][NDW], ra[4][NDW];
+            x264hip_short2 p[4];
 #pragma unroll
-            for( int y = 0; y < 4; y++ )
-#pragma unroll
-                for( int k = 0; k < NDW; k++ )
-                {
-                    fa[y][k] = fe[4 * band + y][k];
-                    ra[y][k] = r[4 * band + y][k];
-                }
-            acc += satd8x4_packed<BD>( fa, ra );
+            for( int x = 0; x < 4; x++ )
+                p[x] = pair_px<BD>( fe[j], x ) - pair_px<BD>( r[j], x );
+            if( j == 0 )
+                p[0] = odd ? p[0] : sat_bias( p[0] );
+            const x264hip_short2 t0 = p[0] + p[1], t1 = p[0] - p[1], t2 = p[2] + p[3], t3 = p[2] - p[3];
+            d[j][0] = t0 + t2; d[j][2] = t0 - t2; d[j][1] = t1 + t3; d[j][3] = t1 - t3;
         }
-        return (int)(acc >> 1);
+#pragma unroll
+        for( int x = 0; x < 4; x++ )
+        {
+            const x264hip_short2 ta = d[0][x] + d[1][x], tb = d[0][x] - d[1][x];
+            const x264hip_short2 pa = __builtin_bit_cast( x264hip_short2, lr_swap1( __builtin_bit_cast( uint32_t, ta ) ) );
+            const x264hip_short2 pb = __builtin_bit_cast( x264hip_short2, lr_swap1( __builtin_bit_cast( uint32_t, tb ) ) );
+            const x264hip_short2 ca = odd ? ta - pa : ta + pa, cb = odd ? tb - pb : tb + pb;
+            acc = __builtin_amdgcn_sad_u16( __builtin_bit_cast( uint32_t, ca ), 0x80008000u, acc );
+            acc = __builtin_amdgcn_sad_u16( __builtin_bit_cast( uint32_t, cb ), 0x80008000u, acc );
+        }
+        return (int)(lr_quad_sum( acc ) >> 1);
     }
 #pragma unroll
-    for( int y = 0; y < 8; y++ )
+    for( int y = 0; y < LR_NR; y++ )
 #pragma unroll
         for( int k = 0; k < NDW; k++ )
             acc = sadp<BD>( fe[y][k], r[y][k], acc );
-    return (int)acc;
+    return (int)lr_quad_sum( acc );
 }
 
 template <int BD> struct LrCtx
 {
     using pixel = typename PT<BD>::pixel;
     static constexpr int NDW = 8 / PT<BD>::PPD;
-    const uint32_t (&fe)[8][NDW];           // fenc block rows (packed pixels), shared by the lists
-    const pixel *p0, *p1, *p2, *p3;         // reference F, H, V, C at the block
+    const uint32_t (&fe)[LR_NR][NDW];       // this lane's fenc rows (packed pixels), shared by the lists
+    const pixel *p0, *p1, *p2, *p3;         // reference F, H, V, C at the block, row 2q
     intptr_t stride;
     const uint16_t *cmx, *cmy;              // p_cost_mvx / p_cost_mvy (cost_mv - mvp)
-    int satd;
+    int satd, q;
     int smin0, smax0, smin1, smax1;         // h->mb.mv_min_spel / mv_max_spel
     int fmin0, fmax0, fmin1, fmax1;         // mv_limit_fpel
 
-    __device__ __forceinline__ LrCtx( const uint32_t (&f)[8][NDW] ) : fe( f ) {}
+    __device__ __forceinline__ LrCtx( const uint32_t (&f)[LR_NR][NDW] ) : fe( f ) {}
 
     // per-block setup of slicetype_mb_cost (slicetype.c:539-557): the lowres mv limits
     // (the vertical ones, set at the first block of each row of the scan, depend on
-    // the row only) and the reference planes at the block
+    // the row only) and the reference planes at the lane's first block row
     __device__ __forceinline__ void setup( const pixel *r0, const pixel *r1, const pixel *r2, const pixel *r3,
                                            intptr_t off, intptr_t s, int x, int y, int mbw, int mbh, int mvr,
-                                           int use_satd )
+                                           int use_satd, int lane_q )
     {
+        q = lane_q;
+        off += (intptr_t)(LR_NR * q) * s;
         p0 = r0 + off;
         p1 = r1 + off;
         p2 = r2 + off;
@@ -113,7 +149,7 @@ template <int BD> struct LrCtx
         const pixel *r = p0 + (intptr_t)my * stride + mx;
         uint32_t acc = 0;
 #pragma unroll
-        for( int y = 0; y < 8; y++ )
+        for( int y = 0; y < LR_NR; y++ )
         {
             uint32_t w[NDW];
             load_row_u<NDW>( r + (intptr_t)y * stride, w );
@@ -121,11 +157,58 @@ template <int BD> struct LrCtx
             for( int k = 0; k < NDW; k++ )
                 acc = sadp<BD>( fe[y][k], w[k], acc );
         }
-        return (int)acc;
+        return (int)lr_quad_sum( acc );
+    }
+
+    // The F plane's window around a full-pel centre (columns cx-2 .. cx+9; this lane's
+    // rows 2q-2 .. 2q+3 of the block, i.e. the rows its two block rows meet for any
+    // vertical offset in [-2, 2]): one dword-aligned load per row, realigned once by
+    // the byte offset all rows share (stride * sizeof(pixel) is a multiple of 4), so
+    // every integer candidate within +-2 of the centre -- a diamond, a hexagon, the
+    // square refine -- is scored from registers.
+    static constexpr int WR = LR_NR + 4, WD = 12 / PT<BD>::PPD;
+    __device__ __forceinline__ void win( int cx, int cy, uint32_t (&w)[WR][WD] ) const
+    {
+        const uintptr_t a = (uintptr_t)(p0 + (intptr_t)(cy - 2) * stride + (cx - 2));
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint8_t *b = (const uint8_t *)(a & ~(uintptr_t)3);
+        const intptr_t sb = stride * (intptr_t)sizeof( pixel );
+#pragma unroll
+        for( int r = 0; r < WR; r++ )
+        {
+            const uint32_t *row = (const uint32_t *)(b + r * sb);
+            uint32_t v[WD + 1];
+#pragma unroll
+            for( int k = 0; k <= WD; k++ )
+                v[k] = row[k];
+#pragma unroll
+            for( int k = 0; k < WD; k++ )
+                w[r][k] = __builtin_amdgcn_alignbyte( v[k + 1], v[k], sh );
+        }
+    }
+
+    // fpel( cx + DX, cy + DY ) from the window of (cx, cy), |DX|, |DY| <= 2
+    template <int DX, int DY> __device__ __forceinline__ int wsad( const uint32_t (&w)[WR][WD] ) const
+    {
+        constexpr int B = (DX + 2) * (int)sizeof( pixel ), D = B >> 2, S = B & 3;
+        uint32_t acc = 0;
+#pragma unroll
+        for( int y = 0; y < LR_NR; y++ )
+#pragma unroll
+            for( int k = 0; k < NDW; k++ )
+            {
+                uint32_t v;
+                if constexpr( S != 0 )
+                    v = __builtin_amdgcn_alignbyte( w[DY + 2 + y][D + k + 1], w[DY + 2 + y][D + k], S );
+                else
+                    v = w[DY + 2 + y][D + k];
+                acc = sadp<BD>( fe[y][k], v, acc );
+            }
+        return (int)lr_quad_sum( acc );
     }
 
     // get_ref (mc.c:221-249) rows at a quarter-pel mv
-    __device__ __forceinline__ void ref_rows( int mx, int my, uint32_t (&r)[8][NDW] ) const
+    __device__ __forceinline__ void ref_rows( int mx, int my, uint32_t (&r)[LR_NR][NDW] ) const
     {
         const int idx = ((my & 3) << 2) + (mx & 3);
         const intptr_t off = (intptr_t)(my >> 2) * stride + (mx >> 2);
@@ -133,7 +216,7 @@ template <int BD> struct LrCtx
         const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((my & 3) == 3) * stride;
         const pixel *s2 = (idx & 5) ? (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((mx & 3) == 3) : s1;
 #pragma unroll
-        for( int y = 0; y < 8; y++ )
+        for( int y = 0; y < LR_NR; y++ )
         {
             uint32_t a[NDW], b[NDW];
             load_row_u<NDW>( s1 + (intptr_t)y * stride, a );
@@ -145,21 +228,21 @@ template <int BD> struct LrCtx
     }
 
     // hpel plane rows addressed directly (TRY_BIDIR for subme <= 1, slicetype.c:594-600)
-    __device__ __forceinline__ void hpel_rows( int mx, int my, uint32_t (&r)[8][NDW] ) const
+    __device__ __forceinline__ void hpel_rows( int mx, int my, uint32_t (&r)[LR_NR][NDW] ) const
     {
         const int i = ((mx & 2) >> 1) + (my & 2);
         const pixel *s = (i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : p3) + (mx >> 2) + (intptr_t)(my >> 2) * stride;
 #pragma unroll
-        for( int y = 0; y < 8; y++ )
+        for( int y = 0; y < LR_NR; y++ )
             load_row_u<NDW>( s + (intptr_t)y * stride, r[y] );
     }
 
     // get_ref at a quarter-pel mv, then SAD or SATD 8x8
     __device__ __forceinline__ int qpel( int mx, int my, bool use_satd ) const
     {
-        uint32_t r[8][NDW];
+        uint32_t r[LR_NR][NDW];
         ref_rows( mx, my, r );
-        return lr_cmp_rows<BD>( fe, r, use_satd );
+        return lr_cmp_rows<BD>( fe, r, use_satd, q );
     }
 
     __device__ __forceinline__ int bits_mvd( int mx, int my ) const { return cmx[mx * 4] + cmy[my * 4]; }
@@ -283,10 +366,12 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         int i = me_range;
         do
         {
-            costs[0] = m.fpel( bmx, bmy - 1 ) + m.bits_mvd( bmx, bmy - 1 );
-            costs[1] = m.fpel( bmx, bmy + 1 ) + m.bits_mvd( bmx, bmy + 1 );
-            costs[2] = m.fpel( bmx - 1, bmy ) + m.bits_mvd( bmx - 1, bmy );
-            costs[3] = m.fpel( bmx + 1, bmy ) + m.bits_mvd( bmx + 1, bmy );
+            uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
+            m.win( bmx, bmy, w );
+            costs[0] = m.template wsad<0, -1>( w ) + m.bits_mvd( bmx, bmy - 1 );
+            costs[1] = m.template wsad<0, 1>( w ) + m.bits_mvd( bmx, bmy + 1 );
+            costs[2] = m.template wsad<-1, 0>( w ) + m.bits_mvd( bmx - 1, bmy );
+            costs[3] = m.template wsad<1, 0>( w ) + m.bits_mvd( bmx + 1, bmy );
             bcost = min( bcost, (costs[0] << 4) + 1 );
             bcost = min( bcost, (costs[1] << 4) + 3 );
             bcost = min( bcost, (costs[2] << 4) + 4 );
@@ -309,8 +394,17 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         (o)[1] = m.fpel( bmx + (c), bmy + (d) ) + m.bits_mvd( bmx + (c), bmy + (d) );                        \
         (o)[2] = m.fpel( bmx + (e), bmy + (f) ) + m.bits_mvd( bmx + (e), bmy + (f) );                        \
     } while( 0 )
-        LR_X3( -2, 0, -1, 2, 1, 2, costs );
-        LR_X3( 2, 0, 1, -2, -1, -2, costs + 4 );
+#define LR_W( DX, DY, W ) (m.template wsad<DX, DY>( W ) + m.bits_mvd( bmx + (DX), bmy + (DY) ))
+        {
+            uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
+            m.win( bmx, bmy, w );
+            costs[0] = LR_W( -2, 0, w );
+            costs[1] = LR_W( -1, 2, w );
+            costs[2] = LR_W( 1, 2, w );
+            costs[4] = LR_W( 2, 0, w );
+            costs[5] = LR_W( 1, -2, w );
+            costs[6] = LR_W( -1, -2, w );
+        }
         bcost <<= 3;
         bcost = min( bcost, (costs[0] << 3) + 2 );
         bcost = min( bcost, (costs[1] << 3) + 3 );
@@ -325,8 +419,20 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
             bmy += c_hex2[dir + 1][1];
             for( int i = (me_range >> 1) - 1; i > 0 && m.in_range( bmx, bmy ); i-- )
             {
-                LR_X3( c_hex2[dir][0], c_hex2[dir][1], c_hex2[dir + 1][0], c_hex2[dir + 1][1], c_hex2[dir + 2][0],
-                       c_hex2[dir + 2][1], costs );
+                // the window scores all six hexagon points (c_hex2[0..5] order); the three
+                // the reference evaluates in this direction, c_hex2[dir .. dir+2], are picked
+                uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
+                m.win( bmx, bmy, w );
+                const int s6[6] = { m.template wsad<-1, -2>( w ), m.template wsad<-2, 0>( w ),
+                                    m.template wsad<-1, 2>( w ), m.template wsad<1, 2>( w ),
+                                    m.template wsad<2, 0>( w ), m.template wsad<1, -2>( w ) };
+                auto pick = [&]( int j ) {
+                    j -= j >= 6 ? 6 : 0;
+                    return j == 0 ? s6[0] : j == 1 ? s6[1] : j == 2 ? s6[2] : j == 3 ? s6[3] : j == 4 ? s6[4] : s6[5];
+                };
+#pragma unroll
+                for( int k = 0; k < 3; k++ )
+                    costs[k] = pick( dir + k ) + m.bits_mvd( bmx + c_hex2[dir + k][0], bmy + c_hex2[dir + k][1] );
                 bcost &= ~7;
                 bcost = min( bcost, (costs[0] << 3) + 1 );
                 bcost = min( bcost, (costs[1] << 3) + 2 );
@@ -340,15 +446,17 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
             }
         }
         bcost >>= 3;
-#undef LR_X3
         bcost <<= 4;
-#pragma unroll
-        for( int k = 1; k <= 8; k++ )
         {
-            const int dx = c_square1[k][0], dy = c_square1[k][1];
-            const int c = m.fpel( bmx + dx, bmy + dy ) + m.bits_mvd( bmx + dx, bmy + dy );
-            bcost = min( bcost, (c << 4) + k );
+            uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
+            m.win( bmx, bmy, w );
+            const int c8[8] = { LR_W( 0, -1, w ), LR_W( 0, 1, w ), LR_W( -1, 0, w ), LR_W( 1, 0, w ),
+                                LR_W( -1, -1, w ), LR_W( -1, 1, w ), LR_W( 1, -1, w ), LR_W( 1, 1, w ) };
+#pragma unroll
+            for( int k = 1; k <= 8; k++ )
+                bcost = min( bcost, (c8[k - 1] << 4) + k );
         }
+#undef LR_W
         bmx += c_square1[bcost & 15][0];
         bmy += c_square1[bcost & 15][1];
         bcost >>= 4;
@@ -510,10 +618,10 @@ __device__ __forceinline__ int lr_list( LrCtx<BD> &m, const int *ring, int x, in
 
 template <int BD>
 __device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, intptr_t stride,
-                                              uint32_t (&fe)[8][8 / PT<BD>::PPD] )
+                                              uint32_t (&fe)[LR_NR][8 / PT<BD>::PPD] )
 {
 #pragma unroll
-    for( int r = 0; r < 8; r++ )
+    for( int r = 0; r < LR_NR; r++ )
     {
         const uint32_t *row = (const uint32_t *)(fb + (intptr_t)r * stride);
 #pragma unroll
@@ -523,7 +631,7 @@ __device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, 
 }
 
 template <int BD>
-__global__ __launch_bounds__( 256 ) void lowres_inter_kernel(
+__global__ __launch_bounds__( 1024 ) void lowres_inter_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *r0,
     const typename PT<BD>::pixel *r1, const typename PT<BD>::pixel *r2, const typename PT<BD>::pixel *r3,
     intptr_t stride, intptr_t rfs, int mbw, int mbh, int me_method, int subme, int satd, int me_range, int mv_range,
@@ -555,24 +663,27 @@ __global__ __launch_bounds__( 256 ) void lowres_inter_kernel(
         eacc[threadIdx.x] = 0;
     int e0 = 0, e1 = 0, e2 = 0;
     const int mvr = 2 * mv_range;
+    const int q = threadIdx.x & 3;
     __syncthreads();
     const int steps = (mbw - 1) + 2 * (mbh - 1) + 1;
     for( int t = 0; t < steps; t++ )
     {
-        for( int y = threadIdx.x; y < mbh; y += blockDim.x )
+        for( int y = threadIdx.x >> 2; y < mbh; y += blockDim.x >> 2 )
         {
             const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
             if( x < 0 || x >= mbw )
                 continue;
             const int mb = x + y * mbw;
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
-            uint32_t fe[8][NDW];
-            lr_load_fenc<BD>( fenc + off, stride, fe );
+            uint32_t fe[LR_NR][NDW];
+            lr_load_fenc<BD>( fenc + off + (intptr_t)(LR_NR * q) * stride, stride, fe );
             LrCtx<BD> m( fe );
-            m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd );
+            m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd, q );
             int mvx, mvy;
             const int cost = lr_list<BD>( m, ring, x, y, mbw, mbh, me_method, subme, me_range, lambda, cost_mv, mvx,
                                           mvy );
+            if( q )
+                continue;                            // the quad's other lanes hold the same results
             ring[4 * y + (x & 3)] = (int)lr_pack( mvx, mvy );
             mvs[2 * mb] = (int16_t)mvx;
             mvs[2 * mb + 1] = (int16_t)mvy;
@@ -643,7 +754,7 @@ __device__ __forceinline__ int lr_bidir( const LrCtx<BD> &m0, const LrCtx<BD> &m
                                          bool hpel, int w )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
-    uint32_t ra[8][NDW], rb[8][NDW];
+    uint32_t ra[LR_NR][NDW], rb[LR_NR][NDW];
     if( hpel )
     {
         m0.hpel_rows( ax, ay, ra );
@@ -655,17 +766,17 @@ __device__ __forceinline__ int lr_bidir( const LrCtx<BD> &m0, const LrCtx<BD> &m
         m1.ref_rows( bx, by, rb );
     }
 #pragma unroll
-    for( int y = 0; y < 8; y++ )
+    for( int y = 0; y < LR_NR; y++ )
 #pragma unroll
         for( int k = 0; k < NDW; k++ )
             ra[y][k] = lr_wavg<BD>( ra[y][k], rb[y][k], w );
-    return lr_cmp_rows<BD>( m0.fe, ra, m0.satd );
+    return lr_cmp_rows<BD>( m0.fe, ra, m0.satd, m0.q );
 }
 
 // B frames (p0 < b < p1): slicetype_mb_cost with b_bidir (slicetype.c:514-713, 758-791).
 // A list is searched on the wavefront when search & (1 << l), else its mv / cost are read.
 template <int BD>
-__global__ __launch_bounds__( 256 ) void lowres_bidir_kernel(
+__global__ __launch_bounds__( 1024 ) void lowres_bidir_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *a0,
     const typename PT<BD>::pixel *a1, const typename PT<BD>::pixel *a2, const typename PT<BD>::pixel *a3,
     intptr_t afs, const typename PT<BD>::pixel *b0, const typename PT<BD>::pixel *b1,
@@ -702,23 +813,24 @@ __global__ __launch_bounds__( 256 ) void lowres_bidir_kernel(
         eacc[threadIdx.x] = 0;
     int e0 = 0, e1 = 0;
     const int mvr = 2 * mv_range;
+    const int q = threadIdx.x & 3;
     const bool hp = subme == 2;                  // h->param.analyse.i_subpel_refine <= 1
     __syncthreads();
     const int steps = (mbw - 1) + 2 * (mbh - 1) + 1;
     for( int t = 0; t < steps; t++ )
     {
-        for( int y = threadIdx.x; y < mbh; y += blockDim.x )
+        for( int y = threadIdx.x >> 2; y < mbh; y += blockDim.x >> 2 )
         {
             const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
             if( x < 0 || x >= mbw )
                 continue;
             const int mb = x + y * mbw;
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
-            uint32_t fe[8][NDW];
-            lr_load_fenc<BD>( fenc + off, stride, fe );
+            uint32_t fe[LR_NR][NDW];
+            lr_load_fenc<BD>( fenc + off + (intptr_t)(LR_NR * q) * stride, stride, fe );
             LrCtx<BD> m0( fe ), m1( fe );
-            m0.setup( a0, a1, a2, a3, off, stride, x, y, mbw, mbh, mvr, satd );
-            m1.setup( b0, b1, b2, b3, off, stride, x, y, mbw, mbh, mvr, satd );
+            m0.setup( a0, a1, a2, a3, off, stride, x, y, mbw, mbh, mvr, satd, q );
+            m1.setup( b0, b1, b2, b3, off, stride, x, y, mbw, mbh, mvr, satd, q );
             int bcost = LR_COST_MAX, list_used = 0;
             // the predicted bidir mvs from p1's list-0 mvs (slicetype.c:623-645)
             int d0x = 0, d0y = 0, d1x = 0, d1y = 0;
@@ -799,6 +911,8 @@ __global__ __launch_bounds__( 256 ) void lowres_bidir_kernel(
                     list_used = 3;
                 }
             }
+            if( q )
+                continue;                            // the quad's other lanes hold the same results
             // slicetype.c:758-790 (no intra in B frames)
             bcost = (bcost >> (BD - 8)) + 4;
             const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
@@ -838,7 +952,7 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
 {
     if( n <= 0 || mbw <= 0 || mbh <= 0 )
         return hipSuccess;
-    const int threads = min( 256, (mbh + 63) / 64 * 64 );
+    const int threads = min( 1024, (4 * mbh + 63) / 64 * 64 );         // a lane quad per block row
     const size_t lds = (size_t)(9 * mbh + 2) * sizeof( int );
     hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n ), dim3( threads ), lds, stream, fenc, ffs, ra[0], ra[1],
                         ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method, subme, satd,
@@ -857,7 +971,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
 {
     if( npairs <= 0 || mbw <= 0 || mbh <= 0 )
         return hipSuccess;
-    const int threads = min( 256, (mbh + 63) / 64 * 64 );
+    const int threads = min( 1024, (4 * mbh + 63) / 64 * 64 );         // a lane quad per block row
     const size_t lds = (size_t)(5 * mbh + 3) * sizeof( int );
     hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs ), dim3( threads ), lds, stream, fenc, ffs, ref[0],
                         ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
