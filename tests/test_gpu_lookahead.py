@@ -156,3 +156,11 @@ def test_lowres_bidir_random(hip, oracle, bd, size):
     """random planes (mvs at the limits), AQ, short range, small and degenerate frames."""
     W, H = size
     _bidir_case(hip, oracle, bd, W, H, 2, 3, 1, 4, True, 100, 39, random=True, aq=True, me_range=8)
+
+
+@pytest.mark.parametrize("bd,H", [(8, 16 * 260), (10, 16 * 130)])
+def test_lowres_tall_frames(hip, oracle, bd, H):
+    """more block rows than one workgroup pass covers (256 rows at 8 bit, 128 at 10 bit):
+    the lane quads walk the rows in several passes per wavefront step."""
+    _case(hip, oracle, bd, 64, H, 2, 1, 4, True, random=True, me_range=8)
+    _bidir_case(hip, oracle, bd, 64, H, 1, 3, 1, 4, True, 128, 32, random=True, me_range=8)
