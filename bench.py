@@ -286,6 +286,22 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     res["lowres_me_pairs_per_s"] = world * max(1, a.steps // 5) * (F - 1) / wall
     res["lowres_me_launch_ms"] = ev_ms
     res["lowres_me_pairs_per_launch"] = F - 1
+    # the same search at a full-chip batch: 16 copies of those pairs in one launch (one
+    # workgroup per pair, 240 of the 256 CUs busy) -- its throughput when the lookahead
+    # hands over many (b, p0) pairs at once; the 15-pair leg above is per-pair latency
+    nrep = 16
+    bf = louts[0][1:].repeat(nrep, 1, 1)
+    br = [p[:-1].repeat(nrep, 1, 1) for p in louts]
+    bi = lint.repeat(nrep, 1)
+    bouts2 = x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span))
+
+    def lbstep():
+        x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span), outs=bouts2)
+    wall, ev_ms = timed(lbstep, max(1, a.steps // 10), 2, world)
+    res["lowres_me_batch_pairs_per_s"] = world * max(1, a.steps // 10) * bf.shape[0] / wall
+    res["lowres_me_batch_launch_ms"] = ev_ms
+    res["lowres_me_batch_pairs_per_launch"] = int(bf.shape[0])
+    del bf, br, bi, bouts2
     # the B-frame leg on the same planes: (p0, b, p1) = (k, k+1, k+2) for the F-2 triplets, both
     # lists searched (a fresh slicetype_frame_cost with b_bidir), p1's list-0 mvs against p0 from
     # one untimed P search as the bidir predictor, equal weights (i_bipred_weight 32, dsf 128)
