@@ -230,6 +230,8 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     wall, ev_ms = timed(hstep, a.steps, a.warmup, world)
     res["hpel_filter_frames_per_s"] = world * a.steps * F / wall
     res["hpel_filter_launch_ms"] = ev_ms
+    # algorithmic bytes: the padded source plane in, the three padded half-pel planes out
+    res["hpel_filter_hbm_frac"] = F * 4 * dev[0].numel() / (ev_ms * 1e-3) / HBM_PEAK
     # fused reconstruction (dequant + idct + add, per-MB qp) on the coefficients of the last
     # DCT+quant step, and the lookahead's half-resolution planes
     dq4, dq8 = x.cqm_dequant([flat] * 8)
@@ -250,6 +252,28 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
         res["recon%d_blocks_per_s" % t] = world * a.steps * blocks / wall
         res["recon%d_hbm_frac" % t] = blocks * bpb / (ev_ms * 1e-3) / HBM_PEAK
         res["recon%d_launch_ms" % t] = ev_ms
+    # the two streaming frame kernels at the transform legs' batch (>= 64 frames per
+    # launch), where the launch ramp and tail no longer dominate
+    fb = tdev[0].numel()
+    thv = [torch.empty_like(tdev[:-1]) for _ in range(3)]
+
+    def h64():
+        x.hpel_filter(tdev[:-1], origin, stride, mbw * 16, mbh * 16, outs=thv)
+    wall, ev_ms = timed(h64, a.steps, a.warmup, world)
+    res["hpel_filter_%d_frames_per_s" % TF] = world * a.steps * TF / wall
+    res["hpel_filter_%d_launch_ms" % TF] = ev_ms
+    res["hpel_filter_%d_hbm_frac" % TF] = TF * 4 * fb / (ev_ms * 1e-3) / HBM_PEAK
+    del thv
+    tl, _ = x.frame_init_lowres(tdev[:-1], origin, stride, mbw * 16, mbh * 16)
+
+    def l64():
+        x.frame_init_lowres(tdev[:-1], origin, stride, mbw * 16, mbh * 16, outs=tl)
+    wall, ev_ms = timed(l64, a.steps, a.warmup, world)
+    lbytes = fb + 4 * tl[0][0].numel()              # source plane in, four padded lowres planes out
+    res["lowres_%d_frames_per_s" % TF] = world * a.steps * TF / wall
+    res["lowres_%d_launch_ms" % TF] = ev_ms
+    res["lowres_%d_hbm_frac" % TF] = TF * lbytes / (ev_ms * 1e-3) / HBM_PEAK
+    del tl
     del recon, tdev, dct, nz
     lw, lh = mbw * 16, mbh * 16
     louts, _ = x.frame_init_lowres(dev[:-1], origin, stride, lw, lh)
@@ -259,6 +283,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     wall, ev_ms = timed(lstep, a.steps, a.warmup, world)
     res["lowres_frames_per_s"] = world * a.steps * F / wall
     res["lowres_launch_ms"] = ev_ms
+    res["lowres_hbm_frac"] = F * (dev[0].numel() + 4 * louts[0][0].numel()) / (ev_ms * 1e-3) / HBM_PEAK
     # the lookahead's intra estimate on those lowres planes (slicetype.c:714-757, subme > 1:
     # 10 predictions + satd_8x8 per 8x8 block, lambda of X264_LOOKAHEAD_QP = 12 -> 1, slicetype.c:47-48)
     iouts = x.lowres_intra_cost(louts[0], x.plane_stride(lw // 2), mbw, mbh, True, True, 1)
