@@ -992,6 +992,104 @@ __global__ __launch_bounds__( 256 ) void lowres_kernel( const typename PT<BD>::p
     *(uint32_t *)(dc + o) = wc;
 }
 
+// 8 bit, one wave per output row for the core and one for the borders.  Core lane
+// k makes output columns 16k .. 16k+15 of all four planes: its three source rows
+// arrive as 33-pixel runs (two aligned 16-byte loads and a dword), v_perm gathers
+// the even / odd / next-even columns, and FILTER(a, b, c, d) = avg( avg( a, b ),
+// avg( c, d ) ) with avg = (x + y + 1) >> 1 per byte is v_lerp_u8 -- ten per output
+// dword-quad, bit-exact -- so each plane row leaves as one 16-byte store per lane.
+// The border wave takes the 32-pixel borders and the last core columns whose
+// source run would pass column W, four pixels per lane through the clamped
+// per-pixel form of lowres_kernel.
+__global__ __launch_bounds__( 128 ) void lowres16_kernel( const uint8_t *__restrict__ src, intptr_t stride,
+                                                          intptr_t fstride, int width, int height,
+                                                          uint8_t *__restrict__ d0, uint8_t *__restrict__ dh,
+                                                          uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                          intptr_t ds, intptr_t dfs )
+{
+    constexpr int PAD = 32;
+    const int wl = width / 2, hl = height / 2;
+    const int y = (int)blockIdx.y - PAD, f = blockIdx.z;
+    const int lane = threadIdx.x & 63;
+    const uint8_t *s = src + f * fstride;
+    const int yc = min( max( y, 0 ), hl - 1 );
+    const uint8_t *r0 = s + (intptr_t)(2 * yc) * stride;
+    const uint8_t *r1 = s + (intptr_t)min( 2 * yc + 1, height - 1 ) * stride;
+    const uint8_t *r2 = s + (intptr_t)min( 2 * yc + 2, height - 1 ) * stride;
+    const intptr_t orow = f * dfs + (intptr_t)y * ds;
+    const int ncore = wl >= 17 ? (wl - 17) / 16 + 1 : 0;     // groups with 16k + 16 <= wl - 1
+    if( threadIdx.x < 64 )
+    {
+        for( int k = lane; k < ncore; k += 64 )
+        {
+            const int xg = 16 * k;
+            uint32_t E[3][5], O[3][4];
+            const uint8_t *rr[3] = { r0, r1, r2 };
+#pragma unroll
+            for( int r = 0; r < 3; r++ )
+            {
+                const uint4 a = *(const uint4 *)(rr[r] + 2 * xg), b = *(const uint4 *)(rr[r] + 2 * xg + 16);
+                const uint32_t v[9] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, *(const uint32_t *)(rr[r] + 2 * xg + 32) };
+#pragma unroll
+                for( int j = 0; j < 4; j++ )
+                {
+                    E[r][j] = __builtin_amdgcn_perm( v[2 * j + 1], v[2 * j], 0x06040200u );
+                    O[r][j] = __builtin_amdgcn_perm( v[2 * j + 1], v[2 * j], 0x07050301u );
+                }
+                E[r][4] = v[8];                                  // byte 0: source column 2*xg + 32
+            }
+            uint32_t w0[4], wh[4], wv[4], wc[4];
+#pragma unroll
+            for( int j = 0; j < 4; j++ )
+            {
+                auto avg = []( uint32_t p, uint32_t q ) { return __builtin_amdgcn_lerp( p, q, 0x01010101u ); };
+                const uint32_t x0 = __builtin_amdgcn_alignbyte( E[0][j + 1], E[0][j], 1 );
+                const uint32_t x1 = __builtin_amdgcn_alignbyte( E[1][j + 1], E[1][j], 1 );
+                const uint32_t x2 = __builtin_amdgcn_alignbyte( E[2][j + 1], E[2][j], 1 );
+                const uint32_t e01 = avg( E[0][j], E[1][j] ), o01 = avg( O[0][j], O[1][j] ), x01 = avg( x0, x1 );
+                const uint32_t e12 = avg( E[1][j], E[2][j] ), o12 = avg( O[1][j], O[2][j] ), x12 = avg( x1, x2 );
+                w0[j] = avg( e01, o01 );
+                wh[j] = avg( o01, x01 );
+                wv[j] = avg( e12, o12 );
+                wc[j] = avg( o12, x12 );
+            }
+            const intptr_t o = orow + xg;
+            *(uint4 *)(d0 + o) = make_uint4( w0[0], w0[1], w0[2], w0[3] );
+            *(uint4 *)(dh + o) = make_uint4( wh[0], wh[1], wh[2], wh[3] );
+            *(uint4 *)(dv + o) = make_uint4( wv[0], wv[1], wv[2], wv[3] );
+            *(uint4 *)(dc + o) = make_uint4( wc[0], wc[1], wc[2], wc[3] );
+        }
+        return;
+    }
+    // border wave: 8 groups of 4 on the left (x in [-32, 0)), the rest from 16 * ncore to wl + 32
+    const int nright = (wl + PAD - 16 * ncore) / 4;
+    for( int gi = lane; gi < 8 + nright; gi += 64 )
+    {
+        const int xg = gi < 8 ? -PAD + 4 * gi : 16 * ncore + 4 * (gi - 8);
+        uint32_t w0 = 0, wh = 0, wv = 0, wc = 0;
+#define FILTER( a, b, c, d ) ((((a + b + 1) >> 1) + ((c + d + 1) >> 1) + 1) >> 1)
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+        {
+            const int xc = min( max( xg + j, 0 ), wl - 1 );
+            const int c0 = 2 * xc, c1 = min( 2 * xc + 1, width - 1 ), c2 = min( 2 * xc + 2, width - 1 );
+            const int a0 = r0[c0], a1 = r0[c1], a2 = r0[c2];
+            const int b0 = r1[c0], b1 = r1[c1], b2 = r1[c2];
+            const int e0 = r2[c0], e1 = r2[c1], e2 = r2[c2];
+            w0 |= (uint32_t)FILTER( a0, b0, a1, b1 ) << (8 * j);
+            wh |= (uint32_t)FILTER( a1, b1, a2, b2 ) << (8 * j);
+            wv |= (uint32_t)FILTER( b0, e0, b1, e1 ) << (8 * j);
+            wc |= (uint32_t)FILTER( b1, e1, b2, e2 ) << (8 * j);
+        }
+#undef FILTER
+        const intptr_t o = orow + xg;
+        *(uint32_t *)(d0 + o) = w0;
+        *(uint32_t *)(dh + o) = wh;
+        *(uint32_t *)(dv + o) = wv;
+        *(uint32_t *)(dc + o) = wc;
+    }
+}
+
 template <int BD>
 hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t stride, intptr_t fstride, int width,
                                      int height, int nframes, typename PT<BD>::pixel *const dst[4], intptr_t ds,
@@ -1000,6 +1098,21 @@ hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t
     if( nframes <= 0 )
         return hipSuccess;
     const int wl = width / 2, hl = height / 2;
+    if constexpr( BD == 8 )
+    {
+        // 16-pixel lanes with 16-byte loads and stores: needs 16-byte aligned rows and a
+        // width of whole macroblocks (X264HIP_LOWRES_VARIANT=1 selects the dword kernel)
+        const char *ev = getenv( "X264HIP_LOWRES_VARIANT" );
+        const uintptr_t al = (uintptr_t)src | (uintptr_t)stride | (uintptr_t)fstride | (uintptr_t)dst[0] |
+                             (uintptr_t)dst[1] | (uintptr_t)dst[2] | (uintptr_t)dst[3] | (uintptr_t)ds | (uintptr_t)dfs;
+        if( !(ev && atoi( ev ) == 1) && !(al & 15) && !(width & 15) )
+        {
+            dim3 g16( 1, (unsigned)(hl + 64), (unsigned)nframes );
+            hipLaunchKernelGGL( lowres16_kernel, g16, dim3( 128 ), 0, st, src, stride, fstride, width, height, dst[0],
+                                dst[1], dst[2], dst[3], ds, dfs );
+            return hipGetLastError();
+        }
+    }
     const int gw = (wl + 64) / PT<BD>::PPD;
     dim3 blk( 256 ), g( (unsigned)((gw + 255) / 256), (unsigned)(hl + 64), (unsigned)nframes );
     hipLaunchKernelGGL( lowres_kernel<BD>, g, blk, 0, st, src, stride, fstride, width, height, dst[0], dst[1], dst[2],
