@@ -321,7 +321,7 @@ __global__ __launch_bounds__( 256 ) void hpel_stream_kernel( const uint8_t *__re
 {
     const int lane = threadIdx.x & 63;
     const int nq = (width + 32) >> 4;                       // column quads over x in [-16, W+16)
-    const int chunk = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if( chunk * 62 >= nq )
         return;                                              // wave-uniform
     const int q = chunk * 62 - 1 + lane;
@@ -464,11 +464,24 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
                            (uintptr_t)fstride) & 15) )
         {
             const int nq = (width + 32) / 16, nchunk = (nq + 61) / 62;
-            // 24-row strips (12: same time, 36 / 48: fewer waves than SIMDs, 0.058 / 0.074 ms)
-            constexpr int R = 24;
-            dim3 g( (nchunk + 3) / 4, (height + 16 + R - 1) / R, nframes );
-            hipLaunchKernelGGL( hpel_stream_kernel<R>, g, dim3( 256 ), 0, stream, src, dh, dv, dc, stride, fstride,
-                                width, height, 8 * 16, 64 * 512 );
+            // one wave per workgroup, so every launched wave has a column chunk (a 4-wave
+            // group left half its waves idle at 1080p's two chunks: with 162 VGPRs the
+            // SIMDs then held ~1.7 working waves, profiles/r01g_pmc_hpel_sq.json), and
+            // 12-row strips: twice the waves of 24-row ones for 5 halo rows per strip
+            // (16 frames: 0.0455 -> 0.0398 ms; 64 frames: 0.166 -> 0.158 ms; 16 rows in
+            // between).  X264HIP_HPEL_ROWS = 16 / 24 selects the taller strips.
+            const char *er = getenv( "X264HIP_HPEL_ROWS" );
+            const int rows = er && (atoi( er ) == 16 || atoi( er ) == 24) ? atoi( er ) : 12;
+            dim3 g( nchunk, (height + 16 + rows - 1) / rows, nframes );
+            if( rows == 24 )
+                hipLaunchKernelGGL( hpel_stream_kernel<24>, g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,
+                                    width, height, 8 * 16, 64 * 512 );
+            else if( rows == 16 )
+                hipLaunchKernelGGL( hpel_stream_kernel<16>, g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,
+                                    width, height, 8 * 16, 64 * 512 );
+            else
+                hipLaunchKernelGGL( hpel_stream_kernel<12>, g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,
+                                    width, height, 8 * 16, 64 * 512 );
             return hipGetLastError();
         }
     }
