@@ -428,7 +428,7 @@ def rates_2160p(x, a, world):
     from pinned host memory (the reference frame is the previous upload, already on
     the device) on a copy stream overlapped with the previous frame's kernels."""
     from x264hip import synth, dist as xd
-    W, H, R = 3840, 2176, a.range                     # 2160 padded to whole MBs
+    W, H, R = 3840, 2160, a.range                     # 240 x 135 MBs (2160 = 135 * 16, no MB padding)
     mbw, mbh = W // 16, H // 16
     nf = 8
     p0, _ = xd.frame_shard(world * nf, world, int(os.environ.get("RANK", "0")))

@@ -11,12 +11,17 @@
  *       x264_quant_function_t  (reference common/quant.h:30-70)
  *     for BIT_DEPTH 8 (pixel=uint8_t, dctcoef=int16_t, udctcoef=uint16_t) and
  *     BIT_DEPTH 10 (pixel=uint16_t, dctcoef=int32_t, udctcoef=uint32_t),
- *     reference common/common.h:93-109.  x264hip_{8,10}_*_init() replace
- *     x264_{8,10}_*_init() (reference common/pixel.c:809, common/dct.c:477,
- *     common/quant.c:414) for the entries this backend implements; the
- *     *_init_hip() forms only override, like x264_pixel_init_altivec()
- *     (reference common/pixel.c:1598-1603).  Every table entry is a
- *     synchronous call that executes on the GPU (one dispatch per call).
+ *     reference common/common.h:93-109.  Both initialiser forms OVERRIDE
+ *     entries, like x264_pixel_init_altivec() (reference common/pixel.c:
+ *     1598-1603): the caller runs its C init x264_{8,10}_*_init() first, then
+ *     x264hip_{8,10}_*_init(cpu, tab) (acts when cpu & X264HIP_CPU_HIP) or
+ *     x264hip_{8,10}_*_init_hip(tab).  Entries this backend implements are
+ *     replaced; every other entry (ssim_*, ssd_nv12_core, intra_*_x9_*, the
+ *     trellis entries, the encoder's mbcmp / fpelcmp aliases) keeps the
+ *     caller's.  Without a usable gfx950 device the table is left untouched
+ *     (reference common/opencl.c:400-409), so no installed entry can ever
+ *     reach a missing device.  Every table entry is a synchronous call that
+ *     executes on the GPU (one dispatch per call).
  *
  *  2. Batched, device-resident entries (x264hip_{8,10}_*_batch, me_*, mb_*):
  *     the same kernels over whole frames / block lists already in HBM, on a
@@ -30,6 +35,7 @@
 #ifndef X264HIP_H
 #define X264HIP_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -314,8 +320,32 @@ X264HIP_DECLARE_TABLES( 10, uint16_t, int32_t, uint32_t )
 int  x264hip_init( int device );
 /* last HIP error text of the calling thread ("" if none) */
 const char *x264hip_last_error( void );
-/* 1 if the library was built for gfx950 and a device is usable */
+/* 1 if a gfx950 device is bound (x264hip_init(0) is tried when none is yet) */
 int  x264hip_available( void );
+/* Bind the calling thread to `device` (a gfx950 device; -1 = back to the
+ * process device of x264hip_init).  Table entries called from this thread then
+ * run on that device, on a stream and staging buffer owned by the thread, so
+ * x264's frame / lookahead threads (reference encoder/encoder.c:1758-1772) can
+ * each drive a different GPU of the node from one process.  Batched entries run
+ * on the stream the caller passes, whose device they use. */
+int  x264hip_set_thread_device( int device );
+/* the calling thread's device (its override, else the process device; -1 if none) */
+int  x264hip_thread_device( void );
+/* Forward a reconstructed reference plane to the GPU encoding the next frame:
+ * one asynchronous xGMI peer copy of `bytes` on `stream` (the
+ * frame-per-GPU pipeline's only device-to-device transfer). */
+int  x264hip_forward_ref( void *dst, int dst_device, const void *src, int src_device, size_t bytes,
+                          void *stream );
+/* one line naming the device and the table entries the HIP backend fills (the
+ * analogue of reference encoder/encoder.c:1676-1706); also printed once to
+ * stderr at the first table fill unless X264HIP_QUIET=1 */
+const char *x264hip_backend_banner( void );
+/* A/B kernel switches by environment name (X264HIP_ME_VARIANT, X264HIP_HPEL_VARIANT,
+ * X264HIP_HPEL_ROWS, X264HIP_SUBPEL_VARIANT, X264HIP_LOWRES_VARIANT, X264HIP_DQ_VARIANT,
+ * X264HIP_RECON_VARIANT, X264HIP_LOWRES_INTRA_VARIANT): the environment seeds them
+ * once; this changes one at run time (-1 = default).  X264HIP_EINVAL for an
+ * unknown name.  Every variant is bit-exact; only speed differs. */
+int  x264hip_set_variant( const char *name, int value );
 
 /*----------------------------------------------------------------------------
  * Per-bit-depth entries.  BD = 8 or 10.

@@ -67,6 +67,7 @@ int main( void )
     }
 
     x264hip_8_pixel_function_t pf;
+    memset( &pf, 0, sizeof(pf) );   /* stands for the caller's C init (the HIP init only overrides) */
     x264hip_8_pixel_init( X264HIP_CPU_HIP, &pf );
     for( int i = 0; i < 8; i++ )
         for( int j = 0; j < 16; j++ )
@@ -96,6 +97,10 @@ int main( void )
     x264hip_8_dct_function_t df;
     x264hip_8_quant_function_t qf;
     x264hip_8_zigzag_function_t zp, zi;
+    memset( &df, 0, sizeof(df) );
+    memset( &qf, 0, sizeof(qf) );
+    memset( &zp, 0, sizeof(zp) );
+    memset( &zi, 0, sizeof(zi) );
     x264hip_8_dct_init( X264HIP_CPU_HIP, &df );
     x264hip_8_quant_init( NULL, X264HIP_CPU_HIP, &qf );
     x264hip_8_zigzag_init( X264HIP_CPU_HIP, &zp, &zi );

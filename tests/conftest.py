@@ -62,3 +62,18 @@ def hip():
     x = load_package()
     x.init(0)
     return x
+
+
+_VARIANT_SWITCHES = ("X264HIP_ME_VARIANT", "X264HIP_HPEL_VARIANT", "X264HIP_HPEL_ROWS", "X264HIP_SUBPEL_VARIANT",
+                     "X264HIP_LOWRES_VARIANT", "X264HIP_DQ_VARIANT", "X264HIP_RECON_VARIANT",
+                     "X264HIP_LOWRES_INTRA_VARIANT")
+
+
+@pytest.fixture(autouse=True)
+def _reset_kernel_variants():
+    """A/B kernel switches (x264hip_set_variant) never leak from one test into the next."""
+    yield
+    x = sys.modules.get("x264hip")
+    if x is not None and getattr(x, "_lib", None) is not None:
+        for name in _VARIANT_SWITCHES:
+            x.set_variant(name, None)

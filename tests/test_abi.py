@@ -118,12 +118,118 @@ def test_table_layout_matches_ctypes(tmp_path):
     assert n_ptr == 8 * 7 + 7 + 4 + 7 * 2 + 1 + 1 + 1 + 4 + 4 + 4 + 3 + 7 * 4 + 7 + 15 + 3 + 6
 
 
-def test_init_without_hip_flag_leaves_table_empty():
-    """x264hip_*_init(cpu without X264HIP_CPU_HIP) fills nothing (no CPU entries)."""
+def _prefilled(struct):
+    """A table whose every pointer slot holds a recognisable non-NULL value, as if the
+    caller's C init (x264_*_init) had filled it."""
+    tab = struct()
+    raw = (ctypes.c_uint64 * (ctypes.sizeof(struct) // 8)).from_buffer(tab)
+    for i in range(len(raw)):
+        raw[i] = 0x5EED0000 + i
+    return tab, bytes(raw)
+
+
+@pytest.mark.parametrize("kind", ["pixel", "dct", "quant", "zigzag"])
+@pytest.mark.parametrize("bd", [8, 10])
+def test_init_leaves_caller_table_untouched_without_device(kind, bd):
+    """No gfx950 device here: neither the flag form (with and without X264HIP_CPU_HIP) nor
+    the _init_hip form may change a table the caller's C init filled (the OpenCL
+    fallback convention, reference common/opencl.c:400-409; every used entry stays
+    non-NULL, encoder/encoder.c:1419-1422)."""
     x = load_package()
-    tab = x.PixelFunctions()
-    x.lib().x264hip_8_pixel_init(0, ctypes.byref(tab))
-    assert not any(bool(tab.sad[i]) for i in range(8))
+    L = x.lib()
+    if L.x264hip_available():
+        pytest.skip("a gfx950 device is visible")
+    struct = {"pixel": x.PixelFunctions, "dct": x.DctFunctions, "quant": x.QuantFunctions,
+              "zigzag": x.ZigzagFunctions}[kind]
+    tab, before = _prefilled(struct)
+    tab2, before2 = _prefilled(struct)
+    init = getattr(L, f"x264hip_{bd}_{kind}_init")
+    init_hip = getattr(L, f"x264hip_{bd}_{kind}_init_hip")
+    for cpu in (0, x.CPU_HIP):
+        if kind == "quant":
+            init(None, cpu, ctypes.byref(tab))
+        elif kind == "zigzag":
+            init(cpu, ctypes.byref(tab), ctypes.byref(tab2))
+        else:
+            init(cpu, ctypes.byref(tab))
+    if kind == "zigzag":
+        init_hip(ctypes.byref(tab), ctypes.byref(tab2))
+    else:
+        init_hip(ctypes.byref(tab))
+    assert bytes((ctypes.c_uint64 * (ctypes.sizeof(struct) // 8)).from_buffer(tab)) == before
+    assert bytes((ctypes.c_uint64 * (ctypes.sizeof(struct) // 8)).from_buffer(tab2)) == before2
+
+
+def test_runtime_entries_without_device():
+    """Runtime calls fail with a status, never abort, when no device exists."""
+    x = load_package()
+    L = x.lib()
+    if L.x264hip_available():
+        pytest.skip("a gfx950 device is visible")
+    assert L.x264hip_init(0) == -3                        # X264HIP_ENODEV
+    assert L.x264hip_set_thread_device(0) == -3
+    assert L.x264hip_thread_device() == -1
+    assert L.x264hip_set_thread_device(-1) == 0
+    assert L.x264hip_set_variant(b"X264HIP_ME_VARIANT", 3) == 0
+    assert L.x264hip_set_variant(b"X264HIP_ME_VARIANT", -1) == 0
+    assert L.x264hip_set_variant(b"NOT_A_SWITCH", 1) == -1
+    assert L.x264hip_forward_ref(None, 0, None, 0, 16, None) == -1
+    assert L.x264hip_forward_ref(None, 0, None, 0, 0, None) == 0
+    assert "no device" in L.x264hip_backend_banner().decode()
+
+
+# ---------------------------------------------------------------- reference layout
+REF = "/root/reference/common"
+
+
+def _struct_fields(body):
+    """Ordered (name, extent) of a C struct body: function pointers `(*name[n])(...)`,
+    plain members `type name[n]`; comments and macro continuations stripped."""
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    body = re.sub(r"//[^\n]*", "", body)
+    body = re.sub(r"#define(?:[^\n]*\\\n)*[^\n]*", "", body)   # TRELLIS_PARAMS (quant.h:57-60)
+    body = body.replace("\\\n", "\n")                            # our header's macro continuations
+    body = body.replace("TRELLIS_PARAMS,", "")
+    out = []
+    for decl in body.split(";"):
+        d = " ".join(decl.split())
+        if not d:
+            continue
+        m = re.match(r"^[\w\s\*]*?\(\s*\*\s*(\w+)\s*(?:\[(\w+)\])?\s*\)", d)
+        if not m:
+            m = re.match(r"^.*?(\w+)\s*(?:\[(\w+)\])?\s*$", d.split("(")[0] if "(" not in d else d)
+        assert m, d
+        name = m.group(1)
+        name = re.sub(r"^x264hip_##BD##_", "", name)
+        out.append((name, m.group(2) or "1"))
+    return out
+
+
+def _ref_struct(path, tname):
+    src = open(path).read()
+    m = re.search(r"typedef struct\s*\{([^{}]*)\}\s*" + tname + r"\s*;", src, re.S)
+    assert m, tname
+    return _struct_fields(m.group(1))
+
+
+def _our_struct(tname):
+    src = open(HEADER).read()
+    m = re.search(r"typedef struct\s*\\\s*\{([^{}]*)\}\s*x264hip_##BD##_" + tname + r"\s*;", src, re.S)
+    assert m, tname
+    return _struct_fields(m.group(1))
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference tree not present (GPU box)")
+@pytest.mark.parametrize("ref_file,tname", [("pixel.h", "pixel_function_t"), ("dct.h", "dct_function_t"),
+                                             ("dct.h", "zigzag_function_t"), ("quant.h", "quant_function_t")])
+def test_tables_match_reference_headers(ref_file, tname):
+    """include/x264hip.h's re-declared tables have the reference's field names, order and
+    array extents (reference common/pixel.h:78-144, dct.h:29-70, quant.h:30-70), parsed
+    from the reference headers as text."""
+    want = _ref_struct(os.path.join(REF, ref_file), "x264_" + tname)
+    got = _our_struct(tname)
+    assert got == want
+    assert len(want) >= 6
 
 
 @pytest.mark.parametrize("bd", [8, 10])

@@ -7,6 +7,8 @@ import ctypes
 
 import numpy as np
 import pytest
+
+from conftest import load_package as _x
 import torch
 
 import checkasm_bufs as cb
@@ -179,9 +181,9 @@ def dq_variant(request, monkeypatch):
     """X264HIP_DQ_VARIANT: 0 / 2 staged / unstaged strip, 1 block-major, 3 / 4 band layout staged /
     direct, 5 half band (transform 4), 6 / 7 packed 16-bit staged / direct (8 bit, transform 8)."""
     if request.param != "default":
-        monkeypatch.setenv("X264HIP_DQ_VARIANT", request.param)
+        _x().set_variant("X264HIP_DQ_VARIANT", request.param)
     else:
-        monkeypatch.delenv("X264HIP_DQ_VARIANT", raising=False)
+        _x().set_variant("X264HIP_DQ_VARIANT", None)
     return request.param
 
 
@@ -222,9 +224,9 @@ def test_mb_dct8_quant_extremes(hip, oracle, monkeypatch, variant, cqm):
     every CQM family (all-ones lists: the uint32 (f + |c|) * mf wraps) at QP 0, 26 and 51;
     20 MBs wide so the last 16-MB strip is partial."""
     if variant != "default":
-        monkeypatch.setenv("X264HIP_DQ_VARIANT", variant)
+        _x().set_variant("X264HIP_DQ_VARIANT", variant)
     else:
-        monkeypatch.delenv("X264HIP_DQ_VARIANT", raising=False)
+        _x().set_variant("X264HIP_DQ_VARIANT", None)
     mbw, mbh = 20, 3
     W, H = 16 * mbw, 16 * mbh
     stride = W + 64

@@ -8,6 +8,8 @@ import ctypes
 
 import numpy as np
 import pytest
+
+from conftest import load_package as _x
 import torch
 
 import checkasm_bufs as cb
@@ -112,9 +114,9 @@ def _lowres_frames(hip, bd, W, H, n, seed):
 def test_lowres_intra_cost(hip, oracle, bd, size, mode, variant, monkeypatch):
     """X264HIP_LOWRES_INTRA_VARIANT: default = block per MB row, 1 = wave per 64 MBs with atomics"""
     if variant == "default":
-        monkeypatch.delenv("X264HIP_LOWRES_INTRA_VARIANT", raising=False)
+        _x().set_variant("X264HIP_LOWRES_INTRA_VARIANT", None)
     else:
-        monkeypatch.setenv("X264HIP_LOWRES_INTRA_VARIANT", variant)
+        _x().set_variant("X264HIP_LOWRES_INTRA_VARIANT", variant)
     W, H = size
     mbw, mbh = W // 16, H // 16
     n = 2

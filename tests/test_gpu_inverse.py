@@ -7,6 +7,8 @@ import ctypes
 
 import numpy as np
 import pytest
+
+from conftest import load_package as _x
 import torch
 
 import checkasm_bufs as cb
@@ -362,9 +364,9 @@ def test_zigzag_sub_batch_random(hip, oracle, bd):
 def recon_variant(request, monkeypatch):
     """X264HIP_RECON_VARIANT: 0 = block-pair lanes for transform 4, 1 = one lane per block."""
     if request.param == "default":
-        monkeypatch.delenv("X264HIP_RECON_VARIANT", raising=False)
+        _x().set_variant("X264HIP_RECON_VARIANT", None)
     else:
-        monkeypatch.setenv("X264HIP_RECON_VARIANT", request.param)
+        _x().set_variant("X264HIP_RECON_VARIANT", request.param)
     return request.param
 
 

@@ -4,6 +4,8 @@ SAD / SATD candidates through get_ref (x264hip_*_subpel_cmp_batch, reference
 refine_subpel encoder/me.c:865-992)."""
 import numpy as np
 import pytest
+
+from conftest import load_package as _x
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -25,9 +27,9 @@ def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
     """X264HIP_HPEL_VARIANT: default = streaming lanes at 8 bit (2) / fused tiles at 10 bit,
     0 = fused single pass over LDS tiles, 1 = interior tiles + border expand."""
     if variant == "default":
-        monkeypatch.delenv("X264HIP_HPEL_VARIANT", raising=False)
+        _x().set_variant("X264HIP_HPEL_VARIANT", None)
     else:
-        monkeypatch.setenv("X264HIP_HPEL_VARIANT", variant)
+        _x().set_variant("X264HIP_HPEL_VARIANT", variant)
     from x264hip import synth
     W, H = size
     gen = synth.make_sequence if W > 100 else synth.random_planes
@@ -50,9 +52,9 @@ def test_subpel_cmp_random(hip, oracle, bd, op, variant, monkeypatch):
     with a per-row branch, 2 = row-per-lane SATD for 8/16-wide blocks, 3 = unaligned
     multi-dword row loads (8-bit default), 5 = dword-aligned loads + alignbyte (10-bit default)."""
     if variant == "default":
-        monkeypatch.delenv("X264HIP_SUBPEL_VARIANT", raising=False)
+        _x().set_variant("X264HIP_SUBPEL_VARIANT", None)
     else:
-        monkeypatch.setenv("X264HIP_SUBPEL_VARIANT", variant)
+        _x().set_variant("X264HIP_SUBPEL_VARIANT", variant)
     from x264hip import synth
     W, H = 160, 96
     planes, stride, origin = synth.random_planes(2, W, H, bd, seed=11)

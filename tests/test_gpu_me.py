@@ -3,6 +3,8 @@ against the oracle's exhaustive search built from the reference sad
 (reference common/pixel.c:55-80, encoder/me.c:618-631)."""
 import numpy as np
 import pytest
+
+from conftest import load_package as _x
 import torch
 
 pytestmark = pytest.mark.gpu
@@ -18,7 +20,7 @@ def _frames(synth, bd, w, h, kind, seed=3):
 def variant(request, monkeypatch):
     """every kernel variant (X264HIP_ME_VARIANT, read per launch) must be exact"""
     if request.param != "default":
-        monkeypatch.setenv("X264HIP_ME_VARIANT", request.param)
+        _x().set_variant("X264HIP_ME_VARIANT", request.param)
     return request.param
 
 

@@ -26,7 +26,7 @@ for bd in (8, 10):
         outs = {}
         times = {}
         for v in VS:
-            os.environ["X264HIP_DQ_VARIANT"] = v
+            sys.modules["x264hip"].set_variant("X264HIP_DQ_VARIANT", v)
             outs[v] = x.mb_dct_quant(t, dev[1:], origin, stride, dev[:-1], origin + 2 * stride + 3, stride, W // 16,
                                      H // 16, F, mf, bias, fenc_frame_stride=fsz, pred_frame_stride=fsz)
             times[v] = []
@@ -39,7 +39,7 @@ for bd in (8, 10):
             assert torch.equal(outs["1"][0], outs[v][0]) and torch.equal(outs["1"][1], outs[v][1]), v
         for rnd in range(5):
             for v in VS:
-                os.environ["X264HIP_DQ_VARIANT"] = v
+                sys.modules["x264hip"].set_variant("X264HIP_DQ_VARIANT", v)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(3):

@@ -19,19 +19,19 @@ for bd in (8, 10):
     outs = {v: [torch.zeros_like(dev) for _ in range(3)] for v in vs}
     run = lambda v: x.hpel_filter(dev, origin, stride, W, H, outs=outs[v])  # noqa
     for v in vs:
-        os.environ["X264HIP_HPEL_VARIANT"] = v
+        sys.modules["x264hip"].set_variant("X264HIP_HPEL_VARIANT", v)
         run(v)
     torch.cuda.synchronize()
     for v in vs:
         for a, b in zip(outs[vs[0]], outs[v]):
             assert torch.equal(a, b), ("variants disagree", bd, v)
-    os.environ["X264HIP_HPEL_VARIANT"] = vs[-1]
+    sys.modules["x264hip"].set_variant("X264HIP_HPEL_VARIANT", vs[-1])
     for _ in range(150):
         run(vs[-1])
     times = {v: [] for v in vs}
     for rnd in range(5):
         for v in vs:
-            os.environ["X264HIP_HPEL_VARIANT"] = v
+            sys.modules["x264hip"].set_variant("X264HIP_HPEL_VARIANT", v)
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(5):
@@ -43,5 +43,5 @@ for bd in (8, 10):
     for v in vs:
         ms = float(np.median(times[v]))
         res[f"bd{bd}_v{v}"] = {"ms": round(ms, 4), "hbm_frac": round(alg / ms / 1e6 / 8000, 3)}
-    os.environ.pop("X264HIP_HPEL_VARIANT", None)
+    sys.modules["x264hip"].set_variant("X264HIP_HPEL_VARIANT", None)
 print(json.dumps(res, indent=1))

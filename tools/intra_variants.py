@@ -22,7 +22,7 @@ for F in (16, 64):
         for name, satd, allm, var, rows in (("satd_all", True, True, "0", True), ("satd_all_v1", True, True, "1", True),
                                             ("satd_all_norows", True, True, "0", False),
                                             ("satd_dhv", True, False, "0", True), ("sad_all", False, True, "0", True)):
-            os.environ["X264HIP_LOWRES_INTRA_VARIANT"] = var
+            sys.modules["x264hip"].set_variant("X264HIP_LOWRES_INTRA_VARIANT", var)
             o = x.lowres_intra_cost(low, ls, mbw, mbh, satd, allm, 1, with_rows=rows)
             run = lambda: x.lowres_intra_cost(low, ls, mbw, mbh, satd, allm, 1, outs=o)  # noqa
             for _ in range(150):

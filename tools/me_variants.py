@@ -17,14 +17,14 @@ for bd in (8, 10):
     vs = (1, 2, 3) if bd == 8 else (1, 2, 5)
     tab = {}
     for v in vs:
-        os.environ["X264HIP_ME_VARIANT"] = str(v)
+        sys.modules["x264hip"].set_variant("X264HIP_ME_VARIANT", str(v))
         tab[v] = x.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, W // 16, H // 16, F, R,
                                   fenc_frame_stride=fs, ref_frame_stride=fs)
     torch.cuda.synchronize()
     for v in vs:
         assert torch.equal(tab[1][..., :2 * R + 1], tab[v][..., :2 * R + 1]), ("variants disagree", v)
     def setv(v):
-        os.environ["X264HIP_ME_VARIANT"] = str(v)
+        sys.modules["x264hip"].set_variant("X264HIP_ME_VARIANT", str(v))
     setv(vs[2])
     for _ in range(150):                              # clock ramp (tools/me_sustain.py)
         x.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, W // 16, H // 16, F, R,

@@ -33,7 +33,7 @@ for bd in (8, 10):
         run = lambda v: x.mb_dequant_idct_add(t, dct, mbw, mbh, F, dmf, qpm, dev[:-1], origin, stride, outs[v],  # noqa
                                               origin, stride, pred_frame_stride=fsz, recon_frame_stride=fsz)
         for v in outs:
-            os.environ["X264HIP_RECON_VARIANT"] = v
+            sys.modules["x264hip"].set_variant("X264HIP_RECON_VARIANT", v)
             run(v)
         torch.cuda.synchronize()
         assert torch.equal(outs["0"], outs["1"])
@@ -42,7 +42,7 @@ for bd in (8, 10):
         times = {v: [] for v in outs}
         for rnd in range(5):
             for v in outs:
-                os.environ["X264HIP_RECON_VARIANT"] = v
+                sys.modules["x264hip"].set_variant("X264HIP_RECON_VARIANT", v)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(3):

@@ -49,18 +49,18 @@ for bd in (8, 10):
         run = lambda v: x.subpel_cmp_batch(op, x.PIXEL_8x8, flat, stride, ref_planes, origin, stride, fo, qxy,  # noqa
                                            scores=sc[v])
         for v in vs:
-            os.environ["X264HIP_SUBPEL_VARIANT"] = v
+            sys.modules["x264hip"].set_variant("X264HIP_SUBPEL_VARIANT", v)
             run(v)
         torch.cuda.synchronize()
         for v in vs:
             assert torch.equal(sc[vs[0]], sc[v]), ("variants disagree", bd, op, v)
-        os.environ["X264HIP_SUBPEL_VARIANT"] = vs[-1]
+        sys.modules["x264hip"].set_variant("X264HIP_SUBPEL_VARIANT", vs[-1])
         for _ in range(150):
             run(vs[-1])
         times = {v: [] for v in vs}
         for rnd in range(5):
             for v in vs:
-                os.environ["X264HIP_SUBPEL_VARIANT"] = v
+                sys.modules["x264hip"].set_variant("X264HIP_SUBPEL_VARIANT", v)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(5):
@@ -71,6 +71,6 @@ for bd in (8, 10):
             ms = float(np.median(times[v]))
             res[f"bd{bd}_{order}_{'satd' if op == 2 else 'sad'}_v{v}"] = {"ms": round(ms, 4),
                                                                   "Gcand_s": round(fo.numel() / ms / 1e6, 1)}
-    os.environ.pop("X264HIP_SUBPEL_VARIANT", None)
+    sys.modules["x264hip"].set_variant("X264HIP_SUBPEL_VARIANT", None)
     del dev, hv
 print(json.dumps(res, indent=1))

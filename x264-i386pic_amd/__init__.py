@@ -25,7 +25,8 @@ __all__ = [
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
     "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "me_table_pitch", "me_esa_argmin", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
-    "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP",
+    "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
+    "backend_banner", "forward_ref",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -82,6 +83,41 @@ def init(device=0):
     rc = lib().x264hip_init(device)
     if rc != 0:
         raise BackendUnavailable(f"x264hip_init({device}) = {rc}: {lib().x264hip_last_error().decode()}")
+
+
+def set_variant(name, value=None):
+    """Select an A/B kernel variant by its environment name (``X264HIP_ME_VARIANT`` ...);
+    ``None`` / -1 restores the default.  Every variant is bit-exact."""
+    v = -1 if value is None or value == "default" else int(value)
+    if lib().x264hip_set_variant(name.encode(), v) != 0:
+        raise ValueError(f"unknown kernel variant switch {name!r}")
+
+
+def set_thread_device(device):
+    """Bind the calling thread's table entries to ``device`` (-1: the process device)."""
+    rc = lib().x264hip_set_thread_device(device)
+    if rc != 0:
+        raise BackendUnavailable(f"x264hip_set_thread_device({device}) = {rc}: {lib().x264hip_last_error().decode()}")
+
+
+def thread_device():
+    return lib().x264hip_thread_device()
+
+
+def backend_banner():
+    return lib().x264hip_backend_banner().decode()
+
+
+def forward_ref(dst, dst_device, src, src_device):
+    """Peer-copy a reconstructed reference (torch tensors of equal size) to the next GPU."""
+    import torch
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != nbytes:
+        raise ValueError("forward_ref: size mismatch")
+    with torch.cuda.device(src.device):
+        _rc(lib().x264hip_forward_ref(_c.c_void_p(dst.data_ptr()), dst_device, _c.c_void_p(src.data_ptr()),
+                                      src_device, nbytes, _stream()), "forward_ref")
+    return dst
 
 
 # ----------------------------------------------------------------- tables
@@ -231,6 +267,14 @@ def _declare(L):
     L.x264hip_init.restype = _c.c_int
     L.x264hip_last_error.restype = _c.c_char_p
     L.x264hip_available.restype = _c.c_int
+    L.x264hip_set_thread_device.argtypes = [_c.c_int]
+    L.x264hip_set_thread_device.restype = _c.c_int
+    L.x264hip_thread_device.restype = _c.c_int
+    L.x264hip_forward_ref.argtypes = [_P, _c.c_int, _P, _c.c_int, _c.c_size_t, _P]
+    L.x264hip_forward_ref.restype = _c.c_int
+    L.x264hip_backend_banner.restype = _c.c_char_p
+    L.x264hip_set_variant.argtypes = [_c.c_char_p, _c.c_int]
+    L.x264hip_set_variant.restype = _c.c_int
     L.x264hip_cqm_dequant.argtypes = [_P, _c.c_int, _P, _P]
     for bd in (8, 10):
         f = lambda n: getattr(L, f"x264hip_{bd}_{n}")  # noqa: E731

@@ -14,13 +14,19 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <atomic>
 #include <mutex>
 
 using namespace x264hip;
 
 // ============================================================ runtime
-static int g_device = -1;
+// The process device (x264hip_init) and an optional per-thread override
+// (x264hip_set_thread_device): x264's frame / lookahead threads may each bind a
+// different GPU of the node.  Per-call table entries run on the calling
+// thread's device, on a stream and pinned staging buffer owned by that thread.
+static std::atomic<int> g_device{ -1 };
 static std::mutex g_init_mutex;
+static thread_local int t_device = -1;
 static thread_local char t_err[256] = "";
 
 static int set_err( hipError_t e, const char *where )
@@ -31,38 +37,90 @@ static int set_err( hipError_t e, const char *where )
 
 extern "C" const char *x264hip_last_error( void ) { return t_err; }
 
-extern "C" int x264hip_init( int device )
+// 0 if `device` is a usable gfx950 device, else an X264HIP_E* code (t_err set)
+static int check_device( int device )
 {
-    std::lock_guard<std::mutex> lk( g_init_mutex );
     int n = 0;
     if( hipGetDeviceCount( &n ) != hipSuccess || n <= 0 )
     {
-        snprintf( t_err, sizeof(t_err), "x264hip_init: no HIP device" );
+        snprintf( t_err, sizeof(t_err), "x264hip: no HIP device" );
         return X264HIP_ENODEV;
     }
     if( device < 0 || device >= n )
+    {
+        snprintf( t_err, sizeof(t_err), "x264hip: device %d out of range (%d devices)", device, n );
         return X264HIP_EINVAL;
+    }
     hipDeviceProp_t prop;
     hipError_t e = hipGetDeviceProperties( &prop, device );
     if( e != hipSuccess )
         return set_err( e, "hipGetDeviceProperties" );
     if( strncmp( prop.gcnArchName, "gfx950", 6 ) )
     {
-        snprintf( t_err, sizeof(t_err), "x264hip_init: device %d is %s, not gfx950", device, prop.gcnArchName );
+        snprintf( t_err, sizeof(t_err), "x264hip: device %d is %s, not gfx950", device, prop.gcnArchName );
         return X264HIP_ENODEV;
     }
-    e = hipSetDevice( device );
+    return X264HIP_OK;
+}
+
+extern "C" int x264hip_init( int device )
+{
+    std::lock_guard<std::mutex> lk( g_init_mutex );
+    int rc = check_device( device );
+    if( rc != X264HIP_OK )
+        return rc;
+    hipError_t e = hipSetDevice( device );
     if( e != hipSuccess )
         return set_err( e, "hipSetDevice" );
-    g_device = device;
+    g_device.store( device, std::memory_order_release );
     return X264HIP_OK;
 }
 
 extern "C" int x264hip_available( void )
 {
-    if( g_device >= 0 )
+    if( g_device.load( std::memory_order_acquire ) >= 0 )
         return 1;
     return x264hip_init( 0 ) == X264HIP_OK;
+}
+
+extern "C" int x264hip_set_thread_device( int device )
+{
+    if( device < 0 )
+    {
+        t_device = -1;
+        return X264HIP_OK;
+    }
+    int rc = check_device( device );
+    if( rc != X264HIP_OK )
+        return rc;
+    hipError_t e = hipSetDevice( device );
+    if( e != hipSuccess )
+        return set_err( e, "hipSetDevice" );
+    t_device = device;
+    return X264HIP_OK;
+}
+
+extern "C" int x264hip_thread_device( void )
+{
+    return t_device >= 0 ? t_device : g_device.load( std::memory_order_acquire );
+}
+
+// reconstructed-reference forward between the GPUs of a frame-per-GPU pipeline
+// (SURVEY.md §8e): one xGMI peer copy on `stream`, asynchronous
+extern "C" int x264hip_forward_ref( void *dst, int dst_device, const void *src, int src_device, size_t bytes,
+                                    void *stream )
+{
+    if( bytes == 0 )
+        return X264HIP_OK;
+    if( !dst || !src || dst_device < 0 || src_device < 0 )
+        return X264HIP_EINVAL;
+    hipError_t e = hipMemcpyPeerAsync( dst, dst_device, src, src_device, bytes, (hipStream_t)stream );
+    if( e == hipErrorInvalidValue )
+    {
+        snprintf( t_err, sizeof(t_err), "x264hip_forward_ref: invalid argument" );
+        return X264HIP_EINVAL;
+    }
+    return e == hipSuccess ? X264HIP_OK : set_err( e, "hipMemcpyPeerAsync" );
 }
 
 [[noreturn]] static void fatal( hipError_t e, const char *where )
@@ -78,34 +136,86 @@ extern "C" int x264hip_available( void )
             fatal( e_, #call );                  \
     } while( 0 )
 
+// ------------------------------------------------------------ kernel variants
+namespace x264hip {
+static const char *const k_variant_env[V_COUNT] = {
+    "X264HIP_ME_VARIANT", "X264HIP_HPEL_VARIANT", "X264HIP_HPEL_ROWS", "X264HIP_SUBPEL_VARIANT",
+    "X264HIP_LOWRES_VARIANT", "X264HIP_DQ_VARIANT", "X264HIP_RECON_VARIANT", "X264HIP_LOWRES_INTRA_VARIANT" };
+
+struct VariantTable
+{
+    std::atomic<int> v[V_COUNT];
+    VariantTable()
+    {
+        for( int i = 0; i < V_COUNT; i++ )
+        {
+            const char *e = getenv( k_variant_env[i] );
+            v[i].store( e && *e ? atoi( e ) : -1, std::memory_order_relaxed );
+        }
+    }
+};
+static VariantTable &variants()
+{
+    static VariantTable t;   // seeded from the environment once, at first use
+    return t;
+}
+int variant( VariantSlot slot ) { return variants().v[slot].load( std::memory_order_relaxed ); }
+} // namespace x264hip
+
+extern "C" int x264hip_set_variant( const char *name, int value )
+{
+    for( int i = 0; i < V_COUNT; i++ )
+        if( name && !strcmp( name, k_variant_env[i] ) )
+        {
+            variants().v[i].store( value < 0 ? -1 : value, std::memory_order_relaxed );
+            return X264HIP_OK;
+        }
+    return X264HIP_EINVAL;
+}
+
 // per-thread stream + pinned staging buffer for the per-call table entries
 namespace {
 struct CallCtx
 {
+    int device = -1;
     hipStream_t stream = nullptr;
     uint8_t *host = nullptr;   // host view
     uint8_t *dev = nullptr;    // device view of the same pinned memory
     static constexpr size_t SIZE = 64 << 10;
-    ~CallCtx()
+    void release()
     {
-        // streams and pinned memory are reclaimed with the HIP context at exit
+        // errors ignored: at process teardown the runtime may already be gone
+        if( stream )
+            (void)hipStreamDestroy( stream );
+        if( host )
+            (void)hipHostFree( host );
+        stream = nullptr;
+        host = dev = nullptr;
+        device = -1;
     }
+    ~CallCtx() { release(); }
 };
 thread_local CallCtx t_call;
 
+// Entries are installed only when x264hip_available() held (see the initialisers
+// below), so a device is always bound here; the thread's override wins.
 CallCtx &call_ctx()
 {
+    const int dev = x264hip_thread_device();
+    if( dev < 0 )
+    {
+        fprintf( stderr, "x264hip: table entry called before x264hip_init\n" );
+        abort();
+    }
+    if( t_call.stream && t_call.device != dev )
+        t_call.release();
     if( !t_call.stream )
     {
-        if( g_device < 0 && x264hip_init( 0 ) != X264HIP_OK )
-        {
-            fprintf( stderr, "x264hip: table entry called without a usable gfx950 device (%s)\n", t_err );
-            abort();
-        }
-        CHECK_FATAL( hipSetDevice( g_device ) );
+        CHECK_FATAL( hipSetDevice( dev ) );
         CHECK_FATAL( hipStreamCreateWithFlags( &t_call.stream, hipStreamNonBlocking ) );
         CHECK_FATAL( hipHostMalloc( (void **)&t_call.host, CallCtx::SIZE, hipHostMallocDefault ) );
         CHECK_FATAL( hipHostGetDevicePointer( (void **)&t_call.dev, t_call.host, 0 ) );
+        t_call.device = dev;
     }
     return t_call;
 }
@@ -875,41 +985,102 @@ static int map_err( hipError_t e, const char *where )
     return set_err( e, where );
 }
 
+// ------------------------------------------------------------ backend banner
+// The analogue of the encoder's "using cpu capabilities" line (reference
+// encoder/encoder.c:1676-1706): which device serves the tables and which entries
+// the HIP backend filled.  Printed once to stderr at the first table fill
+// (X264HIP_QUIET=1 silences it); x264hip_backend_banner() returns the text.
+static char g_banner[768];
+static std::once_flag g_banner_once;
+static std::mutex g_banner_mutex;
+
+static void build_banner()
+{
+    std::lock_guard<std::mutex> lk( g_banner_mutex );
+    const int dev = x264hip_thread_device();
+    hipDeviceProp_t prop;
+    char name[160] = "no device";
+    if( dev >= 0 && hipGetDeviceProperties( &prop, dev ) == hipSuccess )
+        snprintf( name, sizeof(name), "device %d %s (%s, %d CUs)", dev, prop.name, prop.gcnArchName,
+                  prop.multiProcessorCount );
+    snprintf( g_banner, sizeof(g_banner),
+              "x264hip: %s; HIP entries: pixel sad/sad_aligned/ssd/satd[8] sad_x3/x4 satd_x3/x4[7] sa8d[2] "
+              "sa8d_satd var[3] var2[2] hadamard_ac[4] vsad asd8 ads[7] intra_*_x3[10]; dct 17/17; "
+              "quant quant[5] dequant[3] idct_dequant_2x4[2] optimize_chroma[2] denoise decimate[3] coeff_last[16] "
+              "coeff_level_run[15]; zigzag 6+6; kept from the caller's C init: ssim[7] ssd_nv12_core "
+              "ssim_4x4x2_core ssim_end4 intra_*_x9 trellis_cabac_*",
+              name );
+}
+
+static void note_fill()
+{
+    std::call_once( g_banner_once, [] {
+        build_banner();
+        const char *q = getenv( "X264HIP_QUIET" );
+        if( !(q && *q && *q != '0') )
+            fprintf( stderr, "%s\n", g_banner );
+    } );
+}
+
+extern "C" const char *x264hip_backend_banner( void )
+{
+    build_banner();
+    return g_banner;
+}
+
+// Table initialisers.  Both forms only OVERRIDE: the entries this backend
+// implements are replaced, every other entry (ssim_*, the trellis entries,
+// intra_*_x9_*, and the encoder's mbcmp / fpelcmp aliases) keeps what the caller's
+// C init put there.  Without a usable gfx950 device (or without X264HIP_CPU_HIP in
+// `cpu` for the flag form) the table is left untouched, so a host without the GPU
+// keeps its C entries, the convention of reference common/opencl.c:400-409; no
+// entry that could reach a missing device is ever installed.
 #define DEFINE_ENTRIES( BD )                                                                                         \
-    extern "C" void x264hip_##BD##_pixel_init_hip( x264hip_##BD##_pixel_function_t *pixf ) { fill_pixel<BD>( pixf ); } \
+    extern "C" void x264hip_##BD##_pixel_init_hip( x264hip_##BD##_pixel_function_t *pixf )                         \
+    {                                                                                                                \
+        if( pixf && x264hip_available() )                                                                            \
+        {                                                                                                            \
+            fill_pixel<BD>( pixf );                                                                                  \
+            note_fill();                                                                                             \
+        }                                                                                                            \
+    }                                                                                                                \
     extern "C" void x264hip_##BD##_pixel_init( uint32_t cpu, x264hip_##BD##_pixel_function_t *pixf )                \
     {                                                                                                                \
-        memset( pixf, 0, sizeof(*pixf) );                                                                            \
-        if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
-            fill_pixel<BD>( pixf );                                                                                  \
+        if( cpu & X264HIP_CPU_HIP )                                                                                  \
+            x264hip_##BD##_pixel_init_hip( pixf );                                                                   \
     }                                                                                                                \
-    extern "C" void x264hip_##BD##_dct_init_hip( x264hip_##BD##_dct_function_t *d ) { fill_dct<BD>( d ); }          \
-    extern "C" void x264hip_##BD##_dct_init( uint32_t cpu, x264hip_##BD##_dct_function_t *d )                       \
+    extern "C" void x264hip_##BD##_dct_init_hip( x264hip_##BD##_dct_function_t *d )                                 \
     {                                                                                                                \
-        memset( d, 0, sizeof(*d) );                                                                                  \
-        if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
+        if( d && x264hip_available() )                                                                               \
             fill_dct<BD>( d );                                                                                       \
     }                                                                                                                \
-    extern "C" void x264hip_##BD##_quant_init_hip( x264hip_##BD##_quant_function_t *q ) { fill_quant<BD>( q ); }    \
+    extern "C" void x264hip_##BD##_dct_init( uint32_t cpu, x264hip_##BD##_dct_function_t *d )                       \
+    {                                                                                                                \
+        if( cpu & X264HIP_CPU_HIP )                                                                                  \
+            x264hip_##BD##_dct_init_hip( d );                                                                        \
+    }                                                                                                                \
+    extern "C" void x264hip_##BD##_quant_init_hip( x264hip_##BD##_quant_function_t *q )                             \
+    {                                                                                                                \
+        if( q && x264hip_available() )                                                                               \
+            fill_quant<BD>( q );                                                                                     \
+    }                                                                                                                \
     extern "C" void x264hip_##BD##_quant_init( void *h, uint32_t cpu, x264hip_##BD##_quant_function_t *q )          \
     {                                                                                                                \
         (void)h;                                                                                                     \
-        memset( q, 0, sizeof(*q) );                                                                                  \
-        if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
-            fill_quant<BD>( q );                                                                                     \
+        if( cpu & X264HIP_CPU_HIP )                                                                                  \
+            x264hip_##BD##_quant_init_hip( q );                                                                      \
     }                                                                                                                \
     extern "C" void x264hip_##BD##_zigzag_init_hip( x264hip_##BD##_zigzag_function_t *p,                            \
                                                     x264hip_##BD##_zigzag_function_t *i )                            \
     {                                                                                                                \
-        fill_zigzag<BD>( p, i );                                                                                     \
+        if( p && i && x264hip_available() )                                                                          \
+            fill_zigzag<BD>( p, i );                                                                                 \
     }                                                                                                                \
     extern "C" void x264hip_##BD##_zigzag_init( uint32_t cpu, x264hip_##BD##_zigzag_function_t *p,                  \
                                                 x264hip_##BD##_zigzag_function_t *i )                                \
     {                                                                                                                \
-        memset( p, 0, sizeof(*p) );                                                                                  \
-        memset( i, 0, sizeof(*i) );                                                                                  \
-        if( (cpu & X264HIP_CPU_HIP) && x264hip_available() )                                                         \
-            fill_zigzag<BD>( p, i );                                                                                 \
+        if( cpu & X264HIP_CPU_HIP )                                                                                  \
+            x264hip_##BD##_zigzag_init_hip( p, i );                                                                  \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_cqm_init( const uint8_t *const sl[8], int dz_inter, int dz_intra, int b8,         \
                                             PT<BD>::udctcoef *q4m, PT<BD>::udctcoef *q4b, PT<BD>::udctcoef *q8m,     \

@@ -917,8 +917,8 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
     int lpm = transform == 4 ? 16 : transform == 8 ? 4 : 0;
     if( !lpm )
         return hipErrorInvalidValue;
-    const char *ev = getenv( "X264HIP_DQ_VARIANT" );
-    if( !ev || atoi( ev ) != 1 )
+    const int ev = variant( V_DQ );
+    if( ev != 1 )
     {
         // default: strip kernel, one wave per 16 MBs of a row
         int64_t waves = (int64_t)nframes * mbh * ((mbw + 15) / 16);
@@ -927,16 +927,16 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
         dim3 blk( 256 ), g( (unsigned)((waves + 3) / 4) );
         // transform 4 default: variant 5 (0.62-0.71 of HBM vs 0.50-0.52 for variant 0,
         // tools/dq_variants.py); X264HIP_DQ_VARIANT=0 selects the 16-MB staged strip
-        if( transform == 4 && (!ev || atoi( ev ) == 5) )
+        if( transform == 4 && (ev < 0 || ev == 5) )
         {
             const int64_t hw = (int64_t)nframes * mbh * ((mbw + 7) / 8);
             hipLaunchKernelGGL( mb_dct_quant_halfband_kernel<BD>, dim3( (unsigned)((hw + 3) / 4) ), blk, 0, stream, fenc,
                                 fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
             return hipGetLastError();
         }
-        if( transform == 4 && ev && (atoi( ev ) == 3 || atoi( ev ) == 4) )
+        if( transform == 4 && (ev == 3 || ev == 4) )
         {
-            if( atoi( ev ) == 3 )
+            if( ev == 3 )
                 hipLaunchKernelGGL( ( mb_dct_quant_band_kernel<BD, true> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps,
                                     pfs, mbw, mbh, nframes, mf, bias, dct, nz );
             else
@@ -947,9 +947,9 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
         // transform 8 at 8 bit default: variant 6 (packed 16-bit pairs, 7 = its unstaged stores); 0 / 2
         // select the strip kernel
         if constexpr( BD == 8 )
-            if( transform == 8 && (!ev || atoi( ev ) == 6 || atoi( ev ) == 7) )
+            if( transform == 8 && (ev < 0 || ev == 6 || ev == 7) )
             {
-                if( !ev || atoi( ev ) == 6 )
+                if( ev < 0 || ev == 6 )
                     hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<true>, g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs,
                                         mbw, mbh, nframes, mf, bias, dct, nz );
                 else
@@ -957,7 +957,7 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
                                         pfs, mbw, mbh, nframes, mf, bias, dct, nz );
                 return hipGetLastError();
             }
-        const bool stage = !ev || atoi( ev ) != 2;
+        const bool stage = ev != 2;
 #define DQ_STRIP( T, S ) hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, S> ), g, blk, 0, stream, fenc, fs, ffs, \
                                              pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz )
         if( transform == 4 )

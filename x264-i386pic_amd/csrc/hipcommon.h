@@ -189,6 +189,18 @@ template <int BD> __device__ __forceinline__ int upix( uint32_t w, int k )
 
 } // namespace x264hip
 
+// ---- A/B kernel-variant switches ----
+// Seeded once from the X264HIP_*_VARIANT environment variables when the library
+// loads and changed only through x264hip_set_variant(): launchers read an atomic,
+// never the environment.  -1 = the launcher's default.
+namespace x264hip {
+enum VariantSlot
+{
+    V_ME = 0, V_HPEL, V_HPEL_ROWS, V_SUBPEL, V_LOWRES, V_DQ, V_RECON, V_LOWRES_INTRA, V_COUNT
+};
+int variant( VariantSlot slot );
+} // namespace x264hip
+
 // ---- launchers implemented in the .hip files (all enqueue on `stream`) ----
 namespace x264hip {
 template <int BD>

@@ -1168,13 +1168,13 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
 {
     if( mbw <= 0 || mbh <= 0 || nframes <= 0 )
         return hipSuccess;
-    const char *ev = getenv( "X264HIP_RECON_VARIANT" );
+    const int ev = variant( V_RECON );
     // 8 bit: block pairs (0.55 vs 0.43 of HBM, tools/recon_variants.py); 10 bit: one lane
     // per block is faster (0.68 vs 0.58); X264HIP_RECON_VARIANT = 0 / 1 forces either
-    const bool pair = ev ? atoi( ev ) != 1 : BD == 8;
+    const bool pair = ev >= 0 ? ev != 1 : BD == 8;
     // transform 8 at 8 bit: the packed kernel unless X264HIP_RECON_VARIANT = 1 (lane per block, int32)
     if constexpr( BD == 8 )
-        if( transform == 8 && (!ev || atoi( ev ) != 1) )
+        if( transform == 8 && ev != 1 )
         {
             const int64_t total = (int64_t)nframes * mbw * mbh * 4;
             hipLaunchKernelGGL( mb_recon8_pk_kernel, dim3( (unsigned)((total + 255) / 256) ), dim3( 256 ), 0, st, dct,

@@ -346,8 +346,7 @@ hipError_t launch_lowres_intra( const typename PT<BD>::pixel *plane, intptr_t st
 {
     if( mbw <= 0 || mbh <= 0 || nframes <= 0 )
         return hipSuccess;
-    const char *ev = getenv( "X264HIP_LOWRES_INTRA_VARIANT" );
-    const bool per_wave = ev && atoi( ev ) == 1;
+    const bool per_wave = variant( V_LOWRES_INTRA ) == 1;
     if( row_satd && per_wave )
     {
         hipError_t e = hipMemsetAsync( row_satd, 0, sizeof(int32_t) * (size_t)mbh * nframes, st );

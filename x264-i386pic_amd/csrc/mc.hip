@@ -455,8 +455,8 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
 {
     if( nframes <= 0 || width <= 0 || height <= 0 )
         return hipSuccess;
-    const char *ev = getenv( "X264HIP_HPEL_VARIANT" );
-    const int var = ev ? atoi( ev ) : BD == 8 ? 2 : 0;
+    const int ev = variant( V_HPEL );
+    const int var = ev >= 0 ? ev : BD == 8 ? 2 : 0;
     if constexpr( BD == 8 )
     {
         // streaming kernel: needs 16-byte aligned rows (pixel (0,0) and the strides)
@@ -470,8 +470,8 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
             // 12-row strips: twice the waves of 24-row ones for 5 halo rows per strip
             // (16 frames: 0.0455 -> 0.0398 ms; 64 frames: 0.166 -> 0.158 ms; 16 rows in
             // between).  X264HIP_HPEL_ROWS = 16 / 24 selects the taller strips.
-            const char *er = getenv( "X264HIP_HPEL_ROWS" );
-            const int rows = er && (atoi( er ) == 16 || atoi( er ) == 24) ? atoi( er ) : 12;
+            const int er = variant( V_HPEL_ROWS );
+            const int rows = er == 16 || er == 24 ? er : 12;
             dim3 g( nchunk, (height + 16 + rows - 1) / rows, nframes );
             if( rows == 24 )
                 hipLaunchKernelGGL( hpel_stream_kernel<24>, g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,
@@ -867,10 +867,10 @@ hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel 
 {
     if( n <= 0 )
         return hipSuccess;
-    const char *ev = getenv( "X264HIP_SUBPEL_VARIANT" );
+    const int ev = variant( V_SUBPEL );
     // variant 2: one lane per block row (slower on the bench list: 0.25 vs 0.13 ms for
     // 4.7 M 8x8 candidates, the per-candidate set-up is repeated in every row lane)
-    if( op == 2 && i_pixel <= 3 && ev && atoi( ev ) == 2 )
+    if( op == 2 && i_pixel <= 3 && ev == 2 )
     {
         const int h = pix_h( i_pixel );
         const int64_t lanes = (int64_t)n * h;
@@ -887,7 +887,7 @@ hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel 
     // loads (0.101 / 0.193; default at 8 bit), 5 = dword-aligned row loads + alignbyte
     // (0.115 / 0.186; default at 10 bit, and 0.178 against 0.276 for variant 3 when the
     // list is block-major)
-    const int var = ev ? atoi( ev ) : BD == 8 ? 3 : 5;
+    const int var = ev >= 0 ? ev : BD == 8 ? 3 : 5;
     const bool v1 = var == 1;
 #define SP_CASE( OP, I )                                                                                      \
     case I:                                                                                                   \
@@ -1115,10 +1115,10 @@ hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t
     {
         // 16-pixel lanes with 16-byte loads and stores: needs 16-byte aligned rows and a
         // width of whole macroblocks (X264HIP_LOWRES_VARIANT=1 selects the dword kernel)
-        const char *ev = getenv( "X264HIP_LOWRES_VARIANT" );
+        const int ev = variant( V_LOWRES );
         const uintptr_t al = (uintptr_t)src | (uintptr_t)stride | (uintptr_t)fstride | (uintptr_t)dst[0] |
                              (uintptr_t)dst[1] | (uintptr_t)dst[2] | (uintptr_t)dst[3] | (uintptr_t)ds | (uintptr_t)dfs;
-        if( !(ev && atoi( ev ) == 1) && !(al & 15) && !(width & 15) )
+        if( ev != 1 && !(al & 15) && !(width & 15) )
         {
             dim3 g16( 1, (unsigned)(hl + 64), (unsigned)nframes );
             hipLaunchKernelGGL( lowres16_kernel, g16, dim3( 128 ), 0, st, src, stride, fstride, width, height, dst[0],

@@ -435,8 +435,8 @@ static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intp
 // nearly every 128-B line left L2 partially written.)
 static int me_variant()
 {
-    const char *e = getenv( "X264HIP_ME_VARIANT" );
-    return e ? atoi( e ) : 0;
+    const int v = variant( V_ME );
+    return v >= 0 ? v : 0;
 }
 
 template <int R, typename P, typename T>
