@@ -350,28 +350,48 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
     bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)
-    fo, qxy = [], []
+    # one entry per 8x8 block: its half-pel centre (3.5, 2) px; the nine candidates are the
+    # +-1 quarter-pel neighbourhood (subpel_qpel9_batch); the same candidates as a flat
+    # list (one lane per candidate, subpel_cmp_batch) are timed beside it
+    bfo, cxy, fo, qxy = [], [], [], []
     for f in range(F):
+        bfo.append((f + 1) * fstride + origin + by * stride + bx)
+        c = np.stack([4 * bx + 12 + 2, 4 * by + 8 + 4 * f * (fstride // stride)], 1)
+        cxy.append(c.astype(np.int32))
         for dy in (-1, 0, 1):
             for dx in (-1, 0, 1):
-                fo.append((f + 1) * fstride + origin + by * stride + bx)
-                q = np.stack([4 * bx + 12 + 2 + dx, 4 * by + 8 + dy], 1)
-                # frame f's planes: fold the frame offset into the quarter-pel row coordinate
-                q[:, 1] += 4 * f * (fstride // stride)
-                qxy.append(q.astype(np.int32))
+                fo.append(bfo[-1])
+                qxy.append((c + np.array([dx, dy])).astype(np.int32))
+    bfo = torch.from_numpy(np.concatenate(bfo)).cuda()
+    cxy = torch.from_numpy(np.concatenate(cxy)).cuda()
     fo = torch.from_numpy(np.concatenate(fo)).cuda()
     qxy = torch.from_numpy(np.concatenate(qxy)).cuda()
     sc = torch.empty(fo.numel(), dtype=torch.int32, device="cuda")
+    sc9 = torch.empty((bfo.numel(), 9), dtype=torch.int32, device="cuda")
     flat = dev.view(-1)
     ref_planes = [dev.view(-1)] + [h.view(-1) for h in hv]
+
+    def s9step():
+        x.subpel_qpel9_batch(x.CMP_SATD, x.PIXEL_8x8, flat, stride, ref_planes, origin, stride, bfo, cxy, scores=sc9)
+    wall, ev_ms = timed(s9step, a.steps, a.warmup, world)
+    cands = sc9.numel()
+    res["satd8x8_subpel_candidates_per_s"] = world * a.steps * cands / wall
+    res["satd8x8_subpel_launch_ms"] = ev_ms
+    res["satd8x8_candidates_per_launch"] = int(cands)
+    # 444 lane-ops per SATD 8x8 + 192 for the qpel averages, vs the VALU peak
+    res["satd8x8_subpel_frac"] = cands * (444 + 192) / (ev_ms * 1e-3) / VALU_LANE_OPS
 
     def sstep():
         x.subpel_cmp_batch(x.CMP_SATD, x.PIXEL_8x8, flat, stride, ref_planes, origin, stride, fo, qxy, scores=sc)
     wall, ev_ms = timed(sstep, a.steps, a.warmup, world)
-    res["satd8x8_subpel_candidates_per_s"] = world * a.steps * fo.numel() / wall
-    res["satd8x8_subpel_launch_ms"] = ev_ms
-    res["satd8x8_candidates_per_launch"] = int(fo.numel())
-    del nb8, hv, ref_planes, fo, qxy, sc
+    res["satd8x8_subpel_list_candidates_per_s"] = world * a.steps * fo.numel() / wall
+    res["satd8x8_subpel_list_launch_ms"] = ev_ms
+    # both entries score the same candidates (list order: frame, dy, dx, block)
+    nbl = bx.size
+    lst = sc.view(F, 9, nbl).permute(0, 2, 1).reshape(-1, 9)
+    if not torch.equal(lst, sc9):
+        raise SystemExit("bench: subpel_qpel9_batch and subpel_cmp_batch disagree")
+    del nb8, hv, ref_planes, fo, qxy, sc, bfo, cxy, sc9, lst
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
     res.update(rates_2160p(x, a, world))
     return res

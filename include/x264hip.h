@@ -588,6 +588,20 @@ int x264hip_##BD##_subpel_cmp_batch( int op, int i_pixel, const pixel *fenc,    
                                      const int64_t *fenc_off, const int32_t *qpel_xy,           \
                                      int n, int32_t *scores, void *stream );                    \
                                                                                                 \
+/* the 3x3 quarter-pel neighbourhood of a centre: for block i with fenc at                      \
+ * fenc + fenc_off[i] and centre (cx, cy) = centre_xy[2i], centre_xy[2i+1] (quarter             \
+ * pixels, as qpel_xy above), scores[9i + 3(dy+1) + (dx+1)] = op of the candidate               \
+ * (cx+dx, cy+dy), dx, dy in -1..1 -- refine_subpel's quarter-pel diamond around the            \
+ * half-pel winner plus its corners (reference encoder/me.c:950-963).  Equal to nine            \
+ * subpel_cmp_batch candidates; a half-pel centre (even cx, cy) is the fast case                \
+ * (the nine predictions from one set of register windows).  i_pixel 16x16..8x8. */             \
+int x264hip_##BD##_subpel_qpel9_batch( int op, int i_pixel, const pixel *fenc,                  \
+                                       intptr_t fenc_stride, const pixel *fpel,                 \
+                                       const pixel *hpel_h, const pixel *hpel_v,                \
+                                       const pixel *hpel_c, intptr_t ref_stride,                \
+                                       const int64_t *fenc_off, const int32_t *centre_xy,       \
+                                       int n, int32_t *scores, void *stream );                  \
+                                                                                                \
 /* block lists of the reference transforms (dct.c), device arrays;                             \
  * dct holds n consecutive outputs of the selected entry's size. */                             \
 int x264hip_##BD##_sub_dct_batch( int kind, const pixel *fenc, intptr_t fenc_stride,            \

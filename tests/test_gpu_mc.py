@@ -79,6 +79,44 @@ def test_subpel_cmp_random(hip, oracle, bd, op, variant, monkeypatch):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("op", [0, 2])
+def test_subpel_qpel9_random(hip, oracle, bd, op):
+    """the 3x3 quarter-pel neighbourhood entry equals nine get_ref + SAD / SATD candidates of
+    the oracle (me.c:950-963, mc.c:221-249): half-pel centres in all four phase combinations
+    (the register-window path, both diagonal pairings of x264_hpel_ref0/1), quarter-pel
+    centres (the per-candidate path) mixed into the same waves, negative positions."""
+    from x264hip import synth
+    W, H = 160, 96
+    planes, stride, origin = synth.random_planes(2, W, H, bd, seed=13)
+    dev = _dev(planes, bd)
+    hv = hip.hpel_filter(dev[:1], origin, stride, W, H)
+    ref_planes = [dev[0]] + [o[0] for o in hv]
+    host_planes = [planes[0].ravel()] + [_host(o, bd)[0].ravel() for o in hv]
+    rs = np.random.default_rng(31 * op + bd)
+    for i_pixel in range(4):
+        n = 2000
+        bw, bh = hip.PIXEL_SIZES[i_pixel]
+        bx = rs.integers(0, W - bw + 1, n)
+        by = rs.integers(0, H - bh + 1, n)
+        mvx = 2 * rs.integers(-2 * 20, 2 * 20 + 1, n)            # half-pel centres, +-20 px
+        mvy = 2 * rs.integers(-2 * 20, 2 * 20 + 1, n)
+        odd = rs.random(n) < 0.15                                  # some quarter-pel centres
+        mvx[odd] += rs.integers(-1, 2, odd.sum()) | 1
+        cxy = np.stack([4 * bx + mvx, 4 * by + mvy], 1).astype(np.int32)
+        fo = (planes[0].size + origin + by * stride + bx).astype(np.int64)
+        got = hip.subpel_qpel9_batch(op, i_pixel, dev.view(-1), stride, ref_planes, origin, stride,
+                                     torch.from_numpy(fo).cuda(), torch.from_numpy(cxy).cuda()).cpu().numpy()
+        k = np.arange(9)
+        qxy = (cxy[:, None, :] + np.stack([k % 3 - 1, k // 3 - 1], 1)[None]).reshape(-1, 2).astype(np.int32)
+        want = oracle.subpel_list(bd, op, i_pixel, planes.ravel(), stride, host_planes, origin, stride,
+                                  np.repeat(fo, 9), qxy).reshape(n, 9)
+        assert np.array_equal(got, want), (i_pixel, np.argwhere(got != want)[:3])
+    with pytest.raises(RuntimeError):
+        hip.subpel_qpel9_batch(op, 4, dev.view(-1), stride, ref_planes, origin, stride,
+                               torch.from_numpy(fo[:4]).cuda(), torch.from_numpy(cxy[:4]).cuda())
+
+
+@pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("size", [(1920, 1088), (176, 144), (72, 40)])
 def test_frame_init_lowres(hip, oracle, bd, size):
     """x264_frame_init_lowres of 3 frames per call vs the oracle; the source padding holds

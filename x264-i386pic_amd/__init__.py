@@ -23,7 +23,7 @@ import os
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "me_table_pitch", "me_esa_argmin", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref",
@@ -300,6 +300,9 @@ def _declare(L):
         f("me_search_centred").restype = _c.c_int
         f("hpel_filter").argtypes = [_P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P]
         f("subpel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, _c.c_int, _P, _P]
+        f("subpel_qpel9_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, _c.c_int, _P,
+                                            _P]
+        f("subpel_qpel9_batch").restype = _c.c_int
         f("mb_dct_quant").argtypes = [_c.c_int, _P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int,
                                       _P, _P, _P, _P, _P]
         f("pixel_stat_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _IP, _P, _P, _c.c_int, _c.c_int, _P, _P]
@@ -843,6 +846,21 @@ def subpel_cmp_batch(op, i_pixel, fenc, fenc_stride, planes, ref_origin, ref_str
     _rc(getattr(lib(), f"x264hip_{bd}_subpel_cmp_batch")(
         op, i_pixel, _ptr(fenc), fenc_stride, *[_ptr(p, ref_origin) for p in planes], ref_stride,
         _ptr(fenc_off), _ptr(qpel_xy), n, _ptr(scores), _stream()), "subpel_cmp_batch")
+    return scores
+
+
+def subpel_qpel9_batch(op, i_pixel, fenc, fenc_stride, planes, ref_origin, ref_stride, fenc_off, centre_xy,
+                       scores=None):
+    """The 3x3 quarter-pel neighbourhood of each block's centre (x264hip_*_subpel_qpel9_batch):
+    centre_xy int32 [n, 2] quarter-pel positions; returns int32 [n, 9], index 3*(dy+1)+(dx+1)."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = fenc_off.numel()
+    if scores is None:
+        scores = torch.empty((n, 9), dtype=torch.int32, device=fenc.device)
+    _rc(getattr(lib(), f"x264hip_{bd}_subpel_qpel9_batch")(
+        op, i_pixel, _ptr(fenc), fenc_stride, *[_ptr(p, ref_origin) for p in planes], ref_stride,
+        _ptr(fenc_off), _ptr(centre_xy), n, _ptr(scores), _stream()), "subpel_qpel9_batch")
     return scores
 
 

@@ -1267,6 +1267,19 @@ extern "C" const char *x264hip_backend_banner( void )
         return map_err( launch_subpel_cmp<BD>( op, i_pixel, fenc, fs, planes, rs, fo, qxy, n, scores,                \
                                                (hipStream_t)stream ), "subpel_cmp_batch" );                          \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_subpel_qpel9_batch( int op, int i_pixel, const PT<BD>::pixel *fenc, intptr_t fs,  \
+                                                      const PT<BD>::pixel *p0, const PT<BD>::pixel *p1,              \
+                                                      const PT<BD>::pixel *p2, const PT<BD>::pixel *p3, intptr_t rs, \
+                                                      const int64_t *fo, const int32_t *cxy, int n, int32_t *scores, \
+                                                      void *stream )                                                 \
+    {                                                                                                                \
+        if( ( op != X264HIP_CMP_SAD && op != X264HIP_CMP_SATD ) || i_pixel < 0 || i_pixel > 3 || n < 0 ||             \
+            ( n > 0 && ( !fenc || !p0 || !p1 || !p2 || !p3 || !fo || !cxy || !scores ) ) )                           \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
+        return map_err( launch_subpel_qpel9<BD>( op, i_pixel, fenc, fs, planes, rs, fo, cxy, n, scores,              \
+                                                 (hipStream_t)stream ), "subpel_qpel9_batch" );                      \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_sub_dct_batch( int kind, const PT<BD>::pixel *fenc, intptr_t fs,                  \
                                                  const PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fo,          \
                                                  const int64_t *dofs, int n, PT<BD>::dctcoef *dct, void *stream )    \

@@ -746,25 +746,16 @@ __device__ __forceinline__ void load_row_al( const void *p, uint32_t (&out)[NDW]
 // dword-aligned loads + alignbyte (load_row_al); the 8-bit
 // rounding average is one v_lerp_u8 per dword (pixel_avg, mc.c:57).
 template <int BD, int OP, int IPIX, int LD>
-__global__ __launch_bounds__( 256 ) void subpel_cmp3_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
-                                                             intptr_t fs, const typename PT<BD>::pixel *p0,
-                                                             const typename PT<BD>::pixel *p1,
-                                                             const typename PT<BD>::pixel *p2,
-                                                             const typename PT<BD>::pixel *p3, intptr_t rs,
-                                                             const int64_t *__restrict__ fenc_off,
-                                                             const int32_t *__restrict__ qxy, int n,
-                                                             int32_t *__restrict__ scores )
+__device__ __forceinline__ int subpel_score( const typename PT<BD>::pixel *a, intptr_t fs,
+                                             const typename PT<BD>::pixel *p0, const typename PT<BD>::pixel *p1,
+                                             const typename PT<BD>::pixel *p2, const typename PT<BD>::pixel *p3,
+                                             intptr_t rs, int qx, int qy )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int PPD = PT<BD>::PPD;
     constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
     constexpr int NDW = W / PPD;
     constexpr int BAND = (16 / NDW) < 4 ? 4 : (16 / NDW) > H ? H : (16 / NDW);   // rows per load burst
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if( i >= n )
-        return;
-    const int2 q = *(const int2 *)(qxy + 2 * i);
-    const int qx = q.x, qy = q.y;
     const int idx = ((qy & 3) << 2) + (qx & 3);
     const intptr_t off = (intptr_t)(qy >> 2) * rs + (qx >> 2);
     const int i0 = c_hpel_ref0[idx], i1 = c_hpel_ref1[idx];
@@ -772,7 +763,6 @@ __global__ __launch_bounds__( 256 ) void subpel_cmp3_kernel( const typename PT<B
     const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((qx & 3) == 3);
     if( !(idx & 5) )
         s2 = s1;
-    const pixel *a = fenc + fenc_off[i];
     uint32_t acc = 0;
     int sum = 0;
 #pragma unroll
@@ -857,7 +847,181 @@ __global__ __launch_bounds__( 256 ) void subpel_cmp3_kernel( const typename PT<B
         sum = (int)acc;
     else if constexpr( W >= 8 )
         sum = (int)(acc >> 1);
-    scores[i] = sum;
+    return sum;
+}
+
+template <int BD, int OP, int IPIX, int LD>
+__global__ __launch_bounds__( 256 ) void subpel_cmp3_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                             intptr_t fs, const typename PT<BD>::pixel *p0,
+                                                             const typename PT<BD>::pixel *p1,
+                                                             const typename PT<BD>::pixel *p2,
+                                                             const typename PT<BD>::pixel *p3, intptr_t rs,
+                                                             const int64_t *__restrict__ fenc_off,
+                                                             const int32_t *__restrict__ qxy, int n,
+                                                             int32_t *__restrict__ scores )
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    const int2 q = *(const int2 *)(qxy + 2 * i);
+    scores[i] = subpel_score<BD, OP, IPIX, LD>( fenc + fenc_off[i], fs, p0, p1, p2, p3, rs, q.x, q.y );
+}
+
+// ------------------------------------------------------------ qpel neighbourhood of an hpel centre
+// x264hip_*_subpel_qpel9_batch: for block i the 3x3 quarter-pel neighbourhood (dx, dy in
+// -1..1) of a centre (cx, cy) -- refine_subpel's first quarter-pel diamond and its corners
+// (encoder/me.c:950-963), each candidate get_ref (common/mc.c:221-249) + SAD / SATD.
+//
+// In half-pel grid units the four planes are one grid G(u, v) = plane[(v & 1) * 2 + (u & 1)]
+// at pixel (u >> 1, v >> 1) (F, H, V, C; mc.c:173-196).  For a half-pel centre (cx, cy even,
+// hx = cx / 2, hy = cy / 2) every candidate pixel (column k, row j of the block) is G at
+// (hx + 2k + {-1, 0, 1}, hy + 2j + {-1, 0, 1}) or the rounded average of two such samples,
+// x264_hpel_ref0/1 (common/tables.c:183-184) read as: the axial candidates average the centre
+// sample with its half-pel neighbour, and a diagonal candidate averages {centre, diagonal
+// neighbour} when the centre's quarter-pel phases differ ((cx ^ cy) & 2) and {horizontal,
+// vertical neighbour} otherwise -- for all nine candidates of the lane.  So one lane loads four
+// register windows once (the centre samples, the horizontal / vertical / diagonal neighbour
+// samples: 8 x 8, 9 x 8, 8 x 9, 9 x 9 pixels per 8 x 8 tile of the block, streamed in 4-row
+// bands) from its own planes -- the plane choice is a per-lane pointer, not a branch -- and
+// forms all nine predictions in registers: ~5 aligned loads per candidate against 24
+// unaligned ones when each candidate is fetched on its own (subpel_cmp_batch).  A quarter-pel
+// centre (odd cx or cy) takes the per-candidate path for its lane.
+template <int BD>
+__device__ __forceinline__ const typename PT<BD>::pixel *hpel_grid( const typename PT<BD>::pixel *p0,
+                                                                    const typename PT<BD>::pixel *p1,
+                                                                    const typename PT<BD>::pixel *p2,
+                                                                    const typename PT<BD>::pixel *p3, intptr_t rs,
+                                                                    int u, int v )
+{
+    const int pl = ((v & 1) << 1) | (u & 1);
+    const typename PT<BD>::pixel *b = pl == 0 ? p0 : pl == 1 ? p1 : pl == 2 ? p2 : p3;
+    return b + (intptr_t)(v >> 1) * rs + (u >> 1);
+}
+
+template <int BD, int OP, int IPIX>
+__global__ __launch_bounds__( 256 ) void subpel_qpel9_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                              intptr_t fs, const typename PT<BD>::pixel *p0,
+                                                              const typename PT<BD>::pixel *p1,
+                                                              const typename PT<BD>::pixel *p2,
+                                                              const typename PT<BD>::pixel *p3, intptr_t rs,
+                                                              const int64_t *__restrict__ fenc_off,
+                                                              const int32_t *__restrict__ cxy, int n,
+                                                              int32_t *__restrict__ scores )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int PPD = PT<BD>::PPD;
+    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    constexpr int N8 = 8 / PPD;                       // dwords of 8 pixels
+    constexpr int SH = BD == 8 ? 1 : 2;               // bytes of one pixel
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= n )
+        return;
+    const int2 c = *(const int2 *)(cxy + 2 * i);
+    const pixel *a = fenc + fenc_off[i];
+    int32_t *out = scores + (int64_t)9 * i;
+    if( (c.x | c.y) & 1 )
+    {
+        for( int k = 0; k < 9; k++ )
+            out[k] = subpel_score<BD, OP, IPIX, 1>( a, fs, p0, p1, p2, p3, rs, c.x + k % 3 - 1, c.y + k / 3 - 1 );
+        return;
+    }
+    const int hx = c.x >> 1, hy = c.y >> 1;
+    const bool ccxy = (c.x ^ c.y) & 2;
+    const pixel *gcc = hpel_grid<BD>( p0, p1, p2, p3, rs, hx, hy );
+    const pixel *gxc = hpel_grid<BD>( p0, p1, p2, p3, rs, hx - 1, hy );
+    const pixel *gcy = hpel_grid<BD>( p0, p1, p2, p3, rs, hx, hy - 1 );
+    const pixel *gxy = hpel_grid<BD>( p0, p1, p2, p3, rs, hx - 1, hy - 1 );
+    uint32_t acc[9];
+#pragma unroll
+    for( int k = 0; k < 9; k++ )
+        acc[k] = 0;
+#pragma unroll
+    for( int ty = 0; ty < H; ty += 4 )
+#pragma unroll
+        for( int tx = 0; tx < W; tx += 8 )
+        {
+            uint32_t f[4][N8], cc[4][N8], xc[4][N8 + 1], cy[5][N8], xy[5][N8 + 1];
+#pragma unroll
+            for( int y = 0; y < 4; y++ )
+            {
+                load_row_al<N8>( a + (ty + y) * fs + tx, f[y] );
+                load_row_al<N8>( gcc + (ty + y) * rs + tx, cc[y] );
+                load_row_al<N8 + 1>( gxc + (ty + y) * rs + tx, xc[y] );
+            }
+#pragma unroll
+            for( int y = 0; y < 5; y++ )
+            {
+                load_row_al<N8>( gcy + (ty + y) * rs + tx, cy[y] );
+                load_row_al<N8 + 1>( gxy + (ty + y) * rs + tx, xy[y] );
+            }
+#pragma unroll
+            for( int k = 0; k < 9; k++ )
+            {
+                const int dx = k % 3 - 1, dy = k / 3 - 1;
+                uint32_t pr[4][N8];
+#pragma unroll
+                for( int r = 0; r < 4; r++ )
+#pragma unroll
+                    for( int d = 0; d < N8; d++ )
+                    {
+                        const int ry = r + (dy > 0);
+                        const uint32_t cv = cc[r][d];
+                        const uint32_t xs = dx < 0 ? xc[r][d] : __builtin_amdgcn_alignbyte( xc[r][d + 1], xc[r][d], SH );
+                        const uint32_t ys = cy[ry][d];
+                        const uint32_t ds = dx < 0 ? xy[ry][d] : __builtin_amdgcn_alignbyte( xy[ry][d + 1], xy[ry][d], SH );
+                        uint32_t v;
+                        if( dx == 0 && dy == 0 )
+                            v = cv;
+                        else if( dy == 0 )
+                            v = avg_round<BD>( cv, xs );
+                        else if( dx == 0 )
+                            v = avg_round<BD>( cv, ys );
+                        else
+                            v = ccxy ? avg_round<BD>( cv, ds ) : avg_round<BD>( xs, ys );
+                        pr[r][d] = v;
+                    }
+                if constexpr( OP == 0 )
+                {
+#pragma unroll
+                    for( int r = 0; r < 4; r++ )
+#pragma unroll
+                        for( int d = 0; d < N8; d++ )
+                            acc[k] = sadp<BD>( f[r][d], pr[r][d], acc[k] );
+                }
+                else
+                    acc[k] += satd8x4_packed<BD>( f, pr );
+            }
+        }
+#pragma unroll
+    for( int k = 0; k < 9; k++ )
+        out[k] = OP == 0 ? (int)acc[k] : (int)(acc[k] >> 1);
+}
+
+template <int BD>
+hipError_t launch_subpel_qpel9( int op, int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs,
+                                const typename PT<BD>::pixel *const planes[4], intptr_t rs, const int64_t *fenc_off,
+                                const int32_t *cxy, int n, int32_t *scores, hipStream_t stream )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (n + 255) / 256 );
+#define Q9_CASE( OP, I )                                                                                       \
+    case I:                                                                                                    \
+        hipLaunchKernelGGL( ( subpel_qpel9_kernel<BD, OP, I> ), g, blk, 0, stream, fenc, fs, planes[0], planes[1], \
+                            planes[2], planes[3], rs, fenc_off, cxy, n, scores );                              \
+        break;
+    if( op == 0 )
+    {
+        switch( i_pixel ) { Q9_CASE( 0, 0 ) Q9_CASE( 0, 1 ) Q9_CASE( 0, 2 ) Q9_CASE( 0, 3 ) default: return hipErrorInvalidValue; }
+    }
+    else if( op == 2 )
+    {
+        switch( i_pixel ) { Q9_CASE( 2, 0 ) Q9_CASE( 2, 1 ) Q9_CASE( 2, 2 ) Q9_CASE( 2, 3 ) default: return hipErrorInvalidValue; }
+    }
+    else
+        return hipErrorInvalidValue;
+#undef Q9_CASE
+    return hipGetLastError();
 }
 
 template <int BD>
@@ -1139,6 +1303,9 @@ hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t
     template hipError_t launch_subpel_cmp<BD>( int, int, const PT<BD>::pixel *, intptr_t,                      \
                                                const PT<BD>::pixel *const[4], intptr_t, const int64_t *,       \
                                                const int32_t *, int, int32_t *, hipStream_t );      \
+    template hipError_t launch_subpel_qpel9<BD>( int, int, const PT<BD>::pixel *, intptr_t,                    \
+                                                 const PT<BD>::pixel *const[4], intptr_t, const int64_t *,     \
+                                                 const int32_t *, int, int32_t *, hipStream_t );               \
     template hipError_t launch_frame_init_lowres<BD>( const PT<BD>::pixel *, intptr_t, intptr_t, int, int, int,  \
                                                       PT<BD>::pixel *const[4], intptr_t, intptr_t, hipStream_t );
 INST( 8 )
