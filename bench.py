@@ -392,8 +392,75 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     if not torch.equal(lst, sc9):
         raise SystemExit("bench: subpel_qpel9_batch and subpel_cmp_batch disagree")
     del nb8, hv, ref_planes, fo, qxy, sc, bfo, cxy, sc9, lst
+    res.update(rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
     res.update(rates_2160p(x, a, world))
+    return res
+
+
+def tesa_params(mbw, mbh, F, R, centre=(-3, -2)):
+    """TESA search parameters of every MB of F frames: the window centred on a predictor
+    next to the synthetic motion, mv_limit_fpel-shaped limits (analyse.c:330-349), mvp =
+    the centre, no predictor cost to beat; an x264-shaped cost_mv table (lambda 4)."""
+    n1 = mbw * mbh
+    mb = np.arange(F * n1) % n1
+    mbx, mby = mb % mbw, mb // mbw
+    par = np.zeros((F * n1, 8), np.int16)
+    par[:, 0], par[:, 1] = centre
+    par[:, 2], par[:, 3] = 4 * centre[0], 4 * centre[1]
+    par[:, 4], par[:, 5] = -16 * mbx - 24, -16 * mby - 24
+    par[:, 6], par[:, 7] = 16 * (mbw - 1 - mbx) + 20, 16 * (mbh - 1 - mby) + 24
+    init = np.full(F * n1, 1 << 30, np.int32)
+    span = 16384
+    i = np.arange(-span, span + 1)
+    logs = np.where(i == 0, 0.718, 2.0 * np.log2(np.abs(i) + 1) + 1.718)
+    cm = np.minimum((4 * logs + 0.5).astype(np.int64), 65535).astype(np.uint16)
+    return par, init, cm, span
+
+
+def rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
+    """TESA (me.c:653-748, me_range 16, SATD fpelcmp) over the F 1080p pairs: the
+    self-contained form (ads-filtered SADs computed in the kernel) and the form reading
+    the headline kernel's full-search table; plus the integral image it needs."""
+    R = a.range
+    par, init, cm, span = tesa_params(mbw, mbh, F, R)
+    par_d, init_d = torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda()
+    cm_d = torch.from_numpy(cm.view(np.int16)).cuda()
+    H = mbh * 16
+    integ = x.frame_integral(dev[:-1], origin, stride, H)
+
+    def istep():
+        x.frame_integral(dev[:-1], origin, stride, H, out=integ)
+    wall, ev_ms = timed(istep, a.steps, a.warmup, world)
+    res = {"frame_integral_frames_per_s": world * a.steps * F / wall, "frame_integral_launch_ms": ev_ms}
+    out = torch.empty((F * mbw * mbh, 4), dtype=torch.int32, device="cuda")
+
+    def tstep():
+        x.me_tesa(dev[1:], origin, stride, dev[:-1], origin, stride, integ, mbw, mbh, F, R, par_d, init_d,
+                  (cm_d, span), out=out, fenc_frame_stride=fstride, ref_frame_stride=fstride)
+    wall, ev_ms = timed(tstep, a.steps, a.warmup, world)
+    res["tesa_mbs_per_s"] = world * a.steps * F * mbw * mbh / wall
+    res["tesa_launch_ms"] = ev_ms
+    res["tesa_mean_cost_mv_candidates"] = float(out[:, 3].float().mean().item())
+    # the search as an encoder would drive it on the GPU: the exhaustive SAD table around each
+    # MB's predictor (me_search_centred, the headline kernel) then the TESA scan reading it
+    table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
+    org = torch.empty((F * mbw * mbh, 2), dtype=torch.int16, device="cuda")
+    cen = par_d[:, :2].contiguous()
+    out2 = torch.empty_like(out)
+
+    def ttstep():
+        x.me_search_centred(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, cen, table=table,
+                            origin=org, fenc_frame_stride=fstride, ref_frame_stride=fstride)
+        x.me_tesa(dev[1:], origin, stride, dev[:-1], origin, stride, integ, mbw, mbh, F, R, par_d, init_d,
+                  (cm_d, span), table=table, rng=R, origin=org, out=out2, fenc_frame_stride=fstride,
+                  ref_frame_stride=fstride)
+    wall, ev_ms = timed(ttstep, a.steps, a.warmup, world)
+    res["tesa_centred_table_mbs_per_s"] = world * a.steps * F * mbw * mbh / wall
+    res["tesa_centred_table_step_ms"] = ev_ms
+    if not torch.equal(out, out2):
+        raise SystemExit("bench: me_tesa with and without the SAD table disagree")
+    del integ, table, out, out2
     return res
 
 

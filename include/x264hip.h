@@ -553,6 +553,27 @@ int x264hip_##BD##_me_esa_argmin_at( const sadt *table, int range, int n, int me
                                      const int32_t *init_cost, const uint16_t *cost_mv,         \
                                      int32_t *out, void *stream );                              \
                                                                                                 \
+/* TESA integer-pel search per 16x16 macroblock (reference encoder/me.c:653-748,              \
+ * X264_ME_TESA with i_pixel = PIXEL_16x16): ads4 with threshold bsad*17>>4 over the ESA      \
+ * integral image, the SAD threshold list (sad_thresh 10/11/12 by me_range), the halving      \
+ * prune to me_range/2 candidates and COST_MV over the survivors with fpelcmp = satd          \
+ * (satd != 0, mbcmp_init encoder.c:1411,1423-1424) or sad.  fenc / ref point at pixel (0,0) \
+ * of frame 0 (MB-aligned fenc rows: dword-aligned); integral = frame_integral's 8x8 sums,    \
+ * pixel (0,0) of frame 0, row stride = ref_stride (frame.c:273), frame stride                \
+ * integral_frame_stride.  par / init_cost / cost_mv as me_esa_argmin (per MB, frame-major    \
+ * raster).  table (optional, NULL = none): a me_search_full / me_search_centred table of     \
+ * the same pairs (origin NULL for me_search_full); SADs inside it are read, the rest are     \
+ * computed.  out[4*i] = { cost, mx, my, number of COST_MV candidates }.  me_range 1..32.     \
+ * The ESA window, the width-rounded columns and their integral sums must lie inside the      \
+ * padded planes (mv_limit_fpel keeps them there in the encoder). */                          \
+int x264hip_##BD##_me_tesa( const pixel *fenc, intptr_t fenc_stride, intptr_t fenc_frame_stride,  \
+                            const pixel *ref, intptr_t ref_stride, intptr_t ref_frame_stride,   \
+                            const uint16_t *integral, intptr_t integral_frame_stride,           \
+                            int mb_width, int mb_height, int n_frames, int me_range, int satd,  \
+                            const sadt *table, int range, const int16_t *origin,                \
+                            const int16_t *par, const int32_t *init_cost,                       \
+                            const uint16_t *cost_mv, int32_t *out, void *stream );              \
+                                                                                                \
 /* integer-pel ESA decision per macroblock over a me_search_full table (reference            \
  * encoder/me.c:618-631, the plain exhaustive form its ads path :632-771 reproduces):           \
  * par[8*i] = { bmx, bmy (fullpel centre = best predictor), mvp_x, mvp_y (qpel),                \

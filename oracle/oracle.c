@@ -1539,6 +1539,119 @@ void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const i
     }
 }
 
+/* TESA integer-pel search of x264_me_search_ref for PIXEL_16x16, restated from
+ * reference encoder/me.c:618-748 (X264_ME_TESA): enc_dc from sad_x4 against
+ * x264_zero (:643-645), per row the ycost skip, ads4 with threshold bsad*17>>4
+ * (:661-669, ads4 = pixel.c:759-803), the SAD threshold list with the running
+ * COPY1_IF_LT (:670-701; sad_x3 scores equal three sad calls), the halving prune
+ * (:705-734), the drop-the-first-maximum loop (:735-746) and COST_MV over the
+ * survivors (:747-748, me.c:63-70) with fpelcmp = satd when `satd` (mbcmp_init,
+ * encoder.c:1411,1423-1424) else sad.  fenc / ref / integral point at pixel (0,0)
+ * of one frame; the integral image (x264_frame_filter, mc.c:748-782) shares the
+ * ref stride rs (frame.c:273).  par / init_cost / cost_mv as me_esa_argmin.
+ * out[4*i] = { bcost, bmx, bmy, number of COST_MV evaluations }. */
+void FN(me_tesa)( const pixel *fenc, intptr_t fs, const pixel *ref, const uint16_t *integral, intptr_t rs,
+                  int mb_width, int mb_height, int me_range, int satd, const int16_t *par,
+                  const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out )
+{
+    static const pixel zero[16 * 16];
+    const int nmb = mb_width * mb_height;
+    int16_t *xs = malloc( (4 * me_range + 8) * sizeof(int16_t) );
+    uint16_t *fpel = malloc( (4 * me_range + 8) * sizeof(uint16_t) );
+    struct { int sad; int16_t mv[2]; } *mvsads = malloc( (size_t)(2 * me_range + 1) * (4 * me_range + 8) * 8 );
+    for( int i = 0; i < nmb; i++ )
+    {
+        const int mbx = i % mb_width, mby = i / mb_width;
+        const int16_t *p = par + 8 * i;
+        const pixel *p_fenc = fenc + 16 * (mby * fs + mbx);
+        const pixel *p_fref_w = ref + 16 * (mby * rs + mbx);
+        const uint16_t *sums_base = integral + 16 * (mby * rs + mbx);
+        const uint16_t *p_cost_mvx = cost_mv - p[2], *p_cost_mvy = cost_mv - p[3];
+        int bmx = p[0], bmy = p[1], bcost = init_cost[i], ncost = 0;
+        const int min_x = bmx - me_range > p[4] ? bmx - me_range : p[4];
+        const int min_y = bmy - me_range > p[5] ? bmy - me_range : p[5];
+        const int max_x = bmx + me_range < p[6] ? bmx + me_range : p[6];
+        const int max_y = bmy + me_range < p[7] ? bmy + me_range : p[7];
+        const int width = (max_x - min_x + 3) & ~3;
+        const int delta = 8 * rs;
+        int enc_dc[4];
+        for( int k = 0; k < 4; k++ )
+            enc_dc[k] = FN(sad)( 3 /* PIXEL_8x8 */, zero, 16, p_fenc + 8 * (k & 1) + 8 * (k >> 1) * fs, fs );
+        /* cost_fpel_mvx + min_x: cost_mv_fpel[qp][-mvp&3][(-mvp>>2) + x] = cost_mv[qp][4x - mvp]
+         * (analyse.c:161-169) */
+        for( int x = 0; x < width; x++ )
+            fpel[x] = p_cost_mvx[(min_x + x) * 4];
+        int nmvsad = 0, limit;
+        int sad_thresh = me_range <= 16 ? 10 : me_range <= 24 ? 11 : 12;
+        int bsad = FN(sad)( 0 /* PIXEL_16x16 */, p_fenc, fs, p_fref_w + bmy * rs + bmx, rs )
+                 + p_cost_mvx[bmx * 4] + p_cost_mvy[bmy * 4];
+        for( int my = min_y; my <= max_y; my++ )
+        {
+            int ycost = p_cost_mvy[my * 4];
+            if( bsad <= ycost )
+                continue;
+            bsad -= ycost;
+            int xn = FN(ads)( 4, enc_dc, sums_base + min_x + my * rs, delta, fpel, xs, width, bsad * 17 >> 4 );
+            for( int k = 0; k < xn; k++ )
+            {
+                int mx = min_x + xs[k];
+                int sad = FN(sad)( 0 /* PIXEL_16x16 */, p_fenc, fs, p_fref_w + mx + my * rs, rs ) + fpel[xs[k]];
+                if( sad < bsad * sad_thresh >> 3 )
+                {
+                    if( sad < bsad )
+                        bsad = sad;
+                    mvsads[nmvsad].sad = sad + ycost;
+                    mvsads[nmvsad].mv[0] = mx;
+                    mvsads[nmvsad].mv[1] = my;
+                    nmvsad++;
+                }
+            }
+            bsad += ycost;
+        }
+        limit = me_range >> 1;
+        sad_thresh = bsad * sad_thresh >> 3;
+        while( nmvsad > limit * 2 && sad_thresh > bsad )
+        {
+            sad_thresh = (sad_thresh + bsad) >> 1;
+            int k = 0;
+            for( int j = 0; j < nmvsad; j++ )
+                if( mvsads[j].sad <= sad_thresh )
+                    mvsads[k++] = mvsads[j];
+            nmvsad = k;
+        }
+        while( nmvsad > limit )
+        {
+            int bi = 0;
+            for( int k = 1; k < nmvsad; k++ )
+                if( mvsads[k].sad > mvsads[bi].sad )
+                    bi = k;
+            nmvsad--;
+            mvsads[bi] = mvsads[nmvsad];
+        }
+        for( int k = 0; k < nmvsad; k++ )
+        {
+            int mx = mvsads[k].mv[0], my = mvsads[k].mv[1];
+            const pixel *r = p_fref_w + my * rs + mx;
+            int cost = (satd ? FN(satd)( 0 /* PIXEL_16x16 */, p_fenc, fs, r, rs ) : FN(sad)( 0 /* PIXEL_16x16 */, p_fenc, fs, r, rs ))
+                     + p_cost_mvx[mx * 4] + p_cost_mvy[my * 4];
+            ncost++;
+            if( cost < bcost )
+            {
+                bcost = cost;
+                bmx = mx;
+                bmy = my;
+            }
+        }
+        out[4 * i] = bcost;
+        out[4 * i + 1] = bmx;
+        out[4 * i + 2] = bmy;
+        out[4 * i + 3] = ncost;
+    }
+    free( mvsads );
+    free( fpel );
+    free( xs );
+}
+
 /*============================================================================
  * lookahead input — reference common/mc.c:458-507, common/frame.c:535-631
  *==========================================================================*/

@@ -65,6 +65,7 @@ for _bd in (8, 10):
     _f(_bd, "hpel_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int, _P])
     _f(_bd, "get_ref", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int], _P)
     _f(_bd, "me_esa_argmin", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P])
+    _f(_bd, "me_tesa", [_P, _IP, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "me_search_centred", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
     _f(_bd, "subpel_list", [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P])
@@ -265,6 +266,19 @@ def me_esa_argmin(bd, table, rng, me_range, par, init_cost, cost_mv, c0, origin=
     o = None if origin is None else _addr(np.ascontiguousarray(origin, np.int16))
     getattr(_L, f"oracle{bd}_me_esa_argmin")(_addr(t), rng, len(p), me_range, o, _addr(p), _addr(ic),
                                             _addr(cost_mv, c0), _addr(out))
+    return out
+
+
+def me_tesa(bd, fenc, f_origin, fs, ref, r_origin, integral, i_origin, rs, mbw, mbh, me_range, satd, par,
+            init_cost, cost_mv, c0):
+    """TESA decision of one frame (oracle me_tesa, me.c:653-748): int32 [nmb, 4] =
+    (cost, mx, my, COST_MV evaluations).  integral: uint16 array with (0,0) at i_origin, stride rs."""
+    p = np.ascontiguousarray(par, np.int16)
+    ic = np.ascontiguousarray(init_cost, np.int32)
+    out = np.zeros((len(p), 4), np.int32)
+    getattr(_L, f"oracle{bd}_me_tesa")(_addr(fenc, f_origin), fs, _addr(ref, r_origin), _addr(integral, i_origin), rs,
+                                      mbw, mbh, me_range, int(bool(satd)), _addr(p), _addr(ic), _addr(cost_mv, c0),
+                                      _addr(out))
     return out
 
 

@@ -23,7 +23,7 @@ import os
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref",
@@ -297,6 +297,9 @@ def _declare(L):
         f("me_search_centred").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                            _P, _P, _P, _P]
         f("me_esa_argmin_at").restype = _c.c_int
+        f("me_tesa").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _P, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                 _c.c_int, _P, _c.c_int, _P, _P, _P, _P, _P, _P]
+        f("me_tesa").restype = _c.c_int
         f("me_search_centred").restype = _c.c_int
         f("hpel_filter").argtypes = [_P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P]
         f("subpel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, _c.c_int, _P, _P]
@@ -904,3 +907,29 @@ def me_search_centred(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_strid
         _ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs, mb_width, mb_height,
         nframes, rng, _ptr(centre), _ptr(table), _ptr(origin), _stream()), "me_search_centred")
     return table, origin
+
+
+def me_tesa(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, integral, mb_width, mb_height, nframes,
+            me_range, par, init_cost, cost_mv_center, satd=True, table=None, rng=0, origin=None, out=None,
+            fenc_frame_stride=None, ref_frame_stride=None, integral_origin=None):
+    """TESA integer-pel decision per 16x16 MB (x264hip_*_me_tesa, reference encoder/me.c:653-748).
+
+    integral: frame_integral() output [n, rows, ref_stride] (its (0,0) at integral_origin, default
+    PAD*stride+PAD); par int16 [n_mbs, 8], init_cost int32 [n_mbs], cost_mv_center as me_esa_argmin;
+    table / rng / origin: an optional me_search_full / me_search_centred table of the same pairs.
+    Returns int32 [n_mbs, 4] = (cost, mx, my, number of COST_MV candidates)."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = par.shape[0]
+    if out is None:
+        out = torch.empty((n, 4), dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)
+    io = integral_origin if integral_origin is not None else PAD * ref_stride + PAD
+    cm, c0 = cost_mv_center
+    _rc(getattr(lib(), f"x264hip_{bd}_me_tesa")(
+        _ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs, _ptr(integral, io),
+        integral[0].numel() if integral.dim() == 3 else 0, mb_width, mb_height, nframes, me_range, int(bool(satd)),
+        _ptr(table) if table is not None else None, rng, _ptr(origin) if origin is not None else None, _ptr(par),
+        _ptr(init_cost), _ptr(cm, c0), _ptr(out), _stream()), "me_tesa")
+    return out

@@ -1246,6 +1246,21 @@ extern "C" const char *x264hip_backend_banner( void )
         return map_err( launch_me_esa_argmin<BD>( table, range, n, me_range, origin, par, init_cost, cost_mv, out,   \
                                                   (hipStream_t)stream ), "me_esa_argmin_at" );                       \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_tesa( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,                    \
+                                           const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs,                      \
+                                           const uint16_t *integral, intptr_t ifs, int mbw, int mbh, int nframes,    \
+                                           int me_range, int satd, const PT<BD>::sadt *table, int range,             \
+                                           const int16_t *origin, const int16_t *par, const int32_t *init_cost,      \
+                                           const uint16_t *cost_mv, int32_t *out, void *stream )                     \
+    {                                                                                                                \
+        if( mbw < 0 || mbh < 0 || nframes < 0 || me_range < 1 || me_range > 32 || !fenc || !ref || !integral ||      \
+            !par || !init_cost || !cost_mv || !out || ((uintptr_t)fenc & 3) || ((fs * sizeof( PT<BD>::pixel )) & 3) || \
+            (table && (range < 1 || range > 29)) )                                                                   \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_me_tesa<BD>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nframes, me_range, \
+                                            satd, table, range, origin, par, init_cost, cost_mv, out,               \
+                                            (hipStream_t)stream ), "me_tesa" );                                      \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_hpel_filter( const PT<BD>::pixel *src, PT<BD>::pixel *dh, PT<BD>::pixel *dv,       \
                                                PT<BD>::pixel *dc, intptr_t stride, intptr_t fstride, int width,     \
                                                int height, int nframes, void *stream )                              \

@@ -581,4 +581,333 @@ template hipError_t launch_me_esa_argmin<8>( const uint16_t *, int, int, int, co
 template hipError_t launch_me_esa_argmin<10>( const uint32_t *, int, int, int, const int16_t *, const int16_t *,
                                               const int32_t *, const uint16_t *, int32_t *, hipStream_t );
 
+// ---------------------------------------------------------------------------
+// TESA (reference encoder/me.c:653-748) for PIXEL_16x16: one wave per macroblock.
+//
+// The reference walks the window row by row.  Within a row its running bsad only
+// ever drops to a SAD that was appended, and every SAD below bsad is appended
+// (the threshold bsad*sad_thresh>>3 >= bsad), so the bsad a candidate is tested
+// against is min(row-start bsad, prefix minimum of the earlier ADS survivors'
+// SADs).  A row is therefore one lane per column (width <= 64): ads4 and its
+// bsad*17>>4 threshold per lane, the 16x16 SAD on the surviving lanes only, a
+// wave prefix-min, and a ballot + mbcnt append into the LDS mvsads list in
+// column order -- the reference's exact list.  Rows stay sequential (a row's ADS
+// threshold depends on every earlier row).  The halving prune is an in-order
+// LDS compaction, the drop-the-first-maximum loop a wave argmax, and the final
+// COST_MV scores the <= me_range/2 survivors as 8x4 units spread over the lanes
+// (satd_16x16 = the sum of eight satd_8x4, pixel.c:265-306), reduced with the
+// strict-< first-index rule of COPY3_IF_LT.
+template <int BD>
+__device__ __forceinline__ uint32_t tesa_sad16( const uint32_t *fenc_lds, const typename PT<BD>::pixel *r,
+                                                intptr_t rs )
+{
+    constexpr int NDW = 16 / PT<BD>::PPD;
+    uint32_t acc = 0;
+#pragma unroll 4
+    for( int y = 0; y < 16; y++ )
+    {
+        uint32_t w[NDW];
+        load_row_u<NDW>( r + y * rs, w );
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            acc = sadp<BD>( fenc_lds[y * NDW + k], w[k], acc );
+    }
+    return acc;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
+{
+#pragma unroll
+    for( int off = 32; off >= 1; off >>= 1 )
+        v = min( v, (uint32_t)__shfl_xor( (int)v, off ) );
+    return v;
+}
+
+template <int BD, int NR>
+__global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
+                                                        intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
+                                                        intptr_t rs, intptr_t rfs,
+                                                        const uint16_t *__restrict__ integral, intptr_t ifs, int mbw,
+                                                        int mbh, int me_range, int satd,
+                                                        const typename PT<BD>::sadt *__restrict__ table, int R,
+                                                        const int16_t *__restrict__ origin,
+                                                        const int16_t *__restrict__ par,
+                                                        const int32_t *__restrict__ init_cost,
+                                                        const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int NDW = 16 / PT<BD>::PPD;                     // dwords per fenc row
+    extern __shared__ uint64_t mvsads[];                      // { sad, mx | my << 16 }
+    __shared__ uint32_t fl[16 * NDW];
+    const int lane = threadIdx.x;
+    const int64_t mb = blockIdx.x;
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+    const pixel *p_fenc = fenc + f * ffs + 16 * (mby * fs + mbx);
+    const pixel *p_fref = ref + f * rfs + 16 * (mby * rs + mbx);
+    const uint16_t *sums_base = integral + f * ifs + 16 * (mby * rs + mbx);
+    const int16_t *p = par + 8 * mb;
+    const int bmx0 = p[0], bmy0 = p[1];
+    const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
+    const int min_x = max( bmx0 - me_range, (int)p[4] ), min_y = max( bmy0 - me_range, (int)p[5] );
+    const int max_x = min( bmx0 + me_range, (int)p[6] ), max_y = min( bmy0 + me_range, (int)p[7] );
+    const int width = (max_x - min_x + 3) & ~3;
+
+    // fenc -> LDS (row-major dwords) and enc_dc (sad_x4 against x264_zero = the four 8x8 sums)
+    uint32_t dcq[4] = { 0, 0, 0, 0 };
+    for( int i = lane; i < 16 * NDW; i += 64 )
+    {
+        const int y = i / NDW, k = i % NDW;
+        const uint32_t w = *(const uint32_t *)(p_fenc + y * fs + k * PT<BD>::PPD);
+        fl[i] = w;
+        const uint32_t s = sadp<BD>( w, 0u, 0u );
+        const int q = (k * PT<BD>::PPD >= 8) + 2 * (y >= 8);
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+            dcq[j] += q == j ? s : 0u;
+    }
+    int enc_dc[4];
+#pragma unroll
+    for( int j = 0; j < 4; j++ )
+    {
+        uint32_t v = dcq[j];
+#pragma unroll
+        for( int off = 32; off >= 1; off >>= 1 )
+            v += (uint32_t)__shfl_xor( (int)v, off );
+        enc_dc[j] = (int)v;
+    }
+    __syncthreads();
+
+    const int W = 2 * R + 1, P = (W + 3) & ~3;
+    const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
+    const typename PT<BD>::sadt *tab = table ? table + mb * (int64_t)(W * P) : nullptr;
+    auto sad_at = [&]( int mx, int my ) -> uint32_t {
+        const int tx = mx - ox, ty = my - oy;
+        if( tab && tx >= 0 && tx < W && ty >= 0 && ty < W )
+            return (uint32_t)tab[ty * P + tx];
+        return tesa_sad16<BD>( fl, p_fref + my * rs + mx, rs );
+    };
+
+    const int sad_thresh0 = me_range <= 16 ? 10 : me_range <= 24 ? 11 : 12;
+    const bool active = lane < width;
+    const int mx = min_x + lane;
+    const int fpel = active ? (int)cx[mx * 4] : 0;           // cost_fpel_mvx[mx] (analyse.c:161-169)
+    const int bsad0 = (int)sad_at( bmx0, bmy0 ) + (int)cx[bmx0 * 4] + (int)cy[bmy0 * 4];
+    const int rows = max( max_y - min_y + 1, 0 );            // <= 2*me_range+1 <= 65
+    const int delta = 8 * (int)rs;
+    // ycost of row r in lane r (rows 64.. in the second register)
+    const int yc0 = lane < rows ? (int)cy[(min_y + lane) * 4] : 0;
+    const int yc1 = lane + 64 < rows ? (int)cy[(min_y + lane + 64) * 4] : 0;
+
+    // Phase 1 (independent of the scan state, so every load is in flight at once): each
+    // row's ads4 value, and the cost of every candidate that can still pass some row's
+    // threshold -- bsad never rises, so row r's ADS threshold is at most
+    // (bsad0 - ycost)*17>>4.  Both live in registers (NR rows, compile-time indexed).
+    uint32_t adsv[NR], sv[NR];
+#pragma unroll
+    for( int r = 0; r < NR; r++ )
+    {
+        adsv[r] = 0xFFFFFFFFu;
+        if( r < rows && active )
+        {
+            const uint16_t *sp = sums_base + mx + (intptr_t)(min_y + r) * rs;
+            adsv[r] = (uint32_t)(abs( enc_dc[0] - (int)sp[0] ) + abs( enc_dc[1] - (int)sp[8] ) +
+                                 abs( enc_dc[2] - (int)sp[delta] ) + abs( enc_dc[3] - (int)sp[delta + 8] ) + fpel);
+        }
+    }
+#pragma unroll
+    for( int r = 0; r < NR; r++ )
+    {
+        sv[r] = 0xFFFFFFFFu;
+        if( r < rows )
+        {
+            const int ycost = __builtin_amdgcn_readlane( r < 64 ? yc0 : yc1, r & 63 );
+            const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
+            if( adsv[r] < (uint32_t)ub )
+                sv[r] = sad_at( mx, min_y + r ) + (uint32_t)fpel;
+        }
+    }
+
+    // Phase 2: the reference's row scan over the staged values
+    int bsad = bsad0;
+    int nmvsad = 0;
+#pragma unroll
+    for( int r = 0; r < NR; r++ )
+    {
+        const int my = min_y + r;
+        const int ycost = __builtin_amdgcn_readlane( r < 64 ? yc0 : yc1, r & 63 );
+        if( r >= rows || bsad <= ycost )
+            continue;
+        const int b = bsad - ycost;
+        const bool pass = adsv[r] < (uint32_t)(b * 17 >> 4);
+        if( !__ballot( pass ) )
+            continue;                                       // bsad unchanged
+        // a passing lane's cost was staged: b <= bsad0 - ycost
+        const uint32_t s = pass ? sv[r] : 0xFFFFFFFFu;
+        // exclusive prefix minimum over the lanes (the earlier survivors of this row)
+        uint32_t incl = s;
+#pragma unroll
+        for( int off = 1; off < 64; off <<= 1 )
+        {
+            const uint32_t o = (uint32_t)__shfl_up( (int)incl, off );
+            incl = lane >= off ? min( incl, o ) : incl;
+        }
+        uint32_t excl = (uint32_t)__shfl_up( (int)incl, 1 );
+        excl = lane ? excl : 0xFFFFFFFFu;
+        const int bcur = (int)min( (uint32_t)b, excl );
+        const bool app = pass && (int)s < (bcur * sad_thresh0 >> 3);
+        const uint64_t m = __ballot( app );
+        if( app )
+        {
+            const int pos = nmvsad + (int)__builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32),
+                                                                    __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) );
+            mvsads[pos] = (uint64_t)(s + (uint32_t)ycost) | ((uint64_t)(uint16_t)mx << 32) |
+                          ((uint64_t)(uint16_t)my << 48);
+        }
+        nmvsad += __popcll( m );
+        const uint32_t rmin = __shfl( (int)incl, 63 );
+        bsad = min( bsad, (int)rmin + ycost );                // b_final + ycost
+    }
+
+    // keep the best few (me.c:705-746)
+    const int limit = me_range >> 1;
+    int thr = bsad * sad_thresh0 >> 3;
+    while( nmvsad > limit * 2 && thr > bsad )
+    {
+        thr = (thr + bsad) >> 1;
+        int k = 0;
+        for( int base = 0; base < nmvsad; base += 64 )
+        {
+            const int j = base + lane;
+            const uint64_t e = j < nmvsad ? mvsads[j] : 0;
+            const bool keep = j < nmvsad && (int)(uint32_t)e <= thr;
+            const uint64_t m = __ballot( keep );
+            if( keep )
+                mvsads[k + (int)__builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) )] = e;
+            k += __popcll( m );
+        }
+        nmvsad = k;
+    }
+    while( nmvsad > limit )
+    {
+        // first index of the largest sad: max of (sad << 32 | ~index)
+        uint64_t key = 0;
+        for( int j = lane; j < nmvsad; j += 64 )
+        {
+            const uint64_t k = ((uint64_t)(uint32_t)mvsads[j] << 32) | (uint32_t)~j;
+            key = k > key ? k : key;
+        }
+#pragma unroll
+        for( int off = 32; off >= 1; off >>= 1 )
+        {
+            const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor( (int)(key >> 32), off ) << 32) |
+                               (uint32_t)__shfl_xor( (int)(uint32_t)key, off );
+            key = o > key ? o : key;
+        }
+        const int bi = (int)~(uint32_t)key;
+        nmvsad--;
+        if( lane == 0 )
+            mvsads[bi] = mvsads[nmvsad];
+        __syncthreads();
+    }
+
+    // COST_MV over the survivors in list order: eight 8x4 units per candidate
+    uint32_t best = 0xFFFFFFFFu;
+    for( int u0 = 0; u0 < nmvsad * 8; u0 += 64 )
+    {
+        const int u = u0 + lane, k = u >> 3, part = u & 7;
+        uint32_t v = 0;
+        int cmx = 0, cmy = 0;
+        if( k < nmvsad )
+        {
+            const uint64_t e = mvsads[k];
+            cmx = (int16_t)(e >> 32);
+            cmy = (int16_t)(e >> 48);
+            const int bx = 8 * (part & 1), by = 4 * (part >> 1);
+            constexpr int HDW = 8 / PT<BD>::PPD;
+            uint32_t a[4][HDW], rr[4][HDW];
+            const pixel *r = p_fref + (intptr_t)(cmy + by) * rs + cmx + bx;
+#pragma unroll
+            for( int y = 0; y < 4; y++ )
+            {
+                load_row_u<HDW>( r + y * rs, rr[y] );
+#pragma unroll
+                for( int j = 0; j < HDW; j++ )
+                    a[y][j] = fl[(by + y) * NDW + bx / PT<BD>::PPD + j];
+            }
+            if( satd )
+                v = satd8x4_packed<BD>( a, rr ) >> 1;
+            else
+            {
+#pragma unroll
+                for( int y = 0; y < 4; y++ )
+#pragma unroll
+                    for( int j = 0; j < HDW; j++ )
+                        v = sadp<BD>( a[y][j], rr[y][j], v );
+            }
+        }
+        v += (uint32_t)__shfl_xor( (int)v, 1 );
+        v += (uint32_t)__shfl_xor( (int)v, 2 );
+        v += (uint32_t)__shfl_xor( (int)v, 4 );
+        if( k < nmvsad && part == 0 )
+        {
+            const uint32_t cost = v + cx[cmx * 4] + cy[cmy * 4];
+            best = min( best, (cost << 6) | (uint32_t)k );   // k < 64: first index on ties
+        }
+    }
+    best = wave_min_u32( best );
+    if( lane == 0 )
+    {
+        int32_t bcost = init_cost[mb], rx = bmx0, ry = bmy0;
+        if( best != 0xFFFFFFFFu && (int32_t)(best >> 6) < bcost )
+        {
+            const uint64_t e = mvsads[best & 63];
+            bcost = (int32_t)(best >> 6);
+            rx = (int16_t)(e >> 32);
+            ry = (int16_t)(e >> 48);
+        }
+        out[4 * mb] = bcost;
+        out[4 * mb + 1] = rx;
+        out[4 * mb + 2] = ry;
+        out[4 * mb + 3] = nmvsad;
+    }
+}
+
+template <int BD>
+hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                           const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, const uint16_t *integral,
+                           intptr_t ifs, int mbw, int mbh, int nframes, int me_range, int satd,
+                           const typename PT<BD>::sadt *table, int R, const int16_t *origin, const int16_t *par,
+                           const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out, hipStream_t stream )
+{
+    const int64_t nmb = (int64_t)nframes * mbw * mbh;
+    if( nmb <= 0 )
+        return hipSuccess;
+    if( me_range < 1 || me_range > 32 || nmb > 0x7fffffff )
+        return hipErrorInvalidValue;
+    // the mvsads list: at most (2*me_range+1) rows x (2*me_range+3)&~3 columns
+    const size_t lds = (size_t)(2 * me_range + 1) * ((2 * me_range + 3) & ~3) * sizeof( uint64_t );
+    if( me_range <= 16 )
+        hipLaunchKernelGGL( ( me_tesa_kernel<BD, 33> ), dim3( (unsigned)nmb ), dim3( 64 ), lds, stream, fenc, fs, ffs,
+                            ref, rs, rfs, integral, ifs, mbw, mbh, me_range, satd, table, R, origin, par, init_cost,
+                            cost_mv, out );
+    else
+        hipLaunchKernelGGL( ( me_tesa_kernel<BD, 65> ), dim3( (unsigned)nmb ), dim3( 64 ), lds, stream, fenc, fs, ffs,
+                            ref, rs, rfs, integral, ifs, mbw, mbh, me_range, satd, table, R, origin, par, init_cost,
+                            cost_mv, out );
+    return hipGetLastError();
+}
+
+template hipError_t launch_me_tesa<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t,
+                                       const uint16_t *, intptr_t, int, int, int, int, int, const uint16_t *, int,
+                                       const int16_t *, const int16_t *, const int32_t *, const uint16_t *, int32_t *,
+                                       hipStream_t );
+template hipError_t launch_me_tesa<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
+                                        const uint16_t *, intptr_t, int, int, int, int, int, const uint32_t *, int,
+                                        const int16_t *, const int16_t *, const int32_t *, const uint16_t *,
+                                        int32_t *, hipStream_t );
+
 } // namespace x264hip
