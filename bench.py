@@ -393,6 +393,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
         raise SystemExit("bench: subpel_qpel9_batch and subpel_cmp_batch disagree")
     del nb8, hv, ref_planes, fo, qxy, sc, bfo, cxy, sc9, lst
     res.update(rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
+    res.update(rates_ssd(x, a, world, dev, origin, stride, F))
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
     res.update(rates_2160p(x, a, world))
     return res
@@ -462,6 +463,18 @@ def rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
         raise SystemExit("bench: me_tesa with and without the SAD table disagree")
     del integ, table, out, out2
     return res
+
+
+def rates_ssd(x, a, world, dev, origin, stride, F):
+    """plane SSD (x264_pixel_ssd_wxh, the per-frame PSNR sum of encoder.c:2499) over the F
+    1080p pairs: frames/s and the fraction of HBM (two w x h planes read)."""
+    out = torch.empty(F, dtype=torch.int64, device="cuda")
+
+    def step():
+        x.ssd_plane_batch(dev[1:], origin, stride, dev[:-1], origin, stride, a.width, a.height, F, out=out)
+    wall, ev_ms = timed(step, a.steps, a.warmup, world)
+    return {"ssd_plane_frames_per_s": world * a.steps * F / wall, "ssd_plane_launch_ms": ev_ms,
+            "ssd_plane_hbm_frac": F * 2 * a.width * a.height / (ev_ms * 1e-3) / HBM_PEAK}
 
 
 def rates_10bit(x, a, world, mbw, mbh, F):

@@ -553,6 +553,23 @@ int x264hip_##BD##_me_esa_argmin_at( const sadt *table, int range, int n, int me
                                      const int32_t *init_cost, const uint16_t *cost_mv,         \
                                      int32_t *out, void *stream );                              \
                                                                                                 \
+/* plane SSD of n_frames (pix1, pix2) pairs: ssd[f] = x264_pixel_ssd_wxh( pf, pix1 + f*f1,       \
+ * s1, pix2 + f*f2, s2, width, height ) (reference common/pixel.c:112-151, the per-frame       \
+ * PSNR sum of encoder.c:2499).  uint64 results, device pointers; strides in pixels. */        \
+int x264hip_##BD##_ssd_plane_batch( const pixel *pix1, intptr_t stride1, intptr_t frame_stride1, \
+                                    const pixel *pix2, intptr_t stride2, intptr_t frame_stride2, \
+                                    int width, int height, int n_frames, uint64_t *ssd,         \
+                                    void *stream );                                             \
+                                                                                                \
+/* interleaved-chroma SSD: ssd_uv[2*f], ssd_uv[2*f+1] = the ssd_u, ssd_v of                    \
+ * x264_pixel_ssd_nv12( pf, pix1 + f*f1, s1, pix2 + f*f2, s2, width, height, .. )             \
+ * (reference common/pixel.c:153-178, including its tail over width&7 pairs that starts at     \
+ * pixel offset width&~7); width = chroma samples per plane row. */                           \
+int x264hip_##BD##_ssd_nv12_batch( const pixel *pix1, intptr_t stride1, intptr_t frame_stride1, \
+                                   const pixel *pix2, intptr_t stride2, intptr_t frame_stride2, \
+                                   int width, int height, int n_frames, uint64_t *ssd_uv,      \
+                                   void *stream );                                              \
+                                                                                                \
 /* TESA integer-pel search per 16x16 macroblock (reference encoder/me.c:653-748,              \
  * X264_ME_TESA with i_pixel = PIXEL_16x16): ads4 with threshold bsad*17>>4 over the ESA      \
  * integral image, the SAD threshold list (sad_thresh 10/11/12 by me_range), the halving      \

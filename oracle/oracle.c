@@ -85,6 +85,74 @@ int FN(ssd)( int i_pixel, const pixel *pix1, intptr_t s1, const pixel *pix2, int
     return sum;
 }
 
+/* x264_pixel_ssd_wxh, reference common/pixel.c:112-151: 16x16 tiles when both
+ * pointers and strides are 16-aligned, else 8x16, one 8x8 row band, then the
+ * per-pixel right and bottom tails */
+uint64_t FN(ssd_wxh)( const pixel *pix1, intptr_t i_pix1, const pixel *pix2, intptr_t i_pix2, int i_width,
+                      int i_height )
+{
+    uint64_t i_ssd = 0;
+    int y;
+    int align = !(((intptr_t)pix1 | (intptr_t)pix2 | i_pix1 | i_pix2) & 15);
+    for( y = 0; y < i_height - 15; y += 16 )
+    {
+        int x = 0;
+        if( align )
+            for( ; x < i_width - 15; x += 16 )
+                i_ssd += FN(ssd)( 0, pix1 + y * i_pix1 + x, i_pix1, pix2 + y * i_pix2 + x, i_pix2 );
+        for( ; x < i_width - 7; x += 8 )
+            i_ssd += FN(ssd)( 2, pix1 + y * i_pix1 + x, i_pix1, pix2 + y * i_pix2 + x, i_pix2 );
+    }
+    if( y < i_height - 7 )
+        for( int x = 0; x < i_width - 7; x += 8 )
+            i_ssd += FN(ssd)( 3, pix1 + y * i_pix1 + x, i_pix1, pix2 + y * i_pix2 + x, i_pix2 );
+    if( i_width & 7 )
+        for( y = 0; y < (i_height & ~7); y++ )
+            for( int x = i_width & ~7; x < i_width; x++ )
+            {
+                int d = pix1[y * i_pix1 + x] - pix2[y * i_pix2 + x];
+                i_ssd += d * d;
+            }
+    if( i_height & 7 )
+        for( y = i_height & ~7; y < i_height; y++ )
+            for( int x = 0; x < i_width; x++ )
+            {
+                int d = pix1[y * i_pix1 + x] - pix2[y * i_pix2 + x];
+                i_ssd += d * d;
+            }
+    return i_ssd;
+}
+
+/* pixel_ssd_nv12_core + x264_pixel_ssd_nv12, reference common/pixel.c:153-178 (the
+ * tail starts at pixel offset i_width&~7 of the interleaved row, as written there) */
+static void ssd_nv12_core( const pixel *pixuv1, intptr_t stride1, const pixel *pixuv2, intptr_t stride2, int width,
+                           int height, uint64_t *ssd_u, uint64_t *ssd_v )
+{
+    *ssd_u = 0, *ssd_v = 0;
+    for( int y = 0; y < height; y++, pixuv1 += stride1, pixuv2 += stride2 )
+        for( int x = 0; x < width; x++ )
+        {
+            int du = pixuv1[2*x] - pixuv2[2*x];
+            int dv = pixuv1[2*x+1] - pixuv2[2*x+1];
+            *ssd_u += du * du;
+            *ssd_v += dv * dv;
+        }
+}
+
+void FN(ssd_nv12)( const pixel *pix1, intptr_t i_pix1, const pixel *pix2, intptr_t i_pix2, int i_width,
+                   int i_height, uint64_t *ssd_u, uint64_t *ssd_v )
+{
+    ssd_nv12_core( pix1, i_pix1, pix2, i_pix2, i_width & ~7, i_height, ssd_u, ssd_v );
+    if( i_width & 7 )
+    {
+        uint64_t tmp[2];
+        ssd_nv12_core( pix1 + (i_width & ~7), i_pix1, pix2 + (i_width & ~7), i_pix2, i_width & 7, i_height,
+                       &tmp[0], &tmp[1] );
+        *ssd_u += tmp[0];
+        *ssd_v += tmp[1];
+    }
+}
+
 /* HADAMARD4 and the packed two-lane abs, reference common/pixel.c:242-259 */
 #define HADAMARD4( d0, d1, d2, d3, s0, s1, s2, s3 ) {\
     sum2_t t0 = s0 + s1, t1 = s0 - s1, t2 = s2 + s3, t3 = s2 - s3;\

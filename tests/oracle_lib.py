@@ -65,6 +65,8 @@ for _bd in (8, 10):
     _f(_bd, "hpel_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int, _P])
     _f(_bd, "get_ref", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int], _P)
     _f(_bd, "me_esa_argmin", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P])
+    _f(_bd, "ssd_wxh", [_P, _IP, _P, _IP, C.c_int, C.c_int], C.c_uint64)
+    _f(_bd, "ssd_nv12", [_P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P])
     _f(_bd, "me_tesa", [_P, _IP, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "me_search_centred", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
@@ -267,6 +269,19 @@ def me_esa_argmin(bd, table, rng, me_range, par, init_cost, cost_mv, c0, origin=
     getattr(_L, f"oracle{bd}_me_esa_argmin")(_addr(t), rng, len(p), me_range, o, _addr(p), _addr(ic),
                                             _addr(cost_mv, c0), _addr(out))
     return out
+
+
+def ssd_wxh(bd, a, a_off, sa, b, b_off, sb, w, h):
+    """x264_pixel_ssd_wxh over a w x h rectangle (pixel.c:112-151)."""
+    return int(getattr(_L, f"oracle{bd}_ssd_wxh")(_addr(a, a_off), sa, _addr(b, b_off), sb, w, h))
+
+
+def ssd_nv12(bd, a, a_off, sa, b, b_off, sb, w, h):
+    """x264_pixel_ssd_nv12 (pixel.c:153-178): (ssd_u, ssd_v)."""
+    u = np.zeros(1, np.uint64)
+    v = np.zeros(1, np.uint64)
+    getattr(_L, f"oracle{bd}_ssd_nv12")(_addr(a, a_off), sa, _addr(b, b_off), sb, w, h, _addr(u), _addr(v))
+    return int(u[0]), int(v[0])
 
 
 def me_tesa(bd, fenc, f_origin, fs, ref, r_origin, integral, i_origin, rs, mbw, mbh, me_range, satd, par,

@@ -23,7 +23,7 @@ import os
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref",
@@ -300,6 +300,9 @@ def _declare(L):
         f("me_tesa").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _P, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                  _c.c_int, _P, _c.c_int, _P, _P, _P, _P, _P, _P]
         f("me_tesa").restype = _c.c_int
+        for n in ("ssd_plane_batch", "ssd_nv12_batch"):
+            f(n).argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P, _P]
+            f(n).restype = _c.c_int
         f("me_search_centred").restype = _c.c_int
         f("hpel_filter").argtypes = [_P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P]
         f("subpel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, _c.c_int, _P, _P]
@@ -933,3 +936,33 @@ def me_tesa(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, integra
         _ptr(table) if table is not None else None, rng, _ptr(origin) if origin is not None else None, _ptr(par),
         _ptr(init_cost), _ptr(cm, c0), _ptr(out), _stream()), "me_tesa")
     return out
+
+
+def _plane_ssd(name, nv12, pix1, origin1, stride1, pix2, origin2, stride2, width, height, nframes, out,
+               frame_stride1, frame_stride2):
+    import torch
+    bd = _pix_bd(pix1)
+    if out is None:
+        out = torch.empty((nframes, 2) if nv12 else (nframes,), dtype=torch.int64, device=pix1.device)
+    f1 = frame_stride1 if frame_stride1 is not None else (pix1[0].numel() if pix1.dim() == 3 else 0)
+    f2 = frame_stride2 if frame_stride2 is not None else (pix2[0].numel() if pix2.dim() == 3 else 0)
+    _rc(getattr(lib(), f"x264hip_{bd}_{name}")(
+        _ptr(pix1, origin1), stride1, f1, _ptr(pix2, origin2), stride2, f2, width, height, nframes, _ptr(out),
+        _stream()), name)
+    return out
+
+
+def ssd_plane_batch(pix1, origin1, stride1, pix2, origin2, stride2, width, height, nframes, out=None,
+                    frame_stride1=None, frame_stride2=None):
+    """x264_pixel_ssd_wxh per frame pair (x264hip_*_ssd_plane_batch, pixel.c:112-151): int64 [n]
+    (uint64 values)."""
+    return _plane_ssd("ssd_plane_batch", False, pix1, origin1, stride1, pix2, origin2, stride2, width, height,
+                      nframes, out, frame_stride1, frame_stride2)
+
+
+def ssd_nv12_batch(pix1, origin1, stride1, pix2, origin2, stride2, width, height, nframes, out=None,
+                   frame_stride1=None, frame_stride2=None):
+    """x264_pixel_ssd_nv12 per frame pair (x264hip_*_ssd_nv12_batch, pixel.c:153-178): int64 [n, 2] =
+    (ssd_u, ssd_v); width = chroma samples per row."""
+    return _plane_ssd("ssd_nv12_batch", True, pix1, origin1, stride1, pix2, origin2, stride2, width, height,
+                      nframes, out, frame_stride1, frame_stride2)

@@ -1246,6 +1246,24 @@ extern "C" const char *x264hip_backend_banner( void )
         return map_err( launch_me_esa_argmin<BD>( table, range, n, me_range, origin, par, init_cost, cost_mv, out,   \
                                                   (hipStream_t)stream ), "me_esa_argmin_at" );                       \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_ssd_plane_batch( const PT<BD>::pixel *pix1, intptr_t s1, intptr_t f1,             \
+                                                   const PT<BD>::pixel *pix2, intptr_t s2, intptr_t f2, int width,   \
+                                                   int height, int nframes, uint64_t *ssd, void *stream )            \
+    {                                                                                                                \
+        if( width < 0 || height < 0 || nframes < 0 || (nframes && (!pix1 || !pix2 || !ssd)) )                       \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_plane_ssd<BD>( 0, pix1, s1, f1, pix2, s2, f2, width, height, nframes, ssd,            \
+                                              (hipStream_t)stream ), "ssd_plane_batch" );                            \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_ssd_nv12_batch( const PT<BD>::pixel *pix1, intptr_t s1, intptr_t f1,              \
+                                                  const PT<BD>::pixel *pix2, intptr_t s2, intptr_t f2, int width,    \
+                                                  int height, int nframes, uint64_t *ssd_uv, void *stream )          \
+    {                                                                                                                \
+        if( width < 0 || height < 0 || nframes < 0 || (nframes && (!pix1 || !pix2 || !ssd_uv)) )                    \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_plane_ssd<BD>( 1, pix1, s1, f1, pix2, s2, f2, width, height, nframes, ssd_uv,         \
+                                              (hipStream_t)stream ), "ssd_nv12_batch" );                             \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_me_tesa( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,                    \
                                            const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs,                      \
                                            const uint16_t *integral, intptr_t ifs, int mbw, int mbh, int nframes,    \

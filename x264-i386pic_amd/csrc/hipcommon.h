@@ -252,6 +252,10 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
                            const typename PT<BD>::sadt *table, int R, const int16_t *origin, const int16_t *par,
                            const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out, hipStream_t stream );
 template <int BD>
+hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_t s1, intptr_t f1,
+                             const typename PT<BD>::pixel *p2, intptr_t s2, intptr_t f2, int width, int height,
+                             int nframes, uint64_t *out, hipStream_t stream );
+template <int BD>
 hipError_t launch_stat_batch( int op, int i_pixel, const typename PT<BD>::pixel *p1, intptr_t s1,
                               const typename PT<BD>::pixel *p2, intptr_t s2, const int64_t *off1,
                               const int64_t *off2, int height, int n, uint64_t *out, hipStream_t stream );

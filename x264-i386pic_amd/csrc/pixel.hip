@@ -648,3 +648,145 @@ INST( 10 )
 #undef INST
 
 } // namespace x264hip
+
+namespace x264hip {
+
+// ---------------------------------------------------------------------------
+// Plane SSD: x264_pixel_ssd_wxh (reference common/pixel.c:112-151) and
+// x264_pixel_ssd_nv12 (:153-178).  ssd_wxh tiles the plane into 16x16 / 8x16 / 8x8
+// ssd calls plus per-pixel tails; every tile sum is an exact int (<= 256 * 1023^2)
+// and the tiles and tails cover each pixel of the w x h rectangle once, so the
+// uint64 result is the plain sum of d^2 over the rectangle -- what this reduction
+// computes, in any order.  ssd_nv12 runs the core over the first w&~7 (u, v) pairs
+// of each interleaved row and then the tail over w&7 pairs starting at PIXEL
+// offset w&~7 (not pair offset: the tail re-reads pixels of the core, as the
+// reference does); both are segments [c0, c1) of pixel columns with even columns
+// counted as u and odd as v.  One lane per 16-byte chunk of a row (coalesced
+// rows), d^2 pairs by v_dot2_i32_i16 on packed differences, a wave reduction and
+// one 64-bit atomic add per wave.
+template <int BD, bool NV12>
+__global__ __launch_bounds__( 256 ) void plane_ssd_kernel( const typename PT<BD>::pixel *__restrict__ p1, intptr_t s1,
+                                                           intptr_t f1, const typename PT<BD>::pixel *__restrict__ p2,
+                                                           intptr_t s2, intptr_t f2, int c0, int c1, int height,
+                                                           unsigned long long *__restrict__ out )
+{
+    constexpr int CH = 16 / (int)sizeof( typename PT<BD>::pixel );   // pixels per chunk
+    const int f = blockIdx.y;
+    const int nch = (c1 - c0 + CH - 1) / CH;
+    const int64_t items = (int64_t)nch * height;
+    const typename PT<BD>::pixel *a0 = p1 + f * f1, *b0 = p2 + f * f2;
+    uint64_t su = 0, sv = 0;
+    for( int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < items; i += (int64_t)gridDim.x * blockDim.x )
+    {
+        const int y = (int)(i / nch), x = c0 + (int)(i % nch) * CH;
+        const typename PT<BD>::pixel *a = a0 + y * s1 + x, *b = b0 + y * s2 + x;
+        uint32_t iu = 0, iv = 0;
+        if( x + CH <= c1 )
+        {
+            uint32_t wa[4], wb[4];
+            load_row_u<4>( a, wa );
+            load_row_u<4>( b, wb );
+#pragma unroll
+            for( int k = 0; k < 4; k++ )
+            {
+                if constexpr( BD == 8 )
+                {
+                    // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) as 16-bit pairs
+                    const x264hip_short2 ea = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wa[k], 0x0c020c00u ) );
+                    const x264hip_short2 eb = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wb[k], 0x0c020c00u ) );
+                    const x264hip_short2 oa = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wa[k], 0x0c030c01u ) );
+                    const x264hip_short2 ob = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wb[k], 0x0c030c01u ) );
+                    const x264hip_short2 de = ea - eb, dd = oa - ob;
+                    iu = (uint32_t)__builtin_amdgcn_sdot2( de, de, (int)iu, false );
+                    if( NV12 )
+                        iv = (uint32_t)__builtin_amdgcn_sdot2( dd, dd, (int)iv, false );
+                    else
+                        iu = (uint32_t)__builtin_amdgcn_sdot2( dd, dd, (int)iu, false );
+                }
+                else
+                {
+                    const x264hip_short2 d = __builtin_bit_cast( x264hip_short2, wa[k] ) -
+                                             __builtin_bit_cast( x264hip_short2, wb[k] );
+                    if( NV12 )
+                    {
+                        iu += (uint32_t)((int)d.x * d.x);
+                        iv += (uint32_t)((int)d.y * d.y);
+                    }
+                    else
+                        iu = (uint32_t)__builtin_amdgcn_sdot2( d, d, (int)iu, false );
+                }
+            }
+        }
+        else
+        {
+            for( int k = 0; x + k < c1; k++ )
+            {
+                const int d = (int)a[k] - (int)b[k];
+                if( NV12 && ((x + k) & 1) )
+                    iv += (uint32_t)(d * d);
+                else
+                    iu += (uint32_t)(d * d);
+            }
+        }
+        su += iu;
+        sv += iv;
+    }
+#pragma unroll
+    for( int off = 32; off >= 1; off >>= 1 )
+    {
+        su += (uint64_t)__shfl_xor( (unsigned long long)su, off );
+        if( NV12 )
+            sv += (uint64_t)__shfl_xor( (unsigned long long)sv, off );
+    }
+    if( (threadIdx.x & 63) == 0 )
+    {
+        if( su )
+            atomicAdd( out + (NV12 ? 2 * f : f), (unsigned long long)su );
+        if( NV12 && sv )
+            atomicAdd( out + 2 * f + 1, (unsigned long long)sv );
+    }
+}
+
+template <int BD>
+hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_t s1, intptr_t f1,
+                             const typename PT<BD>::pixel *p2, intptr_t s2, intptr_t f2, int width, int height,
+                             int nframes, uint64_t *out, hipStream_t stream )
+{
+    if( nframes <= 0 )
+        return hipSuccess;
+    hipError_t e = hipMemsetAsync( out, 0, (size_t)nframes * (nv12 ? 2 : 1) * sizeof( uint64_t ), stream );
+    if( e != hipSuccess || width <= 0 || height <= 0 )
+        return e;
+    constexpr int CH = 16 / (int)sizeof( typename PT<BD>::pixel );
+    auto go = [&]( int c0, int c1 ) {
+        const int64_t items = (int64_t)((c1 - c0 + CH - 1) / CH) * height;
+        // ~8 chunks per lane: enough bytes in flight per wave, few atomics per frame
+        int64_t nb = (items + 2047) / 2048;
+        nb = nb < 1 ? 1 : nb > 65535 ? 65535 : nb;
+        const unsigned gx = (unsigned)nb;
+        dim3 g( gx, (unsigned)nframes ), blk( 256 );
+        unsigned long long *o = (unsigned long long *)out;
+        if( nv12 )
+            hipLaunchKernelGGL( ( plane_ssd_kernel<BD, true> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0, c1, height, o );
+        else
+            hipLaunchKernelGGL( ( plane_ssd_kernel<BD, false> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0, c1, height, o );
+    };
+    if( !nv12 )
+        go( 0, width );
+    else
+    {
+        const int w8 = width & ~7, w7 = width & 7;
+        if( w8 )
+            go( 0, 2 * w8 );
+        if( w7 )
+            go( w8, w8 + 2 * w7 );
+    }
+    return hipGetLastError();
+}
+
+template hipError_t launch_plane_ssd<8>( int, const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t,
+                                         int, int, int, uint64_t *, hipStream_t );
+template hipError_t launch_plane_ssd<10>( int, const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t,
+                                          intptr_t, int, int, int, uint64_t *, hipStream_t );
+
+} // namespace x264hip
