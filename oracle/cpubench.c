@@ -15,6 +15,10 @@ void oracle8_mb_dct_quant( int transform, const uint8_t *fenc, intptr_t fs, cons
                            int mb_width, int mb_height, const uint16_t *mf, const uint16_t *bias,
                            int16_t *dct, int32_t *nz );
 
+void oracle8_subpel_list( int op, int i_pixel, const uint8_t *fenc, intptr_t fs, const uint8_t *p0,
+                          const uint8_t *p1, const uint8_t *p2, const uint8_t *p3, intptr_t rs,
+                          const int64_t *fenc_off, const int32_t *qxy, int n, int32_t *scores );
+
 typedef struct
 {
     const uint8_t *fenc, *ref;
@@ -88,4 +92,52 @@ int oracle8_mb_dct_quant_mt( int transform, const uint8_t *fenc, intptr_t fs, co
 {
     job_t b = { fenc, pred, fs, ps, mb_width, 0, 0, 0, transform, mf, bias, NULL, dct, nz };
     return run( dq_worker, b, mb_height, nthreads );
+}
+
+typedef struct
+{
+    int op, i_pixel, n;
+    const uint8_t *fenc, *p[4];
+    intptr_t fs, rs;
+    const int64_t *fenc_off;
+    const int32_t *qxy;
+    int32_t *scores;
+} sp_job_t;
+
+static void *sp_worker( void *arg )
+{
+    sp_job_t *j = arg;
+    oracle8_subpel_list( j->op, j->i_pixel, j->fenc, j->fs, j->p[0], j->p[1], j->p[2], j->p[3], j->rs,
+                         j->fenc_off, j->qxy, j->n, j->scores );
+    return NULL;
+}
+
+/* qpel candidate list (get_ref + sad/satd), 8-bit, split into nthreads contiguous
+ * slices; returns threads used */
+int oracle8_subpel_list_mt( int op, int i_pixel, const uint8_t *fenc, intptr_t fs, const uint8_t *p0,
+                            const uint8_t *p1, const uint8_t *p2, const uint8_t *p3, intptr_t rs,
+                            const int64_t *fenc_off, const int32_t *qxy, int n, int32_t *scores, int nthreads )
+{
+    pthread_t th[256];
+    sp_job_t jobs[256];
+    if( nthreads < 1 )
+        nthreads = 1;
+    if( nthreads > 256 )
+        nthreads = 256;
+    if( nthreads > n )
+        nthreads = n > 0 ? n : 1;
+    int i0 = 0;
+    for( int t = 0; t < nthreads; t++ )
+    {
+        int cnt = n / nthreads + (t < n % nthreads);
+        sp_job_t j = { op, i_pixel, cnt, fenc, { p0, p1, p2, p3 }, fs, rs, fenc_off + i0, qxy + 2 * i0,
+                       scores + i0 };
+        jobs[t] = j;
+        i0 += cnt;
+        if( pthread_create( &th[t], NULL, sp_worker, &jobs[t] ) )
+            return -1;
+    }
+    for( int t = 0; t < nthreads; t++ )
+        pthread_join( th[t], NULL );
+    return nthreads;
 }

@@ -117,6 +117,8 @@ _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
 _L.oracle8_mb_dct_quant_mt.restype = C.c_int
+_L.oracle8_subpel_list_mt.argtypes = [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P, C.c_int]
+_L.oracle8_subpel_list_mt.restype = C.c_int
 
 _OPS = {"sad": 0, "ssd": 1, "satd": 2}
 
@@ -256,6 +258,16 @@ def subpel_list(bd, op, i_pixel, fenc, fs, planes, p_origin, rs, fenc_off, qxy):
                                           *[_addr(p, p_origin) for p in planes], rs, _addr(fo), _addr(q),
                                           len(fo), _addr(out))
     return out
+
+
+def subpel_list_mt(op, i_pixel, fenc, fs, planes, p_origin, rs, fenc_off, qxy, nthreads):
+    """8-bit subpel_list split over nthreads (cpubench.c); returns (scores, threads used)."""
+    fo = np.ascontiguousarray(fenc_off, np.int64)
+    q = np.ascontiguousarray(qxy, np.int32)
+    out = np.zeros(len(fo), np.int32)
+    used = _L.oracle8_subpel_list_mt(_OPS.get(op, op), i_pixel, _addr(fenc), fs, *[_addr(p, p_origin) for p in planes],
+                                     rs, _addr(fo), _addr(q), len(fo), _addr(out), nthreads)
+    return out, used
 
 
 def me_esa_argmin(bd, table, rng, me_range, par, init_cost, cost_mv, c0, origin=None):
