@@ -665,72 +665,86 @@ namespace x264hip {
 // rows), d^2 pairs by v_dot2_i32_i16 on packed differences, a wave reduction and
 // one 64-bit atomic add per wave.
 template <int BD, bool NV12>
+__device__ __forceinline__ void ssd_chunk( uint4 a4, uint4 b4, uint32_t &iu, uint32_t &iv )
+{
+    const uint32_t wa[4] = { a4.x, a4.y, a4.z, a4.w }, wb[4] = { b4.x, b4.y, b4.z, b4.w };
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+    {
+        if constexpr( BD == 8 )
+        {
+            // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) as 16-bit pairs
+            const x264hip_short2 ea = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wa[k], 0x0c020c00u ) );
+            const x264hip_short2 eb = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wb[k], 0x0c020c00u ) );
+            const x264hip_short2 oa = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wa[k], 0x0c030c01u ) );
+            const x264hip_short2 ob = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wb[k], 0x0c030c01u ) );
+            const x264hip_short2 de = ea - eb, dd = oa - ob;
+            iu = (uint32_t)__builtin_amdgcn_sdot2( de, de, (int)iu, false );
+            if( NV12 )
+                iv = (uint32_t)__builtin_amdgcn_sdot2( dd, dd, (int)iv, false );
+            else
+                iu = (uint32_t)__builtin_amdgcn_sdot2( dd, dd, (int)iu, false );
+        }
+        else
+        {
+            const x264hip_short2 d = __builtin_bit_cast( x264hip_short2, wa[k] ) -
+                                     __builtin_bit_cast( x264hip_short2, wb[k] );
+            if( NV12 )
+            {
+                iu += (uint32_t)((int)d.x * d.x);
+                iv += (uint32_t)((int)d.y * d.y);
+            }
+            else
+                iu = (uint32_t)__builtin_amdgcn_sdot2( d, d, (int)iu, false );
+        }
+    }
+}
+
+// grid: x = 64-chunk column groups, y = bands of 4 x SSD_ROWS rows (one wave per
+// SSD_ROWS rows), z = frame.  A lane loads its chunk of all SSD_ROWS rows of both
+// planes before any arithmetic (32 independent 16-byte loads in flight); the four
+// waves' sums meet in LDS and each workgroup adds once per output.
+constexpr int SSD_ROWS = 16;
+template <int BD, bool NV12>
 __global__ __launch_bounds__( 256 ) void plane_ssd_kernel( const typename PT<BD>::pixel *__restrict__ p1, intptr_t s1,
                                                            intptr_t f1, const typename PT<BD>::pixel *__restrict__ p2,
                                                            intptr_t s2, intptr_t f2, int c0, int c1, int height,
                                                            unsigned long long *__restrict__ out )
 {
     constexpr int CH = 16 / (int)sizeof( typename PT<BD>::pixel );   // pixels per chunk
-    const int f = blockIdx.y;
-    const int nch = (c1 - c0 + CH - 1) / CH;
-    const int64_t items = (int64_t)nch * height;
-    const typename PT<BD>::pixel *a0 = p1 + f * f1, *b0 = p2 + f * f2;
-    uint64_t su = 0, sv = 0;
-    for( int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < items; i += (int64_t)gridDim.x * blockDim.x )
+    __shared__ uint64_t part[2][4];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int f = blockIdx.z;
+    const int x = c0 + ((int)blockIdx.x * 64 + lane) * CH;
+    const int y0 = ((int)blockIdx.y * 4 + wv) * SSD_ROWS;
+    const typename PT<BD>::pixel *a = p1 + f * f1 + (intptr_t)y0 * s1 + x, *b = p2 + f * f2 + (intptr_t)y0 * s2 + x;
+    uint32_t iu = 0, iv = 0;
+    if( x + CH <= c1 && y0 + SSD_ROWS <= height )
     {
-        const int y = (int)(i / nch), x = c0 + (int)(i % nch) * CH;
-        const typename PT<BD>::pixel *a = a0 + y * s1 + x, *b = b0 + y * s2 + x;
-        uint32_t iu = 0, iv = 0;
-        if( x + CH <= c1 )
-        {
-            uint32_t wa[4], wb[4];
-            load_row_u<4>( a, wa );
-            load_row_u<4>( b, wb );
+        uint4 va[SSD_ROWS], vb[SSD_ROWS];
 #pragma unroll
-            for( int k = 0; k < 4; k++ )
-            {
-                if constexpr( BD == 8 )
-                {
-                    // even pixels (bytes 0, 2) and odd pixels (bytes 1, 3) as 16-bit pairs
-                    const x264hip_short2 ea = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wa[k], 0x0c020c00u ) );
-                    const x264hip_short2 eb = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wb[k], 0x0c020c00u ) );
-                    const x264hip_short2 oa = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wa[k], 0x0c030c01u ) );
-                    const x264hip_short2 ob = __builtin_bit_cast( x264hip_short2, __builtin_amdgcn_perm( 0u, wb[k], 0x0c030c01u ) );
-                    const x264hip_short2 de = ea - eb, dd = oa - ob;
-                    iu = (uint32_t)__builtin_amdgcn_sdot2( de, de, (int)iu, false );
-                    if( NV12 )
-                        iv = (uint32_t)__builtin_amdgcn_sdot2( dd, dd, (int)iv, false );
-                    else
-                        iu = (uint32_t)__builtin_amdgcn_sdot2( dd, dd, (int)iu, false );
-                }
-                else
-                {
-                    const x264hip_short2 d = __builtin_bit_cast( x264hip_short2, wa[k] ) -
-                                             __builtin_bit_cast( x264hip_short2, wb[k] );
-                    if( NV12 )
-                    {
-                        iu += (uint32_t)((int)d.x * d.x);
-                        iv += (uint32_t)((int)d.y * d.y);
-                    }
-                    else
-                        iu = (uint32_t)__builtin_amdgcn_sdot2( d, d, (int)iu, false );
-                }
-            }
-        }
-        else
+        for( int r = 0; r < SSD_ROWS; r++ )
         {
-            for( int k = 0; x + k < c1; k++ )
+            __builtin_memcpy( &va[r], a + r * s1, 16 );
+            __builtin_memcpy( &vb[r], b + r * s2, 16 );
+        }
+#pragma unroll
+        for( int r = 0; r < SSD_ROWS; r++ )
+            ssd_chunk<BD, NV12>( va[r], vb[r], iu, iv );   // <= 16 rows x 16 x 65025 (8 bit) / 8 x 1046529: u32
+    }
+    else if( x < c1 )
+    {
+        for( int r = 0; r < SSD_ROWS && y0 + r < height; r++ )
+            for( int k = 0; k < CH && x + k < c1; k++ )
             {
-                const int d = (int)a[k] - (int)b[k];
+                const int d = (int)a[r * s1 + k] - (int)b[r * s2 + k];
                 if( NV12 && ((x + k) & 1) )
                     iv += (uint32_t)(d * d);
                 else
                     iu += (uint32_t)(d * d);
             }
-        }
-        su += iu;
-        sv += iv;
     }
+    uint64_t su = iu, sv = iv;
 #pragma unroll
     for( int off = 32; off >= 1; off >>= 1 )
     {
@@ -738,12 +752,23 @@ __global__ __launch_bounds__( 256 ) void plane_ssd_kernel( const typename PT<BD>
         if( NV12 )
             sv += (uint64_t)__shfl_xor( (unsigned long long)sv, off );
     }
-    if( (threadIdx.x & 63) == 0 )
+    if( lane == 0 )
     {
+        part[0][wv] = su;
+        part[1][wv] = sv;
+    }
+    __syncthreads();
+    if( threadIdx.x == 0 )
+    {
+        su = part[0][0] + part[0][1] + part[0][2] + part[0][3];
         if( su )
             atomicAdd( out + (NV12 ? 2 * f : f), (unsigned long long)su );
-        if( NV12 && sv )
-            atomicAdd( out + 2 * f + 1, (unsigned long long)sv );
+        if( NV12 )
+        {
+            sv = part[1][0] + part[1][1] + part[1][2] + part[1][3];
+            if( sv )
+                atomicAdd( out + 2 * f + 1, (unsigned long long)sv );
+        }
     }
 }
 
@@ -757,14 +782,13 @@ hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_
     hipError_t e = hipMemsetAsync( out, 0, (size_t)nframes * (nv12 ? 2 : 1) * sizeof( uint64_t ), stream );
     if( e != hipSuccess || width <= 0 || height <= 0 )
         return e;
+    if( nframes > 65535 )
+        return hipErrorInvalidValue;
     constexpr int CH = 16 / (int)sizeof( typename PT<BD>::pixel );
     auto go = [&]( int c0, int c1 ) {
-        const int64_t items = (int64_t)((c1 - c0 + CH - 1) / CH) * height;
-        // ~8 chunks per lane: enough bytes in flight per wave, few atomics per frame
-        int64_t nb = (items + 2047) / 2048;
-        nb = nb < 1 ? 1 : nb > 65535 ? 65535 : nb;
-        const unsigned gx = (unsigned)nb;
-        dim3 g( gx, (unsigned)nframes ), blk( 256 );
+        const int nch = (c1 - c0 + CH - 1) / CH;
+        dim3 g( (unsigned)((nch + 63) / 64), (unsigned)((height + 4 * SSD_ROWS - 1) / (4 * SSD_ROWS)),
+                (unsigned)nframes ), blk( 256 );
         unsigned long long *o = (unsigned long long *)out;
         if( nv12 )
             hipLaunchKernelGGL( ( plane_ssd_kernel<BD, true> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0, c1, height, o );
