@@ -1,0 +1,85 @@
+// HBM probe for the half-pel filter's access pattern (no arithmetic): every lane
+// reads one 16-byte piece per source row and writes it to three output planes,
+// over the same padded 1080p plane geometry and frame count as the hpel bench
+// leg.  Variants: 1 = the streaming kernel's grid (a wave per 62-piece column
+// chunk x ROWS-row strip), 2 = a plain grid-stride copy of the same bytes
+// (1 plane in, 3 out), 3 = a plain 1-in-1-out copy of one plane (reference).
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+template <int ROWS>
+__global__ __launch_bounds__( 64 ) void strip3( const uint8_t *src, uint8_t *a, uint8_t *b, uint8_t *c, long stride,
+                                                long fstride, int pieces, int rows_total )
+{
+    const int lane = threadIdx.x;
+    const int q = blockIdx.x * 64 + lane;
+    if( q >= pieces )
+        return;
+    const int r0 = blockIdx.y * ROWS;
+    const long fo = (long)blockIdx.z * fstride + 16 * q;
+    for( int r = r0; r < r0 + ROWS && r < rows_total; r++ )
+    {
+        const uint4 v = *(const uint4 *)(src + fo + r * stride);
+        *(uint4 *)(a + fo + r * stride) = v;
+        *(uint4 *)(b + fo + r * stride) = v;
+        *(uint4 *)(c + fo + r * stride) = v;
+    }
+}
+
+__global__ void flat3( const uint4 *src, uint4 *a, uint4 *b, uint4 *c, long n )
+{
+    for( long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x )
+    {
+        const uint4 v = src[i];
+        a[i] = v;
+        b[i] = v;
+        c[i] = v;
+    }
+}
+
+__global__ void flat1( const uint4 *src, uint4 *a, long n )
+{
+    for( long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x )
+        a[i] = src[i];
+}
+
+int main( int argc, char **argv )
+{
+    const int F = argc > 1 ? atoi( argv[1] ) : 16;
+    const long stride = 1984, rows = 1152, fstride = stride * rows;
+    const long bytes = F * fstride;
+    uint8_t *s, *a, *b, *c;
+    hipMalloc( &s, bytes ); hipMalloc( &a, bytes ); hipMalloc( &b, bytes ); hipMalloc( &c, bytes );
+    hipMemset( s, 1, bytes );
+    hipEvent_t e0, e1;
+    hipEventCreate( &e0 ); hipEventCreate( &e1 );
+    const int pieces = (int)(stride / 16);
+    for( int v = 1; v <= 3; v++ )
+    {
+        auto run = [&]() {
+            if( v == 1 )
+                hipLaunchKernelGGL( strip3<12>, dim3( (pieces + 63) / 64, (rows + 11) / 12, F ), dim3( 64 ), 0, 0, s, a,
+                                    b, c, stride, fstride, pieces, (int)rows );
+            else if( v == 2 )
+                hipLaunchKernelGGL( flat3, dim3( 4096 ), dim3( 256 ), 0, 0, (const uint4 *)s, (uint4 *)a, (uint4 *)b,
+                                    (uint4 *)c, bytes / 16 );
+            else
+                hipLaunchKernelGGL( flat1, dim3( 4096 ), dim3( 256 ), 0, 0, (const uint4 *)s, (uint4 *)a, bytes / 16 );
+        };
+        for( int i = 0; i < 300; i++ )
+            run();
+        hipEventRecord( e0 );
+        for( int i = 0; i < 100; i++ )
+            run();
+        hipEventRecord( e1 );
+        hipEventSynchronize( e1 );
+        float ms;
+        hipEventElapsedTime( &ms, e0, e1 );
+        ms /= 100;
+        const double moved = v == 3 ? 2.0 * bytes : 4.0 * bytes;
+        printf( "variant %d: %.4f ms, %.2f TB/s, %.3f of 8 TB/s\n", v, ms, moved / ms / 1e9, moved / ms / 1e9 / 8.0 );
+    }
+    return 0;
+}

@@ -314,7 +314,7 @@ template <int HI, int BY> __device__ __forceinline__ uint32_t pack_clip4( const 
 }
 
 template <int HS_ROWS>
-__global__ __launch_bounds__( 256 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
+__global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
                                                              uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
                                                              intptr_t stride, intptr_t fstride, int width,
                                                              int height, int hbias, int cbias )
@@ -327,8 +327,14 @@ __global__ __launch_bounds__( 256 ) void hpel_stream_kernel( const uint8_t *__re
     const int q = chunk * 62 - 1 + lane;
     const bool st = lane >= 1 && lane <= 62 && q < nq;
     const int x0 = -16 + 16 * min( max( q, -1 ), nq );       // halo lanes load clamped columns
-    const int r0 = -8 + (int)blockIdx.y * HS_ROWS;
-    const int r1 = min( r0 + HS_ROWS, height + 8 );
+    // strips 0 .. nstrips-1 cover rows [-8, H+8); the last four replicate row -8 into
+    // rows -32..-9 / row H+7 into H+8..H+31, 12 rows each, so no wave stores more
+    // rows than a strip does (a wave storing all 25 border rows was the launch's tail)
+    const int nstrips = (int)gridDim.y - 4;
+    const int sy = (int)blockIdx.y - nstrips;               // >= 0: border strip
+    const int r0 = sy < 0 ? -8 + (int)blockIdx.y * HS_ROWS : sy < 2 ? -8 : height + 7;
+    const int r1 = sy < 0 ? min( r0 + HS_ROWS, height + 8 ) : r0 + 1;
+    const int b0 = sy < 0 ? 0 : sy < 2 ? -32 + 12 * sy : height + 8 + 12 * (sy - 2);
     const intptr_t fo = (intptr_t)blockIdx.z * fstride + x0;
     const uint8_t *sp = src + fo;
     auto ld = [&]( int row ) { return *(const uint4 *)(sp + (intptr_t)row * stride); };
@@ -359,28 +365,26 @@ __global__ __launch_bounds__( 256 ) void hpel_stream_kernel( const uint8_t *__re
         raw[k] = ld( r0 + 3 + k );
     for( int cy = r0; cy < r1; cy += 6 )
     {
-        uint4 cur[6];
-#pragma unroll
-        for( int k = 0; k < 6; k++ )
-        {
-            cur[k] = raw[k];
-            raw[k] = ld( cy + 9 + k );                       // rows of the next block (<= H + 16 + 8)
-        }
 #pragma unroll
         for( int k = 0; k < 6; k++ )
         {
             const int y = cy + k;
             if( y >= r1 )
                 break;                                       // wave-uniform
-            unpack( cur[k], win[(k + 5) % 6] );              // source row y + 3
+            // source row y + 3 arrived; its slot now fetches row y + 9 (six rows of lead)
+            uint4 cur[6];
+            cur[k] = raw[k];
+            raw[k] = ld( y + 9 );
             // vertical 6-tap intermediates at columns x-2 .. x+19 (int16, exact at 8 bit)
-            hs2 vi[11];
+            hs2 vi[11], hrow[11];
+            unpack( cur[k], win[(k + 5) % 6] );              // source row y + 3
 #pragma unroll
             for( int p = 0; p < 11; p++ )
             {
                 const hs2 a = win[k % 6][p], b = win[(k + 1) % 6][p], c = win[(k + 2) % 6][p];
                 const hs2 d = win[(k + 3) % 6][p], e = win[(k + 4) % 6][p], f = win[(k + 5) % 6][p];
                 vi[p] = (a + f) + (c + d) * (hs2)20 - (b + e) * (hs2)5;
+                hrow[p] = c;
             }
             uint32_t oh[4], ov[4], oc[4];
 #pragma unroll
@@ -395,10 +399,10 @@ __global__ __launch_bounds__( 256 ) void hpel_stream_kernel( const uint8_t *__re
             // H: clip( (t + 16) >> 5 ) computed as clamp( 8t + 128, 0, 0xffff ), byte 1;
             // centre: clip( (t + 512) >> 10 ) as clamp( 64t + 32768, 0, 0xffffff ), byte 2
             int o[4];
-            tap6_h4<0, 8>( win[(k + 2) % 6], hbias, o ); oh[0] = pack_clip4<0xffff, 1>( o );
-            tap6_h4<2, 8>( win[(k + 2) % 6], hbias, o ); oh[1] = pack_clip4<0xffff, 1>( o );
-            tap6_h4<4, 8>( win[(k + 2) % 6], hbias, o ); oh[2] = pack_clip4<0xffff, 1>( o );
-            tap6_h4<6, 8>( win[(k + 2) % 6], hbias, o ); oh[3] = pack_clip4<0xffff, 1>( o );
+            tap6_h4<0, 8>( hrow, hbias, o ); oh[0] = pack_clip4<0xffff, 1>( o );
+            tap6_h4<2, 8>( hrow, hbias, o ); oh[1] = pack_clip4<0xffff, 1>( o );
+            tap6_h4<4, 8>( hrow, hbias, o ); oh[2] = pack_clip4<0xffff, 1>( o );
+            tap6_h4<6, 8>( hrow, hbias, o ); oh[3] = pack_clip4<0xffff, 1>( o );
             tap6_h4<0, 64>( vi, cbias, o ); oc[0] = pack_clip4<0xffffff, 2>( o );
             tap6_h4<2, 64>( vi, cbias, o ); oc[1] = pack_clip4<0xffffff, 2>( o );
             tap6_h4<4, 64>( vi, cbias, o ); oc[2] = pack_clip4<0xffffff, 2>( o );
@@ -429,7 +433,7 @@ __global__ __launch_bounds__( 256 ) void hpel_stream_kernel( const uint8_t *__re
                 const uint4 ev = ox < 0 ? make_uint4( ov[0], ov[0], ov[0], ov[0] ) : make_uint4( ov[3], ov[3], ov[3], ov[3] );
                 const uint4 ec = ox < 0 ? make_uint4( oc[0], oc[0], oc[0], oc[0] ) : make_uint4( oc[3], oc[3], oc[3], oc[3] );
                 // rows: y, or the replicated border rows -32..-8 / H+7..H+31
-                const int ya = y == -8 ? -32 : y, yb = y == height + 7 ? height + 31 : y;
+                const int ya = sy < 0 ? y : b0, yb = sy < 0 ? y : b0 + 11;
                 for( int yy = ya; yy <= yb; yy++ )
                 {
                     const intptr_t o0 = fo + (intptr_t)yy * stride;
@@ -471,17 +475,17 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
             // (16 frames: 0.0455 -> 0.0398 ms; 64 frames: 0.166 -> 0.158 ms; 16 rows in
             // between).  X264HIP_HPEL_ROWS = 16 / 24 selects the taller strips.
             const int er = variant( V_HPEL_ROWS );
-            const int rows = er == 16 || er == 24 ? er : 12;
-            dim3 g( nchunk, (height + 16 + rows - 1) / rows, nframes );
-            if( rows == 24 )
-                hipLaunchKernelGGL( hpel_stream_kernel<24>, g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,
-                                    width, height, 8 * 16, 64 * 512 );
-            else if( rows == 16 )
-                hipLaunchKernelGGL( hpel_stream_kernel<16>, g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,
-                                    width, height, 8 * 16, 64 * 512 );
-            else
-                hipLaunchKernelGGL( hpel_stream_kernel<12>, g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,
-                                    width, height, 8 * 16, 64 * 512 );
+            const int rows = er == 6 || er == 8 || er == 16 || er == 24 ? er : 12;
+            dim3 g( nchunk, (height + 16 + rows - 1) / rows + 4, nframes );
+#define HS_GO( ROWS )                                                                                              \
+    hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,  \
+                        width, height, 8 * 16, 64 * 512 )
+            if( rows == 24 ) HS_GO( 24 );
+            else if( rows == 16 ) HS_GO( 16 );
+            else if( rows == 8 ) HS_GO( 8 );
+            else if( rows == 6 ) HS_GO( 6 );
+            else HS_GO( 12 );
+#undef HS_GO
             return hipGetLastError();
         }
     }
