@@ -563,26 +563,16 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
 // row ring of this pass, the near-zero fast skip, x264_me_search and the cost
 // adjustments.  Returns the list cost; mvx / mvy the list's mv.
 template <int BD>
-__device__ __forceinline__ int lr_list( LrCtx<BD> &m, const int *ring, int x, int y, int mbw, int mbh,
-                                        int me_method, int subme, int me_range, int lambda,
-                                        const uint16_t *cost_mv, int &mvx, int &mvy )
+__device__ __forceinline__ int lr_list( LrCtx<BD> &m, const uint32_t (&pred)[4], int npred, int me_method, int subme,
+                                        int me_range, int lambda, const uint16_t *cost_mv, int &mvx, int &mvy )
 {
     int mvc[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } };
-    int i_mvc = 0;
-    auto add = [&]( int v ) {
-        mvc[i_mvc][0] = (int16_t)(v & 0xffff);
-        mvc[i_mvc][1] = (int16_t)((uint32_t)v >> 16);
-        i_mvc++;
-    };
-    if( x < mbw - 1 )
-        add( ring[4 * y + ((x + 1) & 3)] );
-    if( y < mbh - 1 )
+    const int i_mvc = npred;
+#pragma unroll
+    for( int i = 0; i < 4; i++ )
     {
-        add( ring[4 * (y + 1) + (x & 3)] );
-        if( x > 0 )
-            add( ring[4 * (y + 1) + ((x - 1) & 3)] );
-        if( x < mbw - 1 )
-            add( ring[4 * (y + 1) + ((x + 1) & 3)] );
+        mvc[i][0] = (int16_t)(pred[i] & 0xffff);
+        mvc[i][1] = (int16_t)(pred[i] >> 16);
     }
     int mvpx, mvpy;
     if( i_mvc <= 1 )
@@ -616,6 +606,73 @@ __device__ __forceinline__ int lr_list( LrCtx<BD> &m, const int *ring, int x, in
     return cost;
 }
 
+
+// ---- multi-workgroup wavefront ----
+// A frame pair's block rows are split into bands of LR_BAND rows, one single-wave
+// workgroup each.  A band's rows take their predictors from the LDS ring of the
+// band, except the band's bottom row, whose row-below predictors (x-1, x, x+1 of
+// row y1, written by the band underneath at steps t-1 .. t-3) are read from the
+// mvs output itself: the launcher fills it with a sentinel no mv can take, the
+// producer stores each block's mv as one 32-bit word, and the consumer waits
+// until the three words it needs are no longer the sentinel.  Only bottom-up
+// waits exist and the band underneath has the lower workgroup index, so it is
+// dispatched first and never waits on a later workgroup.
+constexpr int LR_BAND = 16;                      // block rows per workgroup (one wave of lane quads)
+constexpr uint32_t LR_SENTINEL = 0x80808080u;    // mv (-32640, -32640): outside any mv range
+
+__device__ __forceinline__ uint32_t lr_load_mv( const uint32_t *p )
+{
+    return __hip_atomic_load( p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+}
+__device__ __forceinline__ void lr_store_mv( uint32_t *p, uint32_t v )
+{
+    __hip_atomic_store( p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+}
+
+// the predictors of block (x, y) in slicetype_mb_cost's order (slicetype.c:651-663):
+// right, then below, below-left, below-right
+__device__ __forceinline__ int lr_preds( const int *ring, int y0, int y1, const uint32_t *gmv, int x, int y, int mbw,
+                                         int mbh, uint32_t (&pred)[4] )
+{
+    int n = 0;
+#pragma unroll
+    for( int i = 0; i < 4; i++ )
+        pred[i] = 0;
+    if( x < mbw - 1 )
+        pred[n++] = (uint32_t)ring[4 * (y - y0) + ((x + 1) & 3)];
+    if( y < mbh - 1 )
+    {
+        uint32_t b = 0, bl = 0, br = 0;
+        if( y + 1 < y1 )
+        {
+            b = (uint32_t)ring[4 * (y + 1 - y0) + (x & 3)];
+            if( x > 0 )
+                bl = (uint32_t)ring[4 * (y + 1 - y0) + ((x - 1) & 3)];
+            if( x < mbw - 1 )
+                br = (uint32_t)ring[4 * (y + 1 - y0) + ((x + 1) & 3)];
+        }
+        else
+        {
+            const uint32_t *row = gmv + (intptr_t)(y + 1) * mbw;
+            for( int it = 0; it < (1 << 22); it++ )  // bounded: a broken schedule ends, never hangs
+            {
+                b = lr_load_mv( row + x );
+                bl = x > 0 ? lr_load_mv( row + x - 1 ) : 0;
+                br = x < mbw - 1 ? lr_load_mv( row + x + 1 ) : 0;
+                if( b != LR_SENTINEL && bl != LR_SENTINEL && br != LR_SENTINEL )
+                    break;
+                __builtin_amdgcn_s_sleep( 2 );
+            }
+        }
+        pred[n++] = b;
+        if( x > 0 )
+            pred[n++] = bl;
+        if( x < mbw - 1 )
+            pred[n++] = br;
+    }
+    return n;
+}
+
 template <int BD>
 __device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, intptr_t stride,
                                               uint32_t (&fe)[LR_NR][8 / PT<BD>::PPD] )
@@ -631,20 +688,19 @@ __device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, 
 }
 
 template <int BD>
-__global__ __launch_bounds__( 1024 ) void lowres_inter_kernel(
+__global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *r0,
     const typename PT<BD>::pixel *r1, const typename PT<BD>::pixel *r2, const typename PT<BD>::pixel *r3,
     intptr_t stride, intptr_t rfs, int mbw, int mbh, int me_method, int subme, int satd, int me_range, int mv_range,
     int lambda, const uint16_t *__restrict__ cost_mv, const uint16_t *__restrict__ intra_cost,
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
-    uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est )
+    uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
-    extern __shared__ int lr_smem[];
-    int *ring = lr_smem;                         // [mbh][4] packed MVs of the row's 4 latest blocks
-    int *rowacc = lr_smem + 4 * mbh;             // [mbh] AQ-scaled row sums
-    int *eacc = rowacc + mbh;                    // cost_est, cost_est_aq, intra_mbs
-    const int f = blockIdx.x;
+    __shared__ int ring[4 * LR_BAND];            // packed MVs of each band row's 4 latest blocks
+    const int f = blockIdx.x / nbands;
+    const int band = nbands - 1 - (int)(blockIdx.x % nbands);     // index 0 of a pair: the bottom band
+    const int y0 = LR_BAND * band, y1 = min( y0 + LR_BAND, mbh );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     r0 += (intptr_t)f * rfs;
@@ -657,71 +713,64 @@ __global__ __launch_bounds__( 1024 ) void lowres_inter_kernel(
     mvs += 2 * (intptr_t)f * nmb;
     mv_costs += (intptr_t)f * nmb;
     lcosts += (intptr_t)f * nmb;
-    for( int i = threadIdx.x; i < mbh; i += blockDim.x )
-        rowacc[i] = 0;
-    if( threadIdx.x < 3 )
-        eacc[threadIdx.x] = 0;
-    int e0 = 0, e1 = 0, e2 = 0;
+    uint32_t *gmv = (uint32_t *)mvs;
+    int e0 = 0, e1 = 0, e2 = 0, racc = 0;
     const int mvr = 2 * mv_range;
     const int q = threadIdx.x & 3;
-    __syncthreads();
-    const int steps = (mbw - 1) + 2 * (mbh - 1) + 1;
-    for( int t = 0; t < steps; t++ )
+    const int y = y0 + (int)(threadIdx.x >> 2);
+    // steps in which this band has blocks (block (x, y) runs at (W-1-x) + 2(H-1-y))
+    const int t0 = 2 * (mbh - y1), t1 = 2 * (mbh - 1 - y0) + mbw - 1;
+    for( int t = t0; t <= t1; t++ )
     {
-        for( int y = threadIdx.x >> 2; y < mbh; y += blockDim.x >> 2 )
+        const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        if( y < y1 && x >= 0 && x < mbw )
         {
-            const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
-            if( x < 0 || x >= mbw )
-                continue;
             const int mb = x + y * mbw;
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
             uint32_t fe[LR_NR][NDW];
             lr_load_fenc<BD>( fenc + off + (intptr_t)(LR_NR * q) * stride, stride, fe );
             LrCtx<BD> m( fe );
             m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd, q );
+            uint32_t pred[4];
+            const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred );
             int mvx, mvy;
-            const int cost = lr_list<BD>( m, ring, x, y, mbw, mbh, me_method, subme, me_range, lambda, cost_mv, mvx,
-                                          mvy );
-            if( q )
-                continue;                            // the quad's other lanes hold the same results
-            ring[4 * y + (x & 3)] = (int)lr_pack( mvx, mvy );
-            mvs[2 * mb] = (int16_t)mvx;
-            mvs[2 * mb + 1] = (int16_t)mvy;
-            mv_costs[mb] = cost;
-            // slicetype.c:758-790
-            int bcost = (cost >> (BD - 8)) + 4, list_used = 1;
-            const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
-            const int icost = intra_cost[mb];
-            const bool b_intra = icost < bcost;
-            if( b_intra )
+            const int cost = lr_list<BD>( m, pred, np, me_method, subme, me_range, lambda, cost_mv, mvx, mvy );
+            if( q == 0 )
             {
-                bcost = icost;
-                list_used = 0;
+                ring[4 * (y - y0) + (x & 3)] = (int)lr_pack( mvx, mvy );
+                lr_store_mv( gmv + mb, lr_pack( mvx, mvy ) );
+                mv_costs[mb] = cost;
+                // slicetype.c:758-790
+                int bcost = (cost >> (BD - 8)) + 4, list_used = 1;
+                const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
+                const int icost = intra_cost[mb];
+                const bool b_intra = icost < bcost;
+                if( b_intra )
+                {
+                    bcost = icost;
+                    list_used = 0;
+                }
+                const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
+                racc += aq;
+                if( fsm )
+                {
+                    e0 += bcost;
+                    e1 += aq;
+                    e2 += b_intra;
+                }
+                lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
             }
-            const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
-            rowacc[y] += aq;
-            if( fsm )
-            {
-                e0 += bcost;
-                e1 += aq;
-                e2 += b_intra;
-            }
-            lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
         }
         __syncthreads();
     }
-    if( e0 | e1 | e2 )
+    if( q == 0 && y < y1 && row_satd )
+        row_satd[(intptr_t)f * mbh + y] = racc;
+    if( est && (e0 | e1 | e2) )
     {
-        atomicAdd( &eacc[0], e0 );
-        atomicAdd( &eacc[1], e1 );
-        atomicAdd( &eacc[2], e2 );
+        atomicAdd( &est[3 * f], e0 );
+        atomicAdd( &est[3 * f + 1], e1 );
+        atomicAdd( &est[3 * f + 2], e2 );
     }
-    __syncthreads();
-    if( row_satd )
-        for( int i = threadIdx.x; i < mbh; i += blockDim.x )
-            row_satd[(intptr_t)f * mbh + i] = rowacc[i];
-    if( est && threadIdx.x < 3 )
-        est[3 * f + threadIdx.x] = eacc[threadIdx.x];
 }
 
 // pixel_avg / pixel_avg_weight_wxh (mc.c:49-87) of two packed dwords: the rounding
@@ -776,7 +825,7 @@ __device__ __forceinline__ int lr_bidir( const LrCtx<BD> &m0, const LrCtx<BD> &m
 // B frames (p0 < b < p1): slicetype_mb_cost with b_bidir (slicetype.c:514-713, 758-791).
 // A list is searched on the wavefront when search & (1 << l), else its mv / cost are read.
 template <int BD>
-__global__ __launch_bounds__( 1024 ) void lowres_bidir_kernel(
+__global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *a0,
     const typename PT<BD>::pixel *a1, const typename PT<BD>::pixel *a2, const typename PT<BD>::pixel *a3,
     intptr_t afs, const typename PT<BD>::pixel *b0, const typename PT<BD>::pixel *b1,
@@ -785,15 +834,13 @@ __global__ __launch_bounds__( 1024 ) void lowres_bidir_kernel(
     const uint16_t *__restrict__ cost_mv, int search, int16_t *__restrict__ mvs0, int32_t *__restrict__ costs0,
     int16_t *__restrict__ mvs1, int32_t *__restrict__ costs1, const int16_t *__restrict__ p1mvs, int dsf, int weight,
     const uint16_t *__restrict__ invq, uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd,
-    int32_t *__restrict__ est )
+    int32_t *__restrict__ est, int nbands )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
-    extern __shared__ int lr_smem[];
-    int *ring0 = lr_smem;                        // [mbh][4] per list
-    int *ring1 = lr_smem + 4 * mbh;
-    int *rowacc = lr_smem + 8 * mbh;
-    int *eacc = rowacc + mbh;
-    const int f = blockIdx.x;
+    __shared__ int ring0[4 * LR_BAND], ring1[4 * LR_BAND];      // per list
+    const int f = blockIdx.x / nbands;
+    const int band = nbands - 1 - (int)(blockIdx.x % nbands);   // index 0 of a triplet: the bottom band
+    const int y0 = LR_BAND * band, y1 = min( y0 + LR_BAND, mbh );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     a0 += (intptr_t)f * afs; a1 += (intptr_t)f * afs; a2 += (intptr_t)f * afs; a3 += (intptr_t)f * afs;
@@ -807,23 +854,18 @@ __global__ __launch_bounds__( 1024 ) void lowres_bidir_kernel(
     costs0 += (intptr_t)f * nmb;
     costs1 += (intptr_t)f * nmb;
     lcosts += (intptr_t)f * nmb;
-    for( int i = threadIdx.x; i < mbh; i += blockDim.x )
-        rowacc[i] = 0;
-    if( threadIdx.x < 2 )
-        eacc[threadIdx.x] = 0;
-    int e0 = 0, e1 = 0;
+    uint32_t *gmv0 = (uint32_t *)mvs0, *gmv1 = (uint32_t *)mvs1;
+    int e0 = 0, e1 = 0, racc = 0;
     const int mvr = 2 * mv_range;
     const int q = threadIdx.x & 3;
     const bool hp = subme == 2;                  // h->param.analyse.i_subpel_refine <= 1
-    __syncthreads();
-    const int steps = (mbw - 1) + 2 * (mbh - 1) + 1;
-    for( int t = 0; t < steps; t++ )
+    const int y = y0 + (int)(threadIdx.x >> 2);
+    const int t0 = 2 * (mbh - y1), t1 = 2 * (mbh - 1 - y0) + mbw - 1;
+    for( int t = t0; t <= t1; t++ )
     {
-        for( int y = threadIdx.x >> 2; y < mbh; y += blockDim.x >> 2 )
+        const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        if( y < y1 && x >= 0 && x < mbw )
         {
-            const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
-            if( x < 0 || x >= mbw )
-                continue;
             const int mb = x + y * mbw;
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
             uint32_t fe[LR_NR][NDW];
@@ -866,11 +908,15 @@ __global__ __launch_bounds__( 1024 ) void lowres_bidir_kernel(
             int mv0x, mv0y, mv1x, mv1y, lc;
             if( search & 1 )
             {
-                lc = lr_list<BD>( m0, ring0, x, y, mbw, mbh, me_method, subme, me_range, lambda, cost_mv, mv0x, mv0y );
-                ring0[4 * y + (x & 3)] = (int)lr_pack( mv0x, mv0y );
-                mvs0[2 * mb] = (int16_t)mv0x;
-                mvs0[2 * mb + 1] = (int16_t)mv0y;
-                costs0[mb] = lc;
+                uint32_t pred[4];
+                const int np = lr_preds( ring0, y0, y1, gmv0, x, y, mbw, mbh, pred );
+                lc = lr_list<BD>( m0, pred, np, me_method, subme, me_range, lambda, cost_mv, mv0x, mv0y );
+                if( q == 0 )
+                {
+                    ring0[4 * (y - y0) + (x & 3)] = (int)lr_pack( mv0x, mv0y );
+                    lr_store_mv( gmv0 + mb, lr_pack( mv0x, mv0y ) );
+                    costs0[mb] = lc;
+                }
             }
             else
             {
@@ -885,11 +931,15 @@ __global__ __launch_bounds__( 1024 ) void lowres_bidir_kernel(
             }
             if( search & 2 )
             {
-                lc = lr_list<BD>( m1, ring1, x, y, mbw, mbh, me_method, subme, me_range, lambda, cost_mv, mv1x, mv1y );
-                ring1[4 * y + (x & 3)] = (int)lr_pack( mv1x, mv1y );
-                mvs1[2 * mb] = (int16_t)mv1x;
-                mvs1[2 * mb + 1] = (int16_t)mv1y;
-                costs1[mb] = lc;
+                uint32_t pred[4];
+                const int np = lr_preds( ring1, y0, y1, gmv1, x, y, mbw, mbh, pred );
+                lc = lr_list<BD>( m1, pred, np, me_method, subme, me_range, lambda, cost_mv, mv1x, mv1y );
+                if( q == 0 )
+                {
+                    ring1[4 * (y - y0) + (x & 3)] = (int)lr_pack( mv1x, mv1y );
+                    lr_store_mv( gmv1 + mb, lr_pack( mv1x, mv1y ) );
+                    costs1[mb] = lc;
+                }
             }
             else
             {
@@ -911,33 +961,30 @@ __global__ __launch_bounds__( 1024 ) void lowres_bidir_kernel(
                     list_used = 3;
                 }
             }
-            if( q )
-                continue;                            // the quad's other lanes hold the same results
-            // slicetype.c:758-790 (no intra in B frames)
-            bcost = (bcost >> (BD - 8)) + 4;
-            const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
-            const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
-            rowacc[y] += aq;
-            if( fsm )
+            if( q == 0 )
             {
-                e0 += bcost;
-                e1 += aq;
+                // slicetype.c:758-790 (no intra in B frames)
+                bcost = (bcost >> (BD - 8)) + 4;
+                const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
+                const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
+                racc += aq;
+                if( fsm )
+                {
+                    e0 += bcost;
+                    e1 += aq;
+                }
+                lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
             }
-            lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
         }
         __syncthreads();
     }
-    if( e0 | e1 )
+    if( q == 0 && y < y1 && row_satd )
+        row_satd[(intptr_t)f * mbh + y] = racc;
+    if( est && (e0 | e1) )
     {
-        atomicAdd( &eacc[0], e0 );
-        atomicAdd( &eacc[1], e1 );
+        atomicAdd( &est[2 * f], e0 );
+        atomicAdd( &est[2 * f + 1], e1 );
     }
-    __syncthreads();
-    if( row_satd )
-        for( int i = threadIdx.x; i < mbh; i += blockDim.x )
-            row_satd[(intptr_t)f * mbh + i] = rowacc[i];
-    if( est && threadIdx.x < 2 )
-        est[2 * f + threadIdx.x] = eacc[threadIdx.x];
 }
 
 template <int BD>
@@ -952,12 +999,25 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
 {
     if( n <= 0 || mbw <= 0 || mbh <= 0 )
         return hipSuccess;
-    const int threads = min( 1024, (4 * mbh + 63) / 64 * 64 );         // a lane quad per block row
-    const size_t lds = (size_t)(9 * mbh + 2) * sizeof( int );
-    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n ), dim3( threads ), lds, stream, fenc, ffs, ra[0], ra[1],
+    // a searched list's mvs start as the sentinel the bands wait on; the frame sums
+    // are accumulated by every band
+    const size_t mvbytes = (size_t)n * mbw * mbh * 4;
+    hipError_t e = hipSuccess;
+    if( search & 1 )
+        e = hipMemsetAsync( mvs0, 0x80, mvbytes, stream );
+    if( e == hipSuccess && (search & 2) )
+        e = hipMemsetAsync( mvs1, 0x80, mvbytes, stream );
+    if( e == hipSuccess && est )
+        e = hipMemsetAsync( est, 0, (size_t)n * 2 * sizeof( int32_t ), stream );
+    if( e != hipSuccess )
+        return e;
+    const int nbands = (mbh + LR_BAND - 1) / LR_BAND;
+    if( (int64_t)n * nbands > 0x7fffffff )
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( 64 ), 0, stream, fenc, ffs, ra[0], ra[1],
                         ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method, subme, satd,
                         me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, weight,
-                        invq, lowres_costs, row_satd, est );
+                        invq, lowres_costs, row_satd, est, nbands );
     return hipGetLastError();
 }
 
@@ -971,11 +1031,18 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
 {
     if( npairs <= 0 || mbw <= 0 || mbh <= 0 )
         return hipSuccess;
-    const int threads = min( 1024, (4 * mbh + 63) / 64 * 64 );         // a lane quad per block row
-    const size_t lds = (size_t)(5 * mbh + 3) * sizeof( int );
-    hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs ), dim3( threads ), lds, stream, fenc, ffs, ref[0],
+    // mvs start as the sentinel the bands wait on; the frame sums are accumulated by every band
+    hipError_t e = hipMemsetAsync( mvs, 0x80, (size_t)npairs * mbw * mbh * 4, stream );
+    if( e == hipSuccess && est )
+        e = hipMemsetAsync( est, 0, (size_t)npairs * 3 * sizeof( int32_t ), stream );
+    if( e != hipSuccess )
+        return e;
+    const int nbands = (mbh + LR_BAND - 1) / LR_BAND;
+    if( (int64_t)npairs * nbands > 0x7fffffff )
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( 64 ), 0, stream, fenc, ffs, ref[0],
                         ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
-                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est );
+                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands );
     return hipGetLastError();
 }
 
