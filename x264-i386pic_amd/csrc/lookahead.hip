@@ -617,7 +617,7 @@ __device__ __forceinline__ int lr_list( LrCtx<BD> &m, const uint32_t (&pred)[4],
 // until the three words it needs are no longer the sentinel.  Only bottom-up
 // waits exist and the band underneath has the lower workgroup index, so it is
 // dispatched first and never waits on a later workgroup.
-constexpr int LR_BAND = 16;                      // block rows per workgroup (one wave of lane quads)
+constexpr int LR_BAND = 16;                      // max block rows per workgroup (one wave of lane quads)
 constexpr uint32_t LR_SENTINEL = 0x80808080u;    // mv (-32640, -32640): outside any mv range
 
 __device__ __forceinline__ uint32_t lr_load_mv( const uint32_t *p )
@@ -673,6 +673,21 @@ __device__ __forceinline__ int lr_preds( const int *ring, int y0, int y1, const 
     return n;
 }
 
+
+// The mv cost table staged in LDS: every candidate's cost reads p_cost_mvx/y at an index
+// that depends on the previous decision, so these lookups sit on the search's serial
+// chain; |index| <= 2 * (2 * mv_range) + 3 (an mv and a predictor, both within the
+// lowres mv limits), the staged span keeps a margin on top.
+__device__ __forceinline__ int lr_cost_span( int mv_range ) { return 4 * mv_range + 64; }
+__device__ __forceinline__ const uint16_t *lr_stage_cost( uint16_t *lds, const uint16_t *cost_mv, int mv_range )
+{
+    const int span = lr_cost_span( mv_range );
+    for( int i = threadIdx.x; i <= 2 * span; i += blockDim.x )
+        lds[i] = cost_mv[i - span];
+    __syncthreads();
+    return lds + span;
+}
+
 template <int BD>
 __device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, intptr_t stride,
                                               uint32_t (&fe)[LR_NR][8 / PT<BD>::PPD] )
@@ -694,13 +709,15 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     intptr_t stride, intptr_t rfs, int mbw, int mbh, int me_method, int subme, int satd, int me_range, int mv_range,
     int lambda, const uint16_t *__restrict__ cost_mv, const uint16_t *__restrict__ intra_cost,
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
-    uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands )
+    uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands, int brows )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring[4 * LR_BAND];            // packed MVs of each band row's 4 latest blocks
+    extern __shared__ uint16_t lr_cost_lds[];
+    const uint16_t *cml = lr_stage_cost( lr_cost_lds, cost_mv, mv_range );
     const int f = blockIdx.x / nbands;
     const int band = nbands - 1 - (int)(blockIdx.x % nbands);     // index 0 of a pair: the bottom band
-    const int y0 = LR_BAND * band, y1 = min( y0 + LR_BAND, mbh );
+    const int y0 = brows * band, y1 = min( y0 + brows, mbh );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     r0 += (intptr_t)f * rfs;
@@ -734,7 +751,7 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
             uint32_t pred[4];
             const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred );
             int mvx, mvy;
-            const int cost = lr_list<BD>( m, pred, np, me_method, subme, me_range, lambda, cost_mv, mvx, mvy );
+            const int cost = lr_list<BD>( m, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy );
             if( q == 0 )
             {
                 ring[4 * (y - y0) + (x & 3)] = (int)lr_pack( mvx, mvy );
@@ -834,13 +851,15 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const uint16_t *__restrict__ cost_mv, int search, int16_t *__restrict__ mvs0, int32_t *__restrict__ costs0,
     int16_t *__restrict__ mvs1, int32_t *__restrict__ costs1, const int16_t *__restrict__ p1mvs, int dsf, int weight,
     const uint16_t *__restrict__ invq, uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd,
-    int32_t *__restrict__ est, int nbands )
+    int32_t *__restrict__ est, int nbands, int brows )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring0[4 * LR_BAND], ring1[4 * LR_BAND];      // per list
+    extern __shared__ uint16_t lr_cost_lds[];
+    const uint16_t *cml = lr_stage_cost( lr_cost_lds, cost_mv, mv_range );
     const int f = blockIdx.x / nbands;
     const int band = nbands - 1 - (int)(blockIdx.x % nbands);   // index 0 of a triplet: the bottom band
-    const int y0 = LR_BAND * band, y1 = min( y0 + LR_BAND, mbh );
+    const int y0 = brows * band, y1 = min( y0 + brows, mbh );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     a0 += (intptr_t)f * afs; a1 += (intptr_t)f * afs; a2 += (intptr_t)f * afs; a3 += (intptr_t)f * afs;
@@ -910,7 +929,7 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
             {
                 uint32_t pred[4];
                 const int np = lr_preds( ring0, y0, y1, gmv0, x, y, mbw, mbh, pred );
-                lc = lr_list<BD>( m0, pred, np, me_method, subme, me_range, lambda, cost_mv, mv0x, mv0y );
+                lc = lr_list<BD>( m0, pred, np, me_method, subme, me_range, lambda, cml, mv0x, mv0y );
                 if( q == 0 )
                 {
                     ring0[4 * (y - y0) + (x & 3)] = (int)lr_pack( mv0x, mv0y );
@@ -933,7 +952,7 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
             {
                 uint32_t pred[4];
                 const int np = lr_preds( ring1, y0, y1, gmv1, x, y, mbw, mbh, pred );
-                lc = lr_list<BD>( m1, pred, np, me_method, subme, me_range, lambda, cost_mv, mv1x, mv1y );
+                lc = lr_list<BD>( m1, pred, np, me_method, subme, me_range, lambda, cml, mv1x, mv1y );
                 if( q == 0 )
                 {
                     ring1[4 * (y - y0) + (x & 3)] = (int)lr_pack( mv1x, mv1y );
@@ -1011,13 +1030,22 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
         e = hipMemsetAsync( est, 0, (size_t)n * 2 * sizeof( int32_t ), stream );
     if( e != hipSuccess )
         return e;
-    const int nbands = (mbh + LR_BAND - 1) / LR_BAND;
+    // X264HIP_LOOKAHEAD_BAND: block rows per single-wave workgroup (<= 16).  A step costs
+    // the slowest of a wave's row searches (the lanes run in lockstep), so fewer rows per
+    // wave means less divergence; 4 measured best (15 1080p pairs, tools/la_band.py:
+    // P 2.46 / 2.32 / 2.19 / 2.26 ms, B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2)
+    const int bv = variant( V_LA_BAND );
+    const int brows = bv >= 1 && bv <= LR_BAND ? bv : 4;
+    const int nbands = (mbh + brows - 1) / brows;
     if( (int64_t)n * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( 64 ), 0, stream, fenc, ffs, ra[0], ra[1],
+    const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
+    if( mv_range < 1 || lds > 48 * 1024 )
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ra[0], ra[1],
                         ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method, subme, satd,
                         me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, weight,
-                        invq, lowres_costs, row_satd, est, nbands );
+                        invq, lowres_costs, row_satd, est, nbands, brows );
     return hipGetLastError();
 }
 
@@ -1037,12 +1065,21 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
         e = hipMemsetAsync( est, 0, (size_t)npairs * 3 * sizeof( int32_t ), stream );
     if( e != hipSuccess )
         return e;
-    const int nbands = (mbh + LR_BAND - 1) / LR_BAND;
+    // X264HIP_LOOKAHEAD_BAND: block rows per single-wave workgroup (<= 16).  A step costs
+    // the slowest of a wave's row searches (the lanes run in lockstep), so fewer rows per
+    // wave means less divergence; 4 measured best (15 1080p pairs, tools/la_band.py:
+    // P 2.46 / 2.32 / 2.19 / 2.26 ms, B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2)
+    const int bv = variant( V_LA_BAND );
+    const int brows = bv >= 1 && bv <= LR_BAND ? bv : 4;
+    const int nbands = (mbh + brows - 1) / brows;
     if( (int64_t)npairs * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( 64 ), 0, stream, fenc, ffs, ref[0],
+    const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
+    if( mv_range < 1 || lds > 48 * 1024 )
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ref[0],
                         ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
-                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands );
+                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows );
     return hipGetLastError();
 }
 
