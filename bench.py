@@ -400,6 +400,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     del nb8, hv, ref_planes, fo, qxy, sc, bfo, cxy, sc9, lst
     res.update(rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_ssd(x, a, world, dev, origin, stride, F))
+    res.update(rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
     res.update(rates_2160p(x, a, world))
     return res
@@ -468,6 +469,39 @@ def rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     if not torch.equal(out, out2):
         raise SystemExit("bench: me_tesa with and without the SAD table disagree")
     del integ, table, out, out2
+    return res
+
+
+def rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
+    """The ESA decision of every MB of the F pairs (me.c:618-631, window centred on the
+    predictor, here mv 0 so every candidate of the headline table is in the window):
+    the table path (headline kernel + me_esa_argmin) against the fused kernel that never
+    writes the table.  Both count the same 1089 candidates per MB."""
+    R = a.range
+    par, init, cm, span = tesa_params(mbw, mbh, F, R, centre=(0, 0))
+    par_d, init_d = torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda()
+    cm_d = torch.from_numpy(cm.view(np.int16)).cuda()
+    table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
+    out_t = torch.empty((F * mbw * mbh, 3), dtype=torch.int32, device="cuda")
+    out_f = torch.empty_like(out_t)
+
+    def tstep():
+        x.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, table=table,
+                         fenc_frame_stride=fstride, ref_frame_stride=fstride)
+        x.me_esa_argmin(table, R, R, par_d, init_d, (cm_d, span), out=out_t)
+
+    def fstep():
+        x.me_search_esa(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, R, par_d, init_d,
+                        (cm_d, span), out=out_f, fenc_frame_stride=fstride, ref_frame_stride=fstride)
+    cands = F * mbw * mbh * (2 * R + 1) ** 2
+    wall, ev_ms = timed(tstep, a.steps, a.warmup, world)
+    res = {"esa_table_candidates_per_s": world * a.steps * cands / wall, "esa_table_step_ms": ev_ms}
+    wall, ev_ms = timed(fstep, a.steps, a.warmup, world)
+    res["esa_fused_candidates_per_s"] = world * a.steps * cands / wall
+    res["esa_fused_step_ms"] = ev_ms
+    res["esa_fused_frac"] = cands * 256 / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF
+    if not torch.equal(out_t, out_f):
+        raise SystemExit("bench: fused and table ESA decisions disagree")
     return res
 
 

@@ -230,3 +230,53 @@ def test_me_esa_argmin_centred(hip, oracle, bd):
                 if c < best[0]:
                     best = (c, mx, my)
         assert tuple(got[mb]) == best, mb
+
+
+@pytest.mark.parametrize("rng,me_range", [(24, 16), (16, 8), (8, 4), (24, 12)])
+@pytest.mark.parametrize("W,H", [(160, 96), (1920, 1088)])
+def test_me_search_esa_fused(hip, oracle, rng, me_range, W, H):
+    """Fused search + ESA decision (x264hip_8_me_search_esa) equals me_search_centred followed by
+    me_esa_argmin_at on the GPU, and the oracle's centred table + argmin, over predictor centres,
+    clipped windows, mvp-dependent costs and unbeatable predictors."""
+    from x264hip import synth
+    planes, stride, origin = synth.make_sequence(3, W, H, 8, seed=rng + me_range)
+    dev = torch.from_numpy(planes).cuda()
+    fs = planes[0].size
+    mbw, mbh, nf = W // 16, H // 16, 2
+    nmb = mbw * mbh
+    rs = np.random.default_rng(rng * 7 + me_range)
+    par = np.zeros((nf * nmb, 8), np.int16)
+    par[:, 0] = rs.integers(-12, 13, nf * nmb)
+    par[:, 1] = rs.integers(-12, 13, nf * nmb)
+    par[:, 2] = rs.integers(-64, 65, nf * nmb)
+    par[:, 3] = rs.integers(-64, 65, nf * nmb)
+    mb = np.arange(nf * nmb) % nmb
+    mbx, mby = mb % mbw, mb // mbw
+    tight = rs.integers(0, me_range + 1, (nf * nmb, 4)) * (rs.random((nf * nmb, 4)) < 0.3)
+    par[:, 4] = np.minimum(-16 * mbx - 24 + tight[:, 0], par[:, 0])
+    par[:, 5] = np.minimum(-16 * mby - 24 + tight[:, 1], par[:, 1])
+    par[:, 6] = np.maximum(16 * (mbw - 1 - mbx) + 20 - tight[:, 2], par[:, 0])
+    par[:, 7] = np.maximum(16 * (mbh - 1 - mby) + 24 - tight[:, 3], par[:, 1])
+    init = rs.integers(0, 20000, nf * nmb).astype(np.int32)
+    init[::7] = 0
+    cost_mv, c0 = _cost_mv(span=8192)
+    cm_dev = torch.from_numpy(cost_mv.view(np.int16)).cuda()
+    par_d, init_d = torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda()
+    got = hip.me_search_esa(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, nf, rng, me_range, par_d,
+                            init_d, (cm_dev, c0), fenc_frame_stride=fs, ref_frame_stride=fs).cpu().numpy()
+    cen = torch.from_numpy(np.ascontiguousarray(par[:, :2])).cuda()
+    table, org = hip.me_search_centred(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, nf, rng, cen,
+                                       fenc_frame_stride=fs, ref_frame_stride=fs)
+    ref_out = hip.me_esa_argmin(table, rng, me_range, par_d, init_d, (cm_dev, c0), origin=org).cpu().numpy()
+    assert np.array_equal(got, ref_out), np.argwhere((got != ref_out).any(1))[:5]
+    if W == 160:
+        for f in range(nf):
+            sl = slice(f * nmb, (f + 1) * nmb)
+            tab, worg = oracle.me_search_centred(8, planes[f + 1].ravel(), origin, stride, planes[f].ravel(), origin,
+                                                 stride, mbw, mbh, rng, par[sl, :2])
+            p_ = (2 * rng + 1 + 3) & ~3
+            padded = np.zeros((nmb, 2 * rng + 1, p_), tab.dtype)
+            padded[:, :, :2 * rng + 1] = tab.reshape(nmb, 2 * rng + 1, 2 * rng + 1)
+            want = oracle.me_esa_argmin(8, padded, rng, me_range, par[sl], init[sl], cost_mv, c0, origin=worg)
+            assert np.array_equal(got[sl], want), (f, np.argwhere((got[sl] != want).any(1))[:5])
+    assert (got[::7, 0] == 0).all() and (got[:, 0] <= init).all()

@@ -23,7 +23,7 @@ import os
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref",
@@ -966,3 +966,25 @@ def ssd_nv12_batch(pix1, origin1, stride1, pix2, origin2, stride2, width, height
     (ssd_u, ssd_v); width = chroma samples per row."""
     return _plane_ssd("ssd_nv12_batch", True, pix1, origin1, stride1, pix2, origin2, stride2, width, height,
                       nframes, out, frame_stride1, frame_stride2)
+
+
+def me_search_esa(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height, nframes, rng,
+                  me_range, par, init_cost, cost_mv_center, out=None, fenc_frame_stride=None, ref_frame_stride=None):
+    """Fused full search around each MB's predictor + ESA decision (x264hip_8_me_search_esa, 8 bit):
+    the result of me_search_centred(centre = par[:, :2]) followed by me_esa_argmin(origin=...),
+    without the table.  Returns int32 [n, 3] = (cost, mx, my)."""
+    import torch
+    if _pix_bd(fenc) != 8:
+        raise TypeError("me_search_esa is 8-bit")
+    n = par.shape[0]
+    if out is None:
+        out = torch.empty((n, 3), dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)
+    cm, c0 = cost_mv_center
+    fn = lib().x264hip_8_me_search_esa
+    fn.argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P]
+    fn.restype = _c.c_int
+    _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs, mb_width, mb_height,
+           nframes, rng, me_range, _ptr(par), _ptr(init_cost), _ptr(cm, c0), _ptr(out), _stream()), "me_search_esa")
+    return out

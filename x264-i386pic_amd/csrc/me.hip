@@ -237,11 +237,12 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v2_kernel( const typename
 // pitch align4(2R+1); the 0..3 trailing entries hold the SADs of mx = R+1..
 typedef uint64_t u64x2a4 __attribute__( ( ext_vector_type( 2 ), aligned( 4 ) ) );
 
-template <int R, int Y>
+// `sink( c, lo, hi )` receives candidate row c's four finished SADs (packed u16 pairs:
+// columns 4j, 4j+1 in lo, 4j+2, 4j+3 in hi), identical in both lanes of the pair
+template <int R, int Y, class Sink>
 __device__ __forceinline__ void me_row3( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
-                                         uint64_t (&acc)[8], uint64_t *out )
+                                         uint64_t (&acc)[8], Sink &sink )
 {
-    constexpr int P4 = (2 * R + 1 + 3) / 4;     // row pitch in u64 units
     constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
     constexpr int C1 = Y < 2 * R ? Y : 2 * R;
     const uint32_t *row = rbase + Y * rs_dw;
@@ -263,18 +264,18 @@ __device__ __forceinline__ void me_row3( const uint32_t *__restrict__ rbase, int
             uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
             lo += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)lo, 0xB1, 0xF, 0xF, false );
             hi += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)hi, 0xB1, 0xF, 0xF, false );
-            out[c * P4] = ((uint64_t)hi << 32) | lo;
+            sink( c, lo, hi );
         }
         else
             acc[c & 7] = a;
     }
 }
 
-template <int R, int... Ys>
+template <int R, class Sink, int... Ys>
 __device__ __forceinline__ void me_rows3( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
-                                          uint64_t (&acc)[8], uint64_t *out, std::integer_sequence<int, Ys...> )
+                                          uint64_t (&acc)[8], Sink &sink, std::integer_sequence<int, Ys...> )
 {
-    ( me_row3<R, Ys>( rbase, rs_dw, F, acc, out ), ... );
+    ( me_row3<R, Ys>( rbase, rs_dw, F, acc, sink ), ... );
 }
 
 template <int R>
@@ -317,8 +318,155 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t 
     const uint32_t *rbase =
         (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 4 * grp);
     uint64_t *out = (uint64_t *)(table + mb * ((2 * R + 1) * P) + 4 * grp);
+    auto store = [out]( int c, uint32_t lo, uint32_t hi ) { out[c * (P / 4)] = ((uint64_t)hi << 32) | lo; };
     uint64_t acc[8];
-    me_rows3<R>( rbase, (int)(rs / 4), F, acc, out, std::make_integer_sequence<int, 2 * R + 8>{} );
+    me_rows3<R>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
+}
+
+// Fused search + ESA decision (8 bit): the variant-3 lanes of me_search_centred around
+// each MB's predictor (bmx, bmy), but each finished candidate row is turned into
+// me_esa_argmin_at's packed keys (cost << 12 | raster index in the clipped, width-rounded
+// window, encoder/me.c:618-631, cost_mv terms me.c:60-70) and min-reduced in registers
+// instead of written out: the 17.8 MB-per-frame table never leaves the chip.  Each MB's
+// 18 lanes meet through one atomicMin per lane pair into its key slot (out[3*mb]), and
+// me_esa_finish_kernel applies the strict-< update from the predictor cost.
+template <int R>
+__global__ __launch_bounds__( 256 ) void me_full_esa_v3_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
+                                                                intptr_t ffs, const uint8_t *__restrict__ ref,
+                                                                intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                int nframes, int me_range,
+                                                                const int16_t *__restrict__ par,
+                                                                const uint16_t *__restrict__ cost_mv,
+                                                                uint32_t *__restrict__ keys )
+{
+    constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
+    constexpr int W = 2 * R + 1;
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
+    if( slot >= total )
+        return;
+    const int h = (int)(slot & 1);
+    const int grp = (int)((slot >> 1) % G);
+    const int64_t mb = slot / (2 * G);
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+
+    uint32_t F[8][4];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs / 4);
+#pragma unroll
+    for( int r = 0; r < 8; r++ )
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+    const int16_t *p = par + 8 * mb;
+    const int bmx = p[0], bmy = p[1];
+    const int min_x = max( bmx - me_range, (int)p[4] ), min_y = max( bmy - me_range, (int)p[5] );
+    const int max_x = min( bmx + me_range, (int)p[6] ), max_y = min( bmy + me_range, (int)p[7] );
+    const int width = (max_x - min_x + 3) & ~3;
+    const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
+    int ox, oy;
+    const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };   // the window centre: the predictor
+    me_window<8, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
+    const uint32_t *rbase =
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 4 * grp);
+    // the pair's four columns are split: lane h keys columns 4j+2h and 4j+2h+1 (its half of
+    // the packed sums), so both lanes share the epilogue without divergence
+    int ccost[2];
+    uint32_t cinv[2];                            // 0 for a column inside the window, else all ones
+#pragma unroll
+    for( int k = 0; k < 2; k++ )
+    {
+        const int col = 4 * grp + 2 * h + k, mx = ox + col;
+        const bool in = col < W && mx >= min_x && mx < min_x + width;
+        cinv[k] = in ? 0u : 0xFFFFFFFFu;
+        ccost[k] = in ? (int)cx[mx * 4] : 0;
+    }
+    uint32_t key = 0xFFFFFFFFu;
+    const int ibase = ox + 4 * grp + 2 * h - min_x - min_y * width;
+    // branch-free: every row loads a (clamped, always valid) row cost and masks the keys
+    // of rows / columns outside the window with all ones
+    auto reduce = [&]( int c, uint32_t lo, uint32_t hi ) {
+        const int my = oy + c;
+        const uint32_t rinv = my >= min_y && my <= max_y ? 0u : 0xFFFFFFFFu;
+        int yi = 4 * min( max( my, min_y ), max_y );
+        asm volatile( "" : "+v"( yi ) );         // the row cost is loaded here, not hoisted
+        const uint32_t ycost = cy[yi];
+        const uint32_t w = h ? hi : lo;
+        const uint32_t ri = (uint32_t)(my * width + ibase);
+        const uint32_t k0 = (((w & 0xffff) + (uint32_t)ccost[0] + ycost) << 12) | ri;
+        const uint32_t k1 = (((w >> 16) + (uint32_t)ccost[1] + ycost) << 12) | (ri + 1);
+        key = min( key, min( k0 | cinv[0], k1 | cinv[1] ) | rinv );
+        // fold each row into the key where its sums finish: left to itself the compiler
+        // keeps every row's sums live until the end (2 VGPRs a row, half the occupancy)
+        asm volatile( "" : "+v"( key ) );
+    };
+    uint64_t acc[8];
+    me_rows3<R>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
+    key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)key, 0xB1, 0xF, 0xF, false ) );
+    if( !h && key != 0xFFFFFFFFu )
+        atomicMin( keys + 3 * mb, key );
+}
+
+// out[3*mb] holds the MB's best key (0xFFFFFFFF: nothing evaluated); the strict-< update
+// from the predictor result (COPY3_IF_LT, me.h:87-93) turns it into { cost, mx, my }
+__global__ __launch_bounds__( 256 ) void me_esa_finish_kernel( int nmb, int me_range, const int16_t *__restrict__ par,
+                                                               const int32_t *__restrict__ init_cost,
+                                                               int32_t *__restrict__ out )
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if( i >= nmb )
+        return;
+    const int16_t *p = par + 8 * i;
+    const int bmx = p[0], bmy = p[1];
+    const int min_x = max( bmx - me_range, (int)p[4] ), min_y = max( bmy - me_range, (int)p[5] );
+    const int max_x = min( bmx + me_range, (int)p[6] );
+    const int width = (max_x - min_x + 3) & ~3;
+    const uint32_t key = (uint32_t)out[3 * i];
+    int32_t bcost = init_cost[i], rx = bmx, ry = bmy;
+    if( key != 0xFFFFFFFFu && (int32_t)(key >> 12) < bcost )
+    {
+        const int k = (int)(key & 4095);
+        bcost = (int32_t)(key >> 12);
+        ry = min_y + k / width;
+        rx = min_x + k % width;
+    }
+    out[3 * i] = bcost;
+    out[3 * i + 1] = rx;
+    out[3 * i + 2] = ry;
+}
+
+hipError_t launch_me_search_esa8( const uint8_t *fenc, intptr_t fs, intptr_t ffs, const uint8_t *ref, intptr_t rs,
+                                  intptr_t rfs, int mbw, int mbh, int nframes, int range, int me_range,
+                                  const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,
+                                  hipStream_t stream )
+{
+    const int64_t nmb = (int64_t)nframes * mbw * mbh;
+    if( nmb <= 0 )
+        return hipSuccess;
+    if( nmb > 0x7fffffff || (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)fs | (uintptr_t)rs) & 3) )
+        return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync( out, 0xFF, (size_t)nmb * 3 * sizeof( int32_t ), stream );
+    if( e != hipSuccess )
+        return e;
+    const int64_t lanes = nmb * 2 * ((2 * range + 1 + 3) / 4);
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+    switch( range )
+    {
+#define ESA_CASE( R )                                                                                             \
+        case R:                                                                                                   \
+            hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, \
+                                mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                          \
+            break;
+        ESA_CASE( 4 ) ESA_CASE( 8 ) ESA_CASE( 16 ) ESA_CASE( 24 )
+#undef ESA_CASE
+        default: return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL( me_esa_finish_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream, (int)nmb,
+                        me_range, par, init_cost, out );
+    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
