@@ -737,15 +737,28 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     const int y = y0 + (int)(threadIdx.x >> 2);
     // steps in which this band has blocks (block (x, y) runs at (W-1-x) + 2(H-1-y))
     const int t0 = 2 * (mbh - y1), t1 = 2 * (mbh - 1 - y0) + mbw - 1;
+    // a row's next block is x - 1: its fenc rows are fetched one step ahead
+    uint32_t fnext[LR_NR][NDW];
+    auto fetch = [&]( int t ) {
+        const int xn = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        if( y < y1 && xn >= 0 && xn < mbw )
+            lr_load_fenc<BD>( fenc + 8 * (intptr_t)xn + (intptr_t)(8 * y + LR_NR * q) * stride, stride, fnext );
+    };
+    fetch( t0 );
     for( int t = t0; t <= t1; t++ )
     {
         const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        uint32_t fe[LR_NR][NDW];
+#pragma unroll
+        for( int r = 0; r < LR_NR; r++ )
+#pragma unroll
+            for( int k = 0; k < NDW; k++ )
+                fe[r][k] = fnext[r][k];
+        fetch( t + 1 );
         if( y < y1 && x >= 0 && x < mbw )
         {
             const int mb = x + y * mbw;
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
-            uint32_t fe[LR_NR][NDW];
-            lr_load_fenc<BD>( fenc + off + (intptr_t)(LR_NR * q) * stride, stride, fe );
             LrCtx<BD> m( fe );
             m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd, q );
             uint32_t pred[4];
@@ -880,15 +893,28 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const bool hp = subme == 2;                  // h->param.analyse.i_subpel_refine <= 1
     const int y = y0 + (int)(threadIdx.x >> 2);
     const int t0 = 2 * (mbh - y1), t1 = 2 * (mbh - 1 - y0) + mbw - 1;
+    // a row's next block is x - 1: its fenc rows are fetched one step ahead
+    uint32_t fnext[LR_NR][NDW];
+    auto fetch = [&]( int t ) {
+        const int xn = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        if( y < y1 && xn >= 0 && xn < mbw )
+            lr_load_fenc<BD>( fenc + 8 * (intptr_t)xn + (intptr_t)(8 * y + LR_NR * q) * stride, stride, fnext );
+    };
+    fetch( t0 );
     for( int t = t0; t <= t1; t++ )
     {
         const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        uint32_t fe[LR_NR][NDW];
+#pragma unroll
+        for( int r = 0; r < LR_NR; r++ )
+#pragma unroll
+            for( int k = 0; k < NDW; k++ )
+                fe[r][k] = fnext[r][k];
+        fetch( t + 1 );
         if( y < y1 && x >= 0 && x < mbw )
         {
             const int mb = x + y * mbw;
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
-            uint32_t fe[LR_NR][NDW];
-            lr_load_fenc<BD>( fenc + off + (intptr_t)(LR_NR * q) * stride, stride, fe );
             LrCtx<BD> m0( fe ), m1( fe );
             m0.setup( a0, a1, a2, a3, off, stride, x, y, mbw, mbh, mvr, satd, q );
             m1.setup( b0, b1, b2, b3, off, stride, x, y, mbw, mbh, mvr, satd, q );
