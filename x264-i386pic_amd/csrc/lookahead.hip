@@ -891,15 +891,24 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const int mvr = 2 * mv_range;
     const int q = threadIdx.x & 3;
     const bool hp = subme == 2;                  // h->param.analyse.i_subpel_refine <= 1
-    const int y = y0 + (int)(threadIdx.x >> 2);
+    // The wave's four 16-lane groups (roles) work on the same <= 4 block rows at once:
+    // roles 0 and 1 run the list-0 and list-1 searches as one instruction stream (the
+    // same code on per-lane planes, ring and mvs), then roles 0, 1, 2 run the three
+    // TRY_BIDIR evaluations together (the p1-predicted pair, (0, 0), the searched pair);
+    // role 0 gathers the values and makes slicetype_mb_cost's decisions in its order.
+    const int role = (int)(threadIdx.x >> 4);
+    const int rl = (int)(threadIdx.x & 15);      // lane within the role: 4 * row + q
+    const int y = y0 + (rl >> 2);
+    const bool mine = role < 3 && y < y1;
     const int t0 = 2 * (mbh - y1), t1 = 2 * (mbh - 1 - y0) + mbw - 1;
     // a row's next block is x - 1: its fenc rows are fetched one step ahead
     uint32_t fnext[LR_NR][NDW];
     auto fetch = [&]( int t ) {
         const int xn = mbw - 1 - (t - 2 * (mbh - 1 - y));
-        if( y < y1 && xn >= 0 && xn < mbw )
+        if( mine && xn >= 0 && xn < mbw )
             lr_load_fenc<BD>( fenc + 8 * (intptr_t)xn + (intptr_t)(8 * y + LR_NR * q) * stride, stride, fnext );
     };
+    auto from_role = [&]( int v, int r ) { return __shfl( v, rl + 16 * r ); };
     fetch( t0 );
     for( int t = t0; t <= t1; t++ )
     {
@@ -911,119 +920,118 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
             for( int k = 0; k < NDW; k++ )
                 fe[r][k] = fnext[r][k];
         fetch( t + 1 );
-        if( y < y1 && x >= 0 && x < mbw )
+        const bool act = mine && x >= 0 && x < mbw;
+        const int mb = x + y * mbw;
+        const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
+        LrCtx<BD> m0( fe ), m1( fe ), ms( fe );
+        int mvx = 0, mvy = 0, lc = 0;
+        if( act )
         {
-            const int mb = x + y * mbw;
-            const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
-            LrCtx<BD> m0( fe ), m1( fe );
             m0.setup( a0, a1, a2, a3, off, stride, x, y, mbw, mbh, mvr, satd, q );
             m1.setup( b0, b1, b2, b3, off, stride, x, y, mbw, mbh, mvr, satd, q );
-            int bcost = LR_COST_MAX, list_used = 0;
-            // the predicted bidir mvs from p1's list-0 mvs (slicetype.c:623-645)
-            int d0x = 0, d0y = 0, d1x = 0, d1y = 0;
-            if( p1mvs )
+            if( role < 2 )
             {
-                const int rx = p1mvs[2 * mb], ry = p1mvs[2 * mb + 1];
-                d0x = (rx * dsf + 128) >> 8;
-                d0y = (ry * dsf + 128) >> 8;
-                d1x = lr_clip3( d0x - rx, m0.smin0, m0.smax0 );
-                d1y = lr_clip3( d0y - ry, m0.smin1, m0.smax1 );
-                d0x = lr_clip3( d0x, m0.smin0, m0.smax0 );
-                d0y = lr_clip3( d0y, m0.smin1, m0.smax1 );
-                if( hp )
+                // the searching lanes' own context: list `role`'s planes (a per-lane choice
+                // of pointers, not of objects, so nothing goes to scratch)
+                ms.setup( role ? b0 : a0, role ? b1 : a1, role ? b2 : a2, role ? b3 : a3, off, stride, x, y, mbw,
+                          mbh, mvr, satd, q );
+                // list `role`: searched on the wavefront (search & (1 << role)) or read
+                int *ring = role ? ring1 : ring0;
+                uint32_t *gmv = role ? gmv1 : gmv0;
+                int32_t *costs = role ? costs1 : costs0;
+                if( search & (1 << role) )
                 {
-                    d0x &= ~1; d0y &= ~1; d1x &= ~1; d1y &= ~1;
+                    uint32_t pred[4];
+                    const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred );
+                    lc = lr_list<BD>( ms, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy );
+                    if( q == 0 )
+                    {
+                        ring[4 * (y - y0) + (x & 3)] = (int)lr_pack( mvx, mvy );
+                        lr_store_mv( gmv + mb, lr_pack( mvx, mvy ) );
+                        costs[mb] = lc;
+                    }
+                }
+                else
+                {
+                    const uint32_t v = gmv[mb];
+                    mvx = (int16_t)(v & 0xffff);
+                    mvy = (int16_t)(v >> 16);
+                    lc = costs[mb];
                 }
             }
-            int c = lr_bidir<BD>( m0, m1, d0x, d0y, d1x, d1y, hp, weight );
-            if( c < bcost )
+        }
+        const int mv0x = from_role( mvx, 0 ), mv0y = from_role( mvy, 0 ), lc0 = from_role( lc, 0 );
+        const int mv1x = from_role( mvx, 1 ), mv1y = from_role( mvy, 1 ), lc1 = from_role( lc, 1 );
+        // the predicted bidir mvs from p1's list-0 mvs (slicetype.c:623-645)
+        int d0x = 0, d0y = 0, d1x = 0, d1y = 0;
+        if( act && p1mvs )
+        {
+            const int rx = p1mvs[2 * mb], ry = p1mvs[2 * mb + 1];
+            d0x = (rx * dsf + 128) >> 8;
+            d0y = (ry * dsf + 128) >> 8;
+            d1x = lr_clip3( d0x - rx, m0.smin0, m0.smax0 );
+            d1y = lr_clip3( d0y - ry, m0.smin1, m0.smax1 );
+            d0x = lr_clip3( d0x, m0.smin0, m0.smax0 );
+            d0y = lr_clip3( d0y, m0.smin1, m0.smax1 );
+            if( hp )
             {
-                bcost = c;
+                d0x &= ~1; d0y &= ~1; d1x &= ~1; d1y &= ~1;
+            }
+        }
+        const bool dnz = (d0x | d0y | d1x | d1y) != 0, mvnz = (mv0x | mv0y | mv1x | mv1y) != 0;
+        // TRY_BIDIR: role 0 the predicted pair, role 1 (0, 0) (when the prediction is not
+        // zero), role 2 the searched pair (when not zero)
+        int cb = LR_COST_MAX;
+        if( act && (role == 0 || (role == 1 && dnz) || (role == 2 && mvnz)) )
+        {
+            const int ax = role == 0 ? d0x : role == 2 ? mv0x : 0, ay = role == 0 ? d0y : role == 2 ? mv0y : 0;
+            const int bx = role == 0 ? d1x : role == 2 ? mv1x : 0, by = role == 0 ? d1y : role == 2 ? mv1y : 0;
+            cb = lr_bidir<BD>( m0, m1, ax, ay, bx, by, role == 1 ? true : hp, weight );
+        }
+        const int cpred = from_role( cb, 0 ), czero = from_role( cb, 1 ), cmv = from_role( cb, 2 );
+        if( act && role == 0 && q == 0 )
+        {
+            int bcost = LR_COST_MAX, list_used = 0;
+            if( cpred < bcost )
+            {
+                bcost = cpred;
                 list_used = 3;
             }
-            if( d0x | d0y | d1x | d1y )
+            if( dnz && czero < bcost )
             {
-                c = lr_bidir<BD>( m0, m1, 0, 0, 0, 0, true, weight );
-                if( c < bcost )
-                {
-                    bcost = c;
-                    list_used = 3;
-                }
+                bcost = czero;
+                list_used = 3;
             }
-            int mv0x, mv0y, mv1x, mv1y, lc;
-            if( search & 1 )
+            if( lc0 < bcost )
             {
-                uint32_t pred[4];
-                const int np = lr_preds( ring0, y0, y1, gmv0, x, y, mbw, mbh, pred );
-                lc = lr_list<BD>( m0, pred, np, me_method, subme, me_range, lambda, cml, mv0x, mv0y );
-                if( q == 0 )
-                {
-                    ring0[4 * (y - y0) + (x & 3)] = (int)lr_pack( mv0x, mv0y );
-                    lr_store_mv( gmv0 + mb, lr_pack( mv0x, mv0y ) );
-                    costs0[mb] = lc;
-                }
-            }
-            else
-            {
-                mv0x = mvs0[2 * mb];
-                mv0y = mvs0[2 * mb + 1];
-                lc = costs0[mb];
-            }
-            if( lc < bcost )
-            {
-                bcost = lc;
+                bcost = lc0;
                 list_used = 1;
             }
-            if( search & 2 )
+            if( lc1 < bcost )
             {
-                uint32_t pred[4];
-                const int np = lr_preds( ring1, y0, y1, gmv1, x, y, mbw, mbh, pred );
-                lc = lr_list<BD>( m1, pred, np, me_method, subme, me_range, lambda, cml, mv1x, mv1y );
-                if( q == 0 )
-                {
-                    ring1[4 * (y - y0) + (x & 3)] = (int)lr_pack( mv1x, mv1y );
-                    lr_store_mv( gmv1 + mb, lr_pack( mv1x, mv1y ) );
-                    costs1[mb] = lc;
-                }
-            }
-            else
-            {
-                mv1x = mvs1[2 * mb];
-                mv1y = mvs1[2 * mb + 1];
-                lc = costs1[mb];
-            }
-            if( lc < bcost )
-            {
-                bcost = lc;
+                bcost = lc1;
                 list_used = 2;
             }
-            if( mv0x | mv0y | mv1x | mv1y )
+            if( mvnz && 5 * lambda + cmv < bcost )
             {
-                c = 5 * lambda + lr_bidir<BD>( m0, m1, mv0x, mv0y, mv1x, mv1y, hp, weight );
-                if( c < bcost )
-                {
-                    bcost = c;
-                    list_used = 3;
-                }
+                bcost = 5 * lambda + cmv;
+                list_used = 3;
             }
-            if( q == 0 )
+            // slicetype.c:758-790 (no intra in B frames)
+            bcost = (bcost >> (BD - 8)) + 4;
+            const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
+            const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
+            racc += aq;
+            if( fsm )
             {
-                // slicetype.c:758-790 (no intra in B frames)
-                bcost = (bcost >> (BD - 8)) + 4;
-                const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
-                const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
-                racc += aq;
-                if( fsm )
-                {
-                    e0 += bcost;
-                    e1 += aq;
-                }
-                lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
+                e0 += bcost;
+                e1 += aq;
             }
+            lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
         }
         __syncthreads();
     }
-    if( q == 0 && y < y1 && row_satd )
+    if( role == 0 && q == 0 && y < y1 && row_satd )
         row_satd[(intptr_t)f * mbh + y] = racc;
     if( est && (e0 | e1) )
     {
@@ -1062,7 +1070,8 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
     // P 2.46 / 2.32 / 2.19 / 2.26 ms, B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2)
     const int bv = variant( V_LA_BAND );
     const int brows = bv >= 1 && bv <= LR_BAND ? bv : 4;
-    const int nbands = (mbh + brows - 1) / brows;
+    const int brows4 = min( brows, 4 );          // a wave holds four roles of <= 4 rows
+    const int nbands = (mbh + brows4 - 1) / brows4;
     if( (int64_t)n * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
@@ -1071,7 +1080,7 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
     hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ra[0], ra[1],
                         ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method, subme, satd,
                         me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, weight,
-                        invq, lowres_costs, row_satd, est, nbands, brows );
+                        invq, lowres_costs, row_satd, est, nbands, brows4 );
     return hipGetLastError();
 }
 
