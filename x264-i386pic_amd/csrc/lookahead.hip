@@ -253,9 +253,18 @@ template <int BD> struct LrCtx
 };
 
 // x264_me_search_ref (me.c:182-420, 774-790) then refine_subpel (me.c:912-992)
+// role >= 0: the wave's four 16-lane groups run this same search on the same block in
+// lockstep and split each batch of independent candidates (the predictors, the hpel and
+// qpel diamonds): group r scores candidate r, the costs are gathered from the groups
+// and every group makes the same decisions.  role < 0: one group scores them in turn.
+__device__ __forceinline__ int lr_gather( int v, int r )
+{
+    return __shfl( v, (int)(threadIdx.x & 15) + 16 * r );
+}
+
 template <int BD>
 __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int (&mvc)[4][2], int i_mvc,
-                              int me_method, int subme, int me_range, int &omvx, int &omvy, int &ocost )
+                              int me_method, int subme, int me_range, int role, int &omvx, int &omvy, int &ocost )
 {
     int bmx, bmy, bcost = LR_COST_MAX, bpred_cost = LR_COST_MAX;
     uint32_t pmv, bpred_mv = 0;
@@ -275,8 +284,6 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
     {
         int bpx = lr_clip3( mvpx, 4 * m.fmin0, 4 * m.fmax0 ), bpy = lr_clip3( mvpy, 4 * m.fmin1, 4 * m.fmax1 );
         pmv = lr_pack( bpx, bpy );
-        bpred_cost = m.qpel( bpx, bpy, false ) + m.cmx[bpx] + m.cmy[bpy];            // COST_MV_HPEL
-        const int pmv_cost = bpred_cost;
         int valid = 0;
         for( int i = 0; i < i_mvc; i++ )                                              // x264_predictor_clip
         {
@@ -287,15 +294,31 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
             tmp[2 + valid][1] = lr_clip3( mvc[i][1], 4 * m.fmin1, 4 * m.fmax1 );
             valid++;
         }
+        tmp[1][0] = bpx;
+        tmp[1][1] = bpy;
+        // COST_MV_HPEL of slot 0 (the clipped mvp) and of the valid predictors
+        int cpred[4] = { 0, 0, 0, 0 };
+        if( role >= 0 )
+        {
+            const int j = role <= valid ? role : 0;
+            const int mx = tmp[j + 1][0], my = tmp[j + 1][1];
+            const int c = m.qpel( mx, my, false ) + m.cmx[mx] + m.cmy[my];
+#pragma unroll
+            for( int r = 0; r < 4; r++ )
+                cpred[r] = lr_gather( c, r );
+        }
+        else
+            cpred[0] = m.qpel( bpx, bpy, false ) + m.cmx[bpx] + m.cmy[bpy];
+        bpred_cost = cpred[0];
+        const int pmv_cost = bpred_cost;
         if( valid > 0 )
         {
-            tmp[1][0] = bpx;
-            tmp[1][1] = bpy;
             bpred_cost <<= 4;
             for( int i = 1; i <= valid; i++ )
             {
                 const int mx = tmp[i + 1][0], my = tmp[i + 1][1];
-                const int c = m.qpel( mx, my, false ) + m.cmx[mx] + m.cmy[my];
+                const int c = role >= 0 && i < 4 ? (i == 1 ? cpred[1] : i == 2 ? cpred[2] : cpred[3])
+                                                 : m.qpel( mx, my, false ) + m.cmx[mx] + m.cmy[my];
                 if( (c << 4) + i < bpred_cost )
                     bpred_cost = (c << 4) + i;
             }
@@ -511,10 +534,21 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         for( int i = hpel; i > 0; i-- )
         {
             const int omx = bmx, omy = bmy;
-            costs[0] = m.qpel( omx, omy - 2, false ) + m.cmx[omx] + m.cmy[omy - 2];
-            costs[1] = m.qpel( omx, omy + 2, false ) + m.cmx[omx] + m.cmy[omy + 2];
-            costs[2] = m.qpel( omx - 2, omy, false ) + m.cmx[omx - 2] + m.cmy[omy];
-            costs[3] = m.qpel( omx + 2, omy, false ) + m.cmx[omx + 2] + m.cmy[omy];
+            if( role >= 0 )
+            {
+                const int qx = omx + (role == 2 ? -2 : role == 3 ? 2 : 0), qy = omy + (role == 0 ? -2 : role == 1 ? 2 : 0);
+                const int c = m.qpel( qx, qy, false ) + m.cmx[qx] + m.cmy[qy];
+#pragma unroll
+                for( int r = 0; r < 4; r++ )
+                    costs[r] = lr_gather( c, r );
+            }
+            else
+            {
+                costs[0] = m.qpel( omx, omy - 2, false ) + m.cmx[omx] + m.cmy[omy - 2];
+                costs[1] = m.qpel( omx, omy + 2, false ) + m.cmx[omx] + m.cmy[omy + 2];
+                costs[2] = m.qpel( omx - 2, omy, false ) + m.cmx[omx - 2] + m.cmy[omy];
+                costs[3] = m.qpel( omx + 2, omy, false ) + m.cmx[omx + 2] + m.cmy[omy];
+            }
             bcost = min( bcost, (costs[0] << 6) + 2 );
             bcost = min( bcost, (costs[1] << 6) + 6 );
             bcost = min( bcost, (costs[2] << 6) + 16 );
@@ -536,13 +570,22 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
             break;
         const int odir = bdir;
         const int omx = bmx, omy = bmy;
+        int cq[4] = { 0, 0, 0, 0 };
+        if( role >= 0 )
+        {
+            const int qx = omx + (role == 2 ? -1 : role == 3 ? 1 : 0), qy = omy + (role == 0 ? -1 : role == 1 ? 1 : 0);
+            const int c = m.qpel( qx, qy, m.satd ) + m.cmx[qx] + m.cmy[qy];
+#pragma unroll
+            for( int r = 0; r < 4; r++ )
+                cq[r] = lr_gather( c, r );
+        }
 #pragma unroll
         for( int dir = 0; dir < 4; dir++ )
         {
             if( (dir ^ 1) == odir )
                 continue;
             const int qx = omx + (dir == 2 ? -1 : dir == 3 ? 1 : 0), qy = omy + (dir == 0 ? -1 : dir == 1 ? 1 : 0);
-            const int cc = m.qpel( qx, qy, m.satd ) + m.cmx[qx] + m.cmy[qy];
+            const int cc = role >= 0 ? cq[dir] : m.qpel( qx, qy, m.satd ) + m.cmx[qx] + m.cmy[qy];
             if( cc < bcost )
             {
                 bcost = cc;
@@ -564,7 +607,8 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
 // adjustments.  Returns the list cost; mvx / mvy the list's mv.
 template <int BD>
 __device__ __forceinline__ int lr_list( LrCtx<BD> &m, const uint32_t (&pred)[4], int npred, int me_method, int subme,
-                                        int me_range, int lambda, const uint16_t *cost_mv, int &mvx, int &mvy )
+                                        int me_range, int lambda, const uint16_t *cost_mv, int &mvx, int &mvy,
+                                        int role = -1 )
 {
     int mvc[4][2] = { { 0, 0 }, { 0, 0 }, { 0, 0 }, { 0, 0 } };
     const int i_mvc = npred;
@@ -598,7 +642,7 @@ __device__ __forceinline__ int lr_list( LrCtx<BD> &m, const uint32_t (&pred)[4],
     }
     if( !skip )
     {
-        lr_me_search<BD>( m, mvpx, mvpy, mvc, i_mvc, me_method, subme, me_range, mvx, mvy, cost );
+        lr_me_search<BD>( m, mvpx, mvpy, mvc, i_mvc, me_method, subme, me_range, role, mvx, mvy, cost );
         cost -= cost_mv[0];
         if( mvx | mvy )
             cost += 5 * lambda;
@@ -734,7 +778,10 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     int e0 = 0, e1 = 0, e2 = 0, racc = 0;
     const int mvr = 2 * mv_range;
     const int q = threadIdx.x & 3;
-    const int y = y0 + (int)(threadIdx.x >> 2);
+    // four 16-lane groups run each row's search together and split its candidate batches
+    // (lr_me_search's role); group 0 writes the results
+    const int role = (int)(threadIdx.x >> 4);
+    const int y = y0 + (int)((threadIdx.x & 15) >> 2);
     // steps in which this band has blocks (block (x, y) runs at (W-1-x) + 2(H-1-y))
     const int t0 = 2 * (mbh - y1), t1 = 2 * (mbh - 1 - y0) + mbw - 1;
     // a row's next block is x - 1: its fenc rows are fetched one step ahead
@@ -764,8 +811,8 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
             uint32_t pred[4];
             const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred );
             int mvx, mvy;
-            const int cost = lr_list<BD>( m, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy );
-            if( q == 0 )
+            const int cost = lr_list<BD>( m, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy, role );
+            if( q == 0 && role == 0 )
             {
                 ring[4 * (y - y0) + (x & 3)] = (int)lr_pack( mvx, mvy );
                 lr_store_mv( gmv + mb, lr_pack( mvx, mvy ) );
@@ -793,7 +840,7 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
         }
         __syncthreads();
     }
-    if( q == 0 && y < y1 && row_satd )
+    if( q == 0 && role == 0 && y < y1 && row_satd )
         row_satd[(intptr_t)f * mbh + y] = racc;
     if( est && (e0 | e1 | e2) )
     {
@@ -1106,7 +1153,8 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     // P 2.46 / 2.32 / 2.19 / 2.26 ms, B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2)
     const int bv = variant( V_LA_BAND );
     const int brows = bv >= 1 && bv <= LR_BAND ? bv : 4;
-    const int nbands = (mbh + brows - 1) / brows;
+    const int brows4 = min( brows, 4 );          // four groups of <= 4 rows per wave
+    const int nbands = (mbh + brows4 - 1) / brows4;
     if( (int64_t)npairs * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
@@ -1114,7 +1162,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
         return hipErrorInvalidValue;
     hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ref[0],
                         ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
-                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows );
+                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4 );
     return hipGetLastError();
 }
 
