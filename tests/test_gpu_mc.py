@@ -117,10 +117,13 @@ def test_subpel_qpel9_random(hip, oracle, bd, op):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("size", [(1920, 1088), (176, 144), (72, 40)])
-def test_frame_init_lowres(hip, oracle, bd, size):
-    """x264_frame_init_lowres of 3 frames per call vs the oracle; the source padding holds
-    unrelated values (the reference duplicates column W / row H itself)."""
+@pytest.mark.parametrize("size", [(1920, 1088), (176, 144), (72, 40), (3840, 2160), (48, 32)])
+@pytest.mark.parametrize("variant", ["default", "1", "2", "3", "4"])
+def test_frame_init_lowres(hip, oracle, bd, size, variant):
+    """x264_frame_init_lowres of 3 frames per call vs the oracle (every kernel variant); the
+    source padding holds unrelated values (the reference duplicates column W / row H itself)."""
+    if variant != "default":
+        _x().set_variant("X264HIP_LOWRES_VARIANT", variant)
     W, H = size
     n = 3
     rs = np.random.default_rng(bd * 7 + W)

@@ -3,7 +3,8 @@
 // over the same padded 1080p plane geometry and frame count as the hpel bench
 // leg.  Variants: 1 = the streaming kernel's grid (a wave per 62-piece column
 // chunk x ROWS-row strip), 2 = a plain grid-stride copy of the same bytes
-// (1 plane in, 3 out), 3 = a plain 1-in-1-out copy of one plane (reference).
+// (1 plane in, 3 out), 3 = a plain 1-in-1-out copy of one plane (reference), 4 = the
+// frame_init_lowres pattern (three source rows per output row, four half-width planes out).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -25,6 +26,33 @@ __global__ __launch_bounds__( 64 ) void strip3( const uint8_t *src, uint8_t *a, 
         *(uint4 *)(a + fo + r * stride) = v;
         *(uint4 *)(b + fo + r * stride) = v;
         *(uint4 *)(c + fo + r * stride) = v;
+    }
+}
+
+// frame_init_lowres pattern: per output row read source rows 2y, 2y+1, 2y+2 (32 bytes per
+// lane each), write 16 bytes per lane to four half-width planes
+__global__ __launch_bounds__( 64 ) void lowres4( const uint8_t *src, uint8_t *a, uint8_t *b, uint8_t *c, uint8_t *d,
+                                                 long stride, long fstride, long ds, long dfs, int lanes, int hl )
+{
+    const int k = threadIdx.x;
+    if( k >= lanes )
+        return;
+    for( int rr = 0; rr < 2; rr++ )
+    {
+        const int y = blockIdx.y * 2 + rr;
+        if( y >= hl )
+            return;
+        const uint8_t *s = src + blockIdx.z * fstride + (long)(2 * y) * stride + 32 * k;
+        const uint4 x0 = *(const uint4 *)s, x1 = *(const uint4 *)(s + 16);
+        const uint4 y0 = *(const uint4 *)(s + stride), y1 = *(const uint4 *)(s + stride + 16);
+        const uint4 z0 = *(const uint4 *)(s + 2 * stride), z1 = *(const uint4 *)(s + 2 * stride + 16);
+        const uint4 v = make_uint4( x0.x ^ x1.x ^ y0.x ^ y1.x ^ z0.x ^ z1.x, x0.y ^ x1.y ^ y0.y, x0.z ^ y1.z ^ z0.z,
+                                    x1.w ^ y0.w ^ z1.w );
+        const long o = blockIdx.z * dfs + (long)y * ds + 16 * k;
+        *(uint4 *)(a + o) = v;
+        *(uint4 *)(b + o) = v;
+        *(uint4 *)(c + o) = v;
+        *(uint4 *)(d + o) = v;
     }
 }
 
@@ -56,7 +84,11 @@ int main( int argc, char **argv )
     hipEvent_t e0, e1;
     hipEventCreate( &e0 ); hipEventCreate( &e1 );
     const int pieces = (int)(stride / 16);
-    for( int v = 1; v <= 3; v++ )
+    uint8_t *l[4];
+    const long ds = 1024, dfs = ds * (544 + 64), lbytes = F * dfs;
+    for( int i = 0; i < 4; i++ )
+        hipMalloc( &l[i], lbytes );
+    for( int v = 1; v <= 4; v++ )
     {
         auto run = [&]() {
             if( v == 1 )
@@ -65,8 +97,11 @@ int main( int argc, char **argv )
             else if( v == 2 )
                 hipLaunchKernelGGL( flat3, dim3( 4096 ), dim3( 256 ), 0, 0, (const uint4 *)s, (uint4 *)a, (uint4 *)b,
                                     (uint4 *)c, bytes / 16 );
-            else
+            else if( v == 3 )
                 hipLaunchKernelGGL( flat1, dim3( 4096 ), dim3( 256 ), 0, 0, (const uint4 *)s, (uint4 *)a, bytes / 16 );
+            else
+                hipLaunchKernelGGL( lowres4, dim3( 1, 272, F ), dim3( 64 ), 0, 0, s, l[0], l[1], l[2], l[3], stride,
+                                    fstride, ds, dfs, 60, 544 );
         };
         for( int i = 0; i < 300; i++ )
             run();
@@ -78,7 +113,7 @@ int main( int argc, char **argv )
         float ms;
         hipEventElapsedTime( &ms, e0, e1 );
         ms /= 100;
-        const double moved = v == 3 ? 2.0 * bytes : 4.0 * bytes;
+        const double moved = v == 3 ? 2.0 * bytes : v == 4 ? (double)F * (1088 * 1920 + 4 * 544 * 960) : 4.0 * bytes;
         printf( "variant %d: %.4f ms, %.2f TB/s, %.3f of 8 TB/s\n", v, ms, moved / ms / 1e9, moved / ms / 1e9 / 8.0 );
     }
     return 0;

@@ -1271,6 +1271,143 @@ __global__ __launch_bounds__( 128 ) void lowres16_kernel( const uint8_t *__restr
     }
 }
 
+// 8 bit, default: one single-wave workgroup per R output rows of all four planes.
+// Lane k < wl/16 makes output columns 16k .. 16k+15 as in lowres16_kernel; in the last
+// group the source column 2*16k+32 the run ends on would be column W, which the
+// reference duplicates from W-1 (mc.c:465-468), so that one byte is taken from W-1.
+// The wl % 16 columns left over (widths that are not a multiple of 32) go to the next
+// lanes through the clamped per-pixel form, four columns each.  The 32-pixel borders
+// are replicas of columns 0 and wl-1 (plane_expand_border, frame.c:627-631), stored by
+// the lanes that hold those columns: no border wave, every lane's loads for its R rows
+// independent of the other rows.
+template <int R>
+__global__ __launch_bounds__( 64 ) void lowres_rows_kernel( const uint8_t *__restrict__ src, intptr_t stride,
+                                                            intptr_t fstride, int width, int height,
+                                                            uint8_t *__restrict__ d0, uint8_t *__restrict__ dh,
+                                                            uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                            intptr_t ds, intptr_t dfs )
+{
+    constexpr int PAD = 32;
+    const int wl = width / 2, hl = height / 2;
+    const int f = blockIdx.z;
+    const uint8_t *s = src + f * fstride;
+    const int nfull = wl / 16;
+    const int nrem = (wl - 16 * nfull + 3) / 4;               // clamped groups of 4 columns
+    uint8_t *const dst[4] = { d0, dh, dv, dc };
+    auto splat = []( uint32_t w, int byte ) { return __builtin_amdgcn_perm( 0u, w, 0x01010101u * (uint32_t)byte ); };
+    for( int k = threadIdx.x; k < nfull + nrem; k += 64 )
+    {
+#pragma unroll
+        for( int rr = 0; rr < R; rr++ )
+        {
+            const int y = (int)blockIdx.y * R + rr - PAD;
+            const bool live = y < hl + PAD;
+            const int yc = min( max( y, 0 ), hl - 1 );
+            const uint8_t *r0 = s + (intptr_t)(2 * yc) * stride;
+            const uint8_t *r1 = s + (intptr_t)min( 2 * yc + 1, height - 1 ) * stride;
+            const uint8_t *r2 = s + (intptr_t)min( 2 * yc + 2, height - 1 ) * stride;
+            const intptr_t orow = f * dfs + (intptr_t)y * ds;
+            if( k < nfull )
+            {
+                const int xg = 16 * k;
+                const bool edge = 2 * xg + 32 >= width;      // the run's last column is W: take W-1
+                uint32_t E[3][5], O[3][4];
+                const uint8_t *rp[3] = { r0, r1, r2 };
+#pragma unroll
+                for( int r = 0; r < 3; r++ )
+                {
+                    const uint4 a = *(const uint4 *)(rp[r] + 2 * xg), b = *(const uint4 *)(rp[r] + 2 * xg + 16);
+                    const uint32_t v[8] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w };
+#pragma unroll
+                    for( int j = 0; j < 4; j++ )
+                    {
+                        E[r][j] = __builtin_amdgcn_perm( v[2 * j + 1], v[2 * j], 0x06040200u );
+                        O[r][j] = __builtin_amdgcn_perm( v[2 * j + 1], v[2 * j], 0x07050301u );
+                    }
+                    E[r][4] = edge ? b.w >> 24 : *(const uint32_t *)(rp[r] + 2 * xg + 32);
+                }
+                uint32_t w[4][4];
+#pragma unroll
+                for( int j = 0; j < 4; j++ )
+                {
+                    auto avg = []( uint32_t p, uint32_t q ) { return __builtin_amdgcn_lerp( p, q, 0x01010101u ); };
+                    const uint32_t x0 = __builtin_amdgcn_alignbyte( E[0][j + 1], E[0][j], 1 );
+                    const uint32_t x1 = __builtin_amdgcn_alignbyte( E[1][j + 1], E[1][j], 1 );
+                    const uint32_t x2 = __builtin_amdgcn_alignbyte( E[2][j + 1], E[2][j], 1 );
+                    const uint32_t e01 = avg( E[0][j], E[1][j] ), o01 = avg( O[0][j], O[1][j] ), x01 = avg( x0, x1 );
+                    const uint32_t e12 = avg( E[1][j], E[2][j] ), o12 = avg( O[1][j], O[2][j] ), x12 = avg( x1, x2 );
+                    w[0][j] = avg( e01, o01 );
+                    w[1][j] = avg( o01, x01 );
+                    w[2][j] = avg( e12, o12 );
+                    w[3][j] = avg( o12, x12 );
+                }
+                if( live )
+                {
+                    const intptr_t o = orow + xg;
+#pragma unroll
+                    for( int pl = 0; pl < 4; pl++ )
+                    {
+                        *(uint4 *)(dst[pl] + o) = make_uint4( w[pl][0], w[pl][1], w[pl][2], w[pl][3] );
+                        if( k == 0 )
+                        {
+                            // left border: column 0 repeated over x in [-32, 0)
+                            const uint32_t bb = splat( w[pl][0], 0 );
+                            *(uint4 *)(dst[pl] + orow - 32) = make_uint4( bb, bb, bb, bb );
+                            *(uint4 *)(dst[pl] + orow - 16) = make_uint4( bb, bb, bb, bb );
+                        }
+                        if( k == nfull - 1 && !nrem )
+                        {
+                            // right border: column wl-1 repeated over x in [wl, wl+32)
+                            const uint32_t bb = splat( w[pl][3], 3 );
+                            *(uint4 *)(dst[pl] + o + 16) = make_uint4( bb, bb, bb, bb );
+                            *(uint4 *)(dst[pl] + o + 32) = make_uint4( bb, bb, bb, bb );
+                        }
+                    }
+                }
+            }
+            else
+            {
+                const int xg = 16 * nfull + 4 * (k - nfull);
+                uint32_t w[4] = { 0, 0, 0, 0 };
+#define FILTER( a, b, c, d ) ((((a + b + 1) >> 1) + ((c + d + 1) >> 1) + 1) >> 1)
+#pragma unroll
+                for( int j = 0; j < 4; j++ )
+                {
+                    const int xc = min( xg + j, wl - 1 );
+                    const int c0 = 2 * xc, c1 = min( 2 * xc + 1, width - 1 ), c2 = min( 2 * xc + 2, width - 1 );
+                    const int a0 = r0[c0], a1 = r0[c1], a2 = r0[c2];
+                    const int b0 = r1[c0], b1 = r1[c1], b2 = r1[c2];
+                    const int e0 = r2[c0], e1 = r2[c1], e2 = r2[c2];
+                    w[0] |= (uint32_t)FILTER( a0, b0, a1, b1 ) << (8 * j);
+                    w[1] |= (uint32_t)FILTER( a1, b1, a2, b2 ) << (8 * j);
+                    w[2] |= (uint32_t)FILTER( b0, e0, b1, e1 ) << (8 * j);
+                    w[3] |= (uint32_t)FILTER( b1, e1, b2, e2 ) << (8 * j);
+                }
+#undef FILTER
+                if( live )
+                {
+                    const bool last = k == nfull + nrem - 1;
+                    const int nv = wl - xg;                  // valid columns of this group (1..4)
+#pragma unroll
+                    for( int pl = 0; pl < 4; pl++ )
+                    {
+                        uint32_t v = w[pl];
+                        if( last )
+                        {
+                            // columns past wl - 1 repeat it: fill the group, then x in [xg+4, wl+32)
+                            const uint32_t bb = splat( v, nv - 1 );
+                            v = nv >= 4 ? v : (v & (0xFFFFFFFFu >> (8 * (4 - nv)))) | (bb & (0xFFFFFFFFu << (8 * nv)));
+                            for( int x = xg + 4; x < wl + PAD; x += 4 )
+                                *(uint32_t *)(dst[pl] + orow + x) = bb;
+                        }
+                        *(uint32_t *)(dst[pl] + orow + xg) = v;
+                    }
+                }
+            }
+        }
+    }
+}
+
 template <int BD>
 hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t stride, intptr_t fstride, int width,
                                      int height, int nframes, typename PT<BD>::pixel *const dst[4], intptr_t ds,
@@ -1282,11 +1419,28 @@ hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t
     if constexpr( BD == 8 )
     {
         // 16-pixel lanes with 16-byte loads and stores: needs 16-byte aligned rows and a
-        // width of whole macroblocks (X264HIP_LOWRES_VARIANT=1 selects the dword kernel)
+        // width of whole macroblocks (X264HIP_LOWRES_VARIANT=1 selects the dword kernel,
+        // 2 the one-row-per-workgroup kernel with its separate border wave)
         const int ev = variant( V_LOWRES );
         const uintptr_t al = (uintptr_t)src | (uintptr_t)stride | (uintptr_t)fstride | (uintptr_t)dst[0] |
                              (uintptr_t)dst[1] | (uintptr_t)dst[2] | (uintptr_t)dst[3] | (uintptr_t)ds | (uintptr_t)dfs;
-        if( ev != 1 && !(al & 15) && !(width & 15) )
+        if( ev != 1 && ev != 2 && !(al & 15) && !(width & 15) )
+        {
+            // X264HIP_LOWRES_VARIANT = 3 / 4: one / four output rows per wave (default two)
+            const int R = ev == 3 ? 1 : ev == 4 ? 4 : 2;
+            dim3 gr( 1, (unsigned)((hl + 64 + R - 1) / R), (unsigned)nframes );
+            if( R == 1 )
+                hipLaunchKernelGGL( lowres_rows_kernel<1>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
+                                    dst[0], dst[1], dst[2], dst[3], ds, dfs );
+            else if( R == 4 )
+                hipLaunchKernelGGL( lowres_rows_kernel<4>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
+                                    dst[0], dst[1], dst[2], dst[3], ds, dfs );
+            else
+                hipLaunchKernelGGL( lowres_rows_kernel<2>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
+                                    dst[0], dst[1], dst[2], dst[3], ds, dfs );
+            return hipGetLastError();
+        }
+        if( ev == 2 && !(al & 15) && !(width & 15) )
         {
             dim3 g16( 1, (unsigned)(hl + 64), (unsigned)nframes );
             hipLaunchKernelGGL( lowres16_kernel, g16, dim3( 128 ), 0, st, src, stride, fstride, width, height, dst[0],
