@@ -682,16 +682,25 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
     const int n = width > 0 && max_y >= min_y ? width * (max_y - min_y + 1) : 0;
     const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
     const typename PT<BD>::sadt *t = table + mb * (int64_t)(W * P);
+    // lane = window column (width <= 64), rows walked in order: coalesced table reads and
+    // no division per candidate
     uint32_t key = 0xFFFFFFFFu;
-    for( int i = lane; i < n; i += 64 )
+    if( n > 0 && lane < width )
     {
-        const int dy = i / width, dx = i - dy * width;
-        const int mx = min_x + dx, my = min_y + dy;
-        const int tx = mx - ox, ty = my - oy;
-        if( tx < 0 || tx >= W || ty < 0 || ty >= W )
-            continue;                                   // outside the table: not evaluated
-        const uint32_t cost = (uint32_t)t[ty * P + tx] + cost_mv[mx * 4 - mvpx] + cost_mv[my * 4 - mvpy];
-        key = min( key, (cost << 12) | (uint32_t)i );
+        const int mx = min_x + lane, tx = mx - ox;
+        const bool colin = tx >= 0 && tx < W;
+        const uint32_t cxv = colin ? cost_mv[mx * 4 - mvpx] : 0u;
+        // rows in table order, unrolled with the loads independent of each other; a row or
+        // column outside the table is read clamped and masked out of the minimum
+        const int y0 = max( min_y, oy ), y1 = min( max_y, oy + W - 1 );
+        const typename PT<BD>::sadt *col = t + min( max( tx, 0 ), W - 1 );
+#pragma unroll 8
+        for( int my = y0; my <= y1; my++ )
+        {
+            const uint32_t cost = (uint32_t)col[(my - oy) * P] + cxv + cost_mv[my * 4 - mvpy];
+            const uint32_t k = (cost << 12) | (uint32_t)((my - min_y) * width + lane);
+            key = min( key, colin ? k : 0xFFFFFFFFu );
+        }
     }
 #pragma unroll
     for( int off = 32; off >= 1; off >>= 1 )
@@ -771,24 +780,40 @@ __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
     return v;
 }
 
-template <int BD, int NR>
+// SEG lanes per MB: 64 (one MB per wave, me_range <= 32) or 32 (two MBs per wave,
+// me_range <= 16: a row of <= 32 columns fits half a wave), so a wave's serial row
+// chain serves two MBs.  Every per-MB value is uniform within its segment; ballots are
+// masked to the segment, scans and reductions stay inside it, and loops run while any
+// segment still needs them.
+template <int BD, int NR, int SEG>
 __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
                                                         intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
                                                         intptr_t rs, intptr_t rfs,
                                                         const uint16_t *__restrict__ integral, intptr_t ifs, int mbw,
-                                                        int mbh, int me_range, int satd,
+                                                        int mbh, int nmb, int me_range, int satd,
                                                         const typename PT<BD>::sadt *__restrict__ table, int R,
                                                         const int16_t *__restrict__ origin,
                                                         const int16_t *__restrict__ par,
                                                         const int32_t *__restrict__ init_cost,
-                                                        const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out )
+                                                        const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out,
+                                                        int cap )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int NDW = 16 / PT<BD>::PPD;                     // dwords per fenc row
-    extern __shared__ uint64_t mvsads[];                      // { sad, mx | my << 16 }
-    __shared__ uint32_t fl[16 * NDW];
-    const int lane = threadIdx.x;
-    const int64_t mb = blockIdx.x;
+    constexpr int NSEG = 64 / SEG;
+    extern __shared__ uint64_t tesa_lds[];                    // NSEG lists of { sad, mx | my << 16 }
+    __shared__ uint32_t fls[NSEG][16 * NDW];
+    const int sg = (int)threadIdx.x / SEG, lane = (int)threadIdx.x % SEG;
+    const int64_t mbo = (int64_t)blockIdx.x * NSEG + sg;      // this segment's MB
+    const int64_t mb = mbo < nmb ? mbo : nmb - 1;             // a spare segment repeats the last MB
+    const uint64_t segmask = SEG == 64 ? ~0ull : 0xFFFFFFFFull << (32 * sg);
+    uint64_t *mvsads = tesa_lds + (int64_t)sg * cap;
+    uint32_t *fl = fls[sg];
+    auto sball = [&]( bool c ) { return (uint64_t)__ballot( c ) & segmask; };
+    auto rank = [&]( uint64_t m ) {
+        return (int)__builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) );
+    };
+    auto any = []( bool c ) { return __ballot( c ) != 0; };
     const int mbx = (int)(mb % mbw);
     const int64_t t = mb / mbw;
     const int mby = (int)(t % mbh);
@@ -805,7 +830,7 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
 
     // fenc -> LDS (row-major dwords) and enc_dc (sad_x4 against x264_zero = the four 8x8 sums)
     uint32_t dcq[4] = { 0, 0, 0, 0 };
-    for( int i = lane; i < 16 * NDW; i += 64 )
+    for( int i = lane; i < 16 * NDW; i += SEG )
     {
         const int y = i / NDW, k = i % NDW;
         const uint32_t w = *(const uint32_t *)(p_fenc + y * fs + k * PT<BD>::PPD);
@@ -822,7 +847,7 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     {
         uint32_t v = dcq[j];
 #pragma unroll
-        for( int off = 32; off >= 1; off >>= 1 )
+        for( int off = SEG / 2; off >= 1; off >>= 1 )
             v += (uint32_t)__shfl_xor( (int)v, off );
         enc_dc[j] = (int)v;
     }
@@ -843,11 +868,12 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     const int mx = min_x + lane;
     const int fpel = active ? (int)cx[mx * 4] : 0;           // cost_fpel_mvx[mx] (analyse.c:161-169)
     const int bsad0 = (int)sad_at( bmx0, bmy0 ) + (int)cx[bmx0 * 4] + (int)cy[bmy0 * 4];
-    const int rows = max( max_y - min_y + 1, 0 );            // <= 2*me_range+1 <= 65
+    const int rows = max( max_y - min_y + 1, 0 );            // <= 2*me_range+1
     const int delta = 8 * (int)rs;
-    // ycost of row r in lane r (rows 64.. in the second register)
+    // ycost of row r in segment lane r (rows SEG.. in the second register)
     const int yc0 = lane < rows ? (int)cy[(min_y + lane) * 4] : 0;
-    const int yc1 = lane + 64 < rows ? (int)cy[(min_y + lane + 64) * 4] : 0;
+    const int yc1 = lane + SEG < rows ? (int)cy[(min_y + lane + SEG) * 4] : 0;
+    auto ycost_of = [&]( int r ) { return __shfl( r < SEG ? yc0 : yc1, sg * SEG + (r % SEG) ); };
 
     // Phase 1 (independent of the scan state, so every load is in flight at once): each
     // row's ads4 value, and the cost of every candidate that can still pass some row's
@@ -869,9 +895,9 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     for( int r = 0; r < NR; r++ )
     {
         sv[r] = 0xFFFFFFFFu;
+        const int ycost = ycost_of( r );
         if( r < rows )
         {
-            const int ycost = __builtin_amdgcn_readlane( r < 64 ? yc0 : yc1, r & 63 );
             const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
             if( adsv[r] < (uint32_t)ub )
                 sv[r] = sad_at( mx, min_y + r ) + (uint32_t)fpel;
@@ -885,19 +911,18 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     for( int r = 0; r < NR; r++ )
     {
         const int my = min_y + r;
-        const int ycost = __builtin_amdgcn_readlane( r < 64 ? yc0 : yc1, r & 63 );
-        if( r >= rows || bsad <= ycost )
-            continue;
+        const int ycost = ycost_of( r );
+        const bool rowok = r < rows && bsad > ycost;
         const int b = bsad - ycost;
-        const bool pass = adsv[r] < (uint32_t)(b * 17 >> 4);
-        if( !__ballot( pass ) )
-            continue;                                       // bsad unchanged
+        const bool pass = rowok && adsv[r] < (uint32_t)(b * 17 >> 4);
+        if( !any( pass ) )
+            continue;                                       // no segment's bsad changes
         // a passing lane's cost was staged: b <= bsad0 - ycost
         const uint32_t s = pass ? sv[r] : 0xFFFFFFFFu;
-        // exclusive prefix minimum over the lanes (the earlier survivors of this row)
+        // exclusive prefix minimum over the segment's lanes (the earlier survivors of this row)
         uint32_t incl = s;
 #pragma unroll
-        for( int off = 1; off < 64; off <<= 1 )
+        for( int off = 1; off < SEG; off <<= 1 )
         {
             const uint32_t o = (uint32_t)__shfl_up( (int)incl, off );
             incl = lane >= off ? min( incl, o ) : incl;
@@ -906,65 +931,76 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         excl = lane ? excl : 0xFFFFFFFFu;
         const int bcur = (int)min( (uint32_t)b, excl );
         const bool app = pass && (int)s < (bcur * sad_thresh0 >> 3);
-        const uint64_t m = __ballot( app );
+        const uint64_t m = sball( app );
         if( app )
-        {
-            const int pos = nmvsad + (int)__builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32),
-                                                                    __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) );
-            mvsads[pos] = (uint64_t)(s + (uint32_t)ycost) | ((uint64_t)(uint16_t)mx << 32) |
-                          ((uint64_t)(uint16_t)my << 48);
-        }
+            mvsads[nmvsad + rank( m )] = (uint64_t)(s + (uint32_t)ycost) | ((uint64_t)(uint16_t)mx << 32) |
+                                         ((uint64_t)(uint16_t)my << 48);
         nmvsad += __popcll( m );
-        const uint32_t rmin = __shfl( (int)incl, 63 );
-        bsad = min( bsad, (int)rmin + ycost );                // b_final + ycost
+        const uint32_t rmin = (uint32_t)__shfl( (int)incl, sg * SEG + SEG - 1 );
+        if( sball( pass ) )
+            bsad = min( bsad, (int)rmin + ycost );            // b_final + ycost
     }
 
     // keep the best few (me.c:705-746)
     const int limit = me_range >> 1;
     int thr = bsad * sad_thresh0 >> 3;
-    while( nmvsad > limit * 2 && thr > bsad )
+    for( ;; )
     {
-        thr = (thr + bsad) >> 1;
+        const bool need = nmvsad > limit * 2 && thr > bsad;
+        if( !any( need ) )
+            break;
+        if( need )
+            thr = (thr + bsad) >> 1;
         int k = 0;
-        for( int base = 0; base < nmvsad; base += 64 )
+        for( int base = 0; any( need && base < nmvsad ); base += SEG )
         {
             const int j = base + lane;
-            const uint64_t e = j < nmvsad ? mvsads[j] : 0;
-            const bool keep = j < nmvsad && (int)(uint32_t)e <= thr;
-            const uint64_t m = __ballot( keep );
+            const bool in = need && j < nmvsad;
+            const uint64_t e = in ? mvsads[j] : 0;
+            const bool keep = in && (int)(uint32_t)e <= thr;
+            const uint64_t m = sball( keep );
             if( keep )
-                mvsads[k + (int)__builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) )] = e;
+                mvsads[k + rank( m )] = e;
             k += __popcll( m );
         }
-        nmvsad = k;
+        if( need )
+            nmvsad = k;
     }
-    while( nmvsad > limit )
+    for( ;; )
     {
+        const bool need = nmvsad > limit;
+        if( !any( need ) )
+            break;
         // first index of the largest sad: max of (sad << 32 | ~index)
         uint64_t key = 0;
-        for( int j = lane; j < nmvsad; j += 64 )
+        for( int j = lane; any( need && j < nmvsad ); j += SEG )
         {
-            const uint64_t k = ((uint64_t)(uint32_t)mvsads[j] << 32) | (uint32_t)~j;
-            key = k > key ? k : key;
+            if( need && j < nmvsad )
+            {
+                const uint64_t k = ((uint64_t)(uint32_t)mvsads[j] << 32) | (uint32_t)~j;
+                key = k > key ? k : key;
+            }
         }
 #pragma unroll
-        for( int off = 32; off >= 1; off >>= 1 )
+        for( int off = SEG / 2; off >= 1; off >>= 1 )
         {
             const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor( (int)(key >> 32), off ) << 32) |
                                (uint32_t)__shfl_xor( (int)(uint32_t)key, off );
             key = o > key ? o : key;
         }
-        const int bi = (int)~(uint32_t)key;
-        nmvsad--;
-        if( lane == 0 )
-            mvsads[bi] = mvsads[nmvsad];
+        if( need )
+        {
+            const int bi = (int)~(uint32_t)key;
+            nmvsad--;
+            if( lane == 0 )
+                mvsads[bi] = mvsads[nmvsad];
+        }
         __syncthreads();
     }
 
     // COST_MV over the survivors in list order: eight 8x4 units per candidate
     uint32_t best = 0xFFFFFFFFu;
-    for( int u0 = 0; u0 < nmvsad * 8; u0 += 64 )
+    for( int u0 = 0; any( u0 < nmvsad * 8 ); u0 += SEG )
     {
         const int u = u0 + lane, k = u >> 3, part = u & 7;
         uint32_t v = 0;
@@ -977,11 +1013,11 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
             const int bx = 8 * (part & 1), by = 4 * (part >> 1);
             constexpr int HDW = 8 / PT<BD>::PPD;
             uint32_t a[4][HDW], rr[4][HDW];
-            const pixel *r = p_fref + (intptr_t)(cmy + by) * rs + cmx + bx;
+            const pixel *rp = p_fref + (intptr_t)(cmy + by) * rs + cmx + bx;
 #pragma unroll
             for( int y = 0; y < 4; y++ )
             {
-                load_row_u<HDW>( r + y * rs, rr[y] );
+                load_row_u<HDW>( rp + y * rs, rr[y] );
 #pragma unroll
                 for( int j = 0; j < HDW; j++ )
                     a[y][j] = fl[(by + y) * NDW + bx / PT<BD>::PPD + j];
@@ -1006,8 +1042,10 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
             best = min( best, (cost << 6) | (uint32_t)k );   // k < 64: first index on ties
         }
     }
-    best = wave_min_u32( best );
-    if( lane == 0 )
+#pragma unroll
+    for( int off = SEG / 2; off >= 1; off >>= 1 )
+        best = min( best, (uint32_t)__shfl_xor( (int)best, off ) );
+    if( lane == 0 && mbo < nmb )
     {
         int32_t bcost = init_cost[mb], rx = bmx0, ry = bmy0;
         if( best != 0xFFFFFFFFu && (int32_t)(best >> 6) < bcost )
@@ -1036,16 +1074,16 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
         return hipSuccess;
     if( me_range < 1 || me_range > 32 || nmb > 0x7fffffff )
         return hipErrorInvalidValue;
-    // the mvsads list: at most (2*me_range+1) rows x (2*me_range+3)&~3 columns
-    const size_t lds = (size_t)(2 * me_range + 1) * ((2 * me_range + 3) & ~3) * sizeof( uint64_t );
+    // the mvsads list: at most (2*me_range+1) rows x (2*me_range+3)&~3 columns per MB
+    const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
     if( me_range <= 16 )
-        hipLaunchKernelGGL( ( me_tesa_kernel<BD, 33> ), dim3( (unsigned)nmb ), dim3( 64 ), lds, stream, fenc, fs, ffs,
-                            ref, rs, rfs, integral, ifs, mbw, mbh, me_range, satd, table, R, origin, par, init_cost,
-                            cost_mv, out );
+        hipLaunchKernelGGL( ( me_tesa_kernel<BD, 33, 32> ), dim3( (unsigned)((nmb + 1) / 2) ), dim3( 64 ),
+                            2 * (size_t)cap * sizeof( uint64_t ), stream, fenc, fs, ffs, ref, rs, rfs, integral, ifs,
+                            mbw, mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost, cost_mv, out, cap );
     else
-        hipLaunchKernelGGL( ( me_tesa_kernel<BD, 65> ), dim3( (unsigned)nmb ), dim3( 64 ), lds, stream, fenc, fs, ffs,
-                            ref, rs, rfs, integral, ifs, mbw, mbh, me_range, satd, table, R, origin, par, init_cost,
-                            cost_mv, out );
+        hipLaunchKernelGGL( ( me_tesa_kernel<BD, 65, 64> ), dim3( (unsigned)nmb ), dim3( 64 ),
+                            (size_t)cap * sizeof( uint64_t ), stream, fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw,
+                            mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost, cost_mv, out, cap );
     return hipGetLastError();
 }
 
