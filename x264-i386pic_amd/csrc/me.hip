@@ -785,7 +785,7 @@ __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
 // chain serves two MBs.  Every per-MB value is uniform within its segment; ballots are
 // masked to the segment, scans and reductions stay inside it, and loops run while any
 // segment still needs them.
-template <int BD, int NR, int SEG>
+template <int BD, int NR, int SEG, bool TAB>
 __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
                                                         intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
                                                         intptr_t rs, intptr_t rfs,
@@ -855,10 +855,10 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
 
     const int W = 2 * R + 1, P = (W + 3) & ~3;
     const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
-    const typename PT<BD>::sadt *tab = table ? table + mb * (int64_t)(W * P) : nullptr;
+    const typename PT<BD>::sadt *tab = TAB ? table + mb * (int64_t)(W * P) : nullptr;
     auto sad_at = [&]( int mx, int my ) -> uint32_t {
         const int tx = mx - ox, ty = my - oy;
-        if( tab && tx >= 0 && tx < W && ty >= 0 && ty < W )
+        if( TAB && tx >= 0 && tx < W && ty >= 0 && ty < W )
             return (uint32_t)tab[ty * P + tx];
         return tesa_sad16<BD>( fl, p_fref + my * rs + mx, rs );
     };
@@ -891,12 +891,15 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
                                  abs( enc_dc[2] - (int)sp[delta] ) + abs( enc_dc[3] - (int)sp[delta + 8] ) + fpel);
         }
     }
+    // with a table the SADs are reads and are staged too; without one each costs 256
+    // absdiffs in the lane, so they are computed in phase 2 only for the lanes that pass
+    // the actual (shrinking) threshold
 #pragma unroll
     for( int r = 0; r < NR; r++ )
     {
         sv[r] = 0xFFFFFFFFu;
         const int ycost = ycost_of( r );
-        if( r < rows )
+        if( TAB && r < rows )
         {
             const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
             if( adsv[r] < (uint32_t)ub )
@@ -917,8 +920,8 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         const bool pass = rowok && adsv[r] < (uint32_t)(b * 17 >> 4);
         if( !any( pass ) )
             continue;                                       // no segment's bsad changes
-        // a passing lane's cost was staged: b <= bsad0 - ycost
-        const uint32_t s = pass ? sv[r] : 0xFFFFFFFFu;
+        // a passing lane's cost was staged (b <= bsad0 - ycost), or is computed now
+        const uint32_t s = pass ? (TAB ? sv[r] : sad_at( mx, my ) + (uint32_t)fpel) : 0xFFFFFFFFu;
         // exclusive prefix minimum over the segment's lanes (the earlier survivors of this row)
         uint32_t incl = s;
 #pragma unroll
@@ -1076,14 +1079,20 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
         return hipErrorInvalidValue;
     // the mvsads list: at most (2*me_range+1) rows x (2*me_range+3)&~3 columns per MB
     const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
+#define TESA_GO( NR, SEG, T )                                                                                    \
+    hipLaunchKernelGGL( ( me_tesa_kernel<BD, NR, SEG, T> ), dim3( (unsigned)((nmb + 64 / SEG - 1) / (64 / SEG)) ),   \
+                        dim3( 64 ), (64 / SEG) * (size_t)cap * sizeof( uint64_t ), stream, fenc, fs, ffs, ref, rs,  \
+                        rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost,    \
+                        cost_mv, out, cap )
     if( me_range <= 16 )
-        hipLaunchKernelGGL( ( me_tesa_kernel<BD, 33, 32> ), dim3( (unsigned)((nmb + 1) / 2) ), dim3( 64 ),
-                            2 * (size_t)cap * sizeof( uint64_t ), stream, fenc, fs, ffs, ref, rs, rfs, integral, ifs,
-                            mbw, mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost, cost_mv, out, cap );
+    {
+        if( table ) TESA_GO( 33, 32, true ); else TESA_GO( 33, 32, false );
+    }
     else
-        hipLaunchKernelGGL( ( me_tesa_kernel<BD, 65, 64> ), dim3( (unsigned)nmb ), dim3( 64 ),
-                            (size_t)cap * sizeof( uint64_t ), stream, fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw,
-                            mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost, cost_mv, out, cap );
+    {
+        if( table ) TESA_GO( 65, 64, true ); else TESA_GO( 65, 64, false );
+    }
+#undef TESA_GO
     return hipGetLastError();
 }
 
