@@ -340,18 +340,6 @@ int  x264hip_forward_ref( void *dst, int dst_device, const void *src, int src_de
  * analogue of reference encoder/encoder.c:1676-1706); also printed once to
  * stderr at the first table fill unless X264HIP_QUIET=1 */
 const char *x264hip_backend_banner( void );
-
-/* Fused full search + ESA decision (8 bit): me_search_centred around each MB's
- * predictor (centre = par[8*i+0..1]) and me_esa_argmin_at over that window in one
- * pass, the SAD table never written (reference encoder/me.c:618-631).
- * par / init_cost / cost_mv / out as me_esa_argmin_at: out[3*i] = { cost, mx, my };
- * window candidates outside the (2*range+1)^2 square are not evaluated (pick
- * range >= me_range + 6 to cover the rounded window).  range is 4, 8, 16 or 24. */
-int  x264hip_8_me_search_esa( const uint8_t *fenc, intptr_t fenc_stride, intptr_t fenc_frame_stride,
-                              const uint8_t *ref, intptr_t ref_stride, intptr_t ref_frame_stride,
-                              int mb_width, int mb_height, int n_frames, int range, int me_range,
-                              const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv,
-                              int32_t *out, void *stream );
 /* A/B kernel switches by environment name (X264HIP_ME_VARIANT, X264HIP_HPEL_VARIANT,
  * X264HIP_HPEL_ROWS, X264HIP_SUBPEL_VARIANT, X264HIP_LOWRES_VARIANT, X264HIP_DQ_VARIANT,
  * X264HIP_RECON_VARIANT, X264HIP_LOWRES_INTRA_VARIANT): the environment seeds them
@@ -581,6 +569,18 @@ int x264hip_##BD##_ssd_nv12_batch( const pixel *pix1, intptr_t stride1, intptr_t
                                    const pixel *pix2, intptr_t stride2, intptr_t frame_stride2, \
                                    int width, int height, int n_frames, uint64_t *ssd_uv,      \
                                    void *stream );                                              \
+                                                                                                \
+/* Fused full search + ESA decision: me_search_centred around each MB's predictor        \
+ * (centre = par[8*i+0..1]) and me_esa_argmin_at over that window in one pass, the SAD     \
+ * table never written (reference encoder/me.c:618-631).  par / init_cost / cost_mv / out   \
+ * as me_esa_argmin_at: out[3*i] = { cost, mx, my }; window candidates outside the          \
+ * (2*range+1)^2 square are not evaluated (range >= me_range + 6 covers the rounded         \
+ * window).  range is 4, 8, 16 or 24. */                                                    \
+int x264hip_##BD##_me_search_esa( const pixel *fenc, intptr_t fenc_stride, intptr_t fenc_frame_stride, \
+                                  const pixel *ref, intptr_t ref_stride, intptr_t ref_frame_stride,   \
+                                  int mb_width, int mb_height, int n_frames, int range, int me_range, \
+                                  const int16_t *par, const int32_t *init_cost,                       \
+                                  const uint16_t *cost_mv, int32_t *out, void *stream );              \
                                                                                                 \
 /* TESA integer-pel search per 16x16 macroblock (reference encoder/me.c:653-748,              \
  * X264_ME_TESA with i_pixel = PIXEL_16x16): ads4 with threshold bsad*17>>4 over the ESA      \

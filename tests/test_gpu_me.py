@@ -232,15 +232,16 @@ def test_me_esa_argmin_centred(hip, oracle, bd):
         assert tuple(got[mb]) == best, mb
 
 
+@pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("rng,me_range", [(24, 16), (16, 8), (8, 4), (24, 12)])
 @pytest.mark.parametrize("W,H", [(160, 96), (1920, 1088)])
-def test_me_search_esa_fused(hip, oracle, rng, me_range, W, H):
+def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H):
     """Fused search + ESA decision (x264hip_8_me_search_esa) equals me_search_centred followed by
     me_esa_argmin_at on the GPU, and the oracle's centred table + argmin, over predictor centres,
     clipped windows, mvp-dependent costs and unbeatable predictors."""
     from x264hip import synth
-    planes, stride, origin = synth.make_sequence(3, W, H, 8, seed=rng + me_range)
-    dev = torch.from_numpy(planes).cuda()
+    planes, stride, origin = synth.make_sequence(3, W, H, bd, seed=rng + me_range)
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
     mbw, mbh, nf = W // 16, H // 16, 2
     nmb = mbw * mbh
@@ -272,11 +273,11 @@ def test_me_search_esa_fused(hip, oracle, rng, me_range, W, H):
     if W == 160:
         for f in range(nf):
             sl = slice(f * nmb, (f + 1) * nmb)
-            tab, worg = oracle.me_search_centred(8, planes[f + 1].ravel(), origin, stride, planes[f].ravel(), origin,
+            tab, worg = oracle.me_search_centred(bd, planes[f + 1].ravel(), origin, stride, planes[f].ravel(), origin,
                                                  stride, mbw, mbh, rng, par[sl, :2])
             p_ = (2 * rng + 1 + 3) & ~3
             padded = np.zeros((nmb, 2 * rng + 1, p_), tab.dtype)
             padded[:, :, :2 * rng + 1] = tab.reshape(nmb, 2 * rng + 1, 2 * rng + 1)
-            want = oracle.me_esa_argmin(8, padded, rng, me_range, par[sl], init[sl], cost_mv, c0, origin=worg)
+            want = oracle.me_esa_argmin(bd, padded, rng, me_range, par[sl], init[sl], cost_mv, c0, origin=worg)
             assert np.array_equal(got[sl], want), (f, np.argwhere((got[sl] != want).any(1))[:5])
     assert (got[::7, 0] == 0).all() and (got[:, 0] <= init).all()

@@ -970,19 +970,18 @@ def ssd_nv12_batch(pix1, origin1, stride1, pix2, origin2, stride2, width, height
 
 def me_search_esa(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height, nframes, rng,
                   me_range, par, init_cost, cost_mv_center, out=None, fenc_frame_stride=None, ref_frame_stride=None):
-    """Fused full search around each MB's predictor + ESA decision (x264hip_8_me_search_esa, 8 bit):
+    """Fused full search around each MB's predictor + ESA decision (x264hip_*_me_search_esa):
     the result of me_search_centred(centre = par[:, :2]) followed by me_esa_argmin(origin=...),
     without the table.  Returns int32 [n, 3] = (cost, mx, my)."""
     import torch
-    if _pix_bd(fenc) != 8:
-        raise TypeError("me_search_esa is 8-bit")
+    bd = _pix_bd(fenc)
     n = par.shape[0]
     if out is None:
         out = torch.empty((n, 3), dtype=torch.int32, device=fenc.device)
     ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
     rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)
     cm, c0 = cost_mv_center
-    fn = lib().x264hip_8_me_search_esa
+    fn = getattr(lib(), f"x264hip_{bd}_me_search_esa")
     fn.argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P]
     fn.restype = _c.c_int
     _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs, mb_width, mb_height,

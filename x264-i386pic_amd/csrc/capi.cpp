@@ -1265,6 +1265,20 @@ extern "C" const char *x264hip_backend_banner( void )
         return map_err( launch_plane_ssd<BD>( 1, pix1, s1, f1, pix2, s2, f2, width, height, nframes, ssd_uv,         \
                                               (hipStream_t)stream ), "ssd_nv12_batch" );                             \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_search_esa( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,           \
+                                                 const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw,       \
+                                                 int mbh, int nframes, int range, int me_range, const int16_t *par,  \
+                                                 const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,    \
+                                                 void *stream )                                                      \
+    {                                                                                                                \
+        if( mbw < 0 || mbh < 0 || nframes < 0 || !( range == 4 || range == 8 || range == 16 || range == 24 ) ||       \
+            me_range < 0 || 2 * me_range + 4 > 64 ||                                                                 \
+            ((int64_t)nframes * mbw * mbh && (!par || !init_cost || !cost_mv || !out)) )                             \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_me_search_esa<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, me_range,   \
+                                                  par, init_cost, cost_mv, out, (hipStream_t)stream ),               \
+                        "me_search_esa" );                                                                           \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_me_tesa( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,                    \
                                            const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs,                      \
                                            const uint16_t *integral, intptr_t ifs, int mbw, int mbh, int nframes,    \
@@ -1486,17 +1500,4 @@ extern "C" void x264hip_cqm_dequant( const uint8_t *const sl[8], int b8, int32_t
                     dq8[(l * 6 + q) * 64 + i] =
                         k_dequant8_scale[q][k_quant8_scan16[((i >> 1) & 12) | (i & 3)]] * sl[4 + l][i];
     }
-}
-
-// fused full search + ESA decision, 8 bit (me.hip me_full_esa_v3_kernel)
-extern "C" int x264hip_8_me_search_esa( const uint8_t *fenc, intptr_t fs, intptr_t ffs, const uint8_t *ref, intptr_t rs,
-                                        intptr_t rfs, int mbw, int mbh, int nframes, int range, int me_range,
-                                        const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv,
-                                        int32_t *out, void *stream )
-{
-    if( mbw < 0 || mbh < 0 || nframes < 0 || !( range == 4 || range == 8 || range == 16 || range == 24 ) ||
-        me_range < 0 || 2 * me_range + 4 > 64 || ((int64_t)nframes * mbw * mbh && (!par || !init_cost || !cost_mv || !out)) )
-        return X264HIP_EINVAL;
-    return map_err( launch_me_search_esa8( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, me_range, par,
-                                           init_cost, cost_mv, out, (hipStream_t)stream ), "me_search_esa" );
 }

@@ -323,6 +323,190 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t 
     me_rows3<R>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
 }
 
+
+// ---------------------------------------------------------------------------
+// Variant 5 (10 bit, default): the variant-3 layout for 16-bit pixels.  A lane
+// owns two adjacent candidate columns (2g, 2g+1; the first is dword aligned for
+// even R) and half of the fenc rows; per ref row it loads 9 dwords once, forms
+// the odd column's dwords with one v_alignbyte_b32 each, and folds the row into
+// <= 8 candidates x 2 columns with v_sad_u16.  Two u32 SADs leave per store.
+// `sink( c, a0, a1 )` receives candidate row c's two finished SADs (columns 2g, 2g+1),
+// identical in both lanes of the pair
+template <int R, int Y, class Sink>
+__device__ __forceinline__ void me_row5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
+                                         uint32_t (&acc)[8][2], Sink &sink )
+{
+    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    const uint32_t *row = rbase + Y * rs_dw;
+    uint32_t w[9], o[8];
+#pragma unroll
+    for( int k = 0; k < 9; k++ )
+        w[k] = row[k];
+#pragma unroll
+    for( int k = 0; k < 8; k++ )
+        o[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], 2 );
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint32_t a0 = r == 0 ? 0u : acc[c & 7][0], a1 = r == 0 ? 0u : acc[c & 7][1];
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+        {
+            a0 = __builtin_amdgcn_sad_u16( F[r][k], w[k], a0 );
+            a1 = __builtin_amdgcn_sad_u16( F[r][k], o[k], a1 );
+        }
+        if( r == 7 )
+        {
+            a0 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a0, 0xB1, 0xF, 0xF, false );
+            a1 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a1, 0xB1, 0xF, 0xF, false );
+            sink( c, a0, a1 );
+        }
+        else
+        {
+            acc[c & 7][0] = a0;
+            acc[c & 7][1] = a1;
+        }
+    }
+}
+
+template <int R, class Sink, int... Ys>
+__device__ __forceinline__ void me_rows5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
+                                          uint32_t (&acc)[8][2], Sink &sink, std::integer_sequence<int, Ys...> )
+{
+    ( me_row5<R, Ys>( rbase, rs_dw, F, acc, sink ), ... );
+}
+
+template <int R>
+__global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
+                                                                  intptr_t ffs, const uint16_t *__restrict__ ref,
+                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                  int nframes, uint32_t *__restrict__ table,
+                                                                  const int16_t *__restrict__ centre,
+                                                                  int16_t *__restrict__ origin )
+{
+    constexpr int G = (2 * R + 1 + 1) / 2;      // column pairs per MB
+    constexpr int P = (2 * R + 1 + 3) / 4 * 4;
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
+    if( slot >= total )
+        return;
+    const int h = (int)(slot & 1);
+    const int grp = (int)((slot >> 1) % G);
+    const int64_t mb = slot / (2 * G);
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+
+    uint32_t F[8][8];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs / 2);
+#pragma unroll
+    for( int r = 0; r < 8; r++ )
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+    int ox, oy;
+    me_window<10, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    if( origin && grp == 0 && h == 0 )
+    {
+        origin[2 * mb] = (int16_t)ox;
+        origin[2 * mb + 1] = (int16_t)oy;
+    }
+    const uint32_t *rbase =
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 2 * grp);
+    uint32_t *out = table + mb * ((2 * R + 1) * P) + 2 * grp;
+    uint32_t acc[8][2];
+    auto store = [out]( int c, uint32_t a0, uint32_t a1 ) {
+        *(uint2 *)(out + c * ((2 * R + 1 + 3) / 4 * 4)) = make_uint2( a0, a1 );
+    };
+    me_rows5<R>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
+}
+
+template <int R, typename P, typename T>
+static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
+                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
+                       int16_t *origin )
+{
+    if constexpr( sizeof( P ) == 2 )
+        hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
+                            nframes, table, centre, origin );
+}
+
+// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2, 3 (8 bit)
+// or 5 (10 bit); default 3 at 8 bit, 5 at 10 bit.  (A variant that dropped the padded column
+// group and finished the last column in separate waves ran 13-20% slower: the
+// table rows were then written by different waves at different times, so
+// nearly every 128-B line left L2 partially written.)
+static int me_variant()
+{
+    const int v = variant( V_ME );
+    return v >= 0 ? v : 0;
+}
+
+template <int R, typename P, typename T>
+static void launch_v3( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
+                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
+                       int16_t *origin )
+{
+    if constexpr( sizeof( P ) == 1 )
+        hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
+                            nframes, table, centre, origin );
+}
+
+template <int BD>
+hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                           const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                           int nframes, int range, typename PT<BD>::sadt *table, const int16_t *centre,
+                           int16_t *origin, hipStream_t stream )
+{
+    int variant = me_variant();
+    if( !variant )
+        variant = BD == 8 ? 3 : 5;
+    if( (BD != 8 && variant == 3) || (BD == 8 && variant == 5) )
+        variant = 1;
+    // variants 2/3 need dword-aligned fenc rows, dword-multiple strides and (3) a
+    // dword-aligned ref plane
+    if( (((uintptr_t)fenc | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
+          (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant >= 3 ? (uintptr_t)ref : 0)) & 3) )
+        variant = 1;
+    const int64_t groups = variant == 3   ? 2 * ((2 * range + 1 + 3) / 4)
+                           : variant == 5 ? 2 * ((2 * range + 2) / 2)
+                           : variant == 2 ? 2 * (2 * range + 1)
+                                          : (2 * range + 1);
+    const int64_t lanes = (int64_t)nframes * mbh * mbw * groups;
+    if( lanes <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+    switch( range )
+    {
+#define ME_CASE( R ) \
+        case R:                                                                                                   \
+            if( variant == 5 )                                                                                    \
+                launch_v5<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
+            else if( variant == 3 )                                                                               \
+                launch_v3<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
+            else if( variant == 2 )                                                                               \
+                hipLaunchKernelGGL( ( me_full_sad16_v2_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, \
+                                    rfs, mbw, mbh, nframes, table, centre, origin );                              \
+            else                                                                                                  \
+                hipLaunchKernelGGL( ( me_full_sad16_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs,   \
+                                    rfs, mbw, mbh, nframes, table, centre, origin );                              \
+            break;
+        ME_CASE( 4 ) ME_CASE( 8 ) ME_CASE( 16 ) ME_CASE( 24 )
+#undef ME_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template hipError_t launch_me_full<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
+                                       int, int, int, uint16_t *, const int16_t *, int16_t *, hipStream_t );
+template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
+                                        int, int, int, int, uint32_t *, const int16_t *, int16_t *, hipStream_t );
+
 // Fused search + ESA decision (8 bit): the variant-3 lanes of me_search_centred around
 // each MB's predictor (bmx, bmy), but each finished candidate row is turned into
 // me_esa_argmin_at's packed keys (cost << 12 | raster index in the clipped, width-rounded
@@ -438,100 +622,20 @@ __global__ __launch_bounds__( 256 ) void me_esa_finish_kernel( int nmb, int me_r
     out[3 * i + 2] = ry;
 }
 
-hipError_t launch_me_search_esa8( const uint8_t *fenc, intptr_t fs, intptr_t ffs, const uint8_t *ref, intptr_t rs,
-                                  intptr_t rfs, int mbw, int mbh, int nframes, int range, int me_range,
-                                  const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,
-                                  hipStream_t stream )
-{
-    const int64_t nmb = (int64_t)nframes * mbw * mbh;
-    if( nmb <= 0 )
-        return hipSuccess;
-    if( nmb > 0x7fffffff || (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)fs | (uintptr_t)rs) & 3) )
-        return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync( out, 0xFF, (size_t)nmb * 3 * sizeof( int32_t ), stream );
-    if( e != hipSuccess )
-        return e;
-    const int64_t lanes = nmb * 2 * ((2 * range + 1 + 3) / 4);
-    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
-    switch( range )
-    {
-#define ESA_CASE( R )                                                                                             \
-        case R:                                                                                                   \
-            hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, \
-                                mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                          \
-            break;
-        ESA_CASE( 4 ) ESA_CASE( 8 ) ESA_CASE( 16 ) ESA_CASE( 24 )
-#undef ESA_CASE
-        default: return hipErrorInvalidValue;
-    }
-    hipLaunchKernelGGL( me_esa_finish_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream, (int)nmb,
-                        me_range, par, init_cost, out );
-    return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Variant 5 (10 bit, default): the variant-3 layout for 16-bit pixels.  A lane
-// owns two adjacent candidate columns (2g, 2g+1; the first is dword aligned for
-// even R) and half of the fenc rows; per ref row it loads 9 dwords once, forms
-// the odd column's dwords with one v_alignbyte_b32 each, and folds the row into
-// <= 8 candidates x 2 columns with v_sad_u16.  Two u32 SADs leave per store.
-template <int R, int Y>
-__device__ __forceinline__ void me_row5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
-                                         uint32_t (&acc)[8][2], uint32_t *out )
-{
-    constexpr int P = (2 * R + 1 + 3) / 4 * 4;
-    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
-    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
-    const uint32_t *row = rbase + Y * rs_dw;
-    uint32_t w[9], o[8];
-#pragma unroll
-    for( int k = 0; k < 9; k++ )
-        w[k] = row[k];
-#pragma unroll
-    for( int k = 0; k < 8; k++ )
-        o[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], 2 );
-#pragma unroll
-    for( int c = C0; c <= C1; c++ )
-    {
-        const int r = Y - c;
-        uint32_t a0 = r == 0 ? 0u : acc[c & 7][0], a1 = r == 0 ? 0u : acc[c & 7][1];
-#pragma unroll
-        for( int k = 0; k < 8; k++ )
-        {
-            a0 = __builtin_amdgcn_sad_u16( F[r][k], w[k], a0 );
-            a1 = __builtin_amdgcn_sad_u16( F[r][k], o[k], a1 );
-        }
-        if( r == 7 )
-        {
-            a0 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a0, 0xB1, 0xF, 0xF, false );
-            a1 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a1, 0xB1, 0xF, 0xF, false );
-            *(uint2 *)(out + c * P) = make_uint2( a0, a1 );
-        }
-        else
-        {
-            acc[c & 7][0] = a0;
-            acc[c & 7][1] = a1;
-        }
-    }
-}
-
-template <int R, int... Ys>
-__device__ __forceinline__ void me_rows5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
-                                          uint32_t (&acc)[8][2], uint32_t *out, std::integer_sequence<int, Ys...> )
-{
-    ( me_row5<R, Ys>( rbase, rs_dw, F, acc, out ), ... );
-}
-
+// Fused search + ESA decision (10 bit): the variant-5 lanes (two columns per lane pair,
+// u32 sums) around each MB's predictor; lane h of a pair keys column 2g+h.  Keys as the
+// 8-bit form (cost < 2^19 at 10 bit: 261888 + two cost_mv terms).
 template <int R>
-__global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
-                                                                  intptr_t ffs, const uint16_t *__restrict__ ref,
-                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                                                                  int nframes, uint32_t *__restrict__ table,
-                                                                  const int16_t *__restrict__ centre,
-                                                                  int16_t *__restrict__ origin )
+__global__ __launch_bounds__( 256 ) void me_full_esa_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
+                                                                intptr_t ffs, const uint16_t *__restrict__ ref,
+                                                                intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                int nframes, int me_range,
+                                                                const int16_t *__restrict__ par,
+                                                                const uint16_t *__restrict__ cost_mv,
+                                                                uint32_t *__restrict__ keys )
 {
     constexpr int G = (2 * R + 1 + 1) / 2;      // column pairs per MB
-    constexpr int P = (2 * R + 1 + 3) / 4 * 4;
+    constexpr int W = 2 * R + 1;
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
     if( slot >= total )
@@ -552,101 +656,86 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
 #pragma unroll
         for( int k = 0; k < 8; k++ )
             F[r][k] = fe[r * fs_dw + k];
+    const int16_t *p = par + 8 * mb;
+    const int bmx = p[0], bmy = p[1];
+    const int min_x = max( bmx - me_range, (int)p[4] ), min_y = max( bmy - me_range, (int)p[5] );
+    const int max_x = min( bmx + me_range, (int)p[6] ), max_y = min( bmy + me_range, (int)p[7] );
+    const int width = (max_x - min_x + 3) & ~3;
+    const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
     int ox, oy;
-    me_window<10, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
-    if( origin && grp == 0 && h == 0 )
-    {
-        origin[2 * mb] = (int16_t)ox;
-        origin[2 * mb + 1] = (int16_t)oy;
-    }
+    const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };
+    me_window<10, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
     const uint32_t *rbase =
         (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 2 * grp);
-    uint32_t *out = table + mb * ((2 * R + 1) * P) + 2 * grp;
+    const int col = 2 * grp + h, mxc = ox + col;
+    const bool cin = col < W && mxc >= min_x && mxc < min_x + width;
+    const uint32_t cinv = cin ? 0u : 0xFFFFFFFFu;
+    const int ccost = cin ? (int)cx[mxc * 4] : 0;
+    uint32_t key = 0xFFFFFFFFu;
+    const int ibase = mxc - min_x - min_y * width;
+    auto reduce = [&]( int c, uint32_t a0, uint32_t a1 ) {
+        const int my = oy + c;
+        const uint32_t rinv = my >= min_y && my <= max_y ? 0u : 0xFFFFFFFFu;
+        int yi = 4 * min( max( my, min_y ), max_y );
+        asm volatile( "" : "+v"( yi ) );         // the row cost is loaded here, not hoisted
+        const uint32_t ycost = cy[yi];
+        const uint32_t sad = h ? a1 : a0;
+        const uint32_t k = ((sad + (uint32_t)ccost + ycost) << 12) | (uint32_t)(my * width + ibase);
+        key = min( key, k | cinv | rinv );
+        asm volatile( "" : "+v"( key ) );        // fold each row where its sums finish
+    };
     uint32_t acc[8][2];
-    me_rows5<R>( rbase, (int)(rs / 2), F, acc, out, std::make_integer_sequence<int, 2 * R + 8>{} );
-}
-
-template <int R, typename P, typename T>
-static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
-                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
-                       int16_t *origin )
-{
-    if constexpr( sizeof( P ) == 2 )
-        hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
-                            nframes, table, centre, origin );
-}
-
-// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2, 3 (8 bit)
-// or 5 (10 bit); default 3 at 8 bit, 5 at 10 bit.  (A variant that dropped the padded column
-// group and finished the last column in separate waves ran 13-20% slower: the
-// table rows were then written by different waves at different times, so
-// nearly every 128-B line left L2 partially written.)
-static int me_variant()
-{
-    const int v = variant( V_ME );
-    return v >= 0 ? v : 0;
-}
-
-template <int R, typename P, typename T>
-static void launch_v3( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
-                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
-                       int16_t *origin )
-{
-    if constexpr( sizeof( P ) == 1 )
-        hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
-                            nframes, table, centre, origin );
+    me_rows5<R>( rbase, (int)(rs / 2), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
+    key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)key, 0xB1, 0xF, 0xF, false ) );
+    if( !h && key != 0xFFFFFFFFu )
+        atomicMin( keys + 3 * mb, key );
 }
 
 template <int BD>
-hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
-                           const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                           int nframes, int range, typename PT<BD>::sadt *table, const int16_t *centre,
-                           int16_t *origin, hipStream_t stream )
+hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                 const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                 int nframes, int range, int me_range, const int16_t *par, const int32_t *init_cost,
+                                 const uint16_t *cost_mv, int32_t *out, hipStream_t stream )
 {
-    int variant = me_variant();
-    if( !variant )
-        variant = BD == 8 ? 3 : 5;
-    if( (BD != 8 && variant == 3) || (BD == 8 && variant == 5) )
-        variant = 1;
-    // variants 2/3 need dword-aligned fenc rows, dword-multiple strides and (3) a
-    // dword-aligned ref plane
-    if( (((uintptr_t)fenc | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
-          (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant >= 3 ? (uintptr_t)ref : 0)) & 3) )
-        variant = 1;
-    const int64_t groups = variant == 3   ? 2 * ((2 * range + 1 + 3) / 4)
-                           : variant == 5 ? 2 * ((2 * range + 2) / 2)
-                           : variant == 2 ? 2 * (2 * range + 1)
-                                          : (2 * range + 1);
-    const int64_t lanes = (int64_t)nframes * mbh * mbw * groups;
-    if( lanes <= 0 )
+    const int64_t nmb = (int64_t)nframes * mbw * mbh;
+    if( nmb <= 0 )
         return hipSuccess;
+    if( nmb > 0x7fffffff ||
+        (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
+          (uintptr_t)(rs * sizeof( typename PT<BD>::pixel ))) & 3) )
+        return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync( out, 0xFF, (size_t)nmb * 3 * sizeof( int32_t ), stream );
+    if( e != hipSuccess )
+        return e;
+    const int64_t groups = BD == 8 ? (2 * range + 1 + 3) / 4 : (2 * range + 2) / 2;
+    const int64_t lanes = nmb * 2 * groups;
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
     switch( range )
     {
-#define ME_CASE( R ) \
+#define ESA_CASE( R )                                                                                             \
         case R:                                                                                                   \
-            if( variant == 5 )                                                                                    \
-                launch_v5<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
-            else if( variant == 3 )                                                                               \
-                launch_v3<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
-            else if( variant == 2 )                                                                               \
-                hipLaunchKernelGGL( ( me_full_sad16_v2_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, \
-                                    rfs, mbw, mbh, nframes, table, centre, origin );                              \
+            if constexpr( BD == 8 )                                                                               \
+                hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,  \
+                                    mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                 \
             else                                                                                                  \
-                hipLaunchKernelGGL( ( me_full_sad16_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs,   \
-                                    rfs, mbw, mbh, nframes, table, centre, origin );                              \
+                hipLaunchKernelGGL( ( me_full_esa_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,  \
+                                    mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                 \
             break;
-        ME_CASE( 4 ) ME_CASE( 8 ) ME_CASE( 16 ) ME_CASE( 24 )
-#undef ME_CASE
+        ESA_CASE( 4 ) ESA_CASE( 8 ) ESA_CASE( 16 ) ESA_CASE( 24 )
+#undef ESA_CASE
         default: return hipErrorInvalidValue;
     }
+    hipLaunchKernelGGL( me_esa_finish_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream, (int)nmb,
+                        me_range, par, init_cost, out );
     return hipGetLastError();
 }
 
-template hipError_t launch_me_full<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
-                                       int, int, int, uint16_t *, const int16_t *, int16_t *, hipStream_t );
-template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
-                                        int, int, int, int, uint32_t *, const int16_t *, int16_t *, hipStream_t );
+template hipError_t launch_me_search_esa<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t,
+                                             int, int, int, int, int, const int16_t *, const int32_t *,
+                                             const uint16_t *, int32_t *, hipStream_t );
+template hipError_t launch_me_search_esa<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t,
+                                              intptr_t, int, int, int, int, int, const int16_t *, const int32_t *,
+                                              const uint16_t *, int32_t *, hipStream_t );
 
 } // namespace x264hip
 
