@@ -4,7 +4,9 @@
 // leg.  Variants: 1 = the streaming kernel's grid (a wave per 62-piece column
 // chunk x ROWS-row strip), 2 = a plain grid-stride copy of the same bytes
 // (1 plane in, 3 out), 3 = a plain 1-in-1-out copy of one plane (reference), 4 = the
-// frame_init_lowres pattern (three source rows per output row, four half-width planes out).
+// frame_init_lowres pattern (three source rows per output row, four half-width planes out),
+// 5 = the fused DCT+quant pattern (two planes in, 2-byte coefficients out), 6 = the
+// reconstruction pattern (coefficients + prediction in, one plane out).
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdint.h>
@@ -56,6 +58,27 @@ __global__ __launch_bounds__( 64 ) void lowres4( const uint8_t *src, uint8_t *a,
     }
 }
 
+// the fused DCT+quant pattern: two 1-byte planes in (fenc, pred), one 2-byte coefficient
+// stream out (16 B of each input per lane -> 32 B out); and the reconstruction pattern:
+// the 2-byte coefficients + pred in, one plane out
+__global__ void dctpat( const uint4 *fe, const uint4 *pr, uint4 *co, long n16 )
+{
+    for( long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x )
+    {
+        const uint4 a = fe[i], b = pr[i];
+        co[2 * i] = make_uint4( a.x ^ b.x, a.y, b.z, a.w );
+        co[2 * i + 1] = make_uint4( a.z, b.y ^ a.y, b.w, b.x );
+    }
+}
+__global__ void recpat( const uint4 *co, const uint4 *pr, uint4 *out, long n16 )
+{
+    for( long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (long)gridDim.x * blockDim.x )
+    {
+        const uint4 a = co[2 * i], b = co[2 * i + 1], c = pr[i];
+        out[i] = make_uint4( a.x ^ b.x ^ c.x, a.y ^ b.y, a.z ^ c.z, a.w ^ b.w ^ c.w );
+    }
+}
+
 __global__ void flat3( const uint4 *src, uint4 *a, uint4 *b, uint4 *c, long n )
 {
     for( long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x )
@@ -88,7 +111,9 @@ int main( int argc, char **argv )
     const long ds = 1024, dfs = ds * (544 + 64), lbytes = F * dfs;
     for( int i = 0; i < 4; i++ )
         hipMalloc( &l[i], lbytes );
-    for( int v = 1; v <= 4; v++ )
+    uint8_t *co;
+    hipMalloc( &co, 2 * bytes );
+    for( int v = 1; v <= 6; v++ )
     {
         auto run = [&]() {
             if( v == 1 )
@@ -99,6 +124,12 @@ int main( int argc, char **argv )
                                     (uint4 *)c, bytes / 16 );
             else if( v == 3 )
                 hipLaunchKernelGGL( flat1, dim3( 4096 ), dim3( 256 ), 0, 0, (const uint4 *)s, (uint4 *)a, bytes / 16 );
+            else if( v == 5 )
+                hipLaunchKernelGGL( dctpat, dim3( 4096 ), dim3( 256 ), 0, 0, (const uint4 *)s, (const uint4 *)a,
+                                    (uint4 *)co, bytes / 16 );
+            else if( v == 6 )
+                hipLaunchKernelGGL( recpat, dim3( 4096 ), dim3( 256 ), 0, 0, (const uint4 *)co, (const uint4 *)a,
+                                    (uint4 *)b, bytes / 16 );
             else
                 hipLaunchKernelGGL( lowres4, dim3( 1, 272, F ), dim3( 64 ), 0, 0, s, l[0], l[1], l[2], l[3], stride,
                                     fstride, ds, dfs, 60, 544 );
@@ -113,7 +144,8 @@ int main( int argc, char **argv )
         float ms;
         hipEventElapsedTime( &ms, e0, e1 );
         ms /= 100;
-        const double moved = v == 3 ? 2.0 * bytes : v == 4 ? (double)F * (1088 * 1920 + 4 * 544 * 960) : 4.0 * bytes;
+        const double moved = v == 3 ? 2.0 * bytes : v == 4 ? (double)F * (1088 * 1920 + 4 * 544 * 960)
+                           : v == 5 || v == 6 ? 4.0 * bytes : 4.0 * bytes;
         printf( "variant %d: %.4f ms, %.2f TB/s, %.3f of 8 TB/s\n", v, ms, moved / ms / 1e9, moved / ms / 1e9 / 8.0 );
     }
     return 0;
