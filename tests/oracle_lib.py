@@ -10,7 +10,9 @@ import os
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-_L = C.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+# X264HIP_ORACLE_LIB selects another build of the same sources (the sanitizer build,
+# tests/test_cpu_sanitize.py)
+_L = C.CDLL(os.environ.get("X264HIP_ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so"))
 _P, _IP = C.c_void_p, C.c_ssize_t
 
 
