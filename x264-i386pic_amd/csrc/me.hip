@@ -278,7 +278,60 @@ __device__ __forceinline__ void me_rows3( const uint32_t *__restrict__ rbase, in
     ( me_row3<R, Ys>( rbase, rs_dw, F, acc, sink ), ... );
 }
 
-template <int R>
+// the same row step with the next ref row's two loads issued before this row's qsads
+// (one row of lead: the loads' latency is covered by the wave's own 32 qsads as well
+// as by the other waves of the SIMD)
+template <int R, int L, int Y, class Sink>
+__device__ __forceinline__ void me_row3p( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
+                                          uint64_t (&acc)[8], Sink &sink, u64x2a4 (&e)[L], u64x2a4 (&o)[L] )
+{
+    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    const uint64_t win[4] = { e[Y % L][0], o[Y % L][0], e[Y % L][1], o[Y % L][1] };
+    if constexpr( Y + L < 2 * R + 8 )
+    {
+        const uint32_t *row = rbase + (Y + L) * rs_dw;
+        e[Y % L] = *(const u64x2a4 *)row;
+        o[Y % L] = *(const u64x2a4 *)(row + 1);
+    }
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint64_t a = r == 0 ? 0ull : acc[c & 7];
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            a = __builtin_amdgcn_qsad_pk_u16_u8( win[k], F[r][k], a );
+        if( r == 7 )
+        {
+            uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
+            lo += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)lo, 0xB1, 0xF, 0xF, false );
+            hi += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)hi, 0xB1, 0xF, 0xF, false );
+            sink( c, lo, hi );
+        }
+        else
+            acc[c & 7] = a;
+    }
+    // keep the scheduler from hoisting later rows' loads up here (it clusters them all
+    // at the top otherwise: 126 VGPRs, 4 waves)
+    __builtin_amdgcn_sched_barrier( 0 );
+}
+
+template <int R, int L, class Sink, int... Ys>
+__device__ __forceinline__ void me_rows3p( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
+                                           uint64_t (&acc)[8], Sink &sink, std::integer_sequence<int, Ys...> )
+{
+    u64x2a4 e[L], o[L];
+#pragma unroll
+    for( int k = 0; k < L; k++ )
+    {
+        e[k] = *(const u64x2a4 *)(rbase + k * rs_dw);
+        o[k] = *(const u64x2a4 *)(rbase + k * rs_dw + 1);
+    }
+    ( me_row3p<R, L, Ys>( rbase, rs_dw, F, acc, sink, e, o ), ... );
+}
+
+template <int R, int PF = 0>
 __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                   intptr_t ffs, const uint8_t *__restrict__ ref,
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -320,7 +373,10 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t 
     uint64_t *out = (uint64_t *)(table + mb * ((2 * R + 1) * P) + 4 * grp);
     auto store = [out]( int c, uint32_t lo, uint32_t hi ) { out[c * (P / 4)] = ((uint64_t)hi << 32) | lo; };
     uint64_t acc[8];
-    me_rows3<R>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
+    if constexpr( PF > 0 )
+        me_rows3p<R, PF>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
+    else
+        me_rows3<R>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
 }
 
 
@@ -371,6 +427,66 @@ __device__ __forceinline__ void me_row5( const uint32_t *__restrict__ rbase, int
     }
 }
 
+// variant 5 with the next L ref rows' loads issued ahead (as me_row3p)
+template <int R, int L, int Y, class Sink>
+__device__ __forceinline__ void me_row5p( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
+                                          uint32_t (&acc)[8][2], Sink &sink, uint32_t (&ring)[L][9] )
+{
+    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    uint32_t w[9], o[8];
+#pragma unroll
+    for( int k = 0; k < 9; k++ )
+        w[k] = ring[Y % L][k];
+    if constexpr( Y + L < 2 * R + 8 )
+    {
+        const uint32_t *row = rbase + (Y + L) * rs_dw;
+#pragma unroll
+        for( int k = 0; k < 9; k++ )
+            ring[Y % L][k] = row[k];
+    }
+#pragma unroll
+    for( int k = 0; k < 8; k++ )
+        o[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], 2 );
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint32_t a0 = r == 0 ? 0u : acc[c & 7][0], a1 = r == 0 ? 0u : acc[c & 7][1];
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+        {
+            a0 = __builtin_amdgcn_sad_u16( F[r][k], w[k], a0 );
+            a1 = __builtin_amdgcn_sad_u16( F[r][k], o[k], a1 );
+        }
+        if( r == 7 )
+        {
+            a0 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a0, 0xB1, 0xF, 0xF, false );
+            a1 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a1, 0xB1, 0xF, 0xF, false );
+            sink( c, a0, a1 );
+        }
+        else
+        {
+            acc[c & 7][0] = a0;
+            acc[c & 7][1] = a1;
+        }
+    }
+    __builtin_amdgcn_sched_barrier( 0 );
+}
+
+template <int R, int L, class Sink, int... Ys>
+__device__ __forceinline__ void me_rows5p( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
+                                           uint32_t (&acc)[8][2], Sink &sink, std::integer_sequence<int, Ys...> )
+{
+    uint32_t ring[L][9];
+#pragma unroll
+    for( int j = 0; j < L; j++ )
+#pragma unroll
+        for( int k = 0; k < 9; k++ )
+            ring[j][k] = rbase[j * rs_dw + k];
+    ( me_row5p<R, L, Ys>( rbase, rs_dw, F, acc, sink, ring ), ... );
+}
+
 template <int R, class Sink, int... Ys>
 __device__ __forceinline__ void me_rows5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
                                           uint32_t (&acc)[8][2], Sink &sink, std::integer_sequence<int, Ys...> )
@@ -378,7 +494,7 @@ __device__ __forceinline__ void me_rows5( const uint32_t *__restrict__ rbase, in
     ( me_row5<R, Ys>( rbase, rs_dw, F, acc, sink ), ... );
 }
 
-template <int R>
+template <int R, int PF = 0>
 __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
                                                                   intptr_t ffs, const uint16_t *__restrict__ ref,
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -422,7 +538,21 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
     auto store = [out]( int c, uint32_t a0, uint32_t a1 ) {
         *(uint2 *)(out + c * ((2 * R + 1 + 3) / 4 * 4)) = make_uint2( a0, a1 );
     };
-    me_rows5<R>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
+    if constexpr( PF > 0 )
+        me_rows5p<R, PF>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
+    else
+        me_rows5<R>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
+}
+
+// rows of load lead in variants 3 / 5 and the fused ESA kernels (tuning hook
+// X264HIP_ME_LEAD = 0..3, default 2): the next rows' ref loads are issued before the
+// current row's SADs.  At 16 1080p pairs, R 16: 8 bit 0.312 -> 0.300 ms (lead 0 -> 2;
+// 3 no better), 10 bit 0.653 -> 0.617 ms; lead 1 gains little, the compiler reuses the
+// current row's registers for it and so issues it half a row late
+static int me_lead()
+{
+    const int v = variant( V_ME_LEAD );
+    return v >= 0 && v <= 3 ? v : 2;
 }
 
 template <int R, typename P, typename T>
@@ -431,8 +561,18 @@ static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intp
                        int16_t *origin )
 {
     if constexpr( sizeof( P ) == 2 )
-        hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
-                            nframes, table, centre, origin );
+    {
+        const int lead = me_lead();
+        if( lead == 1 )
+            hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R, 1> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
+                                mbw, mbh, nframes, table, centre, origin );
+        else if( lead >= 2 )
+            hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
+                                mbw, mbh, nframes, table, centre, origin );
+        else
+            hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,
+                                mbh, nframes, table, centre, origin );
+    }
 }
 
 // kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2, 3 (8 bit)
@@ -452,8 +592,21 @@ static void launch_v3( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intp
                        int16_t *origin )
 {
     if constexpr( sizeof( P ) == 1 )
-        hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,
-                            nframes, table, centre, origin );
+    {
+        const int lead = me_lead();
+        if( lead == 1 )
+            hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R, 1> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
+                                mbw, mbh, nframes, table, centre, origin );
+        else if( lead == 2 )
+            hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
+                                mbw, mbh, nframes, table, centre, origin );
+        else if( lead == 3 )
+            hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R, 3> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
+                                mbw, mbh, nframes, table, centre, origin );
+        else
+            hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,
+                                mbh, nframes, table, centre, origin );
+    }
 }
 
 template <int BD>
@@ -514,7 +667,7 @@ template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, co
 // instead of written out: the 17.8 MB-per-frame table never leaves the chip.  Each MB's
 // 18 lanes meet through one atomicMin per lane pair into its key slot (out[3*mb]), and
 // me_esa_finish_kernel applies the strict-< update from the predictor cost.
-template <int R>
+template <int R, int PF>
 __global__ __launch_bounds__( 256 ) void me_full_esa_v3_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                 intptr_t ffs, const uint8_t *__restrict__ ref,
                                                                 intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -588,7 +741,10 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v3_kernel( const uint8_t *_
         asm volatile( "" : "+v"( key ) );
     };
     uint64_t acc[8];
-    me_rows3<R>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
+    if constexpr( PF > 0 )
+        me_rows3p<R, PF>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
+    else
+        me_rows3<R>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
     key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)key, 0xB1, 0xF, 0xF, false ) );
     if( !h && key != 0xFFFFFFFFu )
         atomicMin( keys + 3 * mb, key );
@@ -625,7 +781,7 @@ __global__ __launch_bounds__( 256 ) void me_esa_finish_kernel( int nmb, int me_r
 // Fused search + ESA decision (10 bit): the variant-5 lanes (two columns per lane pair,
 // u32 sums) around each MB's predictor; lane h of a pair keys column 2g+h.  Keys as the
 // 8-bit form (cost < 2^19 at 10 bit: 261888 + two cost_mv terms).
-template <int R>
+template <int R, int PF>
 __global__ __launch_bounds__( 256 ) void me_full_esa_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
                                                                 intptr_t ffs, const uint16_t *__restrict__ ref,
                                                                 intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -685,7 +841,10 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v5_kernel( const uint16_t *
         asm volatile( "" : "+v"( key ) );        // fold each row where its sums finish
     };
     uint32_t acc[8][2];
-    me_rows5<R>( rbase, (int)(rs / 2), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
+    if constexpr( PF > 0 )
+        me_rows5p<R, PF>( rbase, (int)(rs / 2), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
+    else
+        me_rows5<R>( rbase, (int)(rs / 2), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
     key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)key, 0xB1, 0xF, 0xF, false ) );
     if( !h && key != 0xFFFFFFFFu )
         atomicMin( keys + 3 * mb, key );
@@ -710,19 +869,23 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
     const int64_t groups = BD == 8 ? (2 * range + 1 + 3) / 4 : (2 * range + 2) / 2;
     const int64_t lanes = nmb * 2 * groups;
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+    const int lead = me_lead();
     switch( range )
     {
+#define ESA_GO( R, L )                                                                                            \
+    if constexpr( BD == 8 )                                                                                       \
+        hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R, L> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,  \
+                            mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                              \
+    else                                                                                                          \
+        hipLaunchKernelGGL( ( me_full_esa_v5_kernel<R, L> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,  \
+                            mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );
 #define ESA_CASE( R )                                                                                             \
         case R:                                                                                                   \
-            if constexpr( BD == 8 )                                                                               \
-                hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,  \
-                                    mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                 \
-            else                                                                                                  \
-                hipLaunchKernelGGL( ( me_full_esa_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,  \
-                                    mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                 \
+            if( lead == 0 ) { ESA_GO( R, 0 ) } else if( lead == 1 ) { ESA_GO( R, 1 ) } else { ESA_GO( R, 2 ) }   \
             break;
         ESA_CASE( 4 ) ESA_CASE( 8 ) ESA_CASE( 16 ) ESA_CASE( 24 )
 #undef ESA_CASE
+#undef ESA_GO
         default: return hipErrorInvalidValue;
     }
     hipLaunchKernelGGL( me_esa_finish_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream, (int)nmb,
