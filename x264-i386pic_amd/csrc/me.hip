@@ -1024,6 +1024,35 @@ __device__ __forceinline__ uint32_t tesa_sad16( const uint32_t *fenc_lds, const 
     return acc;
 }
 
+// inclusive min-scan over each SEG-lane segment (32 or 64) with DPP: row_shr 1/2/4/8
+// inside the 16-lane rows, then row_bcast:15 (and :31 for a 64-lane segment) across
+// them -- no LDS-crossbar round trips (ds_bpermute) on TESA's serial row chain
+template <int SEG> __device__ __forceinline__ uint32_t seg_scan_min( uint32_t x )
+{
+    constexpr int I = (int)0xFFFFFFFF;
+    x = min( x, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)x, 0x111, 0xF, 0xF, false ) );
+    x = min( x, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)x, 0x112, 0xF, 0xF, false ) );
+    x = min( x, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)x, 0x114, 0xF, 0xF, false ) );
+    x = min( x, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)x, 0x118, 0xF, 0xF, false ) );
+    x = min( x, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)x, 0x142, 0xA, 0xF, false ) );
+    if constexpr( SEG == 64 )
+        x = min( x, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)x, 0x143, 0xC, 0xF, false ) );
+    return x;
+}
+
+// value of lane `l` of this lane's segment (l compile-time or wave-uniform), via readlane
+template <int SEG> __device__ __forceinline__ uint32_t seg_lane( uint32_t v, int l, int sg )
+{
+    if constexpr( SEG == 64 )
+        return (uint32_t)__builtin_amdgcn_readlane( (int)v, l );
+    else
+    {
+        const uint32_t a = (uint32_t)__builtin_amdgcn_readlane( (int)v, l );
+        const uint32_t b = (uint32_t)__builtin_amdgcn_readlane( (int)v, 32 + l );
+        return sg ? b : a;
+    }
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
 {
 #pragma unroll
@@ -1053,13 +1082,18 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     using pixel = typename PT<BD>::pixel;
     constexpr int NDW = 16 / PT<BD>::PPD;                     // dwords per fenc row
     constexpr int NSEG = 64 / SEG;
-    extern __shared__ uint64_t tesa_lds[];                    // NSEG lists of { sad, mx | my << 16 }
+    // NSEG mvsads lists.  64-lane segments: { cost, mx | my << 16 } in 8 bytes; 32-lane
+    // segments (me_range <= 16: < 32 columns, <= 33 rows, cost < 2^20) pack cost << 11 |
+    // row << 5 | column into 4 bytes, which halves the LDS a workgroup holds (2 -> 4 waves
+    // per SIMD with 128 VGPRs)
+    using E = typename std::conditional<SEG == 32, uint32_t, uint64_t>::type;
+    extern __shared__ uint64_t tesa_lds[];
     __shared__ uint32_t fls[NSEG][16 * NDW];
     const int sg = (int)threadIdx.x / SEG, lane = (int)threadIdx.x % SEG;
     const int64_t mbo = (int64_t)blockIdx.x * NSEG + sg;      // this segment's MB
     const int64_t mb = mbo < nmb ? mbo : nmb - 1;             // a spare segment repeats the last MB
     const uint64_t segmask = SEG == 64 ? ~0ull : 0xFFFFFFFFull << (32 * sg);
-    uint64_t *mvsads = tesa_lds + (int64_t)sg * cap;
+    E *mvsads = (E *)tesa_lds + (int64_t)sg * cap;
     uint32_t *fl = fls[sg];
     auto sball = [&]( bool c ) { return (uint64_t)__ballot( c ) & segmask; };
     auto rank = [&]( uint64_t m ) {
@@ -1079,6 +1113,15 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     const int min_x = max( bmx0 - me_range, (int)p[4] ), min_y = max( bmy0 - me_range, (int)p[5] );
     const int max_x = min( bmx0 + me_range, (int)p[6] ), max_y = min( bmy0 + me_range, (int)p[7] );
     const int width = (max_x - min_x + 3) & ~3;
+    auto ent = [&]( uint32_t cost, int ex, int ey ) -> E {
+        if constexpr( SEG == 32 )
+            return (cost << 11) | (uint32_t)((ey - min_y) << 5) | (uint32_t)(ex - min_x);
+        else
+            return (uint64_t)cost | ((uint64_t)(uint16_t)ex << 32) | ((uint64_t)(uint16_t)ey << 48);
+    };
+    auto ecost = []( E e ) -> uint32_t { return SEG == 32 ? (uint32_t)(e >> 11) : (uint32_t)e; };
+    auto emx = [&]( E e ) -> int { return SEG == 32 ? min_x + (int)(e & 31) : (int)(int16_t)(e >> 32); };
+    auto emy = [&]( E e ) -> int { return SEG == 32 ? min_y + (int)((e >> 5) & 63) : (int)(int16_t)(e >> 48); };
 
     // fenc -> LDS (row-major dwords) and enc_dc (sad_x4 against x264_zero = the four 8x8 sums)
     uint32_t dcq[4] = { 0, 0, 0, 0 };
@@ -1125,7 +1168,7 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     // ycost of row r in segment lane r (rows SEG.. in the second register)
     const int yc0 = lane < rows ? (int)cy[(min_y + lane) * 4] : 0;
     const int yc1 = lane + SEG < rows ? (int)cy[(min_y + lane + SEG) * 4] : 0;
-    auto ycost_of = [&]( int r ) { return __shfl( r < SEG ? yc0 : yc1, sg * SEG + (r % SEG) ); };
+    auto ycost_of = [&]( int r ) { return (int)seg_lane<SEG>( (uint32_t)(r < SEG ? yc0 : yc1), r % SEG, sg ); };
 
     // Phase 1 (independent of the scan state, so every load is in flight at once): each
     // row's ads4 value, and the cost of every candidate that can still pass some row's
@@ -1175,23 +1218,16 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         // a passing lane's cost was staged (b <= bsad0 - ycost), or is computed now
         const uint32_t s = pass ? (TAB ? sv[r] : sad_at( mx, my ) + (uint32_t)fpel) : 0xFFFFFFFFu;
         // exclusive prefix minimum over the segment's lanes (the earlier survivors of this row)
-        uint32_t incl = s;
-#pragma unroll
-        for( int off = 1; off < SEG; off <<= 1 )
-        {
-            const uint32_t o = (uint32_t)__shfl_up( (int)incl, off );
-            incl = lane >= off ? min( incl, o ) : incl;
-        }
-        uint32_t excl = (uint32_t)__shfl_up( (int)incl, 1 );
-        excl = lane ? excl : 0xFFFFFFFFu;
+        const uint32_t incl = seg_scan_min<SEG>( s );
+        uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)incl, 0x138, 0xF, 0xF, false );
+        excl = lane ? excl : 0xFFFFFFFFu;                   // wave_shr:1 crosses into segment 1's lane 0
         const int bcur = (int)min( (uint32_t)b, excl );
         const bool app = pass && (int)s < (bcur * sad_thresh0 >> 3);
         const uint64_t m = sball( app );
         if( app )
-            mvsads[nmvsad + rank( m )] = (uint64_t)(s + (uint32_t)ycost) | ((uint64_t)(uint16_t)mx << 32) |
-                                         ((uint64_t)(uint16_t)my << 48);
+            mvsads[nmvsad + rank( m )] = ent( s + (uint32_t)ycost, mx, my );
         nmvsad += __popcll( m );
-        const uint32_t rmin = (uint32_t)__shfl( (int)incl, sg * SEG + SEG - 1 );
+        const uint32_t rmin = seg_lane<SEG>( incl, SEG - 1, sg );
         if( sball( pass ) )
             bsad = min( bsad, (int)rmin + ycost );            // b_final + ycost
     }
@@ -1211,8 +1247,8 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         {
             const int j = base + lane;
             const bool in = need && j < nmvsad;
-            const uint64_t e = in ? mvsads[j] : 0;
-            const bool keep = in && (int)(uint32_t)e <= thr;
+            const E e = in ? mvsads[j] : (E)0;
+            const bool keep = in && (int)ecost( e ) <= thr;
             const uint64_t m = sball( keep );
             if( keep )
                 mvsads[k + rank( m )] = e;
@@ -1232,7 +1268,7 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         {
             if( need && j < nmvsad )
             {
-                const uint64_t k = ((uint64_t)(uint32_t)mvsads[j] << 32) | (uint32_t)~j;
+                const uint64_t k = ((uint64_t)ecost( mvsads[j] ) << 32) | (uint32_t)~j;
                 key = k > key ? k : key;
             }
         }
@@ -1262,9 +1298,9 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         int cmx = 0, cmy = 0;
         if( k < nmvsad )
         {
-            const uint64_t e = mvsads[k];
-            cmx = (int16_t)(e >> 32);
-            cmy = (int16_t)(e >> 48);
+            const E e = mvsads[k];
+            cmx = emx( e );
+            cmy = emy( e );
             const int bx = 8 * (part & 1), by = 4 * (part >> 1);
             constexpr int HDW = 8 / PT<BD>::PPD;
             uint32_t a[4][HDW], rr[4][HDW];
@@ -1305,10 +1341,10 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         int32_t bcost = init_cost[mb], rx = bmx0, ry = bmy0;
         if( best != 0xFFFFFFFFu && (int32_t)(best >> 6) < bcost )
         {
-            const uint64_t e = mvsads[best & 63];
+            const E e = mvsads[best & 63];
             bcost = (int32_t)(best >> 6);
-            rx = (int16_t)(e >> 32);
-            ry = (int16_t)(e >> 48);
+            rx = emx( e );
+            ry = emy( e );
         }
         out[4 * mb] = bcost;
         out[4 * mb + 1] = rx;
@@ -1333,7 +1369,7 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
 #define TESA_GO( NR, SEG, T )                                                                                    \
     hipLaunchKernelGGL( ( me_tesa_kernel<BD, NR, SEG, T> ), dim3( (unsigned)((nmb + 64 / SEG - 1) / (64 / SEG)) ),   \
-                        dim3( 64 ), (64 / SEG) * (size_t)cap * sizeof( uint64_t ), stream, fenc, fs, ffs, ref, rs,  \
+                        dim3( 64 ), (64 / SEG) * (size_t)cap * (SEG == 32 ? 4 : 8), stream, fenc, fs, ffs, ref, rs, \
                         rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost,    \
                         cost_mv, out, cap )
     if( me_range <= 16 )
