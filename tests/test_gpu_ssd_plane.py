@@ -25,13 +25,6 @@ def _frames(bd, n, w, h, seed, kind="random"):
     return a, b, stride, 32 * stride + 32
 
 
-@pytest.fixture(params=[None, "1"], ids=["ssd2", "ssd1"])
-def ssdv(request, hip):
-    """default kernel (plane_ssd2_kernel) and X264HIP_SSD_VARIANT=1 (plane_ssd_kernel)"""
-    hip.set_variant("X264HIP_SSD_VARIANT", request.param)
-    return request.param
-
-
 def _dev(p, bd):
     return torch.from_numpy(p.view(np.int16) if bd == 10 else p).cuda()
 
@@ -40,7 +33,7 @@ def _dev(p, bd):
 @pytest.mark.parametrize("w,h,n,kind", [(1920, 1080, 3, "random"), (1917, 1083, 2, "random"), (7, 5, 2, "random"),
                                         (3840, 2160, 1, "random"), (1920, 1080, 1, "extreme"), (8, 8, 4, "random"),
                                         (1920, 1088, 2, "shifted"), (2100, 37, 2, "random")])
-def test_ssd_plane(hip, oracle, ssdv, bd, w, h, n, kind):
+def test_ssd_plane(hip, oracle, bd, w, h, n, kind):
     a, b, stride, org = _frames(bd, n, w, h, w + h + n, kind)
     if kind == "shifted":
         org += 3                                      # chunks off 16-byte alignment
@@ -51,7 +44,7 @@ def test_ssd_plane(hip, oracle, ssdv, bd, w, h, n, kind):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("w,h,n", [(960, 540, 2), (957, 541, 2), (5, 3, 2), (1920, 1080, 1)])
-def test_ssd_nv12(hip, oracle, ssdv, bd, w, h, n):
+def test_ssd_nv12(hip, oracle, bd, w, h, n):
     a, b, stride, org = _frames(bd, n, 2 * w, h, w * 3 + h)
     got = hip.ssd_nv12_batch(_dev(a, bd), org, stride, _dev(b, bd), org, stride, w, h, n).cpu().numpy()
     for f in range(n):

@@ -772,97 +772,6 @@ __global__ __launch_bounds__( 256 ) void plane_ssd_kernel( const typename PT<BD>
     }
 }
 
-// Default plane SSD kernel: a wave covers 128 chunks of a row (two per lane, 2 KB of an
-// 8-bit 1080p row) over SSD_ROWS2 rows, so consecutive lanes and instructions read
-// consecutive bytes of a few rows, with all 4 * SSD_ROWS2 loads in flight before the
-// arithmetic; twice the waves of plane_ssd_kernel at 1080p and no scalar band at the
-// bottom (rows past the plane are skipped per row, wave-uniformly; only a partial chunk
-// at the right edge takes the per-pixel path).
-constexpr int SSD_ROWS2 = 4;
-template <int BD, bool NV12>
-__global__ __launch_bounds__( 256 ) void plane_ssd2_kernel( const typename PT<BD>::pixel *__restrict__ p1, intptr_t s1,
-                                                            intptr_t f1, const typename PT<BD>::pixel *__restrict__ p2,
-                                                            intptr_t s2, intptr_t f2, int c0, int c1, int height,
-                                                            unsigned long long *__restrict__ out )
-{
-    typedef typename PT<BD>::pixel pixel;
-    constexpr int CH = 16 / (int)sizeof( pixel );
-    __shared__ uint64_t part[2][4];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const int f = blockIdx.z;
-    const int y0 = ((int)blockIdx.y * 4 + wv) * SSD_ROWS2;
-    const int nr = min( SSD_ROWS2, height - y0 );            // wave-uniform; <= 0: nothing
-    const int xa = c0 + ((int)blockIdx.x * 128 + lane) * CH, xb = xa + 64 * CH;
-    const pixel *a = p1 + f * f1 + (intptr_t)y0 * s1, *b = p2 + f * f2 + (intptr_t)y0 * s2;
-    const bool fa = xa + CH <= c1, fb = xb + CH <= c1;
-    uint32_t iu = 0, iv = 0;
-    if( nr > 0 )
-    {
-        uint4 va[SSD_ROWS2][2], vb[SSD_ROWS2][2];
-        const uint4 z = make_uint4( 0, 0, 0, 0 );
-#pragma unroll
-        for( int r = 0; r < SSD_ROWS2; r++ )
-        {
-            const bool live = r < nr;
-            va[r][0] = vb[r][0] = va[r][1] = vb[r][1] = z;
-            if( live && fa )
-            {
-                __builtin_memcpy( &va[r][0], a + r * s1 + xa, 16 );
-                __builtin_memcpy( &vb[r][0], b + r * s2 + xa, 16 );
-            }
-            if( live && fb )
-            {
-                __builtin_memcpy( &va[r][1], a + r * s1 + xb, 16 );
-                __builtin_memcpy( &vb[r][1], b + r * s2 + xb, 16 );
-            }
-        }
-#pragma unroll
-        for( int r = 0; r < SSD_ROWS2; r++ )
-        {
-            ssd_chunk<BD, NV12>( va[r][0], vb[r][0], iu, iv );   // zero pairs add nothing
-            ssd_chunk<BD, NV12>( va[r][1], vb[r][1], iu, iv );
-        }
-        // a partial chunk at the right edge (at most one lane of the grid row)
-        const int xp = !fa && xa < c1 ? xa : !fb && xb < c1 ? xb : -1;
-        if( xp >= 0 )
-            for( int r = 0; r < nr; r++ )
-                for( int x = xp; x < c1; x++ )
-                {
-                    const int d = (int)a[r * s1 + x] - (int)b[r * s2 + x];
-                    if( NV12 && (x & 1) )
-                        iv += (uint32_t)(d * d);
-                    else
-                        iu += (uint32_t)(d * d);
-                }
-    }
-    uint64_t su = iu, sv = iv;
-#pragma unroll
-    for( int off = 32; off >= 1; off >>= 1 )
-    {
-        su += (uint64_t)__shfl_xor( (unsigned long long)su, off );
-        if( NV12 )
-            sv += (uint64_t)__shfl_xor( (unsigned long long)sv, off );
-    }
-    if( lane == 0 )
-    {
-        part[0][wv] = su;
-        part[1][wv] = sv;
-    }
-    __syncthreads();
-    if( threadIdx.x == 0 )
-    {
-        su = part[0][0] + part[0][1] + part[0][2] + part[0][3];
-        if( su )
-            atomicAdd( out + (NV12 ? 2 * f : f), (unsigned long long)su );
-        if( NV12 )
-        {
-            sv = part[1][0] + part[1][1] + part[1][2] + part[1][3];
-            if( sv )
-                atomicAdd( out + 2 * f + 1, (unsigned long long)sv );
-        }
-    }
-}
-
 template <int BD>
 hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_t s1, intptr_t f1,
                              const typename PT<BD>::pixel *p2, intptr_t s2, intptr_t f2, int width, int height,
@@ -876,22 +785,9 @@ hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_
     if( nframes > 65535 )
         return hipErrorInvalidValue;
     constexpr int CH = 16 / (int)sizeof( typename PT<BD>::pixel );
-    const bool v1 = variant( V_SSD ) == 1;                  // X264HIP_SSD_VARIANT=1: plane_ssd_kernel
     auto go = [&]( int c0, int c1 ) {
         const int nch = (c1 - c0 + CH - 1) / CH;
         unsigned long long *o = (unsigned long long *)out;
-        if( !v1 )
-        {
-            dim3 g( (unsigned)((nch + 127) / 128), (unsigned)((height + 4 * SSD_ROWS2 - 1) / (4 * SSD_ROWS2)),
-                    (unsigned)nframes ), blk( 256 );
-            if( nv12 )
-                hipLaunchKernelGGL( ( plane_ssd2_kernel<BD, true> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0, c1,
-                                    height, o );
-            else
-                hipLaunchKernelGGL( ( plane_ssd2_kernel<BD, false> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0,
-                                    c1, height, o );
-            return;
-        }
         dim3 g( (unsigned)((nch + 63) / 64), (unsigned)((height + 4 * SSD_ROWS - 1) / (4 * SSD_ROWS)),
                 (unsigned)nframes ), blk( 256 );
         if( nv12 )
