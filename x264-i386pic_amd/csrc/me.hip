@@ -14,6 +14,7 @@
 // lane lifetime.  Candidate my finishes at row my+15 and is stored then.
 #include "hipcommon.h"
 #include <stdlib.h>
+#include <atomic>
 #include <utility>
 
 namespace x264hip {
@@ -1353,6 +1354,41 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     }
 }
 
+// the predictor pairs (par[8*mb], par[8*mb+1]) as me_window's centre array
+__global__ __launch_bounds__( 256 ) void tesa_centre_kernel( int nmb, const int16_t *__restrict__ par,
+                                                             int16_t *__restrict__ centre )
+{
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if( i < nmb )
+    {
+        centre[2 * i] = par[8 * i];
+        centre[2 * i + 1] = par[8 * i + 1];
+    }
+}
+
+// stream-ordered scratch for the self-contained TESA: the device's default pool keeps
+// freed blocks (release threshold raised once per device), so a repeated call re-uses
+// them instead of mapping fresh pages
+static hipError_t tesa_scratch( void **p, size_t bytes, hipStream_t stream )
+{
+    static std::atomic<uint32_t> pooled{ 0 };
+    int dev = 0;
+    hipError_t e = hipGetDevice( &dev );
+    if( e != hipSuccess )
+        return e;
+    if( dev < 32 && !(pooled.load() & (1u << dev)) )
+    {
+        hipMemPool_t pool;
+        if( hipDeviceGetDefaultMemPool( &pool, dev ) == hipSuccess )
+        {
+            uint64_t thr = UINT64_MAX;
+            (void)hipMemPoolSetAttribute( pool, hipMemPoolAttrReleaseThreshold, &thr );
+        }
+        pooled.fetch_or( 1u << dev );
+    }
+    return hipMallocAsync( p, bytes, stream );
+}
+
 template <int BD>
 hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, const uint16_t *integral,
@@ -1365,6 +1401,34 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
         return hipSuccess;
     if( me_range < 1 || me_range > 32 || nmb > 0x7fffffff )
         return hipErrorInvalidValue;
+    if( !table && me_range <= 24 && variant( V_TESA ) != 1 )
+    {
+        // Self-contained call: the ads-filtered SADs cost a lane 16 unaligned row loads
+        // each, so the kernel is address-path bound (2.6 ms per 16 1080p frames).  Every
+        // window SAD from the full-search kernel around the predictors (0.3 ms) and the
+        // table-reading scan give the same decisions in ~1 ms.  (X264HIP_TESA_VARIANT=1:
+        // the in-kernel SADs.)
+        using sadt = typename PT<BD>::sadt;
+        const int TR = me_range <= 4 ? 4 : me_range <= 8 ? 8 : me_range <= 16 ? 16 : 24;
+        const size_t tab = (size_t)nmb * (2 * TR + 1) * (size_t)((2 * TR + 1 + 3) & ~3) * sizeof( sadt );
+        const size_t bytes = tab + (size_t)nmb * 8;
+        void *buf = nullptr;
+        hipError_t e = tesa_scratch( &buf, bytes, stream );
+        if( e != hipSuccess )
+            return e;
+        sadt *ttab = (sadt *)buf;
+        int16_t *cen = (int16_t *)((uint8_t *)buf + tab), *org = cen + 2 * nmb;
+        hipLaunchKernelGGL( tesa_centre_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream,
+                            (int)nmb, par, cen );
+        e = hipGetLastError();
+        if( e == hipSuccess )
+            e = launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, TR, ttab, cen, org, stream );
+        if( e == hipSuccess )
+            e = launch_me_tesa<BD>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nframes, me_range, satd,
+                                    ttab, TR, org, par, init_cost, cost_mv, out, stream );
+        const hipError_t f = hipFreeAsync( buf, stream );
+        return e != hipSuccess ? e : f;
+    }
     // the mvsads list: at most (2*me_range+1) rows x (2*me_range+3)&~3 columns per MB
     const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
 #define TESA_GO( NR, SEG, T )                                                                                    \
