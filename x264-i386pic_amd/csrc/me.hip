@@ -1165,7 +1165,6 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     const int fpel = active ? (int)cx[mx * 4] : 0;           // cost_fpel_mvx[mx] (analyse.c:161-169)
     const int bsad0 = (int)sad_at( bmx0, bmy0 ) + (int)cx[bmx0 * 4] + (int)cy[bmy0 * 4];
     const int rows = max( max_y - min_y + 1, 0 );            // <= 2*me_range+1
-    const int delta = 8 * (int)rs;
     // ycost of row r in segment lane r (rows SEG.. in the second register)
     const int yc0 = lane < rows ? (int)cy[(min_y + lane) * 4] : 0;
     const int yc1 = lane + SEG < rows ? (int)cy[(min_y + lane + SEG) * 4] : 0;
@@ -1175,32 +1174,60 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     // row's ads4 value, and the cost of every candidate that can still pass some row's
     // threshold -- bsad never rises, so row r's ADS threshold is at most
     // (bsad0 - ycost)*17>>4.  Both live in registers (NR rows, compile-time indexed).
+    // Branch-free: every load is issued unconditionally at a clamped (valid) address and
+    // the rows / lanes outside the window are masked afterwards, so the compiler can put
+    // all of them in flight (per-row conditional blocks serialised them), and each
+    // integral row is loaded once although row r's ads reads rows r and r + 8.
     uint32_t adsv[NR], sv[NR];
-#pragma unroll
-    for( int r = 0; r < NR; r++ )
     {
-        adsv[r] = 0xFFFFFFFFu;
-        if( r < rows && active )
+        const int cxm = active ? mx : min_x;
+        uint32_t i0[NR + 8], i8[NR + 8];
+#pragma unroll
+        for( int j = 0; j < NR + 8; j++ )
         {
-            const uint16_t *sp = sums_base + mx + (intptr_t)(min_y + r) * rs;
-            adsv[r] = (uint32_t)(abs( enc_dc[0] - (int)sp[0] ) + abs( enc_dc[1] - (int)sp[8] ) +
-                                 abs( enc_dc[2] - (int)sp[delta] ) + abs( enc_dc[3] - (int)sp[delta + 8] ) + fpel);
+            const uint16_t *sp = sums_base + cxm + (intptr_t)(min_y + min( j, rows + 7 )) * rs;
+            i0[j] = sp[0];
+            i8[j] = sp[8];
+        }
+#pragma unroll
+        for( int r = 0; r < NR; r++ )
+        {
+            const uint32_t a = (uint32_t)(abs( enc_dc[0] - (int)i0[r] ) + abs( enc_dc[1] - (int)i8[r] ) +
+                                          abs( enc_dc[2] - (int)i0[r + 8] ) + abs( enc_dc[3] - (int)i8[r + 8] ) +
+                                          fpel);
+            adsv[r] = r < rows && active ? a : 0xFFFFFFFFu;
         }
     }
-    // with a table the SADs are reads and are staged too; without one each costs 256
-    // absdiffs in the lane, so they are computed in phase 2 only for the lanes that pass
-    // the actual (shrinking) threshold
-#pragma unroll
-    for( int r = 0; r < NR; r++ )
+    // with a table the SADs are reads and are staged too (clamped reads, then the rare
+    // candidate outside the table computed); without one each costs 256 absdiffs in the
+    // lane, so they are computed in phase 2 only for the lanes that pass the actual
+    // (shrinking) threshold
+    if constexpr( TAB )
     {
-        sv[r] = 0xFFFFFFFFu;
-        const int ycost = ycost_of( r );
-        if( TAB && r < rows )
+        const int tx = mx - ox, txc = min( max( tx, 0 ), W - 1 );
+        const bool colin = tx >= 0 && tx < W;
+#pragma unroll
+        for( int r = 0; r < NR; r++ )
         {
-            const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
-            if( adsv[r] < (uint32_t)ub )
-                sv[r] = sad_at( mx, min_y + r ) + (uint32_t)fpel;
+            const int ty = min_y + r - oy;
+            sv[r] = (uint32_t)tab[min( max( ty, 0 ), W - 1 ) * P + txc];
         }
+#pragma unroll
+        for( int r = 0; r < NR; r++ )
+        {
+            const int ycost = ycost_of( r ), ty = min_y + r - oy;
+            const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
+            const bool need = r < rows && adsv[r] < (uint32_t)ub;
+            if( need && !(colin && ty >= 0 && ty < W) )
+                sv[r] = tesa_sad16<BD>( fl, p_fref + (min_y + r) * rs + mx, rs );
+            sv[r] = need ? sv[r] + (uint32_t)fpel : 0xFFFFFFFFu;
+        }
+    }
+    else
+    {
+#pragma unroll
+        for( int r = 0; r < NR; r++ )
+            sv[r] = 0xFFFFFFFFu;
     }
 
     // Phase 2: the reference's row scan over the staged values
