@@ -1120,9 +1120,15 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         else
             return (uint64_t)cost | ((uint64_t)(uint16_t)ex << 32) | ((uint64_t)(uint16_t)ey << 48);
     };
-    auto ecost = []( E e ) -> uint32_t { return SEG == 32 ? (uint32_t)(e >> 11) : (uint32_t)e; };
-    auto emx = [&]( E e ) -> int { return SEG == 32 ? min_x + (int)(e & 31) : (int)(int16_t)(e >> 32); };
-    auto emy = [&]( E e ) -> int { return SEG == 32 ? min_y + (int)((e >> 5) & 63) : (int)(int16_t)(e >> 48); };
+    auto ecost = []( E e ) -> uint32_t {
+        if constexpr( SEG == 32 ) return (uint32_t)(e >> 11); else return (uint32_t)e;
+    };
+    auto emx = [&]( E e ) -> int {
+        if constexpr( SEG == 32 ) return min_x + (int)(e & 31); else return (int)(int16_t)(e >> 32);
+    };
+    auto emy = [&]( E e ) -> int {
+        if constexpr( SEG == 32 ) return min_y + (int)((e >> 5) & 63); else return (int)(int16_t)(e >> 48);
+    };
 
     // fenc -> LDS (row-major dwords) and enc_dc (sad_x4 against x264_zero = the four 8x8 sums)
     uint32_t dcq[4] = { 0, 0, 0, 0 };
@@ -1170,81 +1176,41 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     const int yc1 = lane + SEG < rows ? (int)cy[(min_y + lane + SEG) * 4] : 0;
     auto ycost_of = [&]( int r ) { return (int)seg_lane<SEG>( (uint32_t)(r < SEG ? yc0 : yc1), r % SEG, sg ); };
 
-    // Phase 1 (independent of the scan state, so every load is in flight at once): each
-    // row's ads4 value, and the cost of every candidate that can still pass some row's
-    // threshold -- bsad never rises, so row r's ADS threshold is at most
-    // (bsad0 - ycost)*17>>4.  Both live in registers (NR rows, compile-time indexed).
-    // Branch-free: every load is issued unconditionally at a clamped (valid) address and
-    // the rows / lanes outside the window are masked afterwards, so the compiler can put
-    // all of them in flight (per-row conditional blocks serialised them), and each
-    // integral row is loaded once although row r's ads reads rows r and r + 8.
-    uint32_t adsv[NR], sv[NR];
-    {
-        const int cxm = active ? mx : min_x;
-        uint32_t i0[NR + 8], i8[NR + 8];
-#pragma unroll
-        for( int j = 0; j < NR + 8; j++ )
-        {
-            const uint16_t *sp = sums_base + cxm + (intptr_t)(min_y + min( j, rows + 7 )) * rs;
-            i0[j] = sp[0];
-            i8[j] = sp[8];
-        }
-#pragma unroll
-        for( int r = 0; r < NR; r++ )
-        {
-            const uint32_t a = (uint32_t)(abs( enc_dc[0] - (int)i0[r] ) + abs( enc_dc[1] - (int)i8[r] ) +
-                                          abs( enc_dc[2] - (int)i0[r + 8] ) + abs( enc_dc[3] - (int)i8[r + 8] ) +
-                                          fpel);
-            adsv[r] = r < rows && active ? a : 0xFFFFFFFFu;
-        }
-    }
-    // with a table the SADs are reads and are staged too (clamped reads, then the rare
-    // candidate outside the table computed); without one each costs 256 absdiffs in the
-    // lane, so they are computed in phase 2 only for the lanes that pass the actual
-    // (shrinking) threshold
-    if constexpr( TAB )
-    {
-        const int tx = mx - ox, txc = min( max( tx, 0 ), W - 1 );
-        const bool colin = tx >= 0 && tx < W;
-#pragma unroll
-        for( int r = 0; r < NR; r++ )
-        {
-            const int ty = min_y + r - oy;
-            sv[r] = (uint32_t)tab[min( max( ty, 0 ), W - 1 ) * P + txc];
-        }
-#pragma unroll
-        for( int r = 0; r < NR; r++ )
-        {
-            const int ycost = ycost_of( r ), ty = min_y + r - oy;
-            const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
-            const bool need = r < rows && adsv[r] < (uint32_t)ub;
-            if( need && !(colin && ty >= 0 && ty < W) )
-                sv[r] = tesa_sad16<BD>( fl, p_fref + (min_y + r) * rs + mx, rs );
-            sv[r] = need ? sv[r] + (uint32_t)fpel : 0xFFFFFFFFu;
-        }
-    }
-    else
-    {
-#pragma unroll
-        for( int r = 0; r < NR; r++ )
-            sv[r] = 0xFFFFFFFFu;
-    }
-
-    // Phase 2: the reference's row scan over the staged values
+    // Staging: each row's ads4 value and -- with a table -- the cost of every candidate
+    // that can still pass some row's threshold (bsad never rises, so row r's ADS threshold
+    // is at most (bsad0 - ycost)*17>>4) do not depend on the scan state.  They are loaded
+    // in chunks of CK rows, one chunk ahead of the scan: chunk c + 1's loads are issued
+    // before chunk c's rows are scanned.  Loads are branch-free at clamped (valid)
+    // addresses, the rows / lanes outside the window masked afterwards, and each integral
+    // row is loaded once although row r's ads reads rows r and r + 8.
+    constexpr int CK = 8, NC = (NR + CK - 1) / CK;
+    const int cxm = active ? mx : min_x;
+    const int tx = mx - ox, txc = min( max( tx, 0 ), W - 1 );
+    const bool colin = tx >= 0 && tx < W;
+    auto ldi = [&]( int j, uint32_t &v0, uint32_t &v8 ) {
+        const uint16_t *sp = sums_base + cxm + (intptr_t)(min_y + min( j, rows + 7 )) * rs;
+        v0 = sp[0];
+        v8 = sp[8];
+    };
+    auto ldt = [&]( int r ) -> uint32_t {
+        if constexpr( TAB )
+            return (uint32_t)tab[min( max( min_y + r - oy, 0 ), W - 1 ) * P + txc];
+        else
+            return 0u;
+    };
     int bsad = bsad0;
     int nmvsad = 0;
-#pragma unroll
-    for( int r = 0; r < NR; r++ )
-    {
+    // one row of the reference's scan (me.c:667-703) over its staged values
+    auto scan_row = [&]( int r, uint32_t ads, uint32_t sr ) {
         const int my = min_y + r;
         const int ycost = ycost_of( r );
         const bool rowok = r < rows && bsad > ycost;
         const int b = bsad - ycost;
-        const bool pass = rowok && adsv[r] < (uint32_t)(b * 17 >> 4);
+        const bool pass = rowok && ads < (uint32_t)(b * 17 >> 4);
         if( !any( pass ) )
-            continue;                                       // no segment's bsad changes
+            return;                                         // no segment's bsad changes
         // a passing lane's cost was staged (b <= bsad0 - ycost), or is computed now
-        const uint32_t s = pass ? (TAB ? sv[r] : sad_at( mx, my ) + (uint32_t)fpel) : 0xFFFFFFFFu;
+        const uint32_t s = pass ? (TAB ? sr : sad_at( mx, my ) + (uint32_t)fpel) : 0xFFFFFFFFu;
         // exclusive prefix minimum over the segment's lanes (the earlier survivors of this row)
         const uint32_t incl = seg_scan_min<SEG>( s );
         uint32_t excl = (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)incl, 0x138, 0xF, 0xF, false );
@@ -1258,6 +1224,65 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         const uint32_t rmin = seg_lane<SEG>( incl, SEG - 1, sg );
         if( sball( pass ) )
             bsad = min( bsad, (int)rmin + ycost );            // b_final + ycost
+    };
+    uint32_t a0[CK], a8[CK], b0[CK], b8[CK], tt[CK];        // rows 8c.., rows 8c+8.., table rows 8c..
+#pragma unroll
+    for( int k = 0; k < CK; k++ )
+    {
+        ldi( k, a0[k], a8[k] );
+        ldi( CK + k, b0[k], b8[k] );
+        tt[k] = ldt( k );
+    }
+#pragma unroll
+    for( int c = 0; c < NC; c++ )
+    {
+        uint32_t n0[CK], n8[CK], nt[CK];
+        if( c + 1 < NC )
+        {
+#pragma unroll
+            for( int k = 0; k < CK; k++ )
+            {
+                ldi( CK * (c + 2) + k, n0[k], n8[k] );
+                nt[k] = ldt( CK * (c + 1) + k );
+            }
+        }
+        __builtin_amdgcn_sched_barrier( 0 );
+#pragma unroll
+        for( int k = 0; k < CK; k++ )
+        {
+            const int r = CK * c + k;
+            if( r >= NR )
+                break;
+            const uint32_t av = (uint32_t)(abs( enc_dc[0] - (int)a0[k] ) + abs( enc_dc[1] - (int)a8[k] ) +
+                                           abs( enc_dc[2] - (int)b0[k] ) + abs( enc_dc[3] - (int)b8[k] ) + fpel);
+            const uint32_t ads = r < rows && active ? av : 0xFFFFFFFFu;
+            uint32_t sr = 0xFFFFFFFFu;
+            if constexpr( TAB )
+            {
+                // with a table the SADs are reads (the rare candidate outside it computed)
+                const int ycost = ycost_of( r ), ty = min_y + r - oy;
+                const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
+                const bool need = r < rows && ads < (uint32_t)ub;
+                sr = tt[k];
+                if( need && !(colin && ty >= 0 && ty < W) )
+                    sr = tesa_sad16<BD>( fl, p_fref + (min_y + r) * rs + mx, rs );
+                sr = need ? sr + (uint32_t)fpel : 0xFFFFFFFFu;
+            }
+            scan_row( r, ads, sr );
+        }
+        __builtin_amdgcn_sched_barrier( 0 );
+        if( c + 1 < NC )
+        {
+#pragma unroll
+            for( int k = 0; k < CK; k++ )
+            {
+                a0[k] = b0[k];
+                a8[k] = b8[k];
+                b0[k] = n0[k];
+                b8[k] = n8[k];
+                tt[k] = nt[k];
+            }
+        }
     }
 
     // keep the best few (me.c:705-746)
