@@ -16,10 +16,13 @@ def _frames(synth, bd, w, h, kind, seed=3):
     return synth.random_planes(3, w, h, bd, seed=seed)
 
 
-@pytest.fixture(params=["default", "1", "2", "3", "5"])
+@pytest.fixture(params=["default", "1", "2", "3", "5", "lead0", "lead1", "lead3"])
 def variant(request, monkeypatch):
-    """every kernel variant (X264HIP_ME_VARIANT, read per launch) must be exact"""
-    if request.param != "default":
+    """every kernel variant (X264HIP_ME_VARIANT, read per launch) must be exact, and so must
+    every load lead of the default kernels (X264HIP_ME_LEAD, default 2)"""
+    if request.param.startswith("lead"):
+        _x().set_variant("X264HIP_ME_LEAD", request.param[4:])
+    elif request.param != "default":
         _x().set_variant("X264HIP_ME_VARIANT", request.param)
     return request.param
 
@@ -234,12 +237,14 @@ def test_me_esa_argmin_centred(hip, oracle, bd):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("rng,me_range", [(24, 16), (16, 8), (8, 4), (24, 12)])
-@pytest.mark.parametrize("W,H", [(160, 96), (1920, 1088)])
-def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H):
+@pytest.mark.parametrize("W,H,lead", [(160, 96, None), (160, 96, 0), (160, 96, 1), (1920, 1088, None)])
+def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H, lead):
     """Fused search + ESA decision (x264hip_8_me_search_esa) equals me_search_centred followed by
     me_esa_argmin_at on the GPU, and the oracle's centred table + argmin, over predictor centres,
     clipped windows, mvp-dependent costs and unbeatable predictors."""
     from x264hip import synth
+    if lead is not None:
+        hip.set_variant("X264HIP_ME_LEAD", lead)
     planes, stride, origin = synth.make_sequence(3, W, H, bd, seed=rng + me_range)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
