@@ -726,12 +726,16 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v3_kernel( const uint8_t *_
     const int ibase = ox + 4 * grp + 2 * h - min_x - min_y * width;
     // branch-free: every row loads a (clamped, always valid) row cost and masks the keys
     // of rows / columns outside the window with all ones
+    // the row cost of candidate row c + 1 is loaded while row c is folded (a row of SADs
+    // ahead of its use), the first one before the rows
+    uint32_t ynext = cy[4 * min( max( oy, min_y ), max_y )];
     auto reduce = [&]( int c, uint32_t lo, uint32_t hi ) {
         const int my = oy + c;
         const uint32_t rinv = my >= min_y && my <= max_y ? 0u : 0xFFFFFFFFu;
-        int yi = 4 * min( max( my, min_y ), max_y );
-        asm volatile( "" : "+v"( yi ) );         // the row cost is loaded here, not hoisted
-        const uint32_t ycost = cy[yi];
+        const uint32_t ycost = ynext;
+        int yi = 4 * min( max( my + 1, min_y ), max_y );
+        asm volatile( "" : "+v"( yi ) );         // issued here, not hoisted to the top
+        ynext = cy[yi];
         const uint32_t w = h ? hi : lo;
         const uint32_t ri = (uint32_t)(my * width + ibase);
         const uint32_t k0 = (((w & 0xffff) + (uint32_t)ccost[0] + ycost) << 12) | ri;
@@ -830,12 +834,16 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v5_kernel( const uint16_t *
     const int ccost = cin ? (int)cx[mxc * 4] : 0;
     uint32_t key = 0xFFFFFFFFu;
     const int ibase = mxc - min_x - min_y * width;
+    // the row cost of candidate row c + 1 is loaded while row c is folded (a row of SADs
+    // ahead of its use), the first one before the rows
+    uint32_t ynext = cy[4 * min( max( oy, min_y ), max_y )];
     auto reduce = [&]( int c, uint32_t a0, uint32_t a1 ) {
         const int my = oy + c;
         const uint32_t rinv = my >= min_y && my <= max_y ? 0u : 0xFFFFFFFFu;
-        int yi = 4 * min( max( my, min_y ), max_y );
-        asm volatile( "" : "+v"( yi ) );         // the row cost is loaded here, not hoisted
-        const uint32_t ycost = cy[yi];
+        const uint32_t ycost = ynext;
+        int yi = 4 * min( max( my + 1, min_y ), max_y );
+        asm volatile( "" : "+v"( yi ) );         // issued here, not hoisted to the top
+        ynext = cy[yi];
         const uint32_t sad = h ? a1 : a0;
         const uint32_t k = ((sad + (uint32_t)ccost + ycost) << 12) | (uint32_t)(my * width + ibase);
         key = min( key, k | cinv | rinv );
