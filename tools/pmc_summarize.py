@@ -49,6 +49,6 @@ trace = {"kernel": "me_full_sad16_v3_kernel", "dispatches": len(durs), "headline
          "bench_event_launch_us": b["roofline"]["launch_ms"] * 1e3}
 out["trace"] = trace
 json.dump(trace, open(os.path.join(dst, f"{tag}_me_trace_summary.json"), "w"), indent=1)
-json.dump(out, open(os.path.join(dst, "pmc_me_full.json"), "w"), indent=1)
+json.dump(out, open(os.path.join(dst, f"{tag}_pmc_summary.json"), "w"), indent=1)
 shutil.copy(os.path.join(src, "bench.log"), os.path.join(dst, f"{tag}_bench.log"))
 print(json.dumps(out, indent=1))
