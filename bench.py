@@ -156,7 +156,7 @@ def main():
     absdiff_per_launch = F * mbw * mbh * cand_per_mb * 256
     achieved = absdiff_per_launch / (ev_ms * 1e-3)
     roof = {
-        "kernel": "me_full_sad16_v3_kernel<%d>" % R,
+        "kernel": "me_full_sad16_v7_kernel<%d, 2>" % R,
         "bound": "valu",
         "achieved": achieved / 1e12,
         "peak": SAD_PEAK_ABSDIFF / 1e12,

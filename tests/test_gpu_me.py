@@ -16,7 +16,7 @@ def _frames(synth, bd, w, h, kind, seed=3):
     return synth.random_planes(3, w, h, bd, seed=seed)
 
 
-@pytest.fixture(params=["default", "1", "2", "3", "5", "lead0", "lead1", "lead3"])
+@pytest.fixture(params=["default", "1", "2", "3", "5", "7", "lead0", "lead1", "lead3"])
 def variant(request, monkeypatch):
     """every kernel variant (X264HIP_ME_VARIANT, read per launch) must be exact, and so must
     every load lead of the default kernels (X264HIP_ME_LEAD, default 2)"""

@@ -17,7 +17,7 @@ for bd in (8, 10):
     planes, stride, origin = synth.make_sequence(F + 1, W, H, bd)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
-    vs = [(1, 0)] + ([(3, k) for k in range(4)] if bd == 8 else [(5, k) for k in range(3)])
+    vs = [(1, 0)] + ([(3, k) for k in range(4)] + [(7, 1), (7, 2)] if bd == 8 else [(5, k) for k in range(3)])
 
     def setv(v):
         sys.modules["x264hip"].set_variant("X264HIP_ME_VARIANT", str(v[0]))

@@ -33,9 +33,10 @@ for k, d in out["kernels"].items():
 # per-dispatch durations of the headline kernel from the kernel trace: all
 # dispatches, and the last `steps` ones (the bench's timed region follows its
 # warmup launches of the same kernel; the GPU clock ramps during the first ~100)
+KNAME = b["roofline"]["kernel"].split("<")[0]      # the headline kernel the bench names
 durs = []
 for r in csv.DictReader(open(os.path.join(src, "prof_trace", "run_kernel_trace.csv"))):
-    if "me_full_sad16_v3_kernel" in r["Kernel_Name"]:
+    if KNAME in r["Kernel_Name"]:
         durs.append((int(r["Start_Timestamp"]), (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3))
 durs.sort()
 # the headline leg runs first: its warmup then timed launches are the first warmup + steps
@@ -43,7 +44,7 @@ durs.sort()
 steps, warm = b["steps"], b["warmup"]
 head = durs[:warm + steps]
 timed = head[warm:]
-trace = {"kernel": "me_full_sad16_v3_kernel", "dispatches": len(durs), "headline_dispatches": len(head),
+trace = {"kernel": KNAME, "dispatches": len(durs), "headline_dispatches": len(head),
          "avg_us_headline_all": sum(d for _, d in head) / max(1, len(head)),
          "avg_us_timed_region": sum(d for _, d in timed) / max(1, len(timed)),
          "bench_event_launch_us": b["roofline"]["launch_ms"] * 1e3}

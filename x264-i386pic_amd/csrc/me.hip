@@ -382,6 +382,97 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t 
 
 
 // ---------------------------------------------------------------------------
+// Variant 7 (8 bit): variant 3 with all 16 fenc rows in one lane (no lane pair, no DPP
+// half-sum): up to 16 candidate rows open per ref row (64 v_qsad between two row loads),
+// 2R+16 ref rows per lane, and the lane stores its own four columns.
+template <int R, int L, int Y, class Sink>
+__device__ __forceinline__ void me_row7( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[16][4],
+                                         uint64_t (&acc)[16], Sink &sink, u64x2a4 (&e)[L], u64x2a4 (&o)[L] )
+{
+    constexpr int C0 = Y - 15 > 0 ? Y - 15 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    const uint64_t win[4] = { e[Y % L][0], o[Y % L][0], e[Y % L][1], o[Y % L][1] };
+    if constexpr( Y + L < 2 * R + 16 )
+    {
+        const uint32_t *row = rbase + (Y + L) * rs_dw;
+        e[Y % L] = *(const u64x2a4 *)row;
+        o[Y % L] = *(const u64x2a4 *)(row + 1);
+    }
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint64_t a = r == 0 ? 0ull : acc[c & 15];
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            a = __builtin_amdgcn_qsad_pk_u16_u8( win[k], F[r][k], a );
+        if( r == 15 )
+            sink( c, (uint32_t)a, (uint32_t)(a >> 32) );
+        else
+            acc[c & 15] = a;
+    }
+    __builtin_amdgcn_sched_barrier( 0 );
+}
+
+template <int R, int L, class Sink, int... Ys>
+__device__ __forceinline__ void me_rows7( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[16][4],
+                                          uint64_t (&acc)[16], Sink &sink, std::integer_sequence<int, Ys...> )
+{
+    u64x2a4 e[L], o[L];
+#pragma unroll
+    for( int k = 0; k < L; k++ )
+    {
+        e[k] = *(const u64x2a4 *)(rbase + k * rs_dw);
+        o[k] = *(const u64x2a4 *)(rbase + k * rs_dw + 1);
+    }
+    ( me_row7<R, L, Ys>( rbase, rs_dw, F, acc, sink, e, o ), ... );
+}
+
+template <int R, int L>
+__global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
+                                                                  intptr_t ffs, const uint8_t *__restrict__ ref,
+                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                  int nframes, uint16_t *__restrict__ table,
+                                                                  const int16_t *__restrict__ centre,
+                                                                  int16_t *__restrict__ origin )
+{
+    constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
+    constexpr int P = 4 * G;                    // table row pitch
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)nframes * mbh * mbw * G;
+    if( slot >= total )
+        return;
+    const int grp = (int)(slot % G);
+    const int64_t mb = slot / G;
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+
+    uint32_t F[16][4];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs / 4);
+#pragma unroll
+    for( int r = 0; r < 16; r++ )
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+    int ox, oy;
+    me_window<8, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    if( origin && grp == 0 )
+    {
+        origin[2 * mb] = (int16_t)ox;
+        origin[2 * mb + 1] = (int16_t)oy;
+    }
+    const uint32_t *rbase =
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox + 4 * grp);
+    uint64_t *out = (uint64_t *)(table + mb * ((2 * R + 1) * P) + 4 * grp);
+    auto store = [out]( int c, uint32_t lo, uint32_t hi ) { out[c * (P / 4)] = ((uint64_t)hi << 32) | lo; };
+    uint64_t acc[16];
+    me_rows7<R, L>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 16>{} );
+}
+
+// ---------------------------------------------------------------------------
 // Variant 5 (10 bit, default): the variant-3 layout for 16-bit pixels.  A lane
 // owns two adjacent candidate columns (2g, 2g+1; the first is dword aligned for
 // even R) and half of the fenc rows; per ref row it loads 9 dwords once, forms
@@ -576,8 +667,9 @@ static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intp
     }
 }
 
-// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2, 3 (8 bit)
-// or 5 (10 bit); default 3 at 8 bit, 5 at 10 bit.  (A variant that dropped the padded column
+// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2, 3, 7 (8 bit)
+// or 5 (10 bit); default 7 at 8 bit (0.292 -> 0.281 ms per 16 1080p pairs over variant 3,
+// both with two rows of load lead), 5 at 10 bit.  (A variant that dropped the padded column
 // group and finished the last column in separate waves ran 13-20% slower: the
 // table rows were then written by different waves at different times, so
 // nearly every 128-B line left L2 partially written.)
@@ -610,6 +702,22 @@ static void launch_v3( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intp
     }
 }
 
+template <int R, typename P, typename T>
+static void launch_v7( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
+                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
+                       int16_t *origin )
+{
+    if constexpr( sizeof( P ) == 1 )
+    {
+        if( me_lead() <= 1 )
+            hipLaunchKernelGGL( ( me_full_sad16_v7_kernel<R, 1> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
+                                mbw, mbh, nframes, table, centre, origin );
+        else
+            hipLaunchKernelGGL( ( me_full_sad16_v7_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
+                                mbw, mbh, nframes, table, centre, origin );
+    }
+}
+
 template <int BD>
 hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -618,7 +726,7 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
 {
     int variant = me_variant();
     if( !variant )
-        variant = BD == 8 ? 3 : 5;
+        variant = BD == 8 ? 7 : 5;
     if( (BD != 8 && variant == 3) || (BD == 8 && variant == 5) )
         variant = 1;
     // variants 2/3 need dword-aligned fenc rows, dword-multiple strides and (3) a
@@ -626,7 +734,10 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     if( (((uintptr_t)fenc | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
           (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant >= 3 ? (uintptr_t)ref : 0)) & 3) )
         variant = 1;
-    const int64_t groups = variant == 3   ? 2 * ((2 * range + 1 + 3) / 4)
+    if( variant == 7 && BD != 8 )
+        variant = 1;
+    const int64_t groups = variant == 7   ? (2 * range + 1 + 3) / 4
+                           : variant == 3 ? 2 * ((2 * range + 1 + 3) / 4)
                            : variant == 5 ? 2 * ((2 * range + 2) / 2)
                            : variant == 2 ? 2 * (2 * range + 1)
                                           : (2 * range + 1);
@@ -640,6 +751,8 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
         case R:                                                                                                   \
             if( variant == 5 )                                                                                    \
                 launch_v5<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
+            else if( variant == 7 )                                                                               \
+                launch_v7<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
             else if( variant == 3 )                                                                               \
                 launch_v3<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
             else if( variant == 2 )                                                                               \
