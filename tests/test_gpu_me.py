@@ -237,13 +237,16 @@ def test_me_esa_argmin_centred(hip, oracle, bd):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("rng,me_range", [(24, 16), (16, 8), (8, 4), (24, 12)])
-@pytest.mark.parametrize("W,H,lead", [(160, 96, None), (160, 96, 0), (160, 96, 1), (1920, 1088, None)])
+@pytest.mark.parametrize("W,H,lead", [(160, 96, None), (160, 96, 0), (160, 96, 1), (160, 96, "v3"),
+                                      (1920, 1088, None), (1920, 1088, "v3")])
 def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H, lead):
     """Fused search + ESA decision (x264hip_8_me_search_esa) equals me_search_centred followed by
     me_esa_argmin_at on the GPU, and the oracle's centred table + argmin, over predictor centres,
     clipped windows, mvp-dependent costs and unbeatable predictors."""
     from x264hip import synth
-    if lead is not None:
+    if lead == "v3":                             # the lane-pair kernel (8 bit; 10 bit ignores it)
+        hip.set_variant("X264HIP_ME_VARIANT", 3)
+    elif lead is not None:
         hip.set_variant("X264HIP_ME_LEAD", lead)
     planes, stride, origin = synth.make_sequence(3, W, H, bd, seed=rng + me_range)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()

@@ -868,6 +868,85 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v3_kernel( const uint8_t *_
         atomicMin( keys + 3 * mb, key );
 }
 
+// The fused decision on variant 7's lanes (all 16 fenc rows, four columns per lane): a lane
+// keys its own four columns per finished candidate row, and each of an MB's 9 lanes meets
+// the others through one atomicMin.
+template <int R, int L>
+__global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
+                                                                intptr_t ffs, const uint8_t *__restrict__ ref,
+                                                                intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                int nframes, int me_range,
+                                                                const int16_t *__restrict__ par,
+                                                                const uint16_t *__restrict__ cost_mv,
+                                                                uint32_t *__restrict__ keys )
+{
+    constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
+    constexpr int W = 2 * R + 1;
+    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t total = (int64_t)nframes * mbh * mbw * G;
+    if( slot >= total )
+        return;
+    const int grp = (int)(slot % G);
+    const int64_t mb = slot / G;
+    const int mbx = (int)(mb % mbw);
+    const int64_t t = mb / mbw;
+    const int mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+
+    uint32_t F[16][4];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs / 4);
+#pragma unroll
+    for( int r = 0; r < 16; r++ )
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+    const int16_t *p = par + 8 * mb;
+    const int bmx = p[0], bmy = p[1];
+    const int min_x = max( bmx - me_range, (int)p[4] ), min_y = max( bmy - me_range, (int)p[5] );
+    const int max_x = min( bmx + me_range, (int)p[6] ), max_y = min( bmy + me_range, (int)p[7] );
+    const int width = (max_x - min_x + 3) & ~3;
+    const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
+    int ox, oy;
+    const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };   // the window centre: the predictor
+    me_window<8, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
+    const uint32_t *rbase =
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox + 4 * grp);
+    int ccost[4];
+    uint32_t cinv[4];                            // 0 for a column inside the window, else all ones
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+    {
+        const int col = 4 * grp + k, mx = ox + col;
+        const bool in = col < W && mx >= min_x && mx < min_x + width;
+        cinv[k] = in ? 0u : 0xFFFFFFFFu;
+        ccost[k] = in ? (int)cx[mx * 4] : 0;
+    }
+    uint32_t key = 0xFFFFFFFFu;
+    const int ibase = ox + 4 * grp - min_x - min_y * width;
+    // the row cost of candidate row c + 1 is loaded while row c is folded
+    uint32_t ynext = cy[4 * min( max( oy, min_y ), max_y )];
+    auto reduce = [&]( int c, uint32_t lo, uint32_t hi ) {
+        const int my = oy + c;
+        const uint32_t rinv = my >= min_y && my <= max_y ? 0u : 0xFFFFFFFFu;
+        const uint32_t ycost = ynext;
+        int yi = 4 * min( max( my + 1, min_y ), max_y );
+        asm volatile( "" : "+v"( yi ) );         // issued here, not hoisted to the top
+        ynext = cy[yi];
+        const uint32_t ri = (uint32_t)(my * width + ibase);
+        const uint32_t k0 = (((lo & 0xffff) + (uint32_t)ccost[0] + ycost) << 12) | ri;
+        const uint32_t k1 = (((lo >> 16) + (uint32_t)ccost[1] + ycost) << 12) | (ri + 1);
+        const uint32_t k2 = (((hi & 0xffff) + (uint32_t)ccost[2] + ycost) << 12) | (ri + 2);
+        const uint32_t k3 = (((hi >> 16) + (uint32_t)ccost[3] + ycost) << 12) | (ri + 3);
+        key = min( key, min( min( k0 | cinv[0], k1 | cinv[1] ), min( k2 | cinv[2], k3 | cinv[3] ) ) | rinv );
+        asm volatile( "" : "+v"( key ) );        // fold each row where its sums finish
+    };
+    uint64_t acc[16];
+    me_rows7<R, L>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
+    if( key != 0xFFFFFFFFu )
+        atomicMin( keys + 3 * mb, key );
+}
+
 // out[3*mb] holds the MB's best key (0xFFFFFFFF: nothing evaluated); the strict-< update
 // from the predictor result (COPY3_IF_LT, me.h:87-93) turns it into { cost, mx, my }
 __global__ __launch_bounds__( 256 ) void me_esa_finish_kernel( int nmb, int me_range, const int16_t *__restrict__ par,
@@ -988,16 +1067,24 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
     hipError_t e = hipMemsetAsync( out, 0xFF, (size_t)nmb * 3 * sizeof( int32_t ), stream );
     if( e != hipSuccess )
         return e;
+    // 8 bit: variant 7's lanes (one per column group), X264HIP_ME_VARIANT=3 the lane pairs
+    const bool v7 = BD == 8 && me_variant() != 3;
     const int64_t groups = BD == 8 ? (2 * range + 1 + 3) / 4 : (2 * range + 2) / 2;
-    const int64_t lanes = nmb * 2 * groups;
+    const int64_t lanes = nmb * (v7 ? 1 : 2) * groups;
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
     const int lead = me_lead();
     switch( range )
     {
 #define ESA_GO( R, L )                                                                                            \
     if constexpr( BD == 8 )                                                                                       \
-        hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R, L> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,  \
-                            mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                              \
+    {                                                                                                             \
+        if( v7 )                                                                                                  \
+            hipLaunchKernelGGL( ( me_full_esa_v7_kernel<R, L <= 1 ? 1 : 2> ), g, blk, 0, stream, fenc, fs, ffs,   \
+                                ref, rs, rfs, mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );       \
+        else                                                                                                      \
+            hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R, L> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,   \
+                                mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                     \
+    }                                                                                                             \
     else                                                                                                          \
         hipLaunchKernelGGL( ( me_full_esa_v5_kernel<R, L> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,  \
                             mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );
