@@ -166,12 +166,18 @@ def main():
         "algorithmic_bytes_per_launch": F * (mbw * mbh * 256 + mbw * mbh * 256 + mbw * mbh * cand_per_mb * 2),
         "launch_ms": ev_ms,
     }
-    pmc = os.path.join(ROOT, "profiles", "pmc_me_full.json")
-    if os.path.exists(pmc):
-        with open(pmc) as fh:
+    # HBM bytes per launch from the newest committed PMC summary (tools/gpu_profile.sh +
+    # tools/pmc_summarize.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected),
+    # used only when it profiled this kernel on this workload
+    import glob
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    if pmcs:
+        with open(pmcs[-1]) as fh:
             d = json.load(fh)
-        if d.get("frames") == F and d.get("range") == R and d.get("width") == W:
+        if (d.get("frames") == F and d.get("range") == R and d.get("width") == W
+                and d.get("trace", {}).get("kernel") == roof["kernel"].split("<")[0]):
             roof["traffic"] = d.get("hbm_bytes_per_launch")
+            roof["traffic_source"] = os.path.relpath(pmcs[-1], ROOT)
 
     out = {
         "metric": "SAD+SATD candidate-MVs/sec + DCT+quant blocks/sec, 1080p, 1/2/4/8 GPU",
