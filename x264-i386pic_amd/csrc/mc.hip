@@ -980,8 +980,8 @@ __global__ __launch_bounds__( 256 ) void subpel_qpel9_kernel( const typename PT<
                             v = avg_round<BD>( cv, xs );
                         else if( dx == 0 )
                             v = avg_round<BD>( cv, ys );
-                        else
-                            v = ccxy ? avg_round<BD>( cv, ds ) : avg_round<BD>( xs, ys );
+                        else    // the operands chosen per lane, one average (not two and a select)
+                            v = avg_round<BD>( ccxy ? cv : xs, ccxy ? ds : ys );
                         pr[r][d] = v;
                     }
                 if constexpr( OP == 0 )
