@@ -1249,6 +1249,19 @@ template <int SEG> __device__ __forceinline__ uint32_t seg_scan_min( uint32_t x 
     return x;
 }
 
+// inclusive sum-scan over each SEG-lane segment, as seg_scan_min
+template <int SEG> __device__ __forceinline__ uint32_t seg_scan_add( uint32_t x )
+{
+    x += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)x, 0x111, 0xF, 0xF, false );
+    x += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)x, 0x112, 0xF, 0xF, false );
+    x += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)x, 0x114, 0xF, 0xF, false );
+    x += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)x, 0x118, 0xF, 0xF, false );
+    x += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)x, 0x142, 0xA, 0xF, false );
+    if constexpr( SEG == 64 )
+        x += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)x, 0x143, 0xC, 0xF, false );
+    return x;
+}
+
 // value of lane `l` of this lane's segment (l compile-time or wave-uniform), via readlane
 template <int SEG> __device__ __forceinline__ uint32_t seg_lane( uint32_t v, int l, int sg )
 {
@@ -1353,14 +1366,8 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     }
     int enc_dc[4];
 #pragma unroll
-    for( int j = 0; j < 4; j++ )
-    {
-        uint32_t v = dcq[j];
-#pragma unroll
-        for( int off = SEG / 2; off >= 1; off >>= 1 )
-            v += (uint32_t)__shfl_xor( (int)v, off );
-        enc_dc[j] = (int)v;
-    }
+    for( int j = 0; j < 4; j++ )                              // segment sums: DPP scan + readlane
+        enc_dc[j] = (int)seg_lane<SEG>( seg_scan_add<SEG>( dcq[j] ), SEG - 1, sg );
     __syncthreads();
 
     const int W = 2 * R + 1, P = (W + 3) & ~3;
@@ -1585,18 +1592,18 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
                         v = sadp<BD>( a[y][j], rr[y][j], v );
             }
         }
-        v += (uint32_t)__shfl_xor( (int)v, 1 );
-        v += (uint32_t)__shfl_xor( (int)v, 2 );
-        v += (uint32_t)__shfl_xor( (int)v, 4 );
+        // the eight units of a candidate (lanes 8k .. 8k+7): quad sums by quad_perm, then
+        // row_ror:12 brings lane 8k+4's quad sum to lane 8k
+        v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0xB1, 0xF, 0xF, false );
+        v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0x4E, 0xF, 0xF, false );
+        v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0x12C, 0xF, 0xF, false );
         if( k < nmvsad && part == 0 )
         {
             const uint32_t cost = v + cx[cmx * 4] + cy[cmy * 4];
             best = min( best, (cost << 6) | (uint32_t)k );   // k < 64: first index on ties
         }
     }
-#pragma unroll
-    for( int off = SEG / 2; off >= 1; off >>= 1 )
-        best = min( best, (uint32_t)__shfl_xor( (int)best, off ) );
+    best = seg_lane<SEG>( seg_scan_min<SEG>( best ), SEG - 1, sg );
     if( lane == 0 && mbo < nmb )
     {
         int32_t bcost = init_cost[mb], rx = bmx0, ry = bmy0;
