@@ -18,6 +18,8 @@ class A:
 
 def main():
     x = load_package()
+    if os.environ.get("TESA_LIB"):                   # an A/B build of the library
+        x.LIB_PATH = os.path.abspath(os.environ["TESA_LIB"])
     x.init(0)
     from x264hip import synth
     W, H, F = 1920, 1088, 16

@@ -1283,6 +1283,13 @@ __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
     return v;
 }
 
+// rows per staging chunk of the TESA scan (a build-time knob for A/B builds; divides the
+// 8-row ads offset): 4 rows 0.656 ms per 16 1080p frames (128 VGPRs, 4 waves/SIMD), 2 rows
+// 0.659, 8 rows 0.696 (158 VGPRs, 3 waves)
+#ifndef TESA_CK
+#define TESA_CK 4
+#endif
+
 // SEG lanes per MB: 64 (one MB per wave, me_range <= 32) or 32 (two MBs per wave,
 // me_range <= 16: a row of <= 32 columns fits half a wave), so a wave's serial row
 // chain serves two MBs.  Every per-MB value is uniform within its segment; ballots are
@@ -1398,7 +1405,7 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
     // before chunk c's rows are scanned.  Loads are branch-free at clamped (valid)
     // addresses, the rows / lanes outside the window masked afterwards, and each integral
     // row is loaded once although row r's ads reads rows r and r + 8.
-    constexpr int CK = 8, NC = (NR + CK - 1) / CK;
+    constexpr int CK = TESA_CK, NC = (NR + CK - 1) / CK;
     const int cxm = active ? mx : min_x;
     const int tx = mx - ox, txc = min( max( tx, 0 ), W - 1 );
     const bool colin = tx >= 0 && tx < W;
@@ -1440,14 +1447,19 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         if( sball( pass ) )
             bsad = min( bsad, (int)rmin + ycost );            // b_final + ycost
     };
-    uint32_t a0[CK], a8[CK], b0[CK], b8[CK], tt[CK];        // rows 8c.., rows 8c+8.., table rows 8c..
+    // integral rows in a ring of D chunks: chunk c's ads reads its own rows (slot c % D) and
+    // the rows 8 below (slot (c + 8 / CK) % D); table rows for the current chunk only
+    static_assert( CK == 1 || CK == 2 || CK == 4 || CK == 8, "CK divides the 8-row ads offset" );
+    constexpr int D = 8 / CK + 1;
+    uint32_t i0[D][CK], i8[D][CK], tt[CK];
+#pragma unroll
+    for( int q = 0; q < D; q++ )
+#pragma unroll
+        for( int k = 0; k < CK; k++ )
+            ldi( CK * q + k, i0[q][k], i8[q][k] );
 #pragma unroll
     for( int k = 0; k < CK; k++ )
-    {
-        ldi( k, a0[k], a8[k] );
-        ldi( CK + k, b0[k], b8[k] );
         tt[k] = ldt( k );
-    }
 #pragma unroll
     for( int c = 0; c < NC; c++ )
     {
@@ -1457,19 +1469,21 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
 #pragma unroll
             for( int k = 0; k < CK; k++ )
             {
-                ldi( CK * (c + 2) + k, n0[k], n8[k] );
+                ldi( CK * (c + D) + k, n0[k], n8[k] );    // chunk c + D, into slot c % D after use
                 nt[k] = ldt( CK * (c + 1) + k );
             }
         }
         __builtin_amdgcn_sched_barrier( 0 );
+        const int st = c % D, sb = (c + 8 / CK) % D;
 #pragma unroll
         for( int k = 0; k < CK; k++ )
         {
             const int r = CK * c + k;
             if( r >= NR )
                 break;
-            const uint32_t av = (uint32_t)(abs( enc_dc[0] - (int)a0[k] ) + abs( enc_dc[1] - (int)a8[k] ) +
-                                           abs( enc_dc[2] - (int)b0[k] ) + abs( enc_dc[3] - (int)b8[k] ) + fpel);
+            const uint32_t av = (uint32_t)(abs( enc_dc[0] - (int)i0[st][k] ) + abs( enc_dc[1] - (int)i8[st][k] ) +
+                                           abs( enc_dc[2] - (int)i0[sb][k] ) + abs( enc_dc[3] - (int)i8[sb][k] ) +
+                                           fpel);
             const uint32_t ads = r < rows && active ? av : 0xFFFFFFFFu;
             uint32_t sr = 0xFFFFFFFFu;
             if constexpr( TAB )
@@ -1491,10 +1505,8 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
 #pragma unroll
             for( int k = 0; k < CK; k++ )
             {
-                a0[k] = b0[k];
-                a8[k] = b8[k];
-                b0[k] = n0[k];
-                b8[k] = n8[k];
+                i0[st][k] = n0[k];
+                i8[st][k] = n8[k];
                 tt[k] = nt[k];
             }
         }
