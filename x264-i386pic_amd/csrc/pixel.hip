@@ -564,9 +564,9 @@ hipError_t launch_ads_batch( int i_pixel, const int32_t *enc_dc, const uint16_t 
 constexpr int INTEGRAL_STRIP = 64;
 
 template <int BD, bool SUB8>
-__global__ __launch_bounds__( 256 ) void integral_kernel( const typename PT<BD>::pixel *plane, intptr_t stride,
-                                                          intptr_t fstride, int lines, int padh, uint16_t *integral,
-                                                          intptr_t ifstride )
+__global__ __launch_bounds__( 256 ) void integral_kernel( const typename PT<BD>::pixel *__restrict__ plane,
+                                                          intptr_t stride, intptr_t fstride, int lines, int padh,
+                                                          uint16_t *__restrict__ integral, intptr_t ifstride )
 {
     constexpr int PADV = 32;
     constexpr int PPD = PT<BD>::PPD;
@@ -583,17 +583,23 @@ __global__ __launch_bounds__( 256 ) void integral_kernel( const typename PT<BD>:
     uint16_t *o4 = o8 + stride * (lines + 2 * PADV);
     uint32_t ring8[8] = {}, ring4[4] = {};
     uint32_t acc8 = 0, acc4 = 0;
-    // input rows t0 .. t1+6; after adding row r, acc8 holds rows r-7..r, acc4 rows r-3..r
+    // input rows t0 .. t1+6; after adding row r, acc8 holds rows r-7..r, acc4 rows r-3..r.
+    // A batch's eight row loads are issued together at clamped (valid) rows before any
+    // of them is summed (a per-row guard around each load serialised them: one memory
+    // round trip per row); rows past the strip only feed stores that are masked off.
     for( int r0 = t0; r0 < t1 + 7; r0 += 8 )
     {
+        uint32_t wb[8][8 / PPD];
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+            load_packed<8 / PPD>( src + (intptr_t)min( r0 + k, t1 + 6 ) * stride, wb[k] );
 #pragma unroll
         for( int k = 0; k < 8; k++ )
         {
             const int r = r0 + k;
             if( r < t1 + 7 )
             {
-                uint32_t w[8 / PPD];
-                load_packed<8 / PPD>( src + (intptr_t)r * stride, w );
+                const uint32_t( &w )[8 / PPD] = wb[k];
                 uint32_t h4 = 0, h8 = 0;
 #pragma unroll
                 for( int x = 0; x < 4; x++ )
