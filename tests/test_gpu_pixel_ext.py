@@ -215,11 +215,15 @@ def test_ads_batch_random(hip, oracle, bd):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("sub8x8", [False, True])
-def test_frame_integral(hip, oracle, bd, sub8x8):
+@pytest.mark.parametrize("W,H,variant", [(176, 144, None), (176, 144, 1), (1920, 1088, None)])
+def test_frame_integral(hip, oracle, bd, sub8x8, W, H, variant):
     """whole padded frames (edge-replicated borders, maxed corner), 3 frames per call, against
-    the reference's integral_init loop restated (rows [1-PADV, lines+PADV-8), cols [-PADH, stride-PADH-8))."""
+    the reference's integral_init loop restated (rows [1-PADV, lines+PADV-8), cols [-PADH, stride-PADH-8));
+    the dword-lane kernel (default) and the column-per-lane one (X264HIP_INTEGRAL_VARIANT=1)."""
     from x264hip import synth
-    W, H, n = 176, 144, 3
+    if variant is not None:
+        hip.set_variant("X264HIP_INTEGRAL_VARIANT", variant)
+    n = 3
     planes, stride, origin = synth.make_sequence(n, W, H, bd, start=5)
     planes[1, 40:60, 40:80] = (1 << bd) - 1
     dev = _dev(planes, bd)

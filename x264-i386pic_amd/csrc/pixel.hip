@@ -621,6 +621,112 @@ __global__ __launch_bounds__( 256 ) void integral_kernel( const typename PT<BD>:
     }
 }
 
+// Default form: one lane per source dword (4 columns at 8 bit, 2 at 10 bit).  A lane
+// loads the dwords covering its columns' 8-pixel windows once per row (three at 8 bit, five
+// at 10 bit; neighbouring lanes share cache lines), forms each column's 4- and 8-pixel sums
+// from byte-shifted dwords with v_sad against zero, and stores its columns' sums as one
+// 8- (4-) byte store: 3 loads and 1-2 stores per 4 columns against 8 and 4-8 before.
+template <int BD, bool SUB8>
+__global__ __launch_bounds__( 256 ) void integral_dw_kernel( const typename PT<BD>::pixel *__restrict__ plane,
+                                                             intptr_t stride, intptr_t fstride, int lines, int padh,
+                                                             uint16_t *__restrict__ integral, intptr_t ifstride )
+{
+    constexpr int PADV = 32;
+    constexpr int PPD = PT<BD>::PPD;                        // columns per lane
+    constexpr int ND = 8 / PPD + 1;                          // dwords per row window
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;     // dword index, column PPD * j
+    const int c0 = PPD * j, ncol = (int)stride - 8;
+    if( c0 >= ncol )
+        return;
+    const int rows_end = lines + 2 * PADV - 8;
+    const int t0 = 1 + blockIdx.y * INTEGRAL_STRIP;
+    if( t0 >= rows_end )
+        return;
+    const int t1 = min( t0 + INTEGRAL_STRIP, rows_end );
+    const uint32_t *src = (const uint32_t *)(plane + blockIdx.z * fstride - PADV * stride - padh) + j;
+    const intptr_t sdw = stride / PPD;
+    uint16_t *o8 = integral + blockIdx.z * ifstride - PADV * stride - padh + c0;
+    uint16_t *o4 = o8 + stride * (lines + 2 * PADV);
+    const bool whole = c0 + PPD <= ncol;
+    uint32_t ring8[8][PPD] = {}, ring4[4][PPD] = {};
+    uint32_t acc8[PPD] = {}, acc4[PPD] = {};
+    for( int r0 = t0; r0 < t1 + 7; r0 += 8 )
+    {
+        uint32_t wb[8][ND];
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+        {
+            const uint32_t *rp = src + (intptr_t)min( r0 + k, t1 + 6 ) * sdw;
+#pragma unroll
+            for( int d = 0; d < ND; d++ )
+                wb[k][d] = rp[d];
+        }
+#pragma unroll
+        for( int k = 0; k < 8; k++ )
+        {
+            const int r = r0 + k;
+            if( r >= t1 + 7 )
+                break;
+            uint32_t h4[PPD], h8[PPD];
+#pragma unroll
+            for( int s = 0; s < PPD; s++ )
+            {
+                // column c0 + s: pixels s .. s+3 and s+4 .. s+7 of the window
+                constexpr int SB = BD == 8 ? 1 : 2;          // bytes per pixel
+                uint32_t lo[4 / PPD], hi[4 / PPD];
+#pragma unroll
+                for( int d = 0; d < 4 / PPD; d++ )
+                {
+                    const int b = s * SB;                    // byte shift within dword d
+                    lo[d] = b ? __builtin_amdgcn_alignbyte( wb[k][d + 1], wb[k][d], b ) : wb[k][d];
+                    hi[d] = b ? __builtin_amdgcn_alignbyte( wb[k][d + 1 + 4 / PPD], wb[k][d + 4 / PPD], b )
+                              : wb[k][d + 4 / PPD];
+                }
+                uint32_t a = 0;
+#pragma unroll
+                for( int d = 0; d < 4 / PPD; d++ )
+                    a = sadp<BD>( lo[d], 0u, a );
+                h4[s] = a;
+#pragma unroll
+                for( int d = 0; d < 4 / PPD; d++ )
+                    a = sadp<BD>( hi[d], 0u, a );
+                h8[s] = a;
+            }
+            uint32_t v8[PPD], v4[PPD];
+#pragma unroll
+            for( int s = 0; s < PPD; s++ )
+            {
+                acc8[s] += h8[s] - ring8[k][s];
+                ring8[k][s] = h8[s];
+                acc4[s] += h4[s] - ring4[k & 3][s];
+                ring4[k & 3][s] = h4[s];
+                v8[s] = acc8[s];
+                v4[s] = acc4[s];
+            }
+            auto put = [&]( uint16_t *o, const uint32_t (&v)[PPD] ) {
+                if( whole )
+                {
+                    if constexpr( PPD == 4 )
+                        *(uint2 *)o = make_uint2( (v[0] & 0xffff) | (v[1] << 16), (v[2] & 0xffff) | (v[3] << 16) );
+                    else
+                        *(uint32_t *)o = (v[0] & 0xffff) | (v[1] << 16);
+                }
+                else
+                {
+#pragma unroll
+                    for( int s = 0; s < PPD; s++ )
+                        if( c0 + s < ncol )
+                            o[s] = (uint16_t)v[s];
+                }
+            };
+            if( r - 7 >= t0 )
+                put( o8 + (intptr_t)(r - 7) * stride, v8 );
+            if( SUB8 && r - 3 >= t0 && r - 3 < t1 )
+                put( o4 + (intptr_t)(r - 3) * stride, v4 );
+        }
+    }
+}
+
 template <int BD>
 hipError_t launch_frame_integral( const typename PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride, int lines,
                                   int padh, int sub8x8, int nframes, uint16_t *integral, intptr_t ifstride,
@@ -629,6 +735,26 @@ hipError_t launch_frame_integral( const typename PT<BD>::pixel *plane, intptr_t 
     if( nframes <= 0 )
         return hipSuccess;
     const int rows = lines + 64 - 9;
+    constexpr int PPD = PT<BD>::PPD;
+    // the dword form needs dword-aligned source rows and output columns at multiples of
+    // the lane width (X264HIP_INTEGRAL_VARIANT=1: the column-per-lane kernel)
+    using pixel = typename PT<BD>::pixel;
+    const uintptr_t sb = (uintptr_t)(plane - 32 * stride - padh);
+    const uintptr_t ob = (uintptr_t)(integral - 32 * stride - padh);
+    if( variant( V_INTEGRAL ) != 1 && !((sb | (uintptr_t)(stride * sizeof( pixel )) | (uintptr_t)(fstride * sizeof( pixel ))) & 3) &&
+        !((ob | (uintptr_t)(stride * 2) | (uintptr_t)(ifstride * 2)) & (PPD * 2 - 1)) )
+    {
+        const int ndw = (int)((stride - 8 + PPD - 1) / PPD);
+        dim3 blk( 256 ), g( (unsigned)((ndw + 255) / 256), (unsigned)((rows + INTEGRAL_STRIP - 1) / INTEGRAL_STRIP),
+                            (unsigned)nframes );
+        if( sub8x8 )
+            hipLaunchKernelGGL( ( integral_dw_kernel<BD, true> ), g, blk, 0, st, plane, stride, fstride, lines, padh,
+                                integral, ifstride );
+        else
+            hipLaunchKernelGGL( ( integral_dw_kernel<BD, false> ), g, blk, 0, st, plane, stride, fstride, lines, padh,
+                                integral, ifstride );
+        return hipGetLastError();
+    }
     dim3 blk( 256 ), g( (unsigned)((stride - 8 + 255) / 256), (unsigned)((rows + INTEGRAL_STRIP - 1) / INTEGRAL_STRIP),
                         (unsigned)nframes );
     if( sub8x8 )
