@@ -6,7 +6,8 @@
   half-pel planes -- whole frames, bit-exact against the oracle (the oracle's full
   search runs a 2160p frame in ~2 s);
 * configs[4]: 10-bit 1080p full search (the v5 kernel), its ESA decision and DCT8+quant8
-  at full size, bit-exact.
+  at full size, bit-exact;
+* at both: the fused search + ESA decision and TESA (its own centred table) over whole frames.
 Size-independent properties are checked beside the exact comparison: the zero-MV column
 equals an independent batched sad_16x16, and every window minimum is at most that cost.
 Reference semantics: encoder/me.c:618-631 (ESA window), common/pixel.c:55-80 (sad),
@@ -134,6 +135,35 @@ def test_me_centred_esa_large_frame(hip, oracle, seq4k, seq1080_10, bd):
     wdec = oracle.me_esa_argmin(bd, tab, rng, me_range, par, init, cost_mv, c0, origin=org_h)
     assert np.array_equal(dec, wdec), np.argwhere((dec != wdec).any(1))[:5]
     assert (dec[::13, 0] == 0).all() and (dec[:, 0] <= init).all()
+    # the fused search + decision (no table) over the same frame and predictors
+    fs = planes[0].size
+    fused = hip.me_search_esa(dev[1:], origin, stride, dev[:1], origin, stride, mbw, mbh, 1, rng, me_range,
+                              torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda(), (cm_dev, c0),
+                              fenc_frame_stride=fs, ref_frame_stride=fs).cpu().numpy()
+    assert np.array_equal(fused, wdec), np.argwhere((fused != wdec).any(1))[:5]
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_me_tesa_large_frame(hip, oracle, seq4k, seq1080_10, bd):
+    """TESA over a whole 2160p (8 bit) / 1080p (10 bit) frame at me_range 16 with SATD: the
+    self-contained call (its own centred table) against the oracle restatement of me.c:653-748."""
+    import tesa_cases as tc
+    planes, stride, origin = seq4k if bd == 8 else seq1080_10
+    W, H = (W4K, H4K) if bd == 8 else (1920, 1088)
+    me_range = 16
+    mbw, mbh = W // 16, H // 16
+    dev = _dev(planes, bd)
+    integ = hip.frame_integral(dev[:1], origin, stride, H)
+    par, init = tc.params(mbw, mbh, me_range, seed=bd + 70, centre_spread=6)
+    cmv, c0 = tc.cost_mv()
+    got = hip.me_tesa(dev[1:], origin, stride, dev[:1], origin, stride, integ, mbw, mbh, 1, me_range,
+                      torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda(),
+                      (torch.from_numpy(cmv.view(np.int16)).cuda(), c0)).cpu().numpy()
+    f1, f0 = planes[1].ravel(), planes[0].ravel()
+    ih = oracle.frame_integral(bd, f0, origin, stride, H, tc.PAD, False).ravel()
+    want = oracle.me_tesa(bd, f1, origin, stride, f0, origin, ih, tc.PAD * stride + tc.PAD, stride, mbw, mbh,
+                          me_range, True, par, init, cmv, c0)
+    assert np.array_equal(got, want), np.argwhere((got != want).any(1))[:5]
 
 
 @pytest.mark.parametrize("transform", [4, 8])
