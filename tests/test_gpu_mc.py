@@ -22,10 +22,11 @@ def _host(t, bd):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("size", [(1920, 1088), (80, 48), (176, 144)])
-@pytest.mark.parametrize("variant", ["default", "0", "1"])
+@pytest.mark.parametrize("variant", ["default", "0", "1", "2"])
 def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
-    """X264HIP_HPEL_VARIANT: default = streaming lanes at 8 bit (2) / fused tiles at 10 bit,
-    0 = fused single pass over LDS tiles, 1 = interior tiles + border expand."""
+    """X264HIP_HPEL_VARIANT: default = streaming lanes at 8 bit with packed shift-saturate
+    stores (3) / fused tiles at 10 bit, 0 = fused single pass over LDS tiles, 1 = interior
+    tiles + border expand, 2 = streaming lanes with scaled clamps (med3 + byte picks)."""
     if variant == "default":
         _x().set_variant("X264HIP_HPEL_VARIANT", None)
     else:
@@ -36,6 +37,27 @@ def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
     planes, stride, origin = gen(2, W, H, bd)
     dev = _dev(planes, bd)
     outs = hip.hpel_filter(dev, origin, stride, W, H)
+    for f in range(2):
+        want = oracle.frame_filter(bd, planes[f].ravel().copy(), origin, stride, W, H)
+        for o, w, name in zip(outs, want, "hvc"):
+            got = _host(o, bd)[f][:, :W + 64]
+            w2 = w.reshape(planes[f].shape)[:, :W + 64]
+            assert np.array_equal(got, w2), (f, name, np.argwhere(got != w2)[:4])
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("variant", ["default", "2"])
+def test_hpel_filter_extremes(hip, oracle, bd, variant):
+    """Pixels 0 / PIXEL_MAX only, so the 6-tap sums reach both ends of every clip
+    (H and V: -10 * max .. 42 * max before the shift; centre far beyond int16)."""
+    _x().set_variant("X264HIP_HPEL_VARIANT", None if variant == "default" else variant)
+    from x264hip import synth
+    W, H = 176, 144
+    planes, stride, origin = synth.random_planes(2, W, H, bd, seed=5)
+    planes[:] = np.where(planes & 1, (1 << bd) - 1, 0).astype(planes.dtype)
+    planes[1, ::3] = 0                       # runs of equal rows / columns too
+    planes[1, :, 1::4] = (1 << bd) - 1
+    outs = hip.hpel_filter(_dev(planes, bd), origin, stride, W, H)
     for f in range(2):
         want = oracle.frame_filter(bd, planes[f].ravel().copy(), origin, stride, W, H)
         for o, w, name in zip(outs, want, "hvc"):

@@ -30,7 +30,9 @@ __all__ = [
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libx264hip.so")
+# X264HIP_LIBRARY: an alternative in-tree build of the same library (A/B timing of two
+# builds of one kernel, tools/gpu_ab.sh); the default is the package's own build
+LIB_PATH = os.environ.get("X264HIP_LIBRARY") or os.path.join(_HERE, "libx264hip.so")
 
 # reference common/pixel.h:37-59
 PIXEL_16x16, PIXEL_16x8, PIXEL_8x16, PIXEL_8x8, PIXEL_8x4, PIXEL_4x8, PIXEL_4x4, PIXEL_4x16 = range(8)

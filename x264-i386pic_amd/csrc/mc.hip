@@ -299,6 +299,67 @@ __device__ __forceinline__ void tap6_h4( const hs2 (&P)[N], int bias, int (&o)[4
     o[3] = __builtin_amdgcn_sdot2( P[J + 4], (hs2){ A, 0 }, o[3], false );
 }
 
+// The same four outputs unscaled, the first tap of each chain taking its
+// coefficient pair from a VGPR (k15 = (1, -5), k01 = (0, 1)): that dot2 is then the
+// three-operand form with the SGPR bias as its accumulator, where a literal
+// coefficient forces the two-operand form and a v_mov of the bias into each
+// chain's destination (32 per output row).
+// (the compiler turns even the three-operand builtin into v_mov + v_dot2c, so the
+// first tap is written out)
+template <int BIAS> __device__ __forceinline__ int dot2_first( hs2 p, hs2 k )
+{
+    int d;
+    if constexpr( BIAS <= 64 )
+        asm( "v_dot2_i32_i16 %0, %1, %2, %3" : "=v"( d ) : "v"( as_u( p ) ), "v"( as_u( k ) ), "i"( BIAS ) );
+    else
+        asm( "v_dot2_i32_i16 %0, %1, %2, %3" : "=v"( d ) : "v"( as_u( p ) ), "v"( as_u( k ) ), "s"( BIAS ) );
+    return d;
+}
+
+template <int J, int BIAS, int N>
+__device__ __forceinline__ void tap6_h4v( const hs2 (&P)[N], hs2 k15, hs2 k01, int (&o)[4] )
+{
+    o[0] = dot2_first<BIAS>( P[J], k15 );
+    o[0] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ 20, 20 }, o[0], false );
+    o[0] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ -5, 1 }, o[0], false );
+    o[1] = dot2_first<BIAS>( P[J], k01 );
+    o[1] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ -5, 20 }, o[1], false );
+    o[1] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ 20, -5 }, o[1], false );
+    o[1] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ 1, 0 }, o[1], false );
+    o[2] = dot2_first<BIAS>( P[J + 1], k15 );
+    o[2] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ 20, 20 }, o[2], false );
+    o[2] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ -5, 1 }, o[2], false );
+    o[3] = dot2_first<BIAS>( P[J + 1], k01 );
+    o[3] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ -5, 20 }, o[3], false );
+    o[3] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ 20, -5 }, o[3], false );
+    o[3] = __builtin_amdgcn_sdot2( P[J + 4], (hs2){ 1, 0 }, o[3], false );
+}
+
+// bytes 0-1 = clip( lo >> S ), clip( hi >> S ) by gfx950's v_ashr_pk_u8_i32 (signed
+// shift, unsigned byte saturation).  Bytes 2-3 of its result are not cleared
+// (see shr_clip), so callers take only the low half.
+template <int S> __device__ __forceinline__ uint32_t ashr_pk_u8( int lo, int hi )
+{
+    uint32_t d;
+    asm( "v_ashr_pk_u8_i32 %0, %1, %2, %3" : "=v"( d ) : "v"( lo ), "v"( hi ), "i"( S ) );
+    return d;
+}
+
+// four filter sums (bias included) as four pixels: two packed shifts, one perm
+template <int S> __device__ __forceinline__ uint32_t pack_shr4( const int (&o)[4] )
+{
+    return __builtin_amdgcn_perm( ashr_pk_u8<S>( o[2], o[3] ), ashr_pk_u8<S>( o[0], o[1] ), 0x05040100u );
+}
+
+// two int16 pairs as four pixels clip( v >> 5 ): packed shifts, gfx950's
+// v_sat_pk_u8_i16 (low half only, as above), one perm
+__device__ __forceinline__ uint32_t sat_pk_u8( hs2 v )
+{
+    uint32_t d;
+    asm( "v_sat_pk_u8_i16 %0, %1" : "=v"( d ) : "v"( as_u( v ) ) );
+    return d;
+}
+
 // four scaled filter sums clamped to [0, HI] whose byte BY is the pixel, packed
 // into the bytes of a dword with two v_perm (+ one merge)
 template <int HI, int BY> __device__ __forceinline__ uint32_t pack_clip4( const int (&o)[4] )
@@ -313,7 +374,7 @@ template <int HI, int BY> __device__ __forceinline__ uint32_t pack_clip4( const 
     return __builtin_amdgcn_perm( b[1], b[0], lo ) | __builtin_amdgcn_perm( b[3], b[2], hi );
 }
 
-template <int HS_ROWS>
+template <int HS_ROWS, bool PK>
 __global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
                                                              uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
                                                              intptr_t stride, intptr_t fstride, int width,
@@ -352,6 +413,11 @@ __global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__res
         P[9] = as_s2( __builtin_amdgcn_perm( 0u, dr, 0x0c010c00u ) );
         P[10] = as_s2( __builtin_amdgcn_perm( 0u, dr, 0x0c030c02u ) );
     };
+    // opaque VGPR coefficient pairs (1, -5) / (0, 1) for tap6_h4v's first taps
+    uint32_t k15u, k01u;
+    asm( "v_mov_b32 %0, 0xfffb0001" : "=v"( k15u ) );
+    asm( "v_mov_b32 %0, 0x10000" : "=v"( k01u ) );
+    const hs2 k15 = as_s2( k15u ), k01 = as_s2( k01u );
     hs2 win[6][11];                                          // source rows as even pairs, ring of 6
     uint4 raw[6];                                            // next block's source rows, in flight
 #pragma unroll
@@ -387,26 +453,47 @@ __global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__res
                 hrow[p] = c;
             }
             uint32_t oh[4], ov[4], oc[4];
-#pragma unroll
-            for( int j = 0; j < 4; j++ )
-            {
-                // V: clip( (v + 16) >> 5 ), clamp before the shift
-                hs2 va = vi[1 + 2 * j] + (hs2)16, vb = vi[2 + 2 * j] + (hs2)16;
-                va = __builtin_elementwise_min( __builtin_elementwise_max( va, (hs2)0 ), (hs2)8191 );
-                vb = __builtin_elementwise_min( __builtin_elementwise_max( vb, (hs2)0 ), (hs2)8191 );
-                ov[j] = __builtin_amdgcn_perm( as_u( vb >> (hs2)5 ), as_u( va >> (hs2)5 ), 0x06040200u );
-            }
-            // H: clip( (t + 16) >> 5 ) computed as clamp( 8t + 128, 0, 0xffff ), byte 1;
-            // centre: clip( (t + 512) >> 10 ) as clamp( 64t + 32768, 0, 0xffffff ), byte 2
             int o[4];
-            tap6_h4<0, 8>( hrow, hbias, o ); oh[0] = pack_clip4<0xffff, 1>( o );
-            tap6_h4<2, 8>( hrow, hbias, o ); oh[1] = pack_clip4<0xffff, 1>( o );
-            tap6_h4<4, 8>( hrow, hbias, o ); oh[2] = pack_clip4<0xffff, 1>( o );
-            tap6_h4<6, 8>( hrow, hbias, o ); oh[3] = pack_clip4<0xffff, 1>( o );
-            tap6_h4<0, 64>( vi, cbias, o ); oc[0] = pack_clip4<0xffffff, 2>( o );
-            tap6_h4<2, 64>( vi, cbias, o ); oc[1] = pack_clip4<0xffffff, 2>( o );
-            tap6_h4<4, 64>( vi, cbias, o ); oc[2] = pack_clip4<0xffffff, 2>( o );
-            tap6_h4<6, 64>( vi, cbias, o ); oc[3] = pack_clip4<0xffffff, 2>( o );
+            if constexpr( PK )
+            {
+                // V: clip( (v + 16) >> 5 ) by packed arithmetic shift + byte saturation;
+                // H: clip( (t + 16) >> 5 ), centre: clip( (t + 512) >> 10 ) with the
+                // bias in the accumulator and v_ashr_pk_u8_i32 doing shift and clip
+#pragma unroll
+                for( int j = 0; j < 4; j++ )
+                    ov[j] = __builtin_amdgcn_perm( sat_pk_u8( (vi[2 + 2 * j] + (hs2)16) >> (hs2)5 ),
+                                                   sat_pk_u8( (vi[1 + 2 * j] + (hs2)16) >> (hs2)5 ), 0x05040100u );
+                tap6_h4v<0, 16>( hrow, k15, k01, o ); oh[0] = pack_shr4<5>( o );
+                tap6_h4v<2, 16>( hrow, k15, k01, o ); oh[1] = pack_shr4<5>( o );
+                tap6_h4v<4, 16>( hrow, k15, k01, o ); oh[2] = pack_shr4<5>( o );
+                tap6_h4v<6, 16>( hrow, k15, k01, o ); oh[3] = pack_shr4<5>( o );
+                tap6_h4v<0, 512>( vi, k15, k01, o ); oc[0] = pack_shr4<10>( o );
+                tap6_h4v<2, 512>( vi, k15, k01, o ); oc[1] = pack_shr4<10>( o );
+                tap6_h4v<4, 512>( vi, k15, k01, o ); oc[2] = pack_shr4<10>( o );
+                tap6_h4v<6, 512>( vi, k15, k01, o ); oc[3] = pack_shr4<10>( o );
+            }
+            else
+            {
+#pragma unroll
+                for( int j = 0; j < 4; j++ )
+                {
+                    // V: clip( (v + 16) >> 5 ), clamp before the shift
+                    hs2 va = vi[1 + 2 * j] + (hs2)16, vb = vi[2 + 2 * j] + (hs2)16;
+                    va = __builtin_elementwise_min( __builtin_elementwise_max( va, (hs2)0 ), (hs2)8191 );
+                    vb = __builtin_elementwise_min( __builtin_elementwise_max( vb, (hs2)0 ), (hs2)8191 );
+                    ov[j] = __builtin_amdgcn_perm( as_u( vb >> (hs2)5 ), as_u( va >> (hs2)5 ), 0x06040200u );
+                }
+                // H: clip( (t + 16) >> 5 ) computed as clamp( 8t + 128, 0, 0xffff ), byte 1;
+                // centre: clip( (t + 512) >> 10 ) as clamp( 64t + 32768, 0, 0xffffff ), byte 2
+                tap6_h4<0, 8>( hrow, hbias, o ); oh[0] = pack_clip4<0xffff, 1>( o );
+                tap6_h4<2, 8>( hrow, hbias, o ); oh[1] = pack_clip4<0xffff, 1>( o );
+                tap6_h4<4, 8>( hrow, hbias, o ); oh[2] = pack_clip4<0xffff, 1>( o );
+                tap6_h4<6, 8>( hrow, hbias, o ); oh[3] = pack_clip4<0xffff, 1>( o );
+                tap6_h4<0, 64>( vi, cbias, o ); oc[0] = pack_clip4<0xffffff, 2>( o );
+                tap6_h4<2, 64>( vi, cbias, o ); oc[1] = pack_clip4<0xffffff, 2>( o );
+                tap6_h4<4, 64>( vi, cbias, o ); oc[2] = pack_clip4<0xffffff, 2>( o );
+                tap6_h4<6, 64>( vi, cbias, o ); oc[3] = pack_clip4<0xffffff, 2>( o );
+            }
             if( st )
             {
                 intptr_t ox = 0;                             // extra piece: x in [-32, -16) / [W+16, W+32)
@@ -460,11 +547,11 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
     if( nframes <= 0 || width <= 0 || height <= 0 )
         return hipSuccess;
     const int ev = variant( V_HPEL );
-    const int var = ev >= 0 ? ev : BD == 8 ? 2 : 0;
+    const int var = ev >= 0 ? ev : BD == 8 ? 3 : 0;
     if constexpr( BD == 8 )
     {
         // streaming kernel: needs 16-byte aligned rows (pixel (0,0) and the strides)
-        if( var == 2 && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
+        if( (var == 2 || var == 3) && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
                            (uintptr_t)fstride) & 15) )
         {
             const int nq = (width + 32) / 16, nchunk = (nq + 61) / 62;
@@ -478,13 +565,17 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
             const int rows = er == 6 || er == 8 || er == 16 || er == 24 ? er : 12;
             dim3 g( nchunk, (height + 16 + rows - 1) / rows + 4, nframes );
 #define HS_GO( ROWS )                                                                                              \
-    hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride,  \
-                        width, height, 8 * 16, 64 * 512 )
-            if( rows == 24 ) HS_GO( 24 );
-            else if( rows == 16 ) HS_GO( 16 );
-            else if( rows == 8 ) HS_GO( 8 );
-            else if( rows == 6 ) HS_GO( 6 );
-            else HS_GO( 12 );
+    if( var == 3 )                                                                                                 \
+        hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, \
+                            fstride, width, height, 8 * 16, 64 * 512 );                                            \
+    else                                                                                                           \
+        hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,        \
+                            stride, fstride, width, height, 8 * 16, 64 * 512 )
+            if( rows == 24 ) { HS_GO( 24 ); }
+            else if( rows == 16 ) { HS_GO( 16 ); }
+            else if( rows == 8 ) { HS_GO( 8 ); }
+            else if( rows == 6 ) { HS_GO( 6 ); }
+            else { HS_GO( 12 ); }
 #undef HS_GO
             return hipGetLastError();
         }

@@ -438,16 +438,16 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t 
 {
     constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
     constexpr int P = 4 * G;                    // table row pitch
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)nframes * mbh * mbw * G;
-    if( slot >= total )
+    // 32-bit index decomposition (the launcher keeps the lane count below 2^32): the
+    // int64 divisions by mbw / mbh were ~150 VALU instructions of the prologue
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if( slot >= (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw * (uint32_t)G )
         return;
-    const int grp = (int)(slot % G);
-    const int64_t mb = slot / G;
-    const int mbx = (int)(mb % mbw);
-    const int64_t t = mb / mbw;
-    const int mby = (int)(t % mbh);
-    const int64_t f = t / mbh;
+    const uint32_t mb32 = slot / G, t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+    const int grp = (int)(slot - mb32 * G);
+    const int mbx = (int)(mb32 - t32 * (uint32_t)mbw);
+    const int mby = (int)(t32 - f32 * (uint32_t)mbh);
+    const int64_t mb = mb32, f = f32;
 
     uint32_t F[16][4];
     const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
@@ -734,8 +734,8 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     if( (((uintptr_t)fenc | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
           (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant >= 3 ? (uintptr_t)ref : 0)) & 3) )
         variant = 1;
-    if( variant == 7 && BD != 8 )
-        variant = 1;
+    if( variant == 7 && (BD != 8 || (int64_t)nframes * mbh * mbw * ((2 * range + 1 + 3) / 4) >= (1ll << 32)) )
+        variant = 1;                              // (v7 indexes its lanes in 32 bits)
     const int64_t groups = variant == 7   ? (2 * range + 1 + 3) / 4
                            : variant == 3 ? 2 * ((2 * range + 1 + 3) / 4)
                            : variant == 5 ? 2 * ((2 * range + 2) / 2)
@@ -882,16 +882,16 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
 {
     constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
     constexpr int W = 2 * R + 1;
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)nframes * mbh * mbw * G;
-    if( slot >= total )
+    // 32-bit index decomposition (the launcher keeps the lane count below 2^32): the
+    // int64 divisions by mbw / mbh were ~150 VALU instructions of the prologue
+    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    if( slot >= (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw * (uint32_t)G )
         return;
-    const int grp = (int)(slot % G);
-    const int64_t mb = slot / G;
-    const int mbx = (int)(mb % mbw);
-    const int64_t t = mb / mbw;
-    const int mby = (int)(t % mbh);
-    const int64_t f = t / mbh;
+    const uint32_t mb32 = slot / G, t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+    const int grp = (int)(slot - mb32 * G);
+    const int mbx = (int)(mb32 - t32 * (uint32_t)mbw);
+    const int mby = (int)(t32 - f32 * (uint32_t)mbh);
+    const int64_t mb = mb32, f = f32;
 
     uint32_t F[16][4];
     const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
@@ -1068,7 +1068,7 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
     if( e != hipSuccess )
         return e;
     // 8 bit: variant 7's lanes (one per column group), X264HIP_ME_VARIANT=3 the lane pairs
-    const bool v7 = BD == 8 && me_variant() != 3;
+    const bool v7 = BD == 8 && me_variant() != 3 && nmb * ((2 * range + 1 + 3) / 4) < (1ll << 32);
     const int64_t groups = BD == 8 ? (2 * range + 1 + 3) / 4 : (2 * range + 2) / 2;
     const int64_t lanes = nmb * (v7 ? 1 : 2) * groups;
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
