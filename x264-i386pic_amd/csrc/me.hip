@@ -870,7 +870,11 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v3_kernel( const uint8_t *_
 
 // The fused decision on variant 7's lanes (all 16 fenc rows, four columns per lane): a lane
 // keys its own four columns per finished candidate row, and each of an MB's 9 lanes meets
-// the others through one atomicMin.
+// the others through one atomicMin.  A workgroup holds whole MBs (256 / G of them), whose
+// lanes first stage the MB's per-row key terms in LDS (ycost, row part of the raster
+// index, row validity), so a candidate row costs one LDS read instead of a clamped
+// global load and its index arithmetic.
+template <int R> constexpr int esa7_mbs() { return 256 / ((2 * R + 1 + 3) / 4); }
 template <int R, int L>
 __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                 intptr_t ffs, const uint8_t *__restrict__ ref,
@@ -882,16 +886,22 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
 {
     constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
     constexpr int W = 2 * R + 1;
-    // 32-bit index decomposition (the launcher keeps the lane count below 2^32): the
-    // int64 divisions by mbw / mbh were ~150 VALU instructions of the prologue
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
-    if( slot >= (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw * (uint32_t)G )
-        return;
-    const uint32_t mb32 = slot / G, t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
-    const int grp = (int)(slot - mb32 * G);
+    constexpr int MPW = esa7_mbs<R>();          // whole MBs per workgroup
+    constexpr int SP = W | 1;                   // LDS row-term pitch (odd: spread banks)
+    __shared__ uint32_t s_row[MPW * SP];
+    // lanes past the last MB (and the workgroup's G * MPW .. 255 tail) work on a clamped MB
+    // and publish nothing; every lane reaches the barrier
+    const uint32_t nmb = (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw;
+    const int tid = (int)threadIdx.x;
+    const int lmb = min( tid / G, MPW - 1 );
+    const int grp = tid - lmb * G;              // >= G only in the tail lanes
+    const uint32_t mbr = blockIdx.x * MPW + lmb;
+    const bool live = tid < MPW * G && mbr < nmb;
+    const uint32_t mb32 = min( mbr, nmb - 1 ), t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
     const int mbx = (int)(mb32 - t32 * (uint32_t)mbw);
     const int mby = (int)(t32 - f32 * (uint32_t)mbh);
     const int64_t mb = mb32, f = f32;
+    const int cgrp = min( grp, G - 1 );          // the tail lanes' loads stay inside the MB
 
     uint32_t F[16][4];
     const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
@@ -911,39 +921,59 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
     const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };   // the window centre: the predictor
     me_window<8, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
     const uint32_t *rbase =
-        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox + 4 * grp);
-    int ccost[4];
-    uint32_t cinv[4];                            // 0 for a column inside the window, else all ones
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox + 4 * cgrp);
+    // key = (sad + xcost + ycost) << 12 | raster, raster = (my - min_y) * width + mx - min_x
+    // < 4096, built as sat( ((sad << 12) + C[k]) + S ): C[k] = xcost << 12 | column part,
+    // or 0xF0000000 outside the window (valid keys stay below 196350 << 12 + 4096 <
+    // 0xF0000000, and 0xF0000000 + (65280 << 12) does not wrap); S = ycost << 12 | row
+    // part, or all ones outside the window (the add saturates).  Per candidate row: one
+    // extract + one shift-add + one saturating add per column and two min3.
+    uint32_t ck[4];
 #pragma unroll
     for( int k = 0; k < 4; k++ )
     {
-        const int col = 4 * grp + k, mx = ox + col;
+        const int col = 4 * cgrp + k, mx = ox + col;
         const bool in = col < W && mx >= min_x && mx < min_x + width;
-        cinv[k] = in ? 0u : 0xFFFFFFFFu;
-        ccost[k] = in ? (int)cx[mx * 4] : 0;
+        ck[k] = in ? ((uint32_t)cx[mx * 4] << 12) + (uint32_t)(mx - min_x) : 0xF0000000u;
     }
     uint32_t key = 0xFFFFFFFFu;
-    const int ibase = ox + 4 * grp - min_x - min_y * width;
-    // the row cost of candidate row c + 1 is loaded while row c is folded
-    uint32_t ynext = cy[4 * min( max( oy, min_y ), max_y )];
+    // row terms S[c] = ycost << 12 | (my - min_y) * width for candidate row c (my = oy + c)
+    // inside [min_y, max_y], all ones outside; the MB's lanes stage them together
+    uint32_t *srow = s_row + lmb * SP;
+    if( live )
+    {
+#pragma unroll
+        for( int c0 = 0; c0 < W; c0 += G )
+        {
+            const int c = c0 + grp, my = oy + c;
+            if( c < W )
+                srow[c] = my >= min_y && my <= max_y
+                              ? ((uint32_t)cy[4 * my] << 12) + (uint32_t)((my - min_y) * width)
+                              : 0xFFFFFFFFu;
+        }
+    }
+    __syncthreads();
     auto reduce = [&]( int c, uint32_t lo, uint32_t hi ) {
-        const int my = oy + c;
-        const uint32_t rinv = my >= min_y && my <= max_y ? 0u : 0xFFFFFFFFu;
-        const uint32_t ycost = ynext;
-        int yi = 4 * min( max( my + 1, min_y ), max_y );
-        asm volatile( "" : "+v"( yi ) );         // issued here, not hoisted to the top
-        ynext = cy[yi];
-        const uint32_t ri = (uint32_t)(my * width + ibase);
-        const uint32_t k0 = (((lo & 0xffff) + (uint32_t)ccost[0] + ycost) << 12) | ri;
-        const uint32_t k1 = (((lo >> 16) + (uint32_t)ccost[1] + ycost) << 12) | (ri + 1);
-        const uint32_t k2 = (((hi & 0xffff) + (uint32_t)ccost[2] + ycost) << 12) | (ri + 2);
-        const uint32_t k3 = (((hi >> 16) + (uint32_t)ccost[3] + ycost) << 12) | (ri + 3);
-        key = min( key, min( min( k0 | cinv[0], k1 | cinv[1] ), min( k2 | cinv[2], k3 | cinv[3] ) ) | rinv );
+        // read where the row finishes, not hoisted (an LDS-typed pointer, so the pinned
+        // address stays a ds_read)
+        __attribute__( ( address_space( 3 ) ) ) uint32_t *q = (__attribute__( ( address_space( 3 ) ) ) uint32_t *)srow;
+        asm volatile( "" : "+v"( q ) );
+        const uint32_t S = q[c];
+        // the fields as plain values (else the extract is folded into shift + mask and the
+        // shift-add is lost): extract, v_lshl_add, saturating add
+        uint32_t w0 = lo & 0xffff, w1 = lo >> 16, w2 = hi & 0xffff, w3 = hi >> 16;
+        asm( "" : "+v"( w0 ), "+v"( w1 ), "+v"( w2 ), "+v"( w3 ) );
+        const uint32_t k0 = __builtin_elementwise_add_sat( (w0 << 12) + ck[0], S );
+        const uint32_t k1 = __builtin_elementwise_add_sat( (w1 << 12) + ck[1], S );
+        const uint32_t k2 = __builtin_elementwise_add_sat( (w2 << 12) + ck[2], S );
+        const uint32_t k3 = __builtin_elementwise_add_sat( (w3 << 12) + ck[3], S );
+        key = min( min( key, k0 ), k1 );
+        key = min( min( key, k2 ), k3 );
         asm volatile( "" : "+v"( key ) );        // fold each row where its sums finish
     };
     uint64_t acc[16];
     me_rows7<R, L>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
-    if( key != 0xFFFFFFFFu )
+    if( live && key < 0xF0000000u )
         atomicMin( keys + 3 * mb, key );
 }
 
@@ -1068,10 +1098,12 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
     if( e != hipSuccess )
         return e;
     // 8 bit: variant 7's lanes (one per column group), X264HIP_ME_VARIANT=3 the lane pairs
-    const bool v7 = BD == 8 && me_variant() != 3 && nmb * ((2 * range + 1 + 3) / 4) < (1ll << 32);
+    const bool v7 = BD == 8 && me_variant() != 3;
     const int64_t groups = BD == 8 ? (2 * range + 1 + 3) / 4 : (2 * range + 2) / 2;
     const int64_t lanes = nmb * (v7 ? 1 : 2) * groups;
-    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+    // v7: whole MBs per workgroup (esa7_mbs), the others a flat lane index
+    const int64_t mpw = 256 / ((2 * range + 1 + 3) / 4);
+    dim3 blk( 256 ), g( (unsigned)(v7 ? (nmb + mpw - 1) / mpw : (lanes + 255) / 256) );
     const int lead = me_lead();
     switch( range )
     {
