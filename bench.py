@@ -624,28 +624,38 @@ def rates_2160p(x, a, world):
     copy = torch.cuda.Stream()
     done = [torch.cuda.Event() for _ in range(3)]
     ready = [torch.cuda.Event() for _ in range(3)]
-    ring[0].copy_(host[0])
-    ready[0].record()
-    state = {"n": 0}
+    state = {"n": 0, "how": "sdma"}
 
     def streaming():
         n = state["n"]
         cur, ref = (n + 1) % 3, n % 3
         with torch.cuda.stream(copy):                 # upload frame n+1 while frame n-1's kernels may still run
             copy.wait_event(done[cur])
-            ring[cur].copy_(host[(n + 1) % (nf + 1)], non_blocking=True)
+            if state["how"] == "sdma":                # the runtime's copy engine
+                ring[cur].copy_(host[(n + 1) % (nf + 1)], non_blocking=True)
+            else:                                     # x264hip_upload: a kernel reading the pinned pages
+                x.upload(ring[cur], host[(n + 1) % (nf + 1)])
             ready[cur].record(copy)
         torch.cuda.current_stream().wait_event(ready[cur])
         torch.cuda.current_stream().wait_event(ready[ref])
         work(ring[cur:cur + 1], ring[ref:ref + 1], c_fs=0, r_fs=0)
         done[ref].record()
         state["n"] = n + 1
-    for ev in done:
-        ev.record()
-    wall, _ = timed(streaming, a.steps, min(a.warmup, 50), world)
-    torch.cuda.synchronize()
-    res["2160p_pcie_inclusive_candidates_per_s"] = world * a.steps * cand / wall
-    res["2160p_pcie_inclusive_frame_ms"] = wall / a.steps * 1e3
+    for how in ("sdma", "kernel"):
+        torch.cuda.synchronize()
+        state.update(n=0, how=how)
+        ring[0].copy_(host[0])
+        ready[0].record()
+        for ev in done:
+            ev.record()
+        wall, _ = timed(streaming, a.steps, min(a.warmup, 50), world)
+        torch.cuda.synchronize()
+        res[f"2160p_pcie_{how}_candidates_per_s"] = world * a.steps * cand / wall
+        res[f"2160p_pcie_{how}_frame_ms"] = wall / a.steps * 1e3
+    best = max(("sdma", "kernel"), key=lambda h: res[f"2160p_pcie_{h}_candidates_per_s"])
+    res["2160p_pcie_inclusive_candidates_per_s"] = res[f"2160p_pcie_{best}_candidates_per_s"]
+    res["2160p_pcie_inclusive_frame_ms"] = res[f"2160p_pcie_{best}_frame_ms"]
+    res["2160p_pcie_inclusive_upload"] = best
     res["2160p_upload_bytes_per_frame"] = int(fsz)
     del dev_all, ring, table, host
     return res

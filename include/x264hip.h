@@ -336,6 +336,12 @@ int  x264hip_thread_device( void );
  * frame-per-GPU pipeline's only device-to-device transfer). */
 int  x264hip_forward_ref( void *dst, int dst_device, const void *src, int src_device, size_t bytes,
                           void *stream );
+/* Upload `bytes` of frame planes from page-locked host memory (hipHostMalloc /
+ * hipHostRegister) to device memory: a kernel on `stream` reads the pinned pages
+ * over PCIe (16-byte pieces when both pointers are 16-byte aligned), the streaming
+ * form of configs[3] (H2D per frame overlapped with compute).
+ * Asynchronous; the host buffer must stay untouched until `stream` passes it. */
+int  x264hip_upload( void *dst, const void *host_src, size_t bytes, void *stream );
 /* one line naming the device and the table entries the HIP backend fills (the
  * analogue of reference encoder/encoder.c:1676-1706); also printed once to
  * stderr at the first table fill unless X264HIP_QUIET=1 */

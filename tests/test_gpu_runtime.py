@@ -6,6 +6,7 @@ multi-device readiness"):
   threads (x264's frame / lookahead threads, reference encoder/encoder.c:1758-1772);
 * x264hip_forward_ref: the reconstructed-reference peer copy of the frame-per-GPU pipeline
   (on one GPU it is exercised as a same-device copy);
+* x264hip_upload: frame planes from pinned host memory by a PCIe-read kernel;
 * the backend banner (reference encoder/encoder.c:1676-1706 analogue) names the device.
 """
 import ctypes
@@ -57,6 +58,22 @@ def test_forward_ref_peer_copy(hip):
     assert torch.equal(src, dst)
     with pytest.raises(ValueError):
         hip.forward_ref(dst[:10], 0, src, 0)
+
+
+@pytest.mark.parametrize("nbytes,off", [(8682496, 0), (8682496 + 7, 0), (1 << 20, 3), (5, 0), (17, 1), (0, 0)])
+def test_upload_from_pinned(hip, nbytes, off):
+    """x264hip_upload: the PCIe-read kernel copies page-locked host bytes exactly, in
+    16-byte pieces (aligned, ragged tail) or bytewise (misaligned start)."""
+    rng = np.random.default_rng(nbytes + off)
+    host = torch.from_numpy(rng.integers(0, 256, nbytes + off + 16, dtype=np.uint8)).pin_memory()
+    dev = torch.zeros(nbytes + off + 16, dtype=torch.uint8, device="cuda")
+    hip.upload(dev[off:off + nbytes], host[off:off + nbytes])
+    torch.cuda.synchronize()
+    got = dev.cpu()
+    assert torch.equal(got[off:off + nbytes], host[off:off + nbytes])
+    assert not got[:off].any() and not got[off + nbytes:].any()   # nothing written outside
+    with pytest.raises(ValueError):
+        hip.upload(dev[:4], host[:5])
 
 
 def test_backend_banner(hip):

@@ -26,7 +26,7 @@ __all__ = [
     "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
-    "backend_banner", "forward_ref",
+    "backend_banner", "forward_ref", "upload",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -119,6 +119,16 @@ def forward_ref(dst, dst_device, src, src_device):
     with torch.cuda.device(src.device):
         _rc(lib().x264hip_forward_ref(_c.c_void_p(dst.data_ptr()), dst_device, _c.c_void_p(src.data_ptr()),
                                       src_device, nbytes, _stream()), "forward_ref")
+    return dst
+
+
+def upload(dst, src):
+    """Copy a pinned host tensor into a device tensor of the same size with the
+    library's PCIe-read kernel (x264hip_upload) on the current stream."""
+    nbytes = src.numel() * src.element_size()
+    if dst.numel() * dst.element_size() != nbytes or not src.is_pinned() or not dst.is_cuda:
+        raise ValueError("upload: needs a pinned host source and a device destination of equal size")
+    _rc(lib().x264hip_upload(_c.c_void_p(dst.data_ptr()), _c.c_void_p(src.data_ptr()), nbytes, _stream()), "upload")
     return dst
 
 
@@ -274,6 +284,8 @@ def _declare(L):
     L.x264hip_thread_device.restype = _c.c_int
     L.x264hip_forward_ref.argtypes = [_P, _c.c_int, _P, _c.c_int, _c.c_size_t, _P]
     L.x264hip_forward_ref.restype = _c.c_int
+    L.x264hip_upload.argtypes = [_P, _P, _c.c_size_t, _P]
+    L.x264hip_upload.restype = _c.c_int
     L.x264hip_backend_banner.restype = _c.c_char_p
     L.x264hip_set_variant.argtypes = [_c.c_char_p, _c.c_int]
     L.x264hip_set_variant.restype = _c.c_int

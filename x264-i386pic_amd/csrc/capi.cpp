@@ -123,6 +123,18 @@ extern "C" int x264hip_forward_ref( void *dst, int dst_device, const void *src, 
     return e == hipSuccess ? X264HIP_OK : set_err( e, "hipMemcpyPeerAsync" );
 }
 
+// frame upload from page-locked host memory by a kernel reading the pinned pages
+// (configs[3]'s streaming form; asynchronous on `stream`)
+extern "C" int x264hip_upload( void *dst, const void *host_src, size_t bytes, void *stream )
+{
+    if( bytes == 0 )
+        return X264HIP_OK;
+    if( !dst || !host_src )
+        return X264HIP_EINVAL;
+    hipError_t e = launch_upload( dst, host_src, bytes, (hipStream_t)stream );
+    return e == hipSuccess ? X264HIP_OK : set_err( e, "upload" );
+}
+
 [[noreturn]] static void fatal( hipError_t e, const char *where )
 {
     fprintf( stderr, "x264hip: fatal HIP error in %s: %s\n", where, hipGetErrorString( e ) );

@@ -203,6 +203,7 @@ int variant( VariantSlot slot );
 
 // ---- launchers implemented in the .hip files (all enqueue on `stream`) ----
 namespace x264hip {
+hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t stream );
 template <int BD>
 hipError_t launch_cmp_batch( int op, int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs,
                              const typename PT<BD>::pixel *ref, intptr_t rs, const int64_t *fenc_off,

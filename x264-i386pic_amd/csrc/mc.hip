@@ -1561,3 +1561,54 @@ INST( 8 )
 INST( 10 )
 
 } // namespace x264hip
+
+namespace x264hip {
+
+// ---------------------------------------------------------------------------
+// Frame upload from page-locked host memory (configs[3]'s streaming form): the
+// GPU reads the pinned pages itself over PCIe, 16-byte pieces with four loads in
+// flight per lane, instead of one SDMA engine copy.  Ragged head / tail bytes go
+// one per lane.
+__global__ __launch_bounds__( 256 ) void upload_kernel( uint8_t *__restrict__ dst, const uint8_t *__restrict__ src,
+                                                        size_t n16, size_t bytes )
+{
+    const size_t nthr = (size_t)gridDim.x * blockDim.x;
+    size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint4 *s = (const uint4 *)src;
+    uint4 *d = (uint4 *)dst;
+    for( ; i + 3 * nthr < n16; i += 4 * nthr )
+    {
+        const uint4 a = s[i], b = s[i + nthr], c = s[i + 2 * nthr], e = s[i + 3 * nthr];
+        d[i] = a;
+        d[i + nthr] = b;
+        d[i + 2 * nthr] = c;
+        d[i + 3 * nthr] = e;
+    }
+    for( ; i < n16; i += nthr )
+        d[i] = s[i];
+    const size_t t = 16 * n16 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if( t < bytes )
+        dst[t] = src[t];
+}
+
+hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t stream )
+{
+    if( !bytes )
+        return hipSuccess;
+    // 16-byte pieces need both ends 16-byte aligned; otherwise the byte path only
+    const bool al = !(((uintptr_t)dst | (uintptr_t)src) & 15);
+    const size_t n16 = al ? bytes / 16 : 0;
+    // 2048 workgroups: enough reads in flight to cover the PCIe round trip
+    const unsigned g = (unsigned)std::min<size_t>( 2048, std::max<size_t>( 1, (n16 + 1023) / 1024 ) );
+    if( !al && bytes > (size_t)g * 256 )
+    {
+        hipLaunchKernelGGL( upload_kernel, dim3( (unsigned)((bytes + 255) / 256) ), dim3( 256 ), 0, stream,
+                            (uint8_t *)dst, (const uint8_t *)src, (size_t)0, bytes );
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL( upload_kernel, dim3( g ), dim3( 256 ), 0, stream, (uint8_t *)dst, (const uint8_t *)src, n16,
+                        bytes );
+    return hipGetLastError();
+}
+
+} // namespace x264hip
