@@ -175,6 +175,9 @@ def test_runtime_entries_without_device():
     assert L.x264hip_set_variant(b"NOT_A_SWITCH", 1) == -1
     assert L.x264hip_forward_ref(None, 0, None, 0, 16, None) == -1
     assert L.x264hip_forward_ref(None, 0, None, 0, 0, None) == 0
+    L.x264hip_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    assert L.x264hip_upload(None, None, 16, None) == -1            # EINVAL before any HIP call
+    assert L.x264hip_upload(None, None, 0, None) == 0              # nothing to copy
     assert "no device" in L.x264hip_backend_banner().decode()
 
 
