@@ -22,11 +22,12 @@ def _host(t, bd):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("size", [(1920, 1088), (80, 48), (176, 144)])
-@pytest.mark.parametrize("variant", ["default", "0", "1", "2"])
+@pytest.mark.parametrize("variant", ["default", "0", "1", "2", "4", "5"])
 def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
     """X264HIP_HPEL_VARIANT: default = streaming lanes at 8 bit with packed shift-saturate
     stores (3) / fused tiles at 10 bit, 0 = fused single pass over LDS tiles, 1 = interior
-    tiles + border expand, 2 = streaming lanes with scaled clamps (med3 + byte picks)."""
+    tiles + border expand, 2 = streaming lanes with scaled clamps (med3 + byte picks),
+    4 / 5 = variants 2 / 3 under a 4-waves-per-SIMD register budget."""
     if variant == "default":
         _x().set_variant("X264HIP_HPEL_VARIANT", None)
     else:
@@ -46,7 +47,7 @@ def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("variant", ["default", "2"])
+@pytest.mark.parametrize("variant", ["default", "2", "4", "5"])
 def test_hpel_filter_extremes(hip, oracle, bd, variant):
     """Pixels 0 / PIXEL_MAX only, so the 6-tap sums reach both ends of every clip
     (H and V: -10 * max .. 42 * max before the shift; centre far beyond int16)."""

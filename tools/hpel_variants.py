@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B of the half-pel filter kernels (X264HIP_HPEL_VARIANT: 0 = fused LDS tiles,
 1 = interior tiles + border expand, 2 = streaming lanes with scaled clamps, 3 = streaming
-lanes with packed shift-saturate (8-bit default)) on 16 frames
+lanes with packed shift-saturate (8-bit default), 4 / 5 = 2 / 3 under a 4-waves-per-SIMD
+register budget) on 16 frames
 of 1080p, 8 and 10 bit, interleaved rounds after a clock-settling warmup."""
 import os, sys, json
 import numpy as np
@@ -16,7 +17,7 @@ for bd in (8, 10):
     W, H = 1920, 1088
     planes, stride, origin = synth.make_sequence(F, W, H, bd)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
-    vs = ("0", "1", "2", "3") if bd == 8 else ("0", "1")
+    vs = ("0", "1", "2", "3", "4", "5") if bd == 8 else ("0", "1")
     outs = {v: [torch.zeros_like(dev) for _ in range(3)] for v in vs}
     run = lambda v: x.hpel_filter(dev, origin, stride, W, H, outs=outs[v])  # noqa
     for v in vs:

@@ -375,10 +375,10 @@ template <int HI, int BY> __device__ __forceinline__ uint32_t pack_clip4( const 
 }
 
 template <int HS_ROWS, bool PK>
-__global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
-                                                             uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
-                                                             intptr_t stride, intptr_t fstride, int width,
-                                                             int height, int hbias, int cbias )
+__device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
+                                                  uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                  intptr_t stride, intptr_t fstride, int width, int height,
+                                                  int hbias, int cbias )
 {
     const int lane = threadIdx.x & 63;
     const int nq = (width + 32) >> 4;                       // column quads over x in [-16, W+16)
@@ -539,6 +539,24 @@ __global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__res
     }
 }
 
+template <int HS_ROWS, bool PK>
+__global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
+                                                             uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                             intptr_t stride, intptr_t fstride, int width,
+                                                             int height, int hbias, int cbias )
+{
+    hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias );
+}
+
+// the same kernel under a 4-waves-per-SIMD register budget (<= 128 VGPRs; variants 4 / 5)
+template <int HS_ROWS, bool PK>
+__global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void hpel_stream4_kernel(
+    const uint8_t *__restrict__ src, uint8_t *__restrict__ dh, uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+    intptr_t stride, intptr_t fstride, int width, int height, int hbias, int cbias )
+{
+    hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias );
+}
+
 template <int BD>
 hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD>::pixel *dh,
                                typename PT<BD>::pixel *dv, typename PT<BD>::pixel *dc, intptr_t stride,
@@ -551,7 +569,7 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
     if constexpr( BD == 8 )
     {
         // streaming kernel: needs 16-byte aligned rows (pixel (0,0) and the strides)
-        if( (var == 2 || var == 3) && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
+        if( var >= 2 && var <= 5 && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
                            (uintptr_t)fstride) & 15) )
         {
             const int nq = (width + 32) / 16, nchunk = (nq + 61) / 62;
@@ -568,6 +586,12 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
     if( var == 3 )                                                                                                 \
         hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, \
                             fstride, width, height, 8 * 16, 64 * 512 );                                            \
+    else if( var == 4 )                                                                                            \
+        hipLaunchKernelGGL( ( hpel_stream4_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,       \
+                            stride, fstride, width, height, 8 * 16, 64 * 512 );                                    \
+    else if( var == 5 )                                                                                            \
+        hipLaunchKernelGGL( ( hpel_stream4_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,        \
+                            stride, fstride, width, height, 8 * 16, 64 * 512 );                                    \
     else                                                                                                           \
         hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,        \
                             stride, fstride, width, height, 8 * 16, 64 * 512 )
