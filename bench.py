@@ -38,13 +38,18 @@ HBM_PEAK = 8.0e12
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    # N ranks, one per GPU: started here as child processes when no launcher set WORLD_SIZE
+    ap.add_argument("--gpus", type=int, default=None)
     # the GPU's clocks settle only after ~100 back-to-back launches (~35 ms of load,
     # tools/me_sustain.py: 0.35-0.40 ms per launch at first, 0.306 ms steady), so the
     # default warmup covers the ramp; every step is still a full launch over F pairs
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=150)
-    ap.add_argument("--frames", type=int, default=16, help="frame pairs per step per GPU")
+    # 64 pairs per headline step: a 1.1-ms launch, so the driver's 5 warmup steps already
+    # carry the GPU through most of its ~20-ms clock transient (profiles/r03a_trace_*: after
+    # an idle gap the first launches of the 16-pair step ran 12-30 % slow)
+    ap.add_argument("--frames", type=int, default=64, help="frame pairs per headline step per GPU")
+    ap.add_argument("--xframes", type=int, default=16, help="frame pairs of the side legs (<= --frames)")
     # the streaming transform kernels (DCT+quant, reconstruction) move ~8.5 MB per 1080p
     # frame; SURVEY.md §8d (configs[3]) asks for >= 64 frames per launch so the launch
     # is not dominated by its ramp and tail
@@ -65,9 +70,11 @@ def dist_setup():
     if world > 1:
         import torch.distributed as dist
         # one rank per GPU; X264HIP_DIST_BACKEND=gloo lets several ranks share one GPU
-        # to exercise the N > 1 path functionally on a single-GPU box (not a measurement)
+        # to exercise the N > 1 path functionally on a single-GPU box (not a measurement);
+        # launch_plan has already refused more RCCL ranks than GPUs
         backend = os.environ.get("X264HIP_DIST_BACKEND", "nccl")
-        dev = local % max(1, torch.cuda.device_count())
+        ndev = torch.cuda.device_count()
+        dev = local if backend == "nccl" else local % max(1, ndev)
         torch.cuda.set_device(dev)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
@@ -95,9 +102,23 @@ def max_over_ranks(v, world):
 _SETTLE_S = 0.0
 
 
-def timed(fn, steps, warmup, world):
+def timed(fn, steps, warmup, world, graph=False):
     """Run warmup, then `steps` timed calls bracketed by barrier + synchronize.
-    Returns (wall seconds max over ranks, mean per-launch event ms on this rank)."""
+    Returns (wall seconds max over ranks, mean per-launch event ms on this rank).
+
+    The mean launch time is one HIP event pair on the launch stream around the `steps`
+    back-to-back launches, divided by `steps` (an event between every two launches
+    costs ~11 us of command-processor time per step in the kernel trace,
+    profiles/r03a_*).  graph=True (extra legs whose launches are shorter than the
+    host's per-call overhead, so the queue would drain between Python calls): the
+    `steps` calls are captured once into one HIP graph and the timed region is one
+    replay of it -- the same launches, without host gaps."""
+    if graph:
+        try:
+            return _timed_graph(fn, steps, warmup, world)
+        except RuntimeError as e:                       # capture unsupported: time eagerly
+            print("bench.py: graph capture failed (%s); timing eagerly" % e, file=sys.stderr)
+            torch.cuda.synchronize()
     for _ in range(warmup):
         fn()
     if _SETTLE_S:
@@ -108,24 +129,81 @@ def timed(fn, steps, warmup, world):
     torch.cuda.synchronize()
     barrier(world)
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    for s, e in evs:
-        s.record()
+    s.record()
+    for _ in range(steps):
         fn()
-        e.record()
+    e.record()
     torch.cuda.synchronize()
     barrier(world)
     t1 = time.perf_counter()
-    ev_ms = sum(s.elapsed_time(e) for s, e in evs) / steps
+    ev_ms = s.elapsed_time(e) / steps
     return max_over_ranks(t1 - t0, world), ev_ms
+
+
+def _timed_graph(fn, steps, warmup, world):
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):                       # allocations made before capture
+        fn()
+    torch.cuda.current_stream().wait_stream(side)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(steps):
+            fn()
+    for _ in range(max(1, warmup // max(1, steps))):
+        g.replay()
+    if _SETTLE_S:
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < _SETTLE_S:
+            g.replay()
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    barrier(world)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    s.record()
+    g.replay()
+    e.record()
+    torch.cuda.synchronize()
+    barrier(world)
+    t1 = time.perf_counter()
+    ev_ms = s.elapsed_time(e) / steps
+    del g
+    return max_over_ranks(t1 - t0, world), ev_ms
+
+
+def world_devices(world):
+    """(process-group world size, the device id of every rank) for the JSON line."""
+    dev = torch.cuda.current_device()
+    if world == 1:
+        return 1, [dev]
+    import torch.distributed as dist
+    got = [None] * dist.get_world_size()
+    dist.all_gather_object(got, dev)
+    return dist.get_world_size(), got
 
 
 def main():
     a = parse()
-    world, rank, local = dist_setup()
     x = load_package()
+    from x264hip import dist as xd0
+    try:
+        # torch.cuda.device_count() does not initialise HIP, so a launching parent stays
+        # GPU-free and its ranks are children (never an exec of a GPU process)
+        how, n = xd0.launch_plan(a.gpus, os.environ, torch.cuda.device_count())
+    except xd0.LaunchError as e:
+        print("bench.py: %s" % e, file=sys.stderr)
+        sys.exit(2)
+    if how == "spawn":
+        rc = xd0.spawn_ranks([os.path.abspath(__file__)] + sys.argv[1:], n, os.environ)
+        sys.exit(rc if rc >= 0 else 128 - rc)
+    world, rank, local = dist_setup()
     x.init(torch.cuda.current_device())
+    pg_world, rank_dev = world_devices(world)
     from x264hip import synth
 
     W, H, R, F = a.width, a.height, a.range, a.frames
@@ -183,7 +261,7 @@ def main():
         "metric": "SAD+SATD candidate-MVs/sec + DCT+quant blocks/sec, 1080p, 1/2/4/8 GPU",
         "value": value,
         "unit": "SAD16x16 candidates/s",
-        "n_gpus": world,
+        "n_gpus": pg_world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": ms_per_step,
@@ -195,12 +273,15 @@ def main():
         "config": {"workload": "configs[1]: %dx%d luma, full-search ME range %d, sad_16x16 candidate tables, "
                                "%d frame pairs per GPU per step" % (W, H, R, F),
                    "frames_per_step_per_gpu": F, "mbs_per_frame": mbw * mbh, "candidates_per_mb": cand_per_mb,
-                   "parallelism": "frame-per-GPU x%d" % world},
+                   "parallelism": "frame-per-GPU x%d" % world,
+                   "world_size": pg_world, "rank_devices": rank_dev,
+                   "dist_backend": (os.environ.get("X264HIP_DIST_BACKEND", "nccl") if world > 1 else None)},
         "roofline": roof,
     }
 
     if not a.no_extra:
-        out["extra"] = extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F)
+        XF = min(a.xframes, F)
+        out["extra"] = extra_rates(x, a, world, dev[:XF + 1], origin, stride, fstride, mbw, mbh, XF)
         # the headline kernel again after the extra legs have kept the GPU busy for tens of
         # seconds: its steady-state launch time and roofline fraction, reported beside (never
         # instead of) the timed region above, which starts after only --warmup launches
@@ -240,7 +321,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
         def step(t=t, mf=mf, bs=bs):
             x.mb_dct_quant(t, tdev[1:], origin, stride, tdev[:-1], origin, stride, mbw, mbh, TF, mf, bs, dct=dct,
                            nz=nz, fenc_frame_stride=fstride, pred_frame_stride=fstride)
-        wall, ev_ms = timed(step, a.steps, a.warmup, world)
+        wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
         blocks = nmb * (16 if t == 4 else 4)
         bpb = (16 + 16 + 32) if t == 4 else (64 + 64 + 128)     # fenc + pred in, int16 coefs out
         res["dct%d_quant_blocks_per_s" % t] = world * a.steps * blocks / wall
@@ -253,7 +334,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
     def hstep():
         x.hpel_filter(dev[:-1], origin, stride, mbw * 16, mbh * 16, outs=[h[:-1] for h in hv])
-    wall, ev_ms = timed(hstep, a.steps, a.warmup, world)
+    wall, ev_ms = timed(hstep, a.steps, a.warmup, world, graph=True)
     res["hpel_filter_frames_per_s"] = world * a.steps * F / wall
     res["hpel_filter_launch_ms"] = ev_ms
     # algorithmic bytes: the padded source plane in, the three padded half-pel planes out
@@ -272,7 +353,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
         def rstep(t=t, dqd=dqd):
             x.mb_dequant_idct_add(t, dct, mbw, mbh, TF, dqd, qp_mb, tdev[:-1], origin, stride, recon, origin,
                                   stride, pred_frame_stride=fstride, recon_frame_stride=fstride)
-        wall, ev_ms = timed(rstep, a.steps, a.warmup, world)
+        wall, ev_ms = timed(rstep, a.steps, a.warmup, world, graph=True)
         blocks = nmb * (16 if t == 4 else 4)
         bpb = (32 + 16 + 16) if t == 4 else (128 + 64 + 64)      # int16 coefs + pred in, recon out
         res["recon%d_blocks_per_s" % t] = world * a.steps * blocks / wall
@@ -285,7 +366,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
     def h64():
         x.hpel_filter(tdev[:-1], origin, stride, mbw * 16, mbh * 16, outs=thv)
-    wall, ev_ms = timed(h64, a.steps, a.warmup, world)
+    wall, ev_ms = timed(h64, a.steps, a.warmup, world, graph=True)
     res["hpel_filter_%d_frames_per_s" % TF] = world * a.steps * TF / wall
     res["hpel_filter_%d_launch_ms" % TF] = ev_ms
     res["hpel_filter_%d_hbm_frac" % TF] = TF * 4 * fb / (ev_ms * 1e-3) / HBM_PEAK
@@ -294,7 +375,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
     def l64():
         x.frame_init_lowres(tdev[:-1], origin, stride, mbw * 16, mbh * 16, outs=tl)
-    wall, ev_ms = timed(l64, a.steps, a.warmup, world)
+    wall, ev_ms = timed(l64, a.steps, a.warmup, world, graph=True)
     lbytes = fb + 4 * tl[0][0].numel()              # source plane in, four padded lowres planes out
     res["lowres_%d_frames_per_s" % TF] = world * a.steps * TF / wall
     res["lowres_%d_launch_ms" % TF] = ev_ms
@@ -306,7 +387,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
     def lstep():
         x.frame_init_lowres(dev[:-1], origin, stride, lw, lh, outs=louts)
-    wall, ev_ms = timed(lstep, a.steps, a.warmup, world)
+    wall, ev_ms = timed(lstep, a.steps, a.warmup, world, graph=True)
     res["lowres_frames_per_s"] = world * a.steps * F / wall
     res["lowres_launch_ms"] = ev_ms
     res["lowres_hbm_frac"] = F * (dev[0].numel() + 4 * louts[0][0].numel()) / (ev_ms * 1e-3) / HBM_PEAK
@@ -316,7 +397,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
     def istep():
         x.lowres_intra_cost(louts[0], x.plane_stride(lw // 2), mbw, mbh, True, True, 1, outs=iouts)
-    wall, ev_ms = timed(istep, a.steps, a.warmup, world)
+    wall, ev_ms = timed(istep, a.steps, a.warmup, world, graph=True)
     res["lowres_intra_mbs_per_s"] = world * a.steps * F * mbw * mbh / wall
     res["lowres_intra_launch_ms"] = ev_ms
     # the lookahead's P-frame lowres motion search on the same planes: frame k+1 against
@@ -399,7 +480,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
     def s9step():
         x.subpel_qpel9_batch(x.CMP_SATD, x.PIXEL_8x8, flat, stride, ref_planes, origin, stride, bfo, cxy, scores=sc9)
-    wall, ev_ms = timed(s9step, a.steps, a.warmup, world)
+    wall, ev_ms = timed(s9step, a.steps, a.warmup, world, graph=True)
     cands = sc9.numel()
     res["satd8x8_subpel_candidates_per_s"] = world * a.steps * cands / wall
     res["satd8x8_subpel_launch_ms"] = ev_ms
@@ -409,7 +490,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
     def sstep():
         x.subpel_cmp_batch(x.CMP_SATD, x.PIXEL_8x8, flat, stride, ref_planes, origin, stride, fo, qxy, scores=sc)
-    wall, ev_ms = timed(sstep, a.steps, a.warmup, world)
+    wall, ev_ms = timed(sstep, a.steps, a.warmup, world, graph=True)
     res["satd8x8_subpel_list_candidates_per_s"] = world * a.steps * fo.numel() / wall
     res["satd8x8_subpel_list_launch_ms"] = ev_ms
     # both entries score the same candidates (list order: frame, dy, dx, block)
@@ -459,7 +540,7 @@ def rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
     def istep():
         x.frame_integral(dev[:-1], origin, stride, H, out=integ)
-    wall, ev_ms = timed(istep, a.steps, a.warmup, world)
+    wall, ev_ms = timed(istep, a.steps, a.warmup, world, graph=True)
     res = {"frame_integral_frames_per_s": world * a.steps * F / wall, "frame_integral_launch_ms": ev_ms}
     out = torch.empty((F * mbw * mbh, 4), dtype=torch.int32, device="cuda")
 
@@ -493,12 +574,16 @@ def rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
 
 
 def rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
-    """The ESA decision of every MB of the F pairs (me.c:618-631, window centred on the
-    predictor, here mv 0 so every candidate of the headline table is in the window):
-    the table path (headline kernel + me_esa_argmin) against the fused kernel that never
-    writes the table.  Both count the same 1089 candidates per MB."""
-    R = a.range
-    par, init, cm, span = tesa_params(mbw, mbh, F, R, centre=(0, 0))
+    """The ESA decision of every MB of the F pairs (me.c:618-631, window of me_range 16
+    centred on the predictor, here mv 0): the table path (the full-search kernel at
+    template range 24 + me_esa_argmin) against the fused kernel that never writes the
+    table.  Both evaluate the same 49x49 = 2401 template candidates per MB."""
+    # me_range = the bench's range (x264's default 16); the template holds me.c's rounded
+    # window around an aligned-down origin only with range >= me_range + 6 (8 bit), so the
+    # exact decision needs the 24 template (49x49 candidates per MB evaluated)
+    me_range = a.range
+    R = next(r for r in (4, 8, 16, 24) if r >= me_range + 6)
+    par, init, cm, span = tesa_params(mbw, mbh, F, me_range, centre=(0, 0))
     par_d, init_d = torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda()
     cm_d = torch.from_numpy(cm.view(np.int16)).cuda()
     table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
@@ -508,14 +593,15 @@ def rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     def tstep():
         x.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, table=table,
                          fenc_frame_stride=fstride, ref_frame_stride=fstride)
-        x.me_esa_argmin(table, R, R, par_d, init_d, (cm_d, span), out=out_t)
+        x.me_esa_argmin(table, R, me_range, par_d, init_d, (cm_d, span), out=out_t)
 
     def fstep():
-        x.me_search_esa(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, R, par_d, init_d,
+        x.me_search_esa(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, me_range, par_d, init_d,
                         (cm_d, span), out=out_f, fenc_frame_stride=fstride, ref_frame_stride=fstride)
     cands = F * mbw * mbh * (2 * R + 1) ** 2
     wall, ev_ms = timed(tstep, a.steps, a.warmup, world)
-    res = {"esa_table_candidates_per_s": world * a.steps * cands / wall, "esa_table_step_ms": ev_ms}
+    res = {"esa_table_candidates_per_s": world * a.steps * cands / wall, "esa_table_step_ms": ev_ms,
+           "esa_template_range": R, "esa_me_range": me_range}
     wall, ev_ms = timed(fstep, a.steps, a.warmup, world)
     res["esa_fused_candidates_per_s"] = world * a.steps * cands / wall
     res["esa_fused_step_ms"] = ev_ms
@@ -532,7 +618,7 @@ def rates_ssd(x, a, world, dev, origin, stride, F):
 
     def step():
         x.ssd_plane_batch(dev[1:], origin, stride, dev[:-1], origin, stride, a.width, a.height, F, out=out)
-    wall, ev_ms = timed(step, a.steps, a.warmup, world)
+    wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
     return {"ssd_plane_frames_per_s": world * a.steps * F / wall, "ssd_plane_launch_ms": ev_ms,
             "ssd_plane_hbm_frac": F * 2 * a.width * a.height / (ev_ms * 1e-3) / HBM_PEAK}
 

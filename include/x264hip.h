@@ -350,7 +350,10 @@ const char *x264hip_backend_banner( void );
  * X264HIP_HPEL_ROWS, X264HIP_SUBPEL_VARIANT, X264HIP_LOWRES_VARIANT, X264HIP_DQ_VARIANT,
  * X264HIP_RECON_VARIANT, X264HIP_LOWRES_INTRA_VARIANT): the environment seeds them
  * once; this changes one at run time (-1 = default).  X264HIP_EINVAL for an
- * unknown name.  Every variant is bit-exact; only speed differs. */
+ * unknown name.  Every variant is bit-exact; only speed differs.  One switch is a test
+ * hook, not a variant: X264HIP_LA_POLL bounds the lookahead wavefront's wait for the band
+ * below (default 2^22 tries); 0 forces the timeout path, whose entry then returns
+ * X264HIP_EDEVICE. */
 int  x264hip_set_variant( const char *name, int value );
 
 /*----------------------------------------------------------------------------
@@ -467,7 +470,9 @@ int x264hip_##BD##_lowres_intra_cost( const pixel *lowres, intptr_t stride,     
  * fenc->lowres_mvs (mvs[2*(f*mbs + mb)]), lowres_mv_costs (mv_costs), lowres_costs               \
  * ((list_used << 14) + cost), the AQ-scaled inter row sums row_satd[f*mbh + y]                  \
  * (i_row_satds[b-p0][0]) and est[3f..3f+2] = cost_est, cost_est_aq, intra_mbs.                  \
- * inv_qscale NULL = AQ off; row_satd / est may be NULL. */                                       \
+ * inv_qscale NULL = AQ off; row_satd / est may be NULL.  Synchronous: the call waits            \
+ * for the kernel and returns X264HIP_EDEVICE ("timed out", outputs invalid) if a band's         \
+ * wait for the band below it ran out (a broken dispatch-order premise, never a normal run). */  \
 int x264hip_##BD##_lowres_inter_cost( const pixel *fenc, intptr_t fenc_frame_stride,             \
                                       const pixel *ref_f, const pixel *ref_h,                     \
                                       const pixel *ref_v, const pixel *ref_c, intptr_t stride,   \

@@ -181,6 +181,25 @@ def test_runtime_entries_without_device():
     assert "no device" in L.x264hip_backend_banner().decode()
 
 
+@pytest.mark.parametrize("bd,slack", [(8, 6), (10, 4)])
+def test_centred_esa_range_bound(bd, slack):
+    """the centred ESA entries refuse a template range that cannot hold me.c's
+    rounded window (me.c:621-626) around an aligned-down origin -- range < me_range + 6
+    (8 bit) / + 4 (10 bit) is X264HIP_EINVAL, checked before any HIP call."""
+    x = load_package()
+    L = x.lib()
+    esa = getattr(L, f"x264hip_{bd}_me_search_esa")
+    at = getattr(L, f"x264hip_{bd}_me_esa_argmin_at")
+    V = ctypes.c_void_p
+    for rng, me_range in ((16, 16), (24, 24 - slack + 1), (8, 8 - slack + 1), (16, 16 - slack + 1)):
+        assert esa(V(), 0, 0, V(), 0, 0, 0, 0, 0, rng, me_range, V(), V(), V(), V(), V()) == -1, (rng, me_range)
+        assert at(V(), rng, 0, me_range, V(8), V(), V(), V(), V(), V()) == -1, (rng, me_range)
+    # in bounds: an empty launch is accepted (no frames, nothing to do)
+    for rng, me_range in ((24, 24 - slack), (16, 16 - slack), (8, 8 - slack)):
+        assert esa(V(), 0, 0, V(), 0, 0, 0, 0, 0, rng, me_range, V(), V(), V(), V(), V()) in (0, -2, -3), \
+            (rng, me_range)
+
+
 # ---------------------------------------------------------------- reference layout
 REF = "/root/reference/common"
 

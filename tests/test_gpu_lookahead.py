@@ -164,3 +164,44 @@ def test_lowres_tall_frames(hip, oracle, bd, H):
     the lane quads walk the rows in several passes per wavefront step."""
     _case(hip, oracle, bd, 64, H, 2, 1, 4, True, random=True, me_range=8)
     _bidir_case(hip, oracle, bd, 64, H, 1, 3, 1, 4, True, 128, 32, random=True, me_range=8)
+
+
+@pytest.mark.parametrize("kind", ["inter", "bidir"])
+def test_lowres_wait_timeout_reports_error(hip, oracle, kind):
+    """a band whose wait for the band below runs out stops and the entry
+    fails (X264HIP_EDEVICE, "timed out") instead of using sentinel predictors.  Forced with
+    a poll bound of 0 tries (X264HIP_LA_POLL); the default bound then gives the oracle's
+    results again on the same inputs."""
+    from x264hip import synth
+    W, H = 256, 192                                   # 12 MB rows: 3 bands of 4, two of them wait
+    frames, stride, origin = synth.make_sequence(3, W, H, 8)
+    dev = torch.from_numpy(frames).cuda()
+    lows, ls = hip.frame_init_lowres(dev, origin, stride, W, H)
+    mbw, mbh = W // 16, H // 16
+    nmb = mbw * mbh
+    cm, c0 = oracle.cost_mv_table(1, 512)
+    cmd = (torch.from_numpy(cm.view(np.int16)).cuda(), c0)
+    intra, _, _ = hip.lowres_intra_cost(lows[0], ls, mbw, mbh, True, True, 1)
+
+    def call():
+        if kind == "inter":
+            return hip.lowres_inter_cost(lows[0][1:], [p[:-1] for p in lows], ls, mbw, mbh, intra[1:], cmd)
+        mvs = [torch.zeros((1, nmb, 2), dtype=torch.int16, device="cuda") for _ in range(2)]
+        costs = [torch.zeros((1, nmb), dtype=torch.int32, device="cuda") for _ in range(2)]
+        return hip.lowres_bidir_cost(lows[0][1:2], [p[0:1] for p in lows], [p[2:3] for p in lows], ls, mbw, mbh,
+                                     cmd, 3, mvs[0], costs[0], mvs[1], costs[1])
+
+    hip.set_variant("X264HIP_LA_POLL", 0)
+    try:
+        with pytest.raises(RuntimeError, match="timed out"):
+            call()
+    finally:
+        hip.set_variant("X264HIP_LA_POLL", None)
+    torch.cuda.synchronize()
+    if kind == "inter":
+        got = [g.cpu().numpy() for g in call()]
+        want = oracle.lowres_inter_cost(8, _host(lows[0][1], 8).ravel(), [_host(p[0], 8).ravel() for p in lows],
+                                        32 * ls + 32, ls, mbw, mbh, intra[1].cpu().numpy().view(np.uint16))
+        assert np.array_equal(got[0][0].reshape(want[0].shape), want[0])
+    else:
+        call()

@@ -236,7 +236,7 @@ def test_me_esa_argmin_centred(hip, oracle, bd):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("rng,me_range", [(24, 16), (16, 8), (8, 4), (24, 12)])
+@pytest.mark.parametrize("rng,me_range", [(24, 16), (16, 8), (8, 2), (24, 12)])
 @pytest.mark.parametrize("W,H,lead", [(160, 96, None), (160, 96, 0), (160, 96, 1), (160, 96, "v3"),
                                       (1920, 1088, None), (1920, 1088, "v3")])
 def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H, lead):

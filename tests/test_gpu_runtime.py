@@ -76,6 +76,41 @@ def test_upload_from_pinned(hip, nbytes, off):
         hip.upload(dev[:4], host[:5])
 
 
+def test_upload_registered_and_pageable(hip):
+    """x264hip_upload resolves the source's device address
+    (hipHostGetDevicePointer) so hipHostRegister'd memory works, and refuses pageable
+    memory with X264HIP_EINVAL instead of letting the kernel fault the GPU."""
+    L = hip.lib()
+    L.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    L.hipHostRegister.restype = ctypes.c_int
+    L.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    L.hipHostUnregister.restype = ctypes.c_int
+    L.x264hip_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
+    n = 3 << 20
+    buf = np.random.default_rng(7).integers(0, 256, n + 4096, dtype=np.uint8)
+    base = (buf.ctypes.data + 4095) & ~4095
+    arr = np.frombuffer((ctypes.c_uint8 * n).from_address(base), dtype=np.uint8)
+    dev = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    # pageable: refused, nothing written, no fault
+    assert L.x264hip_upload(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(base), n, None) == -1
+    assert "page-locked" in L.x264hip_last_error().decode()
+    torch.cuda.synchronize()
+    assert not dev.any()
+    assert L.hipHostRegister(ctypes.c_void_p(base), n, 0) == 0
+    try:
+        for off, nb in ((0, n), (5, n - 5), (4096 * 3 + 1, 100000)):
+            dev.zero_()
+            rc = L.x264hip_upload(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(base + off), nb, None)
+            assert rc == 0, L.x264hip_last_error().decode()
+            torch.cuda.synchronize()
+            assert np.array_equal(dev[:nb].cpu().numpy(), arr[off:off + nb])
+        # a range running past the registration is refused
+        assert L.x264hip_upload(ctypes.c_void_p(dev.data_ptr()), ctypes.c_void_p(base + 16), n, None) == -1
+    finally:
+        torch.cuda.synchronize()
+        L.hipHostUnregister(ctypes.c_void_p(base))
+
+
 def test_backend_banner(hip):
     hip.pixel_init(8)
     b = hip.backend_banner()

@@ -78,9 +78,16 @@ extern "C" int x264hip_init( int device )
 
 extern "C" int x264hip_available( void )
 {
-    if( g_device.load( std::memory_order_acquire ) >= 0 )
+    // a thread bound with x264hip_set_thread_device already has its device: the
+    // implicit init below would hipSetDevice(0) over that binding
+    if( t_device >= 0 || g_device.load( std::memory_order_acquire ) >= 0 )
         return 1;
-    return x264hip_init( 0 ) == X264HIP_OK;
+    int cur = -1;
+    const bool had = hipGetDevice( &cur ) == hipSuccess;
+    const int rc = x264hip_init( 0 );
+    if( had && cur != 0 )
+        (void)hipSetDevice( cur );   // leave the caller's current device as it was
+    return rc == X264HIP_OK;
 }
 
 extern "C" int x264hip_set_thread_device( int device )
@@ -131,7 +138,20 @@ extern "C" int x264hip_upload( void *dst, const void *host_src, size_t bytes, vo
         return X264HIP_OK;
     if( !dst || !host_src )
         return X264HIP_EINVAL;
-    hipError_t e = launch_upload( dst, host_src, bytes, (hipStream_t)stream );
+    // the kernel reads the pages through their device address, which for memory
+    // registered with hipHostRegister need not equal the host address; a pageable
+    // range has none (XNACK is off) and is refused instead of faulting the GPU.  Both
+    // ends of the range must resolve into one contiguous mapping.
+    void *d0 = nullptr, *d1 = nullptr;
+    if( hipHostGetDevicePointer( &d0, (void *)host_src, 0 ) != hipSuccess || !d0 ||
+        hipHostGetDevicePointer( &d1, (void *)((const uint8_t *)host_src + bytes - 1), 0 ) != hipSuccess ||
+        (uint8_t *)d1 != (uint8_t *)d0 + bytes - 1 )
+    {
+        (void)hipGetLastError();
+        snprintf( t_err, sizeof(t_err), "x264hip_upload: source is not page-locked host memory" );
+        return X264HIP_EINVAL;
+    }
+    hipError_t e = launch_upload( dst, d0, bytes, (hipStream_t)stream );
     return e == hipSuccess ? X264HIP_OK : set_err( e, "upload" );
 }
 
@@ -154,7 +174,7 @@ static const char *const k_variant_env[V_COUNT] = {
     "X264HIP_ME_VARIANT", "X264HIP_HPEL_VARIANT", "X264HIP_HPEL_ROWS", "X264HIP_SUBPEL_VARIANT",
     "X264HIP_LOWRES_VARIANT", "X264HIP_DQ_VARIANT", "X264HIP_RECON_VARIANT", "X264HIP_LOWRES_INTRA_VARIANT",
     "X264HIP_LOOKAHEAD_BAND", "X264HIP_ME_LEAD", "X264HIP_TESA_VARIANT",
-    "X264HIP_INTEGRAL_VARIANT" };
+    "X264HIP_INTEGRAL_VARIANT", "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS" };
 
 struct VariantTable
 {
@@ -987,10 +1007,23 @@ static int cqm_init( const uint8_t *const sl[8], int dz_inter, int dz_intra, int
 }
 
 // ============================================================ exported entries
+// a centred window's origin is aligned down by up to 3 (8 bit) / 1 (10 bit) pixels and
+// me.c's ads loop rounds the window width up to a multiple of 4 (me.c:621-626, up to 3
+// columns past bmx + me_range): range >= me_range + this covers every candidate the
+// reference evaluates, whatever the centre and the mv limits
+static constexpr int esa_centred_slack( int bd ) { return bd == 8 ? 6 : 4; }
+
 static int map_err( hipError_t e, const char *where )
 {
     if( e == hipSuccess )
         return X264HIP_OK;
+    if( e == hipErrorLaunchTimeOut )
+    {
+        // the lookahead wavefront's status word (lookahead.hip la_status_end)
+        snprintf( t_err, sizeof(t_err), "%s: a band's wait for the band below timed out; outputs are invalid",
+                  where );
+        return X264HIP_EDEVICE;
+    }
     if( e == hipErrorInvalidValue )
     {
         snprintf( t_err, sizeof(t_err), "%s: invalid argument", where );
@@ -1255,7 +1288,8 @@ extern "C" const char *x264hip_backend_banner( void )
                                                     const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out, \
                                                     void *stream )                                                   \
     {                                                                                                                \
-        if( range < 1 || range > 29 || n < 0 || me_range < 0 || 2 * me_range + 4 > 64 || !origin )                   \
+        if( range < 1 || range > 29 || n < 0 || me_range < 0 || 2 * me_range + 4 > 64 || !origin ||                  \
+            range < me_range + esa_centred_slack( BD ) )                                                             \
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_me_esa_argmin<BD>( table, range, n, me_range, origin, par, init_cost, cost_mv, out,   \
                                                   (hipStream_t)stream ), "me_esa_argmin_at" );                       \
@@ -1285,7 +1319,7 @@ extern "C" const char *x264hip_backend_banner( void )
                                                  void *stream )                                                      \
     {                                                                                                                \
         if( mbw < 0 || mbh < 0 || nframes < 0 || !( range == 4 || range == 8 || range == 16 || range == 24 ) ||       \
-            me_range < 0 || 2 * me_range + 4 > 64 ||                                                                 \
+            me_range < 0 || 2 * me_range + 4 > 64 || range < me_range + esa_centred_slack( BD ) ||                  \
             ((int64_t)nframes * mbw * mbh && (!par || !init_cost || !cost_mv || !out)) )                             \
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_me_search_esa<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, me_range,   \

@@ -674,9 +674,12 @@ __device__ __forceinline__ void lr_store_mv( uint32_t *p, uint32_t v )
 }
 
 // the predictors of block (x, y) in slicetype_mb_cost's order (slicetype.c:651-663):
-// right, then below, below-left, below-right
+// right, then below, below-left, below-right.  Returns -1 when the row-below words did
+// not arrive within poll_max tries (or another band already failed): the caller's band
+// then stops, and the launcher reports the failure instead of letting sentinel words
+// act as predictors.
 __device__ __forceinline__ int lr_preds( const int *ring, int y0, int y1, const uint32_t *gmv, int x, int y, int mbw,
-                                         int mbh, uint32_t (&pred)[4] )
+                                         int mbh, uint32_t (&pred)[4], int poll_max, uint32_t *status )
 {
     int n = 0;
 #pragma unroll
@@ -698,14 +701,25 @@ __device__ __forceinline__ int lr_preds( const int *ring, int y0, int y1, const 
         else
         {
             const uint32_t *row = gmv + (intptr_t)(y + 1) * mbw;
-            for( int it = 0; it < (1 << 22); it++ )  // bounded: a broken schedule ends, never hangs
+            bool ok = false;
+            for( int it = 0; it < poll_max; it++ )   // bounded: a broken schedule ends, never hangs
             {
                 b = lr_load_mv( row + x );
                 bl = x > 0 ? lr_load_mv( row + x - 1 ) : 0;
                 br = x < mbw - 1 ? lr_load_mv( row + x + 1 ) : 0;
                 if( b != LR_SENTINEL && bl != LR_SENTINEL && br != LR_SENTINEL )
+                {
+                    ok = true;
+                    break;
+                }
+                if( lr_load_mv( status ) )           // a band below gave up: so does this one
                     break;
                 __builtin_amdgcn_s_sleep( 2 );
+            }
+            if( !ok )
+            {
+                __hip_atomic_fetch_or( status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+                return -1;
             }
         }
         pred[n++] = b;
@@ -753,7 +767,8 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     intptr_t stride, intptr_t rfs, int mbw, int mbh, int me_method, int subme, int satd, int me_range, int mv_range,
     int lambda, const uint16_t *__restrict__ cost_mv, const uint16_t *__restrict__ intra_cost,
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
-    uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands, int brows )
+    uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands, int brows,
+    int poll_max, uint32_t *status )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring[4 * LR_BAND];            // packed MVs of each band row's 4 latest blocks
@@ -802,6 +817,7 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
             for( int k = 0; k < NDW; k++ )
                 fe[r][k] = fnext[r][k];
         fetch( t + 1 );
+        bool failed = false;
         if( y < y1 && x >= 0 && x < mbw )
         {
             const int mb = x + y * mbw;
@@ -809,10 +825,13 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
             LrCtx<BD> m( fe );
             m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd, q );
             uint32_t pred[4];
-            const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred );
-            int mvx, mvy;
-            const int cost = lr_list<BD>( m, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy, role );
-            if( q == 0 && role == 0 )
+            const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred, poll_max, status );
+            // the lanes of the band share candidate batches: a failed wait stops them all
+            failed = __builtin_amdgcn_ballot_w64( np < 0 ) != 0;
+            int mvx = 0, mvy = 0, cost = 0;
+            if( !failed )
+                cost = lr_list<BD>( m, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy, role );
+            if( !failed && q == 0 && role == 0 )
             {
                 ring[4 * (y - y0) + (x & 3)] = (int)lr_pack( mvx, mvy );
                 lr_store_mv( gmv + mb, lr_pack( mvx, mvy ) );
@@ -838,6 +857,8 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
                 lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
             }
         }
+        if( __builtin_amdgcn_ballot_w64( failed ) )
+            return;                                  // the launcher reports it (status word)
         __syncthreads();
     }
     if( q == 0 && role == 0 && y < y1 && row_satd )
@@ -911,7 +932,7 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const uint16_t *__restrict__ cost_mv, int search, int16_t *__restrict__ mvs0, int32_t *__restrict__ costs0,
     int16_t *__restrict__ mvs1, int32_t *__restrict__ costs1, const int16_t *__restrict__ p1mvs, int dsf, int weight,
     const uint16_t *__restrict__ invq, uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd,
-    int32_t *__restrict__ est, int nbands, int brows )
+    int32_t *__restrict__ est, int nbands, int brows, int poll_max, uint32_t *status )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring0[4 * LR_BAND], ring1[4 * LR_BAND];      // per list
@@ -972,6 +993,7 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
         const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
         LrCtx<BD> m0( fe ), m1( fe ), ms( fe );
         int mvx = 0, mvy = 0, lc = 0;
+        bool failed = false;
         if( act )
         {
             m0.setup( a0, a1, a2, a3, off, stride, x, y, mbw, mbh, mvr, satd, q );
@@ -989,9 +1011,12 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
                 if( search & (1 << role) )
                 {
                     uint32_t pred[4];
-                    const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred );
-                    lc = lr_list<BD>( ms, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy );
-                    if( q == 0 )
+                    const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred, poll_max, status );
+                    // the searching lanes run one instruction stream: a failed wait stops them all
+                    failed = __builtin_amdgcn_ballot_w64( np < 0 ) != 0;
+                    if( !failed )
+                        lc = lr_list<BD>( ms, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy );
+                    if( !failed && q == 0 )
                     {
                         ring[4 * (y - y0) + (x & 3)] = (int)lr_pack( mvx, mvy );
                         lr_store_mv( gmv + mb, lr_pack( mvx, mvy ) );
@@ -1007,6 +1032,8 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
                 }
             }
         }
+        if( __builtin_amdgcn_ballot_w64( failed ) )
+            return;                                  // the launcher reports it (status word)
         const int mv0x = from_role( mvx, 0 ), mv0y = from_role( mvy, 0 ), lc0 = from_role( lc, 0 );
         const int mv1x = from_role( mvx, 1 ), mv1y = from_role( mvy, 1 ), lc1 = from_role( lc, 1 );
         // the predicted bidir mvs from p1's list-0 mvs (slicetype.c:623-645)
@@ -1087,6 +1114,76 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     }
 }
 
+// The wavefront's status word: a per-thread, per-device device word the kernel sets when a
+// band's wait for the band underneath ran out (lr_preds), read back after the launch so
+// the entry returns an error instead of costs built on missing predictors.  The wait can
+// only run out if the schedule's premise breaks: the band a workgroup waits on has a
+// lower index, and an XCD dispatches its workgroups in index order, so by induction the
+// lowest unfinished workgroup is resident and never waits -- no residency bound on the
+// batch is needed; the poll bound (X264HIP_LA_POLL, default 2^22 tries) turns a broken
+// premise (preemption, a changed dispatcher) into this error rather than a hang.
+namespace {
+struct LaStatus
+{
+    int device = -1;
+    uint32_t *dev = nullptr;
+    uint32_t *host = nullptr;
+    ~LaStatus()
+    {
+        if( dev )
+            (void)hipFree( dev );
+        if( host )
+            (void)hipHostFree( host );
+    }
+};
+thread_local LaStatus t_la_status;
+
+hipError_t la_status_begin( hipStream_t stream, uint32_t **word )
+{
+    int d = 0;
+    hipError_t e = hipGetDevice( &d );
+    if( e != hipSuccess )
+        return e;
+    LaStatus &st = t_la_status;
+    if( st.device != d )
+    {
+        if( st.dev )
+            (void)hipFree( st.dev );
+        if( st.host )
+            (void)hipHostFree( st.host );
+        st.dev = nullptr;
+        st.host = nullptr;
+        st.device = -1;
+        if( (e = hipMalloc( (void **)&st.dev, sizeof( uint32_t ) )) != hipSuccess )
+            return e;
+        if( (e = hipHostMalloc( (void **)&st.host, sizeof( uint32_t ), hipHostMallocDefault )) != hipSuccess )
+            return e;
+        st.device = d;
+    }
+    *word = st.dev;
+    return hipMemsetAsync( st.dev, 0, sizeof( uint32_t ), stream );
+}
+
+// after the kernel: hipErrorLaunchTimeOut when a band gave up waiting
+hipError_t la_status_end( hipStream_t stream )
+{
+    LaStatus &st = t_la_status;
+    *st.host = 0;
+    hipError_t e = hipMemcpyAsync( st.host, st.dev, sizeof( uint32_t ), hipMemcpyDeviceToHost, stream );
+    if( e == hipSuccess )
+        e = hipStreamSynchronize( stream );
+    if( e != hipSuccess )
+        return e;
+    return *(volatile uint32_t *)st.host ? hipErrorLaunchTimeOut : hipSuccess;
+}
+
+int la_poll_max()
+{
+    const int v = variant( V_LA_POLL );
+    return v >= 0 ? v : 1 << 22;
+}
+} // namespace
+
 template <int BD>
 hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs,
                                 const typename PT<BD>::pixel *const ra[4], intptr_t afs,
@@ -1124,11 +1221,16 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
     if( mv_range < 1 || lds > 48 * 1024 )
         return hipErrorInvalidValue;
+    uint32_t *status = nullptr;
+    if( (e = la_status_begin( stream, &status )) != hipSuccess )
+        return e;
     hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ra[0], ra[1],
                         ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method, subme, satd,
                         me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, weight,
-                        invq, lowres_costs, row_satd, est, nbands, brows4 );
-    return hipGetLastError();
+                        invq, lowres_costs, row_satd, est, nbands, brows4, la_poll_max(), status );
+    if( (e = hipGetLastError()) != hipSuccess )
+        return e;
+    return (search & 3) ? la_status_end( stream ) : hipSuccess;
 }
 
 template <int BD>
@@ -1160,10 +1262,16 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
     if( mv_range < 1 || lds > 48 * 1024 )
         return hipErrorInvalidValue;
+    uint32_t *status = nullptr;
+    if( (e = la_status_begin( stream, &status )) != hipSuccess )
+        return e;
     hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ref[0],
                         ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
-                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4 );
-    return hipGetLastError();
+                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4,
+                        la_poll_max(), status );
+    if( (e = hipGetLastError()) != hipSuccess )
+        return e;
+    return la_status_end( stream );
 }
 
 #define INST( BD )                                                                                              \

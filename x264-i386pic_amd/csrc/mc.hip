@@ -1622,8 +1622,12 @@ hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t 
     // 16-byte pieces need both ends 16-byte aligned; otherwise the byte path only
     const bool al = !(((uintptr_t)dst | (uintptr_t)src) & 15);
     const size_t n16 = al ? bytes / 16 : 0;
-    // 2048 workgroups: enough reads in flight to cover the PCIe round trip
-    const unsigned g = (unsigned)std::min<size_t>( 2048, std::max<size_t>( 1, (n16 + 1023) / 1024 ) );
+    // 2048 workgroups: enough reads in flight to cover the PCIe round trip.
+    // X264HIP_UPLOAD_WGS caps the grid (a few CUs' worth of grid-stride workgroups leave
+    // the rest of the chip to the kernels the upload overlaps)
+    const int wv = variant( V_UPLOAD_WGS );
+    const size_t cap = wv > 0 ? (size_t)wv : 2048;
+    const unsigned g = (unsigned)std::min<size_t>( cap, std::max<size_t>( 1, (n16 + 1023) / 1024 ) );
     if( !al && bytes > (size_t)g * 256 )
     {
         hipLaunchKernelGGL( upload_kernel, dim3( (unsigned)((bytes + 255) / 256) ), dim3( 256 ), 0, stream,
