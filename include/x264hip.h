@@ -356,10 +356,31 @@ const char *x264hip_backend_banner( void );
  * X264HIP_EDEVICE. */
 int  x264hip_set_variant( const char *name, int value );
 
+/* Table lookup mode of the drop-in 16x16 SAD entries (SURVEY.md §7 hard part 1(b)):
+ * x264hip_{8,10}_me_bind registers, for the CALLING THREAD, one frame's full-search result
+ * -- host pointers at pixel (0,0) of the fenc and ref luma planes (x264's padded planes,
+ * common stride), and a host copy of the x264hip_*_me_search_full table of that pair
+ * (range R, row pitch (2R+1+3)&~3, mb_width x mb_height MBs).  While bound,
+ * sad[PIXEL_16x16] (hence fpelcmp under x264's aliasing, encoder.c:1409-1427),
+ * sad_x3[PIXEL_16x16] and sad_x4[PIXEL_16x16] answer on the host, with no dispatch,
+ * every call whose candidate pointer lies in the bound ref plane at a full-pel mv the
+ * table holds (|mv| <= R) for an MB whose pixels equal the caller's fenc block (me.c's
+ * p_fenc, FENC_STRIDE) -- the ESA / exhaustive and pattern searches of me.c:63-70,
+ * 618-771 over that pair.  Every other call dispatches as before; results are identical
+ * either way.  The planes and the table must stay valid and unchanged while bound.
+ * x264hip_me_unbind releases the thread's binding; x264hip_me_bind_stats returns the
+ * thread's hit / miss counts of bound-mode calls (reset when `reset`). */
+void x264hip_me_unbind( void );
+void x264hip_me_bind_stats( uint64_t *hits, uint64_t *misses, int reset );
+
 /*----------------------------------------------------------------------------
  * Per-bit-depth entries.  BD = 8 or 10.
  *--------------------------------------------------------------------------*/
 #define X264HIP_DECLARE_ENTRIES( BD, pixel, dctcoef, udctcoef, sadt )                            \
+/* lookup mode of the 16x16 SAD table entries (see x264hip_me_unbind above); EINVAL for a       \
+ * bad shape (range 1..29, stride >= 16*mb_width + 64) */                                        \
+int x264hip_##BD##_me_bind( const pixel *fenc, const pixel *ref, intptr_t stride,               \
+                            int mb_width, int mb_height, const sadt *table, int range );        \
 /* drop-in table initialisers (see header comment) */                                           \
 void x264hip_##BD##_pixel_init( uint32_t cpu, x264hip_##BD##_pixel_function_t *pixf );          \
 void x264hip_##BD##_pixel_init_hip( x264hip_##BD##_pixel_function_t *pixf );                    \

@@ -26,7 +26,7 @@ __all__ = [
     "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
-    "backend_banner", "forward_ref", "upload",
+    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -290,8 +290,13 @@ def _declare(L):
     L.x264hip_set_variant.argtypes = [_c.c_char_p, _c.c_int]
     L.x264hip_set_variant.restype = _c.c_int
     L.x264hip_cqm_dequant.argtypes = [_P, _c.c_int, _P, _P]
+    L.x264hip_me_unbind.restype = None
+    L.x264hip_me_bind_stats.argtypes = [_P, _P, _c.c_int]
+    L.x264hip_me_bind_stats.restype = None
     for bd in (8, 10):
         f = lambda n: getattr(L, f"x264hip_{bd}_{n}")  # noqa: E731
+        f("me_bind").argtypes = [_P, _P, _IP, _c.c_int, _c.c_int, _P, _c.c_int]
+        f("me_bind").restype = _c.c_int
         f("pixel_init").argtypes = [_c.c_uint32, _P]
         f("dct_init").argtypes = [_c.c_uint32, _P]
         f("quant_init").argtypes = [_P, _c.c_uint32, _P]
@@ -743,6 +748,53 @@ def lowres_bidir_cost(fenc, refs_a, refs_b, lowres_stride, mb_width, mb_height, 
 def plane_stride(width, pad=PAD):
     """x264-style stride of a padded plane: width + 2*pad rounded up to 64 pixels."""
     return (width + 2 * pad + 63) // 64 * 64
+
+
+class MeBinding:
+    """A thread's lookup-mode binding (x264hip_{8,10}_me_bind): keeps the host planes and
+    table alive; ``close()`` (or leaving the ``with`` block) unbinds."""
+
+    def __init__(self, arrays):
+        self._arrays = arrays
+
+    def stats(self, reset=False):
+        h, m = _c.c_uint64(), _c.c_uint64()
+        lib().x264hip_me_bind_stats(_c.byref(h), _c.byref(m), int(reset))
+        return h.value, m.value
+
+    def close(self):
+        lib().x264hip_me_unbind()
+        self._arrays = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+def me_bind(bitdepth, fenc, fenc_origin, ref, ref_origin, stride, mb_width, mb_height, table, rng):
+    """Bind one frame pair's full-search table for the calling thread's 16x16 SAD table
+    entries (lookup mode, include/x264hip.h x264hip_me_bind).  fenc / ref: host numpy
+    planes (uint8 / uint16) with pixel (0,0) at element offset *_origin; table: the
+    me_search_full table of that pair (numpy or torch, copied to host if on the device)."""
+    import numpy as np
+    if hasattr(table, "cpu"):
+        table = table.cpu().numpy()
+    table = np.ascontiguousarray(table)
+    fenc = np.ascontiguousarray(fenc)
+    ref = np.ascontiguousarray(ref)
+    pt = np.uint8 if bitdepth == 8 else np.uint16
+    st = np.uint16 if bitdepth == 8 else np.uint32
+    fenc, ref, table = fenc.view(pt), ref.view(pt), table.view(st)
+    if table.size < mb_width * mb_height * (2 * rng + 1) * me_table_pitch(rng):
+        raise ValueError("me_bind: table smaller than mb_width*mb_height*(2R+1)*pitch")
+    es = fenc.itemsize
+    rc = getattr(lib(), f"x264hip_{bitdepth}_me_bind")(
+        _c.c_void_p(fenc.ctypes.data + fenc_origin * es), _c.c_void_p(ref.ctypes.data + ref_origin * es), stride,
+        mb_width, mb_height, _c.c_void_p(table.ctypes.data), rng)
+    _rc(rc, "me_bind")
+    return MeBinding((fenc, ref, table))
 
 
 def me_table_pitch(rng):

@@ -14,6 +14,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
 #include <atomic>
 #include <mutex>
 
@@ -269,12 +270,130 @@ void stage_block( P *dst, const P *src, intptr_t stride, int w, int h )
 }
 } // namespace
 
+// ============================================================ table lookup mode
+// x264hip_{8,10}_me_bind: the calling thread registers one frame's full-search result
+// (host copies of the fenc and ref luma planes and of the me_search_full table).  While
+// bound, a 16x16 SAD entry (sad / fpelcmp / sad_x3 / sad_x4) whose candidate pointer
+// lies inside the bound ref plane at a full-pel mv the table holds answers from the
+// table on the host, without a dispatch (reference encoder/me.c:63-70 COST_MV over
+// fpelcmp, encoder.c:1409-1427 aliases; me.c's fenc is mb.pic.p_fenc, a copy of the
+// MB at FENC_STRIDE).  The MB being searched is not passed to the entry: it is the one
+// of the <= 9 MBs whose window covers the candidate's offset whose pixels equal the
+// caller's fenc block (MBs with equal pixels have equal SADs, so any match is exact).
+// Anything else -- another plane, a stride mismatch, a window column outside the
+// table, a field MB -- takes the dispatch path, so results never change.
+namespace {
+struct MeBind
+{
+    int bd = 0;                          // 0: nothing bound
+    const uint8_t *fenc = nullptr;       // pixel (0, 0) of the bound planes
+    const uint8_t *ref = nullptr;
+    intptr_t stride = 0;                 // pixels
+    int mbw = 0, mbh = 0, R = 0, pitch = 0, psz = 1;
+    const void *table = nullptr;         // [mbh][mbw][2R+1][pitch] SADs
+    uint64_t hits = 0, misses = 0;
+};
+thread_local MeBind t_bind;
+constexpr int BIND_PAD = 32;             // x264 PADH / PADV (frame.h:32-33)
+
+// SAD of the 16x16 candidate at `cand` (stride s) for the MB whose pixels equal
+// `fenc` (stride fs), from the bound table; false = not answerable here
+template <int BD>
+inline bool bind_lookup16( const typename PT<BD>::pixel *fenc, intptr_t fs, const typename PT<BD>::pixel *cand,
+                           intptr_t s, int *out )
+{
+    using pixel = typename PT<BD>::pixel;
+    const MeBind &b = t_bind;
+    if( b.bd != BD || s != b.stride )
+        return false;
+    const intptr_t d = (const pixel *)cand - (const pixel *)b.ref;
+    // pixel (x, y), x in [-PAD, stride - PAD): the padded rows hold stride pixels
+    intptr_t y = (d + BIND_PAD) >= 0 ? (d + BIND_PAD) / s : -((-(d + BIND_PAD) + s - 1) / s);
+    const intptr_t x = d - y * s;
+    const int R = b.R;
+    if( y < -R || y > 16 * (intptr_t)(b.mbh - 1) + R || x < -R || x > 16 * (intptr_t)(b.mbw - 1) + R )
+        return false;
+    const int mx0 = (int)std::max<intptr_t>( 0, (x - R + 15) >> 4 ), mx1 = (int)std::min<intptr_t>( b.mbw - 1, (x + R) >> 4 );
+    const int my0 = (int)std::max<intptr_t>( 0, (y - R + 15) >> 4 ), my1 = (int)std::min<intptr_t>( b.mbh - 1, (y + R) >> 4 );
+    const pixel *fp = (const pixel *)b.fenc;
+    for( int my = my0; my <= my1; my++ )
+        for( int mx = mx0; mx <= mx1; mx++ )
+        {
+            const pixel *m = fp + (intptr_t)16 * my * s + 16 * mx;
+            int r = 0;
+            while( r < 16 && !memcmp( fenc + r * fs, m + r * s, 16 * sizeof(pixel) ) )
+                r++;
+            if( r < 16 )
+                continue;
+            const int tx = (int)(x - 16 * mx) + R, ty = (int)(y - 16 * my) + R;
+            const size_t i = (((size_t)my * b.mbw + mx) * (2 * R + 1) + ty) * b.pitch + tx;
+            *out = (int)((const typename PT<BD>::sadt *)b.table)[i];
+            return true;
+        }
+    return false;
+}
+} // namespace
+
+#define DEFINE_BIND( BD )                                                                                            \
+    extern "C" int x264hip_##BD##_me_bind( const PT<BD>::pixel *fenc, const PT<BD>::pixel *ref, intptr_t stride,     \
+                                           int mb_width, int mb_height, const PT<BD>::sadt *table, int range )       \
+    {                                                                                                                \
+        if( !fenc || !ref || !table || mb_width <= 0 || mb_height <= 0 || range < 1 || range > 29 ||                 \
+            stride < 16 * (intptr_t)mb_width + 2 * BIND_PAD )                                                        \
+            return X264HIP_EINVAL;                                                                                   \
+        MeBind &b = t_bind;                                                                                          \
+        b.bd = BD;                                                                                                   \
+        b.fenc = (const uint8_t *)fenc;                                                                              \
+        b.ref = (const uint8_t *)ref;                                                                                \
+        b.stride = stride;                                                                                           \
+        b.mbw = mb_width;                                                                                            \
+        b.mbh = mb_height;                                                                                           \
+        b.R = range;                                                                                                 \
+        b.pitch = (2 * range + 1 + 3) & ~3;                                                                          \
+        b.table = table;                                                                                             \
+        return X264HIP_OK;                                                                                           \
+    }
+DEFINE_BIND( 8 )
+DEFINE_BIND( 10 )
+#undef DEFINE_BIND
+
+extern "C" void x264hip_me_unbind( void )
+{
+    const uint64_t h = t_bind.hits, m = t_bind.misses;
+    t_bind = MeBind();
+    t_bind.hits = h;
+    t_bind.misses = m;
+}
+
+extern "C" void x264hip_me_bind_stats( uint64_t *hits, uint64_t *misses, int reset )
+{
+    if( hits )
+        *hits = t_bind.hits;
+    if( misses )
+        *misses = t_bind.misses;
+    if( reset )
+        t_bind.hits = t_bind.misses = 0;
+}
+
 // ============================================================ per-call pixel entries
 template <int BD, int OP, int IPIX>
 static int cmp_call( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::pixel *p2, intptr_t s2 )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    if constexpr( OP == X264HIP_CMP_SAD && IPIX == X264HIP_PIXEL_16x16 )
+    {
+        if( t_bind.bd )
+        {
+            int v;
+            if( bind_lookup16<BD>( p1, s1, p2, s2, &v ) )
+            {
+                t_bind.hits++;
+                return v;
+            }
+            t_bind.misses++;
+        }
+    }
     CallCtx &c = call_ctx();
     pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
     int64_t *off = (int64_t *)(c.host + ST_OFF);
@@ -294,6 +413,24 @@ static void cmpx_call( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *con
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
+    if constexpr( OP == X264HIP_CMP_SAD && IPIX == X264HIP_PIXEL_16x16 )
+    {
+        if( t_bind.bd )
+        {
+            int v[N];
+            int k = 0;
+            while( k < N && bind_lookup16<BD>( fenc, X264HIP_FENC_STRIDE, refs[k], stride, &v[k] ) )
+                k++;
+            if( k == N )
+            {
+                t_bind.hits += N;
+                for( int j = 0; j < N; j++ )
+                    scores[j] = v[j];
+                return;
+            }
+            t_bind.misses += N;
+        }
+    }
     CallCtx &c = call_ctx();
     pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
     int64_t *off = (int64_t *)(c.host + ST_OFF);
