@@ -505,6 +505,37 @@ int x264hip_##BD##_lowres_inter_cost( const pixel *fenc, intptr_t fenc_frame_str
                                       int32_t *mv_costs, uint16_t *lowres_costs,                 \
                                       int32_t *row_satd, int32_t *est, void *stream );           \
                                                                                                 \
+/* lowres_inter_cost with a weighted reference (slicetype.c:603-614 when                         \
+ * x264_weights_analyse( h, fenc, frames[p0], 1 ) picked fenc->weight[0][0],                     \
+ * slicetype.c:859-862; weightp SMART is the default, common/base.c:452): the integer-pel        \
+ * stage reads ref_w = fenc->weighted[0] (the F plane scaled by weight_scale_plane,              \
+ * slicetype.c:490-499; same stride and frame stride as ref_f), the subpel get_refs weight the   \
+ * unweighted hpel planes with m->weight = (w_scale, w_denom, w_offset) (mc.c:221-249,           \
+ * mc_weight mc.c:117-137); the near-zero fast skip still reads ref_f (slicetype.c:680).         \
+ * ref_w NULL = lowres_inter_cost.  denom 0..7, scale and offset in [-128, 127]. */              \
+int x264hip_##BD##_lowres_inter_cost_w( const pixel *fenc, intptr_t fenc_frame_stride,           \
+                                        const pixel *ref_f, const pixel *ref_h,                   \
+                                        const pixel *ref_v, const pixel *ref_c, intptr_t stride, \
+                                        intptr_t ref_frame_stride, int mb_width, int mb_height,  \
+                                        int n_pairs, int me_method, int subme, int satd,         \
+                                        int me_range, int mv_range, int lambda,                  \
+                                        const uint16_t *cost_mv, const uint16_t *intra_cost,     \
+                                        const uint16_t *inv_qscale, int16_t *mvs,                \
+                                        int32_t *mv_costs, uint16_t *lowres_costs,               \
+                                        int32_t *row_satd, int32_t *est, const pixel *ref_w,     \
+                                        int w_scale, int w_denom, int w_offset, void *stream );  \
+                                                                                                \
+/* x264_weight_scale_plane (common/frame.c:825-842) for n_frames planes: dst = mc_weight(src)    \
+ * over the width x height region at the pointers (the reference weights 16-wide strips while   \
+ * x < width-8 and one 8-wide strip after, so up to 7 columns past width are written too);      \
+ * for the lookahead, src = the lowres F plane's top-left border pixel (-32, -32), width =       \
+ * lowres width + 64, height = lowres height + 64.  dst != src. */                               \
+int x264hip_##BD##_weight_scale_plane( pixel *dst, intptr_t dst_stride, intptr_t dst_frame_stride, \
+                                       const pixel *src, intptr_t src_stride,                    \
+                                       intptr_t src_frame_stride, int width, int height,         \
+                                       int n_frames, int scale, int denom, int offset,           \
+                                       void *stream );                                           \
+                                                                                                \
 /* the lookahead's B-frame costs: slicetype_mb_cost with b_bidir (p0 < b < p1,                    \
  * slicetype.c:514-713, 758-791) for n triplets: fenc = lowres[0] of frame b, ref_a /            \
  * ref_b = the four lowres planes (F, H, V, C) of p0 / p1, each with its own frame stride         \

@@ -1512,6 +1512,55 @@ const pixel *FN(get_ref)( pixel *dst, intptr_t *dst_stride, const pixel *const s
     return src1;
 }
 
+/* mc_weight (reference common/mc.c:117-137): explicit weighted prediction of a w x h
+ * block, offset scaled by 1 << (BIT_DEPTH-8); denom 0 has no rounding term.  In place
+ * is allowed (get_ref weights its own average, mc.c:235-236). */
+void FN(mc_weight)( pixel *dst, intptr_t ds, const pixel *src, intptr_t ss, int scale, int denom, int offset,
+                    int w, int h )
+{
+    const int off = offset * (1 << (BIT_DEPTH - 8));
+    for( int y = 0; y < h; y++ )
+        for( int x = 0; x < w; x++ )
+        {
+            const int v = src[y * ss + x];
+            dst[y * ds + x] = (pixel)clip_pixel( denom >= 1 ? ((v * scale + (1 << (denom - 1))) >> denom) + off
+                                                            : v * scale + off );
+        }
+}
+
+/* get_ref with a weight (reference common/mc.c:221-249 with weight->weightfn set):
+ * the qpel average (or the plane itself) then mc_weight into dst */
+static const pixel *get_ref_w( pixel *dst, intptr_t *dst_stride, const pixel *const src[4], intptr_t stride,
+                               int mvx, int mvy, int w, int h, const int *wt )
+{
+    const pixel *r = FN(get_ref)( dst, dst_stride, src, stride, mvx, mvy, w, h );
+    if( !wt )
+        return r;
+    FN(mc_weight)( dst, 16, r, *dst_stride, wt[0], wt[1], wt[2], w, h );
+    *dst_stride = 16;
+    return dst;
+}
+
+/* x264_weight_scale_plane (reference common/frame.c:825-842): the plane weighted in
+ * strips of 16 rows, 16-wide blocks while x < width-8 and one 8-wide block after, so
+ * up to 7 columns past `width` are weighted too (pointers at the region's top-left). */
+void FN(weight_scale_plane)( pixel *dst, intptr_t ds, const pixel *src, intptr_t ss, int width, int height,
+                             int scale, int denom, int offset )
+{
+    while( height > 0 )
+    {
+        const int hh = height < 16 ? height : 16;
+        int x;
+        for( x = 0; x < width - 8; x += 16 )
+            FN(mc_weight)( dst + x, ds, src + x, ss, scale, denom, offset, 16, hh );
+        if( x < width )
+            FN(mc_weight)( dst + x, ds, src + x, ss, scale, denom, offset, 8, hh );
+        height -= 16;
+        dst += 16 * ds;
+        src += 16 * ss;
+    }
+}
+
 /* whole-frame half-pel planes: x264_frame_filter (reference common/mc.c:704-726)
  * over every MB row (rows [-8, H+8), columns [-8, W+8) of hpel_filter) followed by
  * x264_frame_expand_border_filtered (common/frame.c:599-625: edges taken from
@@ -2080,6 +2129,8 @@ typedef struct
 {
     const pixel *fenc;               /* 8x8 block, FENC_STRIDE */
     const pixel *planes[4];          /* F, H, V, C of the reference at the block */
+    const pixel *fw;                 /* p_fref_w: the weighted F plane (= planes[0] unweighted) */
+    const int *wt;                   /* m->weight: { scale, denom, offset } or NULL */
     intptr_t stride;
     const uint16_t *cmx, *cmy;       /* p_cost_mvx / p_cost_mvy = cost_mv - mvp */
     int satd;                        /* mbcmp: satd (else sad) */
@@ -2087,16 +2138,16 @@ typedef struct
     int fpel_min[2], fpel_max[2];    /* mv_limit_fpel */
 } lrme_t;
 
-static int lr_fpel( const lrme_t *m, int mx, int my )          /* fpelcmp on the full-pel plane */
+static int lr_fpel( const lrme_t *m, int mx, int my )          /* fpelcmp on p_fref_w (me.c:63-70) */
 {
-    return FN(sad)( 3, m->fenc, FENC_STRIDE, m->planes[0] + my * m->stride + mx, m->stride );
+    return FN(sad)( 3, m->fenc, FENC_STRIDE, m->fw + my * m->stride + mx, m->stride );
 }
 
-static int lr_qpel( const lrme_t *m, int mx, int my, int satd ) /* get_ref (mc.c:221-249) then cmp */
+static int lr_qpel( const lrme_t *m, int mx, int my, int satd ) /* get_ref (mc.c:221-249, m->weight) then cmp */
 {
     pixel tmp[8 * 16];
     intptr_t ts = 16;
-    const pixel *r = FN(get_ref)( tmp, &ts, m->planes, m->stride, mx, my, 8, 8 );
+    const pixel *r = get_ref_w( tmp, &ts, m->planes, m->stride, mx, my, 8, 8, m->wt );
     return satd ? FN(satd)( 3, m->fenc, FENC_STRIDE, r, ts ) : FN(sad)( 3, m->fenc, FENC_STRIDE, r, ts );
 }
 
@@ -2385,6 +2436,8 @@ static void lr_setup( lrme_t *m, pixel *fbuf, const pixel *fenc, const pixel *co
     m->fenc = fbuf;
     for( int k = 0; k < 4; k++ )
         m->planes[k] = ref[k] + off;
+    m->fw = m->planes[0];
+    m->wt = NULL;
     m->stride = stride;
     m->satd = satd;
     const int mvr = 2 * mv_range;
@@ -2461,11 +2514,37 @@ static int lr_list( lrme_t *m, int16_t *mvs, int mb, int mbx, int mby, int mb_wi
  * fenc->i_intra_cost (x264hip lowres_intra_cost).  Outputs lowres_mvs[mb][2],
  * lowres_mv_costs[mb], lowres_costs[mb] ((list_used << 14) + cost), row_satd[y]
  * (AQ-scaled inter row sums) and est = { cost_est, cost_est_aq, intra_mbs }. */
+void FN(lowres_inter_cost_w)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
+                              const pixel *ref3, const pixel *ref_w, const int *weight, intptr_t stride,
+                              int mb_width, int mb_height, int me_method,
+                              int subme, int satd, int me_range, int mv_range, int lambda, const uint16_t *cost_mv,
+                              const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs, int32_t *mv_costs,
+                              uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] );
+
 void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
                             const pixel *ref3, intptr_t stride, int mb_width, int mb_height, int me_method,
                             int subme, int satd, int me_range, int mv_range, int lambda, const uint16_t *cost_mv,
                             const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs, int32_t *mv_costs,
                             uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] )
+{
+    FN(lowres_inter_cost_w)( fenc, ref0, ref1, ref2, ref3, NULL, NULL, stride, mb_width, mb_height, me_method, subme,
+                             satd, me_range, mv_range, lambda, cost_mv, intra_cost, inv_qscale, mvs, mv_costs,
+                             lowres_costs, row_satd, est );
+}
+
+/* The weighted-reference form (slicetype.c:603-614 with w[0].weightfn set, i.e. when
+ * x264_weights_analyse( h, fenc, frames[p0], 1 ) picked a weight, slicetype.c:859-862):
+ * the integer-pel stage reads fenc->weighted[0] (ref_w, the F plane scaled by
+ * x264_weight_scale_plane, slicetype.c:490-499) and every get_ref of the subpel stages
+ * weights the unweighted hpel planes with m->weight = weight { scale, denom, offset };
+ * the near-zero fast skip still compares against the unweighted F plane
+ * (slicetype.c:680).  ref_w / weight NULL: the unweighted search. */
+void FN(lowres_inter_cost_w)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
+                              const pixel *ref3, const pixel *ref_w, const int *weight, intptr_t stride,
+                              int mb_width, int mb_height, int me_method,
+                              int subme, int satd, int me_range, int mv_range, int lambda, const uint16_t *cost_mv,
+                              const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs, int32_t *mv_costs,
+                              uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] )
 {
     pixel fbuf[8 * FENC_STRIDE];
     const pixel *ref[4] = { ref0, ref1, ref2, ref3 };
@@ -2478,6 +2557,11 @@ void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *r
             const int mb = mbx + mby * mb_width;
             lrme_t m;
             lr_setup( &m, fbuf, fenc, ref, stride, mbx, mby, mb_width, mb_height, mv_range, satd );
+            if( ref_w && weight )
+            {
+                m.fw = ref_w + 8 * mbx + 8 * mby * stride;
+                m.wt = weight;
+            }
             const int cost = lr_list( &m, mvs, mb, mbx, mby, mb_width, mb_height, me_method, subme, me_range, lambda,
                                       cost_mv );
             mv_costs[mb] = cost;

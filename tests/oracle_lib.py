@@ -113,6 +113,10 @@ for _bd in (8, 10):
     _f(_bd, "lowres_intra_cost", [_P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "lowres_inter_cost", [_P, _P, _P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P])
+    _f(_bd, "lowres_inter_cost_w", [_P, _P, _P, _P, _P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P])
+    _f(_bd, "weight_scale_plane", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int])
+    _f(_bd, "mc_weight", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int])
     _f(_bd, "lowres_bidir_cost", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, _P, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P, _P, _P, _P])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
@@ -514,10 +518,20 @@ def cost_mv_table(lam=1, mv_range=512):
     return np.concatenate([half[:0:-1], half]).astype(np.uint16), span
 
 
+def weight_scale_plane(bd, src, src_off, stride, width, height, scale, denom, offset, dst=None):
+    """x264_weight_scale_plane (frame.c:825-842) of the width x height region at src[src_off]
+    (stride), into a copy of src (or dst) at the same offset; returns the destination array."""
+    out = np.array(src, copy=True) if dst is None else dst
+    fn(bd, "weight_scale_plane")(_addr(out, src_off), stride, _addr(src, src_off), stride, width, height, scale,
+                                 denom, offset)
+    return out
+
+
 def lowres_inter_cost(bd, fenc, ref_planes, origin, stride, mbw, mbh, intra_cost, me_method=1, subme=4, satd=True,
-                      me_range=16, mv_range=512, lam=1, cost_mv=None, inv_qscale=None):
+                      me_range=16, mv_range=512, lam=1, cost_mv=None, inv_qscale=None, ref_w=None, weight=None):
     """slicetype_mb_cost's P-frame inter leg over one lowres pair (numpy planes, (0,0) at origin):
-    (mvs int16 [mbs, 2], mv_costs int32 [mbs], lowres_costs uint16 [mbs], row_satd int32 [mbh], est int32 [3])"""
+    (mvs int16 [mbs, 2], mv_costs int32 [mbs], lowres_costs uint16 [mbs], row_satd int32 [mbh], est int32 [3]).
+    ref_w / weight (scale, denom, offset): the weighted-reference form (fenc->weighted[0])."""
     if cost_mv is None:
         cost_mv = cost_mv_table(lam, mv_range)
     cm, c0 = cost_mv
@@ -529,10 +543,12 @@ def lowres_inter_cost(bd, fenc, ref_planes, origin, stride, mbw, mbh, intra_cost
     est = np.zeros(3, np.int32)
     ic = np.ascontiguousarray(intra_cost, np.uint16)
     iq = None if inv_qscale is None else np.ascontiguousarray(inv_qscale, np.uint16)
-    fn(bd, "lowres_inter_cost")(_addr(fenc, origin), *[_addr(p, origin) for p in ref_planes], stride, mbw, mbh,
-                                me_method, subme, int(satd), me_range, mv_range, lam, _addr(cm, c0), _addr(ic),
-                                None if iq is None else _addr(iq), _addr(mvs), _addr(mvc), _addr(lc), _addr(rows),
-                                _addr(est))
+    wt = None if weight is None else np.ascontiguousarray(weight, np.int32)
+    fn(bd, "lowres_inter_cost_w")(_addr(fenc, origin), *[_addr(p, origin) for p in ref_planes],
+                                  None if ref_w is None else _addr(ref_w, origin), None if wt is None else _addr(wt),
+                                  stride, mbw, mbh, me_method, subme, int(satd), me_range, mv_range, lam, _addr(cm, c0),
+                                  _addr(ic), None if iq is None else _addr(iq), _addr(mvs), _addr(mvc), _addr(lc),
+                                  _addr(rows), _addr(est))
     return mvs, mvc, lc, rows, est
 
 

@@ -35,3 +35,60 @@ def test_frame_init_lowres(oracle, bd, size):
     want = _np_lowres(core, bd)
     for g, w in zip(got, want):
         assert np.array_equal(g[:, :W // 2 + 64], w)
+
+
+def _np_weight(p, scale, denom, offset, bd):
+    off = offset << (bd - 8)
+    v = p.astype(np.int64) * scale
+    v = ((v + (1 << (denom - 1))) >> denom) if denom >= 1 else v
+    return np.clip(v + off, 0, (1 << bd) - 1)
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("width,height", [(64, 40), (73, 17), (81, 33), (5, 3)])
+@pytest.mark.parametrize("w", [(40, 5, -6), (1, 0, 3), (127, 7, 0), (-3, 1, 100)])
+def test_weight_scale_plane(oracle, bd, width, height, w):
+    """x264_weight_scale_plane (frame.c:825-842) = mc_weight (mc.c:117-137) of every pixel in
+    the reference's strip coverage: 16-wide blocks while x < width-8, then one 8-wide block,
+    so up to 7 columns past width; nothing else is touched."""
+    stride = 128
+    rs = np.random.default_rng(width * height + bd)
+    src = rs.integers(0, 1 << bd, (height + 2, stride)).astype(np.uint8 if bd == 8 else np.uint16)
+    dst = np.full_like(src, 7)
+    oracle.weight_scale_plane(bd, src, stride, stride, width, height, *w, dst=dst)
+    cov = 0
+    while cov < width - 8:
+        cov += 16
+    cov = cov + 8 if cov < width else cov
+    want = np.full_like(src, 7)
+    want[1:height + 1, :cov] = _np_weight(src[1:height + 1, :cov], *w, bd)
+    assert np.array_equal(dst, want)
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_lowres_weighted_identity(oracle, bd):
+    """The weighted-reference search with the identity weight (scale 1 << denom, offset 0) on the
+    unweighted plane is the unweighted search; a real weight changes the result."""
+    from conftest import load_package
+    load_package()
+    from x264hip import synth
+    W, H = 128, 96
+    frames, stride, origin = synth.make_sequence(2, W, H, bd)
+    lw, lh = W // 2, H // 2
+    ls = synth.plane_stride(lw)
+    per = [oracle.frame_init_lowres(bd, frames[f].ravel(), origin, stride, W, H, ls) for f in range(2)]
+    lows = [np.stack([per[f][k] for f in range(2)]) for k in range(4)]
+    lo = 32 * ls + 32
+    mbw, mbh = W // 16, H // 16
+    intra = np.full(mbw * mbh, 16383, np.uint16)
+    refs = [p[0].ravel() for p in lows]
+    base = oracle.lowres_inter_cost(bd, lows[0][1].ravel(), refs, lo, ls, mbw, mbh, intra)
+    same = oracle.lowres_inter_cost(bd, lows[0][1].ravel(), refs, lo, ls, mbw, mbh, intra, ref_w=refs[0],
+                                    weight=(16, 4, 0))
+    for a, b in zip(base, same):
+        assert np.array_equal(a, b)
+    wt = (23, 5, -9)
+    rw = oracle.weight_scale_plane(bd, lows[0][0], 0, ls, lw + 64, lh + 64, *wt)
+    other = oracle.lowres_inter_cost(bd, lows[0][1].ravel(), refs, lo, ls, mbw, mbh, intra, ref_w=rw.ravel(),
+                                     weight=wt)
+    assert not all(np.array_equal(a, b) for a, b in zip(base, other))

@@ -205,3 +205,50 @@ def test_lowres_wait_timeout_reports_error(hip, oracle, kind):
         assert np.array_equal(got[0][0].reshape(want[0].shape), want[0])
     else:
         call()
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("wt", [(40, 5, -6), (23, 4, 9), (1, 0, 3), (16, 4, 0)])
+def test_lowres_inter_weighted_1080p(hip, oracle, bd, wt):
+    """the weighted-reference P search (slicetype.c:603-614, 859-862) on 1080p
+    pairs whose fenc is a fade of the reference: fenc->weighted[0] from weight_scale_plane
+    (frame.c:825-842, checked against the oracle), then lowres_inter_cost with ref_w + weight,
+    bit-exact vs the oracle (integer stage on the weighted plane, weighted get_ref, unweighted
+    fast skip)."""
+    from x264hip import synth
+    W, H, n = 1920, 1088, 2
+    frames, stride, origin = synth.make_sequence(n + 1, W, H, bd)
+    pmax = (1 << bd) - 1
+    # a fade: each later frame darker and offset (the case weights_analyse catches)
+    for k in range(1, n + 1):
+        frames[k] = np.clip(frames[k].astype(np.int64) * (10 - 2 * k) // 10 + 5 * k, 0, pmax).astype(frames.dtype)
+    dev = torch.from_numpy(frames.view(np.int16) if bd == 10 else frames).cuda()
+    lows, ls = hip.frame_init_lowres(dev, origin, stride, W, H)
+    mbw, mbh = W // 16, H // 16
+    intra, _, _ = hip.lowres_intra_cost(lows[0], ls, mbw, mbh, True, True, 1)
+    cm, c0 = oracle.cost_mv_table(1, 512)
+    cm_dev = torch.from_numpy(cm.view(np.int16)).cuda()
+    refs = [p[:-1] for p in lows]
+    rw = hip.weight_scale_plane(refs[0], ls, W // 2, H // 2, *wt)
+    torch.cuda.synchronize()
+    hl = [_host(p, bd) for p in lows]
+    rwh = _host(rw, bd)
+    for f in range(n):
+        want_w = oracle.weight_scale_plane(bd, hl[0][f], 0, ls, W // 2 + 64, H // 2 + 64, *wt)
+        assert np.array_equal(rwh[f], want_w), f
+    got = hip.lowres_inter_cost(lows[0][1:], refs, ls, mbw, mbh, intra[1:], (cm_dev, c0), ref_w=rw, weight=wt)
+    torch.cuda.synchronize()
+    got = [g.cpu().numpy() for g in got]
+    ih = intra.cpu().numpy().view(np.uint16)
+    lo = 32 * ls + 32
+    for f in range(n):
+        want = oracle.lowres_inter_cost(bd, hl[0][f + 1].ravel(), [p[f].ravel() for p in hl], lo, ls, mbw, mbh,
+                                        ih[f + 1], ref_w=rwh[f].ravel(), weight=wt)
+        for name, g, w in zip(("mvs", "mv_costs", "lowres_costs", "row_satd", "est"), got, want):
+            g = g[f].reshape(w.shape).view(w.dtype) if name == "lowres_costs" else g[f].reshape(w.shape)
+            assert np.array_equal(g, w), (f, name, np.argwhere(g != w)[:4])
+    if wt == (16, 4, 0):                              # the identity weight is the unweighted search
+        plain = hip.lowres_inter_cost(lows[0][1:], refs, ls, mbw, mbh, intra[1:], (cm_dev, c0))
+        torch.cuda.synchronize()
+        for g, p in zip(got, plain):
+            assert np.array_equal(g, p.cpu().numpy())

@@ -79,8 +79,10 @@ def test_me_bind_esa_1080p(hip, oracle, tmp_path):
     assert np.array_equal(tab[..., :2 * R + 1], want16)
     # an oracle table wide enough for every window below (R 24), as the reference's direct SADs
     R2 = 24
-    wide = oracle.me_search_full(8, planes[1].ravel(), origin, stride, planes[0].ravel(), origin, stride, mbw,
-                                 mbh, R2).reshape(nmb, 2 * R2 + 1, 2 * R2 + 1)
+    w2 = oracle.me_search_full(8, planes[1].ravel(), origin, stride, planes[0].ravel(), origin, stride, mbw,
+                               mbh, R2).reshape(nmb, 2 * R2 + 1, 2 * R2 + 1)
+    wide = np.zeros((nmb, 2 * R2 + 1, hip.me_table_pitch(R2)), w2.dtype)     # me_esa_argmin's pitched layout
+    wide[:, :, :2 * R2 + 1] = w2
     rs = np.random.default_rng(2024)
     par = np.zeros((nmb, 8), np.int16)
     par[:, 0] = rs.integers(-1, 2, nmb)

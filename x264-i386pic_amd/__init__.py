@@ -26,7 +26,7 @@ __all__ = [
     "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
-    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding",
+    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -357,6 +357,12 @@ def _declare(L):
                                            _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P, _P,
                                            _P, _P, _P]
         f("lowres_inter_cost").restype = _c.c_int
+        f("lowres_inter_cost_w").argtypes = f("lowres_inter_cost").argtypes[:-1] + [_P, _c.c_int, _c.c_int, _c.c_int,
+                                                                                   _P]
+        f("lowres_inter_cost_w").restype = _c.c_int
+        f("weight_scale_plane").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
+                                            _c.c_int, _c.c_int, _P]
+        f("weight_scale_plane").restype = _c.c_int
         f("lowres_bidir_cost").argtypes = [_P, _IP, _P, _P, _P, _P, _IP, _P, _P, _P, _P, _IP, _IP, _c.c_int,
                                            _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                            _c.c_int, _P, _c.c_int, _P, _P, _P, _P, _P, _c.c_int, _c.c_int, _P, _P,
@@ -682,14 +688,38 @@ def _frame_stride(*planes):
     return fs.pop()
 
 
+def weight_scale_plane(src, lowres_stride, width, height, scale, denom, offset, out=None):
+    """x264_weight_scale_plane over whole padded lowres planes [n, rows, stride] (the
+    reference's call of slicetype.c:490-499: from pixel (-PAD, -PAD), width + 2*PAD columns,
+    height + 2*PAD rows): fenc->weighted[0] of each plane.  Returns `out` (same shape)."""
+    import torch
+    bd = _pix_bd(src)
+    w = width + 2 * PAD
+    cov = 0
+    while cov < w - 8:
+        cov += 16
+    cov = cov + 8 if cov < w else cov
+    if cov > lowres_stride:                            # the last row's strip would leave the plane
+        raise ValueError("weight_scale_plane: the reference's 8/16-wide strips overrun the stride")
+    if out is None:
+        out = torch.empty_like(src)
+    n = src.shape[0]
+    _rc(getattr(lib(), f"x264hip_{bd}_weight_scale_plane")(
+        _ptr(out), lowres_stride, _frame_stride(out), _ptr(src), lowres_stride, _frame_stride(src),
+        width + 2 * PAD, height + 2 * PAD, n, scale, denom, offset, _stream()), "weight_scale_plane")
+    return out
+
+
 def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost, cost_mv_center, me_method=1,
-                      subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None, outs=None):
+                      subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None, outs=None,
+                      ref_w=None, weight=None):
     """The lookahead's P-frame lowres motion search (x264hip_*_lowres_inter_cost) for the pairs
     (fenc[i], refs[*][i]): fenc = lowres[0] planes [n, rows, stride], refs = the four lowres planes
     (F, H, V, C) of the references, same shape; (0,0) at (PAD, PAD).  intra_cost [n, mbs] from
     lowres_intra_cost; cost_mv_center = (uint16-as-int16 tensor, element offset of mvd 0).  Returns
     (mvs int16 [n, mbs, 2], mv_costs int32 [n, mbs], lowres_costs uint16-as-int16 [n, mbs],
-    row_satd int32 [n, mbh], est int32 [n, 3])."""
+    row_satd int32 [n, mbh], est int32 [n, 3]).  ref_w (weighted F planes, weight_scale_plane) and
+    weight = (scale, denom, offset): the weighted-reference search (x264hip_*_lowres_inter_cost_w)."""
     import torch
     bd = _pix_bd(fenc)
     n = fenc.shape[0]
@@ -704,11 +734,15 @@ def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost
     mvs, mvc, lc, rows, est = outs
     cm, c0 = cost_mv_center
     o = PAD * lowres_stride + PAD
-    _rc(getattr(lib(), f"x264hip_{bd}_lowres_inter_cost")(
-        _ptr(fenc, o), _frame_stride(fenc), *[_ptr(r, o) for r in refs], lowres_stride, _frame_stride(*refs),
+    if (ref_w is None) != (weight is None):
+        raise ValueError("lowres_inter_cost: ref_w and weight go together")
+    rfs = _frame_stride(*refs) if ref_w is None else _frame_stride(*refs, ref_w)
+    w = (0, 0, 0) if weight is None else tuple(int(v) for v in weight)
+    _rc(getattr(lib(), f"x264hip_{bd}_lowres_inter_cost_w")(
+        _ptr(fenc, o), _frame_stride(fenc), *[_ptr(r, o) for r in refs], lowres_stride, rfs,
         mb_width, mb_height, n, me_method, subme, int(bool(satd)), me_range, mv_range, lam, _ptr(cm, c0),
         _ptr(intra_cost), _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(mvs), _ptr(mvc), _ptr(lc),
-        _ptr(rows), _ptr(est), _stream()), "lowres_inter_cost")
+        _ptr(rows), _ptr(est), None if ref_w is None else _ptr(ref_w, o), *w, _stream()), "lowres_inter_cost")
     return mvs, mvc, lc, rows, est
 
 

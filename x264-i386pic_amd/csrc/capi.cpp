@@ -1336,18 +1336,21 @@ extern "C" const char *x264hip_backend_banner( void )
                                                  invq, cost, row_satd, est, (hipStream_t)stream ),                   \
                         "lowres_intra_cost" );                                                                       \
     }                                                                                                                \
-    extern "C" int x264hip_##BD##_lowres_inter_cost(                                                               \
+    extern "C" int x264hip_##BD##_lowres_inter_cost_w(                                                             \
         const PT<BD>::pixel *fenc, intptr_t ffs, const PT<BD>::pixel *rf, const PT<BD>::pixel *rh,                  \
         const PT<BD>::pixel *rv, const PT<BD>::pixel *rc, intptr_t stride, intptr_t rfs, int mbw, int mbh,          \
         int npairs, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,                     \
         const uint16_t *cost_mv, const uint16_t *intra_cost, const uint16_t *invq, int16_t *mvs, int32_t *mv_costs,   \
-        uint16_t *lowres_costs, int32_t *row_satd, int32_t *est, void *stream )                                      \
+        uint16_t *lowres_costs, int32_t *row_satd, int32_t *est, const PT<BD>::pixel *ref_w, int w_scale,           \
+        int w_denom, int w_offset, void *stream )                                                                    \
     {                                                                                                                \
         const intptr_t pb = (intptr_t)sizeof( PT<BD>::pixel );                                                       \
         if( mbw < 0 || mbh < 0 || npairs < 0 || ( me_method != 0 && me_method != 1 ) ||                              \
             ( subme != 2 && subme != 4 ) || me_range < 1 || mv_range < 1 || lambda < 0 ||                            \
             ( (uintptr_t)fenc & 3 ) || ( ( stride * pb ) & 3 ) || ( ( ffs * pb ) & 3 ) ||                            \
             stride < 8 * mbw + 64 ||                                                                                 \
+            ( ref_w && ( w_denom < 0 || w_denom > 7 || w_scale < -128 || w_scale > 127 || w_offset < -128 ||         \
+                         w_offset > 127 ) ) ||                                                                       \
             ( (int64_t)mbw * mbh * npairs > 0 &&                                                                     \
               ( !fenc || !rf || !rh || !rv || !rc || !cost_mv || !intra_cost || !mvs || !mv_costs ||                 \
                 !lowres_costs ) ) )                                                                                  \
@@ -1355,8 +1358,34 @@ extern "C" const char *x264hip_backend_banner( void )
         const PT<BD>::pixel *ref[4] = { rf, rh, rv, rc };                                                            \
         return map_err( launch_lowres_inter<BD>( fenc, ffs, ref, stride, rfs, mbw, mbh, npairs, me_method, subme,    \
                                                  satd, me_range, mv_range, lambda, cost_mv, intra_cost, invq, mvs,   \
-                                                 mv_costs, lowres_costs, row_satd, est, (hipStream_t)stream ),       \
+                                                 mv_costs, lowres_costs, row_satd, est, ref_w, w_scale, w_denom,     \
+                                                 w_offset, (hipStream_t)stream ),                                    \
                         "lowres_inter_cost" );                                                                       \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_lowres_inter_cost(                                                               \
+        const PT<BD>::pixel *fenc, intptr_t ffs, const PT<BD>::pixel *rf, const PT<BD>::pixel *rh,                  \
+        const PT<BD>::pixel *rv, const PT<BD>::pixel *rc, intptr_t stride, intptr_t rfs, int mbw, int mbh,          \
+        int npairs, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,                     \
+        const uint16_t *cost_mv, const uint16_t *intra_cost, const uint16_t *invq, int16_t *mvs, int32_t *mv_costs,   \
+        uint16_t *lowres_costs, int32_t *row_satd, int32_t *est, void *stream )                                      \
+    {                                                                                                                \
+        return x264hip_##BD##_lowres_inter_cost_w( fenc, ffs, rf, rh, rv, rc, stride, rfs, mbw, mbh, npairs,          \
+                                                   me_method, subme, satd, me_range, mv_range, lambda, cost_mv,      \
+                                                   intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est,     \
+                                                   nullptr, 0, 0, 0, stream );                                       \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_weight_scale_plane( PT<BD>::pixel *dst, intptr_t ds, intptr_t dfs,               \
+                                                      const PT<BD>::pixel *src, intptr_t ss, intptr_t sfs,          \
+                                                      int width, int height, int nframes, int scale, int denom,     \
+                                                      int offset, void *stream )                                    \
+    {                                                                                                                \
+        if( width < 0 || height < 0 || nframes < 0 || denom < 0 || denom > 7 || scale < -128 || scale > 127 ||      \
+            offset < -128 || offset > 127 ||                                                                         \
+            ( (int64_t)width * height * nframes > 0 && ( !dst || !src || dst == src ) ) )                            \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_weight_plane<BD>( dst, ds, dfs, src, ss, sfs, width, height, nframes, scale, denom,  \
+                                                 offset, (hipStream_t)stream ),                                      \
+                        "weight_scale_plane" );                                                                      \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_lowres_bidir_cost(                                                               \
         const PT<BD>::pixel *fenc, intptr_t ffs, const PT<BD>::pixel *af, const PT<BD>::pixel *ah,                  \

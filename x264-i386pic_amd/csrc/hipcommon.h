@@ -334,7 +334,12 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                 int mbh, int npairs, int me_method, int subme, int satd, int me_range, int mv_range,
                                 int lambda, const uint16_t *cost_mv, const uint16_t *intra_cost,
                                 const uint16_t *invq, int16_t *mvs, int32_t *mv_costs, uint16_t *lowres_costs,
-                                int32_t *row_satd, int32_t *est, hipStream_t stream );
+                                int32_t *row_satd, int32_t *est, const typename PT<BD>::pixel *ref_w, int wscale,
+                                int wdenom, int woffset, hipStream_t stream );
+template <int BD>
+hipError_t launch_weight_plane( typename PT<BD>::pixel *dst, intptr_t ds, intptr_t dfs,
+                                const typename PT<BD>::pixel *src, intptr_t ss, intptr_t sfs, int width, int height,
+                                int nframes, int scale, int denom, int offset, hipStream_t stream );
 template <int BD>
 hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs,
                                 const typename PT<BD>::pixel *const ra[4], intptr_t afs,

@@ -104,12 +104,40 @@ __device__ __forceinline__ int lr_cmp_rows( const uint32_t (&fe)[LR_NR][8 / PT<B
     return (int)lr_quad_sum( acc );
 }
 
+// mc_weight (mc.c:117-137) of one dword of packed pixels: clip( ((p*scale + rnd) >> sh) + off ),
+// rnd = 1 << (denom-1) and sh = denom when denom >= 1, else 0 and 0; off already scaled by
+// 1 << (BD-8).  8 bit in int16 pairs: |p*scale| <= 255*128 and the sum stays inside int16.
+template <int BD> __device__ __forceinline__ uint32_t lr_weight_px( uint32_t v, int sc, int rnd, int sh, int off )
+{
+    if constexpr( BD == 8 )
+    {
+        typedef short ss2 __attribute__( ( ext_vector_type( 2 ) ) );
+        const ss2 scv = (ss2)(short)sc, rv = (ss2)(short)rnd, shv = (ss2)(short)sh, ov = (ss2)(short)off;
+        auto f = [&]( uint32_t x ) {
+            ss2 r = ((__builtin_bit_cast( ss2, x ) * scv + rv) >> shv) + ov;
+            r = __builtin_elementwise_min( __builtin_elementwise_max( r, (ss2)(short)0 ), (ss2)(short)255 );
+            return __builtin_bit_cast( uint32_t, r );
+        };
+        const uint32_t lo = f( __builtin_amdgcn_perm( 0u, v, 0x0c020c00u ) );
+        const uint32_t hi = f( __builtin_amdgcn_perm( 0u, v, 0x0c030c01u ) );
+        return __builtin_amdgcn_perm( hi, lo, 0x06020400u );
+    }
+    else
+    {
+        auto f = [&]( int p ) { return (uint32_t)min( max( ((p * sc + rnd) >> sh) + off, 0 ), 1023 ); };
+        return f( (int)(v & 0xffff) ) | (f( (int)(v >> 16) ) << 16);
+    }
+}
+
 template <int BD> struct LrCtx
 {
     using pixel = typename PT<BD>::pixel;
     static constexpr int NDW = 8 / PT<BD>::PPD;
     const uint32_t (&fe)[LR_NR][NDW];       // this lane's fenc rows (packed pixels), shared by the lists
     const pixel *p0, *p1, *p2, *p3;         // reference F, H, V, C at the block, row 2q
+    const pixel *pw;                        // p_fref_w: the weighted F plane (p0 when unweighted)
+    int wsc, wrnd, wsh, woff;               // m->weight (mc_weight terms)
+    bool wgt;
     intptr_t stride;
     const uint16_t *cmx, *cmy;              // p_cost_mvx / p_cost_mvy (cost_mv - mvp)
     int satd, q;
@@ -131,6 +159,9 @@ template <int BD> struct LrCtx
         p1 = r1 + off;
         p2 = r2 + off;
         p3 = r3 + off;
+        pw = p0;
+        wgt = false;
+        wsc = wrnd = wsh = woff = 0;
         stride = s;
         satd = use_satd;
         smin0 = max( 4 * (-8 * x - 12), -mvr );
@@ -143,10 +174,22 @@ template <int BD> struct LrCtx
         fmax1 = smax1 >> 2;
     }
 
-    // fpelcmp (SAD) at a full-pel offset of the F plane
+    // the weighted-reference form (slicetype.c:609-614): the integer stage on the weighted
+    // F plane rw, the subpel get_refs weighted by (scale, denom, offset)
+    __device__ __forceinline__ void set_weight( const pixel *rw, intptr_t off, int scale, int denom, int offset )
+    {
+        pw = rw + off + (intptr_t)(LR_NR * q) * stride;
+        wgt = true;
+        wsc = scale;
+        wrnd = denom >= 1 ? 1 << (denom - 1) : 0;
+        wsh = denom >= 1 ? denom : 0;
+        woff = offset * (1 << (BD - 8));
+    }
+
+    // fpelcmp (SAD) at a full-pel offset of p_fref_w (me.c:63-70)
     __device__ __forceinline__ int fpel( int mx, int my ) const
     {
-        const pixel *r = p0 + (intptr_t)my * stride + mx;
+        const pixel *r = pw + (intptr_t)my * stride + mx;
         uint32_t acc = 0;
 #pragma unroll
         for( int y = 0; y < LR_NR; y++ )
@@ -169,7 +212,7 @@ template <int BD> struct LrCtx
     static constexpr int WR = LR_NR + 4, WD = 12 / PT<BD>::PPD;
     __device__ __forceinline__ void win( int cx, int cy, uint32_t (&w)[WR][WD] ) const
     {
-        const uintptr_t a = (uintptr_t)(p0 + (intptr_t)(cy - 2) * stride + (cx - 2));
+        const uintptr_t a = (uintptr_t)(pw + (intptr_t)(cy - 2) * stride + (cx - 2));
         const uint32_t sh = (uint32_t)(a & 3);
         const uint8_t *b = (const uint8_t *)(a & ~(uintptr_t)3);
         const intptr_t sb = stride * (intptr_t)sizeof( pixel );
@@ -207,7 +250,8 @@ template <int BD> struct LrCtx
         return (int)lr_quad_sum( acc );
     }
 
-    // get_ref (mc.c:221-249) rows at a quarter-pel mv
+    // get_ref (mc.c:221-249) rows at a quarter-pel mv, weighted by m->weight when W and set
+    template <bool W = true>
     __device__ __forceinline__ void ref_rows( int mx, int my, uint32_t (&r)[LR_NR][NDW] ) const
     {
         const int idx = ((my & 3) << 2) + (mx & 3);
@@ -225,6 +269,14 @@ template <int BD> struct LrCtx
             for( int k = 0; k < NDW; k++ )
                 r[y][k] = avg_round<BD>( a[k], b[k] );
         }
+        if( W && wgt )
+        {
+#pragma unroll
+            for( int y = 0; y < LR_NR; y++ )
+#pragma unroll
+                for( int k = 0; k < NDW; k++ )
+                    r[y][k] = lr_weight_px<BD>( r[y][k], wsc, wrnd, wsh, woff );
+        }
     }
 
     // hpel plane rows addressed directly (TRY_BIDIR for subme <= 1, slicetype.c:594-600)
@@ -237,11 +289,12 @@ template <int BD> struct LrCtx
             load_row_u<NDW>( s + (intptr_t)y * stride, r[y] );
     }
 
-    // get_ref at a quarter-pel mv, then SAD or SATD 8x8
+    // get_ref at a quarter-pel mv, then SAD or SATD 8x8 (W = false: the unweighted planes)
+    template <bool W = true>
     __device__ __forceinline__ int qpel( int mx, int my, bool use_satd ) const
     {
         uint32_t r[LR_NR][NDW];
-        ref_rows( mx, my, r );
+        ref_rows<W>( mx, my, r );
         return lr_cmp_rows<BD>( fe, r, use_satd, q );
     }
 
@@ -636,8 +689,9 @@ __device__ __forceinline__ int lr_list( LrCtx<BD> &m, const uint32_t (&pred)[4],
     bool skip = false;
     if( !mvpx && !mvpy )
     {
-        // fast skip of near-zero residual blocks (slicetype.c:677-686)
-        cost = m.qpel( 0, 0, m.satd );
+        // fast skip of near-zero residual blocks (slicetype.c:677-686): m[l].p_fref[0], the
+        // unweighted F plane, even in the weighted form
+        cost = m.template qpel<false>( 0, 0, m.satd );
         skip = cost < 64;
     }
     if( !skip )
@@ -768,7 +822,7 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     int lambda, const uint16_t *__restrict__ cost_mv, const uint16_t *__restrict__ intra_cost,
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
     uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands, int brows,
-    int poll_max, uint32_t *status )
+    int poll_max, uint32_t *status, const typename PT<BD>::pixel *rw, int wscale, int wdenom, int woffset )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring[4 * LR_BAND];            // packed MVs of each band row's 4 latest blocks
@@ -783,6 +837,8 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     r1 += (intptr_t)f * rfs;
     r2 += (intptr_t)f * rfs;
     r3 += (intptr_t)f * rfs;
+    if( rw )
+        rw += (intptr_t)f * rfs;
     intra_cost += (intptr_t)f * nmb;
     if( invq )
         invq += (intptr_t)f * nmb;
@@ -824,6 +880,8 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
             LrCtx<BD> m( fe );
             m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd, q );
+            if( rw )
+                m.set_weight( rw, off, wscale, wdenom, woffset );
             uint32_t pred[4];
             const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred, poll_max, status );
             // the lanes of the band share candidate batches: a failed wait stops them all
@@ -1239,7 +1297,8 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                 int mbh, int npairs, int me_method, int subme, int satd, int me_range, int mv_range,
                                 int lambda, const uint16_t *cost_mv, const uint16_t *intra_cost,
                                 const uint16_t *invq, int16_t *mvs, int32_t *mv_costs, uint16_t *lowres_costs,
-                                int32_t *row_satd, int32_t *est, hipStream_t stream )
+                                int32_t *row_satd, int32_t *est, const typename PT<BD>::pixel *ref_w, int wscale,
+                                int wdenom, int woffset, hipStream_t stream )
 {
     if( npairs <= 0 || mbw <= 0 || mbh <= 0 )
         return hipSuccess;
@@ -1268,7 +1327,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ref[0],
                         ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
                         lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4,
-                        la_poll_max(), status );
+                        la_poll_max(), status, ref_w, wscale, wdenom, woffset );
     if( (e = hipGetLastError()) != hipSuccess )
         return e;
     return la_status_end( stream );
@@ -1278,7 +1337,8 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     template hipError_t launch_lowres_inter<BD>( const PT<BD>::pixel *, intptr_t, const PT<BD>::pixel *const[4], \
                                                  intptr_t, intptr_t, int, int, int, int, int, int, int, int, int, \
                                                  const uint16_t *, const uint16_t *, const uint16_t *, int16_t *, \
-                                                 int32_t *, uint16_t *, int32_t *, int32_t *, hipStream_t );
+                                                 int32_t *, uint16_t *, int32_t *, int32_t *,                     \
+                                                 const PT<BD>::pixel *, int, int, int, hipStream_t );
 INST( 8 )
 INST( 10 )
 #undef INST

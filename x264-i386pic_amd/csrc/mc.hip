@@ -1615,6 +1615,55 @@ __global__ __launch_bounds__( 256 ) void upload_kernel( uint8_t *__restrict__ ds
         dst[t] = src[t];
 }
 
+// x264_weight_scale_plane (frame.c:825-842) / mc_weight (mc.c:117-137): the weighted copy
+// of a plane region for the lookahead's weighted-reference search (slicetype.c:490-499).
+// Columns [0, cov) of every row, cov = the reference's strip coverage (16-wide blocks while
+// x < width-8, then one 8-wide block: up to 7 columns past width); one lane per 4 pixels.
+template <int BD>
+__global__ __launch_bounds__( 256 ) void weight_plane_kernel( typename PT<BD>::pixel *__restrict__ dst, intptr_t ds,
+                                                              intptr_t dfs, const typename PT<BD>::pixel *__restrict__ src,
+                                                              intptr_t ss, intptr_t sfs, int cov, int height, int scale,
+                                                              int rnd, int sh, int off )
+{
+    const int x = 4 * (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    const int y = (int)blockIdx.y;
+    if( x >= cov )
+        return;
+    const typename PT<BD>::pixel *s = src + (intptr_t)blockIdx.z * sfs + (intptr_t)y * ss + x;
+    typename PT<BD>::pixel *d = dst + (intptr_t)blockIdx.z * dfs + (intptr_t)y * ds + x;
+    constexpr int PMAX = (1 << BD) - 1;
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+        if( x + k < cov )
+            d[k] = (typename PT<BD>::pixel)min( max( (((int)s[k] * scale + rnd) >> sh) + off, 0 ), PMAX );
+}
+
+template <int BD>
+hipError_t launch_weight_plane( typename PT<BD>::pixel *dst, intptr_t ds, intptr_t dfs,
+                                const typename PT<BD>::pixel *src, intptr_t ss, intptr_t sfs, int width, int height,
+                                int nframes, int scale, int denom, int offset, hipStream_t stream )
+{
+    if( width <= 0 || height <= 0 || nframes <= 0 )
+        return hipSuccess;
+    int cov = 0;
+    while( cov < width - 8 )
+        cov += 16;
+    if( cov < width )
+        cov += 8;
+    if( height > 65535 || nframes > 65535 )
+        return hipErrorInvalidValue;
+    const int rnd = denom >= 1 ? 1 << (denom - 1) : 0, sh = denom >= 1 ? denom : 0;
+    hipLaunchKernelGGL( weight_plane_kernel<BD>, dim3( (unsigned)((cov + 1023) / 1024), (unsigned)height,
+                                                       (unsigned)nframes ),
+                        dim3( 256 ), 0, stream, dst, ds, dfs, src, ss, sfs, cov, height, scale, rnd, sh,
+                        offset * (1 << (BD - 8)) );
+    return hipGetLastError();
+}
+template hipError_t launch_weight_plane<8>( uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
+                                            int, int, int, int, int, hipStream_t );
+template hipError_t launch_weight_plane<10>( uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
+                                             int, int, int, int, int, int, hipStream_t );
+
 hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t stream )
 {
     if( !bytes )
