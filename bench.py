@@ -281,7 +281,7 @@ def main():
 
     if not a.no_extra:
         XF = min(a.xframes, F)
-        out["extra"] = extra_rates(x, a, world, dev[:XF + 1], origin, stride, fstride, mbw, mbh, XF)
+        out["extra"] = extra_rates(x, a, world, dev[:XF + 1], origin, stride, fstride, mbw, mbh, XF, full=dev)
         # the headline kernel again after the extra legs have kept the GPU busy for tens of
         # seconds: its steady-state launch time and roofline fraction, reported beside (never
         # instead of) the timed region above, which starts after only --warmup launches
@@ -297,7 +297,7 @@ def main():
         dist.destroy_process_group()
 
 
-def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
+def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=None):
     """configs[2] side rates on the same frames: SATD 8x8 candidates/s and fused
     DCT+quant blocks/s (QP 26, flat16 CQM, inter-luma lists, zero-MV prediction)."""
     res = {}
@@ -500,7 +500,12 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
         raise SystemExit("bench: subpel_qpel9_batch and subpel_cmp_batch disagree")
     del nb8, hv, ref_planes, fo, qxy, sc, bfo, cxy, sc9, lst
     res.update(rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
+    # plane SSD is a streaming reduction: timed at the streaming kernels' >= 64 frames per
+    # launch when the headline batch holds them, and at F beside it
     res.update(rates_ssd(x, a, world, dev, origin, stride, F))
+    if full is not None and full.shape[0] - 1 >= a.tframes:
+        r64 = rates_ssd(x, a, world, full[:a.tframes + 1], origin, stride, a.tframes)
+        res.update({k.replace("ssd_plane", "ssd_plane_%d" % a.tframes): v for k, v in r64.items()})
     res.update(rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
     res.update(rates_2160p(x, a, world))
@@ -707,13 +712,18 @@ def rates_2160p(x, a, world):
     wall, ev_ms = timed(resident, a.steps, min(a.warmup, 50), world)
     res = {"2160p_resident_candidates_per_s": world * a.steps * cand / wall,
            "2160p_resident_frame_ms": wall / a.steps * 1e3}
-    copy = torch.cuda.Stream()
+    # sdma: the runtime's copy engine on a plain side stream; kernel: x264hip_upload on the
+    # copy stream of a CU-partitioned pair (x264hip_stream_pair_create: 16 CUs for the copy,
+    # the other 240 for the search), so the upload's workgroups never wait for CU slots
+    normal = (torch.cuda.current_stream(), torch.cuda.Stream())
+    split = x.stream_pair(16)
     done = [torch.cuda.Event() for _ in range(3)]
     ready = [torch.cuda.Event() for _ in range(3)]
-    state = {"n": 0, "how": "sdma"}
+    state = {"n": 0, "how": "sdma", "streams": normal}
 
     def streaming():
         n = state["n"]
+        comp, copy = state["streams"]
         cur, ref = (n + 1) % 3, n % 3
         with torch.cuda.stream(copy):                 # upload frame n+1 while frame n-1's kernels may still run
             copy.wait_event(done[cur])
@@ -722,27 +732,53 @@ def rates_2160p(x, a, world):
             else:                                     # x264hip_upload: a kernel reading the pinned pages
                 x.upload(ring[cur], host[(n + 1) % (nf + 1)])
             ready[cur].record(copy)
-        torch.cuda.current_stream().wait_event(ready[cur])
-        torch.cuda.current_stream().wait_event(ready[ref])
-        work(ring[cur:cur + 1], ring[ref:ref + 1], c_fs=0, r_fs=0)
-        done[ref].record()
+        with torch.cuda.stream(comp):
+            comp.wait_event(ready[cur])
+            comp.wait_event(ready[ref])
+            work(ring[cur:cur + 1], ring[ref:ref + 1], c_fs=0, r_fs=0)
+            done[ref].record(comp)
         state["n"] = n + 1
+
+    def upload_only():
+        x.upload(ring[1], host[1])
+    # The host link is shared with the node's other GPUs and swings between runs (the same
+    # leg read 0.18-0.25 ms per frame within one process, profiles/r03e_*): the link alone
+    # and the two streaming forms are timed in interleaved rounds and each reported as the
+    # median round, so their ratio compares like with like.
+    rounds = {"upload": [], "sdma": [], "kernel": []}
+    for _ in range(5):
+        wall, _ = timed(upload_only, a.steps, min(a.warmup, 50), world)
+        rounds["upload"].append(wall / a.steps * 1e3)
+        for how, streams in (("sdma", normal), ("kernel", split)):
+            torch.cuda.synchronize()
+            state.update(n=0, how=how, streams=streams)
+            ring[0].copy_(host[0])
+            ready[0].record()
+            for ev in done:
+                ev.record()
+            wall, _ = timed(streaming, a.steps, min(a.warmup, 50), world)
+            torch.cuda.synchronize()
+            rounds[how].append(wall / a.steps * 1e3)
+    med = {k: float(np.median(v)) for k, v in rounds.items()}
+    res["2160p_upload_only_ms"] = med["upload"]
+    res["2160p_upload_only_GBps"] = fsz / (med["upload"] * 1e-3) / 1e9
+    res["2160p_stream_rounds_ms"] = {k: [round(t, 4) for t in v] for k, v in rounds.items()}
     for how in ("sdma", "kernel"):
-        torch.cuda.synchronize()
-        state.update(n=0, how=how)
-        ring[0].copy_(host[0])
-        ready[0].record()
-        for ev in done:
-            ev.record()
-        wall, _ = timed(streaming, a.steps, min(a.warmup, 50), world)
-        torch.cuda.synchronize()
-        res[f"2160p_pcie_{how}_candidates_per_s"] = world * a.steps * cand / wall
-        res[f"2160p_pcie_{how}_frame_ms"] = wall / a.steps * 1e3
+        res[f"2160p_pcie_{how}_candidates_per_s"] = world * cand / (med[how] * 1e-3)
+        res[f"2160p_pcie_{how}_frame_ms"] = med[how]
+    # host time to enqueue one frame (no GPU wait inside streaming()): a leg whose host side
+    # were slower than its GPU side would measure Python, not the link
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        streaming()
+    res["2160p_pcie_kernel_host_enqueue_ms"] = (time.perf_counter() - t0) / a.steps * 1e3
+    torch.cuda.synchronize()
     best = max(("sdma", "kernel"), key=lambda h: res[f"2160p_pcie_{h}_candidates_per_s"])
     res["2160p_pcie_inclusive_candidates_per_s"] = res[f"2160p_pcie_{best}_candidates_per_s"]
     res["2160p_pcie_inclusive_frame_ms"] = res[f"2160p_pcie_{best}_frame_ms"]
     res["2160p_pcie_inclusive_upload"] = best
     res["2160p_upload_bytes_per_frame"] = int(fsz)
+    res["2160p_pcie_inclusive_vs_upload_only"] = res["2160p_pcie_inclusive_frame_ms"] / res["2160p_upload_only_ms"]
     del dev_all, ring, table, host
     return res
 
@@ -790,6 +826,14 @@ def cpu_baseline(planes, origin, stride, mbw, mbh, R, seconds):
     me_rate, me_calls, me_used, me_dt = bounded(
         lambda: orc.me_search_full_mt(fenc, origin, stride, ref, origin, stride, mbw, mbh, R, nthr)[1],
         mbw * mbh * cand_per_mb)
+    # every CPU the process may run on (1 thread and nproc threads); on the GPU
+    # box that is the whole host's count, of which the job's cgroup grants a share
+    if share > nthr:
+        res["all_cpus_candidates_per_s"], _, res["all_cpus_threads"], _ = bounded(
+            lambda: orc.me_search_full_mt(fenc, origin, stride, ref, origin, stride, mbw, mbh, R, share)[1],
+            mbw * mbh * cand_per_mb)
+    else:
+        res["all_cpus_candidates_per_s"], res["all_cpus_threads"] = me_rate, me_used
     band = 4                                          # one thread: 4 MB rows per call keeps the leg bounded
     res["single_thread_candidates_per_s"] = bounded(
         lambda: orc.me_search_full_mt(fenc, origin, stride, ref, origin, stride, mbw, band, R, 1)[1],

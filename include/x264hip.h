@@ -342,6 +342,12 @@ int  x264hip_forward_ref( void *dst, int dst_device, const void *src, int src_de
  * form of configs[3] (H2D per frame overlapped with compute).
  * Asynchronous; the host buffer must stay untouched until `stream` passes it. */
 int  x264hip_upload( void *dst, const void *host_src, size_t bytes, void *stream );
+/* A compute / copy stream pair on complementary CU sets of the current device: *copy on
+ * the first reserve_cus CUs, *compute on the others (hipExtStreamCreateWithCUMask), for
+ * overlapping x264hip_upload of the next frame with the current frame's kernels.
+ * x264hip_stream_destroy releases either. */
+int  x264hip_stream_pair_create( int reserve_cus, void **compute, void **copy );
+int  x264hip_stream_destroy( void *stream );
 /* one line naming the device and the table entries the HIP backend fills (the
  * analogue of reference encoder/encoder.c:1676-1706); also printed once to
  * stderr at the first table fill unless X264HIP_QUIET=1 */

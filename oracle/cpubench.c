@@ -77,12 +77,56 @@ static int run( void *(*fn)( void * ), job_t base, int mb_height, int nthreads )
     return nthreads;
 }
 
+/* more threads than MB rows (the all-CPU leg on a many-core host): each row is cut into
+ * column segments and a thread takes a contiguous run of (row, segment) tasks; a segment's
+ * table entries land where the whole-frame call puts them (one row's MBs are contiguous) */
+typedef struct
+{
+    job_t b;
+    int t0, t1, segs, mb_height;
+} seg_job_t;
+
+static void *me_seg_worker( void *arg )
+{
+    seg_job_t *j = arg;
+    const int w = 2 * j->b.range + 1, W = j->b.mb_width;
+    for( int t = j->t0; t < j->t1; t++ )
+    {
+        const int row = t / j->segs, seg = t % j->segs;
+        const int c0 = W * seg / j->segs, c1 = W * (seg + 1) / j->segs;
+        if( c1 > c0 )
+            oracle8_me_search_full( j->b.fenc + (intptr_t)16 * row * j->b.fs + 16 * c0, j->b.fs,
+                                    j->b.ref + (intptr_t)16 * row * j->b.rs + 16 * c0, j->b.rs, c1 - c0, 1,
+                                    j->b.range, j->b.table + ((size_t)row * W + c0) * w * w );
+    }
+    return NULL;
+}
+
 /* full-search SAD tables of mb rows [0, mb_height), 8-bit; returns threads used */
 int oracle8_me_search_full_mt( const uint8_t *fenc, intptr_t fs, const uint8_t *ref, intptr_t rs,
                                int mb_width, int mb_height, int range, uint16_t *table, int nthreads )
 {
     job_t b = { fenc, ref, fs, rs, mb_width, 0, 0, range, 0, NULL, NULL, table, NULL, NULL };
-    return run( me_worker, b, mb_height, nthreads );
+    if( nthreads <= mb_height )
+        return run( me_worker, b, mb_height, nthreads );
+    if( nthreads > 256 )
+        nthreads = 256;
+    const int segs = (nthreads + mb_height - 1) / mb_height, tasks = segs * mb_height;
+    pthread_t th[256];
+    seg_job_t jobs[256];
+    for( int t = 0; t < nthreads; t++ )
+    {
+        jobs[t].b = b;
+        jobs[t].segs = segs;
+        jobs[t].mb_height = mb_height;
+        jobs[t].t0 = (int)((int64_t)tasks * t / nthreads);
+        jobs[t].t1 = (int)((int64_t)tasks * (t + 1) / nthreads);
+        if( pthread_create( &th[t], NULL, me_seg_worker, &jobs[t] ) )
+            return -1;
+    }
+    for( int t = 0; t < nthreads; t++ )
+        pthread_join( th[t], NULL );
+    return nthreads;
 }
 
 /* fused dct+quant over mb rows [0, mb_height), 8-bit; returns threads used */

@@ -26,7 +26,7 @@ __all__ = [
     "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
-    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane",
+    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -130,6 +130,15 @@ def upload(dst, src):
         raise ValueError("upload: needs a pinned host source and a device destination of equal size")
     _rc(lib().x264hip_upload(_c.c_void_p(dst.data_ptr()), _c.c_void_p(src.data_ptr()), nbytes, _stream()), "upload")
     return dst
+
+
+def stream_pair(reserve_cus=16):
+    """(compute, copy) torch external streams on complementary CU sets of the current device
+    (x264hip_stream_pair_create): the copy stream owns the first `reserve_cus` CUs."""
+    import torch
+    a, b = _c.c_void_p(), _c.c_void_p()
+    _rc(lib().x264hip_stream_pair_create(reserve_cus, _c.byref(a), _c.byref(b)), "stream_pair_create")
+    return torch.cuda.ExternalStream(a.value), torch.cuda.ExternalStream(b.value)
 
 
 # ----------------------------------------------------------------- tables
@@ -286,6 +295,10 @@ def _declare(L):
     L.x264hip_forward_ref.restype = _c.c_int
     L.x264hip_upload.argtypes = [_P, _P, _c.c_size_t, _P]
     L.x264hip_upload.restype = _c.c_int
+    L.x264hip_stream_pair_create.argtypes = [_c.c_int, _P, _P]
+    L.x264hip_stream_pair_create.restype = _c.c_int
+    L.x264hip_stream_destroy.argtypes = [_P]
+    L.x264hip_stream_destroy.restype = _c.c_int
     L.x264hip_backend_banner.restype = _c.c_char_p
     L.x264hip_set_variant.argtypes = [_c.c_char_p, _c.c_int]
     L.x264hip_set_variant.restype = _c.c_int

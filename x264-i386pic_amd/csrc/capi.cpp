@@ -156,6 +156,52 @@ extern "C" int x264hip_upload( void *dst, const void *host_src, size_t bytes, vo
     return e == hipSuccess ? X264HIP_OK : set_err( e, "upload" );
 }
 
+// Two streams on complementary CU sets of the current device (hipExtStreamCreateWithCUMask):
+// `copy` on the first `reserve_cus` CUs, `compute` on the rest.  The frame-streaming
+// pipeline of configs[3] runs the PCIe-read upload of frame n+1 on `copy` while frame n's
+// search runs on `compute`: without the split the upload's workgroups wait for CU slots the
+// full-search kernel holds (0.188 vs 0.169 ms per 2160p frame, profiles/r03b_stream_probe.json).
+extern "C" int x264hip_stream_pair_create( int reserve_cus, void **compute, void **copy )
+{
+    if( !compute || !copy || reserve_cus < 1 )
+        return X264HIP_EINVAL;
+    int dev = 0;
+    hipError_t e = hipGetDevice( &dev );
+    hipDeviceProp_t prop;
+    if( e == hipSuccess )
+        e = hipGetDeviceProperties( &prop, dev );
+    if( e != hipSuccess )
+        return set_err( e, "stream_pair_create" );
+    const int ncu = prop.multiProcessorCount;
+    if( reserve_cus >= ncu || ncu > 1024 )
+        return X264HIP_EINVAL;
+    uint32_t a[32] = { 0 }, b[32] = { 0 };
+    const int nw = (ncu + 31) / 32;
+    for( int i = 0; i < ncu; i++ )
+        (i < reserve_cus ? b : a)[i >> 5] |= 1u << (i & 31);
+    hipStream_t sc = nullptr, sk = nullptr;
+    e = hipExtStreamCreateWithCUMask( &sc, (uint32_t)nw, a );
+    if( e == hipSuccess )
+        e = hipExtStreamCreateWithCUMask( &sk, (uint32_t)nw, b );
+    if( e != hipSuccess )
+    {
+        if( sc )
+            (void)hipStreamDestroy( sc );
+        return set_err( e, "hipExtStreamCreateWithCUMask" );
+    }
+    *compute = sc;
+    *copy = sk;
+    return X264HIP_OK;
+}
+
+extern "C" int x264hip_stream_destroy( void *stream )
+{
+    if( !stream )
+        return X264HIP_OK;
+    hipError_t e = hipStreamDestroy( (hipStream_t)stream );
+    return e == hipSuccess ? X264HIP_OK : set_err( e, "hipStreamDestroy" );
+}
+
 [[noreturn]] static void fatal( hipError_t e, const char *where )
 {
     fprintf( stderr, "x264hip: fatal HIP error in %s: %s\n", where, hipGetErrorString( e ) );
@@ -175,7 +221,7 @@ static const char *const k_variant_env[V_COUNT] = {
     "X264HIP_ME_VARIANT", "X264HIP_HPEL_VARIANT", "X264HIP_HPEL_ROWS", "X264HIP_SUBPEL_VARIANT",
     "X264HIP_LOWRES_VARIANT", "X264HIP_DQ_VARIANT", "X264HIP_RECON_VARIANT", "X264HIP_LOWRES_INTRA_VARIANT",
     "X264HIP_LOOKAHEAD_BAND", "X264HIP_ME_LEAD", "X264HIP_TESA_VARIANT",
-    "X264HIP_INTEGRAL_VARIANT", "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS" };
+    "X264HIP_INTEGRAL_VARIANT", "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS", "X264HIP_ME_XCD", "X264HIP_STREAM_XCD" };
 
 struct VariantTable
 {

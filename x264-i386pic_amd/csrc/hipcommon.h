@@ -196,9 +196,37 @@ template <int BD> __device__ __forceinline__ int upix( uint32_t w, int k )
 namespace x264hip {
 enum VariantSlot
 {
-    V_ME = 0, V_HPEL, V_HPEL_ROWS, V_SUBPEL, V_LOWRES, V_DQ, V_RECON, V_LOWRES_INTRA, V_LA_BAND, V_ME_LEAD, V_TESA, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_COUNT
+    V_ME = 0, V_HPEL, V_HPEL_ROWS, V_SUBPEL, V_LOWRES, V_DQ, V_RECON, V_LOWRES_INTRA, V_LA_BAND, V_ME_LEAD, V_TESA, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_COUNT
 };
 int variant( VariantSlot slot );
+
+// Workgroup index remap that gives each XCD a contiguous range of logical workgroups:
+// the dispatcher deals blocks round-robin over the 8 XCDs (MI355X_MICROARCH.md, workgroup
+// dispatch; observed, for speed only), so block b runs on XCD b % 8.  Logical block
+// L(b) = start of XCD b%8's range + b/8, a bijection on [0, nblocks); neighbouring logical
+// blocks (neighbouring MBs, whose search windows overlap) then share one XCD's L2.
+__device__ __forceinline__ uint32_t xcd_block( uint32_t b, uint32_t nblocks )
+{
+    const uint32_t q = nblocks >> 3, r = nblocks & 7, x = b & 7, i = b >> 3;
+    return x < r ? x * (q + 1) + i : r * (q + 1) + (x - r) * q + i;
+}
+
+// the 3-D form: the grid's blocks in dispatch order (x fastest, then y, then z) remapped by
+// xcd_block when `xcd`, returned as (x, y, z) block coordinates
+struct Blk3
+{
+    uint32_t x, y, z;
+};
+__device__ __forceinline__ Blk3 blk3( bool xcd )
+{
+    if( !xcd )
+        return { blockIdx.x, blockIdx.y, blockIdx.z };
+    const uint32_t gx = gridDim.x, gy = gridDim.y;
+    const uint32_t lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    const uint32_t l = xcd_block( lin, gx * gy * gridDim.z );
+    const uint32_t yz = l / gx;
+    return { l - yz * gx, yz % gy, yz / gy };
+}
 } // namespace x264hip
 
 // ---- launchers implemented in the .hip files (all enqueue on `stream`) ----

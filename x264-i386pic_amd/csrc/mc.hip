@@ -378,11 +378,11 @@ template <int HS_ROWS, bool PK>
 __device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
                                                   uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
                                                   intptr_t stride, intptr_t fstride, int width, int height,
-                                                  int hbias, int cbias )
+                                                  int hbias, int cbias, Blk3 B, int nstrips )
 {
     const int lane = threadIdx.x & 63;
     const int nq = (width + 32) >> 4;                       // column quads over x in [-16, W+16)
-    const int chunk = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const int chunk = (int)B.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if( chunk * 62 >= nq )
         return;                                              // wave-uniform
     const int q = chunk * 62 - 1 + lane;
@@ -391,12 +391,11 @@ __device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ sr
     // strips 0 .. nstrips-1 cover rows [-8, H+8); the last four replicate row -8 into
     // rows -32..-9 / row H+7 into H+8..H+31, 12 rows each, so no wave stores more
     // rows than a strip does (a wave storing all 25 border rows was the launch's tail)
-    const int nstrips = (int)gridDim.y - 4;
-    const int sy = (int)blockIdx.y - nstrips;               // >= 0: border strip
-    const int r0 = sy < 0 ? -8 + (int)blockIdx.y * HS_ROWS : sy < 2 ? -8 : height + 7;
+    const int sy = (int)B.y - nstrips;                      // >= 0: border strip
+    const int r0 = sy < 0 ? -8 + (int)B.y * HS_ROWS : sy < 2 ? -8 : height + 7;
     const int r1 = sy < 0 ? min( r0 + HS_ROWS, height + 8 ) : r0 + 1;
     const int b0 = sy < 0 ? 0 : sy < 2 ? -32 + 12 * sy : height + 8 + 12 * (sy - 2);
-    const intptr_t fo = (intptr_t)blockIdx.z * fstride + x0;
+    const intptr_t fo = (intptr_t)B.z * fstride + x0;
     const uint8_t *sp = src + fo;
     auto ld = [&]( int row ) { return *(const uint4 *)(sp + (intptr_t)row * stride); };
     auto unpack = [&]( uint4 d, hs2 (&P)[11] ) {
@@ -543,18 +542,38 @@ template <int HS_ROWS, bool PK>
 __global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
                                                              uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
                                                              intptr_t stride, intptr_t fstride, int width,
-                                                             int height, int hbias, int cbias )
+                                                             int height, int hbias, int cbias, int xcd )
 {
-    hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias );
+    hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias, blk3( xcd ),
+                                   (int)gridDim.y - 4 );
+}
+
+// persistent form (variant 6): a resident grid of single-wave workgroups walks the
+// (chunk, strip, frame) units grid-stride, so waves drift out of the launch's lockstep and
+// one wave's loads overlap another's arithmetic and stores
+template <int HS_ROWS, bool PK>
+__global__ __launch_bounds__( 64 ) void hpel_persist_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
+                                                              uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                              intptr_t stride, intptr_t fstride, int width,
+                                                              int height, int hbias, int cbias, uint32_t gx,
+                                                              uint32_t gy, uint32_t units )
+{
+    for( uint32_t u = blockIdx.x; u < units; u += gridDim.x )
+    {
+        const uint32_t yz = u / gx;
+        hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias,
+                                       Blk3{ u - yz * gx, yz % gy, yz / gy }, (int)gy - 4 );
+    }
 }
 
 // the same kernel under a 4-waves-per-SIMD register budget (<= 128 VGPRs; variants 4 / 5)
 template <int HS_ROWS, bool PK>
 __global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void hpel_stream4_kernel(
     const uint8_t *__restrict__ src, uint8_t *__restrict__ dh, uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
-    intptr_t stride, intptr_t fstride, int width, int height, int hbias, int cbias )
+    intptr_t stride, intptr_t fstride, int width, int height, int hbias, int cbias, int xcd )
 {
-    hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias );
+    hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias, blk3( xcd ),
+                                   (int)gridDim.y - 4 );
 }
 
 template <int BD>
@@ -569,7 +588,7 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
     if constexpr( BD == 8 )
     {
         // streaming kernel: needs 16-byte aligned rows (pixel (0,0) and the strides)
-        if( var >= 2 && var <= 5 && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
+        if( var >= 2 && var <= 6 && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
                            (uintptr_t)fstride) & 15) )
         {
             const int nq = (width + 32) / 16, nchunk = (nq + 61) / 62;
@@ -582,19 +601,40 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
             const int er = variant( V_HPEL_ROWS );
             const int rows = er == 6 || er == 8 || er == 16 || er == 24 ? er : 12;
             dim3 g( nchunk, (height + 16 + rows - 1) / rows + 4, nframes );
+            // XCD-contiguous strips (adjacent strips' halo rows in one L2; X264HIP_STREAM_XCD=0
+            // turns it off): 0.0329 -> 0.0324 ms at 16 frames, 0.1514 -> 0.1499 at 64
+            // (profiles/r03i_stream_var.json; the persistent form, variant 6, was no faster)
+            const int sxcd = variant( V_STREAM_XCD ) != 0;
 #define HS_GO( ROWS )                                                                                              \
-    if( var == 3 )                                                                                                 \
+    if( var == 6 )                                                                                                 \
+    {                                                                                                              \
+        static int resident_[25] = {};                                                                             \
+        if( !resident_[ROWS] )                                                                                     \
+        {                                                                                                          \
+            int per_cu = 0, dev_ = 0, ncu_ = 0;                                                                    \
+            (void)hipGetDevice( &dev_ );                                                                           \
+            (void)hipDeviceGetAttribute( &ncu_, hipDeviceAttributeMultiprocessorCount, dev_ );                     \
+            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &per_cu, hpel_persist_kernel<ROWS, true>, 64, 0 ); \
+            resident_[ROWS] = std::max( 1, per_cu ) * std::max( 1, ncu_ );                                        \
+        }                                                                                                          \
+        const uint32_t units_ = g.x * g.y * g.z;                                                                   \
+        hipLaunchKernelGGL( ( hpel_persist_kernel<ROWS, true> ), dim3( std::min<uint32_t>( units_,                \
+                                                                                  (uint32_t)resident_[ROWS] ) ),  \
+                            dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride, width, height, 8 * 16,         \
+                            64 * 512, g.x, g.y, units_ );                                                          \
+    }                                                                                                              \
+    else if( var == 3 )                                                                                            \
         hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, \
-                            fstride, width, height, 8 * 16, 64 * 512 );                                            \
+                            fstride, width, height, 8 * 16, 64 * 512, sxcd );                                      \
     else if( var == 4 )                                                                                            \
         hipLaunchKernelGGL( ( hpel_stream4_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,       \
-                            stride, fstride, width, height, 8 * 16, 64 * 512 );                                    \
+                            stride, fstride, width, height, 8 * 16, 64 * 512, sxcd );                              \
     else if( var == 5 )                                                                                            \
         hipLaunchKernelGGL( ( hpel_stream4_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,        \
-                            stride, fstride, width, height, 8 * 16, 64 * 512 );                                    \
+                            stride, fstride, width, height, 8 * 16, 64 * 512, sxcd );                              \
     else                                                                                                           \
         hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,        \
-                            stride, fstride, width, height, 8 * 16, 64 * 512 )
+                            stride, fstride, width, height, 8 * 16, 64 * 512, sxcd )
             if( rows == 24 ) { HS_GO( 24 ); }
             else if( rows == 16 ) { HS_GO( 16 ); }
             else if( rows == 8 ) { HS_GO( 8 ); }
@@ -1396,15 +1436,13 @@ __global__ __launch_bounds__( 128 ) void lowres16_kernel( const uint8_t *__restr
 // the lanes that hold those columns: no border wave, every lane's loads for its R rows
 // independent of the other rows.
 template <int R>
-__global__ __launch_bounds__( 64 ) void lowres_rows_kernel( const uint8_t *__restrict__ src, intptr_t stride,
-                                                            intptr_t fstride, int width, int height,
-                                                            uint8_t *__restrict__ d0, uint8_t *__restrict__ dh,
-                                                            uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
-                                                            intptr_t ds, intptr_t dfs )
+__device__ __forceinline__ void lowres_rows_body( const uint8_t *__restrict__ src, intptr_t stride, intptr_t fstride,
+                                                  int width, int height, uint8_t *__restrict__ d0,
+                                                  uint8_t *__restrict__ dh, uint8_t *__restrict__ dv,
+                                                  uint8_t *__restrict__ dc, intptr_t ds, intptr_t dfs, int by, int f )
 {
     constexpr int PAD = 32;
     const int wl = width / 2, hl = height / 2;
-    const int f = blockIdx.z;
     const uint8_t *s = src + f * fstride;
     const int nfull = wl / 16;
     const int nrem = (wl - 16 * nfull + 3) / 4;               // clamped groups of 4 columns
@@ -1415,7 +1453,7 @@ __global__ __launch_bounds__( 64 ) void lowres_rows_kernel( const uint8_t *__res
 #pragma unroll
         for( int rr = 0; rr < R; rr++ )
         {
-            const int y = (int)blockIdx.y * R + rr - PAD;
+            const int y = by * R + rr - PAD;
             const bool live = y < hl + PAD;
             const int yc = min( max( y, 0 ), hl - 1 );
             const uint8_t *r0 = s + (intptr_t)(2 * yc) * stride;
@@ -1523,6 +1561,31 @@ __global__ __launch_bounds__( 64 ) void lowres_rows_kernel( const uint8_t *__res
     }
 }
 
+template <int R>
+__global__ __launch_bounds__( 64 ) void lowres_rows_kernel( const uint8_t *__restrict__ src, intptr_t stride,
+                                                            intptr_t fstride, int width, int height,
+                                                            uint8_t *__restrict__ d0, uint8_t *__restrict__ dh,
+                                                            uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                            intptr_t ds, intptr_t dfs, int xcd )
+{
+    const Blk3 B = blk3( xcd );
+    lowres_rows_body<R>( src, stride, fstride, width, height, d0, dh, dv, dc, ds, dfs, (int)B.y, (int)B.z );
+}
+
+// persistent form (X264HIP_LOWRES_VARIANT=5): a resident grid walks the (row block, frame)
+// units grid-stride
+template <int R>
+__global__ __launch_bounds__( 64 ) void lowres_rows_persist_kernel( const uint8_t *__restrict__ src, intptr_t stride,
+                                                                    intptr_t fstride, int width, int height,
+                                                                    uint8_t *__restrict__ d0, uint8_t *__restrict__ dh,
+                                                                    uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                                    intptr_t ds, intptr_t dfs, uint32_t gy, uint32_t units )
+{
+    for( uint32_t u = blockIdx.x; u < units; u += gridDim.x )
+        lowres_rows_body<R>( src, stride, fstride, width, height, d0, dh, dv, dc, ds, dfs, (int)(u % gy),
+                             (int)(u / gy) );
+}
+
 template <int BD>
 hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t stride, intptr_t fstride, int width,
                                      int height, int nframes, typename PT<BD>::pixel *const dst[4], intptr_t ds,
@@ -1544,15 +1607,32 @@ hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t
             // X264HIP_LOWRES_VARIANT = 3 / 4: one / four output rows per wave (default two)
             const int R = ev == 3 ? 1 : ev == 4 ? 4 : 2;
             dim3 gr( 1, (unsigned)((hl + 64 + R - 1) / R), (unsigned)nframes );
+            if( ev == 5 )
+            {
+                static int resident = 0;
+                if( !resident )
+                {
+                    int per_cu = 0, dev = 0, ncu = 0;
+                    (void)hipGetDevice( &dev );
+                    (void)hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, dev );
+                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &per_cu, lowres_rows_persist_kernel<2>, 64, 0 );
+                    resident = std::max( 1, per_cu ) * std::max( 1, ncu );
+                }
+                const uint32_t units = gr.y * gr.z;
+                hipLaunchKernelGGL( lowres_rows_persist_kernel<2>, dim3( std::min<uint32_t>( units, (uint32_t)resident ) ),
+                                    dim3( 64 ), 0, st, src, stride, fstride, width, height, dst[0], dst[1], dst[2],
+                                    dst[3], ds, dfs, gr.y, units );
+                return hipGetLastError();
+            }
             if( R == 1 )
                 hipLaunchKernelGGL( lowres_rows_kernel<1>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
-                                    dst[0], dst[1], dst[2], dst[3], ds, dfs );
+                                    dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) == 1 );
             else if( R == 4 )
                 hipLaunchKernelGGL( lowres_rows_kernel<4>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
-                                    dst[0], dst[1], dst[2], dst[3], ds, dfs );
+                                    dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) == 1 );
             else
                 hipLaunchKernelGGL( lowres_rows_kernel<2>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
-                                    dst[0], dst[1], dst[2], dst[3], ds, dfs );
+                                    dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) == 1 );
             return hipGetLastError();
         }
         if( ev == 2 && !(al & 15) && !(width & 15) )
@@ -1671,11 +1751,12 @@ hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t 
     // 16-byte pieces need both ends 16-byte aligned; otherwise the byte path only
     const bool al = !(((uintptr_t)dst | (uintptr_t)src) & 15);
     const size_t n16 = al ? bytes / 16 : 0;
-    // 2048 workgroups: enough reads in flight to cover the PCIe round trip.
-    // X264HIP_UPLOAD_WGS caps the grid (a few CUs' worth of grid-stride workgroups leave
-    // the rest of the chip to the kernels the upload overlaps)
+    // 16 grid-stride workgroups (64 waves, 16 B x 4 loads in flight per lane: 256 KB in
+    // flight) cover the PCIe round trip: 8.68 MB in 0.156 ms = 55.5 GB/s, against 0.198 ms
+    // for one workgroup per 4 KB (profiles/r03b_stream_probe.json), and they leave the rest
+    // of the chip to the kernels the upload overlaps.  X264HIP_UPLOAD_WGS overrides the cap.
     const int wv = variant( V_UPLOAD_WGS );
-    const size_t cap = wv > 0 ? (size_t)wv : 2048;
+    const size_t cap = wv > 0 ? (size_t)wv : 16;
     const unsigned g = (unsigned)std::min<size_t>( cap, std::max<size_t>( 1, (n16 + 1023) / 1024 ) );
     if( !al && bytes > (size_t)g * 256 )
     {

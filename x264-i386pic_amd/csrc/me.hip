@@ -434,13 +434,14 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t 
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
                                                                   int nframes, uint16_t *__restrict__ table,
                                                                   const int16_t *__restrict__ centre,
-                                                                  int16_t *__restrict__ origin )
+                                                                  int16_t *__restrict__ origin, int xcd )
 {
     constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
     constexpr int P = 4 * G;                    // table row pitch
     // 32-bit index decomposition (the launcher keeps the lane count below 2^32): the
     // int64 divisions by mbw / mbh were ~150 VALU instructions of the prologue
-    const uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
+    const uint32_t slot = blk * blockDim.x + threadIdx.x;
     if( slot >= (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw * (uint32_t)G )
         return;
     const uint32_t mb32 = slot / G, t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
@@ -592,11 +593,11 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
                                                                   int nframes, uint32_t *__restrict__ table,
                                                                   const int16_t *__restrict__ centre,
-                                                                  int16_t *__restrict__ origin )
+                                                                  int16_t *__restrict__ origin, int xcd )
 {
     constexpr int G = (2 * R + 1 + 1) / 2;      // column pairs per MB
     constexpr int P = (2 * R + 1 + 3) / 4 * 4;
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t slot = (int64_t)(xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
     if( slot >= total )
         return;
@@ -641,6 +642,11 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
 // current row's SADs.  At 16 1080p pairs, R 16: 8 bit 0.312 -> 0.300 ms (lead 0 -> 2;
 // 3 no better), 10 bit 0.653 -> 0.617 ms; lead 1 gains little, the compiler reuses the
 // current row's registers for it and so issues it half a row late
+// X264HIP_ME_XCD (default 1): XCD-contiguous workgroup ranges (xcd_block).  Same time for
+// the VALU-bound search, 2.3x fewer HBM fetches: neighbouring MBs' overlapping windows hit
+// one XCD's L2 (FETCH_SIZE 160 -> 69 MB per 16 1080p pairs, profiles/r03c_*)
+static int me_xcd() { return variant( V_ME_XCD ) != 0; }
+
 static int me_lead()
 {
     const int v = variant( V_ME_LEAD );
@@ -654,16 +660,16 @@ static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intp
 {
     if constexpr( sizeof( P ) == 2 )
     {
-        const int lead = me_lead();
+        const int lead = me_lead(), xcd = me_xcd();
         if( lead == 1 )
             hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R, 1> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin );
+                                mbw, mbh, nframes, table, centre, origin, xcd );
         else if( lead >= 2 )
             hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin );
+                                mbw, mbh, nframes, table, centre, origin, xcd );
         else
             hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,
-                                mbh, nframes, table, centre, origin );
+                                mbh, nframes, table, centre, origin, xcd );
     }
 }
 
@@ -709,12 +715,13 @@ static void launch_v7( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intp
 {
     if constexpr( sizeof( P ) == 1 )
     {
+        const int xcd = me_xcd();
         if( me_lead() <= 1 )
             hipLaunchKernelGGL( ( me_full_sad16_v7_kernel<R, 1> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin );
+                                mbw, mbh, nframes, table, centre, origin, xcd );
         else
             hipLaunchKernelGGL( ( me_full_sad16_v7_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin );
+                                mbw, mbh, nframes, table, centre, origin, xcd );
     }
 }
 
@@ -882,7 +889,7 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
                                                                 int nframes, int me_range,
                                                                 const int16_t *__restrict__ par,
                                                                 const uint16_t *__restrict__ cost_mv,
-                                                                uint32_t *__restrict__ keys )
+                                                                uint32_t *__restrict__ keys, int xcd )
 {
     constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
     constexpr int W = 2 * R + 1;
@@ -895,7 +902,7 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
     const int tid = (int)threadIdx.x;
     const int lmb = min( tid / G, MPW - 1 );
     const int grp = tid - lmb * G;              // >= G only in the tail lanes
-    const uint32_t mbr = blockIdx.x * MPW + lmb;
+    const uint32_t mbr = (xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * MPW + lmb;
     const bool live = tid < MPW * G && mbr < nmb;
     const uint32_t mb32 = min( mbr, nmb - 1 ), t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
     const int mbx = (int)(mb32 - t32 * (uint32_t)mbw);
@@ -1112,7 +1119,8 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
     {                                                                                                             \
         if( v7 )                                                                                                  \
             hipLaunchKernelGGL( ( me_full_esa_v7_kernel<R, L <= 1 ? 1 : 2> ), g, blk, 0, stream, fenc, fs, ffs,   \
-                                ref, rs, rfs, mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );       \
+                                ref, rs, rfs, mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out,         \
+                                me_xcd() );                                                                       \
         else                                                                                                      \
             hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R, L> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,   \
                                 mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                     \
@@ -1327,8 +1335,8 @@ __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
 // chain serves two MBs.  Every per-MB value is uniform within its segment; ballots are
 // masked to the segment, scans and reductions stay inside it, and loops run while any
 // segment still needs them.
-template <int BD, int NR, int SEG, bool TAB>
-__global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
+template <int BD, int NR, int SEG, bool TAB, bool SPEC = false>
+__global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
                                                         intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
                                                         intptr_t rs, intptr_t rfs,
                                                         const uint16_t *__restrict__ integral, intptr_t ifs, int mbw,
@@ -1507,9 +1515,11 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
         }
         __builtin_amdgcn_sched_barrier( 0 );
         const int st = c % D, sb = (c + 8 / CK) % D;
+        uint32_t sr_k[CK], ads_k[CK];
 #pragma unroll
         for( int k = 0; k < CK; k++ )
         {
+            sr_k[k] = ads_k[k] = 0xFFFFFFFFu;
             const int r = CK * c + k;
             if( r >= NR )
                 break;
@@ -1529,7 +1539,55 @@ __global__ __launch_bounds__( 64 ) void me_tesa_kernel( const typename PT<BD>::p
                     sr = tesa_sad16<BD>( fl, p_fref + (min_y + r) * rs + mx, rs );
                 sr = need ? sr + (uint32_t)fpel : 0xFFFFFFFFu;
             }
-            scan_row( r, ads, sr );
+            if constexpr( TAB && SPEC )
+            {
+                sr_k[k] = sr;
+                ads_k[k] = ads;
+            }
+            else
+                scan_row( r, ads, sr );
+        }
+        if constexpr( TAB && SPEC )
+        {
+            // The row scans do not wait for the running bsad.  A lane staged a cost iff it
+            // can pass some row's threshold ((bsad0 - ycost)*17>>4, the speculative pass); a
+            // lane that passes that but not the actual (bsad - ycost)*17>>4 has
+            // s = SAD + fpel >= ads >= (b*17>>4) >= b (a SAD is at least the sum of its
+            // quadrants' |DC difference|, the ads4 value), so it can neither lower bsad nor
+            // the min( b, prefix ) an append is tested against.  Every row's prefix minimum
+            // is therefore taken over the staged costs up front, and the serial chain per
+            // row is the threshold test, the append ballot and a min.
+            uint32_t excl_k[CK], rmin_k[CK];
+            int yc_k[CK];
+#pragma unroll
+            for( int k = 0; k < CK; k++ )
+            {
+                const uint32_t incl = seg_scan_min<SEG>( sr_k[k] );
+                uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)incl, 0x138, 0xF, 0xF, false );
+                excl_k[k] = lane ? ex : 0xFFFFFFFFu;
+                rmin_k[k] = seg_lane<SEG>( incl, SEG - 1, sg );
+                yc_k[k] = ycost_of( CK * c + k );
+            }
+#pragma unroll
+            for( int k = 0; k < CK; k++ )
+            {
+                const int r = CK * c + k;
+                if( r >= NR )
+                    break;
+                const int my = min_y + r;
+                const int ycost = yc_k[k];
+                const bool rowok = r < rows && bsad > ycost;
+                const int b = bsad - ycost;
+                const bool pass = rowok && ads_k[k] < (uint32_t)(b * 17 >> 4);
+                const int bcur = (int)min( (uint32_t)b, excl_k[k] );
+                const bool app = pass && (int)sr_k[k] < (bcur * sad_thresh0 >> 3);
+                const uint64_t m = sball( app );
+                if( app )
+                    mvsads[nmvsad + rank( m )] = ent( sr_k[k] + (uint32_t)ycost, mx, my );
+                nmvsad += __popcll( m );
+                if( rmin_k[k] != 0xFFFFFFFFu )
+                    bsad = min( bsad, (int)rmin_k[k] + ycost );
+            }
         }
         __builtin_amdgcn_sched_barrier( 0 );
         if( c + 1 < NC )
@@ -1742,18 +1800,28 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     }
     // the mvsads list: at most (2*me_range+1) rows x (2*me_range+3)&~3 columns per MB
     const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
+    // X264HIP_TESA_VARIANT=2: the table scan with the prefix minimum on the bsad chain (the
+    // round-2 form) instead of the speculative row scans
+    const bool spec = variant( V_TESA ) != 2;
 #define TESA_GO( NR, SEG, T )                                                                                    \
+    if( T && spec )                                                                                              \
+        hipLaunchKernelGGL( ( me_tesa_kernel<BD, NR, SEG, T, true> ),                                            \
+                            dim3( (unsigned)((nmb + 64 / SEG - 1) / (64 / SEG)) ), dim3( 64 ),                   \
+                            (64 / SEG) * (size_t)cap * (SEG == 32 ? 4 : 8), stream, fenc, fs, ffs, ref, rs, rfs, \
+                            integral, ifs, mbw, mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost, \
+                            cost_mv, out, cap );                                                                 \
+    else                                                                                                         \
     hipLaunchKernelGGL( ( me_tesa_kernel<BD, NR, SEG, T> ), dim3( (unsigned)((nmb + 64 / SEG - 1) / (64 / SEG)) ),   \
                         dim3( 64 ), (64 / SEG) * (size_t)cap * (SEG == 32 ? 4 : 8), stream, fenc, fs, ffs, ref, rs, \
                         rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost,    \
                         cost_mv, out, cap )
     if( me_range <= 16 )
     {
-        if( table ) TESA_GO( 33, 32, true ); else TESA_GO( 33, 32, false );
+        if( table ) { TESA_GO( 33, 32, true ); } else { TESA_GO( 33, 32, false ); }
     }
     else
     {
-        if( table ) TESA_GO( 65, 64, true ); else TESA_GO( 65, 64, false );
+        if( table ) { TESA_GO( 65, 64, true ); } else { TESA_GO( 65, 64, false ); }
     }
 #undef TESA_GO
     return hipGetLastError();
