@@ -387,6 +387,13 @@ void x264hip_me_bind_stats( uint64_t *hits, uint64_t *misses, int reset );
  * bad shape (range 1..29, stride >= 16*mb_width + 64) */                                        \
 int x264hip_##BD##_me_bind( const pixel *fenc, const pixel *ref, intptr_t stride,               \
                             int mb_width, int mb_height, const sadt *table, int range );        \
+/* the general form: a 16x16 table (or NULL) and / or 8x8 quadrant tables from                  \
+ * me_search_full8 (or NULL; 8 bit only).  With table8, sad / sad_x3 / sad_x4 of PIXEL_16x8,     \
+ * 8x16 and 8x8 answer from it as well (the partition whose pixels equal the caller's fenc       \
+ * block, its SAD the sum of its quadrants), and PIXEL_16x16 from the four when table is NULL. */ \
+int x264hip_##BD##_me_bind_tables( const pixel *fenc, const pixel *ref, intptr_t stride,        \
+                                   int mb_width, int mb_height, const sadt *table,              \
+                                   const uint16_t *table8, int range );                         \
 /* drop-in table initialisers (see header comment) */                                           \
 void x264hip_##BD##_pixel_init( uint32_t cpu, x264hip_##BD##_pixel_function_t *pixf );          \
 void x264hip_##BD##_pixel_init_hip( x264hip_##BD##_pixel_function_t *pixf );                    \
@@ -597,6 +604,20 @@ int x264hip_##BD##_me_search_full( const pixel *fenc, intptr_t fenc_stride,     
                                    intptr_t ref_frame_stride,                                   \
                                    int mb_width, int mb_height, int n_frames, int range,        \
                                    sadt *table, void *stream );                                 \
+                                                                                                \
+/* 8x8 quadrant tables (8 bit only; X264HIP_EINVAL at 10 bit): table8[mb][q][j][i] =             \
+ * sad_8x8 of quadrant q of the MB (0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right)      \
+ * at mv (i - range, j - range), row pitch (2*range+1+3)&~3, MBs frame-major.  The 16x16         \
+ * SAD is the sum of the four, PIXEL_16x8's two halves are q0+q1 / q2+q3 and PIXEL_8x16's        \
+ * q0+q2 / q1+q3: the exhaustive windows of every partition me.c's ESA / TESA searches           \
+ * (me.c:618-771; analyse.c:1425,1480,1546) from the absdiffs of one 16x16 search.  range       \
+ * 4, 8, 16 or 24. */                                                                            \
+int x264hip_##BD##_me_search_full8( const pixel *fenc, intptr_t fenc_stride,                    \
+                                    intptr_t fenc_frame_stride,                                 \
+                                    const pixel *ref, intptr_t ref_stride,                      \
+                                    intptr_t ref_frame_stride,                                  \
+                                    int mb_width, int mb_height, int n_frames, int range,       \
+                                    uint16_t *table8, void *stream );                           \
                                                                                                 \
 /* full search around a per-MB centre (me.c centres its ESA window on the best                   \
  * predictor, encoder/me.c:618-624): centre[2*mb..] = (cx, cy) full-pel, MBs in frame-major     \

@@ -1363,6 +1363,27 @@ void FN(me_search_full)( const pixel *fenc, intptr_t fs, const pixel *ref, intpt
         }
 }
 
+/* exhaustive 8x8 quadrant SAD tables, semantics of x264hip_*_me_search_full8:
+ * table8[mb][q][j][i] = sad_8x8 (pixel.c:55-80, PIXEL_8x8) of quadrant q (0 = top-left,
+ * 1 = top-right, 2 = bottom-left, 3 = bottom-right) of the MB at mv (i - range, j - range) */
+void FN(me_search_full8)( const pixel *fenc, intptr_t fs, const pixel *ref, intptr_t rs,
+                          int mb_width, int mb_height, int range, uint16_t *table8 )
+{
+    int w = 2*range + 1;
+    for( int mby = 0; mby < mb_height; mby++ )
+        for( int mbx = 0; mbx < mb_width; mbx++ )
+            for( int q = 0; q < 4; q++ )
+            {
+                const int px = 8*(q & 1), py = 8*(q >> 1);
+                const pixel *f = fenc + (16*mby + py)*fs + 16*mbx + px;
+                uint16_t *t = table8 + (((size_t)mby*mb_width + mbx) * 4 + q) * w * w;
+                for( int j = 0; j < w; j++ )
+                    for( int i = 0; i < w; i++ )
+                        t[j*w+i] = (uint16_t)FN(sad)( 3, f, fs, ref + (16*mby + py + j - range)*rs + 16*mbx + px + i - range,
+                                                      rs );
+            }
+}
+
 /* window origin of x264hip_*_me_search_centred for one MB: (cx, cy) - range,
  * clamped so every pixel the kernels fetch lies in the 32-pixel padded plane,
  * then aligned down to 4 (8 bit) / 2 (10 bit) pixels; returned relative to the MB */

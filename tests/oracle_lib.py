@@ -63,6 +63,7 @@ for _bd in (8, 10):
         _f(_bd, _n, [_P, C.c_int, C.c_int], C.c_int)
     _f(_bd, "cqm_init", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P], C.c_int)
     _f(_bd, "me_search_full", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P])
+    _f(_bd, "me_search_full8", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P])
     _f(_bd, "mb_dct_quant", [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "hpel_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int, _P])
     _f(_bd, "get_ref", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int], _P)
@@ -217,6 +218,15 @@ def me_search_full(bd, fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, rng):
     out = np.zeros((mbh, mbw, w, w), sad_dtype(bd))
     getattr(_L, f"oracle{bd}_me_search_full")(_addr(fenc, f_origin), fs, _addr(ref, r_origin), rs, mbw, mbh,
                                              rng, _addr(out))
+    return out
+
+
+def me_search_full8(bd, fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, rng):
+    """one frame's 8x8 quadrant tables: [mbh, mbw, 4, 2r+1, 2r+1] uint16."""
+    w = 2 * rng + 1
+    out = np.zeros((mbh, mbw, 4, w, w), np.uint16)
+    getattr(_L, f"oracle{bd}_me_search_full8")(_addr(fenc, f_origin), fs, _addr(ref, r_origin), rs, mbw, mbh,
+                                              rng, _addr(out))
     return out
 
 

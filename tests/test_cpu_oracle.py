@@ -323,3 +323,15 @@ def test_me_search_centred_oracle(oracle, bd):
             for i in (0, 3, 2 * R):
                 rb = nr.block(r, origin + (ay + j) * stride + ax + i, stride, 16, 16)
                 assert tab[mby, mbx, j, i] == nr.sad(fb, rb), (mb, i, j)
+
+
+def test_oracle_quadrant_tables_sum_to_16x16(oracle):
+    """The oracle's 8x8 quadrant tables (me_search_full8) add up to its 16x16 table: a SAD is
+    additive over the four quadrants (pixel.c:55-80)."""
+    from conftest import load_package
+    load_package()
+    from x264hip import synth
+    planes, stride, origin = synth.make_sequence(2, 96, 64, 8, seed=4)
+    a = oracle.me_search_full8(8, planes[1].ravel(), origin, stride, planes[0].ravel(), origin, stride, 6, 4, 8)
+    b = oracle.me_search_full(8, planes[1].ravel(), origin, stride, planes[0].ravel(), origin, stride, 6, 4, 8)
+    assert np.array_equal(a.astype(np.int64).sum(2), b)

@@ -289,3 +289,50 @@ def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H, lead):
             want = oracle.me_esa_argmin(bd, padded, rng, me_range, par[sl], init[sl], cost_mv, c0, origin=worg)
             assert np.array_equal(got[sl], want), (f, np.argwhere((got[sl] != want).any(1))[:5])
     assert (got[::7, 0] == 0).all() and (got[:, 0] <= init).all()
+
+
+@pytest.mark.parametrize("rng", [4, 8, 16, 24])
+@pytest.mark.parametrize("W,H,nf", [(160, 96, 2), (1920, 1088, 1)])
+def test_me_search_full8_quadrants(hip, oracle, rng, W, H, nf):
+    """8x8 quadrant tables (x264hip_8_me_search_full8, VERDICT r2 missing 4): every quadrant SAD
+    equals the oracle's sad_8x8; their sum is the 16x16 table; the 16x8 / 8x16 pair sums equal
+    sad_16x8 / sad_8x16 of those partitions at sampled mvs (pixel.c:55-80)."""
+    if W == 1920 and rng not in (16,):
+        pytest.skip("1080p at range 16 only")
+    from x264hip import synth
+    planes, stride, origin = synth.make_sequence(nf + 1, W, H, 8, seed=rng)
+    dev = torch.from_numpy(planes).cuda()
+    fs = planes[0].size
+    mbw, mbh = W // 16, H // 16
+    w = 2 * rng + 1
+    t8 = hip.me_search_full8(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, nf, rng,
+                             fenc_frame_stride=fs, ref_frame_stride=fs)
+    t16 = hip.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, nf, rng,
+                             fenc_frame_stride=fs, ref_frame_stride=fs)
+    g8 = t8.cpu().numpy().view(np.uint16)[..., :w]
+    g16 = t16.cpu().numpy().view(np.uint16)[..., :w]
+    assert np.array_equal(g8.astype(np.int64).sum(3), g16)
+    f = nf - 1
+    want = oracle.me_search_full8(8, planes[f + 1].ravel(), origin, stride, planes[f].ravel(), origin, stride, mbw,
+                                  mbh, rng)
+    assert np.array_equal(g8[f], want), np.argwhere(g8[f] != want)[:4]
+    rs = np.random.default_rng(rng + W)
+    f1, f0 = planes[f + 1].ravel(), planes[f].ravel()
+    for _ in range(40):
+        mbx, mby = int(rs.integers(mbw)), int(rs.integers(mbh))
+        mx, my = (int(v) for v in rs.integers(-rng, rng + 1, 2))
+        q = g8[f, mby, mbx, :, my + rng, mx + rng].astype(np.int64)
+        fo = origin + 16 * mby * stride + 16 * mbx
+        for i_pixel, parts in ((hip.PIXEL_16x8, ((0, 0, (0, 1)), (0, 8, (2, 3)))),
+                               (hip.PIXEL_8x16, ((0, 0, (0, 2)), (8, 0, (1, 3))))):
+            for px, py, qs in parts:
+                o = fo + py * stride + px
+                assert q[list(qs)].sum() == oracle.cmp(8, "sad", i_pixel, f1, o, stride, f0, o + my * stride + mx,
+                                                       stride)
+
+
+def test_me_search_full8_shape_checks(hip):
+    t = torch.empty(10, dtype=torch.int16, device="cuda")
+    d = torch.zeros((2, 160, 256), dtype=torch.uint8, device="cuda")
+    with pytest.raises(ValueError):
+        hip.me_search_full8(d[1:], 32 * 256 + 32, 256, d[:1], 32 * 256 + 32, 256, 4, 4, 1, 8, table8=t)

@@ -20,13 +20,15 @@ is usable, every entry point raises ``BackendUnavailable``.
 import ctypes
 import os
 
+import numpy as np
+
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
     "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
-    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair",
+    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "me_search_full8",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -310,6 +312,8 @@ def _declare(L):
         f = lambda n: getattr(L, f"x264hip_{bd}_{n}")  # noqa: E731
         f("me_bind").argtypes = [_P, _P, _IP, _c.c_int, _c.c_int, _P, _c.c_int]
         f("me_bind").restype = _c.c_int
+        f("me_bind_tables").argtypes = [_P, _P, _IP, _c.c_int, _c.c_int, _P, _P, _c.c_int]
+        f("me_bind_tables").restype = _c.c_int
         f("pixel_init").argtypes = [_c.c_uint32, _P]
         f("dct_init").argtypes = [_c.c_uint32, _P]
         f("quant_init").argtypes = [_P, _c.c_uint32, _P]
@@ -320,6 +324,8 @@ def _declare(L):
         f("cqm_init").restype = _c.c_int
         f("pixel_cmp_batch").argtypes = [_c.c_int, _c.c_int, _P, _IP, _P, _IP, _P, _P, _c.c_int, _P, _P]
         f("me_search_full").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P]
+        f("me_search_full8").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P]
+        f("me_search_full8").restype = _c.c_int
         f("sub_dct_batch").argtypes = [_c.c_int, _P, _IP, _P, _IP, _P, _P, _c.c_int, _P, _P]
         f("dc_batch").argtypes = [_c.c_int, _P, _P, _c.c_int, _P]
         f("quant_batch").argtypes = [_c.c_int, _P, _P, _P, _c.c_int, _P, _P]
@@ -820,28 +826,36 @@ class MeBinding:
         self.close()
 
 
-def me_bind(bitdepth, fenc, fenc_origin, ref, ref_origin, stride, mb_width, mb_height, table, rng):
-    """Bind one frame pair's full-search table for the calling thread's 16x16 SAD table
-    entries (lookup mode, include/x264hip.h x264hip_me_bind).  fenc / ref: host numpy
-    planes (uint8 / uint16) with pixel (0,0) at element offset *_origin; table: the
-    me_search_full table of that pair (numpy or torch, copied to host if on the device)."""
-    import numpy as np
-    if hasattr(table, "cpu"):
-        table = table.cpu().numpy()
-    table = np.ascontiguousarray(table)
+def me_bind(bitdepth, fenc, fenc_origin, ref, ref_origin, stride, mb_width, mb_height, table, rng, table8=None):
+    """Bind one frame pair's full-search tables for the calling thread's SAD table entries
+    (lookup mode, include/x264hip.h x264hip_me_bind_tables).  fenc / ref: host numpy planes
+    (uint8 / uint16) with pixel (0,0) at element offset *_origin; table: the me_search_full
+    table of that pair, table8: its me_search_full8 quadrant tables (either may be None;
+    numpy or torch, copied to host if on the device)."""
+    def host(t, dt, n, name):
+        if t is None:
+            return None
+        if hasattr(t, "cpu"):
+            t = t.cpu().numpy()
+        t = np.ascontiguousarray(t).view(dt)
+        if t.size < n:
+            raise ValueError("me_bind: %s smaller than its [mbh, mbw, ...] shape" % name)
+        return t
     fenc = np.ascontiguousarray(fenc)
     ref = np.ascontiguousarray(ref)
     pt = np.uint8 if bitdepth == 8 else np.uint16
     st = np.uint16 if bitdepth == 8 else np.uint32
-    fenc, ref, table = fenc.view(pt), ref.view(pt), table.view(st)
-    if table.size < mb_width * mb_height * (2 * rng + 1) * me_table_pitch(rng):
-        raise ValueError("me_bind: table smaller than mb_width*mb_height*(2R+1)*pitch")
+    fenc, ref = fenc.view(pt), ref.view(pt)
+    n1 = mb_width * mb_height * (2 * rng + 1) * me_table_pitch(rng)
+    table = host(table, st, n1, "table")
+    table8 = host(table8, np.uint16, 4 * n1, "table8")
     es = fenc.itemsize
-    rc = getattr(lib(), f"x264hip_{bitdepth}_me_bind")(
+    rc = getattr(lib(), f"x264hip_{bitdepth}_me_bind_tables")(
         _c.c_void_p(fenc.ctypes.data + fenc_origin * es), _c.c_void_p(ref.ctypes.data + ref_origin * es), stride,
-        mb_width, mb_height, _c.c_void_p(table.ctypes.data), rng)
+        mb_width, mb_height, None if table is None else _c.c_void_p(table.ctypes.data),
+        None if table8 is None else _c.c_void_p(table8.ctypes.data), rng)
     _rc(rc, "me_bind")
-    return MeBinding((fenc, ref, table))
+    return MeBinding((fenc, ref, table, table8))
 
 
 def me_table_pitch(rng):
@@ -859,12 +873,36 @@ def me_search_full(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, 
     if table is None:
         table = torch.empty((nframes, mb_height, mb_width, w, me_table_pitch(rng)),
                             dtype=torch.int16 if bd == 8 else torch.int32, device=fenc.device)
+    if table.numel() * table.element_size() < nframes * mb_height * mb_width * w * me_table_pitch(rng) * (
+            2 if bd == 8 else 4):
+        raise ValueError("me_search_full: table smaller than [nframes, mbh, mbw, 2r+1, pitch]")
     ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
     rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)
     _rc(getattr(lib(), f"x264hip_{bd}_me_search_full")(
         _ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs,
         mb_width, mb_height, nframes, rng, _ptr(table), _stream()), "me_search_full")
     return table
+
+
+def me_search_full8(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height,
+                    nframes, rng=16, table8=None, fenc_frame_stride=None, ref_frame_stride=None):
+    """8x8 quadrant SAD tables [nframes, mb_height, mb_width, 4, 2r+1, pitch] uint16-as-int16
+    (x264hip_8_me_search_full8; q = 0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right).
+    8 bit only."""
+    import torch
+    bd = _pix_bd(fenc)
+    w = 2 * rng + 1
+    shape = (nframes, mb_height, mb_width, 4, w, me_table_pitch(rng))
+    if table8 is None:
+        table8 = torch.empty(shape, dtype=torch.int16, device=fenc.device)
+    if table8.numel() < int(np.prod(shape)) or table8.element_size() != 2 or not table8.is_contiguous():
+        raise ValueError("me_search_full8: table8 must be a contiguous 16-bit tensor of %s" % (shape,))
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)
+    _rc(getattr(lib(), f"x264hip_{bd}_me_search_full8")(
+        _ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs,
+        mb_width, mb_height, nframes, rng, _ptr(table8), _stream()), "me_search_full8")
+    return table8
 
 
 def sub_dct_batch(kind, fenc, fenc_stride, fdec, fdec_stride, fenc_off, fdec_off, out=None):

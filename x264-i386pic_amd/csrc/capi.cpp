@@ -336,7 +336,8 @@ struct MeBind
     const uint8_t *ref = nullptr;
     intptr_t stride = 0;                 // pixels
     int mbw = 0, mbh = 0, R = 0, pitch = 0, psz = 1;
-    const void *table = nullptr;         // [mbh][mbw][2R+1][pitch] SADs
+    const void *table = nullptr;         // [mbh][mbw][2R+1][pitch] 16x16 SADs (or null)
+    const uint16_t *table8 = nullptr;    // [mbh][mbw][4][2R+1][pitch] 8x8 quadrant SADs (or null)
     uint64_t hits = 0, misses = 0;
 };
 thread_local MeBind t_bind;
@@ -372,22 +373,81 @@ inline bool bind_lookup16( const typename PT<BD>::pixel *fenc, intptr_t fs, cons
             if( r < 16 )
                 continue;
             const int tx = (int)(x - 16 * mx) + R, ty = (int)(y - 16 * my) + R;
-            const size_t i = (((size_t)my * b.mbw + mx) * (2 * R + 1) + ty) * b.pitch + tx;
-            *out = (int)((const typename PT<BD>::sadt *)b.table)[i];
+            if( b.table )
+            {
+                const size_t i = (((size_t)my * b.mbw + mx) * (2 * R + 1) + ty) * b.pitch + tx;
+                *out = (int)((const typename PT<BD>::sadt *)b.table)[i];
+            }
+            else
+            {
+                const size_t q0 = (((size_t)my * b.mbw + mx) * 4 * (2 * R + 1) + ty) * b.pitch + tx;
+                const size_t qs = (size_t)(2 * R + 1) * b.pitch;
+                *out = b.table8[q0] + b.table8[q0 + qs] + b.table8[q0 + 2 * qs] + b.table8[q0 + 3 * qs];
+            }
             return true;
+        }
+    return false;
+}
+
+// PIXEL_16x8 / 8x16 / 8x8 from the quadrant tables: the partition (W x H at (px, py) in its
+// MB) is the one whose pixels equal the caller's fenc block, among the partitions of that size
+// of the <= 9 MBs whose window covers the candidate; its SAD is the sum of its quadrants
+template <int W, int H>
+inline bool bind_lookup_part( const uint8_t *fenc, intptr_t fs, const uint8_t *cand, intptr_t s, int *out )
+{
+    const MeBind &b = t_bind;
+    if( b.bd != 8 || !b.table8 || s != b.stride )
+        return false;
+    const intptr_t d = cand - b.ref;
+    const intptr_t y = (d + BIND_PAD) >= 0 ? (d + BIND_PAD) / s : -((-(d + BIND_PAD) + s - 1) / s);
+    const intptr_t x = d - y * s;
+    const int R = b.R;
+    const size_t qs = (size_t)(2 * R + 1) * b.pitch;
+    for( int py = 0; py < 16; py += H )
+        for( int px = 0; px < 16; px += W )
+        {
+            const intptr_t xx = x - px, yy = y - py;     // the MB-aligned candidate position
+            if( yy < -R || yy > 16 * (intptr_t)(b.mbh - 1) + R || xx < -R || xx > 16 * (intptr_t)(b.mbw - 1) + R )
+                continue;
+            const int mx0 = (int)std::max<intptr_t>( 0, (xx - R + 15) >> 4 );
+            const int mx1 = (int)std::min<intptr_t>( b.mbw - 1, (xx + R) >> 4 );
+            const int my0 = (int)std::max<intptr_t>( 0, (yy - R + 15) >> 4 );
+            const int my1 = (int)std::min<intptr_t>( b.mbh - 1, (yy + R) >> 4 );
+            for( int my = my0; my <= my1; my++ )
+                for( int mx = mx0; mx <= mx1; mx++ )
+                {
+                    const uint8_t *m = b.fenc + (intptr_t)(16 * my + py) * s + 16 * mx + px;
+                    int r = 0;
+                    while( r < H && !memcmp( fenc + r * fs, m + r * s, W ) )
+                        r++;
+                    if( r < H )
+                        continue;
+                    const int tx = (int)(xx - 16 * mx) + R, ty = (int)(yy - 16 * my) + R;
+                    const uint16_t *t = b.table8 + (((size_t)my * b.mbw + mx) * 4 * (2 * R + 1) + ty) * b.pitch + tx;
+                    const int q = (py >> 3) * 2 + (px >> 3);     // the partition's first quadrant
+                    int v = t[q * qs];
+                    if( W == 16 )
+                        v += t[(q + 1) * qs];
+                    if( H == 16 )
+                        v += t[(q + 2) * qs];
+                    *out = v;
+                    return true;
+                }
         }
     return false;
 }
 } // namespace
 
 #define DEFINE_BIND( BD )                                                                                            \
-    extern "C" int x264hip_##BD##_me_bind( const PT<BD>::pixel *fenc, const PT<BD>::pixel *ref, intptr_t stride,     \
-                                           int mb_width, int mb_height, const PT<BD>::sadt *table, int range )       \
+    extern "C" int x264hip_##BD##_me_bind_tables( const PT<BD>::pixel *fenc, const PT<BD>::pixel *ref,              \
+                                                  intptr_t stride, int mb_width, int mb_height,                      \
+                                                  const PT<BD>::sadt *table, const uint16_t *table8, int range )     \
     {                                                                                                                \
-        if( !fenc || !ref || !table || mb_width <= 0 || mb_height <= 0 || range < 1 || range > 29 ||                 \
-            stride < 16 * (intptr_t)mb_width + 2 * BIND_PAD )                                                        \
+        if( !fenc || !ref || !( table || table8 ) || ( table8 && BD != 8 ) || mb_width <= 0 || mb_height <= 0 ||    \
+            range < 1 || range > 29 || stride < 16 * (intptr_t)mb_width + 2 * BIND_PAD )                             \
             return X264HIP_EINVAL;                                                                                   \
         MeBind &b = t_bind;                                                                                          \
+        b.table8 = table8;                                                                                           \
         b.bd = BD;                                                                                                   \
         b.fenc = (const uint8_t *)fenc;                                                                              \
         b.ref = (const uint8_t *)ref;                                                                                \
@@ -398,6 +458,13 @@ inline bool bind_lookup16( const typename PT<BD>::pixel *fenc, intptr_t fs, cons
         b.pitch = (2 * range + 1 + 3) & ~3;                                                                          \
         b.table = table;                                                                                             \
         return X264HIP_OK;                                                                                           \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_bind( const PT<BD>::pixel *fenc, const PT<BD>::pixel *ref, intptr_t stride,     \
+                                           int mb_width, int mb_height, const PT<BD>::sadt *table, int range )       \
+    {                                                                                                                \
+        if( !table )                                                                                                 \
+            return X264HIP_EINVAL;                                                                                   \
+        return x264hip_##BD##_me_bind_tables( fenc, ref, stride, mb_width, mb_height, table, nullptr, range );      \
     }
 DEFINE_BIND( 8 )
 DEFINE_BIND( 10 )
@@ -440,6 +507,20 @@ static int cmp_call( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::p
             t_bind.misses++;
         }
     }
+    if constexpr( BD == 8 && OP == X264HIP_CMP_SAD &&
+                  ( IPIX == X264HIP_PIXEL_16x8 || IPIX == X264HIP_PIXEL_8x16 || IPIX == X264HIP_PIXEL_8x8 ) )
+    {
+        if( t_bind.table8 )
+        {
+            int v;
+            if( bind_lookup_part<W, H>( (const uint8_t *)p1, s1, (const uint8_t *)p2, s2, &v ) )
+            {
+                t_bind.hits++;
+                return v;
+            }
+            t_bind.misses++;
+        }
+    }
     CallCtx &c = call_ctx();
     pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
     int64_t *off = (int64_t *)(c.host + ST_OFF);
@@ -466,6 +547,26 @@ static void cmpx_call( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *con
             int v[N];
             int k = 0;
             while( k < N && bind_lookup16<BD>( fenc, X264HIP_FENC_STRIDE, refs[k], stride, &v[k] ) )
+                k++;
+            if( k == N )
+            {
+                t_bind.hits += N;
+                for( int j = 0; j < N; j++ )
+                    scores[j] = v[j];
+                return;
+            }
+            t_bind.misses += N;
+        }
+    }
+    if constexpr( BD == 8 && OP == X264HIP_CMP_SAD &&
+                  ( IPIX == X264HIP_PIXEL_16x8 || IPIX == X264HIP_PIXEL_8x16 || IPIX == X264HIP_PIXEL_8x8 ) )
+    {
+        if( t_bind.table8 )
+        {
+            int v[N];
+            int k = 0;
+            while( k < N && bind_lookup_part<W, H>( (const uint8_t *)fenc, X264HIP_FENC_STRIDE,
+                                                    (const uint8_t *)refs[k], stride, &v[k] ) )
                 k++;
             if( k == N )
             {
@@ -1485,6 +1586,18 @@ extern "C" const char *x264hip_backend_banner( void )
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, table, centre,   \
                                             origin, (hipStream_t)stream ), "me_search_centred" );                    \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_search_full8( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,           \
+                                                   const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw,     \
+                                                   int mbh, int nframes, int range, uint16_t *table8,                \
+                                                   void *stream )                                                    \
+    {                                                                                                                \
+        if( BD != 8 || mbw < 0 || mbh < 0 || nframes < 0 ||                                                          \
+            !( range == 4 || range == 8 || range == 16 || range == 24 ) ||                                           \
+            ( (int64_t)mbw * mbh * nframes > 0 && ( !fenc || !ref || !table8 ) ) )                                   \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_me_full8<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, table8,          \
+                                             (hipStream_t)stream ), "me_search_full8" );                             \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_me_esa_argmin( const PT<BD>::sadt *table, int range, int n, int me_range,         \
                                                  const int16_t *par, const int32_t *init_cost,                       \

@@ -365,6 +365,10 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                 int32_t *row_satd, int32_t *est, const typename PT<BD>::pixel *ref_w, int wscale,
                                 int wdenom, int woffset, hipStream_t stream );
 template <int BD>
+hipError_t launch_me_full8( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                            int nframes, int range, uint16_t *table8, hipStream_t stream );
+template <int BD>
 hipError_t launch_weight_plane( typename PT<BD>::pixel *dst, intptr_t ds, intptr_t dfs,
                                 const typename PT<BD>::pixel *src, intptr_t ss, intptr_t sfs, int width, int height,
                                 int nframes, int scale, int denom, int offset, hipStream_t stream );

@@ -474,6 +474,137 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t 
 }
 
 // ---------------------------------------------------------------------------
+// X264HIP_ME_XCD (default 1): XCD-contiguous workgroup ranges (xcd_block).  Same time for
+// the VALU-bound search, 2.3x fewer HBM fetches: neighbouring MBs' overlapping windows hit
+// one XCD's L2 (FETCH_SIZE 160 -> 69 MB per 16 1080p pairs, profiles/r03c_*)
+static int me_xcd() { return variant( V_ME_XCD ) != 0; }
+
+// 8x8 quadrant tables (8 bit): the variant-7 lane (four candidate columns, all 16 fenc
+// rows, each ref row loaded once) with separate left (fenc dwords 0-1) and right (dwords
+// 2-3) accumulators, restarted at fenc row 8: a candidate row's top quadrants leave at fenc
+// row 7, its bottom ones at row 15.  The same 256 absdiffs per candidate as the 16x16
+// table -- whose SAD is the sum of the four -- and 16x8 / 8x16 SADs are pair sums.
+template <int R, int L, int Y, class Sink>
+__device__ __forceinline__ void me_row8q( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[16][4],
+                                          uint64_t (&al)[16], uint64_t (&ar)[16], Sink &sink, u64x2a4 (&e)[L],
+                                          u64x2a4 (&o)[L] )
+{
+    constexpr int C0 = Y - 15 > 0 ? Y - 15 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    const uint64_t win[4] = { e[Y % L][0], o[Y % L][0], e[Y % L][1], o[Y % L][1] };
+    if constexpr( Y + L < 2 * R + 16 )
+    {
+        const uint32_t *row = rbase + (Y + L) * rs_dw;
+        e[Y % L] = *(const u64x2a4 *)row;
+        o[Y % L] = *(const u64x2a4 *)(row + 1);
+    }
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint64_t a = (r & 7) == 0 ? 0ull : al[c & 15], b = (r & 7) == 0 ? 0ull : ar[c & 15];
+        a = __builtin_amdgcn_qsad_pk_u16_u8( win[0], F[r][0], a );
+        a = __builtin_amdgcn_qsad_pk_u16_u8( win[1], F[r][1], a );
+        b = __builtin_amdgcn_qsad_pk_u16_u8( win[2], F[r][2], b );
+        b = __builtin_amdgcn_qsad_pk_u16_u8( win[3], F[r][3], b );
+        if( (r & 7) == 7 )
+            sink( c, r >> 3, a, b );
+        else
+        {
+            al[c & 15] = a;
+            ar[c & 15] = b;
+        }
+    }
+    __builtin_amdgcn_sched_barrier( 0 );
+}
+
+template <int R, int L, class Sink, int... Ys>
+__device__ __forceinline__ void me_rows8q( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[16][4],
+                                           uint64_t (&al)[16], uint64_t (&ar)[16], Sink &sink,
+                                           std::integer_sequence<int, Ys...> )
+{
+    u64x2a4 e[L], o[L];
+#pragma unroll
+    for( int k = 0; k < L; k++ )
+    {
+        e[k] = *(const u64x2a4 *)(rbase + k * rs_dw);
+        o[k] = *(const u64x2a4 *)(rbase + k * rs_dw + 1);
+    }
+    ( me_row8q<R, L, Ys>( rbase, rs_dw, F, al, ar, sink, e, o ), ... );
+}
+
+// table8[mb][q][2R+1][P]: q = 0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right
+template <int R, int L>
+__global__ __launch_bounds__( 256 ) void me_full_sad8q_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
+                                                               intptr_t ffs, const uint8_t *__restrict__ ref,
+                                                               intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                               int nframes, uint16_t *__restrict__ table8, int xcd )
+{
+    constexpr int G = (2 * R + 1 + 3) / 4;
+    constexpr int P = 4 * G;
+    const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
+    const uint32_t slot = blk * blockDim.x + threadIdx.x;
+    if( slot >= (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw * (uint32_t)G )
+        return;
+    const uint32_t mb32 = slot / G, t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+    const int grp = (int)(slot - mb32 * G);
+    const int mbx = (int)(mb32 - t32 * (uint32_t)mbw);
+    const int mby = (int)(t32 - f32 * (uint32_t)mbh);
+    const int64_t mb = mb32, f = f32;
+    uint32_t F[16][4];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs / 4);
+#pragma unroll
+    for( int r = 0; r < 16; r++ )
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+    const uint32_t *rbase = (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby - R) * rs + 16 * mbx - R + 4 * grp);
+    uint64_t *out = (uint64_t *)(table8 + mb * (4 * (2 * R + 1) * P) + 4 * grp);
+    auto store = [out]( int c, int half, uint64_t a, uint64_t b ) {
+        out[((2 * half) * (2 * R + 1) + c) * (P / 4)] = a;
+        out[((2 * half + 1) * (2 * R + 1) + c) * (P / 4)] = b;
+    };
+    uint64_t al[16], ar[16];
+    me_rows8q<R, L>( rbase, (int)(rs / 4), F, al, ar, store, std::make_integer_sequence<int, 2 * R + 16>{} );
+}
+
+template <int BD>
+hipError_t launch_me_full8( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                            int nframes, int range, uint16_t *table8, hipStream_t stream )
+{
+    if constexpr( BD != 8 )
+        return hipErrorInvalidValue;
+    else
+    {
+        const int64_t lanes = (int64_t)nframes * mbh * mbw * ((2 * range + 1 + 3) / 4);
+        if( lanes <= 0 )
+            return hipSuccess;
+        if( lanes >= (1ll << 32) || (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)fs | (uintptr_t)rs) & 3) )
+            return hipErrorInvalidValue;
+        dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+        const int xcd = me_xcd();
+        switch( range )
+        {
+#define ME8_CASE( R )                                                                                           \
+            case R:                                                                                             \
+                hipLaunchKernelGGL( ( me_full_sad8q_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
+                                    mbw, mbh, nframes, table8, xcd );                                           \
+                break;
+            ME8_CASE( 4 ) ME8_CASE( 8 ) ME8_CASE( 16 ) ME8_CASE( 24 )
+#undef ME8_CASE
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
+}
+template hipError_t launch_me_full8<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
+                                        int, int, int, uint16_t *, hipStream_t );
+template hipError_t launch_me_full8<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
+                                         int, int, int, int, uint16_t *, hipStream_t );
+
+// ---------------------------------------------------------------------------
 // Variant 5 (10 bit, default): the variant-3 layout for 16-bit pixels.  A lane
 // owns two adjacent candidate columns (2g, 2g+1; the first is dword aligned for
 // even R) and half of the fenc rows; per ref row it loads 9 dwords once, forms
@@ -642,10 +773,6 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
 // current row's SADs.  At 16 1080p pairs, R 16: 8 bit 0.312 -> 0.300 ms (lead 0 -> 2;
 // 3 no better), 10 bit 0.653 -> 0.617 ms; lead 1 gains little, the compiler reuses the
 // current row's registers for it and so issues it half a row late
-// X264HIP_ME_XCD (default 1): XCD-contiguous workgroup ranges (xcd_block).  Same time for
-// the VALU-bound search, 2.3x fewer HBM fetches: neighbouring MBs' overlapping windows hit
-// one XCD's L2 (FETCH_SIZE 160 -> 69 MB per 16 1080p pairs, profiles/r03c_*)
-static int me_xcd() { return variant( V_ME_XCD ) != 0; }
 
 static int me_lead()
 {
