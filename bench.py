@@ -418,6 +418,16 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     res["lowres_me_pairs_per_s"] = world * max(1, a.steps // 5) * (F - 1) / wall
     res["lowres_me_launch_ms"] = ev_ms
     res["lowres_me_pairs_per_launch"] = F - 1
+    # the same search as x264 runs it with i_lookahead_threads = T (slicetype.c:901-918): T
+    # slices, each its own wavefront (different predictors at slice ends, so different results,
+    # as in the reference)
+    for T in (4, 8):
+        def lsstep(T=T):
+            x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2,
+                                n_slices=T)
+        wall, ev_ms = timed(lsstep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+        res["lowres_me_slices%d_pairs_per_s" % T] = world * max(1, a.steps // 5) * (F - 1) / wall
+        res["lowres_me_slices%d_launch_ms" % T] = ev_ms
     # the same search at a full-chip batch: 16 copies of those pairs in one launch (one
     # workgroup per pair, 240 of the 256 CUs busy) -- its throughput when the lookahead
     # hands over many (b, p0) pairs at once; the 15-pair leg above is per-pair latency

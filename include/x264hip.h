@@ -518,25 +518,31 @@ int x264hip_##BD##_lowres_inter_cost( const pixel *fenc, intptr_t fenc_frame_str
                                       int32_t *mv_costs, uint16_t *lowres_costs,                 \
                                       int32_t *row_satd, int32_t *est, void *stream );           \
                                                                                                 \
-/* lowres_inter_cost with a weighted reference (slicetype.c:603-614 when                         \
+/* lowres_inter_cost with a weighted reference and lookahead slices:                              \
+ * weighted reference (slicetype.c:603-614 when                                                  \
  * x264_weights_analyse( h, fenc, frames[p0], 1 ) picked fenc->weight[0][0],                     \
  * slicetype.c:859-862; weightp SMART is the default, common/base.c:452): the integer-pel        \
  * stage reads ref_w = fenc->weighted[0] (the F plane scaled by weight_scale_plane,              \
  * slicetype.c:490-499; same stride and frame stride as ref_f), the subpel get_refs weight the   \
  * unweighted hpel planes with m->weight = (w_scale, w_denom, w_offset) (mc.c:221-249,           \
  * mc_weight mc.c:117-137); the near-zero fast skip still reads ref_f (slicetype.c:680).         \
- * ref_w NULL = lowres_inter_cost.  denom 0..7, scale and offset in [-128, 127]. */              \
-int x264hip_##BD##_lowres_inter_cost_w( const pixel *fenc, intptr_t fenc_frame_stride,           \
-                                        const pixel *ref_f, const pixel *ref_h,                   \
-                                        const pixel *ref_v, const pixel *ref_c, intptr_t stride, \
-                                        intptr_t ref_frame_stride, int mb_width, int mb_height,  \
-                                        int n_pairs, int me_method, int subme, int satd,         \
-                                        int me_range, int mv_range, int lambda,                  \
-                                        const uint16_t *cost_mv, const uint16_t *intra_cost,     \
-                                        const uint16_t *inv_qscale, int16_t *mvs,                \
-                                        int32_t *mv_costs, uint16_t *lowres_costs,               \
-                                        int32_t *row_satd, int32_t *est, const pixel *ref_w,     \
-                                        int w_scale, int w_denom, int w_offset, void *stream );  \
+ * ref_w NULL = unweighted.  denom 0..7, scale and offset in [-128, 127].  n_slices =          \
+ * param i_lookahead_threads (slicetype.c:901-918): slice i covers MB rows                        \
+ * [(H*i + T/2)/T, (H*(i+1) + T/2)/T) and is scanned on its own, its last row without             \
+ * row-below predictors (slicetype.c:664, i_threadslice_end); every slice runs in parallel on     \
+ * the GPU (1 = lowres_inter_cost's single slice). */                                           \
+int x264hip_##BD##_lowres_inter_cost_ex( const pixel *fenc, intptr_t fenc_frame_stride,          \
+                                         const pixel *ref_f, const pixel *ref_h,                  \
+                                         const pixel *ref_v, const pixel *ref_c, intptr_t stride, \
+                                         intptr_t ref_frame_stride, int mb_width, int mb_height, \
+                                         int n_pairs, int me_method, int subme, int satd,        \
+                                         int me_range, int mv_range, int lambda,                 \
+                                         const uint16_t *cost_mv, const uint16_t *intra_cost,    \
+                                         const uint16_t *inv_qscale, int16_t *mvs,               \
+                                         int32_t *mv_costs, uint16_t *lowres_costs,              \
+                                         int32_t *row_satd, int32_t *est, const pixel *ref_w,    \
+                                         int w_scale, int w_denom, int w_offset, int n_slices,   \
+                                         void *stream );                                         \
                                                                                                 \
 /* x264_weight_scale_plane (common/frame.c:825-842) for n_frames planes: dst = mc_weight(src)    \
  * over the width x height region at the pointers (the reference weights 16-wide strips while   \
@@ -574,6 +580,22 @@ int x264hip_##BD##_lowres_bidir_cost( const pixel *fenc, intptr_t fenc_frame_str
                                       int dist_scale_factor, int bipred_weight,                   \
                                       const uint16_t *inv_qscale, uint16_t *lowres_costs,         \
                                       int32_t *row_satd, int32_t *est, void *stream );           \
+/* lowres_bidir_cost over n_slices lookahead slices (as lowres_inter_cost_ex) */               \
+int x264hip_##BD##_lowres_bidir_cost_ex( const pixel *fenc, intptr_t fenc_frame_stride,          \
+                                         const pixel *ref_a_f, const pixel *ref_a_h,              \
+                                         const pixel *ref_a_v, const pixel *ref_a_c,              \
+                                         intptr_t ref_a_frame_stride, const pixel *ref_b_f,       \
+                                         const pixel *ref_b_h, const pixel *ref_b_v,              \
+                                         const pixel *ref_b_c, intptr_t ref_b_frame_stride,       \
+                                         intptr_t stride, int mb_width, int mb_height, int n,     \
+                                         int me_method, int subme, int satd, int me_range,       \
+                                         int mv_range, int lambda, const uint16_t *cost_mv,       \
+                                         int search, int16_t *mvs0, int32_t *costs0,              \
+                                         int16_t *mvs1, int32_t *costs1, const int16_t *p1_mvs,  \
+                                         int dist_scale_factor, int bipred_weight,                \
+                                         const uint16_t *inv_qscale, uint16_t *lowres_costs,      \
+                                         int32_t *row_satd, int32_t *est, int n_slices,           \
+                                         void *stream );                                          \
                                                                                                 \
 /* ESA integral image of n_frames luma planes (x264_frame_filter, mc.c:748-782;                 \
  * integral_init* mc.c:424-456): plane / integral point at (0,0), rows                          \

@@ -2535,12 +2535,12 @@ static int lr_list( lrme_t *m, int16_t *mvs, int mb, int mbx, int mby, int mb_wi
  * fenc->i_intra_cost (x264hip lowres_intra_cost).  Outputs lowres_mvs[mb][2],
  * lowres_mv_costs[mb], lowres_costs[mb] ((list_used << 14) + cost), row_satd[y]
  * (AQ-scaled inter row sums) and est = { cost_est, cost_est_aq, intra_mbs }. */
-void FN(lowres_inter_cost_w)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
-                              const pixel *ref3, const pixel *ref_w, const int *weight, intptr_t stride,
-                              int mb_width, int mb_height, int me_method,
-                              int subme, int satd, int me_range, int mv_range, int lambda, const uint16_t *cost_mv,
-                              const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs, int32_t *mv_costs,
-                              uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] );
+void FN(lowres_inter_cost_ex)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
+                               const pixel *ref3, const pixel *ref_w, const int *weight, int n_slices,
+                               intptr_t stride, int mb_width, int mb_height, int me_method,
+                               int subme, int satd, int me_range, int mv_range, int lambda, const uint16_t *cost_mv,
+                               const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs,
+                               int32_t *mv_costs, uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] );
 
 void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
                             const pixel *ref3, intptr_t stride, int mb_width, int mb_height, int me_method,
@@ -2548,9 +2548,9 @@ void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *r
                             const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs, int32_t *mv_costs,
                             uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] )
 {
-    FN(lowres_inter_cost_w)( fenc, ref0, ref1, ref2, ref3, NULL, NULL, stride, mb_width, mb_height, me_method, subme,
-                             satd, me_range, mv_range, lambda, cost_mv, intra_cost, inv_qscale, mvs, mv_costs,
-                             lowres_costs, row_satd, est );
+    FN(lowres_inter_cost_ex)( fenc, ref0, ref1, ref2, ref3, NULL, NULL, 1, stride, mb_width, mb_height, me_method,
+                              subme, satd, me_range, mv_range, lambda, cost_mv, intra_cost, inv_qscale, mvs, mv_costs,
+                              lowres_costs, row_satd, est );
 }
 
 /* The weighted-reference form (slicetype.c:603-614 with w[0].weightfn set, i.e. when
@@ -2560,19 +2560,26 @@ void FN(lowres_inter_cost)( const pixel *fenc, const pixel *ref0, const pixel *r
  * weights the unweighted hpel planes with m->weight = weight { scale, denom, offset };
  * the near-zero fast skip still compares against the unweighted F plane
  * (slicetype.c:680).  ref_w / weight NULL: the unweighted search. */
-void FN(lowres_inter_cost_w)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
-                              const pixel *ref3, const pixel *ref_w, const int *weight, intptr_t stride,
-                              int mb_width, int mb_height, int me_method,
-                              int subme, int satd, int me_range, int mv_range, int lambda, const uint16_t *cost_mv,
-                              const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs, int32_t *mv_costs,
-                              uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] )
+void FN(lowres_inter_cost_ex)( const pixel *fenc, const pixel *ref0, const pixel *ref1, const pixel *ref2,
+                               const pixel *ref3, const pixel *ref_w, const int *weight, int n_slices,
+                               intptr_t stride, int mb_width, int mb_height, int me_method,
+                               int subme, int satd, int me_range, int mv_range, int lambda, const uint16_t *cost_mv,
+                               const uint16_t *intra_cost, const uint16_t *inv_qscale, int16_t *mvs,
+                               int32_t *mv_costs, uint16_t *lowres_costs, int32_t *row_satd, int32_t est[3] )
 {
     pixel fbuf[8 * FENC_STRIDE];
     const pixel *ref[4] = { ref0, ref1, ref2, ref3 };
     est[0] = est[1] = est[2] = 0;
     for( int y = 0; y < mb_height; y++ )
         row_satd[y] = 0;
-    for( int mby = mb_height - 1; mby >= 0; mby-- )
+    /* i_lookahead_threads > 1 (slicetype.c:901-918): slice i covers MB rows
+     * [(H*i + T/2)/T, (H*(i+1) + T/2)/T), each scanned on its own (slicetype_slice_cost,
+     * slicetype.c:813-833) with the row-below predictors only inside the slice
+     * (slicetype.c:664, h->i_threadslice_end); the slices' sums add up */
+    for( int sl = 0; sl < n_slices; sl++ )
+    for( int mby = (mb_height * (sl + 1) + n_slices / 2) / n_slices - 1,
+             s0 = (mb_height * sl + n_slices / 2) / n_slices,
+             s1 = (mb_height * (sl + 1) + n_slices / 2) / n_slices; mby >= s0; mby-- )
         for( int mbx = mb_width - 1; mbx >= 0; mbx-- )
         {
             const int mb = mbx + mby * mb_width;
@@ -2583,7 +2590,7 @@ void FN(lowres_inter_cost_w)( const pixel *fenc, const pixel *ref0, const pixel 
                 m.fw = ref_w + 8 * mbx + 8 * mby * stride;
                 m.wt = weight;
             }
-            const int cost = lr_list( &m, mvs, mb, mbx, mby, mb_width, mb_height, me_method, subme, me_range, lambda,
+            const int cost = lr_list( &m, mvs, mb, mbx, mby, mb_width, s1, me_method, subme, me_range, lambda,
                                       cost_mv );
             mv_costs[mb] = cost;
             /* slicetype.c:758-790 */
@@ -2644,6 +2651,13 @@ static int lr_bidir( const lrme_t *m0, const lrme_t *m1, const int mv0[2], const
  * fref1->lowres_mvs[0][p1-p0-1] (NULL: not searched, dmv = 0), dsf = dist_scale_factor,
  * weight = i_bipred_weight.  No intra in B frames.  Outputs lowres_costs[mb]
  * (fenc->lowres_costs[b-p0][p1-b]), row_satd[y] and est = { cost_est, cost_est_aq }. */
+void FN(lowres_bidir_cost_ex)( const pixel *fenc, const pixel *const ref_a[4], const pixel *const ref_b[4],
+                               intptr_t stride, int mb_width, int mb_height, int me_method, int subme, int satd,
+                               int me_range, int mv_range, int lambda, const uint16_t *cost_mv, const int search[2],
+                               int16_t *mvs0, int32_t *costs0, int16_t *mvs1, int32_t *costs1,
+                               const int16_t *p1mvs, int dsf, int weight, const uint16_t *inv_qscale,
+                               uint16_t *lowres_costs, int32_t *row_satd, int32_t est[2], int n_slices );
+
 void FN(lowres_bidir_cost)( const pixel *fenc, const pixel *const ref_a[4], const pixel *const ref_b[4],
                             intptr_t stride, int mb_width, int mb_height, int me_method, int subme, int satd,
                             int me_range, int mv_range, int lambda, const uint16_t *cost_mv, const int search[2],
@@ -2651,11 +2665,27 @@ void FN(lowres_bidir_cost)( const pixel *fenc, const pixel *const ref_a[4], cons
                             int dsf, int weight, const uint16_t *inv_qscale, uint16_t *lowres_costs,
                             int32_t *row_satd, int32_t est[2] )
 {
+    FN(lowres_bidir_cost_ex)( fenc, ref_a, ref_b, stride, mb_width, mb_height, me_method, subme, satd, me_range,
+                              mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, weight,
+                              inv_qscale, lowres_costs, row_satd, est, 1 );
+}
+
+/* the B leg over n_slices lookahead slices (as lowres_inter_cost_ex) */
+void FN(lowres_bidir_cost_ex)( const pixel *fenc, const pixel *const ref_a[4], const pixel *const ref_b[4],
+                               intptr_t stride, int mb_width, int mb_height, int me_method, int subme, int satd,
+                               int me_range, int mv_range, int lambda, const uint16_t *cost_mv, const int search[2],
+                               int16_t *mvs0, int32_t *costs0, int16_t *mvs1, int32_t *costs1,
+                               const int16_t *p1mvs, int dsf, int weight, const uint16_t *inv_qscale,
+                               uint16_t *lowres_costs, int32_t *row_satd, int32_t est[2], int n_slices )
+{
     pixel fbuf[8 * FENC_STRIDE];
     est[0] = est[1] = 0;
     for( int y = 0; y < mb_height; y++ )
         row_satd[y] = 0;
-    for( int mby = mb_height - 1; mby >= 0; mby-- )
+    for( int sl = 0; sl < n_slices; sl++ )
+    for( int mby = (mb_height * (sl + 1) + n_slices / 2) / n_slices - 1,
+             s0 = (mb_height * sl + n_slices / 2) / n_slices,
+             s1 = (mb_height * (sl + 1) + n_slices / 2) / n_slices; mby >= s0; mby-- )
         for( int mbx = mb_width - 1; mbx >= 0; mbx-- )
         {
             const int mb = mbx + mby * mb_width;
@@ -2698,7 +2728,7 @@ void FN(lowres_bidir_cost)( const pixel *fenc, const pixel *const ref_a[4], cons
                 int cost;
                 if( search[l] )
                 {
-                    cost = lr_list( lmm[l], lm[l], mb, mbx, mby, mb_width, mb_height, me_method, subme, me_range,
+                    cost = lr_list( lmm[l], lm[l], mb, mbx, mby, mb_width, s1, me_method, subme, me_range,
                                     lambda, cost_mv );
                     lc[l][mb] = cost;
                 }

@@ -114,12 +114,15 @@ for _bd in (8, 10):
     _f(_bd, "lowres_intra_cost", [_P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "lowres_inter_cost", [_P, _P, _P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P])
-    _f(_bd, "lowres_inter_cost_w", [_P, _P, _P, _P, _P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                    C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P])
+    _f(_bd, "lowres_inter_cost_ex", [_P, _P, _P, _P, _P, _P, _P, C.c_int, _IP, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P, _P, _P, _P])
     _f(_bd, "weight_scale_plane", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int])
     _f(_bd, "mc_weight", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int])
     _f(_bd, "lowres_bidir_cost", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                   C.c_int, _P, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P, _P, _P, _P])
+    _f(_bd, "lowres_bidir_cost_ex", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                     C.c_int, _P, _P, _P, _P, _P, _P, _P, C.c_int, C.c_int, _P, _P, _P, _P,
+                                     C.c_int])
 _L.oracle8_me_search_full_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, C.c_int]
 _L.oracle8_me_search_full_mt.restype = C.c_int
 _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int]
@@ -538,7 +541,8 @@ def weight_scale_plane(bd, src, src_off, stride, width, height, scale, denom, of
 
 
 def lowres_inter_cost(bd, fenc, ref_planes, origin, stride, mbw, mbh, intra_cost, me_method=1, subme=4, satd=True,
-                      me_range=16, mv_range=512, lam=1, cost_mv=None, inv_qscale=None, ref_w=None, weight=None):
+                      me_range=16, mv_range=512, lam=1, cost_mv=None, inv_qscale=None, ref_w=None, weight=None,
+                      n_slices=1):
     """slicetype_mb_cost's P-frame inter leg over one lowres pair (numpy planes, (0,0) at origin):
     (mvs int16 [mbs, 2], mv_costs int32 [mbs], lowres_costs uint16 [mbs], row_satd int32 [mbh], est int32 [3]).
     ref_w / weight (scale, denom, offset): the weighted-reference form (fenc->weighted[0])."""
@@ -554,9 +558,9 @@ def lowres_inter_cost(bd, fenc, ref_planes, origin, stride, mbw, mbh, intra_cost
     ic = np.ascontiguousarray(intra_cost, np.uint16)
     iq = None if inv_qscale is None else np.ascontiguousarray(inv_qscale, np.uint16)
     wt = None if weight is None else np.ascontiguousarray(weight, np.int32)
-    fn(bd, "lowres_inter_cost_w")(_addr(fenc, origin), *[_addr(p, origin) for p in ref_planes],
+    fn(bd, "lowres_inter_cost_ex")(_addr(fenc, origin), *[_addr(p, origin) for p in ref_planes],
                                   None if ref_w is None else _addr(ref_w, origin), None if wt is None else _addr(wt),
-                                  stride, mbw, mbh, me_method, subme, int(satd), me_range, mv_range, lam, _addr(cm, c0),
+                                  n_slices, stride, mbw, mbh, me_method, subme, int(satd), me_range, mv_range, lam, _addr(cm, c0),
                                   _addr(ic), None if iq is None else _addr(iq), _addr(mvs), _addr(mvc), _addr(lc),
                                   _addr(rows), _addr(est))
     return mvs, mvc, lc, rows, est
@@ -564,7 +568,7 @@ def lowres_inter_cost(bd, fenc, ref_planes, origin, stride, mbw, mbh, intra_cost
 
 def lowres_bidir_cost(bd, fenc, ref_a, ref_b, origin, stride, mbw, mbh, search, mvs0, costs0, mvs1, costs1,
                       p1mvs=None, dsf=128, weight=32, me_method=1, subme=4, satd=True, me_range=16, mv_range=512,
-                      lam=1, cost_mv=None, inv_qscale=None):
+                      lam=1, cost_mv=None, inv_qscale=None, n_slices=1):
     """slicetype_mb_cost's B-frame leg over one lowres triplet.  mvs_l int16 [mbs, 2] / costs_l
     int32 [mbs] are read (search bit clear) or written (set); copies are returned:
     (mvs0, costs0, mvs1, costs1, lowres_costs uint16 [mbs], row_satd int32 [mbh], est int32 [2])"""
@@ -582,8 +586,8 @@ def lowres_bidir_cost(bd, fenc, ref_a, ref_b, origin, stride, mbw, mbh, search, 
     pb = (C.c_void_p * 4)(*[p.ctypes.data + origin * p.itemsize for p in ref_b])
     p1 = None if p1mvs is None else np.ascontiguousarray(p1mvs, np.int16)
     iq = None if inv_qscale is None else np.ascontiguousarray(inv_qscale, np.uint16)
-    fn(bd, "lowres_bidir_cost")(_addr(fenc, origin), pa, pb, stride, mbw, mbh, me_method, subme, int(satd),
-                                me_range, mv_range, lam, _addr(cm, c0), srch, _addr(m0), _addr(k0), _addr(m1),
-                                _addr(k1), None if p1 is None else _addr(p1), dsf, weight,
-                                None if iq is None else _addr(iq), _addr(lc), _addr(rows), _addr(est))
+    fn(bd, "lowres_bidir_cost_ex")(_addr(fenc, origin), pa, pb, stride, mbw, mbh, me_method, subme, int(satd),
+                                   me_range, mv_range, lam, _addr(cm, c0), srch, _addr(m0), _addr(k0), _addr(m1),
+                                   _addr(k1), None if p1 is None else _addr(p1), dsf, weight,
+                                   None if iq is None else _addr(iq), _addr(lc), _addr(rows), _addr(est), n_slices)
     return m0, k0, m1, k1, lc, rows, est

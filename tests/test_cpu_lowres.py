@@ -92,3 +92,40 @@ def test_lowres_weighted_identity(oracle, bd):
     other = oracle.lowres_inter_cost(bd, lows[0][1].ravel(), refs, lo, ls, mbw, mbh, intra, ref_w=rw.ravel(),
                                      weight=wt)
     assert not all(np.array_equal(a, b) for a, b in zip(base, other))
+
+
+@pytest.mark.parametrize("n_slices", [2, 3, 5])
+def test_lowres_slices_oracle_properties(oracle, n_slices):
+    """Lookahead slices (i_lookahead_threads > 1, slicetype.c:901-918) in the oracle: the bottom
+    slice scans exactly as the whole frame does (its row-below predictors exist either way),
+    and a slice's results do not depend on the fenc rows of the other slices."""
+    from conftest import load_package
+    load_package()
+    from x264hip import synth
+    W, H = 160, 128
+    frames, stride, origin = synth.random_planes(2, W, H, 8, seed=n_slices)   # searches that wander
+    lw, lh = W // 2, H // 2
+    ls = synth.plane_stride(lw)
+    per = [oracle.frame_init_lowres(8, frames[f].ravel(), origin, stride, W, H, ls) for f in range(2)]
+    lo = 32 * ls + 32
+    mbw, mbh = W // 16, H // 16
+    intra = np.full(mbw * mbh, 16383, np.uint16)
+    refs = [p.ravel() for p in per[0]]
+    fenc = per[1][0].copy()
+    one = oracle.lowres_inter_cost(8, fenc.ravel(), refs, lo, ls, mbw, mbh, intra)
+    sl = oracle.lowres_inter_cost(8, fenc.ravel(), refs, lo, ls, mbw, mbh, intra, n_slices=n_slices)
+    bounds = [((mbh * i + n_slices // 2) // n_slices, (mbh * (i + 1) + n_slices // 2) // n_slices)
+              for i in range(n_slices)]
+    s0, s1 = bounds[-1]
+    rows = slice(s0 * mbw, s1 * mbw)
+    assert np.array_equal(one[0][rows], sl[0][rows]) and np.array_equal(one[1][rows], sl[1][rows])
+    assert np.array_equal(one[3][s0:], sl[3][s0:])
+    assert not (np.array_equal(one[0], sl[0]) and np.array_equal(one[1], sl[1]))   # slice ends lost predictors
+    for i, (a, b) in enumerate(bounds):
+        f2 = fenc.copy()
+        keep = np.zeros(f2.shape[0], bool)
+        keep[32 + 8 * a:32 + 8 * b] = True
+        f2[~keep] = 255 - f2[~keep]                    # the other slices' (and the border) rows
+        got = oracle.lowres_inter_cost(8, f2.ravel(), refs, lo, ls, mbw, mbh, intra, n_slices=n_slices)
+        r = slice(a * mbw, b * mbw)
+        assert np.array_equal(got[0][r], sl[0][r]) and np.array_equal(got[1][r], sl[1][r]), i

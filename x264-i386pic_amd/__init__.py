@@ -376,9 +376,9 @@ def _declare(L):
                                            _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _P, _P,
                                            _P, _P, _P]
         f("lowres_inter_cost").restype = _c.c_int
-        f("lowres_inter_cost_w").argtypes = f("lowres_inter_cost").argtypes[:-1] + [_P, _c.c_int, _c.c_int, _c.c_int,
-                                                                                   _P]
-        f("lowres_inter_cost_w").restype = _c.c_int
+        f("lowres_inter_cost_ex").argtypes = f("lowres_inter_cost").argtypes[:-1] + [_P, _c.c_int, _c.c_int,
+                                                                                    _c.c_int, _c.c_int, _P]
+        f("lowres_inter_cost_ex").restype = _c.c_int
         f("weight_scale_plane").argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                             _c.c_int, _c.c_int, _P]
         f("weight_scale_plane").restype = _c.c_int
@@ -386,6 +386,8 @@ def _declare(L):
                                            _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int,
                                            _c.c_int, _P, _c.c_int, _P, _P, _P, _P, _P, _c.c_int, _c.c_int, _P, _P,
                                            _P, _P, _P]
+        f("lowres_bidir_cost_ex").argtypes = f("lowres_bidir_cost").argtypes[:-1] + [_c.c_int, _P]
+        f("lowres_bidir_cost_ex").restype = _c.c_int
         f("lowres_bidir_cost").restype = _c.c_int
         f("mb_dequant_idct_add").argtypes = [_c.c_int, _P, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _IP, _IP,
                                              _P, _IP, _IP, _P]
@@ -731,7 +733,7 @@ def weight_scale_plane(src, lowres_stride, width, height, scale, denom, offset, 
 
 def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost, cost_mv_center, me_method=1,
                       subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None, outs=None,
-                      ref_w=None, weight=None):
+                      ref_w=None, weight=None, n_slices=1):
     """The lookahead's P-frame lowres motion search (x264hip_*_lowres_inter_cost) for the pairs
     (fenc[i], refs[*][i]): fenc = lowres[0] planes [n, rows, stride], refs = the four lowres planes
     (F, H, V, C) of the references, same shape; (0,0) at (PAD, PAD).  intra_cost [n, mbs] from
@@ -757,19 +759,21 @@ def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost
         raise ValueError("lowres_inter_cost: ref_w and weight go together")
     rfs = _frame_stride(*refs) if ref_w is None else _frame_stride(*refs, ref_w)
     w = (0, 0, 0) if weight is None else tuple(int(v) for v in weight)
-    _rc(getattr(lib(), f"x264hip_{bd}_lowres_inter_cost_w")(
+    _rc(getattr(lib(), f"x264hip_{bd}_lowres_inter_cost_ex")(
         _ptr(fenc, o), _frame_stride(fenc), *[_ptr(r, o) for r in refs], lowres_stride, rfs,
         mb_width, mb_height, n, me_method, subme, int(bool(satd)), me_range, mv_range, lam, _ptr(cm, c0),
         _ptr(intra_cost), _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(mvs), _ptr(mvc), _ptr(lc),
-        _ptr(rows), _ptr(est), None if ref_w is None else _ptr(ref_w, o), *w, _stream()), "lowres_inter_cost")
+        _ptr(rows), _ptr(est), None if ref_w is None else _ptr(ref_w, o), *w, n_slices, _stream()),
+        "lowres_inter_cost")
     return mvs, mvc, lc, rows, est
 
 
 def lowres_bidir_cost(fenc, refs_a, refs_b, lowres_stride, mb_width, mb_height, cost_mv_center, search,
                       mvs0, costs0, mvs1, costs1, p1_mvs=None, dist_scale_factor=128, bipred_weight=32,
                       me_method=1, subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None,
-                      outs=None, a_frame_stride=None, b_frame_stride=None):
-    """The lookahead's B-frame costs (x264hip_*_lowres_bidir_cost) for the triplets (fenc[i],
+                      outs=None, a_frame_stride=None, b_frame_stride=None, n_slices=1):
+    """The lookahead's B-frame costs (x264hip_*_lowres_bidir_cost_ex; n_slices lookahead slices) for
+    the triplets (fenc[i],
     refs_a[*][i], refs_b[*][i]); a reference tensor with one frame and a frame stride of 0 serves
     the whole batch.  mvs_l int16 [n, mbs, 2] / costs_l int32 [n, mbs] are searched into (search
     bit l set) or read.  Returns (lowres_costs uint16-as-int16 [n, mbs], row_satd int32 [n, mbh],
@@ -788,13 +792,13 @@ def lowres_bidir_cost(fenc, refs_a, refs_b, lowres_stride, mb_width, mb_height, 
     o = PAD * lowres_stride + PAD
     afs = _frame_stride(*refs_a) if a_frame_stride is None else a_frame_stride
     bfs = _frame_stride(*refs_b) if b_frame_stride is None else b_frame_stride
-    _rc(getattr(lib(), f"x264hip_{bd}_lowres_bidir_cost")(
+    _rc(getattr(lib(), f"x264hip_{bd}_lowres_bidir_cost_ex")(
         _ptr(fenc, o), _frame_stride(fenc), *[_ptr(r, o) for r in refs_a], afs, *[_ptr(r, o) for r in refs_b], bfs,
         lowres_stride, mb_width, mb_height, n, me_method, subme, int(bool(satd)), me_range, mv_range, lam,
         _ptr(cm, c0), search, _ptr(mvs0), _ptr(costs0), _ptr(mvs1), _ptr(costs1),
         _ptr(p1_mvs) if p1_mvs is not None else None, dist_scale_factor, bipred_weight,
-        _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(lc), _ptr(rows), _ptr(est), _stream()),
-        "lowres_bidir_cost")
+        _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(lc), _ptr(rows), _ptr(est), n_slices,
+        _stream()), "lowres_bidir_cost")
     return lc, rows, est
 
 

@@ -1483,14 +1483,16 @@ extern "C" const char *x264hip_backend_banner( void )
                                                  invq, cost, row_satd, est, (hipStream_t)stream ),                   \
                         "lowres_intra_cost" );                                                                       \
     }                                                                                                                \
-    extern "C" int x264hip_##BD##_lowres_inter_cost_w(                                                             \
+    extern "C" int x264hip_##BD##_lowres_inter_cost_ex(                                                            \
         const PT<BD>::pixel *fenc, intptr_t ffs, const PT<BD>::pixel *rf, const PT<BD>::pixel *rh,                  \
         const PT<BD>::pixel *rv, const PT<BD>::pixel *rc, intptr_t stride, intptr_t rfs, int mbw, int mbh,          \
         int npairs, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,                     \
         const uint16_t *cost_mv, const uint16_t *intra_cost, const uint16_t *invq, int16_t *mvs, int32_t *mv_costs,   \
         uint16_t *lowres_costs, int32_t *row_satd, int32_t *est, const PT<BD>::pixel *ref_w, int w_scale,           \
-        int w_denom, int w_offset, void *stream )                                                                    \
+        int w_denom, int w_offset, int n_slices, void *stream )                                                      \
     {                                                                                                                \
+        if( n_slices < 1 || n_slices > 256 )                                                                         \
+            return X264HIP_EINVAL;                                                                                   \
         const intptr_t pb = (intptr_t)sizeof( PT<BD>::pixel );                                                       \
         if( mbw < 0 || mbh < 0 || npairs < 0 || ( me_method != 0 && me_method != 1 ) ||                              \
             ( subme != 2 && subme != 4 ) || me_range < 1 || mv_range < 1 || lambda < 0 ||                            \
@@ -1506,7 +1508,7 @@ extern "C" const char *x264hip_backend_banner( void )
         return map_err( launch_lowres_inter<BD>( fenc, ffs, ref, stride, rfs, mbw, mbh, npairs, me_method, subme,    \
                                                  satd, me_range, mv_range, lambda, cost_mv, intra_cost, invq, mvs,   \
                                                  mv_costs, lowres_costs, row_satd, est, ref_w, w_scale, w_denom,     \
-                                                 w_offset, (hipStream_t)stream ),                                    \
+                                                 w_offset, n_slices, (hipStream_t)stream ),                          \
                         "lowres_inter_cost" );                                                                       \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_lowres_inter_cost(                                                               \
@@ -1516,10 +1518,10 @@ extern "C" const char *x264hip_backend_banner( void )
         const uint16_t *cost_mv, const uint16_t *intra_cost, const uint16_t *invq, int16_t *mvs, int32_t *mv_costs,   \
         uint16_t *lowres_costs, int32_t *row_satd, int32_t *est, void *stream )                                      \
     {                                                                                                                \
-        return x264hip_##BD##_lowres_inter_cost_w( fenc, ffs, rf, rh, rv, rc, stride, rfs, mbw, mbh, npairs,          \
-                                                   me_method, subme, satd, me_range, mv_range, lambda, cost_mv,      \
-                                                   intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est,     \
-                                                   nullptr, 0, 0, 0, stream );                                       \
+        return x264hip_##BD##_lowres_inter_cost_ex( fenc, ffs, rf, rh, rv, rc, stride, rfs, mbw, mbh, npairs,         \
+                                                    me_method, subme, satd, me_range, mv_range, lambda, cost_mv,     \
+                                                    intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est,    \
+                                                    nullptr, 0, 0, 0, 1, stream );                                   \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_weight_scale_plane( PT<BD>::pixel *dst, intptr_t ds, intptr_t dfs,               \
                                                       const PT<BD>::pixel *src, intptr_t ss, intptr_t sfs,          \
@@ -1534,16 +1536,18 @@ extern "C" const char *x264hip_backend_banner( void )
                                                  offset, (hipStream_t)stream ),                                      \
                         "weight_scale_plane" );                                                                      \
     }                                                                                                                \
-    extern "C" int x264hip_##BD##_lowres_bidir_cost(                                                               \
+    extern "C" int x264hip_##BD##_lowres_bidir_cost_ex(                                                            \
         const PT<BD>::pixel *fenc, intptr_t ffs, const PT<BD>::pixel *af, const PT<BD>::pixel *ah,                  \
         const PT<BD>::pixel *av, const PT<BD>::pixel *ac, intptr_t afs, const PT<BD>::pixel *bf,                    \
         const PT<BD>::pixel *bh, const PT<BD>::pixel *bv, const PT<BD>::pixel *bc, intptr_t bfs, intptr_t stride,   \
         int mbw, int mbh, int n, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,        \
         const uint16_t *cost_mv, int search, int16_t *mvs0, int32_t *costs0, int16_t *mvs1, int32_t *costs1,       \
         const int16_t *p1mvs, int dsf, int weight, const uint16_t *invq, uint16_t *lowres_costs, int32_t *row_satd,  \
-        int32_t *est, void *stream )                                                                                 \
+        int32_t *est, int n_slices, void *stream )                                                                   \
     {                                                                                                                \
         const intptr_t pb = (intptr_t)sizeof( PT<BD>::pixel );                                                       \
+        if( n_slices < 1 || n_slices > 256 )                                                                         \
+            return X264HIP_EINVAL;                                                                                   \
         if( mbw < 0 || mbh < 0 || n < 0 || ( me_method != 0 && me_method != 1 ) || ( subme != 2 && subme != 4 ) ||   \
             me_range < 1 || mv_range < 1 || lambda < 0 || search < 0 || search > 3 || weight < 0 || weight > 64 ||   \
             ( (uintptr_t)fenc & 3 ) || ( ( stride * pb ) & 3 ) || ( ( ffs * pb ) & 3 ) || stride < 8 * mbw + 64 ||   \
@@ -1554,8 +1558,22 @@ extern "C" const char *x264hip_backend_banner( void )
         return map_err( launch_lowres_bidir<BD>( fenc, ffs, ra, afs, rb, bfs, stride, mbw, mbh, n, me_method, subme, \
                                                  satd, me_range, mv_range, lambda, cost_mv, search, mvs0, costs0,    \
                                                  mvs1, costs1, p1mvs, dsf, weight, invq, lowres_costs, row_satd,     \
-                                                 est, (hipStream_t)stream ),                                         \
+                                                 est, n_slices, (hipStream_t)stream ),                               \
                         "lowres_bidir_cost" );                                                                       \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_lowres_bidir_cost(                                                               \
+        const PT<BD>::pixel *fenc, intptr_t ffs, const PT<BD>::pixel *af, const PT<BD>::pixel *ah,                  \
+        const PT<BD>::pixel *av, const PT<BD>::pixel *ac, intptr_t afs, const PT<BD>::pixel *bf,                    \
+        const PT<BD>::pixel *bh, const PT<BD>::pixel *bv, const PT<BD>::pixel *bc, intptr_t bfs, intptr_t stride,   \
+        int mbw, int mbh, int n, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,        \
+        const uint16_t *cost_mv, int search, int16_t *mvs0, int32_t *costs0, int16_t *mvs1, int32_t *costs1,       \
+        const int16_t *p1mvs, int dsf, int weight, const uint16_t *invq, uint16_t *lowres_costs, int32_t *row_satd,  \
+        int32_t *est, void *stream )                                                                                 \
+    {                                                                                                                \
+        return x264hip_##BD##_lowres_bidir_cost_ex( fenc, ffs, af, ah, av, ac, afs, bf, bh, bv, bc, bfs, stride,     \
+                                                    mbw, mbh, n, me_method, subme, satd, me_range, mv_range,         \
+                                                    lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, \
+                                                    weight, invq, lowres_costs, row_satd, est, 1, stream );          \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_frame_integral( const PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride,    \
                                                   int lines, int padh, int sub8x8, int nframes, uint16_t *integral,  \

@@ -363,7 +363,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                 int lambda, const uint16_t *cost_mv, const uint16_t *intra_cost,
                                 const uint16_t *invq, int16_t *mvs, int32_t *mv_costs, uint16_t *lowres_costs,
                                 int32_t *row_satd, int32_t *est, const typename PT<BD>::pixel *ref_w, int wscale,
-                                int wdenom, int woffset, hipStream_t stream );
+                                int wdenom, int woffset, int nslices, hipStream_t stream );
 template <int BD>
 hipError_t launch_me_full8( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                             const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -380,5 +380,5 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                 int lambda, const uint16_t *cost_mv, int search, int16_t *mvs0, int32_t *costs0,
                                 int16_t *mvs1, int32_t *costs1, const int16_t *p1mvs, int dsf, int weight,
                                 const uint16_t *invq, uint16_t *lowres_costs, int32_t *row_satd, int32_t *est,
-                                hipStream_t stream );
+                                int nslices, hipStream_t stream );
 } // namespace x264hip

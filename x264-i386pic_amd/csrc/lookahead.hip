@@ -733,7 +733,7 @@ __device__ __forceinline__ void lr_store_mv( uint32_t *p, uint32_t v )
 // then stops, and the launcher reports the failure instead of letting sentinel words
 // act as predictors.
 __device__ __forceinline__ int lr_preds( const int *ring, int y0, int y1, const uint32_t *gmv, int x, int y, int mbw,
-                                         int mbh, uint32_t (&pred)[4], int poll_max, uint32_t *status )
+                                         int send, uint32_t (&pred)[4], int poll_max, uint32_t *status )
 {
     int n = 0;
 #pragma unroll
@@ -741,7 +741,7 @@ __device__ __forceinline__ int lr_preds( const int *ring, int y0, int y1, const 
         pred[i] = 0;
     if( x < mbw - 1 )
         pred[n++] = (uint32_t)ring[4 * (y - y0) + ((x + 1) & 3)];
-    if( y < mbh - 1 )
+    if( y < send - 1 )                           // the slice's last row has no row below
     {
         uint32_t b = 0, bl = 0, br = 0;
         if( y + 1 < y1 )
@@ -814,6 +814,29 @@ __device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, 
     }
 }
 
+// Lookahead slices (i_lookahead_threads, slicetype.c:901-918): slice i holds MB rows
+// [(H*i + T/2)/T, (H*(i+1) + T/2)/T) and is its own wavefront (slicetype_slice_cost scans it
+// alone; its row-below predictors stop at the slice end, slicetype.c:664).  Band j of a
+// pair: bands are counted slice by slice, bottom band first inside a slice, so a band's
+// producer (the band under it, same slice) always has the lower index.
+__device__ __forceinline__ void lr_band( int j, int mbh, int nslices, int brows, int &s1, int &y0, int &y1 )
+{
+    s1 = y0 = y1 = 0;
+    for( int i = 0; i < nslices; i++ )
+    {
+        const int a = (mbh * i + nslices / 2) / nslices, b = (mbh * (i + 1) + nslices / 2) / nslices;
+        const int nb = (b - a + brows - 1) / brows;
+        if( j < nb )
+        {
+            s1 = b;
+            y1 = b - j * brows;
+            y0 = max( a, y1 - brows );
+            return;
+        }
+        j -= nb;
+    }
+}
+
 template <int BD>
 __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *r0,
@@ -822,15 +845,16 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     int lambda, const uint16_t *__restrict__ cost_mv, const uint16_t *__restrict__ intra_cost,
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
     uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands, int brows,
-    int poll_max, uint32_t *status, const typename PT<BD>::pixel *rw, int wscale, int wdenom, int woffset )
+    int poll_max, uint32_t *status, const typename PT<BD>::pixel *rw, int wscale, int wdenom, int woffset,
+    int nslices )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring[4 * LR_BAND];            // packed MVs of each band row's 4 latest blocks
     extern __shared__ uint16_t lr_cost_lds[];
     const uint16_t *cml = lr_stage_cost( lr_cost_lds, cost_mv, mv_range );
     const int f = blockIdx.x / nbands;
-    const int band = nbands - 1 - (int)(blockIdx.x % nbands);     // index 0 of a pair: the bottom band
-    const int y0 = brows * band, y1 = min( y0 + brows, mbh );
+    int s1, y0, y1;                               // the band's rows [y0, y1) of a slice ending at s1
+    lr_band( (int)(blockIdx.x % nbands), mbh, nslices, brows, s1, y0, y1 );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     r0 += (intptr_t)f * rfs;
@@ -853,19 +877,19 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     // (lr_me_search's role); group 0 writes the results
     const int role = (int)(threadIdx.x >> 4);
     const int y = y0 + (int)((threadIdx.x & 15) >> 2);
-    // steps in which this band has blocks (block (x, y) runs at (W-1-x) + 2(H-1-y))
-    const int t0 = 2 * (mbh - y1), t1 = 2 * (mbh - 1 - y0) + mbw - 1;
+    // steps in which this band has blocks (block (x, y) runs at (W-1-x) + 2(s1-1-y))
+    const int t0 = 2 * (s1 - y1), t1 = 2 * (s1 - 1 - y0) + mbw - 1;
     // a row's next block is x - 1: its fenc rows are fetched one step ahead
     uint32_t fnext[LR_NR][NDW];
     auto fetch = [&]( int t ) {
-        const int xn = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        const int xn = mbw - 1 - (t - 2 * (s1 - 1 - y));
         if( y < y1 && xn >= 0 && xn < mbw )
             lr_load_fenc<BD>( fenc + 8 * (intptr_t)xn + (intptr_t)(8 * y + LR_NR * q) * stride, stride, fnext );
     };
     fetch( t0 );
     for( int t = t0; t <= t1; t++ )
     {
-        const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        const int x = mbw - 1 - (t - 2 * (s1 - 1 - y));
         uint32_t fe[LR_NR][NDW];
 #pragma unroll
         for( int r = 0; r < LR_NR; r++ )
@@ -883,7 +907,7 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
             if( rw )
                 m.set_weight( rw, off, wscale, wdenom, woffset );
             uint32_t pred[4];
-            const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred, poll_max, status );
+            const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, s1, pred, poll_max, status );
             // the lanes of the band share candidate batches: a failed wait stops them all
             failed = __builtin_amdgcn_ballot_w64( np < 0 ) != 0;
             int mvx = 0, mvy = 0, cost = 0;
@@ -990,15 +1014,15 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const uint16_t *__restrict__ cost_mv, int search, int16_t *__restrict__ mvs0, int32_t *__restrict__ costs0,
     int16_t *__restrict__ mvs1, int32_t *__restrict__ costs1, const int16_t *__restrict__ p1mvs, int dsf, int weight,
     const uint16_t *__restrict__ invq, uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd,
-    int32_t *__restrict__ est, int nbands, int brows, int poll_max, uint32_t *status )
+    int32_t *__restrict__ est, int nbands, int brows, int poll_max, uint32_t *status, int nslices )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring0[4 * LR_BAND], ring1[4 * LR_BAND];      // per list
     extern __shared__ uint16_t lr_cost_lds[];
     const uint16_t *cml = lr_stage_cost( lr_cost_lds, cost_mv, mv_range );
     const int f = blockIdx.x / nbands;
-    const int band = nbands - 1 - (int)(blockIdx.x % nbands);   // index 0 of a triplet: the bottom band
-    const int y0 = brows * band, y1 = min( y0 + brows, mbh );
+    int s1, y0, y1;                               // the band's rows [y0, y1) of a slice ending at s1
+    lr_band( (int)(blockIdx.x % nbands), mbh, nslices, brows, s1, y0, y1 );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     a0 += (intptr_t)f * afs; a1 += (intptr_t)f * afs; a2 += (intptr_t)f * afs; a3 += (intptr_t)f * afs;
@@ -1026,11 +1050,11 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const int rl = (int)(threadIdx.x & 15);      // lane within the role: 4 * row + q
     const int y = y0 + (rl >> 2);
     const bool mine = role < 3 && y < y1;
-    const int t0 = 2 * (mbh - y1), t1 = 2 * (mbh - 1 - y0) + mbw - 1;
+    const int t0 = 2 * (s1 - y1), t1 = 2 * (s1 - 1 - y0) + mbw - 1;
     // a row's next block is x - 1: its fenc rows are fetched one step ahead
     uint32_t fnext[LR_NR][NDW];
     auto fetch = [&]( int t ) {
-        const int xn = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        const int xn = mbw - 1 - (t - 2 * (s1 - 1 - y));
         if( mine && xn >= 0 && xn < mbw )
             lr_load_fenc<BD>( fenc + 8 * (intptr_t)xn + (intptr_t)(8 * y + LR_NR * q) * stride, stride, fnext );
     };
@@ -1038,7 +1062,7 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     fetch( t0 );
     for( int t = t0; t <= t1; t++ )
     {
-        const int x = mbw - 1 - (t - 2 * (mbh - 1 - y));
+        const int x = mbw - 1 - (t - 2 * (s1 - 1 - y));
         uint32_t fe[LR_NR][NDW];
 #pragma unroll
         for( int r = 0; r < LR_NR; r++ )
@@ -1069,7 +1093,7 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
                 if( search & (1 << role) )
                 {
                     uint32_t pred[4];
-                    const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, mbh, pred, poll_max, status );
+                    const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, s1, pred, poll_max, status );
                     // the searching lanes run one instruction stream: a failed wait stops them all
                     failed = __builtin_amdgcn_ballot_w64( np < 0 ) != 0;
                     if( !failed )
@@ -1235,6 +1259,15 @@ hipError_t la_status_end( hipStream_t stream )
     return *(volatile uint32_t *)st.host ? hipErrorLaunchTimeOut : hipSuccess;
 }
 
+// bands per frame over the lookahead slices (lr_band)
+int la_nbands( int mbh, int nslices, int brows )
+{
+    int n = 0;
+    for( int i = 0; i < nslices; i++ )
+        n += ((mbh * (i + 1) + nslices / 2) / nslices - (mbh * i + nslices / 2) / nslices + brows - 1) / brows;
+    return n;
+}
+
 int la_poll_max()
 {
     const int v = variant( V_LA_POLL );
@@ -1250,7 +1283,7 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                 int lambda, const uint16_t *cost_mv, int search, int16_t *mvs0, int32_t *costs0,
                                 int16_t *mvs1, int32_t *costs1, const int16_t *p1mvs, int dsf, int weight,
                                 const uint16_t *invq, uint16_t *lowres_costs, int32_t *row_satd, int32_t *est,
-                                hipStream_t stream )
+                                int nslices, hipStream_t stream )
 {
     if( n <= 0 || mbw <= 0 || mbh <= 0 )
         return hipSuccess;
@@ -1273,8 +1306,8 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
     const int bv = variant( V_LA_BAND );
     const int brows = bv >= 1 && bv <= LR_BAND ? bv : 4;
     const int brows4 = min( brows, 4 );          // a wave holds four roles of <= 4 rows
-    const int nbands = (mbh + brows4 - 1) / brows4;
-    if( (int64_t)n * nbands > 0x7fffffff )
+    const int nbands = la_nbands( mbh, nslices, brows4 );
+    if( nslices < 1 || (int64_t)n * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
     if( mv_range < 1 || lds > 48 * 1024 )
@@ -1285,7 +1318,7 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
     hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ra[0], ra[1],
                         ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method, subme, satd,
                         me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, weight,
-                        invq, lowres_costs, row_satd, est, nbands, brows4, la_poll_max(), status );
+                        invq, lowres_costs, row_satd, est, nbands, brows4, la_poll_max(), status, nslices );
     if( (e = hipGetLastError()) != hipSuccess )
         return e;
     return (search & 3) ? la_status_end( stream ) : hipSuccess;
@@ -1298,7 +1331,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                 int lambda, const uint16_t *cost_mv, const uint16_t *intra_cost,
                                 const uint16_t *invq, int16_t *mvs, int32_t *mv_costs, uint16_t *lowres_costs,
                                 int32_t *row_satd, int32_t *est, const typename PT<BD>::pixel *ref_w, int wscale,
-                                int wdenom, int woffset, hipStream_t stream )
+                                int wdenom, int woffset, int nslices, hipStream_t stream )
 {
     if( npairs <= 0 || mbw <= 0 || mbh <= 0 )
         return hipSuccess;
@@ -1315,8 +1348,8 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     const int bv = variant( V_LA_BAND );
     const int brows = bv >= 1 && bv <= LR_BAND ? bv : 4;
     const int brows4 = min( brows, 4 );          // four groups of <= 4 rows per wave
-    const int nbands = (mbh + brows4 - 1) / brows4;
-    if( (int64_t)npairs * nbands > 0x7fffffff )
+    const int nbands = la_nbands( mbh, nslices, brows4 );
+    if( nslices < 1 || (int64_t)npairs * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
     if( mv_range < 1 || lds > 48 * 1024 )
@@ -1327,7 +1360,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ref[0],
                         ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
                         lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4,
-                        la_poll_max(), status, ref_w, wscale, wdenom, woffset );
+                        la_poll_max(), status, ref_w, wscale, wdenom, woffset, nslices );
     if( (e = hipGetLastError()) != hipSuccess )
         return e;
     return la_status_end( stream );
@@ -1338,7 +1371,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                                                  intptr_t, intptr_t, int, int, int, int, int, int, int, int, int, \
                                                  const uint16_t *, const uint16_t *, const uint16_t *, int16_t *, \
                                                  int32_t *, uint16_t *, int32_t *, int32_t *,                     \
-                                                 const PT<BD>::pixel *, int, int, int, hipStream_t );
+                                                 const PT<BD>::pixel *, int, int, int, int, hipStream_t );
 INST( 8 )
 INST( 10 )
 #undef INST
@@ -1347,7 +1380,7 @@ INST( 10 )
                                                  intptr_t, const PT<BD>::pixel *const[4], intptr_t, intptr_t, int,  \
                                                  int, int, int, int, int, int, int, int, const uint16_t *, int,     \
                                                  int16_t *, int32_t *, int16_t *, int32_t *, const int16_t *, int,  \
-                                                 int, const uint16_t *, uint16_t *, int32_t *, int32_t *,           \
+                                                 int, const uint16_t *, uint16_t *, int32_t *, int32_t *, int,      \
                                                  hipStream_t );
 INST( 8 )
 INST( 10 )
