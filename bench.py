@@ -45,10 +45,12 @@ def parse():
     # default warmup covers the ramp; every step is still a full launch over F pairs
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=150)
-    # 64 pairs per headline step: a 1.1-ms launch, so the driver's 5 warmup steps already
-    # carry the GPU through most of its ~20-ms clock transient (profiles/r03a_trace_*: after
-    # an idle gap the first launches of the 16-pair step ran 12-30 % slow)
-    ap.add_argument("--frames", type=int, default=64, help="frame pairs per headline step per GPU")
+    # 128 pairs per headline step: a 2.2-ms launch, so the driver's 5 warmup steps carry the
+    # GPU through most of its ~20-ms clock transient (profiles/r03a_trace_*: after an idle gap
+    # the first launches of a 16-pair step ran 12-30 % slow).  Under the driver's arguments
+    # (--steps 20 --warmup 5): 16 pairs 0.65, 64 pairs 0.77, 128 pairs 0.81 of the SAD
+    # roofline (profiles/r03l_batch/); steady state is 0.82-0.84 at any batch
+    ap.add_argument("--frames", type=int, default=128, help="frame pairs per headline step per GPU")
     ap.add_argument("--xframes", type=int, default=16, help="frame pairs of the side legs (<= --frames)")
     # the streaming transform kernels (DCT+quant, reconstruction) move ~8.5 MB per 1080p
     # frame; SURVEY.md §8d (configs[3]) asks for >= 64 frames per launch so the launch
@@ -300,6 +302,12 @@ def main():
 def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=None):
     """configs[2] side rates on the same frames: SATD 8x8 candidates/s and fused
     DCT+quant blocks/s (QP 26, flat16 CQM, inter-luma lists, zero-MV prediction)."""
+    # configs[3]'s streaming leg first: after any leg that captured and replayed a HIP graph,
+    # this process's two-stream upload / search overlap measured ~25 % slower (0.175 -> 0.22 ms
+    # per 2160p frame whichever graph-timed leg ran before it, GPU_MAX_HW_QUEUES 4, 8 or 16
+    # alike; profiles/r03o_after.log, r03p_after.log) -- a runtime interaction not isolated
+    # further, noted in DESIGN.md §6
+    r2160 = rates_2160p(x, a, world)
     res = {}
     flat = [16] * 64
     q4m, q4b, q8m, q8b = x.cqm_init(8, [flat] * 8)
@@ -518,7 +526,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
         res.update({k.replace("ssd_plane", "ssd_plane_%d" % a.tframes): v for k, v in r64.items()})
     res.update(rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
-    res.update(rates_2160p(x, a, world))
+    res.update(r2160)
     return res
 
 

@@ -1205,18 +1205,14 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
 // batch is needed; the poll bound (X264HIP_LA_POLL, default 2^22 tries) turns a broken
 // premise (preemption, a changed dispatcher) into this error rather than a hang.
 namespace {
+// (no destructor: the words live as long as the process -- freeing them from a
+// thread-exit destructor can run after the HIP runtime has been torn down, which
+// crashed the process at exit under rocprofv3)
 struct LaStatus
 {
     int device = -1;
     uint32_t *dev = nullptr;
     uint32_t *host = nullptr;
-    ~LaStatus()
-    {
-        if( dev )
-            (void)hipFree( dev );
-        if( host )
-            (void)hipHostFree( host );
-    }
 };
 thread_local LaStatus t_la_status;
 
