@@ -791,6 +791,7 @@ def rates_2160p(x, a, world):
         streaming()
     res["2160p_pcie_kernel_host_enqueue_ms"] = (time.perf_counter() - t0) / a.steps * 1e3
     torch.cuda.synchronize()
+    x.stream_pair_destroy(split)
     best = max(("sdma", "kernel"), key=lambda h: res[f"2160p_pcie_{h}_candidates_per_s"])
     res["2160p_pcie_inclusive_candidates_per_s"] = res[f"2160p_pcie_{best}_candidates_per_s"]
     res["2160p_pcie_inclusive_frame_ms"] = res[f"2160p_pcie_{best}_frame_ms"]

@@ -28,7 +28,7 @@ __all__ = [
     "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
-    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "me_search_full8",
+    "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "stream_pair_destroy", "me_search_full8",
 ]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
@@ -141,6 +141,15 @@ def stream_pair(reserve_cus=16):
     a, b = _c.c_void_p(), _c.c_void_p()
     _rc(lib().x264hip_stream_pair_create(reserve_cus, _c.byref(a), _c.byref(b)), "stream_pair_create")
     return torch.cuda.ExternalStream(a.value), torch.cuda.ExternalStream(b.value)
+
+
+def stream_pair_destroy(pair):
+    """Release the streams of stream_pair() (after a device synchronise; the torch wrappers must
+    not be used afterwards)."""
+    import torch
+    torch.cuda.synchronize()
+    for st in pair:
+        _rc(lib().x264hip_stream_destroy(_c.c_void_p(st.cuda_stream)), "stream_destroy")
 
 
 # ----------------------------------------------------------------- tables
