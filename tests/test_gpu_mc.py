@@ -22,14 +22,17 @@ def _host(t, bd):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("size", [(1920, 1088), (80, 48), (176, 144)])
-@pytest.mark.parametrize("variant", ["default", "0", "1", "2", "4", "5"])
+@pytest.mark.parametrize("variant", ["default", "nt", "0", "1", "2", "3", "4", "5", "6"])
 def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
-    """X264HIP_HPEL_VARIANT: default = streaming lanes at 8 bit with packed shift-saturate
-    stores (3) / fused tiles at 10 bit, 0 = fused single pass over LDS tiles, 1 = interior
-    tiles + border expand, 2 = streaming lanes with scaled clamps (med3 + byte picks),
-    4 / 5 = variants 2 / 3 under a 4-waves-per-SIMD register budget."""
-    if variant == "default":
+    """X264HIP_HPEL_VARIANT: default = at 8 bit streaming lanes with counted source-row waits
+    and branch-free buffer stores (7) / fused tiles at 10 bit, 0 = fused single pass over LDS
+    tiles, 1 = interior tiles + border expand, 2 = streaming lanes with scaled clamps (med3 +
+    byte picks), 3 = streaming lanes with packed shift-saturate (7's arithmetic, compiler
+    waits), 4 / 5 = variants 2 / 3 under a 4-waves-per-SIMD register budget, 6 = 3 as a
+    persistent grid; nt = the default with nontemporal stores forced (X264HIP_STREAM_NT=1)."""
+    if variant in ("default", "nt"):
         _x().set_variant("X264HIP_HPEL_VARIANT", None)
+        _x().set_variant("X264HIP_STREAM_NT", 1 if variant == "nt" else None)
     else:
         _x().set_variant("X264HIP_HPEL_VARIANT", variant)
     from x264hip import synth
@@ -47,7 +50,7 @@ def test_hpel_filter(hip, oracle, bd, size, variant, monkeypatch):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("variant", ["default", "2", "4", "5"])
+@pytest.mark.parametrize("variant", ["default", "2", "3", "4", "5"])
 def test_hpel_filter_extremes(hip, oracle, bd, variant):
     """Pixels 0 / PIXEL_MAX only, so the 6-tap sums reach both ends of every clip
     (H and V: -10 * max .. 42 * max before the shift; centre far beyond int16)."""
@@ -141,11 +144,14 @@ def test_subpel_qpel9_random(hip, oracle, bd, op):
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("size", [(1920, 1088), (176, 144), (72, 40), (3840, 2160), (48, 32)])
-@pytest.mark.parametrize("variant", ["default", "1", "2", "3", "4"])
+@pytest.mark.parametrize("variant", ["default", "nt", "1", "2", "3", "4"])
 def test_frame_init_lowres(hip, oracle, bd, size, variant):
-    """x264_frame_init_lowres of 3 frames per call vs the oracle (every kernel variant); the
-    source padding holds unrelated values (the reference duplicates column W / row H itself)."""
-    if variant != "default":
+    """x264_frame_init_lowres of 3 frames per call vs the oracle (every kernel variant; nt = the
+    default with nontemporal stores and XCD-contiguous row blocks forced, X264HIP_STREAM_NT=1);
+    the source padding holds unrelated values (the reference duplicates column W / row H itself)."""
+    if variant == "nt":
+        _x().set_variant("X264HIP_STREAM_NT", 1)
+    elif variant != "default":
         _x().set_variant("X264HIP_LOWRES_VARIANT", variant)
     W, H = size
     n = 3

@@ -1,9 +1,8 @@
 #!/usr/bin/env python3
 """A/B of the 8-bit streaming frame kernels' launch forms, 16 and 64 1080p frames per launch,
 interleaved rounds after a clock warmup; every form's outputs must equal the default's.
-hpel_filter: X264HIP_HPEL_VARIANT 3 (one-shot strips) with X264HIP_STREAM_XCD 0 / 1, and 6
-(persistent grid-stride strips); frame_init_lowres: the default two-row kernel with
-XCD 0 / 1 and X264HIP_LOWRES_VARIANT 5 (persistent).  Usage: stream_var_ab.py [out.json]"""
+hpel_filter (X264HIP_HPEL_VARIANT 3, and 7 with default / forced nontemporal / plain stores) and
+frame_init_lowres (the default two-row kernel with default / nontemporal / plain stores).  Usage: stream_var_ab.py [out.json]"""
 import json
 import os
 import sys
@@ -21,13 +20,14 @@ from x264hip import synth  # noqa: E402
 W, H = 1920, 1088
 planes, stride, origin = synth.make_sequence(64, W, H, 8)
 full = torch.from_numpy(planes).cuda()
-CONF = {"hpel": [{"X264HIP_HPEL_VARIANT": 3, "X264HIP_STREAM_XCD": 0},
-                 {"X264HIP_HPEL_VARIANT": 3, "X264HIP_STREAM_XCD": 1},
-                 {"X264HIP_HPEL_VARIANT": 6}],
-        "lowres": [{"X264HIP_LOWRES_VARIANT": -1, "X264HIP_STREAM_XCD": 0},
-                   {"X264HIP_LOWRES_VARIANT": -1, "X264HIP_STREAM_XCD": 1},
-                   {"X264HIP_LOWRES_VARIANT": 5}]}
-NAMES = ("X264HIP_HPEL_VARIANT", "X264HIP_STREAM_XCD", "X264HIP_LOWRES_VARIANT")
+CONF = {"hpel": [{"X264HIP_HPEL_VARIANT": 3, "X264HIP_STREAM_NT": 0},
+                 {"X264HIP_HPEL_VARIANT": 3},
+                 {"X264HIP_HPEL_VARIANT": 7},
+                 {"X264HIP_HPEL_VARIANT": 7, "X264HIP_STREAM_NT": 0},
+                 {"X264HIP_HPEL_VARIANT": 7, "X264HIP_STREAM_XCD": 0}],
+        "lowres": [{"X264HIP_LOWRES_VARIANT": -1},
+                   {"X264HIP_LOWRES_VARIANT": -1, "X264HIP_STREAM_NT": 0}]}
+NAMES = ("X264HIP_HPEL_VARIANT", "X264HIP_STREAM_XCD", "X264HIP_LOWRES_VARIANT", "X264HIP_STREAM_NT")
 
 
 def setc(c):
@@ -48,8 +48,9 @@ for F in (16, 64):
         setc(c)
         lo.append(x.frame_init_lowres(dev, origin, stride, W, H)[0])
     torch.cuda.synchronize()
-    for i in range(1, 3):
+    for i in range(1, len(CONF["hpel"])):
         assert all(torch.equal(a, b) for a, b in zip(hv[0], hv[i])), ("hpel form changed the output", i)
+    for i in range(1, len(CONF["lowres"])):
         assert all(torch.equal(a, b) for a, b in zip(lo[0], lo[i])), ("lowres form changed the output", i)
     lbytes = fb + 4 * lo[0][0][0].numel()
     legs = {"hpel": (lambda i: x.hpel_filter(dev, origin, stride, W, H, outs=hv[i]), 4 * fb),

@@ -667,7 +667,7 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_band_kernel(
 // Variant 5 (transform 4): as variant 3 with 8 MBs per wave: lane = (band, MB,
 // half) reads 8 pixels per row and transforms two 4x4 blocks; half the LDS per
 // wave (more resident waves) and twice the waves (a shorter tail).
-template <int BD>
+template <int BD, bool NT = false>
 __global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
     const typename PT<BD>::pixel *__restrict__ pred, intptr_t ps, intptr_t pfs, int mbw, int mbh, int nframes,
@@ -736,7 +736,7 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
     const uint4 *src = (const uint4 *)stage;
     uint4 *dst = (uint4 *)(dct + (mbrow + strip * 8) * 256);
     for( int i = lane; i < nvec; i += 64 )
-        dst[i] = src[i];
+        st16<NT>( dst + i, src[i] );
 }
 
 // Variant 6 (8 bit, transform 8, the default there): sub8x8_dct8 + quant_8x8 on
@@ -779,7 +779,7 @@ __device__ __forceinline__ uint32_t dq_asu( dq_s2 v ) { return __builtin_bit_cas
         D( 7, ( a4 >> 2 ) - a7 );                                                       \
     }
 
-template <bool STAGE>
+template <bool STAGE, bool NT = false>
 __global__ __launch_bounds__( 256 ) void mb_dct8_quant_pk_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                   intptr_t ffs, const uint8_t *__restrict__ pred,
                                                                   intptr_t ps, intptr_t pfs, int mbw, int mbh,
@@ -902,7 +902,7 @@ __global__ __launch_bounds__( 256 ) void mb_dct8_quant_pk_kernel( const uint8_t 
     {
         const int s = i >> 3;
         const int k = (((s >> 2) * 2 + (s & 1)) & 7);        // the writer's key
-        dst[i] = stage[s * 8 + ((i & 7) ^ k)];
+        st16<NT>( dst + i, stage[s * 8 + ((i & 7) ^ k)] );
     }
 }
 #undef DCT8_1D_PK
@@ -927,11 +927,18 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
         dim3 blk( 256 ), g( (unsigned)((waves + 3) / 4) );
         // transform 4 default: variant 5 (0.62-0.71 of HBM vs 0.50-0.52 for variant 0,
         // tools/dq_variants.py); X264HIP_DQ_VARIANT=0 selects the 16-MB staged strip
+        // nontemporal coefficient stores (stream_nt): 64 frames 4x4 0.0985 -> 0.0876 ms, 8x8
+        // 0.1029 -> 0.0776 ms; 16 frames 0.0279 -> 0.0267, 0.0263 -> 0.0247 (profiles/r03s_nt_ab.json)
+        const bool nt = stream_nt();
         if( transform == 4 && (ev < 0 || ev == 5) )
         {
             const int64_t hw = (int64_t)nframes * mbh * ((mbw + 7) / 8);
-            hipLaunchKernelGGL( mb_dct_quant_halfband_kernel<BD>, dim3( (unsigned)((hw + 3) / 4) ), blk, 0, stream, fenc,
-                                fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+            if( nt )
+                hipLaunchKernelGGL( ( mb_dct_quant_halfband_kernel<BD, true> ), dim3( (unsigned)((hw + 3) / 4) ), blk,
+                                    0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+            else
+                hipLaunchKernelGGL( mb_dct_quant_halfband_kernel<BD>, dim3( (unsigned)((hw + 3) / 4) ), blk, 0, stream,
+                                    fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
             return hipGetLastError();
         }
         if( transform == 4 && (ev == 3 || ev == 4) )
@@ -949,7 +956,10 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
         if constexpr( BD == 8 )
             if( transform == 8 && (ev < 0 || ev == 6 || ev == 7) )
             {
-                if( ev < 0 || ev == 6 )
+                if( (ev < 0 || ev == 6) && nt )
+                    hipLaunchKernelGGL( ( mb_dct8_quant_pk_kernel<true, true> ), g, blk, 0, stream, fenc, fs, ffs, pred,
+                                        ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+                else if( ev < 0 || ev == 6 )
                     hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<true>, g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs,
                                         mbw, mbh, nframes, mf, bias, dct, nz );
                 else

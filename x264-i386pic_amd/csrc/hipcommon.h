@@ -196,7 +196,7 @@ template <int BD> __device__ __forceinline__ int upix( uint32_t w, int k )
 namespace x264hip {
 enum VariantSlot
 {
-    V_ME = 0, V_HPEL, V_HPEL_ROWS, V_SUBPEL, V_LOWRES, V_DQ, V_RECON, V_LOWRES_INTRA, V_LA_BAND, V_ME_LEAD, V_TESA, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_COUNT
+    V_ME = 0, V_HPEL, V_HPEL_ROWS, V_SUBPEL, V_LOWRES, V_DQ, V_RECON, V_LOWRES_INTRA, V_LA_BAND, V_ME_LEAD, V_TESA, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_STREAM_NT, V_COUNT
 };
 int variant( VariantSlot slot );
 
@@ -226,6 +226,28 @@ __device__ __forceinline__ Blk3 blk3( bool xcd )
     const uint32_t l = xcd_block( lin, gx * gy * gridDim.z );
     const uint32_t yz = l / gx;
     return { l - yz * gx, yz % gy, yz / gy };
+}
+
+// Store policy of the streaming frame kernels (half-pel planes, lowres planes, fused
+// DCT+quant coefficients): nontemporal stores unless X264HIP_STREAM_NT=0.  With every
+// wave's stores on whole 128-B lines they stream faster at any batch
+// (profiles/r03r_pattern.txt: the 1-in-3-out pattern at 64 padded 1080p frames 0.575 ->
+// 0.853 of 8 TB/s; r03s_nt_ab.json / r03w_stream_var.json for the kernels at 16 and 64
+// frames).  Nontemporal stores of partial lines -- 62-piece chunks, every wave boundary
+// mid-line -- were as slow as plain ones (0.569, the pattern `s3nt62u`).
+inline bool stream_nt()
+{
+    return variant( V_STREAM_NT ) != 0;
+}
+
+// a 16-byte store, nontemporal when NT
+template <bool NT> __device__ __forceinline__ void st16( void *p, uint4 v )
+{
+    typedef unsigned int v4u __attribute__( ( ext_vector_type( 4 ) ) );
+    if constexpr( NT )
+        __builtin_nontemporal_store( (v4u){ v.x, v.y, v.z, v.w }, (v4u *)p );
+    else
+        *(uint4 *)p = v;
 }
 } // namespace x264hip
 

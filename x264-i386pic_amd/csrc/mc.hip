@@ -7,6 +7,7 @@
 #include "hipcommon.h"
 
 #include <stdlib.h>
+#include <type_traits>
 
 namespace x264hip {
 
@@ -374,7 +375,7 @@ template <int HI, int BY> __device__ __forceinline__ uint32_t pack_clip4( const 
     return __builtin_amdgcn_perm( b[1], b[0], lo ) | __builtin_amdgcn_perm( b[3], b[2], hi );
 }
 
-template <int HS_ROWS, bool PK>
+template <int HS_ROWS, bool PK, bool NT = false>
 __device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
                                                   uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
                                                   intptr_t stride, intptr_t fstride, int width, int height,
@@ -523,14 +524,14 @@ __device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ sr
                 for( int yy = ya; yy <= yb; yy++ )
                 {
                     const intptr_t o0 = fo + (intptr_t)yy * stride;
-                    *(uint4 *)(dh + o0) = vh;
-                    *(uint4 *)(dv + o0) = vv;
-                    *(uint4 *)(dc + o0) = vc;
+                    st16<NT>( dh + o0, vh );
+                    st16<NT>( dv + o0, vv );
+                    st16<NT>( dc + o0, vc );
                     if( ox )
                     {
-                        *(uint4 *)(dh + o0 + ox) = eh;
-                        *(uint4 *)(dv + o0 + ox) = ev;
-                        *(uint4 *)(dc + o0 + ox) = ec;
+                        st16<NT>( dh + o0 + ox, eh );
+                        st16<NT>( dv + o0 + ox, ev );
+                        st16<NT>( dc + o0 + ox, ec );
                     }
                 }
             }
@@ -538,14 +539,14 @@ __device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ sr
     }
 }
 
-template <int HS_ROWS, bool PK>
+template <int HS_ROWS, bool PK, bool NT = false>
 __global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
                                                              uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
                                                              intptr_t stride, intptr_t fstride, int width,
                                                              int height, int hbias, int cbias, int xcd )
 {
-    hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias, blk3( xcd ),
-                                   (int)gridDim.y - 4 );
+    hpel_stream_body<HS_ROWS, PK, NT>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias, blk3( xcd ),
+                                       (int)gridDim.y - 4 );
 }
 
 // persistent form (variant 6): a resident grid of single-wave workgroups walks the
@@ -576,6 +577,205 @@ __global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) )
                                    (int)gridDim.y - 4 );
 }
 
+// Variant 7 (8-bit default): variant 3's streaming strips with every wave's stores on whole
+// 128-B lines.  Variant 3's waves own 62 column quads (992 bytes of each output row), so
+// every wave boundary splits a line between two waves -- often on two XCDs -- and the
+// partial lines streamed no faster than 0.57 of HBM even with nontemporal stores (the
+// pattern alone: profiles/r03v_pattern64.txt, `s3nt62u` 0.569 vs 0.823 line-aligned).  Here a
+// wave owns 64 16-pixel pieces of x in [-32, W+32) (1 KB, line-aligned), its edge lanes
+// fetch their outer neighbour's dword from memory instead of by DPP, and the replicated
+// border pieces are ordinary lanes: 64 frames 0.1383 -> 0.0927 ms (0.53 -> 0.79 of HBM),
+// 16 frames 0.0312 -> 0.0267 ms with nontemporal stores (profiles/r03w_stream_var.json).
+// Also: a slot is unpacked before it is reloaded (one register tuple, no loop-carried copy:
+// 118 VGPRs, 4 waves per SIMD against variant 3's 140 and 3); every row issues the same
+// three buffer stores (lanes past the row address beyond the buffer's range, so the store
+// is dropped); the source pointer is not __restrict__ and each reload is followed by a
+// compiler memory barrier (as invariant loads the compiler sank the reloads to the end of
+// the six-row group, leaving one row of lead).  The compiler's waitcnt pass, with loads
+// and stores both in flight, waits vmcnt(0) once per six rows.  (Counted waits on asm
+// loads were tried: the compiler copied and reused the registers of loads it could not
+// see in flight.)  The four border strips (rows -32..-9 / H+8..H+31, replicas of rows -8 /
+// H+7) take their own path.
+template <bool NT>
+__device__ __forceinline__ void st16b( uint4 v, __amdgpu_buffer_rsrc_t r, uint32_t off )
+{
+    typedef unsigned int v4u __attribute__( ( ext_vector_type( 4 ) ) );
+    __builtin_amdgcn_raw_buffer_store_b128( (v4u){ v.x, v.y, v.z, v.w }, r, (int)off, 0, NT ? 2 : 0 );
+}
+
+typedef unsigned int hv4u __attribute__( ( ext_vector_type( 4 ) ) );
+
+template <int HS_ROWS, bool NT, bool BORDER>
+__device__ __forceinline__ void hpel_strip7( const uint8_t *src, uint8_t *__restrict__ dh,
+                                             uint8_t *__restrict__ dv, uint8_t *__restrict__ dc, intptr_t stride,
+                                             intptr_t fstride, int width, int height, Blk3 B, int nstrips )
+{
+    // 16-pixel pieces p over x in [-32, W+32): a wave owns 64 of them (1 KB of each output row,
+    // on the 128-B line grid), lane L piece 64 * chunk + L.  q = p - 1 is variant 3's column
+    // quad (x0 = -16 + 16 q); q = -1 / q = nq are the replicated 16-pixel border pieces.
+    const int lane = threadIdx.x & 63;
+    const int nq = (width + 32) >> 4, np = nq + 2;
+    const int chunk = (int)B.x;
+    if( chunk * 64 >= np )
+        return;
+    const int p = chunk * 64 + lane, q = p - 1;
+    const bool st = p < np;
+    const int x0 = -16 + 16 * min( q, nq );                 // lanes past the row load the last piece
+    // lanes 0 / 63 take their outer neighbour's dword from memory, the others by DPP
+    const int xn = lane == 0 ? max( x0 - 4, -32 ) : lane == 63 ? x0 + 16 : x0;
+    const int sy = (int)B.y - nstrips;
+    const int r0 = !BORDER ? -8 + (int)B.y * HS_ROWS : sy < 2 ? -8 : height + 7;
+    const int r1 = !BORDER ? min( r0 + HS_ROWS, height + 8 ) : r0 + 1;
+    const int b0 = !BORDER ? 0 : sy < 2 ? -32 + 12 * sy : height + 8 + 12 * (sy - 2);
+    const uint8_t *sp = src + (intptr_t)B.z * fstride + x0;
+    const uint8_t *spn = src + (intptr_t)B.z * fstride + xn;
+    auto ld = [&]( int row ) { return *(const hv4u *)(sp + (intptr_t)row * stride); };
+    auto ldn = [&]( int row ) { return *(const uint32_t *)(spn + (intptr_t)row * stride); };
+    // the frame's three output planes from row -32, column -32: byte offsets below 2^31
+    const intptr_t fb = (intptr_t)B.z * fstride - 32 * stride - 32;
+    const __amdgpu_buffer_rsrc_t rh = __builtin_amdgcn_make_buffer_rsrc( dh + fb, (short)0, 0x7fffffff, 0x00020000 );
+    const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc( dv + fb, (short)0, 0x7fffffff, 0x00020000 );
+    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc( dc + fb, (short)0, 0x7fffffff, 0x00020000 );
+    constexpr uint32_t OOB = 0x80000000u;                   // >= the range: the store is dropped
+    const uint32_t xo = st ? (uint32_t)(16 * p) : OOB;
+    auto unpack = [&]( hv4u d, uint32_t n, hs2 (&P)[11] ) {
+        uint32_t dl = (uint32_t)__builtin_amdgcn_mov_dpp( (int)d.w, 0x138, 0xF, 0xF, true );   // lane - 1
+        uint32_t dr = (uint32_t)__builtin_amdgcn_mov_dpp( (int)d.x, 0x130, 0xF, 0xF, true );   // lane + 1
+        dl = lane == 0 ? n : dl;
+        dr = lane == 63 ? n : dr;
+        P[0] = as_s2( __builtin_amdgcn_perm( 0u, dl, 0x0c030c02u ) );
+        const uint32_t w[4] = { d.x, d.y, d.z, d.w };
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+        {
+            P[1 + 2 * j] = as_s2( __builtin_amdgcn_perm( 0u, w[j], 0x0c010c00u ) );
+            P[2 + 2 * j] = as_s2( __builtin_amdgcn_perm( 0u, w[j], 0x0c030c02u ) );
+        }
+        P[9] = as_s2( __builtin_amdgcn_perm( 0u, dr, 0x0c010c00u ) );
+        P[10] = as_s2( __builtin_amdgcn_perm( 0u, dr, 0x0c030c02u ) );
+    };
+    uint32_t k15u, k01u;
+    asm( "v_mov_b32 %0, 0xfffb0001" : "=v"( k15u ) );
+    asm( "v_mov_b32 %0, 0x10000" : "=v"( k01u ) );
+    const hs2 k15 = as_s2( k15u ), k01 = as_s2( k01u );
+    hs2 win[6][11];
+    hv4u raw[6];
+    uint32_t rawn[6];
+#pragma unroll
+    for( int k = 0; k < 5; k++ )
+    {
+        raw[k] = ld( r0 - 2 + k );
+        rawn[k] = ldn( r0 - 2 + k );
+    }
+#pragma unroll
+    for( int k = 0; k < 5; k++ )
+        unpack( raw[k], rawn[k], win[k] );
+#pragma unroll
+    for( int k = 0; k < 6; k++ )
+    {
+        raw[k] = ld( r0 + 3 + k );
+        rawn[k] = ldn( r0 + 3 + k );
+    }
+    auto do_row = [&]( auto K, const int y ) {
+        constexpr int k = decltype( K )::value;
+        unpack( raw[k], rawn[k], win[(k + 5) % 6] );
+        const int yl = min( y + 9, r1 + 2 );                // past the strip's last source row: a repeat
+        raw[k] = ld( yl );
+        rawn[k] = ldn( yl );
+        asm volatile( "" ::: "memory" );                    // keep the loads six rows ahead of their use
+        hs2 vi[11], hrow[11];
+#pragma unroll
+        for( int j = 0; j < 11; j++ )
+        {
+            const hs2 a = win[k % 6][j], b = win[(k + 1) % 6][j], c = win[(k + 2) % 6][j];
+            const hs2 d = win[(k + 3) % 6][j], e = win[(k + 4) % 6][j], f = win[(k + 5) % 6][j];
+            vi[j] = (a + f) + (c + d) * (hs2)20 - (b + e) * (hs2)5;
+            hrow[j] = c;
+        }
+        uint32_t oh[4], ov[4], oc[4];
+        int o[4];
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+            ov[j] = __builtin_amdgcn_perm( sat_pk_u8( (vi[2 + 2 * j] + (hs2)16) >> (hs2)5 ),
+                                           sat_pk_u8( (vi[1 + 2 * j] + (hs2)16) >> (hs2)5 ), 0x05040100u );
+        tap6_h4v<0, 16>( hrow, k15, k01, o ); oh[0] = pack_shr4<5>( o );
+        tap6_h4v<2, 16>( hrow, k15, k01, o ); oh[1] = pack_shr4<5>( o );
+        tap6_h4v<4, 16>( hrow, k15, k01, o ); oh[2] = pack_shr4<5>( o );
+        tap6_h4v<6, 16>( hrow, k15, k01, o ); oh[3] = pack_shr4<5>( o );
+        tap6_h4v<0, 512>( vi, k15, k01, o ); oc[0] = pack_shr4<10>( o );
+        tap6_h4v<2, 512>( vi, k15, k01, o ); oc[1] = pack_shr4<10>( o );
+        tap6_h4v<4, 512>( vi, k15, k01, o ); oc[2] = pack_shr4<10>( o );
+        tap6_h4v<6, 512>( vi, k15, k01, o ); oc[3] = pack_shr4<10>( o );
+        // the edge quads: x -16..-5 take pixel -4 / x W+4..W+15 take pixel W+3; the border pieces
+        // (q = -1 / nq) are those pixels repeated, taken from the neighbouring lane
+        const bool lo = q == 0, hi = q == nq - 1, mid = lo || hi;
+        uint32_t selh = lo ? __builtin_amdgcn_perm( 0u, oh[3], 0 ) : __builtin_amdgcn_perm( 0u, oh[0], 0x03030303u );
+        uint32_t selv = lo ? __builtin_amdgcn_perm( 0u, ov[3], 0 ) : __builtin_amdgcn_perm( 0u, ov[0], 0x03030303u );
+        uint32_t selc = lo ? __builtin_amdgcn_perm( 0u, oc[3], 0 ) : __builtin_amdgcn_perm( 0u, oc[0], 0x03030303u );
+        const uint32_t rh_ = (uint32_t)__builtin_amdgcn_mov_dpp( (int)selh, 0x130, 0xF, 0xF, true );
+        const uint32_t rv_ = (uint32_t)__builtin_amdgcn_mov_dpp( (int)selv, 0x130, 0xF, 0xF, true );
+        const uint32_t rc_ = (uint32_t)__builtin_amdgcn_mov_dpp( (int)selc, 0x130, 0xF, 0xF, true );
+        const uint32_t lh_ = (uint32_t)__builtin_amdgcn_mov_dpp( (int)selh, 0x138, 0xF, 0xF, true );
+        const uint32_t lv_ = (uint32_t)__builtin_amdgcn_mov_dpp( (int)selv, 0x138, 0xF, 0xF, true );
+        const uint32_t lc_ = (uint32_t)__builtin_amdgcn_mov_dpp( (int)selc, 0x138, 0xF, 0xF, true );
+        const bool bl = q == -1, br = q == nq, bd = bl || br;
+        selh = bl ? rh_ : br ? lh_ : selh;
+        selv = bl ? rv_ : br ? lv_ : selv;
+        selc = bl ? rc_ : br ? lc_ : selc;
+        const uint4 vh = make_uint4( lo || bd ? selh : oh[0], mid || bd ? selh : oh[1], mid || bd ? selh : oh[2],
+                                     hi || bd ? selh : oh[3] );
+        const uint4 vv = make_uint4( lo || bd ? selv : ov[0], mid || bd ? selv : ov[1], mid || bd ? selv : ov[2],
+                                     hi || bd ? selv : ov[3] );
+        const uint4 vc = make_uint4( lo || bd ? selc : oc[0], mid || bd ? selc : oc[1], mid || bd ? selc : oc[2],
+                                     hi || bd ? selc : oc[3] );
+        if constexpr( !BORDER )
+        {
+            const uint32_t ro = (uint32_t)((y + 32) * stride);
+            st16b<NT>( vh, rh, xo + ro );
+            st16b<NT>( vv, rv, xo + ro );
+            st16b<NT>( vc, rc, xo + ro );
+        }
+        else
+        {
+            for( int yy = b0; yy < b0 + 12; yy++ )
+            {
+                const uint32_t ro = (uint32_t)((yy + 32) * stride);
+                st16b<NT>( vh, rh, xo + ro );
+                st16b<NT>( vv, rv, xo + ro );
+                st16b<NT>( vc, rc, xo + ro );
+            }
+        }
+    };
+    for( int cy = r0; cy < r1; cy += 6 )
+    {
+        do_row( std::integral_constant<int, 0>{}, cy );
+        if( cy + 1 >= r1 ) break;
+        do_row( std::integral_constant<int, 1>{}, cy + 1 );
+        if( cy + 2 >= r1 ) break;
+        do_row( std::integral_constant<int, 2>{}, cy + 2 );
+        if( cy + 3 >= r1 ) break;
+        do_row( std::integral_constant<int, 3>{}, cy + 3 );
+        if( cy + 4 >= r1 ) break;
+        do_row( std::integral_constant<int, 4>{}, cy + 4 );
+        if( cy + 5 >= r1 ) break;
+        do_row( std::integral_constant<int, 5>{}, cy + 5 );
+    }
+}
+
+template <int HS_ROWS, bool NT>
+__global__ __launch_bounds__( 64 ) void hpel_strip7_kernel( const uint8_t *src, uint8_t *__restrict__ dh,
+                                                            uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
+                                                            intptr_t stride, intptr_t fstride, int width, int height,
+                                                            int xcd )
+{
+    const Blk3 B = blk3( xcd );
+    const int nstrips = (int)gridDim.y - 4;
+    if( (int)B.y >= nstrips )
+        hpel_strip7<HS_ROWS, NT, true>( src, dh, dv, dc, stride, fstride, width, height, B, nstrips );
+    else
+        hpel_strip7<HS_ROWS, NT, false>( src, dh, dv, dc, stride, fstride, width, height, B, nstrips );
+}
+
 template <int BD>
 hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD>::pixel *dh,
                                typename PT<BD>::pixel *dv, typename PT<BD>::pixel *dc, intptr_t stride,
@@ -584,11 +784,11 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
     if( nframes <= 0 || width <= 0 || height <= 0 )
         return hipSuccess;
     const int ev = variant( V_HPEL );
-    const int var = ev >= 0 ? ev : BD == 8 ? 3 : 0;
+    int var = ev >= 0 ? ev : BD == 8 ? 7 : 0;
     if constexpr( BD == 8 )
     {
         // streaming kernel: needs 16-byte aligned rows (pixel (0,0) and the strides)
-        if( var >= 2 && var <= 6 && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
+        if( var >= 2 && var <= 7 && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
                            (uintptr_t)fstride) & 15) )
         {
             const int nq = (width + 32) / 16, nchunk = (nq + 61) / 62;
@@ -605,8 +805,15 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
             // turns it off): 0.0329 -> 0.0324 ms at 16 frames, 0.1514 -> 0.1499 at 64
             // (profiles/r03i_stream_var.json; the persistent form, variant 6, was no faster)
             const int sxcd = variant( V_STREAM_XCD ) != 0;
+            const bool snt = stream_nt();
 #define HS_GO( ROWS )                                                                                              \
-    if( var == 6 )                                                                                                 \
+    if( var == 7 && snt )                                                                                          \
+        hipLaunchKernelGGL( ( hpel_strip7_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, \
+                            fstride, width, height, sxcd );                                                        \
+    else if( var == 7 )                                                                                            \
+        hipLaunchKernelGGL( ( hpel_strip7_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride,\
+                            fstride, width, height, sxcd );                                                        \
+    else if( var == 6 )                                                                                            \
     {                                                                                                              \
         static int resident_[25] = {};                                                                             \
         if( !resident_[ROWS] )                                                                                     \
@@ -623,6 +830,9 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
                             dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride, width, height, 8 * 16,         \
                             64 * 512, g.x, g.y, units_ );                                                          \
     }                                                                                                              \
+    else if( var == 3 && snt )                                                                                     \
+        hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, true, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,   \
+                            stride, fstride, width, height, 8 * 16, 64 * 512, sxcd );                              \
     else if( var == 3 )                                                                                            \
         hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, \
                             fstride, width, height, 8 * 16, 64 * 512, sxcd );                                      \
@@ -635,6 +845,15 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
     else                                                                                                           \
         hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,        \
                             stride, fstride, width, height, 8 * 16, 64 * 512, sxcd )
+            if( var == 7 )
+            {
+                // 64-piece chunks; the right border piece must have its left neighbour in its wave
+                const int np = nq + 2;
+                if( (width & 15) || (np - 1) % 64 == 0 )
+                    var = 3;
+                else
+                    g.x = (np + 63) / 64;
+            }
             if( rows == 24 ) { HS_GO( 24 ); }
             else if( rows == 16 ) { HS_GO( 16 ); }
             else if( rows == 8 ) { HS_GO( 8 ); }
@@ -1435,7 +1654,7 @@ __global__ __launch_bounds__( 128 ) void lowres16_kernel( const uint8_t *__restr
 // are replicas of columns 0 and wl-1 (plane_expand_border, frame.c:627-631), stored by
 // the lanes that hold those columns: no border wave, every lane's loads for its R rows
 // independent of the other rows.
-template <int R>
+template <int R, bool NT = false>
 __device__ __forceinline__ void lowres_rows_body( const uint8_t *__restrict__ src, intptr_t stride, intptr_t fstride,
                                                   int width, int height, uint8_t *__restrict__ d0,
                                                   uint8_t *__restrict__ dh, uint8_t *__restrict__ dv,
@@ -1500,20 +1719,20 @@ __device__ __forceinline__ void lowres_rows_body( const uint8_t *__restrict__ sr
 #pragma unroll
                     for( int pl = 0; pl < 4; pl++ )
                     {
-                        *(uint4 *)(dst[pl] + o) = make_uint4( w[pl][0], w[pl][1], w[pl][2], w[pl][3] );
+                        st16<NT>( dst[pl] + o, make_uint4( w[pl][0], w[pl][1], w[pl][2], w[pl][3] ) );
                         if( k == 0 )
                         {
                             // left border: column 0 repeated over x in [-32, 0)
                             const uint32_t bb = splat( w[pl][0], 0 );
-                            *(uint4 *)(dst[pl] + orow - 32) = make_uint4( bb, bb, bb, bb );
-                            *(uint4 *)(dst[pl] + orow - 16) = make_uint4( bb, bb, bb, bb );
+                            st16<NT>( dst[pl] + orow - 32, make_uint4( bb, bb, bb, bb ) );
+                            st16<NT>( dst[pl] + orow - 16, make_uint4( bb, bb, bb, bb ) );
                         }
                         if( k == nfull - 1 && !nrem )
                         {
                             // right border: column wl-1 repeated over x in [wl, wl+32)
                             const uint32_t bb = splat( w[pl][3], 3 );
-                            *(uint4 *)(dst[pl] + o + 16) = make_uint4( bb, bb, bb, bb );
-                            *(uint4 *)(dst[pl] + o + 32) = make_uint4( bb, bb, bb, bb );
+                            st16<NT>( dst[pl] + o + 16, make_uint4( bb, bb, bb, bb ) );
+                            st16<NT>( dst[pl] + o + 32, make_uint4( bb, bb, bb, bb ) );
                         }
                     }
                 }
@@ -1561,7 +1780,7 @@ __device__ __forceinline__ void lowres_rows_body( const uint8_t *__restrict__ sr
     }
 }
 
-template <int R>
+template <int R, bool NT = false>
 __global__ __launch_bounds__( 64 ) void lowres_rows_kernel( const uint8_t *__restrict__ src, intptr_t stride,
                                                             intptr_t fstride, int width, int height,
                                                             uint8_t *__restrict__ d0, uint8_t *__restrict__ dh,
@@ -1569,7 +1788,7 @@ __global__ __launch_bounds__( 64 ) void lowres_rows_kernel( const uint8_t *__res
                                                             intptr_t ds, intptr_t dfs, int xcd )
 {
     const Blk3 B = blk3( xcd );
-    lowres_rows_body<R>( src, stride, fstride, width, height, d0, dh, dv, dc, ds, dfs, (int)B.y, (int)B.z );
+    lowres_rows_body<R, NT>( src, stride, fstride, width, height, d0, dh, dv, dc, ds, dfs, (int)B.y, (int)B.z );
 }
 
 // persistent form (X264HIP_LOWRES_VARIANT=5): a resident grid walks the (row block, frame)
@@ -1630,6 +1849,12 @@ hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t
             else if( R == 4 )
                 hipLaunchKernelGGL( lowres_rows_kernel<4>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
                                     dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) == 1 );
+            else if( stream_nt() )
+                // nontemporal stores + XCD-contiguous row blocks (which lost with plain stores):
+                // 64 frames 0.0789 -> 0.0510 ms, 16 frames 0.0165 -> 0.0145 ms
+                // (profiles/r03r_stream_nt.json)
+                hipLaunchKernelGGL( ( lowres_rows_kernel<2, true> ), gr, dim3( 64 ), 0, st, src, stride, fstride, width,
+                                    height, dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) != 0 );
             else
                 hipLaunchKernelGGL( lowres_rows_kernel<2>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
                                     dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) == 1 );
