@@ -69,7 +69,7 @@ _VARIANT_SWITCHES = ("X264HIP_ME_VARIANT", "X264HIP_HPEL_VARIANT", "X264HIP_HPEL
                      "X264HIP_LOWRES_INTRA_VARIANT", "X264HIP_LOOKAHEAD_BAND",
                      "X264HIP_ME_LEAD", "X264HIP_TESA_VARIANT", "X264HIP_INTEGRAL_VARIANT",
                      "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS",
-                     "X264HIP_ME_XCD", "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT")
+                     "X264HIP_ME_XCD", "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT", "X264HIP_SSD_VARIANT")
 
 
 @pytest.fixture(autouse=True)

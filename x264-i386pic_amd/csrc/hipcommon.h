@@ -196,7 +196,7 @@ template <int BD> __device__ __forceinline__ int upix( uint32_t w, int k )
 namespace x264hip {
 enum VariantSlot
 {
-    V_ME = 0, V_HPEL, V_HPEL_ROWS, V_SUBPEL, V_LOWRES, V_DQ, V_RECON, V_LOWRES_INTRA, V_LA_BAND, V_ME_LEAD, V_TESA, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_STREAM_NT, V_COUNT
+    V_ME = 0, V_HPEL, V_HPEL_ROWS, V_SUBPEL, V_LOWRES, V_DQ, V_RECON, V_LOWRES_INTRA, V_LA_BAND, V_ME_LEAD, V_TESA, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_STREAM_NT, V_SSD, V_COUNT
 };
 int variant( VariantSlot slot );
 

@@ -838,12 +838,11 @@ __device__ __forceinline__ void ssd_chunk( uint4 a4, uint4 b4, uint32_t &iu, uin
 
 // grid: x = 64-chunk column groups (the nv12 tail columns as extra groups after nbx0), y =
 // bands of 4 x SSD_ROWS rows (one wave per SSD_ROWS rows), z = frame.  A lane loads its chunk
-// of all SSD_ROWS rows of both planes before any arithmetic (32 independent 16-byte loads in
-// flight); the four waves' sums meet in LDS.  The frame total needs no zeroed output: each
+// of all SSD_ROWS rows of both planes before any arithmetic (2 x SSD_ROWS independent 16-byte
+// loads in flight); the four waves' sums meet in LDS.  The frame total needs no zeroed output: each
 // workgroup adds into its frame's slot of a library-owned accumulator ring and takes a
 // ticket; the last arriver moves the total to out[] and leaves the slot zero for the next
 // launch (one kernel, no memset and no dependent dispatch).
-constexpr int SSD_ROWS = 16;
 struct SsdSlot
 {
     unsigned long long su, sv;
@@ -851,7 +850,7 @@ struct SsdSlot
 };
 constexpr int SSD_RING = 1 << 16;
 
-template <int BD, bool NV12>
+template <int BD, bool NV12, int SSD_ROWS = 16>
 __global__ __launch_bounds__( 256 ) void plane_ssd_kernel( const typename PT<BD>::pixel *__restrict__ p1, intptr_t s1,
                                                            intptr_t f1, const typename PT<BD>::pixel *__restrict__ p2,
                                                            intptr_t s2, intptr_t f2, int c0a, int c1a, int nbx0,
@@ -1008,16 +1007,25 @@ hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_
         c1b = w7 ? w8 + 2 * w7 : w8;
     }
     const int nbx0 = (c1a - c0a + 64 * CH - 1) / (64 * CH), nbx1 = (c1b - c0b + 64 * CH - 1) / (64 * CH);
-    dim3 g( (unsigned)std::max( 1, nbx0 + nbx1 ), (unsigned)((height + 4 * SSD_ROWS - 1) / (4 * SSD_ROWS)),
-            (unsigned)nframes ),
+    // rows per wave (X264HIP_SSD_VARIANT 0 = 16, 1 = 8, the default, 2 = 4): 16 1080p pairs
+    // 0.0207 / 0.0165 / 0.0228 ms, 64 pairs 0.0515 / 0.0454 / 0.0434 ms (profiles/r03x_ssd_ab.json);
+    // the 16-frame leg is one burst of loads, and twice the waves of half the rows issue it faster
+    const int sv = variant( V_SSD );
+    const int rows = sv == 0 ? 16 : sv == 2 ? 4 : 8;
+    dim3 g( (unsigned)std::max( 1, nbx0 + nbx1 ), (unsigned)((height + 4 * rows - 1) / (4 * rows)), (unsigned)nframes ),
         blk( 256 );
     unsigned long long *o = (unsigned long long *)out;
-    if( nv12 )
-        hipLaunchKernelGGL( ( plane_ssd_kernel<BD, true> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0a, c1a, nbx0,
-                            c0b, c1b, height, o, ring, slot0 );
-    else
-        hipLaunchKernelGGL( ( plane_ssd_kernel<BD, false> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0a, c1a,
-                            nbx0, c0b, c1b, height, o, ring, slot0 );
+#define SSD_GO( R )                                                                                                \
+    if( nv12 )                                                                                                     \
+        hipLaunchKernelGGL( ( plane_ssd_kernel<BD, true, R> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0a, c1a, \
+                            nbx0, c0b, c1b, height, o, ring, slot0 );                                              \
+    else                                                                                                           \
+        hipLaunchKernelGGL( ( plane_ssd_kernel<BD, false, R> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0a,    \
+                            c1a, nbx0, c0b, c1b, height, o, ring, slot0 )
+    if( rows == 8 ) { SSD_GO( 8 ); }
+    else if( rows == 4 ) { SSD_GO( 4 ); }
+    else { SSD_GO( 16 ); }
+#undef SSD_GO
     return hipGetLastError();
 }
 
