@@ -322,12 +322,16 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     tplanes, _, _ = synth.make_sequence(t1 - t0 + 1, mbw * 16, mbh * 16, 8, start=t0)
     tdev = torch.from_numpy(tplanes).cuda()
     del tplanes
+    # the prediction as a buffer of its own (an encoder's motion-compensated prediction is not
+    # the previous source frame): as slices of one sequence every frame would be read twice,
+    # once as a source and once as a prediction, and the second read served from cache
+    tpred = tdev[:-1].clone()
     nmb = TF * mbw * mbh
     dct = torch.empty((nmb, 256), dtype=torch.int16, device="cuda")
     nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
     for t, mf, bs in ((4, mf4, bs4), (8, mf8, bs8)):
         def step(t=t, mf=mf, bs=bs):
-            x.mb_dct_quant(t, tdev[1:], origin, stride, tdev[:-1], origin, stride, mbw, mbh, TF, mf, bs, dct=dct,
+            x.mb_dct_quant(t, tdev[1:], origin, stride, tpred, origin, stride, mbw, mbh, TF, mf, bs, dct=dct,
                            nz=nz, fenc_frame_stride=fstride, pred_frame_stride=fstride)
         wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
         blocks = nmb * (16 if t == 4 else 4)
@@ -389,7 +393,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     res["lowres_%d_launch_ms" % TF] = ev_ms
     res["lowres_%d_hbm_frac" % TF] = TF * lbytes / (ev_ms * 1e-3) / HBM_PEAK
     del tl
-    del recon, tdev, dct, nz
+    del recon, tdev, tpred, dct, nz
     lw, lh = mbw * 16, mbh * 16
     louts, _ = x.frame_init_lowres(dev[:-1], origin, stride, lw, lh)
 
@@ -638,9 +642,13 @@ def rates_ssd(x, a, world, dev, origin, stride, F):
     """plane SSD (x264_pixel_ssd_wxh, the per-frame PSNR sum of encoder.c:2499) over the F
     1080p pairs: frames/s and the fraction of HBM (two w x h planes read)."""
     out = torch.empty(F, dtype=torch.int64, device="cuda")
+    # the reconstructed planes as a buffer of their own (in an encoder fenc and fdec are
+    # different frames): with both operands slices of one sequence, frame f+1 is read as the
+    # source of pair f+1 and the reference of pair f, and the second read comes from cache
+    recon = dev[:-1].clone()
 
     def step():
-        x.ssd_plane_batch(dev[1:], origin, stride, dev[:-1], origin, stride, a.width, a.height, F, out=out)
+        x.ssd_plane_batch(dev[1:], origin, stride, recon, origin, stride, a.width, a.height, F, out=out)
     wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
     return {"ssd_plane_frames_per_s": world * a.steps * F / wall, "ssd_plane_launch_ms": ev_ms,
             "ssd_plane_hbm_frac": F * 2 * a.width * a.height / (ev_ms * 1e-3) / HBM_PEAK}
@@ -678,9 +686,10 @@ def rates_10bit(x, a, world, mbw, mbh, F):
     nmb = TF * mbw * mbh
     dct = torch.empty((nmb, 256), dtype=torch.int32, device="cuda")
     nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
+    pred = dev[:-1].clone()                         # a buffer of its own, as in the 8-bit legs
 
     def dstep():
-        x.mb_dct_quant(8, dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, TF, mf8, bs8, dct=dct,
+        x.mb_dct_quant(8, dev[1:], origin, stride, pred, origin, stride, mbw, mbh, TF, mf8, bs8, dct=dct,
                        nz=nz, fenc_frame_stride=fstride, pred_frame_stride=fstride)
     wall, ev_ms = timed(dstep, a.steps, a.warmup, world)
     blocks = nmb * 4

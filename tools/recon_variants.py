@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""A/B of the fused reconstruction kernels (X264HIP_RECON_VARIANT: 0 = block pairs for
-transform 4, 1 = lane per block), 1080p, F frames, after a clock-settling warmup."""
+"""A/B of the fused reconstruction kernels (X264HIP_RECON_VARIANT: default = block pairs for
+transform 4 / packed transform 8 with sector-aligned waves, 2 = the same unshifted, 1 = lane
+per block), 1080p, F frames, after a clock-settling warmup."""
 import os, sys, json
 import numpy as np
 import torch
@@ -29,16 +30,17 @@ for bd in (8, 10):
                                 torch.from_numpy(mf.copy()).cuda(), torch.from_numpy(bias.copy()).cuda(),
                                 fenc_frame_stride=fsz, pred_frame_stride=fsz)
         dmf = torch.from_numpy((dq4[1] if t == 4 else dq8[1]).copy()).cuda()
-        outs = {v: torch.zeros_like(dev[:-1]) for v in ("0", "1")}
+        outs = {v: torch.zeros_like(dev[:-1]) for v in (None, "2", "1")}
         run = lambda v: x.mb_dequant_idct_add(t, dct, mbw, mbh, F, dmf, qpm, dev[:-1], origin, stride, outs[v],  # noqa
                                               origin, stride, pred_frame_stride=fsz, recon_frame_stride=fsz)
         for v in outs:
             sys.modules["x264hip"].set_variant("X264HIP_RECON_VARIANT", v)
             run(v)
         torch.cuda.synchronize()
-        assert torch.equal(outs["0"], outs["1"])
+        assert torch.equal(outs[None], outs["1"]) and torch.equal(outs[None], outs["2"])
+        sys.modules["x264hip"].set_variant("X264HIP_RECON_VARIANT", None)
         for _ in range(150):
-            run("0")
+            run(None)
         times = {v: [] for v in outs}
         for rnd in range(5):
             for v in outs:
@@ -55,4 +57,8 @@ for bd in (8, 10):
         for v in outs:
             ms = float(np.median(times[v]))
             res[f"bd{bd}_t{t}_v{v}"] = {"ms": ms, "hbm_frac": alg / ms / 1e6 / 8000}
-print(json.dumps(res, indent=1))
+sys.modules["x264hip"].set_variant("X264HIP_RECON_VARIANT", None)
+out = json.dumps(res, indent=1)
+print(out)
+if len(sys.argv) > 2:
+    open(sys.argv[2], "w").write(out + "\n")

@@ -31,7 +31,7 @@ for F in (16, 64):
     for v in (0, 1, 2):
         x.set_variant("X264HIP_SSD_VARIANT", v)
         o = torch.empty(F, dtype=torch.int64, device="cuda")
-        x.ssd_plane_batch(dev[1:], origin, stride, dev[:-1], origin, stride, 1920, 1080, F, out=o)
+        x.ssd_plane_batch(dev[1:], origin, stride, dev[:-1].clone(), origin, stride, 1920, 1080, F, out=o)
         torch.cuda.synchronize()
         outs.append(o.cpu().numpy())
     assert all(np.array_equal(outs[0], o) for o in outs), "SSD variants disagree"

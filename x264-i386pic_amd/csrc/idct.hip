@@ -874,16 +874,20 @@ __global__ __launch_bounds__( 256 ) void mb_recon_kernel( const typename PT<BD>:
 // transform 4, 8-pixel variant: one lane per pair of horizontally adjacent
 // 4x4 blocks (their 32 coefficients are contiguous in the dct4x4 order), so
 // pixel rows move as 8-pixel pieces and a wave covers 8 MBs of one MB row
+// `sh` (0..3) shifts the 8-MB strips left by sh MBs so each strip's 128-byte rows start on a
+// 64-byte sector of the output plane (the plane origin sits 32 bytes into a sector when the
+// padding is 32 pixels): every store then writes whole sectors, and no sector is shared by
+// two waves (see launch_mb_recon)
 template <int BD>
 __global__ __launch_bounds__( 256 ) void mb_recon_pair_kernel( const typename PT<BD>::dctcoef *dct, int mbw, int mbh,
                                                                int nframes, const int32_t *dmf, const int32_t *qp,
                                                                const typename PT<BD>::pixel *pred, intptr_t ps,
                                                                intptr_t pfs, typename PT<BD>::pixel *recon,
-                                                               intptr_t rs, intptr_t rfs )
+                                                               intptr_t rs, intptr_t rfs, int sh )
 {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int spr = (mbw + 7) >> 3;
+    const int spr = (mbw + sh + 7) >> 3;
     if( wave >= (int64_t)nframes * mbh * spr )
         return;
     const int strip = (int)(wave % spr);
@@ -891,8 +895,8 @@ __global__ __launch_bounds__( 256 ) void mb_recon_pair_kernel( const typename PT
     const int mby = (int)(t % mbh);
     const int f = (int)(t / mbh);
     const int m = (lane & 15) >> 1, half = lane & 1, by = lane >> 4;
-    const int mbx = strip * 8 + m;
-    if( mbx >= mbw )
+    const int mbx = strip * 8 + m - sh;
+    if( mbx < 0 || mbx >= mbw )
         return;
     const int64_t mb = ((int64_t)f * mbh + mby) * mbw + mbx;
     const int q = qp[mb];
@@ -1124,11 +1128,13 @@ __device__ __forceinline__ void recon8_pk_block( const int16_t *__restrict__ dct
 }
 #undef IDCT8_1D_PK
 
+// lanes per 8x8-block row: the row's bw blocks shifted right by sh (0..7) lanes and padded to
+// whole waves, so every wave's 512-byte row pieces start on a 64-byte sector (launch_mb_recon)
 __global__ __launch_bounds__( 256 ) void mb_recon8_pk_kernel( const int16_t *__restrict__ dct, int mbw, int mbh,
                                                               int nframes, const int32_t *__restrict__ dmf,
                                                               const int32_t *__restrict__ qp,
                                                               const uint8_t *pred, intptr_t ps, intptr_t pfs,
-                                                              uint8_t *recon, intptr_t rs, intptr_t rfs )
+                                                              uint8_t *recon, intptr_t rs, intptr_t rfs, int sh )
 {
     // the 6 x 64 dequant_mf table in LDS, rows 68 dwords apart (lanes on different qp%6
     // rows read different 16-B slots of a bank row)
@@ -1142,11 +1148,13 @@ __global__ __launch_bounds__( 256 ) void mb_recon8_pk_kernel( const int16_t *__r
     }
     const bool m24 = __syncthreads_and( ok );
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int bw = mbw * 2, bh = mbh * 2;
-    if( t >= (int64_t)nframes * bw * bh )
+    const int bw = mbw * 2, bh = mbh * 2, lpr = (bw + sh + 63) & ~63;
+    if( t >= (int64_t)nframes * lpr * bh )
         return;
-    const int bx = (int)(t % bw);
-    const int64_t r = t / bw;
+    const int bx = (int)(t % lpr) - sh;
+    if( bx < 0 || bx >= bw )
+        return;
+    const int64_t r = t / lpr;
     const int by = (int)(r % bh);
     const int f = (int)(r / bh);
     const int64_t mb = ((int64_t)f * mbh + (by >> 1)) * mbw + (bx >> 1);
@@ -1171,21 +1179,31 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
     const int ev = variant( V_RECON );
     // 8 bit: block pairs (0.55 vs 0.43 of HBM, tools/recon_variants.py); 10 bit: one lane
     // per block is faster (0.68 vs 0.58); X264HIP_RECON_VARIANT = 0 / 1 forces either
-    const bool pair = ev >= 0 ? ev != 1 : BD == 8;
+    const bool pair = ev >= 0 && ev != 2 ? ev != 1 : BD == 8;
     // transform 8 at 8 bit: the packed kernel unless X264HIP_RECON_VARIANT = 1 (lane per block, int32)
+    // Sector alignment of the stores: with row and frame strides multiples of 64 bytes, every
+    // row of the output plane has x = 0 at the same offset within a 64-byte sector; shifting
+    // the waves' pixel ranges by that offset puts every wave's row pieces on whole sectors
+    // (partial sectors shared by two waves were the half-pel planes' bottleneck).
+    // X264HIP_RECON_VARIANT=2 keeps the unshifted layout.
+    const size_t psz = sizeof( typename PT<BD>::pixel );
+    const bool al = ev != 2 && !(((size_t)rs * psz) & 63) && !(((size_t)rfs * psz) & 63);
+    const int off = al ? (int)((uintptr_t)recon & 63) : 0;       // byte offset of x = 0 in its sector
     if constexpr( BD == 8 )
         if( transform == 8 && ev != 1 )
         {
-            const int64_t total = (int64_t)nframes * mbw * mbh * 4;
+            const int sh8 = off % 8 ? 0 : off / 8;                 // 8-pixel blocks
+            const int64_t total = (int64_t)nframes * mbh * 2 * ((mbw * 2 + sh8 + 63) & ~63);
             hipLaunchKernelGGL( mb_recon8_pk_kernel, dim3( (unsigned)((total + 255) / 256) ), dim3( 256 ), 0, st, dct,
-                                mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs, rfs );
+                                mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs, rfs, sh8 );
             return hipGetLastError();
         }
     if( transform == 4 && pair )
     {
-        const int64_t waves = (int64_t)nframes * mbh * ((mbw + 7) / 8);
+        const int sh = off % (16 * (int)psz) ? 0 : off / (16 * (int)psz);   // 16-pixel MBs
+        const int64_t waves = (int64_t)nframes * mbh * ((mbw + sh + 7) / 8);
         hipLaunchKernelGGL( mb_recon_pair_kernel<BD>, dim3( (unsigned)((waves + 3) / 4) ), dim3( 256 ), 0, st, dct,
-                            mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs, rfs );
+                            mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs, rfs, sh );
         return hipGetLastError();
     }
     const int bpm = transform == 8 ? 4 : 16;

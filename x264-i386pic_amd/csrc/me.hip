@@ -13,6 +13,8 @@
 // amortised over 16 candidates.  fenc (16 rows) stays in VGPRs for the whole
 // lane lifetime.  Candidate my finishes at row my+15 and is stored then.
 #include "hipcommon.h"
+#include <mutex>
+#include <string.h>
 #include <stdlib.h>
 #include <atomic>
 #include <utility>
@@ -1862,27 +1864,42 @@ __global__ __launch_bounds__( 256 ) void tesa_centre_kernel( int nmb, const int1
     }
 }
 
-// stream-ordered scratch for the self-contained TESA: the device's default pool keeps
-// freed blocks (release threshold raised once per device), so a repeated call re-uses
-// them instead of mapping fresh pages
+// stream-ordered scratch for the self-contained TESA from a memory pool the library owns,
+// one per device (the device of the launch stream), created with an unbounded release
+// threshold so a repeated call re-uses its blocks instead of mapping fresh pages; the
+// application's default pool is left alone
 static hipError_t tesa_scratch( void **p, size_t bytes, hipStream_t stream )
 {
-    static std::atomic<uint32_t> pooled{ 0 };
+    static std::mutex mu;
+    static hipMemPool_t pools[64] = {};
     int dev = 0;
-    hipError_t e = hipGetDevice( &dev );
+    hipError_t e = stream ? hipStreamGetDevice( stream, &dev ) : hipGetDevice( &dev );
     if( e != hipSuccess )
         return e;
-    if( dev < 32 && !(pooled.load() & (1u << dev)) )
+    if( dev < 0 || dev >= 64 )
+        return hipErrorInvalidDevice;
+    hipMemPool_t pool;
     {
-        hipMemPool_t pool;
-        if( hipDeviceGetDefaultMemPool( &pool, dev ) == hipSuccess )
+        std::lock_guard<std::mutex> lk( mu );
+        if( !pools[dev] )
         {
+            hipMemPoolProps props;
+            memset( &props, 0, sizeof( props ) );
+            props.allocType = hipMemAllocationTypePinned;
+            props.handleTypes = hipMemHandleTypeNone;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            if( (e = hipMemPoolCreate( &pools[dev], &props )) != hipSuccess )
+            {
+                pools[dev] = nullptr;
+                return e;
+            }
             uint64_t thr = UINT64_MAX;
-            (void)hipMemPoolSetAttribute( pool, hipMemPoolAttrReleaseThreshold, &thr );
+            (void)hipMemPoolSetAttribute( pools[dev], hipMemPoolAttrReleaseThreshold, &thr );
         }
-        pooled.fetch_or( 1u << dev );
+        pool = pools[dev];
     }
-    return hipMallocAsync( p, bytes, stream );
+    return hipMallocFromPoolAsync( p, bytes, pool, stream );
 }
 
 template <int BD>
@@ -1909,22 +1926,24 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
         const size_t tab = (size_t)nmb * (2 * TR + 1) * (size_t)((2 * TR + 1 + 3) & ~3) * sizeof( sadt );
         const size_t bytes = tab + (size_t)nmb * 8;
         void *buf = nullptr;
-        hipError_t e = tesa_scratch( &buf, bytes, stream );
-        if( e != hipSuccess )
-            return e;
-        sadt *ttab = (sadt *)buf;
-        int16_t *cen = (int16_t *)((uint8_t *)buf + tab), *org = cen + 2 * nmb;
-        hipLaunchKernelGGL( tesa_centre_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream,
-                            (int)nmb, par, cen );
-        e = hipGetLastError();
-        if( e == hipSuccess )
-            e = launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, TR, ttab, cen, org, stream );
-        if( e == hipSuccess )
-            e = launch_me_tesa<BD>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nframes, me_range, satd,
-                                    ttab, TR, org, par, init_cost, cost_mv, out, stream );
-        const hipError_t f = hipFreeAsync( buf, stream );
-        return e != hipSuccess ? e : f;
+        if( tesa_scratch( &buf, bytes, stream ) == hipSuccess )
+        {
+            sadt *ttab = (sadt *)buf;
+            int16_t *cen = (int16_t *)((uint8_t *)buf + tab), *org = cen + 2 * nmb;
+            hipLaunchKernelGGL( tesa_centre_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream,
+                                (int)nmb, par, cen );
+            hipError_t e = hipGetLastError();
+            if( e == hipSuccess )
+                e = launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, TR, ttab, cen, org, stream );
+            if( e == hipSuccess )
+                e = launch_me_tesa<BD>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nframes, me_range, satd,
+                                        ttab, TR, org, par, init_cost, cost_mv, out, stream );
+            const hipError_t f = hipFreeAsync( buf, stream );
+            return e != hipSuccess ? e : f;
+        }
+        (void)hipGetLastError();                            // no scratch: the in-kernel SADs below
     }
+
     // the mvsads list: at most (2*me_range+1) rows x (2*me_range+3)&~3 columns per MB
     const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
     // X264HIP_TESA_VARIANT=2: the table scan with the prefix minimum on the bsad chain (the

@@ -907,7 +907,24 @@ __global__ __launch_bounds__( 256 ) void plane_ssd_kernel( const typename PT<BD>
         part[1][wv] = sv;
     }
     __syncthreads();
-    if( threadIdx.x == 0 )
+    if( threadIdx.x == 0 && !NV12 )
+    {
+        // one atomic per workgroup: the count in bits 48-63 and the sum below it (a frame's SSD
+        // is < 2^48: 10-bit 8K is 2^45), so the returned word tells the last arriver and the
+        // total at once -- no wait for the add before a separate ticket (one memory round
+        // trip less in every workgroup's tail)
+        SsdSlot *sl = ring + ((slot0 + f) & (SSD_RING - 1));
+        su = part[0][0] + part[0][1] + part[0][2] + part[0][3];
+        const unsigned long long nwg = gridDim.x * gridDim.y, mine = (1ull << 48) + su;
+        const unsigned long long old =
+            __hip_atomic_fetch_add( &sl->su, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+        if( (old >> 48) == nwg - 1 )
+        {
+            out[f] = (old + mine) & ((1ull << 48) - 1);
+            __hip_atomic_store( &sl->su, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+        }
+    }
+    else if( threadIdx.x == 0 )
     {
         SsdSlot *sl = ring + ((slot0 + f) & (SSD_RING - 1));
         su = part[0][0] + part[0][1] + part[0][2] + part[0][3];
@@ -990,6 +1007,11 @@ hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_
         return hipMemsetAsync( out, 0, (size_t)nframes * (nv12 ? 2 : 1) * sizeof( uint64_t ), stream );
     if( nframes > 65535 )
         return hipErrorInvalidValue;
+    // the plane path's packed accumulator: a frame's SSD below 2^48, fewer than 2^16 workgroups
+    const double pmax = (double)((1 << BD) - 1);
+    if( !nv12 && ((double)width * height * pmax * pmax >= 281474976710656.0 ||
+                  (double)((width + 1023) / 1024 + 1) * ((height + 3) / 4 + 1) >= 65536.0) )
+        return hipErrorInvalidValue;
     SsdSlot *ring = nullptr;
     int slot0 = 0;
     hipError_t e = ssd_ring( &ring, nframes, &slot0 );
@@ -1008,8 +1030,8 @@ hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_
     }
     const int nbx0 = (c1a - c0a + 64 * CH - 1) / (64 * CH), nbx1 = (c1b - c0b + 64 * CH - 1) / (64 * CH);
     // rows per wave (X264HIP_SSD_VARIANT 0 = 16, 1 = 8, the default, 2 = 4): 16 1080p pairs
-    // 0.0207 / 0.0165 / 0.0228 ms, 64 pairs 0.0515 / 0.0454 / 0.0434 ms (profiles/r03x_ssd_ab.json);
-    // the 16-frame leg is one burst of loads, and twice the waves of half the rows issue it faster
+    // 0.0195 / 0.0137 / 0.0141 ms with the packed accumulator (profiles/r03aa_ssd_ab.json); the
+    // 16-frame leg is one burst of loads, and twice the waves of half the rows issue it faster
     const int sv = variant( V_SSD );
     const int rows = sv == 0 ? 16 : sv == 2 ? 4 : 8;
     dim3 g( (unsigned)std::max( 1, nbx0 + nbx1 ), (unsigned)((height + 4 * rows - 1) / (4 * rows)), (unsigned)nframes ),
