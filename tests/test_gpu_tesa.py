@@ -37,15 +37,21 @@ def _oracle_frames(oracle, bd, planes, stride, org, H, mbw, mbh, me_range, satd,
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("me_range,satd,kind", [(16, True, "synthetic"), (16, True, "random"),
                                                 (8, False, "synthetic"), (24, True, "random"),
-                                                (4, True, "synthetic"), (32, False, "random")])
-@pytest.mark.parametrize("mode", ["internal", "kernel", "table"])
+                                                (4, True, "synthetic"), (32, False, "random"),
+                                                (12, True, "random"), (9, False, "synthetic")])
+@pytest.mark.parametrize("mode", ["internal", "kernel", "table", "onelaunch"])
 def test_tesa_small(hip, oracle, bd, me_range, satd, kind, mode):
-    """internal: no table given (me_range <= 24 builds one around the predictors);
-    kernel: X264HIP_TESA_VARIANT=1, the SADs computed in the scan; table: a caller's
-    me_search_full table over [-16, 16]"""
+    """internal: no table given (me_range <= 24 builds a table around the predictors, then
+    scans it); kernel: X264HIP_TESA_VARIANT=1, the SADs computed in the scan; table: a
+    caller's me_search_full table over [-16, 16]; onelaunch: X264HIP_TESA_VARIANT=3, the
+    table and the scan in one launch (8 bit, me_range 9..16)"""
     use_table = mode == "table"
     if mode == "kernel":
         hip.set_variant("X264HIP_TESA_VARIANT", 1)
+    if mode == "onelaunch":
+        if bd != 8 or not 8 < me_range <= 16:
+            pytest.skip("the one-launch kernel covers 8 bit, me_range 9..16")
+        hip.set_variant("X264HIP_TESA_VARIANT", 3)
     W, H, nf = 160, 96, 2
     planes, stride, org, dev = _setup(bd, W, H, kind, seed=me_range + bd, nframes=nf)
     mbw, mbh = W // 16, H // 16
@@ -88,12 +94,14 @@ def test_tesa_centred_table(hip, oracle, bd):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("kernel_sads", [False, True])
-def test_tesa_1080p(hip, oracle, bd, kernel_sads):
+@pytest.mark.parametrize("tv", [None, 1, 3])
+def test_tesa_1080p(hip, oracle, bd, tv):
     """every MB of a 1920x1088 frame pair at me_range 16, SATD fpelcmp, vs the oracle
-    (the internal table, and X264HIP_TESA_VARIANT=1's in-scan SADs)."""
-    if kernel_sads:
-        hip.set_variant("X264HIP_TESA_VARIANT", 1)
+    (the internal table, X264HIP_TESA_VARIANT=1's in-scan SADs, =3's one-launch table + scan)."""
+    if tv == 3 and bd != 8:
+        pytest.skip("the one-launch kernel is 8 bit")
+    if tv is not None:
+        hip.set_variant("X264HIP_TESA_VARIANT", tv)
     W, H, me_range = 1920, 1088, 16
     planes, stride, org, dev = _setup(bd, W, H, "synthetic", seed=21)
     mbw, mbh = W // 16, H // 16

@@ -1464,35 +1464,42 @@ __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
 // chain serves two MBs.  Every per-MB value is uniform within its segment; ballots are
 // masked to the segment, scans and reductions stay inside it, and loops run while any
 // segment still needs them.
-template <int BD, int NR, int SEG, bool TAB, bool SPEC = false>
-__global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
-                                                        intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
-                                                        intptr_t rs, intptr_t rfs,
-                                                        const uint16_t *__restrict__ integral, intptr_t ifs, int mbw,
-                                                        int mbh, int nmb, int me_range, int satd,
-                                                        const typename PT<BD>::sadt *__restrict__ table, int R,
-                                                        const int16_t *__restrict__ origin,
-                                                        const int16_t *__restrict__ par,
-                                                        const int32_t *__restrict__ init_cost,
-                                                        const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out,
-                                                        int cap )
+// The LDS a TESA scan touches (fenc rows, mvsads list) belongs to its own wave, and a
+// wave's LDS operations complete in order, so the scan orders its LDS hand-offs between
+// lanes with a wave-scope fence (a compiler barrier) instead of a workgroup barrier: the
+// fused kernel below runs it in waves that take different numbers of MBs.
+__device__ __forceinline__ void tesa_wave_sync()
+{
+    __builtin_amdgcn_fence( __ATOMIC_SEQ_CST, "wavefront" );
+    __builtin_amdgcn_wave_barrier();
+}
+
+// NSEG mvsads lists.  64-lane segments: { cost, mx | my << 16 } in 8 bytes; 32-lane
+// segments (me_range <= 16: < 32 columns, <= 33 rows, cost < 2^20) pack cost << 11 |
+// row << 5 | column into 4 bytes, which halves the LDS a workgroup holds (2 -> 4 waves
+// per SIMD with 128 VGPRs)
+template <int SEG> using tesa_ent = typename std::conditional<SEG == 32, uint32_t, uint64_t>::type;
+
+// One MB per SEG-lane segment of the calling wave: segment sg of the wave scans MB `mbo`
+// (clamped to the last MB; it publishes only when `live` and mbo < nmb) whose table window
+// starts at (ox, oy) relative to the MB.  `mvsads` / `fl` are this segment's LDS list and
+// fenc rows.
+template <int BD, int NR, int SEG, bool TAB, bool SPEC>
+__device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
+                                              const typename PT<BD>::pixel *__restrict__ ref, intptr_t rs, intptr_t rfs,
+                                              const uint16_t *__restrict__ integral, intptr_t ifs, int mbw, int mbh,
+                                              int nmb, int me_range, int satd,
+                                              const typename PT<BD>::sadt *__restrict__ table, int R, int ox, int oy,
+                                              const int16_t *__restrict__ par, const int32_t *__restrict__ init_cost,
+                                              const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out,
+                                              int64_t mbo, bool live, int sg, int lane, tesa_ent<SEG> *mvsads,
+                                              uint32_t *fl )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int NDW = 16 / PT<BD>::PPD;                     // dwords per fenc row
-    constexpr int NSEG = 64 / SEG;
-    // NSEG mvsads lists.  64-lane segments: { cost, mx | my << 16 } in 8 bytes; 32-lane
-    // segments (me_range <= 16: < 32 columns, <= 33 rows, cost < 2^20) pack cost << 11 |
-    // row << 5 | column into 4 bytes, which halves the LDS a workgroup holds (2 -> 4 waves
-    // per SIMD with 128 VGPRs)
-    using E = typename std::conditional<SEG == 32, uint32_t, uint64_t>::type;
-    extern __shared__ uint64_t tesa_lds[];
-    __shared__ uint32_t fls[NSEG][16 * NDW];
-    const int sg = (int)threadIdx.x / SEG, lane = (int)threadIdx.x % SEG;
-    const int64_t mbo = (int64_t)blockIdx.x * NSEG + sg;      // this segment's MB
+    using E = tesa_ent<SEG>;
     const int64_t mb = mbo < nmb ? mbo : nmb - 1;             // a spare segment repeats the last MB
     const uint64_t segmask = SEG == 64 ? ~0ull : 0xFFFFFFFFull << (32 * sg);
-    E *mvsads = (E *)tesa_lds + (int64_t)sg * cap;
-    uint32_t *fl = fls[sg];
     auto sball = [&]( bool c ) { return (uint64_t)__ballot( c ) & segmask; };
     auto rank = [&]( uint64_t m ) {
         return (int)__builtin_amdgcn_mbcnt_hi( (uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo( (uint32_t)m, 0u ) );
@@ -1544,10 +1551,9 @@ __global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) )
 #pragma unroll
     for( int j = 0; j < 4; j++ )                              // segment sums: DPP scan + readlane
         enc_dc[j] = (int)seg_lane<SEG>( seg_scan_add<SEG>( dcq[j] ), SEG - 1, sg );
-    __syncthreads();
+    tesa_wave_sync();
 
     const int W = 2 * R + 1, P = (W + 3) & ~3;
-    const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
     const typename PT<BD>::sadt *tab = TAB ? table + mb * (int64_t)(W * P) : nullptr;
     auto sad_at = [&]( int mx, int my ) -> uint32_t {
         const int tx = mx - ox, ty = my - oy;
@@ -1785,7 +1791,7 @@ __global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) )
             if( lane == 0 )
                 mvsads[bi] = mvsads[nmvsad];
         }
-        __syncthreads();
+        tesa_wave_sync();
     }
 
     // COST_MV over the survivors in list order: eight 8x4 units per candidate
@@ -1835,7 +1841,7 @@ __global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) )
         }
     }
     best = seg_lane<SEG>( seg_scan_min<SEG>( best ), SEG - 1, sg );
-    if( lane == 0 && mbo < nmb )
+    if( lane == 0 && live && mbo < nmb )
     {
         int32_t bcost = init_cost[mb], rx = bmx0, ry = bmy0;
         if( best != 0xFFFFFFFFu && (int32_t)(best >> 6) < bcost )
@@ -1849,6 +1855,115 @@ __global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) )
         out[4 * mb + 1] = rx;
         out[4 * mb + 2] = ry;
         out[4 * mb + 3] = nmvsad;
+    }
+}
+
+template <int BD, int NR, int SEG, bool TAB, bool SPEC = false>
+__global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
+                                                        intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
+                                                        intptr_t rs, intptr_t rfs,
+                                                        const uint16_t *__restrict__ integral, intptr_t ifs, int mbw,
+                                                        int mbh, int nmb, int me_range, int satd,
+                                                        const typename PT<BD>::sadt *__restrict__ table, int R,
+                                                        const int16_t *__restrict__ origin,
+                                                        const int16_t *__restrict__ par,
+                                                        const int32_t *__restrict__ init_cost,
+                                                        const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out,
+                                                        int cap )
+{
+    constexpr int NDW = 16 / PT<BD>::PPD;
+    constexpr int NSEG = 64 / SEG;
+    extern __shared__ uint64_t tesa_lds[];
+    __shared__ uint32_t fls[NSEG][16 * NDW];
+    const int sg = (int)threadIdx.x / SEG, lane = (int)threadIdx.x % SEG;
+    const int64_t mbo = (int64_t)blockIdx.x * NSEG + sg;      // this segment's MB
+    const int64_t mb = mbo < nmb ? mbo : nmb - 1;
+    const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
+    tesa_scan_mb<BD, NR, SEG, TAB, SPEC>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nmb, me_range, satd,
+                                          table, R, ox, oy, par, init_cost, cost_mv, out, mbo, true, sg, lane,
+                                          (tesa_ent<SEG> *)tesa_lds + (int64_t)sg * cap, fls[sg] );
+}
+
+// Self-contained TESA (8 bit, me_range 9..16) as ONE launch (X264HIP_TESA_VARIANT=3, not
+// the default): a workgroup first builds the
+// full-search tables of its 28 MBs around their predictors on variant 7's lanes (the
+// centred search, R = 16) into scratch, then its four waves scan those MBs (two per wave
+// pass, 32-lane segments).  The scan is latency-bound (33 dependent rows per MB) and the
+// table work VALU-bound, so with four workgroups per CU one workgroup's scan runs in the
+// issue slots the others' table rows leave, instead of after the whole table launch; the
+// table is read back by the workgroup that wrote it, mostly from L2.  The global stores are
+// visible to the other waves of the workgroup after the barrier (one CU, one L1).
+// Measured (profiles/r03ad_tesa_*): 0.768 ms per 16 1080p pairs against 0.652 for the two
+// launches.  The workgroups start together and have equal phases, so they stay in phase:
+// the scans of a CU's four workgroups coincide instead of filling each other's table
+// rows, and a wave's four scan passes run back to back at the occupancy the scan alone
+// had.  Nor is the scan's arithmetic small: ~3.7 k VALU per wave (two MBs), ~0.2 ms of
+// issue over the chip, so table (0.275 ms) + scan issue already exceeds 0.45 ms.
+template <int L>
+__global__ __launch_bounds__( 256 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void me_tesa_fused_kernel(
+    const uint8_t *__restrict__ fenc, intptr_t fs, intptr_t ffs, const uint8_t *__restrict__ ref, intptr_t rs,
+    intptr_t rfs, const uint16_t *__restrict__ integral, intptr_t ifs, int mbw, int mbh, int nmb, int me_range,
+    int satd, uint16_t *__restrict__ table, const int16_t *__restrict__ par, const int32_t *__restrict__ init_cost,
+    const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out, int cap, int xcd )
+{
+    constexpr int R = 16, G = (2 * R + 1 + 3) / 4, P = 4 * G, W = 2 * R + 1;
+    constexpr int MPW = 256 / G;                // 28 whole MBs per workgroup
+    constexpr int MPV = (MPW + 3) / 4;          // MBs per wave in the scan (7)
+    extern __shared__ uint64_t tesa_lds[];
+    __shared__ uint32_t fls[4][2][16 * 4];
+    const int tid = (int)threadIdx.x;
+    const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
+    const int64_t mb0 = (int64_t)blk * MPW;
+
+    // table phase (me_full_sad16_v7_kernel's lane: four columns, all 16 fenc rows)
+    {
+        const int lmb = min( tid / G, MPW - 1 );
+        const int grp = min( tid - lmb * G, G - 1 );
+        const int64_t mb = min( mb0 + lmb, (int64_t)nmb - 1 );
+        const uint32_t t32 = (uint32_t)mb / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+        const int mbx = (int)((uint32_t)mb - t32 * (uint32_t)mbw);
+        const int mby = (int)(t32 - f32 * (uint32_t)mbh);
+        uint32_t F[16][4];
+        const uint32_t *fe = (const uint32_t *)(fenc + (int64_t)f32 * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
+        const int fs_dw = (int)(fs / 4);
+#pragma unroll
+        for( int r = 0; r < 16; r++ )
+#pragma unroll
+            for( int k = 0; k < 4; k++ )
+                F[r][k] = fe[r * fs_dw + k];
+        int ox, oy;
+        const int16_t cen[2] = { par[8 * mb], par[8 * mb + 1] };   // the window centre: the predictor
+        me_window<8, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
+        const uint32_t *rbase = (const uint32_t *)(ref + (int64_t)f32 * rfs + (intptr_t)(16 * mby + oy) * rs +
+                                                   16 * mbx + ox + 4 * grp);
+        uint64_t *o64 = (uint64_t *)(table + mb * (W * P) + 4 * grp);
+        // lanes past the workgroup's MBs (or past the last MB) repeat a live lane's MB and
+        // group, so their stores write the same values to the same words: no guard
+        auto store = [o64]( int c, uint32_t lo, uint32_t hi ) { o64[c * (P / 4)] = ((uint64_t)hi << 32) | lo; };
+        uint64_t acc[16];
+        me_rows7<R, L>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 16>{} );
+    }
+    __syncthreads();
+
+    // scan phase: wave w takes MBs [MPV*w, MPV*w + MPV) of the workgroup, two per pass
+    const int w = tid >> 6, sg = (tid >> 5) & 1, lane = tid & 31;
+    tesa_ent<32> *lists = (tesa_ent<32> *)tesa_lds + (int64_t)(2 * w + sg) * cap;
+#pragma unroll 1
+    for( int i = 0; i < MPV; i += 2 )
+    {
+        const int l = MPV * w + i + sg;
+        const bool live = i + sg < MPV && l < MPW;
+        const int64_t mbo = mb0 + min( l, MPW - 1 );
+        const int64_t mb = mbo < nmb ? mbo : nmb - 1;
+        const uint32_t t32 = (uint32_t)mb / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+        int ox, oy;
+        const int16_t cen[2] = { par[8 * mb], par[8 * mb + 1] };
+        me_window<8, R>( cen, 0, (int)((uint32_t)mb - t32 * (uint32_t)mbw), (int)(t32 - f32 * (uint32_t)mbh), mbw,
+                         mbh, ox, oy );
+        tesa_scan_mb<8, 33, 32, true, true>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nmb, me_range,
+                                             satd, table, R, ox, oy, par, init_cost, cost_mv, out, mbo, live, sg,
+                                             lane, lists, fls[w][sg] );
+        tesa_wave_sync();                       // the next pass rewrites this wave's LDS
     }
 }
 
@@ -1914,6 +2029,37 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
         return hipSuccess;
     if( me_range < 1 || me_range > 32 || nmb > 0x7fffffff )
         return hipErrorInvalidValue;
+    // X264HIP_TESA_VARIANT=3: the self-contained call as ONE launch (me_tesa_fused_kernel:
+    // bit-exact, but 0.768 vs 0.652 ms per 16 1080p pairs, so not the default)
+    if constexpr( BD == 8 )
+    {
+        if( !table && me_range > 8 && me_range <= 16 && variant( V_TESA ) == 3 &&
+            !(((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)fs | (uintptr_t)rs) & 3) && nmb * 9 < (1ll << 32) )
+        {
+            constexpr int MPW = 256 / 9;
+            const size_t bytes = (size_t)nmb * 33 * 36 * sizeof( uint16_t );
+            const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
+            void *buf = nullptr;
+            if( tesa_scratch( &buf, bytes, stream ) == hipSuccess )
+            {
+                const int xcd = variant( V_ME_XCD ) != 0;
+                const dim3 g( (unsigned)((nmb + MPW - 1) / MPW) );
+                const size_t lds = (size_t)8 * cap * sizeof( uint32_t );
+                if( me_lead() <= 1 )
+                    hipLaunchKernelGGL( ( me_tesa_fused_kernel<1> ), g, dim3( 256 ), lds, stream, fenc, fs, ffs, ref,
+                                        rs, rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, (uint16_t *)buf,
+                                        par, init_cost, cost_mv, out, cap, xcd );
+                else
+                    hipLaunchKernelGGL( ( me_tesa_fused_kernel<2> ), g, dim3( 256 ), lds, stream, fenc, fs, ffs, ref,
+                                        rs, rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, (uint16_t *)buf,
+                                        par, init_cost, cost_mv, out, cap, xcd );
+                const hipError_t e = hipGetLastError();
+                const hipError_t f = hipFreeAsync( buf, stream );
+                return e != hipSuccess ? e : f;
+            }
+            (void)hipGetLastError();                        // no scratch: the in-kernel SADs below
+        }
+    }
     if( !table && me_range <= 24 && variant( V_TESA ) != 1 )
     {
         // Self-contained call: the ads-filtered SADs cost a lane 16 unaligned row loads
