@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Time the fused DCT+quant legs of bench.py alone (64 1080p pairs, the prediction a
+buffer of its own) for a PMC / trace pass: dq_time.py [frames] [iterations]"""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from __graft_entry__ import load_package  # noqa: E402
+
+
+def main():
+    F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+    n = int(sys.argv[2]) if len(sys.argv) > 2 else 30
+    x = load_package()
+    x.init(0)
+    from x264hip import synth
+    W, H = 1920, 1088
+    mbw, mbh = W // 16, H // 16
+    planes, stride, origin = synth.make_sequence(F + 1, W, H, 8)
+    dev = torch.from_numpy(planes).cuda()
+    pred = dev[:-1].clone()
+    fs = planes[0].size
+    q4m, q4b, q8m, q8b = x.cqm_init(8, [[16] * 64] * 8)
+    nmb = F * mbw * mbh
+    dct = torch.empty((nmb, 256), dtype=torch.int16, device="cuda")
+    nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
+    res = {}
+    for t in (4, 8):
+        mf, bs = (q4m[1, 26], q4b[1, 26]) if t == 4 else (q8m[1, 26], q8b[1, 26])
+        mf, bs = torch.from_numpy(mf.copy()).cuda(), torch.from_numpy(bs.copy()).cuda()
+
+        def step():
+            x.mb_dct_quant(t, dev[1:], origin, stride, pred, origin, stride, mbw, mbh, F, mf, bs, dct=dct, nz=nz,
+                           fenc_frame_stride=fs, pred_frame_stride=fs)
+        for _ in range(100):
+            step()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(n):
+            step()
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / n
+        blocks = nmb * (16 if t == 4 else 4)
+        bpb = 64 if t == 4 else 256
+        res["dct%d_ms" % t] = ms
+        res["dct%d_hbm_frac" % t] = blocks * bpb / (ms * 1e-3) / 8e12
+        res["dct%d_algorithmic_bytes" % t] = blocks * bpb
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
