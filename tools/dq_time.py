@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Time the fused DCT+quant legs of bench.py alone (64 1080p pairs, the prediction a
-buffer of its own) for a PMC / trace pass: dq_time.py [frames] [iterations]"""
+buffer of its own) for a PMC / trace pass: dq_time.py [frames] [iterations] [variant]"""
 import json
 import os
 import sys
@@ -12,7 +12,18 @@ sys.path.insert(0, ROOT)
 from __graft_entry__ import load_package  # noqa: E402
 
 
+# A/B over (X264HIP_DQ_VARIANT, X264HIP_STREAM_XCD) pairs, "d" = the default: the default
+# kernels (sector-shifted strips, 4x4 two strips per wave), variant 5 (one strip per wave),
+# four strips per wave (9), XCD order on (1) and the unshifted strips (2); a fourth argument
+# "default" times the default alone (PMC passes)
+VARIANTS = ("d/d", "5/d", "9/d", "d/1", "d/2")
+ROUNDS = 5
+
+
 def main():
+    global VARIANTS, ROUNDS
+    if len(sys.argv) > 3:
+        VARIANTS, ROUNDS = ("d/d",), 1
     F = int(sys.argv[1]) if len(sys.argv) > 1 else 64
     n = int(sys.argv[2]) if len(sys.argv) > 2 else 30
     x = load_package()
@@ -38,18 +49,30 @@ def main():
                            fenc_frame_stride=fs, pred_frame_stride=fs)
         for _ in range(100):
             step()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(n):
-            step()
-        e.record()
-        torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / n
         blocks = nmb * (16 if t == 4 else 4)
         bpb = 64 if t == 4 else 256
-        res["dct%d_ms" % t] = ms
-        res["dct%d_hbm_frac" % t] = blocks * bpb / (ms * 1e-3) / 8e12
         res["dct%d_algorithmic_bytes" % t] = blocks * bpb
+        times = {v: [] for v in VARIANTS}
+        for _ in range(ROUNDS):                      # interleaved rounds (the clock drifts)
+            for v in VARIANTS:
+                dv, xv = v.split("/")
+                x.set_variant("X264HIP_DQ_VARIANT", None if dv == "d" else int(dv))
+                x.set_variant("X264HIP_STREAM_XCD", None if xv == "d" else int(xv))
+                step()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(n):
+                    step()
+                e.record()
+                torch.cuda.synchronize()
+                times[v].append(s.elapsed_time(e) / n)
+        x.set_variant("X264HIP_STREAM_XCD", None)
+        x.set_variant("X264HIP_DQ_VARIANT", None)
+        for v in VARIANTS:
+            ms = sorted(times[v])[len(times[v]) // 2]
+            tag = "" if v == "d/d" else "_" + v.replace("/", "_")
+            res["dct%d%s_ms" % (t, tag)] = ms
+            res["dct%d%s_hbm_frac" % (t, tag)] = blocks * bpb / (ms * 1e-3) / 8e12
     print(json.dumps(res))
 
 
