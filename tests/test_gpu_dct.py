@@ -261,3 +261,35 @@ def test_mb_dct8_quant_extremes(hip, oracle, monkeypatch, variant, cqm):
                                              mbw, mbh, mf, bias)
                 assert np.array_equal(dct[f * nmb:(f + 1) * nmb], wd), (qp, lst, f)
                 assert np.array_equal(nz[f * nmb:(f + 1) * nmb], wn), (qp, lst, f)
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("transform", [4, 8])
+@pytest.mark.parametrize("dx", [0, 16, 48])
+@pytest.mark.parametrize("stream_xcd", [None, 1, 2])
+def test_mb_dct_quant_strip_alignment(hip, oracle, bd, transform, dx, stream_xcd):
+    """the default fused kernels with their strips shifted onto 64-byte sectors of the source
+    (shift 0-3 MBs from the fenc pointer's offset in its sector: dx moves it), with the
+    XCD-contiguous strip order (X264HIP_STREAM_XCD=1) and unshifted (=2); a ragged
+    20-MB row so the shifted strips begin left of the row and end past it."""
+    from x264hip import synth
+    if stream_xcd is not None:
+        hip.set_variant("X264HIP_STREAM_XCD", stream_xcd)
+    W, H = 320, 64
+    planes, stride, origin = synth.make_sequence(3, W + 64, H, bd, seed=dx + transform)
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
+    fsz = planes[0].size
+    q4m, q4b, q8m, q8b = hip.cqm_init(bd, cb.cqm_lists(0, bd))
+    qp = 20 + 6 * (bd - 8)
+    mf, bias = (q4m[1, qp], q4b[1, qp]) if transform == 4 else (q8m[1, qp], q8b[1, qp])
+    fo, po = origin + dx, origin + stride + 5
+    dct, nz = hip.mb_dct_quant(transform, dev[1:], fo, stride, dev[:-1], po, stride, W // 16, H // 16, 2,
+                               torch.from_numpy(mf.copy()).cuda(), torch.from_numpy(bias.copy()).cuda(),
+                               fenc_frame_stride=fsz, pred_frame_stride=fsz)
+    dct, nz = dct.cpu().numpy(), nz.cpu().numpy()
+    nmb = (W // 16) * (H // 16)
+    for f in range(2):
+        wd, wn = oracle.mb_dct_quant(bd, transform, planes[f + 1].ravel(), fo, stride, planes[f].ravel(), po,
+                                     stride, W // 16, H // 16, mf, bias)
+        assert np.array_equal(dct[f * nmb:(f + 1) * nmb], wd), f
+        assert np.array_equal(nz[f * nmb:(f + 1) * nmb], wn), f

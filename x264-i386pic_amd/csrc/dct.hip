@@ -672,13 +672,14 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
     const typename PT<BD>::pixel *__restrict__ pred, intptr_t ps, intptr_t pfs, int mbw, int mbh, int nframes,
     const typename PT<BD>::udctcoef *__restrict__ mf, const typename PT<BD>::udctcoef *__restrict__ bias,
-    typename PT<BD>::dctcoef *__restrict__ dct, int32_t *__restrict__ nz )
+    typename PT<BD>::dctcoef *__restrict__ dct, int32_t *__restrict__ nz, int xcd, int sh )
 {
     using dctcoef = typename PT<BD>::dctcoef;
     constexpr int PPD = PT<BD>::PPD;
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int spr = (mbw + 7) >> 3;
+    const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
+    const int64_t wave = ((int64_t)blk * blockDim.x + threadIdx.x) >> 6;
+    const int spr = (mbw + sh + 7) >> 3;
     if( wave >= (int64_t)nframes * mbh * spr )
         return;                                               // wave-uniform
     const int strip = (int)(wave % spr);
@@ -686,8 +687,9 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
     const int mby = (int)(t % mbh);
     const int64_t f = t / mbh;
     const int m = (lane & 15) >> 1, half = lane & 1, by = lane >> 4;
-    const int mbx = strip * 8 + m;
-    const bool live = mbx < mbw;
+    const int first = strip * 8 - sh;                         // the strip's first MB (< 0: left of the row)
+    const int mbx = first + m;
+    const bool live = mbx >= 0 && mbx < mbw;
     const int64_t mbrow = (f * mbh + mby) * (int64_t)mbw;
     __shared__ dctcoef lds[4 * 8 * 256];
     dctcoef *stage = lds + (threadIdx.x >> 6) * (8 * 256);
@@ -731,10 +733,10 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
         nz[mbrow + mbx] = mask;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
-    const int nmb = min( 8, mbw - strip * 8 );
-    const int nvec = nmb * 256 * (int)sizeof( dctcoef ) / 16;
-    const uint4 *src = (const uint4 *)stage;
-    uint4 *dst = (uint4 *)(dct + (mbrow + strip * 8) * 256);
+    const int lo = max( first, 0 ), hi = min( first + 8, mbw );
+    const int nvec = (hi - lo) * 256 * (int)sizeof( dctcoef ) / 16;
+    const uint4 *src = (const uint4 *)(stage + (lo - first) * 256);
+    uint4 *dst = (uint4 *)(dct + (mbrow + lo) * 256);
     for( int i = lane; i < nvec; i += 64 )
         st16<NT>( dst + i, src[i] );
 }
@@ -785,11 +787,13 @@ __global__ __launch_bounds__( 256 ) void mb_dct8_quant_pk_kernel( const uint8_t 
                                                                   intptr_t ps, intptr_t pfs, int mbw, int mbh,
                                                                   int nframes, const uint16_t *__restrict__ mf,
                                                                   const uint16_t *__restrict__ bias,
-                                                                  int16_t *__restrict__ dct, int32_t *__restrict__ nz )
+                                                                  int16_t *__restrict__ dct, int32_t *__restrict__ nz,
+                                                                  int xcd, int sh )
 {
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int spr = (mbw + 15) >> 4;
+    const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
+    const int64_t wave = ((int64_t)blk * blockDim.x + threadIdx.x) >> 6;
+    const int spr = (mbw + sh + 15) >> 4;
     if( wave >= (int64_t)nframes * mbh * spr )
         return;                                               // wave-uniform
     const int strip = (int)(wave % spr);
@@ -799,17 +803,21 @@ __global__ __launch_bounds__( 256 ) void mb_dct8_quant_pk_kernel( const uint8_t 
     const int64_t mbrow = (f * mbh + mby) * (int64_t)mbw;
     __shared__ uint4 lds[STAGE ? 4 * 64 * 8 : 1];             // per wave: 64 blocks x 8 chunks of 16 B
     uint4 *stage = lds + (threadIdx.x >> 6) * 512;
-    uint4 *dst = (uint4 *)(dct + (mbrow + strip * 16) * 256);
+    const int first = strip * 16 - sh;                        // the strip's first MB (< 0: left of the row)
+    const int lo = max( first, 0 ), hi = min( first + 16, mbw );
+    // chunk i (16 B) of the strip's MB (first + i / 32) lives at dst[i - c0]
+    const int c0 = (lo - first) * 32;
+    uint4 *dst = (uint4 *)(dct + (mbrow + lo) * 256);
     const int bx = lane & 31, by = lane >> 5;                 // 8x8 block column / row in the strip
-    const int mbx = strip * 16 + (bx >> 1);
-    const bool live = mbx < mbw;
+    const int mbx = first + (bx >> 1);
+    const bool live = mbx >= 0 && mbx < mbw;
     const int slot = (bx >> 1) * 4 + by * 2 + (bx & 1);      // block of the wave's 16 MBs, table order
     const int key = bx & 7;
     int mask = 0;
     if( live )
     {
-        const uint8_t *a = fenc + f * ffs + (intptr_t)(16 * mby + 8 * by) * fs + 256 * strip + 8 * bx;
-        const uint8_t *b = pred + f * pfs + (intptr_t)(16 * mby + 8 * by) * ps + 256 * strip + 8 * bx;
+        const uint8_t *a = fenc + f * ffs + (intptr_t)(16 * mby + 8 * by) * fs + 16 * first + 8 * bx;
+        const uint8_t *b = pred + f * pfs + (intptr_t)(16 * mby + 8 * by) * ps + 16 * first + 8 * bx;
         dq_s2 P[8][4];                                        // P[row][k] = (d[row][2k], d[row][2k+1])
 #pragma unroll
         for( int y = 0; y < 8; y++ )
@@ -886,7 +894,7 @@ __global__ __launch_bounds__( 256 ) void mb_dct8_quant_pk_kernel( const uint8_t 
             if constexpr( STAGE )
                 stage[slot * 8 + (x ^ key)] = v;
             else
-                dst[slot * 8 + x] = v;
+                dst[slot * 8 + x - c0] = v;
         }
     }
     mask |= __builtin_amdgcn_update_dpp( 0, mask, 0xB1, 0xF, 0xF, false );   // lane ^ 1
@@ -897,12 +905,11 @@ __global__ __launch_bounds__( 256 ) void mb_dct8_quant_pk_kernel( const uint8_t 
         return;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
-    const int nmb = min( 16, mbw - strip * 16 );
-    for( int i = lane; i < nmb * 32; i += 64 )
+    for( int i = c0 + lane; i < (hi - first) * 32; i += 64 )
     {
         const int s = i >> 3;
         const int k = (((s >> 2) * 2 + (s & 1)) & 7);        // the writer's key
-        st16<NT>( dst + i, stage[s * 8 + ((i & 7) ^ k)] );
+        st16<NT>( dst + i - c0, stage[s * 8 + ((i & 7) ^ k)] );
     }
 }
 #undef DCT8_1D_PK
@@ -930,15 +937,30 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
         // nontemporal coefficient stores (stream_nt): 64 frames 4x4 0.0985 -> 0.0876 ms, 8x8
         // 0.1029 -> 0.0776 ms; 16 frames 0.0279 -> 0.0267, 0.0263 -> 0.0247 (profiles/r03s_nt_ab.json)
         const bool nt = stream_nt();
+        // XCD-contiguous strips (X264HIP_STREAM_XCD=1 turns them on): a row's neighbouring
+        // strips share the 128-B lines their MB columns straddle, so in one XCD's L2 those
+        // lines are fetched once instead of once per XCD.  With the sector shift below no
+        // line is shared and the order only cost time (64 frames: 0.1056 vs 0.1023 ms for 4x4,
+        // profiles/r03af_dq_ab.log), so it is off by default
+        const int xcd = variant( V_STREAM_XCD ) == 1;
+        // Sector-aligned strips (as launch_mb_recon does for its stores): with row and frame
+        // strides multiples of 64 bytes, x = 0 sits at the same offset in a 64-byte sector on
+        // every row, so shifting the strips left by that offset (in MBs) puts every wave's
+        // row pieces of the source on whole sectors, none shared by two waves
+        // (X264HIP_STREAM_XCD=2 keeps the unshifted strips).
+        const size_t psz = sizeof( typename PT<BD>::pixel );
+        const bool al = variant( V_STREAM_XCD ) != 2 && !(((size_t)fs * psz) & 63) && !(((size_t)ffs * psz) & 63);
+        const int off = al ? (int)((uintptr_t)fenc & 63) : 0;
+        const int sh = off % (16 * (int)psz) ? 0 : off / (16 * (int)psz);
         if( transform == 4 && (ev < 0 || ev == 5) )
         {
-            const int64_t hw = (int64_t)nframes * mbh * ((mbw + 7) / 8);
+            const int64_t hw = (int64_t)nframes * mbh * ((mbw + sh + 7) / 8);
             if( nt )
                 hipLaunchKernelGGL( ( mb_dct_quant_halfband_kernel<BD, true> ), dim3( (unsigned)((hw + 3) / 4) ), blk,
-                                    0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+                                    0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
             else
                 hipLaunchKernelGGL( mb_dct_quant_halfband_kernel<BD>, dim3( (unsigned)((hw + 3) / 4) ), blk, 0, stream,
-                                    fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+                                    fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
             return hipGetLastError();
         }
         if( transform == 4 && (ev == 3 || ev == 4) )
@@ -956,15 +978,16 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
         if constexpr( BD == 8 )
             if( transform == 8 && (ev < 0 || ev == 6 || ev == 7) )
             {
+                g = dim3( (unsigned)(((int64_t)nframes * mbh * ((mbw + sh + 15) / 16) + 3) / 4) );
                 if( (ev < 0 || ev == 6) && nt )
                     hipLaunchKernelGGL( ( mb_dct8_quant_pk_kernel<true, true> ), g, blk, 0, stream, fenc, fs, ffs, pred,
-                                        ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+                                        ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
                 else if( ev < 0 || ev == 6 )
                     hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<true>, g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs,
-                                        mbw, mbh, nframes, mf, bias, dct, nz );
+                                        mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
                 else
                     hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<false>, g, blk, 0, stream, fenc, fs, ffs, pred, ps,
-                                        pfs, mbw, mbh, nframes, mf, bias, dct, nz );
+                                        pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
                 return hipGetLastError();
             }
         const bool stage = ev != 2;
