@@ -176,10 +176,12 @@ def test_dc_and_quant_dc_batch(hip, oracle, bd):
             assert np.array_equal(g[i], want) and nz[i] == wnz, (name, i)
 
 
-@pytest.fixture(params=["default", "nt", "0", "1", "2", "3", "4", "5", "6", "7"])
+@pytest.fixture(params=["default", "nt", "0", "1", "2", "3", "4", "5", "6", "7", "11", "12"])
 def dq_variant(request, monkeypatch):
     """X264HIP_DQ_VARIANT: 0 / 2 staged / unstaged strip, 1 block-major, 3 / 4 band layout staged /
-    direct, 5 half band (transform 4), 6 / 7 packed 16-bit staged / direct (8 bit, transform 8);
+    direct, 5 half band (transform 4), 6 / 7 packed 16-bit staged / direct (8 bit, transform 8),
+    11 / 12 staged strip in one- / four-wave workgroups with the stream store policy (11 is the
+    10-bit transform-8 default);
     nt = the default kernels with nontemporal coefficient stores forced (X264HIP_STREAM_NT=1,
     chosen by footprint above ~192 MiB per launch)."""
     if request.param == "nt":

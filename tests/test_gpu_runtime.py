@@ -133,3 +133,35 @@ def test_init_hip_overrides_only(hip):
         assert all(raw[i] == 0x5EED0000 + i for i in range(i0, i0 + n)), f
     i_sad = hip.PixelFunctions.sad.offset // 8
     assert raw[i_sad] != 0x5EED0000 + i_sad
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_empty_launches(hip, bd):
+    """every hot-path batched entry with no work (0 frames, or a 0-MB-wide frame for the
+    MB-grid entries) returns 0 and writes nothing (the sentinel-filled output stays untouched)"""
+    L = hip.lib()
+    buf = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    out = torch.full((4096,), 0x5A5A5A5A, dtype=torch.int32, device="cuda")
+    P = ctypes.c_void_p(buf.data_ptr())
+    O = ctypes.c_void_p(out.data_ptr())
+    pre = f"x264hip_{bd}_"
+    fn = lambda n: getattr(L, pre + n)
+    dst4 = (ctypes.c_void_p * 4)(*([P.value] * 4))
+    for nf, mbw in ((0, 4), (2, 0)):
+        calls = {
+            "me_search_full": lambda: fn("me_search_full")(P, 64, 0, P, 64, 0, mbw, 2, nf, 16, O, None),
+            "me_search_full8": lambda: fn("me_search_full8")(P, 64, 0, P, 64, 0, mbw, 2, nf, 16, O, None),
+            "me_tesa": lambda: fn("me_tesa")(P, 64, 0, P, 64, 0, P, 0, mbw, 2, nf, 16, 1, None, 0, None, P, P, P,
+                                             O, None),
+            "hpel_filter": lambda: fn("hpel_filter")(P, O, O, O, 64, 0, 64, 32, 0, None),
+            "mb_dct_quant4": lambda: fn("mb_dct_quant")(4, P, 64, 0, P, 64, 0, mbw, 2, nf, P, P, O, O, None),
+            "mb_dct_quant8": lambda: fn("mb_dct_quant")(8, P, 64, 0, P, 64, 0, mbw, 2, nf, P, P, O, O, None),
+            "frame_init_lowres": lambda: fn("frame_init_lowres")(P, 64, 0, 64, 32, 0, dst4, 64, 0, None),
+            "frame_integral": lambda: fn("frame_integral")(P, 64, 0, 32, 32, 0, 0, O, 0, None),
+        }
+        for name, call in calls.items():
+            # the 8x8 quadrant tables exist at 8 bit only: EINVAL at 10, work or not
+            want = -1 if name == "me_search_full8" and bd == 10 else 0
+            assert call() == want, (name, nf, mbw)
+    torch.cuda.synchronize()
+    assert (out == 0x5A5A5A5A).all()

@@ -5,6 +5,7 @@ import json
 import os
 import sys
 
+import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -14,10 +15,12 @@ from __graft_entry__ import load_package  # noqa: E402
 
 # A/B over (X264HIP_DQ_VARIANT, X264HIP_STREAM_XCD) pairs, "d" = the default: the default
 # kernels (sector-shifted strips), XCD order on (1) and the unshifted strips (2); a fourth
-# argument "default" times the default alone (PMC passes).  Rounds r03ag / r03ah also timed
+# argument "default" times the default alone (PMC passes); 11 / 12 = the staged strip
+# kernel with nontemporal stores in one- / four-wave workgroups, 2 = the unstaged strip
+# kernel.  DQ_BD=10: 10-bit planes.  Rounds r03ag / r03ah also timed
 # two and four strips per wave (4x4) and one-wave workgroups (8x8): all within 1 % of the
 # defaults, so those kernels were dropped.
-VARIANTS = ("d/d", "d/1", "d/2")
+VARIANTS = ("d/d", "d/1", "d/2", "11/d", "12/d", "2/d")
 ROUNDS = 5
 
 
@@ -30,19 +33,22 @@ def main():
     x = load_package()
     x.init(0)
     from x264hip import synth
+    bd = int(os.environ.get("DQ_BD", "8"))
     W, H = 1920, 1088
     mbw, mbh = W // 16, H // 16
-    planes, stride, origin = synth.make_sequence(F + 1, W, H, 8)
-    dev = torch.from_numpy(planes).cuda()
+    planes, stride, origin = synth.make_sequence(F + 1, W, H, bd)
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     pred = dev[:-1].clone()
     fs = planes[0].size
-    q4m, q4b, q8m, q8b = x.cqm_init(8, [[16] * 64] * 8)
+    q4m, q4b, q8m, q8b = x.cqm_init(bd, [[16] * 64] * 8)
+    qp = 26 + 6 * (bd - 8)
     nmb = F * mbw * mbh
-    dct = torch.empty((nmb, 256), dtype=torch.int16, device="cuda")
+    dct = torch.empty((nmb, 256), dtype=torch.int16 if bd == 8 else torch.int32, device="cuda")
     nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
-    res = {}
+    res = {"bit_depth": bd}
+    ps = 1 if bd == 8 else 2
     for t in (4, 8):
-        mf, bs = (q4m[1, 26], q4b[1, 26]) if t == 4 else (q8m[1, 26], q8b[1, 26])
+        mf, bs = (q4m[1, qp], q4b[1, qp]) if t == 4 else (q8m[1, qp], q8b[1, qp])
         mf, bs = torch.from_numpy(mf.copy()).cuda(), torch.from_numpy(bs.copy()).cuda()
 
         def step():
@@ -51,7 +57,7 @@ def main():
         for _ in range(100):
             step()
         blocks = nmb * (16 if t == 4 else 4)
-        bpb = 64 if t == 4 else 256
+        bpb = (64 if t == 4 else 256) * ps
         res["dct%d_algorithmic_bytes" % t] = blocks * bpb
         times = {v: [] for v in VARIANTS}
         for _ in range(ROUNDS):                      # interleaved rounds (the clock drifts)

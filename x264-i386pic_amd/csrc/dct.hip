@@ -465,8 +465,11 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_kernel( const typename PT<
 // coalesced); for T=8 lane l owns 8x8 column l%32 of block row l/32 (two
 // 256-byte row segments per load).  The per-MB nz mask is OR-combined across
 // the MB's lanes with DPP / lane swaps.
-template <int BD, int T, bool STAGE>
-__global__ __launch_bounds__( 256 ) void mb_dct_quant_strip_kernel(
+// NT: nontemporal coefficient stores; WPB waves per workgroup (4, or 1: a quarter of the
+// LDS stage per workgroup -- 16 KB instead of 64 at 10 bit, where the stage held the kernel
+// to 2 resident waves per SIMD)
+template <int BD, int T, bool STAGE, bool NT = false, int WPB = 4>
+__global__ __launch_bounds__( 64 * WPB ) void mb_dct_quant_strip_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
     const typename PT<BD>::pixel *__restrict__ pred, intptr_t ps, intptr_t pfs, int mbw, int mbh, int nframes,
     const typename PT<BD>::udctcoef *__restrict__ mf, const typename PT<BD>::udctcoef *__restrict__ bias,
@@ -487,7 +490,7 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_strip_kernel(
     // STAGE: the wave's 16 MBs of coefficients are assembled in LDS and leave as
     // one contiguous run of 16 B per lane stores
     using dctcoef = typename PT<BD>::dctcoef;
-    __shared__ dctcoef lds[STAGE ? 4 * 16 * 256 : 1];
+    __shared__ dctcoef lds[STAGE ? WPB * 16 * 256 : 1];
     dctcoef *stage = lds + (threadIdx.x >> 6) * (16 * 256);
     if constexpr( T == 4 )
     {
@@ -564,7 +567,7 @@ __global__ __launch_bounds__( 256 ) void mb_dct_quant_strip_kernel(
         const uint4 *src = (const uint4 *)stage;
         uint4 *dst = (uint4 *)(dct + (mbrow + strip * 16) * 256);
         for( int i = lane; i < nvec; i += 64 )
-            dst[i] = src[i];
+            st16<NT>( dst + i, src[i] );
     }
 }
 
@@ -991,6 +994,32 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
                 return hipGetLastError();
             }
         const bool stage = ev != 2;
+        // 10-bit transform 8 default: variant 11 (0.2011 vs 0.2165 ms for the four-wave
+        // staged strips with plain stores at 64 1080p pairs, 0.665 vs 0.618 of HBM: the 64 KB
+        // stage of a four-wave workgroup held it to 2 waves per SIMD; profiles/r03aj_dq_ab10.log)
+        const int sv = ev < 0 && BD == 10 && transform == 8 ? 11 : ev;
+        if( sv == 11 || sv == 12 )
+        {
+            // staged strips with the stream store policy (nontemporal unless X264HIP_STREAM_NT=0):
+            // 11 one-wave workgroups, 12 four-wave
+#define DQ_STRIP_W( T, W )                                                                                       \
+    do                                                                                                           \
+    {                                                                                                            \
+        const dim3 gw( W == 1 ? (unsigned)waves : g.x ), bw( 64 * W );                                           \
+        if( nt )                                                                                                 \
+            hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, true, true, W> ), gw, bw, 0, stream, fenc, fs, \
+                                ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );                      \
+        else                                                                                                     \
+            hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, true, false, W> ), gw, bw, 0, stream, fenc,  \
+                                fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );                  \
+    } while( 0 )
+            if( transform == 4 && sv == 11 ) DQ_STRIP_W( 4, 1 );
+            else if( transform == 4 ) DQ_STRIP_W( 4, 4 );
+            else if( sv == 11 ) DQ_STRIP_W( 8, 1 );
+            else DQ_STRIP_W( 8, 4 );
+#undef DQ_STRIP_W
+            return hipGetLastError();
+        }
 #define DQ_STRIP( T, S ) hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, S> ), g, blk, 0, stream, fenc, fs, ffs, \
                                              pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz )
         if( transform == 4 )
