@@ -1,0 +1,42 @@
+"""bench.py's one-line JSON contract on the GPU (short run: 2 timed steps, headline only,
+a 0.3-s CPU sample): the keys the driver and the judge read, their types and the
+consistency of the roofline record with the line's own numbers."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_bench_json_contract():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "2", "--warmup", "1",
+                        "--frames", "8", "--no-extra", "--cpu-seconds", "0.3"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["higher_is_better"] is True and d["scaling"] == "weak" and d["dtype"] == "u8"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    assert "workload" in d["config"] and "model" not in d["config"]
+    rf = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in rf, k
+    assert rf["frac"] == pytest.approx(rf["achieved"] / rf["peak"], rel=1e-6)
+    assert 0 < rf["frac"] < 1
+    # value = candidates per step / step time; launch_ms <= ms_per_step
+    cands = d["config"]["frames_per_step_per_gpu"] * d["config"]["mbs_per_frame"] * d["config"]["candidates_per_mb"]
+    assert d["value"] == pytest.approx(cands / (d["ms_per_step"] * 1e-3), rel=1e-3)
+    assert rf["launch_ms"] <= d["ms_per_step"] * 1.001
+    cb = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in cb, k
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
