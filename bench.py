@@ -250,7 +250,11 @@ def main():
     # tools/pmc_summarize.py: separate FETCH_SIZE / WRITE_SIZE passes, gfx950-corrected),
     # used only when it profiled this kernel on this workload
     import glob
-    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))
+    def _tag_order(path):
+        # round tags rNNx..: r03z < r03aa < r03ab (one letter runs out before two)
+        t = os.path.basename(path).split("_")[0]
+        return (t[:3], len(t), t)
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")), key=_tag_order)
     if pmcs:
         with open(pmcs[-1]) as fh:
             d = json.load(fh)
