@@ -1402,6 +1402,14 @@ __device__ __forceinline__ uint32_t tesa_sad16( const uint32_t *fenc_lds, const 
     return acc;
 }
 
+// |a - b| + c of unsigned 32-bit values (v_sad_u32; clang has no builtin for it)
+__device__ __forceinline__ uint32_t sad_u32( uint32_t a, uint32_t b, uint32_t c )
+{
+    uint32_t d;
+    asm( "v_sad_u32 %0, %1, %2, %3" : "=v"( d ) : "v"( a ), "v"( b ), "v"( c ) );
+    return d;
+}
+
 // inclusive min-scan over each SEG-lane segment (32 or 64) with DPP: row_shr 1/2/4/8
 // inside the 16-lane rows, then row_bcast:15 (and :31 for a 64-lane segment) across
 // them -- no LDS-crossbar round trips (ds_bpermute) on TESA's serial row chain
@@ -1584,14 +1592,19 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
     const int cxm = active ? mx : min_x;
     const int tx = mx - ox, txc = min( max( tx, 0 ), W - 1 );
     const bool colin = tx >= 0 && tx < W;
+    // rows as 24-bit multiplies of small offsets from per-lane bases (j <= 2*32+8 rows of a
+    // stride below 2^18 elements; table rows < 66 of a pitch < 69), not 64-bit address math
+    const uint16_t *ib = sums_base + cxm + (intptr_t)min_y * rs;
+    const uint32_t irs = (uint32_t)rs;
+    const int rmax = rows + 7, ty0 = min_y - oy;
     auto ldi = [&]( int j, uint32_t &v0, uint32_t &v8 ) {
-        const uint16_t *sp = sums_base + cxm + (intptr_t)(min_y + min( j, rows + 7 )) * rs;
+        const uint16_t *sp = ib + __umul24( (uint32_t)min( j, rmax ), irs );
         v0 = sp[0];
         v8 = sp[8];
     };
     auto ldt = [&]( int r ) -> uint32_t {
         if constexpr( TAB )
-            return (uint32_t)tab[min( max( min_y + r - oy, 0 ), W - 1 ) * P + txc];
+            return (uint32_t)tab[__umul24( (uint32_t)min( max( ty0 + r, 0 ), W - 1 ), (uint32_t)P ) + txc];
         else
             return 0u;
     };
@@ -1651,22 +1664,28 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
         __builtin_amdgcn_sched_barrier( 0 );
         const int st = c % D, sb = (c + 8 / CK) % D;
         uint32_t sr_k[CK], ads_k[CK];
+        int ys_k[CK];                                         // the rows' ycost (TAB: read once)
 #pragma unroll
         for( int k = 0; k < CK; k++ )
         {
             sr_k[k] = ads_k[k] = 0xFFFFFFFFu;
+            ys_k[k] = 0;
             const int r = CK * c + k;
             if( r >= NR )
                 break;
-            const uint32_t av = (uint32_t)(abs( enc_dc[0] - (int)i0[st][k] ) + abs( enc_dc[1] - (int)i8[st][k] ) +
-                                           abs( enc_dc[2] - (int)i0[sb][k] ) + abs( enc_dc[3] - (int)i8[sb][k] ) +
-                                           fpel);
+            // |dc - sum| + acc in one v_sad_u32 each (every operand is a non-negative sum)
+            const uint32_t av = sad_u32( (uint32_t)enc_dc[0], i0[st][k],
+                                         sad_u32( (uint32_t)enc_dc[1], i8[st][k],
+                                                  sad_u32( (uint32_t)enc_dc[2], i0[sb][k],
+                                                           sad_u32( (uint32_t)enc_dc[3], i8[sb][k],
+                                                                    (uint32_t)fpel ) ) ) );
             const uint32_t ads = r < rows && active ? av : 0xFFFFFFFFu;
             uint32_t sr = 0xFFFFFFFFu;
             if constexpr( TAB )
             {
                 // with a table the SADs are reads (the rare candidate outside it computed)
                 const int ycost = ycost_of( r ), ty = min_y + r - oy;
+                ys_k[k] = ycost;
                 const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
                 const bool need = r < rows && ads < (uint32_t)ub;
                 sr = tt[k];
@@ -1701,7 +1720,7 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
                 uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)incl, 0x138, 0xF, 0xF, false );
                 excl_k[k] = lane ? ex : 0xFFFFFFFFu;
                 rmin_k[k] = seg_lane<SEG>( incl, SEG - 1, sg );
-                yc_k[k] = ycost_of( CK * c + k );
+                yc_k[k] = ys_k[k];
             }
 #pragma unroll
             for( int k = 0; k < CK; k++ )
@@ -2027,7 +2046,8 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     const int64_t nmb = (int64_t)nframes * mbw * mbh;
     if( nmb <= 0 )
         return hipSuccess;
-    if( me_range < 1 || me_range > 32 || nmb > 0x7fffffff )
+    // (the scan addresses rows by 24-bit products: strides below 2^18 elements)
+    if( me_range < 1 || me_range > 32 || nmb > 0x7fffffff || rs <= 0 || rs >= (1 << 18) )
         return hipErrorInvalidValue;
     // X264HIP_TESA_VARIANT=3: the self-contained call as ONE launch (me_tesa_fused_kernel:
     // bit-exact, but 0.768 vs 0.652 ms per 16 1080p pairs, so not the default)
