@@ -1452,6 +1452,17 @@ template <int SEG> __device__ __forceinline__ uint32_t seg_lane( uint32_t v, int
     }
 }
 
+// the same through the LDS crossbar (ds_bpermute, no VALU): lane l of this lane's segment.
+// For the per-row broadcasts of the TESA scan, where readlane + a per-segment select cost
+// four or five VALU instructions per row; `base` = (segment start lane) * 4.
+template <int SEG> __device__ __forceinline__ uint32_t seg_bcast( uint32_t v, int l, int base )
+{
+    if constexpr( SEG == 64 )
+        return (uint32_t)__builtin_amdgcn_readlane( (int)v, l );
+    else
+        return (uint32_t)__builtin_amdgcn_ds_bpermute( base + 4 * l, (int)v );
+}
+
 __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
 {
 #pragma unroll
@@ -1579,7 +1590,8 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
     // ycost of row r in segment lane r (rows SEG.. in the second register)
     const int yc0 = lane < rows ? (int)cy[(min_y + lane) * 4] : 0;
     const int yc1 = lane + SEG < rows ? (int)cy[(min_y + lane + SEG) * 4] : 0;
-    auto ycost_of = [&]( int r ) { return (int)seg_lane<SEG>( (uint32_t)(r < SEG ? yc0 : yc1), r % SEG, sg ); };
+    const int bbase = 4 * SEG * sg;                           // this segment's lane 0, in bytes
+    auto ycost_of = [&]( int r ) { return (int)seg_bcast<SEG>( (uint32_t)(r < SEG ? yc0 : yc1), r % SEG, bbase ); };
 
     // Staging: each row's ads4 value and -- with a table -- the cost of every candidate
     // that can still pass some row's threshold (bsad never rises, so row r's ADS threshold
@@ -1719,7 +1731,7 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
                 const uint32_t incl = seg_scan_min<SEG>( sr_k[k] );
                 uint32_t ex = (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)incl, 0x138, 0xF, 0xF, false );
                 excl_k[k] = lane ? ex : 0xFFFFFFFFu;
-                rmin_k[k] = seg_lane<SEG>( incl, SEG - 1, sg );
+                rmin_k[k] = seg_bcast<SEG>( incl, SEG - 1, bbase );
                 yc_k[k] = ys_k[k];
             }
 #pragma unroll
@@ -1734,7 +1746,8 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
                 const int b = bsad - ycost;
                 const bool pass = rowok && ads_k[k] < (uint32_t)(b * 17 >> 4);
                 const int bcur = (int)min( (uint32_t)b, excl_k[k] );
-                const bool app = pass && (int)sr_k[k] < (bcur * sad_thresh0 >> 3);
+                // costs < 2^20: a 24-bit multiply (v_mul_lo_u32 is quarter rate)
+                const bool app = pass && (int)sr_k[k] < (__mul24( bcur, sad_thresh0 ) >> 3);
                 const uint64_t m = sball( app );
                 if( app )
                     mvsads[nmvsad + rank( m )] = ent( sr_k[k] + (uint32_t)ycost, mx, my );
