@@ -705,9 +705,10 @@ int x264hip_##BD##_me_search_esa( const pixel *fenc, intptr_t fenc_stride, intpt
  * raster).  table (optional, NULL = none): a me_search_full / me_search_centred table of     \
  * the same pairs (origin NULL for me_search_full); SADs inside it are read, the rest are     \
  * computed.  With no table and me_range <= 24 the call builds one around the predictors in   \
- * stream-ordered scratch (hipMallocAsync, the device's default pool; ~2.4 KB per MB at       \
+ * stream-ordered scratch (a memory pool the library owns per device; ~2.4 KB per MB at      \
  * me_range 16, 8 bit) and reads it: the same decisions, 2.6x faster than in-scan SADs.       \
- * out[4*i] = { cost, mx, my, number of COST_MV candidates }.  me_range 1..32.                \
+ * out[4*i] = { cost, mx, my, number of COST_MV candidates }.  me_range 1..32; ref_stride     \
+ * below 2^18 pixels (the scan addresses rows by 24-bit products), else X264HIP_EINVAL.       \
  * The ESA window, the width-rounded columns and their integral sums must lie inside the      \
  * padded planes (mv_limit_fpel keeps them there in the encoder). */                          \
 int x264hip_##BD##_me_tesa( const pixel *fenc, intptr_t fenc_stride, intptr_t fenc_frame_stride,  \
