@@ -1477,6 +1477,10 @@ __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
 #ifndef TESA_CK
 #define TESA_CK 4
 #endif
+// minimum waves per SIMD of the scan kernel (a build-time knob for A/B builds)
+#ifndef TESA_WPE
+#define TESA_WPE 4
+#endif
 
 // SEG lanes per MB: 64 (one MB per wave, me_range <= 32) or 32 (two MBs per wave,
 // me_range <= 16: a row of <= 32 columns fits half a wave), so a wave's serial row
@@ -1891,7 +1895,7 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
 }
 
 template <int BD, int NR, int SEG, bool TAB, bool SPEC = false>
-__global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
+__global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( TESA_WPE ) ) ) void me_tesa_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
                                                         intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
                                                         intptr_t rs, intptr_t rfs,
                                                         const uint16_t *__restrict__ integral, intptr_t ifs, int mbw,
