@@ -1477,7 +1477,10 @@ __device__ __forceinline__ uint32_t wave_min_u32( uint32_t v )
 #ifndef TESA_CK
 #define TESA_CK 4
 #endif
-// minimum waves per SIMD of the scan kernel (a build-time knob for A/B builds)
+// minimum waves per SIMD of the scan kernel (a build-time knob for A/B builds): at 5 (96
+// VGPRs; LDS then holds ~4.5 waves per SIMD) the scan spills and runs slower -- 0.625 ms with
+// 1-row chunks, 0.655 with 2-row chunks, against 0.583 for 4 waves and 4-row chunks
+// (profiles/r03as/)
 #ifndef TESA_WPE
 #define TESA_WPE 4
 #endif
