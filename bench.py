@@ -429,8 +429,11 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     louts2 = x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span))
 
     def lastep():
-        x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2)
+        x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2,
+                            check=False)
+    # (the lookahead launches are asynchronous: the wavefront status is checked after each leg)
     wall, ev_ms = timed(lastep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+    x.lowres_status()
     res["lowres_me_pairs_per_s"] = world * max(1, a.steps // 5) * (F - 1) / wall
     res["lowres_me_launch_ms"] = ev_ms
     res["lowres_me_pairs_per_launch"] = F - 1
@@ -440,8 +443,9 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     for T in (4, 8):
         def lsstep(T=T):
             x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2,
-                                n_slices=T)
+                                n_slices=T, check=False)
         wall, ev_ms = timed(lsstep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+        x.lowres_status()
         res["lowres_me_slices%d_pairs_per_s" % T] = world * max(1, a.steps // 5) * (F - 1) / wall
         res["lowres_me_slices%d_launch_ms" % T] = ev_ms
     # the same search at a full-chip batch: 16 copies of those pairs in one launch (one
@@ -454,8 +458,9 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     bouts2 = x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span))
 
     def lbstep():
-        x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span), outs=bouts2)
+        x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span), outs=bouts2, check=False)
     wall, ev_ms = timed(lbstep, max(1, a.steps // 10), 2, world)
+    x.lowres_status()
     res["lowres_me_batch_pairs_per_s"] = world * max(1, a.steps // 10) * bf.shape[0] / wall
     res["lowres_me_batch_launch_ms"] = ev_ms
     res["lowres_me_batch_pairs_per_launch"] = int(bf.shape[0])
@@ -474,8 +479,9 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     bouts = x.lowres_bidir_cost(*bargs, p1_mvs=p1m)
 
     def bstep():
-        x.lowres_bidir_cost(*bargs, p1_mvs=p1m, outs=bouts)
+        x.lowres_bidir_cost(*bargs, p1_mvs=p1m, outs=bouts, check=False)
     wall, ev_ms = timed(bstep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+    x.lowres_status()
     res["lowres_bidir_triplets_per_s"] = world * max(1, a.steps // 5) * nt / wall
     res["lowres_bidir_launch_ms"] = ev_ms
     res["lowres_bidir_triplets_per_launch"] = nt
@@ -533,6 +539,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
         r64 = rates_ssd(x, a, world, full[:a.tframes + 1], origin, stride, a.tframes)
         res.update({k.replace("ssd_plane", "ssd_plane_%d" % a.tframes): v for k, v in r64.items()})
     res.update(rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
+    res.update(rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
     res.update(r2160)
     return res
@@ -584,7 +591,7 @@ def rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     res["tesa_mean_cost_mv_candidates"] = float(out[:, 3].float().mean().item())
     # the search as an encoder would drive it on the GPU: the exhaustive SAD table around each
     # MB's predictor (me_search_centred, the headline kernel) then the TESA scan reading it
-    table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
+    table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_centred_pitch(8, R)), dtype=torch.int16, device="cuda")
     org = torch.empty((F * mbw * mbh, 2), dtype=torch.int16, device="cuda")
     cen = par_d[:, :2].contiguous()
     out2 = torch.empty_like(out)
@@ -604,41 +611,99 @@ def rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     return res
 
 
+def esa_window_candidates(par, me_range):
+    """candidates me.c's ESA evaluates per MB (encoder/me.c:621-631): the clipped window's rows
+    times its width rounded as (max_x - min_x + 3) & ~3 -- the algorithmic count the ESA legs'
+    fractions are taken on (1056 per unclipped MB at me_range 16: 33 rows x 32 columns)"""
+    p = par.astype(np.int64)
+    min_x = np.maximum(p[:, 0] - me_range, p[:, 4])
+    min_y = np.maximum(p[:, 1] - me_range, p[:, 5])
+    max_x = np.minimum(p[:, 0] + me_range, p[:, 6])
+    max_y = np.minimum(p[:, 1] + me_range, p[:, 7])
+    width = (max_x - min_x + 3) & ~3
+    return int((np.maximum(max_y - min_y + 1, 0) * np.maximum(width, 0)).sum())
+
+
 def rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     """The ESA decision of every MB of the F pairs (me.c:618-631, window of me_range 16
-    centred on the predictor, here mv 0): the table path (the full-search kernel at
-    template range 24 + me_esa_argmin) against the fused kernel that never writes the
-    table.  Both evaluate the same 49x49 = 2401 template candidates per MB."""
-    # me_range = the bench's range (x264's default 16); the template holds me.c's rounded
-    # window around an aligned-down origin only with range >= me_range + 6 (8 bit), so the
-    # exact decision needs the 24 template (49x49 candidates per MB evaluated)
+    centred on the predictor, here mv 0): the table path (the centred search of me.c's
+    window, template range = me_range, + me_esa_argmin_at) against the fused kernel that
+    never writes the table.  Fractions are taken on the candidates me.c evaluates
+    (esa_window_candidates); the template the kernels compute (2R+1 rows x the centred
+    pitch, the alignment and width-rounding slack columns included) is reported beside."""
     me_range = a.range
-    R = next(r for r in (4, 8, 16, 24) if r >= me_range + 6)
+    R = me_range
     par, init, cm, span = tesa_params(mbw, mbh, F, me_range, centre=(0, 0))
     par_d, init_d = torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda()
     cm_d = torch.from_numpy(cm.view(np.int16)).cuda()
-    table = torch.empty((F, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
+    pitch = x.me_centred_pitch(8, R)
+    table = torch.empty((F, mbh, mbw, 2 * R + 1, pitch), dtype=torch.int16, device="cuda")
+    org = torch.empty((F * mbw * mbh, 2), dtype=torch.int16, device="cuda")
+    cen = par_d[:, :2].contiguous()
     out_t = torch.empty((F * mbw * mbh, 3), dtype=torch.int32, device="cuda")
     out_f = torch.empty_like(out_t)
 
+    def search():
+        x.me_search_centred(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, cen, table=table,
+                            origin=org, fenc_frame_stride=fstride, ref_frame_stride=fstride)
+
+    def argmin():
+        x.me_esa_argmin(table, R, me_range, par_d, init_d, (cm_d, span), out=out_t, origin=org)
+
     def tstep():
-        x.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, table=table,
-                         fenc_frame_stride=fstride, ref_frame_stride=fstride)
-        x.me_esa_argmin(table, R, me_range, par_d, init_d, (cm_d, span), out=out_t)
+        search()
+        argmin()
 
     def fstep():
         x.me_search_esa(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, me_range, par_d, init_d,
                         (cm_d, span), out=out_f, fenc_frame_stride=fstride, ref_frame_stride=fstride)
-    cands = F * mbw * mbh * (2 * R + 1) ** 2
+    cands = esa_window_candidates(par, me_range)
+    tmpl = F * mbw * mbh * (2 * R + 1) * pitch
     wall, ev_ms = timed(tstep, a.steps, a.warmup, world)
     res = {"esa_table_candidates_per_s": world * a.steps * cands / wall, "esa_table_step_ms": ev_ms,
-           "esa_template_range": R, "esa_me_range": me_range}
+           "esa_template_range": R, "esa_me_range": me_range,
+           "esa_window_candidates_per_mb": cands / (F * mbw * mbh),
+           "esa_template_candidates_per_mb": tmpl / (F * mbw * mbh)}
+    search()
+    wall, ev_ms = timed(argmin, a.steps, a.warmup, world, graph=True)
+    tbytes = table.numel() * table.element_size()
+    res["esa_argmin_launch_ms"] = ev_ms
+    res["esa_argmin_table_bytes"] = tbytes
+    res["esa_argmin_hbm_frac"] = tbytes / (ev_ms * 1e-3) / HBM_PEAK
     wall, ev_ms = timed(fstep, a.steps, a.warmup, world)
     res["esa_fused_candidates_per_s"] = world * a.steps * cands / wall
     res["esa_fused_step_ms"] = ev_ms
+    # SAD roofline on me.c's candidates (256 byte absdiffs each); the template's own rate beside
     res["esa_fused_frac"] = cands * 256 / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF
+    res["esa_fused_template_frac"] = tmpl * 256 / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF
     if not torch.equal(out_t, out_f):
         raise SystemExit("bench: fused and table ESA decisions disagree")
+    del table, org
+    return res
+
+
+def rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, bd=8):
+    """8x8 quadrant tables (me_search_full8, the lookup mode's source for PIXEL_16x8 / 8x16 /
+    8x8, analyse.c:1425,1480,1546) over the F pairs at range R: the VALU fraction (256
+    absdiffs per 16x16 candidate, the same work as the 16x16 table) and the HBM fraction of
+    the four quadrant tables written (8 B per candidate at the padded pitch) plus the planes."""
+    R = a.range
+    w, pitch = 2 * R + 1, x.me_table_pitch(R)
+    t8 = torch.empty((F, mbh, mbw, 4, w, pitch), dtype=torch.int16, device="cuda")
+
+    def step():
+        x.me_search_full8(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, table8=t8,
+                          fenc_frame_stride=fstride, ref_frame_stride=fstride)
+    wall, ev_ms = timed(step, a.steps, a.warmup, world)
+    cands = F * mbw * mbh * w * w
+    pre = "full8" if bd == 8 else "full8_10"
+    peak = SAD_PEAK_ABSDIFF if bd == 8 else SAD_PEAK_ABSDIFF / 2
+    es = dev.element_size()
+    moved = t8.numel() * 2 + 2 * F * (mbh * 16 + 64) * stride * es
+    res = {pre + "_candidates_per_s": world * a.steps * cands / wall, pre + "_launch_ms": ev_ms,
+           pre + "_valu_frac": cands * 256 / (ev_ms * 1e-3) / peak,
+           pre + "_hbm_frac": moved / (ev_ms * 1e-3) / HBM_PEAK, pre + "_table_bytes": t8.numel() * 2}
+    del t8
     return res
 
 
@@ -677,7 +742,9 @@ def rates_10bit(x, a, world, mbw, mbh, F):
     cands = F * mbw * mbh * (2 * R + 1) ** 2
     res = {"me10_candidates_per_s": world * a.steps * cands / wall, "me10_launch_ms": ev_ms,
            "me10_absdiff_frac_of_v_sad_u16_peak": cands * 256 / (ev_ms * 1e-3) / VALU_LANE_OPS}
-    del table, dev
+    del table
+    res.update(rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, bd=10))
+    del dev
     flat = [16] * 64
     _, _, q8m, q8b = x.cqm_init(10, [flat] * 8)
     mf8 = torch.from_numpy(q8m[1, 26 + 12].copy()).cuda()

@@ -348,18 +348,35 @@ int  x264hip_upload( void *dst, const void *host_src, size_t bytes, void *stream
  * x264hip_stream_destroy releases either. */
 int  x264hip_stream_pair_create( int reserve_cus, void **compute, void **copy );
 int  x264hip_stream_destroy( void *stream );
+/* release the idle blocks of the library's scratch pools on `device` (all devices for
+ * device < 0).  The self-contained me_tesa takes its table scratch (~2.6 KB per MB at
+ * me_range 16, 8 bit) from a per-device pool that keeps its peak between calls, so repeated
+ * calls do not map fresh pages; this returns it to the device. */
+int  x264hip_trim( int device );
+/* the lookahead wavefront's status: waits for `stream`, then X264HIP_EDEVICE if a
+ * lowres_inter_cost / lowres_bidir_cost launch of the calling thread on the stream's device
+ * timed out waiting for the band below (its outputs are then invalid; see
+ * x264hip_set_variant's X264HIP_LA_POLL), else 0; reporting clears the condition.  The
+ * lookahead entries themselves are asynchronous and capturable: each also reports (and
+ * refuses to launch) once an earlier launch's failure has reached the host. */
+int  x264hip_lowres_status( void *stream );
+/* row pitch (entries) of a me_search_full table (centred = 0: align4(2*range+1)) or a
+ * me_search_centred table (centred = 1: align4(2*range+6) at 8 bit, align4(2*range+4) at
+ * 10 bit -- me.c's ESA window around the centre), 0 for a bad bitdepth / range */
+int  x264hip_me_table_pitch( int bitdepth, int range, int centred );
 /* one line naming the device and the table entries the HIP backend fills (the
  * analogue of reference encoder/encoder.c:1676-1706); also printed once to
  * stderr at the first table fill unless X264HIP_QUIET=1 */
 const char *x264hip_backend_banner( void );
-/* A/B kernel switches by environment name (X264HIP_ME_VARIANT, X264HIP_HPEL_VARIANT,
- * X264HIP_HPEL_ROWS, X264HIP_SUBPEL_VARIANT, X264HIP_LOWRES_VARIANT, X264HIP_DQ_VARIANT,
- * X264HIP_RECON_VARIANT, X264HIP_LOWRES_INTRA_VARIANT): the environment seeds them
- * once; this changes one at run time (-1 = default).  X264HIP_EINVAL for an
- * unknown name.  Every variant is bit-exact; only speed differs.  One switch is a test
- * hook, not a variant: X264HIP_LA_POLL bounds the lookahead wavefront's wait for the band
- * below (default 2^22 tries); 0 forces the timeout path, whose entry then returns
- * X264HIP_EDEVICE. */
+/* Run-time switches by environment name; the environment seeds them once, this changes one
+ * at run time (-1 = default), X264HIP_EINVAL for an unknown name.  Each input has one kernel;
+ * the switches select layout / store options measured within 3 % of the default
+ * (X264HIP_ME_XCD, X264HIP_STREAM_XCD, X264HIP_STREAM_NT) or force a kernel that is the default
+ * for other inputs (X264HIP_TESA_VARIANT=1: the in-scan SADs of me_range > 24;
+ * X264HIP_INTEGRAL_VARIANT=1: the unaligned-plane integral kernel); X264HIP_UPLOAD_WGS caps
+ * the upload grid.  All are bit-exact; only speed differs.  One switch is a test hook:
+ * X264HIP_LA_POLL bounds the lookahead wavefront's wait for the band below (default 2^22
+ * tries); 0 forces the timeout path (see x264hip_lowres_status). */
 int  x264hip_set_variant( const char *name, int value );
 
 /* Table lookup mode of the drop-in 16x16 SAD entries (SURVEY.md §7 hard part 1(b)):
@@ -388,7 +405,7 @@ void x264hip_me_bind_stats( uint64_t *hits, uint64_t *misses, int reset );
 int x264hip_##BD##_me_bind( const pixel *fenc, const pixel *ref, intptr_t stride,               \
                             int mb_width, int mb_height, const sadt *table, int range );        \
 /* the general form: a 16x16 table (or NULL) and / or 8x8 quadrant tables from                  \
- * me_search_full8 (or NULL; 8 bit only).  With table8, sad / sad_x3 / sad_x4 of PIXEL_16x8,     \
+ * me_search_full8 (or NULL).  With table8, sad / sad_x3 / sad_x4 of PIXEL_16x8,                 \
  * 8x16 and 8x8 answer from it as well (the partition whose pixels equal the caller's fenc       \
  * block, its SAD the sum of its quadrants), and PIXEL_16x16 from the four when table is NULL. */ \
 int x264hip_##BD##_me_bind_tables( const pixel *fenc, const pixel *ref, intptr_t stride,        \
@@ -627,7 +644,8 @@ int x264hip_##BD##_me_search_full( const pixel *fenc, intptr_t fenc_stride,     
                                    int mb_width, int mb_height, int n_frames, int range,        \
                                    sadt *table, void *stream );                                 \
                                                                                                 \
-/* 8x8 quadrant tables (8 bit only; X264HIP_EINVAL at 10 bit): table8[mb][q][j][i] =             \
+/* 8x8 quadrant tables (uint16 at both depths: an 8x8 SAD is <= 65472 at 10 bit):               \
+ * table8[mb][q][j][i] =                                                                         \
  * sad_8x8 of quadrant q of the MB (0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right)      \
  * at mv (i - range, j - range), row pitch (2*range+1+3)&~3, MBs frame-major.  The 16x16         \
  * SAD is the sum of the four, PIXEL_16x8's two halves are q0+q1 / q2+q3 and PIXEL_8x16's        \
@@ -641,13 +659,16 @@ int x264hip_##BD##_me_search_full8( const pixel *fenc, intptr_t fenc_stride,    
                                     int mb_width, int mb_height, int n_frames, int range,       \
                                     uint16_t *table8, void *stream );                           \
                                                                                                 \
-/* full search around a per-MB centre (me.c centres its ESA window on the best                   \
- * predictor, encoder/me.c:618-624): centre[2*mb..] = (cx, cy) full-pel, MBs in frame-major     \
- * raster order.  The window origin (cx - range, cy - range) is clamped so every fetched        \
- * pixel stays inside the 32-pixel padding (PADH = PADV = 32, frame.h:32-33) and aligned        \
- * down to 4 (8 bit) / 2 (10 bit) pixels; origin[2*mb..] receives it (mv of table column 0      \
- * and row 0).  table[mb][j][i] = SAD at mv (origin + (i, j)), i, j < 2*range+1, same layout    \
- * as me_search_full (which is this entry with every centre (0, 0)). */                         \
+/* full search of me.c's ESA window around a per-MB centre (me.c centres its window on the    \
+ * best predictor, encoder/me.c:618-626): centre[2*mb..] = (cx, cy) full-pel, MBs in          \
+ * frame-major raster order.  The window origin (cx - range, cy - range) is clamped so every  \
+ * fetched pixel stays inside the 32-pixel padding (PADH = PADV = 32, frame.h:32-33) and      \
+ * aligned down to 4 (8 bit) / 2 (10 bit) pixels; origin[2*mb..] receives it (mv of table     \
+ * column 0 and row 0).  table[mb][j][i] = SAD at mv (origin + (i, j)) for j < 2*range+1 rows \
+ * and i < P = x264hip_me_table_pitch( BD, range, 1 ) columns: align4(2*range+6) at 8 bit,    \
+ * 2*range+4 at 10 bit -- the columns [cx - range, cx + range + 2] me.c's width-rounded       \
+ * window (max_x - min_x + 3) & ~3 can reach, whatever the alignment.  So a window of radius  \
+ * range = me_range holds every candidate of me.c's ESA around that centre. */              \
 int x264hip_##BD##_me_search_centred( const pixel *fenc, intptr_t fenc_stride,                  \
                                       intptr_t fenc_frame_stride,                               \
                                       const pixel *ref, intptr_t ref_stride,                    \
@@ -656,10 +677,9 @@ int x264hip_##BD##_me_search_centred( const pixel *fenc, intptr_t fenc_stride,  
                                       const int16_t *centre, sadt *table, int16_t *origin,      \
                                       void *stream );                                           \
                                                                                                 \
-/* me_esa_argmin over a me_search_centred table: origin[2*i..] as written by it.                \
- * Window candidates outside the table's (2*range+1)^2 square are not evaluated, so             \
- * to reproduce me.c's rounded window (up to 3 columns past bmx + me_range) around a            \
- * centre (bmx, bmy) pick range >= me_range + 6 (8 bit; + 4 at 10 bit: alignment). */          \
+/* me_esa_argmin over a me_search_centred table: origin[2*i..] as written by it.  Centred on   \
+ * the predictor (bmx, bmy) with range >= me_range (else X264HIP_EINVAL) the table holds me.c's \
+ * whole width-rounded window. */                                                              \
 int x264hip_##BD##_me_esa_argmin_at( const sadt *table, int range, int n, int me_range,         \
                                      const int16_t *origin, const int16_t *par,                 \
                                      const int32_t *init_cost, const uint16_t *cost_mv,         \
@@ -685,9 +705,9 @@ int x264hip_##BD##_ssd_nv12_batch( const pixel *pix1, intptr_t stride1, intptr_t
 /* Fused full search + ESA decision: me_search_centred around each MB's predictor        \
  * (centre = par[8*i+0..1]) and me_esa_argmin_at over that window in one pass, the SAD     \
  * table never written (reference encoder/me.c:618-631).  par / init_cost / cost_mv / out   \
- * as me_esa_argmin_at: out[3*i] = { cost, mx, my }; window candidates outside the          \
- * (2*range+1)^2 square are not evaluated (range >= me_range + 6 covers the rounded         \
- * window).  range is 4, 8, 16 or 24. */                                                    \
+ * as me_esa_argmin_at: out[3*i] = { cost, mx, my }.  range is 4, 8, 16 or 24 and at least  \
+ * me_range (the search costs (2*range+1) rows of the centred table's columns: pick the     \
+ * smallest, range = me_range for x264's default merange 16). */                            \
 int x264hip_##BD##_me_search_esa( const pixel *fenc, intptr_t fenc_stride, intptr_t fenc_frame_stride, \
                                   const pixel *ref, intptr_t ref_stride, intptr_t ref_frame_stride,   \
                                   int mb_width, int mb_height, int n_frames, int range, int me_range, \

@@ -1384,12 +1384,21 @@ void FN(me_search_full8)( const pixel *fenc, intptr_t fs, const pixel *ref, intp
             }
 }
 
+/* columns of a x264hip_*_me_search_centred table: me.c's ESA window around the centre,
+ * [cx - range, cx + range + 2] (the width rounding (max_x - min_x + 3) & ~3, me.c:626, ends
+ * up to two columns past max_x) plus the origin's alignment down to a dword (3 / 1 pixels),
+ * rounded up to a multiple of 4 -- every column is a SAD */
+static int cen_pitch( int range )
+{
+    return (2*range + (BIT_DEPTH == 8 ? 6 : 4) + 3) & ~3;
+}
+
 /* window origin of x264hip_*_me_search_centred for one MB: (cx, cy) - range,
  * clamped so every pixel the kernels fetch lies in the 32-pixel padded plane,
  * then aligned down to 4 (8 bit) / 2 (10 bit) pixels; returned relative to the MB */
 static void me_window( int mbx, int mby, int mb_width, int mb_height, int range, int cx, int cy, int *ox, int *oy )
 {
-    const int P = (2*range + 1 + 3) & ~3, al = BIT_DEPTH == 8 ? 4 : 2;
+    const int P = cen_pitch( range ), al = BIT_DEPTH == 8 ? 4 : 2;
     int ax = 16*mbx + cx - range, ay = 16*mby + cy - range;
     int hx = 16*mb_width + 12 - P, hy = 16*mb_height + 16 - 2*range;
     ax = ax < -32 ? -32 : ax > hx ? hx : ax;
@@ -1400,11 +1409,12 @@ static void me_window( int mbx, int mby, int mb_width, int mb_height, int range,
 }
 
 /* semantics of x264hip_*_me_search_centred: table[mb][j][i] = SAD at mv
- * (ox + i, oy + j), i, j < 2*range+1, with (ox, oy) = origin[mb] from me_window */
+ * (ox + i, oy + j), j < 2*range+1, i < cen_pitch(range), with (ox, oy) = origin[mb]
+ * from me_window */
 void FN(me_search_centred)( const pixel *fenc, intptr_t fs, const pixel *ref, intptr_t rs, int mb_width,
                             int mb_height, int range, const int16_t *centre, sadt *table, int16_t *origin )
 {
-    int w = 2*range + 1;
+    int w = 2*range + 1, pw = cen_pitch( range );
     for( int mby = 0; mby < mb_height; mby++ )
         for( int mbx = 0; mbx < mb_width; mbx++ )
         {
@@ -1414,10 +1424,10 @@ void FN(me_search_centred)( const pixel *fenc, intptr_t fs, const pixel *ref, in
             origin[2*mb] = (int16_t)ox;
             origin[2*mb+1] = (int16_t)oy;
             const pixel *f = fenc + 16*(mby*fs + mbx);
-            sadt *t = table + mb * w * w;
+            sadt *t = table + mb * w * pw;
             for( int j = 0; j < w; j++ )
-                for( int i = 0; i < w; i++ )
-                    t[j*w+i] = (sadt)FN(sad)( 0, f, fs, ref + (16*mby + oy + j)*rs + 16*mbx + ox + i, rs );
+                for( int i = 0; i < pw; i++ )
+                    t[j*pw+i] = (sadt)FN(sad)( 0, f, fs, ref + (16*mby + oy + j)*rs + 16*mbx + ox + i, rs );
         }
 }
 
@@ -1640,11 +1650,12 @@ void FN(subpel_list)( int op, int i_pixel, const pixel *fenc, intptr_t fs, const
  * with p_cost_mv* = cost_mv - mvp (me.c:60-70, 230-231), strict-< update from
  * the predictor result (COPY3_IF_LT, me.h:87-93), my-major raster order.
  * par[8*i] = { bmx, bmy, mvp_x, mvp_y, mv_x_min, mv_y_min, mv_x_max, mv_y_max };
- * table rows have pitch align4(2R+1) and are centred on mv (0,0). */
+ * Without an origin the table is a full-search table (2R+1 columns at pitch align4(2R+1),
+ * centred on mv (0,0)); with one, a me_search_centred table (cen_pitch(R) columns). */
 void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const int16_t *origin, const int16_t *par,
                         const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out )
 {
-    const int W = 2 * R + 1, P = (W + 3) & ~3;
+    const int W = 2 * R + 1, P = origin ? cen_pitch( R ) : (W + 3) & ~3, C = origin ? P : W;
     for( int i = 0; i < nmb; i++ )
     {
         const int16_t *p = par + 8 * i;
@@ -1661,7 +1672,7 @@ void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const i
         for( int my = min_y; my <= max_y; my++ )
             for( int mx = min_x; mx < min_x + width; mx++ )
             {
-                if( mx - ox < 0 || mx - ox >= W || my - oy < 0 || my - oy >= W )
+                if( mx - ox < 0 || mx - ox >= C || my - oy < 0 || my - oy >= W )
                     continue;           /* outside the table: not evaluated */
                 int cost = t[(my - oy) * P + mx - ox] + cx[mx * 4] + cy[my * 4];
                 if( cost < bcost )

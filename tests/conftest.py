@@ -64,12 +64,8 @@ def hip():
     return x
 
 
-_VARIANT_SWITCHES = ("X264HIP_ME_VARIANT", "X264HIP_HPEL_VARIANT", "X264HIP_HPEL_ROWS", "X264HIP_SUBPEL_VARIANT",
-                     "X264HIP_LOWRES_VARIANT", "X264HIP_DQ_VARIANT", "X264HIP_RECON_VARIANT",
-                     "X264HIP_LOWRES_INTRA_VARIANT", "X264HIP_LOOKAHEAD_BAND",
-                     "X264HIP_ME_LEAD", "X264HIP_TESA_VARIANT", "X264HIP_INTEGRAL_VARIANT",
-                     "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS",
-                     "X264HIP_ME_XCD", "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT", "X264HIP_SSD_VARIANT")
+_VARIANT_SWITCHES = ("X264HIP_TESA_VARIANT", "X264HIP_INTEGRAL_VARIANT", "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS",
+                     "X264HIP_ME_XCD", "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT")
 
 
 @pytest.fixture(autouse=True)

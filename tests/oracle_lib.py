@@ -329,9 +329,10 @@ def me_tesa(bd, fenc, f_origin, fs, ref, r_origin, integral, i_origin, rs, mbw, 
 
 
 def me_search_centred(bd, fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, rng, centre):
-    """one frame: (table [mbh, mbw, 2r+1, 2r+1], origin int16 [mbh*mbw, 2])."""
+    """one frame: (table [mbh, mbw, 2r+1, me_centred_pitch], origin int16 [mbh*mbw, 2])."""
     w = 2 * rng + 1
-    out = np.zeros((mbh, mbw, w, w), sad_dtype(bd))
+    pw = (2 * rng + (6 if bd == 8 else 4) + 3) // 4 * 4
+    out = np.zeros((mbh, mbw, w, pw), sad_dtype(bd))
     org = np.zeros((mbh * mbw, 2), np.int16)
     c = np.ascontiguousarray(centre, np.int16)
     getattr(_L, f"oracle{bd}_me_search_centred")(_addr(fenc, f_origin), fs, _addr(ref, r_origin), rs, mbw, mbh,

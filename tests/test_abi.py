@@ -170,9 +170,10 @@ def test_runtime_entries_without_device():
     assert L.x264hip_set_thread_device(0) == -3
     assert L.x264hip_thread_device() == -1
     assert L.x264hip_set_thread_device(-1) == 0
-    assert L.x264hip_set_variant(b"X264HIP_ME_VARIANT", 3) == 0
-    assert L.x264hip_set_variant(b"X264HIP_ME_VARIANT", -1) == 0
+    assert L.x264hip_set_variant(b"X264HIP_ME_XCD", 0) == 0
+    assert L.x264hip_set_variant(b"X264HIP_ME_XCD", -1) == 0
     assert L.x264hip_set_variant(b"NOT_A_SWITCH", 1) == -1
+    assert L.x264hip_set_variant(b"X264HIP_ME_VARIANT", 3) == -1          # removed: one kernel per input
     assert L.x264hip_forward_ref(None, 0, None, 0, 16, None) == -1
     assert L.x264hip_forward_ref(None, 0, None, 0, 0, None) == 0
     L.x264hip_upload.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]
@@ -181,23 +182,38 @@ def test_runtime_entries_without_device():
     assert "no device" in L.x264hip_backend_banner().decode()
 
 
-@pytest.mark.parametrize("bd,slack", [(8, 6), (10, 4)])
-def test_centred_esa_range_bound(bd, slack):
-    """the centred ESA entries refuse a template range that cannot hold me.c's
-    rounded window (me.c:621-626) around an aligned-down origin -- range < me_range + 6
-    (8 bit) / + 4 (10 bit) is X264HIP_EINVAL, checked before any HIP call."""
+@pytest.mark.parametrize("bd", [8, 10])
+def test_centred_esa_range_bound(bd):
+    """The centred ESA entries take a template range >= me_range: the centred table holds
+    me.c's whole width-rounded window (me.c:621-626) around an aligned-down origin, so
+    range = me_range is exact; range < me_range is X264HIP_EINVAL, checked before any HIP
+    call, and so is a template range other than 4 / 8 / 16 / 24 for the fused search."""
     x = load_package()
     L = x.lib()
     esa = getattr(L, f"x264hip_{bd}_me_search_esa")
     at = getattr(L, f"x264hip_{bd}_me_esa_argmin_at")
     V = ctypes.c_void_p
-    for rng, me_range in ((16, 16), (24, 24 - slack + 1), (8, 8 - slack + 1), (16, 16 - slack + 1)):
+    for rng, me_range in ((16, 17), (24, 25), (8, 9), (4, 5), (12, 12)):
         assert esa(V(), 0, 0, V(), 0, 0, 0, 0, 0, rng, me_range, V(), V(), V(), V(), V()) == -1, (rng, me_range)
-        assert at(V(), rng, 0, me_range, V(8), V(), V(), V(), V(), V()) == -1, (rng, me_range)
+        if rng != 12:
+            assert at(V(), rng, 0, me_range, V(8), V(), V(), V(), V(), V()) == -1, (rng, me_range)
     # in bounds: an empty launch is accepted (no frames, nothing to do)
-    for rng, me_range in ((24, 24 - slack), (16, 16 - slack), (8, 8 - slack)):
+    for rng, me_range in ((24, 24), (16, 16), (8, 8), (4, 4), (24, 16)):
         assert esa(V(), 0, 0, V(), 0, 0, 0, 0, 0, rng, me_range, V(), V(), V(), V(), V()) in (0, -2, -3), \
             (rng, me_range)
+
+
+def test_table_pitch_entry():
+    """x264hip_me_table_pitch: full tables align4(2R+1), centred tables me.c's ESA window
+    (align4(2R+6) at 8 bit, align4(2R+4) at 10 bit), as the Python mirror computes them."""
+    x = load_package()
+    L = x.lib()
+    for bd in (8, 10):
+        for r in (4, 8, 16, 24, 29):
+            assert L.x264hip_me_table_pitch(bd, r, 0) == x.me_table_pitch(r)
+            assert L.x264hip_me_table_pitch(bd, r, 1) == x.me_centred_pitch(bd, r)
+    assert L.x264hip_me_table_pitch(8, 16, 1) == 40 and L.x264hip_me_table_pitch(10, 16, 1) == 36
+    assert L.x264hip_me_table_pitch(9, 16, 0) == 0 and L.x264hip_me_table_pitch(8, 30, 0) == 0
 
 
 # ---------------------------------------------------------------- reference layout

@@ -307,12 +307,13 @@ def test_me_search_centred_oracle(oracle, bd):
     plain = oracle.me_search_full(bd, f, origin, stride, r, origin, stride, mbw, mbh, R)
     tab, org = oracle.me_search_centred(bd, f, origin, stride, r, origin, stride, mbw, mbh, R,
                                         np.zeros((mbw * mbh, 2), np.int16))
-    assert np.array_equal(tab, plain) and (org == -R).all()
+    P = (2 * R + (6 if bd == 8 else 4) + 3) & ~3           # the ESA window's columns
+    assert tab.shape[-1] == P
+    assert np.array_equal(tab[..., :2 * R + 1], plain) and (org == -R).all()
     rs = np.random.default_rng(bd)
     cen = rs.integers(-40, 41, (mbw * mbh, 2)).astype(np.int16)
     tab, org = oracle.me_search_centred(bd, f, origin, stride, r, origin, stride, mbw, mbh, R, cen)
     al = 4 if bd == 8 else 2
-    P = (2 * R + 1 + 3) & ~3
     for mb in range(mbw * mbh):
         mbx, mby = mb % mbw, mb // mbw
         ax = min(max(16 * mbx + cen[mb, 0] - R, -32), 16 * mbw + 12 - P) & ~(al - 1)
@@ -320,7 +321,7 @@ def test_me_search_centred_oracle(oracle, bd):
         assert (org[mb, 0], org[mb, 1]) == (ax - 16 * mbx, ay - 16 * mby)
         fb = nr.block(f, origin + 16 * mby * stride + 16 * mbx, stride, 16, 16)
         for j in (0, R, 2 * R):
-            for i in (0, 3, 2 * R):
+            for i in (0, 3, 2 * R, P - 1):
                 rb = nr.block(r, origin + (ay + j) * stride + ax + i, stride, 16, 16)
                 assert tab[mby, mbx, j, i] == nr.sad(fb, rb), (mb, i, j)
 

@@ -176,21 +176,14 @@ def test_dc_and_quant_dc_batch(hip, oracle, bd):
             assert np.array_equal(g[i], want) and nz[i] == wnz, (name, i)
 
 
-@pytest.fixture(params=["default", "nt", "0", "1", "2", "3", "4", "5", "6", "7", "11", "12"])
-def dq_variant(request, monkeypatch):
-    """X264HIP_DQ_VARIANT: 0 / 2 staged / unstaged strip, 1 block-major, 3 / 4 band layout staged /
-    direct, 5 half band (transform 4), 6 / 7 packed 16-bit staged / direct (8 bit, transform 8),
-    11 / 12 staged strip in one- / four-wave workgroups with the stream store policy (11 is the
-    10-bit transform-8 default);
-    nt = the default kernels with nontemporal coefficient stores forced (X264HIP_STREAM_NT=1,
-    chosen by footprint above ~192 MiB per launch)."""
-    if request.param == "nt":
-        _x().set_variant("X264HIP_DQ_VARIANT", None)
-        _x().set_variant("X264HIP_STREAM_NT", 1)
-    elif request.param != "default":
-        _x().set_variant("X264HIP_DQ_VARIANT", request.param)
-    else:
-        _x().set_variant("X264HIP_DQ_VARIANT", None)
+@pytest.fixture(params=["default", "nt", "plain"])
+def dq_variant(request):
+    """the store policy of the fused kernels (X264HIP_STREAM_NT): the default, nontemporal
+    coefficient stores forced on (nt) or off (plain); the kernel itself is fixed per transform
+    and bit depth (4x4: half-band strips; 8x8: packed 16-bit pairs at 8 bit, staged one-wave
+    strips at 10 bit)."""
+    if request.param != "default":
+        _x().set_variant("X264HIP_STREAM_NT", 1 if request.param == "nt" else 0)
     return request.param
 
 
@@ -223,7 +216,7 @@ def test_mb_dct_quant_1080p(hip, oracle, bd, transform, dq_variant):
     assert nz.any() and (nz == 0).any()
 
 
-@pytest.mark.parametrize("variant", ["default", "0", "7"])
+@pytest.mark.parametrize("variant", ["default", "plain"])
 @pytest.mark.parametrize("cqm", [0, 3, 5])
 def test_mb_dct8_quant_extremes(hip, oracle, monkeypatch, variant, cqm):
     """8-bit transform 8 at the residual extremes the packed 16-bit kernel's range argument
@@ -231,9 +224,7 @@ def test_mb_dct8_quant_extremes(hip, oracle, monkeypatch, variant, cqm):
     every CQM family (all-ones lists: the uint32 (f + |c|) * mf wraps) at QP 0, 26 and 51;
     20 MBs wide so the last 16-MB strip is partial."""
     if variant != "default":
-        _x().set_variant("X264HIP_DQ_VARIANT", variant)
-    else:
-        _x().set_variant("X264HIP_DQ_VARIANT", None)
+        _x().set_variant("X264HIP_STREAM_NT", 0)
     mbw, mbh = 20, 3
     W, H = 16 * mbw, 16 * mbh
     stride = W + 64

@@ -110,13 +110,8 @@ def _lowres_frames(hip, bd, W, H, n, seed):
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("size", [(1920, 1088), (352, 288), (32, 48), (64, 16), (8320, 64)])
 @pytest.mark.parametrize("mode", ["satd_all", "sad_dc_h_v", "satd_dc_h_v", "sad_all_aq"])
-@pytest.mark.parametrize("variant", ["default", "1"])
-def test_lowres_intra_cost(hip, oracle, bd, size, mode, variant, monkeypatch):
-    """X264HIP_LOWRES_INTRA_VARIANT: default = block per MB row, 1 = wave per 64 MBs with atomics"""
-    if variant == "default":
-        _x().set_variant("X264HIP_LOWRES_INTRA_VARIANT", None)
-    else:
-        _x().set_variant("X264HIP_LOWRES_INTRA_VARIANT", variant)
+def test_lowres_intra_cost(hip, oracle, bd, size, mode):
+    """the lookahead's intra estimate (one workgroup per MB row) vs the oracle"""
     W, H = size
     mbw, mbh = W // 16, H // 16
     n = 2

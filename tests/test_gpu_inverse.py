@@ -360,14 +360,10 @@ def test_zigzag_sub_batch_random(hip, oracle, bd):
             assert np.array_equal(dd.cpu().numpy().view(pdt), want_dst)
 
 
-@pytest.fixture(params=["default", "0", "1", "2"])
-def recon_variant(request, monkeypatch):
-    """X264HIP_RECON_VARIANT: 0 = block-pair lanes for transform 4, 1 = one lane per block, 2 = the
-    default kernels without the sector-aligned wave shift."""
-    if request.param == "default":
-        _x().set_variant("X264HIP_RECON_VARIANT", None)
-    else:
-        _x().set_variant("X264HIP_RECON_VARIANT", request.param)
+@pytest.fixture(params=["default"])
+def recon_variant(request):
+    """one kernel per transform and bit depth (8 bit: block pairs for 4x4, packed int16 pairs for
+    8x8; 10 bit: a lane per block); the sector-aligned wave shift applies to 64-byte strides"""
     return request.param
 
 

@@ -209,6 +209,53 @@ def test_lowres_wait_timeout_reports_error(hip, oracle, kind):
         call()
 
 
+def test_lowres_async_report_and_graph_capture(hip, oracle):
+    """the lookahead entries stay asynchronous.  A timed-out launch (X264HIP_LA_POLL
+    0) returns without waiting; once its status copy has landed the NEXT lookahead call on the
+    thread refuses with the timeout, and the report clears the condition (a following
+    lowres_status is clean).  And the P search captures into a HIP graph whose replay equals
+    the eager launch."""
+    from x264hip import synth
+    W, H = 256, 192
+    frames, stride, origin = synth.make_sequence(3, W, H, 8)
+    dev = torch.from_numpy(frames).cuda()
+    lows, ls = hip.frame_init_lowres(dev, origin, stride, W, H)
+    mbw, mbh = W // 16, H // 16
+    cm, c0 = oracle.cost_mv_table(1, 512)
+    cmd = (torch.from_numpy(cm.view(np.int16)).cuda(), c0)
+    intra, _, _ = hip.lowres_intra_cost(lows[0], ls, mbw, mbh, True, True, 1)
+
+    def call(check, outs=None):
+        return hip.lowres_inter_cost(lows[0][1:], [p[:-1] for p in lows], ls, mbw, mbh, intra[1:], cmd,
+                                     check=check, outs=outs)
+    hip.set_variant("X264HIP_LA_POLL", 0)
+    try:
+        call(False)                                    # returns at once, failure pending
+    finally:
+        hip.set_variant("X264HIP_LA_POLL", None)
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError, match="timed out"):
+        call(False)                                    # the lazy report, nothing launched
+    hip.lowres_status()                                # cleared by the report
+    want = [g.clone() for g in call(True)]
+    outs = tuple(torch.empty_like(g) for g in want)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        call(False, outs)
+    torch.cuda.current_stream().wait_stream(side)
+    for o in outs:
+        o.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        call(False, outs)
+    g.replay()
+    torch.cuda.synchronize()
+    hip.lowres_status()
+    for a, b in zip(outs, want):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("wt", [(40, 5, -6), (23, 4, 9), (1, 0, 3), (16, 4, 0)])
 def test_lowres_inter_weighted_1080p(hip, oracle, bd, wt):

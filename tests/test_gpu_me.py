@@ -16,15 +16,16 @@ def _frames(synth, bd, w, h, kind, seed=3):
     return synth.random_planes(3, w, h, bd, seed=seed)
 
 
-@pytest.fixture(params=["default", "1", "2", "3", "5", "7", "lead0", "lead1", "lead3"])
-def variant(request, monkeypatch):
-    """every kernel variant (X264HIP_ME_VARIANT, read per launch) must be exact, and so must
-    every load lead of the default kernels (X264HIP_ME_LEAD, default 2)"""
-    if request.param.startswith("lead"):
-        _x().set_variant("X264HIP_ME_LEAD", request.param[4:])
-    elif request.param != "default":
-        _x().set_variant("X264HIP_ME_VARIANT", request.param)
+@pytest.fixture(params=["grouped", "generic"])
+def variant(request):
+    """the two kernel forms a launch can take: the grouped lanes (dword-aligned planes, the
+    default) and the generic one-lane-per-column kernel, which serves planes whose MB rows are
+    not dword aligned -- selected here by moving the plane origin one pixel to the right"""
     return request.param
+
+
+def _shift(variant, origin):
+    return origin + 1 if variant == "generic" else origin
 
 
 @pytest.mark.parametrize("bd", [8, 10])
@@ -34,6 +35,7 @@ def test_me_full_small(hip, oracle, bd, rng, kind, variant):
     from x264hip import synth
     w, h = 80, 48
     planes, stride, origin = _frames(synth, bd, w, h, kind)
+    origin = _shift(variant, origin)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
     nf = 2
@@ -55,7 +57,7 @@ def test_me_full_extremes(hip, oracle, bd, variant):
     w, h, rng = 48, 32, 8
     pmax = (1 << bd) - 1
     stride = synth.plane_stride(w)
-    origin = 32 * stride + 32
+    origin = _shift(variant, 32 * stride + 32)
     yy, xx = np.meshgrid(np.arange(h + 64), np.arange(stride), indexing="ij")
     dt = np.uint8 if bd == 8 else np.uint16
     a = (((yy + xx) & 1) * pmax).astype(dt)
@@ -79,6 +81,7 @@ def test_me_full_1080p_properties(hip, oracle, variant):
     from x264hip import synth
     W, H, R = 1920, 1088, 16
     planes, stride, origin = synth.make_sequence(2, W, H, 8)
+    origin = _shift(variant, origin)
     dev = torch.from_numpy(planes).cuda()
     fs = planes[0].size
     mbw, mbh = W // 16, H // 16
@@ -157,10 +160,12 @@ def test_me_esa_argmin(hip, oracle, bd, rng, me_range):
 @pytest.mark.parametrize("rng", [8, 16, 24])
 def test_me_search_centred(hip, oracle, bd, rng, variant):
     """per-MB centres, including ones far enough out that the window is clamped into the
-    padding; table and origin equal the oracle's (all variants)."""
+    padding; the whole ESA-window table (2r+1 rows x me_centred_pitch columns) and the origin
+    equal the oracle's (both kernel forms)."""
     from x264hip import synth
     W, H = 96, 64
     planes, stride, origin = synth.make_sequence(3, W, H, bd, seed=7)
+    origin = _shift(variant, origin)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
     mbw, mbh, nf = W // 16, H // 16, 2
@@ -169,8 +174,9 @@ def test_me_search_centred(hip, oracle, bd, rng, variant):
     cen[::5] = 0
     table, org = hip.me_search_centred(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, nf, rng,
                                        torch.from_numpy(cen).cuda(), fenc_frame_stride=fs, ref_frame_stride=fs)
+    assert table.shape[-1] == hip.me_centred_pitch(bd, rng)
     got = table.cpu().numpy()
-    got = (got.view(np.uint16) if bd == 8 else got.view(np.uint32))[..., :2 * rng + 1]
+    got = got.view(np.uint16) if bd == 8 else got.view(np.uint32)
     org = org.cpu().numpy()
     n1 = mbw * mbh
     for f in range(nf):
@@ -181,12 +187,14 @@ def test_me_search_centred(hip, oracle, bd, rng, variant):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-def test_me_esa_argmin_centred(hip, oracle, bd):
+@pytest.mark.parametrize("rng,me_range", [(16, 16), (24, 16), (8, 8), (24, 24)])
+def test_me_esa_argmin_centred(hip, oracle, bd, rng, me_range):
     """ESA decision around predictor centres (me.c:618-624 centres the window on bmx, bmy):
-    centred table with range = me_range + 8 and origin-aware argmin, vs the oracle."""
+    the centred table of radius range >= me_range (the ESA window: no slack rows or columns
+    beyond the alignment and width rounding) and the origin-aware argmin, vs the oracle and vs
+    a plain exhaustive scan over direct SADs."""
     from x264hip import synth
     W, H = 160, 96
-    rng, me_range = 24, 16
     planes, stride, origin = synth.make_sequence(2, W, H, bd, seed=9)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     mbw, mbh = W // 16, H // 16
@@ -236,18 +244,15 @@ def test_me_esa_argmin_centred(hip, oracle, bd):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("rng,me_range", [(24, 16), (16, 8), (8, 2), (24, 12)])
-@pytest.mark.parametrize("W,H,lead", [(160, 96, None), (160, 96, 0), (160, 96, 1), (160, 96, "v3"),
-                                      (1920, 1088, None), (1920, 1088, "v3")])
-def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H, lead):
-    """Fused search + ESA decision (x264hip_8_me_search_esa) equals me_search_centred followed by
+@pytest.mark.parametrize("rng,me_range", [(16, 16), (24, 16), (16, 8), (8, 8), (8, 2), (24, 24), (4, 4)])
+@pytest.mark.parametrize("W,H", [(160, 96), (1920, 1088)])
+def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H):
+    """Fused search + ESA decision (x264hip_*_me_search_esa) equals me_search_centred followed by
     me_esa_argmin_at on the GPU, and the oracle's centred table + argmin, over predictor centres,
-    clipped windows, mvp-dependent costs and unbeatable predictors."""
+    clipped windows, mvp-dependent costs and unbeatable predictors; range = me_range is exact."""
     from x264hip import synth
-    if lead == "v3":                             # the lane-pair kernel (8 bit; 10 bit ignores it)
-        hip.set_variant("X264HIP_ME_VARIANT", 3)
-    elif lead is not None:
-        hip.set_variant("X264HIP_ME_LEAD", lead)
+    if W == 1920 and (rng, me_range) not in ((16, 16), (24, 16)):
+        pytest.skip("1080p at me_range 16 only")
     planes, stride, origin = synth.make_sequence(3, W, H, bd, seed=rng + me_range)
     dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
@@ -283,25 +288,24 @@ def test_me_search_esa_fused(hip, oracle, bd, rng, me_range, W, H, lead):
             sl = slice(f * nmb, (f + 1) * nmb)
             tab, worg = oracle.me_search_centred(bd, planes[f + 1].ravel(), origin, stride, planes[f].ravel(), origin,
                                                  stride, mbw, mbh, rng, par[sl, :2])
-            p_ = (2 * rng + 1 + 3) & ~3
-            padded = np.zeros((nmb, 2 * rng + 1, p_), tab.dtype)
-            padded[:, :, :2 * rng + 1] = tab.reshape(nmb, 2 * rng + 1, 2 * rng + 1)
-            want = oracle.me_esa_argmin(bd, padded, rng, me_range, par[sl], init[sl], cost_mv, c0, origin=worg)
+            want = oracle.me_esa_argmin(bd, tab.reshape(nmb, 2 * rng + 1, -1), rng, me_range, par[sl], init[sl],
+                                        cost_mv, c0, origin=worg)
             assert np.array_equal(got[sl], want), (f, np.argwhere((got[sl] != want).any(1))[:5])
     assert (got[::7, 0] == 0).all() and (got[:, 0] <= init).all()
 
 
+@pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("rng", [4, 8, 16, 24])
 @pytest.mark.parametrize("W,H,nf", [(160, 96, 2), (1920, 1088, 1)])
-def test_me_search_full8_quadrants(hip, oracle, rng, W, H, nf):
-    """8x8 quadrant tables (x264hip_8_me_search_full8, VERDICT r2 missing 4): every quadrant SAD
+def test_me_search_full8_quadrants(hip, oracle, bd, rng, W, H, nf):
+    """8x8 quadrant tables (x264hip_*_me_search_full8, 8 and 10 bit): every quadrant SAD
     equals the oracle's sad_8x8; their sum is the 16x16 table; the 16x8 / 8x16 pair sums equal
     sad_16x8 / sad_8x16 of those partitions at sampled mvs (pixel.c:55-80)."""
     if W == 1920 and rng not in (16,):
         pytest.skip("1080p at range 16 only")
     from x264hip import synth
-    planes, stride, origin = synth.make_sequence(nf + 1, W, H, 8, seed=rng)
-    dev = torch.from_numpy(planes).cuda()
+    planes, stride, origin = synth.make_sequence(nf + 1, W, H, bd, seed=rng)
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
     mbw, mbh = W // 16, H // 16
     w = 2 * rng + 1
@@ -310,10 +314,11 @@ def test_me_search_full8_quadrants(hip, oracle, rng, W, H, nf):
     t16 = hip.me_search_full(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, nf, rng,
                              fenc_frame_stride=fs, ref_frame_stride=fs)
     g8 = t8.cpu().numpy().view(np.uint16)[..., :w]
-    g16 = t16.cpu().numpy().view(np.uint16)[..., :w]
+    g16 = t16.cpu().numpy()
+    g16 = (g16.view(np.uint16) if bd == 8 else g16.view(np.uint32))[..., :w]
     assert np.array_equal(g8.astype(np.int64).sum(3), g16)
     f = nf - 1
-    want = oracle.me_search_full8(8, planes[f + 1].ravel(), origin, stride, planes[f].ravel(), origin, stride, mbw,
+    want = oracle.me_search_full8(bd, planes[f + 1].ravel(), origin, stride, planes[f].ravel(), origin, stride, mbw,
                                   mbh, rng)
     assert np.array_equal(g8[f], want), np.argwhere(g8[f] != want)[:4]
     rs = np.random.default_rng(rng + W)
@@ -327,7 +332,7 @@ def test_me_search_full8_quadrants(hip, oracle, rng, W, H, nf):
                                (hip.PIXEL_8x16, ((0, 0, (0, 2)), (8, 0, (1, 3))))):
             for px, py, qs in parts:
                 o = fo + py * stride + px
-                assert q[list(qs)].sum() == oracle.cmp(8, "sad", i_pixel, f1, o, stride, f0, o + my * stride + mx,
+                assert q[list(qs)].sum() == oracle.cmp(bd, "sad", i_pixel, f1, o, stride, f0, o + my * stride + mx,
                                                        stride)
 
 

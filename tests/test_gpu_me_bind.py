@@ -172,27 +172,29 @@ def test_me_bind_sad_x4_and_unbound(hip, oracle):
 
 
 @pytest.mark.gpu
-def test_me_bind_partitions_from_quadrant_tables(hip, oracle):
-    """With me_search_full8's quadrant tables bound (x264hip_8_me_bind_tables), sad / sad_x4 of
+@pytest.mark.parametrize("bd", [8, 10])
+def test_me_bind_partitions_from_quadrant_tables(hip, oracle, bd):
+    """With me_search_full8's quadrant tables bound (x264hip_*_me_bind_tables), sad / sad_x4 of
     PIXEL_16x8, 8x16, 8x8 -- and 16x16 with no 16x16 table -- answer from them for every
     partition of every MB (the ESA windows me.c searches per partition, analyse.c:1425-1546),
-    equal to the oracle's SAD."""
+    equal to the oracle's SAD, at 8 and 10 bit (configs[4]'s high-profile lookup mode)."""
     from x264hip import synth
     import ctypes
     W, H, R = 192, 96, 8
     mbw, mbh = W // 16, H // 16
-    planes, stride, origin = synth.make_sequence(2, W, H, 8, seed=21)
-    dev = torch.from_numpy(planes).cuda()
+    planes, stride, origin = synth.make_sequence(2, W, H, bd, seed=21)
+    dev = torch.from_numpy(planes.view(np.int16) if bd == 10 else planes).cuda()
     fs = planes[0].size
+    es = planes.itemsize
     t8 = hip.me_search_full8(dev[1:], origin, stride, dev[:1], origin, stride, mbw, mbh, 1, R,
                              fenc_frame_stride=fs, ref_frame_stride=fs)
-    pixf = hip.pixel_init(8)
+    pixf = hip.pixel_init(bd)
     f1, f0 = planes[1].ravel(), planes[0].ravel()
-    buf = np.zeros(16 * 16, np.uint8)                 # mb.pic.p_fenc: the MB at FENC_STRIDE
+    buf = np.zeros(16 * 16, planes.dtype)             # mb.pic.p_fenc: the MB at FENC_STRIDE
     rs = np.random.default_rng(9)
     parts = {hip.PIXEL_16x16: [(0, 0)], hip.PIXEL_16x8: [(0, 0), (0, 8)], hip.PIXEL_8x16: [(0, 0), (8, 0)],
              hip.PIXEL_8x8: [(0, 0), (8, 0), (0, 8), (8, 8)]}
-    with hip.me_bind(8, f1, origin, f0, origin, stride, mbw, mbh, None, R, table8=t8) as b:
+    with hip.me_bind(bd, f1, origin, f0, origin, stride, mbw, mbh, None, R, table8=t8) as b:
         b.stats(reset=True)
         n = 0
         for mb in range(0, mbw * mbh, 2):
@@ -203,9 +205,9 @@ def test_me_bind_partitions_from_quadrant_tables(hip, oracle):
                 for px, py in offs:
                     mvs = rs.integers(-R, R + 1, (4, 2))
                     po = fo + py * stride + px
-                    fb = buf.ctypes.data + py * 16 + px
-                    ptrs = [f0.ctypes.data + po + int(my) * stride + int(mx) for mx, my in mvs]
-                    want = [oracle.cmp(8, "sad", ip, f1, po, stride, f0, po + int(my) * stride + int(mx), stride)
+                    fb = buf.ctypes.data + es * (py * 16 + px)
+                    ptrs = [f0.ctypes.data + es * (po + int(my) * stride + int(mx)) for mx, my in mvs]
+                    want = [oracle.cmp(bd, "sad", ip, f1, po, stride, f0, po + int(my) * stride + int(mx), stride)
                             for mx, my in mvs]
                     assert pixf.sad[ip](fb, 16, ptrs[0], stride) == want[0], (ip, px, py)
                     sc = (ctypes.c_int * 4)()

@@ -33,10 +33,7 @@ def _dev(p, bd):
 @pytest.mark.parametrize("w,h,n,kind", [(1920, 1080, 3, "random"), (1917, 1083, 2, "random"), (7, 5, 2, "random"),
                                         (3840, 2160, 1, "random"), (1920, 1080, 1, "extreme"), (8, 8, 4, "random"),
                                         (1920, 1088, 2, "shifted"), (2100, 37, 2, "random")])
-@pytest.mark.parametrize("variant", [None, 0, 2])
-def test_ssd_plane(hip, oracle, bd, w, h, n, kind, variant):
-    """X264HIP_SSD_VARIANT: rows per wave 8 (default), 16 (0) or 4 (2)."""
-    _x().set_variant("X264HIP_SSD_VARIANT", variant)
+def test_ssd_plane(hip, oracle, bd, w, h, n, kind):
     a, b, stride, org = _frames(bd, n, w, h, w + h + n, kind)
     if kind == "shifted":
         org += 3                                      # chunks off 16-byte alignment

@@ -39,19 +39,14 @@ def _oracle_frames(oracle, bd, planes, stride, org, H, mbw, mbh, me_range, satd,
                                                 (8, False, "synthetic"), (24, True, "random"),
                                                 (4, True, "synthetic"), (32, False, "random"),
                                                 (12, True, "random"), (9, False, "synthetic")])
-@pytest.mark.parametrize("mode", ["internal", "kernel", "table", "onelaunch"])
+@pytest.mark.parametrize("mode", ["internal", "kernel", "table"])
 def test_tesa_small(hip, oracle, bd, me_range, satd, kind, mode):
-    """internal: no table given (me_range <= 24 builds a table around the predictors, then
-    scans it); kernel: X264HIP_TESA_VARIANT=1, the SADs computed in the scan; table: a
-    caller's me_search_full table over [-16, 16]; onelaunch: X264HIP_TESA_VARIANT=3, the
-    table and the scan in one launch (8 bit, me_range 9..16)"""
+    """internal: no table given (me_range <= 24 builds a centred table around the predictors,
+    then scans it); kernel: X264HIP_TESA_VARIANT=1 forces the SADs computed in the scan (the
+    kernel of me_range > 24); table: a caller's me_search_full table over [-16, 16]"""
     use_table = mode == "table"
     if mode == "kernel":
         hip.set_variant("X264HIP_TESA_VARIANT", 1)
-    if mode == "onelaunch":
-        if bd != 8 or not 8 < me_range <= 16:
-            pytest.skip("the one-launch kernel covers 8 bit, me_range 9..16")
-        hip.set_variant("X264HIP_TESA_VARIANT", 3)
     W, H, nf = 160, 96, 2
     planes, stride, org, dev = _setup(bd, W, H, kind, seed=me_range + bd, nframes=nf)
     mbw, mbh = W // 16, H // 16
@@ -75,9 +70,10 @@ def test_tesa_small(hip, oracle, bd, me_range, satd, kind, mode):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-def test_tesa_centred_table(hip, oracle, bd):
+@pytest.mark.parametrize("me_range,rng", [(16, 16), (16, 24), (12, 16), (8, 8)])
+def test_tesa_centred_table(hip, oracle, bd, me_range, rng):
     """a me_search_centred table around each MB's predictor (origin-aware lookup)."""
-    W, H, me_range, rng = 160, 96, 16, 24
+    W, H = 160, 96
     planes, stride, org, dev = _setup(bd, W, H, "random", seed=5)
     mbw, mbh = W // 16, H // 16
     integ = hip.frame_integral(dev[:1], org, stride, H)
@@ -94,12 +90,10 @@ def test_tesa_centred_table(hip, oracle, bd):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("tv", [None, 1, 3])
+@pytest.mark.parametrize("tv", [None, 1])
 def test_tesa_1080p(hip, oracle, bd, tv):
     """every MB of a 1920x1088 frame pair at me_range 16, SATD fpelcmp, vs the oracle
-    (the internal table, X264HIP_TESA_VARIANT=1's in-scan SADs, =3's one-launch table + scan)."""
-    if tv == 3 and bd != 8:
-        pytest.skip("the one-launch kernel is 8 bit")
+    (the internal centred table, and X264HIP_TESA_VARIANT=1's in-scan SADs)."""
     if tv is not None:
         hip.set_variant("X264HIP_TESA_VARIANT", tv)
     W, H, me_range = 1920, 1088, 16

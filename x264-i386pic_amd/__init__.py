@@ -25,7 +25,7 @@ import numpy as np
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "stream_pair_destroy", "me_search_full8",
@@ -742,14 +742,16 @@ def weight_scale_plane(src, lowres_stride, width, height, scale, denom, offset, 
 
 def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost, cost_mv_center, me_method=1,
                       subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None, outs=None,
-                      ref_w=None, weight=None, n_slices=1):
+                      ref_w=None, weight=None, n_slices=1, check=True):
     """The lookahead's P-frame lowres motion search (x264hip_*_lowres_inter_cost) for the pairs
     (fenc[i], refs[*][i]): fenc = lowres[0] planes [n, rows, stride], refs = the four lowres planes
     (F, H, V, C) of the references, same shape; (0,0) at (PAD, PAD).  intra_cost [n, mbs] from
     lowres_intra_cost; cost_mv_center = (uint16-as-int16 tensor, element offset of mvd 0).  Returns
     (mvs int16 [n, mbs, 2], mv_costs int32 [n, mbs], lowres_costs uint16-as-int16 [n, mbs],
     row_satd int32 [n, mbh], est int32 [n, 3]).  ref_w (weighted F planes, weight_scale_plane) and
-    weight = (scale, denom, offset): the weighted-reference search (x264hip_*_lowres_inter_cost_w)."""
+    weight = (scale, denom, offset): the weighted-reference search (x264hip_*_lowres_inter_cost_w).
+    The launch is asynchronous; check=True then waits for it and raises if its wavefront timed
+    out (lowres_status), check=False leaves that to a later lowres_status() / lookahead call."""
     import torch
     bd = _pix_bd(fenc)
     n = fenc.shape[0]
@@ -774,19 +776,21 @@ def lowres_inter_cost(fenc, refs, lowres_stride, mb_width, mb_height, intra_cost
         _ptr(intra_cost), _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(mvs), _ptr(mvc), _ptr(lc),
         _ptr(rows), _ptr(est), None if ref_w is None else _ptr(ref_w, o), *w, n_slices, _stream()),
         "lowres_inter_cost")
+    if check:
+        lowres_status()
     return mvs, mvc, lc, rows, est
 
 
 def lowres_bidir_cost(fenc, refs_a, refs_b, lowres_stride, mb_width, mb_height, cost_mv_center, search,
                       mvs0, costs0, mvs1, costs1, p1_mvs=None, dist_scale_factor=128, bipred_weight=32,
                       me_method=1, subme=4, satd=True, me_range=16, mv_range=512, lam=1, inv_qscale=None,
-                      outs=None, a_frame_stride=None, b_frame_stride=None, n_slices=1):
+                      outs=None, a_frame_stride=None, b_frame_stride=None, n_slices=1, check=True):
     """The lookahead's B-frame costs (x264hip_*_lowres_bidir_cost_ex; n_slices lookahead slices) for
     the triplets (fenc[i],
     refs_a[*][i], refs_b[*][i]); a reference tensor with one frame and a frame stride of 0 serves
     the whole batch.  mvs_l int16 [n, mbs, 2] / costs_l int32 [n, mbs] are searched into (search
     bit l set) or read.  Returns (lowres_costs uint16-as-int16 [n, mbs], row_satd int32 [n, mbh],
-    est int32 [n, 2])."""
+    est int32 [n, 2]).  check as lowres_inter_cost."""
     import torch
     bd = _pix_bd(fenc)
     n = fenc.shape[0]
@@ -808,7 +812,17 @@ def lowres_bidir_cost(fenc, refs_a, refs_b, lowres_stride, mb_width, mb_height, 
         _ptr(p1_mvs) if p1_mvs is not None else None, dist_scale_factor, bipred_weight,
         _ptr(inv_qscale) if inv_qscale is not None else None, _ptr(lc), _ptr(rows), _ptr(est), n_slices,
         _stream()), "lowres_bidir_cost")
+    if check:
+        lowres_status()
     return lc, rows, est
+
+
+def lowres_status():
+    """Wait for the current stream; raise if a lookahead launch of this thread on its device
+    timed out in the band wavefront (x264hip_lowres_status; reporting clears it)."""
+    f = lib().x264hip_lowres_status
+    f.argtypes, f.restype = [_P], _c.c_int
+    _rc(f(_stream()), "lowres_status")
 
 
 def plane_stride(width, pad=PAD):
@@ -871,9 +885,20 @@ def me_bind(bitdepth, fenc, fenc_origin, ref, ref_origin, stride, mb_width, mb_h
     return MeBinding((fenc, ref, table, table8))
 
 
+def trim(device=-1):
+    """Release the idle blocks of the library's scratch pools (x264hip_trim)."""
+    _rc(lib().x264hip_trim(device), "trim")
+
+
 def me_table_pitch(rng):
     """row pitch of a full-search table: 2*range+1 rounded up to a multiple of 4"""
     return (2 * rng + 1 + 3) // 4 * 4
+
+
+def me_centred_pitch(bitdepth, rng):
+    """row pitch (= columns) of a me_search_centred table: me.c's ESA window around the centre,
+    2*range+6 (8 bit) / 2*range+4 (10 bit) columns rounded up to a multiple of 4"""
+    return (2 * rng + (6 if bitdepth == 8 else 4) + 3) // 4 * 4
 
 
 def me_search_full(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height,
@@ -900,8 +925,8 @@ def me_search_full(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, 
 def me_search_full8(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height,
                     nframes, rng=16, table8=None, fenc_frame_stride=None, ref_frame_stride=None):
     """8x8 quadrant SAD tables [nframes, mb_height, mb_width, 4, 2r+1, pitch] uint16-as-int16
-    (x264hip_8_me_search_full8; q = 0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right).
-    8 bit only."""
+    (x264hip_*_me_search_full8; q = 0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right),
+    8 and 10 bit."""
     import torch
     bd = _pix_bd(fenc)
     w = 2 * rng + 1
@@ -1058,13 +1083,14 @@ def me_esa_argmin(table, rng, me_range, par, init_cost, cost_mv_center, out=None
 
 def me_search_centred(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height, nframes,
                       rng, centre, table=None, origin=None, fenc_frame_stride=None, ref_frame_stride=None):
-    """Full search around per-MB centres (x264hip_*_me_search_centred): centre int16 [n_mbs, 2];
-    returns (table [nframes, mbh, mbw, 2r+1, pitch], origin int16 [n_mbs, 2])."""
+    """Full search of me.c's ESA window around per-MB centres (x264hip_*_me_search_centred):
+    centre int16 [n_mbs, 2]; returns (table [nframes, mbh, mbw, 2r+1, me_centred_pitch(bd, r)],
+    origin int16 [n_mbs, 2])."""
     import torch
     bd = _pix_bd(fenc)
     w = 2 * rng + 1
     if table is None:
-        table = torch.empty((nframes, mb_height, mb_width, w, me_table_pitch(rng)),
+        table = torch.empty((nframes, mb_height, mb_width, w, me_centred_pitch(bd, rng)),
                             dtype=torch.int16 if bd == 8 else torch.int32, device=fenc.device)
     if origin is None:
         origin = torch.empty((nframes * mb_height * mb_width, 2), dtype=torch.int16, device=fenc.device)

@@ -30,6 +30,7 @@ static std::mutex g_init_mutex;
 static thread_local int t_device = -1;
 static thread_local char t_err[256] = "";
 
+static int map_err( hipError_t e, const char *where );
 static int set_err( hipError_t e, const char *where )
 {
     snprintf( t_err, sizeof(t_err), "%s: %s", where, hipGetErrorString( e ) );
@@ -83,12 +84,13 @@ extern "C" int x264hip_available( void )
     // implicit init below would hipSetDevice(0) over that binding
     if( t_device >= 0 || g_device.load( std::memory_order_acquire ) >= 0 )
         return 1;
+    // initialise on the caller's current device (device 0 when it has none), so the device
+    // x264hip_thread_device() reports is the one the entries run on and the caller's
+    // current device is left as it was
     int cur = -1;
-    const bool had = hipGetDevice( &cur ) == hipSuccess;
-    const int rc = x264hip_init( 0 );
-    if( had && cur != 0 )
-        (void)hipSetDevice( cur );   // leave the caller's current device as it was
-    return rc == X264HIP_OK;
+    if( hipGetDevice( &cur ) != hipSuccess || cur < 0 )
+        cur = 0;
+    return x264hip_init( cur ) == X264HIP_OK;
 }
 
 extern "C" int x264hip_set_thread_device( int device )
@@ -202,6 +204,29 @@ extern "C" int x264hip_stream_destroy( void *stream )
     return e == hipSuccess ? X264HIP_OK : set_err( e, "hipStreamDestroy" );
 }
 
+// release the idle blocks of the library's scratch pools (the self-contained TESA's tables)
+// on `device`, or on every device for device < 0; the pools otherwise keep their peak
+extern "C" int x264hip_trim( int device )
+{
+    hipError_t e = scratch_trim( device );
+    return e == hipSuccess ? X264HIP_OK : set_err( e, "x264hip_trim" );
+}
+
+// the lookahead wavefront's status (lookahead.hip lowres_status): waits for `stream`
+extern "C" int x264hip_lowres_status( void *stream )
+{
+    return map_err( lowres_status( (hipStream_t)stream ), "lowres_status" );
+}
+
+// row pitch (entries) of a me_search_full (centred = 0) or me_search_centred (centred = 1)
+// table, or 0 for an unsupported bit depth / range
+extern "C" int x264hip_me_table_pitch( int bitdepth, int range, int centred )
+{
+    if( (bitdepth != 8 && bitdepth != 10) || range < 1 || range > 29 )
+        return 0;
+    return centred ? cen_pitch( bitdepth, range ) : full_pitch( range );
+}
+
 [[noreturn]] static void fatal( hipError_t e, const char *where )
 {
     fprintf( stderr, "x264hip: fatal HIP error in %s: %s\n", where, hipGetErrorString( e ) );
@@ -218,11 +243,8 @@ extern "C" int x264hip_stream_destroy( void *stream )
 // ------------------------------------------------------------ kernel variants
 namespace x264hip {
 static const char *const k_variant_env[V_COUNT] = {
-    "X264HIP_ME_VARIANT", "X264HIP_HPEL_VARIANT", "X264HIP_HPEL_ROWS", "X264HIP_SUBPEL_VARIANT",
-    "X264HIP_LOWRES_VARIANT", "X264HIP_DQ_VARIANT", "X264HIP_RECON_VARIANT", "X264HIP_LOWRES_INTRA_VARIANT",
-    "X264HIP_LOOKAHEAD_BAND", "X264HIP_ME_LEAD", "X264HIP_TESA_VARIANT",
-    "X264HIP_INTEGRAL_VARIANT", "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS", "X264HIP_ME_XCD", "X264HIP_STREAM_XCD",
-    "X264HIP_STREAM_NT", "X264HIP_SSD_VARIANT" };
+    "X264HIP_TESA_VARIANT", "X264HIP_INTEGRAL_VARIANT", "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS", "X264HIP_ME_XCD",
+    "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT" };
 
 struct VariantTable
 {
@@ -393,13 +415,15 @@ inline bool bind_lookup16( const typename PT<BD>::pixel *fenc, intptr_t fs, cons
 // PIXEL_16x8 / 8x16 / 8x8 from the quadrant tables: the partition (W x H at (px, py) in its
 // MB) is the one whose pixels equal the caller's fenc block, among the partitions of that size
 // of the <= 9 MBs whose window covers the candidate; its SAD is the sum of its quadrants
-template <int W, int H>
-inline bool bind_lookup_part( const uint8_t *fenc, intptr_t fs, const uint8_t *cand, intptr_t s, int *out )
+template <int BD, int W, int H>
+inline bool bind_lookup_part( const typename PT<BD>::pixel *fenc, intptr_t fs, const typename PT<BD>::pixel *cand,
+                              intptr_t s, int *out )
 {
+    using pixel = typename PT<BD>::pixel;
     const MeBind &b = t_bind;
-    if( b.bd != 8 || !b.table8 || s != b.stride )
+    if( b.bd != BD || !b.table8 || s != b.stride )
         return false;
-    const intptr_t d = cand - b.ref;
+    const intptr_t d = cand - (const pixel *)b.ref;
     const intptr_t y = (d + BIND_PAD) >= 0 ? (d + BIND_PAD) / s : -((-(d + BIND_PAD) + s - 1) / s);
     const intptr_t x = d - y * s;
     const int R = b.R;
@@ -417,9 +441,9 @@ inline bool bind_lookup_part( const uint8_t *fenc, intptr_t fs, const uint8_t *c
             for( int my = my0; my <= my1; my++ )
                 for( int mx = mx0; mx <= mx1; mx++ )
                 {
-                    const uint8_t *m = b.fenc + (intptr_t)(16 * my + py) * s + 16 * mx + px;
+                    const pixel *m = (const pixel *)b.fenc + (intptr_t)(16 * my + py) * s + 16 * mx + px;
                     int r = 0;
-                    while( r < H && !memcmp( fenc + r * fs, m + r * s, W ) )
+                    while( r < H && !memcmp( fenc + r * fs, m + r * s, W * sizeof( pixel ) ) )
                         r++;
                     if( r < H )
                         continue;
@@ -444,7 +468,7 @@ inline bool bind_lookup_part( const uint8_t *fenc, intptr_t fs, const uint8_t *c
                                                   intptr_t stride, int mb_width, int mb_height,                      \
                                                   const PT<BD>::sadt *table, const uint16_t *table8, int range )     \
     {                                                                                                                \
-        if( !fenc || !ref || !( table || table8 ) || ( table8 && BD != 8 ) || mb_width <= 0 || mb_height <= 0 ||    \
+        if( !fenc || !ref || !( table || table8 ) || mb_width <= 0 || mb_height <= 0 ||                            \
             range < 1 || range > 29 || stride < 16 * (intptr_t)mb_width + 2 * BIND_PAD )                             \
             return X264HIP_EINVAL;                                                                                   \
         MeBind &b = t_bind;                                                                                          \
@@ -508,13 +532,13 @@ static int cmp_call( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::p
             t_bind.misses++;
         }
     }
-    if constexpr( BD == 8 && OP == X264HIP_CMP_SAD &&
+    if constexpr( OP == X264HIP_CMP_SAD &&
                   ( IPIX == X264HIP_PIXEL_16x8 || IPIX == X264HIP_PIXEL_8x16 || IPIX == X264HIP_PIXEL_8x8 ) )
     {
         if( t_bind.table8 )
         {
             int v;
-            if( bind_lookup_part<W, H>( (const uint8_t *)p1, s1, (const uint8_t *)p2, s2, &v ) )
+            if( bind_lookup_part<BD, W, H>( p1, s1, p2, s2, &v ) )
             {
                 t_bind.hits++;
                 return v;
@@ -559,15 +583,14 @@ static void cmpx_call( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *con
             t_bind.misses += N;
         }
     }
-    if constexpr( BD == 8 && OP == X264HIP_CMP_SAD &&
+    if constexpr( OP == X264HIP_CMP_SAD &&
                   ( IPIX == X264HIP_PIXEL_16x8 || IPIX == X264HIP_PIXEL_8x16 || IPIX == X264HIP_PIXEL_8x8 ) )
     {
         if( t_bind.table8 )
         {
             int v[N];
             int k = 0;
-            while( k < N && bind_lookup_part<W, H>( (const uint8_t *)fenc, X264HIP_FENC_STRIDE,
-                                                    (const uint8_t *)refs[k], stride, &v[k] ) )
+            while( k < N && bind_lookup_part<BD, W, H>( fenc, X264HIP_FENC_STRIDE, refs[k], stride, &v[k] ) )
                 k++;
             if( k == N )
             {
@@ -1293,10 +1316,6 @@ static int cqm_init( const uint8_t *const sl[8], int dz_inter, int dz_intra, int
 
 // ============================================================ exported entries
 // a centred window's origin is aligned down by up to 3 (8 bit) / 1 (10 bit) pixels and
-// me.c's ads loop rounds the window width up to a multiple of 4 (me.c:621-626, up to 3
-// columns past bmx + me_range): range >= me_range + this covers every candidate the
-// reference evaluates, whatever the centre and the mv limits
-static constexpr int esa_centred_slack( int bd ) { return bd == 8 ? 6 : 4; }
 
 static int map_err( hipError_t e, const char *where )
 {
@@ -1611,7 +1630,7 @@ extern "C" const char *x264hip_backend_banner( void )
                                                    int mbh, int nframes, int range, uint16_t *table8,                \
                                                    void *stream )                                                    \
     {                                                                                                                \
-        if( BD != 8 || mbw < 0 || mbh < 0 || nframes < 0 ||                                                          \
+        if( mbw < 0 || mbh < 0 || nframes < 0 ||                                                                     \
             !( range == 4 || range == 8 || range == 16 || range == 24 ) ||                                           \
             ( (int64_t)mbw * mbh * nframes > 0 && ( !fenc || !ref || !table8 ) ) )                                   \
             return X264HIP_EINVAL;                                                                                   \
@@ -1633,7 +1652,7 @@ extern "C" const char *x264hip_backend_banner( void )
                                                     void *stream )                                                   \
     {                                                                                                                \
         if( range < 1 || range > 29 || n < 0 || me_range < 0 || 2 * me_range + 4 > 64 || !origin ||                  \
-            range < me_range + esa_centred_slack( BD ) )                                                             \
+            range < me_range )                                                                                       \
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_me_esa_argmin<BD>( table, range, n, me_range, origin, par, init_cost, cost_mv, out,   \
                                                   (hipStream_t)stream ), "me_esa_argmin_at" );                       \
@@ -1663,7 +1682,7 @@ extern "C" const char *x264hip_backend_banner( void )
                                                  void *stream )                                                      \
     {                                                                                                                \
         if( mbw < 0 || mbh < 0 || nframes < 0 || !( range == 4 || range == 8 || range == 16 || range == 24 ) ||       \
-            me_range < 0 || 2 * me_range + 4 > 64 || range < me_range + esa_centred_slack( BD ) ||                  \
+            me_range < 0 || 2 * me_range + 4 > 64 || range < me_range ||                                            \
             ((int64_t)nframes * mbw * mbh && (!par || !init_cost || !cost_mv || !out)) )                             \
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_me_search_esa<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, me_range,   \

@@ -390,76 +390,7 @@ hipError_t launch_quant( int kind, typename PT<BD>::dctcoef *dct, const typename
 }
 
 // ------------------------------------------------- fused mb_dct_quant
-// transform 4: 16 lanes per macroblock, one 4x4 block per lane.
-// transform 8: 4 lanes per macroblock, one 8x8 block per lane.
-template <int BD, int T>
-__global__ __launch_bounds__( 256 ) void mb_dct_quant_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
-                                                              intptr_t fs, intptr_t ffs,
-                                                              const typename PT<BD>::pixel *__restrict__ pred,
-                                                              intptr_t ps, intptr_t pfs, int mbw, int mbh,
-                                                              int nframes,
-                                                              const typename PT<BD>::udctcoef *__restrict__ mf,
-                                                              const typename PT<BD>::udctcoef *__restrict__ bias,
-                                                              typename PT<BD>::dctcoef *__restrict__ dct,
-                                                              int32_t *__restrict__ nz )
-{
-    constexpr int LPM = T == 4 ? 16 : 4;      // lanes per macroblock
-    const int64_t gi = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)nframes * mbh * mbw * LPM;
-    const bool live = gi < total;
-    const int64_t mb = live ? gi / LPM : 0;
-    const int blk = (int)(gi % LPM);
-    const int mbx = (int)(mb % mbw);
-    const int64_t t = mb / mbw;
-    const int mby = (int)(t % mbh);
-    const int64_t f = t / mbh;
-    const typename PT<BD>::pixel *a = fenc + f * ffs + (intptr_t)16 * mby * fs + 16 * mbx;
-    const typename PT<BD>::pixel *b = pred + f * pfs + (intptr_t)16 * mby * ps + 16 * mbx;
-    int nzbit = 0;
-    if( live )
-    {
-        if constexpr( T == 4 )
-        {
-            int i8 = blk >> 2, i4 = blk & 3;
-            int x = (i8 & 1) * 8 + (i4 & 1) * 4, y = (i8 >> 1) * 8 + (i4 >> 1) * 4;
-            int d[4][4], c[16];
-            load_diff<BD, 4>( d, a + y * fs + x, fs, b + y * ps + x, ps );
-            dct4x4_core<BD>( d, c );
-            int acc = 0;
-#pragma unroll
-            for( int k = 0; k < 16; k++ )
-            {
-                c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
-                acc |= c[k];
-            }
-            store_coefs( dct + mb * 256 + blk * 16, c );
-            nzbit = acc != 0;
-        }
-        else
-        {
-            int x = (blk & 1) * 8, y = (blk >> 1) * 8;
-            int d[8][8], c[64];
-            load_diff<BD, 8>( d, a + y * fs + x, fs, b + y * ps + x, ps );
-            dct8x8_core<BD>( d, c );
-            int acc = 0;
-#pragma unroll
-            for( int k = 0; k < 64; k++ )
-            {
-                c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
-                acc |= c[k];
-            }
-            store_coefs( dct + mb * 256 + blk * 64, c );
-            nzbit = acc != 0;
-        }
-    }
-    // gather the per-block nonzero flags of each macroblock (LPM divides 64)
-    uint64_t bal = __ballot( nzbit );
-    const int lane = threadIdx.x & 63;
-    if( live && blk == 0 )
-        nz[mb] = (int32_t)((bal >> (lane & ~(LPM - 1))) & ((1ull << LPM) - 1));
-}
-
-// Strip mapping (default): one wave = one 256-pixel-wide strip of one MB row
+// Strip mapping (10-bit transform 8): one wave = one 256-pixel-wide strip of one MB row
 // (16 macroblocks).  For T=4 lane l owns the 4-pixel column l of the strip and
 // walks its 4 block rows, so every row load is 64 contiguous dwords (fully
 // coalesced); for T=8 lane l owns 8x8 column l%32 of block row l/32 (two
@@ -571,10 +502,7 @@ __global__ __launch_bounds__( 64 * WPB ) void mb_dct_quant_strip_kernel(
     }
 }
 
-// Variant 3 (transform 4): one lane per (MB, 4-row band) of a 16-MB strip, so
-// every row of a band is a single 16-pixel vector load per plane (lanes of a
-// band read 256 contiguous pixels); the lane transforms and quantises the four
-// 4x4 blocks of its band and stages them in LDS like variant 0.
+// 16 pixels of a row as one vector load when aligned
 template <int BD>
 __device__ __forceinline__ void load16( const typename PT<BD>::pixel *p, uint32_t (&w)[16 / PT<BD>::PPD] )
 {
@@ -592,84 +520,11 @@ __device__ __forceinline__ void load16( const typename PT<BD>::pixel *p, uint32_
         load_packed<N>( p, w );
 }
 
-template <int BD, bool STAGE>
-__global__ __launch_bounds__( 256 ) void mb_dct_quant_band_kernel(
-    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
-    const typename PT<BD>::pixel *__restrict__ pred, intptr_t ps, intptr_t pfs, int mbw, int mbh, int nframes,
-    const typename PT<BD>::udctcoef *__restrict__ mf, const typename PT<BD>::udctcoef *__restrict__ bias,
-    typename PT<BD>::dctcoef *__restrict__ dct, int32_t *__restrict__ nz )
-{
-    using dctcoef = typename PT<BD>::dctcoef;
-    constexpr int PPD = PT<BD>::PPD;
-    const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const int spr = (mbw + 15) >> 4;
-    if( wave >= (int64_t)nframes * mbh * spr )
-        return;                                               // wave-uniform
-    const int strip = (int)(wave % spr);
-    const int64_t t = wave / spr;
-    const int mby = (int)(t % mbh);
-    const int64_t f = t / mbh;
-    const int m = lane & 15, by = lane >> 4;                  // MB in the strip, 4-row band
-    const int mbx = strip * 16 + m;
-    const bool live = mbx < mbw;
-    const int64_t mbrow = (f * mbh + mby) * (int64_t)mbw;
-    __shared__ dctcoef lds[STAGE ? 4 * 16 * 256 : 1];
-    dctcoef *stage = STAGE ? lds + (threadIdx.x >> 6) * (16 * 256) : dct + (mbrow + strip * 16) * 256;
-    int mask = 0;
-    if( live )
-    {
-        const typename PT<BD>::pixel *a = fenc + f * ffs + (intptr_t)(16 * mby + 4 * by) * fs + 16 * mbx;
-        const typename PT<BD>::pixel *b = pred + f * pfs + (intptr_t)(16 * mby + 4 * by) * ps + 16 * mbx;
-        int d[4][4][4];                                       // [block][y][x]
-#pragma unroll
-        for( int y = 0; y < 4; y++ )
-        {
-            uint32_t wa[16 / PPD], wb[16 / PPD];
-            load16<BD>( a + y * fs, wa );
-            load16<BD>( b + y * ps, wb );
-#pragma unroll
-            for( int x = 0; x < 16; x++ )
-                d[x >> 2][y][x & 3] = upix<BD>( wa[x / PPD], x % PPD ) - upix<BD>( wb[x / PPD], x % PPD );
-        }
-#pragma unroll
-        for( int bx = 0; bx < 4; bx++ )
-        {
-            int c[16];
-            dct4x4_core<BD>( d[bx], c );
-            int acc = 0;
-#pragma unroll
-            for( int k = 0; k < 16; k++ )
-            {
-                c[k] = sto<BD>( quant_one( c[k], urow( mf, k ), urow( bias, k ) ) );
-                acc |= c[k];
-            }
-            const int i8 = (by >> 1) * 2 + (bx >> 1), i4 = (by & 1) * 2 + (bx & 1);
-            store_coefs( stage + m * 256 + (i8 * 4 + i4) * 16, c );
-            mask |= (acc != 0) << (4 * i8 + i4);
-        }
-    }
-    // OR over the MB's four band lanes (lane ^ 16, lane ^ 32)
-    mask |= __shfl_xor( mask, 16 );
-    mask |= __shfl_xor( mask, 32 );
-    if( live && by == 0 )
-        nz[mbrow + mbx] = mask;
-    if constexpr( STAGE )
-    {
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence( __ATOMIC_RELEASE, "wavefront" );
-        const int nmb = min( 16, mbw - strip * 16 );
-        const int nvec = nmb * 256 * (int)sizeof( dctcoef ) / 16;
-        const uint4 *src = (const uint4 *)stage;
-        uint4 *dst = (uint4 *)(dct + (mbrow + strip * 16) * 256);
-        for( int i = lane; i < nvec; i += 64 )
-            dst[i] = src[i];
-    }
-}
-
-// Variant 5 (transform 4): as variant 3 with 8 MBs per wave: lane = (band, MB,
-// half) reads 8 pixels per row and transforms two 4x4 blocks; half the LDS per
-// wave (more resident waves) and twice the waves (a shorter tail).
+// Transform 4 (both depths): one lane per (4-row band, MB, half) of an 8-MB strip: a lane
+// reads 8 pixels per row and transforms two 4x4 blocks, stages them in LDS so the strip's
+// coefficients leave as contiguous 16-byte stores (0.62-0.71 of HBM against 0.50-0.52 for
+// the 16-MB strip with a lane per 4-pixel column, and a lane per (MB, band) of a 16-MB
+// strip in between; tools/dq_variants.py).
 template <int BD, bool NT = false>
 __global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,
@@ -924,125 +779,66 @@ hipError_t launch_mb_dct_quant( int transform, const typename PT<BD>::pixel *fen
                                 const typename PT<BD>::udctcoef *bias, typename PT<BD>::dctcoef *dct, int32_t *nz,
                                 hipStream_t stream )
 {
-    int lpm = transform == 4 ? 16 : transform == 8 ? 4 : 0;
-    if( !lpm )
+    if( transform != 4 && transform != 8 )
         return hipErrorInvalidValue;
-    const int ev = variant( V_DQ );
-    if( ev != 1 )
+    const int64_t waves = (int64_t)nframes * mbh * ((mbw + 15) / 16);
+    if( waves <= 0 )
+        return hipSuccess;
+    dim3 blk( 256 );
+    // nontemporal coefficient stores (stream_nt): 64 frames 4x4 0.0985 -> 0.0876 ms, 8x8
+    // 0.1029 -> 0.0776 ms; 16 frames 0.0279 -> 0.0267, 0.0263 -> 0.0247 (profiles/r03s_nt_ab.json)
+    const bool nt = stream_nt();
+    // XCD-contiguous strips (X264HIP_STREAM_XCD=1 turns them on): a row's neighbouring
+    // strips share the 128-B lines their MB columns straddle, so in one XCD's L2 those
+    // lines are fetched once instead of once per XCD.  With the sector shift below no
+    // line is shared and the order only cost time (64 frames: 0.1056 vs 0.1023 ms for 4x4,
+    // profiles/r03af_dq_ab.log), so it is off by default
+    const int xcd = variant( V_STREAM_XCD ) == 1;
+    // Sector-aligned strips (as launch_mb_recon does for its stores): with row and frame
+    // strides multiples of 64 bytes, x = 0 sits at the same offset in a 64-byte sector on
+    // every row, so shifting the strips left by that offset (in MBs) puts every wave's
+    // row pieces of the source on whole sectors, none shared by two waves (fetch 1.27x ->
+    // 1.00x of the algorithmic reads for 4x4, 1.11x -> 1.01x for 8x8, profiles/r03ae-af)
+    const size_t psz = sizeof( typename PT<BD>::pixel );
+    const bool al = !(((size_t)fs * psz) & 63) && !(((size_t)ffs * psz) & 63);
+    const int off = al ? (int)((uintptr_t)fenc & 63) : 0;
+    const int sh = off % (16 * (int)psz) ? 0 : off / (16 * (int)psz);
+    if( transform == 4 )
     {
-        // default: strip kernel, one wave per 16 MBs of a row
-        int64_t waves = (int64_t)nframes * mbh * ((mbw + 15) / 16);
-        if( waves <= 0 )
-            return hipSuccess;
-        dim3 blk( 256 ), g( (unsigned)((waves + 3) / 4) );
-        // transform 4 default: variant 5 (0.62-0.71 of HBM vs 0.50-0.52 for variant 0,
-        // tools/dq_variants.py); X264HIP_DQ_VARIANT=0 selects the 16-MB staged strip
-        // nontemporal coefficient stores (stream_nt): 64 frames 4x4 0.0985 -> 0.0876 ms, 8x8
-        // 0.1029 -> 0.0776 ms; 16 frames 0.0279 -> 0.0267, 0.0263 -> 0.0247 (profiles/r03s_nt_ab.json)
-        const bool nt = stream_nt();
-        // XCD-contiguous strips (X264HIP_STREAM_XCD=1 turns them on): a row's neighbouring
-        // strips share the 128-B lines their MB columns straddle, so in one XCD's L2 those
-        // lines are fetched once instead of once per XCD.  With the sector shift below no
-        // line is shared and the order only cost time (64 frames: 0.1056 vs 0.1023 ms for 4x4,
-        // profiles/r03af_dq_ab.log), so it is off by default
-        const int xcd = variant( V_STREAM_XCD ) == 1;
-        // Sector-aligned strips (as launch_mb_recon does for its stores): with row and frame
-        // strides multiples of 64 bytes, x = 0 sits at the same offset in a 64-byte sector on
-        // every row, so shifting the strips left by that offset (in MBs) puts every wave's
-        // row pieces of the source on whole sectors, none shared by two waves
-        // (X264HIP_STREAM_XCD=2 keeps the unshifted strips).
-        const size_t psz = sizeof( typename PT<BD>::pixel );
-        const bool al = variant( V_STREAM_XCD ) != 2 && !(((size_t)fs * psz) & 63) && !(((size_t)ffs * psz) & 63);
-        const int off = al ? (int)((uintptr_t)fenc & 63) : 0;
-        const int sh = off % (16 * (int)psz) ? 0 : off / (16 * (int)psz);
-        if( transform == 4 && (ev < 0 || ev == 5) )
-        {
-            const int64_t hw = (int64_t)nframes * mbh * ((mbw + sh + 7) / 8);
-            if( nt )
-                hipLaunchKernelGGL( ( mb_dct_quant_halfband_kernel<BD, true> ), dim3( (unsigned)((hw + 3) / 4) ), blk,
-                                    0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
-            else
-                hipLaunchKernelGGL( mb_dct_quant_halfband_kernel<BD>, dim3( (unsigned)((hw + 3) / 4) ), blk, 0, stream,
-                                    fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
-            return hipGetLastError();
-        }
-        if( transform == 4 && (ev == 3 || ev == 4) )
-        {
-            if( ev == 3 )
-                hipLaunchKernelGGL( ( mb_dct_quant_band_kernel<BD, true> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps,
-                                    pfs, mbw, mbh, nframes, mf, bias, dct, nz );
-            else
-                hipLaunchKernelGGL( ( mb_dct_quant_band_kernel<BD, false> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps,
-                                    pfs, mbw, mbh, nframes, mf, bias, dct, nz );
-            return hipGetLastError();
-        }
-        // transform 8 at 8 bit default: variant 6 (packed 16-bit pairs, 7 = its unstaged stores); 0 / 2
-        // select the strip kernel
-        if constexpr( BD == 8 )
-            if( transform == 8 && (ev < 0 || ev == 6 || ev == 7) )
-            {
-                g = dim3( (unsigned)(((int64_t)nframes * mbh * ((mbw + sh + 15) / 16) + 3) / 4) );
-                if( (ev < 0 || ev == 6) && nt )
-                    hipLaunchKernelGGL( ( mb_dct8_quant_pk_kernel<true, true> ), g, blk, 0, stream, fenc, fs, ffs, pred,
-                                        ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
-                else if( ev < 0 || ev == 6 )
-                    hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<true>, g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs,
-                                        mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
-                else
-                    hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<false>, g, blk, 0, stream, fenc, fs, ffs, pred, ps,
-                                        pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
-                return hipGetLastError();
-            }
-        const bool stage = ev != 2;
-        // 10-bit transform 8 default: variant 11 (0.2011 vs 0.2165 ms for the four-wave
-        // staged strips with plain stores at 64 1080p pairs, 0.665 vs 0.618 of HBM: the 64 KB
-        // stage of a four-wave workgroup held it to 2 waves per SIMD; profiles/r03aj_dq_ab10.log)
-        const int sv = ev < 0 && BD == 10 && transform == 8 ? 11 : ev;
-        if( sv == 11 || sv == 12 )
-        {
-            // staged strips with the stream store policy (nontemporal unless X264HIP_STREAM_NT=0):
-            // 11 one-wave workgroups, 12 four-wave
-#define DQ_STRIP_W( T, W )                                                                                       \
-    do                                                                                                           \
-    {                                                                                                            \
-        const dim3 gw( W == 1 ? (unsigned)waves : g.x ), bw( 64 * W );                                           \
-        if( nt )                                                                                                 \
-            hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, true, true, W> ), gw, bw, 0, stream, fenc, fs, \
-                                ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );                      \
-        else                                                                                                     \
-            hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, true, false, W> ), gw, bw, 0, stream, fenc,  \
-                                fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz );                  \
-    } while( 0 )
-            if( transform == 4 && sv == 11 ) DQ_STRIP_W( 4, 1 );
-            else if( transform == 4 ) DQ_STRIP_W( 4, 4 );
-            else if( sv == 11 ) DQ_STRIP_W( 8, 1 );
-            else DQ_STRIP_W( 8, 4 );
-#undef DQ_STRIP_W
-            return hipGetLastError();
-        }
-#define DQ_STRIP( T, S ) hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, T, S> ), g, blk, 0, stream, fenc, fs, ffs, \
-                                             pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz )
-        if( transform == 4 )
-        {
-            if( stage ) DQ_STRIP( 4, true ); else DQ_STRIP( 4, false );
-        }
+        const int64_t hw = (int64_t)nframes * mbh * ((mbw + sh + 7) / 8);
+        if( nt )
+            hipLaunchKernelGGL( ( mb_dct_quant_halfband_kernel<BD, true> ), dim3( (unsigned)((hw + 3) / 4) ), blk, 0,
+                                stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
         else
-        {
-            if( stage ) DQ_STRIP( 8, true ); else DQ_STRIP( 8, false );
-        }
-#undef DQ_STRIP
+            hipLaunchKernelGGL( mb_dct_quant_halfband_kernel<BD>, dim3( (unsigned)((hw + 3) / 4) ), blk, 0, stream,
+                                fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
         return hipGetLastError();
     }
-    int64_t lanes = (int64_t)nframes * mbh * mbw * lpm;
-    if( lanes <= 0 )
-        return hipSuccess;
-    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
-    if( transform == 4 )
-        hipLaunchKernelGGL( ( mb_dct_quant_kernel<BD, 4> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh,
-                            nframes, mf, bias, dct, nz );
+    if constexpr( BD == 8 )
+    {
+        // 8 bit: packed 16-bit pair arithmetic, swizzled LDS staging (0.56 -> 0.66 of HBM)
+        const dim3 g( (unsigned)(((int64_t)nframes * mbh * ((mbw + sh + 15) / 16) + 3) / 4) );
+        if( nt )
+            hipLaunchKernelGGL( ( mb_dct8_quant_pk_kernel<true, true> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps,
+                                pfs, mbw, mbh, nframes, mf, bias, dct, nz, xcd, sh );
+        else
+            hipLaunchKernelGGL( mb_dct8_quant_pk_kernel<true>, g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs, mbw,
+                                mbh, nframes, mf, bias, dct, nz, xcd, sh );
+    }
     else
-        hipLaunchKernelGGL( ( mb_dct_quant_kernel<BD, 8> ), g, blk, 0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh,
-                            nframes, mf, bias, dct, nz );
+    {
+        // 10 bit: staged 16-MB strips in one-wave workgroups (0.2011 vs 0.2165 ms for four-wave
+        // workgroups at 64 1080p pairs, 0.665 vs 0.618 of HBM: the 64 KB stage of a four-wave
+        // workgroup held it to 2 waves per SIMD; profiles/r03aj_dq_ab10.log)
+        if( nt )
+            hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, 8, true, true, 1> ), dim3( (unsigned)waves ),
+                                dim3( 64 ), 0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct,
+                                nz );
+        else
+            hipLaunchKernelGGL( ( mb_dct_quant_strip_kernel<BD, 8, true, false, 1> ), dim3( (unsigned)waves ),
+                                dim3( 64 ), 0, stream, fenc, fs, ffs, pred, ps, pfs, mbw, mbh, nframes, mf, bias, dct,
+                                nz );
+    }
     return hipGetLastError();
 }
 

@@ -26,6 +26,17 @@ template <> struct PT<10>
     static constexpr int PPD = 2;
 };
 
+// Motion-search table geometry (me.hip; include/x264hip.h x264hip_me_table_pitch /
+// x264hip_me_centred_pitch).  A full-search table is the (2R+1)^2 square around mv 0 at row
+// pitch align4(2R+1).  A centred table is me.c's ESA window around a predictor: 2R+1 rows
+// and the columns the window can reach past bmx + R -- the width rounding
+// (max_x - min_x + 3) & ~3 (me.c:626) ends up to two columns past max_x -- plus the window
+// origin's alignment down to a dword (3 pixels at 8 bit, 1 at 10 bit).
+__host__ __device__ constexpr int al4( int x ) { return (x + 3) & ~3; }
+__host__ __device__ constexpr int full_pitch( int R ) { return al4( 2 * R + 1 ); }
+__host__ __device__ constexpr int cen_cols( int bd, int R ) { return bd == 8 ? 2 * R + 6 : 2 * R + 4; }
+__host__ __device__ constexpr int cen_pitch( int bd, int R ) { return al4( cen_cols( bd, R ) ); }
+
 // block sizes, reference common/pixel.h:55-59
 __host__ __device__ constexpr int pix_w( int i ) { return i == 0 || i == 1 ? 16 : i <= 4 ? 8 : 4; }
 __host__ __device__ constexpr int pix_h( int i )
@@ -189,14 +200,18 @@ template <int BD> __device__ __forceinline__ int upix( uint32_t w, int k )
 
 } // namespace x264hip
 
-// ---- A/B kernel-variant switches ----
-// Seeded once from the X264HIP_*_VARIANT environment variables when the library
-// loads and changed only through x264hip_set_variant(): launchers read an atomic,
-// never the environment.  -1 = the launcher's default.
+// ---- run-time switches ----
+// Seeded once from the environment when the library loads and changed only through
+// x264hip_set_variant(): launchers read an atomic, never the environment.  -1 = the
+// launcher's default.  Every kernel a switch selects is a default kernel of some input
+// (X264HIP_TESA_VARIANT=1: the in-scan SADs of me_range > 24; X264HIP_INTEGRAL_VARIANT=1: the
+// unaligned-plane kernel) or a layout option within 3 % of the default in a committed A/B
+// (X264HIP_ME_XCD, X264HIP_STREAM_XCD, X264HIP_STREAM_NT); X264HIP_LA_POLL is a test hook and
+// X264HIP_UPLOAD_WGS the upload grid cap.
 namespace x264hip {
 enum VariantSlot
 {
-    V_ME = 0, V_HPEL, V_HPEL_ROWS, V_SUBPEL, V_LOWRES, V_DQ, V_RECON, V_LOWRES_INTRA, V_LA_BAND, V_ME_LEAD, V_TESA, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_STREAM_NT, V_SSD, V_COUNT
+    V_TESA = 0, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_STREAM_NT, V_COUNT
 };
 int variant( VariantSlot slot );
 
@@ -251,8 +266,21 @@ template <bool NT> __device__ __forceinline__ void st16( void *p, uint4 v )
 }
 } // namespace x264hip
 
+// The device a launch runs on: the launch stream's device, or the calling thread's current
+// device for the null stream.  Every launcher that keys device-side state (scratch pools,
+// accumulator rings, status words) by device takes it from here, never from the thread
+// alone: a stream of device 1 with device 0 current must not be handed device-0 memory.
+namespace x264hip {
+inline hipError_t stream_device( hipStream_t stream, int *dev )
+{
+    return stream ? hipStreamGetDevice( stream, dev ) : hipGetDevice( dev );
+}
+} // namespace x264hip
+
 // ---- launchers implemented in the .hip files (all enqueue on `stream`) ----
 namespace x264hip {
+hipError_t scratch_trim( int dev );
+hipError_t lowres_status( hipStream_t stream );
 hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t stream );
 template <int BD>
 hipError_t launch_cmp_batch( int op, int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs,

@@ -1176,21 +1176,21 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
 {
     if( mbw <= 0 || mbh <= 0 || nframes <= 0 )
         return hipSuccess;
-    const int ev = variant( V_RECON );
-    // 8 bit: block pairs (0.55 vs 0.43 of HBM, tools/recon_variants.py); 10 bit: one lane
-    // per block is faster (0.68 vs 0.58); X264HIP_RECON_VARIANT = 0 / 1 forces either
-    const bool pair = ev >= 0 && ev != 2 ? ev != 1 : BD == 8;
-    // transform 8 at 8 bit: the packed kernel unless X264HIP_RECON_VARIANT = 1 (lane per block, int32)
+    if( transform != 4 && transform != 8 )
+        return hipErrorInvalidValue;
+    // 8 bit: block pairs for transform 4 (0.55 vs 0.43 of HBM, tools/recon_variants.py) and
+    // the packed int16-pair kernel for transform 8; 10 bit: one lane per block (0.68 vs 0.58
+    // for the pairs).
     // Sector alignment of the stores: with row and frame strides multiples of 64 bytes, every
     // row of the output plane has x = 0 at the same offset within a 64-byte sector; shifting
     // the waves' pixel ranges by that offset puts every wave's row pieces on whole sectors
     // (partial sectors shared by two waves were the half-pel planes' bottleneck).
-    // X264HIP_RECON_VARIANT=2 keeps the unshifted layout.
     const size_t psz = sizeof( typename PT<BD>::pixel );
-    const bool al = ev != 2 && !(((size_t)rs * psz) & 63) && !(((size_t)rfs * psz) & 63);
+    const bool al = !(((size_t)rs * psz) & 63) && !(((size_t)rfs * psz) & 63);
     const int off = al ? (int)((uintptr_t)recon & 63) : 0;       // byte offset of x = 0 in its sector
     if constexpr( BD == 8 )
-        if( transform == 8 && ev != 1 )
+    {
+        if( transform == 8 )
         {
             const int sh8 = off % 8 ? 0 : off / 8;                 // 8-pixel blocks
             const int64_t total = (int64_t)nframes * mbh * 2 * ((mbw * 2 + sh8 + 63) & ~63);
@@ -1198,9 +1198,7 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
                                 mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs, rfs, sh8 );
             return hipGetLastError();
         }
-    if( transform == 4 && pair )
-    {
-        const int sh = off % (16 * (int)psz) ? 0 : off / (16 * (int)psz);   // 16-pixel MBs
+        const int sh = off % 16 ? 0 : off / 16;                    // 16-pixel MBs
         const int64_t waves = (int64_t)nframes * mbh * ((mbw + sh + 7) / 8);
         hipLaunchKernelGGL( mb_recon_pair_kernel<BD>, dim3( (unsigned)((waves + 3) / 4) ), dim3( 256 ), 0, st, dct,
                             mbw, mbh, nframes, dmf, qp, pred, ps, pfs, recon, rs, rfs, sh );
@@ -1212,11 +1210,9 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
     if( transform == 8 )
         hipLaunchKernelGGL( ( mb_recon_kernel<BD, 8> ), g, blk, 0, st, dct, mbw, mbh, nframes, dmf, qp, pred, ps, pfs,
                             recon, rs, rfs );
-    else if( transform == 4 )
+    else
         hipLaunchKernelGGL( ( mb_recon_kernel<BD, 4> ), g, blk, 0, st, dct, mbw, mbh, nframes, dmf, qp, pred, ps, pfs,
                             recon, rs, rfs );
-    else
-        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -311,34 +311,6 @@ __global__ __launch_bounds__( 256 ) void lowres_intra_row_kernel( const typename
     }
 }
 
-// X264HIP_LOWRES_INTRA_VARIANT=1: grid (ceil(mbw/64), mb_height, n_frames) of single waves,
-// every wave adding its sums atomically
-template <int BD, bool SATD, bool ALL>
-__global__ __launch_bounds__( 64 ) void lowres_intra_kernel( const typename PT<BD>::pixel *plane, intptr_t stride,
-                                                             intptr_t fstride, int mbw, int mbh, int penalty,
-                                                             const uint16_t *invq, uint16_t *cost,
-                                                             int32_t *row_satd, int32_t *est )
-{
-    const int mbx = blockIdx.x * 64 + threadIdx.x, mby = blockIdx.y, f = blockIdx.z;
-    int c_plain = 0, c_aq = 0, c_row = 0;
-    if( mbx < mbw )
-        lowres_mb<BD, SATD, ALL>( plane, stride, fstride, mbx, mby, f, mbw, mbh, penalty, invq, cost, c_row,
-                                  c_plain, c_aq );
-    c_row = wave_sum( c_row );
-    c_plain = wave_sum( c_plain );
-    c_aq = wave_sum( c_aq );
-    if( threadIdx.x == 0 )
-    {
-        if( row_satd )
-            atomicAdd( &row_satd[(int64_t)f * mbh + mby], c_row );
-        if( est )
-        {
-            atomicAdd( &est[2 * f], c_plain );
-            atomicAdd( &est[2 * f + 1], c_aq );
-        }
-    }
-}
-
 template <int BD>
 hipError_t launch_lowres_intra( const typename PT<BD>::pixel *plane, intptr_t stride, intptr_t fstride, int mbw,
                                 int mbh, int nframes, int satd, int all_modes, int lambda, const uint16_t *invq,
@@ -346,13 +318,6 @@ hipError_t launch_lowres_intra( const typename PT<BD>::pixel *plane, intptr_t st
 {
     if( mbw <= 0 || mbh <= 0 || nframes <= 0 )
         return hipSuccess;
-    const bool per_wave = variant( V_LOWRES_INTRA ) == 1;
-    if( row_satd && per_wave )
-    {
-        hipError_t e = hipMemsetAsync( row_satd, 0, sizeof(int32_t) * (size_t)mbh * nframes, st );
-        if( e != hipSuccess )
-            return e;
-    }
     if( est )
     {
         hipError_t e = hipMemsetAsync( est, 0, sizeof(int32_t) * 2 * (size_t)nframes, st );
@@ -364,12 +329,8 @@ hipError_t launch_lowres_intra( const typename PT<BD>::pixel *plane, intptr_t st
 #define L( S, A )                                                                                                    \
     do                                                                                                               \
     {                                                                                                                \
-        if( per_wave )                                                                                               \
-            hipLaunchKernelGGL( ( lowres_intra_kernel<BD, S, A> ), dim3( (mbw + 63) / 64, mbh, nframes ), dim3( 64 ), \
-                                0, st, plane, stride, fstride, mbw, mbh, pen, invq, cost, row_satd, est );           \
-        else                                                                                                         \
-            hipLaunchKernelGGL( ( lowres_intra_row_kernel<BD, S, A> ), dim3( mbh, nframes ), dim3( bt ), 0, st,      \
-                                plane, stride, fstride, mbw, mbh, pen, invq, cost, row_satd, est );                  \
+        hipLaunchKernelGGL( ( lowres_intra_row_kernel<BD, S, A> ), dim3( mbh, nframes ), dim3( bt ), 0, st,          \
+                            plane, stride, fstride, mbw, mbh, pen, invq, cost, row_satd, est );                      \
     } while( 0 )
     if( satd && all_modes )
         L( true, true );

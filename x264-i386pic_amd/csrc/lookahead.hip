@@ -1197,13 +1197,20 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
 }
 
 // The wavefront's status word: a per-thread, per-device device word the kernel sets when a
-// band's wait for the band underneath ran out (lr_preds), read back after the launch so
-// the entry returns an error instead of costs built on missing predictors.  The wait can
-// only run out if the schedule's premise breaks: the band a workgroup waits on has a
-// lower index, and an XCD dispatches its workgroups in index order, so by induction the
-// lowest unfinished workgroup is resident and never waits -- no residency bound on the
-// batch is needed; the poll bound (X264HIP_LA_POLL, default 2^22 tries) turns a broken
-// premise (preemption, a changed dispatcher) into this error rather than a hang.
+// band's wait for the band underneath ran out (lr_preds).  The wait can only run out if the
+// schedule's premise breaks: the band a workgroup waits on has a lower index, and an XCD
+// dispatches its workgroups in index order, so by induction the lowest unfinished workgroup
+// is resident and never waits -- no residency bound on the batch is needed; the poll bound
+// (X264HIP_LA_POLL, default 2^22 tries) turns a broken premise (preemption, a changed
+// dispatcher) into this error rather than a hang.
+// The launches stay asynchronous (and capturable into a graph): the word is sticky on the
+// device, each launch queues a copy of it into pinned host memory behind the kernel and
+// records an event, and the error is reported
+//  * by the next lookahead entry on this thread and device once that copy has landed (the
+//    entry then refuses with X264HIP_EDEVICE before launching anything), and
+//  * by x264hip_lowres_status( stream ), which waits for the stream and reads the word.
+// Reporting clears the word.  Under stream capture no copy is queued; the word is still set
+// by the replayed kernels and x264hip_lowres_status reads it.
 namespace {
 // (no destructor: the words live as long as the process -- freeing them from a
 // thread-exit destructor can run after the HIP runtime has been torn down, which
@@ -1213,48 +1220,113 @@ struct LaStatus
     int device = -1;
     uint32_t *dev = nullptr;
     uint32_t *host = nullptr;
+    hipEvent_t ev = nullptr;
+    bool pending = false;            // a copy of the word is queued behind a launch
 };
 thread_local LaStatus t_la_status;
 
-hipError_t la_status_begin( hipStream_t stream, uint32_t **word )
+// the status word of the stream's device for this thread (allocated on first use)
+hipError_t la_status_get( hipStream_t stream, LaStatus **out )
 {
     int d = 0;
-    hipError_t e = hipGetDevice( &d );
+    hipError_t e = stream_device( stream, &d );
     if( e != hipSuccess )
         return e;
     LaStatus &st = t_la_status;
     if( st.device != d )
     {
-        if( st.dev )
-            (void)hipFree( st.dev );
-        if( st.host )
-            (void)hipHostFree( st.host );
-        st.dev = nullptr;
+        int cur = 0;
+        if( (e = hipGetDevice( &cur )) != hipSuccess || (cur != d && (e = hipSetDevice( d )) != hipSuccess) )
+            return e;
+        st.dev = nullptr;                 // (the old device's words are abandoned, not freed)
         st.host = nullptr;
+        st.ev = nullptr;
+        st.pending = false;
         st.device = -1;
-        if( (e = hipMalloc( (void **)&st.dev, sizeof( uint32_t ) )) != hipSuccess )
+        e = hipMalloc( (void **)&st.dev, sizeof( uint32_t ) );
+        if( e == hipSuccess )
+            e = hipMemset( st.dev, 0, sizeof( uint32_t ) );
+        if( e == hipSuccess )
+            e = hipHostMalloc( (void **)&st.host, sizeof( uint32_t ), hipHostMallocDefault );
+        if( e == hipSuccess )
+            e = hipEventCreateWithFlags( &st.ev, hipEventDisableTiming );
+        if( cur != d )
+            (void)hipSetDevice( cur );
+        if( e != hipSuccess )
             return e;
-        if( (e = hipHostMalloc( (void **)&st.host, sizeof( uint32_t ), hipHostMallocDefault )) != hipSuccess )
-            return e;
+        *st.host = 0;
         st.device = d;
     }
-    *word = st.dev;
+    *out = &st;
+    return hipSuccess;
+}
+
+// a reported timeout clears the sticky word (host and device)
+hipError_t la_status_clear( LaStatus &st, hipStream_t stream )
+{
+    *(volatile uint32_t *)st.host = 0;
     return hipMemsetAsync( st.dev, 0, sizeof( uint32_t ), stream );
 }
 
-// after the kernel: hipErrorLaunchTimeOut when a band gave up waiting
+// before a launch: the word for the kernel, or hipErrorLaunchTimeOut when an earlier launch
+// of this thread on this device is known to have timed out
+hipError_t la_status_begin( hipStream_t stream, uint32_t **word )
+{
+    LaStatus *st = nullptr;
+    hipError_t e = la_status_get( stream, &st );
+    if( e != hipSuccess )
+        return e;
+    if( st->pending && hipEventQuery( st->ev ) == hipSuccess )
+    {
+        st->pending = false;
+        if( *(volatile uint32_t *)st->host )
+        {
+            (void)la_status_clear( *st, stream );
+            return hipErrorLaunchTimeOut;
+        }
+    }
+    *word = st->dev;
+    return hipSuccess;
+}
+
+// after the kernel: queue the word's copy behind it (not under capture)
 hipError_t la_status_end( hipStream_t stream )
 {
     LaStatus &st = t_la_status;
-    *st.host = 0;
-    hipError_t e = hipMemcpyAsync( st.host, st.dev, sizeof( uint32_t ), hipMemcpyDeviceToHost, stream );
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    hipError_t e = hipStreamIsCapturing( stream, &cs );
+    if( e != hipSuccess || cs != hipStreamCaptureStatusNone )
+        return e;
+    e = hipMemcpyAsync( st.host, st.dev, sizeof( uint32_t ), hipMemcpyDeviceToHost, stream );
+    if( e == hipSuccess )
+        e = hipEventRecord( st.ev, stream );
+    st.pending = e == hipSuccess;
+    return e;
+}
+} // namespace
+
+// x264hip_lowres_status: wait for `stream`, then hipErrorLaunchTimeOut if a lookahead launch of
+// this thread on the stream's device timed out since the last report (and clear it)
+hipError_t lowres_status( hipStream_t stream )
+{
+    LaStatus *st = nullptr;
+    hipError_t e = la_status_get( stream, &st );
+    if( e != hipSuccess )
+        return e;
+    e = hipMemcpyAsync( st->host, st->dev, sizeof( uint32_t ), hipMemcpyDeviceToHost, stream );
     if( e == hipSuccess )
         e = hipStreamSynchronize( stream );
     if( e != hipSuccess )
         return e;
-    return *(volatile uint32_t *)st.host ? hipErrorLaunchTimeOut : hipSuccess;
+    st->pending = false;
+    if( !*(volatile uint32_t *)st->host )
+        return hipSuccess;
+    if( (e = la_status_clear( *st, stream )) == hipSuccess )
+        e = hipStreamSynchronize( stream );
+    return e == hipSuccess ? hipErrorLaunchTimeOut : e;
 }
 
+namespace {
 // bands per frame over the lookahead slices (lr_band)
 int la_nbands( int mbh, int nslices, int brows )
 {
@@ -1295,13 +1367,12 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
         e = hipMemsetAsync( est, 0, (size_t)n * 2 * sizeof( int32_t ), stream );
     if( e != hipSuccess )
         return e;
-    // X264HIP_LOOKAHEAD_BAND: block rows per single-wave workgroup (<= 16).  A step costs
-    // the slowest of a wave's row searches (the lanes run in lockstep), so fewer rows per
-    // wave means less divergence; 4 measured best (15 1080p pairs, tools/la_band.py:
-    // P 2.46 / 2.32 / 2.19 / 2.26 ms, B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2)
-    const int bv = variant( V_LA_BAND );
-    const int brows = bv >= 1 && bv <= LR_BAND ? bv : 4;
-    const int brows4 = min( brows, 4 );          // a wave holds four roles of <= 4 rows
+    // block rows per single-wave workgroup: a step costs the slowest of a wave's row
+    // searches (the lanes run in lockstep), so fewer rows per wave means less divergence; 4
+    // measured best (15 1080p pairs, tools/la_band.py: P 2.46 / 2.32 / 2.19 / 2.26 ms,
+    // B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2 rows)
+    constexpr int brows = 4;
+    constexpr int brows4 = brows;                // a wave holds four roles of <= 4 rows
     const int nbands = la_nbands( mbh, nslices, brows4 );
     if( nslices < 1 || (int64_t)n * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
@@ -1317,7 +1388,7 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
                         invq, lowres_costs, row_satd, est, nbands, brows4, la_poll_max(), status, nslices );
     if( (e = hipGetLastError()) != hipSuccess )
         return e;
-    return (search & 3) ? la_status_end( stream ) : hipSuccess;
+    return la_status_end( stream );
 }
 
 template <int BD>
@@ -1337,13 +1408,12 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
         e = hipMemsetAsync( est, 0, (size_t)npairs * 3 * sizeof( int32_t ), stream );
     if( e != hipSuccess )
         return e;
-    // X264HIP_LOOKAHEAD_BAND: block rows per single-wave workgroup (<= 16).  A step costs
-    // the slowest of a wave's row searches (the lanes run in lockstep), so fewer rows per
-    // wave means less divergence; 4 measured best (15 1080p pairs, tools/la_band.py:
-    // P 2.46 / 2.32 / 2.19 / 2.26 ms, B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2)
-    const int bv = variant( V_LA_BAND );
-    const int brows = bv >= 1 && bv <= LR_BAND ? bv : 4;
-    const int brows4 = min( brows, 4 );          // four groups of <= 4 rows per wave
+    // block rows per single-wave workgroup: a step costs the slowest of a wave's row
+    // searches (the lanes run in lockstep), so fewer rows per wave means less divergence; 4
+    // measured best (15 1080p pairs, tools/la_band.py: P 2.46 / 2.32 / 2.19 / 2.26 ms,
+    // B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2 rows)
+    constexpr int brows = 4;
+    constexpr int brows4 = brows;                // four groups of <= 4 rows per wave
     const int nbands = la_nbands( mbh, nslices, brows4 );
     if( nslices < 1 || (int64_t)npairs * nbands > 0x7fffffff )
         return hipErrorInvalidValue;

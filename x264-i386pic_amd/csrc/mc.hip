@@ -13,108 +13,15 @@ namespace x264hip {
 
 // ------------------------------------------------------------ hpel filter
 // The reference filters x in [-8, W+8) and y in [-8, H+8) of each plane, then
-// re-expands the border from the last trusted column/row (x = -4 / W+3,
-// y = -8 / H+7) over the 32-pixel padding.  Interior kernel: one 64x16 tile per
-// workgroup staged through LDS (source with a 2/3-pixel halo, then the
-// vertical 6-tap intermediates that feed the centre plane).
-constexpr int HT_W = 64, HT_H = 16;
-constexpr int HS_W = HT_W + 5, HS_H = HT_H + 5;
-
-template <int BD>
-__device__ __forceinline__ int clip_px( int v )
-{
-    return v < 0 ? 0 : v > PT<BD>::PIXEL_MAX ? PT<BD>::PIXEL_MAX : v;
-}
-
+// re-expands the border from the last trusted column/row (x = -4 / W+3, y = -8 / H+7)
+// over the 32-pixel padding: a border pixel is the filter at the clamped coordinate.
 __device__ __forceinline__ int tap6( int a, int b, int c, int d, int e, int f )
 {
     return a + f - 5 * (b + e) + 20 * (c + d);   // TAPFILTER, mc.c:172
 }
 
-template <int BD>
-__global__ __launch_bounds__( 256 ) void hpel_interior_kernel( const typename PT<BD>::pixel *__restrict__ src,
-                                                               typename PT<BD>::pixel *__restrict__ dh,
-                                                               typename PT<BD>::pixel *__restrict__ dv,
-                                                               typename PT<BD>::pixel *__restrict__ dc,
-                                                               intptr_t stride, intptr_t fstride, int width,
-                                                               int height )
-{
-    using pixel = typename PT<BD>::pixel;
-    constexpr int pad = BD > 9 ? -10 * PT<BD>::PIXEL_MAX : 0;    // mc.c:176
-    __shared__ int s_src[HS_H][HS_W];
-    __shared__ int s_v[HT_H][HS_W];
-    const int x0 = -4 + HT_W * blockIdx.x;      // interior region: x in [-4, W+4)
-    const int y0 = -8 + HT_H * blockIdx.y;      //                  y in [-8, H+8)
-    const intptr_t fo = (intptr_t)blockIdx.z * fstride;
-    const pixel *s = src + fo;
-    for( int i = threadIdx.x; i < HS_H * HS_W; i += 256 )
-    {
-        int r = i / HS_W, c = i % HS_W;
-        // columns past the right padding are never needed by a written pixel
-        s_src[r][c] = x0 - 2 + c < width + 32 ? (int)s[(intptr_t)(y0 - 2 + r) * stride + (x0 - 2 + c)] : 0;
-    }
-    __syncthreads();
-    // vertical intermediates for rows y0..y0+15, columns x0-2 .. x0+66
-    for( int i = threadIdx.x; i < HT_H * HS_W; i += 256 )
-    {
-        int r = i / HS_W, c = i % HS_W;
-        s_v[r][c] = tap6( s_src[r][c], s_src[r + 1][c], s_src[r + 2][c], s_src[r + 3][c], s_src[r + 4][c],
-                          s_src[r + 5][c] );
-    }
-    __syncthreads();
-    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-    const int x = x0 + tx;
-    if( x >= width + 4 )
-        return;
-#pragma unroll
-    for( int k = 0; k < 4; k++ )
-    {
-        const int r = ty * 4 + k, y = y0 + r;
-        if( y >= height + 8 )
-            break;
-        const intptr_t o = fo + (intptr_t)y * stride + x;
-        const int v = s_v[r][tx + 2];
-        dv[o] = (pixel)clip_px<BD>( (v + 16) >> 5 );
-        const int hsum = tap6( s_src[r + 2][tx], s_src[r + 2][tx + 1], s_src[r + 2][tx + 2], s_src[r + 2][tx + 3],
-                               s_src[r + 2][tx + 4], s_src[r + 2][tx + 5] );
-        dh[o] = (pixel)clip_px<BD>( (hsum + 16) >> 5 );
-        // centre: the intermediates pass through int16 storage with the 10-bit bias (mc.c:179-181)
-        int b[6];
-#pragma unroll
-        for( int j = 0; j < 6; j++ )
-            b[j] = (int16_t)(s_v[r][tx + j] + pad);
-        const int csum = tap6( b[0], b[1], b[2], b[3], b[4], b[5] );
-        dc[o] = (pixel)clip_px<BD>( (csum - 32 * pad + 512) >> 10 );
-    }
-}
-
-// border re-expansion of the three planes: every padded pixel outside the
-// interior takes the interior pixel at the clamped coordinate (plane_expand_border,
-// frame.c:612-623 with padh = 28, padv = 24 from the last filtered pixels)
-template <int BD>
-__global__ __launch_bounds__( 256 ) void hpel_expand_kernel( typename PT<BD>::pixel *__restrict__ dh,
-                                                             typename PT<BD>::pixel *__restrict__ dv,
-                                                             typename PT<BD>::pixel *__restrict__ dc,
-                                                             intptr_t stride, intptr_t fstride, int width, int height,
-                                                             int pad )
-{
-    const int pw = width + 2 * pad, ph = height + 2 * pad;
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if( i >= (int64_t)pw * ph )
-        return;
-    const int x = (int)(i % pw) - pad, y = (int)(i / pw) - pad;
-    if( x >= -4 && x < width + 4 && y >= -8 && y < height + 8 )
-        return;
-    const int cx = x < -4 ? -4 : x >= width + 4 ? width + 3 : x;
-    const int cy = y < -8 ? -8 : y >= height + 8 ? height + 7 : y;
-    const intptr_t fo = (intptr_t)blockIdx.y * fstride;
-    const intptr_t d = fo + (intptr_t)y * stride + x, sidx = fo + (intptr_t)cy * stride + cx;
-    dh[d] = dh[sidx];
-    dv[d] = dv[sidx];
-    dc[d] = dc[sidx];
-}
-
-// Fused variant (default): one pass over the whole padded plane.  A pixel of
+// Fused kernel (10 bit, and 8-bit planes whose rows are not 16-byte aligned): one pass over
+// the whole padded plane.  A pixel of
 // the border takes the value the reference copies into it, i.e. the filter at
 // the clamped coordinate (x in [-4, W+3], y in [-8, H+7]); since the clamp is
 // monotonic, a 64x16 output tile needs at most a 76x21 source tile around its
@@ -278,29 +185,7 @@ __device__ __forceinline__ hs2 as_s2( uint32_t v ) { return __builtin_bit_cast( 
 __device__ __forceinline__ uint32_t as_u( hs2 v ) { return __builtin_bit_cast( uint32_t, v ); }
 
 // the four outputs x..x+3 of a horizontal 6-tap over the even pairs P[J..J+4] =
-// (x-2, x-1), (x, x+1), (x+2, x+3), (x+4, x+5), (x+6, x+7), scaled by M (so the
-// clipped result lands on a byte boundary) plus bias
-template <int J, int M, int N>
-__device__ __forceinline__ void tap6_h4( const hs2 (&P)[N], int bias, int (&o)[4] )
-{
-    constexpr short A = M, B = -5 * M, C = 20 * M;
-    o[0] = __builtin_amdgcn_sdot2( P[J], (hs2){ A, B }, bias, false );
-    o[0] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ C, C }, o[0], false );
-    o[0] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ B, A }, o[0], false );
-    o[1] = __builtin_amdgcn_sdot2( P[J], (hs2){ 0, A }, bias, false );
-    o[1] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ B, C }, o[1], false );
-    o[1] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ C, B }, o[1], false );
-    o[1] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ A, 0 }, o[1], false );
-    o[2] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ A, B }, bias, false );
-    o[2] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ C, C }, o[2], false );
-    o[2] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ B, A }, o[2], false );
-    o[3] = __builtin_amdgcn_sdot2( P[J + 1], (hs2){ 0, A }, bias, false );
-    o[3] = __builtin_amdgcn_sdot2( P[J + 2], (hs2){ B, C }, o[3], false );
-    o[3] = __builtin_amdgcn_sdot2( P[J + 3], (hs2){ C, B }, o[3], false );
-    o[3] = __builtin_amdgcn_sdot2( P[J + 4], (hs2){ A, 0 }, o[3], false );
-}
-
-// The same four outputs unscaled, the first tap of each chain taking its
+// (x-2, x-1), (x, x+1), (x+2, x+3), (x+4, x+5), (x+6, x+7), unscaled, the first tap of each chain taking its
 // coefficient pair from a VGPR (k15 = (1, -5), k01 = (0, 1)): that dot2 is then the
 // three-operand form with the SGPR bias as its accumulator, where a literal
 // coefficient forces the two-operand form and a v_mov of the bias into each
@@ -361,25 +246,11 @@ __device__ __forceinline__ uint32_t sat_pk_u8( hs2 v )
     return d;
 }
 
-// four scaled filter sums clamped to [0, HI] whose byte BY is the pixel, packed
-// into the bytes of a dword with two v_perm (+ one merge)
-template <int HI, int BY> __device__ __forceinline__ uint32_t pack_clip4( const int (&o)[4] )
-{
-    uint32_t b[4];
-#pragma unroll
-    for( int k = 0; k < 4; k++ )
-        b[k] = (uint32_t)min( max( o[k], 0 ), HI );
-    // perm selector bytes 0-3 pick from the second operand, 4-7 from the first
-    constexpr uint32_t lo = (uint32_t)BY | ((uint32_t)(BY + 4) << 8) | 0x0c0c0000u;
-    constexpr uint32_t hi = 0x0c0c | ((uint32_t)BY << 16) | ((uint32_t)(BY + 4) << 24);
-    return __builtin_amdgcn_perm( b[1], b[0], lo ) | __builtin_amdgcn_perm( b[3], b[2], hi );
-}
-
-template <int HS_ROWS, bool PK, bool NT = false>
+template <int HS_ROWS, bool NT = false>
 __device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
                                                   uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
                                                   intptr_t stride, intptr_t fstride, int width, int height,
-                                                  int hbias, int cbias, Blk3 B, int nstrips )
+                                                  Blk3 B, int nstrips )
 {
     const int lane = threadIdx.x & 63;
     const int nq = (width + 32) >> 4;                       // column quads over x in [-16, W+16)
@@ -454,46 +325,21 @@ __device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ sr
             }
             uint32_t oh[4], ov[4], oc[4];
             int o[4];
-            if constexpr( PK )
-            {
-                // V: clip( (v + 16) >> 5 ) by packed arithmetic shift + byte saturation;
-                // H: clip( (t + 16) >> 5 ), centre: clip( (t + 512) >> 10 ) with the
-                // bias in the accumulator and v_ashr_pk_u8_i32 doing shift and clip
+            // V: clip( (v + 16) >> 5 ) by packed arithmetic shift + byte saturation;
+            // H: clip( (t + 16) >> 5 ), centre: clip( (t + 512) >> 10 ) with the
+            // bias in the accumulator and v_ashr_pk_u8_i32 doing shift and clip
 #pragma unroll
-                for( int j = 0; j < 4; j++ )
-                    ov[j] = __builtin_amdgcn_perm( sat_pk_u8( (vi[2 + 2 * j] + (hs2)16) >> (hs2)5 ),
-                                                   sat_pk_u8( (vi[1 + 2 * j] + (hs2)16) >> (hs2)5 ), 0x05040100u );
-                tap6_h4v<0, 16>( hrow, k15, k01, o ); oh[0] = pack_shr4<5>( o );
-                tap6_h4v<2, 16>( hrow, k15, k01, o ); oh[1] = pack_shr4<5>( o );
-                tap6_h4v<4, 16>( hrow, k15, k01, o ); oh[2] = pack_shr4<5>( o );
-                tap6_h4v<6, 16>( hrow, k15, k01, o ); oh[3] = pack_shr4<5>( o );
-                tap6_h4v<0, 512>( vi, k15, k01, o ); oc[0] = pack_shr4<10>( o );
-                tap6_h4v<2, 512>( vi, k15, k01, o ); oc[1] = pack_shr4<10>( o );
-                tap6_h4v<4, 512>( vi, k15, k01, o ); oc[2] = pack_shr4<10>( o );
-                tap6_h4v<6, 512>( vi, k15, k01, o ); oc[3] = pack_shr4<10>( o );
-            }
-            else
-            {
-#pragma unroll
-                for( int j = 0; j < 4; j++ )
-                {
-                    // V: clip( (v + 16) >> 5 ), clamp before the shift
-                    hs2 va = vi[1 + 2 * j] + (hs2)16, vb = vi[2 + 2 * j] + (hs2)16;
-                    va = __builtin_elementwise_min( __builtin_elementwise_max( va, (hs2)0 ), (hs2)8191 );
-                    vb = __builtin_elementwise_min( __builtin_elementwise_max( vb, (hs2)0 ), (hs2)8191 );
-                    ov[j] = __builtin_amdgcn_perm( as_u( vb >> (hs2)5 ), as_u( va >> (hs2)5 ), 0x06040200u );
-                }
-                // H: clip( (t + 16) >> 5 ) computed as clamp( 8t + 128, 0, 0xffff ), byte 1;
-                // centre: clip( (t + 512) >> 10 ) as clamp( 64t + 32768, 0, 0xffffff ), byte 2
-                tap6_h4<0, 8>( hrow, hbias, o ); oh[0] = pack_clip4<0xffff, 1>( o );
-                tap6_h4<2, 8>( hrow, hbias, o ); oh[1] = pack_clip4<0xffff, 1>( o );
-                tap6_h4<4, 8>( hrow, hbias, o ); oh[2] = pack_clip4<0xffff, 1>( o );
-                tap6_h4<6, 8>( hrow, hbias, o ); oh[3] = pack_clip4<0xffff, 1>( o );
-                tap6_h4<0, 64>( vi, cbias, o ); oc[0] = pack_clip4<0xffffff, 2>( o );
-                tap6_h4<2, 64>( vi, cbias, o ); oc[1] = pack_clip4<0xffffff, 2>( o );
-                tap6_h4<4, 64>( vi, cbias, o ); oc[2] = pack_clip4<0xffffff, 2>( o );
-                tap6_h4<6, 64>( vi, cbias, o ); oc[3] = pack_clip4<0xffffff, 2>( o );
-            }
+            for( int j = 0; j < 4; j++ )
+                ov[j] = __builtin_amdgcn_perm( sat_pk_u8( (vi[2 + 2 * j] + (hs2)16) >> (hs2)5 ),
+                                               sat_pk_u8( (vi[1 + 2 * j] + (hs2)16) >> (hs2)5 ), 0x05040100u );
+            tap6_h4v<0, 16>( hrow, k15, k01, o ); oh[0] = pack_shr4<5>( o );
+            tap6_h4v<2, 16>( hrow, k15, k01, o ); oh[1] = pack_shr4<5>( o );
+            tap6_h4v<4, 16>( hrow, k15, k01, o ); oh[2] = pack_shr4<5>( o );
+            tap6_h4v<6, 16>( hrow, k15, k01, o ); oh[3] = pack_shr4<5>( o );
+            tap6_h4v<0, 512>( vi, k15, k01, o ); oc[0] = pack_shr4<10>( o );
+            tap6_h4v<2, 512>( vi, k15, k01, o ); oc[1] = pack_shr4<10>( o );
+            tap6_h4v<4, 512>( vi, k15, k01, o ); oc[2] = pack_shr4<10>( o );
+            tap6_h4v<6, 512>( vi, k15, k01, o ); oc[3] = pack_shr4<10>( o );
             if( st )
             {
                 intptr_t ox = 0;                             // extra piece: x in [-32, -16) / [W+16, W+32)
@@ -539,42 +385,15 @@ __device__ __forceinline__ void hpel_stream_body( const uint8_t *__restrict__ sr
     }
 }
 
-template <int HS_ROWS, bool PK, bool NT = false>
+// the fallback for widths the line-aligned chunks cannot take (below): 62 working lanes and
+// two halo lanes per wave
+template <int HS_ROWS, bool NT = false>
 __global__ __launch_bounds__( 64 ) void hpel_stream_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
                                                              uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
                                                              intptr_t stride, intptr_t fstride, int width,
-                                                             int height, int hbias, int cbias, int xcd )
+                                                             int height, int xcd )
 {
-    hpel_stream_body<HS_ROWS, PK, NT>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias, blk3( xcd ),
-                                       (int)gridDim.y - 4 );
-}
-
-// persistent form (variant 6): a resident grid of single-wave workgroups walks the
-// (chunk, strip, frame) units grid-stride, so waves drift out of the launch's lockstep and
-// one wave's loads overlap another's arithmetic and stores
-template <int HS_ROWS, bool PK>
-__global__ __launch_bounds__( 64 ) void hpel_persist_kernel( const uint8_t *__restrict__ src, uint8_t *__restrict__ dh,
-                                                              uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
-                                                              intptr_t stride, intptr_t fstride, int width,
-                                                              int height, int hbias, int cbias, uint32_t gx,
-                                                              uint32_t gy, uint32_t units )
-{
-    for( uint32_t u = blockIdx.x; u < units; u += gridDim.x )
-    {
-        const uint32_t yz = u / gx;
-        hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias,
-                                       Blk3{ u - yz * gx, yz % gy, yz / gy }, (int)gy - 4 );
-    }
-}
-
-// the same kernel under a 4-waves-per-SIMD register budget (<= 128 VGPRs; variants 4 / 5)
-template <int HS_ROWS, bool PK>
-__global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void hpel_stream4_kernel(
-    const uint8_t *__restrict__ src, uint8_t *__restrict__ dh, uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
-    intptr_t stride, intptr_t fstride, int width, int height, int hbias, int cbias, int xcd )
-{
-    hpel_stream_body<HS_ROWS, PK>( src, dh, dv, dc, stride, fstride, width, height, hbias, cbias, blk3( xcd ),
-                                   (int)gridDim.y - 4 );
+    hpel_stream_body<HS_ROWS, NT>( src, dh, dv, dc, stride, fstride, width, height, blk3( xcd ), (int)gridDim.y - 4 );
 }
 
 // Variant 7 (8-bit default): variant 3's streaming strips with every wave's stores on whole
@@ -783,102 +602,49 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
 {
     if( nframes <= 0 || width <= 0 || height <= 0 )
         return hipSuccess;
-    const int ev = variant( V_HPEL );
-    int var = ev >= 0 ? ev : BD == 8 ? 7 : 0;
     if constexpr( BD == 8 )
     {
-        // streaming kernel: needs 16-byte aligned rows (pixel (0,0) and the strides)
-        if( var >= 2 && var <= 7 && !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
-                           (uintptr_t)fstride) & 15) )
+        // streaming strips: need 16-byte aligned rows (pixel (0,0) and the strides)
+        if( !(((uintptr_t)src | (uintptr_t)dh | (uintptr_t)dv | (uintptr_t)dc | (uintptr_t)stride |
+               (uintptr_t)fstride) & 15) )
         {
-            const int nq = (width + 32) / 16, nchunk = (nq + 61) / 62;
-            // one wave per workgroup, so every launched wave has a column chunk (a 4-wave
-            // group left half its waves idle at 1080p's two chunks: with 162 VGPRs the
-            // SIMDs then held ~1.7 working waves, profiles/r01g_pmc_hpel_sq.json), and
-            // 12-row strips: twice the waves of 24-row ones for 5 halo rows per strip
-            // (16 frames: 0.0455 -> 0.0398 ms; 64 frames: 0.166 -> 0.158 ms; 16 rows in
-            // between).  X264HIP_HPEL_ROWS = 16 / 24 selects the taller strips.
-            const int er = variant( V_HPEL_ROWS );
-            const int rows = er == 6 || er == 8 || er == 16 || er == 24 ? er : 12;
-            dim3 g( nchunk, (height + 16 + rows - 1) / rows + 4, nframes );
+            // one wave per workgroup and 12-row strips: twice the waves of 24-row ones for 5
+            // halo rows per strip (16 frames: 0.0455 -> 0.0398 ms; 64 frames: 0.166 -> 0.158 ms;
+            // 6 / 8 / 16 / 24 rows all slower, profiles/r02k_hpel_rows*.json)
+            constexpr int ROWS = 12;
+            const int nq = (width + 32) / 16;
+            dim3 g( (nq + 61) / 62, (height + 16 + ROWS - 1) / ROWS + 4, nframes );
             // XCD-contiguous strips (adjacent strips' halo rows in one L2; X264HIP_STREAM_XCD=0
             // turns it off): 0.0329 -> 0.0324 ms at 16 frames, 0.1514 -> 0.1499 at 64
-            // (profiles/r03i_stream_var.json; the persistent form, variant 6, was no faster)
+            // (profiles/r03i_stream_var.json)
             const int sxcd = variant( V_STREAM_XCD ) != 0;
             const bool snt = stream_nt();
-#define HS_GO( ROWS )                                                                                              \
-    if( var == 7 && snt )                                                                                          \
-        hipLaunchKernelGGL( ( hpel_strip7_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, \
-                            fstride, width, height, sxcd );                                                        \
-    else if( var == 7 )                                                                                            \
-        hipLaunchKernelGGL( ( hpel_strip7_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride,\
-                            fstride, width, height, sxcd );                                                        \
-    else if( var == 6 )                                                                                            \
-    {                                                                                                              \
-        static int resident_[25] = {};                                                                             \
-        if( !resident_[ROWS] )                                                                                     \
-        {                                                                                                          \
-            int per_cu = 0, dev_ = 0, ncu_ = 0;                                                                    \
-            (void)hipGetDevice( &dev_ );                                                                           \
-            (void)hipDeviceGetAttribute( &ncu_, hipDeviceAttributeMultiprocessorCount, dev_ );                     \
-            (void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &per_cu, hpel_persist_kernel<ROWS, true>, 64, 0 ); \
-            resident_[ROWS] = std::max( 1, per_cu ) * std::max( 1, ncu_ );                                        \
-        }                                                                                                          \
-        const uint32_t units_ = g.x * g.y * g.z;                                                                   \
-        hipLaunchKernelGGL( ( hpel_persist_kernel<ROWS, true> ), dim3( std::min<uint32_t>( units_,                \
-                                                                                  (uint32_t)resident_[ROWS] ) ),  \
-                            dim3( 64 ), 0, stream, src, dh, dv, dc, stride, fstride, width, height, 8 * 16,         \
-                            64 * 512, g.x, g.y, units_ );                                                          \
-    }                                                                                                              \
-    else if( var == 3 && snt )                                                                                     \
-        hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, true, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,   \
-                            stride, fstride, width, height, 8 * 16, 64 * 512, sxcd );                              \
-    else if( var == 3 )                                                                                            \
-        hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc, stride, \
-                            fstride, width, height, 8 * 16, 64 * 512, sxcd );                                      \
-    else if( var == 4 )                                                                                            \
-        hipLaunchKernelGGL( ( hpel_stream4_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,       \
-                            stride, fstride, width, height, 8 * 16, 64 * 512, sxcd );                              \
-    else if( var == 5 )                                                                                            \
-        hipLaunchKernelGGL( ( hpel_stream4_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,        \
-                            stride, fstride, width, height, 8 * 16, 64 * 512, sxcd );                              \
-    else                                                                                                           \
-        hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,        \
-                            stride, fstride, width, height, 8 * 16, 64 * 512, sxcd )
-            if( var == 7 )
+            // line-aligned 64-piece chunks (hpel_strip7_kernel) unless the right border piece
+            // would lack its left neighbour in its wave, or the width is not a multiple of 16
+            const int np = nq + 2;
+            if( !(width & 15) && (np - 1) % 64 != 0 )
             {
-                // 64-piece chunks; the right border piece must have its left neighbour in its wave
-                const int np = nq + 2;
-                if( (width & 15) || (np - 1) % 64 == 0 )
-                    var = 3;
+                g.x = (np + 63) / 64;
+                if( snt )
+                    hipLaunchKernelGGL( ( hpel_strip7_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,
+                                        stride, fstride, width, height, sxcd );
                 else
-                    g.x = (np + 63) / 64;
+                    hipLaunchKernelGGL( ( hpel_strip7_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv,
+                                        dc, stride, fstride, width, height, sxcd );
             }
-            if( rows == 24 ) { HS_GO( 24 ); }
-            else if( rows == 16 ) { HS_GO( 16 ); }
-            else if( rows == 8 ) { HS_GO( 8 ); }
-            else if( rows == 6 ) { HS_GO( 6 ); }
-            else { HS_GO( 12 ); }
-#undef HS_GO
+            else if( snt )
+                hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, true> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,
+                                    stride, fstride, width, height, sxcd );
+            else
+                hipLaunchKernelGGL( ( hpel_stream_kernel<ROWS, false> ), g, dim3( 64 ), 0, stream, src, dh, dv, dc,
+                                    stride, fstride, width, height, sxcd );
             return hipGetLastError();
         }
     }
-    if( var != 1 )
-    {
-        // fused single pass; needs 4-pixel aligned rows (width + 64 covered by whole tiles of 4)
-        dim3 g( (width + 64 + HF_W - 1) / HF_W, (height + 64 + HF_H - 1) / HF_H, nframes );
-        hipLaunchKernelGGL( ( hpel_fused_kernel<BD> ), g, dim3( 256 ), 0, stream, src, dh, dv, dc, stride, fstride,
-                            width, height );
-        return hipGetLastError();
-    }
-    dim3 g1( (width + 8 + HT_W - 1) / HT_W, (height + 16 + HT_H - 1) / HT_H, nframes );
-    hipLaunchKernelGGL( ( hpel_interior_kernel<BD> ), g1, dim3( 256 ), 0, stream, src, dh, dv, dc, stride, fstride,
-                        width, height );
-    const int pad = 32;
-    const int64_t npx = (int64_t)(width + 2 * pad) * (height + 2 * pad);
-    dim3 g2( (unsigned)((npx + 255) / 256), nframes );
-    hipLaunchKernelGGL( ( hpel_expand_kernel<BD> ), g2, dim3( 256 ), 0, stream, dh, dv, dc, stride, fstride, width,
-                        height, pad );
+    // fused single pass; needs 4-pixel aligned rows (width + 64 covered by whole tiles of 4)
+    dim3 g( (width + 64 + HF_W - 1) / HF_W, (height + 64 + HF_H - 1) / HF_H, nframes );
+    hipLaunchKernelGGL( ( hpel_fused_kernel<BD> ), g, dim3( 256 ), 0, stream, src, dh, dv, dc, stride, fstride, width,
+                        height );
     return hipGetLastError();
 }
 
@@ -891,207 +657,6 @@ template <int BD> __device__ __forceinline__ uint32_t avg_packed( uint32_t a, ui
 {
     constexpr uint32_t keep = BD == 8 ? 0x7F7F7F7Fu : 0x7FFF7FFFu;
     return (a | b) - (((a ^ b) >> 1) & keep);
-}
-
-template <int BD, int OP, int IPIX>
-__global__ __launch_bounds__( 256 ) void subpel_cmp_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
-                                                            intptr_t fs, const typename PT<BD>::pixel *p0,
-                                                            const typename PT<BD>::pixel *p1,
-                                                            const typename PT<BD>::pixel *p2,
-                                                            const typename PT<BD>::pixel *p3, intptr_t rs,
-                                                            const int64_t *__restrict__ fenc_off,
-                                                            const int32_t *__restrict__ qxy, int n,
-                                                            int32_t *__restrict__ scores )
-{
-    using pixel = typename PT<BD>::pixel;
-    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
-    constexpr int NDW = W / PT<BD>::PPD;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if( i >= n )
-        return;
-    const int qx = qxy[2 * i], qy = qxy[2 * i + 1];
-    const int idx = ((qy & 3) << 2) + (qx & 3);
-    const intptr_t off = (intptr_t)(qy >> 2) * rs + (qx >> 2);
-    // plane selection by value keeps the pointers in the global address space
-    // (an indexed local array of pointers would turn every load into a flat load)
-    const int i0 = c_hpel_ref0[idx], i1 = c_hpel_ref1[idx];
-    const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((qy & 3) == 3) * rs;
-    const bool two = idx & 5;
-    const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((qx & 3) == 3);
-    const pixel *a = fenc + fenc_off[i];
-    int sum = 0;
-    uint32_t acc = 0;
-    // 4-row bands keep the register footprint at 2 x 4 x NDW dwords
-#pragma unroll
-    for( int ty = 0; ty < H; ty += 4 )
-    {
-        uint32_t fr[4][NDW], rr[4][NDW];
-#pragma unroll
-        for( int y = 0; y < 4; y++ )
-        {
-            load_packed<NDW>( a + (ty + y) * fs, fr[y] );
-            load_packed<NDW>( s1 + (ty + y) * rs, rr[y] );
-            if( two )
-            {
-                uint32_t t[NDW];
-                load_packed<NDW>( s2 + (ty + y) * rs, t );
-#pragma unroll
-                for( int k = 0; k < NDW; k++ )
-                    rr[y][k] = avg_packed<BD>( rr[y][k], t[k] );
-            }
-        }
-        if constexpr( OP == 0 )
-        {
-#pragma unroll
-            for( int y = 0; y < 4; y++ )
-#pragma unroll
-                for( int k = 0; k < NDW; k++ )
-                    acc = sadp<BD>( fr[y][k], rr[y][k], acc );
-        }
-        else if constexpr( W >= 8 )
-        {
-            // SATD in 8x4 packed pairs; every tile sum is even, so one final >> 1
-#pragma unroll
-            for( int tx = 0; tx < W; tx += 8 )
-            {
-                uint32_t fa[4][8 / PT<BD>::PPD], ra[4][8 / PT<BD>::PPD];
-#pragma unroll
-                for( int y = 0; y < 4; y++ )
-#pragma unroll
-                    for( int k = 0; k < 8 / PT<BD>::PPD; k++ )
-                    {
-                        fa[y][k] = fr[y][tx / PT<BD>::PPD + k];
-                        ra[y][k] = rr[y][tx / PT<BD>::PPD + k];
-                    }
-                acc += satd8x4_packed<BD>( fa, ra );
-            }
-        }
-        else
-        {
-            // SATD: (sum |H4 D H4^T|) >> 1 per 4x4 tile (pixel.c:265-332)
-#pragma unroll
-            for( int tx = 0; tx < W; tx += 4 )
-            {
-                int d[4][4];
-#pragma unroll
-                for( int y = 0; y < 4; y++ )
-                {
-#pragma unroll
-                    for( int x = 0; x < 4; x++ )
-                    {
-                        const int px = tx + x;
-                        d[y][x] = upix<BD>( fr[y][px / PT<BD>::PPD], px % PT<BD>::PPD ) -
-                                  upix<BD>( rr[y][px / PT<BD>::PPD], px % PT<BD>::PPD );
-                    }
-                    int t0 = d[y][0] + d[y][1], t1 = d[y][0] - d[y][1], t2 = d[y][2] + d[y][3], t3 = d[y][2] - d[y][3];
-                    d[y][0] = t0 + t2; d[y][2] = t0 - t2; d[y][1] = t1 + t3; d[y][3] = t1 - t3;
-                }
-                int s4 = 0;
-#pragma unroll
-                for( int x = 0; x < 4; x++ )
-                {
-                    int t0 = d[0][x] + d[1][x], t1 = d[0][x] - d[1][x], t2 = d[2][x] + d[3][x], t3 = d[2][x] - d[3][x];
-                    s4 += abs( t0 + t2 ) + abs( t0 - t2 ) + abs( t1 + t3 ) + abs( t1 - t3 );
-                }
-                sum += s4 >> 1;
-            }
-        }
-    }
-    if constexpr( OP == 0 )
-        sum = (int)acc;
-    else if constexpr( W >= 8 )
-        sum = (int)(acc >> 1);
-    scores[i] = sum;
-}
-
-// Variant 2: SATD candidates with one lane per block row (W 8 / 16, H 8 / 16): the H lanes
-// of a candidate hold its rows, so a wave's row loads of horizontally adjacent
-// candidates (the usual list order: consecutive blocks at one qpel phase) touch
-// few cache lines; the horizontal 4-point Hadamards run in packed 16-bit pairs
-// inside the lane, the vertical ones are DPP quad butterflies across the four
-// lanes of a 4-row band.  Same result as the per-lane kernel (sum of |coef| is
-// invariant to the coefficient order).
-template <int BD>
-__device__ __forceinline__ x264hip_short2 dpp_quad( x264hip_short2 v, int ctrl_sel )
-{
-    const int iv = __builtin_bit_cast( int, v );
-    const int r = ctrl_sel == 0 ? __builtin_amdgcn_update_dpp( 0, iv, 0xB1, 0xF, 0xF, false )    // lane ^ 1
-                                : __builtin_amdgcn_update_dpp( 0, iv, 0x4E, 0xF, 0xF, false );   // lane ^ 2
-    return __builtin_bit_cast( x264hip_short2, r );
-}
-
-template <int BD, int IPIX>
-__global__ __launch_bounds__( 256 ) void subpel_satd_rows_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
-                                                                  intptr_t fs, const typename PT<BD>::pixel *p0,
-                                                                  const typename PT<BD>::pixel *p1,
-                                                                  const typename PT<BD>::pixel *p2,
-                                                                  const typename PT<BD>::pixel *p3, intptr_t rs,
-                                                                  const int64_t *__restrict__ fenc_off,
-                                                                  const int32_t *__restrict__ qxy, int n,
-                                                                  int32_t *__restrict__ scores )
-{
-    using pixel = typename PT<BD>::pixel;
-    constexpr int W = pix_w( IPIX ), H = pix_h( IPIX );
-    constexpr int NDW = W / PT<BD>::PPD;
-    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t i = t / H;
-    const int r = (int)(t % H);
-    if( i >= n )
-        return;                                   // whole candidates only (H divides 64)
-    const int qx = qxy[2 * i], qy = qxy[2 * i + 1];
-    const int idx = ((qy & 3) << 2) + (qx & 3);
-    const intptr_t off = (intptr_t)(qy >> 2) * rs + (qx >> 2) + (intptr_t)r * rs;
-    const int i0 = c_hpel_ref0[idx], i1 = c_hpel_ref1[idx];
-    const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((qy & 3) == 3) * rs;
-    const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((qx & 3) == 3);
-    uint32_t fr[NDW], rr[NDW];
-    load_packed<NDW>( fenc + fenc_off[i] + (intptr_t)r * fs, fr );
-    load_packed<NDW>( s1, rr );
-    if( idx & 5 )
-    {
-        uint32_t tt[NDW];
-        load_packed<NDW>( s2, tt );
-#pragma unroll
-        for( int k = 0; k < NDW; k++ )
-            rr[k] = avg_packed<BD>( rr[k], tt[k] );
-    }
-    uint32_t acc = 0;
-#pragma unroll
-    for( int tx = 0; tx < W; tx += 8 )
-    {
-        uint32_t fa[8 / PT<BD>::PPD], ra[8 / PT<BD>::PPD];
-#pragma unroll
-        for( int k = 0; k < 8 / PT<BD>::PPD; k++ )
-        {
-            fa[k] = fr[tx / PT<BD>::PPD + k];
-            ra[k] = rr[tx / PT<BD>::PPD + k];
-        }
-        x264hip_short2 p[4];
-#pragma unroll
-        for( int x = 0; x < 4; x++ )
-            p[x] = pair_px<BD>( fa, x ) - pair_px<BD>( ra, x );
-        const x264hip_short2 t0 = p[0] + p[1], t1 = p[0] - p[1], t2 = p[2] + p[3], t3 = p[2] - p[3];
-        x264hip_short2 h[4] = { t0 + t2, t0 - t2, t1 + t3, t1 - t3 };
-        // vertical butterflies over the quad of rows: stage 1 lanes (0,1), stage 2 lanes (0,2)
-        const bool odd = r & 1, hi2 = r & 2;
-#pragma unroll
-        for( int k = 0; k < 4; k++ )
-        {
-            x264hip_short2 o = dpp_quad<BD>( h[k], 0 );
-            h[k] = odd ? o - h[k] : h[k] + o;
-            o = dpp_quad<BD>( h[k], 1 );
-            h[k] = hi2 ? o - h[k] : h[k] + o;
-            const x264hip_short2 m = __builtin_elementwise_max( h[k], (x264hip_short2)0 - h[k] );
-            acc = __builtin_amdgcn_udot2( __builtin_bit_cast( unsigned short __attribute__( ( ext_vector_type( 2 ) ) ), m ),
-                                          (unsigned short __attribute__( ( ext_vector_type( 2 ) ) ))1, acc, false );
-        }
-    }
-    // sum over the candidate's H lanes
-#pragma unroll
-    for( int m = 1; m < H; m <<= 1 )
-        acc += (uint32_t)__shfl_xor( (int)acc, m, H );
-    if( r == 0 )
-        scores[i] = (int)(acc >> 1);
 }
 
 // Row of NDW packed dwords at an arbitrary pixel address from dword-aligned loads:
@@ -1116,8 +681,7 @@ __device__ __forceinline__ void load_row_al( const void *p, uint32_t (&out)[NDW]
         out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
 }
 
-// Variants 3 / 5 (LD = 0 / 1): lane per candidate like variant 1, without its per-row
-// branch and realignment.  The second plane pointer equals the first when the
+// One lane per candidate (LD = 0 at 8 bit, 1 at 10 bit).  The second plane pointer equals the first when the
 // qpel phase needs one plane (avg(a, a) = a), so every band's rows are issued
 // as one burst of loads; rows are fetched with unaligned 4/8/16-byte global
 // loads (amdhsa runs with unaligned access enabled: no alignbyte) or, LD = 1,
@@ -1409,39 +973,16 @@ hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel 
 {
     if( n <= 0 )
         return hipSuccess;
-    const int ev = variant( V_SUBPEL );
-    // variant 2: one lane per block row (slower on the bench list: 0.25 vs 0.13 ms for
-    // 4.7 M 8x8 candidates, the per-candidate set-up is repeated in every row lane)
-    if( op == 2 && i_pixel <= 3 && ev == 2 )
-    {
-        const int h = pix_h( i_pixel );
-        const int64_t lanes = (int64_t)n * h;
-        dim3 g( (unsigned)((lanes + 255) / 256) );
-#define SR_CASE( I )                                                                                              case I: hipLaunchKernelGGL( ( subpel_satd_rows_kernel<BD, I> ), g, dim3( 256 ), 0, stream, fenc, fs,                                      planes[0], planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores ); break;
-        switch( i_pixel ) { SR_CASE( 0 ) SR_CASE( 1 ) SR_CASE( 2 ) SR_CASE( 3 ) }
-#undef SR_CASE
-        return hipGetLastError();
-    }
     dim3 blk( 256 ), g( (n + 255) / 256 );
-    // variants (tools/subpel_variants.py, 4.7 M 8x8 SATD candidates of bench.py's list):
-    // 1 = the first lane-per-candidate kernel (dwordx2 + dword loads, a per-row branch for
-    // the second plane; 0.129 ms 8 bit / 0.215 ms 10 bit), 3 = unaligned multi-dword row
-    // loads (0.101 / 0.193; default at 8 bit), 5 = dword-aligned row loads + alignbyte
-    // (0.115 / 0.186; default at 10 bit, and 0.178 against 0.276 for variant 3 when the
-    // list is block-major)
-    const int var = ev >= 0 ? ev : BD == 8 ? 3 : 5;
-    const bool v1 = var == 1;
+    // the row loads (tools/subpel_variants.py, 4.7 M 8x8 SATD candidates of bench.py's list):
+    // unaligned multi-dword loads at 8 bit (0.101 ms against 0.115 for dword-aligned loads +
+    // alignbyte, and 0.129 for the first dwordx2 + dword kernel), dword-aligned loads +
+    // alignbyte at 10 bit (0.186 against 0.193; 0.178 against 0.276 on block-major lists)
+    constexpr int LD = BD == 8 ? 0 : 1;
 #define SP_CASE( OP, I )                                                                                      \
     case I:                                                                                                   \
-        if( v1 )                                                                                              \
-            hipLaunchKernelGGL( ( subpel_cmp_kernel<BD, OP, I> ), g, blk, 0, stream, fenc, fs, planes[0],     \
-                                planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores );              \
-        else if( var == 3 )                                                                                   \
-            hipLaunchKernelGGL( ( subpel_cmp3_kernel<BD, OP, I, 0> ), g, blk, 0, stream, fenc, fs, planes[0], \
-                                planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores );              \
-        else                                                                                                  \
-            hipLaunchKernelGGL( ( subpel_cmp3_kernel<BD, OP, I, 1> ), g, blk, 0, stream, fenc, fs, planes[0], \
-                                planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores );              \
+        hipLaunchKernelGGL( ( subpel_cmp3_kernel<BD, OP, I, LD> ), g, blk, 0, stream, fenc, fs, planes[0],    \
+                            planes[1], planes[2], planes[3], rs, fenc_off, qxy, n, scores );                  \
         break;
     if( op == 0 )
     {
@@ -1547,106 +1088,12 @@ __global__ __launch_bounds__( 256 ) void lowres_kernel( const typename PT<BD>::p
     *(uint32_t *)(dc + o) = wc;
 }
 
-// 8 bit, one wave per output row for the core and one for the borders.  Core lane
-// k makes output columns 16k .. 16k+15 of all four planes: its three source rows
-// arrive as 33-pixel runs (two aligned 16-byte loads and a dword), v_perm gathers
-// the even / odd / next-even columns, and FILTER(a, b, c, d) = avg( avg( a, b ),
-// avg( c, d ) ) with avg = (x + y + 1) >> 1 per byte is v_lerp_u8 -- ten per output
-// dword-quad, bit-exact -- so each plane row leaves as one 16-byte store per lane.
-// The border wave takes the 32-pixel borders and the last core columns whose
-// source run would pass column W, four pixels per lane through the clamped
-// per-pixel form of lowres_kernel.
-__global__ __launch_bounds__( 128 ) void lowres16_kernel( const uint8_t *__restrict__ src, intptr_t stride,
-                                                          intptr_t fstride, int width, int height,
-                                                          uint8_t *__restrict__ d0, uint8_t *__restrict__ dh,
-                                                          uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
-                                                          intptr_t ds, intptr_t dfs )
-{
-    constexpr int PAD = 32;
-    const int wl = width / 2, hl = height / 2;
-    const int y = (int)blockIdx.y - PAD, f = blockIdx.z;
-    const int lane = threadIdx.x & 63;
-    const uint8_t *s = src + f * fstride;
-    const int yc = min( max( y, 0 ), hl - 1 );
-    const uint8_t *r0 = s + (intptr_t)(2 * yc) * stride;
-    const uint8_t *r1 = s + (intptr_t)min( 2 * yc + 1, height - 1 ) * stride;
-    const uint8_t *r2 = s + (intptr_t)min( 2 * yc + 2, height - 1 ) * stride;
-    const intptr_t orow = f * dfs + (intptr_t)y * ds;
-    const int ncore = wl >= 17 ? (wl - 17) / 16 + 1 : 0;     // groups with 16k + 16 <= wl - 1
-    if( threadIdx.x < 64 )
-    {
-        for( int k = lane; k < ncore; k += 64 )
-        {
-            const int xg = 16 * k;
-            uint32_t E[3][5], O[3][4];
-            const uint8_t *rr[3] = { r0, r1, r2 };
-#pragma unroll
-            for( int r = 0; r < 3; r++ )
-            {
-                const uint4 a = *(const uint4 *)(rr[r] + 2 * xg), b = *(const uint4 *)(rr[r] + 2 * xg + 16);
-                const uint32_t v[9] = { a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, *(const uint32_t *)(rr[r] + 2 * xg + 32) };
-#pragma unroll
-                for( int j = 0; j < 4; j++ )
-                {
-                    E[r][j] = __builtin_amdgcn_perm( v[2 * j + 1], v[2 * j], 0x06040200u );
-                    O[r][j] = __builtin_amdgcn_perm( v[2 * j + 1], v[2 * j], 0x07050301u );
-                }
-                E[r][4] = v[8];                                  // byte 0: source column 2*xg + 32
-            }
-            uint32_t w0[4], wh[4], wv[4], wc[4];
-#pragma unroll
-            for( int j = 0; j < 4; j++ )
-            {
-                auto avg = []( uint32_t p, uint32_t q ) { return __builtin_amdgcn_lerp( p, q, 0x01010101u ); };
-                const uint32_t x0 = __builtin_amdgcn_alignbyte( E[0][j + 1], E[0][j], 1 );
-                const uint32_t x1 = __builtin_amdgcn_alignbyte( E[1][j + 1], E[1][j], 1 );
-                const uint32_t x2 = __builtin_amdgcn_alignbyte( E[2][j + 1], E[2][j], 1 );
-                const uint32_t e01 = avg( E[0][j], E[1][j] ), o01 = avg( O[0][j], O[1][j] ), x01 = avg( x0, x1 );
-                const uint32_t e12 = avg( E[1][j], E[2][j] ), o12 = avg( O[1][j], O[2][j] ), x12 = avg( x1, x2 );
-                w0[j] = avg( e01, o01 );
-                wh[j] = avg( o01, x01 );
-                wv[j] = avg( e12, o12 );
-                wc[j] = avg( o12, x12 );
-            }
-            const intptr_t o = orow + xg;
-            *(uint4 *)(d0 + o) = make_uint4( w0[0], w0[1], w0[2], w0[3] );
-            *(uint4 *)(dh + o) = make_uint4( wh[0], wh[1], wh[2], wh[3] );
-            *(uint4 *)(dv + o) = make_uint4( wv[0], wv[1], wv[2], wv[3] );
-            *(uint4 *)(dc + o) = make_uint4( wc[0], wc[1], wc[2], wc[3] );
-        }
-        return;
-    }
-    // border wave: 8 groups of 4 on the left (x in [-32, 0)), the rest from 16 * ncore to wl + 32
-    const int nright = (wl + PAD - 16 * ncore) / 4;
-    for( int gi = lane; gi < 8 + nright; gi += 64 )
-    {
-        const int xg = gi < 8 ? -PAD + 4 * gi : 16 * ncore + 4 * (gi - 8);
-        uint32_t w0 = 0, wh = 0, wv = 0, wc = 0;
-#define FILTER( a, b, c, d ) ((((a + b + 1) >> 1) + ((c + d + 1) >> 1) + 1) >> 1)
-#pragma unroll
-        for( int j = 0; j < 4; j++ )
-        {
-            const int xc = min( max( xg + j, 0 ), wl - 1 );
-            const int c0 = 2 * xc, c1 = min( 2 * xc + 1, width - 1 ), c2 = min( 2 * xc + 2, width - 1 );
-            const int a0 = r0[c0], a1 = r0[c1], a2 = r0[c2];
-            const int b0 = r1[c0], b1 = r1[c1], b2 = r1[c2];
-            const int e0 = r2[c0], e1 = r2[c1], e2 = r2[c2];
-            w0 |= (uint32_t)FILTER( a0, b0, a1, b1 ) << (8 * j);
-            wh |= (uint32_t)FILTER( a1, b1, a2, b2 ) << (8 * j);
-            wv |= (uint32_t)FILTER( b0, e0, b1, e1 ) << (8 * j);
-            wc |= (uint32_t)FILTER( b1, e1, b2, e2 ) << (8 * j);
-        }
-#undef FILTER
-        const intptr_t o = orow + xg;
-        *(uint32_t *)(d0 + o) = w0;
-        *(uint32_t *)(dh + o) = wh;
-        *(uint32_t *)(dv + o) = wv;
-        *(uint32_t *)(dc + o) = wc;
-    }
-}
-
 // 8 bit, default: one single-wave workgroup per R output rows of all four planes.
-// Lane k < wl/16 makes output columns 16k .. 16k+15 as in lowres16_kernel; in the last
+// Lane k < wl/16 makes output columns 16k .. 16k+15: its three source rows arrive as
+// 33-pixel runs (two aligned 16-byte loads and a dword), v_perm gathers the even / odd /
+// next-even columns, and FILTER(a, b, c, d) = avg( avg( a, b ), avg( c, d ) ) with
+// avg = (x + y + 1) >> 1 per byte is v_lerp_u8 -- ten per output dword-quad, bit-exact --
+// so each plane row leaves as one 16-byte store per lane.  In the last
 // group the source column 2*16k+32 the run ends on would be column W, which the
 // reference duplicates from W-1 (mc.c:465-468), so that one byte is taken from W-1.
 // The wl % 16 columns left over (widths that are not a multiple of 32) go to the next
@@ -1791,20 +1238,6 @@ __global__ __launch_bounds__( 64 ) void lowres_rows_kernel( const uint8_t *__res
     lowres_rows_body<R, NT>( src, stride, fstride, width, height, d0, dh, dv, dc, ds, dfs, (int)B.y, (int)B.z );
 }
 
-// persistent form (X264HIP_LOWRES_VARIANT=5): a resident grid walks the (row block, frame)
-// units grid-stride
-template <int R>
-__global__ __launch_bounds__( 64 ) void lowres_rows_persist_kernel( const uint8_t *__restrict__ src, intptr_t stride,
-                                                                    intptr_t fstride, int width, int height,
-                                                                    uint8_t *__restrict__ d0, uint8_t *__restrict__ dh,
-                                                                    uint8_t *__restrict__ dv, uint8_t *__restrict__ dc,
-                                                                    intptr_t ds, intptr_t dfs, uint32_t gy, uint32_t units )
-{
-    for( uint32_t u = blockIdx.x; u < units; u += gridDim.x )
-        lowres_rows_body<R>( src, stride, fstride, width, height, d0, dh, dv, dc, ds, dfs, (int)(u % gy),
-                             (int)(u / gy) );
-}
-
 template <int BD>
 hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t stride, intptr_t fstride, int width,
                                      int height, int nframes, typename PT<BD>::pixel *const dst[4], intptr_t ds,
@@ -1815,41 +1248,16 @@ hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t
     const int wl = width / 2, hl = height / 2;
     if constexpr( BD == 8 )
     {
-        // 16-pixel lanes with 16-byte loads and stores: needs 16-byte aligned rows and a
-        // width of whole macroblocks (X264HIP_LOWRES_VARIANT=1 selects the dword kernel,
-        // 2 the one-row-per-workgroup kernel with its separate border wave)
-        const int ev = variant( V_LOWRES );
+        // 16-pixel lanes with 16-byte loads and stores, two output rows per wave (one / four
+        // rows, the one-row-per-workgroup kernel and a persistent grid were all slower,
+        // profiles/r02h_lowres_variants*.json, r03i_stream_var.json): needs 16-byte aligned
+        // rows and a width of whole macroblocks; else the dword kernel below
         const uintptr_t al = (uintptr_t)src | (uintptr_t)stride | (uintptr_t)fstride | (uintptr_t)dst[0] |
                              (uintptr_t)dst[1] | (uintptr_t)dst[2] | (uintptr_t)dst[3] | (uintptr_t)ds | (uintptr_t)dfs;
-        if( ev != 1 && ev != 2 && !(al & 15) && !(width & 15) )
+        if( !(al & 15) && !(width & 15) )
         {
-            // X264HIP_LOWRES_VARIANT = 3 / 4: one / four output rows per wave (default two)
-            const int R = ev == 3 ? 1 : ev == 4 ? 4 : 2;
-            dim3 gr( 1, (unsigned)((hl + 64 + R - 1) / R), (unsigned)nframes );
-            if( ev == 5 )
-            {
-                static int resident = 0;
-                if( !resident )
-                {
-                    int per_cu = 0, dev = 0, ncu = 0;
-                    (void)hipGetDevice( &dev );
-                    (void)hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, dev );
-                    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor( &per_cu, lowres_rows_persist_kernel<2>, 64, 0 );
-                    resident = std::max( 1, per_cu ) * std::max( 1, ncu );
-                }
-                const uint32_t units = gr.y * gr.z;
-                hipLaunchKernelGGL( lowres_rows_persist_kernel<2>, dim3( std::min<uint32_t>( units, (uint32_t)resident ) ),
-                                    dim3( 64 ), 0, st, src, stride, fstride, width, height, dst[0], dst[1], dst[2],
-                                    dst[3], ds, dfs, gr.y, units );
-                return hipGetLastError();
-            }
-            if( R == 1 )
-                hipLaunchKernelGGL( lowres_rows_kernel<1>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
-                                    dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) == 1 );
-            else if( R == 4 )
-                hipLaunchKernelGGL( lowres_rows_kernel<4>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
-                                    dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) == 1 );
-            else if( stream_nt() )
+            dim3 gr( 1, (unsigned)((hl + 64 + 1) / 2), (unsigned)nframes );
+            if( stream_nt() )
                 // nontemporal stores + XCD-contiguous row blocks (which lost with plain stores):
                 // 64 frames 0.0789 -> 0.0510 ms, 16 frames 0.0165 -> 0.0145 ms
                 // (profiles/r03r_stream_nt.json)
@@ -1858,13 +1266,6 @@ hipError_t launch_frame_init_lowres( const typename PT<BD>::pixel *src, intptr_t
             else
                 hipLaunchKernelGGL( lowres_rows_kernel<2>, gr, dim3( 64 ), 0, st, src, stride, fstride, width, height,
                                     dst[0], dst[1], dst[2], dst[3], ds, dfs, variant( V_STREAM_XCD ) == 1 );
-            return hipGetLastError();
-        }
-        if( ev == 2 && !(al & 15) && !(width & 15) )
-        {
-            dim3 g16( 1, (unsigned)(hl + 64), (unsigned)nframes );
-            hipLaunchKernelGGL( lowres16_kernel, g16, dim3( 128 ), 0, st, src, stride, fstride, width, height, dst[0],
-                                dst[1], dst[2], dst[3], ds, dfs );
             return hipGetLastError();
         }
     }

@@ -1,17 +1,27 @@
 // Exhaustive integer-pel 16x16 SAD search tables (the candidate set of the
 // reference's ESA/plain exhaustive search, encoder/me.c:618-631, before the
-// mv-cost term COST_MV adds, me.c:63-70).
+// mv-cost term COST_MV adds, me.c:63-70), the fused ESA decision and the decision
+// over a table.
 //
-// Layout of the work: one lane owns one candidate COLUMN (mx) of one
-// macroblock's (2R+1)x(2R+1) window; lanes are dealt MB-major, so the 64 lanes
-// of a wave cover ~2 MBs and every lane does identical work (no idle lanes for
-// any R).  The lane walks the 2R+16 window rows top to bottom, fetching each
-// 16-pixel ref row ONCE (aligned dwords + v_alignbyte_b32) and folding it into
-// the (up to 16) candidates my whose 16-row footprint covers that row:
+// Table geometry (hipcommon.h full_pitch / cen_cols / cen_pitch, include/x264hip.h):
+//  * a full-search table (me_search_full) is the (2R+1)^2 square around mv 0, rows at
+//    pitch align4(2R+1);
+//  * a centred table (me_search_centred, and the window the fused ESA decision keys) is
+//    me.c's ESA window around a predictor (bmx, bmy): 2R+1 rows, and the columns the
+//    window can reach -- [bmx - R, bmx + R + 2] (the width rounding (max_x - min_x + 3) & ~3
+//    of me.c:626 ends up to two columns past max_x) plus the origin's alignment down to a
+//    dword (3 pixels at 8 bit, 1 at 10 bit): 2R+6 columns at 8 bit, 2R+4 at 10 bit.  So a
+//    template of radius me_range holds every candidate me.c evaluates, and nothing else
+//    but the slack columns.
+//
+// Layout of the work (generic kernel, the unaligned-plane fallback): one lane owns one
+// candidate COLUMN (mx) of one macroblock's window and walks the 2R+16 ref rows top to
+// bottom, fetching each 16-pixel ref row ONCE and folding it into the (up to 16)
+// candidates my whose 16-row footprint covers that row:
 //   acc[my] += sad(fenc row (y - my), ref row y)      (v_sad_u8 / v_sad_u16)
-// so ref traffic is 1/16 of a per-candidate loop and the realignment cost is
-// amortised over 16 candidates.  fenc (16 rows) stays in VGPRs for the whole
-// lane lifetime.  Candidate my finishes at row my+15 and is stored then.
+// fenc (16 rows) stays in VGPRs for the whole lane lifetime.  Candidate my finishes at
+// row my+15 and is stored then.  The grouped kernels below (four columns per lane with
+// v_qsad_pk_u16_u8 at 8 bit, column pairs with v_sad_u16 at 10 bit) are the defaults.
 #include "hipcommon.h"
 #include <mutex>
 #include <string.h>
@@ -23,13 +33,12 @@ namespace x264hip {
 
 // one window row Y (compile-time): fold ref row Y into every candidate whose
 // footprint covers it; candidate c uses fenc row Y - c.
-template <int BD, int R, int Y>
+template <int BD, int R, int P, int Y>
 __device__ __forceinline__ void me_row( const typename PT<BD>::pixel *rb, intptr_t rs,
                                         const uint32_t (&F)[16][16 / PT<BD>::PPD], uint32_t (&acc)[16],
                                         typename PT<BD>::sadt *out )
 {
     constexpr int NDW = 16 / PT<BD>::PPD;
-    constexpr int W = 2 * R + 1;
     constexpr int C0 = Y - 15 > 0 ? Y - 15 : 0;
     constexpr int C1 = Y < 2 * R ? Y : 2 * R;
     uint32_t rr[NDW];
@@ -43,31 +52,31 @@ __device__ __forceinline__ void me_row( const typename PT<BD>::pixel *rb, intptr
         for( int k = 0; k < NDW; k++ )
             a = sadp<BD>( F[r][k], rr[k], a );
         if( r == 15 )
-            out[c * ((W + 3) & ~3)] = (typename PT<BD>::sadt)a;
+            out[c * P] = (typename PT<BD>::sadt)a;
         else
             acc[c & 15] = a;
     }
 }
 
-template <int BD, int R, int... Ys>
+template <int BD, int R, int P, int... Ys>
 __device__ __forceinline__ void me_rows( const typename PT<BD>::pixel *rb, intptr_t rs,
                                          const uint32_t (&F)[16][16 / PT<BD>::PPD], uint32_t (&acc)[16],
                                          typename PT<BD>::sadt *out, std::integer_sequence<int, Ys...> )
 {
-    ( me_row<BD, R, Ys>( rb, rs, F, acc, out ), ... );
+    ( me_row<BD, R, P, Ys>( rb, rs, F, acc, out ), ... );
 }
 
-// Window origin of one MB (me_search_centred; the plain search is the
-// special case centre = (0, 0)): (cx, cy) - R, clamped so that every pixel
-// any variant fetches lies in the 32-pixel padded plane (x264's PADH = PADV =
-// 32, common/frame.h:32-33), then aligned down to 4 (8 bit) / 2 (10 bit)
-// pixels so the grouped variants keep dword-aligned rows.  For centre (0, 0)
-// and R <= 24 neither step changes anything.  Returned relative to the MB.
-template <int BD, int R>
+// Window origin of one MB (me_search_centred; the plain search is the special case
+// centre = (0, 0)): (cx, cy) - R, clamped so that every pixel a kernel fetches lies in the
+// 32-pixel padded plane (x264's PADH = PADV = 32, common/frame.h:32-33) -- P columns wide,
+// 2R+1 rows -- then aligned down to 4 (8 bit) / 2 (10 bit) pixels so the grouped kernels
+// keep dword-aligned rows.  For centre (0, 0) and R <= 24 neither step changes anything.
+// Returned relative to the MB.
+template <int BD, int R, int P>
 __device__ __forceinline__ void me_window( const int16_t *__restrict__ centre, int64_t mb, int mbx, int mby, int mbw,
                                            int mbh, int &ox, int &oy )
 {
-    constexpr int P = (2 * R + 1 + 3) & ~3, AL = BD == 8 ? 4 : 2;
+    constexpr int AL = BD == 8 ? 4 : 2;
     int ax = 16 * mbx - R, ay = 16 * mby - R;
     if( centre )
     {
@@ -81,7 +90,9 @@ __device__ __forceinline__ void me_window( const int16_t *__restrict__ centre, i
     oy = ay - 16 * mby;
 }
 
-template <int BD, int R>
+// generic kernel: one lane per table column (NCOL columns, pitch align4(NCOL)); serves
+// planes whose rows or strides are not dword aligned
+template <int BD, int R, int NCOL>
 __global__ __launch_bounds__( 256 ) void me_full_sad16_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
                                                                intptr_t fs, intptr_t ffs,
                                                                const typename PT<BD>::pixel *__restrict__ ref,
@@ -90,14 +101,14 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_kernel( const typename PT
                                                                const int16_t *__restrict__ centre,
                                                                int16_t *__restrict__ origin )
 {
-    constexpr int W = 2 * R + 1;
+    constexpr int W = 2 * R + 1, P = al4( NCOL );
     constexpr int NDW = 16 / PT<BD>::PPD;   // dwords per 16-pixel row
     const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)nframes * mbh * mbw * W;
+    const int64_t total = (int64_t)nframes * mbh * mbw * NCOL;
     if( slot >= total )
         return;
-    const int col = (int)(slot % W);
-    const int64_t mb = slot / W;
+    const int col = (int)(slot % NCOL);
+    const int64_t mb = slot / NCOL;
     const int mbx = (int)(mb % mbw);
     const int64_t t = mb / mbw;
     const int mby = (int)(t % mbh);
@@ -111,282 +122,33 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_kernel( const typename PT
         load_packed<NDW>( fe + r * fs, F[r] );
 
     int ox, oy;
-    me_window<BD, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    me_window<BD, R, P>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
     if( origin && col == 0 )
     {
         origin[2 * mb] = (int16_t)ox;
         origin[2 * mb + 1] = (int16_t)oy;
     }
     const typename PT<BD>::pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox + col;
-    typename PT<BD>::sadt *out = table + mb * (W * ((W + 3) & ~3)) + col;
+    typename PT<BD>::sadt *out = table + mb * (W * P) + col;
 
     uint32_t acc[16];
-    me_rows<BD, R>( rb, rs, F, acc, out, std::make_integer_sequence<int, 2 * R + 16>{} );
+    me_rows<BD, R, P>( rb, rs, F, acc, out, std::make_integer_sequence<int, 2 * R + 16>{} );
 }
 
-
-// ---------------------------------------------------------------------------
-// Variant 2: two lanes per candidate column.  Lane h (0/1) keeps only fenc rows
-// 8h..8h+7 in VGPRs and walks ref rows 8h + (0 .. 2R+7), so both lanes of a
-// column finish candidate my at the same step; their partial sums meet through
-// one DPP quad-perm add.  Halving the resident fenc halves the VGPR footprint
-// and lets the 10-bit path keep its fenc rows in registers too.
-// Requirements (checked by the launcher, else variant 1 runs): fenc base and
-// both strides are dword multiples, so a lane's byte shift is the same on
-// every row and rows are plain dword loads (the 5th dword of a row is read
-// unconditionally: it lies inside the plane padding, range + 4 <= PAD).
-template <int BD, int R, int Y>
-__device__ __forceinline__ void me_row2( const uint32_t *__restrict__ rbase, int rs_dw, uint32_t sh,
-                                         const uint32_t (&F)[8][16 / PT<BD>::PPD], uint32_t (&acc)[8],
-                                         typename PT<BD>::sadt *out )
-{
-    constexpr int NDW = 16 / PT<BD>::PPD;
-    constexpr int W = 2 * R + 1;
-    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
-    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
-    const uint32_t *row = rbase + Y * rs_dw;
-    uint32_t w[NDW + 1], rr[NDW];
-#pragma unroll
-    for( int k = 0; k <= NDW; k++ )
-        w[k] = row[k];
-#pragma unroll
-    for( int k = 0; k < NDW; k++ )
-        rr[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], sh );
-#pragma unroll
-    for( int c = C0; c <= C1; c++ )
-    {
-        const int r = Y - c;
-        uint32_t a = r == 0 ? 0u : acc[c & 7];
-#pragma unroll
-        for( int k = 0; k < NDW; k++ )
-            a = sadp<BD>( F[r][k], rr[k], a );
-        if( r == 7 )
-        {
-            // partner lane (lane ^ 1) holds the other 8 rows: quad_perm [1,0,3,2];
-            // both lanes store the same total to the same address (no branch)
-            uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a, 0xB1, 0xF, 0xF, false );
-            out[c * ((W + 3) & ~3)] = (typename PT<BD>::sadt)(a + other);
-        }
-        else
-            acc[c & 7] = a;
-    }
-}
-
-template <int BD, int R, int... Ys>
-__device__ __forceinline__ void me_rows2( const uint32_t *__restrict__ rbase, int rs_dw, uint32_t sh,
-                                          const uint32_t (&F)[8][16 / PT<BD>::PPD], uint32_t (&acc)[8],
-                                          typename PT<BD>::sadt *out, std::integer_sequence<int, Ys...> )
-{
-    ( me_row2<BD, R, Ys>( rbase, rs_dw, sh, F, acc, out ), ... );
-}
-
-template <int BD, int R>
-__global__ __launch_bounds__( 256 ) void me_full_sad16_v2_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
-                                                                  intptr_t fs, intptr_t ffs,
-                                                                  const typename PT<BD>::pixel *__restrict__ ref,
-                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                                                                  int nframes, typename PT<BD>::sadt *__restrict__ table,
-                                                                  const int16_t *__restrict__ centre,
-                                                                  int16_t *__restrict__ origin )
-{
-    using pixel = typename PT<BD>::pixel;
-    constexpr int W = 2 * R + 1;
-    constexpr int NDW = 16 / PT<BD>::PPD;
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * W);
-    if( slot >= total )
-        return;                                 // pairs never straddle: 2W is even
-    const int h = (int)(slot & 1);
-    const int col = (int)((slot >> 1) % W);
-    const int64_t mb = slot / (2 * W);
-    const int mbx = (int)(mb % mbw);
-    const int64_t t = mb / mbw;
-    const int mby = (int)(t % mbh);
-    const int64_t f = t / mbh;
-
-    uint32_t F[8][NDW];
-    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
-    const int fs_dw = (int)(fs * sizeof(pixel) / 4);
-#pragma unroll
-    for( int r = 0; r < 8; r++ )
-#pragma unroll
-        for( int k = 0; k < NDW; k++ )
-            F[r][k] = fe[r * fs_dw + k];
-
-    int ox, oy;
-    me_window<BD, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
-    if( origin && col == 0 && h == 0 )
-    {
-        origin[2 * mb] = (int16_t)ox;
-        origin[2 * mb + 1] = (int16_t)oy;
-    }
-    const pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + col;
-    const uint32_t sh = (uint32_t)((uintptr_t)rb & 3);
-    const uint32_t *rbase = (const uint32_t *)((const char *)rb - sh);
-    typename PT<BD>::sadt *out = table + mb * (W * ((W + 3) & ~3)) + col;
-    uint32_t acc[8];
-    me_rows2<BD, R>( rbase, (int)(rs * sizeof(pixel) / 4), sh, F, acc, out,
-                     std::make_integer_sequence<int, 2 * R + 8>{} );
-}
-
-// ---------------------------------------------------------------------------
-// Variant 3 (8 bit): four candidate columns per lane with v_qsad_pk_u16_u8.
-// One qsad compares a fenc dword with the four byte-shifted dwords of an 8-byte
-// ref window and accumulates four packed u16 SADs, so a lane covers columns
-// 4j..4j+3 with no realignment at all; as in variant 2 the lane pair (h = 0/1)
-// splits the 16 fenc rows and meets through a DPP add (u16 halves cannot carry:
-// each half-sum <= 8*16*255 = 32640).  Per ref row a lane issues 2 loads for
-// 4 columns x 8 candidates, 4x fewer than variant 1.  Rows of the table have
-// pitch align4(2R+1); the 0..3 trailing entries hold the SADs of mx = R+1..
 typedef uint64_t u64x2a4 __attribute__( ( ext_vector_type( 2 ), aligned( 4 ) ) );
 
-// `sink( c, lo, hi )` receives candidate row c's four finished SADs (packed u16 pairs:
-// columns 4j, 4j+1 in lo, 4j+2, 4j+3 in hi), identical in both lanes of the pair
-template <int R, int Y, class Sink>
-__device__ __forceinline__ void me_row3( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
-                                         uint64_t (&acc)[8], Sink &sink )
-{
-    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
-    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
-    const uint32_t *row = rbase + Y * rs_dw;
-    // two overlapping 16-byte loads give the four 8-byte windows as aligned
-    // register pairs (w0w1, w2w3 | w1w2, w3w4): no register shuffling
-    const u64x2a4 e = *(const u64x2a4 *)row;
-    const u64x2a4 o = *(const u64x2a4 *)(row + 1);
-    const uint64_t win[4] = { e[0], o[0], e[1], o[1] };
-#pragma unroll
-    for( int c = C0; c <= C1; c++ )
-    {
-        const int r = Y - c;
-        uint64_t a = r == 0 ? 0ull : acc[c & 7];
-#pragma unroll
-        for( int k = 0; k < 4; k++ )
-            a = __builtin_amdgcn_qsad_pk_u16_u8( win[k], F[r][k], a );
-        if( r == 7 )
-        {
-            uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
-            lo += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)lo, 0xB1, 0xF, 0xF, false );
-            hi += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)hi, 0xB1, 0xF, 0xF, false );
-            sink( c, lo, hi );
-        }
-        else
-            acc[c & 7] = a;
-    }
-}
-
-template <int R, class Sink, int... Ys>
-__device__ __forceinline__ void me_rows3( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
-                                          uint64_t (&acc)[8], Sink &sink, std::integer_sequence<int, Ys...> )
-{
-    ( me_row3<R, Ys>( rbase, rs_dw, F, acc, sink ), ... );
-}
-
-// the same row step with the next ref row's two loads issued before this row's qsads
-// (one row of lead: the loads' latency is covered by the wave's own 32 qsads as well
-// as by the other waves of the SIMD)
-template <int R, int L, int Y, class Sink>
-__device__ __forceinline__ void me_row3p( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
-                                          uint64_t (&acc)[8], Sink &sink, u64x2a4 (&e)[L], u64x2a4 (&o)[L] )
-{
-    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
-    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
-    const uint64_t win[4] = { e[Y % L][0], o[Y % L][0], e[Y % L][1], o[Y % L][1] };
-    if constexpr( Y + L < 2 * R + 8 )
-    {
-        const uint32_t *row = rbase + (Y + L) * rs_dw;
-        e[Y % L] = *(const u64x2a4 *)row;
-        o[Y % L] = *(const u64x2a4 *)(row + 1);
-    }
-#pragma unroll
-    for( int c = C0; c <= C1; c++ )
-    {
-        const int r = Y - c;
-        uint64_t a = r == 0 ? 0ull : acc[c & 7];
-#pragma unroll
-        for( int k = 0; k < 4; k++ )
-            a = __builtin_amdgcn_qsad_pk_u16_u8( win[k], F[r][k], a );
-        if( r == 7 )
-        {
-            uint32_t lo = (uint32_t)a, hi = (uint32_t)(a >> 32);
-            lo += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)lo, 0xB1, 0xF, 0xF, false );
-            hi += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)hi, 0xB1, 0xF, 0xF, false );
-            sink( c, lo, hi );
-        }
-        else
-            acc[c & 7] = a;
-    }
-    // keep the scheduler from hoisting later rows' loads up here (it clusters them all
-    // at the top otherwise: 126 VGPRs, 4 waves)
-    __builtin_amdgcn_sched_barrier( 0 );
-}
-
-template <int R, int L, class Sink, int... Ys>
-__device__ __forceinline__ void me_rows3p( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
-                                           uint64_t (&acc)[8], Sink &sink, std::integer_sequence<int, Ys...> )
-{
-    u64x2a4 e[L], o[L];
-#pragma unroll
-    for( int k = 0; k < L; k++ )
-    {
-        e[k] = *(const u64x2a4 *)(rbase + k * rs_dw);
-        o[k] = *(const u64x2a4 *)(rbase + k * rs_dw + 1);
-    }
-    ( me_row3p<R, L, Ys>( rbase, rs_dw, F, acc, sink, e, o ), ... );
-}
-
-template <int R, int PF = 0>
-__global__ __launch_bounds__( 256 ) void me_full_sad16_v3_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
-                                                                  intptr_t ffs, const uint8_t *__restrict__ ref,
-                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                                                                  int nframes, uint16_t *__restrict__ table,
-                                                                  const int16_t *__restrict__ centre,
-                                                                  int16_t *__restrict__ origin )
-{
-    constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
-    constexpr int P = 4 * G;                    // table row pitch
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
-    if( slot >= total )
-        return;
-    const int h = (int)(slot & 1);
-    const int grp = (int)((slot >> 1) % G);
-    const int64_t mb = slot / (2 * G);
-    const int mbx = (int)(mb % mbw);
-    const int64_t t = mb / mbw;
-    const int mby = (int)(t % mbh);
-    const int64_t f = t / mbh;
-
-    uint32_t F[8][4];
-    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
-    const int fs_dw = (int)(fs / 4);
-#pragma unroll
-    for( int r = 0; r < 8; r++ )
-#pragma unroll
-        for( int k = 0; k < 4; k++ )
-            F[r][k] = fe[r * fs_dw + k];
-    int ox, oy;
-    me_window<8, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
-    if( origin && grp == 0 && h == 0 )
-    {
-        origin[2 * mb] = (int16_t)ox;
-        origin[2 * mb + 1] = (int16_t)oy;
-    }
-    const uint32_t *rbase =
-        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 4 * grp);
-    uint64_t *out = (uint64_t *)(table + mb * ((2 * R + 1) * P) + 4 * grp);
-    auto store = [out]( int c, uint32_t lo, uint32_t hi ) { out[c * (P / 4)] = ((uint64_t)hi << 32) | lo; };
-    uint64_t acc[8];
-    if constexpr( PF > 0 )
-        me_rows3p<R, PF>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
-    else
-        me_rows3<R>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
-}
-
+// rows of ref-load lead in the grouped kernels: the loads of ref rows Y+1, Y+2 are issued
+// before row Y's SADs (16 1080p pairs, R 16: 8 bit 0.312 -> 0.300 ms from no lead to two
+// rows, 10 bit 0.653 -> 0.617 ms; a third row gained nothing, profiles of round 1-2)
+constexpr int ME_LEAD = 2;
 
 // ---------------------------------------------------------------------------
-// Variant 7 (8 bit): variant 3 with all 16 fenc rows in one lane (no lane pair, no DPP
-// half-sum): up to 16 candidate rows open per ref row (64 v_qsad between two row loads),
-// 2R+16 ref rows per lane, and the lane stores its own four columns.
+// 8 bit: one lane owns four adjacent candidate columns 4g..4g+3 and all 16 fenc rows;
+// per ref row it issues two overlapping 16-byte loads (the four 8-byte windows arrive as
+// aligned register pairs, no realignment) and folds the row into the <= 16 candidate rows
+// whose footprint covers it, 16 byte absdiffs per v_qsad_pk_u16_u8 (a column's packed u16
+// sum cannot carry: 16*16*255 < 2^16).  `sink( c, lo, hi )` receives candidate row c's four
+// finished SADs as packed u16 pairs (columns 4g, 4g+1 in lo, 4g+2, 4g+3 in hi).
 template <int R, int L, int Y, class Sink>
 __device__ __forceinline__ void me_row7( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[16][4],
                                          uint64_t (&acc)[16], Sink &sink, u64x2a4 (&e)[L], u64x2a4 (&o)[L] )
@@ -413,6 +175,7 @@ __device__ __forceinline__ void me_row7( const uint32_t *__restrict__ rbase, int
         else
             acc[c & 15] = a;
     }
+    // keep the scheduler from hoisting later rows' loads up here
     __builtin_amdgcn_sched_barrier( 0 );
 }
 
@@ -430,7 +193,8 @@ __device__ __forceinline__ void me_rows7( const uint32_t *__restrict__ rbase, in
     ( me_row7<R, L, Ys>( rbase, rs_dw, F, acc, sink, e, o ), ... );
 }
 
-template <int R, int L>
+// one lane per column group of G (full: align4(2R+1) / 4, centred: cen_pitch / 4)
+template <int R, int G>
 __global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                   intptr_t ffs, const uint8_t *__restrict__ ref,
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -438,7 +202,6 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t 
                                                                   const int16_t *__restrict__ centre,
                                                                   int16_t *__restrict__ origin, int xcd )
 {
-    constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
     constexpr int P = 4 * G;                    // table row pitch
     // 32-bit index decomposition (the launcher keeps the lane count below 2^32): the
     // int64 divisions by mbw / mbh were ~150 VALU instructions of the prologue
@@ -461,7 +224,7 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t 
         for( int k = 0; k < 4; k++ )
             F[r][k] = fe[r * fs_dw + k];
     int ox, oy;
-    me_window<8, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    me_window<8, R, P>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
     if( origin && grp == 0 )
     {
         origin[2 * mb] = (int16_t)ox;
@@ -472,7 +235,7 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t 
     uint64_t *out = (uint64_t *)(table + mb * ((2 * R + 1) * P) + 4 * grp);
     auto store = [out]( int c, uint32_t lo, uint32_t hi ) { out[c * (P / 4)] = ((uint64_t)hi << 32) | lo; };
     uint64_t acc[16];
-    me_rows7<R, L>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 16>{} );
+    me_rows7<R, ME_LEAD>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 16>{} );
 }
 
 // ---------------------------------------------------------------------------
@@ -481,11 +244,11 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v7_kernel( const uint8_t 
 // one XCD's L2 (FETCH_SIZE 160 -> 69 MB per 16 1080p pairs, profiles/r03c_*)
 static int me_xcd() { return variant( V_ME_XCD ) != 0; }
 
-// 8x8 quadrant tables (8 bit): the variant-7 lane (four candidate columns, all 16 fenc
-// rows, each ref row loaded once) with separate left (fenc dwords 0-1) and right (dwords
-// 2-3) accumulators, restarted at fenc row 8: a candidate row's top quadrants leave at fenc
-// row 7, its bottom ones at row 15.  The same 256 absdiffs per candidate as the 16x16
-// table -- whose SAD is the sum of the four -- and 16x8 / 8x16 SADs are pair sums.
+// 8x8 quadrant tables (8 bit): the four-column lane with separate left (fenc dwords 0-1)
+// and right (dwords 2-3) accumulators, restarted at fenc row 8: a candidate row's top
+// quadrants leave at fenc row 7, its bottom ones at row 15.  The same 256 absdiffs per
+// candidate as the 16x16 table -- whose SAD is the sum of the four -- and 16x8 / 8x16
+// SADs are pair sums.
 template <int R, int L, int Y, class Sink>
 __device__ __forceinline__ void me_row8q( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[16][4],
                                           uint64_t (&al)[16], uint64_t (&ar)[16], Sink &sink, u64x2a4 (&e)[L],
@@ -536,14 +299,13 @@ __device__ __forceinline__ void me_rows8q( const uint32_t *__restrict__ rbase, i
 }
 
 // table8[mb][q][2R+1][P]: q = 0 top-left, 1 top-right, 2 bottom-left, 3 bottom-right
-template <int R, int L>
+template <int R>
 __global__ __launch_bounds__( 256 ) void me_full_sad8q_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                intptr_t ffs, const uint8_t *__restrict__ ref,
                                                                intptr_t rs, intptr_t rfs, int mbw, int mbh,
                                                                int nframes, uint16_t *__restrict__ table8, int xcd )
 {
-    constexpr int G = (2 * R + 1 + 3) / 4;
-    constexpr int P = 4 * G;
+    constexpr int P = full_pitch( R ), G = P / 4;
     const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
     const uint32_t slot = blk * blockDim.x + threadIdx.x;
     if( slot >= (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw * (uint32_t)G )
@@ -568,92 +330,16 @@ __global__ __launch_bounds__( 256 ) void me_full_sad8q_kernel( const uint8_t *__
         out[((2 * half + 1) * (2 * R + 1) + c) * (P / 4)] = b;
     };
     uint64_t al[16], ar[16];
-    me_rows8q<R, L>( rbase, (int)(rs / 4), F, al, ar, store, std::make_integer_sequence<int, 2 * R + 16>{} );
+    me_rows8q<R, ME_LEAD>( rbase, (int)(rs / 4), F, al, ar, store, std::make_integer_sequence<int, 2 * R + 16>{} );
 }
-
-template <int BD>
-hipError_t launch_me_full8( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
-                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                            int nframes, int range, uint16_t *table8, hipStream_t stream )
-{
-    if constexpr( BD != 8 )
-        return hipErrorInvalidValue;
-    else
-    {
-        const int64_t lanes = (int64_t)nframes * mbh * mbw * ((2 * range + 1 + 3) / 4);
-        if( lanes <= 0 )
-            return hipSuccess;
-        if( lanes >= (1ll << 32) || (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)fs | (uintptr_t)rs) & 3) )
-            return hipErrorInvalidValue;
-        dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
-        const int xcd = me_xcd();
-        switch( range )
-        {
-#define ME8_CASE( R )                                                                                           \
-            case R:                                                                                             \
-                hipLaunchKernelGGL( ( me_full_sad8q_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
-                                    mbw, mbh, nframes, table8, xcd );                                           \
-                break;
-            ME8_CASE( 4 ) ME8_CASE( 8 ) ME8_CASE( 16 ) ME8_CASE( 24 )
-#undef ME8_CASE
-            default: return hipErrorInvalidValue;
-        }
-        return hipGetLastError();
-    }
-}
-template hipError_t launch_me_full8<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
-                                        int, int, int, uint16_t *, hipStream_t );
-template hipError_t launch_me_full8<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
-                                         int, int, int, int, uint16_t *, hipStream_t );
 
 // ---------------------------------------------------------------------------
-// Variant 5 (10 bit, default): the variant-3 layout for 16-bit pixels.  A lane
-// owns two adjacent candidate columns (2g, 2g+1; the first is dword aligned for
-// even R) and half of the fenc rows; per ref row it loads 9 dwords once, forms
-// the odd column's dwords with one v_alignbyte_b32 each, and folds the row into
-// <= 8 candidates x 2 columns with v_sad_u16.  Two u32 SADs leave per store.
+// 10 bit: a lane owns two adjacent candidate columns (2g, 2g+1; the first is dword aligned
+// for even R) and half of the fenc rows (lane pair h = 0/1: rows 8h..8h+7); per ref row it
+// loads 9 dwords once (L rows ahead), forms the odd column's dwords with one
+// v_alignbyte_b32 each, and folds the row into <= 8 candidates x 2 columns with v_sad_u16.
 // `sink( c, a0, a1 )` receives candidate row c's two finished SADs (columns 2g, 2g+1),
-// identical in both lanes of the pair
-template <int R, int Y, class Sink>
-__device__ __forceinline__ void me_row5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
-                                         uint32_t (&acc)[8][2], Sink &sink )
-{
-    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
-    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
-    const uint32_t *row = rbase + Y * rs_dw;
-    uint32_t w[9], o[8];
-#pragma unroll
-    for( int k = 0; k < 9; k++ )
-        w[k] = row[k];
-#pragma unroll
-    for( int k = 0; k < 8; k++ )
-        o[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], 2 );
-#pragma unroll
-    for( int c = C0; c <= C1; c++ )
-    {
-        const int r = Y - c;
-        uint32_t a0 = r == 0 ? 0u : acc[c & 7][0], a1 = r == 0 ? 0u : acc[c & 7][1];
-#pragma unroll
-        for( int k = 0; k < 8; k++ )
-        {
-            a0 = __builtin_amdgcn_sad_u16( F[r][k], w[k], a0 );
-            a1 = __builtin_amdgcn_sad_u16( F[r][k], o[k], a1 );
-        }
-        if( r == 7 )
-        {
-            a0 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a0, 0xB1, 0xF, 0xF, false );
-            a1 += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)a1, 0xB1, 0xF, 0xF, false );
-            sink( c, a0, a1 );
-        }
-        else
-        {
-            acc[c & 7][0] = a0;
-            acc[c & 7][1] = a1;
-        }
-    }
-}
-
-// variant 5 with the next L ref rows' loads issued ahead (as me_row3p)
+// identical in both lanes of the pair after the DPP add.
 template <int R, int L, int Y, class Sink>
 __device__ __forceinline__ void me_row5p( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
                                           uint32_t (&acc)[8][2], Sink &sink, uint32_t (&ring)[L][9] )
@@ -713,14 +399,8 @@ __device__ __forceinline__ void me_rows5p( const uint32_t *__restrict__ rbase, i
     ( me_row5p<R, L, Ys>( rbase, rs_dw, F, acc, sink, ring ), ... );
 }
 
-template <int R, class Sink, int... Ys>
-__device__ __forceinline__ void me_rows5( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
-                                          uint32_t (&acc)[8][2], Sink &sink, std::integer_sequence<int, Ys...> )
-{
-    ( me_row5<R, Ys>( rbase, rs_dw, F, acc, sink ), ... );
-}
-
-template <int R, int PF = 0>
+// G column pairs per MB (full: R+1, centred: cen_cols(10, R) / 2), row pitch P
+template <int R, int G, int P>
 __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
                                                                   intptr_t ffs, const uint16_t *__restrict__ ref,
                                                                   intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -728,8 +408,6 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
                                                                   const int16_t *__restrict__ centre,
                                                                   int16_t *__restrict__ origin, int xcd )
 {
-    constexpr int G = (2 * R + 1 + 1) / 2;      // column pairs per MB
-    constexpr int P = (2 * R + 1 + 3) / 4 * 4;
     const int64_t slot = (int64_t)(xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
     if( slot >= total )
@@ -751,7 +429,7 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
         for( int k = 0; k < 8; k++ )
             F[r][k] = fe[r * fs_dw + k];
     int ox, oy;
-    me_window<10, R>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
+    me_window<10, R, P>( centre, mb, mbx, mby, mbw, mbh, ox, oy );
     if( origin && grp == 0 && h == 0 )
     {
         origin[2 * mb] = (int16_t)ox;
@@ -761,174 +439,87 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
         (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 2 * grp);
     uint32_t *out = table + mb * ((2 * R + 1) * P) + 2 * grp;
     uint32_t acc[8][2];
-    auto store = [out]( int c, uint32_t a0, uint32_t a1 ) {
-        *(uint2 *)(out + c * ((2 * R + 1 + 3) / 4 * 4)) = make_uint2( a0, a1 );
+    auto store = [out, h]( int c, uint32_t a0, uint32_t a1 ) {
+        if( !h )                                // both lanes of the pair hold the sums
+            *(uint2 *)(out + c * P) = make_uint2( a0, a1 );
     };
-    if constexpr( PF > 0 )
-        me_rows5p<R, PF>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
-    else
-        me_rows5<R>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
+    me_rows5p<R, ME_LEAD>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
 }
 
-// rows of load lead in variants 3 / 5 and the fused ESA kernels (tuning hook
-// X264HIP_ME_LEAD = 0..3, default 2): the next rows' ref loads are issued before the
-// current row's SADs.  At 16 1080p pairs, R 16: 8 bit 0.312 -> 0.300 ms (lead 0 -> 2;
-// 3 no better), 10 bit 0.653 -> 0.617 ms; lead 1 gains little, the compiler reuses the
-// current row's registers for it and so issues it half a row late
-
-static int me_lead()
+// 10-bit quadrant tables: the column-pair lane of the 16x16 kernel, whose fenc row half h is
+// already a quadrant row (h = 0 top, 1 bottom); the 8 dwords of a fenc row split into the
+// left (dwords 0-3) and right (4-7) accumulators, so a lane's candidate row leaves as four
+// 8x8 SADs (two columns x left / right) at fenc row 7 without the pair's DPP add.  An 8x8
+// SAD at 10 bit is at most 64 * 1023 = 65472: the quadrant tables stay uint16.
+template <int R, int L, int Y, class Sink>
+__device__ __forceinline__ void me_row5q( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
+                                          uint32_t (&acc)[8][4], Sink &sink, uint32_t (&ring)[L][9] )
 {
-    const int v = variant( V_ME_LEAD );
-    return v >= 0 && v <= 3 ? v : 2;
-}
-
-template <int R, typename P, typename T>
-static void launch_v5( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
-                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
-                       int16_t *origin )
-{
-    if constexpr( sizeof( P ) == 2 )
+    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    uint32_t w[9], o[8];
+#pragma unroll
+    for( int k = 0; k < 9; k++ )
+        w[k] = ring[Y % L][k];
+    if constexpr( Y + L < 2 * R + 8 )
     {
-        const int lead = me_lead(), xcd = me_xcd();
-        if( lead == 1 )
-            hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R, 1> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin, xcd );
-        else if( lead >= 2 )
-            hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin, xcd );
+        const uint32_t *row = rbase + (Y + L) * rs_dw;
+#pragma unroll
+        for( int k = 0; k < 9; k++ )
+            ring[Y % L][k] = row[k];
+    }
+#pragma unroll
+    for( int k = 0; k < 8; k++ )
+        o[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], 2 );
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint32_t a[4];
+#pragma unroll
+        for( int j = 0; j < 4; j++ )
+            a[j] = r == 0 ? 0u : acc[c & 7][j];
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            a[0] = __builtin_amdgcn_sad_u16( F[r][k], w[k], a[0] );              // column 2g, left
+            a[1] = __builtin_amdgcn_sad_u16( F[r][k], o[k], a[1] );              // column 2g+1, left
+            a[2] = __builtin_amdgcn_sad_u16( F[r][k + 4], w[k + 4], a[2] );      // column 2g, right
+            a[3] = __builtin_amdgcn_sad_u16( F[r][k + 4], o[k + 4], a[3] );      // column 2g+1, right
+        }
+        if( r == 7 )
+            sink( c, a[0] | (a[1] << 16), a[2] | (a[3] << 16) );
         else
-            hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,
-                                mbh, nframes, table, centre, origin, xcd );
+        {
+#pragma unroll
+            for( int j = 0; j < 4; j++ )
+                acc[c & 7][j] = a[j];
+        }
     }
+    __builtin_amdgcn_sched_barrier( 0 );
 }
 
-// kernel variant (tuning hook, read per launch): X264HIP_ME_VARIANT = 1, 2, 3, 7 (8 bit)
-// or 5 (10 bit); default 7 at 8 bit (0.292 -> 0.281 ms per 16 1080p pairs over variant 3,
-// both with two rows of load lead), 5 at 10 bit.  (A variant that dropped the padded column
-// group and finished the last column in separate waves ran 13-20% slower: the
-// table rows were then written by different waves at different times, so
-// nearly every 128-B line left L2 partially written.)
-static int me_variant()
+template <int R, int L, class Sink, int... Ys>
+__device__ __forceinline__ void me_rows5q( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][8],
+                                           uint32_t (&acc)[8][4], Sink &sink, std::integer_sequence<int, Ys...> )
 {
-    const int v = variant( V_ME );
-    return v >= 0 ? v : 0;
+    uint32_t ring[L][9];
+#pragma unroll
+    for( int j = 0; j < L; j++ )
+#pragma unroll
+        for( int k = 0; k < 9; k++ )
+            ring[j][k] = rbase[j * rs_dw + k];
+    ( me_row5q<R, L, Ys>( rbase, rs_dw, F, acc, sink, ring ), ... );
 }
 
-template <int R, typename P, typename T>
-static void launch_v3( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
-                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
-                       int16_t *origin )
+template <int R>
+__global__ __launch_bounds__( 256 ) void me_full_sad8q_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
+                                                                  intptr_t ffs, const uint16_t *__restrict__ ref,
+                                                                  intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                  int nframes, uint16_t *__restrict__ table8, int xcd )
 {
-    if constexpr( sizeof( P ) == 1 )
-    {
-        const int lead = me_lead();
-        if( lead == 1 )
-            hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R, 1> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin );
-        else if( lead == 2 )
-            hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin );
-        else if( lead == 3 )
-            hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R, 3> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin );
-        else
-            hipLaunchKernelGGL( ( me_full_sad16_v3_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,
-                                mbh, nframes, table, centre, origin );
-    }
-}
-
-template <int R, typename P, typename T>
-static void launch_v7( dim3 g, dim3 blk, hipStream_t stream, const P *fenc, intptr_t fs, intptr_t ffs, const P *ref,
-                       intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, T *table, const int16_t *centre,
-                       int16_t *origin )
-{
-    if constexpr( sizeof( P ) == 1 )
-    {
-        const int xcd = me_xcd();
-        if( me_lead() <= 1 )
-            hipLaunchKernelGGL( ( me_full_sad16_v7_kernel<R, 1> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin, xcd );
-        else
-            hipLaunchKernelGGL( ( me_full_sad16_v7_kernel<R, 2> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                                mbw, mbh, nframes, table, centre, origin, xcd );
-    }
-}
-
-template <int BD>
-hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
-                           const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                           int nframes, int range, typename PT<BD>::sadt *table, const int16_t *centre,
-                           int16_t *origin, hipStream_t stream )
-{
-    int variant = me_variant();
-    if( !variant )
-        variant = BD == 8 ? 7 : 5;
-    if( (BD != 8 && variant == 3) || (BD == 8 && variant == 5) )
-        variant = 1;
-    // variants 2/3 need dword-aligned fenc rows, dword-multiple strides and (3) a
-    // dword-aligned ref plane
-    if( (((uintptr_t)fenc | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
-          (uintptr_t)(rs * sizeof( typename PT<BD>::pixel )) | (variant >= 3 ? (uintptr_t)ref : 0)) & 3) )
-        variant = 1;
-    if( variant == 7 && (BD != 8 || (int64_t)nframes * mbh * mbw * ((2 * range + 1 + 3) / 4) >= (1ll << 32)) )
-        variant = 1;                              // (v7 indexes its lanes in 32 bits)
-    const int64_t groups = variant == 7   ? (2 * range + 1 + 3) / 4
-                           : variant == 3 ? 2 * ((2 * range + 1 + 3) / 4)
-                           : variant == 5 ? 2 * ((2 * range + 2) / 2)
-                           : variant == 2 ? 2 * (2 * range + 1)
-                                          : (2 * range + 1);
-    const int64_t lanes = (int64_t)nframes * mbh * mbw * groups;
-    if( lanes <= 0 )
-        return hipSuccess;
-    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
-    switch( range )
-    {
-#define ME_CASE( R ) \
-        case R:                                                                                                   \
-            if( variant == 5 )                                                                                    \
-                launch_v5<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
-            else if( variant == 7 )                                                                               \
-                launch_v7<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
-            else if( variant == 3 )                                                                               \
-                launch_v3<R>( g, blk, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin ); \
-            else if( variant == 2 )                                                                               \
-                hipLaunchKernelGGL( ( me_full_sad16_v2_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, \
-                                    rfs, mbw, mbh, nframes, table, centre, origin );                              \
-            else                                                                                                  \
-                hipLaunchKernelGGL( ( me_full_sad16_kernel<BD, R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs,   \
-                                    rfs, mbw, mbh, nframes, table, centre, origin );                              \
-            break;
-        ME_CASE( 4 ) ME_CASE( 8 ) ME_CASE( 16 ) ME_CASE( 24 )
-#undef ME_CASE
-        default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-}
-
-template hipError_t launch_me_full<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
-                                       int, int, int, uint16_t *, const int16_t *, int16_t *, hipStream_t );
-template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
-                                        int, int, int, int, uint32_t *, const int16_t *, int16_t *, hipStream_t );
-
-// Fused search + ESA decision (8 bit): the variant-3 lanes of me_search_centred around
-// each MB's predictor (bmx, bmy), but each finished candidate row is turned into
-// me_esa_argmin_at's packed keys (cost << 12 | raster index in the clipped, width-rounded
-// window, encoder/me.c:618-631, cost_mv terms me.c:60-70) and min-reduced in registers
-// instead of written out: the 17.8 MB-per-frame table never leaves the chip.  Each MB's
-// 18 lanes meet through one atomicMin per lane pair into its key slot (out[3*mb]), and
-// me_esa_finish_kernel applies the strict-< update from the predictor cost.
-template <int R, int PF>
-__global__ __launch_bounds__( 256 ) void me_full_esa_v3_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
-                                                                intptr_t ffs, const uint8_t *__restrict__ ref,
-                                                                intptr_t rs, intptr_t rfs, int mbw, int mbh,
-                                                                int nframes, int me_range,
-                                                                const int16_t *__restrict__ par,
-                                                                const uint16_t *__restrict__ cost_mv,
-                                                                uint32_t *__restrict__ keys )
-{
-    constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
-    constexpr int W = 2 * R + 1;
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int G = R + 1, P = full_pitch( R );
+    const int64_t slot = (int64_t)(xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
     if( slot >= total )
         return;
@@ -939,79 +530,131 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v3_kernel( const uint8_t *_
     const int64_t t = mb / mbw;
     const int mby = (int)(t % mbh);
     const int64_t f = t / mbh;
-
-    uint32_t F[8][4];
+    uint32_t F[8][8];
     const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
-    const int fs_dw = (int)(fs / 4);
+    const int fs_dw = (int)(fs / 2);
 #pragma unroll
     for( int r = 0; r < 8; r++ )
 #pragma unroll
-        for( int k = 0; k < 4; k++ )
+        for( int k = 0; k < 8; k++ )
             F[r][k] = fe[r * fs_dw + k];
-    const int16_t *p = par + 8 * mb;
-    const int bmx = p[0], bmy = p[1];
-    const int min_x = max( bmx - me_range, (int)p[4] ), min_y = max( bmy - me_range, (int)p[5] );
-    const int max_x = min( bmx + me_range, (int)p[6] ), max_y = min( bmy + me_range, (int)p[7] );
-    const int width = (max_x - min_x + 3) & ~3;
-    const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
-    int ox, oy;
-    const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };   // the window centre: the predictor
-    me_window<8, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
     const uint32_t *rbase =
-        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 4 * grp);
-    // the pair's four columns are split: lane h keys columns 4j+2h and 4j+2h+1 (its half of
-    // the packed sums), so both lanes share the epilogue without divergence
-    int ccost[2];
-    uint32_t cinv[2];                            // 0 for a column inside the window, else all ones
-#pragma unroll
-    for( int k = 0; k < 2; k++ )
-    {
-        const int col = 4 * grp + 2 * h + k, mx = ox + col;
-        const bool in = col < W && mx >= min_x && mx < min_x + width;
-        cinv[k] = in ? 0u : 0xFFFFFFFFu;
-        ccost[k] = in ? (int)cx[mx * 4] : 0;
-    }
-    uint32_t key = 0xFFFFFFFFu;
-    const int ibase = ox + 4 * grp + 2 * h - min_x - min_y * width;
-    // branch-free: every row loads a (clamped, always valid) row cost and masks the keys
-    // of rows / columns outside the window with all ones
-    // the row cost of candidate row c + 1 is loaded while row c is folded (a row of SADs
-    // ahead of its use), the first one before the rows
-    uint32_t ynext = cy[4 * min( max( oy, min_y ), max_y )];
-    auto reduce = [&]( int c, uint32_t lo, uint32_t hi ) {
-        const int my = oy + c;
-        const uint32_t rinv = my >= min_y && my <= max_y ? 0u : 0xFFFFFFFFu;
-        const uint32_t ycost = ynext;
-        int yi = 4 * min( max( my + 1, min_y ), max_y );
-        asm volatile( "" : "+v"( yi ) );         // issued here, not hoisted to the top
-        ynext = cy[yi];
-        const uint32_t w = h ? hi : lo;
-        const uint32_t ri = (uint32_t)(my * width + ibase);
-        const uint32_t k0 = (((w & 0xffff) + (uint32_t)ccost[0] + ycost) << 12) | ri;
-        const uint32_t k1 = (((w >> 16) + (uint32_t)ccost[1] + ycost) << 12) | (ri + 1);
-        key = min( key, min( k0 | cinv[0], k1 | cinv[1] ) | rinv );
-        // fold each row into the key where its sums finish: left to itself the compiler
-        // keeps every row's sums live until the end (2 VGPRs a row, half the occupancy)
-        asm volatile( "" : "+v"( key ) );
+        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h - R) * rs + 16 * mbx - R + 2 * grp);
+    // quadrants 2h (left) and 2h + 1 (right), columns 2g, 2g+1 as one dword each
+    uint32_t *ql = (uint32_t *)(table8 + (mb * 4 + 2 * h) * ((2 * R + 1) * P) + 2 * grp);
+    uint32_t *qr = ql + (2 * R + 1) * P / 2;
+    auto store = [ql, qr]( int c, uint32_t l, uint32_t r ) {
+        ql[c * (P / 2)] = l;
+        qr[c * (P / 2)] = r;
     };
-    uint64_t acc[8];
-    if constexpr( PF > 0 )
-        me_rows3p<R, PF>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
-    else
-        me_rows3<R>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
-    key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)key, 0xB1, 0xF, 0xF, false ) );
-    if( !h && key != 0xFFFFFFFFu )
-        atomicMin( keys + 3 * mb, key );
+    uint32_t acc[8][4];
+    me_rows5q<R, ME_LEAD>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
 }
 
-// The fused decision on variant 7's lanes (all 16 fenc rows, four columns per lane): a lane
-// keys its own four columns per finished candidate row, and each of an MB's 9 lanes meets
-// the others through one atomicMin.  A workgroup holds whole MBs (256 / G of them), whose
-// lanes first stage the MB's per-row key terms in LDS (ycost, row part of the raster
-// index, row validity), so a candidate row costs one LDS read instead of a clamped
+template <int BD>
+hipError_t launch_me_full8( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                            const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                            int nframes, int range, uint16_t *table8, hipStream_t stream )
+{
+    constexpr int PSZ = sizeof( typename PT<BD>::pixel );
+    const int64_t lanes = (int64_t)nframes * mbh * mbw * (BD == 8 ? full_pitch( range ) / 4 : 2 * (range + 1));
+    if( lanes <= 0 )
+        return hipSuccess;
+    if( lanes >= (1ll << 32) || (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)(fs * PSZ) | (uintptr_t)(rs * PSZ) |
+                                  (uintptr_t)table8) & 3) )
+        return hipErrorInvalidValue;
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+    const int xcd = me_xcd();
+    switch( range )
+    {
+#define ME8_CASE( R )                                                                                           \
+        case R:                                                                                                 \
+            if constexpr( BD == 8 )                                                                             \
+                hipLaunchKernelGGL( ( me_full_sad8q_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
+                                    mbw, mbh, nframes, table8, xcd );                                           \
+            else                                                                                                \
+                hipLaunchKernelGGL( ( me_full_sad8q_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs,  \
+                                    rfs, mbw, mbh, nframes, table8, xcd );                                      \
+            break;
+        ME8_CASE( 4 ) ME8_CASE( 8 ) ME8_CASE( 16 ) ME8_CASE( 24 )
+#undef ME8_CASE
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+template hipError_t launch_me_full8<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
+                                        int, int, int, uint16_t *, hipStream_t );
+template hipError_t launch_me_full8<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
+                                         int, int, int, int, uint16_t *, hipStream_t );
+
+// Full-search / centred tables.  The grouped kernels need dword-aligned fenc rows,
+// dword-multiple strides and a dword-aligned ref plane (and, at 8 bit, a lane count below
+// 2^32); anything else runs the generic kernel (one lane per column, realigned loads).
+template <int BD>
+hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                           const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                           int nframes, int range, typename PT<BD>::sadt *table, const int16_t *centre,
+                           int16_t *origin, hipStream_t stream )
+{
+    constexpr int PSZ = sizeof( typename PT<BD>::pixel );
+    const bool cen = centre != nullptr;
+    const int64_t nmb = (int64_t)nframes * mbh * mbw;
+    if( nmb <= 0 )
+        return hipSuccess;
+    const int ncol = cen ? cen_pitch( BD, range ) : 2 * range + 1;
+    const int64_t groups = BD == 8 ? al4( ncol ) / 4 : 2 * (cen ? cen_cols( 10, range ) / 2 : range + 1);
+    bool grouped = !(((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)(fs * PSZ) | (uintptr_t)(rs * PSZ)) & 3);
+    if( BD == 8 && nmb * groups >= (1ll << 32) )
+        grouped = false;                        // (the 8-bit kernel indexes its lanes in 32 bits)
+    const int64_t lanes = nmb * (grouped ? groups : ncol);
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+    const int xcd = me_xcd();
+    switch( range )
+    {
+#define ME_GO( R, CEN )                                                                                           \
+    if( !grouped )                                                                                                \
+        hipLaunchKernelGGL( ( me_full_sad16_kernel<BD, R, CEN ? cen_pitch( BD, R ) : 2 * R + 1> ), g, blk, 0,    \
+                            stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin );      \
+    else if constexpr( BD == 8 )                                                                                  \
+        hipLaunchKernelGGL( ( me_full_sad16_v7_kernel<R, (CEN ? cen_pitch( 8, R ) : full_pitch( R )) / 4> ), g,   \
+                            blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre, origin, \
+                            xcd );                                                                                \
+    else                                                                                                          \
+        hipLaunchKernelGGL( ( me_full_sad16_v5_kernel<R, CEN ? cen_cols( 10, R ) / 2 : R + 1,                     \
+                                                      CEN ? cen_pitch( 10, R ) : full_pitch( R )> ),              \
+                            g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, table, centre,     \
+                            origin, xcd );
+#define ME_CASE( R )                                                                                              \
+        case R:                                                                                                   \
+            if( cen ) { ME_GO( R, true ) } else { ME_GO( R, false ) }                                             \
+            break;
+        ME_CASE( 4 ) ME_CASE( 8 ) ME_CASE( 16 ) ME_CASE( 24 )
+#undef ME_CASE
+#undef ME_GO
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+template hipError_t launch_me_full<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
+                                       int, int, int, uint16_t *, const int16_t *, int16_t *, hipStream_t );
+template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
+                                        int, int, int, int, uint32_t *, const int16_t *, int16_t *, hipStream_t );
+
+// ---------------------------------------------------------------------------
+// Fused search + ESA decision (8 bit): the four-column lanes of the centred search around
+// each MB's predictor, but each finished candidate row is turned into me_esa_argmin_at's
+// packed keys (cost << 12 | raster index in the clipped, width-rounded window,
+// encoder/me.c:618-631, cost_mv terms me.c:60-70) and min-reduced in registers instead of
+// written out: the table never leaves the chip.  Each of an MB's G lanes meets the others
+// through one atomicMin into the MB's key slot (out[3*mb]), and me_esa_finish_kernel applies
+// the strict-< update from the predictor cost.  A workgroup holds whole MBs (256 / G of
+// them), whose lanes first stage the MB's per-row key terms in LDS (ycost, row part of the
+// raster index, row validity), so a candidate row costs one LDS read instead of a clamped
 // global load and its index arithmetic.
-template <int R> constexpr int esa7_mbs() { return 256 / ((2 * R + 1 + 3) / 4); }
-template <int R, int L>
+template <int R> constexpr int esa7_groups() { return cen_pitch( 8, R ) / 4; }
+template <int R> constexpr int esa7_mbs() { return 256 / esa7_groups<R>(); }
+template <int R>
 __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                 intptr_t ffs, const uint8_t *__restrict__ ref,
                                                                 intptr_t rs, intptr_t rfs, int mbw, int mbh,
@@ -1020,8 +663,9 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
                                                                 const uint16_t *__restrict__ cost_mv,
                                                                 uint32_t *__restrict__ keys, int xcd )
 {
-    constexpr int G = (2 * R + 1 + 3) / 4;      // column groups per MB
-    constexpr int W = 2 * R + 1;
+    constexpr int G = esa7_groups<R>();         // column groups per MB
+    constexpr int P = 4 * G;
+    constexpr int W = 2 * R + 1;                // candidate rows
     constexpr int MPW = esa7_mbs<R>();          // whole MBs per workgroup
     constexpr int SP = W | 1;                   // LDS row-term pitch (odd: spread banks)
     __shared__ uint32_t s_row[MPW * SP];
@@ -1055,7 +699,7 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
     const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
     int ox, oy;
     const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };   // the window centre: the predictor
-    me_window<8, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
+    me_window<8, R, P>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
     const uint32_t *rbase =
         (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox + 4 * cgrp);
     // key = (sad + xcost + ycost) << 12 | raster, raster = (my - min_y) * width + mx - min_x
@@ -1068,8 +712,8 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
 #pragma unroll
     for( int k = 0; k < 4; k++ )
     {
-        const int col = 4 * cgrp + k, mx = ox + col;
-        const bool in = col < W && mx >= min_x && mx < min_x + width;
+        const int mx = ox + 4 * cgrp + k;
+        const bool in = mx >= min_x && mx < min_x + width;
         ck[k] = in ? ((uint32_t)cx[mx * 4] << 12) + (uint32_t)(mx - min_x) : 0xF0000000u;
     }
     uint32_t key = 0xFFFFFFFFu;
@@ -1108,7 +752,7 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
         asm volatile( "" : "+v"( key ) );        // fold each row where its sums finish
     };
     uint64_t acc[16];
-    me_rows7<R, L>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
+    me_rows7<R, ME_LEAD>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
     if( live && key < 0xF0000000u )
         atomicMin( keys + 3 * mb, key );
 }
@@ -1141,21 +785,21 @@ __global__ __launch_bounds__( 256 ) void me_esa_finish_kernel( int nmb, int me_r
     out[3 * i + 2] = ry;
 }
 
-// Fused search + ESA decision (10 bit): the variant-5 lanes (two columns per lane pair,
-// u32 sums) around each MB's predictor; lane h of a pair keys column 2g+h.  Keys as the
-// 8-bit form (cost < 2^19 at 10 bit: 261888 + two cost_mv terms).
-template <int R, int PF>
+// Fused search + ESA decision (10 bit): the column-pair lanes (u32 sums) of the centred
+// search around each MB's predictor; lane h of a pair keys column 2g+h.  Keys as the 8-bit
+// form (cost < 2^19 at 10 bit: 261888 + two cost_mv terms).
+template <int R>
 __global__ __launch_bounds__( 256 ) void me_full_esa_v5_kernel( const uint16_t *__restrict__ fenc, intptr_t fs,
                                                                 intptr_t ffs, const uint16_t *__restrict__ ref,
                                                                 intptr_t rs, intptr_t rfs, int mbw, int mbh,
                                                                 int nframes, int me_range,
                                                                 const int16_t *__restrict__ par,
                                                                 const uint16_t *__restrict__ cost_mv,
-                                                                uint32_t *__restrict__ keys )
+                                                                uint32_t *__restrict__ keys, int xcd )
 {
-    constexpr int G = (2 * R + 1 + 1) / 2;      // column pairs per MB
-    constexpr int W = 2 * R + 1;
-    const int64_t slot = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    constexpr int G = cen_cols( 10, R ) / 2;    // column pairs per MB
+    constexpr int P = cen_pitch( 10, R );
+    const int64_t slot = (int64_t)(xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * blockDim.x + threadIdx.x;
     const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
     if( slot >= total )
         return;
@@ -1183,11 +827,11 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v5_kernel( const uint16_t *
     const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
     int ox, oy;
     const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };
-    me_window<10, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
+    me_window<10, R, P>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
     const uint32_t *rbase =
         (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 2 * grp);
-    const int col = 2 * grp + h, mxc = ox + col;
-    const bool cin = col < W && mxc >= min_x && mxc < min_x + width;
+    const int mxc = ox + 2 * grp + h;
+    const bool cin = mxc >= min_x && mxc < min_x + width;
     const uint32_t cinv = cin ? 0u : 0xFFFFFFFFu;
     const int ccost = cin ? (int)cx[mxc * 4] : 0;
     uint32_t key = 0xFFFFFFFFu;
@@ -1208,10 +852,7 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v5_kernel( const uint16_t *
         asm volatile( "" : "+v"( key ) );        // fold each row where its sums finish
     };
     uint32_t acc[8][2];
-    if constexpr( PF > 0 )
-        me_rows5p<R, PF>( rbase, (int)(rs / 2), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
-    else
-        me_rows5<R>( rbase, (int)(rs / 2), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
+    me_rows5p<R, ME_LEAD>( rbase, (int)(rs / 2), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 8>{} );
     key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( (int)0xFFFFFFFF, (int)key, 0xB1, 0xF, 0xF, false ) );
     if( !h && key != 0xFFFFFFFFu )
         atomicMin( keys + 3 * mb, key );
@@ -1233,37 +874,24 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
     hipError_t e = hipMemsetAsync( out, 0xFF, (size_t)nmb * 3 * sizeof( int32_t ), stream );
     if( e != hipSuccess )
         return e;
-    // 8 bit: variant 7's lanes (one per column group), X264HIP_ME_VARIANT=3 the lane pairs
-    const bool v7 = BD == 8 && me_variant() != 3;
-    const int64_t groups = BD == 8 ? (2 * range + 1 + 3) / 4 : (2 * range + 2) / 2;
-    const int64_t lanes = nmb * (v7 ? 1 : 2) * groups;
-    // v7: whole MBs per workgroup (esa7_mbs), the others a flat lane index
-    const int64_t mpw = 256 / ((2 * range + 1 + 3) / 4);
-    dim3 blk( 256 ), g( (unsigned)(v7 ? (nmb + mpw - 1) / mpw : (lanes + 255) / 256) );
-    const int lead = me_lead();
+    // 8 bit: whole MBs per workgroup (esa7_mbs); 10 bit: a flat lane index over column pairs
+    const int64_t mpw = 256 / (cen_pitch( 8, range ) / 4);
+    const int64_t lanes = nmb * 2 * (cen_cols( 10, range ) / 2);
+    dim3 blk( 256 ), g( (unsigned)(BD == 8 ? (nmb + mpw - 1) / mpw : (lanes + 255) / 256) );
+    const int xcd = me_xcd();
     switch( range )
     {
-#define ESA_GO( R, L )                                                                                            \
-    if constexpr( BD == 8 )                                                                                       \
-    {                                                                                                             \
-        if( v7 )                                                                                                  \
-            hipLaunchKernelGGL( ( me_full_esa_v7_kernel<R, L <= 1 ? 1 : 2> ), g, blk, 0, stream, fenc, fs, ffs,   \
-                                ref, rs, rfs, mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out,         \
-                                me_xcd() );                                                                       \
-        else                                                                                                      \
-            hipLaunchKernelGGL( ( me_full_esa_v3_kernel<R, L> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs,   \
-                                mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );                     \
-    }                                                                                                             \
-    else                                                                                                          \
-        hipLaunchKernelGGL( ( me_full_esa_v5_kernel<R, L> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw,  \
-                            mbh, nframes, me_range, par, cost_mv, (uint32_t *)out );
 #define ESA_CASE( R )                                                                                             \
         case R:                                                                                                   \
-            if( lead == 0 ) { ESA_GO( R, 0 ) } else if( lead == 1 ) { ESA_GO( R, 1 ) } else { ESA_GO( R, 2 ) }   \
+            if constexpr( BD == 8 )                                                                               \
+                hipLaunchKernelGGL( ( me_full_esa_v7_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
+                                    mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out, xcd );            \
+            else                                                                                                  \
+                hipLaunchKernelGGL( ( me_full_esa_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
+                                    mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out, xcd );            \
             break;
         ESA_CASE( 4 ) ESA_CASE( 8 ) ESA_CASE( 16 ) ESA_CASE( 24 )
 #undef ESA_CASE
-#undef ESA_GO
         default: return hipErrorInvalidValue;
     }
     hipLaunchKernelGGL( me_esa_finish_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream, (int)nmb,
@@ -1278,58 +906,73 @@ template hipError_t launch_me_search_esa<10>( const uint16_t *, intptr_t, intptr
                                               intptr_t, int, int, int, int, int, const int16_t *, const int32_t *,
                                               const uint16_t *, int32_t *, hipStream_t );
 
-} // namespace x264hip
-
-namespace x264hip {
-
 // ---------------------------------------------------------------------------
-// ESA decision over a full-search table (reference encoder/me.c:618-631 plain
-// exhaustive form, equal to its ads path :632-771): one wave per macroblock.
-// Each lane scans every 64th candidate of the clipped window in my-major raster
-// order and keeps the packed key (cost << 12 | raster index); a wave min over
-// the keys returns the lowest cost and, among equal costs, the first in
-// raster order — what the strict-< scan of the reference keeps — which then
-// replaces the predictor result only if strictly better (COPY3_IF_LT).
+// ESA decision over a table (reference encoder/me.c:618-631 plain exhaustive form, equal
+// to its ads path :632-771): one wave per macroblock.  The MB's table rows are read as
+// 4-entry chunks (8 bytes at 8 bit, 16 at 10 bit): lane l takes chunk l % NCH of rows
+// y0 + l / NCH, + RPS, ... (NCH = pitch / 4 chunks per row, RPS = 64 / NCH rows per step),
+// so one step's loads are one contiguous, coalesced run of the table.  A lane's columns are
+// fixed, so their cost_mv terms are read once; the row term once per step.  Each entry's
+// key (cost << 12 | raster index in the clipped, width-rounded window) is built as
+// sat( (sad << 12) + C[k] + S ) with C[k] = 0xC0000000 outside the window (valid keys stay
+// below 392958 << 12 + 4096 < 0xC0000000 at either depth; 0xC0000000 + (261888 << 12) does
+// not wrap), a wave min picks the lowest cost and, among equal costs, the first in raster
+// order -- what the strict-< scan of the reference keeps -- and it replaces the predictor
+// result only if strictly better (COPY3_IF_LT, me.h:87-93).
+// Table geometry: rows = 2R+1 at `pitch`, `cols` valid columns, window origin (ox, oy)
+// from `origin` (centred tables) or (-R, -R) (full tables).
 template <int BD>
 __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT<BD>::sadt *__restrict__ table, int R,
-                                                               int nmb, int me_range,
+                                                               int cols, int pitch, int nmb, int me_range,
                                                                const int16_t *__restrict__ origin,
                                                                const int16_t *__restrict__ par,
                                                                const int32_t *__restrict__ init_cost,
                                                                const uint16_t *__restrict__ cost_mv,
                                                                int32_t *__restrict__ out )
 {
+    using chunk = typename std::conditional<BD == 8, uint2, uint4>::type;
     const int lane = threadIdx.x & 63;
     const int64_t mb = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     if( mb >= nmb )
         return;                                                    // wave-uniform
-    const int W = 2 * R + 1, P = (W + 3) & ~3;
+    const int W = 2 * R + 1;
+    const int nch = pitch >> 2, rps = 64 / nch;                    // pitch <= 64: >= 4 rows per step
+    const int rr = lane / nch, ch = lane - rr * nch;
     const int16_t *p = par + 8 * mb;
     const int bmx = p[0], bmy = p[1], mvpx = p[2], mvpy = p[3];
     const int min_x = max( bmx - me_range, (int)p[4] ), min_y = max( bmy - me_range, (int)p[5] );
     const int max_x = min( bmx + me_range, (int)p[6] ), max_y = min( bmy + me_range, (int)p[7] );
     const int width = (max_x - min_x + 3) & ~3;
-    const int n = width > 0 && max_y >= min_y ? width * (max_y - min_y + 1) : 0;
     const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
-    const typename PT<BD>::sadt *t = table + mb * (int64_t)(W * P);
-    // lane = window column (width <= 64), rows walked in order: coalesced table reads and
-    // no division per candidate
-    uint32_t key = 0xFFFFFFFFu;
-    if( n > 0 && lane < width )
+    const int y0 = max( min_y, oy ), y1 = min( max_y, oy + W - 1 );
+    const chunk *t = (const chunk *)(table + mb * (int64_t)(W * pitch)) + ch;
+    uint32_t ck[4];
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
     {
-        const int mx = min_x + lane, tx = mx - ox;
-        const bool colin = tx >= 0 && tx < W;
-        const uint32_t cxv = colin ? cost_mv[mx * 4 - mvpx] : 0u;
-        // rows in table order, unrolled with the loads independent of each other; a row or
-        // column outside the table is read clamped and masked out of the minimum
-        const int y0 = max( min_y, oy ), y1 = min( max_y, oy + W - 1 );
-        const typename PT<BD>::sadt *col = t + min( max( tx, 0 ), W - 1 );
-#pragma unroll 8
-        for( int my = y0; my <= y1; my++ )
+        const int tx = 4 * ch + k, mx = ox + tx;
+        const bool in = tx < cols && mx >= min_x && mx < min_x + width;
+        ck[k] = in ? ((uint32_t)cost_mv[mx * 4 - mvpx] << 12) + (uint32_t)(mx - min_x) : 0xC0000000u;
+    }
+    uint32_t key = 0xFFFFFFFFu;
+    if( rr < rps && width > 0 )
+    {
+        for( int my = y0 + rr; my <= y1; my += rps )
         {
-            const uint32_t cost = (uint32_t)col[(my - oy) * P] + cxv + cost_mv[my * 4 - mvpy];
-            const uint32_t k = (cost << 12) | (uint32_t)((my - min_y) * width + lane);
-            key = min( key, colin ? k : 0xFFFFFFFFu );
+            const chunk v = t[(my - oy) * nch];
+            const uint32_t S = ((uint32_t)cost_mv[my * 4 - mvpy] << 12) + (uint32_t)((my - min_y) * width);
+            uint32_t s[4];
+            if constexpr( BD == 8 )
+            {
+                s[0] = v.x & 0xffff; s[1] = v.x >> 16; s[2] = v.y & 0xffff; s[3] = v.y >> 16;
+            }
+            else
+            {
+                s[0] = v.x; s[1] = v.y; s[2] = v.z; s[3] = v.w;
+            }
+#pragma unroll
+            for( int k = 0; k < 4; k++ )
+                key = min( key, __builtin_elementwise_add_sat( (s[k] << 12) + ck[k], S ) );
         }
     }
 #pragma unroll
@@ -1338,7 +981,7 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
     if( lane == 0 )
     {
         int32_t bcost = init_cost[mb], rx = bmx, ry = bmy;
-        if( key != 0xFFFFFFFFu && (int32_t)(key >> 12) < bcost )
+        if( key < 0xC0000000u && (int32_t)(key >> 12) < bcost )
         {
             const int i = (int)(key & 4095);
             bcost = (int32_t)(key >> 12);
@@ -1358,8 +1001,13 @@ hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int 
 {
     if( nmb <= 0 )
         return hipSuccess;
-    hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD> ), dim3( (nmb + 3) / 4 ), dim3( 256 ), 0, stream, table, R, nmb,
-                        me_range, origin, par, init_cost, cost_mv, out );
+    // centred tables (an origin given) hold the ESA window's columns, full tables the square
+    const int cols = origin ? cen_cols( BD, R ) : 2 * R + 1;
+    const int pitch = origin ? cen_pitch( BD, R ) : full_pitch( R );
+    if( pitch > 64 || ((uintptr_t)table & (BD == 8 ? 7 : 15)) )
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD> ), dim3( (nmb + 3) / 4 ), dim3( 256 ), 0, stream, table, R, cols,
+                        pitch, nmb, me_range, origin, par, init_cost, cost_mv, out );
     return hipGetLastError();
 }
 
@@ -1515,7 +1163,8 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
                                               const typename PT<BD>::pixel *__restrict__ ref, intptr_t rs, intptr_t rfs,
                                               const uint16_t *__restrict__ integral, intptr_t ifs, int mbw, int mbh,
                                               int nmb, int me_range, int satd,
-                                              const typename PT<BD>::sadt *__restrict__ table, int R, int ox, int oy,
+                                              const typename PT<BD>::sadt *__restrict__ table, int R, int tcols, int tpitch,
+                                              int ox, int oy,
                                               const int16_t *__restrict__ par, const int32_t *__restrict__ init_cost,
                                               const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out,
                                               int64_t mbo, bool live, int sg, int lane, tesa_ent<SEG> *mvsads,
@@ -1579,11 +1228,12 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
         enc_dc[j] = (int)seg_lane<SEG>( seg_scan_add<SEG>( dcq[j] ), SEG - 1, sg );
     tesa_wave_sync();
 
-    const int W = 2 * R + 1, P = (W + 3) & ~3;
+    // table: 2R+1 rows of tcols valid columns at pitch tpitch (centred or full geometry)
+    const int W = 2 * R + 1, P = tpitch;
     const typename PT<BD>::sadt *tab = TAB ? table + mb * (int64_t)(W * P) : nullptr;
     auto sad_at = [&]( int mx, int my ) -> uint32_t {
         const int tx = mx - ox, ty = my - oy;
-        if( TAB && tx >= 0 && tx < W && ty >= 0 && ty < W )
+        if( TAB && tx >= 0 && tx < tcols && ty >= 0 && ty < W )
             return (uint32_t)tab[ty * P + tx];
         return tesa_sad16<BD>( fl, p_fref + my * rs + mx, rs );
     };
@@ -1609,8 +1259,8 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
     // row is loaded once although row r's ads reads rows r and r + 8.
     constexpr int CK = TESA_CK, NC = (NR + CK - 1) / CK;
     const int cxm = active ? mx : min_x;
-    const int tx = mx - ox, txc = min( max( tx, 0 ), W - 1 );
-    const bool colin = tx >= 0 && tx < W;
+    const int tx = mx - ox, txc = min( max( tx, 0 ), tcols - 1 );
+    const bool colin = tx >= 0 && tx < tcols;
     // rows as 24-bit multiplies of small offsets from per-lane bases (j <= 2*32+8 rows of a
     // stride below 2^18 elements; table rows < 66 of a pitch < 69), not 64-bit address math
     const uint16_t *ib = sums_base + cxm + (intptr_t)min_y * rs;
@@ -1904,7 +1554,7 @@ __global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( TESA_WP
                                                         const uint16_t *__restrict__ integral, intptr_t ifs, int mbw,
                                                         int mbh, int nmb, int me_range, int satd,
                                                         const typename PT<BD>::sadt *__restrict__ table, int R,
-                                                        const int16_t *__restrict__ origin,
+                                                        int tcols, int tpitch, const int16_t *__restrict__ origin,
                                                         const int16_t *__restrict__ par,
                                                         const int32_t *__restrict__ init_cost,
                                                         const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out,
@@ -1919,91 +1569,8 @@ __global__ __launch_bounds__( 64 ) __attribute__( ( amdgpu_waves_per_eu( TESA_WP
     const int64_t mb = mbo < nmb ? mbo : nmb - 1;
     const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
     tesa_scan_mb<BD, NR, SEG, TAB, SPEC>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nmb, me_range, satd,
-                                          table, R, ox, oy, par, init_cost, cost_mv, out, mbo, true, sg, lane,
-                                          (tesa_ent<SEG> *)tesa_lds + (int64_t)sg * cap, fls[sg] );
-}
-
-// Self-contained TESA (8 bit, me_range 9..16) as ONE launch (X264HIP_TESA_VARIANT=3, not
-// the default): a workgroup first builds the
-// full-search tables of its 28 MBs around their predictors on variant 7's lanes (the
-// centred search, R = 16) into scratch, then its four waves scan those MBs (two per wave
-// pass, 32-lane segments).  The scan is latency-bound (33 dependent rows per MB) and the
-// table work VALU-bound, so with four workgroups per CU one workgroup's scan runs in the
-// issue slots the others' table rows leave, instead of after the whole table launch; the
-// table is read back by the workgroup that wrote it, mostly from L2.  The global stores are
-// visible to the other waves of the workgroup after the barrier (one CU, one L1).
-// Measured (profiles/r03ad_tesa_*): 0.768 ms per 16 1080p pairs against 0.652 for the two
-// launches.  The workgroups start together and have equal phases, so they stay in phase:
-// the scans of a CU's four workgroups coincide instead of filling each other's table
-// rows, and a wave's four scan passes run back to back at the occupancy the scan alone
-// had.  Nor is the scan's arithmetic small: ~3.7 k VALU per wave (two MBs), ~0.2 ms of
-// issue over the chip, so table (0.275 ms) + scan issue already exceeds 0.45 ms.
-template <int L>
-__global__ __launch_bounds__( 256 ) __attribute__( ( amdgpu_waves_per_eu( 4 ) ) ) void me_tesa_fused_kernel(
-    const uint8_t *__restrict__ fenc, intptr_t fs, intptr_t ffs, const uint8_t *__restrict__ ref, intptr_t rs,
-    intptr_t rfs, const uint16_t *__restrict__ integral, intptr_t ifs, int mbw, int mbh, int nmb, int me_range,
-    int satd, uint16_t *__restrict__ table, const int16_t *__restrict__ par, const int32_t *__restrict__ init_cost,
-    const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out, int cap, int xcd )
-{
-    constexpr int R = 16, G = (2 * R + 1 + 3) / 4, P = 4 * G, W = 2 * R + 1;
-    constexpr int MPW = 256 / G;                // 28 whole MBs per workgroup
-    constexpr int MPV = (MPW + 3) / 4;          // MBs per wave in the scan (7)
-    extern __shared__ uint64_t tesa_lds[];
-    __shared__ uint32_t fls[4][2][16 * 4];
-    const int tid = (int)threadIdx.x;
-    const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
-    const int64_t mb0 = (int64_t)blk * MPW;
-
-    // table phase (me_full_sad16_v7_kernel's lane: four columns, all 16 fenc rows)
-    {
-        const int lmb = min( tid / G, MPW - 1 );
-        const int grp = min( tid - lmb * G, G - 1 );
-        const int64_t mb = min( mb0 + lmb, (int64_t)nmb - 1 );
-        const uint32_t t32 = (uint32_t)mb / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
-        const int mbx = (int)((uint32_t)mb - t32 * (uint32_t)mbw);
-        const int mby = (int)(t32 - f32 * (uint32_t)mbh);
-        uint32_t F[16][4];
-        const uint32_t *fe = (const uint32_t *)(fenc + (int64_t)f32 * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
-        const int fs_dw = (int)(fs / 4);
-#pragma unroll
-        for( int r = 0; r < 16; r++ )
-#pragma unroll
-            for( int k = 0; k < 4; k++ )
-                F[r][k] = fe[r * fs_dw + k];
-        int ox, oy;
-        const int16_t cen[2] = { par[8 * mb], par[8 * mb + 1] };   // the window centre: the predictor
-        me_window<8, R>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
-        const uint32_t *rbase = (const uint32_t *)(ref + (int64_t)f32 * rfs + (intptr_t)(16 * mby + oy) * rs +
-                                                   16 * mbx + ox + 4 * grp);
-        uint64_t *o64 = (uint64_t *)(table + mb * (W * P) + 4 * grp);
-        // lanes past the workgroup's MBs (or past the last MB) repeat a live lane's MB and
-        // group, so their stores write the same values to the same words: no guard
-        auto store = [o64]( int c, uint32_t lo, uint32_t hi ) { o64[c * (P / 4)] = ((uint64_t)hi << 32) | lo; };
-        uint64_t acc[16];
-        me_rows7<R, L>( rbase, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 16>{} );
-    }
-    __syncthreads();
-
-    // scan phase: wave w takes MBs [MPV*w, MPV*w + MPV) of the workgroup, two per pass
-    const int w = tid >> 6, sg = (tid >> 5) & 1, lane = tid & 31;
-    tesa_ent<32> *lists = (tesa_ent<32> *)tesa_lds + (int64_t)(2 * w + sg) * cap;
-#pragma unroll 1
-    for( int i = 0; i < MPV; i += 2 )
-    {
-        const int l = MPV * w + i + sg;
-        const bool live = i + sg < MPV && l < MPW;
-        const int64_t mbo = mb0 + min( l, MPW - 1 );
-        const int64_t mb = mbo < nmb ? mbo : nmb - 1;
-        const uint32_t t32 = (uint32_t)mb / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
-        int ox, oy;
-        const int16_t cen[2] = { par[8 * mb], par[8 * mb + 1] };
-        me_window<8, R>( cen, 0, (int)((uint32_t)mb - t32 * (uint32_t)mbw), (int)(t32 - f32 * (uint32_t)mbh), mbw,
-                         mbh, ox, oy );
-        tesa_scan_mb<8, 33, 32, true, true>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nmb, me_range,
-                                             satd, table, R, ox, oy, par, init_cost, cost_mv, out, mbo, live, sg,
-                                             lane, lists, fls[w][sg] );
-        tesa_wave_sync();                       // the next pass rewrites this wave's LDS
-    }
+                                          table, R, tcols, tpitch, ox, oy, par, init_cost, cost_mv, out, mbo, true, sg,
+                                          lane, (tesa_ent<SEG> *)tesa_lds + (int64_t)sg * cap, fls[sg] );
 }
 
 // the predictor pairs (par[8*mb], par[8*mb+1]) as me_window's centre array
@@ -2021,21 +1588,21 @@ __global__ __launch_bounds__( 256 ) void tesa_centre_kernel( int nmb, const int1
 // stream-ordered scratch for the self-contained TESA from a memory pool the library owns,
 // one per device (the device of the launch stream), created with an unbounded release
 // threshold so a repeated call re-uses its blocks instead of mapping fresh pages; the
-// application's default pool is left alone
+// application's default pool is left alone.  x264hip_trim() returns the pool's idle blocks.
+static std::mutex g_pool_mu;
+static hipMemPool_t g_pools[64] = {};
 static hipError_t tesa_scratch( void **p, size_t bytes, hipStream_t stream )
 {
-    static std::mutex mu;
-    static hipMemPool_t pools[64] = {};
     int dev = 0;
-    hipError_t e = stream ? hipStreamGetDevice( stream, &dev ) : hipGetDevice( &dev );
+    hipError_t e = stream_device( stream, &dev );
     if( e != hipSuccess )
         return e;
     if( dev < 0 || dev >= 64 )
         return hipErrorInvalidDevice;
     hipMemPool_t pool;
     {
-        std::lock_guard<std::mutex> lk( mu );
-        if( !pools[dev] )
+        std::lock_guard<std::mutex> lk( g_pool_mu );
+        if( !g_pools[dev] )
         {
             hipMemPoolProps props;
             memset( &props, 0, sizeof( props ) );
@@ -2043,17 +1610,31 @@ static hipError_t tesa_scratch( void **p, size_t bytes, hipStream_t stream )
             props.handleTypes = hipMemHandleTypeNone;
             props.location.type = hipMemLocationTypeDevice;
             props.location.id = dev;
-            if( (e = hipMemPoolCreate( &pools[dev], &props )) != hipSuccess )
+            if( (e = hipMemPoolCreate( &g_pools[dev], &props )) != hipSuccess )
             {
-                pools[dev] = nullptr;
+                g_pools[dev] = nullptr;
                 return e;
             }
             uint64_t thr = UINT64_MAX;
-            (void)hipMemPoolSetAttribute( pools[dev], hipMemPoolAttrReleaseThreshold, &thr );
+            (void)hipMemPoolSetAttribute( g_pools[dev], hipMemPoolAttrReleaseThreshold, &thr );
         }
-        pool = pools[dev];
+        pool = g_pools[dev];
     }
     return hipMallocFromPoolAsync( p, bytes, pool, stream );
+}
+
+// release the scratch pool's unused blocks of `dev` (all devices for dev < 0)
+hipError_t scratch_trim( int dev )
+{
+    std::lock_guard<std::mutex> lk( g_pool_mu );
+    for( int d = 0; d < 64; d++ )
+        if( g_pools[d] && (dev < 0 || dev == d) )
+        {
+            const hipError_t e = hipMemPoolTrimTo( g_pools[d], 0 );
+            if( e != hipSuccess )
+                return e;
+        }
+    return hipSuccess;
 }
 
 template <int BD>
@@ -2069,47 +1650,19 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     // (the scan addresses rows by 24-bit products: strides below 2^18 elements)
     if( me_range < 1 || me_range > 32 || nmb > 0x7fffffff || rs <= 0 || rs >= (1 << 18) )
         return hipErrorInvalidValue;
-    // X264HIP_TESA_VARIANT=3: the self-contained call as ONE launch (me_tesa_fused_kernel:
-    // bit-exact, but 0.768 vs 0.652 ms per 16 1080p pairs, so not the default)
-    if constexpr( BD == 8 )
-    {
-        if( !table && me_range > 8 && me_range <= 16 && variant( V_TESA ) == 3 &&
-            !(((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)fs | (uintptr_t)rs) & 3) && nmb * 9 < (1ll << 32) )
-        {
-            constexpr int MPW = 256 / 9;
-            const size_t bytes = (size_t)nmb * 33 * 36 * sizeof( uint16_t );
-            const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
-            void *buf = nullptr;
-            if( tesa_scratch( &buf, bytes, stream ) == hipSuccess )
-            {
-                const int xcd = variant( V_ME_XCD ) != 0;
-                const dim3 g( (unsigned)((nmb + MPW - 1) / MPW) );
-                const size_t lds = (size_t)8 * cap * sizeof( uint32_t );
-                if( me_lead() <= 1 )
-                    hipLaunchKernelGGL( ( me_tesa_fused_kernel<1> ), g, dim3( 256 ), lds, stream, fenc, fs, ffs, ref,
-                                        rs, rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, (uint16_t *)buf,
-                                        par, init_cost, cost_mv, out, cap, xcd );
-                else
-                    hipLaunchKernelGGL( ( me_tesa_fused_kernel<2> ), g, dim3( 256 ), lds, stream, fenc, fs, ffs, ref,
-                                        rs, rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, (uint16_t *)buf,
-                                        par, init_cost, cost_mv, out, cap, xcd );
-                const hipError_t e = hipGetLastError();
-                const hipError_t f = hipFreeAsync( buf, stream );
-                return e != hipSuccess ? e : f;
-            }
-            (void)hipGetLastError();                        // no scratch: the in-kernel SADs below
-        }
-    }
+    // (X264HIP_TESA_VARIANT=1 forces the in-scan SADs -- the me_range > 24 kernel -- at any
+    // range: a test hook for that path)
     if( !table && me_range <= 24 && variant( V_TESA ) != 1 )
     {
         // Self-contained call: the ads-filtered SADs cost a lane 16 unaligned row loads
         // each, so the kernel is address-path bound (2.6 ms per 16 1080p frames).  Every
         // window SAD from the full-search kernel around the predictors (0.3 ms) and the
-        // table-reading scan give the same decisions in ~1 ms.  (X264HIP_TESA_VARIANT=1:
-        // the in-kernel SADs.)
+        // table-reading scan give the same decisions in ~1 ms.  The table is the centred
+        // (ESA-window) geometry, so every candidate the scan can reach is a read.  (The
+        // in-kernel SADs remain for me_range > 24 and when no scratch can be had.)
         using sadt = typename PT<BD>::sadt;
         const int TR = me_range <= 4 ? 4 : me_range <= 8 ? 8 : me_range <= 16 ? 16 : 24;
-        const size_t tab = (size_t)nmb * (2 * TR + 1) * (size_t)((2 * TR + 1 + 3) & ~3) * sizeof( sadt );
+        const size_t tab = (size_t)nmb * (2 * TR + 1) * (size_t)cen_pitch( BD, TR ) * sizeof( sadt );
         const size_t bytes = tab + (size_t)nmb * 8;
         void *buf = nullptr;
         if( tesa_scratch( &buf, bytes, stream ) == hipSuccess )
@@ -2132,21 +1685,18 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
 
     // the mvsads list: at most (2*me_range+1) rows x (2*me_range+3)&~3 columns per MB
     const int cap = (2 * me_range + 1) * ((2 * me_range + 3) & ~3);
-    // X264HIP_TESA_VARIANT=2: the table scan with the prefix minimum on the bsad chain (the
-    // round-2 form) instead of the speculative row scans
-    const bool spec = variant( V_TESA ) != 2;
+    // table geometry: centred (an origin given) or full
+    const int tcols = origin ? cen_cols( BD, R ) : 2 * R + 1;
+    const int tpitch = origin ? cen_pitch( BD, R ) : full_pitch( R );
+    if( table && (R < 1 || tpitch > 64) )
+        return hipErrorInvalidValue;
+    // with a table the speculative row scans (SPEC: every row's prefix minimum taken over the
+    // staged costs up front), without one the SADs computed in the scan
 #define TESA_GO( NR, SEG, T )                                                                                    \
-    if( T && spec )                                                                                              \
-        hipLaunchKernelGGL( ( me_tesa_kernel<BD, NR, SEG, T, true> ),                                            \
-                            dim3( (unsigned)((nmb + 64 / SEG - 1) / (64 / SEG)) ), dim3( 64 ),                   \
-                            (64 / SEG) * (size_t)cap * (SEG == 32 ? 4 : 8), stream, fenc, fs, ffs, ref, rs, rfs, \
-                            integral, ifs, mbw, mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost, \
-                            cost_mv, out, cap );                                                                 \
-    else                                                                                                         \
-    hipLaunchKernelGGL( ( me_tesa_kernel<BD, NR, SEG, T> ), dim3( (unsigned)((nmb + 64 / SEG - 1) / (64 / SEG)) ),   \
+    hipLaunchKernelGGL( ( me_tesa_kernel<BD, NR, SEG, T, T> ), dim3( (unsigned)((nmb + 64 / SEG - 1) / (64 / SEG)) ), \
                         dim3( 64 ), (64 / SEG) * (size_t)cap * (SEG == 32 ? 4 : 8), stream, fenc, fs, ffs, ref, rs, \
-                        rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, table, R, origin, par, init_cost,    \
-                        cost_mv, out, cap )
+                        rfs, integral, ifs, mbw, mbh, (int)nmb, me_range, satd, table, R, tcols, tpitch, origin, par, \
+                        init_cost, cost_mv, out, cap )
     if( me_range <= 16 )
     {
         if( table ) { TESA_GO( 33, 32, true ); } else { TESA_GO( 33, 32, false ); }

@@ -961,15 +961,17 @@ __global__ __launch_bounds__( 256 ) void plane_ssd_kernel( const typename PT<BD>
     }
 }
 
-// the accumulator ring of the calling device (zeroed once; every launch leaves its slots
-// zero), and disjoint slot ranges for launches that may be in flight together
-static hipError_t ssd_ring( SsdSlot **ring, int nslots, int *slot0 )
+// the accumulator ring of the launch stream's device (zeroed once; every launch leaves its
+// slots zero), and disjoint slot ranges for launches that may be in flight together.  The
+// slot range is fixed when a launch is enqueued, so a captured graph holds its range: replays
+// of one graph must not run concurrently with each other (sequential replays are fine).
+static hipError_t ssd_ring( hipStream_t stream, SsdSlot **ring, int nslots, int *slot0 )
 {
     static std::mutex mu;
     static SsdSlot *rings[64] = {};
     static std::atomic<uint64_t> next{ 0 };
     int dev = 0;
-    hipError_t e = hipGetDevice( &dev );
+    hipError_t e = stream_device( stream, &dev );
     if( e != hipSuccess )
         return e;
     if( dev < 0 || dev >= 64 || nslots > SSD_RING )
@@ -978,15 +980,18 @@ static hipError_t ssd_ring( SsdSlot **ring, int nslots, int *slot0 )
         std::lock_guard<std::mutex> lk( mu );
         if( !rings[dev] )
         {
+            int cur = 0;
+            if( (e = hipGetDevice( &cur )) != hipSuccess || (cur != dev && (e = hipSetDevice( dev )) != hipSuccess) )
+                return e;
             SsdSlot *r = nullptr;
-            if( (e = hipMalloc( (void **)&r, sizeof( SsdSlot ) * SSD_RING )) != hipSuccess )
-                return e;
-            if( (e = hipMemset( r, 0, sizeof( SsdSlot ) * SSD_RING )) != hipSuccess ||
-                (e = hipDeviceSynchronize()) != hipSuccess )
-            {
+            e = hipMalloc( (void **)&r, sizeof( SsdSlot ) * SSD_RING );
+            if( e == hipSuccess && ((e = hipMemset( r, 0, sizeof( SsdSlot ) * SSD_RING )) != hipSuccess ||
+                                    (e = hipDeviceSynchronize()) != hipSuccess) )
                 (void)hipFree( r );
+            if( cur != dev )
+                (void)hipSetDevice( cur );
+            if( e != hipSuccess )
                 return e;
-            }
             rings[dev] = r;
         }
     }
@@ -1014,7 +1019,7 @@ hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_
         return hipErrorInvalidValue;
     SsdSlot *ring = nullptr;
     int slot0 = 0;
-    hipError_t e = ssd_ring( &ring, nframes, &slot0 );
+    hipError_t e = ssd_ring( stream, &ring, nframes, &slot0 );
     if( e != hipSuccess )
         return e;
     constexpr int CH = 16 / (int)sizeof( typename PT<BD>::pixel );
@@ -1029,11 +1034,10 @@ hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_
         c1b = w7 ? w8 + 2 * w7 : w8;
     }
     const int nbx0 = (c1a - c0a + 64 * CH - 1) / (64 * CH), nbx1 = (c1b - c0b + 64 * CH - 1) / (64 * CH);
-    // rows per wave (X264HIP_SSD_VARIANT 0 = 16, 1 = 8, the default, 2 = 4): 16 1080p pairs
-    // 0.0195 / 0.0137 / 0.0141 ms with the packed accumulator (profiles/r03aa_ssd_ab.json); the
-    // 16-frame leg is one burst of loads, and twice the waves of half the rows issue it faster
-    const int sv = variant( V_SSD );
-    const int rows = sv == 0 ? 16 : sv == 2 ? 4 : 8;
+    // 8 rows per wave: 16 1080p pairs 0.0195 / 0.0137 / 0.0141 ms for 16 / 8 / 4 rows with the
+    // packed accumulator (profiles/r03aa_ssd_ab.json); the 16-frame leg is one burst of loads,
+    // and twice the waves of half the rows issue it faster
+    constexpr int rows = 8;
     dim3 g( (unsigned)std::max( 1, nbx0 + nbx1 ), (unsigned)((height + 4 * rows - 1) / (4 * rows)), (unsigned)nframes ),
         blk( 256 );
     unsigned long long *o = (unsigned long long *)out;
@@ -1044,9 +1048,7 @@ hipError_t launch_plane_ssd( int nv12, const typename PT<BD>::pixel *p1, intptr_
     else                                                                                                           \
         hipLaunchKernelGGL( ( plane_ssd_kernel<BD, false, R> ), g, blk, 0, stream, p1, s1, f1, p2, s2, f2, c0a,    \
                             c1a, nbx0, c0b, c1b, height, o, ring, slot0 )
-    if( rows == 8 ) { SSD_GO( 8 ); }
-    else if( rows == 4 ) { SSD_GO( 4 ); }
-    else { SSD_GO( 16 ); }
+    SSD_GO( rows );
 #undef SSD_GO
     return hipGetLastError();
 }
