@@ -679,7 +679,49 @@ def rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     if not torch.equal(out_t, out_f):
         raise SystemExit("bench: fused and table ESA decisions disagree")
     del table, org
+    res.update(rates_refine(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, par, out_f, cm_d, span))
     return res
+
+
+def rates_refine(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, par, esa_out, cm_d, span):
+    """configs[2]'s "SATD_8x8 subpel refine" at full resolution: refine_subpel (me.c:865-992) of
+    every 16x16 MB of the F pairs as x264_me_search_ref runs it at subme 7 (x264's default: two
+    hpel diamonds of SAD over get_ref blocks, the SATD re-score, two qpel SATD diamonds), started
+    from the ESA decisions above (m->mv = 4 * the integer winner, m->cost its cost), mv limits of
+    analyse.c:336-349.  VALU fraction on the reference's own cmp calls (counted per MB by the
+    kernel, equal to the oracle's count in tests/test_gpu_refine.py): a SATD call costs SURVEY §8d's
+    444 + 192 lane-ops per 64 pixels, a SAD call 0.75 lane-op slots per pixel (a half-rate
+    v_sad_u8 per 4 absdiffs and a v_lerp_u8 per 4 qpel averages)."""
+    n = F * mbw * mbh
+    hv = x.hpel_filter(dev[:-1], origin, stride, mbw * 16, mbh * 16)
+    planes = [dev[:-1]] + list(hv)
+    mb = np.arange(n) % (mbw * mbh)
+    mbx, mby = mb % mbw, mb // mbw
+    pos = np.stack([np.arange(n) // (mbw * mbh), 16 * mbx, 16 * mby], 1).astype(np.int32)
+    rpar = np.zeros((n, 8), np.int16)
+    rpar[:, 2:4] = par[:, 2:4]                                  # mvp (qpel)
+    rpar[:, 4], rpar[:, 5] = 4 * (-16 * mbx - 24), 4 * (-16 * mby - 24)
+    rpar[:, 6], rpar[:, 7] = 4 * (16 * (mbw - 1 - mbx) + 24), 4 * (16 * (mbh - 1 - mby) + 24)
+    rpar_d = torch.from_numpy(rpar).cuda()
+    rpar_d[:, 0:2] = (esa_out[:, 1:3] * 4).to(torch.int16)      # m->mv = the integer winner, qpel
+    init = esa_out[:, 0].contiguous()
+    pos_d = torch.from_numpy(pos).cuda()
+    out = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+    ne = torch.empty(n, dtype=torch.int32, device="cuda")
+
+    def step():
+        x.me_refine_subpel(dev[1:], origin, stride, planes, origin, stride, x.PIXEL_16x16, 7, pos_d, rpar_d, init,
+                           (cm_d, span), out=out, fenc_frame_stride=fstride, ref_frame_stride=fstride, nevals=ne)
+    wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
+    nsad = int((ne & 0xFFFF).sum().item())
+    nsatd = int((ne >> 16).sum().item())
+    work = nsad * 256 * 0.75 + nsatd * 256 * (444 + 192) / 64
+    moved = (out[:, 1:3] != rpar_d[:, 0:2].int()).any(1).float().mean().item()
+    del hv, planes
+    return {"refine16_mbs_per_s": world * a.steps * n / wall, "refine16_launch_ms": ev_ms,
+            "refine16_mbs_per_launch": n, "refine16_sad_calls_per_mb": nsad / n,
+            "refine16_satd_calls_per_mb": nsatd / n, "refine16_moved_frac": moved,
+            "refine16_valu_frac": work / (ev_ms * 1e-3) / VALU_LANE_OPS}
 
 
 def rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, bd=8):

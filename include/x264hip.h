@@ -788,6 +788,31 @@ int x264hip_##BD##_subpel_qpel9_batch( int op, int i_pixel, const pixel *fenc,  
                                        const int64_t *fenc_off, const int32_t *centre_xy,       \
                                        int n, int32_t *scores, void *stream );                  \
                                                                                                 \
+/* refine_subpel (reference encoder/me.c:865-992) for n partitions of size i_pixel (16x16,    \
+ * 16x8, 8x16, 8x8) of n_frames (fenc, ref) pairs: the subpel stage x264_me_search_ref runs      \
+ * after its integer search (refine_qpel = 0: subpel_iterations[subme][2..3], me.c:791-797) or   \
+ * x264_me_refine_qpel (refine_qpel = 1: [0..1], me.c:801-810) -- the halfpel diamond of         \
+ * fpelcmp over get_ref blocks (SAD; SATD when fpel_satd, i.e. TESA, and subme > 1,              \
+ * encoder.c:1423-1426), the SATD re-score of its winner, the quarterpel diamond of              \
+ * mbcmp_unaligned (SATD for subme > 1) with the odir skip, or subme 1's single qpel diamond.   \
+ * fenc: pixel (0,0) of frame 0 (frame stride fenc_frame_stride); fpel / hpel_h / hpel_v /      \
+ * hpel_c: the reference's F plane and hpel_filter's planes, pixel (0,0) of frame 0, common     \
+ * stride and frame stride.  pos[3*i] = { frame, x, y } (the partition's top-left pixel);        \
+ * par[8*i] = { mvx, mvy (qpel start, m->mv), mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel x, y  \
+ * (h->mb.mv_min_spel / mv_max_spel) }; init_cost[i] = m->cost; cost_mv at mvd 0.                \
+ * out[4*i] = { m->cost, m->mv[0], m->mv[1], m->cost_mv } (16-byte aligned); nevals (or NULL):  \
+ * the reference's cmp calls per partition, SADs | SATDs << 16.  Luma only (no b_chroma_me),     \
+ * no multi-reference threshold, unweighted references. */                                      \
+int x264hip_##BD##_me_refine_subpel( const pixel *fenc, intptr_t fenc_stride,                   \
+                                     intptr_t fenc_frame_stride, const pixel *fpel,             \
+                                     const pixel *hpel_h, const pixel *hpel_v,                  \
+                                     const pixel *hpel_c, intptr_t ref_stride,                  \
+                                     intptr_t ref_frame_stride, int i_pixel, int subme,         \
+                                     int refine_qpel, int fpel_satd, const int32_t *pos,        \
+                                     const int16_t *par, const int32_t *init_cost,              \
+                                     const uint16_t *cost_mv, int n, int32_t *out,              \
+                                     int32_t *nevals, void *stream );                           \
+                                                                                                \
 /* block lists of the reference transforms (dct.c), device arrays;                             \
  * dct holds n consecutive outputs of the selected entry's size. */                             \
 int x264hip_##BD##_sub_dct_batch( int kind, const pixel *fenc, intptr_t fenc_stride,            \

@@ -1688,6 +1688,131 @@ void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const i
     }
 }
 
+/* refine_subpel (reference encoder/me.c:865-992) for a list of partitions, semantics of
+ * x264hip_*_me_refine_subpel: luma only (b_chroma_me = 0), p_halfpel_thresh = NULL, no
+ * weights.  Iterations from subpel_iterations (me.c:38-50): refine_qpel = 0 is the call
+ * of x264_me_search_ref (me.c:791-797, entries 2-3), 1 the one of x264_me_refine_qpel
+ * (me.c:801-810, entries 0-1).  fpelcmp = satd iff fpel_satd (TESA) and subme > 1,
+ * mbcmp_unaligned = satd iff subme > 1 (encoder.c:1411-1426).  fenc / planes point at
+ * pixel (0,0) of one frame (planes = F, H, V, C); pos[2*i] = the partition's top-left
+ * pixel; par[8*i] = { mvx, mvy (qpel, m->mv), mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel
+ * x, y }; cost[i] = m->cost; cost_mv at mvd 0.  out[4*i] = { cost, mvx, mvy, cost_mv };
+ * nevals[i] (when given) = the number of sad | satd calls << 16 the reference makes. */
+static const uint8_t subpel_iterations[12][4] = { {0,0,0,0}, {1,1,0,0}, {0,1,1,0}, {0,2,1,0}, {0,2,1,1},
+                                                  {0,2,1,2}, {0,0,2,2}, {0,0,2,2}, {0,0,4,10}, {0,0,4,10},
+                                                  {0,0,4,10}, {0,0,4,10} };
+void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs, int i_pixel,
+                           int subme, int refine_qpel, int fpel_satd, const int32_t *pos, const int16_t *par,
+                           const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out, int32_t *nevals )
+{
+    const int bw = pixel_w[i_pixel], bh = pixel_h[i_pixel];
+    const int hpel_iters = subpel_iterations[subme][refine_qpel ? 0 : 2];
+    const int qpel_iters = subpel_iterations[subme][refine_qpel ? 1 : 3];
+    const int fsatd = fpel_satd && subme > 1, qsatd = subme > 1;
+    for( int i = 0; i < n; i++ )
+    {
+        const pixel *f = fenc + pos[2*i+1] * fs + pos[2*i];
+        const pixel *q[4];
+        for( int k = 0; k < 4; k++ )
+            q[k] = planes[k] + pos[2*i+1] * rs + pos[2*i];
+        const int16_t *p = par + 8 * i;
+        const uint16_t *p_cost_mvx = cost_mv - p[2], *p_cost_mvy = cost_mv - p[3];
+        const int mv_min_spel[2] = { p[4], p[5] }, mv_max_spel[2] = { p[6], p[7] };
+        pixel tmp[16 * 16];
+#define RS_CMP( use_satd, mx, my ) ( ts = 16, r = FN(get_ref)( tmp, &ts, q, rs, mx, my, bw, bh ), \
+                                     (use_satd) ? (nsatd++, FN(satd)( i_pixel, f, fs, r, ts ))  \
+                                                : (nsad++, FN(sad)( i_pixel, f, fs, r, ts )) )
+        int nsad = 0, nsatd = 0;
+        intptr_t ts;
+        const pixel *r;
+        int bmx = p[0], bmy = p[1], bcost = cost[i];
+        int odir = -1, bdir;
+        int costs[4];
+        if( hpel_iters )
+        {
+            if( subme < 3 )
+            {
+                int mx = p[2] < mv_min_spel[0] + 2 ? mv_min_spel[0] + 2 : p[2] > mv_max_spel[0] - 2 ? mv_max_spel[0] - 2 : p[2];
+                int my = p[3] < mv_min_spel[1] + 2 ? mv_min_spel[1] + 2 : p[3] > mv_max_spel[1] - 2 ? mv_max_spel[1] - 2 : p[3];
+                if( (mx - bmx) | (my - bmy) )
+                {
+                    int c = RS_CMP( fsatd, mx, my ) + p_cost_mvx[mx] + p_cost_mvy[my];
+                    if( c < bcost ) { bcost = c; bmx = mx; bmy = my; }
+                }
+            }
+            bcost <<= 6;
+            for( int it = hpel_iters; it > 0; it-- )
+            {
+                int omx = bmx, omy = bmy;
+                costs[0] = RS_CMP( fsatd, omx, omy - 2 ) + p_cost_mvx[omx] + p_cost_mvy[omy - 2];
+                costs[1] = RS_CMP( fsatd, omx, omy + 2 ) + p_cost_mvx[omx] + p_cost_mvy[omy + 2];
+                costs[2] = RS_CMP( fsatd, omx - 2, omy ) + p_cost_mvx[omx - 2] + p_cost_mvy[omy];
+                costs[3] = RS_CMP( fsatd, omx + 2, omy ) + p_cost_mvx[omx + 2] + p_cost_mvy[omy];
+                if( (costs[0] << 6) + 2 < bcost ) bcost = (costs[0] << 6) + 2;
+                if( (costs[1] << 6) + 6 < bcost ) bcost = (costs[1] << 6) + 6;
+                if( (costs[2] << 6) + 16 < bcost ) bcost = (costs[2] << 6) + 16;
+                if( (costs[3] << 6) + 48 < bcost ) bcost = (costs[3] << 6) + 48;
+                if( !(bcost & 63) )
+                    break;
+                bmx -= (int32_t)((uint32_t)bcost << 26) >> 29;
+                bmy -= (int32_t)((uint32_t)bcost << 29) >> 29;
+                bcost &= ~63;
+            }
+            bcost >>= 6;
+        }
+        if( !refine_qpel && qsatd != fsatd )
+        {
+            /* bcost = COST_MAX; COST_MV_SATD( bmx, bmy, -1 ) */
+            bcost = RS_CMP( qsatd, bmx, bmy ) + p_cost_mvx[bmx] + p_cost_mvy[bmy];
+        }
+        if( subme != 1 )
+        {
+            bdir = -1;
+            for( int it = qpel_iters; it > 0; it-- )
+            {
+                if( bmy <= mv_min_spel[1] || bmy >= mv_max_spel[1] || bmx <= mv_min_spel[0] || bmx >= mv_max_spel[0] )
+                    break;
+                odir = bdir;
+                int omx = bmx, omy = bmy;
+                static const int8_t qd[4][2] = { {0,-1}, {0,1}, {-1,0}, {1,0} };
+                for( int dir = 0; dir < 4; dir++ )
+                {
+                    if( !refine_qpel && (dir ^ 1) == odir )
+                        continue;
+                    int mx = omx + qd[dir][0], my = omy + qd[dir][1];
+                    int c = RS_CMP( qsatd, mx, my ) + p_cost_mvx[mx] + p_cost_mvy[my];
+                    if( c < bcost ) { bcost = c; bmx = mx; bmy = my; bdir = dir; }
+                }
+                if( bmx == omx && bmy == omy )
+                    break;
+            }
+        }
+        else if( bmy > mv_min_spel[1] && bmy < mv_max_spel[1] && bmx > mv_min_spel[0] && bmx < mv_max_spel[0] )
+        {
+            int omx = bmx, omy = bmy;
+            costs[0] = RS_CMP( fsatd, omx, omy - 1 ) + p_cost_mvx[omx] + p_cost_mvy[omy - 1];
+            costs[1] = RS_CMP( fsatd, omx, omy + 1 ) + p_cost_mvx[omx] + p_cost_mvy[omy + 1];
+            costs[2] = RS_CMP( fsatd, omx - 1, omy ) + p_cost_mvx[omx - 1] + p_cost_mvy[omy];
+            costs[3] = RS_CMP( fsatd, omx + 1, omy ) + p_cost_mvx[omx + 1] + p_cost_mvy[omy];
+            bcost <<= 4;
+            if( (costs[0] << 4) + 1 < bcost ) bcost = (costs[0] << 4) + 1;
+            if( (costs[1] << 4) + 3 < bcost ) bcost = (costs[1] << 4) + 3;
+            if( (costs[2] << 4) + 4 < bcost ) bcost = (costs[2] << 4) + 4;
+            if( (costs[3] << 4) + 12 < bcost ) bcost = (costs[3] << 4) + 12;
+            bmx -= (int32_t)((uint32_t)bcost << 28) >> 30;
+            bmy -= (int32_t)((uint32_t)bcost << 30) >> 30;
+            bcost >>= 4;
+        }
+#undef RS_CMP
+        out[4*i] = bcost;
+        out[4*i+1] = bmx;
+        out[4*i+2] = bmy;
+        out[4*i+3] = p_cost_mvx[bmx] + p_cost_mvy[bmy];
+        if( nevals )
+            nevals[i] = nsad | (nsatd << 16);
+    }
+}
+
 /* TESA integer-pel search of x264_me_search_ref for PIXEL_16x16, restated from
  * reference encoder/me.c:618-748 (X264_ME_TESA): enc_dc from sad_x4 against
  * x264_zero (:643-645), per row the ycost skip, ads4 with threshold bsad*17>>4

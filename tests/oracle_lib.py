@@ -72,6 +72,8 @@ for _bd in (8, 10):
     _f(_bd, "ssd_nv12", [_P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P])
     _f(_bd, "me_tesa", [_P, _IP, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "me_search_centred", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P])
+    _f(_bd, "me_refine_subpel", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P,
+                                 _P])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
     _f(_bd, "subpel_list", [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P])
     _f(_bd, "sa8d", [C.c_int, _P, _IP, _P, _IP], C.c_int)
@@ -338,6 +340,24 @@ def me_search_centred(bd, fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, rng, 
     getattr(_L, f"oracle{bd}_me_search_centred")(_addr(fenc, f_origin), fs, _addr(ref, r_origin), rs, mbw, mbh,
                                                 rng, _addr(c), _addr(out), _addr(org))
     return out, org
+
+
+def me_refine_subpel(bd, fenc, f_origin, fs, planes, r_origin, rs, i_pixel, subme, pos_xy, par, cost, cost_mv, c0,
+                     refine_qpel=False, fpel_satd=False, counts=False):
+    """one frame: refine_subpel (me.c:865-992) of the partitions at pos_xy int32 [n, 2]; planes =
+    the four reference planes (numpy, same layout); returns int32 [n, 4] (and the per-partition
+    cmp-call counts, sad | satd << 16, with counts=True)."""
+    n = len(pos_xy)
+    pos = np.ascontiguousarray(pos_xy, np.int32)
+    p = np.ascontiguousarray(par, np.int16)
+    c = np.ascontiguousarray(cost, np.int32)
+    out = np.zeros((n, 4), np.int32)
+    ne = np.zeros(n, np.int32)
+    arr = (C.c_void_p * 4)(*[_addr(q, r_origin).value for q in planes])
+    getattr(_L, f"oracle{bd}_me_refine_subpel")(_addr(fenc, f_origin), fs, arr, rs, i_pixel, subme,
+                                               int(bool(refine_qpel)), int(bool(fpel_satd)), _addr(pos), _addr(p),
+                                               _addr(c), _addr(cost_mv, c0), n, _addr(out), _addr(ne))
+    return (out, ne) if counts else out
 
 
 # ---------------------------------------------------------------- further pixel entries

@@ -1,0 +1,40 @@
+"""Shared inputs of the refine_subpel tests (test_cpu_refine.py, test_gpu_refine.py): partition
+lists with analyse.c-shaped mv limits and an x264-shaped mv cost table."""
+import numpy as np
+
+# partitions of an MB per i_pixel (16x16, 16x8, 8x16, 8x8): top-left offsets
+PARTS = {0: [(0, 0)], 1: [(0, 0), (0, 8)], 2: [(0, 0), (8, 0)], 3: [(0, 0), (8, 0), (0, 8), (8, 8)]}
+
+
+def cost_mv(lam=40, span=8192):
+    """symmetric lambda * bits table (analyse.c:143-157 shape), mvd 0 at index span"""
+    i = np.arange(-span, span + 1)
+    logs = np.where(i == 0, 0.718, 2.0 * np.log2(np.abs(i) + 1) + 1.718)
+    return np.minimum((lam * logs + 0.5).astype(np.int64), 65535).astype(np.uint16), span
+
+
+def jobs(mbw, mbh, nframes, i_pixel, seed, motion=(12, 8), spread=24):
+    """per partition: (frame, x, y), par = (mvx, mvy, mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel
+    x, y) and a start cost; start mvs around the sequence's true motion (qpel), inside
+    [mv_min_spel + 24, mv_max_spel - 24] (the integer search's 6-pixel fpel border,
+    analyse.c:333-349) so every candidate the schedule can reach lies in the padding"""
+    rs = np.random.default_rng(seed)
+    pos, par = [], []
+    for f in range(nframes):
+        for mby in range(mbh):
+            for mbx in range(mbw):
+                for px, py in PARTS[i_pixel]:
+                    mn = (4 * (-16 * mbx - 24), 4 * (-16 * mby - 24))
+                    mx_ = (4 * (16 * (mbw - mbx - 1) + 24), 4 * (16 * (mbh - mby - 1) + 24))
+                    mv = [int(np.clip(motion[k] + rs.integers(-spread, spread + 1), mn[k] + 24, mx_[k] - 24))
+                          for k in range(2)]
+                    if rs.random() < 0.3:                                  # full-pel starts (bmv_spel)
+                        mv = [int(np.clip(4 * ((v + 2) >> 2), mn[k] + 24, mx_[k] - 24)) for k, v in enumerate(mv)]
+                    mvp = [int(v) for v in rs.integers(-40, 41, 2)]
+                    pos.append((f, 16 * mbx + px, 16 * mby + py))
+                    par.append((mv[0], mv[1], mvp[0], mvp[1], mn[0], mn[1], mx_[0], mx_[1]))
+    pos = np.array(pos, np.int32)
+    par = np.array(par, np.int16)
+    cost = rs.integers(200, 6000, len(pos)).astype(np.int32)
+    cost[::9] = 0                                                         # nothing beats the start
+    return pos, par, cost

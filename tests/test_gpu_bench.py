@@ -40,3 +40,30 @@ def test_bench_json_contract():
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in cb, k
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_gloo():
+    """The N-rank path the driver's scaling run uses:
+    bench.py --gpus 2 starts its own two ranks (a fresh child process; this process is never
+    exec'd), both on the box's one GPU over gloo, and rank 0 prints one line whose value is the
+    two ranks' candidates over the max-over-ranks step time."""
+    import time
+    env = dict(os.environ, X264HIP_DIST_BACKEND="gloo")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    t0 = time.perf_counter()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--frames", "2", "--no-extra",
+                        "--no-cpu", "--steps", "2", "--warmup", "1"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    wall = time.perf_counter() - t0
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    c = d["config"]
+    assert d["n_gpus"] == 2 and c["world_size"] == 2 and c["rank_devices"] == [0, 0]
+    assert d["steps"] == 2 and d["warmup"] == 1 and d["scaling"] == "weak"
+    assert d["ms_per_step"] * d["steps"] * 1e-3 < wall
+    cands = 2 * c["frames_per_step_per_gpu"] * c["mbs_per_frame"] * c["candidates_per_mb"]
+    assert d["value"] == pytest.approx(cands / (d["ms_per_step"] * 1e-3), rel=1e-3)

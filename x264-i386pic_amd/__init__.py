@@ -25,7 +25,7 @@ import numpy as np
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "stream_pair_destroy", "me_search_full8",
@@ -1057,6 +1057,32 @@ def subpel_qpel9_batch(op, i_pixel, fenc, fenc_stride, planes, ref_origin, ref_s
         op, i_pixel, _ptr(fenc), fenc_stride, *[_ptr(p, ref_origin) for p in planes], ref_stride,
         _ptr(fenc_off), _ptr(centre_xy), n, _ptr(scores), _stream()), "subpel_qpel9_batch")
     return scores
+
+
+def me_refine_subpel(fenc, fenc_origin, fenc_stride, planes, ref_origin, ref_stride, i_pixel, subme, pos, par,
+                     init_cost, cost_mv_center, refine_qpel=False, fpel_satd=False, out=None, fenc_frame_stride=None,
+                     ref_frame_stride=None, nevals=None):
+    """refine_subpel (encoder/me.c:865-992) of n partitions (x264hip_*_me_refine_subpel): planes =
+    [F, H, V, C] tensors of the references (hpel_filter's), pos int32 [n, 3] = (frame, x, y), par
+    int16 [n, 8] = (mvx, mvy, mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel x, y), init_cost int32
+    [n]; returns int32 [n, 4] = (cost, mvx, mvy, cost_mv).  nevals: optional int32 [n] receiving
+    the reference's cmp calls per partition (SADs | SATDs << 16)."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = pos.shape[0]
+    if out is None:
+        out = torch.empty((n, 4), dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else _frame_stride(*planes)
+    cm, c0 = cost_mv_center
+    fn = getattr(lib(), f"x264hip_{bd}_me_refine_subpel")
+    fn.argtypes = [_P, _IP, _IP, _P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P,
+                   _c.c_int, _P, _P, _P]
+    fn.restype = _c.c_int
+    _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, *[_ptr(p, ref_origin) for p in planes], ref_stride, rfs,
+           i_pixel, subme, int(bool(refine_qpel)), int(bool(fpel_satd)), _ptr(pos), _ptr(par), _ptr(init_cost),
+           _ptr(cm, c0), n, _ptr(out), _ptr(nevals) if nevals is not None else None, _stream()), "me_refine_subpel")
+    return out
 
 
 def me_esa_argmin(table, rng, me_range, par, init_cost, cost_mv_center, out=None, origin=None):
