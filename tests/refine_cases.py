@@ -13,7 +13,7 @@ def cost_mv(lam=40, span=8192):
     return np.minimum((lam * logs + 0.5).astype(np.int64), 65535).astype(np.uint16), span
 
 
-def jobs(mbw, mbh, nframes, i_pixel, seed, motion=(12, 8), spread=24):
+def jobs(mbw, mbh, nframes, i_pixel, seed, motion=(12, 8), spread=24, cost_scale=1):
     """per partition: (frame, x, y), par = (mvx, mvy, mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel
     x, y) and a start cost; start mvs around the sequence's true motion (qpel), inside
     [mv_min_spel + 24, mv_max_spel - 24] (the integer search's 6-pixel fpel border,
@@ -35,6 +35,6 @@ def jobs(mbw, mbh, nframes, i_pixel, seed, motion=(12, 8), spread=24):
                     par.append((mv[0], mv[1], mvp[0], mvp[1], mn[0], mn[1], mx_[0], mx_[1]))
     pos = np.array(pos, np.int32)
     par = np.array(par, np.int16)
-    cost = rs.integers(200, 6000, len(pos)).astype(np.int32)
+    cost = (rs.integers(200, 6000, len(pos)) * cost_scale).astype(np.int32)
     cost[::9] = 0                                                         # nothing beats the start
     return pos, par, cost

@@ -21,18 +21,19 @@ def _host(t, bd):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("size", [(1920, 1088), (80, 48), (176, 144), (72, 40)])
+@pytest.mark.parametrize("size", [(1920, 1088), (80, 48), (176, 144), (976, 32)])
 @pytest.mark.parametrize("variant", ["default", "nt", "plain", "unaligned"])
 def test_hpel_filter(hip, oracle, bd, size, variant):
-    """Every kernel form hpel_filter can take: at 8 bit the line-aligned strips (widths that are
-    a multiple of 16), the 62-lane strips (72 wide) and, for planes whose rows are not 16-byte
+    """Every kernel form hpel_filter can take: at 8 bit the line-aligned strips, the 62-lane strips
+    (976 wide: the right border piece would start a 64-piece chunk of its own) and, for planes
+    whose rows are not 16-byte
     aligned (unaligned: the origin moved 4 pixels right), the fused LDS tiles, which also serve
     10 bit; with the default store policy, nontemporal stores forced (nt) or plain stores."""
     if variant in ("nt", "plain"):
         _x().set_variant("X264HIP_STREAM_NT", 1 if variant == "nt" else 0)
     from x264hip import synth
     W, H = size
-    if variant == "unaligned" and W > 200:
+    if variant == "unaligned" and W > 1000:
         pytest.skip("the shifted origin needs stride slack")
     gen = synth.make_sequence if W > 100 else synth.random_planes
     planes, stride, origin = gen(2, W, H, bd)
@@ -49,7 +50,7 @@ def test_hpel_filter(hip, oracle, bd, size, variant):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("W,H", [(176, 144), (72, 40)])
+@pytest.mark.parametrize("W,H", [(176, 144), (976, 32)])
 def test_hpel_filter_extremes(hip, oracle, bd, W, H):
     """Pixels 0 / PIXEL_MAX only, so the 6-tap sums reach both ends of every clip
     (H and V: -10 * max .. 42 * max before the shift; centre far beyond int16)."""

@@ -1276,7 +1276,11 @@ hipError_t la_status_begin( hipStream_t stream, uint32_t **word )
     hipError_t e = la_status_get( stream, &st );
     if( e != hipSuccess )
         return e;
-    if( st->pending && hipEventQuery( st->ev ) == hipSuccess )
+    // no event query under capture (it would invalidate the capture): the report waits
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if( (e = hipStreamIsCapturing( stream, &cs )) != hipSuccess )
+        return e;
+    if( cs == hipStreamCaptureStatusNone && st->pending && hipEventQuery( st->ev ) == hipSuccess )
     {
         st->pending = false;
         if( *(volatile uint32_t *)st->host )

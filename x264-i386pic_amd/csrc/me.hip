@@ -914,9 +914,9 @@ template hipError_t launch_me_search_esa<10>( const uint16_t *, intptr_t, intptr
 // so one step's loads are one contiguous, coalesced run of the table.  A lane's columns are
 // fixed, so their cost_mv terms are read once; the row term once per step.  Each entry's
 // key (cost << 12 | raster index in the clipped, width-rounded window) is built as
-// sat( (sad << 12) + C[k] + S ) with C[k] = 0xC0000000 outside the window (valid keys stay
-// below 392958 << 12 + 4096 < 0xC0000000 at either depth; 0xC0000000 + (261888 << 12) does
-// not wrap), a wave min picks the lowest cost and, among equal costs, the first in raster
+// sat( sat( (sad << 12) + C[k] ) + S ) with C[k] = all ones outside the window or the table's
+// columns, so whatever such an entry holds (a full 10-bit table's padding columns are never
+// written) its key saturates (valid keys stay below 392958 << 12 + 4096), a wave min picks the lowest cost and, among equal costs, the first in raster
 // order -- what the strict-< scan of the reference keeps -- and it replaces the predictor
 // result only if strictly better (COPY3_IF_LT, me.h:87-93).
 // Table geometry: rows = 2R+1 at `pitch`, `cols` valid columns, window origin (ox, oy)
@@ -952,7 +952,7 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
     {
         const int tx = 4 * ch + k, mx = ox + tx;
         const bool in = tx < cols && mx >= min_x && mx < min_x + width;
-        ck[k] = in ? ((uint32_t)cost_mv[mx * 4 - mvpx] << 12) + (uint32_t)(mx - min_x) : 0xC0000000u;
+        ck[k] = in ? ((uint32_t)cost_mv[mx * 4 - mvpx] << 12) + (uint32_t)(mx - min_x) : 0xFFFFFFFFu;
     }
     uint32_t key = 0xFFFFFFFFu;
     if( rr < rps && width > 0 )
@@ -972,7 +972,7 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
             }
 #pragma unroll
             for( int k = 0; k < 4; k++ )
-                key = min( key, __builtin_elementwise_add_sat( (s[k] << 12) + ck[k], S ) );
+                key = min( key, __builtin_elementwise_add_sat( __builtin_elementwise_add_sat( s[k] << 12, ck[k] ), S ) );
         }
     }
 #pragma unroll
