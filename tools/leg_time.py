@@ -1,0 +1,43 @@
+#!/usr/bin/env python3
+"""Run bench.py side legs alone on the bench's 16-pair 1080p workload (for rocprofv3 trace /
+PMC passes and A/Bs): leg_time.py LEG [steps] [pairs] with LEG one of esa (the ESA table and
+fused legs, then refine_subpel chained from the ESA decisions), full8 (the quadrant tables),
+tesa.  Prints the legs' JSON."""
+import json
+import os
+import sys
+import types
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    leg = sys.argv[1]
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
+    F = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+    x = bench.load_package()
+    x.init(0)
+    from x264hip import synth
+    a = types.SimpleNamespace(steps=steps, warmup=5, range=16, tframes=64)
+    W, H = 1920, 1088
+    mbw, mbh = W // 16, H // 16
+    planes, stride, origin = synth.make_sequence(F + 1, W, H, 8)
+    dev = torch.from_numpy(planes).cuda()
+    fs = planes[0].size
+    if leg == "esa":
+        res = bench.rates_esa(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
+    elif leg == "full8":
+        res = bench.rates_full8(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
+    elif leg == "tesa":
+        res = bench.rates_tesa(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
+    else:
+        raise SystemExit("unknown leg %s" % leg)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()

@@ -932,9 +932,11 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
 {
     using chunk = typename std::conditional<BD == 8, uint2, uint4>::type;
     const int lane = threadIdx.x & 63;
-    const int64_t mb = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    // the MB index is wave-uniform: made a scalar, so its par / origin / init_cost words are
+    // scalar loads and the address path carries only the table and cost_mv reads
+    const int mb = __builtin_amdgcn_readfirstlane( (int)((blockIdx.x * blockDim.x + threadIdx.x) >> 6) );
     if( mb >= nmb )
-        return;                                                    // wave-uniform
+        return;
     const int W = 2 * R + 1;
     const int nch = pitch >> 2, rps = 64 / nch;                    // pitch <= 64: >= 4 rows per step
     const int rr = lane / nch, ch = lane - rr * nch;
@@ -946,33 +948,43 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
     const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
     const int y0 = max( min_y, oy ), y1 = min( max_y, oy + W - 1 );
     const chunk *t = (const chunk *)(table + mb * (int64_t)(W * pitch)) + ch;
+    // the MB's cost_mv terms in two gathers -- column c's in lane c, table row r's in lane r --
+    // handed to the lanes that use them by ds_bpermute (the LDS crossbar, not the address
+    // path the table loads need): a lane's four columns once, a row's term once per step
+    const int cl = min( lane, pitch - 1 ), mxl = ox + cl;
+    const bool cin = cl < cols && mxl >= min_x && mxl < min_x + width;
+    const uint32_t ckl = cin ? ((uint32_t)cost_mv[mxl * 4 - mvpx] << 12) + (uint32_t)(mxl - min_x) : 0xFFFFFFFFu;
+    const int myl = min( max( oy + lane, y0 ), y1 );
+    const uint32_t Sl = ((uint32_t)cost_mv[myl * 4 - mvpy] << 12) + (uint32_t)((myl - min_y) * width);
     uint32_t ck[4];
 #pragma unroll
     for( int k = 0; k < 4; k++ )
-    {
-        const int tx = 4 * ch + k, mx = ox + tx;
-        const bool in = tx < cols && mx >= min_x && mx < min_x + width;
-        ck[k] = in ? ((uint32_t)cost_mv[mx * 4 - mvpx] << 12) + (uint32_t)(mx - min_x) : 0xFFFFFFFFu;
-    }
+        ck[k] = (uint32_t)__builtin_amdgcn_ds_bpermute( 4 * (4 * ch + k), (int)ckl );
     uint32_t key = 0xFFFFFFFFu;
-    if( rr < rps && width > 0 )
+    if( width > 0 )
     {
-        for( int my = y0 + rr; my <= y1; my += rps )
+        for( int my0 = y0; my0 <= y1; my0 += rps )                  // wave-uniform trip count
         {
-            const chunk v = t[(my - oy) * nch];
-            const uint32_t S = ((uint32_t)cost_mv[my * 4 - mvpy] << 12) + (uint32_t)((my - min_y) * width);
-            uint32_t s[4];
-            if constexpr( BD == 8 )
+            const int my = my0 + rr;
+            const bool live = rr < rps && my <= y1;
+            const uint32_t S = (uint32_t)__builtin_amdgcn_ds_bpermute( 4 * min( my - oy, 63 ), (int)Sl );
+            if( live )
             {
-                s[0] = v.x & 0xffff; s[1] = v.x >> 16; s[2] = v.y & 0xffff; s[3] = v.y >> 16;
-            }
-            else
-            {
-                s[0] = v.x; s[1] = v.y; s[2] = v.z; s[3] = v.w;
-            }
+                const chunk v = t[(my - oy) * nch];
+                uint32_t s[4];
+                if constexpr( BD == 8 )
+                {
+                    s[0] = v.x & 0xffff; s[1] = v.x >> 16; s[2] = v.y & 0xffff; s[3] = v.y >> 16;
+                }
+                else
+                {
+                    s[0] = v.x; s[1] = v.y; s[2] = v.z; s[3] = v.w;
+                }
 #pragma unroll
-            for( int k = 0; k < 4; k++ )
-                key = min( key, __builtin_elementwise_add_sat( __builtin_elementwise_add_sat( s[k] << 12, ck[k] ), S ) );
+                for( int k = 0; k < 4; k++ )
+                    key = min( key, __builtin_elementwise_add_sat(
+                                        __builtin_elementwise_add_sat( s[k] << 12, ck[k] ), S ) );
+            }
         }
     }
 #pragma unroll

@@ -29,6 +29,23 @@ static const uint8_t k_subpel_iterations[12][4] = { { 0, 0, 0, 0 }, { 1, 1, 0, 0
                                                     { 0, 0, 4, 10 }, { 0, 0, 4, 10 }, { 0, 0, 4, 10 },
                                                     { 0, 0, 4, 10 } };
 
+// NDW packed dwords at an arbitrary pixel address: the NDW + 1 dword-aligned words holding
+// them (one vector load), realigned (the extra word re-reads the last one when aligned)
+template <int NDW>
+__device__ __forceinline__ void load_al( const void *p, uint32_t (&out)[NDW] )
+{
+    typedef const __attribute__( ( address_space( 1 ) ) ) uint32_t gword;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    gword *base = (gword *)((uintptr_t)p & ~(uintptr_t)3);
+    uint32_t w[NDW + 1];
+#pragma unroll
+    for( int i = 0; i <= NDW; i++ )
+        w[i] = base[i];
+#pragma unroll
+    for( int i = 0; i < NDW; i++ )
+        out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
+}
+
 // the lane's 8x4 tile of get_ref( mvx, mvy ) scored against its fenc tile: SAD, or the sum of
 // |coef| of the tile's two 4x4 Hadamards (even; halved by the caller)
 template <int BD, bool SATD>
@@ -43,20 +60,25 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
     const int i0 = c_ref0[idx], i1 = c_ref1[idx];
     const pixel *s1 = (i0 == 0 ? q[0] : i0 == 1 ? q[1] : i0 == 2 ? q[2] : q[3]) + off + ((mvy & 3) == 3) * rs;
     const pixel *s2 = (i1 == 0 ? q[0] : i1 == 1 ? q[1] : i1 == 2 ? q[2] : q[3]) + off + ((mvx & 3) == 3);
-    if( !(idx & 5) )
-        s2 = s1;                            // one plane: avg( a, a ) = a
-    uint32_t r1[4][HDW], r2[4][HDW];
+    // rows as dword-aligned loads realigned with v_alignbyte: the address path takes a
+    // byte-misaligned 8-byte lane load at ~2x the cost of an aligned 12-byte one
+    // (profiles/r01d_ta_probe.txt), and it binds this kernel (TA busy ~100 %, r04d)
+    uint32_t r1[4][HDW];
 #pragma unroll
     for( int y = 0; y < 4; y++ )
+        load_al<HDW>( s1 + y * rs, r1[y] );
+    if( idx & 5 )                           // two planes: the rounding average (one plane: avg( a, a ) = a)
     {
-        load_row_u<HDW>( s1 + y * rs, r1[y] );
-        load_row_u<HDW>( s2 + y * rs, r2[y] );
+        uint32_t r2[4][HDW];
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+            load_al<HDW>( s2 + y * rs, r2[y] );
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+#pragma unroll
+            for( int k = 0; k < HDW; k++ )
+                r1[y][k] = avg_round<BD>( r1[y][k], r2[y][k] );
     }
-#pragma unroll
-    for( int y = 0; y < 4; y++ )
-#pragma unroll
-        for( int k = 0; k < HDW; k++ )
-            r1[y][k] = avg_round<BD>( r1[y][k], r2[y][k] );
     if constexpr( SATD )
         return satd8x4_packed<BD>( fa, r1 );
     else
@@ -132,10 +154,12 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         uint32_t v = 0;
         if( tile )
             v = satd ? tile_cost<BD, true>( fa, q, rs, mx[g], my[g] ) >> 1 : tile_cost<BD, false>( fa, q, rs, mx[g], my[g] );
+        if( u == 0 )                                      // the group's mv cost, once
+            v += (uint32_t)cmx[mx[g]] + (uint32_t)cmy[my[g]];
         v = group_sum( v );
 #pragma unroll
         for( int k = 0; k < 4; k++ )
-            c[k] = (int)__shfl( (int)v, sbase + 8 * k ) + (int)cmx[mx[k]] + (int)cmy[my[k]];
+            c[k] = (int)__shfl( (int)v, sbase + 8 * k );
     };
     auto eval1 = [&]( int mx, int my, bool satd ) {
         const int m4x[4] = { mx, mx, mx, mx }, m4y[4] = { my, my, my, my };
