@@ -416,76 +416,8 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     wall, ev_ms = timed(istep, a.steps, a.warmup, world, graph=True)
     res["lowres_intra_mbs_per_s"] = world * a.steps * F * mbw * mbh / wall
     res["lowres_intra_launch_ms"] = ev_ms
-    # the lookahead's P-frame lowres motion search on the same planes: frame k+1 against
-    # frame k for the F-1 pairs, HEX + subme 4 (lowres_context_init for subme > 1), range 16,
-    # lambda 1, cost_mv[X264_LOOKAHEAD_QP] over +-8*512 (analyse.c:143-157)
-    span = 8 * 512
-    ii = np.arange(span + 1, dtype=np.float32)
-    logs = np.where(ii == 0, np.float32(0.718), np.log2(ii + np.float32(1)) * np.float32(2) + np.float32(1.718))
-    half = np.minimum((logs.astype(np.float32) + np.float32(0.5)).astype(np.int64), 65535).astype(np.uint16)
-    cm = torch.from_numpy(np.concatenate([half[:0:-1], half]).view(np.int16)).cuda()
-    lref = [p[:-1] for p in louts]
-    lint = iouts[0][1:]
-    louts2 = x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span))
-
-    def lastep():
-        x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2,
-                            check=False)
-    # (the lookahead launches are asynchronous: the wavefront status is checked after each leg)
-    wall, ev_ms = timed(lastep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
-    x.lowres_status()
-    res["lowres_me_pairs_per_s"] = world * max(1, a.steps // 5) * (F - 1) / wall
-    res["lowres_me_launch_ms"] = ev_ms
-    res["lowres_me_pairs_per_launch"] = F - 1
-    # the same search as x264 runs it with i_lookahead_threads = T (slicetype.c:901-918): T
-    # slices, each its own wavefront (different predictors at slice ends, so different results,
-    # as in the reference)
-    for T in (4, 8):
-        def lsstep(T=T):
-            x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2,
-                                n_slices=T, check=False)
-        wall, ev_ms = timed(lsstep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
-        x.lowres_status()
-        res["lowres_me_slices%d_pairs_per_s" % T] = world * max(1, a.steps // 5) * (F - 1) / wall
-        res["lowres_me_slices%d_launch_ms" % T] = ev_ms
-    # the same search at a full-chip batch: 16 copies of those pairs in one launch (one
-    # workgroup per pair, 240 of the 256 CUs busy) -- its throughput when the lookahead
-    # hands over many (b, p0) pairs at once; the 15-pair leg above is per-pair latency
-    nrep = 16
-    bf = louts[0][1:].repeat(nrep, 1, 1)
-    br = [p[:-1].repeat(nrep, 1, 1) for p in louts]
-    bi = lint.repeat(nrep, 1)
-    bouts2 = x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span))
-
-    def lbstep():
-        x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span), outs=bouts2, check=False)
-    wall, ev_ms = timed(lbstep, max(1, a.steps // 10), 2, world)
-    x.lowres_status()
-    res["lowres_me_batch_pairs_per_s"] = world * max(1, a.steps // 10) * bf.shape[0] / wall
-    res["lowres_me_batch_launch_ms"] = ev_ms
-    res["lowres_me_batch_pairs_per_launch"] = int(bf.shape[0])
-    del bf, br, bi, bouts2
-    # the B-frame leg on the same planes: (p0, b, p1) = (k, k+1, k+2) for the F-2 triplets, both
-    # lists searched (a fresh slicetype_frame_cost with b_bidir), p1's list-0 mvs against p0 from
-    # one untimed P search as the bidir predictor, equal weights (i_bipred_weight 32, dsf 128)
-    ls_ = x.plane_stride(lw // 2)
-    nt = F - 2
-    nmb_ = mbw * mbh
-    p1m = x.lowres_inter_cost(louts[0][2:], [p[:-2] for p in louts], ls_, mbw, mbh, iouts[0][2:], (cm, span))[0]
-    bm = [torch.empty((nt, nmb_, 2), dtype=torch.int16, device="cuda") for _ in range(2)]
-    bk = [torch.empty((nt, nmb_), dtype=torch.int32, device="cuda") for _ in range(2)]
-    bargs = (louts[0][1:-1], [p[:-2] for p in louts], [p[2:] for p in louts], ls_, mbw, mbh, (cm, span), 3,
-             bm[0], bk[0], bm[1], bk[1])
-    bouts = x.lowres_bidir_cost(*bargs, p1_mvs=p1m)
-
-    def bstep():
-        x.lowres_bidir_cost(*bargs, p1_mvs=p1m, outs=bouts, check=False)
-    wall, ev_ms = timed(bstep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
-    x.lowres_status()
-    res["lowres_bidir_triplets_per_s"] = world * max(1, a.steps // 5) * nt / wall
-    res["lowres_bidir_launch_ms"] = ev_ms
-    res["lowres_bidir_triplets_per_launch"] = nt
-    del louts, iouts, louts2, lref, lint, p1m, bm, bk, bouts, bargs
+    res.update(rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F))
+    del louts, iouts
     nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
     bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)
@@ -563,6 +495,83 @@ def tesa_params(mbw, mbh, F, R, centre=(-3, -2)):
     logs = np.where(i == 0, 0.718, 2.0 * np.log2(np.abs(i) + 1) + 1.718)
     cm = np.minimum((4 * logs + 0.5).astype(np.int64), 65535).astype(np.uint16)
     return par, init, cm, span
+
+
+def rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F):
+    """The lookahead's lowres motion searches over the F lowres frames (frame_init_lowres
+    planes louts, intra costs iouts): P pairs (1, 4 and 8 slices, and a 240-pair batch) and
+    B triplets."""
+    res = {}
+    # the lookahead's P-frame lowres motion search on the same planes: frame k+1 against
+    # frame k for the F-1 pairs, HEX + subme 4 (lowres_context_init for subme > 1), range 16,
+    # lambda 1, cost_mv[X264_LOOKAHEAD_QP] over +-8*512 (analyse.c:143-157)
+    span = 8 * 512
+    ii = np.arange(span + 1, dtype=np.float32)
+    logs = np.where(ii == 0, np.float32(0.718), np.log2(ii + np.float32(1)) * np.float32(2) + np.float32(1.718))
+    half = np.minimum((logs.astype(np.float32) + np.float32(0.5)).astype(np.int64), 65535).astype(np.uint16)
+    cm = torch.from_numpy(np.concatenate([half[:0:-1], half]).view(np.int16)).cuda()
+    lref = [p[:-1] for p in louts]
+    lint = iouts[0][1:]
+    louts2 = x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span))
+
+    def lastep():
+        x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2,
+                            check=False)
+    # (the lookahead launches are asynchronous: the wavefront status is checked after each leg)
+    wall, ev_ms = timed(lastep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+    x.lowres_status()
+    res["lowres_me_pairs_per_s"] = world * max(1, a.steps // 5) * (F - 1) / wall
+    res["lowres_me_launch_ms"] = ev_ms
+    res["lowres_me_pairs_per_launch"] = F - 1
+    # the same search as x264 runs it with i_lookahead_threads = T (slicetype.c:901-918): T
+    # slices, each its own wavefront (different predictors at slice ends, so different results,
+    # as in the reference)
+    for T in (4, 8):
+        def lsstep(T=T):
+            x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span), outs=louts2,
+                                n_slices=T, check=False)
+        wall, ev_ms = timed(lsstep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+        x.lowres_status()
+        res["lowres_me_slices%d_pairs_per_s" % T] = world * max(1, a.steps // 5) * (F - 1) / wall
+        res["lowres_me_slices%d_launch_ms" % T] = ev_ms
+    # the same search at a full-chip batch: 16 copies of those pairs in one launch (one
+    # workgroup per pair, 240 of the 256 CUs busy) -- its throughput when the lookahead
+    # hands over many (b, p0) pairs at once; the 15-pair leg above is per-pair latency
+    nrep = 16
+    bf = louts[0][1:].repeat(nrep, 1, 1)
+    br = [p[:-1].repeat(nrep, 1, 1) for p in louts]
+    bi = lint.repeat(nrep, 1)
+    bouts2 = x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span))
+
+    def lbstep():
+        x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span), outs=bouts2, check=False)
+    wall, ev_ms = timed(lbstep, max(1, a.steps // 10), 2, world)
+    x.lowres_status()
+    res["lowres_me_batch_pairs_per_s"] = world * max(1, a.steps // 10) * bf.shape[0] / wall
+    res["lowres_me_batch_launch_ms"] = ev_ms
+    res["lowres_me_batch_pairs_per_launch"] = int(bf.shape[0])
+    del bf, br, bi, bouts2
+    # the B-frame leg on the same planes: (p0, b, p1) = (k, k+1, k+2) for the F-2 triplets, both
+    # lists searched (a fresh slicetype_frame_cost with b_bidir), p1's list-0 mvs against p0 from
+    # one untimed P search as the bidir predictor, equal weights (i_bipred_weight 32, dsf 128)
+    ls_ = x.plane_stride(lw // 2)
+    nt = F - 2
+    nmb_ = mbw * mbh
+    p1m = x.lowres_inter_cost(louts[0][2:], [p[:-2] for p in louts], ls_, mbw, mbh, iouts[0][2:], (cm, span))[0]
+    bm = [torch.empty((nt, nmb_, 2), dtype=torch.int16, device="cuda") for _ in range(2)]
+    bk = [torch.empty((nt, nmb_), dtype=torch.int32, device="cuda") for _ in range(2)]
+    bargs = (louts[0][1:-1], [p[:-2] for p in louts], [p[2:] for p in louts], ls_, mbw, mbh, (cm, span), 3,
+             bm[0], bk[0], bm[1], bk[1])
+    bouts = x.lowres_bidir_cost(*bargs, p1_mvs=p1m)
+
+    def bstep():
+        x.lowres_bidir_cost(*bargs, p1_mvs=p1m, outs=bouts, check=False)
+    wall, ev_ms = timed(bstep, max(1, a.steps // 5), max(1, a.warmup // 10), world)
+    x.lowres_status()
+    res["lowres_bidir_triplets_per_s"] = world * max(1, a.steps // 5) * nt / wall
+    res["lowres_bidir_launch_ms"] = ev_ms
+    res["lowres_bidir_triplets_per_launch"] = nt
+    return res
 
 
 def rates_tesa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):

@@ -2,7 +2,7 @@
 """Run bench.py side legs alone on the bench's 16-pair 1080p workload (for rocprofv3 trace /
 PMC passes and A/Bs): leg_time.py LEG [steps] [pairs] with LEG one of esa (the ESA table and
 fused legs, then refine_subpel chained from the ESA decisions), full8 (the quadrant tables),
-tesa.  Prints the legs' JSON."""
+tesa, la (the lookahead's P and B searches).  Prints the legs' JSON."""
 import json
 import os
 import sys
@@ -34,6 +34,10 @@ def main():
         res = bench.rates_full8(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
     elif leg == "tesa":
         res = bench.rates_tesa(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
+    elif leg == "la":
+        louts, _ = x.frame_init_lowres(dev[:-1], origin, stride, W, H)
+        iouts = x.lowres_intra_cost(louts[0], x.plane_stride(W // 2), mbw, mbh, True, True, 1)
+        res = bench.rates_lookahead(x, a, 1, louts, iouts, W, mbw, mbh, F)
     else:
         raise SystemExit("unknown leg %s" % leg)
     print(json.dumps(res))

@@ -70,6 +70,27 @@ __device__ __forceinline__ void load_packed( const void *p, uint32_t (&out)[NDW]
         out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
 }
 
+// NDW packed dwords at an arbitrary pixel address from the dword-aligned words holding them
+// (one vector load of NDW + 1 words; the last re-reads word NDW-1 when aligned, so no byte
+// past the row's dwords is touched), realigned with v_alignbyte.  On gfx950 the address path
+// takes a byte-misaligned 8-byte lane load at ~2x the cycles of an aligned 12-byte one and a
+// misaligned 16-byte one at ~4x (tools/ta_probe.hip, profiles/r01d_ta_probe.txt).
+template <int NDW>
+__device__ __forceinline__ void load_al( const void *p, uint32_t (&out)[NDW] )
+{
+    typedef const __attribute__( ( address_space( 1 ) ) ) uint32_t gword;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    gword *base = (gword *)((uintptr_t)p & ~(uintptr_t)3);
+    uint32_t w[NDW + 1];
+#pragma unroll
+    for( int i = 0; i < NDW; i++ )
+        w[i] = base[i];
+    w[NDW] = base[sh ? NDW : NDW - 1];
+#pragma unroll
+    for( int i = 0; i < NDW; i++ )
+        out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
+}
+
 // rounding-up average of packed pixels (pixel_avg, reference common/mc.c:57): one
 // v_lerp_u8 per dword at 8 bit
 template <int BD> __device__ __forceinline__ uint32_t avg_round( uint32_t a, uint32_t b )

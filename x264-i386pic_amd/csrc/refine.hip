@@ -29,23 +29,6 @@ static const uint8_t k_subpel_iterations[12][4] = { { 0, 0, 0, 0 }, { 1, 1, 0, 0
                                                     { 0, 0, 4, 10 }, { 0, 0, 4, 10 }, { 0, 0, 4, 10 },
                                                     { 0, 0, 4, 10 } };
 
-// NDW packed dwords at an arbitrary pixel address: the NDW + 1 dword-aligned words holding
-// them (one vector load), realigned (the extra word re-reads the last one when aligned)
-template <int NDW>
-__device__ __forceinline__ void load_al( const void *p, uint32_t (&out)[NDW] )
-{
-    typedef const __attribute__( ( address_space( 1 ) ) ) uint32_t gword;
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
-    gword *base = (gword *)((uintptr_t)p & ~(uintptr_t)3);
-    uint32_t w[NDW + 1];
-#pragma unroll
-    for( int i = 0; i <= NDW; i++ )
-        w[i] = base[i];
-#pragma unroll
-    for( int i = 0; i < NDW; i++ )
-        out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
-}
-
 // the lane's 8x4 tile of get_ref( mvx, mvy ) scored against its fenc tile: SAD, or the sum of
 // |coef| of the tile's two 4x4 Hadamards (even; halved by the caller)
 template <int BD, bool SATD>
