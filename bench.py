@@ -418,6 +418,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     res["lowres_intra_launch_ms"] = ev_ms
     res.update(rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F))
     del louts, iouts
+    res.update(rates_weightp(x, a, world, dev, origin, stride, mbw, mbh))
     nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
     bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)
@@ -497,6 +498,54 @@ def tesa_params(mbw, mbh, F, R, centre=(-3, -2)):
     return par, init, cm, span
 
 
+def lookahead_cost_mv():
+    """cost_mv[X264_LOOKAHEAD_QP] over +-8*512 (analyse.c:143-157, lambda 1): (device table, mvd-0 index)"""
+    span = 8 * 512
+    ii = np.arange(span + 1, dtype=np.float32)
+    logs = np.where(ii == 0, np.float32(0.718), np.log2(ii + np.float32(1)) * np.float32(2) + np.float32(1.718))
+    half = np.minimum((logs.astype(np.float32) + np.float32(0.5)).astype(np.int64), 65535).astype(np.uint16)
+    return torch.from_numpy(np.concatenate([half[:0:-1], half]).view(np.int16)).cuda(), span
+
+
+def rates_weightp(x, a, world, dev, origin, stride, mbw, mbh):
+    """x264_weights_analyse (slicetype.c:284-501) on a fade of the bench's first frame pair (frame 1
+    scaled by 0.85, +12; the bench sequence is luma only): the lookahead's call (the guessed weight
+    and the weighted lowres plane, slicetype.c:859-862) and the encoder's call at subme 7 with the
+    pair's lowres mvs (slicetype.c:1939-1943).  Each call is synchronous (one batch of candidate
+    costs, a stream synchronise, the host's replay of the search): per-call wall time.  Beside it
+    the frame statistics kernel (ac_energy_mb's sums, ratecontrol.c:225-257) per 1080p frame."""
+    W, H = mbw * 16, mbh * 16
+    fade = (dev[1].float() * 0.85 + 12).round().clamp(0, 255).to(torch.uint8)
+    pair = torch.stack([dev[0], fade])
+    louts, ls = x.frame_init_lowres(pair, origin, stride, W, H)
+    intra = x.lowres_intra_cost(louts[0][1:], ls, mbw, mbh, True, True, 1)[0]
+    st = torch.empty(6, dtype=torch.int64, device="cuda")
+
+    def sstep():
+        x.frame_pixel_stats(pair[1], origin, stride, mbw, mbh, out=st)
+    wall, ev_ms = timed(sstep, a.steps, a.warmup, world, graph=True)
+    res = {"pixel_stats_frames_per_s": world * a.steps / wall, "pixel_stats_launch_ms": ev_ms}
+    stats = []
+    for i in range(2):
+        v = x.frame_pixel_stats(pair[i], origin, stride, mbw, mbh).cpu().numpy().view(np.uint64)
+        stats.append(([int(t) for t in v[:3]], [int(t) for t in v[3:]]))
+    cm, span = lookahead_cost_mv()
+    mvs = x.lowres_inter_cost(louts[0][1:], [p[:1] for p in louts], ls, mbw, mbh, intra, (cm, span))[0][0]
+    wl = torch.zeros_like(louts[0][0])
+    fl, rl = louts[0][1], [p[0] for p in louts]
+    for name, kw in (("la", dict(b_lookahead=True, weighted_lowres=wl)),
+                     ("enc", dict(b_lookahead=False, subme=7, mvs=mvs))):
+        w = None
+
+        def wstep(kw=kw):
+            nonlocal w
+            w = x.weights_analyse(fl, rl, ls, mbw, mbh, intra[0], stats[1], stats[0], **kw)
+        wall, _ = timed(wstep, max(1, a.steps // 2), 2, world)
+        res["weightp_%s_ms" % name] = wall / max(1, a.steps // 2) * 1e3
+        res["weightp_%s_weight" % name] = list(w[0][0])
+    return res
+
+
 def rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F):
     """The lookahead's lowres motion searches over the F lowres frames (frame_init_lowres
     planes louts, intra costs iouts): P pairs (1, 4 and 8 slices, and a 240-pair batch) and
@@ -505,11 +554,7 @@ def rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F):
     # the lookahead's P-frame lowres motion search on the same planes: frame k+1 against
     # frame k for the F-1 pairs, HEX + subme 4 (lowres_context_init for subme > 1), range 16,
     # lambda 1, cost_mv[X264_LOOKAHEAD_QP] over +-8*512 (analyse.c:143-157)
-    span = 8 * 512
-    ii = np.arange(span + 1, dtype=np.float32)
-    logs = np.where(ii == 0, np.float32(0.718), np.log2(ii + np.float32(1)) * np.float32(2) + np.float32(1.718))
-    half = np.minimum((logs.astype(np.float32) + np.float32(0.5)).astype(np.int64), 65535).astype(np.uint16)
-    cm = torch.from_numpy(np.concatenate([half[:0:-1], half]).view(np.int16)).cuda()
+    cm, span = lookahead_cost_mv()
     lref = [p[:-1] for p in louts]
     lint = iouts[0][1:]
     louts2 = x.lowres_inter_cost(louts[0][1:], lref, x.plane_stride(lw // 2), mbw, mbh, lint, (cm, span))

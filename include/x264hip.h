@@ -153,6 +153,23 @@ enum
 
 struct x264hip_run_level_t;   /* opaque; only its pointer appears (quant.h:61-63) */
 
+/* x264_weight_t (common/mc.h:236-245) as x264_weights_analyse leaves it: weighted = the
+ * reference's weightfn != NULL (SET_WEIGHT, mc.h:249-258), the other fields whatever the
+ * search wrote, weighted or not */
+typedef struct x264hip_weight_t
+{
+    int32_t weighted, scale, denom, offset;
+} x264hip_weight_t;
+
+/* cost kinds of x264hip_*_weight_cost_batch (slicetype.c:191-282) */
+enum
+{
+    X264HIP_WCOST_LUMA = 0,        /* weight_cost_luma: lowres 8x8 mbcmp, min intra cost */
+    X264HIP_WCOST_CHROMA420 = 1,   /* weight_cost_chroma, 8x8 asd8 of an NV12 plane */
+    X264HIP_WCOST_CHROMA422 = 2,   /* weight_cost_chroma, 8x16 asd8 of an NV16 plane */
+    X264HIP_WCOST_CHROMA444 = 3,   /* weight_cost_chroma444: 16x16 mbcmp of a chroma plane */
+};
+
 /*----------------------------------------------------------------------------
  * Table declarations, instantiated per bit depth.
  *--------------------------------------------------------------------------*/
@@ -897,6 +914,62 @@ int x264hip_##BD##_mb_dequant_idct_add( int transform, const dctcoef *dct, int m
                                         intptr_t pred_stride, intptr_t pred_frame_stride,       \
                                         pixel *recon, intptr_t recon_stride,                    \
                                         intptr_t recon_frame_stride, void *stream );               \
+                                                                                                \
+/* the frame statistics x264_weights_analyse reads: fenc->i_pixel_sum[3] / i_pixel_ssd[3] as    \
+ * x264_adaptive_quant_frame leaves them for a progressive frame (ac_energy_mb's stores,          \
+ * encoder/ratecontrol.c:225-257, 289-299, then the mean removal of :406-414; the sum wraps as    \
+ * its uint32 field does).  chroma_format 0 = 4:0:0, 1 = 4:2:0, 2 = 4:2:2 (chroma_u = the        \
+ * interleaved NV12 / NV16 plane, chroma_v unused), 3 = 4:4:4 (chroma_u, chroma_v).  Planes      \
+ * at pixel (0,0).  stats = device uint64[6]: sum[0..2] then ssd[0..2]. */                         \
+int x264hip_##BD##_frame_pixel_stats( const pixel *luma, intptr_t luma_stride,                  \
+                                      const pixel *chroma_u, const pixel *chroma_v,              \
+                                      intptr_t chroma_stride, int mb_width, int mb_height,       \
+                                      int chroma_format, uint64_t *stats, void *stream );        \
+                                                                                                \
+/* weight_cost_luma / weight_cost_chroma / weight_cost_chroma444 (slicetype.c:191-282) of      \
+ * n_cands candidate weights in one batch: costs[i] (device uint32) = the reference's value    \
+ * with cands[i] (host array) as w, i.e. including weight_slice_header_cost when                \
+ * cands[i].weighted, and the unweighted (w == NULL) cost otherwise.  kind                      \
+ * X264HIP_WCOST_*: LUMA -- fenc = fenc->lowres[0], ref[0..3] = ref->lowres[0..3] (only [0]     \
+ * without mvs), stride = i_stride_lowres, intra_cost = fenc->i_intra_cost; CHROMA420/422 --    \
+ * fenc / ref[0] = the NV12 / NV16 planes (plane 0 = U, 1 = V); CHROMA444 -- fenc / ref[0] =    \
+ * one chroma plane.  mvs = fenc->lowres_mvs[0][ref0_distance] (NULL when its first entry is     \
+ * 0x7FFF): the motion-compensated reference of weight_cost_init_luma / _chroma /               \
+ * _chroma444 (slicetype.c:77-168) is formed on the fly; ref planes carry expanded borders.     \
+ * satd = the mbcmp choice; lambda = x264_lambda_tab[X264_LOOKAHEAD_QP]; n_slices as            \
+ * weight_slice_header_cost counts them. */                                                     \
+int x264hip_##BD##_weight_cost_batch( int kind, const pixel *fenc, const pixel *const ref[4],   \
+                                      intptr_t stride, int mb_width, int mb_height,             \
+                                      const uint16_t *intra_cost, const int16_t *mvs, int satd,  \
+                                      int plane, int lambda, int n_slices,                       \
+                                      const x264hip_weight_t *cands, int n_cands,                \
+                                      uint32_t *costs, void *stream );                           \
+                                                                                                \
+/* x264_weights_analyse( h, fenc, ref, b_lookahead ) (encoder/slicetype.c:284-501): the         \
+ * explicit weights of ref for fenc, luma and (outside the lookahead, after a luma weight)      \
+ * chroma.  fenc_lowres / ref_lowres[0..3] / lowres_stride / intra_cost / mvs as                \
+ * weight_cost_batch's LUMA (intra_cost from lowres_intra_cost: the reference computes it       \
+ * first when !fenc->b_intra_calculated, slicetype.c:364-369); fenc_chroma / ref_chroma =       \
+ * { NV12 plane, NULL } or { U, V } (4:4:4), chroma_stride, unused in the lookahead;            \
+ * fenc_sum .. ref_ssd = the frames' i_pixel_sum / i_pixel_ssd (frame_pixel_stats); subme =     \
+ * param i_subpel_refine; satd = the mbcmp choice; weightp_fake = (i_weighted_pred ==           \
+ * X264_WEIGHTP_FAKE).  Writes weights[3] (fenc->weight[0][0..2]), *cost_delta                   \
+ * (fenc->f_weighted_cost_delta[i_delta_index], FAKE only, may be NULL) and, in the lookahead    \
+ * with a luma weight, weighted_lowres (fenc->weighted[0]: at (0,0), lowres_stride, 32-pixel     \
+ * border; NULL = skip) by x264_weight_scale_plane.  Synchronous: every candidate of a plane    \
+ * is scored in one batch on the stream and the host replays the reference's search over the   \
+ * costs (one stream synchronise for luma, one for chroma); not capturable. */                  \
+int x264hip_##BD##_weights_analyse( const pixel *fenc_lowres, const pixel *const ref_lowres[4], \
+                                    intptr_t lowres_stride, int mb_width, int mb_height,        \
+                                    const uint16_t *intra_cost, const int16_t *mvs,             \
+                                    int chroma_format, const pixel *const fenc_chroma[2],       \
+                                    const pixel *const ref_chroma[2], intptr_t chroma_stride,   \
+                                    const uint32_t fenc_sum[3], const uint64_t fenc_ssd[3],     \
+                                    const uint32_t ref_sum[3], const uint64_t ref_ssd[3],       \
+                                    int b_lookahead, int subme, int satd, int lambda,           \
+                                    int n_slices, int weightp_fake, pixel *weighted_lowres,     \
+                                    x264hip_weight_t weights[3], float *cost_delta,             \
+                                    void *stream );                                             \
                                                                                                 \
 /* lookahead input: x264_frame_init_lowres (mc.c:458-507, frame.c:627-631) of n_frames          \
  * luma planes of width x height (i_width[0] x i_lines[0]; src at (0,0)): the four              \

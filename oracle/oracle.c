@@ -2892,3 +2892,537 @@ void FN(lowres_bidir_cost_ex)( const pixel *fenc, const pixel *const ref_a[4], c
             lowres_costs[mb] = (uint16_t)((bcost < 16383 ? bcost : 16383) + (list_used << 14));
         }
 }
+
+/*============================================================================
+ * weighted-prediction analysis — reference encoder/slicetype.c:63-501 (the
+ * weight search), encoder/ratecontrol.c:225-257,406-414 (the frame statistics it
+ * reads), common/mc.c:252-283 (mc_chroma)
+ *==========================================================================*/
+#include <math.h>
+
+/* mc_chroma (common/mc.c:252-283): eighth-pel bilinear of an interleaved (NV12) plane
+ * into separate U and V blocks */
+void FN(mc_chroma)( pixel *dstu, pixel *dstv, intptr_t ds, const pixel *src, intptr_t ss, int mvx, int mvy,
+                    int w, int h )
+{
+    const int dx = mvx & 7, dy = mvy & 7;
+    const int cA = (8 - dx) * (8 - dy), cB = dx * (8 - dy), cC = (8 - dx) * dy, cD = dx * dy;
+    src += (mvy >> 3) * ss + (mvx >> 3) * 2;
+    for( int y = 0; y < h; y++, dstu += ds, dstv += ds, src += ss )
+    {
+        const pixel *s1 = src + ss;
+        for( int x = 0; x < w; x++ )
+        {
+            dstu[x] = (pixel)((cA * src[2*x] + cB * src[2*x + 2] + cC * s1[2*x] + cD * s1[2*x + 2] + 32) >> 6);
+            dstv[x] = (pixel)((cA * src[2*x + 1] + cB * src[2*x + 3] + cC * s1[2*x + 1] + cD * s1[2*x + 3] + 32) >> 6);
+        }
+    }
+}
+
+/* The frame statistics x264_weights_analyse reads (fenc->i_pixel_sum / i_pixel_ssd):
+ * ac_energy_mb's stores over every MB of a progressive frame (ratecontrol.c:225-257,
+ * 289-299; PIXEL_VAR_C per plane, chroma deinterleaved as load_deinterleave_chroma_fenc
+ * does), the uint32 sum wrapping as the field does, then the mean removal of
+ * ratecontrol.c:406-414.  chroma_format 0 = 4:0:0, 1 = 4:2:0, 2 = 4:2:2 (NV12/NV16 plane 1),
+ * 3 = 4:4:4 (planes 1 and 2). */
+void FN(frame_pixel_stats)( const pixel *const plane[3], const intptr_t stride[3], int mb_width, int mb_height,
+                            int chroma_format, uint32_t sum[3], uint64_t ssd[3] )
+{
+    const int hs = chroma_format == 1 || chroma_format == 2, vs = chroma_format == 1;
+    for( int i = 0; i < 3; i++ )
+        sum[i] = 0, ssd[i] = 0;
+    for( int mby = 0; mby < mb_height; mby++ )
+        for( int mbx = 0; mbx < mb_width; mbx++ )
+        {
+            uint64_t v = FN(var)( 0, plane[0] + 16 * mbx + 16 * mby * stride[0], stride[0] );
+            sum[0] += (uint32_t)v;
+            ssd[0] += v >> 32;
+            if( chroma_format == 3 )
+                for( int p = 1; p <= 2; p++ )
+                {
+                    v = FN(var)( 0, plane[p] + 16 * mbx + 16 * mby * stride[p], stride[p] );
+                    sum[p] += (uint32_t)v;
+                    ssd[p] += v >> 32;
+                }
+            else if( chroma_format )
+            {
+                const int h = 16 >> vs;
+                pixel buf[16 * 16];
+                const pixel *s = plane[1] + 16 * mbx + h * mby * stride[1];
+                for( int y = 0; y < h; y++ )
+                    for( int x = 0; x < 8; x++ )
+                    {
+                        buf[y * 16 + x] = s[y * stride[1] + 2 * x];
+                        buf[y * 16 + 8 + x] = s[y * stride[1] + 2 * x + 1];
+                    }
+                for( int p = 1; p <= 2; p++ )
+                {
+                    v = FN(var)( h == 8 ? 3 : 2, buf + 8 * (p - 1), 16 );
+                    sum[p] += (uint32_t)v;
+                    ssd[p] += v >> 32;
+                }
+            }
+        }
+    for( int i = 0; i < 3; i++ )
+    {
+        const uint64_t s = sum[i];
+        const uint64_t w = (uint64_t)(16 * mb_width >> (i && hs)), h = (uint64_t)(16 * mb_height >> (i && vs));
+        ssd[i] = ssd[i] - (s * s + w * h / 2) / (w * h);
+    }
+}
+
+/* x264_weight_t as the search leaves it: weighted = (weightfn != NULL) */
+typedef struct { int weighted, scale, denom, offset; } FN(wp_t);
+
+static int wp_ue_tab( unsigned v )   /* x264_ue_size_tab[v] (common/bitstream.h:201-219) */
+{
+    int n = 0;
+    while( v >> (n + 1) )
+        n++;
+    return v ? 2 * n + 1 : 1;
+}
+static int wp_size_ue( unsigned v ) { return wp_ue_tab( v + 1 ); }        /* bitstream.h:278-281 */
+static int wp_size_se( int v )                                            /* bitstream.h:291-299 */
+{
+    int tmp = 1 - v * 2;
+    if( tmp < 0 )
+        tmp = v * 2;
+    return tmp < 256 ? wp_ue_tab( tmp ) : wp_ue_tab( tmp >> 8 ) + 16;
+}
+
+/* weight_slice_header_cost (slicetype.c:170-189); lambda = x264_lambda_tab[X264_LOOKAHEAD_QP] */
+static int wp_header_cost( const FN(wp_t) *w, int b_chroma, int lambda, int numslices )
+{
+    if( b_chroma )
+        lambda *= 4;
+    const int denom_cost = wp_size_ue( w->denom ) * (2 - b_chroma);
+    return lambda * numslices * (10 + denom_cost + 2 * (wp_size_se( w->scale ) + wp_size_se( w->offset )));
+}
+
+typedef struct
+{
+    const pixel *fenc_lr;            /* fenc->lowres[0] at (0,0) */
+    const pixel *const *ref_lr;      /* ref->lowres[0..3] at (0,0) */
+    intptr_t lrs;                    /* i_stride_lowres */
+    int mbw, mbh;
+    const uint16_t *intra;           /* fenc->i_intra_cost */
+    const int16_t *mvs;              /* fenc->lowres_mvs[0][ref0_distance], NULL = 0x7FFF (not searched) */
+    int cf;                          /* chroma format */
+    const pixel *const *fplane, *const *rplane;   /* full-resolution planes at (0,0) */
+    const intptr_t *ps;              /* their strides */
+    int satd, lambda, numslices;
+} FN(wpctx_t);
+
+/* weight_cost_luma (slicetype.c:191-222): mbcmp 8x8 of the (weighted) reference against the
+ * lowres fenc, each MB capped at its intra cost, plus the header cost when weighted */
+static unsigned wp_cost_luma( const FN(wpctx_t) *c, const pixel *src, intptr_t ss, const FN(wp_t) *w )
+{
+    unsigned cost = 0;
+    pixel buf[64];
+    for( int y = 0, mb = 0; y < 8 * c->mbh; y += 8 )
+        for( int x = 0; x < 8 * c->mbw; x += 8, mb++ )
+        {
+            const pixel *r = src + y * ss + x;
+            intptr_t rs = ss;
+            if( w )
+            {
+                FN(mc_weight)( buf, 8, r, ss, w->scale, w->denom, w->offset, 8, 8 );
+                r = buf;
+                rs = 8;
+            }
+            const pixel *f = c->fenc_lr + y * c->lrs + x;
+            const int cmp = c->satd ? FN(satd)( 3, r, rs, f, c->lrs ) : FN(sad)( 3, r, rs, f, c->lrs );
+            cost += cmp < c->intra[mb] ? cmp : c->intra[mb];
+        }
+    if( w )
+        cost += wp_header_cost( w, 0, c->lambda, c->numslices );
+    return cost;
+}
+
+/* weight_cost_chroma (slicetype.c:224-255): asd8 (the DC difference) of 8 x (16 >> vshift)
+ * blocks of the (weighted) motion-compensated reference plane against the fenc plane */
+static unsigned wp_cost_chroma( const FN(wpctx_t) *c, const pixel *ref, const pixel *src, intptr_t s,
+                                const FN(wp_t) *w )
+{
+    unsigned cost = 0;
+    const int h = c->cf == 1 ? 8 : 16;
+    pixel buf[8 * 16];
+    for( int y = 0; y < h * c->mbh; y += h )
+        for( int x = 0; x < 8 * c->mbw; x += 8 )
+        {
+            if( w )
+            {
+                FN(mc_weight)( buf, 8, ref + y * s + x, s, w->scale, w->denom, w->offset, 8, h );
+                cost += FN(asd8)( buf, 8, src + y * s + x, s, h );
+            }
+            else
+                cost += FN(asd8)( ref + y * s + x, s, src + y * s + x, s, h );
+        }
+    if( w )
+        cost += wp_header_cost( w, 1, c->lambda, c->numslices );
+    return cost;
+}
+
+/* weight_cost_chroma444 (slicetype.c:257-282): mbcmp 16x16 of the (weighted) reference plane */
+static unsigned wp_cost_444( const FN(wpctx_t) *c, const pixel *ref, intptr_t rs, int p, const FN(wp_t) *w )
+{
+    unsigned cost = 0;
+    pixel buf[256];
+    const pixel *src = c->fplane[p];
+    const intptr_t s = c->ps[p];
+    for( int y = 0; y < 16 * c->mbh; y += 16 )
+        for( int x = 0; x < 16 * c->mbw; x += 16 )
+        {
+            const pixel *r = ref + y * rs + x;
+            intptr_t st = rs;
+            if( w )
+            {
+                FN(mc_weight)( buf, 16, r, rs, w->scale, w->denom, w->offset, 16, 16 );
+                r = buf;
+                st = 16;
+            }
+            cost += c->satd ? FN(satd)( 0, r, st, src + y * s + x, s ) : FN(sad)( 0, r, st, src + y * s + x, s );
+        }
+    if( w )
+        cost += wp_header_cost( w, 1, c->lambda, c->numslices );
+    return cost;
+}
+
+/* the motion-compensated lowres reference of weight_cost_init_luma (slicetype.c:77-103):
+ * get_ref of each 8x8 block at lowres_mvs + the block position, into a buffer of stride 8*mbw */
+static pixel *wp_mc_luma( const FN(wpctx_t) *c )
+{
+    const intptr_t st = 8 * c->mbw;
+    pixel *buf = malloc( sizeof(pixel) * 64 * c->mbw * c->mbh );
+    for( int y = 0, mb = 0; y < 8 * c->mbh; y += 8 )
+        for( int x = 0; x < 8 * c->mbw; x += 8, mb++ )
+        {
+            pixel tmp[64];
+            intptr_t ts = 8;
+            const pixel *r = FN(get_ref)( tmp, &ts, c->ref_lr, c->lrs, c->mvs[2 * mb] + (x << 2),
+                                          c->mvs[2 * mb + 1] + (y << 2), 8, 8 );
+            for( int j = 0; j < 8; j++ )
+                memcpy( buf + (y + j) * st + x, r + j * ts, 8 * sizeof(pixel) );
+        }
+    return buf;
+}
+
+/* weight_cost_init_chroma444 (slicetype.c:142-168): 16x16 copies at lowres_mvs / 2 */
+static pixel *wp_mc_444( const FN(wpctx_t) *c, int p )
+{
+    const intptr_t st = 16 * c->mbw;
+    pixel *buf = malloc( sizeof(pixel) * 256 * c->mbw * c->mbh );
+    for( int y = 0, mb = 0; y < 16 * c->mbh; y += 16 )
+        for( int x = 0; x < 16 * c->mbw; x += 16, mb++ )
+        {
+            const int mvx = c->mvs[2 * mb] / 2, mvy = c->mvs[2 * mb + 1] / 2;
+            const pixel *s = c->rplane[p] + y * c->ps[p] + x + mvx + mvy * c->ps[p];
+            for( int j = 0; j < 16; j++ )
+                memcpy( buf + (y + j) * st + x, s + j * c->ps[p], 16 * sizeof(pixel) );
+        }
+    return buf;
+}
+
+/* weight_cost_init_chroma (slicetype.c:111-140): U / V of the reference -- mc_chroma of
+ * lowres_mvs (mvy scaled by 2 >> vshift) or the plane deinterleaved -- and of fenc, stride 8*mbw */
+static void wp_mc_chroma( const FN(wpctx_t) *c, pixel **mcu, pixel **mcv, pixel **fu, pixel **fv )
+{
+    const int vs = c->cf == 1, h = 16 >> vs;
+    const intptr_t st = 8 * c->mbw, ps = c->ps[1];
+    const size_t n = sizeof(pixel) * 8 * c->mbw * h * c->mbh;
+    *mcu = malloc( n ); *mcv = malloc( n ); *fu = malloc( n ); *fv = malloc( n );
+    for( int y = 0, mb = 0; y < h * c->mbh; y += h )
+        for( int x = 0; x < 8 * c->mbw; x += 8, mb++ )
+        {
+            if( c->mvs )
+                FN(mc_chroma)( *mcu + y * st + x, *mcv + y * st + x, st, c->rplane[1] + y * ps + 2 * x, ps,
+                               c->mvs[2 * mb], 2 * c->mvs[2 * mb + 1] >> vs, 8, h );
+            for( int j = 0; j < h; j++ )
+                for( int i = 0; i < 8; i++ )
+                {
+                    const intptr_t o = (y + j) * ps + 2 * (x + i);
+                    if( !c->mvs )
+                    {
+                        (*mcu)[(y + j) * st + x + i] = c->rplane[1][o];
+                        (*mcv)[(y + j) * st + x + i] = c->rplane[1][o + 1];
+                    }
+                    (*fu)[(y + j) * st + x + i] = c->fplane[1][o];
+                    (*fv)[(y + j) * st + x + i] = c->fplane[1][o + 1];
+                }
+        }
+}
+
+/* weight_cost_luma / _chroma / _chroma444 of n candidates (cands[4i..4i+3] = weighted, scale,
+ * denom, offset; weighted 0 = the w == NULL cost) -- the per-candidate check of
+ * x264hip_*_weight_cost_batch.  kind 0: fenc / ref[0..3] lowres; 1 / 2: NV12 / NV16 planes,
+ * plane 0 = U, 1 = V; 3: one 4:4:4 chroma plane. */
+void FN(weight_cost_list)( int kind, const pixel *fenc, const pixel *const ref[4], intptr_t stride, int mbw,
+                           int mbh, const uint16_t *intra, const int16_t *mvs, int satd, int plane, int lambda,
+                           int numslices, const int *cands, int n, uint32_t *out )
+{
+    const pixel *fp[3] = { fenc, fenc, fenc }, *rp[3] = { ref[0], ref[0], ref[0] };
+    const intptr_t ps[3] = { stride, stride, stride };
+    const FN(wpctx_t) c = { fenc, ref, stride, mbw, mbh, intra, mvs, kind == 3 ? 3 : kind, fp, rp, ps, satd, lambda,
+                            numslices };
+    pixel *b0 = NULL, *b1 = NULL, *b2 = NULL, *b3 = NULL;
+    for( int i = 0; i < n; i++ )
+    {
+        const FN(wp_t) w = { cands[4 * i], cands[4 * i + 1], cands[4 * i + 2], cands[4 * i + 3] };
+        const FN(wp_t) *wp = w.weighted ? &w : NULL;
+        if( kind == 0 )
+        {
+            if( mvs && !b0 )
+                b0 = wp_mc_luma( &c );
+            out[i] = b0 ? wp_cost_luma( &c, b0, 8 * mbw, wp ) : wp_cost_luma( &c, ref[0], stride, wp );
+        }
+        else if( kind == 3 )
+        {
+            if( mvs && !b0 )
+                b0 = wp_mc_444( &c, 1 );
+            out[i] = b0 ? wp_cost_444( &c, b0, 16 * mbw, 1, wp ) : wp_cost_444( &c, ref[0], stride, 1, wp );
+        }
+        else
+        {
+            if( !b0 )
+                wp_mc_chroma( &c, &b0, &b1, &b2, &b3 );
+            out[i] = wp_cost_chroma( &c, plane ? b1 : b0, plane ? b3 : b2, 8 * mbw, wp );
+        }
+    }
+    free( b0 ); free( b1 ); free( b2 ); free( b3 );
+}
+
+static int wp_clip3( int v, int lo, int hi ) { return v < lo ? lo : v > hi ? hi : v; }
+static double wp_clip3f( double v, double lo, double hi ) { return v < lo ? lo : v > hi ? hi : v; }
+
+/* weight_get_h264 (slicetype.c:63-75) */
+static void wp_get_h264( int weight_nonh264, int offset, FN(wp_t) *w )
+{
+    w->offset = offset;
+    w->denom = 7;
+    w->scale = weight_nonh264;
+    while( w->denom > 0 && w->scale > 127 )
+    {
+        w->denom--;
+        w->scale >>= 1;
+    }
+    w->scale = w->scale < 127 ? w->scale : 127;
+}
+
+#define WP_SET( w, b, s, d, o ) do { (w).scale = (s); (w).denom = (d); (w).offset = (o); (w).weighted = (b); } while( 0 )
+
+/* x264_weights_analyse (slicetype.c:284-501) for one (fenc, ref) pair.  fsum / fssd /
+ * rsum / rssd = fenc / ref i_pixel_sum / i_pixel_ssd; subme = param i_subpel_refine;
+ * weightp_fake = (param i_weighted_pred == X264_WEIGHTP_FAKE).  The caller's ref planes
+ * carry expanded borders (the reference expands the chroma border itself,
+ * slicetype.c:124 / :151).  Writes weights[3] (fenc->weight[0][0..2]), *cost_delta
+ * (fenc->f_weighted_cost_delta[i_delta_index], FAKE only) and, in the lookahead with a
+ * luma weight, the weighted lowres plane (slicetype.c:490-500) at wlr (its (0,0), stride
+ * lrs, 32-pixel border) when wlr is not NULL. */
+void FN(weights_analyse)( const pixel *fenc_lr, const pixel *const ref_lr[4], intptr_t lrs, int mbw, int mbh,
+                          const uint16_t *intra, const int16_t *mvs, int cf, const pixel *const fplane[3],
+                          const pixel *const rplane[3], const intptr_t ps[3], const uint32_t fsum[3],
+                          const uint64_t fssd[3], const uint32_t rsum[3], const uint64_t rssd[3], int b_lookahead,
+                          int subme, int satd, int lambda, int numslices, int weightp_fake, FN(wp_t) weights[3],
+                          float *cost_delta, pixel *wlr )
+{
+    const FN(wpctx_t) c = { fenc_lr, ref_lr, lrs, mbw, mbh, intra, mvs, cf, fplane, rplane, ps, satd, lambda,
+                            numslices };
+    const int hs = cf == 1 || cf == 2, vs = cf == 1;
+    const float epsilon = 1.f / 128.f;
+    WP_SET( weights[0], 0, 1, 0, 0 );
+    WP_SET( weights[1], 0, 1, 0, 0 );
+    WP_SET( weights[2], 0, 1, 0, 0 );
+    int chroma_initted = 0;
+    float guess_scale[3], fenc_mean[3], ref_mean[3];
+    for( int plane = 0; plane <= 2 * !b_lookahead; plane++ )
+    {
+        if( !plane || cf )
+        {
+            const int zero_bias = !rssd[plane];
+            const float fenc_var = fssd[plane] + zero_bias;
+            const float ref_var = rssd[plane] + zero_bias;
+            const int npx = (16 * mbh >> (plane ? vs : 0)) * (16 * mbw >> (plane ? hs : 0));
+            guess_scale[plane] = sqrtf( fenc_var / ref_var );
+            fenc_mean[plane] = (float)(fsum[plane] + zero_bias) / npx / (1 << (BIT_DEPTH - 8));
+            ref_mean[plane] = (float)(rsum[plane] + zero_bias) / npx / (1 << (BIT_DEPTH - 8));
+        }
+        else
+        {
+            guess_scale[plane] = 1;
+            fenc_mean[plane] = 0;
+            ref_mean[plane] = 0;
+        }
+    }
+
+    int chroma_denom = 7;
+    if( !b_lookahead )
+        while( chroma_denom > 0 )
+        {
+            const float thresh = 127.f / (1 << chroma_denom);
+            if( guess_scale[1] < thresh && guess_scale[2] < thresh )
+                break;
+            chroma_denom--;
+        }
+
+    pixel *mcl = NULL, *mcu = NULL, *mcv = NULL, *fu = NULL, *fv = NULL, *mc444 = NULL;
+    for( int plane = 0; plane < (cf ? 3 : 1) && !(plane && (!weights[0].weighted || b_lookahead)); plane++ )
+    {
+        int minoff, minscale, mindenom, found;
+        unsigned minscore, origscore;
+        if( fabsf( ref_mean[plane] - fenc_mean[plane] ) < 0.5f && fabsf( 1.f - guess_scale[plane] ) < epsilon )
+        {
+            WP_SET( weights[plane], 0, 1, 0, 0 );
+            continue;
+        }
+        if( plane )
+        {
+            weights[plane].denom = chroma_denom;
+            weights[plane].scale = wp_clip3( round( guess_scale[plane] * (1 << chroma_denom) ), 0, 255 );
+            if( weights[plane].scale > 127 )
+            {
+                weights[1].weighted = weights[2].weighted = 0;
+                break;
+            }
+        }
+        else
+            wp_get_h264( round( guess_scale[plane] * 128 ), 0, &weights[plane] );
+
+        found = 0;
+        mindenom = weights[plane].denom;
+        minscale = weights[plane].scale;
+        minoff = 0;
+
+        /* the motion-compensated reference: weight_cost_init_luma / _chroma / _chroma444
+         * (slicetype.c:77-168) */
+        const pixel *mref;
+        intptr_t mrs;
+        if( !plane )
+        {
+            if( mvs )
+            {
+                if( !mcl )
+                    mcl = wp_mc_luma( &c );
+                mref = mcl;
+                mrs = 8 * mbw;
+            }
+            else
+            {
+                mref = ref_lr[0];
+                mrs = lrs;
+            }
+            origscore = minscore = wp_cost_luma( &c, mref, mrs, NULL );
+        }
+        else if( cf == 3 )
+        {
+            if( mvs )
+            {
+                free( mc444 );
+                mc444 = wp_mc_444( &c, plane );
+                mref = mc444;
+                mrs = 16 * mbw;
+            }
+            else
+            {
+                mref = rplane[plane];
+                mrs = ps[plane];
+            }
+            origscore = minscore = wp_cost_444( &c, mref, mrs, plane, NULL );
+        }
+        else
+        {
+            const intptr_t st = 8 * mbw;
+            if( !chroma_initted++ )
+                wp_mc_chroma( &c, &mcu, &mcv, &fu, &fv );
+            mref = plane == 1 ? mcu : mcv;
+            mrs = st;
+            origscore = minscore = wp_cost_chroma( &c, mref, plane == 1 ? fu : fv, st, NULL );
+        }
+
+        if( !minscore )
+            continue;
+
+        static const uint8_t weight_check_distance[][2] = {
+            {0,0},{0,0},{0,1},{0,1}, {0,1},{0,1},{0,1},{1,1}, {1,1},{2,1},{2,1},{4,2} };
+        const int scale_dist = b_lookahead ? 0 : weight_check_distance[subme][0];
+        const int offset_dist = b_lookahead ? 0 : weight_check_distance[subme][1];
+        const int start_scale = wp_clip3( minscale - scale_dist, 0, 127 );
+        const int end_scale = wp_clip3( minscale + scale_dist, 0, 127 );
+        for( int i_scale = start_scale; i_scale <= end_scale; i_scale++ )
+        {
+            int cur_scale = i_scale;
+            int cur_offset = fenc_mean[plane] - ref_mean[plane] * cur_scale / (1 << mindenom) + 0.5f * b_lookahead;
+            if( cur_offset < -128 || cur_offset > 127 )
+            {
+                cur_offset = wp_clip3( cur_offset, -128, 127 );
+                cur_scale = wp_clip3f( (1 << mindenom) * (fenc_mean[plane] - cur_offset) / ref_mean[plane] + 0.5f, 0,
+                                       127 );
+            }
+            const int start_offset = wp_clip3( cur_offset - offset_dist, -128, 127 );
+            const int end_offset = wp_clip3( cur_offset + offset_dist, -128, 127 );
+            for( int i_off = start_offset; i_off <= end_offset; i_off++ )
+            {
+                WP_SET( weights[plane], 1, cur_scale, mindenom, i_off );
+                unsigned s;
+                if( !plane )
+                    s = wp_cost_luma( &c, mref, mrs, &weights[plane] );
+                else if( cf == 3 )
+                    s = wp_cost_444( &c, mref, mrs, plane, &weights[plane] );
+                else
+                    s = wp_cost_chroma( &c, mref, plane == 1 ? fu : fv, mrs, &weights[plane] );
+                if( s < minscore )
+                {
+                    minscore = s;
+                    minscale = cur_scale;
+                    minoff = i_off;
+                    found = 1;
+                }
+                if( minoff == start_offset && i_off != start_offset )
+                    break;
+            }
+        }
+
+        if( !plane )
+            while( mindenom > 0 && !(minscale & 1) )
+            {
+                mindenom--;
+                minscale >>= 1;
+            }
+
+        if( !found || (minscale == 1 << mindenom && minoff == 0) || (float)minscore / origscore > 0.998f )
+        {
+            WP_SET( weights[plane], 0, 1, 0, 0 );
+            continue;
+        }
+        WP_SET( weights[plane], 1, minscale, mindenom, minoff );
+        if( weightp_fake && weights[0].weighted && !plane && cost_delta )
+            *cost_delta = (float)minscore / origscore;
+    }
+
+    if( weights[1].weighted || weights[2].weighted )
+    {
+        int denom = weights[1].weighted ? weights[1].denom : weights[2].denom;
+        const int both = weights[1].weighted && weights[2].weighted;
+        while( (!both && denom == 7) ||
+               (denom > 0 && !(weights[1].weighted && (weights[1].scale & 1)) &&
+                !(weights[2].weighted && (weights[2].scale & 1))) )
+        {
+            denom--;
+            for( int i = 1; i <= 2; i++ )
+                if( weights[i].weighted )
+                {
+                    weights[i].scale >>= 1;
+                    weights[i].denom = denom;
+                }
+        }
+    }
+
+    if( weights[0].weighted && b_lookahead && wlr )
+        FN(weight_scale_plane)( wlr - 32 - 32 * lrs, lrs, ref_lr[0] - 32 - 32 * lrs, lrs, 8 * mbw + 64, 8 * mbh + 64,
+                                weights[0].scale, weights[0].denom, weights[0].offset );
+    free( mcl );
+    free( mcu );
+    free( mcv );
+    free( fu );
+    free( fv );
+    free( mc444 );
+}

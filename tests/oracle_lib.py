@@ -612,3 +612,77 @@ def lowres_bidir_cost(bd, fenc, ref_a, ref_b, origin, stride, mbw, mbh, search, 
                                    _addr(k1), None if p1 is None else _addr(p1), dsf, weight,
                                    None if iq is None else _addr(iq), _addr(lc), _addr(rows), _addr(est), n_slices)
     return m0, k0, m1, k1, lc, rows, est
+
+
+# ---- weighted-prediction analysis (slicetype.c:63-501, ratecontrol.c:225-257,406-414) ----
+for _bd in (8, 10):
+    _f(_bd, "mc_chroma", [_P, _P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int])
+    _f(_bd, "frame_pixel_stats", [_P, _P, C.c_int, C.c_int, C.c_int, _P, _P])
+    _f(_bd, "weight_cost_list", [C.c_int, _P, _P, _IP, C.c_int, C.c_int, _P, _P, C.c_int, C.c_int, C.c_int,
+                                 C.c_int, _P, C.c_int, _P])
+    _f(_bd, "weights_analyse", [_P, _P, _IP, C.c_int, C.c_int, _P, _P, C.c_int, _P, _P, _P, _P, _P, _P, _P,
+                                C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P])
+
+
+def _ptrs(arrs_offs):
+    return (C.c_void_p * len(arrs_offs))(*[None if a is None else a.ctypes.data + int(o) * a.itemsize
+                                           for a, o in arrs_offs])
+
+
+def mc_chroma(bd, src, s_off, ss, mvx, mvy, w, h):
+    """mc_chroma (mc.c:252-283) of an interleaved plane: (u, v) uint arrays [h, w]"""
+    u = np.zeros((h, w), pixel_dtype(bd))
+    v = np.zeros((h, w), pixel_dtype(bd))
+    fn(bd, "mc_chroma")(_addr(u), _addr(v), w, _addr(src, s_off), ss, mvx, mvy, w, h)
+    return u, v
+
+
+def frame_pixel_stats(bd, planes, origins, strides, mbw, mbh, chroma_format):
+    """(sum uint32 [3], ssd uint64 [3]) as x264_adaptive_quant_frame leaves i_pixel_sum / i_pixel_ssd;
+    planes = [luma, NV12 plane or U, V (4:4:4) or None]"""
+    s = np.zeros(3, np.uint32)
+    d = np.zeros(3, np.uint64)
+    pp = _ptrs([(p, o) if p is not None else (None, 0) for p, o in zip(planes, origins)])
+    st = (C.c_ssize_t * 3)(*[int(x) for x in strides])
+    fn(bd, "frame_pixel_stats")(pp, st, mbw, mbh, chroma_format, _addr(s), _addr(d))
+    return s, d
+
+
+def weight_cost_list(bd, kind, fenc, refs, origin, stride, mbw, mbh, cands, intra=None, mvs=None, satd=True,
+                     plane=0, lam=1, n_slices=1):
+    """weight_cost_luma / _chroma / _chroma444 of each (weighted, scale, denom, offset) in cands: uint32 [n]"""
+    c = np.ascontiguousarray(np.array(cands, np.int32).reshape(-1, 4))
+    out = np.zeros(len(c), np.uint32)
+    rp = _ptrs([(r, origin) for r in refs] + [(None, 0)] * (4 - len(refs)))
+    ic = None if intra is None else np.ascontiguousarray(intra, np.uint16)
+    mv = None if mvs is None else np.ascontiguousarray(mvs, np.int16)
+    fn(bd, "weight_cost_list")(kind, _addr(fenc, origin), rp, stride, mbw, mbh, None if ic is None else _addr(ic),
+                               None if mv is None else _addr(mv), int(satd), plane, lam, n_slices, _addr(c), len(c),
+                               _addr(out))
+    return out
+
+
+def weights_analyse(bd, fenc_lr, ref_lr, lr_origin, lrs, mbw, mbh, intra, fstats, rstats, mvs=None,
+                    chroma_format=0, fenc_c=(None, None), ref_c=(None, None), c_origin=0, cs=0, b_lookahead=True,
+                    subme=7, satd=True, lam=1, n_slices=1, weightp_fake=False, weighted=None):
+    """x264_weights_analyse: (weights int32 [3, 4] = (weighted, scale, denom, offset), cost_delta or None).
+    fstats / rstats = (sum [3], ssd [3]); weighted (lowres plane array like ref_lr[0]) receives the
+    weighted lowres reference in the lookahead."""
+    w = np.zeros((3, 4), np.int32)
+    cd = np.full(1, -1.0, np.float32)
+    ic = np.ascontiguousarray(intra, np.uint16)
+    mv = None if mvs is None else np.ascontiguousarray(mvs, np.int16)
+    rl = _ptrs([(r, lr_origin) for r in ref_lr])
+    fp = _ptrs([(fenc_lr, lr_origin), (fenc_c[0], c_origin), (fenc_c[1], c_origin)])
+    rp = _ptrs([(ref_lr[0], lr_origin), (ref_c[0], c_origin), (ref_c[1], c_origin)])
+    ps = (C.c_ssize_t * 3)(lrs, cs, cs)
+    if chroma_format in (1, 2):   # the oracle reads NV12 as plane[1]
+        fp[2], rp[2] = fp[1], rp[1]
+    fs_ = np.array(fstats[0], np.uint32), np.array(fstats[1], np.uint64)
+    rs_ = np.array(rstats[0], np.uint32), np.array(rstats[1], np.uint64)
+    fn(bd, "weights_analyse")(_addr(fenc_lr, lr_origin), rl, lrs, mbw, mbh, _addr(ic),
+                              None if mv is None else _addr(mv), chroma_format, fp, rp, ps, _addr(fs_[0]),
+                              _addr(fs_[1]), _addr(rs_[0]), _addr(rs_[1]), int(b_lookahead), subme, int(satd), lam,
+                              n_slices, int(weightp_fake), w.ctypes.data, _addr(cd),
+                              None if weighted is None else _addr(weighted, lr_origin))
+    return w, (None if cd[0] == -1.0 else float(cd[0]))

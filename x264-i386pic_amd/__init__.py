@@ -817,6 +817,95 @@ def lowres_bidir_cost(fenc, refs_a, refs_b, lowres_stride, mb_width, mb_height, 
     return lc, rows, est
 
 
+class Weight(_c.Structure):
+    """x264hip_weight_t: x264_weight_t as x264_weights_analyse leaves it (weighted = weightfn set)"""
+    _fields_ = [("weighted", _c.c_int32), ("scale", _c.c_int32), ("denom", _c.c_int32), ("offset", _c.c_int32)]
+
+    def tuple(self):
+        return (self.weighted, self.scale, self.denom, self.offset)
+
+
+WCOST_LUMA, WCOST_CHROMA420, WCOST_CHROMA422, WCOST_CHROMA444 = 0, 1, 2, 3
+
+
+def _plane_ptr(t, origin):
+    return None if t is None else _ptr(t, origin)
+
+
+def frame_pixel_stats(luma, luma_origin, luma_stride, mb_width, mb_height, chroma_format=0, chroma_u=None,
+                      chroma_v=None, chroma_origin=0, chroma_stride=0, out=None):
+    """fenc->i_pixel_sum / i_pixel_ssd of one frame (x264hip_*_frame_pixel_stats): int64 tensor [6] =
+    sum[0..2], ssd[0..2] (uint64 bit patterns).  chroma_u = the NV12 / NV16 plane for 4:2:0 / 4:2:2."""
+    import torch
+    bd = _pix_bd(luma)
+    if out is None:
+        out = torch.empty(6, dtype=torch.int64, device=luma.device)
+    f = getattr(lib(), f"x264hip_{bd}_frame_pixel_stats")
+    f.argtypes = [_P, _IP, _P, _P, _IP, _c.c_int, _c.c_int, _c.c_int, _P, _P]
+    _rc(f(_ptr(luma, luma_origin), luma_stride, _plane_ptr(chroma_u, chroma_origin),
+          _plane_ptr(chroma_v, chroma_origin), chroma_stride, mb_width, mb_height, chroma_format, _ptr(out),
+          _stream()), "frame_pixel_stats")
+    return out
+
+
+def _weights(cands):
+    arr = (Weight * max(1, len(cands)))()
+    for i, c in enumerate(cands):
+        arr[i] = Weight(*[int(v) for v in c])
+    return arr
+
+
+def weight_cost_batch(kind, fenc, refs, origin, stride, mb_width, mb_height, cands, intra_cost=None, mvs=None,
+                      satd=True, plane=0, lam=1, n_slices=1, out=None):
+    """weight_cost_luma / _chroma / _chroma444 (slicetype.c:191-282) of every (weighted, scale, denom,
+    offset) in cands (x264hip_*_weight_cost_batch): uint32-as-int32 tensor [n].  fenc / refs = planes
+    with pixel (0,0) at element `origin` (refs: the four lowres planes for WCOST_LUMA with mvs, else one)."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = len(cands)
+    if out is None:
+        out = torch.empty(max(1, n), dtype=torch.int32, device=fenc.device)
+    rp = (_P * 4)(*([r.data_ptr() + origin * r.element_size() for r in refs] + [None] * (4 - len(refs))))
+    f = getattr(lib(), f"x264hip_{bd}_weight_cost_batch")
+    f.argtypes = [_c.c_int, _P, _P, _IP, _c.c_int, _c.c_int, _P, _P, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P,
+                  _c.c_int, _P, _P]
+    _rc(f(kind, _ptr(fenc, origin), rp, stride, mb_width, mb_height,
+          None if intra_cost is None else _ptr(intra_cost), None if mvs is None else _ptr(mvs), int(bool(satd)),
+          plane, lam, n_slices, _weights(cands), n, _ptr(out), _stream()), "weight_cost_batch")
+    return out[:n]
+
+
+def weights_analyse(fenc_lowres, ref_lowres, lowres_stride, mb_width, mb_height, intra_cost, fenc_stats,
+                    ref_stats, mvs=None, chroma_format=0, fenc_chroma=(None, None), ref_chroma=(None, None),
+                    chroma_origin=0, chroma_stride=0, b_lookahead=True, subme=7, satd=True, lam=1, n_slices=1,
+                    weightp_fake=False, weighted_lowres=None):
+    """x264_weights_analyse (x264hip_*_weights_analyse; synchronous).  Lowres planes are single frames
+    [rows, stride] with (0,0) at (PAD, PAD); ref_lowres = the four planes (F, H, V, C); chroma planes
+    have (0,0) at chroma_origin.  fenc_stats / ref_stats = (sum [3], ssd [3]) host ints.  Returns
+    (weights [(weighted, scale, denom, offset)] * 3, cost_delta or None); weighted_lowres (a plane
+    like ref_lowres[0]) receives fenc->weighted[0] in the lookahead when a luma weight is found."""
+    bd = _pix_bd(fenc_lowres)
+    o = PAD * lowres_stride + PAD
+    rl = (_P * 4)(*[r.data_ptr() + o * r.element_size() for r in ref_lowres])
+    fc = (_P * 2)(*[None if t is None else t.data_ptr() + chroma_origin * t.element_size() for t in fenc_chroma])
+    rc = (_P * 2)(*[None if t is None else t.data_ptr() + chroma_origin * t.element_size() for t in ref_chroma])
+    fsum = (_c.c_uint32 * 3)(*[int(v) & 0xFFFFFFFF for v in fenc_stats[0]])
+    fssd = (_c.c_uint64 * 3)(*[int(v) & 0xFFFFFFFFFFFFFFFF for v in fenc_stats[1]])
+    rsum = (_c.c_uint32 * 3)(*[int(v) & 0xFFFFFFFF for v in ref_stats[0]])
+    rssd = (_c.c_uint64 * 3)(*[int(v) & 0xFFFFFFFFFFFFFFFF for v in ref_stats[1]])
+    w = (Weight * 3)()
+    cd = _c.c_float(-1.0)
+    f = getattr(lib(), f"x264hip_{bd}_weights_analyse")
+    f.argtypes = [_P, _P, _IP, _c.c_int, _c.c_int, _P, _P, _c.c_int, _P, _P, _IP, _P, _P, _P, _P, _c.c_int,
+                  _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P]
+    _rc(f(_ptr(fenc_lowres, o), rl, lowres_stride, mb_width, mb_height, _ptr(intra_cost),
+          None if mvs is None else _ptr(mvs), chroma_format, fc, rc, chroma_stride, fsum, fssd, rsum, rssd,
+          int(bool(b_lookahead)), subme, int(bool(satd)), lam, n_slices, int(bool(weightp_fake)),
+          None if weighted_lowres is None else _ptr(weighted_lowres, o), w, _c.byref(cd), _stream()),
+        "weights_analyse")
+    return [w[i].tuple() for i in range(3)], (None if cd.value == -1.0 else cd.value)
+
+
 def lowres_status():
     """Wait for the current stream; raise if a lookahead launch of this thread on its device
     timed out in the band wavefront (x264hip_lowres_status; reporting clears it)."""

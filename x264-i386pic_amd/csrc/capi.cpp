@@ -1863,6 +1863,77 @@ extern "C" const char *x264hip_backend_banner( void )
         return map_err( launch_frame_init_lowres<BD>( src, stride, fstride, width, height, nframes, dst, ds, dfs,     \
                                                       (hipStream_t)stream ), "frame_init_lowres" );                  \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_frame_pixel_stats( const PT<BD>::pixel *luma, intptr_t ls,                        \
+                                                     const PT<BD>::pixel *cu, const PT<BD>::pixel *cv, intptr_t cs,  \
+                                                     int mbw, int mbh, int cf, uint64_t *stats, void *stream )       \
+    {                                                                                                                \
+        if( mbw < 0 || mbh < 0 || cf < 0 || cf > 3 || !stats || ( mbw * mbh > 0 && !luma ) ||                        \
+            ( mbw * mbh > 0 && cf && !cu ) || ( mbw * mbh > 0 && cf == 3 && !cv ) )                                  \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_frame_stats<BD>( luma, ls, cu, cv, cs, mbw, mbh, cf, stats, (hipStream_t)stream ),   \
+                        "frame_pixel_stats" );                                                                       \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_weight_cost_batch( int kind, const PT<BD>::pixel *fenc,                           \
+                                                     const PT<BD>::pixel *const ref[4], intptr_t stride, int mbw,    \
+                                                     int mbh, const uint16_t *intra, const int16_t *mvs, int satd,   \
+                                                     int plane, int lambda, int n_slices,                            \
+                                                     const x264hip_weight_t *cands, int n, uint32_t *costs,          \
+                                                     void *stream )                                                  \
+    {                                                                                                                \
+        if( kind < 0 || kind > 3 || mbw < 0 || mbh < 0 || n < 0 || lambda < 0 || n_slices < 1 ||                     \
+            ( (kind == 1 || kind == 2) && ( plane < 0 || plane > 1 ) ) )                                             \
+            return X264HIP_EINVAL;                                                                                   \
+        if( n > 0 && ( !cands || !costs ) )                                                                          \
+            return X264HIP_EINVAL;                                                                                   \
+        for( int i = 0; i < n; i++ )                                                                                 \
+            if( cands[i].weighted && ( cands[i].scale < 0 || cands[i].scale > 255 || cands[i].denom < 0 ||          \
+                                       cands[i].denom > 7 || cands[i].offset < -128 || cands[i].offset > 127 ) )     \
+                return X264HIP_EINVAL;                                                                               \
+        if( n > 0 && mbw * mbh > 0 &&                                                                                \
+            ( !fenc || !ref || !ref[0] || ( kind == 0 && !intra ) ||                                                 \
+              ( kind == 0 && mvs && ( !ref[1] || !ref[2] || !ref[3] ) ) ) )                                          \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_weight_cost<BD>( kind, fenc, stride, ref, stride, mbw, mbh, intra, mvs, satd,        \
+                                                kind == 1 || kind == 2 ? plane : 0, lambda, n_slices, cands, n,      \
+                                                costs, (hipStream_t)stream ), "weight_cost_batch" );                 \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_weights_analyse(                                                                 \
+        const PT<BD>::pixel *fenc_lr, const PT<BD>::pixel *const ref_lr[4], intptr_t lrs, int mbw, int mbh,          \
+        const uint16_t *intra, const int16_t *mvs, int cf, const PT<BD>::pixel *const fenc_c[2],                     \
+        const PT<BD>::pixel *const ref_c[2], intptr_t cs, const uint32_t fsum[3], const uint64_t fssd[3],            \
+        const uint32_t rsum[3], const uint64_t rssd[3], int b_lookahead, int subme, int satd, int lambda,            \
+        int n_slices, int weightp_fake, PT<BD>::pixel *wlr, x264hip_weight_t weights[3], float *cost_delta,          \
+        void *stream )                                                                                               \
+    {                                                                                                                \
+        if( mbw <= 0 || mbh <= 0 || cf < 0 || cf > 3 || subme < 0 || subme > 11 || lambda < 0 || n_slices < 1 ||     \
+            !fenc_lr || !ref_lr || !ref_lr[0] || !intra || !fsum || !fssd || !rsum || !rssd || !weights ||           \
+            ( mvs && ( !ref_lr[1] || !ref_lr[2] || !ref_lr[3] ) ) ||                                                 \
+            ( !b_lookahead && cf && ( !fenc_c || !ref_c || !fenc_c[0] || !ref_c[0] ||                                \
+                                      ( cf == 3 && ( !fenc_c[1] || !ref_c[1] ) ) ) ) )                               \
+            return X264HIP_EINVAL;                                                                                   \
+        WpInput<BD> in;                                                                                              \
+        memset( &in, 0, sizeof( in ) );                                                                              \
+        in.fenc_lr = fenc_lr;                                                                                        \
+        for( int i = 0; i < 4; i++ )                                                                                 \
+            in.ref_lr[i] = ref_lr[i];                                                                                \
+        in.lrs = lrs; in.mbw = mbw; in.mbh = mbh; in.intra = intra; in.mvs = mvs; in.cf = cf;                        \
+        if( !b_lookahead && cf )                                                                                     \
+            for( int i = 0; i < 2; i++ )                                                                             \
+            {                                                                                                        \
+                in.fenc_c[i] = fenc_c[i];                                                                            \
+                in.ref_c[i] = ref_c[i];                                                                              \
+            }                                                                                                        \
+        in.cs = cs;                                                                                                  \
+        for( int i = 0; i < 3; i++ )                                                                                 \
+        {                                                                                                            \
+            in.fenc_sum[i] = fsum[i]; in.ref_sum[i] = rsum[i];                                                       \
+            in.fenc_ssd[i] = fssd[i]; in.ref_ssd[i] = rssd[i];                                                       \
+        }                                                                                                            \
+        in.b_lookahead = !!b_lookahead; in.subme = subme; in.satd = satd; in.lambda = lambda;                        \
+        in.numslices = n_slices; in.weightp_fake = weightp_fake;                                                     \
+        return map_err( weights_analyse<BD>( in, weights, cost_delta, wlr, (hipStream_t)stream ),                    \
+                        "weights_analyse" );                                                                         \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_mb_dequant_idct_add( int transform, const PT<BD>::dctcoef *dct, int mbw, int mbh,  \
                                                        int nframes, const int32_t *dmf, const int32_t *qp,           \
                                                        const PT<BD>::pixel *pred, intptr_t ps, intptr_t pfs,         \

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "x264hip.h"
+
 namespace x264hip {
 
 template <int BD> struct PT;
@@ -301,6 +303,7 @@ inline hipError_t stream_device( hipStream_t stream, int *dev )
 // ---- launchers implemented in the .hip files (all enqueue on `stream`) ----
 namespace x264hip {
 hipError_t scratch_trim( int dev );
+hipError_t scratch_alloc( void **p, size_t bytes, hipStream_t stream );   // free with hipFreeAsync
 hipError_t lowres_status( hipStream_t stream );
 hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t stream );
 template <int BD>
@@ -445,6 +448,34 @@ template <int BD>
 hipError_t launch_me_full8( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                             const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
                             int nframes, int range, uint16_t *table8, hipStream_t stream );
+// x264_weights_analyse's inputs (weightp.hip; include/x264hip.h x264hip_*_weights_analyse)
+template <int BD> struct WpInput
+{
+    const typename PT<BD>::pixel *fenc_lr;     // fenc->lowres[0] at (0,0)
+    const typename PT<BD>::pixel *ref_lr[4];   // ref->lowres[0..3] at (0,0)
+    intptr_t lrs;                              // i_stride_lowres
+    int mbw, mbh;
+    const uint16_t *intra;                     // fenc->i_intra_cost
+    const int16_t *mvs;                        // fenc->lowres_mvs[0][ref0_distance] or NULL
+    int cf;                                    // chroma format 0..3
+    const typename PT<BD>::pixel *fenc_c[2], *ref_c[2];   // NV12 plane in [0], or the U, V planes (4:4:4)
+    intptr_t cs;
+    uint32_t fenc_sum[3], ref_sum[3];
+    uint64_t fenc_ssd[3], ref_ssd[3];
+    int b_lookahead, subme, satd, lambda, numslices, weightp_fake;
+};
+template <int BD>
+hipError_t weights_analyse( const WpInput<BD> &in, x264hip_weight_t weights[3], float *cost_delta,
+                            typename PT<BD>::pixel *wlr, hipStream_t stream );
+template <int BD>
+hipError_t launch_weight_cost( int kind, const typename PT<BD>::pixel *fenc, intptr_t fs,
+                               const typename PT<BD>::pixel *const ref[4], intptr_t rs, int mbw, int mbh,
+                               const uint16_t *intra, const int16_t *mvs, int satd, int plane, int lambda,
+                               int numslices, const x264hip_weight_t *cands, int n, uint32_t *out, hipStream_t stream );
+template <int BD>
+hipError_t launch_frame_stats( const typename PT<BD>::pixel *y, intptr_t ys, const typename PT<BD>::pixel *u,
+                               const typename PT<BD>::pixel *v, intptr_t cs, int mbw, int mbh, int cf,
+                               uint64_t *stats, hipStream_t stream );
 template <int BD>
 hipError_t launch_weight_plane( typename PT<BD>::pixel *dst, intptr_t ds, intptr_t dfs,
                                 const typename PT<BD>::pixel *src, intptr_t ss, intptr_t sfs, int width, int height,

@@ -1597,13 +1597,13 @@ __global__ __launch_bounds__( 256 ) void tesa_centre_kernel( int nmb, const int1
     }
 }
 
-// stream-ordered scratch for the self-contained TESA from a memory pool the library owns,
+// stream-ordered scratch (the self-contained TESA, the weight search) from a memory pool the library owns,
 // one per device (the device of the launch stream), created with an unbounded release
 // threshold so a repeated call re-uses its blocks instead of mapping fresh pages; the
 // application's default pool is left alone.  x264hip_trim() returns the pool's idle blocks.
 static std::mutex g_pool_mu;
 static hipMemPool_t g_pools[64] = {};
-static hipError_t tesa_scratch( void **p, size_t bytes, hipStream_t stream )
+hipError_t scratch_alloc( void **p, size_t bytes, hipStream_t stream )
 {
     int dev = 0;
     hipError_t e = stream_device( stream, &dev );
@@ -1677,7 +1677,7 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
         const size_t tab = (size_t)nmb * (2 * TR + 1) * (size_t)cen_pitch( BD, TR ) * sizeof( sadt );
         const size_t bytes = tab + (size_t)nmb * 8;
         void *buf = nullptr;
-        if( tesa_scratch( &buf, bytes, stream ) == hipSuccess )
+        if( scratch_alloc( &buf, bytes, stream ) == hipSuccess )
         {
             sadt *ttab = (sadt *)buf;
             int16_t *cen = (int16_t *)((uint8_t *)buf + tab), *org = cen + 2 * nmb;
