@@ -989,6 +989,50 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_lookahead(orc, planes, origin, stride, mbw, mbh, nthr, bounded):
+    """CPU anchors of the lookahead legs on the same frames: the P search (lowres_inter_cost,
+    HEX subme 4) per pair and the B leg (lowres_bidir_cost, both lists searched) per triplet --
+    one thread, and nthr threads over independent pairs (ctypes drops the GIL in the oracle) --
+    and x264_weights_analyse on the bench's fade of frame 1 (one thread, per call)."""
+    from concurrent.futures import ThreadPoolExecutor
+    W, H = mbw * 16, mbh * 16
+    ls = (W // 2 + 64 + 63) // 64 * 64
+    lo = 32 * ls + 32
+    nf = min(planes.shape[0], 5)
+    lr = [[p.ravel() for p in orc.frame_init_lowres(8, planes[i].ravel(), origin, stride, W, H, ls)] for i in range(nf)]
+    ic = [orc.lowres_intra_cost(8, lr[i][0], lo, ls, mbw, mbh, lam=1)[0] for i in range(nf)]
+    res = {}
+
+    def p_pair(k):
+        return orc.lowres_inter_cost(8, lr[k + 1][0], lr[k], lo, ls, mbw, mbh, ic[k + 1])
+
+    def b_trip(k):
+        z = np.zeros((mbw * mbh, 2), np.int16)
+        c = np.zeros(mbw * mbh, np.int32)
+        return orc.lowres_bidir_cost(8, lr[k + 1][0], lr[k], lr[k + 2], lo, ls, mbw, mbh, 3, z, c, z, c)
+
+    pool = ThreadPoolExecutor(nthr)
+    for name, fn, n in (("lowres_me_pairs_per_s", p_pair, nf - 1), ("lowres_bidir_triplets_per_s", b_trip, nf - 2)):
+        res[name + "_1t"] = bounded(lambda fn=fn: fn(0) and 1, 1)[0]
+        jobs = [k % n for k in range(nthr)]
+        res[name] = bounded(lambda fn=fn, jobs=jobs: list(pool.map(fn, jobs)) and 1, len(jobs))[0]
+    pool.shutdown()
+    # the weight search: frame 1 faded (x 0.85 + 12) against frame 0, as rates_weightp
+    fade = np.clip(np.floor(planes[1].astype(np.float64) * 0.85 + 12 + 0.5), 0, 255).astype(np.uint8)
+    fl = [p.ravel() for p in orc.frame_init_lowres(8, fade.ravel(), origin, stride, W, H, ls)]
+    fic = orc.lowres_intra_cost(8, fl[0], lo, ls, mbw, mbh, lam=1)[0]
+    st = [orc.frame_pixel_stats(8, [p.ravel(), None, None], [origin, 0, 0], [stride, 0, 0], mbw, mbh, 0)
+          for p in (fade, planes[0])]
+    mvs = orc.lowres_inter_cost(8, fl[0], lr[0], lo, ls, mbw, mbh, fic)[0]
+    res["pixel_stats_frames_per_s_1t"] = bounded(lambda: orc.frame_pixel_stats(
+        8, [fade.ravel(), None, None], [origin, 0, 0], [stride, 0, 0], mbw, mbh, 0) and 1, 1)[0]
+    for name, kw in (("la", dict(b_lookahead=True)), ("enc", dict(b_lookahead=False, subme=7, mvs=mvs))):
+        rate = bounded(lambda kw=kw: orc.weights_analyse(8, fl[0], lr[0], lo, ls, mbw, mbh, fic, st[0], st[1],
+                                                         **kw) and 1, 1)[0]
+        res["weightp_%s_ms_1t" % name] = 1e3 / rate
+    return res
+
+
 def cpu_baseline(planes, origin, stride, mbw, mbh, R, seconds):
     """The oracle (kind "port": reference C kernels restated, -O3 -march=x86-64-v3) on the
     host cores, each leg time-bounded: the headline full-search tables (value: the box's
@@ -1053,6 +1097,7 @@ def cpu_baseline(planes, origin, stride, mbw, mbh, R, seconds):
     for n, key in ((nthr, "satd8x8_subpel_candidates_per_s"), (1, "satd8x8_subpel_candidates_per_s_1t")):
         res[key] = bounded(lambda n=n: orc.subpel_list_mt("satd", 3, fenc, stride, sp_planes, origin, stride, fo,
                                                           qxy, n)[1], len(fo))[0]
+    res.update(cpu_lookahead(orc, planes, origin, stride, mbw, mbh, nthr, bounded))
     return {"value": me_rate, "unit": "SAD16x16 candidates/s", "cores": me_used, "kind": "port",
             "cpu_model": cpu_model(), "cpus_visible": share,
             "sample": "%d full 1080p frames (%d candidates) of the same workload, %d threads, %.1f s wall; "

@@ -16,8 +16,8 @@
  *     1598-1603): the caller runs its C init x264_{8,10}_*_init() first, then
  *     x264hip_{8,10}_*_init(cpu, tab) (acts when cpu & X264HIP_CPU_HIP) or
  *     x264hip_{8,10}_*_init_hip(tab).  Entries this backend implements are
- *     replaced; every other entry (ssim_*, ssd_nv12_core, intra_*_x9_*, the
- *     trellis entries, the encoder's mbcmp / fpelcmp aliases) keeps the
+ *     replaced; every other entry (intra_*_x9_*, the trellis entries, the
+ *     never-initialised ssim[7], the encoder's mbcmp / fpelcmp aliases) keeps the
  *     caller's.  Without a usable gfx950 device the table is left untouched
  *     (reference common/opencl.c:400-409), so no installed entry can ever
  *     reach a missing device.  Every table entry is a synchronous call that
@@ -914,6 +914,14 @@ int x264hip_##BD##_mb_dequant_idct_add( int transform, const dctcoef *dct, int m
                                         intptr_t pred_stride, intptr_t pred_frame_stride,       \
                                         pixel *recon, intptr_t recon_stride,                    \
                                         intptr_t recon_frame_stride, void *stream );               \
+                                                                                                \
+/* x264_pixel_ssim_wxh (common/pixel.c:690-714) of two planes (device pointers at the region's  \
+ * top-left, as encoder.c:2517-2528 passes them): *ssim (device float) = the reference's float  \
+ * sum, accumulated in its order (bit-identical), *cnt (host, may be NULL) = its window count.  \
+ * Reads 4x4 blocks up to column 4*(width/4) - 1 and row 4*(height/4) - 1. */                    \
+int x264hip_##BD##_ssim_wxh( const pixel *pix1, intptr_t stride1, const pixel *pix2,            \
+                             intptr_t stride2, int width, int height, float *ssim, int *cnt,    \
+                             void *stream );                                                    \
                                                                                                 \
 /* the frame statistics x264_weights_analyse reads: fenc->i_pixel_sum[3] / i_pixel_ssd[3] as    \
  * x264_adaptive_quant_frame leaves them for a progressive frame (ac_energy_mb's stores,          \

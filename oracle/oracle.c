@@ -3426,3 +3426,87 @@ void FN(weights_analyse)( const pixel *fenc_lr, const pixel *const ref_lr[4], in
     free( fv );
     free( mc444 );
 }
+
+/*============================================================================
+ * SSIM — reference common/pixel.c:627-714
+ *==========================================================================*/
+void FN(ssim_4x4x2_core)( const pixel *pix1, intptr_t stride1, const pixel *pix2, intptr_t stride2, int sums[2][4] )
+{
+    for( int z = 0; z < 2; z++, pix1 += 4, pix2 += 4 )
+    {
+        uint32_t s1 = 0, s2 = 0, ss = 0, s12 = 0;
+        for( int y = 0; y < 4; y++ )
+            for( int x = 0; x < 4; x++ )
+            {
+                const int a = pix1[x + y * stride1], b = pix2[x + y * stride2];
+                s1 += a;
+                s2 += b;
+                ss += a * a;
+                ss += b * b;
+                s12 += a * b;
+            }
+        sums[z][0] = s1;
+        sums[z][1] = s2;
+        sums[z][2] = ss;
+        sums[z][3] = s12;
+    }
+}
+
+/* ssim_end1: float arithmetic above 9 bits, int below (the reference's overflow note) */
+static float ssim_end1( int s1, int s2, int ss, int s12 )
+{
+#if BIT_DEPTH > 9
+    static const float c1 = .01 * .01 * PIXEL_MAX * PIXEL_MAX * 64;
+    static const float c2 = .03 * .03 * PIXEL_MAX * PIXEL_MAX * 64 * 63;
+    const float fs1 = s1, fs2 = s2, fss = ss, fs12 = s12;
+    const float vars = fss * 64 - fs1 * fs1 - fs2 * fs2;
+    const float covar = fs12 * 64 - fs1 * fs2;
+    return (float)(2 * fs1 * fs2 + c1) * (float)(2 * covar + c2) / ((float)(fs1 * fs1 + fs2 * fs2 + c1) * (float)(vars + c2));
+#else
+    static const int c1 = (int)(.01 * .01 * PIXEL_MAX * PIXEL_MAX * 64 + .5);
+    static const int c2 = (int)(.03 * .03 * PIXEL_MAX * PIXEL_MAX * 64 * 63 + .5);
+    const int vars = ss * 64 - s1 * s1 - s2 * s2;
+    const int covar = s12 * 64 - s1 * s2;
+    return (float)(2 * s1 * s2 + c1) * (float)(2 * covar + c2) / ((float)(s1 * s1 + s2 * s2 + c1) * (float)(vars + c2));
+#endif
+}
+
+float FN(ssim_end4)( int sum0[5][4], int sum1[5][4], int width )
+{
+    float ssim = 0.0;
+    for( int i = 0; i < width; i++ )
+        ssim += ssim_end1( sum0[i][0] + sum0[i + 1][0] + sum1[i][0] + sum1[i + 1][0],
+                           sum0[i][1] + sum0[i + 1][1] + sum1[i][1] + sum1[i + 1][1],
+                           sum0[i][2] + sum0[i + 1][2] + sum1[i][2] + sum1[i + 1][2],
+                           sum0[i][3] + sum0[i + 1][3] + sum1[i][3] + sum1[i + 1][3] );
+    return ssim;
+}
+
+/* x264_pixel_ssim_wxh: the two sum rows swap as the window row advances */
+float FN(ssim_wxh)( const pixel *pix1, intptr_t stride1, const pixel *pix2, intptr_t stride2, int width, int height,
+                    int *cnt )
+{
+    int z = 0;
+    float ssim = 0.0;
+    int (*buf)[4] = malloc( sizeof(int) * 4 * (2 * ((width >> 2) + 3)) );
+    int (*sum0)[4] = buf, (*sum1)[4] = buf + (width >> 2) + 3;
+    width >>= 2;
+    height >>= 2;
+    for( int y = 1; y < height; y++ )
+    {
+        for( ; z <= y; z++ )
+        {
+            int (*t)[4] = sum0;
+            sum0 = sum1;
+            sum1 = t;
+            for( int x = 0; x < width; x += 2 )
+                FN(ssim_4x4x2_core)( &pix1[4 * (x + z * stride1)], stride1, &pix2[4 * (x + z * stride2)], stride2,
+                                     (int (*)[4])&sum0[x] );
+        }
+        for( int x = 0; x < width - 1; x += 4 )
+            ssim += FN(ssim_end4)( sum0 + x, sum1 + x, width - x - 1 < 4 ? width - x - 1 : 4 );
+    }
+    *cnt = (height - 1) * (width - 1);
+    free( buf );
+    return ssim;
+}

@@ -686,3 +686,29 @@ def weights_analyse(bd, fenc_lr, ref_lr, lr_origin, lrs, mbw, mbh, intra, fstats
                               n_slices, int(weightp_fake), w.ctypes.data, _addr(cd),
                               None if weighted is None else _addr(weighted, lr_origin))
     return w, (None if cd[0] == -1.0 else float(cd[0]))
+
+
+# ---- SSIM (pixel.c:627-714) ----
+for _bd in (8, 10):
+    _f(_bd, "ssim_4x4x2_core", [_P, _IP, _P, _IP, _P])
+    _f(_bd, "ssim_end4", [_P, _P, C.c_int], C.c_float)
+    _f(_bd, "ssim_wxh", [_P, _IP, _P, _IP, C.c_int, C.c_int, _P], C.c_float)
+
+
+def ssim_4x4x2_core(bd, a, a_off, sa, b, b_off, sb):
+    s = np.zeros((2, 4), np.int32)
+    fn(bd, "ssim_4x4x2_core")(_addr(a, a_off), sa, _addr(b, b_off), sb, _addr(s))
+    return s
+
+
+def ssim_end4(bd, sum0, sum1, width):
+    s0 = np.ascontiguousarray(sum0, np.int32).reshape(5, 4)
+    s1 = np.ascontiguousarray(sum1, np.int32).reshape(5, 4)
+    return np.float32(fn(bd, "ssim_end4")(_addr(s0), _addr(s1), width))
+
+
+def ssim_wxh(bd, a, a_off, sa, b, b_off, sb, width, height):
+    """x264_pixel_ssim_wxh: (ssim float32, cnt)"""
+    cnt = C.c_int(0)
+    v = fn(bd, "ssim_wxh")(_addr(a, a_off), sa, _addr(b, b_off), sb, width, height, C.byref(cnt))
+    return np.float32(v), cnt.value

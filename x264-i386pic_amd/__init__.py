@@ -184,6 +184,9 @@ ZSUB_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P)
 ZSUBAC_T = _c.CFUNCTYPE(_c.c_int, _P, _P, _P, _P)
 ZINTER_T = _c.CFUNCTYPE(None, _P, _P, _P)
 INTRA_X3_T = _c.CFUNCTYPE(None, _P, _P, _P)                        # intra_*_x3(fenc, fdec|edge, res[3])
+SSD_NV12_T = _c.CFUNCTYPE(None, _P, _IP, _P, _IP, _c.c_int, _c.c_int, _P, _P)   # ssd_nv12_core
+SSIM_CORE_T = _c.CFUNCTYPE(None, _P, _IP, _P, _IP, _P)             # ssim_4x4x2_core(p1, s1, p2, s2, sums)
+SSIM_END4_T = _c.CFUNCTYPE(_c.c_float, _P, _P, _c.c_int)           # ssim_end4(sum0, sum1, width)
 
 
 class PixelFunctions(_c.Structure):
@@ -193,8 +196,8 @@ class PixelFunctions(_c.Structure):
         ("sa8d", CMP_T * 4), ("mbcmp", CMP_T * 8), ("mbcmp_unaligned", CMP_T * 8),
         ("fpelcmp", CMP_T * 8), ("fpelcmp_x3", CMP_X3_T * 7), ("fpelcmp_x4", CMP_X4_T * 7),
         ("sad_aligned", CMP_T * 8), ("vsad", VSAD_T), ("asd8", ASD8_T), ("sa8d_satd", CMP64_T * 1),
-        ("var", VAR_T * 4), ("var2", VAR2_T * 4), ("hadamard_ac", VAR_T * 4), ("ssd_nv12_core", _P),
-        ("ssim_4x4x2_core", _P), ("ssim_end4", _P),
+        ("var", VAR_T * 4), ("var2", VAR2_T * 4), ("hadamard_ac", VAR_T * 4),
+        ("ssd_nv12_core", SSD_NV12_T), ("ssim_4x4x2_core", SSIM_CORE_T), ("ssim_end4", SSIM_END4_T),
         ("sad_x3", CMP_X3_T * 7), ("sad_x4", CMP_X4_T * 7),
         ("satd_x3", CMP_X3_T * 7), ("satd_x4", CMP_X4_T * 7), ("ads", ADS_T * 7),
     ] + [(n, INTRA_X3_T) for n in (
@@ -830,6 +833,20 @@ WCOST_LUMA, WCOST_CHROMA420, WCOST_CHROMA422, WCOST_CHROMA444 = 0, 1, 2, 3
 
 def _plane_ptr(t, origin):
     return None if t is None else _ptr(t, origin)
+
+
+def ssim_wxh(pix1, origin1, stride1, pix2, origin2, stride2, width, height):
+    """x264_pixel_ssim_wxh (x264hip_*_ssim_wxh): (ssim float, cnt); planes with the region's
+    top-left at element origin1 / origin2"""
+    import torch
+    bd = _pix_bd(pix1)
+    out = torch.empty(1, dtype=torch.float32, device=pix1.device)
+    cnt = _c.c_int(0)
+    f = getattr(lib(), f"x264hip_{bd}_ssim_wxh")
+    f.argtypes = [_P, _IP, _P, _IP, _c.c_int, _c.c_int, _P, _P, _P]
+    _rc(f(_ptr(pix1, origin1), stride1, _ptr(pix2, origin2), stride2, width, height, _ptr(out), _c.byref(cnt),
+          _stream()), "ssim_wxh")
+    return float(out.item()), cnt.value
 
 
 def frame_pixel_stats(luma, luma_origin, luma_stride, mb_width, mb_height, chroma_format=0, chroma_u=None,

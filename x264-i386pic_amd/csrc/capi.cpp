@@ -677,6 +677,88 @@ template <int BD>
 static int c_asd8( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::pixel *p2, intptr_t s2, int height )
 { return height < 1 ? 0 : (int)stat_call<BD, X264HIP_STAT_ASD8, 3>( p1, s1, p2, s2, 8, height, height ); }
 
+// ssim_4x4x2_core (pixel.c:627-652): the two 4x4 blocks at pix1 / pix2 staged as one 8x4 block each
+template <int BD>
+static void c_ssim_4x4x2_core( const typename PT<BD>::pixel *p1, intptr_t s1, const typename PT<BD>::pixel *p2,
+                               intptr_t s2, int sums[2][4] )
+{
+    using pixel = typename PT<BD>::pixel;
+    CallCtx &c = call_ctx();
+    pixel *a = (pixel *)(c.host + ST_A), *b = (pixel *)(c.host + ST_B);
+    int32_t *out = (int32_t *)(c.host + ST_SC);
+    stage_block( a, p1, s1, 8, 4 );
+    stage_block( b, p2, s2, 8, 4 );
+    CHECK_FATAL( launch_ssim_core<BD>( dview( c, a ), 8, dview( c, b ), 8, dview( c, out ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    memcpy( sums, out, 8 * sizeof( int ) );
+}
+
+// ssim_end4 (pixel.c:679-688) of the caller's two sum rows (5 x 4 ints each, width <= 4)
+template <int BD>
+static float c_ssim_end4( int sum0[5][4], int sum1[5][4], int width )
+{
+    CallCtx &c = call_ctx();
+    int32_t *s = (int32_t *)(c.host + ST_A);
+    float *out = (float *)(c.host + ST_SC);
+    memcpy( s, sum0, 20 * sizeof( int ) );
+    memcpy( s + 20, sum1, 20 * sizeof( int ) );
+    CHECK_FATAL( launch_ssim_end4<BD>( dview( c, s ), dview( c, s + 20 ), width, dview( c, out ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    return *out;
+}
+
+// ssd_nv12_core (pixel.c:128-151; x264_pixel_ssd_nv12 hands it the width & ~7 core of whole
+// chroma planes): both interleaved regions staged into a per-thread pinned buffer that
+// grows to the largest region seen, then the plane SSD kernel's NV12 form
+namespace {
+struct BigStage
+{
+    int device = -1;
+    uint8_t *host = nullptr, *dev = nullptr;
+    size_t size = 0;
+    ~BigStage()
+    {
+        if( host )
+            (void)hipHostFree( host );
+    }
+};
+thread_local BigStage t_big;
+}
+template <int BD>
+static void c_ssd_nv12_core( typename PT<BD>::pixel *p1, intptr_t s1, typename PT<BD>::pixel *p2, intptr_t s2,
+                             int width, int height, uint64_t *ssd_u, uint64_t *ssd_v )
+{
+    using pixel = typename PT<BD>::pixel;
+    if( width <= 0 || height <= 0 )
+    {
+        *ssd_u = *ssd_v = 0;
+        return;
+    }
+    CallCtx &c = call_ctx();
+    const size_t plane = (size_t)2 * width * height * sizeof( pixel );
+    const size_t need = 2 * plane + 64;
+    if( t_big.device != c.device || t_big.size < need )
+    {
+        if( t_big.host )
+            CHECK_FATAL( hipHostFree( t_big.host ) );
+        t_big.host = nullptr;
+        CHECK_FATAL( hipHostMalloc( (void **)&t_big.host, need, hipHostMallocDefault ) );
+        CHECK_FATAL( hipHostGetDevicePointer( (void **)&t_big.dev, t_big.host, 0 ) );
+        t_big.size = need;
+        t_big.device = c.device;
+    }
+    pixel *a = (pixel *)t_big.host, *b = (pixel *)(t_big.host + plane);
+    stage_block( a, p1, s1, 2 * width, height );
+    stage_block( b, p2, s2, 2 * width, height );
+    uint64_t *out = (uint64_t *)(c.host + ST_SC);
+    CHECK_FATAL( launch_plane_ssd<BD>( 1, (const pixel *)t_big.dev, 2 * width, 0,
+                                       (const pixel *)(t_big.dev + plane), 2 * width, 0, width, height, 1,
+                                       dview( c, out ), c.stream ) );
+    CHECK_FATAL( hipStreamSynchronize( c.stream ) );
+    *ssd_u = out[0];
+    *ssd_v = out[1];
+}
+
 // var2: U at fenc[x], V at fenc[x + FENC_STRIDE/2]; fdec stride FDEC_STRIDE (pixel.c:203-227)
 template <int BD, int IPIX>
 static int c_var2( typename PT<BD>::pixel *fenc, typename PT<BD>::pixel *fdec, int ssd[2] )
@@ -1158,6 +1240,10 @@ static void fill_pixel( Tab *pf )
     pf->hadamard_ac[3] = c_hadamard_ac<BD, 3>;
     pf->vsad = c_vsad<BD>;
     pf->asd8 = c_asd8<BD>;
+    // ssim and the NV12 SSD core (pixel.c:861-865)
+    pf->ssd_nv12_core = c_ssd_nv12_core<BD>;
+    pf->ssim_4x4x2_core = c_ssim_4x4x2_core<BD>;
+    pf->ssim_end4 = c_ssim_end4<BD>;
     // ads slots with the reference's aliasing (pixel.c:835-838, 1605-1608)
     pf->ads[0] = c_ads<0>;
     pf->ads[1] = c_ads<1>;
@@ -1356,10 +1442,11 @@ static void build_banner()
                   prop.multiProcessorCount );
     snprintf( g_banner, sizeof(g_banner),
               "x264hip: %s; HIP entries: pixel sad/sad_aligned/ssd/satd[8] sad_x3/x4 satd_x3/x4[7] sa8d[2] "
-              "sa8d_satd var[3] var2[2] hadamard_ac[4] vsad asd8 ads[7] intra_*_x3[10]; dct 17/17; "
+              "sa8d_satd var[3] var2[2] hadamard_ac[4] vsad asd8 ads[7] intra_*_x3[10] ssd_nv12_core "
+              "ssim_4x4x2_core ssim_end4; dct 17/17; "
               "quant quant[5] dequant[3] idct_dequant_2x4[2] optimize_chroma[2] denoise decimate[3] coeff_last[16] "
-              "coeff_level_run[15]; zigzag 6+6; kept from the caller's C init: ssim[7] ssd_nv12_core "
-              "ssim_4x4x2_core ssim_end4 intra_*_x9 trellis_cabac_*",
+              "coeff_level_run[15]; zigzag 6+6; kept from the caller's C init: intra_*_x9 trellis_cabac_* "
+              "(ssim[7] is never set by the reference)",
               name );
 }
 
@@ -1380,8 +1467,8 @@ extern "C" const char *x264hip_backend_banner( void )
 }
 
 // Table initialisers.  Both forms only OVERRIDE: the entries this backend
-// implements are replaced, every other entry (ssim_*, the trellis entries,
-// intra_*_x9_*, and the encoder's mbcmp / fpelcmp aliases) keeps what the caller's
+// implements are replaced, every other entry (the trellis entries, intra_*_x9_*, the
+// never-initialised ssim[7], and the encoder's mbcmp / fpelcmp aliases) keeps what the caller's
 // C init put there.  Without a usable gfx950 device (or without X264HIP_CPU_HIP in
 // `cpu` for the flag form) the table is left untouched, so a host without the GPU
 // keeps its C entries, the convention of reference common/opencl.c:400-409; no
@@ -1862,6 +1949,17 @@ extern "C" const char *x264hip_backend_banner( void )
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_frame_init_lowres<BD>( src, stride, fstride, width, height, nframes, dst, ds, dfs,     \
                                                       (hipStream_t)stream ), "frame_init_lowres" );                  \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_ssim_wxh( const PT<BD>::pixel *p1, intptr_t s1, const PT<BD>::pixel *p2,          \
+                                            intptr_t s2, int width, int height, float *ssim, int *cnt,              \
+                                            void *stream )                                                           \
+    {                                                                                                                \
+        if( width < 0 || height < 0 || !ssim || ( width >= 8 && height >= 8 && ( !p1 || !p2 ) ) )                   \
+            return X264HIP_EINVAL;                                                                                   \
+        if( cnt )                                                                                                    \
+            *cnt = ( (height >> 2) - 1 ) * ( (width >> 2) - 1 );                                                     \
+        return map_err( launch_ssim_wxh<BD>( p1, s1, p2, s2, width, height, ssim, (hipStream_t)stream ),             \
+                        "ssim_wxh" );                                                                                \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_frame_pixel_stats( const PT<BD>::pixel *luma, intptr_t ls,                        \
                                                      const PT<BD>::pixel *cu, const PT<BD>::pixel *cv, intptr_t cs,  \

@@ -477,6 +477,14 @@ hipError_t launch_frame_stats( const typename PT<BD>::pixel *y, intptr_t ys, con
                                const typename PT<BD>::pixel *v, intptr_t cs, int mbw, int mbh, int cf,
                                uint64_t *stats, hipStream_t stream );
 template <int BD>
+hipError_t launch_ssim_wxh( const typename PT<BD>::pixel *p1, intptr_t s1, const typename PT<BD>::pixel *p2,
+                            intptr_t s2, int width, int height, float *out, hipStream_t stream );
+template <int BD>
+hipError_t launch_ssim_core( const typename PT<BD>::pixel *p1, intptr_t s1, const typename PT<BD>::pixel *p2,
+                             intptr_t s2, int *out, hipStream_t stream );
+template <int BD>
+hipError_t launch_ssim_end4( const int *s0, const int *s1, int width, float *out, hipStream_t stream );
+template <int BD>
 hipError_t launch_weight_plane( typename PT<BD>::pixel *dst, intptr_t ds, intptr_t dfs,
                                 const typename PT<BD>::pixel *src, intptr_t ss, intptr_t sfs, int width, int height,
                                 int nframes, int scale, int denom, int offset, hipStream_t stream );

@@ -15,6 +15,8 @@
 #include <math.h>
 #include <string.h>
 
+#include <algorithm>
+
 namespace x264hip {
 
 // candidate list of one launch: c = scale | denom << 8 | weighted << 11 | (offset + 256) << 12;
@@ -379,7 +381,7 @@ template hipError_t launch_weight_cost<10>( int, const uint16_t *, intptr_t, con
                                             const x264hip_weight_t *, int, uint32_t *, hipStream_t );
 
 // ---- frame statistics: ac_energy_mb's stores (ratecontrol.c:225-257, 289-299) ----
-__device__ __forceinline__ uint32_t wave_sum( uint32_t v )
+__device__ __forceinline__ unsigned long long wave_sum64( unsigned long long v )
 {
 #pragma unroll
     for( int m = 1; m < 64; m <<= 1 )
@@ -387,9 +389,12 @@ __device__ __forceinline__ uint32_t wave_sum( uint32_t v )
     return v;
 }
 
-// one wave per MB: PIXEL_VAR_C's (sum, sum of squares) of the 16x16 luma block and of the
-// chroma blocks (8 x 16>>vshift deinterleaved, or 16x16 planes for 4:4:4), added into
-// acc[plane] (sums) / acc[3 + plane] (squares)
+// PIXEL_VAR_C's (sum, sum of squares) of every MB's 16x16 luma block and chroma blocks (8 x
+// 16>>vshift deinterleaved from the NV12 / NV16 plane, or the 16x16 blocks of the 4:4:4
+// planes), summed into acc[plane] (sums) / acc[3 + plane] (squares).  A wave walks MBs
+// grid-stride (luma: lane = row * 4 + 4-pixel column group) with 64-bit lane accumulators;
+// one wave reduction and one atomic per quantity per workgroup at the end.  The sums' low 32
+// bits are the uint32 field's wrapped total (addition mod 2^32 commutes).
 template <int BD>
 __global__ __launch_bounds__( 256 ) void frame_stats_kernel( const typename PT<BD>::pixel *__restrict__ y,
                                                              intptr_t ys, const typename PT<BD>::pixel *__restrict__ u,
@@ -397,53 +402,57 @@ __global__ __launch_bounds__( 256 ) void frame_stats_kernel( const typename PT<B
                                                              intptr_t cs, int mbw, int mbh, int cf,
                                                              unsigned long long *__restrict__ acc )
 {
-    const int lane = threadIdx.x & 63;
-    const int mb = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if( mb >= mbw * mbh )
-        return;
-    const int mby = mb / mbw, mbx = mb - mby * mbw;
-    auto sq4 = [&]( const typename PT<BD>::pixel *p, intptr_t s, int plane ) {
-        const typename PT<BD>::pixel *q = p + (intptr_t)(16 * mby + (lane >> 2)) * s + 16 * mbx + 4 * (lane & 3);
+    constexpr int PPD = PT<BD>::PPD, NDW = 4 / PPD;
+    __shared__ unsigned long long part[4][6];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long a[6] = { 0, 0, 0, 0, 0, 0 };
+    const int nmb = mbw * mbh;
+    auto sq4 = [&]( const typename PT<BD>::pixel *p, intptr_t s, int mbx, int mby, int plane ) {
+        uint32_t w[NDW];
+        load_al<NDW>( p + (intptr_t)(16 * mby + (lane >> 2)) * s + 16 * mbx + 4 * (lane & 3), w );
         uint32_t sum = 0, sqr = 0;
 #pragma unroll
         for( int k = 0; k < 4; k++ )
         {
-            const uint32_t x = q[k];
+            const uint32_t x = (uint32_t)upix<BD>( w[k / PPD], k % PPD );
             sum += x;
             sqr += x * x;
         }
-        sum = wave_sum( sum );
-        sqr = wave_sum( sqr );
-        if( lane == 0 )
-        {
-            atomicAdd( acc + plane, (unsigned long long)sum );
-            atomicAdd( acc + 3 + plane, (unsigned long long)sqr );
-        }
+        a[plane] += sum;
+        a[3 + plane] += sqr;
     };
-    sq4( y, ys, 0 );
-    if( cf == 3 )
+    for( int mb = blockIdx.x * 4 + wave; mb < nmb; mb += gridDim.x * 4 )
     {
-        sq4( u, cs, 1 );
-        sq4( v, cs, 2 );
+        const int mby = mb / mbw, mbx = mb - mby * mbw;
+        sq4( y, ys, mbx, mby, 0 );
+        if( cf == 3 )
+        {
+            sq4( u, cs, mbx, mby, 1 );
+            sq4( v, cs, mbx, mby, 2 );
+        }
+        else if( cf )
+        {
+            const int H = cf == 1 ? 8 : 16;
+            for( int row = lane >> 3; row < H; row += 8 )
+            {
+                const typename PT<BD>::pixel *q = u + (intptr_t)(H * mby + row) * cs + 16 * mbx + 2 * (lane & 7);
+                const uint32_t p0 = q[0], p1 = q[1];
+                a[1] += p0; a[4] += p0 * p0; a[2] += p1; a[5] += p1 * p1;
+            }
+        }
     }
-    else if( cf )
+#pragma unroll
+    for( int i = 0; i < 6; i++ )
     {
-        const int H = cf == 1 ? 8 : 16;
-        uint32_t su = 0, qu = 0, sv = 0, qv = 0;
-        for( int row = lane >> 3; row < H; row += 8 )
-        {
-            const typename PT<BD>::pixel *q = u + (intptr_t)(H * mby + row) * cs + 16 * mbx + 2 * (lane & 7);
-            const uint32_t a = q[0], b = q[1];
-            su += a; qu += a * a; sv += b; qv += b * b;
-        }
-        su = wave_sum( su ); qu = wave_sum( qu ); sv = wave_sum( sv ); qv = wave_sum( qv );
+        const unsigned long long t = wave_sum64( a[i] );
         if( lane == 0 )
-        {
-            atomicAdd( acc + 1, (unsigned long long)su );
-            atomicAdd( acc + 4, (unsigned long long)qu );
-            atomicAdd( acc + 2, (unsigned long long)sv );
-            atomicAdd( acc + 5, (unsigned long long)qv );
-        }
+            part[wave][i] = t;
+    }
+    __syncthreads();
+    if( threadIdx.x < 6 )
+    {
+        const int i = threadIdx.x;
+        atomicAdd( acc + i, part[0][i] + part[1][i] + part[2][i] + part[3][i] );
     }
 }
 
@@ -470,7 +479,7 @@ hipError_t launch_frame_stats( const typename PT<BD>::pixel *y, intptr_t ys, con
     if( e != hipSuccess )
         return e;
     if( mbw > 0 && mbh > 0 )
-        hipLaunchKernelGGL( frame_stats_kernel<BD>, dim3( (unsigned)((mbw * mbh + 3) / 4) ), dim3( 256 ), 0, stream,
+        hipLaunchKernelGGL( frame_stats_kernel<BD>, dim3( (unsigned)std::min( (mbw * mbh + 3) / 4, 1024 ) ), dim3( 256 ), 0, stream,
                             y, ys, u, v, cs, mbw, mbh, cf, (unsigned long long *)stats );
     hipLaunchKernelGGL( frame_stats_finish_kernel, dim3( 1 ), dim3( 64 ), 0, stream, (unsigned long long *)stats,
                         mbw > 0 ? mbw : 1, mbh > 0 ? mbh : 1, cf );
