@@ -921,7 +921,7 @@ template hipError_t launch_me_search_esa<10>( const uint16_t *, intptr_t, intptr
 // result only if strictly better (COPY3_IF_LT, me.h:87-93).
 // Table geometry: rows = 2R+1 at `pitch`, `cols` valid columns, window origin (ox, oy)
 // from `origin` (centred tables) or (-R, -R) (full tables).
-template <int BD>
+template <int BD, int MAXS>
 __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT<BD>::sadt *__restrict__ table, int R,
                                                                int cols, int pitch, int nmb, int me_range,
                                                                const int16_t *__restrict__ origin,
@@ -947,7 +947,18 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
     const int width = (max_x - min_x + 3) & ~3;
     const int ox = origin ? origin[2 * mb] : -R, oy = origin ? origin[2 * mb + 1] : -R;
     const int y0 = max( min_y, oy ), y1 = min( max_y, oy + W - 1 );
+    const int nsteps = width > 0 && y1 >= y0 ? (y1 - y0 + rps) / rps : 0;   // wave-uniform, <= MAXS
     const chunk *t = (const chunk *)(table + mb * (int64_t)(W * pitch)) + ch;
+    // every step's table chunk is requested before any is used: one memory round trip per MB
+    // instead of one per step (the loop form waited on each step's load in turn)
+    chunk v[MAXS];
+#pragma unroll
+    for( int st = 0; st < MAXS; st++ )
+    {
+        const int my = y0 + st * rps + rr;
+        if( st < nsteps && rr < rps && my <= y1 )
+            v[st] = t[(my - oy) * nch];
+    }
     // the MB's cost_mv terms in two gathers -- column c's in lane c, table row r's in lane r --
     // handed to the lanes that use them by ds_bpermute (the LDS crossbar, not the address
     // path the table loads need): a lane's four columns once, a row's term once per step
@@ -961,30 +972,26 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
     for( int k = 0; k < 4; k++ )
         ck[k] = (uint32_t)__builtin_amdgcn_ds_bpermute( 4 * (4 * ch + k), (int)ckl );
     uint32_t key = 0xFFFFFFFFu;
-    if( width > 0 )
-    {
-        for( int my0 = y0; my0 <= y1; my0 += rps )                  // wave-uniform trip count
-        {
-            const int my = my0 + rr;
-            const bool live = rr < rps && my <= y1;
-            const uint32_t S = (uint32_t)__builtin_amdgcn_ds_bpermute( 4 * min( my - oy, 63 ), (int)Sl );
-            if( live )
-            {
-                const chunk v = t[(my - oy) * nch];
-                uint32_t s[4];
-                if constexpr( BD == 8 )
-                {
-                    s[0] = v.x & 0xffff; s[1] = v.x >> 16; s[2] = v.y & 0xffff; s[3] = v.y >> 16;
-                }
-                else
-                {
-                    s[0] = v.x; s[1] = v.y; s[2] = v.z; s[3] = v.w;
-                }
 #pragma unroll
-                for( int k = 0; k < 4; k++ )
-                    key = min( key, __builtin_elementwise_add_sat(
-                                        __builtin_elementwise_add_sat( s[k] << 12, ck[k] ), S ) );
+    for( int st = 0; st < MAXS; st++ )
+    {
+        const int my = y0 + st * rps + rr;
+        const uint32_t S = (uint32_t)__builtin_amdgcn_ds_bpermute( 4 * min( max( my - oy, 0 ), 63 ), (int)Sl );
+        if( st < nsteps && rr < rps && my <= y1 )
+        {
+            uint32_t s4[4];
+            if constexpr( BD == 8 )
+            {
+                s4[0] = v[st].x & 0xffff; s4[1] = v[st].x >> 16; s4[2] = v[st].y & 0xffff; s4[3] = v[st].y >> 16;
             }
+            else
+            {
+                s4[0] = v[st].x; s4[1] = v[st].y; s4[2] = v[st].z; s4[3] = v[st].w;
+            }
+#pragma unroll
+            for( int k = 0; k < 4; k++ )
+                key = min( key, __builtin_elementwise_add_sat(
+                                    __builtin_elementwise_add_sat( s4[k] << 12, ck[k] ), S ) );
         }
     }
 #pragma unroll
@@ -1018,8 +1025,20 @@ hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int 
     const int pitch = origin ? cen_pitch( BD, R ) : full_pitch( R );
     if( pitch > 64 || ((uintptr_t)table & (BD == 8 ? 7 : 15)) )
         return hipErrorInvalidValue;
-    hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD> ), dim3( (nmb + 3) / 4 ), dim3( 256 ), 0, stream, table, R, cols,
-                        pitch, nmb, me_range, origin, par, init_cost, cost_mv, out );
+    // steps of 64 / (pitch / 4) rows cover the 2R+1 table rows
+    const int rps = 64 / (pitch >> 2), steps = (2 * R + 1 + rps - 1) / rps;
+    const dim3 g( (unsigned)((nmb + 3) / 4) ), b( 256 );
+    if( steps <= 4 )
+        hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD, 4> ), g, b, 0, stream, table, R, cols, pitch, nmb, me_range,
+                            origin, par, init_cost, cost_mv, out );
+    else if( steps <= 8 )
+        hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD, 8> ), g, b, 0, stream, table, R, cols, pitch, nmb, me_range,
+                            origin, par, init_cost, cost_mv, out );
+    else if( steps <= 16 )
+        hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD, 16> ), g, b, 0, stream, table, R, cols, pitch, nmb, me_range,
+                            origin, par, init_cost, cost_mv, out );
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
