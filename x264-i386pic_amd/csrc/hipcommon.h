@@ -93,6 +93,26 @@ __device__ __forceinline__ void load_al( const void *p, uint32_t (&out)[NDW] )
         out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
 }
 
+// load_al's form for padded planes: the NDW + 1 consecutive dwords from the aligned-down
+// address as ONE vector load (global_load_dwordx{2,3,4,...}); the conditional re-read of
+// load_al splits it into single-dword loads plus a select, which refine_subpel's address
+// path measured at 0.138 -> 0.185 ms per 130560 MBs.  Reads up to 4 bytes past the pixels
+// asked for: only for planes with a border (x264's 32-pixel padding).
+template <int NDW>
+__device__ __forceinline__ void load_al_pad( const void *p, uint32_t (&out)[NDW] )
+{
+    typedef const __attribute__( ( address_space( 1 ) ) ) uint32_t gword;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+    gword *base = (gword *)((uintptr_t)p & ~(uintptr_t)3);
+    uint32_t w[NDW + 1];
+#pragma unroll
+    for( int i = 0; i <= NDW; i++ )
+        w[i] = base[i];
+#pragma unroll
+    for( int i = 0; i < NDW; i++ )
+        out[i] = __builtin_amdgcn_alignbyte( w[i + 1], w[i], sh );
+}
+
 // rounding-up average of packed pixels (pixel_avg, reference common/mc.c:57): one
 // v_lerp_u8 per dword at 8 bit
 template <int BD> __device__ __forceinline__ uint32_t avg_round( uint32_t a, uint32_t b )

@@ -195,7 +195,7 @@ template <int BD> struct LrCtx
         for( int y = 0; y < LR_NR; y++ )
         {
             uint32_t w[NDW];
-            load_al<NDW>( r + (intptr_t)y * stride, w );
+            load_al_pad<NDW>( r + (intptr_t)y * stride, w );
 #pragma unroll
             for( int k = 0; k < NDW; k++ )
                 acc = sadp<BD>( fe[y][k], w[k], acc );
@@ -260,7 +260,7 @@ template <int BD> struct LrCtx
         const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((my & 3) == 3) * stride;
 #pragma unroll
         for( int y = 0; y < LR_NR; y++ )
-            load_al<NDW>( s1 + (intptr_t)y * stride, r[y] );
+            load_al_pad<NDW>( s1 + (intptr_t)y * stride, r[y] );
         if( idx & 5 )                       // two planes: the rounding average
         {
             const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((mx & 3) == 3);
@@ -268,7 +268,7 @@ template <int BD> struct LrCtx
             for( int y = 0; y < LR_NR; y++ )
             {
                 uint32_t b[NDW];
-                load_al<NDW>( s2 + (intptr_t)y * stride, b );
+                load_al_pad<NDW>( s2 + (intptr_t)y * stride, b );
 #pragma unroll
                 for( int k = 0; k < NDW; k++ )
                     r[y][k] = avg_round<BD>( r[y][k], b[k] );
@@ -291,7 +291,7 @@ template <int BD> struct LrCtx
         const pixel *s = (i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : p3) + (mx >> 2) + (intptr_t)(my >> 2) * stride;
 #pragma unroll
         for( int y = 0; y < LR_NR; y++ )
-            load_al<NDW>( s + (intptr_t)y * stride, r[y] );
+            load_al_pad<NDW>( s + (intptr_t)y * stride, r[y] );
     }
 
     // get_ref at a quarter-pel mv, then SAD or SATD 8x8 (W = false: the unweighted planes)

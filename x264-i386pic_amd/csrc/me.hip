@@ -994,10 +994,18 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
                                     __builtin_elementwise_add_sat( s4[k] << 12, ck[k] ), S ) );
         }
     }
-#pragma unroll
-    for( int off = 32; off >= 1; off >>= 1 )
-        key = min( key, (uint32_t)__shfl_xor( (int)key, off ) );
-    if( lane == 0 )
+    // the wave minimum by DPP (row_shr 1/2/4/8, row_bcast 15/31): lane 63 ends with it, no
+    // LDS-crossbar round trips on the MB's tail
+    {
+        constexpr int I = (int)0xFFFFFFFF;
+        key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)key, 0x111, 0xF, 0xF, false ) );
+        key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)key, 0x112, 0xF, 0xF, false ) );
+        key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)key, 0x114, 0xF, 0xF, false ) );
+        key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)key, 0x118, 0xF, 0xF, false ) );
+        key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)key, 0x142, 0xA, 0xF, false ) );
+        key = min( key, (uint32_t)__builtin_amdgcn_update_dpp( I, (int)key, 0x143, 0xC, 0xF, false ) );
+    }
+    if( lane == 63 )
     {
         int32_t bcost = init_cost[mb], rx = bmx, ry = bmy;
         if( key < 0xC0000000u && (int32_t)(key >> 12) < bcost )

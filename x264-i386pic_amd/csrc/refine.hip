@@ -49,13 +49,13 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
     uint32_t r1[4][HDW];
 #pragma unroll
     for( int y = 0; y < 4; y++ )
-        load_al<HDW>( s1 + y * rs, r1[y] );
+        load_al_pad<HDW>( s1 + y * rs, r1[y] );
     if( idx & 5 )                           // two planes: the rounding average (one plane: avg( a, a ) = a)
     {
         uint32_t r2[4][HDW];
 #pragma unroll
         for( int y = 0; y < 4; y++ )
-            load_al<HDW>( s2 + y * rs, r2[y] );
+            load_al_pad<HDW>( s2 + y * rs, r2[y] );
 #pragma unroll
         for( int y = 0; y < 4; y++ )
 #pragma unroll

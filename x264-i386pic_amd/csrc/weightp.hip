@@ -36,7 +36,7 @@ __device__ __forceinline__ void wp_row8( const typename PT<BD>::pixel *p, int (&
 {
     constexpr int PPD = PT<BD>::PPD, NDW = 8 / PPD;
     uint32_t w[NDW];
-    load_al<NDW>( p, w );
+    load_al_pad<NDW>( p, w );
 #pragma unroll
     for( int k = 0; k < 8; k++ )
         o[k] = upix<BD>( w[k / PPD], k % PPD );
@@ -108,11 +108,11 @@ __global__ __launch_bounds__( 256 ) void wp_cost8_kernel( const typename PT<BD>:
         const typename PT<BD>::pixel *s1 = P[c_hpel_ref0[q]] + off + ((mvy & 3) == 3) * rs;
         constexpr int PPD = PT<BD>::PPD, NDW = 8 / PPD;
         uint32_t w1[NDW];
-        load_al<NDW>( s1, w1 );
+        load_al_pad<NDW>( s1, w1 );
         if( q & 5 )
         {
             uint32_t w2[NDW];
-            load_al<NDW>( P[c_hpel_ref1[q]] + off + ((mvx & 3) == 3), w2 );
+            load_al_pad<NDW>( P[c_hpel_ref1[q]] + off + ((mvx & 3) == 3), w2 );
 #pragma unroll
             for( int i = 0; i < NDW; i++ )
                 w1[i] = avg_round<BD>( w1[i], w2[i] );
@@ -211,7 +211,7 @@ __global__ __launch_bounds__( 256 ) void wp_chroma_kernel( const typename PT<BD>
     {
         constexpr int NDW = 16 / PPD;
         uint32_t w[NDW];
-        load_al<NDW>( fenc + (intptr_t)(H * by + r) * fs + 16 * bx, w );
+        load_al_pad<NDW>( fenc + (intptr_t)(H * by + r) * fs + 16 * bx, w );
 #pragma unroll
         for( int x = 0; x < 8; x++ )
         {
@@ -229,8 +229,8 @@ __global__ __launch_bounds__( 256 ) void wp_chroma_kernel( const typename PT<BD>
             ref + (intptr_t)(H * by + r + (mvy >> 3)) * rs + 16 * bx + (mvx >> 3) * 2 + pl;
         constexpr int NDW = (18 + PPD - 1) / PPD;
         uint32_t a[NDW], c[NDW];
-        load_al<NDW>( s, a );
-        load_al<NDW>( s + rs, c );
+        load_al_pad<NDW>( s, a );
+        load_al_pad<NDW>( s + rs, c );
 #pragma unroll
         for( int x = 0; x < 8; x++ )
         {
@@ -243,7 +243,7 @@ __global__ __launch_bounds__( 256 ) void wp_chroma_kernel( const typename PT<BD>
     {
         constexpr int NDW = 16 / PPD;
         uint32_t w[NDW];
-        load_al<NDW>( ref + (intptr_t)(H * by + r) * rs + 16 * bx, w );
+        load_al_pad<NDW>( ref + (intptr_t)(H * by + r) * rs + 16 * bx, w );
 #pragma unroll
         for( int x = 0; x < 8; x++ )
         {
@@ -409,7 +409,7 @@ __global__ __launch_bounds__( 256 ) void frame_stats_kernel( const typename PT<B
     const int nmb = mbw * mbh;
     auto sq4 = [&]( const typename PT<BD>::pixel *p, intptr_t s, int mbx, int mby, int plane ) {
         uint32_t w[NDW];
-        load_al<NDW>( p + (intptr_t)(16 * mby + (lane >> 2)) * s + 16 * mbx + 4 * (lane & 3), w );
+        load_al_pad<NDW>( p + (intptr_t)(16 * mby + (lane >> 2)) * s + 16 * mbx + 4 * (lane & 3), w );
         uint32_t sum = 0, sqr = 0;
 #pragma unroll
         for( int k = 0; k < 4; k++ )
