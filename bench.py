@@ -419,6 +419,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     res.update(rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F))
     del louts, iouts
     res.update(rates_weightp(x, a, world, dev, origin, stride, mbw, mbh))
+    res.update(rates_ssim(x, a, world, dev, origin, stride, mbw, mbh))
     nb8 = mbw * mbh * 4
     ys, xs = np.meshgrid(np.arange(mbh * 2), np.arange(mbw * 2), indexing="ij")
     bx, by = (xs.ravel() * 8).astype(np.int64), (ys.ravel() * 8).astype(np.int64)
@@ -544,6 +545,20 @@ def rates_weightp(x, a, world, dev, origin, stride, mbw, mbh):
         res["weightp_%s_ms" % name] = wall / max(1, a.steps // 2) * 1e3
         res["weightp_%s_weight" % name] = list(w[0][0])
     return res
+
+
+def rates_ssim(x, a, world, dev, origin, stride, mbw, mbh):
+    """x264_pixel_ssim_wxh (pixel.c:690-714) over a whole 1080p frame pair as one call (the
+    encoder calls it per filtered band, encoder.c:2517-2528): frames per second including the
+    ordered float sum; per-frame input 2 x 1920 x 1088 bytes."""
+    W, H = mbw * 16, mbh * 16
+    cnt = [0]
+
+    def step():
+        cnt[0] = x.ssim_wxh(dev[1], origin + 2, stride, dev[0], origin + 2, stride, W - 2, H)[1]
+    wall, _ = timed(step, max(1, a.steps // 2), 2, world)
+    n = max(1, a.steps // 2)
+    return {"ssim_frames_per_s": world * n / wall, "ssim_ms": wall / n * 1e3, "ssim_windows": cnt[0]}
 
 
 def rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F):
@@ -1030,6 +1045,10 @@ def cpu_lookahead(orc, planes, origin, stride, mbw, mbh, nthr, bounded):
         rate = bounded(lambda kw=kw: orc.weights_analyse(8, fl[0], lr[0], lo, ls, mbw, mbh, fic, st[0], st[1],
                                                          **kw) and 1, 1)[0]
         res["weightp_%s_ms_1t" % name] = 1e3 / rate
+    # SSIM of the 1080p pair as rates_ssim measures it
+    res["ssim_frames_per_s_1t"] = bounded(lambda: orc.ssim_wxh(8, planes[1].ravel(), origin + 2, stride,
+                                                               planes[0].ravel(), origin + 2, stride, W - 2, H)
+                                          and 1, 1)[0]
     return res
 
 

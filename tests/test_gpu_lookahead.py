@@ -322,3 +322,31 @@ def test_lowres_inter_slices_random(hip, oracle, n_slices):
 @pytest.mark.parametrize("n_slices", [2, 4])
 def test_lowres_bidir_slices(hip, oracle, bd, n_slices):
     _bidir_case(hip, oracle, bd, 1920, 1088, 2, 3, 1, 4, True, 171, 43, n_slices=n_slices)
+
+
+@pytest.mark.parametrize("helper", [0, 1])
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("kind", ["inter", "inter_random", "inter_slices", "bidir", "weighted", "timeout"])
+def test_lowres_helper_forced(hip, oracle, helper, bd, kind):
+    """The helper wave (a second wave per band that reads the reference / fenc lines the search
+    reaches a few steps later: L2 warming only) is on by default when every band's workgroup fits
+    on the GPU at once, so the other tests here run with it; X264HIP_LA_HELPER forces it off (the
+    plain single-wave form, what large batches use) or on.  Either way the results are the
+    oracle's, and a failed wait still ends the band with the timeout error."""
+    hip.set_variant("X264HIP_LA_HELPER", helper)
+    try:
+        if kind == "inter":
+            _case(hip, oracle, bd, 1920, 1088, 2, 1, 4, True)
+        elif kind == "inter_random":
+            _case(hip, oracle, bd, 176, 144, 3, 1, 4, True, random=True, aq=True, me_range=8)
+        elif kind == "inter_slices":
+            _case(hip, oracle, bd, 1920, 1088, 2, 0, 2, False, n_slices=4)
+        elif kind == "bidir":
+            test_lowres_bidir_1080p(hip, oracle, bd, 1, 4, True, 43)
+        elif kind == "weighted":
+            test_lowres_inter_weighted_1080p(hip, oracle, bd, (40, 5, -6))
+        elif bd == 8:
+            test_lowres_wait_timeout_reports_error(hip, oracle, "inter")
+            test_lowres_wait_timeout_reports_error(hip, oracle, "bidir")
+    finally:
+        hip.set_variant("X264HIP_LA_HELPER", None)

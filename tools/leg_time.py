@@ -40,6 +40,7 @@ def main():
         res = bench.rates_lookahead(x, a, 1, louts, iouts, W, mbw, mbh, F)
     elif leg == "wp":
         res = bench.rates_weightp(x, a, 1, dev, origin, stride, mbw, mbh)
+        res.update(bench.rates_ssim(x, a, 1, dev, origin, stride, mbw, mbh))
     else:
         raise SystemExit("unknown leg %s" % leg)
     print(json.dumps(res))

@@ -254,7 +254,8 @@ template <int BD> __device__ __forceinline__ int upix( uint32_t w, int k )
 namespace x264hip {
 enum VariantSlot
 {
-    V_TESA = 0, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_STREAM_NT, V_COUNT
+    V_TESA = 0, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_STREAM_NT, V_LA_HELPER,
+    V_COUNT
 };
 int variant( VariantSlot slot );
 

@@ -819,6 +819,53 @@ __device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, 
     }
 }
 
+// The helper wave (la_help): a second wave in the band's workgroup that reads,
+// LR_AHEAD steps before the searching wave gets there, one dword of every pixel row the band's
+// searches can reach in the column its blocks enter -- the reference planes (rows 8*y0 - 16 ..
+// 8*y1 + 16, one per lane) and fenc -- so the search finds those lines in L2.  Its loads wait
+// on its own counters, not the searching wave's.  It follows the searching wave's step
+// through an LDS word (`prog`, > t1 when the band is done or has failed) and stops after
+// `poll_max` polls in any case.
+constexpr int LR_AHEAD = 4;
+template <int BD, int NP>
+__device__ __forceinline__ void lr_helper( const typename PT<BD>::pixel *const (&pl)[NP],
+                                        const typename PT<BD>::pixel *fenc, intptr_t stride, int mbw, int s1, int y0,
+                                        int y1, int t0, int t1, const volatile int *prog, int poll_max )
+{
+    const int r = 8 * y0 - 16 + (int)(threadIdx.x & 63);
+    const int yb = min( max( r >> 3, y0 ), y1 - 1 );
+    const bool in_band = r >= 8 * y0 && r < 8 * y1;
+    uint32_t acc = 0;
+    int done = t0 - 1;
+    for( int it = 0; it < poll_max; it++ )
+    {
+        const int cur = *prog;
+        if( cur > t1 )
+            break;
+        const int target = min( cur + LR_AHEAD, t1 );
+        while( done < target )
+        {
+            done++;
+            const int x = min( max( mbw - 1 - (done - 2 * (s1 - 1 - yb)), 0 ), mbw - 1 );
+            const intptr_t o = (intptr_t)r * stride + ((8 * x - 24) & ~(4 / (int)sizeof( typename PT<BD>::pixel ) - 1));
+#pragma unroll
+            for( int k = 0; k < NP; k++ )
+                acc += *(const uint32_t *)(pl[k] + o);
+            if( in_band )
+                acc += *(const uint32_t *)(fenc + (intptr_t)r * stride + 8 * x);
+        }
+        __asm__ volatile( "" ::"v"( acc ) );
+        __builtin_amdgcn_s_sleep( 1 );
+    }
+}
+// the searching wave's step barrier when the helper shares the workgroup: the ring is the
+// one wave's own LDS, so ordering its accesses is enough
+__device__ __forceinline__ void lr_wave_sync()
+{
+    __builtin_amdgcn_fence( __ATOMIC_SEQ_CST, "wavefront" );
+    __builtin_amdgcn_wave_barrier();
+}
+
 // Lookahead slices (i_lookahead_threads, slicetype.c:901-918): slice i holds MB rows
 // [(H*i + T/2)/T, (H*(i+1) + T/2)/T) and is its own wavefront (slicetype_slice_cost scans it
 // alone; its row-below predictors stop at the slice end, slicetype.c:664).  Band j of a
@@ -843,7 +890,7 @@ __device__ __forceinline__ void lr_band( int j, int mbh, int nslices, int brows,
 }
 
 template <int BD>
-__global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
+__global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *r0,
     const typename PT<BD>::pixel *r1, const typename PT<BD>::pixel *r2, const typename PT<BD>::pixel *r3,
     intptr_t stride, intptr_t rfs, int mbw, int mbh, int me_method, int subme, int satd, int me_range, int mv_range,
@@ -851,10 +898,11 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
     uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands, int brows,
     int poll_max, uint32_t *status, const typename PT<BD>::pixel *rw, int wscale, int wdenom, int woffset,
-    int nslices )
+    int nslices, int help )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring[4 * LR_BAND];            // packed MVs of each band row's 4 latest blocks
+    __shared__ int prog;                         // the searching wave's step (helper wave)
     extern __shared__ uint16_t lr_cost_lds[];
     const uint16_t *cml = lr_stage_cost( lr_cost_lds, cost_mv, mv_range );
     const int f = blockIdx.x / nbands;
@@ -884,12 +932,31 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
     const int y = y0 + (int)((threadIdx.x & 15) >> 2);
     // steps in which this band has blocks (block (x, y) runs at (W-1-x) + 2(s1-1-y))
     const int t0 = 2 * (s1 - y1), t1 = 2 * (s1 - 1 - y0) + mbw - 1;
-    // a row's next block is x - 1: its fenc rows are fetched one step ahead
+    if( help )
+    {
+        if( threadIdx.x == 0 )
+            *(volatile int *)&prog = t0;
+        __syncthreads();
+        if( threadIdx.x >= 64 )
+        {
+            const typename PT<BD>::pixel *const hpl[5] = { r0, r1, r2, r3, rw ? rw : r0 };
+            lr_helper<BD, 5>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, &prog, poll_max );
+            return;
+        }
+    }
+    // a row's next block is x - 1: its fenc rows, intra cost and AQ factor are fetched one
+    // step ahead (read after the search, they would add a memory round to every step)
     uint32_t fnext[LR_NR][NDW];
+    int inext = 0, qnext = 0;
     auto fetch = [&]( int t ) {
         const int xn = mbw - 1 - (t - 2 * (s1 - 1 - y));
         if( y < y1 && xn >= 0 && xn < mbw )
+        {
             lr_load_fenc<BD>( fenc + 8 * (intptr_t)xn + (intptr_t)(8 * y + LR_NR * q) * stride, stride, fnext );
+            inext = intra_cost[xn + y * mbw];
+            if( invq )
+                qnext = invq[xn + y * mbw];
+        }
     };
     fetch( t0 );
     for( int t = t0; t <= t1; t++ )
@@ -901,6 +968,7 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
 #pragma unroll
             for( int k = 0; k < NDW; k++ )
                 fe[r][k] = fnext[r][k];
+        const int icost = inext, iq = qnext;
         fetch( t + 1 );
         bool failed = false;
         if( y < y1 && x >= 0 && x < mbw )
@@ -926,14 +994,13 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
                 // slicetype.c:758-790
                 int bcost = (cost >> (BD - 8)) + 4, list_used = 1;
                 const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
-                const int icost = intra_cost[mb];
                 const bool b_intra = icost < bcost;
                 if( b_intra )
                 {
                     bcost = icost;
                     list_used = 0;
                 }
-                const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
+                const int aq = invq ? (bcost * iq + 128) >> 8 : bcost;
                 racc += aq;
                 if( fsm )
                 {
@@ -945,8 +1012,16 @@ __global__ __launch_bounds__( 64 ) void lowres_inter_kernel(
             }
         }
         if( __builtin_amdgcn_ballot_w64( failed ) )
+        {
+            if( help && threadIdx.x == 0 )
+                *(volatile int *)&prog = t1 + 1;
             return;                                  // the launcher reports it (status word)
-        __syncthreads();
+        }
+        // one searching wave per band: ordering its own LDS ring accesses is enough (a
+        // __syncthreads here also waited for the step's global stores to drain)
+        lr_wave_sync();
+        if( help && threadIdx.x == 0 )
+            *(volatile int *)&prog = t + 1;
     }
     if( q == 0 && role == 0 && y < y1 && row_satd )
         row_satd[(intptr_t)f * mbh + y] = racc;
@@ -1010,7 +1085,7 @@ __device__ __forceinline__ int lr_bidir( const LrCtx<BD> &m0, const LrCtx<BD> &m
 // B frames (p0 < b < p1): slicetype_mb_cost with b_bidir (slicetype.c:514-713, 758-791).
 // A list is searched on the wavefront when search & (1 << l), else its mv / cost are read.
 template <int BD>
-__global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
+__global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *a0,
     const typename PT<BD>::pixel *a1, const typename PT<BD>::pixel *a2, const typename PT<BD>::pixel *a3,
     intptr_t afs, const typename PT<BD>::pixel *b0, const typename PT<BD>::pixel *b1,
@@ -1019,10 +1094,11 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const uint16_t *__restrict__ cost_mv, int search, int16_t *__restrict__ mvs0, int32_t *__restrict__ costs0,
     int16_t *__restrict__ mvs1, int32_t *__restrict__ costs1, const int16_t *__restrict__ p1mvs, int dsf, int weight,
     const uint16_t *__restrict__ invq, uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd,
-    int32_t *__restrict__ est, int nbands, int brows, int poll_max, uint32_t *status, int nslices )
+    int32_t *__restrict__ est, int nbands, int brows, int poll_max, uint32_t *status, int nslices, int help )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring0[4 * LR_BAND], ring1[4 * LR_BAND];      // per list
+    __shared__ int prog;                                        // the searching wave's step
     extern __shared__ uint16_t lr_cost_lds[];
     const uint16_t *cml = lr_stage_cost( lr_cost_lds, cost_mv, mv_range );
     const int f = blockIdx.x / nbands;
@@ -1056,12 +1132,33 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
     const int y = y0 + (rl >> 2);
     const bool mine = role < 3 && y < y1;
     const int t0 = 2 * (s1 - y1), t1 = 2 * (s1 - 1 - y0) + mbw - 1;
-    // a row's next block is x - 1: its fenc rows are fetched one step ahead
+    if( help )
+    {
+        if( threadIdx.x == 0 )
+            *(volatile int *)&prog = t0;
+        __syncthreads();
+        if( threadIdx.x >= 64 )
+        {
+            const typename PT<BD>::pixel *const hpl[8] = { a0, a1, a2, a3, b0, b1, b2, b3 };
+            lr_helper<BD, 8>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, &prog, poll_max );
+            return;
+        }
+    }
+    // a row's next block is x - 1: its fenc rows, p1 mv and AQ factor are fetched one step
+    // ahead (read after the searches, they would add a memory round to every step)
     uint32_t fnext[LR_NR][NDW];
+    uint32_t pnext = 0;
+    int qnext = 0;
     auto fetch = [&]( int t ) {
         const int xn = mbw - 1 - (t - 2 * (s1 - 1 - y));
         if( mine && xn >= 0 && xn < mbw )
+        {
             lr_load_fenc<BD>( fenc + 8 * (intptr_t)xn + (intptr_t)(8 * y + LR_NR * q) * stride, stride, fnext );
+            if( p1mvs )
+                pnext = *(const uint32_t *)(p1mvs + 2 * (xn + y * mbw));
+            if( invq )
+                qnext = invq[xn + y * mbw];
+        }
     };
     auto from_role = [&]( int v, int r ) { return __shfl( v, rl + 16 * r ); };
     fetch( t0 );
@@ -1074,6 +1171,8 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
 #pragma unroll
             for( int k = 0; k < NDW; k++ )
                 fe[r][k] = fnext[r][k];
+        const uint32_t p1w = pnext;
+        const int iq = qnext;
         fetch( t + 1 );
         const bool act = mine && x >= 0 && x < mbw;
         const int mb = x + y * mbw;
@@ -1120,14 +1219,18 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
             }
         }
         if( __builtin_amdgcn_ballot_w64( failed ) )
+        {
+            if( help && threadIdx.x == 0 )
+                *(volatile int *)&prog = t1 + 1;
             return;                                  // the launcher reports it (status word)
+        }
         const int mv0x = from_role( mvx, 0 ), mv0y = from_role( mvy, 0 ), lc0 = from_role( lc, 0 );
         const int mv1x = from_role( mvx, 1 ), mv1y = from_role( mvy, 1 ), lc1 = from_role( lc, 1 );
         // the predicted bidir mvs from p1's list-0 mvs (slicetype.c:623-645)
         int d0x = 0, d0y = 0, d1x = 0, d1y = 0;
         if( act && p1mvs )
         {
-            const int rx = p1mvs[2 * mb], ry = p1mvs[2 * mb + 1];
+            const int rx = (int16_t)(p1w & 0xffff), ry = (int16_t)(p1w >> 16);
             d0x = (rx * dsf + 128) >> 8;
             d0y = (ry * dsf + 128) >> 8;
             d1x = lr_clip3( d0x - rx, m0.smin0, m0.smax0 );
@@ -1181,7 +1284,7 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
             // slicetype.c:758-790 (no intra in B frames)
             bcost = (bcost >> (BD - 8)) + 4;
             const bool fsm = (x > 0 && x < mbw - 1 && y > 0 && y < mbh - 1) || mbw <= 2 || mbh <= 2;
-            const int aq = invq ? (bcost * invq[mb] + 128) >> 8 : bcost;
+            const int aq = invq ? (bcost * iq + 128) >> 8 : bcost;
             racc += aq;
             if( fsm )
             {
@@ -1190,7 +1293,11 @@ __global__ __launch_bounds__( 64 ) void lowres_bidir_kernel(
             }
             lcosts[mb] = (uint16_t)(min( bcost, 16383 ) + (list_used << 14));
         }
-        __syncthreads();
+        // one searching wave per band: ordering its own LDS ring accesses is enough (a
+        // __syncthreads here also waited for the step's global stores to drain)
+        lr_wave_sync();
+        if( help && threadIdx.x == 0 )
+            *(volatile int *)&prog = t + 1;
     }
     if( role == 0 && q == 0 && y < y1 && row_satd )
         row_satd[(intptr_t)f * mbh + y] = racc;
@@ -1350,6 +1457,22 @@ int la_poll_max()
     const int v = variant( V_LA_POLL );
     return v >= 0 ? v : 1 << 22;
 }
+
+// the helper wave of lr_helper: on when every band's workgroup, helper included, is resident at
+// once (it rides on wave slots the launch leaves idle: the 15-pair launches; a 240-pair batch
+// would double its waves and queue them), X264HIP_LA_HELPER=0 / 1 forces it off / on
+int la_help( const void *kernel, int64_t nwg, size_t lds, hipStream_t stream )
+{
+    const int v = variant( V_LA_HELPER );
+    if( v >= 0 )
+        return v == 1;
+    int dev = 0, cus = 0, per_cu = 0;
+    if( stream_device( stream, &dev ) != hipSuccess ||
+        hipDeviceGetAttribute( &cus, hipDeviceAttributeMultiprocessorCount, dev ) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor( &per_cu, kernel, 128, lds ) != hipSuccess )
+        return 0;
+    return nwg <= (int64_t)cus * per_cu;
+}
 } // namespace
 
 template <int BD>
@@ -1391,10 +1514,12 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
     uint32_t *status = nullptr;
     if( (e = la_status_begin( stream, &status )) != hipSuccess )
         return e;
-    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ra[0], ra[1],
-                        ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method, subme, satd,
-                        me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs, dsf, weight,
-                        invq, lowres_costs, row_satd, est, nbands, brows4, la_poll_max(), status, nslices );
+    const int help = la_help( (const void *)lowres_bidir_kernel<BD>, (int64_t)n * nbands, lds, stream );
+    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs,
+                        ra[0], ra[1], ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method,
+                        subme, satd, me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs,
+                        dsf, weight, invq, lowres_costs, row_satd, est, nbands, brows4, la_poll_max(), status,
+                        nslices, help );
     if( (e = hipGetLastError()) != hipSuccess )
         return e;
     return la_status_end( stream );
@@ -1432,10 +1557,11 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     uint32_t *status = nullptr;
     if( (e = la_status_begin( stream, &status )) != hipSuccess )
         return e;
-    hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( 64 ), lds, stream, fenc, ffs, ref[0],
-                        ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
-                        lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4,
-                        la_poll_max(), status, ref_w, wscale, wdenom, woffset, nslices );
+    const int help = la_help( (const void *)lowres_inter_kernel<BD>, (int64_t)npairs * nbands, lds, stream );
+    hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc,
+                        ffs, ref[0], ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range,
+                        mv_range, lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands,
+                        brows4, la_poll_max(), status, ref_w, wscale, wdenom, woffset, nslices, help );
     if( (e = hipGetLastError()) != hipSuccess )
         return e;
     return la_status_end( stream );

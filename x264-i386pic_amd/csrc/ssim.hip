@@ -90,15 +90,65 @@ __global__ __launch_bounds__( 256 ) void ssim_groups_kernel( const int4 *__restr
     g[i] = ssim_end4_dev<BD>( sums + (intptr_t)y * nx + x, sums + (intptr_t)(y - 1) * nx + x, n );
 }
 
-// the reference's accumulation order: row by row, group by group, into one float
-__global__ void ssim_total_kernel( const float *__restrict__ g, int n, float *__restrict__ out )
+// the reference's accumulation order: row by row, group by group, into one float.  The sum is
+// one dependent chain, so one lane runs it -- from LDS: the wave loads the next 1024 group
+// values (coalesced, in flight while lane 0 adds the current ones) and stores them to the
+// other half of a double buffer.
+__global__ __launch_bounds__( 64 ) void ssim_total_kernel( const float *__restrict__ g, int n, float *__restrict__ out )
 {
-    if( threadIdx.x )
-        return;
+    constexpr int CH = 1024;
+    __shared__ float4 buf[2][CH / 4];
+    const int lane = threadIdx.x;
+    float4 v[CH / 256];
+    auto load = [&]( int c ) {
+#pragma unroll
+        for( int j = 0; j < CH / 256; j++ )
+        {
+            const int i = c * CH + 4 * (j * 64 + lane);
+            v[j] = i + 3 < n ? *(const float4 *)(g + i)
+                             : make_float4( i < n ? g[i] : 0.f, i + 1 < n ? g[i + 1] : 0.f,
+                                            i + 2 < n ? g[i + 2] : 0.f, 0.f );
+        }
+    };
     float ssim = 0.0f;
-    for( int i = 0; i < n; i++ )
-        ssim += g[i];
-    *out = ssim;
+    const int nc = (n + CH - 1) / CH;
+    load( 0 );
+    for( int c = 0; c < nc; c++ )
+    {
+#pragma unroll
+        for( int j = 0; j < CH / 256; j++ )
+            buf[c & 1][j * 64 + lane] = v[j];
+        __syncthreads();
+        if( c + 1 < nc )
+            load( c + 1 );
+        if( lane == 0 )
+        {
+            const int m = min( CH, n - c * CH );
+            const float4 *b = buf[c & 1];
+            int i = 0;
+            for( ; i + 64 <= m; i += 64 )        // 16 LDS reads in flight, then 64 ordered adds
+            {
+                float4 t[16];
+#pragma unroll
+                for( int k = 0; k < 16; k++ )
+                    t[k] = b[(i >> 2) + k];
+#pragma unroll
+                for( int k = 0; k < 16; k++ )
+                {
+                    ssim += t[k].x;
+                    ssim += t[k].y;
+                    ssim += t[k].z;
+                    ssim += t[k].w;
+                }
+            }
+            const float *bf = (const float *)b;
+            for( ; i < m; i++ )
+                ssim += bf[i];
+        }
+        __syncthreads();
+    }
+    if( lane == 0 )
+        *out = ssim;
 }
 
 template <int BD>
