@@ -952,7 +952,7 @@ __device__ __forceinline__ EsaGeo esa_geo( const int16_t *par, const int16_t *or
 // never waits for those (vmcnt retires in order), and the table loads are branch-free, so the
 // compiler's wait counts stay exact.  (Fetching the next MB's cost gathers early too measured
 // 0.0986 ms: no better.)
-template <int BD, int MAXS>
+template <int BD, int MAXS, int E>
 __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT<BD>::sadt *__restrict__ table, int R,
                                                                int cols, int pitch, int nmb, int me_range,
                                                                const int16_t *__restrict__ origin,
@@ -961,7 +961,9 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
                                                                const uint16_t *__restrict__ cost_mv,
                                                                int32_t *__restrict__ out )
 {
-    using chunk = typename std::conditional<BD == 8, uint2, uint4>::type;
+    // a lane's chunk: E table entries (8 bit: 4 = 8 bytes, or 8 = 16 bytes when the pitch allows;
+    // 10 bit: 4 = 16 bytes)
+    using chunk = typename std::conditional<BD == 8 && E == 4, uint2, uint4>::type;
     const int lane = threadIdx.x & 63;
     // the MB index is wave-uniform: made a scalar, so its par / origin / init_cost words are
     // scalar loads and the address path carries only the table and cost_mv reads
@@ -970,7 +972,7 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
     if( mb >= nmb )
         return;
     const int W = 2 * R + 1;
-    const int nch = pitch >> 2, rps = 64 / nch;                    // pitch <= 64: >= 4 rows per step
+    const int nch = pitch / E, rps = 64 / nch;                     // pitch <= 64: >= 4 rows per step
     const int rr = lane / nch, ch = lane - rr * nch;
     // branch-free: every lane loads every step at a row clamped into the MB's table (the
     // lanes and steps outside the window are masked where the values are used), so the
@@ -1007,10 +1009,10 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
         const EsaGeo gn = esa_geo( par, origin, mbf, R, me_range, rps );
         chunk vn[MAXS];
         fetch( gn, mbf, vn );
-        uint32_t ck[4];
+        uint32_t ck[E];
 #pragma unroll
-        for( int k = 0; k < 4; k++ )
-            ck[k] = (uint32_t)__builtin_amdgcn_ds_bpermute( 4 * (4 * ch + k), (int)ckl );
+        for( int k = 0; k < E; k++ )
+            ck[k] = (uint32_t)__builtin_amdgcn_ds_bpermute( 4 * (E * ch + k), (int)ckl );
         uint32_t key = 0xFFFFFFFFu;
 #pragma unroll
         for( int st = 0; st < MAXS; st++ )
@@ -1019,17 +1021,22 @@ __global__ __launch_bounds__( 256 ) void me_esa_argmin_kernel( const typename PT
             const uint32_t S = (uint32_t)__builtin_amdgcn_ds_bpermute( 4 * min( max( my - g.oy, 0 ), 63 ), (int)Sl );
             if( st < g.nsteps && rr < rps && my <= g.y1 )
             {
-                uint32_t s4[4];
-                if constexpr( BD == 8 )
+                uint32_t s4[E];
+                if constexpr( BD == 8 && E == 4 )
                 {
                     s4[0] = v[st].x & 0xffff; s4[1] = v[st].x >> 16; s4[2] = v[st].y & 0xffff; s4[3] = v[st].y >> 16;
+                }
+                else if constexpr( BD == 8 )
+                {
+                    s4[0] = v[st].x & 0xffff; s4[1] = v[st].x >> 16; s4[2] = v[st].y & 0xffff; s4[3] = v[st].y >> 16;
+                    s4[4] = v[st].z & 0xffff; s4[5] = v[st].z >> 16; s4[6] = v[st].w & 0xffff; s4[7] = v[st].w >> 16;
                 }
                 else
                 {
                     s4[0] = v[st].x; s4[1] = v[st].y; s4[2] = v[st].z; s4[3] = v[st].w;
                 }
 #pragma unroll
-                for( int k = 0; k < 4; k++ )
+                for( int k = 0; k < E; k++ )
                     key = min( key, __builtin_elementwise_add_sat(
                                         __builtin_elementwise_add_sat( s4[k] << 12, ck[k] ), S ) );
             }
@@ -1080,25 +1087,43 @@ hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int 
     const int pitch = origin ? cen_pitch( BD, R ) : full_pitch( R );
     if( pitch > 64 || ((uintptr_t)table & (BD == 8 ? 7 : 15)) )
         return hipErrorInvalidValue;
-    // steps of 64 / (pitch / 4) rows cover the 2R+1 table rows (the kernel is instantiated
-    // for the exact count, since it loads every step); 8 waves of every SIMD of the 256 CUs
-    // walk the MBs (fewer when there are fewer MBs)
-    const int rps = 64 / (pitch >> 2), steps = (2 * R + 1 + rps - 1) / rps;
-    const int waves = std::min( nmb, 256 * 4 * 8 );
+    // steps of 64 / (pitch / E) rows cover the 2R+1 table rows (the kernel is instantiated
+    // for the exact count, since it loads every step); 16 waves of every SIMD of the 256 CUs
+    // walk the MBs (fewer when there are fewer MBs; 4 / 8 / 12 / 16 per SIMD: 0.100 / 0.085 /
+    // 0.083 / 0.081 ms, profiles/r04w_*).  8-bit tables whose pitch is a multiple of 8 entries
+    // (the centred ones) are read 16 bytes per lane (E = 8): half the load instructions, 0.094 ->
+    // 0.079-0.084 ms for the 16-pair 1080p table (profiles/r04v_*).
+    const bool wide = BD == 8 && pitch % 8 == 0 && !((uintptr_t)table & 15);
+    const int E = wide ? 8 : 4;
+    const int rps = 64 / (pitch / E), steps = (2 * R + 1 + rps - 1) / rps;
+    const int waves = std::min( nmb, 256 * 4 * 16 );
     const dim3 g( (unsigned)((waves + 3) / 4) ), b( 256 );
-    switch( steps )
+#define ARGMIN_CASE( S, EE )                                                                                     \
+    case S:                                                                                                      \
+        hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD, S, EE> ), g, b, 0, stream, table, R, cols, pitch, nmb,      \
+                            me_range, origin, par, init_cost, cost_mv, out );                                    \
+        break;
+    if( wide )
     {
-#define ARGMIN_CASE( S )                                                                                         \
-        case S:                                                                                                  \
-            hipLaunchKernelGGL( ( me_esa_argmin_kernel<BD, S> ), g, b, 0, stream, table, R, cols, pitch, nmb,      \
-                                me_range, origin, par, init_cost, cost_mv, out );                                \
-            break;
-        ARGMIN_CASE( 1 ) ARGMIN_CASE( 2 ) ARGMIN_CASE( 3 ) ARGMIN_CASE( 4 ) ARGMIN_CASE( 5 ) ARGMIN_CASE( 6 )
-        ARGMIN_CASE( 7 ) ARGMIN_CASE( 8 ) ARGMIN_CASE( 9 ) ARGMIN_CASE( 10 ) ARGMIN_CASE( 11 ) ARGMIN_CASE( 12 )
-        ARGMIN_CASE( 13 ) ARGMIN_CASE( 14 ) ARGMIN_CASE( 15 ) ARGMIN_CASE( 16 )
-#undef ARGMIN_CASE
-        default: return hipErrorInvalidValue;
+        switch( steps )
+        {
+            ARGMIN_CASE( 1, 8 ) ARGMIN_CASE( 2, 8 ) ARGMIN_CASE( 3, 8 ) ARGMIN_CASE( 4, 8 ) ARGMIN_CASE( 5, 8 )
+            ARGMIN_CASE( 6, 8 ) ARGMIN_CASE( 7, 8 ) ARGMIN_CASE( 8, 8 )
+            default: return hipErrorInvalidValue;
+        }
     }
+    else
+    {
+        switch( steps )
+        {
+            ARGMIN_CASE( 1, 4 ) ARGMIN_CASE( 2, 4 ) ARGMIN_CASE( 3, 4 ) ARGMIN_CASE( 4, 4 ) ARGMIN_CASE( 5, 4 )
+            ARGMIN_CASE( 6, 4 ) ARGMIN_CASE( 7, 4 ) ARGMIN_CASE( 8, 4 ) ARGMIN_CASE( 9, 4 ) ARGMIN_CASE( 10, 4 )
+            ARGMIN_CASE( 11, 4 ) ARGMIN_CASE( 12, 4 ) ARGMIN_CASE( 13, 4 ) ARGMIN_CASE( 14, 4 ) ARGMIN_CASE( 15, 4 )
+            ARGMIN_CASE( 16, 4 )
+            default: return hipErrorInvalidValue;
+        }
+    }
+#undef ARGMIN_CASE
     return hipGetLastError();
 }
 
