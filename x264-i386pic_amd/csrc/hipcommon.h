@@ -8,6 +8,18 @@
 
 namespace x264hip {
 
+// a small table (entries < 2^b) as bit fields of one word, entry i in bits [b*i, b*i + b): a
+// per-lane index then reads an immediate with a shift and mask instead of a memory load on
+// the dependent chain
+template <int N> constexpr uint32_t pack_fields( const uint8_t ( &a )[N], int b )
+{
+    uint32_t r = 0;
+    for( int i = 0; i < N; i++ )
+        r |= (uint32_t)a[i] << (b * i);
+    return r;
+}
+__device__ __forceinline__ int field( uint32_t k, int b, int i ) { return (int)((k >> (b * i)) & ((1u << b) - 1)); }
+
 template <int BD> struct PT;
 template <> struct PT<8>
 {

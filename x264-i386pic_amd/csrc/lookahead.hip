@@ -22,12 +22,34 @@
 
 namespace x264hip {
 
-__constant__ uint8_t c_lr_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };   // x264_hpel_ref0
-__constant__ uint8_t c_lr_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };   // x264_hpel_ref1
-__constant__ int8_t c_hex2[8][2] = { { -1, -2 }, { -2, 0 }, { -1, 2 }, { 1, 2 }, { 2, 0 }, { 1, -2 }, { -1, -2 }, { -2, 0 } };
-__constant__ uint8_t c_mod6m1[8] = { 5, 0, 1, 2, 3, 4, 5, 0 };
-__constant__ int8_t c_square1[9][2] = { { 0, 0 }, { 0, -1 }, { 0, 1 }, { -1, 0 }, { 1, 0 },
-                                        { -1, -1 }, { -1, 1 }, { 1, -1 }, { 1, 1 } };
+// The reference's small tables (tables.c hpel_ref0/1, me.c mod6m1/hex2/square1; pinned to the
+// reference text by tests/test_ref_tables.py).  The searches index them with per-lane values
+// on their serial chain, so the kernels read them as bit fields of compile-time words
+// (an immediate shift and mask) rather than as memory: a table load was one more dependent
+// memory round per hexagon step and per get_ref.
+constexpr uint8_t c_lr_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };   // x264_hpel_ref0
+constexpr uint8_t c_lr_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };   // x264_hpel_ref1
+constexpr int8_t c_hex2[8][2] = { { -1, -2 }, { -2, 0 }, { -1, 2 }, { 1, 2 }, { 2, 0 }, { 1, -2 }, { -1, -2 }, { -2, 0 } };
+constexpr uint8_t c_mod6m1[8] = { 5, 0, 1, 2, 3, 4, 5, 0 };
+constexpr int8_t c_square1[9][2] = { { 0, 0 }, { 0, -1 }, { 0, 1 }, { -1, 0 }, { 1, 0 },
+                                     { -1, -1 }, { -1, 1 }, { 1, -1 }, { 1, 1 } };
+// signed entries biased by `bias`, as bit fields (pack_fields)
+template <int N> constexpr uint32_t lr_pack_s( const int8_t ( &a )[N][2], int c, int b, int bias )
+{
+    uint32_t r = 0;
+    for( int i = 0; i < N; i++ )
+        r |= (uint32_t)(a[i][c] + bias) << (b * i);
+    return r;
+}
+constexpr uint32_t k_lr_ref0 = pack_fields( c_lr_ref0, 2 ), k_lr_ref1 = pack_fields( c_lr_ref1, 2 );
+constexpr uint32_t k_hex2_x = lr_pack_s( c_hex2, 0, 3, 2 ), k_hex2_y = lr_pack_s( c_hex2, 1, 3, 2 );
+constexpr uint32_t k_mod6m1 = pack_fields( c_mod6m1, 3 );
+constexpr uint32_t k_square1_x = lr_pack_s( c_square1, 0, 2, 1 ), k_square1_y = lr_pack_s( c_square1, 1, 2, 1 );
+__device__ __forceinline__ int lr_hex2_x( int j ) { return (int)((k_hex2_x >> (3 * j)) & 7) - 2; }
+__device__ __forceinline__ int lr_hex2_y( int j ) { return (int)((k_hex2_y >> (3 * j)) & 7) - 2; }
+__device__ __forceinline__ int lr_mod6m1( int j ) { return (int)((k_mod6m1 >> (3 * j)) & 7); }
+__device__ __forceinline__ int lr_square1_x( int k ) { return (int)((k_square1_x >> (2 * k)) & 3) - 1; }
+__device__ __forceinline__ int lr_square1_y( int k ) { return (int)((k_square1_y >> (2 * k)) & 3) - 1; }
 
 constexpr int LR_COST_MAX = 1 << 28;
 
@@ -212,9 +234,12 @@ template <int BD> struct LrCtx
     static constexpr int WR = LR_NR + 4, WD = 12 / PT<BD>::PPD;
     __device__ __forceinline__ void win( int cx, int cy, uint32_t (&w)[WR][WD] ) const
     {
-        const uintptr_t a = (uintptr_t)(pw + (intptr_t)(cy - 2) * stride + (cx - 2));
-        const uint32_t sh = (uint32_t)(a & 3);
-        const uint8_t *b = (const uint8_t *)(a & ~(uintptr_t)3);
+        // (the aligned base by pointer arithmetic, not through an integer: the loads stay
+        // global_load, where an integer round trip made them flat loads, which also count
+        // against the LDS wait counter)
+        const pixel *p = pw + (intptr_t)(cy - 2) * stride + (cx - 2);
+        const uint32_t sh = (uint32_t)((uintptr_t)p & 3);
+        const uint8_t *b = (const uint8_t *)p - sh;
         const intptr_t sb = stride * (intptr_t)sizeof( pixel );
 #pragma unroll
         for( int r = 0; r < WR; r++ )
@@ -256,7 +281,7 @@ template <int BD> struct LrCtx
     {
         const int idx = ((my & 3) << 2) + (mx & 3);
         const intptr_t off = (intptr_t)(my >> 2) * stride + (mx >> 2);
-        const int i0 = c_lr_ref0[idx], i1 = c_lr_ref1[idx];
+        const int i0 = (int)((k_lr_ref0 >> (2 * idx)) & 3), i1 = (int)((k_lr_ref1 >> (2 * idx)) & 3);
         const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((my & 3) == 3) * stride;
 #pragma unroll
         for( int y = 0; y < LR_NR; y++ )
@@ -496,8 +521,8 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         if( bcost & 7 )
         {
             int dir = (bcost & 7) - 2;
-            bmx += c_hex2[dir + 1][0];
-            bmy += c_hex2[dir + 1][1];
+            bmx += lr_hex2_x( dir + 1 );
+            bmy += lr_hex2_y( dir + 1 );
             for( int i = (me_range >> 1) - 1; i > 0 && m.in_range( bmx, bmy ); i-- )
             {
                 // the window scores all six hexagon points (c_hex2[0..5] order); the three
@@ -513,7 +538,7 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
                 };
 #pragma unroll
                 for( int k = 0; k < 3; k++ )
-                    costs[k] = pick( dir + k ) + m.bits_mvd( bmx + c_hex2[dir + k][0], bmy + c_hex2[dir + k][1] );
+                    costs[k] = pick( dir + k ) + m.bits_mvd( bmx + lr_hex2_x( dir + k ), bmy + lr_hex2_y( dir + k ) );
                 bcost &= ~7;
                 bcost = min( bcost, (costs[0] << 3) + 1 );
                 bcost = min( bcost, (costs[1] << 3) + 2 );
@@ -521,9 +546,9 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
                 if( !(bcost & 7) )
                     break;
                 dir += (bcost & 7) - 2;
-                dir = c_mod6m1[dir + 1];
-                bmx += c_hex2[dir + 1][0];
-                bmy += c_hex2[dir + 1][1];
+                dir = lr_mod6m1( dir + 1 );
+                bmx += lr_hex2_x( dir + 1 );
+                bmy += lr_hex2_y( dir + 1 );
             }
         }
         bcost >>= 3;
@@ -538,8 +563,8 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
                 bcost = min( bcost, (c8[k - 1] << 4) + k );
         }
 #undef LR_W
-        bmx += c_square1[bcost & 15][0];
-        bmy += c_square1[bcost & 15][1];
+        bmx += lr_square1_x( bcost & 15 );
+        bmy += lr_square1_y( bcost & 15 );
         bcost >>= 4;
     }
 #undef LR_COST_MV
@@ -830,7 +855,7 @@ constexpr int LR_AHEAD = 4;
 template <int BD, int NP>
 __device__ __forceinline__ void lr_helper( const typename PT<BD>::pixel *const (&pl)[NP],
                                         const typename PT<BD>::pixel *fenc, intptr_t stride, int mbw, int s1, int y0,
-                                        int y1, int t0, int t1, const volatile int *prog, int poll_max )
+                                        int y1, int t0, int t1, int &prog, int poll_max )
 {
     const int r = 8 * y0 - 16 + (int)(threadIdx.x & 63);
     const int yb = min( max( r >> 3, y0 ), y1 - 1 );
@@ -839,7 +864,7 @@ __device__ __forceinline__ void lr_helper( const typename PT<BD>::pixel *const (
     int done = t0 - 1;
     for( int it = 0; it < poll_max; it++ )
     {
-        const int cur = *prog;
+        const int cur = __hip_atomic_load( &prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP );
         if( cur > t1 )
             break;
         const int target = min( cur + LR_AHEAD, t1 );
@@ -857,6 +882,11 @@ __device__ __forceinline__ void lr_helper( const typename PT<BD>::pixel *const (
         __asm__ volatile( "" ::"v"( acc ) );
         __builtin_amdgcn_s_sleep( 1 );
     }
+}
+// the searching wave's step for the helper (an LDS word: ds_write, not a flat store)
+__device__ __forceinline__ void lr_prog_set( int &prog, int v )
+{
+    __hip_atomic_store( &prog, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP );
 }
 // the searching wave's step barrier when the helper shares the workgroup: the ring is the
 // one wave's own LDS, so ordering its accesses is enough
@@ -935,12 +965,12 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     if( help )
     {
         if( threadIdx.x == 0 )
-            *(volatile int *)&prog = t0;
+            lr_prog_set( prog, t0 );
         __syncthreads();
         if( threadIdx.x >= 64 )
         {
             const typename PT<BD>::pixel *const hpl[5] = { r0, r1, r2, r3, rw ? rw : r0 };
-            lr_helper<BD, 5>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, &prog, poll_max );
+            lr_helper<BD, 5>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, prog, poll_max );
             return;
         }
     }
@@ -1014,14 +1044,14 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
         if( __builtin_amdgcn_ballot_w64( failed ) )
         {
             if( help && threadIdx.x == 0 )
-                *(volatile int *)&prog = t1 + 1;
+                lr_prog_set( prog, t1 + 1 );
             return;                                  // the launcher reports it (status word)
         }
         // one searching wave per band: ordering its own LDS ring accesses is enough (a
         // __syncthreads here also waited for the step's global stores to drain)
         lr_wave_sync();
         if( help && threadIdx.x == 0 )
-            *(volatile int *)&prog = t + 1;
+            lr_prog_set( prog, t + 1 );
     }
     if( q == 0 && role == 0 && y < y1 && row_satd )
         row_satd[(intptr_t)f * mbh + y] = racc;
@@ -1135,12 +1165,12 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
     if( help )
     {
         if( threadIdx.x == 0 )
-            *(volatile int *)&prog = t0;
+            lr_prog_set( prog, t0 );
         __syncthreads();
         if( threadIdx.x >= 64 )
         {
             const typename PT<BD>::pixel *const hpl[8] = { a0, a1, a2, a3, b0, b1, b2, b3 };
-            lr_helper<BD, 8>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, &prog, poll_max );
+            lr_helper<BD, 8>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, prog, poll_max );
             return;
         }
     }
@@ -1221,7 +1251,7 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
         if( __builtin_amdgcn_ballot_w64( failed ) )
         {
             if( help && threadIdx.x == 0 )
-                *(volatile int *)&prog = t1 + 1;
+                lr_prog_set( prog, t1 + 1 );
             return;                                  // the launcher reports it (status word)
         }
         const int mv0x = from_role( mvx, 0 ), mv0y = from_role( mvy, 0 ), lc0 = from_role( lc, 0 );
@@ -1297,7 +1327,7 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
         // __syncthreads here also waited for the step's global stores to drain)
         lr_wave_sync();
         if( help && threadIdx.x == 0 )
-            *(volatile int *)&prog = t + 1;
+            lr_prog_set( prog, t + 1 );
     }
     if( role == 0 && q == 0 && y < y1 && row_satd )
         row_satd[(intptr_t)f * mbh + y] = racc;

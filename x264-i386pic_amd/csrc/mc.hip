@@ -649,8 +649,8 @@ hipError_t launch_hpel_filter( const typename PT<BD>::pixel *src, typename PT<BD
 }
 
 // ------------------------------------------------------------ qpel candidates
-__constant__ uint8_t c_hpel_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };
-__constant__ uint8_t c_hpel_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };
+constexpr uint8_t c_hpel_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };
+constexpr uint8_t c_hpel_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };
 
 // rounding-up average of packed pixels, (a + b + 1) >> 1 per pixel (pixel_avg, mc.c:57)
 template <int BD> __device__ __forceinline__ uint32_t avg_packed( uint32_t a, uint32_t b )
@@ -700,7 +700,8 @@ __device__ __forceinline__ int subpel_score( const typename PT<BD>::pixel *a, in
     constexpr int BAND = (16 / NDW) < 4 ? 4 : (16 / NDW) > H ? H : (16 / NDW);   // rows per load burst
     const int idx = ((qy & 3) << 2) + (qx & 3);
     const intptr_t off = (intptr_t)(qy >> 2) * rs + (qx >> 2);
-    const int i0 = c_hpel_ref0[idx], i1 = c_hpel_ref1[idx];
+    constexpr uint32_t k0 = pack_fields( c_hpel_ref0, 2 ), k1 = pack_fields( c_hpel_ref1, 2 );
+    const int i0 = field( k0, 2, idx ), i1 = field( k1, 2, idx );
     const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((qy & 3) == 3) * rs;
     const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((qx & 3) == 3);
     if( !(idx & 5) )

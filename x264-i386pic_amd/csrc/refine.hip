@@ -20,8 +20,8 @@
 
 namespace x264hip {
 
-__constant__ uint8_t c_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };   // x264_hpel_ref0
-__constant__ uint8_t c_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };   // x264_hpel_ref1
+constexpr uint8_t c_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };   // x264_hpel_ref0
+constexpr uint8_t c_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };   // x264_hpel_ref1
 
 // subpel_iterations (me.c:38-50): { refine_hpel, refine_qpel, me_hpel, me_qpel }
 static const uint8_t k_subpel_iterations[12][4] = { { 0, 0, 0, 0 }, { 1, 1, 0, 0 }, { 0, 1, 1, 0 }, { 0, 2, 1, 0 },
@@ -33,16 +33,20 @@ static const uint8_t k_subpel_iterations[12][4] = { { 0, 0, 0, 0 }, { 1, 1, 0, 0
 // |coef| of the tile's two 4x4 Hadamards (even; halved by the caller)
 template <int BD, bool SATD>
 __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD>::PPD],
-                                               const typename PT<BD>::pixel *const (&q)[4], intptr_t rs, int mvx,
-                                               int mvy )
+                                               const typename PT<BD>::pixel *q0, const typename PT<BD>::pixel *q1,
+                                               const typename PT<BD>::pixel *q2, const typename PT<BD>::pixel *q3,
+                                               intptr_t rs, int mvx, int mvy )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD;
     const int idx = ((mvy & 3) << 2) + (mvx & 3);
     const intptr_t off = (intptr_t)(mvy >> 2) * rs + (mvx >> 2);
-    const int i0 = c_ref0[idx], i1 = c_ref1[idx];
-    const pixel *s1 = (i0 == 0 ? q[0] : i0 == 1 ? q[1] : i0 == 2 ? q[2] : q[3]) + off + ((mvy & 3) == 3) * rs;
-    const pixel *s2 = (i1 == 0 ? q[0] : i1 == 1 ? q[1] : i1 == 2 ? q[2] : q[3]) + off + ((mvx & 3) == 3);
+    constexpr uint32_t k0 = pack_fields( c_ref0, 2 ), k1 = pack_fields( c_ref1, 2 );
+    const int i0 = field( k0, 2, idx ), i1 = field( k1, 2, idx );
+    // (four separate pointers, not an array: a select over an array's elements was folded into
+    // an indexed load, which put the array in scratch memory)
+    const pixel *s1 = (i0 == 0 ? q0 : i0 == 1 ? q1 : i0 == 2 ? q2 : q3) + off + ((mvy & 3) == 3) * rs;
+    const pixel *s2 = (i1 == 0 ? q0 : i1 == 1 ? q1 : i1 == 2 ? q2 : q3) + off + ((mvx & 3) == 3);
     // rows as dword-aligned loads realigned with v_alignbyte: the address path takes a
     // byte-misaligned 8-byte lane load at ~2x the cost of an aligned 12-byte one
     // (profiles/r01d_ta_probe.txt), and it binds this kernel (TA busy ~100 %, r04d)
@@ -114,7 +118,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     for( int y = 0; y < 4; y++ )
         load_row_u<HDW>( fe + y * fs, fa[y] );
     const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
-    const pixel *const q[4] = { p0 + qo, p1 + qo, p2 + qo, p3 + qo };
+    const pixel *const q0 = p0 + qo, *const q1 = p1 + qo, *const q2 = p2 + qo, *const q3 = p3 + qo;
 
     const int16_t *p = par + 8 * j;
     const int mvpx = p[2], mvpy = p[3];
@@ -134,11 +138,16 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     // one candidate per group: group g scores (mx[g], my[g]); every lane gets the four costs
     // (pixel cost + p_cost_mvx[mx] + p_cost_mvy[my])
     auto eval4 = [&]( const int (&mx)[4], const int (&my)[4], bool satd, int (&c)[4] ) {
+        // (the group's candidate by selects: indexing the arrays with the lane's group put them
+        // in scratch memory)
+        const int gx = g == 0 ? mx[0] : g == 1 ? mx[1] : g == 2 ? mx[2] : mx[3];
+        const int gy = g == 0 ? my[0] : g == 1 ? my[1] : g == 2 ? my[2] : my[3];
         uint32_t v = 0;
         if( tile )
-            v = satd ? tile_cost<BD, true>( fa, q, rs, mx[g], my[g] ) >> 1 : tile_cost<BD, false>( fa, q, rs, mx[g], my[g] );
+            v = satd ? tile_cost<BD, true>( fa, q0, q1, q2, q3, rs, gx, gy ) >> 1
+                     : tile_cost<BD, false>( fa, q0, q1, q2, q3, rs, gx, gy );
         if( u == 0 )                                      // the group's mv cost, once
-            v += (uint32_t)cmx[mx[g]] + (uint32_t)cmy[my[g]];
+            v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
         v = group_sum( v );
 #pragma unroll
         for( int k = 0; k < 4; k++ )

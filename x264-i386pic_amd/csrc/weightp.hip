@@ -28,8 +28,8 @@ struct WpCands
     int n;
 };
 
-__constant__ uint8_t c_hpel_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };   // common/tables.c:183
-__constant__ uint8_t c_hpel_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };   // common/tables.c:184
+constexpr uint8_t c_hpel_ref0[16] = { 0, 1, 1, 1, 0, 1, 1, 1, 2, 3, 3, 3, 0, 1, 1, 1 };   // common/tables.c:183
+constexpr uint8_t c_hpel_ref1[16] = { 0, 0, 1, 0, 2, 2, 3, 2, 2, 2, 3, 2, 2, 2, 3, 2 };   // common/tables.c:184
 
 template <int BD>
 __device__ __forceinline__ void wp_row8( const typename PT<BD>::pixel *p, int (&o)[8] )
@@ -105,14 +105,14 @@ __global__ __launch_bounds__( 256 ) void wp_cost8_kernel( const typename PT<BD>:
         const int q = ((mvy & 3) << 2) + (mvx & 3);
         const intptr_t off = (intptr_t)(mvy >> 2) * rs + (mvx >> 2) + (intptr_t)r * rs;
         const typename PT<BD>::pixel *P[4] = { r0, r1, r2, r3 };
-        const typename PT<BD>::pixel *s1 = P[c_hpel_ref0[q]] + off + ((mvy & 3) == 3) * rs;
+        const typename PT<BD>::pixel *s1 = P[field( pack_fields( c_hpel_ref0, 2 ), 2, q )] + off + ((mvy & 3) == 3) * rs;
         constexpr int PPD = PT<BD>::PPD, NDW = 8 / PPD;
         uint32_t w1[NDW];
         load_al_pad<NDW>( s1, w1 );
         if( q & 5 )
         {
             uint32_t w2[NDW];
-            load_al_pad<NDW>( P[c_hpel_ref1[q]] + off + ((mvx & 3) == 3), w2 );
+            load_al_pad<NDW>( P[field( pack_fields( c_hpel_ref1, 2 ), 2, q )] + off + ((mvx & 3) == 3), w2 );
 #pragma unroll
             for( int i = 0; i < NDW; i++ )
                 w1[i] = avg_round<BD>( w1[i], w2[i] );
