@@ -919,7 +919,9 @@ __device__ __forceinline__ void lr_band( int j, int mbh, int nslices, int brows,
     }
 }
 
-template <int BD>
+// WGT: the weighted-reference form (rw, the scale / denom / offset); the unweighted kernel
+// carries none of its code or live values
+template <int BD, bool WGT>
 __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *r0,
     const typename PT<BD>::pixel *r1, const typename PT<BD>::pixel *r2, const typename PT<BD>::pixel *r3,
@@ -944,7 +946,7 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     r1 += (intptr_t)f * rfs;
     r2 += (intptr_t)f * rfs;
     r3 += (intptr_t)f * rfs;
-    if( rw )
+    if( WGT )
         rw += (intptr_t)f * rfs;
     intra_cost += (intptr_t)f * nmb;
     if( invq )
@@ -969,7 +971,7 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
         __syncthreads();
         if( threadIdx.x >= 64 )
         {
-            const typename PT<BD>::pixel *const hpl[5] = { r0, r1, r2, r3, rw ? rw : r0 };
+            const typename PT<BD>::pixel *const hpl[5] = { r0, r1, r2, r3, WGT ? rw : r0 };
             lr_helper<BD, 5>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, prog, poll_max );
             return;
         }
@@ -1007,7 +1009,7 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
             LrCtx<BD> m( fe );
             m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd, q );
-            if( rw )
+            if constexpr( WGT )
                 m.set_weight( rw, off, wscale, wdenom, woffset );
             uint32_t pred[4];
             const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, s1, pred, poll_max, status );
@@ -1587,11 +1589,17 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     uint32_t *status = nullptr;
     if( (e = la_status_begin( stream, &status )) != hipSuccess )
         return e;
-    const int help = la_help( (const void *)lowres_inter_kernel<BD>, (int64_t)npairs * nbands, lds, stream );
-    hipLaunchKernelGGL( lowres_inter_kernel<BD>, dim3( npairs * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc,
-                        ffs, ref[0], ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range,
-                        mv_range, lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands,
-                        brows4, la_poll_max(), status, ref_w, wscale, wdenom, woffset, nslices, help );
+    auto go = [&]( auto kernel ) {
+        const int help = la_help( (const void *)kernel, (int64_t)npairs * nbands, lds, stream );
+        hipLaunchKernelGGL( kernel, dim3( npairs * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs, ref[0],
+                            ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
+                            lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands,
+                            brows4, la_poll_max(), status, ref_w, wscale, wdenom, woffset, nslices, help );
+    };
+    if( ref_w )
+        go( lowres_inter_kernel<BD, true> );
+    else
+        go( lowres_inter_kernel<BD, false> );
     if( (e = hipGetLastError()) != hipSuccess )
         return e;
     return la_status_end( stream );
