@@ -336,16 +336,37 @@ template <int BD> struct LrCtx
 };
 
 // x264_me_search_ref (me.c:182-420, 774-790) then refine_subpel (me.c:912-992)
-// role >= 0: the wave's four 16-lane groups run this same search on the same block in
-// lockstep and split each batch of independent candidates (the predictors, the hpel and
-// qpel diamonds): group r scores candidate r, the costs are gathered from the groups
-// and every group makes the same decisions.  role < 0: one group scores them in turn.
-__device__ __forceinline__ int lr_gather( int v, int r )
+// role >= 0: NG groups of the wave (lanes 64/NG apart) run this same search on the same block
+// in lockstep and split each batch of (up to four) independent candidates -- the predictors,
+// the hpel and qpel diamonds: with NG = 4 group r scores candidate r, with NG = 2 candidates r
+// and r + 2 -- the costs are gathered from the groups and every group makes the same
+// decisions.  role < 0: one group scores them in turn.
+template <int NG> __device__ __forceinline__ int lr_gather( int v, int r )
 {
-    return __shfl( v, (int)(threadIdx.x & 15) + 16 * r );
+    constexpr int S = 64 / NG;
+    return __shfl( v, (int)(threadIdx.x & (S - 1)) + S * r );
+}
+// a batch of four candidates split over the NG groups: cand( k ) scores candidate k
+template <int NG, typename F> __device__ __forceinline__ void lr_batch4( int role, F cand, int (&out)[4] )
+{
+    if constexpr( NG == 4 )
+    {
+        const int c = cand( role );
+#pragma unroll
+        for( int r = 0; r < 4; r++ )
+            out[r] = lr_gather<4>( c, r );
+    }
+    else
+    {
+        const int c0 = cand( role ), c1 = cand( role + 2 );
+        out[0] = lr_gather<2>( c0, 0 );
+        out[1] = lr_gather<2>( c0, 1 );
+        out[2] = lr_gather<2>( c1, 0 );
+        out[3] = lr_gather<2>( c1, 1 );
+    }
 }
 
-template <int BD>
+template <int BD, int NG = 4>
 __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int (&mvc)[4][2], int i_mvc,
                               int me_method, int subme, int me_range, int role, int &omvx, int &omvy, int &ocost )
 {
@@ -382,14 +403,11 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         // COST_MV_HPEL of slot 0 (the clipped mvp) and of the valid predictors
         int cpred[4] = { 0, 0, 0, 0 };
         if( role >= 0 )
-        {
-            const int j = role <= valid ? role : 0;
-            const int mx = tmp[j + 1][0], my = tmp[j + 1][1];
-            const int c = m.qpel( mx, my, false ) + m.cmx[mx] + m.cmy[my];
-#pragma unroll
-            for( int r = 0; r < 4; r++ )
-                cpred[r] = lr_gather( c, r );
-        }
+            lr_batch4<NG>( role, [&]( int k ) {
+                const int j = k <= valid ? k : 0;
+                const int mx = tmp[j + 1][0], my = tmp[j + 1][1];
+                return m.qpel( mx, my, false ) + m.cmx[mx] + m.cmy[my];
+            }, cpred );
         else
             cpred[0] = m.qpel( bpx, bpy, false ) + m.cmx[bpx] + m.cmy[bpy];
         bpred_cost = cpred[0];
@@ -619,11 +637,14 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
             const int omx = bmx, omy = bmy;
             if( role >= 0 )
             {
-                const int qx = omx + (role == 2 ? -2 : role == 3 ? 2 : 0), qy = omy + (role == 0 ? -2 : role == 1 ? 2 : 0);
-                const int c = m.qpel( qx, qy, false ) + m.cmx[qx] + m.cmy[qy];
+                int c4[4];
+                lr_batch4<NG>( role, [&]( int k ) {
+                    const int qx = omx + (k == 2 ? -2 : k == 3 ? 2 : 0), qy = omy + (k == 0 ? -2 : k == 1 ? 2 : 0);
+                    return m.qpel( qx, qy, false ) + m.cmx[qx] + m.cmy[qy];
+                }, c4 );
 #pragma unroll
                 for( int r = 0; r < 4; r++ )
-                    costs[r] = lr_gather( c, r );
+                    costs[r] = c4[r];
             }
             else
             {
@@ -655,13 +676,10 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         const int omx = bmx, omy = bmy;
         int cq[4] = { 0, 0, 0, 0 };
         if( role >= 0 )
-        {
-            const int qx = omx + (role == 2 ? -1 : role == 3 ? 1 : 0), qy = omy + (role == 0 ? -1 : role == 1 ? 1 : 0);
-            const int c = m.qpel( qx, qy, m.satd ) + m.cmx[qx] + m.cmy[qy];
-#pragma unroll
-            for( int r = 0; r < 4; r++ )
-                cq[r] = lr_gather( c, r );
-        }
+            lr_batch4<NG>( role, [&]( int k ) {
+                const int qx = omx + (k == 2 ? -1 : k == 3 ? 1 : 0), qy = omy + (k == 0 ? -1 : k == 1 ? 1 : 0);
+                return m.qpel( qx, qy, m.satd ) + m.cmx[qx] + m.cmy[qy];
+            }, cq );
 #pragma unroll
         for( int dir = 0; dir < 4; dir++ )
         {
@@ -688,7 +706,7 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
 // one list of slicetype_mb_cost (slicetype.c:645-702): reverse-order predictors from the
 // row ring of this pass, the near-zero fast skip, x264_me_search and the cost
 // adjustments.  Returns the list cost; mvx / mvy the list's mv.
-template <int BD>
+template <int BD, int NG = 4>
 __device__ __forceinline__ int lr_list( LrCtx<BD> &m, const uint32_t (&pred)[4], int npred, int me_method, int subme,
                                         int me_range, int lambda, const uint16_t *cost_mv, int &mvx, int &mvy,
                                         int role = -1 )
@@ -726,7 +744,7 @@ __device__ __forceinline__ int lr_list( LrCtx<BD> &m, const uint32_t (&pred)[4],
     }
     if( !skip )
     {
-        lr_me_search<BD>( m, mvpx, mvpy, mvc, i_mvc, me_method, subme, me_range, role, mvx, mvy, cost );
+        lr_me_search<BD, NG>( m, mvpx, mvpy, mvc, i_mvc, me_method, subme, me_range, role, mvx, mvy, cost );
         cost -= cost_mv[0];
         if( mvx | mvy )
             cost += 5 * lambda;
@@ -1155,14 +1173,15 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
     const int q = threadIdx.x & 3;
     const bool hp = subme == 2;                  // h->param.analyse.i_subpel_refine <= 1
     // The wave's four 16-lane groups (roles) work on the same <= 4 block rows at once:
-    // roles 0 and 1 run the list-0 and list-1 searches as one instruction stream (the
-    // same code on per-lane planes, ring and mvs), then roles 0, 1, 2 run the three
-    // TRY_BIDIR evaluations together (the p1-predicted pair, (0, 0), the searched pair);
-    // role 0 gathers the values and makes slicetype_mb_cost's decisions in its order.
+    // roles 0 / 2 run the list-0 search and roles 1 / 3 the list-1 search as one instruction
+    // stream (the same code on per-lane planes, ring and mvs; each list's two groups split its
+    // candidate batches), then roles 0, 1, 2 run the three TRY_BIDIR evaluations together (the
+    // p1-predicted pair, (0, 0), the searched pair); role 0 gathers the values and makes
+    // slicetype_mb_cost's decisions in its order.
     const int role = (int)(threadIdx.x >> 4);
     const int rl = (int)(threadIdx.x & 15);      // lane within the role: 4 * row + q
     const int y = y0 + (rl >> 2);
-    const bool mine = role < 3 && y < y1;
+    const bool mine = y < y1;                    // (role 3 helps the list-1 search)
     const int t0 = 2 * (s1 - y1), t1 = 2 * (s1 - 1 - y0) + mbw - 1;
     if( help )
     {
@@ -1216,25 +1235,27 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
         {
             m0.setup( a0, a1, a2, a3, off, stride, x, y, mbw, mbh, mvr, satd, q );
             m1.setup( b0, b1, b2, b3, off, stride, x, y, mbw, mbh, mvr, satd, q );
-            if( role < 2 )
             {
-                // the searching lanes' own context: list `role`'s planes (a per-lane choice
-                // of pointers, not of objects, so nothing goes to scratch)
-                ms.setup( role ? b0 : a0, role ? b1 : a1, role ? b2 : a2, role ? b3 : a3, off, stride, x, y, mbw,
+                // every role searches: list `lst` = role & 1 on groups lg = role >> 1 (two
+                // groups per list split its candidate batches); the searching lanes' own
+                // context: the list's planes (a per-lane choice of pointers, not of objects,
+                // so nothing goes to scratch)
+                const int lst = role & 1, lg = role >> 1;
+                ms.setup( lst ? b0 : a0, lst ? b1 : a1, lst ? b2 : a2, lst ? b3 : a3, off, stride, x, y, mbw,
                           mbh, mvr, satd, q );
-                // list `role`: searched on the wavefront (search & (1 << role)) or read
-                int *ring = role ? ring1 : ring0;
-                uint32_t *gmv = role ? gmv1 : gmv0;
-                int32_t *costs = role ? costs1 : costs0;
-                if( search & (1 << role) )
+                // list `lst`: searched on the wavefront (search & (1 << lst)) or read
+                int *ring = lst ? ring1 : ring0;
+                uint32_t *gmv = lst ? gmv1 : gmv0;
+                int32_t *costs = lst ? costs1 : costs0;
+                if( search & (1 << lst) )
                 {
                     uint32_t pred[4];
                     const int np = lr_preds( ring, y0, y1, gmv, x, y, mbw, s1, pred, poll_max, status );
                     // the searching lanes run one instruction stream: a failed wait stops them all
                     failed = __builtin_amdgcn_ballot_w64( np < 0 ) != 0;
                     if( !failed )
-                        lc = lr_list<BD>( ms, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy );
-                    if( !failed && q == 0 )
+                        lc = lr_list<BD, 2>( ms, pred, np, me_method, subme, me_range, lambda, cml, mvx, mvy, lg );
+                    if( !failed && q == 0 && lg == 0 )
                     {
                         ring[4 * (y - y0) + (x & 3)] = (int)lr_pack( mvx, mvy );
                         lr_store_mv( gmv + mb, lr_pack( mvx, mvy ) );
