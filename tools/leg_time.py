@@ -2,7 +2,8 @@
 """Run bench.py side legs alone on the bench's 16-pair 1080p workload (for rocprofv3 trace /
 PMC passes and A/Bs): leg_time.py LEG [steps] [pairs] with LEG one of esa (the ESA table and
 fused legs, then refine_subpel chained from the ESA decisions), full8 (the quadrant tables),
-tesa, la (the lookahead's P and B searches), wp (the weight search).  Prints the legs' JSON."""
+tesa, la (the lookahead's P and B searches), wp (the weight search), me10 (configs[4]'s 10-bit
+full search, quadrant tables and 8x8 DCT+quant).  Prints the legs' JSON."""
 import json
 import os
 import sys
@@ -38,6 +39,8 @@ def main():
         louts, _ = x.frame_init_lowres(dev[:-1], origin, stride, W, H)
         iouts = x.lowres_intra_cost(louts[0], x.plane_stride(W // 2), mbw, mbh, True, True, 1)
         res = bench.rates_lookahead(x, a, 1, louts, iouts, W, mbw, mbh, F)
+    elif leg == "me10":
+        res = bench.rates_10bit(x, a, 1, mbw, mbh, F)
     elif leg == "wp":
         res = bench.rates_weightp(x, a, 1, dev, origin, stride, mbw, mbh)
         res.update(bench.rates_ssim(x, a, 1, dev, origin, stride, mbw, mbh))

@@ -408,17 +408,17 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
                                                                   const int16_t *__restrict__ centre,
                                                                   int16_t *__restrict__ origin, int xcd )
 {
-    const int64_t slot = (int64_t)(xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
-    if( slot >= total )
+    // 32-bit index decomposition as in v7 (the launcher keeps the lane count below 2^32)
+    const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
+    const uint32_t slot = blk * blockDim.x + threadIdx.x;
+    if( slot >= (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw * (uint32_t)(2 * G) )
         return;
     const int h = (int)(slot & 1);
-    const int grp = (int)((slot >> 1) % G);
-    const int64_t mb = slot / (2 * G);
-    const int mbx = (int)(mb % mbw);
-    const int64_t t = mb / mbw;
-    const int mby = (int)(t % mbh);
-    const int64_t f = t / mbh;
+    const uint32_t mb32 = slot / (2 * G), t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+    const int grp = (int)((slot >> 1) - mb32 * G);
+    const int mbx = (int)(mb32 - t32 * (uint32_t)mbw);
+    const int mby = (int)(t32 - f32 * (uint32_t)mbh);
+    const int64_t mb = mb32, f = f32;
 
     uint32_t F[8][8];
     const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
@@ -439,10 +439,11 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_v5_kernel( const uint16_t
         (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 2 * grp);
     uint32_t *out = table + mb * ((2 * R + 1) * P) + 2 * grp;
     uint32_t acc[8][2];
-    auto store = [out, h]( int c, uint32_t a0, uint32_t a1 ) {
-        if( !h )                                // both lanes of the pair hold the sums
-            *(uint2 *)(out + c * P) = make_uint2( a0, a1 );
-    };
+    // both lanes of the pair hold the sums and both store them (to the same address): with
+    // the store predicated on h == 0 the compiler kept every row's sums live across the
+    // branch -- 220 VGPRs and 2 waves per SIMD instead of 118 and 4, the round-4 regression
+    // of 0.617 -> 0.71 ms per 16 1080p pairs
+    auto store = [out]( int c, uint32_t a0, uint32_t a1 ) { *(uint2 *)(out + c * P) = make_uint2( a0, a1 ); };
     me_rows5p<R, ME_LEAD>( rbase, (int)(rs / 2), F, acc, store, std::make_integer_sequence<int, 2 * R + 8>{} );
 }
 
@@ -519,17 +520,16 @@ __global__ __launch_bounds__( 256 ) void me_full_sad8q_v5_kernel( const uint16_t
                                                                   int nframes, uint16_t *__restrict__ table8, int xcd )
 {
     constexpr int G = R + 1, P = full_pitch( R );
-    const int64_t slot = (int64_t)(xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * blockDim.x + threadIdx.x;
-    const int64_t total = (int64_t)nframes * mbh * mbw * (2 * G);
-    if( slot >= total )
+    const uint32_t blk = xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x;
+    const uint32_t slot = blk * blockDim.x + threadIdx.x;
+    if( slot >= (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw * (uint32_t)(2 * G) )
         return;
     const int h = (int)(slot & 1);
-    const int grp = (int)((slot >> 1) % G);
-    const int64_t mb = slot / (2 * G);
-    const int mbx = (int)(mb % mbw);
-    const int64_t t = mb / mbw;
-    const int mby = (int)(t % mbh);
-    const int64_t f = t / mbh;
+    const uint32_t mb32 = slot / (2 * G), t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+    const int grp = (int)((slot >> 1) - mb32 * G);
+    const int mbx = (int)(mb32 - t32 * (uint32_t)mbw);
+    const int mby = (int)(t32 - f32 * (uint32_t)mbh);
+    const int64_t mb = mb32, f = f32;
     uint32_t F[8][8];
     const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
     const int fs_dw = (int)(fs / 2);
@@ -604,8 +604,8 @@ hipError_t launch_me_full( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
     const int ncol = cen ? cen_pitch( BD, range ) : 2 * range + 1;
     const int64_t groups = BD == 8 ? al4( ncol ) / 4 : 2 * (cen ? cen_cols( 10, range ) / 2 : range + 1);
     bool grouped = !(((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)(fs * PSZ) | (uintptr_t)(rs * PSZ)) & 3);
-    if( BD == 8 && nmb * groups >= (1ll << 32) )
-        grouped = false;                        // (the 8-bit kernel indexes its lanes in 32 bits)
+    if( nmb * groups >= (1ll << 32) )
+        grouped = false;                        // (the grouped kernels index their lanes in 32 bits)
     const int64_t lanes = nmb * (grouped ? groups : ncol);
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
     const int xcd = me_xcd();
