@@ -161,6 +161,26 @@ typedef struct x264hip_weight_t
     int32_t weighted, scale, denom, offset;
 } x264hip_weight_t;
 
+/* what x264hip_*_me_refine_subpel_ex adds to the luma-only refine (reference encoder/me.c:
+ * 826-863, 872-875): chroma ME (h->mb.b_chroma_me, on for P slices at subme >= 5 by default,
+ * common/macroblock.c:507-509) and weighted references (m->weight = h->sh.weight[i_ref],
+ * encoder/analyse.c:1248-1250).  fenc_chroma / ref_chroma: device pointers at pixel (0,0) of
+ * frame 0 -- 4:2:0 / 4:2:2: the frame's interleaved NV12 / NV16 plane (fenc->plane[1]) in [0];
+ * 4:4:4: fenc's U, V planes in [0..1] and the reference's U planes F, H, V, C (x264_frame_filter's
+ * filtered[1][0..3]) in ref_chroma[0..3], V's in [4..7].  Frame strides step the pos[] frame
+ * index as the luma ones do. */
+typedef struct x264hip_refine_ext_t
+{
+    int32_t b_chroma_me;            /* h->mb.b_chroma_me */
+    int32_t chroma_format;          /* 1 = 4:2:0, 2 = 4:2:2, 3 = 4:4:4 (read when b_chroma_me) */
+    int32_t mvy_offset;             /* me.c:875 (0 for progressive frames) */
+    x264hip_weight_t weight[3];     /* m->weight[0..2] (weighted = 0: weightfn == NULL) */
+    const void *fenc_chroma[2];
+    intptr_t fenc_chroma_stride, fenc_chroma_frame_stride;
+    const void *ref_chroma[8];
+    intptr_t ref_chroma_stride, ref_chroma_frame_stride;
+} x264hip_refine_ext_t;
+
 /* cost kinds of x264hip_*_weight_cost_batch (slicetype.c:191-282) */
 enum
 {
@@ -820,8 +840,13 @@ int x264hip_##BD##_subpel_qpel9_batch( int op, int i_pixel, const pixel *fenc,  
  * par[8*i] = { mvx, mvy (qpel start, m->mv), mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel x, y  \
  * (h->mb.mv_min_spel / mv_max_spel) }; init_cost[i] = m->cost; cost_mv at mvd 0.                \
  * out[4*i] = { m->cost, m->mv[0], m->mv[1], m->cost_mv } (16-byte aligned); nevals (or NULL):  \
- * the reference's cmp calls per partition, SADs | SATDs << 16.  Luma only (no b_chroma_me),     \
- * no multi-reference threshold, unweighted references. */                                      \
+ * the reference's cmp calls per partition: luma SADs | luma SATDs << 16 | chroma mbcmp calls     \
+ * << 24.  No multi-reference threshold (p_halfpel_thresh = NULL).  This form is luma-only with  \
+ * unweighted references; _ex takes x264hip_refine_ext_t (NULL = the same as this form): every  \
+ * luma get_ref weighted by weight[0] (mc.c:221-249), and with b_chroma_me COST_MV_SATD's       \
+ * chroma cost (mc_chroma + mbcmp[chromapix] of U then V, or get_ref + mbcmp_unaligned of the    \
+ * U / V hpel planes at 4:4:4, weighted by weight[1] / weight[2]) added as the reference adds   \
+ * it, including the SATD re-score of the hpel winner (me.c:925-929). */                         \
 int x264hip_##BD##_me_refine_subpel( const pixel *fenc, intptr_t fenc_stride,                   \
                                      intptr_t fenc_frame_stride, const pixel *fpel,             \
                                      const pixel *hpel_h, const pixel *hpel_v,                  \
@@ -831,6 +856,16 @@ int x264hip_##BD##_me_refine_subpel( const pixel *fenc, intptr_t fenc_stride,   
                                      const int16_t *par, const int32_t *init_cost,              \
                                      const uint16_t *cost_mv, int n, int32_t *out,              \
                                      int32_t *nevals, void *stream );                           \
+int x264hip_##BD##_me_refine_subpel_ex( const pixel *fenc, intptr_t fenc_stride,                \
+                                        intptr_t fenc_frame_stride, const pixel *fpel,          \
+                                        const pixel *hpel_h, const pixel *hpel_v,               \
+                                        const pixel *hpel_c, intptr_t ref_stride,               \
+                                        intptr_t ref_frame_stride, int i_pixel, int subme,      \
+                                        int refine_qpel, int fpel_satd, const int32_t *pos,     \
+                                        const int16_t *par, const int32_t *init_cost,           \
+                                        const uint16_t *cost_mv, int n, int32_t *out,           \
+                                        int32_t *nevals, const x264hip_refine_ext_t *ext,       \
+                                        void *stream );                                         \
                                                                                                 \
 /* block lists of the reference transforms (dct.c), device arrays;                             \
  * dct holds n consecutive outputs of the selected entry's size. */                             \

@@ -1689,40 +1689,137 @@ void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const i
 }
 
 /* refine_subpel (reference encoder/me.c:865-992) for a list of partitions, semantics of
- * x264hip_*_me_refine_subpel: luma only (b_chroma_me = 0), p_halfpel_thresh = NULL, no
- * weights.  Iterations from subpel_iterations (me.c:38-50): refine_qpel = 0 is the call
- * of x264_me_search_ref (me.c:791-797, entries 2-3), 1 the one of x264_me_refine_qpel
- * (me.c:801-810, entries 0-1).  fpelcmp = satd iff fpel_satd (TESA) and subme > 1,
- * mbcmp_unaligned = satd iff subme > 1 (encoder.c:1411-1426).  fenc / planes point at
- * pixel (0,0) of one frame (planes = F, H, V, C); pos[2*i] = the partition's top-left
- * pixel; par[8*i] = { mvx, mvy (qpel, m->mv), mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel
- * x, y }; cost[i] = m->cost; cost_mv at mvd 0.  out[4*i] = { cost, mvx, mvy, cost_mv };
- * nevals[i] (when given) = the number of sad | satd calls << 16 the reference makes. */
+ * x264hip_*_me_refine_subpel_ex: p_halfpel_thresh = NULL.  Iterations from subpel_iterations
+ * (me.c:38-50): refine_qpel = 0 is the call of x264_me_search_ref (me.c:791-797, entries
+ * 2-3), 1 the one of x264_me_refine_qpel (me.c:801-810, entries 0-1).  fpelcmp = satd iff
+ * fpel_satd (TESA) and subme > 1, mbcmp / mbcmp_unaligned = satd iff subme > 1
+ * (encoder.c:1409-1426).  fenc / planes point at pixel (0,0) of one frame (planes = F, H, V,
+ * C); pos[2*i] = the partition's top-left pixel; par[8*i] = { mvx, mvy (qpel, m->mv), mvp_x,
+ * mvp_y, mv_min_spel x, y, mv_max_spel x, y }; cost[i] = m->cost; cost_mv at mvd 0.
+ * out[4*i] = { cost, mvx, mvy, cost_mv }; nevals[i] (when given) = the reference's cmp calls:
+ * luma SADs | luma SATDs << 16 | chroma mbcmp calls << 24.
+ * ext (NULL = luma only, unweighted) = { b_chroma_me (h->mb.b_chroma_me), chroma_format (1
+ * 4:2:0, 2 4:2:2, 3 4:4:4), mvy_offset (me.c:875), then m->weight[0..2] as { weighted,
+ * scale, denom, offset } }.  fenc_c = the frame's NV12 / NV16 plane in [0] or its U, V planes
+ * (4:4:4), stride fcs; ref_c = the reference's NV12 / NV16 plane in [0] or (4:4:4) the F, H,
+ * V, C planes of U then of V, stride rcs; all at pixel (0,0). */
 static const uint8_t subpel_iterations[12][4] = { {0,0,0,0}, {1,1,0,0}, {0,1,1,0}, {0,2,1,0}, {0,2,1,1},
                                                   {0,2,1,2}, {0,0,2,2}, {0,0,2,2}, {0,0,4,10}, {0,0,4,10},
                                                   {0,0,4,10}, {0,0,4,10} };
-void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs, int i_pixel,
-                           int subme, int refine_qpel, int fpel_satd, const int32_t *pos, const int16_t *par,
-                           const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out, int32_t *nevals )
+/* x264_luma2chroma_pixel (reference common/pixel.h:70-76), partitions 16x16 .. 8x8 */
+static const uint8_t luma2chroma_pixel[4][4] = { { 0 }, { 3, 4, 5, 6 }, { 2, 3, 7, 5 }, { 0, 1, 2, 3 } };
+void FN(mc_chroma)( pixel *dstu, pixel *dstv, intptr_t ds, const pixel *src, intptr_t ss, int mvx, int mvy,
+                    int w, int h );
+
+typedef struct
+{
+    int b_chroma_me, cf, mvy_offset, satd, i_pixel, bx, by;
+    const int *wt[3];                    /* { scale, denom, offset } of a weighted plane, or NULL */
+    const pixel *fenc_c[2], *ref_c[8];
+    intptr_t fcs, rcs;
+    int nchroma;
+} FN(rs_chroma_t);
+
+/* the chroma half of COST_MV_SATD (me.c:833-861): U's cost added when the luma cost beats
+ * bcost, then V's when the sum still does */
+static int FN(rs_chroma)( FN(rs_chroma_t) *c, int mx, int my, int cost, int bcost )
+{
+    const int i_pixel = c->i_pixel, bw = pixel_w[i_pixel], bh = pixel_h[i_pixel];
+    pixel pix[2][16 * 16];
+    if( c->cf == 3 )
+    {
+        for( int p = 0; p < 2 && cost < bcost; p++ )
+        {
+            const pixel *q[4];
+            for( int k = 0; k < 4; k++ )
+                q[k] = c->ref_c[4 * p + k] + c->by * c->rcs + c->bx;
+            intptr_t ts = 16;
+            const pixel *r = get_ref_w( pix[p], &ts, q, c->rcs, mx, my, bw, bh, c->wt[1 + p] );
+            const pixel *f = c->fenc_c[p] + c->by * c->fcs + c->bx;
+            cost += c->satd ? FN(satd)( i_pixel, f, c->fcs, r, ts ) : FN(sad)( i_pixel, f, c->fcs, r, ts );
+            c->nchroma++;
+        }
+        return cost;
+    }
+    const int vs = c->cf == 1, cw = bw >> 1, ch = bh >> vs, cpix = luma2chroma_pixel[c->cf][i_pixel];
+    const intptr_t crow = (intptr_t)(c->by >> vs);
+    FN(mc_chroma)( pix[0], pix[1], 16, c->ref_c[0] + crow * c->rcs + c->bx, c->rcs, mx,
+                   2 * (my + c->mvy_offset) >> vs, cw, ch );
+    pixel fe[2][16 * 16];
+    for( int y = 0; y < ch; y++ )
+        for( int x = 0; x < cw; x++ )
+            for( int p = 0; p < 2; p++ )
+                fe[p][16 * y + x] = c->fenc_c[0][(crow + y) * c->fcs + c->bx + 2 * x + p];
+    for( int p = 0; p < 2 && cost < bcost; p++ )
+    {
+        if( c->wt[1 + p] )
+            FN(mc_weight)( pix[p], 16, pix[p], 16, c->wt[1 + p][0], c->wt[1 + p][1], c->wt[1 + p][2], cw, ch );
+        cost += c->satd ? FN(satd)( cpix, fe[p], 16, pix[p], 16 ) : FN(sad)( cpix, fe[p], 16, pix[p], 16 );
+        c->nchroma++;
+    }
+    return cost;
+}
+
+void FN(me_refine_subpel_ex)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs,
+                              int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
+                              const int16_t *par, const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out,
+                              int32_t *nevals, const int32_t *ext, const pixel *const fenc_c[2], intptr_t fcs,
+                              const pixel *const ref_c[8], intptr_t rcs )
 {
     const int bw = pixel_w[i_pixel], bh = pixel_h[i_pixel];
     const int hpel_iters = subpel_iterations[subme][refine_qpel ? 0 : 2];
     const int qpel_iters = subpel_iterations[subme][refine_qpel ? 1 : 3];
     const int fsatd = fpel_satd && subme > 1, qsatd = subme > 1;
+    /* me.c:872: every partition here is <= PIXEL_8x8 */
+    const int b_chroma_me = ext && ext[0];
+    FN(rs_chroma_t) cc = { 0 };
+    const int *wt0 = NULL;
+    int wbuf[3][3];
+    if( ext )
+    {
+        cc.b_chroma_me = b_chroma_me;
+        cc.cf = ext[1];
+        cc.mvy_offset = ext[2];
+        cc.satd = qsatd;
+        cc.i_pixel = i_pixel;
+        for( int p = 0; p < 3; p++ )
+        {
+            for( int k = 0; k < 3; k++ )
+                wbuf[p][k] = ext[4 + 4 * p + k];
+            cc.wt[p] = ext[3 + 4 * p] ? wbuf[p] : NULL;
+        }
+        wt0 = cc.wt[0];
+        if( b_chroma_me )
+        {
+            for( int p = 0; p < 2; p++ )
+                cc.fenc_c[p] = fenc_c[p];
+            for( int p = 0; p < 8; p++ )
+                cc.ref_c[p] = ref_c[p];
+            cc.fcs = fcs;
+            cc.rcs = rcs;
+        }
+    }
     for( int i = 0; i < n; i++ )
     {
         const pixel *f = fenc + pos[2*i+1] * fs + pos[2*i];
         const pixel *q[4];
         for( int k = 0; k < 4; k++ )
             q[k] = planes[k] + pos[2*i+1] * rs + pos[2*i];
+        cc.bx = pos[2*i];
+        cc.by = pos[2*i+1];
+        cc.nchroma = 0;
         const int16_t *p = par + 8 * i;
         const uint16_t *p_cost_mvx = cost_mv - p[2], *p_cost_mvy = cost_mv - p[3];
         const int mv_min_spel[2] = { p[4], p[5] }, mv_max_spel[2] = { p[6], p[7] };
         pixel tmp[16 * 16];
-#define RS_CMP( use_satd, mx, my ) ( ts = 16, r = FN(get_ref)( tmp, &ts, q, rs, mx, my, bw, bh ), \
+        /* get_ref with m->weight[0] (mc.c:221-249), then fpelcmp / mbcmp_unaligned */
+#define RS_CMP( use_satd, mx, my ) ( ts = 16, r = get_ref_w( tmp, &ts, q, rs, mx, my, bw, bh, wt0 ), \
                                      (use_satd) ? (nsatd++, FN(satd)( i_pixel, f, fs, r, ts ))  \
                                                 : (nsad++, FN(sad)( i_pixel, f, fs, r, ts )) )
-        int nsad = 0, nsatd = 0;
+        /* COST_MV_SATD's cost (me.c:826-863) against the running bcost */
+#define RS_SATD( mx, my ) ( c_ = RS_CMP( qsatd, mx, my ) + p_cost_mvx[mx] + p_cost_mvy[my],           \
+                            (b_chroma_me && c_ < bcost) ? FN(rs_chroma)( &cc, mx, my, c_, bcost ) : c_ )
+        int nsad = 0, nsatd = 0, c_;
         intptr_t ts;
         const pixel *r;
         int bmx = p[0], bmy = p[1], bcost = cost[i];
@@ -1760,10 +1857,11 @@ void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const pl
             }
             bcost >>= 6;
         }
-        if( !refine_qpel && qsatd != fsatd )
+        if( !refine_qpel && (qsatd != fsatd || b_chroma_me) )
         {
-            /* bcost = COST_MAX; COST_MV_SATD( bmx, bmy, -1 ) */
-            bcost = RS_CMP( qsatd, bmx, bmy ) + p_cost_mvx[bmx] + p_cost_mvy[bmy];
+            /* bcost = COST_MAX; COST_MV_SATD( bmx, bmy, -1 ) (me.c:925-929) */
+            bcost = 1 << 28;
+            bcost = RS_SATD( bmx, bmy );
         }
         if( subme != 1 )
         {
@@ -1780,7 +1878,7 @@ void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const pl
                     if( !refine_qpel && (dir ^ 1) == odir )
                         continue;
                     int mx = omx + qd[dir][0], my = omy + qd[dir][1];
-                    int c = RS_CMP( qsatd, mx, my ) + p_cost_mvx[mx] + p_cost_mvy[my];
+                    int c = RS_SATD( mx, my );
                     if( c < bcost ) { bcost = c; bmx = mx; bmy = my; bdir = dir; }
                 }
                 if( bmx == omx && bmy == omy )
@@ -1803,14 +1901,23 @@ void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const pl
             bmy -= (int32_t)((uint32_t)bcost << 30) >> 30;
             bcost >>= 4;
         }
+#undef RS_SATD
 #undef RS_CMP
         out[4*i] = bcost;
         out[4*i+1] = bmx;
         out[4*i+2] = bmy;
         out[4*i+3] = p_cost_mvx[bmx] + p_cost_mvy[bmy];
         if( nevals )
-            nevals[i] = nsad | (nsatd << 16);
+            nevals[i] = nsad | (nsatd << 16) | (cc.nchroma << 24);
     }
+}
+
+void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs, int i_pixel,
+                           int subme, int refine_qpel, int fpel_satd, const int32_t *pos, const int16_t *par,
+                           const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out, int32_t *nevals )
+{
+    FN(me_refine_subpel_ex)( fenc, fs, planes, rs, i_pixel, subme, refine_qpel, fpel_satd, pos, par, cost, cost_mv,
+                             n, out, nevals, NULL, NULL, 0, NULL, 0 );
 }
 
 /* TESA integer-pel search of x264_me_search_ref for PIXEL_16x16, restated from

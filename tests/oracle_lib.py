@@ -74,6 +74,8 @@ for _bd in (8, 10):
     _f(_bd, "me_search_centred", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P])
     _f(_bd, "me_refine_subpel", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P,
                                  _P])
+    _f(_bd, "me_refine_subpel_ex", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int,
+                                    _P, _P, _P, _P, _IP, _P, _IP])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
     _f(_bd, "subpel_list", [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P])
     _f(_bd, "sa8d", [C.c_int, _P, _IP, _P, _IP], C.c_int)
@@ -342,11 +344,24 @@ def me_search_centred(bd, fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, rng, 
     return out, org
 
 
+def refine_ext(b_chroma_me=0, chroma_format=1, mvy_offset=0, weights=(None, None, None)):
+    """the ext[15] array of me_refine_subpel_ex: b_chroma_me, chroma_format, mvy_offset, then
+    m->weight[0..2] as (weighted, scale, denom, offset); weights[p] = (scale, denom, offset) or None"""
+    e = [int(b_chroma_me), int(chroma_format), int(mvy_offset)]
+    for w in weights:
+        e += [0, 0, 0, 0] if w is None else [1] + [int(v) for v in w]
+    return np.array(e, np.int32)
+
+
 def me_refine_subpel(bd, fenc, f_origin, fs, planes, r_origin, rs, i_pixel, subme, pos_xy, par, cost, cost_mv, c0,
-                     refine_qpel=False, fpel_satd=False, counts=False):
+                     refine_qpel=False, fpel_satd=False, counts=False, ext=None, fenc_c=None, fc_origin=0, fcs=0,
+                     ref_c=None, rc_origin=0, rcs=0):
     """one frame: refine_subpel (me.c:865-992) of the partitions at pos_xy int32 [n, 2]; planes =
     the four reference planes (numpy, same layout); returns int32 [n, 4] (and the per-partition
-    cmp-call counts, sad | satd << 16, with counts=True)."""
+    cmp-call counts, luma sad | luma satd << 16 | chroma mbcmp << 24, with counts=True).  ext
+    (refine_ext) turns on chroma ME / weighted references: fenc_c = [NV12 plane] or [U, V],
+    ref_c = [NV12 plane] or the F, H, V, C planes of U then V (4:4:4), with their origins /
+    strides."""
     n = len(pos_xy)
     pos = np.ascontiguousarray(pos_xy, np.int32)
     p = np.ascontiguousarray(par, np.int16)
@@ -354,9 +369,13 @@ def me_refine_subpel(bd, fenc, f_origin, fs, planes, r_origin, rs, i_pixel, subm
     out = np.zeros((n, 4), np.int32)
     ne = np.zeros(n, np.int32)
     arr = (C.c_void_p * 4)(*[_addr(q, r_origin).value for q in planes])
-    getattr(_L, f"oracle{bd}_me_refine_subpel")(_addr(fenc, f_origin), fs, arr, rs, i_pixel, subme,
-                                               int(bool(refine_qpel)), int(bool(fpel_satd)), _addr(pos), _addr(p),
-                                               _addr(c), _addr(cost_mv, c0), n, _addr(out), _addr(ne))
+    fca = (C.c_void_p * 2)(*([_addr(q, fc_origin).value for q in (fenc_c or [])] + [None] * 2)[:2])
+    rca = (C.c_void_p * 8)(*([_addr(q, rc_origin).value for q in (ref_c or [])] + [None] * 8)[:8])
+    e = None if ext is None else np.ascontiguousarray(ext, np.int32)
+    getattr(_L, f"oracle{bd}_me_refine_subpel_ex")(_addr(fenc, f_origin), fs, arr, rs, i_pixel, subme,
+                                                  int(bool(refine_qpel)), int(bool(fpel_satd)), _addr(pos), _addr(p),
+                                                  _addr(c), _addr(cost_mv, c0), n, _addr(out), _addr(ne),
+                                                  None if e is None else _addr(e), fca, fcs, rca, rcs)
     return (out, ne) if counts else out
 
 

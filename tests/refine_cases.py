@@ -38,3 +38,40 @@ def jobs(mbw, mbh, nframes, i_pixel, seed, motion=(12, 8), spread=24, cost_scale
     cost = (rs.integers(200, 6000, len(pos)) * cost_scale).astype(np.int32)
     cost[::9] = 0                                                         # nothing beats the start
     return pos, par, cost
+
+
+# ---------------------------------------------------------------- chroma ME / weighted references
+# (x264's default preset: b_chroma_me on P slices at subme >= 5, common/macroblock.c:507-509)
+LUMA2CHROMA = {1: [3, 4, 5, 6], 2: [2, 3, 7, 5], 3: [0, 1, 2, 3]}     # common/pixel.h:70-76
+
+
+class ChromaCase:
+    """one (ref, fenc) frame pair of weightp_cases.make_pair in chroma format cf with everything
+    refine_subpel's chroma ME reads: the luma hpel planes, the NV12 / NV16 planes (4:2:0 / 4:2:2)
+    or the U, V planes and their hpel planes (4:4:4).  fade: the luma / chroma fades of fenc
+    (the content weighted references exist for)."""
+
+    def __init__(self, bd, W, H, cf, seed=1, fade=False):
+        import numpy_ref as nr
+        import weightp_cases as wc
+        lf, cfade = ((0.8, 20.0), ((0.9, 6.0), (1.1, -5.0))) if fade else ((1.0, 0.0), ((1.0, 0.0), (1.0, 0.0)))
+        self.ref, self.fenc = wc.make_pair(bd, W, H, cf, luma_fade=lf, chroma_fade=cfade, seed=seed)
+        self.bd, self.W, self.H, self.cf = bd, W, H, cf
+        r, f = self.ref, self.fenc
+        self.stride, self.origin = r.ys, r.yo
+        self.luma = [r.y.ravel()] + [h.ravel() for h in nr.hpel_planes(r.y, 32, W, H, bd)]
+        self.fenc_y = f.y.ravel()
+        self.cs, self.co = r.cs, r.co
+        if cf in (1, 2):
+            self.fenc_c = [f.nv.ravel()]
+            self.ref_c = [r.nv.ravel()]
+        else:
+            self.fenc_c = [f.u.ravel(), f.v.ravel()]
+            self.ref_c = []
+            for p in (r.u, r.v):
+                self.ref_c += [p.ravel()] + [h.ravel() for h in nr.hpel_planes(p, 32, W, H, bd)]
+
+
+# weights near the fades above (luma 0.8 * 32 / 32, +20; U 0.9, +6; V 1.1, -5), denom 0 on one
+FADE_WEIGHTS = ((26, 5, 20), (29, 5, 6), (9, 3, -5))
+FADE_WEIGHTS_DENOM0 = ((1, 0, 20), None, (1, 0, -5))

@@ -25,7 +25,7 @@ import numpy as np
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "refine_ext", "RefineExt", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "stream_pair_destroy", "me_search_full8",
@@ -1165,14 +1165,47 @@ def subpel_qpel9_batch(op, i_pixel, fenc, fenc_stride, planes, ref_origin, ref_s
     return scores
 
 
+class RefineExt(_c.Structure):
+    """x264hip_refine_ext_t: chroma ME and weighted references of me_refine_subpel_ex"""
+    _fields_ = [("b_chroma_me", _c.c_int32), ("chroma_format", _c.c_int32), ("mvy_offset", _c.c_int32),
+                ("weight", Weight * 3), ("fenc_chroma", _c.c_void_p * 2), ("fenc_chroma_stride", _c.c_ssize_t),
+                ("fenc_chroma_frame_stride", _c.c_ssize_t), ("ref_chroma", _c.c_void_p * 8),
+                ("ref_chroma_stride", _c.c_ssize_t), ("ref_chroma_frame_stride", _c.c_ssize_t)]
+
+
+def refine_ext(b_chroma_me=0, chroma_format=1, mvy_offset=0, weights=(None, None, None), fenc_chroma=(),
+               fenc_chroma_origin=0, fenc_chroma_stride=0, ref_chroma=(), ref_chroma_origin=0, ref_chroma_stride=0):
+    """the x264hip_refine_ext_t of me_refine_subpel(ext=...): weights[p] = (scale, denom, offset)
+    or None (m->weight[0..2]); fenc_chroma = [NV12 / NV16 tensor] or [U, V] (4:4:4), ref_chroma =
+    [NV12 / NV16 tensor] or the F, H, V, C tensors of U then V ([n, rows, stride] each, the
+    chroma (0,0) at *_origin).  Frame strides are the tensors' own."""
+    e = RefineExt()
+    e.b_chroma_me, e.chroma_format, e.mvy_offset = int(b_chroma_me), int(chroma_format), int(mvy_offset)
+    for k, w in enumerate(weights):
+        if w is not None:
+            e.weight[k] = Weight(1, *[int(v) for v in w])
+    for k, t in enumerate(fenc_chroma):
+        e.fenc_chroma[k] = _ptr(t, fenc_chroma_origin).value
+    for k, t in enumerate(ref_chroma):
+        e.ref_chroma[k] = _ptr(t, ref_chroma_origin).value
+    e.fenc_chroma_stride, e.ref_chroma_stride = fenc_chroma_stride, ref_chroma_stride
+    if fenc_chroma:
+        e.fenc_chroma_frame_stride = _frame_stride(*fenc_chroma)
+    if ref_chroma:
+        e.ref_chroma_frame_stride = _frame_stride(*ref_chroma)
+    e._keep = (tuple(fenc_chroma), tuple(ref_chroma))    # the tensors outlive the call
+    return e
+
+
 def me_refine_subpel(fenc, fenc_origin, fenc_stride, planes, ref_origin, ref_stride, i_pixel, subme, pos, par,
                      init_cost, cost_mv_center, refine_qpel=False, fpel_satd=False, out=None, fenc_frame_stride=None,
-                     ref_frame_stride=None, nevals=None):
-    """refine_subpel (encoder/me.c:865-992) of n partitions (x264hip_*_me_refine_subpel): planes =
-    [F, H, V, C] tensors of the references (hpel_filter's), pos int32 [n, 3] = (frame, x, y), par
-    int16 [n, 8] = (mvx, mvy, mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel x, y), init_cost int32
-    [n]; returns int32 [n, 4] = (cost, mvx, mvy, cost_mv).  nevals: optional int32 [n] receiving
-    the reference's cmp calls per partition (SADs | SATDs << 16)."""
+                     ref_frame_stride=None, nevals=None, ext=None):
+    """refine_subpel (encoder/me.c:865-992) of n partitions (x264hip_*_me_refine_subpel, or _ex
+    with ext = refine_ext(...): chroma ME / weighted references): planes = [F, H, V, C] tensors
+    of the references (hpel_filter's), pos int32 [n, 3] = (frame, x, y), par int16 [n, 8] = (mvx,
+    mvy, mvp_x, mvp_y, mv_min_spel x, y, mv_max_spel x, y), init_cost int32 [n]; returns int32
+    [n, 4] = (cost, mvx, mvy, cost_mv).  nevals: optional int32 [n] receiving the reference's cmp
+    calls per partition (luma SADs | luma SATDs << 16 | chroma calls << 24)."""
     import torch
     bd = _pix_bd(fenc)
     n = pos.shape[0]
@@ -1181,13 +1214,19 @@ def me_refine_subpel(fenc, fenc_origin, fenc_stride, planes, ref_origin, ref_str
     ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
     rfs = ref_frame_stride if ref_frame_stride is not None else _frame_stride(*planes)
     cm, c0 = cost_mv_center
-    fn = getattr(lib(), f"x264hip_{bd}_me_refine_subpel")
-    fn.argtypes = [_P, _IP, _IP, _P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P,
-                   _c.c_int, _P, _P, _P]
+    args = [_ptr(fenc, fenc_origin), fenc_stride, ffs, *[_ptr(p, ref_origin) for p in planes], ref_stride, rfs,
+            i_pixel, subme, int(bool(refine_qpel)), int(bool(fpel_satd)), _ptr(pos), _ptr(par), _ptr(init_cost),
+            _ptr(cm, c0), n, _ptr(out), _ptr(nevals) if nevals is not None else None]
+    types = [_P, _IP, _IP, _P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P,
+             _c.c_int, _P, _P]
+    name = f"x264hip_{bd}_me_refine_subpel" + ("_ex" if ext is not None else "")
+    if ext is not None:
+        args.append(_c.byref(ext))
+        types.append(_P)
+    fn = getattr(lib(), name)
+    fn.argtypes = types + [_P]
     fn.restype = _c.c_int
-    _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, *[_ptr(p, ref_origin) for p in planes], ref_stride, rfs,
-           i_pixel, subme, int(bool(refine_qpel)), int(bool(fpel_satd)), _ptr(pos), _ptr(par), _ptr(init_cost),
-           _ptr(cm, c0), n, _ptr(out), _ptr(nevals) if nevals is not None else None, _stream()), "me_refine_subpel")
+    _rc(fn(*args, _stream()), name)
     return out
 
 

@@ -382,7 +382,8 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
                                     const typename PT<BD>::pixel *const planes[4], intptr_t rs, intptr_t rfs,
                                     int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
                                     const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int n,
-                                    int32_t *out, int32_t *nevals, hipStream_t stream );
+                                    int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *ext,
+                                    hipStream_t stream );
 template <int BD>
 hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int nmb, int me_range,
                                  const int16_t *origin, const int16_t *par, const int32_t *init_cost,

@@ -13,9 +13,22 @@
 // (satd_8x4, pixel.c:290-309, summed over tiles as PIXEL_SATD_C does); the group's tiles
 // meet through DPP adds and every lane of the segment reads the four candidate costs and
 // takes the reference's decisions itself (the packed bcost << 6 / << 4 codes, COPY*_IF_LT's
-// strict <, the odir skip), so the segment's lanes stay in step without LDS.  Luma only:
-// the chroma ME of b_chroma_me (me.c:833-861) is outside the hot path, as are the
-// multi-reference early exit (p_halfpel_thresh = NULL) and weighted references.
+// strict <, the odir skip), so the segment's lanes stay in step without LDS.  The
+// multi-reference early exit (p_halfpel_thresh) is the caller's (it is NULL here).
+//
+// The EXT forms add what x264's default preset runs on P slices (b_chroma_me at subme >= 5,
+// common/macroblock.c:507-509) and weighted references (m->weight, analyse.c:1248-1250):
+// every luma get_ref weighted by weight[0] (mc.c:235-242), and COST_MV_SATD's chroma branch
+// (me.c:833-861) -- U's cost added when the luma cost beats the running bcost, V's when the
+// sum still does.  A qpel diamond's four luma costs come first; a candidate whose luma cost
+// does not beat the step's starting bcost cannot win (bcost only falls within a step), so
+// the chroma pass runs only when some segment of the wave has such a candidate, and each
+// segment replays the reference's sequence over the full costs (the U / V calls counted as
+// the reference makes them).  4:2:0 / 4:2:2 (EXT 1): each group's eight lanes split the
+// candidate's chroma 4x4 blocks of both planes (one or two per lane), each lane rebuilding
+// mc_chroma (mc.c:252-283) for its block from the interleaved plane, weighting it and scoring
+// it with the 4x4 Hadamard (or SAD); 4:4:4 (EXT 2): the luma tile schedule over the U and V
+// hpel planes with get_ref and weight[1] / weight[2].
 #include "hipcommon.h"
 
 namespace x264hip {
@@ -29,13 +42,35 @@ static const uint8_t k_subpel_iterations[12][4] = { { 0, 0, 0, 0 }, { 1, 1, 0, 0
                                                     { 0, 0, 4, 10 }, { 0, 0, 4, 10 }, { 0, 0, 4, 10 },
                                                     { 0, 0, 4, 10 } };
 
-// the lane's 8x4 tile of get_ref( mvx, mvy ) scored against its fenc tile: SAD, or the sum of
-// |coef| of the tile's two 4x4 Hadamards (even; halved by the caller)
-template <int BD, bool SATD>
+// explicit weight of one plane (x264_weight_t, mc.c:117-137): rnd = 1 << (denom - 1) or 0,
+// offset already scaled by 1 << (BIT_DEPTH - 8)
+struct RsWeight
+{
+    int on, scale, denom, rnd, offset;
+};
+
+// mc_weight of packed pixels: clip( ((v * scale + rnd) >> denom) + offset ) per pixel
+template <int BD> __device__ __forceinline__ uint32_t weigh_packed( uint32_t w, const RsWeight &wt )
+{
+    constexpr int PPD = PT<BD>::PPD, SH = 32 / PPD;
+    uint32_t r = 0;
+#pragma unroll
+    for( int k = 0; k < PPD; k++ )
+    {
+        const int v = upix<BD>( w, k );
+        r |= (uint32_t)clip_pix<BD>( ((v * wt.scale + wt.rnd) >> wt.denom) + wt.offset ) << (SH * k);
+    }
+    return r;
+}
+
+// the lane's 8x4 tile of get_ref( mvx, mvy ) (weighted when WGT and wt.on) scored against its
+// fenc tile: SAD, or the sum of |coef| of the tile's two 4x4 Hadamards (even; halved by the
+// caller)
+template <int BD, bool SATD, bool WGT = false>
 __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD>::PPD],
                                                const typename PT<BD>::pixel *q0, const typename PT<BD>::pixel *q1,
                                                const typename PT<BD>::pixel *q2, const typename PT<BD>::pixel *q3,
-                                               intptr_t rs, int mvx, int mvy )
+                                               intptr_t rs, int mvx, int mvy, const RsWeight wt = {} )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD;
@@ -66,6 +101,13 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
             for( int k = 0; k < HDW; k++ )
                 r1[y][k] = avg_round<BD>( r1[y][k], r2[y][k] );
     }
+    if constexpr( WGT )
+        if( wt.on )
+#pragma unroll
+            for( int y = 0; y < 4; y++ )
+#pragma unroll
+                for( int k = 0; k < HDW; k++ )
+                    r1[y][k] = weigh_packed<BD>( r1[y][k], wt );
     if constexpr( SATD )
         return satd8x4_packed<BD>( fa, r1 );
     else
@@ -80,6 +122,71 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
     }
 }
 
+// 4x4 Hadamard sum |coef| >> 1 (satd_4x4, pixel.c:265-288) or SAD of a difference block
+__device__ __forceinline__ uint32_t block4_cost( const int (&d)[4][4], bool satd )
+{
+    uint32_t acc = 0;
+    if( !satd )
+    {
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+#pragma unroll
+            for( int x = 0; x < 4; x++ )
+                acc += (uint32_t)abs( d[y][x] );
+        return acc;
+    }
+    int t[4][4];
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+    {
+        const int a0 = d[y][0] + d[y][1], a1 = d[y][0] - d[y][1], a2 = d[y][2] + d[y][3], a3 = d[y][2] - d[y][3];
+        t[y][0] = a0 + a2; t[y][2] = a0 - a2; t[y][1] = a1 + a3; t[y][3] = a1 - a3;
+    }
+#pragma unroll
+    for( int x = 0; x < 4; x++ )
+    {
+        const int a0 = t[0][x] + t[1][x], a1 = t[0][x] - t[1][x], a2 = t[2][x] + t[3][x], a3 = t[2][x] - t[3][x];
+        acc += (uint32_t)(abs( a0 + a2 ) + abs( a0 - a2 ) + abs( a1 + a3 ) + abs( a1 - a3 ));
+    }
+    return acc >> 1;
+}
+
+// one 4x4 block of plane p of mc_chroma (mc.c:252-283) at chroma mv (mvx, mvyc) eighth-pels,
+// weighted by wt when on, scored against the lane's fenc block fb (row y: pixel x in packed
+// word x / PPD).  s = the interleaved plane at the block's top-left, plane p's sample.
+template <int BD>
+__device__ __forceinline__ uint32_t nv_block_cost( const typename PT<BD>::pixel *s, intptr_t rcs, int mvx, int mvyc,
+                                                   const uint32_t (&fb)[4][4 / PT<BD>::PPD],
+                                                   const RsWeight &wt, bool satd )
+{
+    constexpr int NDW = BD == 8 ? 3 : 5;    // the row's 5 samples of plane p, every other pixel from s
+    const int dx = mvx & 7, dy = mvyc & 7;
+    const int cA = (8 - dx) * (8 - dy), cB = dx * (8 - dy), cC = (8 - dx) * dy, cD = dx * dy;
+    s += (intptr_t)(mvyc >> 3) * rcs + (mvx >> 3) * 2;
+    int v[5][5];
+#pragma unroll
+    for( int r = 0; r < 5; r++ )
+    {
+        uint32_t w[NDW];
+        load_al_pad<NDW>( s + r * rcs, w );
+#pragma unroll
+        for( int x = 0; x < 5; x++ )
+            v[r][x] = BD == 8 ? (int)((w[x >> 1] >> (16 * (x & 1))) & 0xff) : (int)(w[x] & 0xffff);
+    }
+    int d[4][4];
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+#pragma unroll
+        for( int x = 0; x < 4; x++ )
+        {
+            int m = (cA * v[y][x] + cB * v[y][x + 1] + cC * v[y + 1][x] + cD * v[y + 1][x + 1] + 32) >> 6;
+            if( wt.on )
+                m = clip_pix<BD>( ((m * wt.scale + wt.rnd) >> wt.denom) + wt.offset );
+            d[y][x] = upix<BD>( fb[y][x / PT<BD>::PPD], x % PT<BD>::PPD ) - m;
+        }
+    return block4_cost( d, satd );
+}
+
 // the eight tiles of each group summed into the group's first lane (quad sums by quad_perm,
 // then row_ror:12 brings lane 8k+4's quad sum to lane 8k)
 __device__ __forceinline__ uint32_t group_sum( uint32_t v )
@@ -90,13 +197,24 @@ __device__ __forceinline__ uint32_t group_sum( uint32_t v )
     return v;
 }
 
-template <int BD, int IPIX, bool FSATD>
+// the EXT inputs of a launch (x264hip_refine_ext_t), by value in the kernel arguments
+template <int BD> struct RsExt
+{
+    const typename PT<BD>::pixel *fenc_c[2];   // NV12 / NV16 plane, or U, V: pixel (0,0) of frame 0
+    const typename PT<BD>::pixel *ref_c[8];    // NV12 / NV16 plane, or U's F, H, V, C then V's
+    intptr_t fcs, ffcs, rcs, rfcs;
+    int chroma, vs, mvy_offset;                // b_chroma_me, CHROMA_V_SHIFT, me.c:875's offset
+    RsWeight wt[3];                            // m->weight[0..2]
+};
+
+template <int BD, int IPIX, bool FSATD, int EXT>
 __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs, const typename PT<BD>::pixel *p0,
     const typename PT<BD>::pixel *p1, const typename PT<BD>::pixel *p2, const typename PT<BD>::pixel *p3,
     intptr_t rs, intptr_t rfs, int n, int hpel_iters, int qpel_iters, int subme, int refine_qpel,
     const int32_t *__restrict__ pos, const int16_t *__restrict__ par, const int32_t *__restrict__ init_cost,
-    const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out, int32_t *__restrict__ nevals )
+    const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out, int32_t *__restrict__ nevals,
+    const RsExt<BD> ext )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD;
@@ -120,6 +238,63 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
     const pixel *const q0 = p0 + qo, *const q1 = p1 + qo, *const q2 = p2 + qo, *const q3 = p3 + qo;
 
+    // ---- EXT: the weight of the luma get_ref, the lane's chroma blocks / tiles ----
+    const RsWeight wt0 = ext.wt[0];
+    const bool chroma = EXT && ext.chroma;                // launch-uniform
+    constexpr int CDW = 4 / PT<BD>::PPD;                  // packed words of a 4-pixel chroma row
+    const pixel *cref[2] = { nullptr, nullptr };          // EXT 1: the lane's blocks in the ref plane
+    uint32_t cfb[2][4][CDW] = {};                         //        and their fenc rows
+    int cpl[2] = { -1, -1 };                              //        plane (0 U, 1 V; -1 none)
+    uint32_t fu[4][HDW] = {}, fv[4][HDW] = {};            // EXT 2: the fenc tiles of U and V
+    const pixel *u0 = nullptr, *u1 = nullptr, *u2 = nullptr, *u3 = nullptr;   // and their hpel planes
+    const pixel *v0 = nullptr, *v1 = nullptr, *v2 = nullptr, *v3 = nullptr;   // (no arrays: scratch)
+    if constexpr( EXT == 1 )
+    {
+        if( chroma )
+        {
+            // chroma block cw x ch of the partition (luma2chroma_pixel, pixel.h:70-76) in 4x4
+            // blocks, U's then V's; lane u takes blocks u and u + 8
+            constexpr int CW = BW / 2, BXN = CW / 4;
+            const int ch = BH >> ext.vs, ncb = BXN * (ch / 4);
+            const intptr_t crow = by >> ext.vs;
+#pragma unroll
+            for( int k = 0; k < 2; k++ )
+            {
+                const int b = u + 8 * k;
+                if( b < 2 * ncb )
+                {
+                    const int p = b >= ncb, jb = b - p * ncb;
+                    const int cx = 4 * (jb % BXN), cy = 4 * (jb / BXN);
+                    cpl[k] = p;
+                    cref[k] = ext.ref_c[0] + f * ext.rfcs + (crow + cy) * ext.rcs + bx + 2 * cx + p;
+                    const pixel *fc = ext.fenc_c[0] + f * ext.ffcs + (crow + cy) * ext.fcs + bx + 2 * cx + p;
+#pragma unroll
+                    for( int y = 0; y < 4; y++ )
+#pragma unroll
+                        for( int x = 0; x < 4; x++ )
+                            cfb[k][y][x / PT<BD>::PPD] |= (uint32_t)fc[y * ext.fcs + 2 * x]
+                                                          << ((32 / PT<BD>::PPD) * (x % PT<BD>::PPD));
+                }
+            }
+        }
+    }
+    else if constexpr( EXT == 2 )
+    {
+        if( chroma )
+        {
+            const intptr_t fco = (intptr_t)f * ext.ffcs + (intptr_t)(by + uy) * ext.fcs + bx + ux;
+#pragma unroll
+            for( int y = 0; y < 4; y++ )
+            {
+                load_row_u<HDW>( ext.fenc_c[0] + fco + y * ext.fcs, fu[y] );
+                load_row_u<HDW>( ext.fenc_c[1] + fco + y * ext.fcs, fv[y] );
+            }
+            const intptr_t rco = (intptr_t)f * ext.rfcs + (intptr_t)(by + uy) * ext.rcs + bx + ux;
+            u0 = ext.ref_c[0] + rco; u1 = ext.ref_c[1] + rco; u2 = ext.ref_c[2] + rco; u3 = ext.ref_c[3] + rco;
+            v0 = ext.ref_c[4] + rco; v1 = ext.ref_c[5] + rco; v2 = ext.ref_c[6] + rco; v3 = ext.ref_c[7] + rco;
+        }
+    }
+
     const int16_t *p = par + 8 * j;
     const int mvpx = p[2], mvpy = p[3];
     const int minx = p[4], miny = p[5], maxx = p[6], maxy = p[7];
@@ -127,7 +302,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     int bmx = p[0], bmy = p[1];
     int bcost = init_cost[j];
     const bool qsatd = subme > 1;                         // mbcmp_unaligned (encoder.c:1411-1413)
-    int nsad = 0, nsatd = 0;                              // the reference's fpelcmp / mbcmp calls
+    int nsad = 0, nsatd = 0, nchroma = 0;                 // the reference's fpelcmp / mbcmp calls
     auto count = [&]( bool satd, int k ) {
         if( satd )
             nsatd += k;
@@ -144,8 +319,8 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         const int gy = g == 0 ? my[0] : g == 1 ? my[1] : g == 2 ? my[2] : my[3];
         uint32_t v = 0;
         if( tile )
-            v = satd ? tile_cost<BD, true>( fa, q0, q1, q2, q3, rs, gx, gy ) >> 1
-                     : tile_cost<BD, false>( fa, q0, q1, q2, q3, rs, gx, gy );
+            v = satd ? tile_cost<BD, true, EXT != 0>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 ) >> 1
+                     : tile_cost<BD, false, EXT != 0>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 );
         if( u == 0 )                                      // the group's mv cost, once
             v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
         v = group_sum( v );
@@ -158,6 +333,68 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         int c[4];
         eval4( m4x, m4y, satd, c );
         return c[0];
+    };
+    // the chroma costs (mbcmp: SATD for subme > 1) of the diamond of step st around (ox, oy) in
+    // the order (0, -st), (0, +st), (-st, 0), (+st, 0) -- st = 0: the centre in every group: U in
+    // cu, V in cv.  (The group's candidate by arithmetic: the selects of eval4 became an indexed
+    // scratch load here.)
+    auto evalc4 = [&]( int ox, int oy, int st, int (&cu)[4], int (&cv)[4] ) {
+        const int gx = ox + (g == 2 ? -st : g == 3 ? st : 0);
+        const int gy = oy + (g == 0 ? -st : g == 1 ? st : 0);
+        uint32_t vu = 0, vv = 0;
+        if constexpr( EXT == 1 )
+        {
+            const int mvyc = (2 * (gy + ext.mvy_offset)) >> ext.vs;
+#pragma unroll
+            for( int k = 0; k < 2; k++ )
+                if( cpl[k] >= 0 )
+                {
+                    const uint32_t c = nv_block_cost<BD>( cref[k], ext.rcs, gx, mvyc, cfb[k], ext.wt[1 + cpl[k]],
+                                                          qsatd );
+                    if( cpl[k] )
+                        vv += c;
+                    else
+                        vu += c;
+                }
+        }
+        else if constexpr( EXT == 2 )
+        {
+            if( tile )
+            {
+                if( qsatd )
+                {
+                    vu = tile_cost<BD, true, true>( fu, u0, u1, u2, u3, ext.rcs, gx, gy, ext.wt[1] ) >> 1;
+                    vv = tile_cost<BD, true, true>( fv, v0, v1, v2, v3, ext.rcs, gx, gy, ext.wt[2] ) >> 1;
+                }
+                else
+                {
+                    vu = tile_cost<BD, false, true>( fu, u0, u1, u2, u3, ext.rcs, gx, gy, ext.wt[1] );
+                    vv = tile_cost<BD, false, true>( fv, v0, v1, v2, v3, ext.rcs, gx, gy, ext.wt[2] );
+                }
+            }
+        }
+        vu = group_sum( vu );
+        vv = group_sum( vv );
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            cu[k] = (int)__shfl( (int)vu, sbase + 8 * k );
+            cv[k] = (int)__shfl( (int)vv, sbase + 8 * k );
+        }
+    };
+    // COST_MV_SATD's chroma branch (me.c:833-861) on a luma cost c against bcost
+    auto add_chroma = [&]( int c, int cu, int cv, int bc ) {
+        if( c < bc )
+        {
+            nchroma++;
+            c += cu;
+            if( c < bc )
+            {
+                nchroma++;
+                c += cv;
+            }
+        }
+        return c;
     };
 
     // halfpel diamond (me.c:885-923)
@@ -209,11 +446,19 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         bcost >>= 6;
     }
 
-    // the hpel winner re-scored with mbcmp when it differs from fpelcmp (me.c:925-929)
-    if( !refine_qpel && qsatd && !FSATD )
+    // the hpel winner re-scored with mbcmp when it differs from fpelcmp or chroma ME is on
+    // (me.c:925-929: bcost = COST_MAX, COST_MV_SATD)
+    if( !refine_qpel && ((qsatd && !FSATD) || chroma) )
     {
-        bcost = eval1( bmx, bmy, true );
-        count( true, 1 );
+        bcost = eval1( bmx, bmy, qsatd );
+        count( qsatd, 1 );
+        if constexpr( EXT != 0 )
+            if( chroma )
+            {
+                int cu[4], cv[4];
+                evalc4( bmx, bmy, 0, cu, cv );
+                bcost = add_chroma( bcost, cu[0], cv[0], 1 << 28 );
+            }
     }
 
     if( subme != 1 )
@@ -232,20 +477,33 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
             const int mx[4] = { omx, omx, omx - 1, omx + 1 }, my[4] = { omy - 1, omy + 1, omy, omy };
             int c[4];
             eval4( mx, my, qsatd, c );
+            int cu[4] = { 0, 0, 0, 0 }, cv[4] = { 0, 0, 0, 0 };
+            if constexpr( EXT != 0 )
+                if( chroma )
+                {
+                    // a candidate whose luma cost does not beat the step's starting bcost never wins
+                    bool need = false;
+#pragma unroll
+                    for( int d = 0; d < 4; d++ )
+                        need |= act && (refine_qpel || (d ^ 1) != odir) && c[d] < bcost;
+                    if( __any( need ) )
+                        evalc4( omx, omy, 1, cu, cv );
+                }
             if( act )
             {
 #pragma unroll
                 for( int d = 0; d < 4; d++ )
-                    if( (refine_qpel || (d ^ 1) != odir) )
-                        count( qsatd, 1 );
-#pragma unroll
-                for( int d = 0; d < 4; d++ )
-                    if( (refine_qpel || (d ^ 1) != odir) && c[d] < bcost )
+                    if( refine_qpel || (d ^ 1) != odir )
                     {
-                        bcost = c[d];
-                        bmx = mx[d];
-                        bmy = my[d];
-                        bdir = d;
+                        count( qsatd, 1 );
+                        const int cd = chroma ? add_chroma( c[d], cu[d], cv[d], bcost ) : c[d];
+                        if( cd < bcost )
+                        {
+                            bcost = cd;
+                            bmx = mx[d];
+                            bmy = my[d];
+                            bdir = d;
+                        }
                     }
                 if( bmx == omx && bmy == omy )
                     act = false;
@@ -278,7 +536,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     {
         *(int4 *)(out + 4 * j) = make_int4( bcost, bmx, bmy, (int)cmx[bmx] + (int)cmy[bmy] );
         if( nevals )
-            nevals[j] = nsad | (nsatd << 16);
+            nevals[j] = nsad | (nsatd << 16) | (nchroma << 24);
     }
 }
 
@@ -287,8 +545,10 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
                                     const typename PT<BD>::pixel *const planes[4], intptr_t rs, intptr_t rfs,
                                     int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
                                     const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int n,
-                                    int32_t *out, int32_t *nevals, hipStream_t stream )
+                                    int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *xe,
+                                    hipStream_t stream )
 {
+    using pixel = typename PT<BD>::pixel;
     if( n <= 0 )
         return hipSuccess;
     if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || ((uintptr_t)out & 15) )
@@ -297,15 +557,53 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
     const int qpel = k_subpel_iterations[subme][refine_qpel ? 1 : 3];
     // fpelcmp is SATD only under TESA with subme > 1 (encoder.c:1423-1426)
     const bool fs_satd = fpel_satd && subme > 1;
+    RsExt<BD> ext = {};
+    int mode = 0;
+    if( xe )
+    {
+        for( int k = 0; k < 3; k++ )
+        {
+            const x264hip_weight_t &w = xe->weight[k];
+            if( w.weighted && (w.denom < 0 || w.denom > 7) )
+                return hipErrorInvalidValue;
+            ext.wt[k] = { w.weighted ? 1 : 0, w.scale, w.weighted ? w.denom : 0,
+                          w.weighted && w.denom > 0 ? 1 << (w.denom - 1) : 0, w.offset * (1 << (BD - 8)) };
+        }
+        const int cf = xe->chroma_format;
+        if( xe->b_chroma_me )
+        {
+            if( cf < 1 || cf > 3 || !xe->fenc_chroma[0] || !xe->ref_chroma[0] ||
+                (cf == 3 && (!xe->fenc_chroma[1] || !xe->ref_chroma[1] || !xe->ref_chroma[2] ||
+                             !xe->ref_chroma[3] || !xe->ref_chroma[4] || !xe->ref_chroma[5] ||
+                             !xe->ref_chroma[6] || !xe->ref_chroma[7])) )
+                return hipErrorInvalidValue;
+            ext.chroma = 1;
+            ext.vs = cf == 1;
+            ext.mvy_offset = xe->mvy_offset;
+            for( int k = 0; k < 2; k++ )
+                ext.fenc_c[k] = (const pixel *)xe->fenc_chroma[k];
+            for( int k = 0; k < 8; k++ )
+                ext.ref_c[k] = (const pixel *)xe->ref_chroma[k];
+            ext.fcs = xe->fenc_chroma_stride;
+            ext.ffcs = xe->fenc_chroma_frame_stride;
+            ext.rcs = xe->ref_chroma_stride;
+            ext.rfcs = xe->ref_chroma_frame_stride;
+            mode = cf == 3 ? 2 : 1;
+        }
+        else if( ext.wt[0].on )
+            mode = 1;                                     // weighted luma, no chroma
+    }
     const int64_t segs = (int64_t)n;
     dim3 blk( 256 ), g( (unsigned)((segs * 32 + 255) / 256) );
-#define RS_GO( I, F )                                                                                             \
-    hipLaunchKernelGGL( ( me_refine_subpel_kernel<BD, I, F> ), g, blk, 0, stream, fenc, fs, ffs, planes[0],       \
+#define RS_GO( I, F, E )                                                                                          \
+    hipLaunchKernelGGL( ( me_refine_subpel_kernel<BD, I, F, E> ), g, blk, 0, stream, fenc, fs, ffs, planes[0],    \
                         planes[1], planes[2], planes[3], rs, rfs, n, hpel, qpel, subme, refine_qpel ? 1 : 0, pos,   \
-                        par, init_cost, cost_mv, out, nevals )
+                        par, init_cost, cost_mv, out, nevals, ext )
+#define RS_MODE( I, F )                                                                                           \
+    if( mode == 0 ) { RS_GO( I, F, 0 ); } else if( mode == 1 ) { RS_GO( I, F, 1 ); } else { RS_GO( I, F, 2 ); }
 #define RS_CASE( I )                                                                                              \
     case I:                                                                                                       \
-        if( fs_satd ) { RS_GO( I, true ); } else { RS_GO( I, false ); }                                           \
+        if( fs_satd ) { RS_MODE( I, true ); } else { RS_MODE( I, false ); }                                       \
         break;
     switch( i_pixel )
     {
@@ -313,6 +611,7 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
         default: return hipErrorInvalidValue;
     }
 #undef RS_CASE
+#undef RS_MODE
 #undef RS_GO
     return hipGetLastError();
 }
@@ -320,10 +619,10 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
 template hipError_t launch_me_refine_subpel<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *const[4],
                                                 intptr_t, intptr_t, int, int, int, int, const int32_t *,
                                                 const int16_t *, const int32_t *, const uint16_t *, int, int32_t *,
-                                                int32_t *, hipStream_t );
+                                                int32_t *, const x264hip_refine_ext_t *, hipStream_t );
 template hipError_t launch_me_refine_subpel<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *const[4],
                                                  intptr_t, intptr_t, int, int, int, int, const int32_t *,
                                                  const int16_t *, const int32_t *, const uint16_t *, int, int32_t *,
-                                                 int32_t *, hipStream_t );
+                                                 int32_t *, const x264hip_refine_ext_t *, hipStream_t );
 
 } // namespace x264hip
