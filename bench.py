@@ -473,6 +473,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
         r64 = rates_ssd(x, a, world, full[:a.tframes + 1], origin, stride, a.tframes)
         res.update({k.replace("ssd_plane", "ssd_plane_%d" % a.tframes): v for k, v in r64.items()})
     res.update(rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
+    res.update(rates_refine(x, a, world, mbw, mbh, F))
     res.update(rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
     res.update(r2160)
@@ -748,49 +749,96 @@ def rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     if not torch.equal(out_t, out_f):
         raise SystemExit("bench: fused and table ESA decisions disagree")
     del table, org
-    res.update(rates_refine(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, par, out_f, cm_d, span))
     return res
 
 
-def rates_refine(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, par, esa_out, cm_d, span):
-    """configs[2]'s "SATD_8x8 subpel refine" at full resolution: refine_subpel (me.c:865-992) of
-    every 16x16 MB of the F pairs as x264_me_search_ref runs it at subme 7 (x264's default: two
-    hpel diamonds of SAD over get_ref blocks, the SATD re-score, two qpel SATD diamonds), started
-    from the ESA decisions above (m->mv = 4 * the integer winner, m->cost its cost), mv limits of
-    analyse.c:336-349.  VALU fraction on the reference's own cmp calls (counted per MB by the
-    kernel, equal to the oracle's count in tests/test_gpu_refine.py): a SATD call costs SURVEY §8d's
-    444 + 192 lane-ops per 64 pixels, a SAD call 0.75 lane-op slots per pixel (a half-rate
-    v_sad_u8 per 4 absdiffs and a v_lerp_u8 per 4 qpel averages)."""
-    n = F * mbw * mbh
-    hv = x.hpel_filter(dev[:-1], origin, stride, mbw * 16, mbh * 16)
+def rates_refine(x, a, world, mbw, mbh, F):
+    """configs[2]'s "SATD_8x8 subpel refine" at full resolution, as x264's default preset runs it
+    on P slices: refine_subpel (me.c:865-992) at subme 7 (two hpel diamonds of SAD over get_ref
+    blocks, the SATD re-score, two qpel SATD diamonds) with b_chroma_me (common/macroblock.c:
+    507-509: COST_MV_SATD adds mc_chroma + SATD of U, then V, me.c:833-861) over F 1080p 4:2:0
+    pairs of synth.make_subpel_sequence, whose motion is (3.25, 2.5) pixels per frame -- the
+    optimum lies at quarter-pel positions, so the diamonds move.  Each partition starts from its
+    integer decision: the fused ESA winner of its MB (me_range 16 around mv 0; m->mv = 4 * the
+    winner, m->cost its SAD + mv cost, for 8x8 partitions the partition's own SAD there), mv
+    limits of analyse.c:336-349.  Legs: 16x16 with chroma ME (refine16_*), 16x16 luma only
+    (refine16_luma_*), 8x8 partitions with chroma ME (refine8_*).  VALU fraction on the
+    reference's own cmp calls (counted per partition by the kernel, equal to the oracle's count
+    in tests/test_gpu_refine*.py): a luma SATD call costs SURVEY §8d's 444 + 192 lane-ops per 64
+    pixels, a SAD call 0.75 lane-op slots per pixel (a half-rate v_sad_u8 per 4 absdiffs and a
+    v_lerp_u8 per 4 qpel averages), a chroma call the same SATD cost plus 9 lane-ops per pixel
+    for mc_chroma's bilinear tap."""
+    from x264hip import synth, dist as xd
+    W, H = mbw * 16, mbh * 16
+    p0, p1 = xd.frame_shard(world * F, world, int(os.environ.get("RANK", "0")))
+    luma, stride, origin, nv, cs, co = synth.make_subpel_sequence(p1 - p0 + 1, W, H, 8, start=p0)
+    dev = torch.from_numpy(luma).cuda()
+    nvd = torch.from_numpy(nv).cuda()
+    fstride = luma[0].size
+    del luma, nv
+    me_range = 16
+    par, init, cm, span = tesa_params(mbw, mbh, F, me_range, centre=(0, 0))
+    cm_d = torch.from_numpy(cm.view(np.int16)).cuda()
+    esa = torch.empty((F * mbw * mbh, 3), dtype=torch.int32, device="cuda")
+    x.me_search_esa(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, me_range, me_range,
+                    torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda(), (cm_d, span), out=esa,
+                    fenc_frame_stride=fstride, ref_frame_stride=fstride)
+    hv = x.hpel_filter(dev[:-1], origin, stride, W, H)
     planes = [dev[:-1]] + list(hv)
-    mb = np.arange(n) % (mbw * mbh)
-    mbx, mby = mb % mbw, mb // mbw
-    pos = np.stack([np.arange(n) // (mbw * mbh), 16 * mbx, 16 * mby], 1).astype(np.int32)
-    rpar = np.zeros((n, 8), np.int16)
-    rpar[:, 2:4] = par[:, 2:4]                                  # mvp (qpel)
-    rpar[:, 4], rpar[:, 5] = 4 * (-16 * mbx - 24), 4 * (-16 * mby - 24)
-    rpar[:, 6], rpar[:, 7] = 4 * (16 * (mbw - 1 - mbx) + 24), 4 * (16 * (mbh - 1 - mby) + 24)
-    rpar_d = torch.from_numpy(rpar).cuda()
-    rpar_d[:, 0:2] = (esa_out[:, 1:3] * 4).to(torch.int16)      # m->mv = the integer winner, qpel
-    init = esa_out[:, 0].contiguous()
-    pos_d = torch.from_numpy(pos).cuda()
-    out = torch.empty((n, 4), dtype=torch.int32, device="cuda")
-    ne = torch.empty(n, dtype=torch.int32, device="cuda")
+    ext = x.refine_ext(1, 1, 0, fenc_chroma=[nvd[1:]], fenc_chroma_origin=co, fenc_chroma_stride=cs,
+                       ref_chroma=[nvd[:-1]], ref_chroma_origin=co, ref_chroma_stride=cs)
+    n1 = F * mbw * mbh
+    mb = np.arange(n1) % (mbw * mbh)
+    emv = esa[:, 1:3].cpu().numpy().astype(np.int64)
+    res = {"refine_workload": "1080p 4:2:0 make_subpel_sequence, motion (3.25, 2.5) px/frame, subme 7, "
+                              "b_chroma_me on (refine16_luma_*: off), starts at the fused-ESA winners"}
+    for leg, i_pixel, chroma in (("refine16", 0, True), ("refine16_luma", 0, False), ("refine8", 3, True)):
+        parts = rc_parts = [(0, 0)] if i_pixel == 0 else [(0, 0), (8, 0), (0, 8), (8, 8)]
+        k = len(parts)
+        n = n1 * k
+        j = np.repeat(np.arange(n1), k)
+        ox = np.tile([p[0] for p in rc_parts], n1)
+        oy = np.tile([p[1] for p in rc_parts], n1)
+        mbx, mby = mb[j] % mbw, mb[j] // mbw
+        pos = np.stack([j // (mbw * mbh), 16 * mbx + ox, 16 * mby + oy], 1).astype(np.int32)
+        rpar = np.zeros((n, 8), np.int16)
+        rpar[:, 0], rpar[:, 1] = 4 * emv[j, 0], 4 * emv[j, 1]
+        rpar[:, 4], rpar[:, 5] = 4 * (-16 * mbx - 24), 4 * (-16 * mby - 24)
+        rpar[:, 6], rpar[:, 7] = 4 * (16 * (mbw - 1 - mbx) + 24), 4 * (16 * (mbh - 1 - mby) + 24)
+        if i_pixel == 0:
+            init_d = esa[:, 0].contiguous()
+        else:                                       # the partition's SAD at the winner + its mv cost
+            fo = torch.from_numpy(((pos[:, 0] + 1) * fstride + origin + pos[:, 2] * stride + pos[:, 1])
+                                  .astype(np.int64)).cuda()
+            ro = torch.from_numpy((pos[:, 0] * fstride + origin + (pos[:, 2] + emv[j, 1]) * stride + pos[:, 1]
+                                   + emv[j, 0]).astype(np.int64)).cuda()
+            sad = x.pixel_cmp_batch(0, i_pixel, dev, stride, dev, stride, fo, ro)
+            mvc = cm[span + 4 * emv[j, 0]].astype(np.int64) + cm[span + 4 * emv[j, 1]]
+            init_d = (sad + torch.from_numpy(mvc.astype(np.int32)).cuda()).int().contiguous()
+        rpar_d = torch.from_numpy(rpar).cuda()
+        pos_d = torch.from_numpy(pos).cuda()
+        out = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+        ne = torch.empty(n, dtype=torch.int32, device="cuda")
 
-    def step():
-        x.me_refine_subpel(dev[1:], origin, stride, planes, origin, stride, x.PIXEL_16x16, 7, pos_d, rpar_d, init,
-                           (cm_d, span), out=out, fenc_frame_stride=fstride, ref_frame_stride=fstride, nevals=ne)
-    wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
-    nsad = int((ne & 0xFFFF).sum().item())
-    nsatd = int((ne >> 16).sum().item())
-    work = nsad * 256 * 0.75 + nsatd * 256 * (444 + 192) / 64
-    moved = (out[:, 1:3] != rpar_d[:, 0:2].int()).any(1).float().mean().item()
-    del hv, planes
-    return {"refine16_mbs_per_s": world * a.steps * n / wall, "refine16_launch_ms": ev_ms,
-            "refine16_mbs_per_launch": n, "refine16_sad_calls_per_mb": nsad / n,
-            "refine16_satd_calls_per_mb": nsatd / n, "refine16_moved_frac": moved,
-            "refine16_valu_frac": work / (ev_ms * 1e-3) / VALU_LANE_OPS}
+        def step(i_pixel=i_pixel, pos_d=pos_d, rpar_d=rpar_d, init_d=init_d, out=out, ne=ne, chroma=chroma):
+            x.me_refine_subpel(dev[1:], origin, stride, planes, origin, stride, i_pixel, 7, pos_d, rpar_d, init_d,
+                               (cm_d, span), out=out, fenc_frame_stride=fstride, ref_frame_stride=fstride,
+                               nevals=ne, ext=ext if chroma else None)
+        wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
+        nsad = int((ne & 0xFFFF).sum().item())
+        nsatd = int(((ne >> 16) & 0xFF).sum().item())
+        nchroma = int((ne >> 24).sum().item())
+        px = 256 if i_pixel == 0 else 64
+        work = nsad * px * 0.75 + nsatd * px * (444 + 192) / 64 + nchroma * (px // 4) * ((444 + 192) / 64 + 9)
+        moved = (out[:, 1:3] != rpar_d[:, 0:2].int()).any(1).float().mean().item()
+        qpel = ((out[:, 1:3] & 1) != 0).any(1).float().mean().item()
+        res.update({leg + "_partitions_per_s": world * a.steps * n / wall, leg + "_launch_ms": ev_ms,
+                    leg + "_partitions_per_launch": n, leg + "_sad_calls_per_part": nsad / n,
+                    leg + "_satd_calls_per_part": nsatd / n, leg + "_chroma_calls_per_part": nchroma / n,
+                    leg + "_moved_frac": moved, leg + "_qpel_frac": qpel,
+                    leg + "_valu_frac": work / (ev_ms * 1e-3) / VALU_LANE_OPS})
+    del hv, planes, dev, nvd
+    return res
 
 
 def rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, bd=8):

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Run bench.py side legs alone on the bench's 16-pair 1080p workload (for rocprofv3 trace /
 PMC passes and A/Bs): leg_time.py LEG [steps] [pairs] with LEG one of esa (the ESA table and
-fused legs, then refine_subpel chained from the ESA decisions), full8 (the quadrant tables),
+fused legs), refine (refine_subpel with chroma ME on the quarter-pel sequence), full8 (the quadrant tables),
 tesa, la (the lookahead's P and B searches), wp (the weight search), me10 (configs[4]'s 10-bit
 full search, quadrant tables and 8x8 DCT+quant).  Prints the legs' JSON."""
 import json
@@ -31,6 +31,8 @@ def main():
     fs = planes[0].size
     if leg == "esa":
         res = bench.rates_esa(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
+    elif leg == "refine":
+        res = bench.rates_refine(x, a, 1, mbw, mbh, F)
     elif leg == "full8":
         res = bench.rates_full8(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
     elif leg == "tesa":

@@ -60,3 +60,57 @@ def random_planes(nframes, width, height, bitdepth=8, pad=PAD, seed=7):
     dt = np.uint8 if bitdepth == 8 else np.uint16
     out = rng.integers(0, 1 << bitdepth, size=(nframes, height + 2 * pad, stride)).astype(dt)
     return out, stride, pad * stride + pad
+
+
+def _smooth_field(rng, K, fmax):
+    """K random cosine components (fx, fy in cycles/pixel, phase, amplitude ~ 1/f)"""
+    f = rng.uniform(0.01, fmax, size=(K, 2)) * rng.choice([-1, 1], size=(K, 2))
+    ph = rng.uniform(0, 2 * np.pi, size=K)
+    amp = 1.0 / np.hypot(f[:, 0], f[:, 1])
+    return f, ph, amp / amp.sum()
+
+
+def _eval_field(field, xs, ys):
+    """sum_i amp_i cos(2 pi (fx_i x + fy_i y) + ph_i) on the grid ys x xs (separable: two outer
+    products per component)"""
+    f, ph, amp = field
+    out = np.zeros((len(ys), len(xs)))
+    for (fx, fy), p, a in zip(f, ph, amp):
+        ax, by = 2 * np.pi * fx * xs, 2 * np.pi * fy * ys + p
+        out += a * (np.outer(np.cos(by), np.cos(ax)) - np.outer(np.sin(by), np.sin(ax)))
+    return out
+
+
+def make_subpel_sequence(nframes, width, height, bitdepth=8, pad=PAD, seed=3, start=0, motion=(13, 10)):
+    """A 4:2:0 sequence with quarter-pel motion, for the subpel refine legs: frame k samples a
+    smooth random field (24 cosine components up to 0.22 cycles/pixel) displaced by k * motion
+    quarter pixels (default (3.25, 2.5) pixels per frame), plus +-1 noise (seed k); its chroma
+    samples two fields of their own at half resolution with the same motion (k * motion eighth
+    pixels of chroma) and is stored interleaved (NV12, x264's fenc->plane[1] layout) with 16
+    rows and 16 chroma pixels (32 elements) of edge replication (x264's 4:2:0 chroma padding).
+    Returns (luma[nframes, h+2pad, stride], stride, origin, nv12[nframes, h/2+32, cstride],
+    cstride, corigin)."""
+    pmax = (1 << bitdepth) - 1
+    rng = np.random.Generator(np.random.PCG64(seed))
+    fields = [_smooth_field(rng, 24, 0.22) for _ in range(3)]
+    stride = plane_stride(width, pad)
+    cw, ch, cpad = width // 2, height // 2, 16
+    cstride = (2 * cw + 4 * cpad + 63) // 64 * 64
+    dt = np.uint8 if bitdepth == 8 else np.uint16
+    luma = np.zeros((nframes, height + 2 * pad, stride), dt)
+    nv = np.zeros((nframes, ch + 2 * cpad, cstride), dt)
+    for i in range(nframes):
+        k = start + i
+        nrng = np.random.Generator(np.random.PCG64(2000 + k))
+        dx, dy = k * motion[0] / 4.0, k * motion[1] / 4.0
+        y = _eval_field(fields[0], np.arange(width) + dx, np.arange(height) + dy)
+        y = np.clip(np.floor((0.5 + 1.6 * y) * pmax + 0.5) + nrng.integers(-1, 2, size=y.shape), 0, pmax)
+        luma[i] = np.pad(y, ((pad, pad), (pad, stride - width - pad)), mode="edge").astype(dt)
+        planes = []
+        for p in (1, 2):
+            c = _eval_field(fields[p], np.arange(cw) + dx / 2, np.arange(ch) + dy / 2)
+            c = np.clip(np.floor((0.5 + 1.2 * c) * pmax + 0.5) + nrng.integers(-1, 2, size=c.shape), 0, pmax)
+            planes.append(np.pad(c, ((cpad, cpad), (cpad, cpad)), mode="edge"))
+        nv[i, :, 0:2 * (cw + 2 * cpad):2] = planes[0]
+        nv[i, :, 1:2 * (cw + 2 * cpad):2] = planes[1]
+    return luma, stride, pad * stride + pad, nv, cstride, cpad * cstride + 2 * cpad
