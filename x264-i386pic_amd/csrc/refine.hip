@@ -3,10 +3,10 @@
 // (me.c:791-797, hpel / qpel iterations of subpel_iterations[subme][2..3], me.c:38-50) or
 // x264_me_refine_qpel runs on a winner (me.c:801-810, [0..1]).
 //
-// One 32-lane segment per partition, two partitions per wave: four groups of eight lanes, a
-// lane per 8x4 tile of the partition (16x16: eight tiles; 16x8 / 8x16: four; 8x8: two).
-// A step that scores four candidates (the hpel diamond of fpelcmp_x4, the qpel diamond of
-// COST_MV_SATD) gives group g candidate g; a one-candidate step (the predictor's subpel
+// One segment of 4 * NT lanes per partition, NT = its 8x4 tiles (16x16: eight, 16x8 / 8x16:
+// four, 8x8: two), so a wave holds 2, 4 or 8 partitions: four groups of NT lanes, a lane per
+// tile.  A step that scores four candidates (the hpel diamond of fpelcmp_x4, the qpel diamond
+// of COST_MV_SATD) gives group g candidate g; a one-candidate step (the predictor's subpel
 // component, the SATD re-score of the hpel winner) runs the same candidate in every group.
 // Each lane rebuilds get_ref (mc.c:221-249: the plane pair of x264_hpel_ref0/1 and the
 // rounding average) for its tile and scores it with SAD or the packed 8x4 SATD
@@ -187,13 +187,15 @@ __device__ __forceinline__ uint32_t nv_block_cost( const typename PT<BD>::pixel 
     return block4_cost( d, satd );
 }
 
-// the eight tiles of each group summed into the group's first lane (quad sums by quad_perm,
-// then row_ror:12 brings lane 8k+4's quad sum to lane 8k)
-__device__ __forceinline__ uint32_t group_sum( uint32_t v )
+// the NT tiles of each group summed into the group's first lane (pair sums, quad sums by
+// quad_perm, then for NT = 8 row_ror:12 brings lane 8k+4's quad sum to lane 8k)
+template <int NT> __device__ __forceinline__ uint32_t group_sum( uint32_t v )
 {
     v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0xB1, 0xF, 0xF, false );
-    v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0x4E, 0xF, 0xF, false );
-    v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0x12C, 0xF, 0xF, false );
+    if constexpr( NT >= 4 )
+        v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0x4E, 0xF, 0xF, false );
+    if constexpr( NT >= 8 )
+        v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0x12C, 0xF, 0xF, false );
     return v;
 }
 
@@ -220,14 +222,14 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     constexpr int HDW = 8 / PT<BD>::PPD;
     constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TX = BW / 8, NT = TX * (BH / 4);
     const int lane = (int)(threadIdx.x & 63);
-    const int sbase = lane & 32;                          // the segment's first lane
-    const int g = (lane >> 3) & 3, u = lane & 7;
-    const int64_t jo = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 5;
+    constexpr int SL = 4 * NT, SH = NT == 8 ? 5 : NT == 4 ? 4 : 3;   // segment lanes, log2
+    const int sbase = lane & (64 - SL);                   // the segment's first lane
+    const int g = (lane / NT) & 3, u = lane & (NT - 1);
+    const int64_t jo = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> SH;
     const bool live = jo < n;                             // segment-uniform
     const int64_t j = live ? jo : n - 1;                  // a spare segment repeats the last job
-    const bool tile = u < NT;
-    const int tu = tile ? u : 0;
-    const int ux = 8 * (tu % TX), uy = 4 * (tu / TX);
+    constexpr bool tile = true;                           // every lane holds a tile
+    const int ux = 8 * (u % TX), uy = 4 * (u / TX);
     const int f = pos[3 * j], bx = pos[3 * j + 1], by = pos[3 * j + 2];
 
     uint32_t fa[4][HDW];
@@ -253,14 +255,14 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         if( chroma )
         {
             // chroma block cw x ch of the partition (luma2chroma_pixel, pixel.h:70-76) in 4x4
-            // blocks, U's then V's; lane u takes blocks u and u + 8
+            // blocks, U's then V's (at most 4 * NT of them); lane u takes blocks u and u + NT
             constexpr int CW = BW / 2, BXN = CW / 4;
             const int ch = BH >> ext.vs, ncb = BXN * (ch / 4);
             const intptr_t crow = by >> ext.vs;
 #pragma unroll
             for( int k = 0; k < 2; k++ )
             {
-                const int b = u + 8 * k;
+                const int b = u + NT * k;
                 if( b < 2 * ncb )
                 {
                     const int p = b >= ncb, jb = b - p * ncb;
@@ -323,10 +325,10 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
                      : tile_cost<BD, false, EXT != 0>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 );
         if( u == 0 )                                      // the group's mv cost, once
             v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
-        v = group_sum( v );
+        v = group_sum<NT>( v );
 #pragma unroll
         for( int k = 0; k < 4; k++ )
-            c[k] = (int)__shfl( (int)v, sbase + 8 * k );
+            c[k] = (int)__shfl( (int)v, sbase + NT * k );
     };
     auto eval1 = [&]( int mx, int my, bool satd ) {
         const int m4x[4] = { mx, mx, mx, mx }, m4y[4] = { my, my, my, my };
@@ -373,13 +375,13 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
                 }
             }
         }
-        vu = group_sum( vu );
-        vv = group_sum( vv );
+        vu = group_sum<NT>( vu );
+        vv = group_sum<NT>( vv );
 #pragma unroll
         for( int k = 0; k < 4; k++ )
         {
-            cu[k] = (int)__shfl( (int)vu, sbase + 8 * k );
-            cv[k] = (int)__shfl( (int)vv, sbase + 8 * k );
+            cu[k] = (int)__shfl( (int)vu, sbase + NT * k );
+            cv[k] = (int)__shfl( (int)vv, sbase + NT * k );
         }
     };
     // COST_MV_SATD's chroma branch (me.c:833-861) on a luma cost c against bcost
@@ -593,8 +595,9 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
         else if( ext.wt[0].on )
             mode = 1;                                     // weighted luma, no chroma
     }
-    const int64_t segs = (int64_t)n;
-    dim3 blk( 256 ), g( (unsigned)((segs * 32 + 255) / 256) );
+    // 4 * (the partition's 8x4 tiles) lanes per partition (me_refine_subpel_kernel's segments)
+    const int64_t lanes = (int64_t)n * 4 * (pix_w( i_pixel ) / 8) * (pix_h( i_pixel ) / 4);
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
 #define RS_GO( I, F, E )                                                                                          \
     hipLaunchKernelGGL( ( me_refine_subpel_kernel<BD, I, F, E> ), g, blk, 0, stream, fenc, fs, ffs, planes[0],    \
                         planes[1], planes[2], planes[3], rs, rfs, n, hpel, qpel, subme, refine_qpel ? 1 : 0, pos,   \
