@@ -236,7 +236,8 @@ def main():
     absdiff_per_launch = F * mbw * mbh * cand_per_mb * 256
     achieved = absdiff_per_launch / (ev_ms * 1e-3)
     roof = {
-        "kernel": "me_full_sad16_v7_kernel<%d, 2>" % R,
+        # the launched template: <range, table pitch in dwords> (me.hip launch_me_full)
+        "kernel": "me_full_sad16_v7_kernel<%d, %d>" % (R, x.me_table_pitch(R) // 4),
         "bound": "valu",
         "achieved": achieved / 1e12,
         "peak": SAD_PEAK_ABSDIFF / 1e12,

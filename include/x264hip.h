@@ -1001,7 +1001,10 @@ int x264hip_##BD##_weight_cost_batch( int kind, const pixel *fenc, const pixel *
  * X264_WEIGHTP_FAKE).  Writes weights[3] (fenc->weight[0][0..2]), *cost_delta                   \
  * (fenc->f_weighted_cost_delta[i_delta_index], FAKE only, may be NULL) and, in the lookahead    \
  * with a luma weight, weighted_lowres (fenc->weighted[0]: at (0,0), lowres_stride, 32-pixel     \
- * border; NULL = skip) by x264_weight_scale_plane.  Synchronous: every candidate of a plane    \
+ * border; NULL = skip) by x264_weight_scale_plane over columns [-32, width + 32) and the rows    \
+ * of the 32-row border: the reference starts at buffer_lowres (-PADH_ALIGN, i.e. -64 at 8 bit,   \
+ * slicetype.c:489-497), so columns [-PADH_ALIGN, -32), which no lowres search reads, keep       \
+ * whatever the caller's buffer held.  Synchronous: every candidate of a plane                   \
  * is scored in one batch on the stream and the host replays the reference's search over the   \
  * costs (one stream synchronise for luma, one for chroma); not capturable. */                  \
 int x264hip_##BD##_weights_analyse( const pixel *fenc_lowres, const pixel *const ref_lowres[4], \

@@ -708,19 +708,17 @@ static float c_ssim_end4( int sum0[5][4], int sum1[5][4], int width )
 }
 
 // ssd_nv12_core (pixel.c:128-151; x264_pixel_ssd_nv12 hands it the width & ~7 core of whole
-// chroma planes): both interleaved regions staged into a per-thread pinned buffer that
-// grows to the largest region seen, then the plane SSD kernel's NV12 form
+// chroma planes): both interleaved regions staged into a per-thread pinned buffer that grows to
+// the largest region seen, copied to a device buffer of the same size in one hipMemcpyAsync (the
+// kernel then reads HBM, not the host link), then the plane SSD kernel's NV12 form.  (No
+// destructor, as LaStatus: a thread-exit destructor can run after the HIP runtime is torn
+// down; the buffers live as long as the thread's process.)
 namespace {
 struct BigStage
 {
     int device = -1;
     uint8_t *host = nullptr, *dev = nullptr;
     size_t size = 0;
-    ~BigStage()
-    {
-        if( host )
-            (void)hipHostFree( host );
-    }
 };
 thread_local BigStage t_big;
 }
@@ -741,15 +739,19 @@ static void c_ssd_nv12_core( typename PT<BD>::pixel *p1, intptr_t s1, typename P
     {
         if( t_big.host )
             CHECK_FATAL( hipHostFree( t_big.host ) );
-        t_big.host = nullptr;
+        if( t_big.dev )
+            (void)hipFree( t_big.dev );         // (a buffer of the previous device: freed where it lives)
+        t_big.host = t_big.dev = nullptr;
+        t_big.size = 0;
         CHECK_FATAL( hipHostMalloc( (void **)&t_big.host, need, hipHostMallocDefault ) );
-        CHECK_FATAL( hipHostGetDevicePointer( (void **)&t_big.dev, t_big.host, 0 ) );
+        CHECK_FATAL( hipMalloc( (void **)&t_big.dev, need ) );
         t_big.size = need;
         t_big.device = c.device;
     }
     pixel *a = (pixel *)t_big.host, *b = (pixel *)(t_big.host + plane);
     stage_block( a, p1, s1, 2 * width, height );
     stage_block( b, p2, s2, 2 * width, height );
+    CHECK_FATAL( hipMemcpyAsync( t_big.dev, t_big.host, 2 * plane, hipMemcpyHostToDevice, c.stream ) );
     uint64_t *out = (uint64_t *)(c.host + ST_SC);
     CHECK_FATAL( launch_plane_ssd<BD>( 1, (const pixel *)t_big.dev, 2 * width, 0,
                                        (const pixel *)(t_big.dev + plane), 2 * width, 0, width, height, 1,

@@ -878,6 +878,9 @@ __device__ __forceinline__ void lr_helper( const typename PT<BD>::pixel *const (
     const int r = 8 * y0 - 16 + (int)(threadIdx.x & 63);
     const int yb = min( max( r >> 3, y0 ), y1 - 1 );
     const bool in_band = r >= 8 * y0 && r < 8 * y1;
+    // rows past the band's reach stay unread: a one-row last band (y0 = mbh - 1) would otherwise
+    // read up to row 8 * mbh + 39, past the 32-row padding of the plane's last frame
+    const bool in_reach = r < 8 * y1 + 16;
     uint32_t acc = 0;
     int done = t0 - 1;
     for( int it = 0; it < poll_max; it++ )
@@ -891,9 +894,10 @@ __device__ __forceinline__ void lr_helper( const typename PT<BD>::pixel *const (
             done++;
             const int x = min( max( mbw - 1 - (done - 2 * (s1 - 1 - yb)), 0 ), mbw - 1 );
             const intptr_t o = (intptr_t)r * stride + ((8 * x - 24) & ~(4 / (int)sizeof( typename PT<BD>::pixel ) - 1));
+            if( in_reach )
 #pragma unroll
-            for( int k = 0; k < NP; k++ )
-                acc += *(const uint32_t *)(pl[k] + o);
+                for( int k = 0; k < NP; k++ )
+                    acc += *(const uint32_t *)(pl[k] + o);
             if( in_band )
                 acc += *(const uint32_t *)(fenc + (intptr_t)r * stride + 8 * x);
         }
@@ -1388,7 +1392,11 @@ struct LaStatus
     hipEvent_t ev = nullptr;
     bool pending = false;            // a copy of the word is queued behind a launch
 };
-thread_local LaStatus t_la_status;
+// one slot per device, allocated on the device's first use and kept: a thread that alternates
+// between devices keeps each device's word (and a timeout recorded on it) instead of trading
+// one for the other
+constexpr int LA_MAX_DEVICES = 64;
+thread_local LaStatus t_la_status[LA_MAX_DEVICES];
 
 // the status word of the stream's device for this thread (allocated on first use)
 hipError_t la_status_get( hipStream_t stream, LaStatus **out )
@@ -1397,17 +1405,14 @@ hipError_t la_status_get( hipStream_t stream, LaStatus **out )
     hipError_t e = stream_device( stream, &d );
     if( e != hipSuccess )
         return e;
-    LaStatus &st = t_la_status;
+    if( d < 0 || d >= LA_MAX_DEVICES )
+        return hipErrorInvalidDevice;
+    LaStatus &st = t_la_status[d];
     if( st.device != d )
     {
         int cur = 0;
         if( (e = hipGetDevice( &cur )) != hipSuccess || (cur != d && (e = hipSetDevice( d )) != hipSuccess) )
             return e;
-        st.dev = nullptr;                 // (the old device's words are abandoned, not freed)
-        st.host = nullptr;
-        st.ev = nullptr;
-        st.pending = false;
-        st.device = -1;
         e = hipMalloc( (void **)&st.dev, sizeof( uint32_t ) );
         if( e == hipSuccess )
             e = hipMemset( st.dev, 0, sizeof( uint32_t ) );
@@ -1418,8 +1423,19 @@ hipError_t la_status_get( hipStream_t stream, LaStatus **out )
         if( cur != d )
             (void)hipSetDevice( cur );
         if( e != hipSuccess )
+        {
+            // (a partial allocation is released; the slot stays unset and is retried)
+            if( st.dev )
+                (void)hipFree( st.dev );
+            if( st.host )
+                (void)hipHostFree( st.host );
+            st.dev = nullptr;
+            st.host = nullptr;
+            st.ev = nullptr;
             return e;
+        }
         *st.host = 0;
+        st.pending = false;
         st.device = d;
     }
     *out = &st;
@@ -1461,9 +1477,13 @@ hipError_t la_status_begin( hipStream_t stream, uint32_t **word )
 // after the kernel: queue the word's copy behind it (not under capture)
 hipError_t la_status_end( hipStream_t stream )
 {
-    LaStatus &st = t_la_status;
+    LaStatus *stp = nullptr;
+    hipError_t e = la_status_get( stream, &stp );
+    if( e != hipSuccess )
+        return e;
+    LaStatus &st = *stp;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    hipError_t e = hipStreamIsCapturing( stream, &cs );
+    e = hipStreamIsCapturing( stream, &cs );
     if( e != hipSuccess || cs != hipStreamCaptureStatusNone )
         return e;
     e = hipMemcpyAsync( st.host, st.dev, sizeof( uint32_t ), hipMemcpyDeviceToHost, stream );
@@ -1554,7 +1574,7 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
         return e;
     // block rows per single-wave workgroup: a step costs the slowest of a wave's row
     // searches (the lanes run in lockstep), so fewer rows per wave means less divergence; 4
-    // measured best (15 1080p pairs, tools/la_band.py: P 2.46 / 2.32 / 2.19 / 2.26 ms,
+    // measured best (15 1080p pairs, round-2 band sweep, profiles/r02e_la_band.json: P 2.46 / 2.32 / 2.19 / 2.26 ms,
     // B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2 rows)
     constexpr int brows = 4;
     constexpr int brows4 = brows;                // a wave holds four roles of <= 4 rows
@@ -1597,7 +1617,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
         return e;
     // block rows per single-wave workgroup: a step costs the slowest of a wave's row
     // searches (the lanes run in lockstep), so fewer rows per wave means less divergence; 4
-    // measured best (15 1080p pairs, tools/la_band.py: P 2.46 / 2.32 / 2.19 / 2.26 ms,
+    // measured best (15 1080p pairs, round-2 band sweep, profiles/r02e_la_band.json: P 2.46 / 2.32 / 2.19 / 2.26 ms,
     // B 5.42 / 5.11 / 4.65 / 4.80 ms for 16 / 8 / 4 / 2 rows)
     constexpr int brows = 4;
     constexpr int brows4 = brows;                // four groups of <= 4 rows per wave
