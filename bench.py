@@ -550,17 +550,39 @@ def rates_weightp(x, a, world, dev, origin, stride, mbw, mbh):
 
 
 def rates_ssim(x, a, world, dev, origin, stride, mbw, mbh):
-    """x264_pixel_ssim_wxh (pixel.c:690-714) over a whole 1080p frame pair as one call (the
-    encoder calls it per filtered band, encoder.c:2517-2528): frames per second including the
-    ordered float sum; per-frame input 2 x 1920 x 1088 bytes."""
+    """x264_pixel_ssim_wxh (pixel.c:690-714) of 1080p frame pairs: as the encoder calls it, once
+    per filtered MB-row band (encoder.c:2412-2420, 2516-2528; 68 bands per frame, each band's
+    float independent), batched by x264hip_*_ssim_bands -- one frame per launch (ssim_bands_*)
+    and every frame of the batch in one launch (ssim_bands_batch_*) -- and, beside it, the whole
+    frame as one x264_pixel_ssim_wxh call (ssim_*: one ordered float chain).  Frames per second
+    including the ordered float sums; per-frame input 2 x 1920 x 1088 bytes."""
     W, H = mbw * 16, mbh * 16
     cnt = [0]
+    F = dev.shape[0] - 1
+    hgt = min(H, a.height)
 
     def step():
         cnt[0] = x.ssim_wxh(dev[1], origin + 2, stride, dev[0], origin + 2, stride, W - 2, H)[1]
     wall, _ = timed(step, max(1, a.steps // 2), 2, world)
     n = max(1, a.steps // 2)
-    return {"ssim_frames_per_s": world * n / wall, "ssim_ms": wall / n * 1e3, "ssim_windows": cnt[0]}
+    res = {"ssim_frames_per_s": world * n / wall, "ssim_ms": wall / n * 1e3, "ssim_windows": cnt[0]}
+    bands = torch.from_numpy(x.ssim_encoder_bands(mbh, hgt)).cuda()
+    out1 = torch.empty((1, bands.shape[0]), dtype=torch.float32, device="cuda")
+    outb = torch.empty((F, bands.shape[0]), dtype=torch.float32, device="cuda")
+
+    def bstep():
+        x.ssim_bands(dev[1:2], origin + 2, stride, dev[0:1], origin + 2, stride, W - 2, bands, out=out1)
+
+    def fstep():
+        x.ssim_bands(dev[1:], origin + 2, stride, dev[:-1], origin + 2, stride, W - 2, bands, out=outb)
+    wall, ev_ms = timed(bstep, a.steps, a.warmup, world, graph=True)
+    res.update({"ssim_bands_frames_per_s": world * a.steps / wall, "ssim_bands_launch_ms": ev_ms,
+                "ssim_bands_per_frame": int(bands.shape[0])})
+    wall, ev_ms = timed(fstep, a.steps, a.warmup, world, graph=True)
+    res.update({"ssim_bands_batch_frames_per_s": world * a.steps * F / wall, "ssim_bands_batch_launch_ms": ev_ms,
+                "ssim_bands_batch_frames": F,
+                "ssim_bands_batch_hbm_frac": F * 2 * W * hgt / (ev_ms * 1e-3) / HBM_PEAK})
+    return res
 
 
 def rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F):
@@ -1094,10 +1116,21 @@ def cpu_lookahead(orc, planes, origin, stride, mbw, mbh, nthr, bounded):
         rate = bounded(lambda kw=kw: orc.weights_analyse(8, fl[0], lr[0], lo, ls, mbw, mbh, fic, st[0], st[1],
                                                          **kw) and 1, 1)[0]
         res["weightp_%s_ms_1t" % name] = 1e3 / rate
-    # SSIM of the 1080p pair as rates_ssim measures it
+    # SSIM of the 1080p pair as rates_ssim measures it: the whole frame on one thread, and the
+    # encoder's 68 bands over the CPU share's threads (ctypes releases the GIL in the oracle)
     res["ssim_frames_per_s_1t"] = bounded(lambda: orc.ssim_wxh(8, planes[1].ravel(), origin + 2, stride,
                                                                planes[0].ravel(), origin + 2, stride, W - 2, H)
                                           and 1, 1)[0]
+    import importlib
+    bands = importlib.import_module("x264hip").ssim_encoder_bands(mbh, min(H, 1080))
+    fa, fb = planes[1].ravel(), planes[0].ravel()
+
+    def band(b):
+        y, h = int(b[0]), int(b[1])
+        return orc.ssim_wxh(8, fa, origin + 2 + y * stride, stride, fb, origin + 2 + y * stride, stride, W - 2, h)
+    pool = ThreadPoolExecutor(nthr)
+    res["ssim_bands_frames_per_s"] = bounded(lambda: list(pool.map(band, bands)) and 1, 1)[0]
+    pool.shutdown()
     return res
 
 

@@ -867,6 +867,31 @@ int x264hip_##BD##_me_refine_subpel_ex( const pixel *fenc, intptr_t fenc_stride,
                                         int32_t *nevals, const x264hip_refine_ext_t *ext,       \
                                         void *stream );                                         \
                                                                                                 \
+/* x264_me_search_ref (reference encoder/me.c:182-798) for n partitions of size i_pixel (16x16 ..  \
+ * 8x8) with me_method X264_ME_DIA (0), X264_ME_HEX (1, x264's default, common/base.c:439) or      \
+ * X264_ME_UMH (2): the predictor checks over mvp and the mvc list (x264_predictor_clip /          \
+ * _roundclip, common/common.h:774-805), the integer search (UMH with its adaptive range), the    \
+ * qpel conversion (me.c:774-789), then refine_subpel when subme >= 2 as me_refine_subpel_ex      \
+ * runs it (ext: chroma ME, m->weight; weight[0] also weights the predictors' get_ref).           \
+ * fpel_w = m->p_fref_w (the weighted F plane, the integer search's; = fpel unweighted); fpel /    \
+ * hpel_*: m->p_fref.  pos[3*i] = { frame, x, y }; par[12*i] = { mvp_x, mvp_y (qpel),              \
+ * h->mb.mv_limit_fpel min x, y, max x, y, mv_min_spel x, y, mv_max_spel x, y, i_mvc, 0 };         \
+ * mvc[28*i + 2*k] = candidate k (qpel, k < i_mvc <= 14).  out[4*i] = { m->cost, m->mv[0],         \
+ * m->mv[1], m->cost_mv } (16-byte aligned); nevals (or NULL) = int32 [n][2]: the integer stage's  \
+ * fpelcmp calls | get_ref calls << 16, then the refine's counts (me_refine_subpel's format).      \
+ * p_halfpel_thresh = NULL (the multi-reference early exit is sequential across references).     \
+ * me_range 4 .. 64. */                                                                          \
+int x264hip_##BD##_me_search_ref( const pixel *fenc, intptr_t fenc_stride,                      \
+                                  intptr_t fenc_frame_stride, const pixel *fpel_w,              \
+                                  const pixel *fpel, const pixel *hpel_h, const pixel *hpel_v,  \
+                                  const pixel *hpel_c, intptr_t ref_stride,                     \
+                                  intptr_t ref_frame_stride, int i_pixel, int me_method,        \
+                                  int subme, int me_range, const int32_t *pos,                  \
+                                  const int16_t *par, const int16_t *mvc,                       \
+                                  const uint16_t *cost_mv, int n, int32_t *out,                 \
+                                  int32_t *nevals, const x264hip_refine_ext_t *ext,             \
+                                  void *stream );                                               \
+                                                                                                \
 /* block lists of the reference transforms (dct.c), device arrays;                             \
  * dct holds n consecutive outputs of the selected entry's size. */                             \
 int x264hip_##BD##_sub_dct_batch( int kind, const pixel *fenc, intptr_t fenc_stride,            \
@@ -959,6 +984,20 @@ int x264hip_##BD##_mb_dequant_idct_add( int transform, const dctcoef *dct, int m
 int x264hip_##BD##_ssim_wxh( const pixel *pix1, intptr_t stride1, const pixel *pix2,            \
                              intptr_t stride2, int width, int height, float *ssim, int *cnt,    \
                              void *stream );                                                    \
+                                                                                                \
+/* the encoder's SSIM (encoder.c:2516-2528): x264_pixel_ssim_wxh of every filtered MB-row band  \
+ * of n_frames frame pairs in one launch.  pix1 / pix2: the planes at the bands' left column     \
+ * (plane + 2 as the encoder passes them), frame strides step the frames; bands: device int32    \
+ * pairs (first row, height) relative to pix1 / pix2 -- per MB row mb_y of a thread slice         \
+ * [start, end): min_y = mb_y - 1, first = 16*min_y - 4*!b_start + (b_start ? 2 : -6),           \
+ * last = min( 16*mb_y - 4*!b_end, i_height ), height = last - first (encoder.c:2412-2420,       \
+ * 2490, 2520) -- all of width `width` (i_width - 2).  ssim (device float[n_frames * n_bands]) =   \
+ * each band's float, bit-identical to the reference's; the band's window count is              \
+ * (height/4 - 1) * (width/4 - 1).  width <= 8192. */                                            \
+int x264hip_##BD##_ssim_bands( const pixel *pix1, intptr_t stride1, intptr_t frame_stride1,      \
+                               const pixel *pix2, intptr_t stride2, intptr_t frame_stride2,      \
+                               int width, const int32_t *bands, int n_bands, int n_frames,       \
+                               float *ssim, void *stream );                                      \
                                                                                                 \
 /* the frame statistics x264_weights_analyse reads: fenc->i_pixel_sum[3] / i_pixel_ssd[3] as    \
  * x264_adaptive_quant_frame leaves them for a progressive frame (ac_energy_mb's stores,          \

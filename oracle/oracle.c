@@ -1920,6 +1920,395 @@ void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const pl
                              n, out, nevals, NULL, NULL, 0, NULL, 0 );
 }
 
+/* x264_me_search_ref (reference encoder/me.c:182-798) for a list of partitions of one frame
+ * with me = DIA (0), HEX (1) or UMH (2) and p_halfpel_thresh = NULL: the predictor checks
+ * (:214-318, x264_predictor_clip / _roundclip common/common.h:774-805), the integer search
+ * (:320-616; UMH's adaptive range with x264_predictor_difference, common/base.h:248-257), the
+ * qpel conversion (:774-789), then refine_subpel as FN(me_refine_subpel_ex) runs it when
+ * subme >= 2 (:791-797).  fpelcmp = SAD (encoder.c:1421-1424 outside TESA).  fenc / planes /
+ * fw at pixel (0,0) of one frame: planes = the reference's F, H, V, C (m->p_fref, for
+ * COST_MV_HPEL with m->weight[0] and the refine), fw = p_fref_w (the weighted F plane; = F
+ * unweighted).  pos[2*i] = the partition's top-left; par[12*i] = { mvp_x, mvp_y (qpel),
+ * mv_limit_fpel min x, y, max x, y, mv_min_spel x, y, mv_max_spel x, y, i_mvc, 0 }; mvc[32*i
+ * + 2*k] = candidate k (qpel, k < i_mvc <= 14).  ext / fenc_c / ref_c: as me_refine_subpel_ex
+ * (weight[0] also weights COST_MV_HPEL's get_ref).  out[4*i] = { m->cost, m->mv[0], m->mv[1],
+ * m->cost_mv } as x264_me_search_ref leaves them; nevals[2*i] (when given) = the integer
+ * stage's fpelcmp calls on p_fref_w | its get_ref calls << 16, nevals[2*i+1] = the refine's
+ * counts (me_refine_subpel_ex's format). */
+#define SR_MVC_MAX 14
+static inline uint32_t sr_pack( int a, int b ) { return (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)b << 16); }
+static inline int sr_clip3( int v, int lo, int hi ) { return v < lo ? lo : v > hi ? hi : v; }
+typedef struct
+{
+    const pixel *fenc, *fw;
+    const pixel *q[4];
+    intptr_t fs, rs;
+    int i_pixel;
+    const int *wt;
+    int nf, nh;
+} FN(sr_t);
+
+static int FN(sr_fpel)( FN(sr_t) *c, int mx, int my )           /* fpelcmp on p_fref_w */
+{
+    c->nf++;
+    return FN(sad)( c->i_pixel, c->fenc, c->fs, c->fw + my * c->rs + mx, c->rs );
+}
+
+static int FN(sr_hpel)( FN(sr_t) *c, int mx, int my )           /* COST_MV_HPEL's get_ref + fpelcmp */
+{
+    pixel tmp[16 * 16];
+    intptr_t ts = 16;
+    const pixel *r = get_ref_w( tmp, &ts, c->q, c->rs, mx, my, pixel_w[c->i_pixel], pixel_h[c->i_pixel], c->wt );
+    c->nh++;
+    return FN(sad)( c->i_pixel, c->fenc, c->fs, r, ts );
+}
+
+void FN(me_search_ref)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], const pixel *fw, intptr_t rs,
+                        int i_pixel, int me_method, int subme, int me_range, const int32_t *pos, const int16_t *par,
+                        const int16_t *mvc_all, const uint16_t *cost_mv, int n, int32_t *out, int32_t *nevals,
+                        const int32_t *ext, const pixel *const fenc_c[2], intptr_t fcs, const pixel *const ref_c[8],
+                        intptr_t rcs )
+{
+    static const uint8_t mod6m1[8] = { 5,0,1,2,3,4,5,0 };                                                /* me.c:53 */
+    static const int8_t hex2[8][2] = { {-1,-2}, {-2,0}, {-1,2}, {1,2}, {2,0}, {1,-2}, {-1,-2}, {-2,0} }; /* me.c:55 */
+    static const int8_t square1[9][2] = { {0,0}, {0,-1}, {0,1}, {-1,0}, {1,0}, {-1,-1}, {-1,1}, {1,-1}, {1,1} };
+    static const int8_t hex4[16][2] = { { 0,-4}, { 0, 4}, {-2,-3}, { 2,-3}, {-4,-2}, { 4,-2}, {-4,-1}, { 4,-1},
+                                        {-4, 0}, { 4, 0}, {-4, 1}, { 4, 1}, {-4, 2}, { 4, 2}, {-2, 3}, { 2, 3} };
+    static const uint8_t pixel_size_shift[7] = { 0, 1, 1, 2, 3, 3, 4 };
+    static const uint8_t range_mul[4][4] = { { 3, 3, 4, 4 }, { 3, 4, 4, 4 }, { 4, 4, 4, 5 }, { 4, 4, 5, 6 } };
+    int wbuf[3];
+    const int *wt0 = NULL;
+    if( ext && ext[3] )
+    {
+        wbuf[0] = ext[4]; wbuf[1] = ext[5]; wbuf[2] = ext[6];
+        wt0 = wbuf;
+    }
+    for( int j = 0; j < n; j++ )
+    {
+        const int bx = pos[2*j], by = pos[2*j+1];
+        const int16_t *p = par + 12 * j;
+        FN(sr_t) c = { fenc + by * fs + bx, fw + by * rs + bx, { NULL }, fs, rs, i_pixel, wt0, 0, 0 };
+        for( int k = 0; k < 4; k++ )
+            c.q[k] = planes[k] + by * rs + bx;
+        const int mvp[2] = { p[0], p[1] };
+        const int mv_x_min = p[2], mv_y_min = p[3], mv_x_max = p[4], mv_y_max = p[5];
+        const int i_mvc = p[10];
+        int16_t (*mvc)[2] = (int16_t (*)[2])(mvc_all + 2 * SR_MVC_MAX * j);
+        const uint16_t *p_cost_mvx = cost_mv - mvp[0], *p_cost_mvy = cost_mv - mvp[1];
+        int i_me_range = me_range;
+        int bmx, bmy, bcost = 1 << 28, bpred_cost = 1 << 28;
+        int omx, omy, pmx, pmy;
+        uint32_t pmv, bpred_mv = 0;
+        int16_t tmp[16][2];
+        int costs[16];
+#define SR_BITS( mx, my ) (p_cost_mvx[(mx) * 4] + p_cost_mvy[(my) * 4])
+#define SR_COST_MV( mx, my ) do { int c_ = FN(sr_fpel)( &c, mx, my ) + SR_BITS( mx, my ); \
+                                  if( c_ < bcost ) { bcost = c_; bmx = (mx); bmy = (my); } } while( 0 )
+#define SR_IN( mx, my ) ( (mx) >= mv_x_min && (mx) <= mv_x_max && (my) >= mv_y_min && (my) <= mv_y_max )
+        if( subme >= 3 )
+        {
+            int bpx = sr_clip3( mvp[0], 4 * mv_x_min, 4 * mv_x_max );
+            int bpy = sr_clip3( mvp[1], 4 * mv_y_min, 4 * mv_y_max );
+            pmv = sr_pack( bpx, bpy );
+            pmx = (bpx + 2) >> 2;
+            pmy = (bpy + 2) >> 2;
+            bpred_cost = FN(sr_hpel)( &c, bpx, bpy ) + p_cost_mvx[bpx] + p_cost_mvy[bpy];
+            const int pmv_cost = bpred_cost;
+            if( i_mvc > 0 )
+            {
+                int valid = 0;
+                for( int i = 0; i < i_mvc; i++ )
+                {
+                    uint32_t v = sr_pack( mvc[i][0], mvc[i][1] );
+                    if( !v || v == pmv )
+                        continue;
+                    tmp[2 + valid][0] = sr_clip3( mvc[i][0], 4 * mv_x_min, 4 * mv_x_max );
+                    tmp[2 + valid][1] = sr_clip3( mvc[i][1], 4 * mv_y_min, 4 * mv_y_max );
+                    valid++;
+                }
+                if( valid > 0 )
+                {
+                    tmp[1][0] = bpx; tmp[1][1] = bpy;
+                    bpred_cost <<= 4;
+                    for( int i = 1; i <= valid; i++ )
+                    {
+                        int mx = tmp[i + 1][0], my = tmp[i + 1][1];
+                        int cc = FN(sr_hpel)( &c, mx, my ) + p_cost_mvx[mx] + p_cost_mvy[my];
+                        if( (cc << 4) + i < bpred_cost )
+                            bpred_cost = (cc << 4) + i;
+                    }
+                    bpx = tmp[(bpred_cost & 15) + 1][0];
+                    bpy = tmp[(bpred_cost & 15) + 1][1];
+                    bpred_cost >>= 4;
+                }
+            }
+            bmx = (bpx + 2) >> 2;
+            bmy = (bpy + 2) >> 2;
+            bpred_mv = sr_pack( bpx, bpy );
+            if( bpred_mv & 0x00030003 )
+                SR_COST_MV( bmx, bmy );
+            else
+                bcost = bpred_cost;
+            if( pmv )
+            {
+                if( bmx | bmy )
+                    SR_COST_MV( 0, 0 );
+            }
+            else if( pmv_cost < bcost )
+            {
+                bcost = pmv_cost;
+                bmx = bmy = 0;
+            }
+        }
+        else
+        {
+            bmx = pmx = sr_clip3( (mvp[0] + 2) >> 2, mv_x_min, mv_x_max );
+            bmy = pmy = sr_clip3( (mvp[1] + 2) >> 2, mv_y_min, mv_y_max );
+            pmv = sr_pack( bmx, bmy );
+            bcost = FN(sr_fpel)( &c, bmx, bmy );
+            if( i_mvc > 0 )
+            {
+                int valid = 0;
+                for( int i = 0; i < i_mvc; i++ )
+                {
+                    int mx = (mvc[i][0] + 2) >> 2, my = (mvc[i][1] + 2) >> 2;
+                    uint32_t v = sr_pack( mx, my );
+                    if( !v || v == pmv )
+                        continue;
+                    tmp[2 + valid][0] = sr_clip3( mx, mv_x_min, mv_x_max );
+                    tmp[2 + valid][1] = sr_clip3( my, mv_y_min, mv_y_max );
+                    valid++;
+                }
+                if( valid > 0 )
+                {
+                    tmp[1][0] = bmx; tmp[1][1] = bmy;
+                    bcost <<= 4;
+                    for( int i = 1; i <= valid; i++ )
+                    {
+                        int mx = tmp[i + 1][0], my = tmp[i + 1][1];
+                        int cc = FN(sr_fpel)( &c, mx, my ) + SR_BITS( mx, my );
+                        if( (cc << 4) + i < bcost )
+                            bcost = (cc << 4) + i;
+                    }
+                    bmx = tmp[(bcost & 15) + 1][0];
+                    bmy = tmp[(bcost & 15) + 1][1];
+                    bcost >>= 4;
+                }
+            }
+            if( pmv )
+                SR_COST_MV( 0, 0 );
+        }
+
+        int hex = me_method == 1;
+        if( me_method == 0 )
+        {
+            bcost <<= 4;
+            int i = i_me_range;
+            do
+            {
+                costs[0] = FN(sr_fpel)( &c, bmx, bmy - 1 ) + SR_BITS( bmx, bmy - 1 );
+                costs[1] = FN(sr_fpel)( &c, bmx, bmy + 1 ) + SR_BITS( bmx, bmy + 1 );
+                costs[2] = FN(sr_fpel)( &c, bmx - 1, bmy ) + SR_BITS( bmx - 1, bmy );
+                costs[3] = FN(sr_fpel)( &c, bmx + 1, bmy ) + SR_BITS( bmx + 1, bmy );
+                if( (costs[0] << 4) + 1 < bcost ) bcost = (costs[0] << 4) + 1;
+                if( (costs[1] << 4) + 3 < bcost ) bcost = (costs[1] << 4) + 3;
+                if( (costs[2] << 4) + 4 < bcost ) bcost = (costs[2] << 4) + 4;
+                if( (costs[3] << 4) + 12 < bcost ) bcost = (costs[3] << 4) + 12;
+                if( !(bcost & 15) )
+                    break;
+                bmx -= (int32_t)((uint32_t)bcost << 28) >> 30;
+                bmy -= (int32_t)((uint32_t)bcost << 30) >> 30;
+                bcost &= ~15;
+            } while( --i && SR_IN( bmx, bmy ) );
+            bcost >>= 4;
+        }
+        else if( me_method == 2 )
+        {
+            /* UMH (me.c:422-616) */
+#define SR_DIA1( cx, cy ) do { omx = (cx); omy = (cy); SR_COST_MV( omx, omy - 1 ); SR_COST_MV( omx, omy + 1 ); \
+                               SR_COST_MV( omx - 1, omy ); SR_COST_MV( omx + 1, omy ); } while( 0 )
+#define SR_CROSS( start, x_max, y_max ) do { \
+            for( int i_ = (start); i_ < (x_max); i_ += 2 ) { \
+                if( omx + i_ <= mv_x_max ) SR_COST_MV( omx + i_, omy ); \
+                if( omx - i_ >= mv_x_min ) SR_COST_MV( omx - i_, omy ); } \
+            for( int i_ = (start); i_ < (y_max); i_ += 2 ) { \
+                if( omy + i_ <= mv_y_max ) SR_COST_MV( omx, omy + i_ ); \
+                if( omy - i_ >= mv_y_min ) SR_COST_MV( omx, omy - i_ ); } } while( 0 )
+#define SR_THRESH( v ) ( bcost < ((v) >> pixel_size_shift[i_pixel]) )
+            int cross_start = 1;
+            const int ucost1 = bcost;
+            SR_DIA1( pmx, pmy );
+            if( pmx | pmy )
+                SR_DIA1( 0, 0 );
+            const int ucost2 = bcost;
+            if( (bmx | bmy) && ((bmx - pmx) | (bmy - pmy)) )
+                SR_DIA1( bmx, bmy );
+            if( bcost == ucost2 )
+                cross_start = 3;
+            omx = bmx; omy = bmy;
+            int done = 0;
+            if( bcost == ucost2 && SR_THRESH( 2000 ) )
+            {
+                static const int8_t oct[8][2] = { {0,-2}, {-1,-1}, {1,-1}, {-2,0}, {2,0}, {-1,1}, {1,1}, {0,2} };
+                for( int k = 0; k < 8; k++ )
+                    SR_COST_MV( omx + oct[k][0], omy + oct[k][1] );
+                if( bcost == ucost1 && SR_THRESH( 500 ) )
+                    done = 1;
+                else if( bcost == ucost2 )
+                {
+                    int range = (i_me_range >> 1) | 1;
+                    SR_CROSS( 3, range, range );
+                    static const int8_t oct2[8][2] = { {-1,-2}, {1,-2}, {-2,-1}, {2,-1}, {-2,1}, {2,1}, {-1,2}, {1,2} };
+                    for( int k = 0; k < 8; k++ )
+                        SR_COST_MV( omx + oct2[k][0], omy + oct2[k][1] );
+                    if( bcost == ucost2 )
+                        done = 1;
+                    cross_start = range + 2;
+                }
+            }
+            if( !done )
+            {
+                if( i_mvc )
+                {
+                    int mvd, denom = 1;
+                    if( i_mvc == 1 )
+                        mvd = i_pixel == 0 ? 25 : abs( mvp[0] - mvc[0][0] ) + abs( mvp[1] - mvc[0][1] );
+                    else
+                    {
+                        denom = i_mvc - 1;
+                        mvd = 0;
+                        if( i_pixel != 0 )
+                        {
+                            mvd = abs( mvp[0] - mvc[0][0] ) + abs( mvp[1] - mvc[0][1] );
+                            denom++;
+                        }
+                        for( int i = 0; i < i_mvc - 1; i++ )
+                            mvd += abs( mvc[i][0] - mvc[i + 1][0] ) + abs( mvc[i][1] - mvc[i + 1][1] );
+                    }
+                    const int sad_ctx = SR_THRESH( 1000 ) ? 0 : SR_THRESH( 2000 ) ? 1 : SR_THRESH( 4000 ) ? 2 : 3;
+                    const int mvd_ctx = mvd < 10 * denom ? 0 : mvd < 20 * denom ? 1 : mvd < 40 * denom ? 2 : 3;
+                    i_me_range = i_me_range * range_mul[mvd_ctx][sad_ctx] >> 2;
+                }
+                SR_CROSS( cross_start, i_me_range, i_me_range >> 1 );
+                SR_COST_MV( omx - 2, omy - 2 );
+                SR_COST_MV( omx - 2, omy + 2 );
+                SR_COST_MV( omx + 2, omy - 2 );
+                SR_COST_MV( omx + 2, omy + 2 );
+                omx = bmx; omy = bmy;
+                int i = 1;
+                do
+                {
+                    for( int k = 0; k < 16; k++ )
+                    {
+                        const int mx = omx + hex4[k][0] * i, my = omy + hex4[k][1] * i;
+                        if( SR_IN( mx, my ) )
+                            SR_COST_MV( mx, my );
+                    }
+                } while( ++i <= i_me_range >> 2 );
+                if( SR_IN( bmx, bmy ) )
+                    hex = 1;
+            }
+#undef SR_DIA1
+#undef SR_CROSS
+#undef SR_THRESH
+        }
+        if( hex )
+        {
+            /* hexagon (me.c:344-403), then the square refine (:404-418) */
+#define SR_X3( a, b, cc, d, e, f, o ) do { \
+            (o)[0] = FN(sr_fpel)( &c, bmx + (a), bmy + (b) ) + SR_BITS( bmx + (a), bmy + (b) ); \
+            (o)[1] = FN(sr_fpel)( &c, bmx + (cc), bmy + (d) ) + SR_BITS( bmx + (cc), bmy + (d) ); \
+            (o)[2] = FN(sr_fpel)( &c, bmx + (e), bmy + (f) ) + SR_BITS( bmx + (e), bmy + (f) ); } while( 0 )
+            SR_X3( -2, 0, -1, 2, 1, 2, costs );
+            SR_X3( 2, 0, 1, -2, -1, -2, costs + 4 );
+            bcost <<= 3;
+            if( (costs[0] << 3) + 2 < bcost ) bcost = (costs[0] << 3) + 2;
+            if( (costs[1] << 3) + 3 < bcost ) bcost = (costs[1] << 3) + 3;
+            if( (costs[2] << 3) + 4 < bcost ) bcost = (costs[2] << 3) + 4;
+            if( (costs[4] << 3) + 5 < bcost ) bcost = (costs[4] << 3) + 5;
+            if( (costs[5] << 3) + 6 < bcost ) bcost = (costs[5] << 3) + 6;
+            if( (costs[6] << 3) + 7 < bcost ) bcost = (costs[6] << 3) + 7;
+            if( bcost & 7 )
+            {
+                int dir = (bcost & 7) - 2;
+                bmx += hex2[dir + 1][0];
+                bmy += hex2[dir + 1][1];
+                for( int i = (i_me_range >> 1) - 1; i > 0 && SR_IN( bmx, bmy ); i-- )
+                {
+                    SR_X3( hex2[dir][0], hex2[dir][1], hex2[dir + 1][0], hex2[dir + 1][1], hex2[dir + 2][0],
+                           hex2[dir + 2][1], costs );
+                    bcost &= ~7;
+                    if( (costs[0] << 3) + 1 < bcost ) bcost = (costs[0] << 3) + 1;
+                    if( (costs[1] << 3) + 2 < bcost ) bcost = (costs[1] << 3) + 2;
+                    if( (costs[2] << 3) + 3 < bcost ) bcost = (costs[2] << 3) + 3;
+                    if( !(bcost & 7) )
+                        break;
+                    dir += (bcost & 7) - 2;
+                    dir = mod6m1[dir + 1];
+                    bmx += hex2[dir + 1][0];
+                    bmy += hex2[dir + 1][1];
+                }
+            }
+            bcost >>= 3;
+#undef SR_X3
+            bcost <<= 4;
+            for( int k = 0; k < 8; k++ )
+            {
+                const int cc = FN(sr_fpel)( &c, bmx + square1[k + 1][0], bmy + square1[k + 1][1] )
+                             + SR_BITS( bmx + square1[k + 1][0], bmy + square1[k + 1][1] );
+                if( (cc << 4) + k + 1 < bcost )
+                    bcost = (cc << 4) + k + 1;
+            }
+            bmx += square1[bcost & 15][0];
+            bmy += square1[bcost & 15][1];
+            bcost >>= 4;
+        }
+#undef SR_COST_MV
+#undef SR_IN
+        /* -> qpel mv (me.c:774-789) */
+        int mx, my, cst, cmv;
+        if( subme < 3 )
+        {
+            cmv = SR_BITS( bmx, bmy );
+            cst = bcost + (sr_pack( bmx, bmy ) == pmv ? cmv : 0);
+            mx = 4 * bmx;
+            my = 4 * bmy;
+        }
+        else
+        {
+            if( bpred_cost < bcost )
+            {
+                mx = (int16_t)(bpred_mv & 0xffff);
+                my = (int16_t)(bpred_mv >> 16);
+            }
+            else
+            {
+                mx = 4 * bmx;
+                my = 4 * bmy;
+            }
+            cst = bpred_cost < bcost ? bpred_cost : bcost;
+            cmv = p_cost_mvx[mx] + p_cost_mvy[my];    /* (refine_subpel sets m->cost_mv) */
+        }
+#undef SR_BITS
+        out[4*j] = cst;
+        out[4*j+1] = mx;
+        out[4*j+2] = my;
+        out[4*j+3] = cmv;
+        if( nevals )
+        {
+            nevals[2*j] = c.nf | (c.nh << 16);
+            nevals[2*j+1] = 0;
+        }
+        if( subme >= 2 )
+        {
+            const int16_t rp[8] = { (int16_t)mx, (int16_t)my, (int16_t)mvp[0], (int16_t)mvp[1], p[6], p[7], p[8], p[9] };
+            const int32_t rpos[2] = { bx, by };
+            FN(me_refine_subpel_ex)( fenc, fs, planes, rs, i_pixel, subme, 0, 0, rpos, rp, &cst, cost_mv, 1,
+                                     out + 4 * j, nevals ? nevals + 2 * j + 1 : NULL, ext, fenc_c, fcs, ref_c, rcs );
+        }
+    }
+}
+
 /* TESA integer-pel search of x264_me_search_ref for PIXEL_16x16, restated from
  * reference encoder/me.c:618-748 (X264_ME_TESA): enc_dc from sad_x4 against
  * x264_zero (:643-645), per row the ycost skip, ads4 with threshold bsad*17>>4

@@ -74,6 +74,8 @@ for _bd in (8, 10):
     _f(_bd, "me_search_centred", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P])
     _f(_bd, "me_refine_subpel", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P,
                                  _P])
+    _f(_bd, "me_search_ref", [_P, _IP, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P,
+                              _P, _P, _P, _IP, _P, _IP])
     _f(_bd, "me_refine_subpel_ex", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int,
                                     _P, _P, _P, _P, _IP, _P, _IP])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
@@ -377,6 +379,29 @@ def me_refine_subpel(bd, fenc, f_origin, fs, planes, r_origin, rs, i_pixel, subm
                                                   _addr(c), _addr(cost_mv, c0), n, _addr(out), _addr(ne),
                                                   None if e is None else _addr(e), fca, fcs, rca, rcs)
     return (out, ne) if counts else out
+
+
+def me_search_ref(bd, fenc, f_origin, fs, planes, fw, r_origin, rs, i_pixel, me_method, subme, me_range, pos_xy,
+                  par, mvc, cost_mv, c0, ext=None, fenc_c=None, fc_origin=0, fcs=0, ref_c=None, rc_origin=0, rcs=0):
+    """one frame: x264_me_search_ref (me.c:182-798) of the partitions at pos_xy int32 [n, 2] with
+    me_method 0 DIA / 1 HEX / 2 UMH; par int16 [n, 12], mvc int16 [n, 14, 2] (search_cases.jobs);
+    planes = F, H, V, C, fw = the weighted F plane (or F).  Returns int32 [n, 4] = (cost, mvx, mvy,
+    cost_mv) and the call counts int32 [n, 2] (integer stage fpel | get_ref << 16, the refine's)."""
+    n = len(pos_xy)
+    pos = np.ascontiguousarray(pos_xy, np.int32)
+    p = np.ascontiguousarray(par, np.int16)
+    m = np.ascontiguousarray(mvc, np.int16)
+    out = np.zeros((n, 4), np.int32)
+    ne = np.zeros((n, 2), np.int32)
+    arr = (C.c_void_p * 4)(*[_addr(q, r_origin).value for q in planes])
+    fca = (C.c_void_p * 2)(*([_addr(q, fc_origin).value for q in (fenc_c or [])] + [None] * 2)[:2])
+    rca = (C.c_void_p * 8)(*([_addr(q, rc_origin).value for q in (ref_c or [])] + [None] * 8)[:8])
+    e = None if ext is None else np.ascontiguousarray(ext, np.int32)
+    getattr(_L, f"oracle{bd}_me_search_ref")(_addr(fenc, f_origin), fs, arr, _addr(fw, r_origin), rs, i_pixel,
+                                            me_method, subme, me_range, _addr(pos), _addr(p), _addr(m),
+                                            _addr(cost_mv, c0), n, _addr(out), _addr(ne),
+                                            None if e is None else _addr(e), fca, fcs, rca, rcs)
+    return out, ne
 
 
 # ---------------------------------------------------------------- further pixel entries

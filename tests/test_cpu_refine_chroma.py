@@ -89,6 +89,13 @@ def refine_chroma_py(cc, x, y, i_pixel, par, cost, cm, c0, subme, refine_qpel, b
     qpel = SUBPEL_ITERATIONS[subme][1 if refine_qpel else 3]
     bmx, bmy, bcost = int(par[0]), int(par[1]), int(cost)
     if hpel:
+        if subme < 3:                                       # the predictor's subpel component (me.c:889-895)
+            px = min(max(mvp[0], mn[0] + 2), mx_[0] - 2)
+            py = min(max(mvp[1], mn[1] + 2), mx_[1] - 2)
+            if (px - bmx) | (py - bmy):
+                c = luma(False, px, py) + cmx(px) + cmy(py)
+                if c < bcost:
+                    bcost, bmx, bmy = c, px, py
         bcost = _s32(bcost << 6)
         for _ in range(hpel):
             omx, omy = bmx, bmy

@@ -81,3 +81,15 @@ def test_ssim_core_end4_vs_numpy(oracle, bd):
                 q = s0[i] + s0[i + 1] + s1[i] + s1[i + 1]
                 g = F(g + np_end1(bd, *[int(v) for v in q]))
             assert oracle.ssim_end4(bd, s0, s1, width).tobytes() == g.tobytes()
+
+
+def test_ssim_encoder_bands():
+    """fdec_filter_row's SSIM bands (encoder.c:2412-2420, 2490, 2520) for a 1080p frame, one slice
+    and two thread slices (b_start / b_end at the slice edges)"""
+    from conftest import load_package
+    x = load_package()
+    b = x.ssim_encoder_bands(68, 1080)
+    assert len(b) == 68
+    assert tuple(b[0]) == (2, 10) and tuple(b[1]) == (6, 22) and tuple(b[-1]) == (1062, 18)
+    s = x.ssim_encoder_bands(68, 1080, [(0, 34), (34, 68)])
+    assert len(s) == 68 and tuple(s[33]) == (518, 26) and tuple(s[34]) == (546, 10)

@@ -85,3 +85,30 @@ def test_table_ssim_entries(hip, oracle, bd):
                        ctypes.byref(sv))
     wu, wv = oracle.ssd_nv12(bd, u.ravel(), 0, u.shape[1], v.ravel(), 0, v.shape[1], cw, chh)
     assert (su.value, sv.value) == (int(wu), int(wv))
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("W,H,slices", [(1920, 1080, None), (1920, 1080, [(0, 17), (17, 34), (34, 51), (51, 68)]),
+                                        (352, 288, None), (3840, 2160, None)])
+def test_ssim_bands(hip, oracle, bd, W, H, slices):
+    """every encoder band of two frame pairs in one launch (encoder.c:2412-2420, 2516-2528), each
+    band's float bit-identical to the oracle's x264_pixel_ssim_wxh on it, and the frame's double
+    sum equal to the encoder's"""
+    mbh = (H + 15) // 16
+    bands = hip.ssim_encoder_bands(mbh, H, slices)
+    pairs = [_planes(oracle, bd, W, H, bd + W + k) for k in range(2)]
+    s = pairs[0][0].shape[1]
+    a = _dev(np.stack([p[0] for p in pairs]))
+    b = _dev(np.stack([p[1] for p in pairs]))
+    got = hip.ssim_bands(a, 2, s, b, 2, s, W - 2, torch.from_numpy(bands).cuda()).cpu().numpy()
+    for f, (pa, pb) in enumerate(pairs):
+        total, wtotal = 0.0, 0.0
+        for i, (y, h) in enumerate(bands):
+            want, wcnt = oracle.ssim_wxh(bd, pa.ravel(), 2 + int(y) * s, s, pb.ravel(), 2 + int(y) * s, s, W - 2,
+                                         int(h))
+            assert got[f, i].tobytes() == want.tobytes(), (f, i, y, h, got[f, i], want)
+            assert wcnt == (h // 4 - 1) * ((W - 2) // 4 - 1)
+            total += float(got[f, i])
+            wtotal += float(want)
+        assert total == wtotal
+

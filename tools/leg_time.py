@@ -23,7 +23,7 @@ def main():
     x = bench.load_package()
     x.init(0)
     from x264hip import synth
-    a = types.SimpleNamespace(steps=steps, warmup=5, range=16, tframes=64)
+    a = types.SimpleNamespace(steps=steps, warmup=5, range=16, tframes=64, width=1920, height=1080)
     W, H = 1920, 1088
     mbw, mbh = W // 16, H // 16
     planes, stride, origin = synth.make_sequence(F + 1, W, H, 8)

@@ -25,7 +25,7 @@ import numpy as np
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "refine_ext", "RefineExt", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "me_search_ref", "ssim_bands", "ssim_encoder_bands", "refine_ext", "RefineExt", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "stream_pair_destroy", "me_search_full8",
@@ -849,6 +849,43 @@ def ssim_wxh(pix1, origin1, stride1, pix2, origin2, stride2, width, height):
     return float(out.item()), cnt.value
 
 
+def ssim_encoder_bands(mb_height, height, slices=None):
+    """the (first row, height) of every band the encoder measures SSIM on (encoder.c:2412-2420,
+    2490, 2516-2528: fdec_filter_row per MB row of each thread slice [start, end), relative to
+    plane + 2), int32 [n, 2]; slices defaults to one slice [0, mb_height)"""
+    import numpy as np
+    out = []
+    for start, end in (slices or [(0, mb_height)]):
+        for mb_y in range(start + 1, end + 1):
+            min_y = mb_y - 1
+            b_start, b_end = min_y == start, mb_y == end
+            minpix = min_y * 16 - 4 * (not b_start)
+            maxpix = min(mb_y * 16 - 4 * (not b_end), height)
+            minpix += 2 if b_start else -6
+            out.append((minpix, maxpix - minpix))
+    return np.array(out, np.int32).reshape(-1, 2)
+
+
+def ssim_bands(pix1, origin1, stride1, pix2, origin2, stride2, width, bands, out=None):
+    """x264hip_*_ssim_bands: every band's x264_pixel_ssim_wxh float of every frame pair, float32
+    tensor [n_frames, n_bands]; pix* [n, rows, stride] tensors, origin* = element offset of the
+    bands' left column at row 0 (plane (2, 0) as the encoder passes it), bands = int32 tensor
+    [n_bands, 2] on the device (ssim_encoder_bands)"""
+    import torch
+    bd = _pix_bd(pix1)
+    nf = pix1.shape[0] if pix1.dim() == 3 else 1
+    nb = bands.shape[0]
+    if out is None:
+        out = torch.empty((nf, nb), dtype=torch.float32, device=pix1.device)
+    f = getattr(lib(), f"x264hip_{bd}_ssim_bands")
+    f.argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _P, _c.c_int, _c.c_int, _P, _P]
+    f1 = pix1.stride(0) if pix1.dim() == 3 else 0
+    f2 = pix2.stride(0) if pix2.dim() == 3 else 0
+    _rc(f(_ptr(pix1, origin1), stride1, f1, _ptr(pix2, origin2), stride2, f2, width, _ptr(bands), nb, nf, _ptr(out),
+          _stream()), "ssim_bands")
+    return out
+
+
 def frame_pixel_stats(luma, luma_origin, luma_stride, mb_width, mb_height, chroma_format=0, chroma_u=None,
                       chroma_v=None, chroma_origin=0, chroma_stride=0, out=None):
     """fenc->i_pixel_sum / i_pixel_ssd of one frame (x264hip_*_frame_pixel_stats): int64 tensor [6] =
@@ -1227,6 +1264,35 @@ def me_refine_subpel(fenc, fenc_origin, fenc_stride, planes, ref_origin, ref_str
     fn.argtypes = types + [_P]
     fn.restype = _c.c_int
     _rc(fn(*args, _stream()), name)
+    return out
+
+
+def me_search_ref(fenc, fenc_origin, fenc_stride, fpel_w, planes, ref_origin, ref_stride, i_pixel, me_method, subme,
+                  me_range, pos, par, mvc, cost_mv_center, out=None, fenc_frame_stride=None, ref_frame_stride=None,
+                  nevals=None, ext=None):
+    """x264_me_search_ref (encoder/me.c:182-798) of n partitions (x264hip_*_me_search_ref): me_method
+    0 DIA / 1 HEX / 2 UMH; fpel_w = the weighted F plane the integer search reads (m->p_fref_w, or
+    planes[0]); planes = [F, H, V, C]; pos int32 [n, 3] = (frame, x, y); par int16 [n, 12] = (mvp
+    x, y, mv_limit_fpel min x, y, max x, y, mv_min_spel x, y, mv_max_spel x, y, i_mvc, 0); mvc
+    int16 [n, 14, 2]; ext = refine_ext(...) for chroma ME / weights.  Returns int32 [n, 4] =
+    (m->cost, m->mv x, y, m->cost_mv); nevals: optional int32 [n, 2] (integer stage fpel | get_ref
+    << 16, refine counts)."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = pos.shape[0]
+    if out is None:
+        out = torch.empty((n, 4), dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else _frame_stride(fpel_w, *planes)
+    cm, c0 = cost_mv_center
+    fn = getattr(lib(), f"x264hip_{bd}_me_search_ref")
+    fn.argtypes = [_P, _IP, _IP, _P, _P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P,
+                   _P, _c.c_int, _P, _P, _P, _P]
+    fn.restype = _c.c_int
+    _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(fpel_w, ref_origin), *[_ptr(p, ref_origin) for p in planes],
+           ref_stride, rfs, i_pixel, me_method, subme, me_range, _ptr(pos), _ptr(par), _ptr(mvc), _ptr(cm, c0), n,
+           _ptr(out), _ptr(nevals) if nevals is not None else None, _c.byref(ext) if ext is not None else None,
+           _stream()), "me_search_ref")
     return out
 
 

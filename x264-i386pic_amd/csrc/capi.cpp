@@ -1861,6 +1861,23 @@ extern "C" const char *x264hip_backend_banner( void )
                                                      fpel_satd, pos, par, init_cost, cost_mv, n, out, nevals, ext,  \
                                                      (hipStream_t)stream ), "me_refine_subpel_ex" );                 \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_search_ref( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,              \
+                                                 const PT<BD>::pixel *fw, const PT<BD>::pixel *p0,                   \
+                                                 const PT<BD>::pixel *p1, const PT<BD>::pixel *p2,                   \
+                                                 const PT<BD>::pixel *p3, intptr_t rs, intptr_t rfs, int i_pixel,    \
+                                                 int me_method, int subme, int me_range, const int32_t *pos,         \
+                                                 const int16_t *par, const int16_t *mvc, const uint16_t *cost_mv,    \
+                                                 int n, int32_t *out, int32_t *nevals,                               \
+                                                 const x264hip_refine_ext_t *ext, void *stream )                     \
+    {                                                                                                                \
+        if( n < 0 || ( n > 0 && ( !fenc || !fw || !p0 || !p1 || !p2 || !p3 || !pos || !par || !mvc || !cost_mv ||   \
+                                  !out ) ) )                                                                         \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
+        return map_err( launch_me_search_ref<BD>( fenc, fs, ffs, fw, planes, rs, rfs, i_pixel, me_method, subme,     \
+                                                  me_range, pos, par, mvc, cost_mv, n, out, nevals, ext,             \
+                                                  (hipStream_t)stream ), "me_search_ref" );                          \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_sub_dct_batch( int kind, const PT<BD>::pixel *fenc, intptr_t fs,                  \
                                                  const PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fo,          \
                                                  const int64_t *dofs, int n, PT<BD>::dctcoef *dct, void *stream )    \
@@ -1969,6 +1986,17 @@ extern "C" const char *x264hip_backend_banner( void )
             return X264HIP_EINVAL;                                                                                   \
         return map_err( launch_frame_init_lowres<BD>( src, stride, fstride, width, height, nframes, dst, ds, dfs,     \
                                                       (hipStream_t)stream ), "frame_init_lowres" );                  \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_ssim_bands( const PT<BD>::pixel *p1, intptr_t s1, intptr_t f1,                    \
+                                              const PT<BD>::pixel *p2, intptr_t s2, intptr_t f2, int width,          \
+                                              const int32_t *bands, int n_bands, int n_frames, float *ssim,          \
+                                              void *stream )                                                         \
+    {                                                                                                                \
+        if( width < 0 || width > 8192 || n_bands < 0 || n_frames < 0 ||                                             \
+            ( n_bands > 0 && n_frames > 0 && ( !p1 || !p2 || !bands || !ssim ) ) )                                   \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_ssim_bands<BD>( p1, s1, f1, p2, s2, f2, width, bands, n_bands, n_frames, ssim,        \
+                                               (hipStream_t)stream ), "ssim_bands" );                                \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_ssim_wxh( const PT<BD>::pixel *p1, intptr_t s1, const PT<BD>::pixel *p2,          \
                                             intptr_t s2, int width, int height, float *ssim, int *cnt,              \

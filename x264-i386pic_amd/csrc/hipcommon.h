@@ -385,6 +385,13 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
                                     int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *ext,
                                     hipStream_t stream );
 template <int BD>
+hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                 const typename PT<BD>::pixel *fw, const typename PT<BD>::pixel *const planes[4],
+                                 intptr_t rs, intptr_t rfs, int i_pixel, int me_method, int subme, int me_range,
+                                 const int32_t *pos, const int16_t *par, const int16_t *mvc, const uint16_t *cost_mv,
+                                 int n, int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *ext,
+                                 hipStream_t stream );
+template <int BD>
 hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int nmb, int me_range,
                                  const int16_t *origin, const int16_t *par, const int32_t *init_cost,
                                  const uint16_t *cost_mv, int32_t *out, hipStream_t stream );
@@ -513,6 +520,10 @@ hipError_t launch_frame_stats( const typename PT<BD>::pixel *y, intptr_t ys, con
 template <int BD>
 hipError_t launch_ssim_wxh( const typename PT<BD>::pixel *p1, intptr_t s1, const typename PT<BD>::pixel *p2,
                             intptr_t s2, int width, int height, float *out, hipStream_t stream );
+template <int BD>
+hipError_t launch_ssim_bands( const typename PT<BD>::pixel *p1, intptr_t s1, intptr_t f1,
+                              const typename PT<BD>::pixel *p2, intptr_t s2, intptr_t f2, int width,
+                              const int32_t *bands, int nbands, int nframes, float *out, hipStream_t stream );
 template <int BD>
 hipError_t launch_ssim_core( const typename PT<BD>::pixel *p1, intptr_t s1, const typename PT<BD>::pixel *p2,
                              intptr_t s2, int *out, hipStream_t stream );

@@ -215,7 +215,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     const typename PT<BD>::pixel *p1, const typename PT<BD>::pixel *p2, const typename PT<BD>::pixel *p3,
     intptr_t rs, intptr_t rfs, int n, int hpel_iters, int qpel_iters, int subme, int refine_qpel,
     const int32_t *__restrict__ pos, const int16_t *__restrict__ par, const int32_t *__restrict__ init_cost,
-    const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out, int32_t *__restrict__ nevals,
+    const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out, int32_t *__restrict__ nevals, int nstride,
     const RsExt<BD> ext )
 {
     using pixel = typename PT<BD>::pixel;
@@ -538,17 +538,59 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     {
         *(int4 *)(out + 4 * j) = make_int4( bcost, bmx, bmy, (int)cmx[bmx] + (int)cmy[bmy] );
         if( nevals )
-            nevals[j] = nsad | (nsatd << 16) | (nchroma << 24);
+            nevals[j * nstride] = nsad | (nsatd << 16) | (nchroma << 24);
     }
 }
 
+// the EXT inputs of x264hip_refine_ext_t for the kernels (mode: 0 plain, 1 weighted luma and / or
+// 4:2:0 / 4:2:2 chroma ME, 2 4:4:4 chroma ME), or hipErrorInvalidValue
+template <int BD> hipError_t rs_ext( const x264hip_refine_ext_t *xe, RsExt<BD> &ext, int &mode )
+{
+    using pixel = typename PT<BD>::pixel;
+    ext = {};
+    mode = 0;
+    if( !xe )
+        return hipSuccess;
+    for( int k = 0; k < 3; k++ )
+    {
+        const x264hip_weight_t &w = xe->weight[k];
+        if( w.weighted && (w.denom < 0 || w.denom > 7) )
+            return hipErrorInvalidValue;
+        ext.wt[k] = { w.weighted ? 1 : 0, w.scale, w.weighted ? w.denom : 0,
+                      w.weighted && w.denom > 0 ? 1 << (w.denom - 1) : 0, w.offset * (1 << (BD - 8)) };
+    }
+    const int cf = xe->chroma_format;
+    if( xe->b_chroma_me )
+    {
+        if( cf < 1 || cf > 3 || !xe->fenc_chroma[0] || !xe->ref_chroma[0] ||
+            (cf == 3 && (!xe->fenc_chroma[1] || !xe->ref_chroma[1] || !xe->ref_chroma[2] || !xe->ref_chroma[3] ||
+                         !xe->ref_chroma[4] || !xe->ref_chroma[5] || !xe->ref_chroma[6] || !xe->ref_chroma[7])) )
+            return hipErrorInvalidValue;
+        ext.chroma = 1;
+        ext.vs = cf == 1;
+        ext.mvy_offset = xe->mvy_offset;
+        for( int k = 0; k < 2; k++ )
+            ext.fenc_c[k] = (const pixel *)xe->fenc_chroma[k];
+        for( int k = 0; k < 8; k++ )
+            ext.ref_c[k] = (const pixel *)xe->ref_chroma[k];
+        ext.fcs = xe->fenc_chroma_stride;
+        ext.ffcs = xe->fenc_chroma_frame_stride;
+        ext.rcs = xe->ref_chroma_stride;
+        ext.rfcs = xe->ref_chroma_frame_stride;
+        mode = cf == 3 ? 2 : 1;
+    }
+    else if( ext.wt[0].on )
+        mode = 1;                                         // weighted luma, no chroma
+    return hipSuccess;
+}
+
 template <int BD>
-hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
-                                    const typename PT<BD>::pixel *const planes[4], intptr_t rs, intptr_t rfs,
-                                    int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
-                                    const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int n,
-                                    int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *xe,
-                                    hipStream_t stream )
+static hipError_t refine_launch( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                 const typename PT<BD>::pixel *const planes[4], intptr_t rs, intptr_t rfs,
+                                 int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
+                                 const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int n,
+                                 int32_t *out, int32_t *nevals, int nstride, const x264hip_refine_ext_t *xe,
+                                 hipStream_t stream )
 {
     using pixel = typename PT<BD>::pixel;
     if( n <= 0 )
@@ -559,49 +601,17 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
     const int qpel = k_subpel_iterations[subme][refine_qpel ? 1 : 3];
     // fpelcmp is SATD only under TESA with subme > 1 (encoder.c:1423-1426)
     const bool fs_satd = fpel_satd && subme > 1;
-    RsExt<BD> ext = {};
-    int mode = 0;
-    if( xe )
-    {
-        for( int k = 0; k < 3; k++ )
-        {
-            const x264hip_weight_t &w = xe->weight[k];
-            if( w.weighted && (w.denom < 0 || w.denom > 7) )
-                return hipErrorInvalidValue;
-            ext.wt[k] = { w.weighted ? 1 : 0, w.scale, w.weighted ? w.denom : 0,
-                          w.weighted && w.denom > 0 ? 1 << (w.denom - 1) : 0, w.offset * (1 << (BD - 8)) };
-        }
-        const int cf = xe->chroma_format;
-        if( xe->b_chroma_me )
-        {
-            if( cf < 1 || cf > 3 || !xe->fenc_chroma[0] || !xe->ref_chroma[0] ||
-                (cf == 3 && (!xe->fenc_chroma[1] || !xe->ref_chroma[1] || !xe->ref_chroma[2] ||
-                             !xe->ref_chroma[3] || !xe->ref_chroma[4] || !xe->ref_chroma[5] ||
-                             !xe->ref_chroma[6] || !xe->ref_chroma[7])) )
-                return hipErrorInvalidValue;
-            ext.chroma = 1;
-            ext.vs = cf == 1;
-            ext.mvy_offset = xe->mvy_offset;
-            for( int k = 0; k < 2; k++ )
-                ext.fenc_c[k] = (const pixel *)xe->fenc_chroma[k];
-            for( int k = 0; k < 8; k++ )
-                ext.ref_c[k] = (const pixel *)xe->ref_chroma[k];
-            ext.fcs = xe->fenc_chroma_stride;
-            ext.ffcs = xe->fenc_chroma_frame_stride;
-            ext.rcs = xe->ref_chroma_stride;
-            ext.rfcs = xe->ref_chroma_frame_stride;
-            mode = cf == 3 ? 2 : 1;
-        }
-        else if( ext.wt[0].on )
-            mode = 1;                                     // weighted luma, no chroma
-    }
+    RsExt<BD> ext;
+    int mode;
+    if( rs_ext<BD>( xe, ext, mode ) != hipSuccess )
+        return hipErrorInvalidValue;
     // 4 * (the partition's 8x4 tiles) lanes per partition (me_refine_subpel_kernel's segments)
     const int64_t lanes = (int64_t)n * 4 * (pix_w( i_pixel ) / 8) * (pix_h( i_pixel ) / 4);
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
 #define RS_GO( I, F, E )                                                                                          \
     hipLaunchKernelGGL( ( me_refine_subpel_kernel<BD, I, F, E> ), g, blk, 0, stream, fenc, fs, ffs, planes[0],    \
                         planes[1], planes[2], planes[3], rs, rfs, n, hpel, qpel, subme, refine_qpel ? 1 : 0, pos,   \
-                        par, init_cost, cost_mv, out, nevals, ext )
+                        par, init_cost, cost_mv, out, nevals, nstride, ext )
 #define RS_MODE( I, F )                                                                                           \
     if( mode == 0 ) { RS_GO( I, F, 0 ); } else if( mode == 1 ) { RS_GO( I, F, 1 ); } else { RS_GO( I, F, 2 ); }
 #define RS_CASE( I )                                                                                              \
@@ -618,6 +628,597 @@ hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t
 #undef RS_GO
     return hipGetLastError();
 }
+
+template <int BD>
+hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                    const typename PT<BD>::pixel *const planes[4], intptr_t rs, intptr_t rfs,
+                                    int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
+                                    const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int n,
+                                    int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *xe,
+                                    hipStream_t stream )
+{
+    return refine_launch<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, refine_qpel, fpel_satd, pos, par,
+                              init_cost, cost_mv, n, out, nevals, 1, xe, stream );
+}
+
+// ---------------------------------------------------------------------------------------------
+// x264_me_search_ref's integer stage (reference encoder/me.c:182-789) for a batch of partitions:
+// the predictor checks (:214-318), DIA (:322-342), HEX (:344-419) or UMH (:422-616, then its
+// me_hex2), and the qpel conversion; refine_subpel follows as the kernel above (launch_me_search_ref).
+// The lane layout is refine_subpel's: a segment of 4 * NT lanes per partition, four groups of NT
+// tile lanes, group g scoring the step's candidate g (fpelcmp = SAD of the 8x4 tiles on p_fref_w,
+// or COST_MV_HPEL's get_ref of the hpel planes weighted by m->weight[0]).  Every step's
+// candidates are scored together and then taken in the reference's order with its strict-<
+// updates, so a step of up to four COST_MV / COST_MV_X3 / X4 calls is one evaluation; the
+// searches' control flow is per segment (each segment's lanes hold the same state), the
+// segments of a wave stepping through their own paths.  Lists whose length depends on the
+// state -- the predictors (x264_predictor_clip / _roundclip drop zero and pmv-equal entries),
+// UMH's cross and hexagon grid (range checks) -- are walked as slots, a slot outside the mv
+// range not scored (and not read: it may lie past the padding).
+namespace {
+constexpr int SR_MVC = 14;                                // candidates per partition (mvc_temp+2 of me.c:195)
+__device__ __forceinline__ uint32_t sr_pack( int a, int b ) { return (uint32_t)(uint16_t)a | ((uint32_t)(uint16_t)b << 16); }
+__device__ __forceinline__ int sr_clip( int v, int lo, int hi ) { return min( max( v, lo ), hi ); }
+// hex2 (me.c:55), square1 (:56) and hex4 (:534-539) as bit fields (offset + bias)
+constexpr uint8_t k_hex2x[8] = { 1, 0, 1, 3, 4, 3, 1, 0 }, k_hex2y[8] = { 0, 2, 4, 4, 2, 0, 0, 2 };   // +2
+constexpr uint8_t k_sq1x[9] = { 1, 1, 1, 0, 2, 0, 0, 2, 2 }, k_sq1y[9] = { 1, 0, 2, 1, 1, 0, 2, 0, 2 };  // +1
+constexpr uint8_t k_mod6m1[8] = { 5, 0, 1, 2, 3, 4, 5, 0 };
+constexpr uint8_t k_hex4x0[8] = { 4, 4, 2, 6, 0, 8, 0, 8 }, k_hex4x1[8] = { 0, 8, 0, 8, 0, 8, 2, 6 };   // +4
+constexpr uint8_t k_hex4y0[8] = { 0, 8, 1, 1, 2, 2, 3, 3 }, k_hex4y1[8] = { 4, 4, 5, 5, 6, 6, 7, 7 };   // +4
+constexpr uint8_t k_psize_shift[7] = { 0, 1, 1, 2, 3, 3, 4 };
+}
+
+template <int BD, int IPIX, bool WGT>
+__global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
+    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs, const typename PT<BD>::pixel *fw,
+    const typename PT<BD>::pixel *p0, const typename PT<BD>::pixel *p1, const typename PT<BD>::pixel *p2,
+    const typename PT<BD>::pixel *p3, intptr_t rs, intptr_t rfs, int n, int me_method, int subme, int me_range,
+    const int32_t *__restrict__ pos, const int16_t *__restrict__ par, const int16_t *__restrict__ mvc,
+    const uint16_t *__restrict__ cost_mv, const RsWeight wt0, int32_t *__restrict__ out,
+    int16_t *__restrict__ rpar, int32_t *__restrict__ rinit, int32_t *__restrict__ nevals )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int HDW = 8 / PT<BD>::PPD;
+    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TX = BW / 8, NT = TX * (BH / 4);
+    constexpr int SL = 4 * NT, SH = NT == 8 ? 5 : NT == 4 ? 4 : 3;
+    constexpr int COST_MAX = 1 << 28;
+    const int lane = (int)(threadIdx.x & 63);
+    const int sbase = lane & (64 - SL);
+    const int g = (lane / NT) & 3, u = lane & (NT - 1);
+    const int64_t jo = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> SH;
+    const bool live = jo < n;
+    const int64_t j = live ? jo : n - 1;
+    const int ux = 8 * (u % TX), uy = 4 * (u / TX);
+    const int f = pos[3 * j], bx = pos[3 * j + 1], by = pos[3 * j + 2];
+
+    uint32_t fa[4][HDW];
+    const pixel *fe = fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux;
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+        load_row_u<HDW>( fe + y * fs, fa[y] );
+    const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
+    const pixel *const q0 = p0 + qo, *const q1 = p1 + qo, *const q2 = p2 + qo, *const q3 = p3 + qo;
+    const pixel *const qw = fw + qo;
+
+    const int16_t *p = par + 12 * j;
+    const int mvpx = p[0], mvpy = p[1];
+    const int xmin = p[2], ymin = p[3], xmax = p[4], ymax = p[5];
+    const int i_mvc = min( (int)p[10], SR_MVC );
+    const int16_t *mc = mvc + 2 * SR_MVC * j;
+    const uint16_t *cmx = cost_mv - mvpx, *cmy = cost_mv - mvpy;
+    int nf = 0, nh = 0;                                   // the reference's fpelcmp / get_ref calls
+
+    // mode 0: fpelcmp on p_fref_w + BITS_MVD; 1: COST_MV_HPEL (get_ref + qpel mv cost); 2: fpelcmp
+    // alone.  Group g scores (gx, gy) (not read when !ok); c[k] = group k's cost.
+    auto evalc = [&]( int gx, int gy, int mode, bool ok, int (&c)[4] ) {
+        uint32_t v = 0;
+        if( ok )
+        {
+            if( mode == 1 )
+            {
+                v = tile_cost<BD, false, WGT>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 );
+                if( u == 0 )
+                    v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
+            }
+            else
+            {
+                v = tile_cost<BD, false, false>( fa, qw, qw, qw, qw, rs, 4 * gx, 4 * gy );
+                if( u == 0 && mode == 0 )
+                    v += (uint32_t)cmx[4 * gx] + (uint32_t)cmy[4 * gy];
+            }
+        }
+        v = group_sum<NT>( v );
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            c[k] = (int)__shfl( (int)v, sbase + NT * k );
+    };
+    auto in_range = [&]( int mx, int my ) { return mx >= xmin && mx <= xmax && my >= ymin && my <= ymax; };
+
+    int bmx, bmy, bcost = COST_MAX, bpred_cost = COST_MAX, pmx, pmy;
+    uint32_t pmv, bpred_mv = 0;
+    int c[4];
+    auto upd = [&]( int cc, int mx, int my ) {
+        nf++;
+        if( cc < bcost )
+        {
+            bcost = cc;
+            bmx = mx;
+            bmy = my;
+        }
+    };
+    // the want-th entry of x264_predictor_clip (qpel) / _roundclip (fpel) over the mvc list
+    auto pred = [&]( int want, int &ox, int &oy ) {
+        int cnt = 0;
+        bool found = false;
+        for( int i = 0; i < i_mvc && !found; i++ )
+        {
+            int mx = mc[2 * i], my = mc[2 * i + 1];
+            if( subme < 3 )
+            {
+                mx = (mx + 2) >> 2;
+                my = (my + 2) >> 2;
+            }
+            const uint32_t v = sr_pack( mx, my );
+            if( !v || v == pmv )
+                continue;
+            if( cnt == want )
+            {
+                found = true;
+                ox = subme >= 3 ? sr_clip( mx, 4 * xmin, 4 * xmax ) : sr_clip( mx, xmin, xmax );
+                oy = subme >= 3 ? sr_clip( my, 4 * ymin, 4 * ymax ) : sr_clip( my, ymin, ymax );
+            }
+            cnt++;
+        }
+        return found;
+    };
+    auto nvalid = [&]() {
+        int cnt = 0;
+        for( int i = 0; i < i_mvc; i++ )
+        {
+            int mx = mc[2 * i], my = mc[2 * i + 1];
+            if( subme < 3 )
+            {
+                mx = (mx + 2) >> 2;
+                my = (my + 2) >> 2;
+            }
+            const uint32_t v = sr_pack( mx, my );
+            cnt += v && v != pmv;
+        }
+        return cnt;
+    };
+
+    if( subme >= 3 )
+    {
+        int bpx = sr_clip( mvpx, 4 * xmin, 4 * xmax ), bpy = sr_clip( mvpy, 4 * ymin, 4 * ymax );
+        pmv = sr_pack( bpx, bpy );
+        pmx = (bpx + 2) >> 2;
+        pmy = (bpy + 2) >> 2;
+        evalc( bpx, bpy, 1, true, c );
+        nh++;
+        bpred_cost = c[0];
+        const int pmv_cost = bpred_cost;
+        const int nv = nvalid();
+        if( nv > 0 )
+        {
+            bpred_cost <<= 4;
+            for( int b = 0; b < nv; b += 4 )
+            {
+                int gx = 0, gy = 0;
+                const bool ok = b + g < nv && pred( b + g, gx, gy );
+                evalc( gx, gy, 1, ok, c );
+#pragma unroll
+                for( int k = 0; k < 4; k++ )
+                    if( b + k < nv )
+                    {
+                        nh++;
+                        if( (c[k] << 4) + b + k + 1 < bpred_cost )
+                            bpred_cost = (c[k] << 4) + b + k + 1;
+                    }
+            }
+            if( bpred_cost & 15 )
+                pred( (bpred_cost & 15) - 1, bpx, bpy );
+            bpred_cost >>= 4;
+        }
+        bmx = (bpx + 2) >> 2;
+        bmy = (bpy + 2) >> 2;
+        bpred_mv = sr_pack( bpx, bpy );
+        // COST_MV( bmx, bmy ) of a subpel predictor and the zero vector, scored together
+        const bool sub = bpred_mv & 0x00030003, zero = pmv && (bmx | bmy);
+        evalc( g == 0 ? bmx : 0, g == 0 ? bmy : 0, 0, (g == 0 && sub) || (g == 1 && zero), c );
+        if( sub )
+            upd( c[0], bmx, bmy );
+        else
+            bcost = bpred_cost;
+        if( pmv )
+        {
+            if( zero )
+                upd( c[1], 0, 0 );
+        }
+        else if( pmv_cost < bcost )
+        {
+            bcost = pmv_cost;
+            bmx = bmy = 0;
+        }
+    }
+    else
+    {
+        bmx = pmx = sr_clip( (mvpx + 2) >> 2, xmin, xmax );
+        bmy = pmy = sr_clip( (mvpy + 2) >> 2, ymin, ymax );
+        pmv = sr_pack( bmx, bmy );
+        evalc( bmx, bmy, 2, true, c );
+        nf++;
+        bcost = c[0];
+        const int nv = nvalid();
+        if( nv > 0 )
+        {
+            bcost <<= 4;
+            for( int b = 0; b < nv; b += 4 )
+            {
+                int gx = 0, gy = 0;
+                const bool ok = b + g < nv && pred( b + g, gx, gy );
+                evalc( gx, gy, 0, ok, c );
+#pragma unroll
+                for( int k = 0; k < 4; k++ )
+                    if( b + k < nv )
+                    {
+                        nf++;
+                        if( (c[k] << 4) + b + k + 1 < bcost )
+                            bcost = (c[k] << 4) + b + k + 1;
+                    }
+            }
+            if( bcost & 15 )
+                pred( (bcost & 15) - 1, bmx, bmy );
+            bcost >>= 4;
+        }
+        if( pmv )
+        {
+            evalc( 0, 0, 0, true, c );
+            upd( c[0], 0, 0 );
+        }
+    }
+
+    // the diamond of radius 1 around (cx, cy) in COST_MV_X4's order (0,-1) (0,1) (-1,0) (1,0)
+    auto dia = [&]( int cx, int cy ) {
+        evalc( cx + (g == 2 ? -1 : g == 3 ? 1 : 0), cy + (g == 0 ? -1 : g == 1 ? 1 : 0), 0, true, c );
+    };
+    bool hex = me_method == 1;
+    int i_me_range = me_range;
+    if( me_method == 0 )
+    {
+        bcost <<= 4;
+        int i = i_me_range;
+        do
+        {
+            dia( bmx, bmy );
+            nf += 4;
+            if( (c[0] << 4) + 1 < bcost ) bcost = (c[0] << 4) + 1;
+            if( (c[1] << 4) + 3 < bcost ) bcost = (c[1] << 4) + 3;
+            if( (c[2] << 4) + 4 < bcost ) bcost = (c[2] << 4) + 4;
+            if( (c[3] << 4) + 12 < bcost ) bcost = (c[3] << 4) + 12;
+            if( !(bcost & 15) )
+                break;
+            bmx -= (int32_t)((uint32_t)bcost << 28) >> 30;
+            bmy -= (int32_t)((uint32_t)bcost << 30) >> 30;
+            bcost &= ~15;
+        } while( --i && in_range( bmx, bmy ) );
+        bcost >>= 4;
+    }
+    else if( me_method == 2 )
+    {
+        // UMH (me.c:422-616)
+        auto dia1 = [&]( int cx, int cy ) {
+            dia( cx, cy );
+            upd( c[0], cx, cy - 1 );
+            upd( c[1], cx, cy + 1 );
+            upd( c[2], cx - 1, cy );
+            upd( c[3], cx + 1, cy );
+        };
+        auto thresh = [&]( int v ) { return bcost < (v >> k_psize_shift[IPIX]); };
+        int omx, omy;
+        // CROSS( start, x_max, y_max ) around (omx, omy) (me.c:152-176): slot 2k / 2k+1 = +i / -i
+        auto cross = [&]( int start, int x_max, int y_max ) {
+            const int nhs = x_max > start ? 2 * ((x_max - start + 1) >> 1) : 0;
+            const int nvs = y_max > start ? 2 * ((y_max - start + 1) >> 1) : 0;
+            auto slot = [&]( int sl, int &mx, int &my ) {
+                const bool v = sl >= nhs;
+                const int s2 = v ? sl - nhs : sl;
+                const int d = (start + 2 * (s2 >> 1)) * ((s2 & 1) ? -1 : 1);
+                mx = omx + (v ? 0 : d);
+                my = omy + (v ? d : 0);
+                return sl < nhs + nvs && in_range( mx, my );
+            };
+            for( int b = 0; b < nhs + nvs; b += 4 )
+            {
+                int gx, gy;
+                const bool ok = slot( b + g, gx, gy );
+                evalc( gx, gy, 0, ok, c );
+#pragma unroll
+                for( int k = 0; k < 4; k++ )
+                {
+                    int mx, my;
+                    if( slot( b + k, mx, my ) )
+                        upd( c[k], mx, my );
+                }
+            }
+        };
+        int cross_start = 1;
+        const int ucost1 = bcost;
+        dia1( pmx, pmy );
+        if( pmx | pmy )
+            dia1( 0, 0 );
+        const int ucost2 = bcost;
+        if( (bmx | bmy) && ((bmx - pmx) | (bmy - pmy)) )
+            dia1( bmx, bmy );
+        if( bcost == ucost2 )
+            cross_start = 3;
+        omx = bmx;
+        omy = bmy;
+        bool done = false;
+        if( bcost == ucost2 && thresh( 2000 ) )
+        {
+            // COST_MV_X4( 0,-2, -1,-1, 1,-1, -2,0 ), COST_MV_X4( 2,0, -1,1, 1,1, 0,2 )
+            evalc( omx + (g == 0 ? 0 : g == 1 ? -1 : g == 2 ? 1 : -2), omy + (g == 0 ? -2 : g == 3 ? 0 : -1), 0, true,
+                   c );
+            upd( c[0], omx, omy - 2 );
+            upd( c[1], omx - 1, omy - 1 );
+            upd( c[2], omx + 1, omy - 1 );
+            upd( c[3], omx - 2, omy );
+            evalc( omx + (g == 0 ? 2 : g == 1 ? -1 : g == 2 ? 1 : 0), omy + (g == 0 ? 0 : g == 3 ? 2 : 1), 0, true,
+                   c );
+            upd( c[0], omx + 2, omy );
+            upd( c[1], omx - 1, omy + 1 );
+            upd( c[2], omx + 1, omy + 1 );
+            upd( c[3], omx, omy + 2 );
+            if( bcost == ucost1 && thresh( 500 ) )
+                done = true;
+            else if( bcost == ucost2 )
+            {
+                const int range = (i_me_range >> 1) | 1;
+                cross( 3, range, range );
+                // COST_MV_X4( -1,-2, 1,-2, -2,-1, 2,-1 ), COST_MV_X4( -2,1, 2,1, -1,2, 1,2 )
+                evalc( omx + (g == 0 ? -1 : g == 1 ? 1 : g == 2 ? -2 : 2), omy + (g < 2 ? -2 : -1), 0, true, c );
+                upd( c[0], omx - 1, omy - 2 );
+                upd( c[1], omx + 1, omy - 2 );
+                upd( c[2], omx - 2, omy - 1 );
+                upd( c[3], omx + 2, omy - 1 );
+                evalc( omx + (g == 0 ? -2 : g == 1 ? 2 : g == 2 ? -1 : 1), omy + (g < 2 ? 1 : 2), 0, true, c );
+                upd( c[0], omx - 2, omy + 1 );
+                upd( c[1], omx + 2, omy + 1 );
+                upd( c[2], omx - 1, omy + 2 );
+                upd( c[3], omx + 1, omy + 2 );
+                if( bcost == ucost2 )
+                    done = true;
+                cross_start = range + 2;
+            }
+        }
+        if( !done )
+        {
+            if( i_mvc )
+            {
+                // the adaptive range (me.c:469-519; x264_predictor_difference, common/base.h:248-257)
+                int mvd, denom = 1;
+                if( i_mvc == 1 )
+                    mvd = IPIX == 0 ? 25 : abs( mvpx - mc[0] ) + abs( mvpy - mc[1] );
+                else
+                {
+                    denom = i_mvc - 1;
+                    mvd = 0;
+                    if( IPIX != 0 )
+                    {
+                        mvd = abs( mvpx - mc[0] ) + abs( mvpy - mc[1] );
+                        denom++;
+                    }
+                    for( int i = 0; i < i_mvc - 1; i++ )
+                        mvd += abs( mc[2 * i] - mc[2 * i + 2] ) + abs( mc[2 * i + 1] - mc[2 * i + 3] );
+                }
+                const int sad_ctx = thresh( 1000 ) ? 0 : thresh( 2000 ) ? 1 : thresh( 4000 ) ? 2 : 3;
+                const int mvd_ctx = mvd < 10 * denom ? 0 : mvd < 20 * denom ? 1 : mvd < 40 * denom ? 2 : 3;
+                // range_mul[mvd_ctx][sad_ctx] (me.c:474-480) as 4-bit fields
+                constexpr uint32_t rm[4] = { 0x4433u, 0x4443u, 0x5444u, 0x6544u };
+                const uint32_t row = mvd_ctx == 0 ? rm[0] : mvd_ctx == 1 ? rm[1] : mvd_ctx == 2 ? rm[2] : rm[3];
+                i_me_range = i_me_range * (int)((row >> (4 * sad_ctx)) & 15) >> 2;
+            }
+            cross( cross_start, i_me_range, i_me_range >> 1 );
+            // COST_MV_X4( -2,-2, -2,2, 2,-2, 2,2 )
+            evalc( omx + (g < 2 ? -2 : 2), omy + ((g & 1) ? 2 : -2), 0, true, c );
+            upd( c[0], omx - 2, omy - 2 );
+            upd( c[1], omx - 2, omy + 2 );
+            upd( c[2], omx + 2, omy - 2 );
+            upd( c[3], omx + 2, omy + 2 );
+            // hexagon grid (me.c:527-612): 16 points per ring, range-checked
+            omx = bmx;
+            omy = bmy;
+            int i = 1;
+            do
+            {
+#pragma unroll
+                for( int e = 0; e < 4; e++ )
+                {
+                    // ring points 4e .. 4e+3 (hex4 as 4-bit fields, +4)
+                    constexpr uint32_t hx[2] = { pack_fields( k_hex4x0, 4 ), pack_fields( k_hex4x1, 4 ) };
+                    constexpr uint32_t hy[2] = { pack_fields( k_hex4y0, 4 ), pack_fields( k_hex4y1, 4 ) };
+                    const int gx = omx + (field( hx[e >> 1], 4, 4 * (e & 1) + g ) - 4) * i;
+                    const int gy = omy + (field( hy[e >> 1], 4, 4 * (e & 1) + g ) - 4) * i;
+                    evalc( gx, gy, 0, in_range( gx, gy ), c );
+#pragma unroll
+                    for( int k = 0; k < 4; k++ )
+                    {
+                        const int kx = omx + (field( hx[e >> 1], 4, 4 * (e & 1) + k ) - 4) * i;
+                        const int ky = omy + (field( hy[e >> 1], 4, 4 * (e & 1) + k ) - 4) * i;
+                        if( in_range( kx, ky ) )
+                            upd( c[k], kx, ky );
+                    }
+                }
+            } while( ++i <= i_me_range >> 2 );
+            hex = in_range( bmx, bmy );
+        }
+    }
+    if( hex )
+    {
+        // hexagon (me.c:344-403): COST_MV_X3_DIR( -2,0, -1,2, 1,2 ), COST_MV_X3_DIR( 2,0, 1,-2, -1,-2 )
+        constexpr uint32_t h2x = pack_fields( k_hex2x, 3 ), h2y = pack_fields( k_hex2y, 3 );
+        evalc( bmx + (g == 0 ? -2 : g == 1 ? -1 : g == 2 ? 1 : 2), bmy + (g == 0 || g == 3 ? 0 : 2), 0, true, c );
+        int c2[4];
+        evalc( bmx + (g == 0 ? 1 : -1), bmy - 2, 0, g < 2, c2 );
+        nf += 6;
+        bcost <<= 3;
+        if( (c[0] << 3) + 2 < bcost ) bcost = (c[0] << 3) + 2;
+        if( (c[1] << 3) + 3 < bcost ) bcost = (c[1] << 3) + 3;
+        if( (c[2] << 3) + 4 < bcost ) bcost = (c[2] << 3) + 4;
+        if( (c[3] << 3) + 5 < bcost ) bcost = (c[3] << 3) + 5;
+        if( (c2[0] << 3) + 6 < bcost ) bcost = (c2[0] << 3) + 6;
+        if( (c2[1] << 3) + 7 < bcost ) bcost = (c2[1] << 3) + 7;
+        if( bcost & 7 )
+        {
+            int dir = (bcost & 7) - 2;
+            bmx += field( h2x, 3, dir + 1 ) - 2;
+            bmy += field( h2y, 3, dir + 1 ) - 2;
+            for( int i = (i_me_range >> 1) - 1; i > 0 && in_range( bmx, bmy ); i-- )
+            {
+                // COST_MV_X3_DIR( hex2[dir], hex2[dir+1], hex2[dir+2] )
+                const int d = dir + (g < 3 ? g : 0);
+                evalc( bmx + field( h2x, 3, d ) - 2, bmy + field( h2y, 3, d ) - 2, 0, g < 3, c );
+                nf += 3;
+                bcost &= ~7;
+                if( (c[0] << 3) + 1 < bcost ) bcost = (c[0] << 3) + 1;
+                if( (c[1] << 3) + 2 < bcost ) bcost = (c[1] << 3) + 2;
+                if( (c[2] << 3) + 3 < bcost ) bcost = (c[2] << 3) + 3;
+                if( !(bcost & 7) )
+                    break;
+                dir += (bcost & 7) - 2;
+                dir = field( pack_fields( k_mod6m1, 3 ), 3, dir + 1 );
+                bmx += field( h2x, 3, dir + 1 ) - 2;
+                bmy += field( h2y, 3, dir + 1 ) - 2;
+            }
+        }
+        bcost >>= 3;
+        // square refine (me.c:404-418)
+        bcost <<= 4;
+        dia( bmx, bmy );
+        if( (c[0] << 4) + 1 < bcost ) bcost = (c[0] << 4) + 1;
+        if( (c[1] << 4) + 2 < bcost ) bcost = (c[1] << 4) + 2;
+        if( (c[2] << 4) + 3 < bcost ) bcost = (c[2] << 4) + 3;
+        if( (c[3] << 4) + 4 < bcost ) bcost = (c[3] << 4) + 4;
+        evalc( bmx + (g < 2 ? -1 : 1), bmy + ((g & 1) ? 1 : -1), 0, true, c );
+        if( (c[0] << 4) + 5 < bcost ) bcost = (c[0] << 4) + 5;
+        if( (c[1] << 4) + 6 < bcost ) bcost = (c[1] << 4) + 6;
+        if( (c[2] << 4) + 7 < bcost ) bcost = (c[2] << 4) + 7;
+        if( (c[3] << 4) + 8 < bcost ) bcost = (c[3] << 4) + 8;
+        nf += 8;
+        constexpr uint32_t s1x = pack_fields( k_sq1x, 2 ), s1y = pack_fields( k_sq1y, 2 );
+        bmx += field( s1x, 2, bcost & 15 ) - 1;
+        bmy += field( s1y, 2, bcost & 15 ) - 1;
+        bcost >>= 4;
+    }
+
+    // -> qpel mv (me.c:774-789)
+    int mx, my, cst, cmv;
+    if( subme < 3 )
+    {
+        cmv = (int)cmx[4 * bmx] + (int)cmy[4 * bmy];
+        cst = bcost + (sr_pack( bmx, bmy ) == pmv ? cmv : 0);
+        mx = 4 * bmx;
+        my = 4 * bmy;
+    }
+    else
+    {
+        if( bpred_cost < bcost )
+        {
+            mx = (int16_t)(bpred_mv & 0xffff);
+            my = (int16_t)(bpred_mv >> 16);
+        }
+        else
+        {
+            mx = 4 * bmx;
+            my = 4 * bmy;
+        }
+        cst = min( bpred_cost, bcost );
+        cmv = (int)cmx[mx] + (int)cmy[my];
+    }
+    if( live && lane == sbase )
+    {
+        *(int4 *)(out + 4 * j) = make_int4( cst, mx, my, cmv );
+        if( rpar )
+        {
+            *(int4 *)(rpar + 8 * j) = make_int4( (int)sr_pack( mx, my ), (int)sr_pack( mvpx, mvpy ),
+                                                 (int)sr_pack( p[6], p[7] ), (int)sr_pack( p[8], p[9] ) );
+            rinit[j] = cst;
+        }
+        if( nevals )
+        {
+            nevals[2 * j] = nf | (nh << 16);
+            if( subme < 2 )
+                nevals[2 * j + 1] = 0;                    // no refine_subpel (me.c:792)
+        }
+    }
+}
+
+template <int BD>
+hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                 const typename PT<BD>::pixel *fw, const typename PT<BD>::pixel *const planes[4],
+                                 intptr_t rs, intptr_t rfs, int i_pixel, int me_method, int subme, int me_range,
+                                 const int32_t *pos, const int16_t *par, const int16_t *mvc, const uint16_t *cost_mv,
+                                 int n, int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *xe,
+                                 hipStream_t stream )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    if( i_pixel < 0 || i_pixel > 3 || me_method < 0 || me_method > 2 || subme < 1 || subme > 11 || me_range < 4 ||
+        me_range > 64 || ((uintptr_t)out & 15) )
+        return hipErrorInvalidValue;
+    RsExt<BD> ext;
+    int mode;
+    if( rs_ext<BD>( xe, ext, mode ) != hipSuccess )
+        return hipErrorInvalidValue;
+    const bool refine = subme >= 2;
+    void *buf = nullptr;
+    int16_t *rpar = nullptr;
+    int32_t *rinit = nullptr;
+    hipError_t e = hipSuccess;
+    if( refine )
+    {
+        if( (e = scratch_alloc( &buf, (size_t)n * 20 + 16, stream )) != hipSuccess )
+            return e;
+        rpar = (int16_t *)buf;
+        rinit = (int32_t *)((char *)buf + (size_t)n * 16);
+    }
+    const int64_t lanes = (int64_t)n * 4 * (pix_w( i_pixel ) / 8) * (pix_h( i_pixel ) / 4);
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+#define SR_GO( I, W )                                                                                             \
+    hipLaunchKernelGGL( ( me_search_ref_kernel<BD, I, W> ), g, blk, 0, stream, fenc, fs, ffs, fw, planes[0],      \
+                        planes[1], planes[2], planes[3], rs, rfs, n, me_method, subme, me_range, pos, par, mvc,     \
+                        cost_mv, ext.wt[0], out, rpar, rinit, nevals )
+#define SR_CASE( I )                                                                                              \
+    case I:                                                                                                       \
+        if( ext.wt[0].on ) { SR_GO( I, true ); } else { SR_GO( I, false ); }                                      \
+        break;
+    switch( i_pixel )
+    {
+        SR_CASE( 0 ) SR_CASE( 1 ) SR_CASE( 2 ) SR_CASE( 3 )
+        default: break;
+    }
+#undef SR_CASE
+#undef SR_GO
+    e = hipGetLastError();
+    if( e == hipSuccess && refine )
+        e = refine_launch<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, 0, 0, pos, rpar, rinit, cost_mv, n, out,
+                               nevals ? nevals + 1 : nullptr, 2, xe, stream );
+    if( buf )
+    {
+        const hipError_t ef = hipFreeAsync( buf, stream );
+        if( e == hipSuccess )
+            e = ef;
+    }
+    return e;
+}
+template hipError_t launch_me_search_ref<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, const uint8_t *const[4],
+                                             intptr_t, intptr_t, int, int, int, int, const int32_t *, const int16_t *,
+                                             const int16_t *, const uint16_t *, int, int32_t *, int32_t *,
+                                             const x264hip_refine_ext_t *, hipStream_t );
+template hipError_t launch_me_search_ref<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *,
+                                              const uint16_t *const[4], intptr_t, intptr_t, int, int, int, int,
+                                              const int32_t *, const int16_t *, const int16_t *, const uint16_t *, int,
+                                              int32_t *, int32_t *, const x264hip_refine_ext_t *, hipStream_t );
 
 template hipError_t launch_me_refine_subpel<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *const[4],
                                                 intptr_t, intptr_t, int, int, int, int, const int32_t *,

@@ -181,6 +181,88 @@ template hipError_t launch_ssim_wxh<8>( const uint8_t *, intptr_t, const uint8_t
 template hipError_t launch_ssim_wxh<10>( const uint16_t *, intptr_t, const uint16_t *, intptr_t, int, int, float *,
                                          hipStream_t );
 
+// The encoder's form (encoder.c:2516-2528): x264_pixel_ssim_wxh once per filtered MB-row band,
+// each band's float independent of the others (the encoder adds them in double).  One
+// workgroup per (band, frame) walks the band's window rows as the reference does, keeping its
+// last two rows of 4x4 block sums in LDS (sum0 / sum1 of pixel.c:697-712): the workgroup
+// computes a block row's sums, then every group's ssim_end4, then lane 0 adds the row's groups
+// in order into the band's float -- the reference's accumulation, bit-identical, with the
+// bands (68 per 1080p frame) running side by side instead of in one chain.
+template <int BD>
+__global__ __launch_bounds__( 256 ) void ssim_bands_kernel( const typename PT<BD>::pixel *__restrict__ p1,
+                                                            intptr_t s1, intptr_t f1,
+                                                            const typename PT<BD>::pixel *__restrict__ p2,
+                                                            intptr_t s2, intptr_t f2, int nx,
+                                                            const int2 *__restrict__ bands, int nbands,
+                                                            float *__restrict__ out )
+{
+    extern __shared__ int4 ssim_lds[];
+    const int b = blockIdx.x, f = blockIdx.y;
+    const int2 bd = bands[b];
+    const int nz = bd.y >> 2, ng = (nx - 1 + 3) / 4;
+    float *grp = (float *)(ssim_lds + 2 * nx);             // (rows by arithmetic: an array of the two row
+                                                            // pointers made them generic, flat accesses)
+    const typename PT<BD>::pixel *a0 = p1 + f * f1 + (intptr_t)bd.x * s1, *b0 = p2 + f * f2 + (intptr_t)bd.x * s2;
+    float ssim = 0.0f;
+    for( int z = 0; z < nz; z++ )
+    {
+        int4 *cur = ssim_lds + (z & 1) * nx;
+        for( int x = threadIdx.x; x < nx; x += blockDim.x )
+        {
+            const typename PT<BD>::pixel *a = a0 + (intptr_t)4 * z * s1 + 4 * x, *c = b0 + (intptr_t)4 * z * s2 + 4 * x;
+            uint32_t t1 = 0, t2 = 0, ss = 0, s12 = 0;
+#pragma unroll
+            for( int y = 0; y < 4; y++ )
+#pragma unroll
+                for( int k = 0; k < 4; k++ )
+                {
+                    const uint32_t u = a[y * s1 + k], v = c[y * s2 + k];
+                    t1 += u;
+                    t2 += v;
+                    ss += u * u + v * v;
+                    s12 += u * v;
+                }
+            cur[x] = make_int4( (int)t1, (int)t2, (int)ss, (int)s12 );
+        }
+        __syncthreads();
+        if( z == 0 )
+            continue;
+        for( int gi = threadIdx.x; gi < ng; gi += blockDim.x )
+        {
+            const int x = 4 * gi;
+            // ssim_end4( sum0 = this row, sum1 = the row above ) (pixel.c:708-709)
+            grp[gi] = ssim_end4_dev<BD>( cur + x, ssim_lds + ((z - 1) & 1) * nx + x, min( 4, nx - x - 1 ) );
+        }
+        __syncthreads();
+        if( threadIdx.x == 0 )
+            for( int gi = 0; gi < ng; gi++ )
+                ssim += grp[gi];
+        __syncthreads();
+    }
+    if( threadIdx.x == 0 )
+        out[(intptr_t)f * nbands + b] = ssim;
+}
+
+template <int BD>
+hipError_t launch_ssim_bands( const typename PT<BD>::pixel *p1, intptr_t s1, intptr_t f1,
+                              const typename PT<BD>::pixel *p2, intptr_t s2, intptr_t f2, int width,
+                              const int32_t *bands, int nbands, int nframes, float *out, hipStream_t stream )
+{
+    const int nx = width >> 2;
+    if( nbands <= 0 || nframes <= 0 )
+        return hipSuccess;
+    if( nx > 2048 )
+        return hipErrorInvalidValue;
+    const size_t lds = sizeof( int4 ) * 2 * (size_t)nx + sizeof( float ) * (size_t)((nx + 2) / 4 + 1);
+    hipLaunchKernelGGL( ssim_bands_kernel<BD>, dim3( (unsigned)nbands, (unsigned)nframes ), dim3( 256 ), lds, stream,
+                        p1, s1, f1, p2, s2, f2, nx, (const int2 *)bands, nbands, out );
+    return hipGetLastError();
+}
+template hipError_t launch_ssim_bands<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t, int,
+                                          const int32_t *, int, int, float *, hipStream_t );
+template hipError_t launch_ssim_bands<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
+                                           int, const int32_t *, int, int, float *, hipStream_t );
+
 // the per-call table entries' kernels: ssim_4x4x2_core of one block pair (8 ints out) and
 // ssim_end4 of staged sum rows
 template <int BD>
