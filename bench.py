@@ -860,7 +860,76 @@ def rates_refine(x, a, world, mbw, mbh, F):
                     leg + "_satd_calls_per_part": nsatd / n, leg + "_chroma_calls_per_part": nchroma / n,
                     leg + "_moved_frac": moved, leg + "_qpel_frac": qpel,
                     leg + "_valu_frac": work / (ev_ms * 1e-3) / VALU_LANE_OPS})
+    res.update(rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes, ext, cm, cm_d, span))
     del hv, planes, dev, nvd
+    return res
+
+
+def search_params(mbw, mbh, F, i_pixel, seed=7, motion=(13, 10)):
+    """x264_me_search_ref inputs per partition of F frames (x264hip_*_me_search_ref's par / mvc):
+    mv limits of analyse.c:330-349 (mv_limit_fpel with the 6-pixel fpel border); a synthetic
+    predictor -- x264's mvp and mvc come from the already-coded neighbours (common/mvpred.c), which a
+    frame-batched search does not have, so mvp = the true motion +- 8 qpel and four candidates
+    (two near the motion, one at zero, one far) stand in for them."""
+    rs = np.random.default_rng(seed)
+    parts = [(0, 0)] if i_pixel == 0 else [(0, 0), (8, 0), (0, 8), (8, 8)]
+    n1 = F * mbw * mbh
+    mb = np.repeat(np.arange(n1), len(parts))
+    n = len(mb)
+    mbx, mby = (mb % (mbw * mbh)) % mbw, (mb % (mbw * mbh)) // mbw
+    pos = np.stack([mb // (mbw * mbh), 16 * mbx + np.tile([p[0] for p in parts], n1),
+                    16 * mby + np.tile([p[1] for p in parts], n1)], 1).astype(np.int32)
+    par = np.zeros((n, 12), np.int16)
+    par[:, 0] = motion[0] + rs.integers(-8, 9, n)
+    par[:, 1] = motion[1] + rs.integers(-8, 9, n)
+    par[:, 6], par[:, 7] = 4 * (-16 * mbx - 24), 4 * (-16 * mby - 24)
+    par[:, 8], par[:, 9] = 4 * (16 * (mbw - 1 - mbx) + 24), 4 * (16 * (mbh - 1 - mby) + 24)
+    par[:, 2], par[:, 3] = (par[:, 6] >> 2) + 6, (par[:, 7] >> 2) + 6
+    par[:, 4], par[:, 5] = (par[:, 8] >> 2) - 6, (par[:, 9] >> 2) - 6
+    par[:, 10] = 4
+    mvc = np.zeros((n, 14, 2), np.int16)
+    mvc[:, 0, 0], mvc[:, 0, 1] = motion[0] + rs.integers(-6, 7, n), motion[1] + rs.integers(-6, 7, n)
+    mvc[:, 1, 0], mvc[:, 1, 1] = motion[0] + rs.integers(-16, 17, n), motion[1] + rs.integers(-16, 17, n)
+    mvc[:, 3, 0], mvc[:, 3, 1] = rs.integers(-120, 121, n), rs.integers(-80, 81, n)
+    return pos, par, mvc
+
+
+def rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes, ext, cm, cm_d, span):
+    """x264_me_search_ref at full resolution (x264hip_*_me_search_ref: predictors, integer search,
+    refine_subpel with chroma ME) as x264's default preset runs it on P slices -- HEX, subme 7,
+    me_range 16 (common/base.c:439-441) -- over every 16x16 MB (search16_hex_*) and every 8x8
+    partition (search8_hex_*) of the F pairs of rates_refine's quarter-pel sequence, and UMH
+    (--me umh, the slower presets) on 16x16 (search16_umh_*).  Rates in partitions/s; the
+    candidates the reference evaluates (its fpelcmp / get_ref / refine calls, counted by the
+    kernels) give the absdiff rate against the v_sad_u8 peak."""
+    res = {"search_workload": "rates_refine's sequence, synthetic mvp / mvc (search_params), subme 7, me_range 16, "
+                              "b_chroma_me on, the whole x264_me_search_ref per launch"}
+    for leg, i_pixel, me in (("search16_hex", 0, 1), ("search16_umh", 0, 2), ("search8_hex", 3, 1)):
+        pos, par, mvc = search_params(mbw, mbh, F, i_pixel)
+        n = len(pos)
+        pos_d, par_d, mvc_d = (torch.from_numpy(v).cuda() for v in (pos, par, mvc))
+        out = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+        ne = torch.empty((n, 2), dtype=torch.int32, device="cuda")
+
+        def step(i_pixel=i_pixel, me=me, pos_d=pos_d, par_d=par_d, mvc_d=mvc_d, out=out, ne=ne):
+            x.me_search_ref(dev[1:], origin, stride, dev[:-1], planes, origin, stride, i_pixel, me, 7, 16, pos_d,
+                            par_d, mvc_d, (cm_d, span), out=out, fenc_frame_stride=fstride,
+                            ref_frame_stride=fstride, nevals=ne, ext=ext)
+        wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
+        nf = int((ne[:, 0] & 0xFFFF).sum().item())
+        nh = int((ne[:, 0] >> 16).sum().item())
+        rsad = int((ne[:, 1] & 0xFFFF).sum().item())
+        rsatd = int(((ne[:, 1] >> 16) & 0xFF).sum().item())
+        rchroma = int((ne[:, 1] >> 24).sum().item())
+        px = 256 if i_pixel == 0 else 64
+        cands = nf + nh + rsad + rsatd
+        res.update({leg + "_partitions_per_s": world * a.steps * n / wall, leg + "_launch_ms": ev_ms,
+                    leg + "_partitions_per_launch": n, leg + "_fpel_calls_per_part": nf / n,
+                    leg + "_hpel_calls_per_part": nh / n, leg + "_refine_sad_per_part": rsad / n,
+                    leg + "_refine_satd_per_part": rsatd / n, leg + "_refine_chroma_per_part": rchroma / n,
+                    leg + "_candidates_per_s": world * a.steps * cands / wall,
+                    leg + "_absdiff_frac": cands * px / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF,
+                    leg + "_mv_found_frac": ((out[:, 1] == 13) & (out[:, 2] == 10)).float().mean().item()})
     return res
 
 
@@ -1134,6 +1203,38 @@ def cpu_lookahead(orc, planes, origin, stride, mbw, mbh, nthr, bounded):
     return res
 
 
+def cpu_search(orc, mbw, mbh, nthr, bounded):
+    """The oracle's x264_me_search_ref (HEX, subme 7, chroma ME: rates_search's search16_hex leg) on
+    one pair of rates_refine's quarter-pel sequence, on one thread and on the CPU share's threads
+    (a frame's MB rows split over them; ctypes releases the GIL in the oracle)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from x264hip import synth
+    W, H = mbw * 16, mbh * 16
+    luma, stride, origin, nv, cs, co = synth.make_subpel_sequence(2, W, H, 8)
+    ref, fenc = luma[0].ravel(), luma[1].ravel()
+    planes = [ref] + [h.ravel() for h in orc.frame_filter(8, ref, origin, stride, W, H)]
+    pos, par, mvc = search_params(mbw, mbh, 1, 0)
+    par_c = np.ascontiguousarray(par)
+    span = 16384
+    i = np.arange(-span, span + 1)
+    logs = np.where(i == 0, 0.718, 2.0 * np.log2(np.abs(i) + 1) + 1.718)
+    cm = np.minimum((4 * logs + 0.5).astype(np.int64), 65535).astype(np.uint16)
+    ext = orc.refine_ext(1, 1)
+
+    def rows(r0, r1):
+        sel = slice(r0 * mbw, r1 * mbw)
+        return orc.me_search_ref(8, fenc, origin, stride, planes, ref, origin, stride, 0, 1, 7, 16, pos[sel, 1:],
+                                 par_c[sel], mvc[sel], cm, span, ext=ext, fenc_c=[nv[1].ravel()], fc_origin=co,
+                                 fcs=cs, ref_c=[nv[0].ravel()], rc_origin=co, rcs=cs)
+    res = {"search16_hex_partitions_per_s_1t": bounded(lambda: rows(0, 4) and 1, 4 * mbw)[0]}
+    pool = ThreadPoolExecutor(nthr)
+    cuts = [(mbh * k // nthr, mbh * (k + 1) // nthr) for k in range(nthr)]
+    res["search16_hex_partitions_per_s"] = bounded(lambda: list(pool.map(lambda c: rows(*c), cuts)) and 1,
+                                                   mbw * mbh)[0]
+    pool.shutdown()
+    return res
+
+
 def cpu_baseline(planes, origin, stride, mbw, mbh, R, seconds):
     """The oracle (kind "port": reference C kernels restated, -O3 -march=x86-64-v3) on the
     host cores, each leg time-bounded: the headline full-search tables (value: the box's
@@ -1199,6 +1300,7 @@ def cpu_baseline(planes, origin, stride, mbw, mbh, R, seconds):
         res[key] = bounded(lambda n=n: orc.subpel_list_mt("satd", 3, fenc, stride, sp_planes, origin, stride, fo,
                                                           qxy, n)[1], len(fo))[0]
     res.update(cpu_lookahead(orc, planes, origin, stride, mbw, mbh, nthr, bounded))
+    res.update(cpu_search(orc, mbw, mbh, nthr, bounded))
     return {"value": me_rate, "unit": "SAD16x16 candidates/s", "cores": me_used, "kind": "port",
             "cpu_model": cpu_model(), "cpus_visible": share,
             "sample": "%d full 1080p frames (%d candidates) of the same workload, %d threads, %.1f s wall; "
