@@ -36,6 +36,151 @@ SAD_PEAK_ABSDIFF = 2 * VALU_LANE_OPS          # 157.3 T absdiff/s
 HBM_PEAK = 8.0e12
 
 
+def workload_2160p(x, a, world, rank, pg_world, rank_dev):
+    """configs[3] as its own bench line (--workload 2160p): one 2160p frame per GPU per step, frame-
+    per-GPU across the node (rank r encodes frames of its own shard; no collective on the data
+    path).  A step = the new frame's upload from pinned host memory on a copy stream (overlapped
+    with the previous step's kernels), its half-pel planes (it is the next step's reference),
+    the full-search SAD table (range R) against the previous frame and its decision
+    (me_esa_argmin over the whole table: the exhaustive search of me.c:618-631), refine_subpel at
+    subme 7 (two hpel SAD diamonds, the SATD re-score, two qpel SATD diamonds: x264's default
+    subme) from the decisions, and the fused 4x4 DCT + quant.  value = every rank's candidates
+    (the table's (2R+1)^2 per MB + the refine's SAD / SATD calls, counted by the kernel) over
+    the max-over-ranks wall of the timed steps, H2D included."""
+    from x264hip import synth, dist as xd
+    W, H, R = 3840, 2160, a.range
+    mbw, mbh = W // 16, H // 16
+    nmb = mbw * mbh
+    nf = 8
+    p0, _ = xd.frame_shard(world * nf, world, rank)
+    planes, stride, origin = synth.make_sequence(nf + 1, W, H, 8, start=p0)
+    fsz = planes[0].size
+    host = torch.from_numpy(planes).pin_memory()
+    del planes
+    ring = torch.empty((3,) + tuple(host.shape[1:]), dtype=torch.uint8, device="cuda")
+    hp = [[torch.empty_like(ring[0:1]) for _ in range(3)] for _ in range(3)]
+    table = torch.empty((1, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
+    par, init, cm, span = tesa_params(mbw, mbh, 1, R, centre=(0, 0))
+    par_d, init_d = torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda()
+    cm_d = torch.from_numpy(cm.view(np.int16)).cuda()
+    dec = torch.empty((nmb, 3), dtype=torch.int32, device="cuda")
+    mb = np.arange(nmb)
+    mbx, mby = mb % mbw, mb // mbw
+    pos_d = torch.from_numpy(np.stack([0 * mb, 16 * mbx, 16 * mby], 1).astype(np.int32)).cuda()
+    rpar = np.zeros((nmb, 8), np.int16)
+    rpar[:, 4], rpar[:, 5] = 4 * (-16 * mbx - 24), 4 * (-16 * mby - 24)
+    rpar[:, 6], rpar[:, 7] = 4 * (16 * (mbw - 1 - mbx) + 24), 4 * (16 * (mbh - 1 - mby) + 24)
+    rpar_d = torch.from_numpy(rpar).cuda()
+    rout = torch.empty((nmb, 4), dtype=torch.int32, device="cuda")
+    ne = torch.empty(nmb, dtype=torch.int32, device="cuda")
+    flat = [16] * 64
+    q4m, q4b, _, _ = x.cqm_init(8, [flat] * 8)
+    mf4 = torch.from_numpy(q4m[1, 26].copy()).cuda()
+    bs4 = torch.from_numpy(q4b[1, 26].copy()).cuda()
+    dct = torch.empty((nmb, 256), dtype=torch.int16, device="cuda")
+    nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
+
+    def search(cur, ref):
+        x.me_search_full(cur, origin, stride, ref, origin, stride, mbw, mbh, 1, R, table=table,
+                         fenc_frame_stride=fsz, ref_frame_stride=fsz)
+
+    def frame(c, r):
+        """the compute of one frame: ring slot c against slot r (r's hpel planes already built)"""
+        cur, ref = ring[c:c + 1], ring[r:r + 1]
+        x.hpel_filter(cur, origin, stride, W, H, outs=hp[c])
+        search(cur, ref)
+        x.me_esa_argmin(table, R, R, par_d, init_d, (cm_d, span), out=dec)
+        rpar_d[:, 0:2] = (dec[:, 1:3] * 4).to(torch.int16)
+        x.me_refine_subpel(cur, origin, stride, [ref] + hp[r], origin, stride, x.PIXEL_16x16, 7, pos_d, rpar_d,
+                           dec[:, 0].contiguous(), (cm_d, span), out=rout, fenc_frame_stride=fsz,
+                           ref_frame_stride=fsz, nevals=ne)
+        x.mb_dct_quant(4, cur, origin, stride, ref, origin, stride, mbw, mbh, 1, mf4, bs4, dct=dct, nz=nz,
+                       fenc_frame_stride=fsz, pred_frame_stride=fsz)
+
+    # the refine's candidates per frame pair of the shard (the same pairs the timed steps cycle)
+    ring[0].copy_(host[0])
+    x.hpel_filter(ring[0:1], origin, stride, W, H, outs=hp[0])
+    rcands = []
+    for i in range(nf):
+        c, r = (i + 1) % 3, i % 3
+        ring[c].copy_(host[i + 1])
+        frame(c, r)
+        rcands.append(int((ne & 0xFFFF).sum().item()) + int(((ne >> 16) & 0xFF).sum().item()))
+    cand_frame = nmb * (2 * R + 1) ** 2 + float(np.mean(rcands))
+
+    comp, copy = torch.cuda.current_stream(), torch.cuda.Stream()
+    done = [torch.cuda.Event() for _ in range(3)]
+    ready = [torch.cuda.Event() for _ in range(3)]
+    state = {"n": 0}
+
+    def step():
+        n = state["n"]
+        c, r = (n + 1) % 3, n % 3
+        with torch.cuda.stream(copy):                 # upload frame n+1 while frame n's kernels may still run
+            copy.wait_event(done[c])
+            ring[c].copy_(host[(n + 1) % (nf + 1)], non_blocking=True)
+            ready[c].record(copy)
+        comp.wait_event(ready[c])
+        frame(c, r)
+        done[r].record(comp)
+        state["n"] = n + 1
+    torch.cuda.synchronize()
+    ring[0].copy_(host[0])
+    x.hpel_filter(ring[0:1], origin, stride, W, H, outs=hp[0])
+    ready[0].record()
+    for ev in done:
+        ev.record()
+    wall, ev_ms = timed(step, a.steps, a.warmup, world)
+    value = world * a.steps * cand_frame / wall
+    # the dominant kernel alone (the SAD table of one 2160p frame), events on its stream
+    _, s_ms = timed(lambda: search(ring[1:2], ring[0:1]), a.steps, a.warmup, world)
+    absd = nmb * (2 * R + 1) ** 2 * 256
+    roof = {"kernel": "me_full_sad16_v7_kernel<%d, %d>" % (R, x.me_table_pitch(R) // 4), "bound": "valu",
+            "achieved": absd / (s_ms * 1e-3) / 1e12, "peak": SAD_PEAK_ABSDIFF / 1e12,
+            "unit": "T byte-absdiff/s (algorithmic: 256 per 16x16 candidate)",
+            "frac": absd / (s_ms * 1e-3) / SAD_PEAK_ABSDIFF, "traffic": None, "launch_ms": s_ms,
+            "algorithmic_bytes_per_launch": 2 * nmb * 256 + nmb * (2 * R + 1) ** 2 * 2}
+    out = {
+        "metric": "SAD+SATD candidate-MVs/sec + DCT+quant blocks/sec, 1080p, 1/2/4/8 GPU",
+        "value": value,
+        "unit": "candidate MVs/s (SAD16x16 full-search table + refine_subpel SAD/SATD calls)",
+        "n_gpus": pg_world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": wall / a.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "configs[3]: 3840x2160 luma, full-search ME range %d (SAD table + decision) + "
+                               "refine_subpel subme 7 (SAD/SATD) + 4x4 DCT/quant per frame, one frame per GPU "
+                               "per step streamed from pinned host memory (H2D in the timed region)" % R,
+                   "frames_per_step_per_gpu": 1, "mbs_per_frame": nmb,
+                   "candidates_per_mb": cand_frame / nmb, "table_candidates_per_mb": (2 * R + 1) ** 2,
+                   "refine_candidates_per_frame": float(np.mean(rcands)), "upload_bytes_per_frame": int(fsz),
+                   "parallelism": "frame-per-GPU x%d" % world, "world_size": pg_world, "rank_devices": rank_dev,
+                   "dist_backend": (os.environ.get("X264HIP_DIST_BACKEND", "nccl") if world > 1 else None)},
+        "roofline": roof,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_lib as orc  # cpu_baseline leg only
+        f0, f1 = host[1].numpy().ravel(), host[0].numpy().ravel()
+        try:
+            share = len(os.sched_getaffinity(0))
+        except AttributeError:
+            share = os.cpu_count() or 1
+        nthr = min(16, share)
+        band = 16                                     # MB rows of the sample per call
+        t0, calls = time.perf_counter(), 0
+        while True:
+            orc.me_search_full_mt(f0, origin, stride, f1, origin, stride, mbw, band, R, nthr)
+            calls += 1
+            if time.perf_counter() - t0 >= a.cpu_seconds:
+                break
+        dt = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": calls * mbw * band * (2 * R + 1) ** 2 / dt, "unit": "SAD16x16 candidates/s",
+                               "cores": nthr, "kind": "port", "cpu_model": cpu_model(),
+                               "sample": "%d calls of the full search over %d of the frame's %d MB rows, %d "
+                                         "threads, %.1f s" % (calls, band, mbh, nthr, dt)}
+    del ring, hp, table, host
+    return out
+
+
 def parse():
     ap = argparse.ArgumentParser()
     # N ranks, one per GPU: started here as child processes when no launcher set WORLD_SIZE
@@ -59,6 +204,9 @@ def parse():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--range", type=int, default=16)
+    # configs[1] (the default headline) or configs[3]: a 2160p frame per GPU per step, full search +
+    # refine_subpel + DCT/quant, the new frame streamed from pinned host memory (workload_2160p)
+    ap.add_argument("--workload", choices=("1080p", "2160p"), default="1080p")
     ap.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     ap.add_argument("--no-extra", action="store_true", help="skip the configs[2] side rates")
     ap.add_argument("--cpu-seconds", type=float, default=1.5, help="wall-clock bound of the CPU sample")
@@ -207,6 +355,14 @@ def main():
     x.init(torch.cuda.current_device())
     pg_world, rank_dev = world_devices(world)
     from x264hip import synth
+    if a.workload == "2160p":
+        out = workload_2160p(x, a, world, rank, pg_world, rank_dev)
+        if rank == 0:
+            print(json.dumps(out))
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return
 
     W, H, R, F = a.width, a.height, a.range, a.frames
     mbw, mbh = (W + 15) // 16, (H + 15) // 16

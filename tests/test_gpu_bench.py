@@ -67,3 +67,29 @@ def test_bench_two_ranks_gloo():
     assert d["ms_per_step"] * d["steps"] * 1e-3 < wall
     cands = 2 * c["frames_per_step_per_gpu"] * c["mbs_per_frame"] * c["candidates_per_mb"]
     assert d["value"] == pytest.approx(cands / (d["ms_per_step"] * 1e-3), rel=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gpus", [1, 2])
+def test_bench_2160p_workload(gpus):
+    """bench.py --workload 2160p (configs[3]: a 2160p frame per GPU per step, full search + refine +
+    DCT/quant, H2D in the timed region): one line, config.workload = configs[3], value = the ranks'
+    candidates per step over the step time; with --gpus 2 the two ranks share the box's GPU over
+    gloo (the path the driver's 8-GPU scaling run takes over RCCL)."""
+    env = dict(os.environ, X264HIP_DIST_BACKEND="gloo")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--workload", "2160p", "--gpus", str(gpus),
+                        "--steps", "3", "--warmup", "2", "--cpu-seconds", "0.3"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    c = d["config"]
+    assert c["workload"].startswith("configs[3]") and d["n_gpus"] == gpus and c["world_size"] == gpus
+    assert c["candidates_per_mb"] > c["table_candidates_per_mb"] and c["mbs_per_frame"] == 240 * 135
+    cands = gpus * c["frames_per_step_per_gpu"] * c["mbs_per_frame"] * c["candidates_per_mb"]
+    assert d["value"] == pytest.approx(cands / (d["ms_per_step"] * 1e-3), rel=1e-3)
+    assert 0 < d["roofline"]["frac"] < 1
+    assert ("cpu_baseline" in d) == (gpus == 1)
