@@ -74,3 +74,4 @@ def test_refine_subpel_args(hip):
         with pytest.raises(RuntimeError):
             hip.me_refine_subpel(p, 32 * 256 + 32, 256, [p, p, p, p], 32 * 256 + 32, 256, i_pixel, subme, pos, par,
                                  t[:1], (t.view(torch.int16), 0))
+

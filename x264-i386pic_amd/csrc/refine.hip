@@ -305,7 +305,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     int bcost = init_cost[j];
     const bool qsatd = subme > 1;                         // mbcmp_unaligned (encoder.c:1411-1413)
     int nsad = 0, nsatd = 0, nchroma = 0;                 // the reference's fpelcmp / mbcmp calls
-    auto count = [&]( bool satd, int k ) {
+    auto count = [&]( bool satd, int k ) __attribute__( ( always_inline ) ) {
         if( satd )
             nsatd += k;
         else
@@ -314,7 +314,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
 
     // one candidate per group: group g scores (mx[g], my[g]); every lane gets the four costs
     // (pixel cost + p_cost_mvx[mx] + p_cost_mvy[my])
-    auto eval4 = [&]( const int (&mx)[4], const int (&my)[4], bool satd, int (&c)[4] ) {
+    auto eval4 = [&]( const int (&mx)[4], const int (&my)[4], bool satd, int (&c)[4] ) __attribute__( ( always_inline ) ) {
         // (the group's candidate by selects: indexing the arrays with the lane's group put them
         // in scratch memory)
         const int gx = g == 0 ? mx[0] : g == 1 ? mx[1] : g == 2 ? mx[2] : mx[3];
@@ -330,7 +330,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         for( int k = 0; k < 4; k++ )
             c[k] = (int)__shfl( (int)v, sbase + NT * k );
     };
-    auto eval1 = [&]( int mx, int my, bool satd ) {
+    auto eval1 = [&]( int mx, int my, bool satd ) __attribute__( ( always_inline ) ) {
         const int m4x[4] = { mx, mx, mx, mx }, m4y[4] = { my, my, my, my };
         int c[4];
         eval4( m4x, m4y, satd, c );
@@ -340,7 +340,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     // the order (0, -st), (0, +st), (-st, 0), (+st, 0) -- st = 0: the centre in every group: U in
     // cu, V in cv.  (The group's candidate by arithmetic: the selects of eval4 became an indexed
     // scratch load here.)
-    auto evalc4 = [&]( int ox, int oy, int st, int (&cu)[4], int (&cv)[4] ) {
+    auto evalc4 = [&]( int ox, int oy, int st, int (&cu)[4], int (&cv)[4] ) __attribute__( ( always_inline ) ) {
         const int gx = ox + (g == 2 ? -st : g == 3 ? st : 0);
         const int gy = oy + (g == 0 ? -st : g == 1 ? st : 0);
         uint32_t vu = 0, vv = 0;
@@ -385,7 +385,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         }
     };
     // COST_MV_SATD's chroma branch (me.c:833-861) on a luma cost c against bcost
-    auto add_chroma = [&]( int c, int cu, int cv, int bc ) {
+    auto add_chroma = [&]( int c, int cu, int cv, int bc ) __attribute__( ( always_inline ) ) {
         if( c < bc )
         {
             nchroma++;
@@ -710,7 +710,7 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
 
     // mode 0: fpelcmp on p_fref_w + BITS_MVD; 1: COST_MV_HPEL (get_ref + qpel mv cost); 2: fpelcmp
     // alone.  Group g scores (gx, gy) (not read when !ok); c[k] = group k's cost.
-    auto evalc = [&]( int gx, int gy, int mode, bool ok, int (&c)[4] ) {
+    auto evalc = [&]( int gx, int gy, int mode, bool ok, int (&c)[4] ) __attribute__( ( always_inline ) ) {
         uint32_t v = 0;
         if( ok )
         {
@@ -732,12 +732,12 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
         for( int k = 0; k < 4; k++ )
             c[k] = (int)__shfl( (int)v, sbase + NT * k );
     };
-    auto in_range = [&]( int mx, int my ) { return mx >= xmin && mx <= xmax && my >= ymin && my <= ymax; };
+    auto in_range = [&]( int mx, int my ) __attribute__( ( always_inline ) ) { return mx >= xmin && mx <= xmax && my >= ymin && my <= ymax; };
 
     int bmx, bmy, bcost = COST_MAX, bpred_cost = COST_MAX, pmx, pmy;
     uint32_t pmv, bpred_mv = 0;
     int c[4];
-    auto upd = [&]( int cc, int mx, int my ) {
+    auto upd = [&]( int cc, int mx, int my ) __attribute__( ( always_inline ) ) {
         nf++;
         if( cc < bcost )
         {
@@ -747,7 +747,7 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
         }
     };
     // the want-th entry of x264_predictor_clip (qpel) / _roundclip (fpel) over the mvc list
-    auto pred = [&]( int want, int &ox, int &oy ) {
+    auto pred = [&]( int want, int &ox, int &oy ) __attribute__( ( always_inline ) ) {
         int cnt = 0;
         bool found = false;
         for( int i = 0; i < i_mvc && !found; i++ )
@@ -771,7 +771,7 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
         }
         return found;
     };
-    auto nvalid = [&]() {
+    auto nvalid = [&]() __attribute__( ( always_inline ) ) {
         int cnt = 0;
         for( int i = 0; i < i_mvc; i++ )
         {
@@ -878,7 +878,7 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
     }
 
     // the diamond of radius 1 around (cx, cy) in COST_MV_X4's order (0,-1) (0,1) (-1,0) (1,0)
-    auto dia = [&]( int cx, int cy ) {
+    auto dia = [&]( int cx, int cy ) __attribute__( ( always_inline ) ) {
         evalc( cx + (g == 2 ? -1 : g == 3 ? 1 : 0), cy + (g == 0 ? -1 : g == 1 ? 1 : 0), 0, true, c );
     };
     bool hex = me_method == 1;
@@ -906,20 +906,20 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
     else if( me_method == 2 )
     {
         // UMH (me.c:422-616)
-        auto dia1 = [&]( int cx, int cy ) {
+        auto dia1 = [&]( int cx, int cy ) __attribute__( ( always_inline ) ) {
             dia( cx, cy );
             upd( c[0], cx, cy - 1 );
             upd( c[1], cx, cy + 1 );
             upd( c[2], cx - 1, cy );
             upd( c[3], cx + 1, cy );
         };
-        auto thresh = [&]( int v ) { return bcost < (v >> k_psize_shift[IPIX]); };
+        auto thresh = [&]( int v ) __attribute__( ( always_inline ) ) { return bcost < (v >> k_psize_shift[IPIX]); };
         int omx, omy;
         // CROSS( start, x_max, y_max ) around (omx, omy) (me.c:152-176): slot 2k / 2k+1 = +i / -i
-        auto cross = [&]( int start, int x_max, int y_max ) {
+        auto cross = [&]( int start, int x_max, int y_max ) __attribute__( ( always_inline ) ) {
             const int nhs = x_max > start ? 2 * ((x_max - start + 1) >> 1) : 0;
             const int nvs = y_max > start ? 2 * ((y_max - start + 1) >> 1) : 0;
-            auto slot = [&]( int sl, int &mx, int &my ) {
+            auto slot = [&]( int sl, int &mx, int &my ) __attribute__( ( always_inline ) ) {
                 const bool v = sl >= nhs;
                 const int s2 = v ? sl - nhs : sl;
                 const int d = (start + 2 * (s2 >> 1)) * ((s2 & 1) ? -1 : 1);
