@@ -652,7 +652,14 @@ template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, co
 // them), whose lanes first stage the MB's per-row key terms in LDS (ycost, row part of the
 // raster index, row validity), so a candidate row costs one LDS read instead of a clamped
 // global load and its index arithmetic.
-template <int R> constexpr int esa7_groups() { return cen_pitch( 8, R ) / 4; }
+// Column groups: an unclipped window's candidates -- width (2R + 3) & ~3 from min_x = bmx - R,
+// me.c:626 -- start at most 3 columns past the dword-aligned origin, so G = ceil(((2R+3) & ~3)
+// + 3) / 4) groups hold them (9 at R = 16: 36 columns, where the full centred pitch has 40).
+// A window whose columns reach further (clipped on the left, so the rounded width runs up to
+// two columns past max_x, or an origin clamped at the frame's right edge) needs one more
+// group: the workgroup's spare lanes (256 - MPW * G of them) take those MBs' extra group, and
+// an MB beyond the spare lanes has its group 0 run the extra columns after its own.
+template <int R> constexpr int esa7_groups() { return ((((2 * R + 3) & ~3) + 3) + 3) / 4; }
 template <int R> constexpr int esa7_mbs() { return 256 / esa7_groups<R>(); }
 template <int R>
 __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
@@ -664,64 +671,56 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
                                                                 uint32_t *__restrict__ keys, int xcd )
 {
     constexpr int G = esa7_groups<R>();         // column groups per MB
-    constexpr int P = 4 * G;
+    constexpr int P = cen_pitch( 8, R );        // the centred template's pitch (me_window's clamp)
     constexpr int W = 2 * R + 1;                // candidate rows
     constexpr int MPW = esa7_mbs<R>();          // whole MBs per workgroup
+    constexpr int NSP = 256 - MPW * G;          // spare lanes: extra groups of wide windows
     constexpr int SP = W | 1;                   // LDS row-term pitch (odd: spread banks)
     __shared__ uint32_t s_row[MPW * SP];
-    // lanes past the last MB (and the workgroup's G * MPW .. 255 tail) work on a clamped MB
-    // and publish nothing; every lane reaches the barrier
+    __shared__ uint32_t s_need[MPW];
     const uint32_t nmb = (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw;
     const int tid = (int)threadIdx.x;
-    const int lmb = min( tid / G, MPW - 1 );
-    const int grp = tid - lmb * G;              // >= G only in the tail lanes
-    const uint32_t mbr = (xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * MPW + lmb;
-    const bool live = tid < MPW * G && mbr < nmb;
-    const uint32_t mb32 = min( mbr, nmb - 1 ), t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
-    const int mbx = (int)(mb32 - t32 * (uint32_t)mbw);
-    const int mby = (int)(t32 - f32 * (uint32_t)mbh);
-    const int64_t mb = mb32, f = f32;
-    const int cgrp = min( grp, G - 1 );          // the tail lanes' loads stay inside the MB
+    const bool spare = tid >= MPW * G;
+    const uint32_t wg0 = (xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * MPW;
 
-    uint32_t F[16][4];
-    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
-    const int fs_dw = (int)(fs / 4);
-#pragma unroll
-    for( int r = 0; r < 16; r++ )
-#pragma unroll
-        for( int k = 0; k < 4; k++ )
-            F[r][k] = fe[r * fs_dw + k];
-    const int16_t *p = par + 8 * mb;
-    const int bmx = p[0], bmy = p[1];
-    const int min_x = max( bmx - me_range, (int)p[4] ), min_y = max( bmy - me_range, (int)p[5] );
-    const int max_x = min( bmx + me_range, (int)p[6] ), max_y = min( bmy + me_range, (int)p[7] );
-    const int width = (max_x - min_x + 3) & ~3;
-    const uint16_t *cx = cost_mv - p[2], *cy = cost_mv - p[3];
-    int ox, oy;
-    const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };   // the window centre: the predictor
-    me_window<8, R, P>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
-    const uint32_t *rbase =
-        (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox + 4 * cgrp);
-    // key = (sad + xcost + ycost) << 12 | raster, raster = (my - min_y) * width + mx - min_x
-    // < 4096, built as sat( ((sad << 12) + C[k]) + S ): C[k] = xcost << 12 | column part,
-    // or 0xF0000000 outside the window (valid keys stay below 196350 << 12 + 4096 <
-    // 0xF0000000, and 0xF0000000 + (65280 << 12) does not wrap); S = ycost << 12 | row
-    // part, or all ones outside the window (the add saturates).  Per candidate row: one
-    // extract + one shift-add + one saturating add per column and two min3.
-    uint32_t ck[4];
-#pragma unroll
-    for( int k = 0; k < 4; k++ )
-    {
-        const int mx = ox + 4 * cgrp + k;
-        const bool in = mx >= min_x && mx < min_x + width;
-        ck[k] = in ? ((uint32_t)cx[mx * 4] << 12) + (uint32_t)(mx - min_x) : 0xF0000000u;
-    }
-    uint32_t key = 0xFFFFFFFFu;
+    // the MB-dependent terms of workgroup MB slot `slot`
+    int lmb, grp, mbx, mby, bmx, bmy, min_x, min_y, max_x, max_y, width, ox, oy;
+    int64_t mb, f;
+    bool live;
+    const uint16_t *cx, *cy;
+    auto setup = [&]( int slot ) __attribute__( ( always_inline ) ) {
+        lmb = slot;
+        const uint32_t mbr = wg0 + (uint32_t)slot;
+        live = mbr < nmb;
+        const uint32_t mb32 = min( mbr, nmb - 1 ), t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+        mbx = (int)(mb32 - t32 * (uint32_t)mbw);
+        mby = (int)(t32 - f32 * (uint32_t)mbh);
+        mb = mb32;
+        f = f32;
+        const int16_t *p = par + 8 * mb;
+        bmx = p[0];
+        bmy = p[1];
+        min_x = max( bmx - me_range, (int)p[4] );
+        min_y = max( bmy - me_range, (int)p[5] );
+        max_x = min( bmx + me_range, (int)p[6] );
+        max_y = min( bmy + me_range, (int)p[7] );
+        width = (max_x - min_x + 3) & ~3;
+        cx = cost_mv - p[2];
+        cy = cost_mv - p[3];
+        const int16_t cen[2] = { (int16_t)bmx, (int16_t)bmy };   // the window centre: the predictor
+        me_window<8, R, P>( cen, 0, mbx, mby, mbw, mbh, ox, oy );
+    };
+    setup( spare ? 0 : tid / G );
+    grp = spare ? G : tid - lmb * G;
+    // this MB's window needs the columns past the G groups
+    const bool need = live && min_x + width - 1 - ox >= 4 * G;
+    if( !spare && grp == 0 )
+        s_need[lmb] = need;
     // row terms S[c] = ycost << 12 | (my - min_y) * width for candidate row c (my = oy + c)
     // inside [min_y, max_y], all ones outside; the MB's lanes stage them together
-    uint32_t *srow = s_row + lmb * SP;
-    if( live )
+    if( !spare && live )
     {
+        uint32_t *srow = s_row + lmb * SP;
 #pragma unroll
         for( int c0 = 0; c0 < W; c0 += G )
         {
@@ -733,6 +732,61 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
         }
     }
     __syncthreads();
+    // the extra groups: spare lane s takes the s-th MB that needs one; past the spare lanes the
+    // MB's group 0 runs the extra columns itself after its own
+    bool twice = false;
+    if constexpr( NSP > 0 )
+    {
+        if( spare )
+        {
+            int k = tid - MPW * G, slot = -1;
+            for( int i = 0; i < MPW && slot < 0; i++ )
+                if( s_need[i] && k-- == 0 )
+                    slot = i;
+            if( slot >= 0 )
+                setup( slot );
+            else
+                live = false;
+        }
+        else if( grp == 0 && need )
+        {
+            int rank = 0;
+            for( int i = 0; i < lmb; i++ )
+                rank += s_need[i] ? 1 : 0;
+            twice = rank >= NSP;
+        }
+    }
+    else
+        twice = !spare && grp == 0 && need;
+
+    uint32_t F[16][4];
+    const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby) * fs + 16 * mbx);
+    const int fs_dw = (int)(fs / 4);
+#pragma unroll
+    for( int r = 0; r < 16; r++ )
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            F[r][k] = fe[r * fs_dw + k];
+    const uint32_t *rmb = (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + oy) * rs + 16 * mbx + ox);
+    // key = (sad + xcost + ycost) << 12 | raster, raster = (my - min_y) * width + mx - min_x
+    // < 4096, built as sat( ((sad << 12) + C[k]) + S ): C[k] = xcost << 12 | column part,
+    // or 0xF0000000 outside the window (valid keys stay below 196350 << 12 + 4096 <
+    // 0xF0000000, and 0xF0000000 + (65280 << 12) does not wrap); S = ycost << 12 | row
+    // part, or all ones outside the window (the add saturates).  Per candidate row: one
+    // extract + one shift-add + one saturating add per column and two min3.
+    uint32_t ck[4];
+    auto columns = [&]( int g ) __attribute__( ( always_inline ) ) {
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            const int mx = ox + 4 * g + k;
+            const bool in = mx >= min_x && mx < min_x + width;
+            ck[k] = in ? ((uint32_t)cx[mx * 4] << 12) + (uint32_t)(mx - min_x) : 0xF0000000u;
+        }
+    };
+    columns( grp );
+    uint32_t key = 0xFFFFFFFFu;
+    uint32_t *srow = s_row + lmb * SP;
     auto reduce = [&]( int c, uint32_t lo, uint32_t hi ) {
         // read where the row finishes, not hoisted (an LDS-typed pointer, so the pinned
         // address stays a ds_read)
@@ -752,7 +806,12 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
         asm volatile( "" : "+v"( key ) );        // fold each row where its sums finish
     };
     uint64_t acc[16];
-    me_rows7<R, ME_LEAD>( rbase, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
+    me_rows7<R, ME_LEAD>( rmb + grp, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
+    if( twice )
+    {
+        columns( G );
+        me_rows7<R, ME_LEAD>( rmb + G, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
+    }
     if( live && key < 0xF0000000u )
         atomicMin( keys + 3 * mb, key );
 }
@@ -875,7 +934,8 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
     if( e != hipSuccess )
         return e;
     // 8 bit: whole MBs per workgroup (esa7_mbs); 10 bit: a flat lane index over column pairs
-    const int64_t mpw = 256 / (cen_pitch( 8, range ) / 4);
+    const int64_t mpw = range == 4 ? esa7_mbs<4>() : range == 8 ? esa7_mbs<8>() : range == 16 ? esa7_mbs<16>()
+                                                                                               : esa7_mbs<24>();
     const int64_t lanes = nmb * 2 * (cen_cols( 10, range ) / 2);
     dim3 blk( 256 ), g( (unsigned)(BD == 8 ? (nmb + mpw - 1) / mpw : (lanes + 255) / 256) );
     const int xcd = me_xcd();
