@@ -661,14 +661,19 @@ template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, co
 // an MB beyond the spare lanes has its group 0 run the extra columns after its own.
 template <int R> constexpr int esa7_groups() { return ((((2 * R + 3) & ~3) + 3) + 3) / 4; }
 template <int R> constexpr int esa7_mbs() { return 256 / esa7_groups<R>(); }
-template <int R>
+// TAB: the same lanes write the centred table instead (the self-contained TESA's scratch table,
+// launch_me_tesa): every column an MB's window can reach, the slack columns of unclipped
+// windows left unwritten -- no scan reads them.
+template <int R, bool TAB>
 __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *__restrict__ fenc, intptr_t fs,
                                                                 intptr_t ffs, const uint8_t *__restrict__ ref,
                                                                 intptr_t rs, intptr_t rfs, int mbw, int mbh,
                                                                 int nframes, int me_range,
                                                                 const int16_t *__restrict__ par,
                                                                 const uint16_t *__restrict__ cost_mv,
-                                                                uint32_t *__restrict__ keys, int xcd )
+                                                                uint32_t *__restrict__ keys, int xcd,
+                                                                uint16_t *__restrict__ tab,
+                                                                int16_t *__restrict__ torg )
 {
     constexpr int G = esa7_groups<R>();         // column groups per MB
     constexpr int P = cen_pitch( 8, R );        // the centred template's pitch (me_window's clamp)
@@ -718,7 +723,12 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
         s_need[lmb] = need;
     // row terms S[c] = ycost << 12 | (my - min_y) * width for candidate row c (my = oy + c)
     // inside [min_y, max_y], all ones outside; the MB's lanes stage them together
-    if( !spare && live )
+    if( TAB && !spare && live && grp == 0 )
+    {
+        torg[2 * mb] = (int16_t)ox;
+        torg[2 * mb + 1] = (int16_t)oy;
+    }
+    if( !TAB && !spare && live )
     {
         uint32_t *srow = s_row + lmb * SP;
 #pragma unroll
@@ -806,14 +816,32 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
         asm volatile( "" : "+v"( key ) );        // fold each row where its sums finish
     };
     uint64_t acc[16];
-    me_rows7<R, ME_LEAD>( rmb + grp, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
-    if( twice )
+    if constexpr( TAB )
     {
-        columns( G );
-        me_rows7<R, ME_LEAD>( rmb + G, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
+        // (a lane past the last MB rewrites the last MB's values)
+        uint64_t *out = (uint64_t *)(tab + mb * ((2 * R + 1) * P) + 4 * grp);
+        auto store = [&out]( int c, uint32_t lo, uint32_t hi ) { out[c * (P / 4)] = ((uint64_t)hi << 32) | lo; };
+        if( live )
+        {
+            me_rows7<R, ME_LEAD>( rmb + grp, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 16>{} );
+            if( twice )
+            {
+                out = (uint64_t *)(tab + mb * ((2 * R + 1) * P) + 4 * G);
+                me_rows7<R, ME_LEAD>( rmb + G, (int)(rs / 4), F, acc, store, std::make_integer_sequence<int, 2 * R + 16>{} );
+            }
+        }
     }
-    if( live && key < 0xF0000000u )
-        atomicMin( keys + 3 * mb, key );
+    else
+    {
+        me_rows7<R, ME_LEAD>( rmb + grp, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
+        if( twice )
+        {
+            columns( G );
+            me_rows7<R, ME_LEAD>( rmb + G, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
+        }
+        if( live && key < 0xF0000000u )
+            atomicMin( keys + 3 * mb, key );
+    }
 }
 
 // out[3*mb] holds the MB's best key (0xFFFFFFFF: nothing evaluated); the strict-< update
@@ -944,8 +972,9 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
 #define ESA_CASE( R )                                                                                             \
         case R:                                                                                                   \
             if constexpr( BD == 8 )                                                                               \
-                hipLaunchKernelGGL( ( me_full_esa_v7_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
-                                    mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out, xcd );            \
+                hipLaunchKernelGGL( ( me_full_esa_v7_kernel<R, false> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, \
+                                    rfs, mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out, xcd,         \
+                                    nullptr, nullptr );                                                           \
             else                                                                                                  \
                 hipLaunchKernelGGL( ( me_full_esa_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
                                     mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out, xcd );            \
@@ -1849,7 +1878,30 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
                                 (int)nmb, par, cen );
             hipError_t e = hipGetLastError();
             if( e == hipSuccess )
-                e = launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, TR, ttab, cen, org, stream );
+            {
+                if constexpr( BD == 8 )
+                {
+                    // 8 bit: the fused ESA's lanes (9 column groups at TR 16, the window's extra
+                    // group only where it reaches past them) write the table: 40 -> 36 columns of
+                    // work per MB against launch_me_full's whole centred template (round 4's
+                    // wider template, 36 -> 40 columns, was TESA's 0.58 -> 0.62 ms)
+                    switch( TR )
+                    {
+#define TT_CASE( RR )                                                                                             \
+                        case RR:                                                                                  \
+                            hipLaunchKernelGGL( ( me_full_esa_v7_kernel<RR, true> ),                              \
+                                                dim3( (unsigned)((nmb + esa7_mbs<RR>() - 1) / esa7_mbs<RR>()) ),  \
+                                                dim3( 256 ), 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,    \
+                                                nframes, me_range, par, cost_mv, nullptr, me_xcd(), ttab, org );  \
+                            break;
+                        TT_CASE( 4 ) TT_CASE( 8 ) TT_CASE( 16 ) TT_CASE( 24 )
+#undef TT_CASE
+                    }
+                    e = hipGetLastError();
+                }
+                else
+                    e = launch_me_full<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, TR, ttab, cen, org, stream );
+            }
             if( e == hipSuccess )
                 e = launch_me_tesa<BD>( fenc, fs, ffs, ref, rs, rfs, integral, ifs, mbw, mbh, nframes, me_range, satd,
                                         ttab, TR, org, par, init_cost, cost_mv, out, stream );
