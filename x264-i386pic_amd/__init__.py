@@ -664,7 +664,10 @@ def frame_init_lowres(planes, origin, stride, width, height, outs=None):
     wl, hl = width // 2, height // 2
     ls = plane_stride(wl)
     if outs is None:
-        outs = [torch.zeros((n, hl + 2 * PAD, ls), dtype=planes.dtype, device=planes.device) for _ in range(4)]
+        # one buffer, the four planes equally spaced as x264's buffer_lowres (frame.c), which the
+        # lookahead kernels address by plane index
+        buf = torch.zeros((4, n, hl + 2 * PAD, ls), dtype=planes.dtype, device=planes.device)
+        outs = [buf[k] for k in range(4)]
     ptrs = (_P * 4)(*[o.data_ptr() + (PAD * ls + PAD) * o.element_size() for o in outs])
     _rc(getattr(lib(), f"x264hip_{bd}_frame_init_lowres")(
         _ptr(planes, origin), stride, planes[0].numel(), width, height, n, ptrs, ls, outs[0][0].numel(), _stream()),

@@ -158,6 +158,8 @@ template <int BD> struct LrCtx
     const uint32_t (&fe)[LR_NR][NDW];       // this lane's fenc rows (packed pixels), shared by the lists
     const pixel *p0, *p1, *p2, *p3;         // reference F, H, V, C at the block, row 2q
     const pixel *pw;                        // p_fref_w: the weighted F plane (p0 when unweighted)
+    intptr_t pd;                            // p1 - p0 when the planes are equally spaced (x264's
+                                            // buffer_lowres, frame.c), else 0
     int wsc, wrnd, wsh, woff;               // m->weight (mc_weight terms)
     bool wgt;
     intptr_t stride;
@@ -182,6 +184,8 @@ template <int BD> struct LrCtx
         p2 = r2 + off;
         p3 = r3 + off;
         pw = p0;
+        const intptr_t d1 = r1 - r0;
+        pd = (r2 - r1 == d1 && r3 - r2 == d1) ? d1 : 0;
         wgt = false;
         wsc = wrnd = wsh = woff = 0;
         stride = s;
@@ -282,13 +286,16 @@ template <int BD> struct LrCtx
         const int idx = ((my & 3) << 2) + (mx & 3);
         const intptr_t off = (intptr_t)(my >> 2) * stride + (mx >> 2);
         const int i0 = (int)((k_lr_ref0 >> (2 * idx)) & 3), i1 = (int)((k_lr_ref1 >> (2 * idx)) & 3);
-        const pixel *s1 = (i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off + ((my & 3) == 3) * stride;
+        // (equally spaced planes: the plane by one multiply-add instead of three 64-bit selects)
+        const pixel *s1 = (pd ? p0 + i0 * pd : i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off +
+                          ((my & 3) == 3) * stride;
 #pragma unroll
         for( int y = 0; y < LR_NR; y++ )
             load_al_pad<NDW>( s1 + (intptr_t)y * stride, r[y] );
         if( idx & 5 )                       // two planes: the rounding average
         {
-            const pixel *s2 = (i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off + ((mx & 3) == 3);
+            const pixel *s2 = (pd ? p0 + i1 * pd : i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off +
+                              ((mx & 3) == 3);
 #pragma unroll
             for( int y = 0; y < LR_NR; y++ )
             {
@@ -313,7 +320,8 @@ template <int BD> struct LrCtx
     __device__ __forceinline__ void hpel_rows( int mx, int my, uint32_t (&r)[LR_NR][NDW] ) const
     {
         const int i = ((mx & 2) >> 1) + (my & 2);
-        const pixel *s = (i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : p3) + (mx >> 2) + (intptr_t)(my >> 2) * stride;
+        const pixel *s = (pd ? p0 + i * pd : i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : p3) + (mx >> 2) +
+                         (intptr_t)(my >> 2) * stride;
 #pragma unroll
         for( int y = 0; y < LR_NR; y++ )
             load_al_pad<NDW>( s + (intptr_t)y * stride, r[y] );
