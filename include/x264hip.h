@@ -556,7 +556,9 @@ int x264hip_##BD##_lowres_intra_cost( const pixel *lowres, intptr_t stride,     
  * For n_pairs (fenc, ref) pairs of lowres frames -- fenc = lowres[0] of frame b,                \
  * ref = lowres[0..3] (F, H, V, C) of frame p0, pointers at pixel (0,0), frame                   \
  * strides apart, common stride, 32 pixels of border, (0,0) and stride 4-byte                    \
- * aligned -- and intra_cost[f*mbs + mb] from lowres_intra_cost, writes                          \
+ * aligned; the four planes equally spaced as x264's buffer_lowres (frame.c:281)                 \
+ * are read in place, other layouts are first gathered into a stream-ordered scratch -- \
+ * and intra_cost[f*mbs + mb] from lowres_intra_cost, writes                                     \
  * fenc->lowres_mvs (mvs[2*(f*mbs + mb)]), lowres_mv_costs (mv_costs), lowres_costs               \
  * ((list_used << 14) + cost), the AQ-scaled inter row sums row_satd[f*mbh + y]                  \
  * (i_row_satds[b-p0][0]) and est[3f..3f+2] = cost_est, cost_est_aq, intra_mbs.                  \

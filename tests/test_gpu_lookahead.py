@@ -15,7 +15,19 @@ def _host(t, bd):
     return a.view(np.uint16) if bd == 10 else a
 
 
-def _case(hip, oracle, bd, W, H, npairs, me_method, subme, satd, random=False, aq=False, me_range=16, n_slices=1):
+def _unequal(lows):
+    """the four lowres planes at slots 0, 1, 3, 4 of one buffer: not equally spaced, so the
+    launch gathers them into its scratch first (LaPlanes, lookahead.hip)"""
+    buf = torch.zeros((5,) + tuple(lows[0].shape), dtype=lows[0].dtype, device=lows[0].device)
+    out = []
+    for k, p in zip((0, 1, 3, 4), lows):
+        buf[k].copy_(p)
+        out.append(buf[k])
+    return out
+
+
+def _case(hip, oracle, bd, W, H, npairs, me_method, subme, satd, random=False, aq=False, me_range=16, n_slices=1,
+          unequal=False):
     from x264hip import synth
     gen = synth.random_planes if random else synth.make_sequence
     frames, stride, origin = gen(npairs + 1, W, H, bd)
@@ -30,7 +42,7 @@ def _case(hip, oracle, bd, W, H, npairs, me_method, subme, satd, random=False, a
         iq_np = np.random.default_rng(W + bd).integers(100, 700, (npairs + 1, mbw * mbh)).astype(np.uint16)
         iq = torch.from_numpy(iq_np.view(np.int16)).cuda()
     fenc = lows[0][1:]
-    refs = [p[:-1] for p in lows]
+    refs = [p[:-1] for p in (_unequal(lows) if unequal else lows)]
     got = hip.lowres_inter_cost(fenc, refs, ls, mbw, mbh, intra[1:], (cm_dev, c0), me_method=me_method,
                                 subme=subme, satd=satd, me_range=me_range, inv_qscale=None if iq is None else iq[1:],
                                 n_slices=n_slices)
@@ -66,6 +78,38 @@ def test_lowres_inter_random(hip, oracle, bd, size):
     _case(hip, oracle, bd, W, H, 3, 1, 4, True, random=True, aq=True, me_range=8)
 
 
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("size", [(176, 144), (96, 16), (640, 352)])
+def test_lowres_inter_unequal_planes(hip, oracle, bd, size):
+    """reference planes that are not equally spaced (separate allocations, unlike x264's
+    buffer_lowres): gathered by the launch, same results; random planes reach the mv limits"""
+    W, H = size
+    _case(hip, oracle, bd, W, H, 3, 1, 4, True, random=True, me_range=16, unequal=True)
+
+
+def test_lowres_unequal_one_reference(hip, oracle):
+    """one reference frame per list serving the batch (frame stride 0), its planes not equally
+    spaced: the gathered copy holds one frame; results equal the equally spaced layout's"""
+    from x264hip import synth
+    W, H = 176, 144
+    frames, stride, origin = synth.random_planes(5, W, H, 8)
+    lows, ls = hip.frame_init_lowres(torch.from_numpy(frames).cuda(), origin, stride, W, H)
+    mbw, mbh = W // 16, H // 16
+    nmb = mbw * mbh
+    cm, c0 = oracle.cost_mv_table(1, 512)
+    cmd = (torch.from_numpy(cm.view(np.int16)).cuda(), c0)
+    res = []
+    for planes in (lows, _unequal(lows)):
+        mvs = [torch.zeros((3, nmb, 2), dtype=torch.int16, device="cuda") for _ in range(2)]
+        costs = [torch.zeros((3, nmb), dtype=torch.int32, device="cuda") for _ in range(2)]
+        out = hip.lowres_bidir_cost(lows[0][1:4], [p[0:1] for p in planes], [p[4:5] for p in planes], ls, mbw, mbh,
+                                    cmd, 3, mvs[0], costs[0], mvs[1], costs[1], dist_scale_factor=100,
+                                    bipred_weight=39, a_frame_stride=0, b_frame_stride=0)
+        res.append(list(out) + mvs + costs)
+    for g, w in zip(*res):
+        assert torch.equal(g, w)
+
+
 def test_lowres_inter_identical(hip, oracle):
     """ref == fenc: the fast skip everywhere (mv 0, cost 0)."""
     from x264hip import synth
@@ -83,7 +127,7 @@ def test_lowres_inter_identical(hip, oracle):
 
 
 def _bidir_case(hip, oracle, bd, W, H, n, search, me_method, subme, satd, dsf, weight, with_p1=True, random=False,
-                aq=False, me_range=16, n_slices=1):
+                aq=False, me_range=16, n_slices=1, unequal=False):
     """n B triplets (p0, b, p1) = (3i, 3i+1, 3i+2) of one sequence; the list searches (or the
     cached mvs of a first pass) and every output against the oracle."""
     from x264hip import synth
@@ -97,8 +141,8 @@ def _bidir_case(hip, oracle, bd, W, H, n, search, me_method, subme, satd, dsf, w
     cmd = (torch.from_numpy(cm.view(np.int16)).cuda(), c0)
     kw = dict(me_method=me_method, subme=subme, satd=satd, me_range=me_range)
     fenc = lows[0][1::3]
-    ra = [p[0::3] for p in lows]
-    rb = [p[2::3] for p in lows]
+    ra = [p[0::3] for p in (_unequal(lows) if unequal else lows)]
+    rb = [p[2::3] for p in (_unequal(lows) if unequal else lows)]
     ic = torch.full((n, nmb), 16383, dtype=torch.int16, device="cuda")
     p1mvs = None
     if with_p1:
@@ -158,6 +202,13 @@ def test_lowres_bidir_random(hip, oracle, bd, size):
     """random planes (mvs at the limits), AQ, short range, small and degenerate frames."""
     W, H = size
     _bidir_case(hip, oracle, bd, W, H, 2, 3, 1, 4, True, 100, 39, random=True, aq=True, me_range=8)
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("search", [3, 1])
+def test_lowres_bidir_unequal_planes(hip, oracle, bd, search):
+    """B triplets whose list-0 / list-1 planes are not equally spaced (gathered by the launch)"""
+    _bidir_case(hip, oracle, bd, 176, 144, 2, search, 1, 4, True, 100, 39, random=True, unequal=True)
 
 
 @pytest.mark.parametrize("bd,H", [(8, 16 * 260), (10, 16 * 130)])

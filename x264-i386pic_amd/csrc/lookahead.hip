@@ -156,10 +156,10 @@ template <int BD> struct LrCtx
     using pixel = typename PT<BD>::pixel;
     static constexpr int NDW = 8 / PT<BD>::PPD;
     const uint32_t (&fe)[LR_NR][NDW];       // this lane's fenc rows (packed pixels), shared by the lists
-    const pixel *p0, *p1, *p2, *p3;         // reference F, H, V, C at the block, row 2q
+    const pixel *p0;                        // reference F at the block, row 2q (H, V, C follow at pd)
     const pixel *pw;                        // p_fref_w: the weighted F plane (p0 when unweighted)
-    intptr_t pd;                            // p1 - p0 when the planes are equally spaced (x264's
-                                            // buffer_lowres, frame.c), else 0
+    intptr_t pd;                            // the planes' spacing (x264's buffer_lowres, frame.c;
+                                            // the launchers stage unequal planes)
     int wsc, wrnd, wsh, woff;               // m->weight (mc_weight terms)
     bool wgt;
     intptr_t stride;
@@ -173,19 +173,15 @@ template <int BD> struct LrCtx
     // per-block setup of slicetype_mb_cost (slicetype.c:539-557): the lowres mv limits
     // (the vertical ones, set at the first block of each row of the scan, depend on
     // the row only) and the reference planes at the lane's first block row
-    __device__ __forceinline__ void setup( const pixel *r0, const pixel *r1, const pixel *r2, const pixel *r3,
+    __device__ __forceinline__ void setup( const pixel *r0, intptr_t rpd,
                                            intptr_t off, intptr_t s, int x, int y, int mbw, int mbh, int mvr,
                                            int use_satd, int lane_q )
     {
         q = lane_q;
         off += (intptr_t)(LR_NR * q) * s;
         p0 = r0 + off;
-        p1 = r1 + off;
-        p2 = r2 + off;
-        p3 = r3 + off;
+        pd = rpd;
         pw = p0;
-        const intptr_t d1 = r1 - r0;
-        pd = (r2 - r1 == d1 && r3 - r2 == d1) ? d1 : 0;
         wgt = false;
         wsc = wrnd = wsh = woff = 0;
         stride = s;
@@ -286,16 +282,14 @@ template <int BD> struct LrCtx
         const int idx = ((my & 3) << 2) + (mx & 3);
         const intptr_t off = (intptr_t)(my >> 2) * stride + (mx >> 2);
         const int i0 = (int)((k_lr_ref0 >> (2 * idx)) & 3), i1 = (int)((k_lr_ref1 >> (2 * idx)) & 3);
-        // (equally spaced planes: the plane by one multiply-add instead of three 64-bit selects)
-        const pixel *s1 = (pd ? p0 + i0 * pd : i0 == 0 ? p0 : i0 == 1 ? p1 : i0 == 2 ? p2 : p3) + off +
-                          ((my & 3) == 3) * stride;
+        // (the plane by one multiply-add: the four planes equally spaced)
+        const pixel *s1 = p0 + i0 * pd + off + ((my & 3) == 3) * stride;
 #pragma unroll
         for( int y = 0; y < LR_NR; y++ )
             load_al_pad<NDW>( s1 + (intptr_t)y * stride, r[y] );
         if( idx & 5 )                       // two planes: the rounding average
         {
-            const pixel *s2 = (pd ? p0 + i1 * pd : i1 == 0 ? p0 : i1 == 1 ? p1 : i1 == 2 ? p2 : p3) + off +
-                              ((mx & 3) == 3);
+            const pixel *s2 = p0 + i1 * pd + off + ((mx & 3) == 3);
 #pragma unroll
             for( int y = 0; y < LR_NR; y++ )
             {
@@ -320,8 +314,7 @@ template <int BD> struct LrCtx
     __device__ __forceinline__ void hpel_rows( int mx, int my, uint32_t (&r)[LR_NR][NDW] ) const
     {
         const int i = ((mx & 2) >> 1) + (my & 2);
-        const pixel *s = (pd ? p0 + i * pd : i == 0 ? p0 : i == 1 ? p1 : i == 2 ? p2 : p3) + (mx >> 2) +
-                         (intptr_t)(my >> 2) * stride;
+        const pixel *s = p0 + i * pd + (mx >> 2) + (intptr_t)(my >> 2) * stride;
 #pragma unroll
         for( int y = 0; y < LR_NR; y++ )
             load_al_pad<NDW>( s + (intptr_t)y * stride, r[y] );
@@ -954,13 +947,13 @@ __device__ __forceinline__ void lr_band( int j, int mbh, int nslices, int brows,
 template <int BD, bool WGT>
 __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *r0,
-    const typename PT<BD>::pixel *r1, const typename PT<BD>::pixel *r2, const typename PT<BD>::pixel *r3,
+    intptr_t rpd,
     intptr_t stride, intptr_t rfs, int mbw, int mbh, int me_method, int subme, int satd, int me_range, int mv_range,
     int lambda, const uint16_t *__restrict__ cost_mv, const uint16_t *__restrict__ intra_cost,
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
     uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands, int brows,
-    int poll_max, uint32_t *status, const typename PT<BD>::pixel *rw, int wscale, int wdenom, int woffset,
-    int nslices, int help )
+    int poll_max, uint32_t *status, const typename PT<BD>::pixel *rw, intptr_t wfs, int wscale, int wdenom,
+    int woffset, int nslices, int help )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring[4 * LR_BAND];            // packed MVs of each band row's 4 latest blocks
@@ -973,11 +966,8 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     r0 += (intptr_t)f * rfs;
-    r1 += (intptr_t)f * rfs;
-    r2 += (intptr_t)f * rfs;
-    r3 += (intptr_t)f * rfs;
     if( WGT )
-        rw += (intptr_t)f * rfs;
+        rw += (intptr_t)f * wfs;
     intra_cost += (intptr_t)f * nmb;
     if( invq )
         invq += (intptr_t)f * nmb;
@@ -1001,7 +991,7 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
         __syncthreads();
         if( threadIdx.x >= 64 )
         {
-            const typename PT<BD>::pixel *const hpl[5] = { r0, r1, r2, r3, WGT ? rw : r0 };
+            const typename PT<BD>::pixel *const hpl[5] = { r0, r0 + rpd, r0 + 2 * rpd, r0 + 3 * rpd, WGT ? rw : r0 };
             lr_helper<BD, 5>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, prog, poll_max );
             return;
         }
@@ -1038,7 +1028,7 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
             const int mb = x + y * mbw;
             const intptr_t off = 8 * (intptr_t)x + 8 * (intptr_t)y * stride;
             LrCtx<BD> m( fe );
-            m.setup( r0, r1, r2, r3, off, stride, x, y, mbw, mbh, mvr, satd, q );
+            m.setup( r0, rpd, off, stride, x, y, mbw, mbh, mvr, satd, q );
             if constexpr( WGT )
                 m.set_weight( rw, off, wscale, wdenom, woffset );
             uint32_t pred[4];
@@ -1148,10 +1138,8 @@ __device__ __forceinline__ int lr_bidir( const LrCtx<BD> &m0, const LrCtx<BD> &m
 // A list is searched on the wavefront when search & (1 << l), else its mv / cost are read.
 template <int BD>
 __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
-    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *a0,
-    const typename PT<BD>::pixel *a1, const typename PT<BD>::pixel *a2, const typename PT<BD>::pixel *a3,
-    intptr_t afs, const typename PT<BD>::pixel *b0, const typename PT<BD>::pixel *b1,
-    const typename PT<BD>::pixel *b2, const typename PT<BD>::pixel *b3, intptr_t bfs, intptr_t stride, int mbw,
+    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *a0, intptr_t apd,
+    intptr_t afs, const typename PT<BD>::pixel *b0, intptr_t bpd, intptr_t bfs, intptr_t stride, int mbw,
     int mbh, int me_method, int subme, int satd, int me_range, int mv_range, int lambda,
     const uint16_t *__restrict__ cost_mv, int search, int16_t *__restrict__ mvs0, int32_t *__restrict__ costs0,
     int16_t *__restrict__ mvs1, int32_t *__restrict__ costs1, const int16_t *__restrict__ p1mvs, int dsf, int weight,
@@ -1168,8 +1156,8 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
     lr_band( (int)(blockIdx.x % nbands), mbh, nslices, brows, s1, y0, y1 );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
-    a0 += (intptr_t)f * afs; a1 += (intptr_t)f * afs; a2 += (intptr_t)f * afs; a3 += (intptr_t)f * afs;
-    b0 += (intptr_t)f * bfs; b1 += (intptr_t)f * bfs; b2 += (intptr_t)f * bfs; b3 += (intptr_t)f * bfs;
+    a0 += (intptr_t)f * afs;
+    b0 += (intptr_t)f * bfs;
     if( invq )
         invq += (intptr_t)f * nmb;
     if( p1mvs )
@@ -1202,7 +1190,8 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
         __syncthreads();
         if( threadIdx.x >= 64 )
         {
-            const typename PT<BD>::pixel *const hpl[8] = { a0, a1, a2, a3, b0, b1, b2, b3 };
+            const typename PT<BD>::pixel *const hpl[8] = { a0, a0 + apd, a0 + 2 * apd, a0 + 3 * apd,
+                                                           b0, b0 + bpd, b0 + 2 * bpd, b0 + 3 * bpd };
             lr_helper<BD, 8>( hpl, fenc, stride, mbw, s1, y0, y1, t0, t1, prog, poll_max );
             return;
         }
@@ -1245,16 +1234,15 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
         bool failed = false;
         if( act )
         {
-            m0.setup( a0, a1, a2, a3, off, stride, x, y, mbw, mbh, mvr, satd, q );
-            m1.setup( b0, b1, b2, b3, off, stride, x, y, mbw, mbh, mvr, satd, q );
+            m0.setup( a0, apd, off, stride, x, y, mbw, mbh, mvr, satd, q );
+            m1.setup( b0, bpd, off, stride, x, y, mbw, mbh, mvr, satd, q );
             {
                 // every role searches: list `lst` = role & 1 on groups lg = role >> 1 (two
                 // groups per list split its candidate batches); the searching lanes' own
                 // context: the list's planes (a per-lane choice of pointers, not of objects,
                 // so nothing goes to scratch)
                 const int lst = role & 1, lg = role >> 1;
-                ms.setup( lst ? b0 : a0, lst ? b1 : a1, lst ? b2 : a2, lst ? b3 : a3, off, stride, x, y, mbw,
-                          mbh, mvr, satd, q );
+                ms.setup( lst ? b0 : a0, lst ? bpd : apd, off, stride, x, y, mbw, mbh, mvr, satd, q );
                 // list `lst`: searched on the wavefront (search & (1 << lst)) or read
                 int *ring = lst ? ring1 : ring0;
                 uint32_t *gmv = lst ? gmv1 : gmv0;
@@ -1556,6 +1544,57 @@ int la_help( const void *kernel, int64_t nwg, size_t lds, hipStream_t stream )
 }
 } // namespace
 
+// The kernels take a reference's four lowres planes (F, H, V, C) as the F plane and one
+// spacing: x264 allocates them so, in one buffer_lowres (frame.c:209, 281), and one spacing
+// instead of three more 64-bit pointers keeps the kernels' scalar registers (and spills) down.
+// Planes that are not equally spaced are gathered first, stream-ordered, into a scratch
+// buffer: per plane and frame the rows -16 .. 8 * mbh + 16 from column -32 (every row the
+// search and the helper wave can reach, lr_helper), spaced evenly.
+template <typename pixel>
+__global__ __launch_bounds__( 256 ) void lowres_gather_kernel( const pixel *p0, const pixel *p1, const pixel *p2,
+                                                               const pixel *p3, intptr_t fs, intptr_t lo,
+                                                               intptr_t len, pixel *dst )
+{
+    const int k = blockIdx.z;
+    const pixel *src = (k == 0 ? p0 : k == 1 ? p1 : k == 2 ? p2 : p3) + (intptr_t)blockIdx.y * fs - lo;
+    pixel *d = dst + ((intptr_t)k * gridDim.y + blockIdx.y) * len;
+    for( intptr_t i = (intptr_t)blockIdx.x * 256 + threadIdx.x; i < len; i += (intptr_t)gridDim.x * 256 )
+        d[i] = src[i];
+}
+
+template <typename pixel> struct LaPlanes
+{
+    const pixel *base = nullptr;                 // the F plane at (0, 0) of frame 0
+    intptr_t pd = 0, fs = 0;                     // plane spacing, frame stride
+    pixel *scratch = nullptr;
+
+    hipError_t init( const pixel *const p[4], intptr_t frame_stride, intptr_t stride, int nframes, int mbh,
+                     hipStream_t st )
+    {
+        const intptr_t d = p[1] - p[0];
+        fs = frame_stride;
+        if( d != 0 && p[2] - p[1] == d && p[3] - p[2] == d )
+        {
+            base = p[0];
+            pd = d;
+            return hipSuccess;
+        }
+        const int nf = frame_stride ? nframes : 1;
+        const intptr_t lo = 16 * stride + 32, len = (8 * (intptr_t)mbh + 33) * stride;
+        hipError_t e = hipMallocAsync( (void **)&scratch, (size_t)(4 * nf) * len * sizeof( pixel ), st );
+        if( e != hipSuccess )
+            return e;
+        const int nx = (int)std::min<intptr_t>( (len + 255) / 256, 64 );
+        hipLaunchKernelGGL( lowres_gather_kernel<pixel>, dim3( nx, nf, 4 ), dim3( 256 ), 0, st, p[0], p[1], p[2],
+                            p[3], frame_stride, lo, len, scratch );
+        base = scratch + lo;
+        pd = (intptr_t)nf * len;
+        fs = frame_stride ? len : 0;
+        return hipGetLastError();
+    }
+    hipError_t done( hipStream_t st ) { return scratch ? hipFreeAsync( scratch, st ) : hipSuccess; }
+};
+
 template <int BD>
 hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs,
                                 const typename PT<BD>::pixel *const ra[4], intptr_t afs,
@@ -1592,16 +1631,30 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
     if( mv_range < 1 || lds > 48 * 1024 )
         return hipErrorInvalidValue;
+    LaPlanes<typename PT<BD>::pixel> pa, pb;
+    if( (e = pa.init( ra, afs, stride, n, mbh, stream )) != hipSuccess ||
+        (e = pb.init( rb, bfs, stride, n, mbh, stream )) != hipSuccess )
+    {
+        (void)pa.done( stream );
+        (void)pb.done( stream );
+        return e;
+    }
     uint32_t *status = nullptr;
     if( (e = la_status_begin( stream, &status )) != hipSuccess )
+    {
+        (void)pa.done( stream );
+        (void)pb.done( stream );
         return e;
+    }
     const int help = la_help( (const void *)lowres_bidir_kernel<BD>, (int64_t)n * nbands, lds, stream );
     hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs,
-                        ra[0], ra[1], ra[2], ra[3], afs, rb[0], rb[1], rb[2], rb[3], bfs, stride, mbw, mbh, me_method,
+                        pa.base, pa.pd, pa.fs, pb.base, pb.pd, pb.fs, stride, mbw, mbh, me_method,
                         subme, satd, me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs,
                         dsf, weight, invq, lowres_costs, row_satd, est, nbands, brows4, la_poll_max(), status,
                         nslices, help );
-    if( (e = hipGetLastError()) != hipSuccess )
+    e = hipGetLastError();
+    const hipError_t ea = pa.done( stream ), eb = pb.done( stream );
+    if( e != hipSuccess || (e = ea) != hipSuccess || (e = eb) != hipSuccess )
         return e;
     return la_status_end( stream );
 }
@@ -1635,21 +1688,32 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
     if( mv_range < 1 || lds > 48 * 1024 )
         return hipErrorInvalidValue;
+    LaPlanes<typename PT<BD>::pixel> pr;
+    if( (e = pr.init( ref, rfs, stride, npairs, mbh, stream )) != hipSuccess )
+    {
+        (void)pr.done( stream );
+        return e;
+    }
     uint32_t *status = nullptr;
     if( (e = la_status_begin( stream, &status )) != hipSuccess )
+    {
+        (void)pr.done( stream );
         return e;
+    }
     auto go = [&]( auto kernel ) {
         const int help = la_help( (const void *)kernel, (int64_t)npairs * nbands, lds, stream );
-        hipLaunchKernelGGL( kernel, dim3( npairs * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs, ref[0],
-                            ref[1], ref[2], ref[3], stride, rfs, mbw, mbh, me_method, subme, satd, me_range, mv_range,
-                            lambda, cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands,
-                            brows4, la_poll_max(), status, ref_w, wscale, wdenom, woffset, nslices, help );
+        hipLaunchKernelGGL( kernel, dim3( npairs * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs, pr.base,
+                            pr.pd, stride, pr.fs, mbw, mbh, me_method, subme, satd, me_range, mv_range, lambda,
+                            cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4,
+                            la_poll_max(), status, ref_w, rfs, wscale, wdenom, woffset, nslices, help );
     };
     if( ref_w )
         go( lowres_inter_kernel<BD, true> );
     else
         go( lowres_inter_kernel<BD, false> );
-    if( (e = hipGetLastError()) != hipSuccess )
+    e = hipGetLastError();
+    const hipError_t ef = pr.done( stream );
+    if( e != hipSuccess || (e = ef) != hipSuccess )
         return e;
     return la_status_end( stream );
 }

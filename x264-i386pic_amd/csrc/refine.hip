@@ -592,7 +592,6 @@ static hipError_t refine_launch( const typename PT<BD>::pixel *fenc, intptr_t fs
                                  int32_t *out, int32_t *nevals, int nstride, const x264hip_refine_ext_t *xe,
                                  hipStream_t stream )
 {
-    using pixel = typename PT<BD>::pixel;
     if( n <= 0 )
         return hipSuccess;
     if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || ((uintptr_t)out & 15) )
