@@ -374,6 +374,18 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
     int bmx, bmy, bcost = LR_COST_MAX, bpred_cost = LR_COST_MAX;
     uint32_t pmv, bpred_mv = 0;
     int tmp[6][2];
+    // the integer search's window and its centre ((wx, wy) = the centre it was loaded at; a
+    // search step whose centre is unchanged scores from it instead of loading it again)
+    uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
+    int wx = 0x7fff, wy = 0x7fff;
+    auto window = [&]() __attribute__( ( always_inline ) ) {
+        if( bmx != wx || bmy != wy )
+        {
+            m.win( bmx, bmy, w );
+            wx = bmx;
+            wy = bmy;
+        }
+    };
 #define LR_COST_MV( mx, my )                                                                                  \
     do                                                                                                        \
     {                                                                                                         \
@@ -431,14 +443,29 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         bmx = (bpx + 2) >> 2;
         bmy = (bpy + 2) >> 2;
         bpred_mv = lr_pack( bpx, bpy );
+        // the integer search's first window, at the rounded predictor, and the (0, 0)
+        // candidate's rows go out together: COST_MV( bmx, bmy ) is the window's centre, and
+        // the search starts from this window unless (0, 0) wins -- one memory round where
+        // the candidates in turn took three
+        m.win( bmx, bmy, w );
+        wx = bmx;
+        wy = bmy;
+        const int z = m.fpel( 0, 0 );
         if( bpred_mv & 0x00030003u )
-            LR_COST_MV( bmx, bmy );
+            bcost = m.template wsad<0, 0>( w ) + m.bits_mvd( bmx, bmy );
         else
             bcost = bpred_cost;
         if( pmv )
         {
             if( bmx | bmy )
-                LR_COST_MV( 0, 0 );
+            {
+                const int c0 = z + m.bits_mvd( 0, 0 );
+                if( c0 < bcost )
+                {
+                    bcost = c0;
+                    bmx = bmy = 0;
+                }
+            }
         }
         else if( pmv_cost < bcost )
         {
@@ -491,8 +518,7 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         int i = me_range;
         do
         {
-            uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
-            m.win( bmx, bmy, w );
+            window();
             costs[0] = m.template wsad<0, -1>( w ) + m.bits_mvd( bmx, bmy - 1 );
             costs[1] = m.template wsad<0, 1>( w ) + m.bits_mvd( bmx, bmy + 1 );
             costs[2] = m.template wsad<-1, 0>( w ) + m.bits_mvd( bmx - 1, bmy );
@@ -521,8 +547,7 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
     } while( 0 )
 #define LR_W( DX, DY, W ) (m.template wsad<DX, DY>( W ) + m.bits_mvd( bmx + (DX), bmy + (DY) ))
         {
-            uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
-            m.win( bmx, bmy, w );
+            window();
             costs[0] = LR_W( -2, 0, w );
             costs[1] = LR_W( -1, 2, w );
             costs[2] = LR_W( 1, 2, w );
@@ -546,8 +571,7 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
             {
                 // the window scores all six hexagon points (c_hex2[0..5] order); the three
                 // the reference evaluates in this direction, c_hex2[dir .. dir+2], are picked
-                uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
-                m.win( bmx, bmy, w );
+                window();
                 const int s6[6] = { m.template wsad<-1, -2>( w ), m.template wsad<-2, 0>( w ),
                                     m.template wsad<-1, 2>( w ), m.template wsad<1, 2>( w ),
                                     m.template wsad<2, 0>( w ), m.template wsad<1, -2>( w ) };
@@ -573,8 +597,7 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         bcost >>= 3;
         bcost <<= 4;
         {
-            uint32_t w[LrCtx<BD>::WR][LrCtx<BD>::WD];
-            m.win( bmx, bmy, w );
+            window();                                    // the last hexagon step's, unless it moved
             const int c8[8] = { LR_W( 0, -1, w ), LR_W( 0, 1, w ), LR_W( -1, 0, w ), LR_W( 1, 0, w ),
                                 LR_W( -1, -1, w ), LR_W( -1, 1, w ), LR_W( 1, -1, w ), LR_W( 1, 1, w ) };
 #pragma unroll
