@@ -275,39 +275,48 @@ template <int BD> struct LrCtx
         return (int)lr_quad_sum( acc );
     }
 
-    // get_ref (mc.c:221-249) rows at a quarter-pel mv, weighted by m->weight when W and set
-    template <bool W = true>
-    __device__ __forceinline__ void ref_rows( int mx, int my, uint32_t (&r)[LR_NR][NDW] ) const
+    // get_ref (mc.c:221-249) rows at N quarter-pel mvs, weighted by m->weight when W and set.
+    // Branch-free: a one-plane position reads its plane twice (the rounding average of equal
+    // pixels is the pixel), so every candidate's loads are issued before any is waited on --
+    // N candidates cost one memory round
+    template <bool W = true, int N>
+    __device__ __forceinline__ void ref_rows_n( const int (&mx)[N], const int (&my)[N],
+                                                uint32_t (&r)[N][LR_NR][NDW] ) const
     {
-        const int idx = ((my & 3) << 2) + (mx & 3);
-        const intptr_t off = (intptr_t)(my >> 2) * stride + (mx >> 2);
-        const int i0 = (int)((k_lr_ref0 >> (2 * idx)) & 3), i1 = (int)((k_lr_ref1 >> (2 * idx)) & 3);
-        // (the plane by one multiply-add: the four planes equally spaced)
-        const pixel *s1 = p0 + i0 * pd + off + ((my & 3) == 3) * stride;
+        uint32_t b[N][LR_NR][NDW];
 #pragma unroll
-        for( int y = 0; y < LR_NR; y++ )
-            load_al_pad<NDW>( s1 + (intptr_t)y * stride, r[y] );
-        if( idx & 5 )                       // two planes: the rounding average
+        for( int n = 0; n < N; n++ )
         {
-            const pixel *s2 = p0 + i1 * pd + off + ((mx & 3) == 3);
+            const int idx = ((my[n] & 3) << 2) + (mx[n] & 3);
+            const intptr_t off = (intptr_t)(my[n] >> 2) * stride + (mx[n] >> 2);
+            const int i0 = (int)((k_lr_ref0 >> (2 * idx)) & 3), i1 = (int)((k_lr_ref1 >> (2 * idx)) & 3);
+            // (the plane by one multiply-add: the four planes equally spaced)
+            const pixel *s1 = p0 + i0 * pd + off + ((my[n] & 3) == 3) * stride;
+            const pixel *s2 = (idx & 5) ? p0 + i1 * pd + off + ((mx[n] & 3) == 3) : s1;
 #pragma unroll
             for( int y = 0; y < LR_NR; y++ )
             {
-                uint32_t b[NDW];
-                load_al_pad<NDW>( s2 + (intptr_t)y * stride, b );
-#pragma unroll
-                for( int k = 0; k < NDW; k++ )
-                    r[y][k] = avg_round<BD>( r[y][k], b[k] );
+                load_al_pad<NDW>( s1 + (intptr_t)y * stride, r[n][y] );
+                load_al_pad<NDW>( s2 + (intptr_t)y * stride, b[n][y] );
             }
         }
-        if( W && wgt )
-        {
+#pragma unroll
+        for( int n = 0; n < N; n++ )
 #pragma unroll
             for( int y = 0; y < LR_NR; y++ )
 #pragma unroll
                 for( int k = 0; k < NDW; k++ )
-                    r[y][k] = lr_weight_px<BD>( r[y][k], wsc, wrnd, wsh, woff );
-        }
+                {
+                    r[n][y][k] = avg_round<BD>( r[n][y][k], b[n][y][k] );
+                    if( W && wgt )
+                        r[n][y][k] = lr_weight_px<BD>( r[n][y][k], wsc, wrnd, wsh, woff );
+                }
+    }
+    template <bool W = true>
+    __device__ __forceinline__ void ref_rows( int mx, int my, uint32_t (&r)[LR_NR][NDW] ) const
+    {
+        const int ax[1] = { mx }, ay[1] = { my };
+        ref_rows_n<W, 1>( ax, ay, *reinterpret_cast<uint32_t( * )[1][LR_NR][NDW]>( &r ) );
     }
 
     // hpel plane rows addressed directly (TRY_BIDIR for subme <= 1, slicetype.c:594-600)
@@ -327,6 +336,17 @@ template <int BD> struct LrCtx
         uint32_t r[LR_NR][NDW];
         ref_rows<W>( mx, my, r );
         return lr_cmp_rows<BD>( fe, r, use_satd, q );
+    }
+    // two / three positions in one memory round: their SAD or SATD each (sat[n])
+    template <bool W = true, int N>
+    __device__ __forceinline__ void qpel_n( const int (&mx)[N], const int (&my)[N], const bool (&sat)[N],
+                                            int (&c)[N] ) const
+    {
+        uint32_t r[N][LR_NR][NDW];
+        ref_rows_n<W, N>( mx, my, r );
+#pragma unroll
+        for( int n = 0; n < N; n++ )
+            c[n] = lr_cmp_rows<BD>( fe, r[n], sat[n], q ) + cmx[mx[n]] + cmy[my[n]];
     }
 
     __device__ __forceinline__ int bits_mvd( int mx, int my ) const { return cmx[mx * 4] + cmy[my * 4]; }
@@ -689,8 +709,10 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         }
         bcost >>= 6;
     }
-    if( m.satd )
-        bcost = m.qpel( bmx, bmy, true ) + m.cmx[bmx] + m.cmy[bmy];                  // COST_MV_SATD( bmx, bmy, -1 )
+    // COST_MV_SATD( bmx, bmy, -1 ) (me.c:925 for the lookahead's refine): with the lane groups,
+    // in the first qpel iteration's memory round -- every group reads the centre beside its
+    // own candidate(s); else (no qpel step, the mv limits, one group) on its own
+    bool rescored = !m.satd;
     int bdir = -1;
     for( int i = qpel; i > 0; i-- )
     {
@@ -699,11 +721,52 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         const int odir = bdir;
         const int omx = bmx, omy = bmy;
         int cq[4] = { 0, 0, 0, 0 };
-        if( role >= 0 )
-            lr_batch4<NG>( role, [&]( int k ) {
-                const int qx = omx + (k == 2 ? -1 : k == 3 ? 1 : 0), qy = omy + (k == 0 ? -1 : k == 1 ? 1 : 0);
-                return m.qpel( qx, qy, m.satd ) + m.cmx[qx] + m.cmy[qy];
-            }, cq );
+        auto qpos = [&]( int k, int &qx, int &qy ) __attribute__( ( always_inline ) ) {
+            qx = omx + (k == 2 ? -1 : k == 3 ? 1 : 0);
+            qy = omy + (k == 0 ? -1 : k == 1 ? 1 : 0);
+        };
+        if( role >= 0 && !rescored )
+        {
+            if constexpr( NG == 4 )
+            {
+                int ax[2] = { omx, 0 }, ay[2] = { omy, 0 }, c2[2];
+                const bool st[2] = { true, m.satd != 0 };
+                qpos( role, ax[1], ay[1] );
+                m.qpel_n( ax, ay, st, c2 );
+                bcost = c2[0];
+#pragma unroll
+                for( int r = 0; r < 4; r++ )
+                    cq[r] = lr_gather<4>( c2[1], r );
+            }
+            else
+            {
+                int ax[3] = { omx, 0, 0 }, ay[3] = { omy, 0, 0 }, c3[3];
+                const bool st[3] = { true, m.satd != 0, m.satd != 0 };
+                qpos( role, ax[1], ay[1] );
+                qpos( role + 2, ax[2], ay[2] );
+                m.qpel_n( ax, ay, st, c3 );
+                bcost = c3[0];
+                cq[0] = lr_gather<2>( c3[1], 0 );
+                cq[1] = lr_gather<2>( c3[1], 1 );
+                cq[2] = lr_gather<2>( c3[2], 0 );
+                cq[3] = lr_gather<2>( c3[2], 1 );
+            }
+            rescored = true;
+        }
+        else
+        {
+            if( !rescored )
+            {
+                bcost = m.qpel( bmx, bmy, true ) + m.cmx[bmx] + m.cmy[bmy];
+                rescored = true;
+            }
+            if( role >= 0 )
+                lr_batch4<NG>( role, [&]( int k ) {
+                    int qx, qy;
+                    qpos( k, qx, qy );
+                    return m.qpel( qx, qy, m.satd ) + m.cmx[qx] + m.cmy[qy];
+                }, cq );
+        }
 #pragma unroll
         for( int dir = 0; dir < 4; dir++ )
         {
@@ -722,6 +785,8 @@ __device__ void lr_me_search( const LrCtx<BD> &m, int mvpx, int mvpy, const int 
         if( bmx == omx && bmy == omy )
             break;
     }
+    if( !rescored )
+        bcost = m.qpel( bmx, bmy, true ) + m.cmx[bmx] + m.cmy[bmy];
     omvx = bmx;
     omvy = bmy;
     ocost = bcost;
