@@ -412,7 +412,9 @@ const char *x264hip_backend_banner( void );
  * for other inputs (X264HIP_TESA_VARIANT=1: the in-scan SADs of me_range > 24;
  * X264HIP_INTEGRAL_VARIANT=1: the unaligned-plane integral kernel); X264HIP_UPLOAD_WGS caps
  * the upload grid; X264HIP_LA_HELPER=0 / 1 forces the lookahead's L2-warming helper wave off /
- * on (default: on when every band's workgroup fits on the GPU at once).  All are bit-exact;
+ * on (default: on when every band's workgroup fits on the GPU at once); X264HIP_LA_XCD=0 / 1
+ * forces the lookahead's bands of one frame pair onto one XCD off / on (default: on under the
+ * same condition).  All are bit-exact;
  * only speed differs.  One switch is a test hook:
  * X264HIP_LA_POLL bounds the lookahead wavefront's wait for the band below (default 2^22
  * tries); 0 forces the timeout path (see x264hip_lowres_status). */

@@ -65,7 +65,8 @@ def hip():
 
 
 _VARIANT_SWITCHES = ("X264HIP_TESA_VARIANT", "X264HIP_INTEGRAL_VARIANT", "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS",
-                     "X264HIP_ME_XCD", "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT", "X264HIP_LA_HELPER")
+                     "X264HIP_ME_XCD", "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT", "X264HIP_LA_HELPER",
+                     "X264HIP_LA_XCD")
 
 
 @pytest.fixture(autouse=True)

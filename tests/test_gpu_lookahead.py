@@ -401,3 +401,29 @@ def test_lowres_helper_forced(hip, oracle, helper, bd, kind):
             test_lowres_wait_timeout_reports_error(hip, oracle, "bidir")
     finally:
         hip.set_variant("X264HIP_LA_HELPER", None)
+
+
+@pytest.mark.parametrize("xcd", [0, 1])
+@pytest.mark.parametrize("kind", ["inter", "inter_random", "inter_slices", "bidir", "weighted", "timeout"])
+def test_lowres_xcd_forced(hip, oracle, xcd, kind):
+    """The band placement (lr_unit): by default every band of a pair runs on one XCD when the
+    grid is resident at once, so the other tests here run with it; X264HIP_LA_XCD forces it off
+    (bands in block order, what large batches use) or on (nine-pair launches leave the last
+    XCD's blocks idle).  Either way the results are the oracle's."""
+    hip.set_variant("X264HIP_LA_XCD", xcd)
+    try:
+        if kind == "inter":
+            _case(hip, oracle, 8, 1920, 1088, 9, 1, 4, True)
+        elif kind == "inter_random":
+            _case(hip, oracle, 10, 176, 144, 3, 1, 4, True, random=True, aq=True, me_range=8)
+        elif kind == "inter_slices":
+            _case(hip, oracle, 8, 1920, 1088, 2, 0, 2, False, n_slices=4)
+        elif kind == "bidir":
+            _bidir_case(hip, oracle, 8, 640, 352, 9, 3, 1, 4, True, 171, 43)
+        elif kind == "weighted":
+            test_lowres_inter_weighted_1080p(hip, oracle, 8, (40, 5, -6))
+        else:
+            test_lowres_wait_timeout_reports_error(hip, oracle, "inter")
+            test_lowres_wait_timeout_reports_error(hip, oracle, "bidir")
+    finally:
+        hip.set_variant("X264HIP_LA_XCD", None)

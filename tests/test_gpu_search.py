@@ -86,3 +86,11 @@ def test_search_args(hip):
         with pytest.raises(RuntimeError):
             hip.me_search_ref(p, 32 * 256 + 32, 256, p, [p, p, p, p], 32 * 256 + 32, 256, i_pixel, me, subme, rng,
                               pos, par, mvc, (t.view(torch.int16), 0))
+
+
+@pytest.mark.parametrize("bd,me_method", [(8, 1), (10, 2)])
+def test_search_2160p(hip, oracle, bd, me_method):
+    """every 16x16 partition of a 3840x2160 frame pair (configs[3]'s frame size): HEX at 8 bit,
+    UMH at 10 bit, subme 7 with chroma ME"""
+    got, par, ne = _run(hip, oracle, bd, 1, 3840, 2160, 1, 0, me_method, 7, 16, 0, 1, seed=71 + bd)
+    assert (got[:, 1:3] != 0).any(1).mean() > 0.5

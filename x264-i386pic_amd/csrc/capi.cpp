@@ -244,7 +244,7 @@ extern "C" int x264hip_me_table_pitch( int bitdepth, int range, int centred )
 namespace x264hip {
 static const char *const k_variant_env[V_COUNT] = {
     "X264HIP_TESA_VARIANT", "X264HIP_INTEGRAL_VARIANT", "X264HIP_LA_POLL", "X264HIP_UPLOAD_WGS", "X264HIP_ME_XCD",
-    "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT", "X264HIP_LA_HELPER" };
+    "X264HIP_STREAM_XCD", "X264HIP_STREAM_NT", "X264HIP_LA_HELPER", "X264HIP_LA_XCD" };
 
 struct VariantTable
 {

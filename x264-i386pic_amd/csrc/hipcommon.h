@@ -267,6 +267,7 @@ namespace x264hip {
 enum VariantSlot
 {
     V_TESA = 0, V_INTEGRAL, V_LA_POLL, V_UPLOAD_WGS, V_ME_XCD, V_STREAM_XCD, V_STREAM_NT, V_LA_HELPER,
+    V_LA_XCD,
     V_COUNT
 };
 int variant( VariantSlot slot );

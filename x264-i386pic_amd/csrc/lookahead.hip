@@ -951,6 +951,26 @@ __device__ __forceinline__ void lr_load_fenc( const typename PT<BD>::pixel *fb, 
     }
 }
 
+// The band a workgroup runs: pair f, band j.  xpairs = 0: block b is band b % nbands of pair
+// b / nbands.  Else every band of a pair runs on one XCD (the dispatcher deals blocks
+// round-robin over the 8 XCDs, block b on XCD b % 8): XCD x's i-th block is band i % nbands
+// of pair x + 8 * (i / nbands), so the bands that share reference rows and hand mvs over
+// share an L2, and a band's producer (band j - 1, block b - 8) is still dispatched first.
+// Blocks past the last pair (xpairs not a multiple of 8) return.
+__device__ __forceinline__ bool lr_unit( int nbands, int xpairs, int &f, int &j )
+{
+    if( !xpairs )
+    {
+        f = (int)blockIdx.x / nbands;
+        j = (int)blockIdx.x % nbands;
+        return true;
+    }
+    const int x = (int)(blockIdx.x & 7), i = (int)(blockIdx.x >> 3);
+    f = x + 8 * (i / nbands);
+    j = i % nbands;
+    return f < xpairs;
+}
+
 // The helper wave (la_help): a second wave in the band's workgroup that reads,
 // LR_AHEAD steps before the searching wave gets there, one dword of every pixel row the band's
 // searches can reach in the column its blocks enter -- the reference planes (rows 8*y0 - 16 ..
@@ -1041,16 +1061,18 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     const uint16_t *__restrict__ invq, int16_t *__restrict__ mvs, int32_t *__restrict__ mv_costs,
     uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd, int32_t *__restrict__ est, int nbands, int brows,
     int poll_max, uint32_t *status, const typename PT<BD>::pixel *rw, intptr_t wfs, int wscale, int wdenom,
-    int woffset, int nslices, int help )
+    int woffset, int nslices, int help, int xpairs )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring[4 * LR_BAND];            // packed MVs of each band row's 4 latest blocks
     __shared__ int prog;                         // the searching wave's step (helper wave)
     extern __shared__ uint16_t lr_cost_lds[];
     const uint16_t *cml = lr_stage_cost( lr_cost_lds, cost_mv, mv_range );
-    const int f = blockIdx.x / nbands;
+    int f, jb;
+    if( !lr_unit( nbands, xpairs, f, jb ) )
+        return;
     int s1, y0, y1;                               // the band's rows [y0, y1) of a slice ending at s1
-    lr_band( (int)(blockIdx.x % nbands), mbh, nslices, brows, s1, y0, y1 );
+    lr_band( jb, mbh, nslices, brows, s1, y0, y1 );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     r0 += (intptr_t)f * rfs;
@@ -1232,16 +1254,19 @@ __global__ __launch_bounds__( 128 ) void lowres_bidir_kernel(
     const uint16_t *__restrict__ cost_mv, int search, int16_t *__restrict__ mvs0, int32_t *__restrict__ costs0,
     int16_t *__restrict__ mvs1, int32_t *__restrict__ costs1, const int16_t *__restrict__ p1mvs, int dsf, int weight,
     const uint16_t *__restrict__ invq, uint16_t *__restrict__ lcosts, int32_t *__restrict__ row_satd,
-    int32_t *__restrict__ est, int nbands, int brows, int poll_max, uint32_t *status, int nslices, int help )
+    int32_t *__restrict__ est, int nbands, int brows, int poll_max, uint32_t *status, int nslices, int help,
+    int xpairs )
 {
     constexpr int NDW = LrCtx<BD>::NDW;
     __shared__ int ring0[4 * LR_BAND], ring1[4 * LR_BAND];      // per list
     __shared__ int prog;                                        // the searching wave's step
     extern __shared__ uint16_t lr_cost_lds[];
     const uint16_t *cml = lr_stage_cost( lr_cost_lds, cost_mv, mv_range );
-    const int f = blockIdx.x / nbands;
+    int f, jb;
+    if( !lr_unit( nbands, xpairs, f, jb ) )
+        return;
     int s1, y0, y1;                               // the band's rows [y0, y1) of a slice ending at s1
-    lr_band( (int)(blockIdx.x % nbands), mbh, nslices, brows, s1, y0, y1 );
+    lr_band( jb, mbh, nslices, brows, s1, y0, y1 );
     const int nmb = mbw * mbh;
     fenc += (intptr_t)f * ffs;
     a0 += (intptr_t)f * afs;
@@ -1609,6 +1634,7 @@ int la_nbands( int mbh, int nslices, int brows )
     return n;
 }
 
+
 int la_poll_max()
 {
     const int v = variant( V_LA_POLL );
@@ -1618,17 +1644,35 @@ int la_poll_max()
 // the helper wave of lr_helper: on when every band's workgroup, helper included, is resident at
 // once (it rides on wave slots the launch leaves idle: the 15-pair launches; a 240-pair batch
 // would double its waves and queue them), X264HIP_LA_HELPER=0 / 1 forces it off / on
+// every one of nwg two-wave workgroups of `kernel` resident at once
+bool la_fits( const void *kernel, int64_t nwg, size_t lds, hipStream_t stream )
+{
+    int dev = 0, cus = 0, per_cu = 0;
+    if( stream_device( stream, &dev ) != hipSuccess ||
+        hipDeviceGetAttribute( &cus, hipDeviceAttributeMultiprocessorCount, dev ) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor( &per_cu, kernel, 128, lds ) != hipSuccess )
+        return false;
+    return nwg <= (int64_t)cus * per_cu;
+}
 int la_help( const void *kernel, int64_t nwg, size_t lds, hipStream_t stream )
 {
     const int v = variant( V_LA_HELPER );
     if( v >= 0 )
         return v == 1;
-    int dev = 0, cus = 0, per_cu = 0;
-    if( stream_device( stream, &dev ) != hipSuccess ||
-        hipDeviceGetAttribute( &cus, hipDeviceAttributeMultiprocessorCount, dev ) != hipSuccess ||
-        hipOccupancyMaxActiveBlocksPerMultiprocessor( &per_cu, kernel, 128, lds ) != hipSuccess )
-        return 0;
-    return nwg <= (int64_t)cus * per_cu;
+    return la_fits( kernel, nwg, lds, stream );
+}
+
+// The grid of n units (pairs / triplets) of nbands bands, and lr_unit's xpairs: every band of a
+// unit on one XCD when that grid is resident at once (the 15-pair launches: P 1.229 -> 1.203,
+// B 1.783 -> 1.752 ms, 4 slices 0.823 -> 0.790 in an interleaved A/B, profiles/r05x_la_xcd_ab.log;
+// a 240-pair batch, which queues its workgroups, ran slower so: 2.25 -> 2.38 ms), else in
+// block order.  X264HIP_LA_XCD=0 / 1 forces it off / on.
+int64_t la_grid( const void *kernel, int n, int nbands, size_t lds, hipStream_t stream, int &xpairs )
+{
+    const int64_t nx = (int64_t)8 * nbands * ((n + 7) / 8);
+    const int v = variant( V_LA_XCD );
+    xpairs = (v == 1 || (v < 0 && la_fits( kernel, nx, lds, stream ))) ? n : 0;
+    return xpairs ? nx : (int64_t)n * nbands;
 }
 } // namespace
 
@@ -1714,7 +1758,7 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
     constexpr int brows = 4;
     constexpr int brows4 = brows;                // a wave holds four roles of <= 4 rows
     const int nbands = la_nbands( mbh, nslices, brows4 );
-    if( nslices < 1 || (int64_t)n * nbands > 0x7fffffff )
+    if( nslices < 1 || (int64_t)(n + 8) * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
     if( mv_range < 1 || lds > 48 * 1024 )
@@ -1734,12 +1778,14 @@ hipError_t launch_lowres_bidir( const typename PT<BD>::pixel *fenc, intptr_t ffs
         (void)pb.done( stream );
         return e;
     }
-    const int help = la_help( (const void *)lowres_bidir_kernel<BD>, (int64_t)n * nbands, lds, stream );
-    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( n * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs,
+    int xp = 0;
+    const int64_t nwg = la_grid( (const void *)lowres_bidir_kernel<BD>, n, nbands, lds, stream, xp );
+    const int help = la_help( (const void *)lowres_bidir_kernel<BD>, nwg, lds, stream );
+    hipLaunchKernelGGL( lowres_bidir_kernel<BD>, dim3( (unsigned)nwg ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs,
                         pa.base, pa.pd, pa.fs, pb.base, pb.pd, pb.fs, stride, mbw, mbh, me_method,
                         subme, satd, me_range, mv_range, lambda, cost_mv, search, mvs0, costs0, mvs1, costs1, p1mvs,
                         dsf, weight, invq, lowres_costs, row_satd, est, nbands, brows4, la_poll_max(), status,
-                        nslices, help );
+                        nslices, help, xp );
     e = hipGetLastError();
     const hipError_t ea = pa.done( stream ), eb = pb.done( stream );
     if( e != hipSuccess || (e = ea) != hipSuccess || (e = eb) != hipSuccess )
@@ -1771,7 +1817,7 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
     constexpr int brows = 4;
     constexpr int brows4 = brows;                // four groups of <= 4 rows per wave
     const int nbands = la_nbands( mbh, nslices, brows4 );
-    if( nslices < 1 || (int64_t)npairs * nbands > 0x7fffffff )
+    if( nslices < 1 || (int64_t)(npairs + 8) * nbands > 0x7fffffff )
         return hipErrorInvalidValue;
     const size_t lds = (size_t)(2 * (4 * mv_range + 64) + 1) * sizeof( uint16_t );
     if( mv_range < 1 || lds > 48 * 1024 )
@@ -1789,11 +1835,13 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
         return e;
     }
     auto go = [&]( auto kernel ) {
-        const int help = la_help( (const void *)kernel, (int64_t)npairs * nbands, lds, stream );
-        hipLaunchKernelGGL( kernel, dim3( npairs * nbands ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs, pr.base,
+        int xp = 0;
+        const int64_t nwg = la_grid( (const void *)kernel, npairs, nbands, lds, stream, xp );
+        const int help = la_help( (const void *)kernel, nwg, lds, stream );
+        hipLaunchKernelGGL( kernel, dim3( (unsigned)nwg ), dim3( help ? 128 : 64 ), lds, stream, fenc, ffs, pr.base,
                             pr.pd, stride, pr.fs, mbw, mbh, me_method, subme, satd, me_range, mv_range, lambda,
                             cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4,
-                            la_poll_max(), status, ref_w, rfs, wscale, wdenom, woffset, nslices, help );
+                            la_poll_max(), status, ref_w, rfs, wscale, wdenom, woffset, nslices, help, xp );
     };
     if( ref_w )
         go( lowres_inter_kernel<BD, true> );
