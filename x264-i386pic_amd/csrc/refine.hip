@@ -330,11 +330,18 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         for( int k = 0; k < 4; k++ )
             c[k] = (int)__shfl( (int)v, sbase + NT * k );
     };
+    // one candidate: group 0 scores it, the other groups' lanes stay masked off (no loads)
     auto eval1 = [&]( int mx, int my, bool satd ) __attribute__( ( always_inline ) ) {
-        const int m4x[4] = { mx, mx, mx, mx }, m4y[4] = { my, my, my, my };
-        int c[4];
-        eval4( m4x, m4y, satd, c );
-        return c[0];
+        uint32_t v = 0;
+        if( g == 0 )
+        {
+            v = satd ? tile_cost<BD, true, EXT != 0>( fa, q0, q1, q2, q3, rs, mx, my, wt0 ) >> 1
+                     : tile_cost<BD, false, EXT != 0>( fa, q0, q1, q2, q3, rs, mx, my, wt0 );
+            if( u == 0 )
+                v += (uint32_t)cmx[mx] + (uint32_t)cmy[my];
+        }
+        v = group_sum<NT>( v );
+        return (int)__shfl( (int)v, sbase );
     };
     // the chroma costs (mbcmp: SATD for subme > 1) of the diamond of step st around (ox, oy) in
     // the order (0, -st), (0, +st), (-st, 0), (+st, 0) -- st = 0: the centre in every group: U in
@@ -344,12 +351,13 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         const int gx = ox + (g == 2 ? -st : g == 3 ? st : 0);
         const int gy = oy + (g == 0 ? -st : g == 1 ? st : 0);
         uint32_t vu = 0, vv = 0;
+        const bool on = st != 0 || g == 0;               // st = 0: group 0 scores the centre alone
         if constexpr( EXT == 1 )
         {
             const int mvyc = (2 * (gy + ext.mvy_offset)) >> ext.vs;
 #pragma unroll
             for( int k = 0; k < 2; k++ )
-                if( cpl[k] >= 0 )
+                if( on && cpl[k] >= 0 )
                 {
                     const uint32_t c = nv_block_cost<BD>( cref[k], ext.rcs, gx, mvyc, cfb[k], ext.wt[1 + cpl[k]],
                                                           qsatd );
@@ -361,7 +369,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         }
         else if constexpr( EXT == 2 )
         {
-            if( tile )
+            if( tile && on )
             {
                 if( qsatd )
                 {
