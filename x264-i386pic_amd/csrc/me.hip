@@ -647,8 +647,9 @@ template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, co
 // packed keys (cost << 12 | raster index in the clipped, width-rounded window,
 // encoder/me.c:618-631, cost_mv terms me.c:60-70) and min-reduced in registers instead of
 // written out: the table never leaves the chip.  Each of an MB's G lanes meets the others
-// through one atomicMin into the MB's key slot (out[3*mb]), and me_esa_finish_kernel applies
-// the strict-< update from the predictor cost.  A workgroup holds whole MBs (256 / G of
+// through one LDS atomicMin into the MB's key slot, and after the workgroup's barrier one lane
+// per MB applies the strict-< update from the predictor cost and writes { cost, mx, my } (no
+// key fill, no finishing kernel: 10 bit keeps those).  A workgroup holds whole MBs (256 / G of
 // them), whose lanes first stage the MB's per-row key terms in LDS (ycost, row part of the
 // raster index, row validity), so a candidate row costs one LDS read instead of a clamped
 // global load and its index arithmetic.
@@ -673,7 +674,8 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
                                                                 const uint16_t *__restrict__ cost_mv,
                                                                 uint32_t *__restrict__ keys, int xcd,
                                                                 uint16_t *__restrict__ tab,
-                                                                int16_t *__restrict__ torg )
+                                                                int16_t *__restrict__ torg,
+                                                                const int32_t *__restrict__ init_cost )
 {
     constexpr int G = esa7_groups<R>();         // column groups per MB
     constexpr int P = cen_pitch( 8, R );        // the centred template's pitch (me_window's clamp)
@@ -683,6 +685,7 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
     constexpr int SP = W | 1;                   // LDS row-term pitch (odd: spread banks)
     __shared__ uint32_t s_row[MPW * SP];
     __shared__ uint32_t s_need[MPW];
+    __shared__ uint32_t s_key[MPW];             // the MBs' best keys (the workgroup holds whole MBs)
     const uint32_t nmb = (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw;
     const int tid = (int)threadIdx.x;
     const bool spare = tid >= MPW * G;
@@ -720,7 +723,10 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
     // this MB's window needs the columns past the G groups
     const bool need = live && min_x + width - 1 - ox >= 4 * G;
     if( !spare && grp == 0 )
+    {
         s_need[lmb] = need;
+        s_key[lmb] = 0xFFFFFFFFu;
+    }
     // row terms S[c] = ycost << 12 | (my - min_y) * width for candidate row c (my = oy + c)
     // inside [min_y, max_y], all ones outside; the MB's lanes stage them together
     if( TAB && !spare && live && grp == 0 )
@@ -840,7 +846,29 @@ __global__ __launch_bounds__( 256 ) void me_full_esa_v7_kernel( const uint8_t *_
             me_rows7<R, ME_LEAD>( rmb + G, (int)(rs / 4), F, acc, reduce, std::make_integer_sequence<int, 2 * R + 16>{} );
         }
         if( live && key < 0xF0000000u )
-            atomicMin( keys + 3 * mb, key );
+            atomicMin( &s_key[lmb], key );
+        __syncthreads();
+        // the strict-< update from the predictor result (COPY3_IF_LT, me.h:87-93): { cost, mx, my }
+        if( tid < MPW && wg0 + (uint32_t)tid < nmb )
+        {
+            const int64_t i = wg0 + (uint32_t)tid;
+            const int16_t *q = par + 8 * i;
+            const int qx = q[0], qy = q[1];
+            const int mnx = max( qx - me_range, (int)q[4] ), mny = max( qy - me_range, (int)q[5] );
+            const int wd = (min( qx + me_range, (int)q[6] ) - mnx + 3) & ~3;
+            const uint32_t k = s_key[tid];
+            int32_t bc = init_cost[i], rx = qx, ry = qy;
+            if( k != 0xFFFFFFFFu && (int32_t)(k >> 12) < bc )
+            {
+                const int ki = (int)(k & 4095);
+                bc = (int32_t)(k >> 12);
+                ry = mny + ki / wd;
+                rx = mnx + ki % wd;
+            }
+            keys[3 * i] = (uint32_t)bc;
+            keys[3 * i + 1] = (uint32_t)rx;
+            keys[3 * i + 2] = (uint32_t)ry;
+        }
     }
 }
 
@@ -958,9 +986,14 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
         (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
           (uintptr_t)(rs * sizeof( typename PT<BD>::pixel ))) & 3) )
         return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync( out, 0xFF, (size_t)nmb * 3 * sizeof( int32_t ), stream );
-    if( e != hipSuccess )
-        return e;
+    // 10 bit: the lanes meet in out[3*mb] by atomicMin, then me_esa_finish_kernel; 8 bit: in
+    // the workgroup's LDS, which also applies the predictor update (no fill, no second kernel)
+    if( BD != 8 )
+    {
+        const hipError_t e = hipMemsetAsync( out, 0xFF, (size_t)nmb * 3 * sizeof( int32_t ), stream );
+        if( e != hipSuccess )
+            return e;
+    }
     // 8 bit: whole MBs per workgroup (esa7_mbs); 10 bit: a flat lane index over column pairs
     const int64_t mpw = range == 4 ? esa7_mbs<4>() : range == 8 ? esa7_mbs<8>() : range == 16 ? esa7_mbs<16>()
                                                                                                : esa7_mbs<24>();
@@ -974,7 +1007,7 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
             if constexpr( BD == 8 )                                                                               \
                 hipLaunchKernelGGL( ( me_full_esa_v7_kernel<R, false> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, \
                                     rfs, mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out, xcd,         \
-                                    nullptr, nullptr );                                                           \
+                                    nullptr, nullptr, init_cost );                                                \
             else                                                                                                  \
                 hipLaunchKernelGGL( ( me_full_esa_v5_kernel<R> ), g, blk, 0, stream, fenc, fs, ffs, ref, rs, rfs, \
                                     mbw, mbh, nframes, me_range, par, cost_mv, (uint32_t *)out, xcd );            \
@@ -983,8 +1016,9 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
 #undef ESA_CASE
         default: return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL( me_esa_finish_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream, (int)nmb,
-                        me_range, par, init_cost, out );
+    if( BD != 8 )
+        hipLaunchKernelGGL( me_esa_finish_kernel, dim3( (unsigned)((nmb + 255) / 256) ), dim3( 256 ), 0, stream,
+                            (int)nmb, me_range, par, init_cost, out );
     return hipGetLastError();
 }
 
@@ -1892,7 +1926,8 @@ hipError_t launch_me_tesa( const typename PT<BD>::pixel *fenc, intptr_t fs, intp
                             hipLaunchKernelGGL( ( me_full_esa_v7_kernel<RR, true> ),                              \
                                                 dim3( (unsigned)((nmb + esa7_mbs<RR>() - 1) / esa7_mbs<RR>()) ),  \
                                                 dim3( 256 ), 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,    \
-                                                nframes, me_range, par, cost_mv, nullptr, me_xcd(), ttab, org );  \
+                                                nframes, me_range, par, cost_mv, nullptr, me_xcd(), ttab, org,    \
+                                                nullptr );                                                        \
                             break;
                         TT_CASE( 4 ) TT_CASE( 8 ) TT_CASE( 16 ) TT_CASE( 24 )
 #undef TT_CASE
