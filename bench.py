@@ -779,7 +779,9 @@ def rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F):
     # hands over many (b, p0) pairs at once; the 15-pair leg above is per-pair latency
     nrep = 16
     bf = louts[0][1:].repeat(nrep, 1, 1)
-    br = [p[:-1].repeat(nrep, 1, 1) for p in louts]
+    # the four planes of the references in one buffer, equally spaced (x264's buffer_lowres)
+    bb = torch.stack([p[:-1] for p in louts]).repeat(1, nrep, 1, 1)
+    br = [bb[k] for k in range(4)]
     bi = lint.repeat(nrep, 1)
     bouts2 = x.lowres_inter_cost(bf, br, x.plane_stride(lw // 2), mbw, mbh, bi, (cm, span))
 
@@ -790,7 +792,7 @@ def rates_lookahead(x, a, world, louts, iouts, lw, mbw, mbh, F):
     res["lowres_me_batch_pairs_per_s"] = world * max(1, a.steps // 10) * bf.shape[0] / wall
     res["lowres_me_batch_launch_ms"] = ev_ms
     res["lowres_me_batch_pairs_per_launch"] = int(bf.shape[0])
-    del bf, br, bi, bouts2
+    del bf, br, bb, bi, bouts2
     # the B-frame leg on the same planes: (p0, b, p1) = (k, k+1, k+2) for the F-2 triplets, both
     # lists searched (a fresh slicetype_frame_cost with b_bidir), p1's list-0 mvs against p0 from
     # one untimed P search as the bidir predictor, equal weights (i_bipred_weight 32, dsf 128)

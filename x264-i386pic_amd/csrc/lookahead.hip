@@ -1713,7 +1713,7 @@ template <typename pixel> struct LaPlanes
         }
         const int nf = frame_stride ? nframes : 1;
         const intptr_t lo = 16 * stride + 32, len = (8 * (intptr_t)mbh + 33) * stride;
-        hipError_t e = hipMallocAsync( (void **)&scratch, (size_t)(4 * nf) * len * sizeof( pixel ), st );
+        hipError_t e = scratch_alloc( (void **)&scratch, (size_t)(4 * nf) * len * sizeof( pixel ), st );
         if( e != hipSuccess )
             return e;
         const int nx = (int)std::min<intptr_t>( (len + 255) / 256, 64 );
