@@ -1505,11 +1505,18 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
     const uint16_t *ib = sums_base + cxm + (intptr_t)min_y * rs;
     const uint32_t irs = (uint32_t)rs;
     const int rmax = rows + 7, ty0 = min_y - oy;
-    auto ldi = [&]( int j, uint32_t &v0, uint32_t &v8 ) {
+    // (the row's two sums packed in one dword, sum at +8 in the high half: one v_sad_u16 then
+    // scores both of a row's ADS terms against the packed encode sums)
+    auto ldi = [&]( int j, uint32_t &pv ) {
         const uint16_t *sp = ib + __umul24( (uint32_t)min( j, rmax ), irs );
-        v0 = sp[0];
-        v8 = sp[8];
+        pv = __builtin_amdgcn_perm( (uint32_t)sp[8], (uint32_t)sp[0], 0x05040100u );
     };
+    const uint32_t dc01 = (uint32_t)enc_dc[0] | ((uint32_t)enc_dc[1] << 16);
+    const uint32_t dc23 = (uint32_t)enc_dc[2] | ((uint32_t)enc_dc[3] << 16);
+    // every candidate a lane can stage is in the table (the row / column ranges of the window
+    // inside the table's): wave-uniform, so the per-row test for the rare outside candidate
+    // is skipped by a scalar branch
+    const bool covered = !TAB || __all( (!active || colin) && (rows == 0 || (min_y - oy >= 0 && max_y - oy < W)) );
     auto ldt = [&]( int r ) -> uint32_t {
         if constexpr( TAB )
             return (uint32_t)tab[__umul24( (uint32_t)min( max( ty0 + r, 0 ), W - 1 ), (uint32_t)P ) + txc];
@@ -1547,25 +1554,25 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
     // the rows 8 below (slot (c + 8 / CK) % D); table rows for the current chunk only
     static_assert( CK == 1 || CK == 2 || CK == 4 || CK == 8, "CK divides the 8-row ads offset" );
     constexpr int D = 8 / CK + 1;
-    uint32_t i0[D][CK], i8[D][CK], tt[CK];
+    uint32_t ip[D][CK], tt[CK];
 #pragma unroll
     for( int q = 0; q < D; q++ )
 #pragma unroll
         for( int k = 0; k < CK; k++ )
-            ldi( CK * q + k, i0[q][k], i8[q][k] );
+            ldi( CK * q + k, ip[q][k] );
 #pragma unroll
     for( int k = 0; k < CK; k++ )
         tt[k] = ldt( k );
 #pragma unroll
     for( int c = 0; c < NC; c++ )
     {
-        uint32_t n0[CK], n8[CK], nt[CK];
+        uint32_t n0[CK], nt[CK];
         if( c + 1 < NC )
         {
 #pragma unroll
             for( int k = 0; k < CK; k++ )
             {
-                ldi( CK * (c + D) + k, n0[k], n8[k] );    // chunk c + D, into slot c % D after use
+                ldi( CK * (c + D) + k, n0[k] );           // chunk c + D, into slot c % D after use
                 nt[k] = ldt( CK * (c + 1) + k );
             }
         }
@@ -1581,12 +1588,9 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
             const int r = CK * c + k;
             if( r >= NR )
                 break;
-            // |dc - sum| + acc in one v_sad_u32 each (every operand is a non-negative sum)
-            const uint32_t av = sad_u32( (uint32_t)enc_dc[0], i0[st][k],
-                                         sad_u32( (uint32_t)enc_dc[1], i8[st][k],
-                                                  sad_u32( (uint32_t)enc_dc[2], i0[sb][k],
-                                                           sad_u32( (uint32_t)enc_dc[3], i8[sb][k],
-                                                                    (uint32_t)fpel ) ) ) );
+            // |dc - sum| + acc, two terms per v_sad_u16 (sums and DCs are 16-bit)
+            const uint32_t av = __builtin_amdgcn_sad_u16( ip[st][k], dc01,
+                                                          __builtin_amdgcn_sad_u16( ip[sb][k], dc23, (uint32_t)fpel ) );
             const uint32_t ads = r < rows && active ? av : 0xFFFFFFFFu;
             uint32_t sr = 0xFFFFFFFFu;
             if constexpr( TAB )
@@ -1597,7 +1601,7 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
                 const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
                 const bool need = r < rows && ads < (uint32_t)ub;
                 sr = tt[k];
-                if( need && !(colin && ty >= 0 && ty < W) )
+                if( !covered && need && !(colin && ty >= 0 && ty < W) )
                     sr = tesa_sad16<BD>( fl, p_fref + (min_y + r) * rs + mx, rs );
                 sr = need ? sr + (uint32_t)fpel : 0xFFFFFFFFu;
             }
@@ -1658,8 +1662,7 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
 #pragma unroll
             for( int k = 0; k < CK; k++ )
             {
-                i0[st][k] = n0[k];
-                i8[st][k] = n8[k];
+                ip[st][k] = n0[k];
                 tt[k] = nt[k];
             }
         }
