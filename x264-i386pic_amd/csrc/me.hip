@@ -1488,6 +1488,11 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
     const int yc1 = lane + SEG < rows ? (int)cy[(min_y + lane + SEG) * 4] : 0;
     const int bbase = 4 * SEG * sg;                           // this segment's lane 0, in bytes
     auto ycost_of = [&]( int r ) { return (int)seg_bcast<SEG>( (uint32_t)(r < SEG ? yc0 : yc1), r % SEG, bbase ); };
+    // row r's speculative ADS bound (bsad0 - ycost)*17>>4 (0 when ycost >= bsad0), per lane like
+    // the ycosts and broadcast the same way
+    auto ubound = [&]( int yc ) { return bsad0 > yc ? (bsad0 - yc) * 17 >> 4 : 0; };
+    const int ub0 = ubound( yc0 ), ub1 = ubound( yc1 );
+    auto ub_of = [&]( int r ) { return (int)seg_bcast<SEG>( (uint32_t)(r < SEG ? ub0 : ub1), r % SEG, bbase ); };
 
     // Staging: each row's ads4 value and -- with a table -- the cost of every candidate
     // that can still pass some row's threshold (bsad never rises, so row r's ADS threshold
@@ -1598,7 +1603,7 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
                 // with a table the SADs are reads (the rare candidate outside it computed)
                 const int ycost = ycost_of( r ), ty = min_y + r - oy;
                 ys_k[k] = ycost;
-                const int ub = bsad0 > ycost ? (bsad0 - ycost) * 17 >> 4 : 0;
+                const int ub = ub_of( r );
                 const bool need = r < rows && ads < (uint32_t)ub;
                 sr = tt[k];
                 if( !covered && need && !(colin && ty >= 0 && ty < W) )
@@ -1699,25 +1704,40 @@ __device__ __forceinline__ void tesa_scan_mb( const typename PT<BD>::pixel *__re
         if( !any( need ) )
             break;
         // first index of the largest sad: max of (sad << 32 | ~index)
-        uint64_t key = 0;
-        for( int j = lane; any( need && j < nmvsad ); j += SEG )
+        int bi;
+        if constexpr( SEG == 32 )
         {
-            if( need && j < nmvsad )
-            {
-                const uint64_t k = ((uint64_t)ecost( mvsads[j] ) << 32) | (uint32_t)~j;
-                key = k > key ? k : key;
-            }
+            // 32-bit keys (cost < 2^21, index < 2^11: the list holds <= 33 x 32 entries): the
+            // segment's maximum as the DPP prefix minimum of the complements
+            uint32_t nk = 0xFFFFFFFFu;
+            for( int j = lane; any( need && j < nmvsad ); j += SEG )
+                if( need && j < nmvsad )
+                    nk = min( nk, ~((ecost( mvsads[j] ) << 11) | (2047u - (uint32_t)j)) );
+            const uint32_t km = ~seg_lane<SEG>( seg_scan_min<SEG>( nk ), SEG - 1, sg );
+            bi = 2047 - (int)(km & 2047u);
         }
-#pragma unroll
-        for( int off = SEG / 2; off >= 1; off >>= 1 )
+        else
         {
-            const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor( (int)(key >> 32), off ) << 32) |
-                               (uint32_t)__shfl_xor( (int)(uint32_t)key, off );
-            key = o > key ? o : key;
+            uint64_t key = 0;
+            for( int j = lane; any( need && j < nmvsad ); j += SEG )
+            {
+                if( need && j < nmvsad )
+                {
+                    const uint64_t k = ((uint64_t)ecost( mvsads[j] ) << 32) | (uint32_t)~j;
+                    key = k > key ? k : key;
+                }
+            }
+#pragma unroll
+            for( int off = SEG / 2; off >= 1; off >>= 1 )
+            {
+                const uint64_t o = ((uint64_t)(uint32_t)__shfl_xor( (int)(key >> 32), off ) << 32) |
+                                   (uint32_t)__shfl_xor( (int)(uint32_t)key, off );
+                key = o > key ? o : key;
+            }
+            bi = (int)~(uint32_t)key;
         }
         if( need )
         {
-            const int bi = (int)~(uint32_t)key;
             nmvsad--;
             if( lane == 0 )
                 mvsads[bi] = mvsads[nmvsad];
