@@ -1712,6 +1712,8 @@ template <typename pixel> struct LaPlanes
             return hipSuccess;
         }
         const int nf = frame_stride ? nframes : 1;
+        if( nf > 65535 )                          // (the gather grid's y dimension)
+            return hipErrorInvalidValue;
         const intptr_t lo = 16 * stride + 32, len = (8 * (intptr_t)mbh + 33) * stride;
         hipError_t e = scratch_alloc( (void **)&scratch, (size_t)(4 * nf) * len * sizeof( pixel ), st );
         if( e != hipSuccess )
