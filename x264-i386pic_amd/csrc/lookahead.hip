@@ -1052,7 +1052,7 @@ __device__ __forceinline__ void lr_band( int j, int mbh, int nslices, int brows,
 
 // WGT: the weighted-reference form (rw, the scale / denom / offset); the unweighted kernel
 // carries none of its code or live values
-template <int BD, bool WGT>
+template <int BD, bool WGT, bool LAT>
 __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t ffs, const typename PT<BD>::pixel *r0,
     intptr_t rpd,
@@ -1084,6 +1084,22 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
     mvs += 2 * (intptr_t)f * nmb;
     mv_costs += (intptr_t)f * nmb;
     lcosts += (intptr_t)f * nmb;
+    // LAT (a launch whose bands are all resident: each step's latency is the time): the output
+    // pointers, stored to once per step, held in VGPRs (an opaque per-lane zero added) --
+    // scalar registers are the kernel's scarce ones (their spills go through VGPR lanes); the
+    // extra VGPRs cost a wave per SIMD, which a queued (throughput) launch keeps
+    if constexpr( LAT )
+    {
+        int z;
+        asm volatile( "v_mov_b32 %0, 0" : "=v"( z ) );
+        mv_costs += z;
+        lcosts += z;
+        intra_cost += z;
+        if( invq )
+            invq += z;
+        if( row_satd )
+            row_satd += z;
+    }
     uint32_t *gmv = (uint32_t *)mvs;
     int e0 = 0, e1 = 0, e2 = 0, racc = 0;
     const int mvr = 2 * mv_range;
@@ -1845,10 +1861,22 @@ hipError_t launch_lowres_inter( const typename PT<BD>::pixel *fenc, intptr_t ffs
                             cost_mv, intra_cost, invq, mvs, mv_costs, lowres_costs, row_satd, est, nbands, brows4,
                             la_poll_max(), status, ref_w, rfs, wscale, wdenom, woffset, nslices, help, xp );
     };
+    // the latency form when its grid (bands placed by XCD) is resident at once
+    const int64_t nx = (int64_t)8 * nbands * ((npairs + 7) / 8);
     if( ref_w )
-        go( lowres_inter_kernel<BD, true> );
+    {
+        if( la_fits( (const void *)lowres_inter_kernel<BD, true, true>, nx, lds, stream ) )
+            go( lowres_inter_kernel<BD, true, true> );
+        else
+            go( lowres_inter_kernel<BD, true, false> );
+    }
     else
-        go( lowres_inter_kernel<BD, false> );
+    {
+        if( la_fits( (const void *)lowres_inter_kernel<BD, false, true>, nx, lds, stream ) )
+            go( lowres_inter_kernel<BD, false, true> );
+        else
+            go( lowres_inter_kernel<BD, false, false> );
+    }
     e = hipGetLastError();
     const hipError_t ef = pr.done( stream );
     if( e != hipSuccess || (e = ef) != hipSuccess )
