@@ -1095,6 +1095,8 @@ __global__ __launch_bounds__( 128 ) void lowres_inter_kernel(
         mv_costs += z;
         lcosts += z;
         intra_cost += z;
+        mvs += z;
+        fenc += z;
         if( invq )
             invq += z;
         if( row_satd )
