@@ -1,4 +1,4 @@
-# PMC passes over a tool script (first argument, e.g. tools/hpel_variants.py): SQ issue/stall,
+# PMC passes over a tool script (first argument, e.g. tools/tesa_time.py): SQ issue/stall,
 # cache and address path, HBM; one counter group per rocprofv3 run
 set -o pipefail
 R=$GRAFT_REPO_ROOT
