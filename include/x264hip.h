@@ -845,7 +845,8 @@ int x264hip_##BD##_subpel_qpel9_batch( int op, int i_pixel, const pixel *fenc,  
  * (h->mb.mv_min_spel / mv_max_spel) }; init_cost[i] = m->cost; cost_mv at mvd 0.                \
  * out[4*i] = { m->cost, m->mv[0], m->mv[1], m->cost_mv } (16-byte aligned); nevals (or NULL):  \
  * the reference's cmp calls per partition: luma SADs | luma SATDs << 16 | chroma mbcmp calls     \
- * << 24.  No multi-reference threshold (p_halfpel_thresh = NULL).  This form is luma-only with  \
+ * << 24.  No multi-reference threshold (p_halfpel_thresh = NULL; see _me_search_ref_thresh /    \
+ * _me_refine_qpel_refdupe).  This form is luma-only with                                        \
  * unweighted references; _ex takes x264hip_refine_ext_t (NULL = the same as this form): every  \
  * luma get_ref weighted by weight[0] (mc.c:221-249), and with b_chroma_me COST_MV_SATD's       \
  * chroma cost (mc_chroma + mbcmp[chromapix] of U then V, or get_ref + mbcmp_unaligned of the    \
@@ -870,6 +871,22 @@ int x264hip_##BD##_me_refine_subpel_ex( const pixel *fenc, intptr_t fenc_stride,
                                         const uint16_t *cost_mv, int n, int32_t *out,           \
                                         int32_t *nevals, const x264hip_refine_ext_t *ext,       \
                                         void *stream );                                         \
+/* x264_me_refine_qpel_refdupe (reference encoder/me.c:812-815): refine_subpel with no halfpel   \
+ * iterations and min(2, subpel_iterations[subme][3]) quarterpel ones, the search analyse.c:1279- \
+ * 1283 runs instead of x264_me_search_ref on a reference that duplicates reference 0 (par's mv  \
+ * = reference 0's result, a->l0.mvc[0][0]; init_cost = m->cost as the caller's x264_me_t holds   \
+ * it).  Arguments as me_refine_subpel_ex; halfpel_thresh / ref_cost as me_search_ref_thresh. */  \
+int x264hip_##BD##_me_refine_qpel_refdupe( const pixel *fenc, intptr_t fenc_stride,             \
+                                           intptr_t fenc_frame_stride, const pixel *fpel,       \
+                                           const pixel *hpel_h, const pixel *hpel_v,            \
+                                           const pixel *hpel_c, intptr_t ref_stride,            \
+                                           intptr_t ref_frame_stride, int i_pixel, int subme,   \
+                                           int fpel_satd, const int32_t *pos,                   \
+                                           const int16_t *par, const int32_t *init_cost,        \
+                                           const uint16_t *cost_mv, int n, int32_t *out,        \
+                                           int32_t *nevals, int32_t *halfpel_thresh,            \
+                                           const int32_t *ref_cost,                             \
+                                           const x264hip_refine_ext_t *ext, void *stream );     \
                                                                                                 \
 /* x264_me_search_ref (reference encoder/me.c:182-798) for n partitions of size i_pixel (16x16 ..  \
  * 8x8) with me_method X264_ME_DIA (0), X264_ME_HEX (1, x264's default, common/base.c:439) or      \
@@ -883,7 +900,7 @@ int x264hip_##BD##_me_refine_subpel_ex( const pixel *fenc, intptr_t fenc_stride,
  * mvc[28*i + 2*k] = candidate k (qpel, k < i_mvc <= 14).  out[4*i] = { m->cost, m->mv[0],         \
  * m->mv[1], m->cost_mv } (16-byte aligned); nevals (or NULL) = int32 [n][2]: the integer stage's  \
  * fpelcmp calls | get_ref calls << 16, then the refine's counts (me_refine_subpel's format).      \
- * p_halfpel_thresh = NULL (the multi-reference early exit is sequential across references).     \
+ * p_halfpel_thresh = NULL here; me_search_ref_thresh below takes it.                           \
  * me_range 4 .. 64. */                                                                          \
 int x264hip_##BD##_me_search_ref( const pixel *fenc, intptr_t fenc_stride,                      \
                                   intptr_t fenc_frame_stride, const pixel *fpel_w,              \
@@ -895,6 +912,27 @@ int x264hip_##BD##_me_search_ref( const pixel *fenc, intptr_t fenc_stride,      
                                   const uint16_t *cost_mv, int n, int32_t *out,                 \
                                   int32_t *nevals, const x264hip_refine_ext_t *ext,             \
                                   void *stream );                                               \
+/* me_search_ref with the multi-reference early exit, x264_me_search_ref( ..., p_halfpel_thresh ) \
+ * (reference me.c:931-944 inside refine_subpel; x264's default ref = 3 with b_early_terminate,  \
+ * common/base.c:384, encoder/analyse.c:303, 1260-1261): halfpel_thresh = int32 [n], partition i's \
+ * i_halfpel_thresh (INT_MAX before its MB's first reference), read and written in place;        \
+ * ref_cost = int32 [n] (or NULL = 0), the partition's i_ref_cost for this reference -- the      \
+ * threshold is held less it during the search, as analyse.c:1271 / 1310 do around the call.     \
+ * The caller chains one MB's references as one launch per reference.  When the exit fires the  \
+ * refine returns before its quarterpel diamond with m->cost, m->mv written and m->cost_mv left   \
+ * as it was: out[4*i+3] keeps what the caller stored there.  halfpel_thresh = NULL is            \
+ * me_search_ref.  Only subme >= 2 runs the refine (and so reads the threshold), as me.c:792. */  \
+int x264hip_##BD##_me_search_ref_thresh( const pixel *fenc, intptr_t fenc_stride,               \
+                                         intptr_t fenc_frame_stride, const pixel *fpel_w,       \
+                                         const pixel *fpel, const pixel *hpel_h,                \
+                                         const pixel *hpel_v, const pixel *hpel_c,              \
+                                         intptr_t ref_stride, intptr_t ref_frame_stride,        \
+                                         int i_pixel, int me_method, int subme, int me_range,   \
+                                         const int32_t *pos, const int16_t *par,                \
+                                         const int16_t *mvc, const uint16_t *cost_mv, int n,    \
+                                         int32_t *out, int32_t *nevals,                         \
+                                         int32_t *halfpel_thresh, const int32_t *ref_cost,      \
+                                         const x264hip_refine_ext_t *ext, void *stream );       \
                                                                                                 \
 /* block lists of the reference transforms (dct.c), device arrays;                             \
  * dct holds n consecutive outputs of the selected entry's size. */                             \

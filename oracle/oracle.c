@@ -1689,7 +1689,8 @@ void FN(me_esa_argmin)( const sadt *table, int R, int nmb, int me_range, const i
 }
 
 /* refine_subpel (reference encoder/me.c:865-992) for a list of partitions, semantics of
- * x264hip_*_me_refine_subpel_ex: p_halfpel_thresh = NULL.  Iterations from subpel_iterations
+ * x264hip_*_me_refine_subpel_ex (p_halfpel_thresh = NULL; refine_core below takes it, for
+ * me_refine_qpel_refdupe and me_search_ref_thresh).  Iterations from subpel_iterations
  * (me.c:38-50): refine_qpel = 0 is the call of x264_me_search_ref (me.c:791-797, entries
  * 2-3), 1 the one of x264_me_refine_qpel (me.c:801-810, entries 0-1).  fpelcmp = satd iff
  * fpel_satd (TESA) and subme > 1, mbcmp / mbcmp_unaligned = satd iff subme > 1
@@ -1760,15 +1761,22 @@ static int FN(rs_chroma)( FN(rs_chroma_t) *c, int mx, int my, int cost, int bcos
     return cost;
 }
 
-void FN(me_refine_subpel_ex)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs,
-                              int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
-                              const int16_t *par, const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out,
-                              int32_t *nevals, const int32_t *ext, const pixel *const fenc_c[2], intptr_t fcs,
-                              const pixel *const ref_c[8], intptr_t rcs )
+/* kind 0: x264_me_search_ref's refine (me.c:794-796), 1: x264_me_refine_qpel (:801-810), 2:
+ * x264_me_refine_qpel_refdupe (:812-815).  thr (or NULL): per partition *p_halfpel_thresh,
+ * read and written (me.c:931-944); rcost (or NULL = 0): the i_ref_cost analyse.c:1271 / 1310
+ * subtract from it before the call and add back after.  On the early exit out[4*i+3]
+ * (m->cost_mv) is left as it was. */
+static void FN(refine_core)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs,
+                             int i_pixel, int subme, int kind, int fpel_satd, const int32_t *pos,
+                             const int16_t *par, const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out,
+                             int32_t *nevals, const int32_t *ext, const pixel *const fenc_c[2], intptr_t fcs,
+                             const pixel *const ref_c[8], intptr_t rcs, int32_t *thr, const int32_t *rcost )
 {
     const int bw = pixel_w[i_pixel], bh = pixel_h[i_pixel];
-    const int hpel_iters = subpel_iterations[subme][refine_qpel ? 0 : 2];
-    const int qpel_iters = subpel_iterations[subme][refine_qpel ? 1 : 3];
+    const int refine_qpel = kind == 1;
+    const int hpel_iters = kind == 2 ? 0 : subpel_iterations[subme][refine_qpel ? 0 : 2];
+    const int qpel_iters = kind == 2 ? (subpel_iterations[subme][3] < 2 ? subpel_iterations[subme][3] : 2)
+                                     : subpel_iterations[subme][refine_qpel ? 1 : 3];
     const int fsatd = fpel_satd && subme > 1, qsatd = subme > 1;
     /* me.c:872: every partition here is <= PIXEL_8x8 */
     const int b_chroma_me = ext && ext[0];
@@ -1863,6 +1871,25 @@ void FN(me_refine_subpel_ex)( const pixel *fenc, intptr_t fs, const pixel *const
             bcost = 1 << 28;
             bcost = RS_SATD( bmx, bmy );
         }
+        if( thr )
+        {
+            /* early termination when examining multiple reference frames (me.c:931-944) */
+            const int rc = rcost ? rcost[i] : 0;
+            int t = thr[i] - rc;
+            const int early = (bcost * 7) >> 3 > t;
+            if( !early && bcost < t )
+                t = bcost;
+            thr[i] = t + rc;
+            if( early )
+            {
+                out[4*i] = bcost;
+                out[4*i+1] = bmx;
+                out[4*i+2] = bmy;
+                if( nevals )
+                    nevals[i] = nsad | (nsatd << 16) | (cc.nchroma << 24);
+                continue;
+            }
+        }
         if( subme != 1 )
         {
             bdir = -1;
@@ -1912,6 +1939,27 @@ void FN(me_refine_subpel_ex)( const pixel *fenc, intptr_t fs, const pixel *const
     }
 }
 
+void FN(me_refine_subpel_ex)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs,
+                              int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
+                              const int16_t *par, const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out,
+                              int32_t *nevals, const int32_t *ext, const pixel *const fenc_c[2], intptr_t fcs,
+                              const pixel *const ref_c[8], intptr_t rcs )
+{
+    FN(refine_core)( fenc, fs, planes, rs, i_pixel, subme, !!refine_qpel, fpel_satd, pos, par, cost, cost_mv, n, out,
+                     nevals, ext, fenc_c, fcs, ref_c, rcs, NULL, NULL );
+}
+
+/* x264_me_refine_qpel_refdupe (me.c:812-815) with p_halfpel_thresh (thr, rcost as refine_core) */
+void FN(me_refine_qpel_refdupe)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs,
+                                 int i_pixel, int subme, int fpel_satd, const int32_t *pos, const int16_t *par,
+                                 const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out, int32_t *nevals,
+                                 const int32_t *ext, const pixel *const fenc_c[2], intptr_t fcs,
+                                 const pixel *const ref_c[8], intptr_t rcs, int32_t *thr, const int32_t *rcost )
+{
+    FN(refine_core)( fenc, fs, planes, rs, i_pixel, subme, 2, fpel_satd, pos, par, cost, cost_mv, n, out, nevals, ext,
+                     fenc_c, fcs, ref_c, rcs, thr, rcost );
+}
+
 void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], intptr_t rs, int i_pixel,
                            int subme, int refine_qpel, int fpel_satd, const int32_t *pos, const int16_t *par,
                            const int32_t *cost, const uint16_t *cost_mv, int n, int32_t *out, int32_t *nevals )
@@ -1921,7 +1969,8 @@ void FN(me_refine_subpel)( const pixel *fenc, intptr_t fs, const pixel *const pl
 }
 
 /* x264_me_search_ref (reference encoder/me.c:182-798) for a list of partitions of one frame
- * with me = DIA (0), HEX (1) or UMH (2) and p_halfpel_thresh = NULL: the predictor checks
+ * with me = DIA (0), HEX (1) or UMH (2) (me_search_ref_thresh: with p_halfpel_thresh as
+ * refine_core reads it; me_search_ref: NULL): the predictor checks
  * (:214-318, x264_predictor_clip / _roundclip common/common.h:774-805), the integer search
  * (:320-616; UMH's adaptive range with x264_predictor_difference, common/base.h:248-257), the
  * qpel conversion (:774-789), then refine_subpel as FN(me_refine_subpel_ex) runs it when
@@ -1963,11 +2012,12 @@ static int FN(sr_hpel)( FN(sr_t) *c, int mx, int my )           /* COST_MV_HPEL'
     return FN(sad)( c->i_pixel, c->fenc, c->fs, r, ts );
 }
 
-void FN(me_search_ref)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], const pixel *fw, intptr_t rs,
-                        int i_pixel, int me_method, int subme, int me_range, const int32_t *pos, const int16_t *par,
-                        const int16_t *mvc_all, const uint16_t *cost_mv, int n, int32_t *out, int32_t *nevals,
-                        const int32_t *ext, const pixel *const fenc_c[2], intptr_t fcs, const pixel *const ref_c[8],
-                        intptr_t rcs )
+void FN(me_search_ref_thresh)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], const pixel *fw,
+                               intptr_t rs, int i_pixel, int me_method, int subme, int me_range, const int32_t *pos,
+                               const int16_t *par, const int16_t *mvc_all, const uint16_t *cost_mv, int n,
+                               int32_t *out, int32_t *nevals, const int32_t *ext, const pixel *const fenc_c[2],
+                               intptr_t fcs, const pixel *const ref_c[8], intptr_t rcs, int32_t *thr,
+                               const int32_t *rcost )
 {
     static const uint8_t mod6m1[8] = { 5,0,1,2,3,4,5,0 };                                                /* me.c:53 */
     static const int8_t hex2[8][2] = { {-1,-2}, {-2,0}, {-1,2}, {1,2}, {2,0}, {1,-2}, {-1,-2}, {-2,0} }; /* me.c:55 */
@@ -2290,10 +2340,6 @@ void FN(me_search_ref)( const pixel *fenc, intptr_t fs, const pixel *const plane
             cmv = p_cost_mvx[mx] + p_cost_mvy[my];    /* (refine_subpel sets m->cost_mv) */
         }
 #undef SR_BITS
-        out[4*j] = cst;
-        out[4*j+1] = mx;
-        out[4*j+2] = my;
-        out[4*j+3] = cmv;
         if( nevals )
         {
             nevals[2*j] = c.nf | (c.nh << 16);
@@ -2303,10 +2349,28 @@ void FN(me_search_ref)( const pixel *fenc, intptr_t fs, const pixel *const plane
         {
             const int16_t rp[8] = { (int16_t)mx, (int16_t)my, (int16_t)mvp[0], (int16_t)mvp[1], p[6], p[7], p[8], p[9] };
             const int32_t rpos[2] = { bx, by };
-            FN(me_refine_subpel_ex)( fenc, fs, planes, rs, i_pixel, subme, 0, 0, rpos, rp, &cst, cost_mv, 1,
-                                     out + 4 * j, nevals ? nevals + 2 * j + 1 : NULL, ext, fenc_c, fcs, ref_c, rcs );
+            FN(refine_core)( fenc, fs, planes, rs, i_pixel, subme, 0, 0, rpos, rp, &cst, cost_mv, 1, out + 4 * j,
+                             nevals ? nevals + 2 * j + 1 : NULL, ext, fenc_c, fcs, ref_c, rcs, thr ? thr + j : NULL,
+                             rcost ? rcost + j : NULL );
+        }
+        else
+        {
+            out[4*j] = cst;
+            out[4*j+1] = mx;
+            out[4*j+2] = my;
+            out[4*j+3] = cmv;
         }
     }
+}
+
+void FN(me_search_ref)( const pixel *fenc, intptr_t fs, const pixel *const planes[4], const pixel *fw, intptr_t rs,
+                        int i_pixel, int me_method, int subme, int me_range, const int32_t *pos, const int16_t *par,
+                        const int16_t *mvc_all, const uint16_t *cost_mv, int n, int32_t *out, int32_t *nevals,
+                        const int32_t *ext, const pixel *const fenc_c[2], intptr_t fcs, const pixel *const ref_c[8],
+                        intptr_t rcs )
+{
+    FN(me_search_ref_thresh)( fenc, fs, planes, fw, rs, i_pixel, me_method, subme, me_range, pos, par, mvc_all, cost_mv,
+                              n, out, nevals, ext, fenc_c, fcs, ref_c, rcs, NULL, NULL );
 }
 
 /* TESA integer-pel search of x264_me_search_ref for PIXEL_16x16, restated from

@@ -78,6 +78,10 @@ for _bd in (8, 10):
                               _P, _P, _P, _IP, _P, _IP])
     _f(_bd, "me_refine_subpel_ex", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int,
                                     _P, _P, _P, _P, _IP, _P, _IP])
+    _f(_bd, "me_search_ref_thresh", [_P, _IP, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P,
+                                     C.c_int, _P, _P, _P, _P, _IP, _P, _IP, _P, _P])
+    _f(_bd, "me_refine_qpel_refdupe", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P, _P,
+                                       _P, _P, _IP, _P, _IP, _P, _P])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
     _f(_bd, "subpel_list", [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P])
     _f(_bd, "sa8d", [C.c_int, _P, _IP, _P, _IP], C.c_int)
@@ -382,25 +386,59 @@ def me_refine_subpel(bd, fenc, f_origin, fs, planes, r_origin, rs, i_pixel, subm
 
 
 def me_search_ref(bd, fenc, f_origin, fs, planes, fw, r_origin, rs, i_pixel, me_method, subme, me_range, pos_xy,
-                  par, mvc, cost_mv, c0, ext=None, fenc_c=None, fc_origin=0, fcs=0, ref_c=None, rc_origin=0, rcs=0):
+                  par, mvc, cost_mv, c0, ext=None, fenc_c=None, fc_origin=0, fcs=0, ref_c=None, rc_origin=0, rcs=0,
+                  thresh=None, ref_cost=None, out_fill=0):
     """one frame: x264_me_search_ref (me.c:182-798) of the partitions at pos_xy int32 [n, 2] with
     me_method 0 DIA / 1 HEX / 2 UMH; par int16 [n, 12], mvc int16 [n, 14, 2] (search_cases.jobs);
     planes = F, H, V, C, fw = the weighted F plane (or F).  Returns int32 [n, 4] = (cost, mvx, mvy,
-    cost_mv) and the call counts int32 [n, 2] (integer stage fpel | get_ref << 16, the refine's)."""
+    cost_mv) and the call counts int32 [n, 2] (integer stage fpel | get_ref << 16, the refine's).
+    thresh: int32 [n] p_halfpel_thresh per partition, updated in place (me_search_ref_thresh),
+    ref_cost int32 [n] (or None); out starts filled with out_fill (the early exit leaves
+    cost_mv as it was)."""
     n = len(pos_xy)
     pos = np.ascontiguousarray(pos_xy, np.int32)
     p = np.ascontiguousarray(par, np.int16)
     m = np.ascontiguousarray(mvc, np.int16)
-    out = np.zeros((n, 4), np.int32)
+    out = np.full((n, 4), out_fill, np.int32)
     ne = np.zeros((n, 2), np.int32)
     arr = (C.c_void_p * 4)(*[_addr(q, r_origin).value for q in planes])
     fca = (C.c_void_p * 2)(*([_addr(q, fc_origin).value for q in (fenc_c or [])] + [None] * 2)[:2])
     rca = (C.c_void_p * 8)(*([_addr(q, rc_origin).value for q in (ref_c or [])] + [None] * 8)[:8])
     e = None if ext is None else np.ascontiguousarray(ext, np.int32)
-    getattr(_L, f"oracle{bd}_me_search_ref")(_addr(fenc, f_origin), fs, arr, _addr(fw, r_origin), rs, i_pixel,
-                                            me_method, subme, me_range, _addr(pos), _addr(p), _addr(m),
-                                            _addr(cost_mv, c0), n, _addr(out), _addr(ne),
-                                            None if e is None else _addr(e), fca, fcs, rca, rcs)
+    args = [_addr(fenc, f_origin), fs, arr, _addr(fw, r_origin), rs, i_pixel, me_method, subme, me_range, _addr(pos),
+            _addr(p), _addr(m), _addr(cost_mv, c0), n, _addr(out), _addr(ne), None if e is None else _addr(e), fca, fcs,
+            rca, rcs]
+    if thresh is None:
+        getattr(_L, f"oracle{bd}_me_search_ref")(*args)
+    else:
+        assert thresh.dtype == np.int32 and thresh.flags.c_contiguous and len(thresh) == n
+        rcst = None if ref_cost is None else np.ascontiguousarray(ref_cost, np.int32)
+        getattr(_L, f"oracle{bd}_me_search_ref_thresh")(*args, _addr(thresh), None if rcst is None else _addr(rcst))
+    return out, ne
+
+
+def me_refine_qpel_refdupe(bd, fenc, f_origin, fs, planes, r_origin, rs, i_pixel, subme, pos_xy, par, cost, cost_mv,
+                           c0, thresh=None, ref_cost=None, out_fill=0, fpel_satd=False, ext=None, fenc_c=None,
+                           fc_origin=0, fcs=0, ref_c=None, rc_origin=0, rcs=0):
+    """one frame: x264_me_refine_qpel_refdupe (me.c:812-815) of the partitions at pos_xy; par /
+    cost as me_refine_subpel, thresh / ref_cost / out_fill as me_search_ref.  Returns (out, counts)."""
+    n = len(pos_xy)
+    pos = np.ascontiguousarray(pos_xy, np.int32)
+    p = np.ascontiguousarray(par, np.int16)
+    c = np.ascontiguousarray(cost, np.int32)
+    out = np.full((n, 4), out_fill, np.int32)
+    ne = np.zeros(n, np.int32)
+    arr = (C.c_void_p * 4)(*[_addr(q, r_origin).value for q in planes])
+    fca = (C.c_void_p * 2)(*([_addr(q, fc_origin).value for q in (fenc_c or [])] + [None] * 2)[:2])
+    rca = (C.c_void_p * 8)(*([_addr(q, rc_origin).value for q in (ref_c or [])] + [None] * 8)[:8])
+    e = None if ext is None else np.ascontiguousarray(ext, np.int32)
+    if thresh is not None:
+        assert thresh.dtype == np.int32 and thresh.flags.c_contiguous and len(thresh) == n
+    rcst = None if ref_cost is None else np.ascontiguousarray(ref_cost, np.int32)
+    getattr(_L, f"oracle{bd}_me_refine_qpel_refdupe")(
+        _addr(fenc, f_origin), fs, arr, rs, i_pixel, subme, int(bool(fpel_satd)), _addr(pos), _addr(p), _addr(c),
+        _addr(cost_mv, c0), n, _addr(out), _addr(ne), None if e is None else _addr(e), fca, fcs, rca, rcs,
+        None if thresh is None else _addr(thresh), None if rcst is None else _addr(rcst))
     return out, ne
 
 

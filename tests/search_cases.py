@@ -298,3 +298,38 @@ def search_ref_py(fenc, planes, fw, origin, stride, x, y, i_pixel, par, mvc, cm,
     else:
         mx, my = 4 * bmx, 4 * bmy
     return (min(bpred_cost, bcost), mx, my, cmx(mx) + cmy(my)), tuple(nf)
+
+
+class MultiRef:
+    """one current frame and nref references of it (x264's default ref = 3, common/base.c:384):
+    weightp_cases.make_pair with one seed gives every pair the same texture as its `ref` frame,
+    so that frame is the current one and each pair's shifted, noised `fenc` frame is a reference
+    -- reference k shows the current frame moved by -shifts[k] with noise noises[k] (a noisier
+    reference loses to a cleaner one: the content the early exit exists for).  refs[k] carries
+    ChromaCase's fields (luma F, H, V, C; ref_c), the current frame fenc_y / fenc_c."""
+
+    def __init__(self, bd, W, H, cf, seed, shifts=((3, 2), (-2, 1), (1, -3)), noises=(1, 8, 2)):
+        import numpy_ref as nr
+        import weightp_cases as wc
+        self.bd, self.W, self.H, self.cf, self.shifts = bd, W, H, cf, shifts
+        pairs = [wc.make_pair(bd, W, H, cf, seed=seed, shift=s, noise=z) for s, z in zip(shifts, noises)]
+        cur = pairs[0][0]
+        self.stride, self.origin, self.cs, self.co = cur.ys, cur.yo, cur.cs, cur.co
+        self.fenc_y = cur.y.ravel()
+        self.fenc_c = [cur.nv.ravel()] if cf in (1, 2) else [cur.u.ravel(), cur.v.ravel()]
+        self.refs = []
+        for _, r in pairs:
+            o = type("Ref", (), {})()
+            o.luma = [r.y.ravel()] + [h.ravel() for h in nr.hpel_planes(r.y, 32, W, H, bd)]
+            if cf in (1, 2):
+                o.ref_c = [r.nv.ravel()]
+            else:
+                o.ref_c = []
+                for p in (r.u, r.v):
+                    o.ref_c += [p.ravel()] + [h.ravel() for h in nr.hpel_planes(p, 32, W, H, bd)]
+            self.refs.append(o)
+
+    def jobs(self, k, i_pixel, seed):
+        """search_cases.jobs around reference k's true motion (-4 * shift qpel)"""
+        sx, sy = self.shifts[k]
+        return jobs(self.W // 16, self.H // 16, 1, i_pixel, seed=seed, motion=(-4 * sx, -4 * sy))

@@ -36,9 +36,13 @@ def _mc_chroma(nv, off, stride, mvx, mvy, w, h):
     return out
 
 
-def refine_chroma_py(cc, x, y, i_pixel, par, cost, cm, c0, subme, refine_qpel, b_chroma_me, weights, mvy_offset=0):
+def refine_chroma_py(cc, x, y, i_pixel, par, cost, cm, c0, subme, refine_qpel, b_chroma_me, weights, mvy_offset=0,
+                     refdupe=False, thresh=None, ref_cost=0):
     """refine_subpel (me.c:865-992) with COST_MV_SATD's chroma branch; returns (cost, mvx, mvy,
-    cost_mv) and the call counts (sad, satd, chroma)"""
+    cost_mv) and the call counts (sad, satd, chroma).  refdupe: x264_me_refine_qpel_refdupe's
+    iterations (me.c:812-815); thresh: a one-element list holding *p_halfpel_thresh (me.c:931-944),
+    updated, with ref_cost subtracted around the call as analyse.c:1271 / 1310 do -- on the early
+    exit cost_mv is None (m->cost_mv untouched)"""
     bd, cf = cc.bd, cc.cf
     bw, bh = nr.SIZES[i_pixel]
     qsatd = subme > 1
@@ -85,8 +89,8 @@ def refine_chroma_py(cc, x, y, i_pixel, par, cost, cm, c0, subme, refine_qpel, b
         return c
 
     mn, mx_ = (int(par[4]), int(par[5])), (int(par[6]), int(par[7]))
-    hpel = SUBPEL_ITERATIONS[subme][0 if refine_qpel else 2]
-    qpel = SUBPEL_ITERATIONS[subme][1 if refine_qpel else 3]
+    hpel = 0 if refdupe else SUBPEL_ITERATIONS[subme][0 if refine_qpel else 2]
+    qpel = min(2, SUBPEL_ITERATIONS[subme][3]) if refdupe else SUBPEL_ITERATIONS[subme][1 if refine_qpel else 3]
     bmx, bmy, bcost = int(par[0]), int(par[1]), int(cost)
     if hpel:
         if subme < 3:                                       # the predictor's subpel component (me.c:889-895)
@@ -111,6 +115,14 @@ def refine_chroma_py(cc, x, y, i_pixel, par, cost, cm, c0, subme, refine_qpel, b
         bcost >>= 6
     if not refine_qpel and (qsatd or b_chroma_me):
         bcost = satd_cost(bmx, bmy, 1 << 28)
+    if thresh is not None:
+        t = thresh[0] - ref_cost
+        early = (bcost * 7) >> 3 > t
+        if not early and bcost < t:
+            t = bcost
+        thresh[0] = t + ref_cost
+        if early:
+            return (bcost, bmx, bmy, None), n[0] | (n[1] << 16) | (n[2] << 24)
     bdir = -1
     for _ in range(qpel):
         if bmy <= mn[1] or bmy >= mx_[1] or bmx <= mn[0] or bmx >= mx_[0]:

@@ -94,3 +94,156 @@ def test_search_2160p(hip, oracle, bd, me_method):
     UMH at 10 bit, subme 7 with chroma ME"""
     got, par, ne = _run(hip, oracle, bd, 1, 3840, 2160, 1, 0, me_method, 7, 16, 0, 1, seed=71 + bd)
     assert (got[:, 1:3] != 0).any(1).mean() > 0.5
+
+
+INT_MAX = (1 << 31) - 1
+
+
+def _chain(hip, oracle, bd, W, H, i_pixel, me_method, subme, seed, nref=3):
+    """x264's default ref = 3 loop (analyse.c:1260-1314): one launch per reference with the
+    partition's p_halfpel_thresh chained through them and the i_ref_cost adjustments, the HIP
+    threshold / outputs / call counts against the oracle's after every reference; returns how
+    many partitions took the early exit"""
+    cf = 1
+    mr = sc.MultiRef(bd, W, H, cf, seed=seed)
+    rows = mr.fenc_y.size // mr.stride
+    crows = mr.fenc_c[0].size // mr.cs
+    fenc = _t(mr.fenc_y.reshape(1, rows, -1), bd)
+    fenc_c = [_t(mr.fenc_c[0].reshape(1, crows, -1), bd)]
+    cm, c0 = rc.cost_mv()
+    cmd = torch.from_numpy(cm.view(np.int16)).cuda()
+    oext = oracle.refine_ext(1, cf, 0, (None, None, None))
+    n = len(mr.jobs(0, i_pixel, 0)[0])
+    thr = np.full(n, INT_MAX, np.int32)
+    thr_d = torch.from_numpy(thr.copy()).cuda()
+    early = 0
+    for k in range(nref):
+        r = mr.refs[k]
+        luma = [_t(p.reshape(1, rows, -1), bd) for p in r.luma]
+        ref_c = [_t(r.ref_c[0].reshape(1, crows, -1), bd)]
+        ext = hip.refine_ext(1, cf, 0, (None, None, None), fenc_chroma=fenc_c, fenc_chroma_origin=mr.co,
+                             fenc_chroma_stride=mr.cs, ref_chroma=ref_c, ref_chroma_origin=mr.co,
+                             ref_chroma_stride=mr.cs)
+        pos, par, mvc = mr.jobs(k, i_pixel, seed=seed + 17 * k)
+        rcost = np.full(n, 40 if k == 0 else 120, np.int32)
+        out = torch.full((n, 4), -7, dtype=torch.int32, device="cuda")
+        ne = torch.full((n, 2), -1, dtype=torch.int32, device="cuda")
+        hip.me_search_ref(fenc, mr.origin, mr.stride, luma[0], luma, mr.origin, mr.stride, i_pixel, me_method, subme,
+                          16, torch.from_numpy(pos).cuda(), torch.from_numpy(par).cuda(), torch.from_numpy(mvc).cuda(),
+                          (cmd, c0), out=out, nevals=ne, ext=ext, halfpel_thresh=thr_d,
+                          ref_cost=torch.from_numpy(rcost).cuda())
+        want, wne = oracle.me_search_ref(bd, mr.fenc_y, mr.origin, mr.stride, r.luma, r.luma[0], mr.origin, mr.stride,
+                                         i_pixel, me_method, subme, 16, pos[:, 1:], par, mvc, cm, c0, ext=oext,
+                                         fenc_c=mr.fenc_c, fc_origin=mr.co, fcs=mr.cs, ref_c=r.ref_c, rc_origin=mr.co,
+                                         rcs=mr.cs, thresh=thr, ref_cost=rcost, out_fill=-7)
+        got = out.cpu().numpy()
+        bad = np.argwhere((got != want).any(1)).ravel()
+        assert not len(bad), (k, bad[:4], got[bad[:4]], want[bad[:4]])
+        ne = ne.cpu().numpy()
+        badn = np.argwhere((ne != wne).any(1)).ravel()
+        assert not len(badn), (k, badn[:4], ne[badn[:4]], wne[badn[:4]])
+        assert np.array_equal(thr_d.cpu().numpy(), thr), k
+        early += int((want[:, 3] == -7).sum())
+    return early, n
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("me_method", [1, 2])
+@pytest.mark.parametrize("i_pixel", [0, 3])
+def test_search_thresh_chain_small(hip, oracle, bd, me_method, i_pixel):
+    early, n = _chain(hip, oracle, bd, 96, 64, i_pixel, me_method, 7, seed=5 + bd + me_method)
+    assert early > 0
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("me_method", [1, 2])
+def test_search_thresh_chain_1080p(hip, oracle, bd, me_method):
+    """x264's default P16x16 path (ref 3, b_early_terminate, HEX or UMH, subme 7, chroma ME) over
+    a whole 1920x1088 frame"""
+    early, n = _chain(hip, oracle, bd, 1920, 1088, 0, me_method, 7, seed=31 + bd)
+    assert 0 < early < 2 * n
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("subme", [2, 5, 7, 9])
+def test_refdupe(hip, oracle, bd, subme):
+    """x264_me_refine_qpel_refdupe (me.c:812-815) on a reference duplicating reference 0
+    (analyse.c:1279-1283), after reference 0's search with the threshold"""
+    W, H, cf, i_pixel = 96, 64, 1, 0
+    mr = sc.MultiRef(bd, W, H, cf, seed=9 + bd)
+    rows, crows = mr.fenc_y.size // mr.stride, mr.fenc_c[0].size // mr.cs
+    r = mr.refs[0]
+    fenc = _t(mr.fenc_y.reshape(1, rows, -1), bd)
+    luma = [_t(p.reshape(1, rows, -1), bd) for p in r.luma]
+    chroma = int(subme >= 5)
+    ext = hip.refine_ext(chroma, cf, 0, (None, None, None), fenc_chroma=[_t(mr.fenc_c[0].reshape(1, crows, -1), bd)],
+                         fenc_chroma_origin=mr.co, fenc_chroma_stride=mr.cs,
+                         ref_chroma=[_t(r.ref_c[0].reshape(1, crows, -1), bd)], ref_chroma_origin=mr.co,
+                         ref_chroma_stride=mr.cs)
+    oext = oracle.refine_ext(chroma, cf, 0, (None, None, None))
+    cm, c0 = rc.cost_mv()
+    cmd = torch.from_numpy(cm.view(np.int16)).cuda()
+    pos, par, mvc = mr.jobs(0, i_pixel, seed=subme)
+    n = len(pos)
+    thr = np.full(n, INT_MAX, np.int32)
+    rc0 = np.full(n, 40, np.int32)
+    out0, _ = oracle.me_search_ref(bd, mr.fenc_y, mr.origin, mr.stride, r.luma, r.luma[0], mr.origin, mr.stride,
+                                   i_pixel, 1, subme, 16, pos[:, 1:], par, mvc, cm, c0, ext=oext, fenc_c=mr.fenc_c,
+                                   fc_origin=mr.co, fcs=mr.cs, ref_c=r.ref_c, rc_origin=mr.co, rcs=mr.cs, thresh=thr,
+                                   ref_cost=rc0)
+    rpar = np.stack([out0[:, 1], out0[:, 2], par[:, 0] + 4, par[:, 1] - 4, par[:, 6], par[:, 7], par[:, 8], par[:, 9]],
+                    1).astype(np.int16)
+    init = (out0[:, 0] + rc0).astype(np.int32)
+    rc1 = np.full(n, 120, np.int32)
+    thr_d = torch.from_numpy(thr.copy()).cuda()
+    out = torch.full((n, 4), -7, dtype=torch.int32, device="cuda")
+    ne = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    hip.me_refine_qpel_refdupe(fenc, mr.origin, mr.stride, luma, mr.origin, mr.stride, i_pixel, subme,
+                               torch.from_numpy(pos).cuda(), torch.from_numpy(rpar).cuda(),
+                               torch.from_numpy(init).cuda(), (cmd, c0), halfpel_thresh=thr_d,
+                               ref_cost=torch.from_numpy(rc1).cuda(), out=out, nevals=ne, ext=ext)
+    want, wne = oracle.me_refine_qpel_refdupe(bd, mr.fenc_y, mr.origin, mr.stride, r.luma, mr.origin, mr.stride,
+                                              i_pixel, subme, pos[:, 1:], rpar, init, cm, c0, thresh=thr,
+                                              ref_cost=rc1, out_fill=-7, ext=oext, fenc_c=mr.fenc_c, fc_origin=mr.co,
+                                              fcs=mr.cs, ref_c=r.ref_c, rc_origin=mr.co, rcs=mr.cs)
+    assert np.array_equal(out.cpu().numpy(), want)
+    assert np.array_equal(ne.cpu().numpy(), wne)
+    assert np.array_equal(thr_d.cpu().numpy(), thr)
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+@pytest.mark.parametrize("i_pixel", [0, 3])
+@pytest.mark.parametrize("subme", [1, 7])
+def test_search_umh_cross_past_limit(hip, oracle, bd, i_pixel, subme):
+    """UMH's CROSS range-checks only the axis it moves along (me.c:152-176): with mv_limit_fpel's
+    max one pixel short of the true motion (3, 2) the predictors clip to the limit, DIA1_ITER
+    scores the true match one step past it unchecked (me.c:146-150), and the crosses around that
+    winner run at an out-of-range omx / omy -- the reference scores those points"""
+    W, H, cf = 96, 64, 1
+    cc = rc.ChromaCase(bd, W, H, cf, seed=13 + bd)
+    pos, par, mvc = sc.jobs(W // 16, H // 16, 1, i_pixel, seed=3 + subme)
+    par[:, 4] = np.minimum(par[:, 4], 2)                     # fpel x max: true 3
+    par[:, 5] = np.minimum(par[:, 5], 1)                     # fpel y max: true 2
+    rows, crows = cc.ref.y.shape[0], cc.ref.nv.shape[0]
+    fenc = _t(cc.fenc_y.reshape(1, rows, -1), bd)
+    luma = [_t(p.reshape(1, rows, -1), bd) for p in cc.luma]
+    chroma = int(subme >= 5)
+    ext = hip.refine_ext(chroma, cf, 0, (None, None, None), fenc_chroma=[_t(cc.fenc_c[0].reshape(1, crows, -1), bd)],
+                         fenc_chroma_origin=cc.co, fenc_chroma_stride=cc.cs,
+                         ref_chroma=[_t(cc.ref_c[0].reshape(1, crows, -1), bd)], ref_chroma_origin=cc.co,
+                         ref_chroma_stride=cc.cs)
+    cm, c0 = rc.cost_mv()
+    cmd = torch.from_numpy(cm.view(np.int16)).cuda()
+    ne = torch.full((len(pos), 2), -1, dtype=torch.int32, device="cuda")
+    got = hip.me_search_ref(fenc, cc.origin, cc.stride, luma[0], luma, cc.origin, cc.stride, i_pixel, 2, subme, 16,
+                            torch.from_numpy(pos).cuda(), torch.from_numpy(par).cuda(), torch.from_numpy(mvc).cuda(),
+                            (cmd, c0), nevals=ne, ext=ext).cpu().numpy()
+    want, wne = oracle.me_search_ref(bd, cc.fenc_y, cc.origin, cc.stride, cc.luma, cc.luma[0], cc.origin, cc.stride,
+                                     i_pixel, 2, subme, 16, pos[:, 1:], par, mvc, cm, c0,
+                                     ext=oracle.refine_ext(chroma, cf, 0, (None, None, None)), fenc_c=cc.fenc_c,
+                                     fc_origin=cc.co, fcs=cc.cs, ref_c=cc.ref_c, rc_origin=cc.co, rcs=cc.cs)
+    bad = np.argwhere((got != want).any(1)).ravel()
+    assert not len(bad), (bad[:4], got[bad[:4]], want[bad[:4]])
+    assert np.array_equal(ne.cpu().numpy(), wne)
+    if subme == 1:                                           # integer winners past the limit exist
+        assert ((want[:, 1] == 12) | (want[:, 2] == 8)).any()

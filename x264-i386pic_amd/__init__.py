@@ -1272,14 +1272,17 @@ def me_refine_subpel(fenc, fenc_origin, fenc_stride, planes, ref_origin, ref_str
 
 def me_search_ref(fenc, fenc_origin, fenc_stride, fpel_w, planes, ref_origin, ref_stride, i_pixel, me_method, subme,
                   me_range, pos, par, mvc, cost_mv_center, out=None, fenc_frame_stride=None, ref_frame_stride=None,
-                  nevals=None, ext=None):
+                  nevals=None, ext=None, halfpel_thresh=None, ref_cost=None):
     """x264_me_search_ref (encoder/me.c:182-798) of n partitions (x264hip_*_me_search_ref): me_method
     0 DIA / 1 HEX / 2 UMH; fpel_w = the weighted F plane the integer search reads (m->p_fref_w, or
     planes[0]); planes = [F, H, V, C]; pos int32 [n, 3] = (frame, x, y); par int16 [n, 12] = (mvp
     x, y, mv_limit_fpel min x, y, max x, y, mv_min_spel x, y, mv_max_spel x, y, i_mvc, 0); mvc
     int16 [n, 14, 2]; ext = refine_ext(...) for chroma ME / weights.  Returns int32 [n, 4] =
     (m->cost, m->mv x, y, m->cost_mv); nevals: optional int32 [n, 2] (integer stage fpel | get_ref
-    << 16, refine counts)."""
+    << 16, refine counts).  halfpel_thresh: int32 [n] p_halfpel_thresh per partition, read and
+    written (x264hip_*_me_search_ref_thresh, me.c:931-944), with ref_cost int32 [n] or None (the
+    i_ref_cost analyse.c:1271 / 1310 hold it less during the search); on the early exit
+    out[i, 3] keeps what `out` held."""
     import torch
     bd = _pix_bd(fenc)
     n = pos.shape[0]
@@ -1288,14 +1291,46 @@ def me_search_ref(fenc, fenc_origin, fenc_stride, fpel_w, planes, ref_origin, re
     ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
     rfs = ref_frame_stride if ref_frame_stride is not None else _frame_stride(fpel_w, *planes)
     cm, c0 = cost_mv_center
-    fn = getattr(lib(), f"x264hip_{bd}_me_search_ref")
+    thr = halfpel_thresh is not None
+    name = f"x264hip_{bd}_me_search_ref" + ("_thresh" if thr else "")
+    fn = getattr(lib(), name)
     fn.argtypes = [_P, _IP, _IP, _P, _P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P,
-                   _P, _c.c_int, _P, _P, _P, _P]
+                   _P, _c.c_int, _P, _P] + ([_P, _P] if thr else []) + [_P, _P]
     fn.restype = _c.c_int
+    extra = [_ptr(halfpel_thresh), _ptr(ref_cost) if ref_cost is not None else None] if thr else []
     _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(fpel_w, ref_origin), *[_ptr(p, ref_origin) for p in planes],
            ref_stride, rfs, i_pixel, me_method, subme, me_range, _ptr(pos), _ptr(par), _ptr(mvc), _ptr(cm, c0), n,
-           _ptr(out), _ptr(nevals) if nevals is not None else None, _c.byref(ext) if ext is not None else None,
-           _stream()), "me_search_ref")
+           _ptr(out), _ptr(nevals) if nevals is not None else None, *extra,
+           _c.byref(ext) if ext is not None else None, _stream()), name)
+    return out
+
+
+def me_refine_qpel_refdupe(fenc, fenc_origin, fenc_stride, planes, ref_origin, ref_stride, i_pixel, subme, pos, par,
+                           init_cost, cost_mv_center, halfpel_thresh=None, ref_cost=None, fpel_satd=False, out=None,
+                           fenc_frame_stride=None, ref_frame_stride=None, nevals=None, ext=None):
+    """x264_me_refine_qpel_refdupe (encoder/me.c:812-815) of n partitions
+    (x264hip_*_me_refine_qpel_refdupe): arguments as me_refine_subpel (par's mv = reference 0's
+    result, init_cost = m->cost as the caller holds it), halfpel_thresh / ref_cost as
+    me_search_ref."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = pos.shape[0]
+    if out is None:
+        out = torch.empty((n, 4), dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else _frame_stride(*planes)
+    cm, c0 = cost_mv_center
+    name = f"x264hip_{bd}_me_refine_qpel_refdupe"
+    fn = getattr(lib(), name)
+    fn.argtypes = [_P, _IP, _IP, _P, _P, _P, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P, _c.c_int,
+                   _P, _P, _P, _P, _P, _P]
+    fn.restype = _c.c_int
+    _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, *[_ptr(p, ref_origin) for p in planes], ref_stride, rfs, i_pixel,
+           subme, int(bool(fpel_satd)), _ptr(pos), _ptr(par), _ptr(init_cost), _ptr(cm, c0), n, _ptr(out),
+           _ptr(nevals) if nevals is not None else None,
+           _ptr(halfpel_thresh) if halfpel_thresh is not None else None,
+           _ptr(ref_cost) if ref_cost is not None else None, _c.byref(ext) if ext is not None else None, _stream()),
+        name)
     return out
 
 

@@ -1839,9 +1839,10 @@ extern "C" const char *x264hip_backend_banner( void )
             ( n > 0 && ( !fenc || !p0 || !p1 || !p2 || !p3 || !pos || !par || !init_cost || !cost_mv || !out ) ) )   \
             return X264HIP_EINVAL;                                                                                   \
         const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
-        return map_err( launch_me_refine_subpel<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, refine_qpel,    \
+        return map_err( launch_me_refine_subpel<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, !!refine_qpel,  \
                                                      fpel_satd, pos, par, init_cost, cost_mv, n, out, nevals,       \
-                                                     nullptr, (hipStream_t)stream ), "me_refine_subpel" );           \
+                                                     nullptr, nullptr, nullptr, (hipStream_t)stream ),               \
+                        "me_refine_subpel" );                                                                        \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_me_refine_subpel_ex( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,       \
                                                        const PT<BD>::pixel *p0, const PT<BD>::pixel *p1,             \
@@ -1857,9 +1858,29 @@ extern "C" const char *x264hip_backend_banner( void )
             ( n > 0 && ( !fenc || !p0 || !p1 || !p2 || !p3 || !pos || !par || !init_cost || !cost_mv || !out ) ) )   \
             return X264HIP_EINVAL;                                                                                   \
         const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
-        return map_err( launch_me_refine_subpel<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, refine_qpel,    \
-                                                     fpel_satd, pos, par, init_cost, cost_mv, n, out, nevals, ext,  \
-                                                     (hipStream_t)stream ), "me_refine_subpel_ex" );                 \
+        return map_err( launch_me_refine_subpel<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, !!refine_qpel,  \
+                                                     fpel_satd, pos, par, init_cost, cost_mv, n, out, nevals,       \
+                                                     nullptr, nullptr, ext, (hipStream_t)stream ),                   \
+                        "me_refine_subpel_ex" );                                                                     \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_refine_qpel_refdupe( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,    \
+                                                          const PT<BD>::pixel *p0, const PT<BD>::pixel *p1,          \
+                                                          const PT<BD>::pixel *p2, const PT<BD>::pixel *p3,          \
+                                                          intptr_t rs, intptr_t rfs, int i_pixel, int subme,         \
+                                                          int fpel_satd, const int32_t *pos, const int16_t *par,     \
+                                                          const int32_t *init_cost, const uint16_t *cost_mv, int n,  \
+                                                          int32_t *out, int32_t *nevals, int32_t *halfpel_thresh,    \
+                                                          const int32_t *ref_cost, const x264hip_refine_ext_t *ext,  \
+                                                          void *stream )                                             \
+    {                                                                                                                \
+        if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || n < 0 ||                                        \
+            ( n > 0 && ( !fenc || !p0 || !p1 || !p2 || !p3 || !pos || !par || !init_cost || !cost_mv || !out ) ) )   \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
+        return map_err( launch_me_refine_subpel<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, 2, fpel_satd,   \
+                                                     pos, par, init_cost, cost_mv, n, out, nevals, halfpel_thresh,  \
+                                                     ref_cost, ext, (hipStream_t)stream ),                           \
+                        "me_refine_qpel_refdupe" );                                                                  \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_me_search_ref( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,              \
                                                  const PT<BD>::pixel *fw, const PT<BD>::pixel *p0,                   \
@@ -1875,8 +1896,27 @@ extern "C" const char *x264hip_backend_banner( void )
             return X264HIP_EINVAL;                                                                                   \
         const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
         return map_err( launch_me_search_ref<BD>( fenc, fs, ffs, fw, planes, rs, rfs, i_pixel, me_method, subme,     \
-                                                  me_range, pos, par, mvc, cost_mv, n, out, nevals, ext,             \
-                                                  (hipStream_t)stream ), "me_search_ref" );                          \
+                                                  me_range, pos, par, mvc, cost_mv, n, out, nevals, nullptr,         \
+                                                  nullptr, ext, (hipStream_t)stream ), "me_search_ref" );            \
+    }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_search_ref_thresh( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,       \
+                                                        const PT<BD>::pixel *fw, const PT<BD>::pixel *p0,            \
+                                                        const PT<BD>::pixel *p1, const PT<BD>::pixel *p2,            \
+                                                        const PT<BD>::pixel *p3, intptr_t rs, intptr_t rfs,          \
+                                                        int i_pixel, int me_method, int subme, int me_range,         \
+                                                        const int32_t *pos, const int16_t *par, const int16_t *mvc,  \
+                                                        const uint16_t *cost_mv, int n, int32_t *out,                \
+                                                        int32_t *nevals, int32_t *halfpel_thresh,                    \
+                                                        const int32_t *ref_cost, const x264hip_refine_ext_t *ext,    \
+                                                        void *stream )                                               \
+    {                                                                                                                \
+        if( n < 0 || ( n > 0 && ( !fenc || !fw || !p0 || !p1 || !p2 || !p3 || !pos || !par || !mvc || !cost_mv ||   \
+                                  !out ) ) )                                                                         \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
+        return map_err( launch_me_search_ref<BD>( fenc, fs, ffs, fw, planes, rs, rfs, i_pixel, me_method, subme,     \
+                                                  me_range, pos, par, mvc, cost_mv, n, out, nevals, halfpel_thresh,  \
+                                                  ref_cost, ext, (hipStream_t)stream ), "me_search_ref_thresh" );    \
     }                                                                                                                \
     extern "C" int x264hip_##BD##_sub_dct_batch( int kind, const PT<BD>::pixel *fenc, intptr_t fs,                  \
                                                  const PT<BD>::pixel *fdec, intptr_t ds, const int64_t *fo,          \

@@ -381,17 +381,17 @@ hipError_t launch_subpel_qpel9( int op, int i_pixel, const typename PT<BD>::pixe
 template <int BD>
 hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                                     const typename PT<BD>::pixel *const planes[4], intptr_t rs, intptr_t rfs,
-                                    int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
+                                    int i_pixel, int subme, int kind, int fpel_satd, const int32_t *pos,
                                     const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int n,
-                                    int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *ext,
-                                    hipStream_t stream );
+                                    int32_t *out, int32_t *nevals, int32_t *thr, const int32_t *rcost,
+                                    const x264hip_refine_ext_t *ext, hipStream_t stream );
 template <int BD>
 hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                                  const typename PT<BD>::pixel *fw, const typename PT<BD>::pixel *const planes[4],
                                  intptr_t rs, intptr_t rfs, int i_pixel, int me_method, int subme, int me_range,
                                  const int32_t *pos, const int16_t *par, const int16_t *mvc, const uint16_t *cost_mv,
-                                 int n, int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *ext,
-                                 hipStream_t stream );
+                                 int n, int32_t *out, int32_t *nevals, int32_t *thr, const int32_t *rcost,
+                                 const x264hip_refine_ext_t *ext, hipStream_t stream );
 template <int BD>
 hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int nmb, int me_range,
                                  const int16_t *origin, const int16_t *par, const int32_t *init_cost,

@@ -14,7 +14,10 @@
 // meet through DPP adds and every lane of the segment reads the four candidate costs and
 // takes the reference's decisions itself (the packed bcost << 6 / << 4 codes, COPY*_IF_LT's
 // strict <, the odir skip), so the segment's lanes stay in step without LDS.  The
-// multi-reference early exit (p_halfpel_thresh) is the caller's (it is NULL here).
+// multi-reference early exit (p_halfpel_thresh, me.c:931-944) reads and writes a per-partition
+// threshold when the caller passes one: the references of one MB chain through it, one launch
+// per reference (analyse.c:1260-1314), with the caller's i_ref_cost adjustments around each
+// search (analyse.c:1271, 1310) applied in the kernel from a per-partition ref_cost.
 //
 // The EXT forms add what x264's default preset runs on P slices (b_chroma_me at subme >= 5,
 // common/macroblock.c:507-509) and weighted references (m->weight, analyse.c:1248-1250):
@@ -216,7 +219,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     intptr_t rs, intptr_t rfs, int n, int hpel_iters, int qpel_iters, int subme, int refine_qpel,
     const int32_t *__restrict__ pos, const int16_t *__restrict__ par, const int32_t *__restrict__ init_cost,
     const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out, int32_t *__restrict__ nevals, int nstride,
-    const RsExt<BD> ext )
+    int32_t *__restrict__ thr, const int32_t *__restrict__ rcost, const RsExt<BD> ext )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD;
@@ -471,11 +474,26 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
             }
     }
 
+    // the multi-reference early exit (me.c:931-944) against *p_halfpel_thresh, which the caller
+    // holds less this reference's i_ref_cost during the search (analyse.c:1271, 1310)
+    bool early = false;
+    if( thr )
+    {
+        const int rc = rcost ? rcost[j] : 0;
+        int t = thr[j] - rc;
+        if( (bcost * 7) >> 3 > t )
+            early = true;                                 // m->cost, m->mv; m->cost_mv untouched
+        else if( bcost < t )
+            t = bcost;
+        if( live && lane == sbase )
+            thr[j] = t + rc;
+    }
+
     if( subme != 1 )
     {
         // quarterpel diamond (me.c:946-963)
         int bdir = -1;
-        bool act = true;
+        bool act = !early;
         for( int i = qpel_iters; i > 0; i-- )
         {
             if( bmy <= miny || bmy >= maxy || bmx <= minx || bmx >= maxx )
@@ -520,10 +538,10 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
             }
         }
     }
-    else if( __any( bmy > miny && bmy < maxy && bmx > minx && bmx < maxx ) )
+    else if( __any( !early && bmy > miny && bmy < maxy && bmx > minx && bmx < maxx ) )
     {
         // subme 1 (me.c:964-986): one qpel diamond of fpelcmp over mc_luma blocks
-        const bool act = bmy > miny && bmy < maxy && bmx > minx && bmx < maxx;
+        const bool act = !early && bmy > miny && bmy < maxy && bmx > minx && bmx < maxx;
         const int omx = bmx, omy = bmy;
         const int mx[4] = { omx, omx, omx - 1, omx + 1 }, my[4] = { omy - 1, omy + 1, omy, omy };
         int c[4];
@@ -544,7 +562,14 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
 
     if( live && lane == sbase )
     {
-        *(int4 *)(out + 4 * j) = make_int4( bcost, bmx, bmy, (int)cmx[bmx] + (int)cmy[bmy] );
+        if( early )
+        {
+            out[4 * j] = bcost;
+            out[4 * j + 1] = bmx;
+            out[4 * j + 2] = bmy;
+        }
+        else
+            *(int4 *)(out + 4 * j) = make_int4( bcost, bmx, bmy, (int)cmx[bmx] + (int)cmy[bmy] );
         if( nevals )
             nevals[j * nstride] = nsad | (nsatd << 16) | (nchroma << 24);
     }
@@ -595,17 +620,21 @@ template <int BD> hipError_t rs_ext( const x264hip_refine_ext_t *xe, RsExt<BD> &
 template <int BD>
 static hipError_t refine_launch( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                                  const typename PT<BD>::pixel *const planes[4], intptr_t rs, intptr_t rfs,
-                                 int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
+                                 int i_pixel, int subme, int kind, int fpel_satd, const int32_t *pos,
                                  const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int n,
-                                 int32_t *out, int32_t *nevals, int nstride, const x264hip_refine_ext_t *xe,
-                                 hipStream_t stream )
+                                 int32_t *out, int32_t *nevals, int nstride, int32_t *thr, const int32_t *rcost,
+                                 const x264hip_refine_ext_t *xe, hipStream_t stream )
 {
     if( n <= 0 )
         return hipSuccess;
-    if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || ((uintptr_t)out & 15) )
+    if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || kind < 0 || kind > 2 || ((uintptr_t)out & 15) )
         return hipErrorInvalidValue;
-    const int hpel = k_subpel_iterations[subme][refine_qpel ? 0 : 2];
-    const int qpel = k_subpel_iterations[subme][refine_qpel ? 1 : 3];
+    // kind 0: x264_me_search_ref's refine (me.c:794-796), 1: x264_me_refine_qpel (:801-810),
+    // 2: x264_me_refine_qpel_refdupe (:812-815)
+    const int refine_qpel = kind == 1;
+    const int hpel = kind == 2 ? 0 : k_subpel_iterations[subme][refine_qpel ? 0 : 2];
+    const int qpel = kind == 2 ? min( 2, (int)k_subpel_iterations[subme][3] )
+                               : k_subpel_iterations[subme][refine_qpel ? 1 : 3];
     // fpelcmp is SATD only under TESA with subme > 1 (encoder.c:1423-1426)
     const bool fs_satd = fpel_satd && subme > 1;
     RsExt<BD> ext;
@@ -618,7 +647,7 @@ static hipError_t refine_launch( const typename PT<BD>::pixel *fenc, intptr_t fs
 #define RS_GO( I, F, E )                                                                                          \
     hipLaunchKernelGGL( ( me_refine_subpel_kernel<BD, I, F, E> ), g, blk, 0, stream, fenc, fs, ffs, planes[0],    \
                         planes[1], planes[2], planes[3], rs, rfs, n, hpel, qpel, subme, refine_qpel ? 1 : 0, pos,   \
-                        par, init_cost, cost_mv, out, nevals, nstride, ext )
+                        par, init_cost, cost_mv, out, nevals, nstride, thr, rcost, ext )
 #define RS_MODE( I, F )                                                                                           \
     if( mode == 0 ) { RS_GO( I, F, 0 ); } else if( mode == 1 ) { RS_GO( I, F, 1 ); } else { RS_GO( I, F, 2 ); }
 #define RS_CASE( I )                                                                                              \
@@ -639,13 +668,13 @@ static hipError_t refine_launch( const typename PT<BD>::pixel *fenc, intptr_t fs
 template <int BD>
 hipError_t launch_me_refine_subpel( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                                     const typename PT<BD>::pixel *const planes[4], intptr_t rs, intptr_t rfs,
-                                    int i_pixel, int subme, int refine_qpel, int fpel_satd, const int32_t *pos,
+                                    int i_pixel, int subme, int kind, int fpel_satd, const int32_t *pos,
                                     const int16_t *par, const int32_t *init_cost, const uint16_t *cost_mv, int n,
-                                    int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *xe,
-                                    hipStream_t stream )
+                                    int32_t *out, int32_t *nevals, int32_t *thr, const int32_t *rcost,
+                                    const x264hip_refine_ext_t *xe, hipStream_t stream )
 {
-    return refine_launch<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, refine_qpel, fpel_satd, pos, par,
-                              init_cost, cost_mv, n, out, nevals, 1, xe, stream );
+    return refine_launch<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, kind, fpel_satd, pos, par,
+                              init_cost, cost_mv, n, out, nevals, 1, thr, rcost, xe, stream );
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -932,7 +961,10 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
                 const int d = (start + 2 * (s2 >> 1)) * ((s2 & 1) ? -1 : 1);
                 mx = omx + (v ? 0 : d);
                 my = omy + (v ? d : 0);
-                return sl < nhs + nvs && in_range( mx, my );
+                // CROSS checks the moving axis only (me.c:160-173): omx / omy may lie a step past the
+                // other axis' limit (DIA1_ITER scores pmx +- 1, pmy +- 1 unchecked)
+                const int a = v ? my : mx, lo = v ? ymin : xmin, hi = v ? ymax : xmax;
+                return sl < nhs + nvs && (d > 0 ? a <= hi : a >= lo);
             };
             for( int b = 0; b < nhs + nvs; b += 4 )
             {
@@ -1144,8 +1176,9 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
     }
     if( live && lane == sbase )
     {
-        *(int4 *)(out + 4 * j) = make_int4( cst, mx, my, cmv );
-        if( rpar )
+        if( !rpar )                                       // (with the refine, out is the refine's)
+            *(int4 *)(out + 4 * j) = make_int4( cst, mx, my, cmv );
+        else
         {
             *(int4 *)(rpar + 8 * j) = make_int4( (int)sr_pack( mx, my ), (int)sr_pack( mvpx, mvpy ),
                                                  (int)sr_pack( p[6], p[7] ), (int)sr_pack( p[8], p[9] ) );
@@ -1165,8 +1198,8 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
                                  const typename PT<BD>::pixel *fw, const typename PT<BD>::pixel *const planes[4],
                                  intptr_t rs, intptr_t rfs, int i_pixel, int me_method, int subme, int me_range,
                                  const int32_t *pos, const int16_t *par, const int16_t *mvc, const uint16_t *cost_mv,
-                                 int n, int32_t *out, int32_t *nevals, const x264hip_refine_ext_t *xe,
-                                 hipStream_t stream )
+                                 int n, int32_t *out, int32_t *nevals, int32_t *thr, const int32_t *rcost,
+                                 const x264hip_refine_ext_t *xe, hipStream_t stream )
 {
     if( n <= 0 )
         return hipSuccess;
@@ -1209,7 +1242,7 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
     e = hipGetLastError();
     if( e == hipSuccess && refine )
         e = refine_launch<BD>( fenc, fs, ffs, planes, rs, rfs, i_pixel, subme, 0, 0, pos, rpar, rinit, cost_mv, n, out,
-                               nevals ? nevals + 1 : nullptr, 2, xe, stream );
+                               nevals ? nevals + 1 : nullptr, 2, thr, rcost, xe, stream );
     if( buf )
     {
         const hipError_t ef = hipFreeAsync( buf, stream );
@@ -1220,20 +1253,23 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
 }
 template hipError_t launch_me_search_ref<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, const uint8_t *const[4],
                                              intptr_t, intptr_t, int, int, int, int, const int32_t *, const int16_t *,
-                                             const int16_t *, const uint16_t *, int, int32_t *, int32_t *,
-                                             const x264hip_refine_ext_t *, hipStream_t );
+                                             const int16_t *, const uint16_t *, int, int32_t *, int32_t *, int32_t *,
+                                             const int32_t *, const x264hip_refine_ext_t *, hipStream_t );
 template hipError_t launch_me_search_ref<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *,
                                               const uint16_t *const[4], intptr_t, intptr_t, int, int, int, int,
                                               const int32_t *, const int16_t *, const int16_t *, const uint16_t *, int,
-                                              int32_t *, int32_t *, const x264hip_refine_ext_t *, hipStream_t );
+                                              int32_t *, int32_t *, int32_t *, const int32_t *, const x264hip_refine_ext_t *,
+                                              hipStream_t );
 
 template hipError_t launch_me_refine_subpel<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *const[4],
                                                 intptr_t, intptr_t, int, int, int, int, const int32_t *,
                                                 const int16_t *, const int32_t *, const uint16_t *, int, int32_t *,
-                                                int32_t *, const x264hip_refine_ext_t *, hipStream_t );
+                                                int32_t *, int32_t *, const int32_t *, const x264hip_refine_ext_t *,
+                                                hipStream_t );
 template hipError_t launch_me_refine_subpel<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *const[4],
                                                  intptr_t, intptr_t, int, int, int, int, const int32_t *,
                                                  const int16_t *, const int32_t *, const uint16_t *, int, int32_t *,
-                                                 int32_t *, const x264hip_refine_ext_t *, hipStream_t );
+                                                 int32_t *, int32_t *, const int32_t *, const x264hip_refine_ext_t *,
+                                                 hipStream_t );
 
 } // namespace x264hip
