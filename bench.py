@@ -1019,6 +1019,8 @@ def rates_refine(x, a, world, mbw, mbh, F):
                     leg + "_moved_frac": moved, leg + "_qpel_frac": qpel,
                     leg + "_valu_frac": work / (ev_ms * 1e-3) / VALU_LANE_OPS})
     res.update(rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes, ext, cm, cm_d, span))
+    res.update(rates_search_ref3(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes, (nvd, co, cs), cm_d,
+                                 span))
     del hv, planes, dev, nvd
     return res
 
@@ -1089,6 +1091,59 @@ def rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes,
                     leg + "_absdiff_frac": cands * px / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF,
                     leg + "_mv_found_frac": ((out[:, 1] == 13) & (out[:, 2] == 10)).float().mean().item()})
     return res
+
+
+def rates_search_ref3(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes, chroma, cm_d, span):
+    """x264's default P16x16 search over three references (ref = 3, common/base.c:384, with
+    b_early_terminate, analyse.c:303): mb_analyse_inter_p16x16's loop (analyse.c:1260-1314) as one
+    x264hip_*_me_search_ref_thresh launch per reference, every MB's p_halfpel_thresh chained
+    through them (me.c:931-944) with the i_ref_cost adjustments (analyse.c:1271, 1310).  Frames
+    3..F of rates_refine's sequence search references 1, 2 and 3 frames back (true motion 1x, 2x,
+    3x the per-frame (13, 10) qpel; synthetic predictors around it, search_params); i_ref_cost =
+    lambda * te() bits of ref 0 / 1 / 2 at num_ref_idx 3 (1, 3, 3 bits, lambda 12 -- qp 26's
+    x264_lambda_tab).  Rates: MB-reference searches/s (search16_hex_ref3_partitions_per_s) and
+    MBs/s (all three references), the fraction of later-reference searches the exit ended."""
+    if F < 3:
+        return {}
+    Fr = F - 2
+    n = Fr * mbw * mbh
+    INT_MAX = (1 << 31) - 1
+    thr = torch.full((n,), INT_MAX, dtype=torch.int32, device="cuda")
+    legs = []
+    for k in range(3):
+        pos, par, mvc = search_params(mbw, mbh, Fr, 0, seed=7 + k, motion=(13 * (k + 1), 10 * (k + 1)))
+        rf = slice(2 - k, F - k)                    # reference k + 1 frames back (planes: frames 0 .. F-1)
+        nvd, co, cs = chroma
+        ek = x.refine_ext(1, 1, 0, fenc_chroma=[nvd[3:]], fenc_chroma_origin=co, fenc_chroma_stride=cs,
+                          ref_chroma=[nvd[rf]], ref_chroma_origin=co, ref_chroma_stride=cs)
+        legs.append(dict(pos=torch.from_numpy(pos).cuda(), par=torch.from_numpy(par).cuda(),
+                         mvc=torch.from_numpy(mvc).cuda(), planes=[p[rf] for p in planes], ext=ek,
+                         rcost=torch.full((n,), 12 * (1 if k == 0 else 3), dtype=torch.int32, device="cuda"),
+                         out=torch.full((n, 4), -7, dtype=torch.int32, device="cuda"),
+                         ne=torch.empty((n, 2), dtype=torch.int32, device="cuda")))
+
+    def step():
+        thr.fill_(INT_MAX)
+        for L in legs:
+            x.me_search_ref(dev[3:], origin, stride, L["planes"][0], L["planes"], origin, stride, 0, 1, 7, 16, L["pos"],
+                            L["par"], L["mvc"], (cm_d, span), out=L["out"], fenc_frame_stride=fstride,
+                            ref_frame_stride=fstride, nevals=L["ne"], ext=L["ext"], halfpel_thresh=thr,
+                            ref_cost=L["rcost"])
+    wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
+    for L in legs:                                  # the last step's outputs: mark the early exits
+        L["out"][:, 3].fill_(-7)
+    step()
+    torch.cuda.synchronize()
+    early = [int((L["out"][:, 3] == -7).sum().item()) for L in legs]
+    qcalls = [int(((L["ne"][:, 1] >> 16) & 0xFF).sum().item()) for L in legs]
+    return {"search16_hex_ref3_partitions_per_s": world * a.steps * 3 * n / wall,
+            "search16_hex_ref3_mbs_per_s": world * a.steps * n / wall,
+            "search16_hex_ref3_step_ms": ev_ms, "search16_hex_ref3_mbs_per_step": n,
+            "search16_hex_ref3_early_exit_frac": [e / n for e in early],
+            "search16_hex_ref3_refine_satd_per_part": [q / n for q in qcalls],
+            "search16_hex_ref3_workload": "frames 3..F of rates_refine's sequence, references 1 / 2 / 3 frames "
+                                          "back, HEX subme 7 me_range 16 chroma ME, i_ref_cost 12 / 36 / 36, "
+                                          "one launch per reference, p_halfpel_thresh chained"}
 
 
 def rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, bd=8):
