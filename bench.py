@@ -37,29 +37,38 @@ HBM_PEAK = 8.0e12
 
 
 def workload_2160p(x, a, world, rank, pg_world, rank_dev):
-    """configs[3] as its own bench line (--workload 2160p): one 2160p frame per GPU per step, frame-
-    per-GPU across the node (rank r encodes frames of its own shard; no collective on the data
-    path).  A step = the new frame's upload from pinned host memory on a copy stream (overlapped
-    with the previous step's kernels), its half-pel planes (it is the next step's reference),
-    the full-search SAD table (range R) against the previous frame and its decision
-    (me_esa_argmin over the whole table: the exhaustive search of me.c:618-631), refine_subpel at
-    subme 7 (two hpel SAD diamonds, the SATD re-score, two qpel SATD diamonds: x264's default
-    subme) from the decisions, and the fused 4x4 DCT + quant.  value = every rank's candidates
-    (the table's (2R+1)^2 per MB + the refine's SAD / SATD calls, counted by the kernel) over
-    the max-over-ranks wall of the timed steps, H2D included."""
+    """configs[3] as its own bench line (--workload 2160p): one 2160p 4:2:0 frame per GPU per step,
+    frame-per-GPU across the node (rank r encodes frames of its own shard; no collective on the
+    data path).  The frames are synth.make_subpel_sequence's (quarter-pel motion (3.25, 2.5) px per
+    frame, so the refine's diamonds move), held in pinned host memory as unpadded pictures, as
+    x264_encoder_encode receives them.  A step = the new picture's luma and NV12 planes uploaded
+    by x264hip_upload_plane (the PCIe read fused with x264_frame_expand_border) on the copy stream
+    of a CU-partitioned stream pair (x264hip_stream_pair_create), overlapped with the previous
+    step's kernels on the compute stream: its half-pel planes (it is the next step's reference),
+    the exhaustive search of me.c:618-631 (range R around mv 0) against the previous frame with
+    its decision, fused (x264hip_8_me_search_esa: no table in HBM), refine_subpel at
+    subme 7 with chroma ME (x264's default preset on P slices: two hpel SAD diamonds, the SATD
+    re-score with U / V, two qpel SATD diamonds, common/macroblock.c:507-509) from the decisions,
+    and the fused 4x4 DCT + quant.  value = every rank's candidates (the table's (2R+1)^2 per MB
+    + the refine's SAD / SATD calls, counted by the kernel) over the max-over-ranks wall of the
+    timed steps, H2D included."""
     from x264hip import synth, dist as xd
     W, H, R = 3840, 2160, a.range
     mbw, mbh = W // 16, H // 16
     nmb = mbw * mbh
     nf = 8
     p0, _ = xd.frame_shard(world * nf, world, rank)
-    planes, stride, origin = synth.make_sequence(nf + 1, W, H, 8, start=p0)
-    fsz = planes[0].size
-    host = torch.from_numpy(planes).pin_memory()
-    del planes
-    ring = torch.empty((3,) + tuple(host.shape[1:]), dtype=torch.uint8, device="cuda")
+    luma, stride, origin, nv, cs, co = synth.make_subpel_sequence(nf + 1, W, H, 8, start=p0)
+    pad, cpad = synth.PAD, 16
+    # the pictures: unpadded planes in pinned memory (x264_picture_t's planes)
+    host_y = torch.from_numpy(np.ascontiguousarray(luma[:, pad:pad + H, pad:pad + W])).pin_memory()
+    host_c = torch.from_numpy(np.ascontiguousarray(nv[:, cpad:cpad + H // 2, 2 * cpad:2 * cpad + W])).pin_memory()
+    up_bytes = (host_y[0].numel() + host_c[0].numel())
+    fsz, csz = luma[0].size, nv[0].size
+    del luma, nv
+    ring = torch.empty((3, H + 2 * pad, stride), dtype=torch.uint8, device="cuda")
+    cring = torch.empty((3, H // 2 + 2 * cpad, cs), dtype=torch.uint8, device="cuda")
     hp = [[torch.empty_like(ring[0:1]) for _ in range(3)] for _ in range(3)]
-    table = torch.empty((1, mbh, mbw, 2 * R + 1, x.me_table_pitch(R)), dtype=torch.int16, device="cuda")
     par, init, cm, span = tesa_params(mbw, mbh, 1, R, centre=(0, 0))
     par_d, init_d = torch.from_numpy(par).cuda(), torch.from_numpy(init).cuda()
     cm_d = torch.from_numpy(cm.view(np.int16)).cuda()
@@ -71,6 +80,7 @@ def workload_2160p(x, a, world, rank, pg_world, rank_dev):
     rpar[:, 4], rpar[:, 5] = 4 * (-16 * mbx - 24), 4 * (-16 * mby - 24)
     rpar[:, 6], rpar[:, 7] = 4 * (16 * (mbw - 1 - mbx) + 24), 4 * (16 * (mbh - 1 - mby) + 24)
     rpar_d = torch.from_numpy(rpar).cuda()
+    rinit = torch.empty(nmb, dtype=torch.int32, device="cuda")
     rout = torch.empty((nmb, 4), dtype=torch.int32, device="cuda")
     ne = torch.empty(nmb, dtype=torch.int32, device="cuda")
     flat = [16] * 64
@@ -79,36 +89,52 @@ def workload_2160p(x, a, world, rank, pg_world, rank_dev):
     bs4 = torch.from_numpy(q4b[1, 26].copy()).cuda()
     dct = torch.empty((nmb, 256), dtype=torch.int16, device="cuda")
     nz = torch.empty(nmb, dtype=torch.int32, device="cuda")
+    # chroma ME inputs per (cur, ref) ring pair (x264hip_refine_ext_t), built once
+    exts = {(c, r): x.refine_ext(1, 1, 0, fenc_chroma=[cring[c:c + 1]], fenc_chroma_origin=co, fenc_chroma_stride=cs,
+                                 ref_chroma=[cring[r:r + 1]], ref_chroma_origin=co, ref_chroma_stride=cs)
+            for c in range(3) for r in range(3) if c != r}
 
-    def search(cur, ref):
-        x.me_search_full(cur, origin, stride, ref, origin, stride, mbw, mbh, 1, R, table=table,
-                         fenc_frame_stride=fsz, ref_frame_stride=fsz)
+    # one x264hip_upload_planes launch per picture (luma + NV12), its records built once
+    ups = {(slot, i): [x.plane_upload(ring[slot], origin, stride, host_y[i], unit=1, pad_x=pad, pad_y=pad),
+                       x.plane_upload(cring[slot], co, cs, host_c[i], unit=2, pad_x=2 * cpad, pad_y=cpad)]
+           for slot in range(3) for i in range(nf + 1)}
+
+    def upload(slot, i):
+        x.upload_planes(ups[(slot, i)])
+
+    def esa(cur, ref):
+        """the exhaustive search of me.c:618-631 over range R around mv 0 with its decision, fused
+        (x264hip_8_me_search_esa: the SAD table never leaves the chip)"""
+        x.me_search_esa(cur, origin, stride, ref, origin, stride, mbw, mbh, 1, R, R, par_d, init_d, (cm_d, span),
+                        out=dec, fenc_frame_stride=fsz, ref_frame_stride=fsz)
 
     def frame(c, r):
         """the compute of one frame: ring slot c against slot r (r's hpel planes already built)"""
         cur, ref = ring[c:c + 1], ring[r:r + 1]
         x.hpel_filter(cur, origin, stride, W, H, outs=hp[c])
-        search(cur, ref)
-        x.me_esa_argmin(table, R, R, par_d, init_d, (cm_d, span), out=dec)
-        rpar_d[:, 0:2] = (dec[:, 1:3] * 4).to(torch.int16)
+        esa(cur, ref)
+        rpar_d[:, 0:2] = dec[:, 1:3] * 4
+        rinit.copy_(dec[:, 0])
         x.me_refine_subpel(cur, origin, stride, [ref] + hp[r], origin, stride, x.PIXEL_16x16, 7, pos_d, rpar_d,
-                           dec[:, 0].contiguous(), (cm_d, span), out=rout, fenc_frame_stride=fsz,
-                           ref_frame_stride=fsz, nevals=ne)
+                           rinit, (cm_d, span), out=rout, fenc_frame_stride=fsz, ref_frame_stride=fsz, nevals=ne,
+                           ext=exts[(c, r)])
         x.mb_dct_quant(4, cur, origin, stride, ref, origin, stride, mbw, mbh, 1, mf4, bs4, dct=dct, nz=nz,
                        fenc_frame_stride=fsz, pred_frame_stride=fsz)
 
     # the refine's candidates per frame pair of the shard (the same pairs the timed steps cycle)
-    ring[0].copy_(host[0])
+    upload(0, 0)
     x.hpel_filter(ring[0:1], origin, stride, W, H, outs=hp[0])
-    rcands = []
+    rcands, rchroma, moved = [], [], []
     for i in range(nf):
         c, r = (i + 1) % 3, i % 3
-        ring[c].copy_(host[i + 1])
+        upload(c, i + 1)
         frame(c, r)
         rcands.append(int((ne & 0xFFFF).sum().item()) + int(((ne >> 16) & 0xFF).sum().item()))
+        rchroma.append(int((ne >> 24).sum().item()))
+        moved.append((rout[:, 1:3] != rpar_d[:, 0:2].int()).any(1).float().mean().item())
     cand_frame = nmb * (2 * R + 1) ** 2 + float(np.mean(rcands))
 
-    comp, copy = torch.cuda.current_stream(), torch.cuda.Stream()
+    comp, copy = x.stream_pair(16)
     done = [torch.cuda.Event() for _ in range(3)]
     ready = [torch.cuda.Event() for _ in range(3)]
     state = {"n": 0}
@@ -118,40 +144,72 @@ def workload_2160p(x, a, world, rank, pg_world, rank_dev):
         c, r = (n + 1) % 3, n % 3
         with torch.cuda.stream(copy):                 # upload frame n+1 while frame n's kernels may still run
             copy.wait_event(done[c])
-            ring[c].copy_(host[(n + 1) % (nf + 1)], non_blocking=True)
+            upload(c, (n + 1) % (nf + 1))
             ready[c].record(copy)
-        comp.wait_event(ready[c])
-        frame(c, r)
-        done[r].record(comp)
+        with torch.cuda.stream(comp):
+            comp.wait_event(ready[c])
+            frame(c, r)
+            done[r].record(comp)
         state["n"] = n + 1
+
+    def reset():
+        torch.cuda.synchronize()
+        state["n"] = 0
+        upload(0, 0)
+        x.hpel_filter(ring[0:1], origin, stride, W, H, outs=hp[0])
+        for ev in ready + done:
+            ev.record()
+        torch.cuda.synchronize()
+    reset()
+    cur_stream = torch.cuda.current_stream()
+    wall, _ = timed(step, a.steps, a.warmup, world)
+    cur_stream.wait_stream(comp)
+    # the parts alone: the upload (both planes) and the compute of one frame
+    reset()
+    with torch.cuda.stream(copy):
+        _, up_ms = timed(lambda: upload(1, 1), a.steps, min(a.warmup, 20), world)
+    with torch.cuda.stream(comp):
+        _, comp_ms = timed(lambda: frame(1, 0), a.steps, min(a.warmup, 20), world)
+    # host time to enqueue one step (no GPU wait inside step())
+    reset()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    host_ms = (time.perf_counter() - t0) / a.steps * 1e3
     torch.cuda.synchronize()
-    ring[0].copy_(host[0])
-    x.hpel_filter(ring[0:1], origin, stride, W, H, outs=hp[0])
-    ready[0].record()
-    for ev in done:
-        ev.record()
-    wall, ev_ms = timed(step, a.steps, a.warmup, world)
     value = world * a.steps * cand_frame / wall
-    # the dominant kernel alone (the SAD table of one 2160p frame), events on its stream
-    _, s_ms = timed(lambda: search(ring[1:2], ring[0:1]), a.steps, a.warmup, world)
+    # the dominant kernel alone (the fused search + decision of one 2160p frame) on the compute
+    # stream's 240 CUs, events on that stream
+    with torch.cuda.stream(comp):
+        _, s_ms = timed(lambda: esa(ring[1:2], ring[0:1]), a.steps, a.warmup, world)
+    torch.cuda.synchronize()
+    x.stream_pair_destroy((comp, copy))
     absd = nmb * (2 * R + 1) ** 2 * 256
-    roof = {"kernel": "me_full_sad16_v7_kernel<%d, %d>" % (R, x.me_table_pitch(R) // 4), "bound": "valu",
+    roof = {"kernel": "me_full_esa_v7_kernel<%d, false>" % R, "bound": "valu",
             "achieved": absd / (s_ms * 1e-3) / 1e12, "peak": SAD_PEAK_ABSDIFF / 1e12,
             "unit": "T byte-absdiff/s (algorithmic: 256 per 16x16 candidate)",
             "frac": absd / (s_ms * 1e-3) / SAD_PEAK_ABSDIFF, "traffic": None, "launch_ms": s_ms,
-            "algorithmic_bytes_per_launch": 2 * nmb * 256 + nmb * (2 * R + 1) ** 2 * 2}
+            "cus": 240, "peak_note": "peak is the whole chip's 256 CUs; the kernel runs on the compute stream's 240",
+            "algorithmic_bytes_per_launch": 2 * nmb * 256 + nmb * 12}
+    ms = wall / a.steps * 1e3
     out = {
         "metric": "SAD+SATD candidate-MVs/sec + DCT+quant blocks/sec, 1080p, 1/2/4/8 GPU",
         "value": value,
         "unit": "candidate MVs/s (SAD16x16 full-search table + refine_subpel SAD/SATD calls)",
-        "n_gpus": pg_world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": wall / a.steps * 1e3,
+        "n_gpus": pg_world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": ms,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
-        "config": {"workload": "configs[3]: 3840x2160 luma, full-search ME range %d (SAD table + decision) + "
-                               "refine_subpel subme 7 (SAD/SATD) + 4x4 DCT/quant per frame, one frame per GPU "
-                               "per step streamed from pinned host memory (H2D in the timed region)" % R,
-                   "frames_per_step_per_gpu": 1, "mbs_per_frame": nmb,
+        "config": {"workload": "configs[3]: 3840x2160 4:2:0, full-search ME range %d (fused search + ESA decision) + "
+                               "refine_subpel subme 7 with chroma ME (SAD/SATD + U/V SATD) + 4x4 DCT/quant per "
+                               "frame, one frame per GPU per step uploaded from pinned host pictures (luma + "
+                               "NV12, borders expanded on the way in; H2D in the timed region)" % R,
+                   "content": "synth.make_subpel_sequence: quarter-pel motion (3.25, 2.5) px per frame",
+                   "b_chroma_me": 1, "frames_per_step_per_gpu": 1, "mbs_per_frame": nmb,
                    "candidates_per_mb": cand_frame / nmb, "table_candidates_per_mb": (2 * R + 1) ** 2,
-                   "refine_candidates_per_frame": float(np.mean(rcands)), "upload_bytes_per_frame": int(fsz),
+                   "refine_candidates_per_frame": float(np.mean(rcands)),
+                   "refine_chroma_calls_per_frame": float(np.mean(rchroma)),
+                   "refine_moved_frac": float(np.mean(moved)), "upload_bytes_per_frame": int(up_bytes),
+                   "upload_ms": up_ms, "upload_GBps": up_bytes / (up_ms * 1e-3) / 1e9, "compute_ms": comp_ms,
+                   "host_enqueue_ms": host_ms, "step_vs_upload": ms / up_ms,
                    "parallelism": "frame-per-GPU x%d" % world, "world_size": pg_world, "rank_devices": rank_dev,
                    "dist_backend": (os.environ.get("X264HIP_DIST_BACKEND", "nccl") if world > 1 else None)},
         "roofline": roof,
@@ -159,7 +217,8 @@ def workload_2160p(x, a, world, rank, pg_world, rank_dev):
     if rank == 0 and world == 1 and not a.no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import oracle_lib as orc  # cpu_baseline leg only
-        f0, f1 = host[1].numpy().ravel(), host[0].numpy().ravel()
+        f0 = ring[1].cpu().numpy().ravel()
+        f1 = ring[0].cpu().numpy().ravel()
         try:
             share = len(os.sched_getaffinity(0))
         except AttributeError:
@@ -177,7 +236,7 @@ def workload_2160p(x, a, world, rank, pg_world, rank_dev):
                                "cores": nthr, "kind": "port", "cpu_model": cpu_model(),
                                "sample": "%d calls of the full search over %d of the frame's %d MB rows, %d "
                                          "threads, %.1f s" % (calls, band, mbh, nthr, dt)}
-    del ring, hp, table, host
+    del ring, cring, hp, host_y, host_c
     return out
 
 

@@ -379,6 +379,26 @@ int  x264hip_forward_ref( void *dst, int dst_device, const void *src, int src_de
  * form of configs[3] (H2D per frame overlapped with compute).
  * Asynchronous; the host buffer must stay untouched until `stream` passes it. */
 int  x264hip_upload( void *dst, const void *host_src, size_t bytes, void *stream );
+/* Upload one picture plane (width_bytes x height at host_src, rows src_stride apart, page-locked)
+ * into a padded frame plane: dst = its pixel (0,0); the plane copy of x264_frame_copy_picture
+ * (common/frame.c:393-521) with plane_expand_border (frame.c:535-554) fused -- the edge element of
+ * `unit` bytes (1 / 2: 8 / 10-bit luma; 2 / 4: an NV12 / NV16 plane, per component) repeated over
+ * pad_x bytes left and right, then rows 0 and height-1 with their pads over pad_y rows above and
+ * below.  width_bytes, pad_x and both strides multiples of 16, both pointers 16-byte aligned.
+ * Asynchronous on `stream`, as x264hip_upload. */
+int  x264hip_upload_plane( void *dst, intptr_t dst_stride, const void *host_src, intptr_t src_stride,
+                           int width_bytes, int height, int unit, int pad_x, int pad_y, void *stream );
+/* the planes of one picture (luma + NV12 / NV16, or Y, U, V; 1..3) in one launch, each as
+ * x264hip_upload_plane describes it, so the link does not drain between planes */
+typedef struct x264hip_plane_upload_t
+{
+    void *dst;
+    intptr_t dst_stride;
+    const void *host_src;
+    intptr_t src_stride;
+    int32_t width_bytes, height, unit, pad_x, pad_y;
+} x264hip_plane_upload_t;
+int  x264hip_upload_planes( int n, const x264hip_plane_upload_t *planes, void *stream );
 /* A compute / copy stream pair on complementary CU sets of the current device: *copy on
  * the first reserve_cus CUs, *compute on the others (hipExtStreamCreateWithCUMask), for
  * overlapping x264hip_upload of the next frame with the current frame's kernels.

@@ -166,3 +166,78 @@ def test_empty_launches(hip, bd):
     assert fn("me_tesa")(P, 64, 0, P, 1 << 18, 0, P, 0, 1, 1, 1, 16, 1, None, 0, None, P, P, P, O, None) == -1
     torch.cuda.synchronize()
     assert (out == 0x5A5A5A5A).all()
+
+
+def _expand_ref(plane, pad_x, pad_y, unit):
+    """plane_expand_border (reference common/frame.c:535-554) of a picture plane, in numpy: the
+    edge element of `unit` bytes repeated over pad_x bytes, then the first / last padded rows"""
+    h, wb = plane.shape
+    e = plane.reshape(h, wb // unit, unit)
+    left = np.repeat(e[:, :1], pad_x // unit, axis=1)
+    right = np.repeat(e[:, -1:], pad_x // unit, axis=1)
+    rows = np.concatenate([left, e, right], 1).reshape(h, wb + 2 * pad_x)
+    return np.concatenate([np.repeat(rows[:1], pad_y, 0), rows, np.repeat(rows[-1:], pad_y, 0)], 0)
+
+
+@pytest.mark.parametrize("W,H,unit,pad_x,pad_y", [(96, 64, 1, 32, 32), (96, 32, 2, 32, 32), (192, 64, 2, 64, 32),
+                                                   (192, 32, 4, 64, 16), (3840, 2160, 1, 32, 32),
+                                                   (3840, 1080, 2, 32, 32), (48, 1, 1, 16, 3)])
+def test_upload_plane_expands_borders(hip, W, H, unit, pad_x, pad_y):
+    """x264hip_upload_plane: a pinned picture plane lands in the padded plane with the borders
+    plane_expand_border writes (luma, NV12 per component, 10-bit units), nothing outside them"""
+    rng = np.random.default_rng(W + H + unit)
+    src_stride = W + 32
+    host_np = rng.integers(0, 256, (H, src_stride), dtype=np.uint8)
+    host = torch.from_numpy(host_np).pin_memory()
+    ds = (W + 2 * pad_x + 64 + 63) // 64 * 64
+    rows = H + 2 * pad_y + 2
+    dev = torch.full((rows * ds,), 0xA5, dtype=torch.uint8, device="cuda")
+    origin = (pad_y + 1) * ds + pad_x
+    hip.upload_plane(dev, origin, ds, host[:, :W], unit=unit, pad_x=pad_x, pad_y=pad_y)
+    torch.cuda.synchronize()
+    got = dev.cpu().numpy().reshape(rows, ds)
+    want = _expand_ref(host_np[:, :W], pad_x, pad_y, unit)
+    assert np.array_equal(got[1:1 + H + 2 * pad_y, :W + 2 * pad_x], want)
+    assert (got[0] == 0xA5).all() and (got[-1] == 0xA5).all() and (got[:, W + 2 * pad_x:] == 0xA5).all()
+
+
+def test_upload_plane_refuses(hip):
+    dev = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    pinned = torch.zeros((16, 64), dtype=torch.uint8).pin_memory()
+    L = hip.lib()
+    ptr = ctypes.c_void_p(dev.data_ptr() + 32 * 256 + 32)
+    # width not a multiple of 16, a pad band not a multiple of 16, a bad unit, pageable memory
+    for wb, unit, px in ((40, 1, 32), (64, 1, 24), (64, 3, 32)):
+        assert L.x264hip_upload_plane(ptr, 256, ctypes.c_void_p(pinned.data_ptr()), 64, wb, 16, unit, px, 32,
+                                      None) != 0
+    page = np.zeros((16, 64), np.uint8)
+    assert L.x264hip_upload_plane(ptr, 256, ctypes.c_void_p(page.ctypes.data), 64, 64, 16, 1, 32, 32, None) != 0
+    torch.cuda.synchronize()
+    assert not dev.any()
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_upload_planes_picture(hip, bd):
+    """x264hip_upload_planes: a 4:2:0 picture's luma and NV12 planes in one launch, each padded as
+    plane_expand_border pads it (x264_frame_expand_border / _chroma)"""
+    W, H = 160, 96
+    es = 1 if bd == 8 else 2
+    dt = np.uint8 if bd == 8 else np.uint16
+    rng = np.random.default_rng(bd)
+    y = rng.integers(0, 1 << bd, (H, W)).astype(dt)
+    c = rng.integers(0, 1 << bd, (H // 2, W)).astype(dt)             # interleaved U, V
+    hy, hc = torch.from_numpy(y).pin_memory(), torch.from_numpy(c).pin_memory()
+    tdt = torch.uint8 if bd == 8 else torch.int16
+    ys, cs = (W + 64 + 63) // 64 * 64, (W + 64 + 63) // 64 * 64
+    dy = torch.zeros(((H + 64) * ys,), dtype=tdt, device="cuda")
+    dc = torch.zeros(((H // 2 + 32) * cs,), dtype=tdt, device="cuda")
+    hip.upload_planes([hip.plane_upload(dy, 32 * ys + 32, ys, hy, unit=es, pad_x=32 * es, pad_y=32),
+                       hip.plane_upload(dc, 16 * cs + 32, cs, hc, unit=2 * es, pad_x=32 * es, pad_y=16)])
+    torch.cuda.synchronize()
+    gy = dy.cpu().numpy().view(dt).reshape(H + 64, ys)[:, :W + 64]
+    gc = dc.cpu().numpy().view(dt).reshape(H // 2 + 32, cs)[:, :W + 64]
+    assert np.array_equal(gy, np.pad(y, 32, mode="edge"))
+    u, v = c[:, 0::2], c[:, 1::2]
+    wc = np.zeros((H // 2 + 32, W + 64), dt)
+    wc[:, 0::2], wc[:, 1::2] = np.pad(u, 16, mode="edge"), np.pad(v, 16, mode="edge")
+    assert np.array_equal(gc, wc)

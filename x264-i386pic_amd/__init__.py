@@ -134,6 +134,42 @@ def upload(dst, src):
     return dst
 
 
+class PlaneUpload(ctypes.Structure):
+    """x264hip_plane_upload_t"""
+    _fields_ = [("dst", ctypes.c_void_p), ("dst_stride", ctypes.c_ssize_t), ("host_src", ctypes.c_void_p),
+                ("src_stride", ctypes.c_ssize_t), ("width_bytes", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("unit", ctypes.c_int32), ("pad_x", ctypes.c_int32), ("pad_y", ctypes.c_int32)]
+
+
+def plane_upload(dst, dst_origin, dst_stride, src, unit=1, pad_x=32, pad_y=32):
+    """one x264hip_plane_upload_t: the pinned host picture plane `src` [height, width] (rows may be
+    longer) into the padded device plane `dst` whose pixel (0,0) is element dst_origin (dst_stride
+    elements per row), borders expanded by pad_x bytes / pad_y rows, unit = the edge element's
+    bytes"""
+    if not src.is_pinned() or not dst.is_cuda:
+        raise ValueError("plane_upload: needs a pinned host source and a device destination")
+    es = dst.element_size()
+    return PlaneUpload(dst.data_ptr() + dst_origin * es, dst_stride * es, src.data_ptr(),
+                       src.stride(0) * src.element_size(), src.shape[1] * src.element_size(), src.shape[0], unit,
+                       pad_x, pad_y)
+
+
+def upload_planes(uploads):
+    """x264hip_upload_planes: the plane_upload() records of one picture (1..3) in one launch on
+    the current stream"""
+    arr = (PlaneUpload * len(uploads))(*uploads)
+    _rc(lib().x264hip_upload_planes(len(uploads), arr, _stream()), "upload_planes")
+
+
+def upload_plane(dst, dst_origin, dst_stride, src, unit=1, pad_x=32, pad_y=32):
+    """x264hip_upload_plane: one picture plane (see plane_upload)"""
+    u = plane_upload(dst, dst_origin, dst_stride, src, unit, pad_x, pad_y)
+    _rc(lib().x264hip_upload_plane(_c.c_void_p(u.dst), _c.c_ssize_t(u.dst_stride), _c.c_void_p(u.host_src),
+                                   _c.c_ssize_t(u.src_stride), u.width_bytes, u.height, unit, pad_x, pad_y,
+                                   _stream()), "upload_plane")
+    return dst
+
+
 def stream_pair(reserve_cus=16):
     """(compute, copy) torch external streams on complementary CU sets of the current device
     (x264hip_stream_pair_create): the copy stream owns the first `reserve_cus` CUs."""
@@ -309,6 +345,10 @@ def _declare(L):
     L.x264hip_forward_ref.restype = _c.c_int
     L.x264hip_upload.argtypes = [_P, _P, _c.c_size_t, _P]
     L.x264hip_upload.restype = _c.c_int
+    L.x264hip_upload_plane.argtypes = [_P, _IP, _P, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P]
+    L.x264hip_upload_plane.restype = _c.c_int
+    L.x264hip_upload_planes.argtypes = [_c.c_int, _P, _P]
+    L.x264hip_upload_planes.restype = _c.c_int
     L.x264hip_stream_pair_create.argtypes = [_c.c_int, _P, _P]
     L.x264hip_stream_pair_create.restype = _c.c_int
     L.x264hip_stream_destroy.argtypes = [_P]

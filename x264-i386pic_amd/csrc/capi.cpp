@@ -158,6 +158,53 @@ extern "C" int x264hip_upload( void *dst, const void *host_src, size_t bytes, vo
     return e == hipSuccess ? X264HIP_OK : set_err( e, "upload" );
 }
 
+// picture planes from page-locked host memory into padded planes, borders expanded
+static bool pinned_range( const void *p, size_t bytes, const void **dev )
+{
+    void *d0 = nullptr, *d1 = nullptr;
+    if( hipHostGetDevicePointer( &d0, (void *)p, 0 ) != hipSuccess || !d0 ||
+        hipHostGetDevicePointer( &d1, (void *)((const uint8_t *)p + bytes - 1), 0 ) != hipSuccess ||
+        (uint8_t *)d1 != (uint8_t *)d0 + bytes - 1 )
+    {
+        (void)hipGetLastError();
+        return false;
+    }
+    *dev = d0;
+    return true;
+}
+
+extern "C" int x264hip_upload_planes( int n, const x264hip_plane_upload_t *pl, void *stream )
+{
+    if( n < 1 || n > 3 || !pl )
+        return X264HIP_EINVAL;
+    UploadPlane q[3];
+    for( int k = 0; k < n; k++ )
+    {
+        const x264hip_plane_upload_t &u = pl[k];
+        if( !u.dst || !u.host_src || u.width_bytes <= 0 || u.height <= 0 || u.src_stride < u.width_bytes ||
+            u.dst_stride < u.width_bytes + 2 * (intptr_t)u.pad_x )
+            return X264HIP_EINVAL;
+        const void *d = nullptr;
+        if( !pinned_range( u.host_src, (size_t)u.src_stride * (u.height - 1) + u.width_bytes, &d ) )
+        {
+            snprintf( t_err, sizeof(t_err), "x264hip_upload_planes: source is not page-locked host memory" );
+            return X264HIP_EINVAL;
+        }
+        q[k] = { u.dst, d, u.dst_stride, u.src_stride, u.width_bytes, u.height, u.unit, u.pad_x, u.pad_y };
+    }
+    hipError_t e = launch_upload_planes( n, q, (hipStream_t)stream );
+    return e == hipSuccess ? X264HIP_OK : set_err( e, "upload_planes" );
+}
+
+extern "C" int x264hip_upload_plane( void *dst, intptr_t dst_stride, const void *host_src, intptr_t src_stride,
+                                     int width_bytes, int height, int unit, int pad_x, int pad_y, void *stream )
+{
+    if( width_bytes <= 0 || height <= 0 )
+        return X264HIP_OK;
+    const x264hip_plane_upload_t u = { dst, dst_stride, host_src, src_stride, width_bytes, height, unit, pad_x, pad_y };
+    return x264hip_upload_planes( 1, &u, stream );
+}
+
 // Two streams on complementary CU sets of the current device (hipExtStreamCreateWithCUMask):
 // `copy` on the first `reserve_cus` CUs, `compute` on the rest.  The frame-streaming
 // pipeline of configs[3] runs the PCIe-read upload of frame n+1 on `copy` while frame n's

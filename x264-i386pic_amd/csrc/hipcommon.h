@@ -340,6 +340,14 @@ hipError_t scratch_trim( int dev );
 hipError_t scratch_alloc( void **p, size_t bytes, hipStream_t stream );   // free with hipFreeAsync
 hipError_t lowres_status( hipStream_t stream );
 hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t stream );
+struct UploadPlane
+{
+    void *dst;
+    const void *src;                    // device address of the pinned source
+    intptr_t ds, ss;
+    int width_bytes, height, unit, pad_x, pad_y;
+};
+hipError_t launch_upload_planes( int n, const UploadPlane *planes, hipStream_t stream );
 template <int BD>
 hipError_t launch_cmp_batch( int op, int i_pixel, const typename PT<BD>::pixel *fenc, intptr_t fs,
                              const typename PT<BD>::pixel *ref, intptr_t rs, const int64_t *fenc_off,

@@ -1371,6 +1371,133 @@ template hipError_t launch_weight_plane<8>( uint8_t *, intptr_t, intptr_t, const
 template hipError_t launch_weight_plane<10>( uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t, intptr_t,
                                              int, int, int, int, int, int, hipStream_t );
 
+// ---------------------------------------------------------------------------
+// A picture plane from page-locked host memory into a padded frame plane: x264_frame_copy_
+// picture's plane copy (common/frame.c:393-521) fused with plane_expand_border (frame.c:535-554,
+// as x264_frame_expand_border / _chroma run it over a whole frame), so the link carries the
+// picture's own bytes and the pads are written from the registers that hold the edge.  Lane i
+// of the grid-stride loop moves 16-byte chunk i of the w16 x h chunk grid (four in flight per
+// lane, as upload_kernel); the chunk at a row's left / right end also writes its row's pad
+// band (the edge element of `unit` bytes repeated: 1 or 2 for luma, 2 or 4 for an NV12 /
+// NV16 plane), and rows 0 / h-1 are written again into the pad_y rows above / below (the
+// padded rows, corners included).
+__device__ __forceinline__ uint4 unit_fill( uint4 v, int unit, bool last )
+{
+    // the first (last = false) or last element of v, repeated over 16 bytes
+    uint32_t w = last ? v.w : v.x;
+    if( unit == 1 )
+        w = last ? (w >> 24) * 0x01010101u : (w & 0xff) * 0x01010101u;
+    else if( unit == 2 )
+        w = last ? (w >> 16) * 0x00010001u : (w & 0xffff) * 0x00010001u;
+    return make_uint4( w, w, w, w );
+}
+
+// up to three planes of one picture per launch (luma + NV12, or Y, U, V): one chunk grid over
+// all of them, so the link never drains between planes
+struct UpPlanes
+{
+    uint8_t *dst[3];
+    const uint8_t *src[3];
+    intptr_t ds[3], ss[3];
+    uint32_t w16[3], h[3], end[3];      // chunks per row, rows, cumulative chunk count
+    uint32_t unit[3], padx16[3], pad_y[3];
+    int n;
+};
+
+// (the plane's fields by select, never by a dynamic index: indexing the kernel-argument arrays
+// copies them to scratch memory)
+template <typename T> __device__ __forceinline__ T psel( const T (&a)[3], int k ) { return k == 0 ? a[0] : k == 1 ? a[1] : a[2]; }
+
+__global__ __launch_bounds__( 256 ) void upload_plane_kernel( const UpPlanes P )
+{
+    const uint32_t total = P.end[2], nthr = gridDim.x * blockDim.x;
+    // plane, row and column of chunk i (32-bit index math: a 2160p picture is 0.78 M chunks)
+    auto locate = [&]( uint32_t i, int &k, uint32_t &y, uint32_t &c ) __attribute__( ( always_inline ) ) {
+        k = i >= P.end[0] ? (i >= P.end[1] ? 2 : 1) : 0;
+        const uint32_t j = i - (k == 0 ? 0u : k == 1 ? P.end[0] : P.end[1]), w = psel( P.w16, k );
+        y = j / w;
+        c = j - y * w;
+    };
+    auto get = [&]( uint32_t i ) __attribute__( ( always_inline ) ) {
+        int k;
+        uint32_t y, c;
+        locate( i, k, y, c );
+        return *((const uint4 *)(psel( P.src, k ) + (intptr_t)y * psel( P.ss, k )) + c);
+    };
+    auto put = [&]( uint32_t i, uint4 v ) __attribute__( ( always_inline ) ) {
+        int k;
+        uint32_t y, c;
+        locate( i, k, y, c );
+        const int h = (int)psel( P.h, k ), py = (int)psel( P.pad_y, k ), px = (int)psel( P.padx16, k );
+        const int y0 = y == 0 ? -py : (int)y, y1 = (int)y == h - 1 ? h - 1 + py : (int)y;
+        const bool l = c == 0, r = c == psel( P.w16, k ) - 1;
+        const int unit = (int)psel( P.unit, k );
+        const uint4 fl = l ? unit_fill( v, unit, false ) : v;
+        const uint4 fr = r ? unit_fill( v, unit, true ) : v;
+        uint8_t *const dk = psel( P.dst, k );
+        const intptr_t dsk = psel( P.ds, k );
+        for( int yy = y0; yy <= y1; yy++ )
+        {
+            uint4 *d = (uint4 *)(dk + (intptr_t)yy * dsk) + c;
+            *d = v;
+            if( l )
+                for( int q = 1; q <= px; q++ )
+                    d[-q] = fl;
+            if( r )
+                for( int q = 1; q <= px; q++ )
+                    d[q] = fr;
+        }
+    };
+    uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    for( ; i + 3 * nthr < total; i += 4 * nthr )
+    {
+        const uint4 a = get( i ), b = get( i + nthr ), c = get( i + 2 * nthr ), e = get( i + 3 * nthr );
+        put( i, a );
+        put( i + nthr, b );
+        put( i + 2 * nthr, c );
+        put( i + 3 * nthr, e );
+    }
+    for( ; i < total; i += nthr )
+        put( i, get( i ) );
+}
+
+hipError_t launch_upload_planes( int n, const UploadPlane *pl, hipStream_t stream )
+{
+    if( n < 1 || n > 3 )
+        return hipErrorInvalidValue;
+    UpPlanes P = {};
+    uint64_t total = 0;
+    for( int k = 0; k < n; k++ )
+    {
+        const UploadPlane &q = pl[k];
+        if( q.width_bytes <= 0 || q.height <= 0 || ((q.width_bytes | q.pad_x | (int)(q.ds & 15) | (int)(q.ss & 15)) & 15) ||
+            (((uintptr_t)q.dst | (uintptr_t)q.src) & 15) || (q.unit != 1 && q.unit != 2 && q.unit != 4) ||
+            q.pad_x < 0 || q.pad_y < 0 )
+            return hipErrorInvalidValue;
+        P.dst[k] = (uint8_t *)q.dst;
+        P.src[k] = (const uint8_t *)q.src;
+        P.ds[k] = q.ds;
+        P.ss[k] = q.ss;
+        P.w16[k] = (uint32_t)(q.width_bytes / 16);
+        P.h[k] = (uint32_t)q.height;
+        total += (uint64_t)P.w16[k] * P.h[k];
+        if( total >= (1ull << 31) )
+            return hipErrorInvalidValue;
+        P.end[k] = (uint32_t)total;
+        P.unit[k] = (uint32_t)q.unit;
+        P.padx16[k] = (uint32_t)(q.pad_x / 16);
+        P.pad_y[k] = (uint32_t)q.pad_y;
+    }
+    for( int k = n; k < 3; k++ )
+        P.end[k] = (uint32_t)total;
+    P.n = n;
+    const int wv = variant( V_UPLOAD_WGS );
+XX
+    const unsigned g = (unsigned)std::min<size_t>( cap, std::max<size_t>( 1, (total + 1023) / 1024 ) );
+    hipLaunchKernelGGL( upload_plane_kernel, dim3( g ), dim3( 256 ), 0, stream, P );
+    return hipGetLastError();
+}
+
 hipError_t launch_upload( void *dst, const void *src, size_t bytes, hipStream_t stream )
 {
     if( !bytes )

@@ -71,14 +71,14 @@ def _smooth_field(rng, K, fmax):
 
 
 def _eval_field(field, xs, ys):
-    """sum_i amp_i cos(2 pi (fx_i x + fy_i y) + ph_i) on the grid ys x xs (separable: two outer
-    products per component)"""
+    """sum_i amp_i cos(2 pi (fx_i x + fy_i y) + ph_i) on the grid ys x xs: separable, so one
+    rank-2K product [cos by_i, -sin by_i] . [cos ax_i, sin ax_i]^T (a 2160p field in ~0.1 s)"""
     f, ph, amp = field
-    out = np.zeros((len(ys), len(xs)))
-    for (fx, fy), p, a in zip(f, ph, amp):
-        ax, by = 2 * np.pi * fx * xs, 2 * np.pi * fy * ys + p
-        out += a * (np.outer(np.cos(by), np.cos(ax)) - np.outer(np.sin(by), np.sin(ax)))
-    return out
+    by = 2 * np.pi * np.outer(ys, f[:, 1]) + ph            # [len(ys), K]
+    ax = 2 * np.pi * np.outer(xs, f[:, 0])                 # [len(xs), K]
+    left = np.concatenate([np.cos(by) * amp, -np.sin(by) * amp], 1)
+    right = np.concatenate([np.cos(ax), np.sin(ax)], 1)
+    return left @ right.T
 
 
 def make_subpel_sequence(nframes, width, height, bitdepth=8, pad=PAD, seed=3, start=0, motion=(13, 10)):
