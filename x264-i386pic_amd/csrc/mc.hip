@@ -1492,7 +1492,9 @@ hipError_t launch_upload_planes( int n, const UploadPlane *pl, hipStream_t strea
         P.end[k] = (uint32_t)total;
     P.n = n;
     const int wv = variant( V_UPLOAD_WGS );
-XX
+    // 32 workgroups (two per CU of the copy stream's 16): a 2160p 4:2:0 picture in 0.232 ms
+    // against 0.247 with upload_kernel's 16 (profiles/r06f_upload_wgs.txt)
+    const size_t cap = wv > 0 ? (size_t)wv : 32;
     const unsigned g = (unsigned)std::min<size_t>( cap, std::max<size_t>( 1, (total + 1023) / 1024 ) );
     hipLaunchKernelGGL( upload_plane_kernel, dim3( g ), dim3( 256 ), 0, stream, P );
     return hipGetLastError();
