@@ -154,40 +154,106 @@ __device__ __forceinline__ uint32_t block4_cost( const int (&d)[4][4], bool satd
     return acc >> 1;
 }
 
-// one 4x4 block of plane p of mc_chroma (mc.c:252-283) at chroma mv (mvx, mvyc) eighth-pels,
-// weighted by wt when on, scored against the lane's fenc block fb (row y: pixel x in packed
-// word x / PPD).  s = the interleaved plane at the block's top-left, plane p's sample.
-template <int BD>
-__device__ __forceinline__ uint32_t nv_block_cost( const typename PT<BD>::pixel *s, intptr_t rcs, int mvx, int mvyc,
-                                                   const uint32_t (&fb)[4][4 / PT<BD>::PPD],
-                                                   const RsWeight &wt, bool satd )
+// The chroma cost of one 4x4 position of mc_chroma (mc.c:252-283) in both planes at once, split
+// over a lane pair: NV12 / NV16 interleave U and V, so a sample pair (U x, V x) is one packed
+// 16-bit pair (v_perm of the bytes at 8 bit, the dword itself at 10 bit) and every step runs on
+// the two planes together -- the bilinear taps as packed u16 multiply-adds (cA..cD sum to 64, so
+// 64 * 1023 + 32 fits), the differences and the Hadamard as packed i16 (|coef| <= 8 * 1023).
+// Lane half hh computes output rows 2hh, 2hh+1 (source rows 2hh .. 2hh+2) and their row
+// transform and first column butterfly; the last butterfly is |a + b| + |a - b| = 2 max(|a|, |b|),
+// so each lane takes two of the four columns, gets the partner's t of those columns by one DPP
+// swap per word, and adds max(|t|, |t'|): the pair's sum is satd_4x4's sum |coef| >> 1
+// (pixel.c:265-288) exactly.  The odd lane negates its columns 2, 3 of differences, which swaps
+// its row transform's outputs 0, 1 with 2, 3: each lane then keeps its outputs 0, 1 and sends
+// 2, 3, with no lane-dependent select.  s = the interleaved plane at the position's top-left U
+// sample, row 2hh; fb = the lane's two fenc rows as (U, V) pairs.  Returns U's partial cost | V's
+// << 16.
+typedef unsigned short rs_us2 __attribute__( ( ext_vector_type( 2 ) ) );
+__device__ __forceinline__ rs_us2 as_us2( uint32_t v ) { return __builtin_bit_cast( rs_us2, v ); }
+__device__ __forceinline__ x264hip_short2 as_s2( rs_us2 v ) { return __builtin_bit_cast( x264hip_short2, v ); }
+__device__ __forceinline__ uint32_t as_u32( x264hip_short2 v ) { return __builtin_bit_cast( uint32_t, v ); }
+
+template <int BD> __device__ __forceinline__ rs_us2 nv_pair( const uint32_t *w, int x )
 {
-    constexpr int NDW = BD == 8 ? 3 : 5;    // the row's 5 samples of plane p, every other pixel from s
-    const int dx = mvx & 7, dy = mvyc & 7;
-    const int cA = (8 - dx) * (8 - dy), cB = dx * (8 - dy), cC = (8 - dx) * dy, cD = dx * dy;
+    // the (U, V) samples of pixel x of a row of interleaved words, as u16 lanes
+    if constexpr( BD == 8 )
+        return as_us2( __builtin_amdgcn_perm( 0u, w[x >> 1], (x & 1) ? 0x0c030c02u : 0x0c010c00u ) );
+    else
+        return as_us2( w[x] );
+}
+
+template <int BD>
+__device__ __forceinline__ uint32_t nv_pair_cost( const typename PT<BD>::pixel *s, intptr_t rcs, int mvx, int mvyc,
+                                                  const uint32_t (&fb)[2][4], const RsWeight &wu,
+                                                  const RsWeight &wv, bool satd, bool hh )
+{
+    constexpr int NDW = BD == 8 ? 3 : 5;    // five (U, V) pairs of a source row
+    const uint32_t dx = mvx & 7, dy = mvyc & 7;
+    const rs_us2 kA = (rs_us2)(uint16_t)((8 - dx) * (8 - dy)), kB = (rs_us2)(uint16_t)(dx * (8 - dy));
+    const rs_us2 kC = (rs_us2)(uint16_t)((8 - dx) * dy), kD = (rs_us2)(uint16_t)(dx * dy);
     s += (intptr_t)(mvyc >> 3) * rcs + (mvx >> 3) * 2;
-    int v[5][5];
+    uint32_t w[3][NDW];
 #pragma unroll
-    for( int r = 0; r < 5; r++ )
-    {
-        uint32_t w[NDW];
-        load_al_pad<NDW>( s + r * rcs, w );
+    for( int r = 0; r < 3; r++ )
+        load_al_pad<NDW>( s + r * rcs, w[r] );
+    x264hip_short2 d[2][4];
 #pragma unroll
-        for( int x = 0; x < 5; x++ )
-            v[r][x] = BD == 8 ? (int)((w[x >> 1] >> (16 * (x & 1))) & 0xff) : (int)(w[x] & 0xffff);
-    }
-    int d[4][4];
-#pragma unroll
-    for( int y = 0; y < 4; y++ )
+    for( int y = 0; y < 2; y++ )
 #pragma unroll
         for( int x = 0; x < 4; x++ )
         {
-            int m = (cA * v[y][x] + cB * v[y][x + 1] + cC * v[y + 1][x] + cD * v[y + 1][x + 1] + 32) >> 6;
-            if( wt.on )
-                m = clip_pix<BD>( ((m * wt.scale + wt.rnd) >> wt.denom) + wt.offset );
-            d[y][x] = upix<BD>( fb[y][x / PT<BD>::PPD], x % PT<BD>::PPD ) - m;
+            rs_us2 m = (kA * nv_pair<BD>( w[y], x ) + kB * nv_pair<BD>( w[y], x + 1 ) + kC * nv_pair<BD>( w[y + 1], x ) +
+                        kD * nv_pair<BD>( w[y + 1], x + 1 ) + (rs_us2)32) >> (rs_us2)6;
+            if( wu.on | wv.on )
+            {
+                int lo = m.x, hi = m.y;
+                if( wu.on )
+                    lo = clip_pix<BD>( ((lo * wu.scale + wu.rnd) >> wu.denom) + wu.offset );
+                if( wv.on )
+                    hi = clip_pix<BD>( ((hi * wv.scale + wv.rnd) >> wv.denom) + wv.offset );
+                m = (rs_us2){ (uint16_t)lo, (uint16_t)hi };
+            }
+            d[y][x] = __builtin_bit_cast( x264hip_short2, fb[y][x] ) - as_s2( m );
         }
-    return block4_cost( d, satd );
+    x264hip_short2 acc = { 0, 0 };
+    if( !satd )
+    {
+#pragma unroll
+        for( int y = 0; y < 2; y++ )
+#pragma unroll
+            for( int x = 0; x < 4; x++ )
+                acc += __builtin_elementwise_abs( d[y][x] );
+        return as_u32( acc );
+    }
+    const x264hip_short2 sg = hh ? (x264hip_short2)-1 : (x264hip_short2)1;
+    x264hip_short2 t[2][4];
+#pragma unroll
+    for( int y = 0; y < 2; y++ )
+    {
+        const x264hip_short2 a0 = d[y][0] + d[y][1], a1 = d[y][0] - d[y][1];
+        const x264hip_short2 a2 = sg * (d[y][2] + d[y][3]), a3 = sg * (d[y][2] - d[y][3]);
+        t[y][0] = a0 + a2; t[y][2] = a0 - a2; t[y][1] = a1 + a3; t[y][3] = a1 - a3;
+    }
+    // rows 0 + 1 and 0 - 1 of the lane's pair of rows; outputs 0, 1 kept, 2, 3 sent (quad_perm
+    // [1,0,3,2]); max(|a|, |b|) = max(max(a, b), -min(a, b))
+    x264hip_short2 own[4], snd[4];
+#pragma unroll
+    for( int x = 0; x < 2; x++ )
+    {
+        own[x] = t[0][x] + t[1][x];
+        own[2 + x] = t[0][x] - t[1][x];
+        snd[x] = t[0][2 + x] + t[1][2 + x];
+        snd[2 + x] = t[0][2 + x] - t[1][2 + x];
+    }
+#pragma unroll
+    for( int j = 0; j < 4; j++ )
+    {
+        const x264hip_short2 r = __builtin_bit_cast(
+            x264hip_short2, __builtin_amdgcn_mov_dpp( (int)as_u32( snd[j] ), 0xB1, 0xF, 0xF, false ) );
+        acc += __builtin_elementwise_max( __builtin_elementwise_max( own[j], r ),
+                                          -__builtin_elementwise_min( own[j], r ) );
+    }
+    return as_u32( acc );
 }
 
 // the NT tiles of each group summed into the group's first lane (pair sums, quad sums by
@@ -246,10 +312,13 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     // ---- EXT: the weight of the luma get_ref, the lane's chroma blocks / tiles ----
     const RsWeight wt0 = ext.wt[0];
     const bool chroma = EXT && ext.chroma;                // launch-uniform
-    constexpr int CDW = 4 / PT<BD>::PPD;                  // packed words of a 4-pixel chroma row
-    const pixel *cref[2] = { nullptr, nullptr };          // EXT 1: the lane's blocks in the ref plane
-    uint32_t cfb[2][4][CDW] = {};                         //        and their fenc rows
-    int cpl[2] = { -1, -1 };                              //        plane (0 U, 1 V; -1 none)
+    constexpr int FDW = 8 / PT<BD>::PPD;                  // words of a 4-pixel interleaved chroma row
+    const pixel *cref[2] = { nullptr, nullptr };          // EXT 1: the lane's positions in the ref plane
+    // their two fenc rows, in LDS (word-major: a word of every lane is one conflict-free row) --
+    // in VGPRs they pushed the kernel past 128 registers, 4 -> 3 waves per SIMD
+    __shared__ uint32_t s_cfb[EXT == 1 ? 2 * 2 * 4 : 1][256];
+    bool has[2] = { false, false };
+    const bool hh = u & 1;                                //        the lane's half of a position
     uint32_t fu[4][HDW] = {}, fv[4][HDW] = {};            // EXT 2: the fenc tiles of U and V
     const pixel *u0 = nullptr, *u1 = nullptr, *u2 = nullptr, *u3 = nullptr;   // and their hpel planes
     const pixel *v0 = nullptr, *v1 = nullptr, *v2 = nullptr, *v3 = nullptr;   // (no arrays: scratch)
@@ -258,27 +327,30 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         if( chroma )
         {
             // chroma block cw x ch of the partition (luma2chroma_pixel, pixel.h:70-76) in 4x4
-            // blocks, U's then V's (at most 4 * NT of them); lane u takes blocks u and u + NT
+            // positions of both planes (at most NT of them); lane pair (2q, 2q+1) takes positions
+            // q and q + NT / 2, lane 2q + hh their rows 2hh, 2hh+1
             constexpr int CW = BW / 2, BXN = CW / 4;
-            const int ch = BH >> ext.vs, ncb = BXN * (ch / 4);
+            const int ch = BH >> ext.vs, npos = BXN * (ch / 4);
             const intptr_t crow = by >> ext.vs;
 #pragma unroll
             for( int k = 0; k < 2; k++ )
             {
-                const int b = u + NT * k;
-                if( b < 2 * ncb )
+                const int q = (u >> 1) + (NT / 2) * k;
+                if( q < npos )
                 {
-                    const int p = b >= ncb, jb = b - p * ncb;
-                    const int cx = 4 * (jb % BXN), cy = 4 * (jb / BXN);
-                    cpl[k] = p;
-                    cref[k] = ext.ref_c[0] + f * ext.rfcs + (crow + cy) * ext.rcs + bx + 2 * cx + p;
-                    const pixel *fc = ext.fenc_c[0] + f * ext.ffcs + (crow + cy) * ext.fcs + bx + 2 * cx + p;
+                    const int cx = 4 * (q % BXN), cy = 4 * (q / BXN) + 2 * hh;
+                    has[k] = true;
+                    cref[k] = ext.ref_c[0] + f * ext.rfcs + (crow + cy) * ext.rcs + bx + 2 * cx;
+                    const pixel *fc = ext.fenc_c[0] + f * ext.ffcs + (crow + cy) * ext.fcs + bx + 2 * cx;
 #pragma unroll
-                    for( int y = 0; y < 4; y++ )
+                    for( int y = 0; y < 2; y++ )
+                    {
+                        uint32_t r[FDW];
+                        load_row_u<FDW>( fc + y * ext.fcs, r );
 #pragma unroll
-                        for( int x = 0; x < 4; x++ )
-                            cfb[k][y][x / PT<BD>::PPD] |= (uint32_t)fc[y * ext.fcs + 2 * x]
-                                                          << ((32 / PT<BD>::PPD) * (x % PT<BD>::PPD));
+                        for( int i = 0; i < 4; i++ )       // as (U, V) pairs
+                            s_cfb[(2 * k + y) * 4 + i][threadIdx.x] = as_u32( as_s2( nv_pair<BD>( r, i ) ) );
+                    }
                 }
             }
         }
@@ -358,17 +430,21 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         if constexpr( EXT == 1 )
         {
             const int mvyc = (2 * (gy + ext.mvy_offset)) >> ext.vs;
+            uint32_t pk = 0;                              // U | V << 16 (no carry: <= 2 * 4 * 8184)
 #pragma unroll
             for( int k = 0; k < 2; k++ )
-                if( on && cpl[k] >= 0 )
+                if( on && has[k] )
                 {
-                    const uint32_t c = nv_block_cost<BD>( cref[k], ext.rcs, gx, mvyc, cfb[k], ext.wt[1 + cpl[k]],
-                                                          qsatd );
-                    if( cpl[k] )
-                        vv += c;
-                    else
-                        vu += c;
+                    uint32_t fb[2][4];
+#pragma unroll
+                    for( int y = 0; y < 2; y++ )
+#pragma unroll
+                        for( int i = 0; i < 4; i++ )
+                            fb[y][i] = s_cfb[(2 * k + y) * 4 + i][threadIdx.x];
+                    pk += nv_pair_cost<BD>( cref[k], ext.rcs, gx, mvyc, fb, ext.wt[1], ext.wt[2], qsatd, hh );
                 }
+            vu = pk & 0xffff;
+            vv = pk >> 16;
         }
         else if constexpr( EXT == 2 )
         {
