@@ -185,3 +185,57 @@ int oracle8_subpel_list_mt( int op, int i_pixel, const uint8_t *fenc, intptr_t f
         pthread_join( th[t], NULL );
     return nthreads;
 }
+
+float oracle8_ssim_wxh( const uint8_t *pix1, intptr_t stride1, const uint8_t *pix2, intptr_t stride2, int width,
+                        int height, int *cnt );
+
+typedef struct
+{
+    const uint8_t *p1, *p2;
+    intptr_t s1, s2;
+    int width, b0, b1;
+    const int32_t *bands;
+    float *ssim;
+    int32_t *cnt;
+} ssim_job_t;
+
+static void *ssim_worker( void *arg )
+{
+    ssim_job_t *j = arg;
+    for( int b = j->b0; b < j->b1; b++ )
+    {
+        const int y = j->bands[2 * b], h = j->bands[2 * b + 1];
+        int c = 0;
+        j->ssim[b] = oracle8_ssim_wxh( j->p1 + (intptr_t)y * j->s1, j->s1, j->p2 + (intptr_t)y * j->s2, j->s2,
+                                       j->width, h, &c );
+        j->cnt[b] = c;
+    }
+    return NULL;
+}
+
+/* the encoder's SSIM bands (x264hip.ssim_encoder_bands: { y, h } pairs) of one frame pair, split
+ * into nthreads contiguous runs of bands: one thread per run instead of one host task per band
+ * (a band is ~17 us of work at 1080p, less than a thread-pool hand-off); returns threads used */
+int oracle8_ssim_bands_mt( const uint8_t *pix1, intptr_t stride1, const uint8_t *pix2, intptr_t stride2, int width,
+                           const int32_t *bands, int nbands, float *ssim, int32_t *cnt, int nthreads )
+{
+    pthread_t th[256];
+    ssim_job_t jobs[256];
+    if( nthreads < 1 )
+        nthreads = 1;
+    if( nthreads > 256 )
+        nthreads = 256;
+    if( nthreads > nbands )
+        nthreads = nbands > 0 ? nbands : 1;
+    for( int t = 0; t < nthreads; t++ )
+    {
+        ssim_job_t j = { pix1, pix2, stride1, stride2, width, (int)((int64_t)nbands * t / nthreads),
+                         (int)((int64_t)nbands * (t + 1) / nthreads), bands, ssim, cnt };
+        jobs[t] = j;
+        if( pthread_create( &th[t], NULL, ssim_worker, &jobs[t] ) )
+            return -1;
+    }
+    for( int t = 0; t < nthreads; t++ )
+        pthread_join( th[t], NULL );
+    return nthreads;
+}

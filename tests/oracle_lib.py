@@ -139,6 +139,8 @@ _L.oracle8_mb_dct_quant_mt.argtypes = [C.c_int, _P, _IP, _P, _IP, C.c_int, C.c_i
 _L.oracle8_mb_dct_quant_mt.restype = C.c_int
 _L.oracle8_subpel_list_mt.argtypes = [C.c_int, C.c_int, _P, _IP, _P, _P, _P, _P, _IP, _P, _P, C.c_int, _P, C.c_int]
 _L.oracle8_subpel_list_mt.restype = C.c_int
+_L.oracle8_ssim_bands_mt.argtypes = [_P, _IP, _P, _IP, C.c_int, _P, C.c_int, _P, _P, C.c_int]
+_L.oracle8_ssim_bands_mt.restype = C.c_int
 
 _OPS = {"sad": 0, "ssd": 1, "satd": 2}
 
@@ -787,6 +789,18 @@ def ssim_end4(bd, sum0, sum1, width):
     s0 = np.ascontiguousarray(sum0, np.int32).reshape(5, 4)
     s1 = np.ascontiguousarray(sum1, np.int32).reshape(5, 4)
     return np.float32(fn(bd, "ssim_end4")(_addr(s0), _addr(s1), width))
+
+
+def ssim_bands_mt(a, a_off, sa, b, b_off, sb, width, bands, nthreads):
+    """8-bit x264_pixel_ssim_wxh over the { y, h } bands of a frame pair on nthreads pthreads
+    (cpubench.c): (ssim float32 [nbands], cnt int32 [nbands])"""
+    bd_ = np.ascontiguousarray(bands, np.int32)
+    out = np.zeros(len(bd_), np.float32)
+    cnt = np.zeros(len(bd_), np.int32)
+    used = _L.oracle8_ssim_bands_mt(_addr(a, a_off), sa, _addr(b, b_off), sb, width, _addr(bd_), len(bd_),
+                                    _addr(out), _addr(cnt), nthreads)
+    assert used > 0
+    return out, cnt
 
 
 def ssim_wxh(bd, a, a_off, sa, b, b_off, sb, width, height):

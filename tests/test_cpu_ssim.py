@@ -93,3 +93,20 @@ def test_ssim_encoder_bands():
     assert tuple(b[0]) == (2, 10) and tuple(b[1]) == (6, 22) and tuple(b[-1]) == (1062, 18)
     s = x.ssim_encoder_bands(68, 1080, [(0, 34), (34, 68)])
     assert len(s) == 68 and tuple(s[33]) == (518, 26) and tuple(s[34]) == (546, 10)
+
+
+def test_ssim_bands_mt_matches_per_band(oracle):
+    """cpubench.c's threaded band driver (bench.py's CPU SSIM anchor) returns each band's
+    x264_pixel_ssim_wxh exactly"""
+    import conftest
+    conftest.load_package()
+    from x264hip import synth, ssim_encoder_bands
+    W, H = 256, 128
+    planes, stride, origin = synth.make_sequence(2, W, H, 8)
+    bands = ssim_encoder_bands(H // 16, H)
+    a, b = planes[1].ravel(), planes[0].ravel()
+    got, cnt = oracle.ssim_bands_mt(a, origin + 2, stride, b, origin + 2, stride, W - 2, bands, 3)
+    for k, (y, h) in enumerate(bands):
+        want, wc = oracle.ssim_wxh(8, a, origin + 2 + int(y) * stride, stride, b, origin + 2 + int(y) * stride, stride,
+                                   W - 2, int(h))
+        assert got[k] == want and cnt[k] == wc

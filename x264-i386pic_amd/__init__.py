@@ -33,7 +33,7 @@ __all__ = [
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # X264HIP_LIBRARY: an alternative in-tree build of the same library (A/B timing of two
-# builds of one kernel, tools/gpu_ab.sh); the default is the package's own build
+# builds of one kernel, tools/lib_ab.py); the default is the package's own build
 LIB_PATH = os.environ.get("X264HIP_LIBRARY") or os.path.join(_HERE, "libx264hip.so")
 
 # reference common/pixel.h:37-59

@@ -524,7 +524,7 @@ __device__ __forceinline__ void load16( const typename PT<BD>::pixel *p, uint32_
 // reads 8 pixels per row and transforms two 4x4 blocks, stages them in LDS so the strip's
 // coefficients leave as contiguous 16-byte stores (0.62-0.71 of HBM against 0.50-0.52 for
 // the 16-MB strip with a lane per 4-pixel column, and a lane per (MB, band) of a 16-MB
-// strip in between; tools/dq_variants.py).
+// strip in between: a round-3 A/B whose driver was removed with the losing kernels).
 template <int BD, bool NT = false>
 __global__ __launch_bounds__( 256 ) void mb_dct_quant_halfband_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs,

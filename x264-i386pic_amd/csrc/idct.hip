@@ -1178,7 +1178,7 @@ hipError_t launch_mb_recon( int transform, const typename PT<BD>::dctcoef *dct, 
         return hipSuccess;
     if( transform != 4 && transform != 8 )
         return hipErrorInvalidValue;
-    // 8 bit: block pairs for transform 4 (0.55 vs 0.43 of HBM, tools/recon_variants.py) and
+    // 8 bit: block pairs for transform 4 (0.55 vs 0.43 of HBM in a round-3 A/B, driver since removed) and
     // the packed int16-pair kernel for transform 8; 10 bit: one lane per block (0.68 vs 0.58
     // for the pairs).
     // Sector alignment of the stores: with row and frame strides multiples of 64 bytes, every

@@ -975,7 +975,8 @@ hipError_t launch_subpel_cmp( int op, int i_pixel, const typename PT<BD>::pixel 
     if( n <= 0 )
         return hipSuccess;
     dim3 blk( 256 ), g( (n + 255) / 256 );
-    // the row loads (tools/subpel_variants.py, 4.7 M 8x8 SATD candidates of bench.py's list):
+    // the row loads (a round-2 A/B over 4.7 M 8x8 SATD candidates of bench.py's list; the A/B driver was removed
+    // with the losing variants):
     // unaligned multi-dword loads at 8 bit (0.101 ms against 0.115 for dword-aligned loads +
     // alignbyte, and 0.129 for the first dwordx2 + dword kernel), dword-aligned loads +
     // alignbyte at 10 bit (0.186 against 0.193; 0.178 against 0.276 on block-major lists)
