@@ -1080,6 +1080,9 @@ def rates_refine(x, a, world, mbw, mbh, F):
     res.update(rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes, ext, cm, cm_d, span))
     res.update(rates_search_ref3(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes, (nvd, co, cs), cm_d,
                                  span))
+    # planes hold frames 0 .. F-1 (the references of rates_refine's pairs); list 1 of B frame k+1
+    # is frame k+2 <= F-1
+    res.update(rates_bidir(x, a, world, mbw, mbh, F - 1, dev, stride, origin, fstride, planes, cm_d, span))
     del hv, planes, dev, nvd
     return res
 
@@ -1149,6 +1152,52 @@ def rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes,
                     leg + "_candidates_per_s": world * a.steps * cands / wall,
                     leg + "_absdiff_frac": cands * px / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF,
                     leg + "_mv_found_frac": ((out[:, 1] == 13) & (out[:, 2] == 10)).float().mean().item()})
+    return res
+
+
+def rates_bidir(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes, cm_d, span):
+    """x264_me_refine_bidir_satd (me.c:994-1183) over every 16x16 MB (bidir16_*) and every 8x8
+    partition (bidir8_*) of F B frames of rates_refine's quarter-pel sequence: frame k+1 between
+    list 0 = frame k and list 1 = frame k+2 (true motion +(13, 10) and -(13, 10) qpel), starting
+    from the true mvs +- 4 qpel (the list searches' winners stand-in), mvps +- 8, i_weight 32
+    (the default without weighted bipred) on half the partitions and 24 on the rest, SATD mbcmp.
+    Rates in partitions/s; the pairs the reference scores (mbcmp calls counted by the kernel)
+    give the absdiff-equivalent work."""
+    if F < 2:
+        return {}
+    Fb = F - 1
+    res = {"bidir_workload": "rates_refine's sequence, B frame k+1 between frames k and k+2, starts true mv +- 4 "
+                             "qpel, i_weight 32 / 24, SATD"}
+    for leg, i_pixel in (("bidir16", 0), ("bidir8", 3)):
+        pos, par, _ = search_params(mbw, mbh, Fb, i_pixel, seed=11)
+        n = len(pos)
+        rs = np.random.default_rng(12)
+        bp = np.zeros((n, 12), np.int16)
+        bp[:, 0], bp[:, 1] = 13 + rs.integers(-4, 5, n), 10 + rs.integers(-4, 5, n)
+        bp[:, 2], bp[:, 3] = -13 + rs.integers(-4, 5, n), -10 + rs.integers(-4, 5, n)
+        bp[:, 4], bp[:, 5] = 13 + rs.integers(-8, 9, n), 10 + rs.integers(-8, 9, n)
+        bp[:, 6], bp[:, 7] = -13 + rs.integers(-8, 9, n), -10 + rs.integers(-8, 9, n)
+        bp[:, 8:12] = par[:, 6:10]
+        wt = np.where(rs.random(n) < 0.5, 32, 24).astype(np.int32)
+        pos_d, bp_d, wt_d = (torch.from_numpy(v).cuda() for v in (pos, bp, wt))
+        out = torch.empty((n, 4), dtype=torch.int32, device="cuda")
+        ne = torch.empty(n, dtype=torch.int32, device="cuda")
+        l0 = [pl[0:Fb] for pl in planes]
+        l1 = [pl[2:Fb + 2] for pl in planes]
+
+        def step(i_pixel=i_pixel, pos_d=pos_d, bp_d=bp_d, wt_d=wt_d, out=out, ne=ne, l0=l0, l1=l1):
+            x.me_refine_bidir(dev[1:Fb + 1], origin, stride, l0, l1, origin, stride, i_pixel, pos_d, bp_d, wt_d,
+                              (cm_d, span), out=out, nevals=ne, fenc_frame_stride=fstride, ref_frame_stride=fstride)
+        wall, ev_ms = timed(step, a.steps, a.warmup, world, graph=True)
+        calls = int((ne & 0xFFFF).sum().item())
+        passes = int((ne >> 16).sum().item())
+        px = 256 if i_pixel == 0 else 64
+        res.update({leg + "_partitions_per_s": world * a.steps * n / wall, leg + "_launch_ms": ev_ms,
+                    leg + "_partitions_per_launch": n, leg + "_calls_per_part": calls / n,
+                    leg + "_passes_per_part": passes / n,
+                    leg + "_pairs_per_s": world * a.steps * calls / wall,
+                    leg + "_found_frac": ((out[:, 0] == 13) & (out[:, 1] == 10) & (out[:, 2] == -13) &
+                                          (out[:, 3] == -10)).float().mean().item()})
     return res
 
 

@@ -932,6 +932,31 @@ int x264hip_##BD##_me_search_ref( const pixel *fenc, intptr_t fenc_stride,      
                                   const uint16_t *cost_mv, int n, int32_t *out,                 \
                                   int32_t *nevals, const x264hip_refine_ext_t *ext,             \
                                   void *stream );                                               \
+/* x264_me_refine_bidir_satd (reference encoder/me.c:994-1183, rd = 0) for n bipred partitions   \
+ * of size i_pixel (16x16 .. 8x8) -- the 4-D diamond over (mv0, mv1) that refine_bidir runs on   \
+ * every B_BI_BI / D_BI_8x8 partition at subme >= 5 (analyse.c:2692-2730): up to 8 passes over   \
+ * dia4d's 33 pairs, a pair's visited bit (coordinates mod 8) skipping it in later passes, each   \
+ * pair scored as mc.avg[i_pixel]( list 0 get_ref, list 1 get_ref, i_weight ) (unweighted          \
+ * references; i_weight 32 the rounding average, else the implicit-weight average, mc.c:49-99)   \
+ * by mbcmp (SATD when mbcmp_satd, i.e. subme > 1, else SAD) plus the four mv costs.  The        \
+ * early return when a mv lies within 8 qpel of the spel limits.  l0* / l1*: the list 0 / list 1  \
+ * references' F, H, V, C planes at pixel (0,0) of frame 0 (common stride and frame stride;       \
+ * pos's frame index steps both and fenc's).  pos[3*i] = { frame, x, y }; par[12*i] = { m0 mv x,  \
+ * y, m1 mv x, y, m0 mvp x, y, m1 mvp x, y, mv_min_spel x, y, mv_max_spel x, y }; weight[i] =       \
+ * i_weight (h->mb.bipred_weight).  out[4*i] = { m0 mv x, y, m1 mv x, y } (16-byte aligned);       \
+ * cost (or NULL) = the last bcost (internal in the reference; 1 << 28 after the early return);    \
+ * nevals (or NULL) = mbcmp calls | passes << 16. */                                               \
+int x264hip_##BD##_me_refine_bidir_satd( const pixel *fenc, intptr_t fenc_stride,                \
+                                         intptr_t fenc_frame_stride, const pixel *l0_fpel,      \
+                                         const pixel *l0_hpel_h, const pixel *l0_hpel_v,        \
+                                         const pixel *l0_hpel_c, const pixel *l1_fpel,          \
+                                         const pixel *l1_hpel_h, const pixel *l1_hpel_v,        \
+                                         const pixel *l1_hpel_c, intptr_t ref_stride,           \
+                                         intptr_t ref_frame_stride, int i_pixel,                \
+                                         int mbcmp_satd, const int32_t *pos,                    \
+                                         const int16_t *par, const int32_t *weight,             \
+                                         const uint16_t *cost_mv, int n, int32_t *out,          \
+                                         int32_t *cost, int32_t *nevals, void *stream );        \
 /* me_search_ref with the multi-reference early exit, x264_me_search_ref( ..., p_halfpel_thresh ) \
  * (reference me.c:931-944 inside refine_subpel; x264's default ref = 3 with b_early_terminate,  \
  * common/base.c:384, encoder/analyse.c:303, 1260-1261): halfpel_thresh = int32 [n], partition i's \

@@ -2373,6 +2373,103 @@ void FN(me_search_ref)( const pixel *fenc, intptr_t fs, const pixel *const plane
                               n, out, nevals, ext, fenc_c, fcs, ref_c, rcs, NULL, NULL );
 }
 
+/* x264_me_refine_bidir_satd (reference encoder/me.c:994-1183 with rd = 0) for a list of bipred
+ * partitions of one frame: up to 8 passes over the 33 (mv0, mv1) pairs of dia4d around the
+ * current pair, skipping pairs whose visited bit (m0x&7, m0y&7, m1x&7, m1y&7) an earlier pass
+ * set, each scored as mc.avg[i_pixel] of the two lists' get_ref blocks (unweighted references,
+ * x264_weight_none; i_weight 32: the rounding average, else pixel_avg_weight_wxh, mc.c:49-99)
+ * by mbcmp (satd when `satd`, else sad) plus the four mv costs; COPY2_IF_LT in j order, then a
+ * move by dia4d[bestj] or the end.  The early return when either mv lies within 8 qpel of
+ * mv_min_spel / mv_max_spel (:1077-1081).  planes0 / planes1: list 0 / 1 reference F, H, V, C at
+ * pixel (0,0); pos[2*i] = the partition's top-left; par[12*i] = { m0 mv x, y, m1 mv x, y, m0 mvp
+ * x, y, m1 mvp x, y, mv_min_spel x, y, mv_max_spel x, y }; weight[i] = i_weight.  out[4*i] =
+ * { m0 mv x, y, m1 mv x, y }; cost[i] (or NULL) = the final bcost (COST_MAX after the early
+ * return; the reference keeps it internal); nevals[i] (or NULL) = mbcmp calls | passes << 16. */
+void FN(me_refine_bidir)( const pixel *fenc, intptr_t fs, const pixel *const planes0[4],
+                          const pixel *const planes1[4], intptr_t rs, int i_pixel, int satd, const int32_t *pos,
+                          const int16_t *par, const int32_t *weight, const uint16_t *cost_mv, int n, int32_t *out,
+                          int32_t *cost, int32_t *nevals )
+{
+    static const int8_t dia4d[33][4] = {                                                        /* me.c:1064-1075 */
+        {0,0,0,0},
+        {0,0,0,1}, {0,0,0,-1}, {0,0,1,0}, {0,0,-1,0},
+        {0,1,0,0}, {0,-1,0,0}, {1,0,0,0}, {-1,0,0,0},
+        {0,0,1,1}, {0,0,-1,-1},{0,1,1,0}, {0,-1,-1,0},
+        {1,1,0,0}, {-1,-1,0,0},{1,0,0,1}, {-1,0,0,-1},
+        {0,1,0,1}, {0,-1,0,-1},{1,0,1,0}, {-1,0,-1,0},
+        {0,0,-1,1},{0,0,1,-1}, {0,-1,1,0},{0,1,-1,0},
+        {-1,1,0,0},{1,-1,0,0}, {1,0,0,-1},{-1,0,0,1},
+        {0,-1,0,1},{0,1,0,-1}, {-1,0,1,0},{1,0,-1,0},
+    };
+    const int bw = pixel_w[i_pixel], bh = pixel_h[i_pixel];
+    for( int i = 0; i < n; i++ )
+    {
+        const int bx = pos[2*i], by = pos[2*i+1];
+        const int16_t *p = par + 12 * i;
+        const pixel *f = fenc + by * fs + bx;
+        const pixel *q0[4], *q1[4];
+        for( int k = 0; k < 4; k++ )
+        {
+            q0[k] = planes0[k] + by * rs + bx;
+            q1[k] = planes1[k] + by * rs + bx;
+        }
+        int bm0x = p[0], bm0y = p[1], bm1x = p[2], bm1y = p[3];
+        const uint16_t *c0x = cost_mv - p[4], *c0y = cost_mv - p[5], *c1x = cost_mv - p[6], *c1y = cost_mv - p[7];
+        const int minx = p[8], miny = p[9], maxx = p[10], maxy = p[11];
+        const int w1 = weight[i], w2 = 64 - w1;
+        int bcost = 1 << 28, ncalls = 0, npass = 0;
+        uint8_t visited[8][8][8];
+        if( !(bm0y < miny + 8 || bm1y < miny + 8 || bm0y > maxy - 8 || bm1y > maxy - 8 ||
+              bm0x < minx + 8 || bm1x < minx + 8 || bm0x > maxx - 8 || bm1x > maxx - 8) )
+        {
+            memset( visited, 0, sizeof(visited) );
+            for( int pass = 0; pass < 8; pass++ )
+            {
+                int bestj = 0;
+                npass++;
+                for( int j = !!pass; j < 33; j++ )
+                {
+                    const int m0x = dia4d[j][0] + bm0x, m0y = dia4d[j][1] + bm0y;
+                    const int m1x = dia4d[j][2] + bm1x, m1y = dia4d[j][3] + bm1y;
+                    if( pass && (visited[m0x & 7][m0y & 7][m1x & 7] & (1 << (m1y & 7))) )
+                        continue;
+                    visited[m0x & 7][m0y & 7][m1x & 7] |= 1 << (m1y & 7);
+                    pixel b0[16 * 16], b1[16 * 16], avg[16 * 16];
+                    intptr_t s0 = 16, s1 = 16;
+                    const pixel *r0 = FN(get_ref)( b0, &s0, q0, rs, m0x, m0y, bw, bh );
+                    const pixel *r1 = FN(get_ref)( b1, &s1, q1, rs, m1x, m1y, bw, bh );
+                    for( int y = 0; y < bh; y++ )
+                        for( int x = 0; x < bw; x++ )
+                            avg[16 * y + x] = w1 == 32 ? (r0[y * s0 + x] + r1[y * s1 + x] + 1) >> 1
+                                                       : clip_pixel( (r0[y * s0 + x] * w1 + r1[y * s1 + x] * w2 + 32) >> 6 );
+                    const int c = (satd ? FN(satd)( i_pixel, f, fs, avg, 16 ) : FN(sad)( i_pixel, f, fs, avg, 16 ))
+                                + c0x[m0x] + c0y[m0y] + c1x[m1x] + c1y[m1y];
+                    ncalls++;
+                    if( c < bcost )
+                    {
+                        bcost = c;
+                        bestj = j;
+                    }
+                }
+                if( !bestj )
+                    break;
+                bm0x += dia4d[bestj][0];
+                bm0y += dia4d[bestj][1];
+                bm1x += dia4d[bestj][2];
+                bm1y += dia4d[bestj][3];
+            }
+        }
+        out[4*i] = bm0x;
+        out[4*i+1] = bm0y;
+        out[4*i+2] = bm1x;
+        out[4*i+3] = bm1y;
+        if( cost )
+            cost[i] = bcost;
+        if( nevals )
+            nevals[i] = ncalls | (npass << 16);
+    }
+}
+
 /* TESA integer-pel search of x264_me_search_ref for PIXEL_16x16, restated from
  * reference encoder/me.c:618-748 (X264_ME_TESA): enc_dc from sad_x4 against
  * x264_zero (:643-645), per row the ycost skip, ads4 with threshold bsad*17>>4

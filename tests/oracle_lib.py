@@ -80,6 +80,7 @@ for _bd in (8, 10):
                                     _P, _P, _P, _P, _IP, _P, _IP])
     _f(_bd, "me_search_ref_thresh", [_P, _IP, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P,
                                      C.c_int, _P, _P, _P, _P, _IP, _P, _IP, _P, _P])
+    _f(_bd, "me_refine_bidir", [_P, _IP, _P, _P, _IP, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P, _P, _P])
     _f(_bd, "me_refine_qpel_refdupe", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, C.c_int, _P, _P,
                                        _P, _P, _IP, _P, _IP, _P, _P])
     _f(_bd, "frame_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int])
@@ -417,6 +418,27 @@ def me_search_ref(bd, fenc, f_origin, fs, planes, fw, r_origin, rs, i_pixel, me_
         rcst = None if ref_cost is None else np.ascontiguousarray(ref_cost, np.int32)
         getattr(_L, f"oracle{bd}_me_search_ref_thresh")(*args, _addr(thresh), None if rcst is None else _addr(rcst))
     return out, ne
+
+
+def me_refine_bidir(bd, fenc, f_origin, fs, planes0, planes1, r_origin, rs, i_pixel, satd, pos_xy, par, weight,
+                    cost_mv, c0):
+    """one frame: x264_me_refine_bidir_satd (me.c:994-1183) of the partitions at pos_xy int32 [n, 2];
+    planes0 / planes1 = F, H, V, C of the list 0 / 1 references; par int16 [n, 12] = (m0 mv x, y,
+    m1 mv x, y, m0 mvp x, y, m1 mvp x, y, mv_min_spel x, y, mv_max_spel x, y); weight int32 [n].
+    Returns (out int32 [n, 4] = m0 mv, m1 mv; cost int32 [n]; counts int32 [n] = calls | passes << 16)."""
+    n = len(pos_xy)
+    pos = np.ascontiguousarray(pos_xy, np.int32)
+    p = np.ascontiguousarray(par, np.int16)
+    w = np.ascontiguousarray(weight, np.int32)
+    out = np.zeros((n, 4), np.int32)
+    cost = np.zeros(n, np.int32)
+    ne = np.zeros(n, np.int32)
+    a0 = (C.c_void_p * 4)(*[_addr(q, r_origin).value for q in planes0])
+    a1 = (C.c_void_p * 4)(*[_addr(q, r_origin).value for q in planes1])
+    getattr(_L, f"oracle{bd}_me_refine_bidir")(_addr(fenc, f_origin), fs, a0, a1, rs, i_pixel, int(bool(satd)),
+                                              _addr(pos), _addr(p), _addr(w), _addr(cost_mv, c0), n, _addr(out),
+                                              _addr(cost), _addr(ne))
+    return out, cost, ne
 
 
 def me_refine_qpel_refdupe(bd, fenc, f_origin, fs, planes, r_origin, rs, i_pixel, subme, pos_xy, par, cost, cost_mv,

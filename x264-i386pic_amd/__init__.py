@@ -1345,6 +1345,33 @@ def me_search_ref(fenc, fenc_origin, fenc_stride, fpel_w, planes, ref_origin, re
     return out
 
 
+def me_refine_bidir(fenc, fenc_origin, fenc_stride, planes0, planes1, ref_origin, ref_stride, i_pixel, pos, par,
+                    weight, cost_mv_center, satd=True, out=None, cost=None, nevals=None, fenc_frame_stride=None,
+                    ref_frame_stride=None):
+    """x264_me_refine_bidir_satd (encoder/me.c:994-1183) of n bipred partitions
+    (x264hip_*_me_refine_bidir_satd): planes0 / planes1 = [F, H, V, C] of the list 0 / 1
+    references, pos int32 [n, 3] = (frame, x, y), par int16 [n, 12] = (m0 mv x, y, m1 mv x, y,
+    m0 mvp x, y, m1 mvp x, y, mv_min_spel x, y, mv_max_spel x, y), weight int32 [n].  Returns
+    int32 [n, 4] = (m0 mv x, y, m1 mv x, y); cost / nevals: optional int32 [n] outputs."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = pos.shape[0]
+    if out is None:
+        out = torch.empty((n, 4), dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else _frame_stride(*planes0, *planes1)
+    cm, c0 = cost_mv_center
+    name = f"x264hip_{bd}_me_refine_bidir_satd"
+    fn = getattr(lib(), name)
+    fn.argtypes = [_P, _IP, _IP] + [_P] * 8 + [_IP, _IP, _c.c_int, _c.c_int, _P, _P, _P, _P, _c.c_int, _P, _P, _P, _P]
+    fn.restype = _c.c_int
+    _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, *[_ptr(p, ref_origin) for p in planes0],
+           *[_ptr(p, ref_origin) for p in planes1], ref_stride, rfs, i_pixel, int(bool(satd)), _ptr(pos), _ptr(par),
+           _ptr(weight), _ptr(cm, c0), n, _ptr(out), _ptr(cost) if cost is not None else None,
+           _ptr(nevals) if nevals is not None else None, _stream()), name)
+    return out
+
+
 def me_refine_qpel_refdupe(fenc, fenc_origin, fenc_stride, planes, ref_origin, ref_stride, i_pixel, subme, pos, par,
                            init_cost, cost_mv_center, halfpel_thresh=None, ref_cost=None, fpel_satd=False, out=None,
                            fenc_frame_stride=None, ref_frame_stride=None, nevals=None, ext=None):

@@ -1946,6 +1946,22 @@ extern "C" const char *x264hip_backend_banner( void )
                                                   me_range, pos, par, mvc, cost_mv, n, out, nevals, nullptr,         \
                                                   nullptr, ext, (hipStream_t)stream ), "me_search_ref" );            \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_refine_bidir_satd(                                                           \
+        const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs, const PT<BD>::pixel *l0f, const PT<BD>::pixel *l0h,     \
+        const PT<BD>::pixel *l0v, const PT<BD>::pixel *l0c, const PT<BD>::pixel *l1f, const PT<BD>::pixel *l1h,       \
+        const PT<BD>::pixel *l1v, const PT<BD>::pixel *l1c, intptr_t rs, intptr_t rfs, int i_pixel, int mbcmp_satd,   \
+        const int32_t *pos, const int16_t *par, const int32_t *weight, const uint16_t *cost_mv, int n, int32_t *out,  \
+        int32_t *cost, int32_t *nevals, void *stream )                                                               \
+    {                                                                                                                \
+        if( i_pixel < 0 || i_pixel > 3 || n < 0 ||                                                                   \
+            ( n > 0 && ( !fenc || !l0f || !l0h || !l0v || !l0c || !l1f || !l1h || !l1v || !l1c || !pos || !par ||     \
+                         !weight || !cost_mv || !out ) ) )                                                           \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *p0[4] = { l0f, l0h, l0v, l0c }, *p1[4] = { l1f, l1h, l1v, l1c };                        \
+        return map_err( launch_me_refine_bidir<BD>( fenc, fs, ffs, p0, p1, rs, rfs, i_pixel, mbcmp_satd, pos, par,   \
+                                                    weight, cost_mv, n, out, cost, nevals, (hipStream_t)stream ),    \
+                        "me_refine_bidir_satd" );                                                                    \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_me_search_ref_thresh( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,       \
                                                         const PT<BD>::pixel *fw, const PT<BD>::pixel *p0,            \
                                                         const PT<BD>::pixel *p1, const PT<BD>::pixel *p2,            \

@@ -401,6 +401,13 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
                                  int n, int32_t *out, int32_t *nevals, int32_t *thr, const int32_t *rcost,
                                  const x264hip_refine_ext_t *ext, hipStream_t stream );
 template <int BD>
+hipError_t launch_me_refine_bidir( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                   const typename PT<BD>::pixel *const planes0[4],
+                                   const typename PT<BD>::pixel *const planes1[4], intptr_t rs, intptr_t rfs,
+                                   int i_pixel, int satd, const int32_t *pos, const int16_t *par, const int32_t *weight,
+                                   const uint16_t *cost_mv, int n, int32_t *out, int32_t *cost, int32_t *nevals,
+                                   hipStream_t stream );
+template <int BD>
 hipError_t launch_me_esa_argmin( const typename PT<BD>::sadt *table, int R, int nmb, int me_range,
                                  const int16_t *origin, const int16_t *par, const int32_t *init_cost,
                                  const uint16_t *cost_mv, int32_t *out, hipStream_t stream );

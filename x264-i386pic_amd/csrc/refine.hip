@@ -1327,6 +1327,245 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
     }
     return e;
 }
+// ---------------------------------------------------------------------------------------------
+// x264_me_refine_bidir_satd (reference encoder/me.c:994-1183, rd = 0) for a batch of bipred
+// partitions.  A segment of 8 groups x NT tile lanes per partition (16x16: a wave; 8x8: 16
+// lanes); a pass's 33 (or 32) dia4d pairs run as rounds of eight, group g scoring pair 8r + g:
+// each lane rebuilds both lists' get_ref blocks of its 8x4 tile (mc.c:221-249, unweighted),
+// averages them as mc.avg[i_pixel] does (the rounding average at i_weight 32, else
+// pixel_avg_weight_wxh, mc.c:77-99) and scores the tile against fenc with mbcmp; the groups meet
+// by DPP and shuffles and every lane replays COPY2_IF_LT in j order.  The visited bits (one per
+// (m0x, m0y, m1x, m1y) mod 8, 4096 per partition) sit in LDS: a pass never revisits a pair of
+// its own (dia4d's offsets are within +-1, so two pairs of one pass never alias mod 8), so a
+// round reads the bits before its own are set.
+__constant__ uint8_t c_dia4d[33] = {               // me.c:1064-1075, (d + 1) in 2-bit fields
+    0x55, 0x95, 0x15, 0x65, 0x45, 0x59, 0x51, 0x56, 0x54, 0xA5, 0x05, 0x69, 0x41, 0x5A, 0x50, 0x96, 0x14,
+    0x99, 0x11, 0x66, 0x44, 0x85, 0x25, 0x61, 0x49, 0x58, 0x52, 0x16, 0x94, 0x91, 0x19, 0x64, 0x46 };
+__device__ __forceinline__ int dia4d( int j, int c ) { return (int)((c_dia4d[j] >> (2 * c)) & 3) - 1; }
+
+// the lane's 8x4 tile of get_ref( mvx, mvy ) (unweighted)
+template <int BD>
+__device__ __forceinline__ void ref_tile( const typename PT<BD>::pixel *q0, const typename PT<BD>::pixel *q1,
+                                          const typename PT<BD>::pixel *q2, const typename PT<BD>::pixel *q3,
+                                          intptr_t rs, int mvx, int mvy, uint32_t (&r1)[4][8 / PT<BD>::PPD] )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int HDW = 8 / PT<BD>::PPD;
+    const int idx = ((mvy & 3) << 2) + (mvx & 3);
+    const intptr_t off = (intptr_t)(mvy >> 2) * rs + (mvx >> 2);
+    constexpr uint32_t k0 = pack_fields( c_ref0, 2 ), k1 = pack_fields( c_ref1, 2 );
+    const int i0 = field( k0, 2, idx ), i1 = field( k1, 2, idx );
+    const pixel *s1 = (i0 == 0 ? q0 : i0 == 1 ? q1 : i0 == 2 ? q2 : q3) + off + ((mvy & 3) == 3) * rs;
+    const pixel *s2 = (i1 == 0 ? q0 : i1 == 1 ? q1 : i1 == 2 ? q2 : q3) + off + ((mvx & 3) == 3);
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+        load_al_pad<HDW>( s1 + y * rs, r1[y] );
+    if( idx & 5 )
+    {
+        uint32_t r2[4][HDW];
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+            load_al_pad<HDW>( s2 + y * rs, r2[y] );
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+#pragma unroll
+            for( int k = 0; k < HDW; k++ )
+                r1[y][k] = avg_round<BD>( r1[y][k], r2[y][k] );
+    }
+}
+
+template <int BD, int IPIX, bool SATD>
+__global__ __launch_bounds__( 256 ) void me_refine_bidir_kernel(
+    const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs, const typename PT<BD>::pixel *a0,
+    const typename PT<BD>::pixel *a1, const typename PT<BD>::pixel *a2, const typename PT<BD>::pixel *a3,
+    const typename PT<BD>::pixel *b0, const typename PT<BD>::pixel *b1, const typename PT<BD>::pixel *b2,
+    const typename PT<BD>::pixel *b3, intptr_t rs, intptr_t rfs, int n, const int32_t *__restrict__ pos,
+    const int16_t *__restrict__ par, const int32_t *__restrict__ weight, const uint16_t *__restrict__ cost_mv,
+    int32_t *__restrict__ out, int32_t *__restrict__ cost, int32_t *__restrict__ nevals )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int HDW = 8 / PT<BD>::PPD, PPD = PT<BD>::PPD;
+    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TX = BW / 8, NT = TX * (BH / 4);
+    constexpr int SL = 8 * NT, SH = NT == 8 ? 6 : NT == 4 ? 5 : 4;
+    constexpr int COST_MAX = 1 << 28, NONE = 0x7fffffff;
+    __shared__ uint32_t s_vis[256 / SL][128];
+    const int lane = (int)(threadIdx.x & 63);
+    const int sbase = lane & (64 - SL), seg = (int)threadIdx.x >> SH;
+    const int g = (lane / NT) & 7, u = lane & (NT - 1);
+    const int64_t jo = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> SH;
+    const bool live = jo < n;
+    const int64_t j = live ? jo : n - 1;
+    const int ux = 8 * (u % TX), uy = 4 * (u / TX);
+    const int f = pos[3 * j], bx = pos[3 * j + 1], by = pos[3 * j + 2];
+
+    uint32_t fa[4][HDW];
+    const pixel *fe = fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux;
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+        load_row_u<HDW>( fe + y * fs, fa[y] );
+    const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
+    const pixel *const p0 = a0 + qo, *const p1 = a1 + qo, *const p2 = a2 + qo, *const p3 = a3 + qo;
+    const pixel *const r0 = b0 + qo, *const r1 = b1 + qo, *const r2 = b2 + qo, *const r3 = b3 + qo;
+
+    const int16_t *p = par + 12 * j;
+    int bm0x = p[0], bm0y = p[1], bm1x = p[2], bm1y = p[3];
+    const uint16_t *c0x = cost_mv - p[4], *c0y = cost_mv - p[5], *c1x = cost_mv - p[6], *c1y = cost_mv - p[7];
+    const int minx = p[8], miny = p[9], maxx = p[10], maxy = p[11];
+    const int w1 = weight[j], w2 = 64 - w1;
+    int bcost = COST_MAX, ncalls = 0, npass = 0;
+    bool act = !(bm0y < miny + 8 || bm1y < miny + 8 || bm0y > maxy - 8 || bm1y > maxy - 8 || bm0x < minx + 8 ||
+                 bm1x < minx + 8 || bm0x > maxx - 8 || bm1x > maxx - 8);
+    uint32_t *vis = s_vis[seg];
+#pragma unroll
+    for( int i = lane - sbase; i < 128; i += SL )
+        vis[i] = 0;
+    for( int pass = 0; pass < 8; pass++ )
+    {
+        if( !__any( act ) )
+            break;
+        int bestj = 0;
+        if( act )
+            npass++;
+        const int j0 = pass ? 1 : 0;
+        for( int r = 0; r < (pass ? 4 : 5); r++ )
+        {
+            const int jj = j0 + 8 * r + g;                // this group's pair
+            const int jc = jj < 33 ? jj : 0;
+            const int m0x = bm0x + dia4d( jc, 0 ), m0y = bm0y + dia4d( jc, 1 );
+            const int m1x = bm1x + dia4d( jc, 2 ), m1y = bm1y + dia4d( jc, 3 );
+            const int key = ((m0x & 7) << 9) | ((m0y & 7) << 6) | ((m1x & 7) << 3) | (m1y & 7);
+            const bool ok = act && jj < 33 && !(pass && ((vis[key >> 5] >> (key & 31)) & 1));
+            uint32_t v = 0;
+            if( ok )
+            {
+                uint32_t t0[4][HDW], t1[4][HDW];
+                ref_tile<BD>( p0, p1, p2, p3, rs, m0x, m0y, t0 );
+                ref_tile<BD>( r0, r1, r2, r3, rs, m1x, m1y, t1 );
+                if( w1 == 32 )
+                {
+#pragma unroll
+                    for( int y = 0; y < 4; y++ )
+#pragma unroll
+                        for( int k = 0; k < HDW; k++ )
+                            t0[y][k] = avg_round<BD>( t0[y][k], t1[y][k] );
+                }
+                else
+                {
+#pragma unroll
+                    for( int y = 0; y < 4; y++ )
+#pragma unroll
+                        for( int k = 0; k < HDW; k++ )
+                        {
+                            uint32_t o = 0;
+#pragma unroll
+                            for( int e = 0; e < PPD; e++ )
+                                o |= (uint32_t)clip_pix<BD>( (upix<BD>( t0[y][k], e ) * w1 + upix<BD>( t1[y][k], e ) * w2 +
+                                                              32) >> 6 ) << ((32 / PPD) * e);
+                            t0[y][k] = o;
+                        }
+                }
+                if constexpr( SATD )
+                    v = satd8x4_packed<BD>( fa, t0 ) >> 1;
+                else
+                {
+#pragma unroll
+                    for( int y = 0; y < 4; y++ )
+#pragma unroll
+                        for( int k = 0; k < HDW; k++ )
+                            v = sadp<BD>( fa[y][k], t0[y][k], v );
+                }
+                if( u == 0 )
+                {
+                    v += (uint32_t)c0x[m0x] + (uint32_t)c0y[m0y] + (uint32_t)c1x[m1x] + (uint32_t)c1y[m1y];
+                    atomicOr( &vis[key >> 5], 1u << (key & 31) );
+                }
+            }
+            else if( u == 0 )
+                v = NONE;
+            v = group_sum<NT>( v );
+            int c[8];
+#pragma unroll
+            for( int k = 0; k < 8; k++ )
+                c[k] = (int)__shfl( (int)v, sbase + NT * k );
+            if( act )
+            {
+#pragma unroll
+                for( int k = 0; k < 8; k++ )
+                    if( c[k] != NONE )
+                    {
+                        ncalls++;
+                        if( c[k] < bcost )
+                        {
+                            bcost = c[k];
+                            bestj = j0 + 8 * r + k;
+                        }
+                    }
+            }
+        }
+        if( act )
+        {
+            if( !bestj )
+                act = false;
+            else
+            {
+                bm0x += dia4d( bestj, 0 );
+                bm0y += dia4d( bestj, 1 );
+                bm1x += dia4d( bestj, 2 );
+                bm1y += dia4d( bestj, 3 );
+            }
+        }
+    }
+    if( live && lane == sbase )
+    {
+        *(int4 *)(out + 4 * j) = make_int4( bm0x, bm0y, bm1x, bm1y );
+        if( cost )
+            cost[j] = bcost;
+        if( nevals )
+            nevals[j] = ncalls | (npass << 16);
+    }
+}
+
+template <int BD>
+hipError_t launch_me_refine_bidir( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                   const typename PT<BD>::pixel *const planes0[4],
+                                   const typename PT<BD>::pixel *const planes1[4], intptr_t rs, intptr_t rfs,
+                                   int i_pixel, int satd, const int32_t *pos, const int16_t *par, const int32_t *weight,
+                                   const uint16_t *cost_mv, int n, int32_t *out, int32_t *cost, int32_t *nevals,
+                                   hipStream_t stream )
+{
+    if( n <= 0 )
+        return hipSuccess;
+    if( i_pixel < 0 || i_pixel > 3 || ((uintptr_t)out & 15) )
+        return hipErrorInvalidValue;
+    // 8 * (the partition's 8x4 tiles) lanes per partition
+    const int64_t lanes = (int64_t)n * 8 * (pix_w( i_pixel ) / 8) * (pix_h( i_pixel ) / 4);
+    dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
+#define BI_GO( I, S )                                                                                             \
+    hipLaunchKernelGGL( ( me_refine_bidir_kernel<BD, I, S> ), g, blk, 0, stream, fenc, fs, ffs, planes0[0],         \
+                        planes0[1], planes0[2], planes0[3], planes1[0], planes1[1], planes1[2], planes1[3], rs, rfs, \
+                        n, pos, par, weight, cost_mv, out, cost, nevals )
+#define BI_CASE( I )                                                                                              \
+    case I:                                                                                                       \
+        if( satd ) { BI_GO( I, true ); } else { BI_GO( I, false ); }                                              \
+        break;
+    switch( i_pixel )
+    {
+        BI_CASE( 0 ) BI_CASE( 1 ) BI_CASE( 2 ) BI_CASE( 3 )
+        default: return hipErrorInvalidValue;
+    }
+#undef BI_CASE
+#undef BI_GO
+    return hipGetLastError();
+}
+template hipError_t launch_me_refine_bidir<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *const[4],
+                                               const uint8_t *const[4], intptr_t, intptr_t, int, int, const int32_t *,
+                                               const int16_t *, const int32_t *, const uint16_t *, int, int32_t *,
+                                               int32_t *, int32_t *, hipStream_t );
+template hipError_t launch_me_refine_bidir<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *const[4],
+                                                const uint16_t *const[4], intptr_t, intptr_t, int, int, const int32_t *,
+                                                const int16_t *, const int32_t *, const uint16_t *, int, int32_t *,
+                                                int32_t *, int32_t *, hipStream_t );
+
 template hipError_t launch_me_search_ref<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, const uint8_t *const[4],
                                              intptr_t, intptr_t, int, int, int, int, const int32_t *, const int16_t *,
                                              const int16_t *, const uint16_t *, int, int32_t *, int32_t *, int32_t *,
