@@ -851,8 +851,9 @@ int x264hip_##BD##_subpel_qpel9_batch( int op, int i_pixel, const pixel *fenc,  
                                        const int64_t *fenc_off, const int32_t *centre_xy,       \
                                        int n, int32_t *scores, void *stream );                  \
                                                                                                 \
-/* refine_subpel (reference encoder/me.c:865-992) for n partitions of size i_pixel (16x16,    \
- * 16x8, 8x16, 8x8) of n_frames (fenc, ref) pairs: the subpel stage x264_me_search_ref runs      \
+/* refine_subpel (reference encoder/me.c:865-992) for n partitions of size i_pixel (16x16 ..   \
+ * 4x4, PIXEL_16x16 .. PIXEL_4x4 = 0 .. 6) of n_frames (fenc, ref) pairs: the subpel stage      \
+ * x264_me_search_ref runs                                                                      \
  * after its integer search (refine_qpel = 0: subpel_iterations[subme][2..3], me.c:791-797) or   \
  * x264_me_refine_qpel (refine_qpel = 1: [0..1], me.c:801-810) -- the halfpel diamond of         \
  * fpelcmp over get_ref blocks (SAD; SATD when fpel_satd, i.e. TESA, and subme > 1,              \
@@ -909,7 +910,8 @@ int x264hip_##BD##_me_refine_qpel_refdupe( const pixel *fenc, intptr_t fenc_stri
                                            const x264hip_refine_ext_t *ext, void *stream );     \
                                                                                                 \
 /* x264_me_search_ref (reference encoder/me.c:182-798) for n partitions of size i_pixel (16x16 ..  \
- * 8x8) with me_method X264_ME_DIA (0), X264_ME_HEX (1, x264's default, common/base.c:439) or      \
+ * 4x4; UMH on PIXEL_4x4 goes to the hexagon after its predictor diamonds, me.c:438-439) with     \
+ * me_method X264_ME_DIA (0), X264_ME_HEX (1, x264's default, common/base.c:439) or               \
  * X264_ME_UMH (2): the predictor checks over mvp and the mvc list (x264_predictor_clip /          \
  * _roundclip, common/common.h:774-805), the integer search (UMH with its adaptive range), the    \
  * qpel conversion (me.c:774-789), then refine_subpel when subme >= 2 as me_refine_subpel_ex      \

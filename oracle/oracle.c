@@ -1778,8 +1778,8 @@ static void FN(refine_core)( const pixel *fenc, intptr_t fs, const pixel *const 
     const int qpel_iters = kind == 2 ? (subpel_iterations[subme][3] < 2 ? subpel_iterations[subme][3] : 2)
                                      : subpel_iterations[subme][refine_qpel ? 1 : 3];
     const int fsatd = fpel_satd && subme > 1, qsatd = subme > 1;
-    /* me.c:872: every partition here is <= PIXEL_8x8 */
-    const int b_chroma_me = ext && ext[0];
+    /* me.c:872: b_chroma_me && (i_pixel <= PIXEL_8x8 || CHROMA444) */
+    const int b_chroma_me = ext && ext[0] && (i_pixel <= 3 || ext[1] == 3);
     FN(rs_chroma_t) cc = { 0 };
     const int *wt0 = NULL;
     int wbuf[3][3];
@@ -2190,6 +2190,10 @@ void FN(me_search_ref_thresh)( const pixel *fenc, intptr_t fs, const pixel *cons
             SR_DIA1( pmx, pmy );
             if( pmx | pmy )
                 SR_DIA1( 0, 0 );
+            if( i_pixel == 6 )                 /* PIXEL_4x4: goto me_hex2 (me.c:438-439) */
+                hex = 1;
+            else
+            {
             const int ucost2 = bcost;
             if( (bmx | bmy) && ((bmx - pmx) | (bmy - pmy)) )
                 SR_DIA1( bmx, bmy );
@@ -2257,6 +2261,7 @@ void FN(me_search_ref_thresh)( const pixel *fenc, intptr_t fs, const pixel *cons
                 } while( ++i <= i_me_range >> 2 );
                 if( SR_IN( bmx, bmy ) )
                     hex = 1;
+            }
             }
 #undef SR_DIA1
 #undef SR_CROSS

@@ -4,6 +4,11 @@ import numpy as np
 
 # partitions of an MB per i_pixel (16x16, 16x8, 8x16, 8x8): top-left offsets
 PARTS = {0: [(0, 0)], 1: [(0, 0), (0, 8)], 2: [(0, 0), (8, 0)], 3: [(0, 0), (8, 0), (0, 8), (8, 8)]}
+# the sub-8x8 partitions of each 8x8 (PIXEL_8x4 / 4x8 / 4x4, analyse.c:1685-1760)
+_Q = [(0, 0), (8, 0), (0, 8), (8, 8)]
+PARTS[4] = [(qx, qy + dy) for qx, qy in _Q for dy in (0, 4)]
+PARTS[5] = [(qx + dx, qy) for qx, qy in _Q for dx in (0, 4)]
+PARTS[6] = [(qx + dx, qy + dy) for qx, qy in _Q for dy in (0, 4) for dx in (0, 4)]
 
 
 def cost_mv(lam=40, span=8192):

@@ -201,6 +201,8 @@ def search_ref_py(fenc, planes, fw, origin, stride, x, y, i_pixel, par, mvc, cm,
         dia1(pmx, pmy)
         if pmx | pmy:
             dia1(0, 0)
+        if i_pixel == 6:                                     # PIXEL_4x4: goto me_hex2 (me.c:438-439)
+            return _umh_tail_hex(st, fpel, bits, inr, me_range, subme, bpred_cost, bpred_mv, pmv, cmx, cmy, nf)
         ucost2 = st["bcost"]
         if (st["bmx"] | st["bmy"]) and ((st["bmx"] - pmx) | (st["bmy"] - pmy)):
             dia1(st["bmx"], st["bmy"])
@@ -250,6 +252,11 @@ def search_ref_py(fenc, planes, fw, origin, stride, x, y, i_pixel, par, mvc, cm,
                 if i > me_range >> 2:
                     break
             hexs = inr(st["bmx"], st["bmy"])
+    return _umh_tail_hex(st, fpel, bits, inr, me_range, subme, bpred_cost, bpred_mv, pmv, cmx, cmy, nf, hexs)
+
+
+def _umh_tail_hex(st, fpel, bits, inr, me_range, subme, bpred_cost, bpred_mv, pmv, cmx, cmy, nf, hexs=True):
+    """the hexagon + square refine (me.c:344-419) when hexs, then the qpel conversion (me.c:774-789)"""
     if hexs:
         bmx, bmy = st["bmx"], st["bmy"]
 

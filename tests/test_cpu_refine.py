@@ -87,7 +87,7 @@ def refine_py(planes, fenc, origin, stride, x, y, bw, bh, par, cost, cm, c0, sub
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("i_pixel", [0, 1, 2, 3])
+@pytest.mark.parametrize("i_pixel", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("subme,refine_qpel,fpel_satd", [(1, 0, 0), (2, 0, 0), (2, 0, 1), (4, 0, 0), (7, 0, 0),
                                                          (7, 1, 0), (7, 0, 1), (9, 0, 0), (3, 1, 0)])
 def test_refine_oracle_vs_python(oracle, bd, i_pixel, subme, refine_qpel, fpel_satd):

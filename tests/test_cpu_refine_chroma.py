@@ -82,6 +82,8 @@ def refine_chroma_py(cc, x, y, i_pixel, par, cost, cm, c0, subme, refine_qpel, b
     cmx = lambda v: int(cm[c0 + v - mvp[0]])
     cmy = lambda v: int(cm[c0 + v - mvp[1]])
 
+    b_chroma_me = b_chroma_me and (i_pixel <= 3 or cf == 3)          # me.c:872
+
     def satd_cost(mx, my, bcost):
         c = luma(qsatd, mx, my) + cmx(mx) + cmy(my)
         if b_chroma_me and c < bcost:
@@ -142,7 +144,7 @@ def refine_chroma_py(cc, x, y, i_pixel, par, cost, cm, c0, subme, refine_qpel, b
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("cf", [1, 2, 3])
-@pytest.mark.parametrize("i_pixel", [0, 1, 2, 3])
+@pytest.mark.parametrize("i_pixel", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("subme,refine_qpel,b_chroma_me,wsel", [(7, 0, 1, 0), (5, 0, 1, 1), (9, 0, 1, 2),
                                                                 (5, 1, 1, 1), (7, 0, 0, 1)])
 def test_refine_chroma_oracle_vs_python(oracle, bd, cf, i_pixel, subme, refine_qpel, b_chroma_me, wsel):
@@ -163,8 +165,10 @@ def test_refine_chroma_oracle_vs_python(oracle, bd, cf, i_pixel, subme, refine_q
                                     refine_qpel, b_chroma_me, weights)
         assert tuple(got[i]) == want and ne[i] == wn, (i, got[i], want, hex(ne[i]), hex(wn))
         moved += (want[1], want[2]) != (int(par[i, 0]), int(par[i, 1]))
-    if b_chroma_me:
+    if b_chroma_me and (i_pixel <= 3 or cf == 3):            # me.c:872
         assert (ne >> 24).sum() > 0                        # the chroma branch ran
+    elif b_chroma_me:
+        assert not (ne >> 24).any()                        # sub-8x8 at 4:2:0 / 4:2:2: no chroma ME
 
 
 def test_refine_chroma_changes_decisions(oracle):

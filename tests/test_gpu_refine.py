@@ -46,7 +46,7 @@ def _run(hip, oracle, bd, W, H, nframes, i_pixel, subme, refine_qpel, fpel_satd,
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("i_pixel", [0, 1, 2, 3])
+@pytest.mark.parametrize("i_pixel", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("subme", [1, 2, 4, 7, 9])
 @pytest.mark.parametrize("refine_qpel,fpel_satd", [(0, 0), (1, 0), (0, 1)])
 def test_refine_subpel_small(hip, oracle, bd, i_pixel, subme, refine_qpel, fpel_satd):
@@ -58,7 +58,7 @@ def test_refine_subpel_small(hip, oracle, bd, i_pixel, subme, refine_qpel, fpel_
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("i_pixel", [0, 3])
+@pytest.mark.parametrize("i_pixel", [0, 3, 4, 6])
 def test_refine_subpel_1080p(hip, oracle, bd, i_pixel):
     """every partition of a 1920x1088 frame pair at subme 7 (x264's default preset), x264_me_search_ref's
     iterations (two hpel, two qpel)"""
@@ -70,7 +70,7 @@ def test_refine_subpel_args(hip):
     p = torch.zeros((2, 160, 256), dtype=torch.uint8, device="cuda")
     pos = torch.zeros((1, 3), dtype=torch.int32, device="cuda")
     par = torch.zeros((1, 8), dtype=torch.int16, device="cuda")
-    for i_pixel, subme in ((4, 7), (0, 0), (0, 12)):
+    for i_pixel, subme in ((7, 7), (0, 0), (0, 12)):
         with pytest.raises(RuntimeError):
             hip.me_refine_subpel(p, 32 * 256 + 32, 256, [p, p, p, p], 32 * 256 + 32, 256, i_pixel, subme, pos, par,
                                  t[:1], (t.view(torch.int16), 0))

@@ -63,7 +63,7 @@ W_NONE, W_FADE, W_D0 = (None, None, None), rc.FADE_WEIGHTS, rc.FADE_WEIGHTS_DENO
 
 @pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("cf", [1, 2, 3])
-@pytest.mark.parametrize("i_pixel", [0, 1, 2, 3])
+@pytest.mark.parametrize("i_pixel", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("subme,refine_qpel,b_chroma_me,wsel,fpel_satd", [
     (7, 0, 1, 0, 0), (5, 0, 1, 1, 0), (9, 0, 1, 2, 0), (5, 1, 1, 1, 0), (7, 0, 0, 1, 0), (7, 0, 1, 0, 1)])
 def test_refine_chroma_small(hip, oracle, bd, cf, i_pixel, subme, refine_qpel, b_chroma_me, wsel, fpel_satd):
@@ -71,14 +71,16 @@ def test_refine_chroma_small(hip, oracle, bd, cf, i_pixel, subme, refine_qpel, b
     got, par, ne = _run(hip, oracle, bd, cf, 96, 64, 2, i_pixel, subme, refine_qpel, b_chroma_me, weights,
                         fpel_satd=fpel_satd, seed=bd + 3 * i_pixel + cf,
                         cost_scale=16 if refine_qpel else 1)
-    if b_chroma_me:
+    if b_chroma_me and (i_pixel <= 3 or cf == 3):           # me.c:872
         assert (ne >> 24).sum() > 0                       # the chroma branch ran
+    elif b_chroma_me:
+        assert not (ne >> 24).any()                       # sub-8x8 at 4:2:0 / 4:2:2: no chroma ME
     if subme >= 5 and not refine_qpel:
         assert (got[:, 1:3] != par[:, :2]).any(1).mean() > 0.02
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("cf,i_pixel", [(1, 0), (1, 3), (3, 0)])
+@pytest.mark.parametrize("cf,i_pixel", [(1, 0), (1, 3), (3, 0), (1, 6), (3, 5)])
 def test_refine_chroma_1080p(hip, oracle, bd, cf, i_pixel):
     """every partition of a 1920x1088 frame pair at subme 7 with b_chroma_me (x264's default P-slice
     settings), x264_me_search_ref's iterations"""

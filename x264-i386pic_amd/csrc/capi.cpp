@@ -1882,7 +1882,7 @@ extern "C" const char *x264hip_backend_banner( void )
                                                     const int32_t *init_cost, const uint16_t *cost_mv, int n,        \
                                                     int32_t *out, int32_t *nevals, void *stream )                    \
     {                                                                                                                \
-        if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || n < 0 ||                                        \
+        if( i_pixel < 0 || i_pixel > 6 || subme < 1 || subme > 11 || n < 0 ||                                        \
             ( n > 0 && ( !fenc || !p0 || !p1 || !p2 || !p3 || !pos || !par || !init_cost || !cost_mv || !out ) ) )   \
             return X264HIP_EINVAL;                                                                                   \
         const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
@@ -1901,7 +1901,7 @@ extern "C" const char *x264hip_backend_banner( void )
                                                        int32_t *nevals, const x264hip_refine_ext_t *ext,             \
                                                        void *stream )                                                \
     {                                                                                                                \
-        if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || n < 0 ||                                        \
+        if( i_pixel < 0 || i_pixel > 6 || subme < 1 || subme > 11 || n < 0 ||                                        \
             ( n > 0 && ( !fenc || !p0 || !p1 || !p2 || !p3 || !pos || !par || !init_cost || !cost_mv || !out ) ) )   \
             return X264HIP_EINVAL;                                                                                   \
         const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
@@ -1920,7 +1920,7 @@ extern "C" const char *x264hip_backend_banner( void )
                                                           const int32_t *ref_cost, const x264hip_refine_ext_t *ext,  \
                                                           void *stream )                                             \
     {                                                                                                                \
-        if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || n < 0 ||                                        \
+        if( i_pixel < 0 || i_pixel > 6 || subme < 1 || subme > 11 || n < 0 ||                                        \
             ( n > 0 && ( !fenc || !p0 || !p1 || !p2 || !p3 || !pos || !par || !init_cost || !cost_mv || !out ) ) )   \
             return X264HIP_EINVAL;                                                                                   \
         const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \

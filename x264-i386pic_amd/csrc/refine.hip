@@ -69,14 +69,14 @@ template <int BD> __device__ __forceinline__ uint32_t weigh_packed( uint32_t w, 
 // the lane's 8x4 tile of get_ref( mvx, mvy ) (weighted when WGT and wt.on) scored against its
 // fenc tile: SAD, or the sum of |coef| of the tile's two 4x4 Hadamards (even; halved by the
 // caller)
-template <int BD, bool SATD, bool WGT = false>
+template <int BD, bool SATD, bool WGT = false, int TW = 8>
 __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD>::PPD],
                                                const typename PT<BD>::pixel *q0, const typename PT<BD>::pixel *q1,
                                                const typename PT<BD>::pixel *q2, const typename PT<BD>::pixel *q3,
                                                intptr_t rs, int mvx, int mvy, const RsWeight wt = {} )
 {
     using pixel = typename PT<BD>::pixel;
-    constexpr int HDW = 8 / PT<BD>::PPD;
+    constexpr int HDW = 8 / PT<BD>::PPD, LW = HDW * TW / 8;   // words of a row; of the tile's row
     const int idx = ((mvy & 3) << 2) + (mvx & 3);
     const intptr_t off = (intptr_t)(mvy >> 2) * rs + (mvx >> 2);
     constexpr uint32_t k0 = pack_fields( c_ref0, 2 ), k1 = pack_fields( c_ref1, 2 );
@@ -91,17 +91,23 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
     uint32_t r1[4][HDW];
 #pragma unroll
     for( int y = 0; y < 4; y++ )
-        load_al_pad<HDW>( s1 + y * rs, r1[y] );
+    {
+        uint32_t t[LW];
+        load_al_pad<LW>( s1 + y * rs, t );
+#pragma unroll
+        for( int k = 0; k < HDW; k++ )
+            r1[y][k] = k < LW ? t[k] : 0u;
+    }
     if( idx & 5 )                           // two planes: the rounding average (one plane: avg( a, a ) = a)
     {
-        uint32_t r2[4][HDW];
+        uint32_t r2[4][LW];
 #pragma unroll
         for( int y = 0; y < 4; y++ )
-            load_al_pad<HDW>( s2 + y * rs, r2[y] );
+            load_al_pad<LW>( s2 + y * rs, r2[y] );
 #pragma unroll
         for( int y = 0; y < 4; y++ )
 #pragma unroll
-            for( int k = 0; k < HDW; k++ )
+            for( int k = 0; k < LW; k++ )
                 r1[y][k] = avg_round<BD>( r1[y][k], r2[y][k] );
     }
     if constexpr( WGT )
@@ -109,8 +115,9 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
 #pragma unroll
             for( int y = 0; y < 4; y++ )
 #pragma unroll
-                for( int k = 0; k < HDW; k++ )
+                for( int k = 0; k < LW; k++ )
                     r1[y][k] = weigh_packed<BD>( r1[y][k], wt );
+    // a 4-wide tile (TW 4) is the 8x4 SATD's left 4x4 with zero differences on the right
     if constexpr( SATD )
         return satd8x4_packed<BD>( fa, r1 );
     else
@@ -119,9 +126,36 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
 #pragma unroll
         for( int y = 0; y < 4; y++ )
 #pragma unroll
-            for( int k = 0; k < HDW; k++ )
+            for( int k = 0; k < LW; k++ )
                 acc = sadp<BD>( fa[y][k], r1[y][k], acc );
         return acc;
+    }
+}
+
+// a partition's tiles (reference common/pixel.h:55-59): 8x4 for widths >= 8, 4x4 for the 4-wide
+// sub-8x8 partitions (satd_4x4 per 4x4, pixel.c:265-288, 311-332); NT tiles, SH = log2 of the
+// lanes a segment of G groups takes
+template <int IPIX> constexpr int tile_w() { return pix_w( IPIX ) >= 8 ? 8 : 4; }
+template <int IPIX> constexpr int tile_n() { return (pix_w( IPIX ) / tile_w<IPIX>()) * (pix_h( IPIX ) / 4); }
+constexpr int ilog2( int v ) { return v <= 1 ? 0 : 1 + ilog2( v / 2 ); }
+__host__ __device__ constexpr int part_tiles( int i_pixel )
+{
+    return (pix_w( i_pixel ) >= 8 ? pix_w( i_pixel ) / 8 : 1) * (pix_h( i_pixel ) / 4);
+}
+// the fenc rows of the lane's tile (4-wide: the right half zero)
+template <int BD, int TW>
+__device__ __forceinline__ void load_fenc_tile( const typename PT<BD>::pixel *fe, intptr_t fs,
+                                                uint32_t (&fa)[4][8 / PT<BD>::PPD] )
+{
+    constexpr int HDW = 8 / PT<BD>::PPD, LW = HDW * TW / 8;
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+    {
+        uint32_t t[LW];
+        load_row_u<LW>( fe + y * fs, t );
+#pragma unroll
+        for( int k = 0; k < HDW; k++ )
+            fa[y][k] = k < LW ? t[k] : 0u;
     }
 }
 
@@ -260,7 +294,8 @@ __device__ __forceinline__ uint32_t nv_pair_cost( const typename PT<BD>::pixel *
 // quad_perm, then for NT = 8 row_ror:12 brings lane 8k+4's quad sum to lane 8k)
 template <int NT> __device__ __forceinline__ uint32_t group_sum( uint32_t v )
 {
-    v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0xB1, 0xF, 0xF, false );
+    if constexpr( NT >= 2 )
+        v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0xB1, 0xF, 0xF, false );
     if constexpr( NT >= 4 )
         v += (uint32_t)__builtin_amdgcn_update_dpp( 0, (int)v, 0x4E, 0xF, 0xF, false );
     if constexpr( NT >= 8 )
@@ -289,29 +324,27 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD;
-    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TX = BW / 8, NT = TX * (BH / 4);
+    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TW = tile_w<IPIX>(), TX = BW / TW, NT = tile_n<IPIX>();
     const int lane = (int)(threadIdx.x & 63);
-    constexpr int SL = 4 * NT, SH = NT == 8 ? 5 : NT == 4 ? 4 : 3;   // segment lanes, log2
+    constexpr int SL = 4 * NT, SH = ilog2( SL );          // segment lanes, log2
     const int sbase = lane & (64 - SL);                   // the segment's first lane
     const int g = (lane / NT) & 3, u = lane & (NT - 1);
     const int64_t jo = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> SH;
     const bool live = jo < n;                             // segment-uniform
     const int64_t j = live ? jo : n - 1;                  // a spare segment repeats the last job
     constexpr bool tile = true;                           // every lane holds a tile
-    const int ux = 8 * (u % TX), uy = 4 * (u / TX);
+    const int ux = TW * (u % TX), uy = 4 * (u / TX);
     const int f = pos[3 * j], bx = pos[3 * j + 1], by = pos[3 * j + 2];
 
     uint32_t fa[4][HDW];
-    const pixel *fe = fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux;
-#pragma unroll
-    for( int y = 0; y < 4; y++ )
-        load_row_u<HDW>( fe + y * fs, fa[y] );
+    load_fenc_tile<BD, TW>( fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux, fs, fa );
     const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
     const pixel *const q0 = p0 + qo, *const q1 = p1 + qo, *const q2 = p2 + qo, *const q3 = p3 + qo;
 
     // ---- EXT: the weight of the luma get_ref, the lane's chroma blocks / tiles ----
     const RsWeight wt0 = ext.wt[0];
-    const bool chroma = EXT && ext.chroma;                // launch-uniform
+    // b_chroma_me = h->mb.b_chroma_me && (i_pixel <= PIXEL_8x8 || CHROMA444) (me.c:872)
+    const bool chroma = EXT && ext.chroma && (IPIX <= 3 || EXT == 2);   // launch-uniform
     constexpr int FDW = 8 / PT<BD>::PPD;                  // words of a 4-pixel interleaved chroma row
     const pixel *cref[2] = { nullptr, nullptr };          // EXT 1: the lane's positions in the ref plane
     // their two fenc rows, in LDS (word-major: a word of every lane is one conflict-free row) --
@@ -322,7 +355,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     uint32_t fu[4][HDW] = {}, fv[4][HDW] = {};            // EXT 2: the fenc tiles of U and V
     const pixel *u0 = nullptr, *u1 = nullptr, *u2 = nullptr, *u3 = nullptr;   // and their hpel planes
     const pixel *v0 = nullptr, *v1 = nullptr, *v2 = nullptr, *v3 = nullptr;   // (no arrays: scratch)
-    if constexpr( EXT == 1 )
+    if constexpr( EXT == 1 && IPIX <= 3 )
     {
         if( chroma )
         {
@@ -360,12 +393,8 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         if( chroma )
         {
             const intptr_t fco = (intptr_t)f * ext.ffcs + (intptr_t)(by + uy) * ext.fcs + bx + ux;
-#pragma unroll
-            for( int y = 0; y < 4; y++ )
-            {
-                load_row_u<HDW>( ext.fenc_c[0] + fco + y * ext.fcs, fu[y] );
-                load_row_u<HDW>( ext.fenc_c[1] + fco + y * ext.fcs, fv[y] );
-            }
+            load_fenc_tile<BD, TW>( ext.fenc_c[0] + fco, ext.fcs, fu );
+            load_fenc_tile<BD, TW>( ext.fenc_c[1] + fco, ext.fcs, fv );
             const intptr_t rco = (intptr_t)f * ext.rfcs + (intptr_t)(by + uy) * ext.rcs + bx + ux;
             u0 = ext.ref_c[0] + rco; u1 = ext.ref_c[1] + rco; u2 = ext.ref_c[2] + rco; u3 = ext.ref_c[3] + rco;
             v0 = ext.ref_c[4] + rco; v1 = ext.ref_c[5] + rco; v2 = ext.ref_c[6] + rco; v3 = ext.ref_c[7] + rco;
@@ -396,8 +425,8 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         const int gy = g == 0 ? my[0] : g == 1 ? my[1] : g == 2 ? my[2] : my[3];
         uint32_t v = 0;
         if( tile )
-            v = satd ? tile_cost<BD, true, EXT != 0>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 ) >> 1
-                     : tile_cost<BD, false, EXT != 0>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 );
+            v = satd ? tile_cost<BD, true, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 ) >> 1
+                     : tile_cost<BD, false, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 );
         if( u == 0 )                                      // the group's mv cost, once
             v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
         v = group_sum<NT>( v );
@@ -410,8 +439,8 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         uint32_t v = 0;
         if( g == 0 )
         {
-            v = satd ? tile_cost<BD, true, EXT != 0>( fa, q0, q1, q2, q3, rs, mx, my, wt0 ) >> 1
-                     : tile_cost<BD, false, EXT != 0>( fa, q0, q1, q2, q3, rs, mx, my, wt0 );
+            v = satd ? tile_cost<BD, true, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, mx, my, wt0 ) >> 1
+                     : tile_cost<BD, false, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, mx, my, wt0 );
             if( u == 0 )
                 v += (uint32_t)cmx[mx] + (uint32_t)cmy[my];
         }
@@ -427,7 +456,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         const int gy = oy + (g == 0 ? -st : g == 1 ? st : 0);
         uint32_t vu = 0, vv = 0;
         const bool on = st != 0 || g == 0;               // st = 0: group 0 scores the centre alone
-        if constexpr( EXT == 1 )
+        if constexpr( EXT == 1 && IPIX <= 3 )
         {
             const int mvyc = (2 * (gy + ext.mvy_offset)) >> ext.vs;
             uint32_t pk = 0;                              // U | V << 16 (no carry: <= 2 * 4 * 8184)
@@ -452,13 +481,13 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
             {
                 if( qsatd )
                 {
-                    vu = tile_cost<BD, true, true>( fu, u0, u1, u2, u3, ext.rcs, gx, gy, ext.wt[1] ) >> 1;
-                    vv = tile_cost<BD, true, true>( fv, v0, v1, v2, v3, ext.rcs, gx, gy, ext.wt[2] ) >> 1;
+                    vu = tile_cost<BD, true, true, TW>( fu, u0, u1, u2, u3, ext.rcs, gx, gy, ext.wt[1] ) >> 1;
+                    vv = tile_cost<BD, true, true, TW>( fv, v0, v1, v2, v3, ext.rcs, gx, gy, ext.wt[2] ) >> 1;
                 }
                 else
                 {
-                    vu = tile_cost<BD, false, true>( fu, u0, u1, u2, u3, ext.rcs, gx, gy, ext.wt[1] );
-                    vv = tile_cost<BD, false, true>( fv, v0, v1, v2, v3, ext.rcs, gx, gy, ext.wt[2] );
+                    vu = tile_cost<BD, false, true, TW>( fu, u0, u1, u2, u3, ext.rcs, gx, gy, ext.wt[1] );
+                    vv = tile_cost<BD, false, true, TW>( fv, v0, v1, v2, v3, ext.rcs, gx, gy, ext.wt[2] );
                 }
             }
         }
@@ -703,7 +732,7 @@ static hipError_t refine_launch( const typename PT<BD>::pixel *fenc, intptr_t fs
 {
     if( n <= 0 )
         return hipSuccess;
-    if( i_pixel < 0 || i_pixel > 3 || subme < 1 || subme > 11 || kind < 0 || kind > 2 || ((uintptr_t)out & 15) )
+    if( i_pixel < 0 || i_pixel > 6 || subme < 1 || subme > 11 || kind < 0 || kind > 2 || ((uintptr_t)out & 15) )
         return hipErrorInvalidValue;
     // kind 0: x264_me_search_ref's refine (me.c:794-796), 1: x264_me_refine_qpel (:801-810),
     // 2: x264_me_refine_qpel_refdupe (:812-815)
@@ -717,8 +746,8 @@ static hipError_t refine_launch( const typename PT<BD>::pixel *fenc, intptr_t fs
     int mode;
     if( rs_ext<BD>( xe, ext, mode ) != hipSuccess )
         return hipErrorInvalidValue;
-    // 4 * (the partition's 8x4 tiles) lanes per partition (me_refine_subpel_kernel's segments)
-    const int64_t lanes = (int64_t)n * 4 * (pix_w( i_pixel ) / 8) * (pix_h( i_pixel ) / 4);
+    // 4 * (the partition's tiles) lanes per partition (me_refine_subpel_kernel's segments)
+    const int64_t lanes = (int64_t)n * 4 * part_tiles( i_pixel );
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
 #define RS_GO( I, F, E )                                                                                          \
     hipLaunchKernelGGL( ( me_refine_subpel_kernel<BD, I, F, E> ), g, blk, 0, stream, fenc, fs, ffs, planes[0],    \
@@ -732,7 +761,7 @@ static hipError_t refine_launch( const typename PT<BD>::pixel *fenc, intptr_t fs
         break;
     switch( i_pixel )
     {
-        RS_CASE( 0 ) RS_CASE( 1 ) RS_CASE( 2 ) RS_CASE( 3 )
+        RS_CASE( 0 ) RS_CASE( 1 ) RS_CASE( 2 ) RS_CASE( 3 ) RS_CASE( 4 ) RS_CASE( 5 ) RS_CASE( 6 )
         default: return hipErrorInvalidValue;
     }
 #undef RS_CASE
@@ -791,8 +820,8 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD;
-    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TX = BW / 8, NT = TX * (BH / 4);
-    constexpr int SL = 4 * NT, SH = NT == 8 ? 5 : NT == 4 ? 4 : 3;
+    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TW = tile_w<IPIX>(), TX = BW / TW, NT = tile_n<IPIX>();
+    constexpr int SL = 4 * NT, SH = ilog2( SL );
     constexpr int COST_MAX = 1 << 28;
     const int lane = (int)(threadIdx.x & 63);
     const int sbase = lane & (64 - SL);
@@ -800,14 +829,11 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
     const int64_t jo = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> SH;
     const bool live = jo < n;
     const int64_t j = live ? jo : n - 1;
-    const int ux = 8 * (u % TX), uy = 4 * (u / TX);
+    const int ux = TW * (u % TX), uy = 4 * (u / TX);
     const int f = pos[3 * j], bx = pos[3 * j + 1], by = pos[3 * j + 2];
 
     uint32_t fa[4][HDW];
-    const pixel *fe = fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux;
-#pragma unroll
-    for( int y = 0; y < 4; y++ )
-        load_row_u<HDW>( fe + y * fs, fa[y] );
+    load_fenc_tile<BD, TW>( fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux, fs, fa );
     const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
     const pixel *const q0 = p0 + qo, *const q1 = p1 + qo, *const q2 = p2 + qo, *const q3 = p3 + qo;
     const pixel *const qw = fw + qo;
@@ -828,13 +854,13 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
         {
             if( mode == 1 )
             {
-                v = tile_cost<BD, false, WGT>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 );
+                v = tile_cost<BD, false, WGT, TW>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 );
                 if( u == 0 )
                     v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
             }
             else
             {
-                v = tile_cost<BD, false, false>( fa, qw, qw, qw, qw, rs, 4 * gx, 4 * gy );
+                v = tile_cost<BD, false, false, TW>( fa, qw, qw, qw, qw, rs, 4 * gx, 4 * gy );
                 if( u == 0 && mode == 0 )
                     v += (uint32_t)cmx[4 * gx] + (uint32_t)cmy[4 * gy];
             }
@@ -1061,6 +1087,10 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
         dia1( pmx, pmy );
         if( pmx | pmy )
             dia1( 0, 0 );
+        if constexpr( IPIX == 6 )                         // PIXEL_4x4: goto me_hex2 (me.c:438-439)
+            hex = true;
+        else
+        {
         const int ucost2 = bcost;
         if( (bmx | bmy) && ((bmx - pmx) | (bmy - pmy)) )
             dia1( bmx, bmy );
@@ -1166,6 +1196,7 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
                 }
             } while( ++i <= i_me_range >> 2 );
             hex = in_range( bmx, bmy );
+        }
         }
     }
     if( hex )
@@ -1279,7 +1310,7 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
 {
     if( n <= 0 )
         return hipSuccess;
-    if( i_pixel < 0 || i_pixel > 3 || me_method < 0 || me_method > 2 || subme < 1 || subme > 11 || me_range < 4 ||
+    if( i_pixel < 0 || i_pixel > 6 || me_method < 0 || me_method > 2 || subme < 1 || subme > 11 || me_range < 4 ||
         me_range > 64 || ((uintptr_t)out & 15) )
         return hipErrorInvalidValue;
     RsExt<BD> ext;
@@ -1298,7 +1329,7 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
         rpar = (int16_t *)buf;
         rinit = (int32_t *)((char *)buf + (size_t)n * 16);
     }
-    const int64_t lanes = (int64_t)n * 4 * (pix_w( i_pixel ) / 8) * (pix_h( i_pixel ) / 4);
+    const int64_t lanes = (int64_t)n * 4 * part_tiles( i_pixel );
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
 #define SR_GO( I, W )                                                                                             \
     hipLaunchKernelGGL( ( me_search_ref_kernel<BD, I, W> ), g, blk, 0, stream, fenc, fs, ffs, fw, planes[0],      \
@@ -1310,7 +1341,7 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
         break;
     switch( i_pixel )
     {
-        SR_CASE( 0 ) SR_CASE( 1 ) SR_CASE( 2 ) SR_CASE( 3 )
+        SR_CASE( 0 ) SR_CASE( 1 ) SR_CASE( 2 ) SR_CASE( 3 ) SR_CASE( 4 ) SR_CASE( 5 ) SR_CASE( 6 )
         default: break;
     }
 #undef SR_CASE
@@ -1385,8 +1416,8 @@ __global__ __launch_bounds__( 256 ) void me_refine_bidir_kernel(
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD, PPD = PT<BD>::PPD;
-    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TX = BW / 8, NT = TX * (BH / 4);
-    constexpr int SL = 8 * NT, SH = NT == 8 ? 6 : NT == 4 ? 5 : 4;
+    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TW = tile_w<IPIX>(), TX = BW / TW, NT = tile_n<IPIX>();
+    constexpr int SL = 8 * NT, SH = ilog2( SL );
     constexpr int COST_MAX = 1 << 28, NONE = 0x7fffffff;
     __shared__ uint32_t s_vis[256 / SL][128];
     const int lane = (int)(threadIdx.x & 63);
@@ -1395,14 +1426,11 @@ __global__ __launch_bounds__( 256 ) void me_refine_bidir_kernel(
     const int64_t jo = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> SH;
     const bool live = jo < n;
     const int64_t j = live ? jo : n - 1;
-    const int ux = 8 * (u % TX), uy = 4 * (u / TX);
+    const int ux = TW * (u % TX), uy = 4 * (u / TX);
     const int f = pos[3 * j], bx = pos[3 * j + 1], by = pos[3 * j + 2];
 
     uint32_t fa[4][HDW];
-    const pixel *fe = fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux;
-#pragma unroll
-    for( int y = 0; y < 4; y++ )
-        load_row_u<HDW>( fe + y * fs, fa[y] );
+    load_fenc_tile<BD, TW>( fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux, fs, fa );
     const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
     const pixel *const p0 = a0 + qo, *const p1 = a1 + qo, *const p2 = a2 + qo, *const p3 = a3 + qo;
     const pixel *const r0 = b0 + qo, *const r1 = b1 + qo, *const r2 = b2 + qo, *const r3 = b3 + qo;
