@@ -1094,7 +1094,9 @@ def search_params(mbw, mbh, F, i_pixel, seed=7, motion=(13, 10)):
     frame-batched search does not have, so mvp = the true motion +- 8 qpel and four candidates
     (two near the motion, one at zero, one far) stand in for them."""
     rs = np.random.default_rng(seed)
-    parts = [(0, 0)] if i_pixel == 0 else [(0, 0), (8, 0), (0, 8), (8, 8)]
+    q = [(0, 0), (8, 0), (0, 8), (8, 8)]
+    parts = {0: [(0, 0)], 3: q, 4: [(x, y + d) for x, y in q for d in (0, 4)],
+             6: [(x + dx, y + dy) for x, y in q for dy in (0, 4) for dx in (0, 4)]}[i_pixel]
     n1 = F * mbw * mbh
     mb = np.repeat(np.arange(n1), len(parts))
     n = len(mb)
@@ -1121,12 +1123,15 @@ def rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes,
     refine_subpel with chroma ME) as x264's default preset runs it on P slices -- HEX, subme 7,
     me_range 16 (common/base.c:439-441) -- over every 16x16 MB (search16_hex_*) and every 8x8
     partition (search8_hex_*) of the F pairs of rates_refine's quarter-pel sequence, and UMH
-    (--me umh, the slower presets) on 16x16 (search16_umh_*).  Rates in partitions/s; the
+    (--me umh, the slower presets) on 16x16 (search16_umh_*), every 4x4 partition (search4_hex_*:
+    --partitions p4x4, analyse.c:1685-1760) and the exhaustive ESA window (search16_esa_*: --me
+    esa, me.c:618-631).  Rates in partitions/s; the
     candidates the reference evaluates (its fpelcmp / get_ref / refine calls, counted by the
     kernels) give the absdiff rate against the v_sad_u8 peak."""
     res = {"search_workload": "rates_refine's sequence, synthetic mvp / mvc (search_params), subme 7, me_range 16, "
                               "b_chroma_me on, the whole x264_me_search_ref per launch"}
-    for leg, i_pixel, me in (("search16_hex", 0, 1), ("search16_umh", 0, 2), ("search8_hex", 3, 1)):
+    for leg, i_pixel, me in (("search16_hex", 0, 1), ("search16_umh", 0, 2), ("search8_hex", 3, 1),
+                             ("search4_hex", 6, 1), ("search16_esa", 0, 3)):
         pos, par, mvc = search_params(mbw, mbh, F, i_pixel)
         n = len(pos)
         pos_d, par_d, mvc_d = (torch.from_numpy(v).cuda() for v in (pos, par, mvc))
@@ -1143,7 +1148,7 @@ def rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes,
         rsad = int((ne[:, 1] & 0xFFFF).sum().item())
         rsatd = int(((ne[:, 1] >> 16) & 0xFF).sum().item())
         rchroma = int((ne[:, 1] >> 24).sum().item())
-        px = 256 if i_pixel == 0 else 64
+        px = {0: 256, 3: 64, 4: 32, 6: 16}[i_pixel]
         cands = nf + nh + rsad + rsatd
         res.update({leg + "_partitions_per_s": world * a.steps * n / wall, leg + "_launch_ms": ev_ms,
                     leg + "_partitions_per_launch": n, leg + "_fpel_calls_per_part": nf / n,

@@ -911,8 +911,11 @@ int x264hip_##BD##_me_refine_qpel_refdupe( const pixel *fenc, intptr_t fenc_stri
                                                                                                 \
 /* x264_me_search_ref (reference encoder/me.c:182-798) for n partitions of size i_pixel (16x16 ..  \
  * 4x4; UMH on PIXEL_4x4 goes to the hexagon after its predictor diamonds, me.c:438-439) with     \
- * me_method X264_ME_DIA (0), X264_ME_HEX (1, x264's default, common/base.c:439) or               \
- * X264_ME_UMH (2): the predictor checks over mvp and the mvc list (x264_predictor_clip /          \
+ * me_method X264_ME_DIA (0), X264_ME_HEX (1, x264's default, common/base.c:439),                 \
+ * X264_ME_UMH (2) or X264_ME_ESA (3: the window of me.c:618-631 around the predictor stage's      \
+ * winner, every candidate scored -- the decision the successive elimination of :750-768 also     \
+ * reaches; nevals then counts the exhaustive form's calls; TESA stays with me_tesa): the          \
+ * predictor checks over mvp and the mvc list (x264_predictor_clip /                              \
  * _roundclip, common/common.h:774-805), the integer search (UMH with its adaptive range), the    \
  * qpel conversion (me.c:774-789), then refine_subpel when subme >= 2 as me_refine_subpel_ex      \
  * runs it (ext: chroma ME, m->weight; weight[0] also weights the predictors' get_ref).           \

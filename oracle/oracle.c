@@ -2172,6 +2172,21 @@ void FN(me_search_ref_thresh)( const pixel *fenc, intptr_t fs, const pixel *cons
             } while( --i && SR_IN( bmx, bmy ) );
             bcost >>= 4;
         }
+        else if( me_method == 3 )
+        {
+            /* ESA (me.c:618-631): the exhaustive form the reference keeps under #if 0 (:627-631),
+             * which its successive elimination (ads, :750-768) equals in bcost / bmx / bmy: ads
+             * only drops candidates whose DC bound cannot beat bcost.  The width rounds up to a
+             * multiple of 4 (columns past max_x scored). */
+            const int min_x = bmx - i_me_range > mv_x_min ? bmx - i_me_range : mv_x_min;
+            const int min_y = bmy - i_me_range > mv_y_min ? bmy - i_me_range : mv_y_min;
+            const int max_x = bmx + i_me_range < mv_x_max ? bmx + i_me_range : mv_x_max;
+            const int max_y = bmy + i_me_range < mv_y_max ? bmy + i_me_range : mv_y_max;
+            const int width = (max_x - min_x + 3) & ~3;
+            for( int my = min_y; my <= max_y; my++ )
+                for( int mx = min_x; mx < min_x + width; mx++ )
+                    SR_COST_MV( mx, my );
+        }
         else if( me_method == 2 )
         {
             /* UMH (me.c:422-616) */

@@ -175,6 +175,15 @@ def search_ref_py(fenc, planes, fw, origin, stride, x, y, i_pixel, par, mvc, cm,
             if not (i and inr(bmx, bmy)):
                 break
         st["bcost"], st["bmx"], st["bmy"] = b >> 4, bmx, bmy
+    elif me_method == 3:
+        # ESA: me.c:627-631's exhaustive form (the SEA of :750-768 gives the same decision)
+        bmx, bmy = st["bmx"], st["bmy"]
+        min_x, min_y = max(bmx - me_range, xmin), max(bmy - me_range, ymin)
+        max_x, max_y = min(bmx + me_range, xmax), min(bmy + me_range, ymax)
+        width = (max_x - min_x + 3) & ~3
+        for my in range(min_y, max_y + 1):
+            for mx in range(min_x, min_x + width):
+                cost_mv(mx, my)
     elif me_method == 2:
         thresh = lambda v: st["bcost"] < (v >> PIXEL_SIZE_SHIFT[i_pixel])
 

@@ -22,7 +22,7 @@ def _case(bd, cf, W, H, fade, seed):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("me_method", [0, 1, 2])
+@pytest.mark.parametrize("me_method", [0, 1, 2, 3])
 @pytest.mark.parametrize("i_pixel", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("subme,fade,chroma", [(1, 0, 0), (2, 0, 0), (4, 1, 0), (7, 0, 1), (9, 1, 1)])
 def test_search_oracle_vs_python(oracle, bd, me_method, i_pixel, subme, fade, chroma):

@@ -59,7 +59,7 @@ def _run(hip, oracle, bd, cf, W, H, nframes, i_pixel, me_method, subme, me_range
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("me_method", [0, 1, 2])
+@pytest.mark.parametrize("me_method", [0, 1, 2, 3])
 @pytest.mark.parametrize("i_pixel", [0, 1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("subme,fade,chroma", [(1, 0, 0), (2, 0, 0), (4, 1, 0), (7, 0, 1), (9, 1, 1)])
 def test_search_small(hip, oracle, bd, me_method, i_pixel, subme, fade, chroma):
@@ -68,7 +68,7 @@ def test_search_small(hip, oracle, bd, me_method, i_pixel, subme, fade, chroma):
 
 
 @pytest.mark.parametrize("bd", [8, 10])
-@pytest.mark.parametrize("me_method,i_pixel", [(1, 0), (2, 0), (1, 3), (1, 6), (2, 6), (2, 4)])
+@pytest.mark.parametrize("me_method,i_pixel", [(1, 0), (2, 0), (1, 3), (1, 6), (2, 6), (2, 4), (3, 0), (3, 3)])
 def test_search_1080p(hip, oracle, bd, me_method, i_pixel):
     """every partition of a 1920x1088 frame pair at x264's default settings (HEX, subme 7, chroma ME
     on P slices) and UMH"""
@@ -82,7 +82,7 @@ def test_search_args(hip):
     pos = torch.zeros((1, 3), dtype=torch.int32, device="cuda")
     par = torch.zeros((1, 12), dtype=torch.int16, device="cuda")
     mvc = torch.zeros((1, 14, 2), dtype=torch.int16, device="cuda")
-    for i_pixel, me, subme, rng in ((7, 1, 7, 16), (0, 3, 7, 16), (0, 1, 0, 16), (0, 1, 7, 2), (0, 1, 7, 65)):
+    for i_pixel, me, subme, rng in ((7, 1, 7, 16), (0, 4, 7, 16), (0, 1, 0, 16), (0, 1, 7, 2), (0, 1, 7, 65)):
         with pytest.raises(RuntimeError):
             hip.me_search_ref(p, 32 * 256 + 32, 256, p, [p, p, p, p], 32 * 256 + 32, 256, i_pixel, me, subme, rng,
                               pos, par, mvc, (t.view(torch.int16), 0))

@@ -1041,6 +1041,36 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
         } while( --i && in_range( bmx, bmy ) );
         bcost >>= 4;
     }
+    else if( me_method == 3 )
+    {
+        // ESA (me.c:618-631, 750-768): every candidate of the window around the predictor stage's
+        // (bmx, bmy), the width rounded up to a multiple of 4 (columns past max_x included), in
+        // raster order with COST_MV's strict <.  The reference's successive elimination (ads on
+        // the integral image) only skips candidates that cannot beat bcost, so the exhaustive
+        // form it keeps under #if 0 (me.c:627-631) gives the same bcost / bmx / bmy; a round
+        // scores four adjacent columns of one row (width is a multiple of 4)
+        const int min_x = max( bmx - i_me_range, xmin ), min_y = max( bmy - i_me_range, ymin );
+        const int max_x = min( bmx + i_me_range, xmax ), max_y = min( bmy + i_me_range, ymax );
+        const int width = (max_x - min_x + 3) & ~3;
+        int my = min_y, cx = 0;
+        bool more = width > 0 && min_y <= max_y;
+        while( __any( more ) )
+        {
+            evalc( min_x + cx + g, my, 0, more, c );
+            if( more )
+            {
+#pragma unroll
+                for( int k = 0; k < 4; k++ )
+                    upd( c[k], min_x + cx + k, my );
+                cx += 4;
+                if( cx >= width )
+                {
+                    cx = 0;
+                    more = ++my <= max_y;
+                }
+            }
+        }
+    }
     else if( me_method == 2 )
     {
         // UMH (me.c:422-616)
@@ -1310,7 +1340,7 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
 {
     if( n <= 0 )
         return hipSuccess;
-    if( i_pixel < 0 || i_pixel > 6 || me_method < 0 || me_method > 2 || subme < 1 || subme > 11 || me_range < 4 ||
+    if( i_pixel < 0 || i_pixel > 6 || me_method < 0 || me_method > 3 || subme < 1 || subme > 11 || me_range < 4 ||
         me_range > 64 || ((uintptr_t)out & 15) )
         return hipErrorInvalidValue;
     RsExt<BD> ext;
