@@ -434,6 +434,26 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         for( int k = 0; k < 4; k++ )
             c[k] = (int)__shfl( (int)v, sbase + NT * k );
     };
+    // eval4 (SATD) with the diamond's centre (cx, cy) scored beside each group's candidate in the
+    // same memory round: the hpel winner's COST_MV_SATD (me.c:925-929) merged into the first
+    // quarterpel diamond's round; cc = the centre's cost
+    auto eval4c = [&]( const int (&mx)[4], const int (&my)[4], int cx, int cy, int (&c)[4], int &cc ) __attribute__( ( always_inline ) ) {
+        const int gx = g == 0 ? mx[0] : g == 1 ? mx[1] : g == 2 ? mx[2] : mx[3];
+        const int gy = g == 0 ? my[0] : g == 1 ? my[1] : g == 2 ? my[2] : my[3];
+        uint32_t vc = tile_cost<BD, true, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, cx, cy, wt0 ) >> 1;
+        uint32_t v = tile_cost<BD, true, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 ) >> 1;
+        if( u == 0 )
+        {
+            v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
+            vc += (uint32_t)cmx[cx] + (uint32_t)cmy[cy];
+        }
+        v = group_sum<NT>( v );
+        vc = group_sum<NT>( vc );
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+            c[k] = (int)__shfl( (int)v, sbase + NT * k );
+        cc = (int)__shfl( (int)vc, sbase );
+    };
     // one candidate: group 0 scores it, the other groups' lanes stay masked off (no loads)
     auto eval1 = [&]( int mx, int my, bool satd ) __attribute__( ( always_inline ) ) {
         uint32_t v = 0;
@@ -500,6 +520,40 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
             cv[k] = (int)__shfl( (int)vv, sbase + NT * k );
         }
     };
+    // evalc4 of the unit diamond around (ox, oy) with the centre's chroma in the same round (EXT 1;
+    // the merged re-score, as eval4c): cuc / cvc = the centre's U / V costs
+    auto evalc4c = [&]( int ox, int oy, int (&cu)[4], int (&cv)[4], int &cuc, int &cvc ) __attribute__( ( always_inline ) ) {
+        const int gx = ox + (g == 2 ? -1 : g == 3 ? 1 : 0);
+        const int gy = oy + (g == 0 ? -1 : g == 1 ? 1 : 0);
+        uint32_t pk = 0, pc = 0;
+        if constexpr( EXT == 1 && IPIX <= 3 )
+        {
+            const int mvyc = (2 * (gy + ext.mvy_offset)) >> ext.vs, mvyo = (2 * (oy + ext.mvy_offset)) >> ext.vs;
+#pragma unroll
+            for( int k = 0; k < 2; k++ )
+                if( has[k] )
+                {
+                    uint32_t fb[2][4];
+#pragma unroll
+                    for( int y = 0; y < 2; y++ )
+#pragma unroll
+                        for( int i = 0; i < 4; i++ )
+                            fb[y][i] = s_cfb[(2 * k + y) * 4 + i][threadIdx.x];
+                    pc += nv_pair_cost<BD>( cref[k], ext.rcs, ox, mvyo, fb, ext.wt[1], ext.wt[2], qsatd, hh );
+                    pk += nv_pair_cost<BD>( cref[k], ext.rcs, gx, mvyc, fb, ext.wt[1], ext.wt[2], qsatd, hh );
+                }
+        }
+        const uint32_t vu = group_sum<NT>( pk & 0xffff ), vv = group_sum<NT>( pk >> 16 );
+        const uint32_t wu = group_sum<NT>( pc & 0xffff ), wv = group_sum<NT>( pc >> 16 );
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            cu[k] = (int)__shfl( (int)vu, sbase + NT * k );
+            cv[k] = (int)__shfl( (int)vv, sbase + NT * k );
+        }
+        cuc = (int)__shfl( (int)wu, sbase );
+        cvc = (int)__shfl( (int)wv, sbase );
+    };
     // COST_MV_SATD's chroma branch (me.c:833-861) on a luma cost c against bcost
     auto add_chroma = [&]( int c, int cu, int cv, int bc ) __attribute__( ( always_inline ) ) {
         if( c < bc )
@@ -565,8 +619,28 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     }
 
     // the hpel winner re-scored with mbcmp when it differs from fpelcmp or chroma ME is on
-    // (me.c:925-929: bcost = COST_MAX, COST_MV_SATD)
-    if( !refine_qpel && ((qsatd && !FSATD) || chroma) )
+    // (me.c:925-929: bcost = COST_MAX, COST_MV_SATD).  With a quarterpel diamond to follow (SATD
+    // mbcmp, 4:2:0 / 4:2:2 or no chroma) the re-score rides in the diamond's first round: the
+    // diamond's candidates around the hpel winner do not depend on the re-scored cost, only its
+    // decisions do, so every group scores its candidate and the winner together (luma, then
+    // chroma) and the first iteration below takes those costs
+    const bool resc = !refine_qpel && ((qsatd && !FSATD) || chroma);
+    const bool merged = resc && qsatd && subme != 1 && qpel_iters > 0 && (!chroma || EXT == 1);   // uniform
+    int c1[4], cu1[4] = { 0, 0, 0, 0 }, cv1[4] = { 0, 0, 0, 0 };
+    if( merged )
+    {
+        const int mx[4] = { bmx, bmx, bmx - 1, bmx + 1 }, my[4] = { bmy - 1, bmy + 1, bmy, bmy };
+        eval4c( mx, my, bmx, bmy, c1, bcost );
+        count( qsatd, 1 );
+        if constexpr( EXT == 1 )
+            if( chroma )
+            {
+                int cuc, cvc;
+                evalc4c( bmx, bmy, cu1, cv1, cuc, cvc );
+                bcost = add_chroma( bcost, cuc, cvc, 1 << 28 );
+            }
+    }
+    else if( resc )
     {
         bcost = eval1( bmx, bmy, qsatd );
         count( qsatd, 1 );
@@ -609,8 +683,20 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
             const int omx = bmx, omy = bmy;
             const int mx[4] = { omx, omx, omx - 1, omx + 1 }, my[4] = { omy - 1, omy + 1, omy, omy };
             int c[4];
-            eval4( mx, my, qsatd, c );
             int cu[4] = { 0, 0, 0, 0 }, cv[4] = { 0, 0, 0, 0 };
+            if( merged && i == qpel_iters )               // the first round's costs, scored with the re-score
+            {
+#pragma unroll
+                for( int d = 0; d < 4; d++ )
+                {
+                    c[d] = c1[d];
+                    cu[d] = cu1[d];
+                    cv[d] = cv1[d];
+                }
+            }
+            else
+            {
+            eval4( mx, my, qsatd, c );
             if constexpr( EXT != 0 )
                 if( chroma )
                 {
@@ -622,6 +708,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
                     if( __any( need ) )
                         evalc4( omx, omy, 1, cu, cv );
                 }
+            }
             if( act )
             {
 #pragma unroll
