@@ -896,7 +896,42 @@ constexpr uint8_t k_hex4y0[8] = { 0, 8, 1, 1, 2, 2, 3, 3 }, k_hex4y1[8] = { 4, 4
 constexpr uint8_t k_psize_shift[7] = { 0, 1, 1, 2, 3, 3, 4 };
 }
 
-template <int BD, int IPIX, bool WGT>
+// the lane's full-pel tile SAD at four adjacent candidate columns x0 .. x0+3 of one row: one
+// window load per tile row (TW + 3 pixels), each candidate's row realigned from it
+template <int BD, int TW>
+__device__ __forceinline__ void sad4_tile( const uint32_t (&fa)[4][8 / PT<BD>::PPD], const typename PT<BD>::pixel *q,
+                                           intptr_t rs, uint32_t (&acc)[4] )
+{
+    constexpr int PPD = PT<BD>::PPD, LW = TW / PPD;                  // words of a tile row
+    constexpr int NW = (TW + 3 + PPD - 1) / PPD;                      // words of the window
+    constexpr int BPP = 4 / PPD;                                      // bytes per pixel
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+        acc[k] = 0;
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+    {
+        uint32_t t[NW], w[NW + 1];
+        load_al_pad<NW>( q + y * rs, t );
+#pragma unroll
+        for( int i = 0; i < NW; i++ )
+            w[i] = t[i];
+        w[NW] = 0;
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            const int sh = k * BPP, o = sh / 4, sub = sh % 4;
+#pragma unroll
+            for( int i = 0; i < LW; i++ )
+            {
+                const uint32_t wk = sub ? __builtin_amdgcn_alignbyte( w[i + o + 1], w[i + o], sub ) : w[i + o];
+                acc[k] = sadp<BD>( fa[y][i], wk, acc[k] );
+            }
+        }
+    }
+}
+
+template <int BD, int IPIX, bool WGT, bool ESA>
 __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
     const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs, intptr_t ffs, const typename PT<BD>::pixel *fw,
     const typename PT<BD>::pixel *p0, const typename PT<BD>::pixel *p1, const typename PT<BD>::pixel *p2,
@@ -1106,9 +1141,9 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
     auto dia = [&]( int cx, int cy ) __attribute__( ( always_inline ) ) {
         evalc( cx + (g == 2 ? -1 : g == 3 ? 1 : 0), cy + (g == 0 ? -1 : g == 1 ? 1 : 0), 0, true, c );
     };
-    bool hex = me_method == 1;
+    bool hex = !ESA && me_method == 1;
     int i_me_range = me_range;
-    if( me_method == 0 )
+    if( !ESA && me_method == 0 )
     {
         bcost <<= 4;
         int i = i_me_range;
@@ -1128,7 +1163,7 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
         } while( --i && in_range( bmx, bmy ) );
         bcost >>= 4;
     }
-    else if( me_method == 3 )
+    else if constexpr( ESA )                              // (its own instance: the other methods keep 5 waves)
     {
         // ESA (me.c:618-631, 750-768): every candidate of the window around the predictor stage's
         // (bmx, bmy), the width rounded up to a multiple of 4 (columns past max_x included), in
@@ -1138,24 +1173,54 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
         // scores four adjacent columns of one row (width is a multiple of 4)
         const int min_x = max( bmx - i_me_range, xmin ), min_y = max( bmy - i_me_range, ymin );
         const int max_x = min( bmx + i_me_range, xmax ), max_y = min( bmy + i_me_range, ymax );
-        const int width = (max_x - min_x + 3) & ~3;
-        int my = min_y, cx = 0;
-        bool more = width > 0 && min_y <= max_y;
-        while( __any( more ) )
+        const int width = (max_x - min_x + 3) & ~3, nrows = width > 0 ? max( max_y - min_y + 1, 0 ) : 0;
+        // the first minimum in raster order is the least (cost, raster index) key, so the
+        // candidates may be scored in any order: group g takes rows g, g + 4, ..., a lane four
+        // columns of its row per round (one window load per tile row)
+        uint64_t best = ~0ull;
+        for( int r0 = 0; __any( r0 < nrows ); r0 += 4 )
         {
-            evalc( min_x + cx + g, my, 0, more, c );
-            if( more )
+            const int r = r0 + g, my = min_y + r;
+            for( int cx = 0; __any( r0 < nrows && cx < width ); cx += 4 )
             {
+                const bool ok = r < nrows && cx < width;
+                uint32_t sa[4] = { 0, 0, 0, 0 };
+                if( ok )
+                    sad4_tile<BD, TW>( fa, qw + (intptr_t)my * rs + min_x + cx, rs, sa );
 #pragma unroll
                 for( int k = 0; k < 4; k++ )
-                    upd( c[k], min_x + cx + k, my );
-                cx += 4;
-                if( cx >= width )
+                    sa[k] = group_sum<NT>( sa[k] );
+                if( ok && u == 0 )
                 {
-                    cx = 0;
-                    more = ++my <= max_y;
+                    const uint32_t cy = cmy[4 * my], rbase = (uint32_t)(r * width + cx);
+#pragma unroll
+                    for( int k = 0; k < 4; k++ )
+                    {
+                        const uint32_t cost = sa[k] + cmx[4 * (min_x + cx + k)] + cy;
+                        const uint64_t key = ((uint64_t)cost << 32) | (rbase + k);
+                        best = key < best ? key : best;
+                    }
                 }
             }
+        }
+        // the segment's groups meet (lane u == 0 of each group holds its rows' best)
+        uint64_t seg = ~0ull;
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            const int src = sbase + NT * k;
+            const uint64_t o = ((uint64_t)(uint32_t)__shfl( (int)(best >> 32), src ) << 32) |
+                               (uint32_t)__shfl( (int)(uint32_t)best, src );
+            seg = o < seg ? o : seg;
+        }
+        best = seg;
+        nf += width * nrows;
+        if( best != ~0ull && (int)(best >> 32) < bcost )
+        {
+            const int ri = (int)(uint32_t)best;
+            bcost = (int)(best >> 32);
+            bmy = min_y + ri / width;
+            bmx = min_x + ri % width;
         }
     }
     else if( me_method == 2 )
@@ -1449,7 +1514,12 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
     const int64_t lanes = (int64_t)n * 4 * part_tiles( i_pixel );
     dim3 blk( 256 ), g( (unsigned)((lanes + 255) / 256) );
 #define SR_GO( I, W )                                                                                             \
-    hipLaunchKernelGGL( ( me_search_ref_kernel<BD, I, W> ), g, blk, 0, stream, fenc, fs, ffs, fw, planes[0],      \
+    if( me_method == 3 )                                                                                          \
+        hipLaunchKernelGGL( ( me_search_ref_kernel<BD, I, W, true> ), g, blk, 0, stream, fenc, fs, ffs, fw,       \
+                            planes[0], planes[1], planes[2], planes[3], rs, rfs, n, me_method, subme, me_range,   \
+                            pos, par, mvc, cost_mv, ext.wt[0], out, rpar, rinit, nevals );                        \
+    else                                                                                                          \
+    hipLaunchKernelGGL( ( me_search_ref_kernel<BD, I, W, false> ), g, blk, 0, stream, fenc, fs, ffs, fw, planes[0], \
                         planes[1], planes[2], planes[3], rs, rfs, n, me_method, subme, me_range, pos, par, mvc,     \
                         cost_mv, ext.wt[0], out, rpar, rinit, nevals )
 #define SR_CASE( I )                                                                                              \
