@@ -112,3 +112,21 @@ def test_ssim_bands(hip, oracle, bd, W, H, slices):
             wtotal += float(want)
         assert total == wtotal
 
+
+
+@pytest.mark.parametrize("bd", [8, 10])
+def test_ssim_bands_max_width(hip, oracle, bd):
+    """the widest band x264hip_*_ssim_bands accepts (nx = width / 4 = 2047 4x4 columns,
+    two rows of sums in LDS: 65.5 KB of dynamic LDS, inside gfx950's 160 KB per workgroup), each
+    band bit-identical to x264_pixel_ssim_wxh; one column more is refused"""
+    W, H = 8192, 48
+    bands = hip.ssim_encoder_bands(H // 16, H)
+    pa, pb = _planes(oracle, bd, W, H, 77 + bd)
+    s = pa.shape[1]
+    a, b = _dev(pa[None]), _dev(pb[None])
+    got = hip.ssim_bands(a, 2, s, b, 2, s, W - 2, torch.from_numpy(bands).cuda()).cpu().numpy()
+    for i, (y, h) in enumerate(bands):
+        want, _ = oracle.ssim_wxh(bd, pa.ravel(), 2 + int(y) * s, s, pb.ravel(), 2 + int(y) * s, s, W - 2, int(h))
+        assert got[0, i].tobytes() == want.tobytes(), (i, got[0, i], want)
+    with pytest.raises(RuntimeError):
+        hip.ssim_bands(a, 0, s, b, 0, s, 8196, torch.from_numpy(bands).cuda())
