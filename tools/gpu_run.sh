@@ -7,6 +7,7 @@
 #   driver        bench.py --steps 20 --warmup 5 -> gpurun_out/TAG_bench_driver.log
 #   profile       tools/gpu_profile.sh (trace + FETCH / WRITE PMC of the default bench)
 #   py:SCRIPT     python tools/SCRIPT (args after '='), stdout -> gpurun_out/TAG_SCRIPT.log
+#   envab:VAR     headline-only bench, VAR=0 / VAR=1 interleaved 3 times -> gpurun_out/TAG_envab.log
 # Every GPU step runs under its own time limit; the first failing step ends the run.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -43,6 +44,16 @@ for step in "$@"; do
       timeout -k 10 600 python -u tools/$script $args > gpurun_out/${TAG}_${script%.py}.log 2>&1 \
         || { tail -30 gpurun_out/${TAG}_${script%.py}.log; exit 9; }
       tail -30 gpurun_out/${TAG}_${script%.py}.log ;;
+    envab:*)
+      var=${step#envab:}
+      for i in 1 2 3; do
+        for v in 0 1; do
+          env $var=$v timeout -k 10 200 python bench.py --no-cpu --no-extra > gpurun_out/${TAG}_ab.json 2>&1 \
+            || { tail -20 gpurun_out/${TAG}_ab.json; exit 10; }
+          echo "$var=$v $(python -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['roofline']['frac'])" gpurun_out/${TAG}_ab.json)" \
+            | tee -a gpurun_out/${TAG}_envab.log
+        done
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

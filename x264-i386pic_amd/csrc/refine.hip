@@ -942,7 +942,7 @@ __global__ __launch_bounds__( 256 ) void me_search_ref_kernel(
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD;
-    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TW = tile_w<IPIX>(), TX = BW / TW, NT = tile_n<IPIX>();
+    constexpr int BW = pix_w( IPIX ), TW = tile_w<IPIX>(), TX = BW / TW, NT = tile_n<IPIX>();
     constexpr int SL = 4 * NT, SH = ilog2( SL );
     constexpr int COST_MAX = 1 << 28;
     const int lane = (int)(threadIdx.x & 63);
@@ -1603,7 +1603,7 @@ __global__ __launch_bounds__( 256 ) void me_refine_bidir_kernel(
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD, PPD = PT<BD>::PPD;
-    constexpr int BW = pix_w( IPIX ), BH = pix_h( IPIX ), TW = tile_w<IPIX>(), TX = BW / TW, NT = tile_n<IPIX>();
+    constexpr int BW = pix_w( IPIX ), TW = tile_w<IPIX>(), TX = BW / TW, NT = tile_n<IPIX>();
     constexpr int SL = 8 * NT, SH = ilog2( SL );
     constexpr int COST_MAX = 1 << 28, NONE = 0x7fffffff;
     __shared__ uint32_t s_vis[256 / SL][128];
