@@ -691,6 +691,7 @@ def extra_rates(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, full=Non
     res.update(rates_esa(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_refine(x, a, world, mbw, mbh, F))
     res.update(rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
+    res.update(rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F))
     res.update(rates_10bit(x, a, world, mbw, mbh, F))
     res.update(r2160)
     return res
@@ -1281,6 +1282,56 @@ def rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, bd=8):
            pre + "_valu_frac": cands * 256 / (ev_ms * 1e-3) / peak,
            pre + "_hbm_frac": moved / (ev_ms * 1e-3) / HBM_PEAK, pre + "_table_bytes": t8.numel() * 2}
     del t8
+    return res
+
+
+def rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
+    """ESA decisions of every MB's eight sub-partitions (me_search_esa8: PIXEL_16x8 x2, 8x16 x2,
+    8x8 x4, me.c:618-631 per partition, analyse.c:1425,1480,1546) over the F pairs at me_range
+    16, template radius 16 around each MB's centre (mv 0).  Two contents: every partition's
+    window centred on its MB's (the shared-absdiff pass decides all of them), and a quarter of
+    the partitions starting from a predictor up to 3 pixels off it (x264 starts each partition
+    from its own best predictor; those windows' outside strips take the direct pass).  The
+    fraction is taken on the shared work, 256 byte absdiffs per 16x16 window candidate (the
+    quadrant-table search's basis, full8_valu_frac); the first content is checked against the
+    direct pass alone (range 0)."""
+    me_range = R = a.range
+    n1 = mbw * mbh
+    par1, init1, cm, span = tesa_params(mbw, mbh, F, me_range, centre=(0, 0))
+    par = np.repeat(par1, 8, axis=0)
+    init = np.repeat(init1, 8)
+    cm_d = torch.from_numpy(cm.view(np.int16)).cuda()
+    cen_d = torch.zeros((F * n1, 2), dtype=torch.int16, device="cuda")
+    rs = np.random.default_rng(17)
+    par_s = par.copy()
+    move = rs.random(len(par)) < 0.25
+    off = rs.integers(-3, 4, (len(par), 2))
+    par_s[:, 0] += np.where(move, off[:, 0], 0).astype(np.int16)
+    par_s[:, 1] += np.where(move, off[:, 1], 0).astype(np.int16)
+    par_s[:, 2], par_s[:, 3] = 4 * par_s[:, 0], 4 * par_s[:, 1]
+    out = torch.empty((len(par), 3), dtype=torch.int32, device="cuda")
+    init_d = torch.from_numpy(init).cuda()
+    res = {}
+    for tag, pp in (("esa8", par), ("esa8_spread", par_s)):
+        par_d = torch.from_numpy(pp).cuda()
+
+        def step(par_d=par_d):
+            x.me_search_esa8(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, me_range, cen_d,
+                             par_d, init_d, (cm_d, span), out=out, fenc_frame_stride=fstride,
+                             ref_frame_stride=fstride)
+        wall, ev_ms = timed(step, a.steps, a.warmup, world)
+        cands = esa_window_candidates(par1, me_range)        # 16x16 windows: the shared absdiffs
+        res[tag + "_step_ms"] = ev_ms
+        res[tag + "_partitions_per_s"] = world * a.steps * len(pp) / wall
+        res[tag + "_frac"] = cands * 256 / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF
+        if tag == "esa8":
+            direct = x.me_search_esa8(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, 0, me_range,
+                                      cen_d, par_d, init_d, (cm_d, span), fenc_frame_stride=fstride,
+                                      ref_frame_stride=fstride)
+            if not torch.equal(out, direct):
+                raise SystemExit("bench: me_search_esa8 template and direct passes disagree")
+        else:
+            res[tag + "_moved_fraction"] = float(move.mean())
     return res
 
 

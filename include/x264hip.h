@@ -777,6 +777,25 @@ int x264hip_##BD##_me_search_esa( const pixel *fenc, intptr_t fenc_stride, intpt
                                   const int16_t *par, const int32_t *init_cost,                       \
                                   const uint16_t *cost_mv, int32_t *out, void *stream );              \
                                                                                                 \
+/* ESA decisions of every MB's eight sub-partitions (reference encoder/me.c:618-631 for      \
+ * PIXEL_16x8 top / bottom, 8x16 left / right, 8x8 TL / TR / BL / BR -- partition p of MB mb at \
+ * index i = 8*mb + p, the block offsets of analyse.c:1425,1480,1546): par[8*i] / init_cost[i] \
+ * / cost_mv / out[3*i] = { cost, mx, my } as me_esa_argmin, per partition (each its own       \
+ * window, mvp and predictor).  The partitions share their absdiffs (a partition's SAD is the   \
+ * sum of the MB's 8x8 quadrant SADs) over a template of radius range (4, 8, 16, 24) around     \
+ * centre[2*mb..] (full-pel; NULL = mv 0) with me_search_centred's origin; a partition whose  \
+ * window reaches outside it gets the rest of its window from direct SADs, so the decisions     \
+ * are me.c's for any inputs, fastest when the partitions' windows are centred on the MB's      \
+ * (centre = the 16x16 decision, range = me_range).  range 0 (and any range at 10 bit) takes   \
+ * every candidate directly.  me_range <= 30; fenc / ref / strides dword aligned; every        \
+ * window (width-rounded) must lie inside the padded ref plane. */                              \
+int x264hip_##BD##_me_search_esa8( const pixel *fenc, intptr_t fenc_stride, intptr_t fenc_frame_stride, \
+                                   const pixel *ref, intptr_t ref_stride, intptr_t ref_frame_stride,   \
+                                   int mb_width, int mb_height, int n_frames, int range, int me_range, \
+                                   const int16_t *centre, const int16_t *par,                          \
+                                   const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,    \
+                                   void *stream );                                                     \
+                                                                                                \
 /* TESA integer-pel search per 16x16 macroblock (reference encoder/me.c:653-748,              \
  * X264_ME_TESA with i_pixel = PIXEL_16x16): ads4 with threshold bsad*17>>4 over the ESA      \
  * integral image, the SAD threshold list (sad_thresh 10/11/12 by me_range), the halving      \

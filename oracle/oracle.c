@@ -1384,6 +1384,52 @@ void FN(me_search_full8)( const pixel *fenc, intptr_t fs, const pixel *ref, intp
             }
 }
 
+/* ESA decisions of an MB's eight sub-partitions, semantics of x264hip_*_me_search_esa8: the
+ * plain exhaustive form of encoder/me.c:618-631 (what its ads path reproduces) for each of
+ * PIXEL_16x8 (partitions 0, 1: rows 0 / 8), PIXEL_8x16 (2, 3: columns 0 / 8) and PIXEL_8x8
+ * (4..7: (8(i&1), 8(i>>1))), at the block offsets of analyse.c:1425,1480,1546.  The window is
+ * [max(bmx - me_range, mv_x_min), min(bmx + me_range, mv_x_max)] x the same in y with the width
+ * rounded (max_x - min_x + 3) & ~3; cost = sad of the partition (pixel.c:55-80) +
+ * cost_mv[4*mx - mvp_x] + cost_mv[4*my - mvp_y] (COST_MV, me.c:63-70), strict-< update from
+ * (init_cost, bmx, bmy) in my-major raster order (COPY3_IF_LT, me.h:87-93).  par[(8*mb + p)*8]
+ * as me_esa_argmin's, init_cost[8*mb + p], out[(8*mb + p)*3] = { cost, mx, my }. */
+static const uint8_t esa8_part[8][3] = { { 1, 0, 0 }, { 1, 0, 8 }, { 2, 0, 0 }, { 2, 8, 0 },
+                                         { 3, 0, 0 }, { 3, 8, 0 }, { 3, 0, 8 }, { 3, 8, 8 } };
+void FN(me_search_esa8)( const pixel *fenc, intptr_t fs, const pixel *ref, intptr_t rs, int mb_width,
+                         int mb_height, int me_range, const int16_t *par, const int32_t *init_cost,
+                         const uint16_t *cost_mv, int32_t *out )
+{
+    for( int mb = 0; mb < mb_width * mb_height; mb++ )
+        for( int p = 0; p < 8; p++ )
+        {
+            const int i = 8 * mb + p, ipix = esa8_part[p][0];
+            const int bx = 16 * (mb % mb_width) + esa8_part[p][1], by = 16 * (mb / mb_width) + esa8_part[p][2];
+            const int16_t *q = par + 8 * i;
+            int bmx = q[0], bmy = q[1], bcost = init_cost[i];
+            const uint16_t *cx = cost_mv - q[2], *cy = cost_mv - q[3];
+            const int min_x = bmx - me_range > q[4] ? bmx - me_range : q[4];
+            const int min_y = bmy - me_range > q[5] ? bmy - me_range : q[5];
+            const int max_x = bmx + me_range < q[6] ? bmx + me_range : q[6];
+            const int max_y = bmy + me_range < q[7] ? bmy + me_range : q[7];
+            const int width = (max_x - min_x + 3) & ~3;
+            for( int my = min_y; my <= max_y; my++ )
+                for( int mx = min_x; mx < min_x + width; mx++ )
+                {
+                    int cost = FN(sad)( ipix, fenc + by * fs + bx, fs, ref + (by + my) * rs + bx + mx, rs )
+                             + cx[mx * 4] + cy[my * 4];
+                    if( cost < bcost )
+                    {
+                        bcost = cost;
+                        bmx = mx;
+                        bmy = my;
+                    }
+                }
+            out[3 * i] = bcost;
+            out[3 * i + 1] = bmx;
+            out[3 * i + 2] = bmy;
+        }
+}
+
 /* columns of a x264hip_*_me_search_centred table: me.c's ESA window around the centre,
  * [cx - range, cx + range + 2] (the width rounding (max_x - min_x + 3) & ~3, me.c:626, ends
  * up to two columns past max_x) plus the origin's alignment down to a dword (3 / 1 pixels),

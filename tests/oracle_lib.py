@@ -68,6 +68,7 @@ for _bd in (8, 10):
     _f(_bd, "hpel_filter", [_P, _P, _P, _P, _IP, C.c_int, C.c_int, _P])
     _f(_bd, "get_ref", [_P, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int], _P)
     _f(_bd, "me_esa_argmin", [_P, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P, _P])
+    _f(_bd, "me_search_esa8", [_P, _IP, _P, _IP, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
     _f(_bd, "ssd_wxh", [_P, _IP, _P, _IP, C.c_int, C.c_int], C.c_uint64)
     _f(_bd, "ssd_nv12", [_P, _IP, _P, _IP, C.c_int, C.c_int, _P, _P])
     _f(_bd, "me_tesa", [_P, _IP, _P, _P, _IP, C.c_int, C.c_int, C.c_int, C.c_int, _P, _P, _P, _P])
@@ -312,6 +313,17 @@ def me_esa_argmin(bd, table, rng, me_range, par, init_cost, cost_mv, c0, origin=
     o = None if origin is None else _addr(np.ascontiguousarray(origin, np.int16))
     getattr(_L, f"oracle{bd}_me_esa_argmin")(_addr(t), rng, len(p), me_range, o, _addr(p), _addr(ic),
                                             _addr(cost_mv, c0), _addr(out))
+    return out
+
+
+def me_search_esa8(bd, fenc, f_origin, fs, ref, r_origin, rs, mbw, mbh, me_range, par, init_cost, cost_mv, c0):
+    """one frame: ESA decisions of every MB's eight sub-partitions (16x8 x2, 8x16 x2, 8x8 x4);
+    par int16 [nmb*8, 8], init_cost int32 [nmb*8] -> out int32 [nmb*8, 3]."""
+    p = np.ascontiguousarray(par, np.int16)
+    ic = np.ascontiguousarray(init_cost, np.int32)
+    out = np.zeros((len(p), 3), np.int32)
+    getattr(_L, f"oracle{bd}_me_search_esa8")(_addr(fenc, f_origin), fs, _addr(ref, r_origin), rs, mbw, mbh,
+                                             me_range, _addr(p), _addr(ic), _addr(cost_mv, c0), _addr(out))
     return out
 
 

@@ -3,7 +3,8 @@
 PMC passes and A/Bs): leg_time.py LEG [steps] [pairs] with LEG one of esa (the ESA table and
 fused legs), refine (refine_subpel with chroma ME on the quarter-pel sequence), full8 (the quadrant tables),
 tesa, la (the lookahead's P and B searches), wp (the weight search), me10 (configs[4]'s 10-bit
-full search, quadrant tables and 8x8 DCT+quant).  Prints the legs' JSON."""
+full search, quadrant tables and 8x8 DCT+quant), esa8 (the sub-partition ESA decisions beside the
+quadrant tables).  Prints the legs' JSON."""
 import json
 import os
 import sys
@@ -35,6 +36,9 @@ def main():
         res = bench.rates_refine(x, a, 1, mbw, mbh, F)
     elif leg == "full8":
         res = bench.rates_full8(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
+    elif leg == "esa8":
+        res = bench.rates_full8(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
+        res.update(bench.rates_esa8(x, a, 1, dev, origin, stride, fs, mbw, mbh, F))
     elif leg == "tesa":
         res = bench.rates_tesa(x, a, 1, dev, origin, stride, fs, mbw, mbh, F)
     elif leg == "la":

@@ -25,7 +25,7 @@ import numpy as np
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "me_search_ref", "ssim_bands", "ssim_encoder_bands", "refine_ext", "RefineExt", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "me_search_ref", "ssim_bands", "ssim_encoder_bands", "refine_ext", "RefineExt", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "me_search_esa8", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "stream_pair_destroy", "me_search_full8",
@@ -1498,6 +1498,31 @@ def ssd_nv12_batch(pix1, origin1, stride1, pix2, origin2, stride2, width, height
     (ssd_u, ssd_v); width = chroma samples per row."""
     return _plane_ssd("ssd_nv12_batch", True, pix1, origin1, stride1, pix2, origin2, stride2, width, height,
                       nframes, out, frame_stride1, frame_stride2)
+
+
+def me_search_esa8(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height, nframes, rng,
+                   me_range, centre, par, init_cost, cost_mv_center, out=None, fenc_frame_stride=None,
+                   ref_frame_stride=None):
+    """ESA decisions of every MB's eight sub-partitions (x264hip_*_me_search_esa8; 16x8 top /
+    bottom, 8x16 left / right, 8x8 TL / TR / BL / BR at index 8*mb + p): par int16 [8*n_mbs, 8],
+    init_cost int32 [8*n_mbs], centre int16 [n_mbs, 2] (the shared template's centre, None =
+    mv 0), rng the template radius (0 = direct SADs only).  Returns int32 [8*n_mbs, 3]."""
+    import torch
+    bd = _pix_bd(fenc)
+    n = par.shape[0]
+    if out is None:
+        out = torch.empty((n, 3), dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else (ref[0].numel() if ref.dim() == 3 else 0)
+    cm, c0 = cost_mv_center
+    fn = getattr(lib(), f"x264hip_{bd}_me_search_esa8")
+    fn.argtypes = [_P, _IP, _IP, _P, _IP, _IP, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _c.c_int, _P, _P, _P, _P,
+                   _P, _P]
+    fn.restype = _c.c_int
+    _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(ref, ref_origin), ref_stride, rfs, mb_width, mb_height,
+           nframes, rng, me_range, None if centre is None else _ptr(centre), _ptr(par), _ptr(init_cost),
+           _ptr(cm, c0), _ptr(out), _stream()), "me_search_esa8")
+    return out
 
 
 def me_search_esa(fenc, fenc_origin, fenc_stride, ref, ref_origin, ref_stride, mb_width, mb_height, nframes, rng,

@@ -1825,6 +1825,22 @@ extern "C" const char *x264hip_backend_banner( void )
                                                   par, init_cost, cost_mv, out, (hipStream_t)stream ),               \
                         "me_search_esa" );                                                                           \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_search_esa8( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,          \
+                                                  const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw,      \
+                                                  int mbh, int nframes, int range, int me_range,                     \
+                                                  const int16_t *centre, const int16_t *par,                         \
+                                                  const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out,   \
+                                                  void *stream )                                                     \
+    {                                                                                                                \
+        if( mbw < 0 || mbh < 0 || nframes < 0 ||                                                                     \
+            !( range == 0 || range == 4 || range == 8 || range == 16 || range == 24 ) || me_range < 0 ||             \
+            2 * me_range + 4 > 64 || ((int64_t)nframes * mbw * mbh && (!fenc || !ref || !par || !init_cost ||        \
+                                                                       !cost_mv || !out)) )                          \
+            return X264HIP_EINVAL;                                                                                   \
+        return map_err( launch_me_search_esa8<BD>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, range, me_range,  \
+                                                   centre, par, init_cost, cost_mv, out, (hipStream_t)stream ),      \
+                        "me_search_esa8" );                                                                          \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_me_tesa( const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,                    \
                                            const PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs,                      \
                                            const uint16_t *integral, intptr_t ifs, int mbw, int mbh, int nframes,    \

@@ -426,6 +426,12 @@ hipError_t launch_me_search_esa( const typename PT<BD>::pixel *fenc, intptr_t fs
                                  const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
                                  int nframes, int range, int me_range, const int16_t *par, const int32_t *init_cost,
                                  const uint16_t *cost_mv, int32_t *out, hipStream_t stream );
+// sub-partition ESA decisions (me.hip): x264hip_*_me_search_esa8
+template <int BD>
+hipError_t launch_me_search_esa8( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                  const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                  int nframes, int range, int me_range, const int16_t *centre, const int16_t *par,
+                                  const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out, hipStream_t stream );
 template <int BD>
 hipError_t launch_stat_batch( int op, int i_pixel, const typename PT<BD>::pixel *p1, intptr_t s1,
                               const typename PT<BD>::pixel *p2, intptr_t s2, const int64_t *off1,

@@ -662,6 +662,7 @@ template hipError_t launch_me_full<10>( const uint16_t *, intptr_t, intptr_t, co
 // an MB beyond the spare lanes has its group 0 run the extra columns after its own.
 template <int R> constexpr int esa7_groups() { return ((((2 * R + 3) & ~3) + 3) + 3) / 4; }
 template <int R> constexpr int esa7_mbs() { return 256 / esa7_groups<R>(); }
+constexpr int esa7_groups_rt( int R ) { return ((((2 * R + 3) & ~3) + 3) + 3) / 4; }
 // TAB: the same lanes write the centred table instead (the self-contained TESA's scratch table,
 // launch_me_tesa): every column an MB's window can reach, the slack columns of unclipped
 // windows left unwritten -- no scan reads them.
@@ -2003,5 +2004,467 @@ template hipError_t launch_me_tesa<10>( const uint16_t *, intptr_t, intptr_t, co
                                         const uint16_t *, intptr_t, int, int, int, int, int, const uint32_t *, int,
                                         const int16_t *, const int16_t *, const int32_t *, const uint16_t *,
                                         int32_t *, hipStream_t );
+
+// ---------------------------------------------------------------------------
+// Sub-partition ESA decisions (x264hip_*_me_search_esa8): x264's ESA (encoder/me.c:618-631)
+// for an MB's eight sub-partitions -- PIXEL_16x8 top / bottom, 8x16 left / right, 8x8 TL, TR,
+// BL, BR (analyse.c:1425,1480,1546) -- each with its own window, mvp and predictor cost.  A
+// partition's SAD is the sum of the MB's 8x8 quadrant SADs at the same mv, so one pass of
+// absdiffs over a template serves all eight.
+//
+// Pass 1 (8 bit, me_esa8_kernel): the centred template of radius R around a per-MB centre --
+// 2R+1 rows, G = esa7_groups<R>() four-column groups (36 columns at R = 16) from the
+// dword-aligned origin me_window gives -- with each column group split over a lane PAIR: lane
+// h = 0 folds fenc rows 0-7 and h = 1 rows 8-15 (2R+8 ref rows each, 8 candidate rows in flight,
+// left and right 8-column accumulators).  When a candidate row's sums finish, both lanes of the
+// pair hold their two quadrants and swap one of them over DPP, so each lane keys exactly four
+// partitions with the same instructions (slot 0 its left quadrant, 1 its right one, 2 their sum
+// = its 16x8 half, 3 its quadrant column's 8x16 = own quadrant + the partner's): h = 0 keys
+// 8x8 TL, TR, 16x8 top, 8x16 left; h = 1 8x8 BL, BR, 16x8 bottom, 8x16 right.  Keys are
+// me_esa_argmin's (cost << 12 | raster index in the partition's window): v_mad_u32_u16 of the
+// packed sum's half with the column term, min over the row's four columns, then the row term's
+// saturating add (sat(min_k(x_k) + S) = min_k(sat(x_k + S))).  An MB's lanes meet in LDS; one
+// lane per partition then applies the strict-< update from the predictor cost when the
+// partition's whole window lies in the template.
+// Pass 2 (me_esa8_rest_kernel, any bit depth): one wave per listed partition evaluates the
+// window candidates outside the template with direct SADs and merges them into pass 1's key
+// -- partitions whose window is centred elsewhere than the MB's template (x264 starts each
+// partition from its own best predictor), or every partition at 10 bit / range 0.  So the
+// decisions are me.c's for any inputs; the template only decides how much is shared.
+__host__ __device__ constexpr int esa8_part( int h, int s ) { return s == 0 ? 4 + 2 * h : s == 1 ? 5 + 2 * h : s == 2 ? h : 2 + h; }
+template <int R> constexpr int esa8_mbs() { return 256 / (2 * esa7_groups<R>()); }
+
+// me_window's template origin with run-time R and P (the same arithmetic)
+__device__ __forceinline__ void esa8_window( int R, int P, int cx, int cy, int mbx, int mby, int mbw, int mbh, int &ox,
+                                             int &oy )
+{
+    int ax = 16 * mbx - R + cx, ay = 16 * mby - R + cy;
+    ax = min( max( ax, -32 ), 16 * mbw + 12 - P );
+    ay = min( max( ay, -32 ), 16 * mbh + 16 - 2 * R );
+    ax &= ~3;
+    ox = ax - 16 * mbx;
+    oy = ay - 16 * mby;
+}
+
+__device__ __forceinline__ uint32_t esa8_mad( uint32_t v, uint32_t c, uint32_t s4096, bool hi )
+{
+    uint32_t d;
+    if( hi )
+        asm( "v_mad_u32_u16 %0, %1, %2, %3 op_sel:[1,0,0,0]" : "=v"( d ) : "v"( v ), "s"( s4096 ), "v"( c ) );
+    else
+        asm( "v_mad_u32_u16 %0, %1, %2, %3" : "=v"( d ) : "v"( v ), "s"( s4096 ), "v"( c ) );
+    return d;
+}
+
+template <int R, int L, int Y, class Sink>
+__device__ __forceinline__ void me_row_e8( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
+                                           uint64_t (&al)[8], uint64_t (&ar)[8], Sink &sink, u64x2a4 (&e)[L],
+                                           u64x2a4 (&o)[L] )
+{
+    constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
+    constexpr int C1 = Y < 2 * R ? Y : 2 * R;
+    const uint64_t win[4] = { e[Y % L][0], o[Y % L][0], e[Y % L][1], o[Y % L][1] };
+    if constexpr( Y + L < 2 * R + 8 )
+    {
+        const uint32_t *row = rbase + (Y + L) * rs_dw;
+        e[Y % L] = *(const u64x2a4 *)row;
+        o[Y % L] = *(const u64x2a4 *)(row + 1);
+    }
+#pragma unroll
+    for( int c = C0; c <= C1; c++ )
+    {
+        const int r = Y - c;
+        uint64_t a = r == 0 ? 0ull : al[c & 7], b = r == 0 ? 0ull : ar[c & 7];
+        a = __builtin_amdgcn_qsad_pk_u16_u8( win[0], F[r][0], a );
+        a = __builtin_amdgcn_qsad_pk_u16_u8( win[1], F[r][1], a );
+        b = __builtin_amdgcn_qsad_pk_u16_u8( win[2], F[r][2], b );
+        b = __builtin_amdgcn_qsad_pk_u16_u8( win[3], F[r][3], b );
+        if( r == 7 )
+            sink( c, a, b );
+        else
+        {
+            al[c & 7] = a;
+            ar[c & 7] = b;
+        }
+    }
+    __builtin_amdgcn_sched_barrier( 0 );
+}
+
+template <int R, int L, class Sink, int... Ys>
+__device__ __forceinline__ void me_rows_e8( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
+                                            uint64_t (&al)[8], uint64_t (&ar)[8], Sink &sink,
+                                            std::integer_sequence<int, Ys...> )
+{
+    u64x2a4 e[L], o[L];
+#pragma unroll
+    for( int k = 0; k < L; k++ )
+    {
+        e[k] = *(const u64x2a4 *)(rbase + k * rs_dw);
+        o[k] = *(const u64x2a4 *)(rbase + k * rs_dw + 1);
+    }
+    ( me_row_e8<R, L, Ys>( rbase, rs_dw, F, al, ar, sink, e, o ), ... );
+}
+
+typedef uint16_t u16x2 __attribute__( ( ext_vector_type( 2 ) ) );
+__device__ __forceinline__ uint64_t pk_add_u16x4( uint64_t a, uint64_t b )
+{
+    const u16x2 lo = __builtin_bit_cast( u16x2, (uint32_t)a ) + __builtin_bit_cast( u16x2, (uint32_t)b );
+    const u16x2 hi = __builtin_bit_cast( u16x2, (uint32_t)(a >> 32) ) + __builtin_bit_cast( u16x2, (uint32_t)(b >> 32) );
+    return ((uint64_t)__builtin_bit_cast( uint32_t, hi ) << 32) | __builtin_bit_cast( uint32_t, lo );
+}
+
+template <int R>
+__global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restrict__ fenc, intptr_t fs, intptr_t ffs,
+                                                         const uint8_t *__restrict__ ref, intptr_t rs, intptr_t rfs,
+                                                         int mbw, int mbh, int nframes, int me_range,
+                                                         const int16_t *__restrict__ centre,
+                                                         const int16_t *__restrict__ par,
+                                                         const int32_t *__restrict__ init_cost,
+                                                         const uint16_t *__restrict__ cost_mv,
+                                                         int32_t *__restrict__ out, int32_t *__restrict__ list,
+                                                         uint32_t *__restrict__ count, int xcd )
+{
+    constexpr int G = esa7_groups<R>();         // column groups per MB
+    constexpr int P = 4 * G;                    // template columns
+    constexpr int W = 2 * R + 1;                // template rows
+    constexpr int MPW = esa8_mbs<R>();          // whole MBs per workgroup
+    __shared__ __attribute__( ( aligned( 16 ) ) ) uint32_t s_row[MPW * W * 8];   // row terms [mb][c][h*4 + slot]
+    __shared__ int4 s_win[MPW * 8];             // { min_x, min_y, max_y, width } per partition
+    __shared__ int2 s_mvp[MPW * 8];
+    __shared__ int2 s_org[MPW];
+    __shared__ uint32_t s_key[MPW * 8];
+    const uint32_t nmb = (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw;
+    const int tid = (int)threadIdx.x;
+    const bool spare = tid >= MPW * 2 * G;
+    const uint32_t wg0 = (xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * MPW;
+    const int lmb = spare ? 0 : tid / (2 * G), lane = tid - lmb * 2 * G, grp = lane >> 1, h = lane & 1;
+    const uint32_t mbr = wg0 + (uint32_t)lmb;
+    const bool live = !spare && mbr < nmb;
+    const uint32_t mb32 = min( mbr, nmb - 1 ), t32 = mb32 / (uint32_t)mbw, f32 = t32 / (uint32_t)mbh;
+    const int mbx = (int)(mb32 - t32 * (uint32_t)mbw), mby = (int)(t32 - f32 * (uint32_t)mbh);
+    const int64_t mb = mb32, f = f32;
+    int ox, oy;
+    esa8_window( R, P, centre ? centre[2 * mb] : 0, centre ? centre[2 * mb + 1] : 0, mbx, mby, mbw, mbh, ox, oy );
+    // the partitions' windows (the MB's lanes, 2G of them: 6 at R = 4), the template origin,
+    // the key slots
+    if( !spare )
+    {
+        for( int j = lane; j < 8; j += 2 * G )
+        {
+            const int16_t *q = par + 8 * (8 * mb + j);
+            const int bmx = q[0], bmy = q[1];
+            const int min_x = max( bmx - me_range, (int)q[4] ), min_y = max( bmy - me_range, (int)q[5] );
+            const int max_x = min( bmx + me_range, (int)q[6] ), max_y = min( bmy + me_range, (int)q[7] );
+            s_win[lmb * 8 + j] = make_int4( min_x, min_y, max_y, (max_x - min_x + 3) & ~3 );
+            s_mvp[lmb * 8 + j] = make_int2( q[2], q[3] );
+            s_key[lmb * 8 + j] = 0xFFFFFFFFu;
+        }
+        if( lane == 0 )
+            s_org[lmb] = make_int2( ox, oy );
+    }
+    __syncthreads();
+    // row terms S = ycost << 12 | (my - min_y) * width inside [min_y, max_y], all ones outside
+    if( !spare )
+        for( int e = lane; e < W * 8; e += 2 * G )
+        {
+            const int c = e >> 3, idx = e & 7, p = esa8_part( idx >> 2, idx & 3 ), my = oy + c;
+            const int4 w = s_win[lmb * 8 + p];
+            s_row[(lmb * W + c) * 8 + idx] = my >= w.y && my <= w.z
+                                                 ? ((uint32_t)cost_mv[4 * my - s_mvp[lmb * 8 + p].y] << 12) +
+                                                       (uint32_t)((my - w.y) * w.w)
+                                                 : 0xFFFFFFFFu;
+        }
+    // column terms C = xcost << 12 | (mx - min_x) inside the window's columns, 0xF0000000 outside
+    uint32_t C[4][4];
+#pragma unroll
+    for( int sl = 0; sl < 4; sl++ )
+    {
+        const int p = esa8_part( h, sl );
+        const int4 w = s_win[lmb * 8 + p];
+        const int mvpx = s_mvp[lmb * 8 + p].x;
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            const int mx = ox + 4 * grp + k;
+            C[sl][k] = mx >= w.x && mx < w.x + w.w ? ((uint32_t)cost_mv[4 * mx - mvpx] << 12) + (uint32_t)(mx - w.x)
+                                                     : 0xF0000000u;
+        }
+    }
+    __syncthreads();
+    uint32_t key[4] = { 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu };
+    if( !spare )
+    {
+        uint32_t F[8][4];
+        const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
+        const int fs_dw = (int)(fs / 4);
+#pragma unroll
+        for( int r = 0; r < 8; r++ )
+#pragma unroll
+            for( int k = 0; k < 4; k++ )
+                F[r][k] = fe[r * fs_dw + k];
+        const uint32_t *rbase =
+            (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox) + grp;
+        const uint32_t s4096 = 4096u;
+        __attribute__( ( address_space( 3 ) ) ) uint32_t *srow =
+            (__attribute__( ( address_space( 3 ) ) ) uint32_t *)(s_row + lmb * W * 8 + 4 * h);
+        auto fold = [&]( uint64_t v, const uint32_t (&c)[4], uint32_t S, uint32_t &k ) __attribute__( ( always_inline ) ) {
+            const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+            const uint32_t k0 = esa8_mad( lo, c[0], s4096, false ), k1 = esa8_mad( lo, c[1], s4096, true );
+            const uint32_t k2 = esa8_mad( hi, c[2], s4096, false ), k3 = esa8_mad( hi, c[3], s4096, true );
+            const uint32_t m = min( min( min( k0, k1 ), k2 ), k3 );
+            k = min( k, __builtin_elementwise_add_sat( m, S ) );
+        };
+        auto sink = [&]( int c, uint64_t a, uint64_t b ) {
+            __attribute__( ( address_space( 3 ) ) ) uint32_t *q = srow;
+            asm volatile( "" : "+v"( q ) );     // read where the row finishes
+            typedef uint32_t u32x4 __attribute__( ( ext_vector_type( 4 ) ) );
+            const u32x4 S = *(__attribute__( ( address_space( 3 ) ) ) const u32x4 *)(q + c * 8);
+            // h = 0 sends its right quadrant (TR) and receives BL; h = 1 sends BL, receives TR
+            // (a lane-dependent window order instead of these selects cost more address
+            // arithmetic than the selects: 0.492 -> 0.522 ms per 16 1080p pairs)
+            const uint64_t send = h ? a : b, mine = h ? b : a;
+            const uint32_t r0 = (uint32_t)__builtin_amdgcn_mov_dpp( (int)(uint32_t)send, 0xB1, 0xF, 0xF, false );
+            const uint32_t r1 = (uint32_t)__builtin_amdgcn_mov_dpp( (int)(uint32_t)(send >> 32), 0xB1, 0xF, 0xF, false );
+            const uint64_t recv = ((uint64_t)r1 << 32) | r0;
+            fold( a, C[0], S.x, key[0] );
+            fold( b, C[1], S.y, key[1] );
+            fold( pk_add_u16x4( a, b ), C[2], S.z, key[2] );
+            fold( pk_add_u16x4( mine, recv ), C[3], S.w, key[3] );
+            asm volatile( "" : "+v"( key[0] ), "+v"( key[1] ), "+v"( key[2] ), "+v"( key[3] ) );
+        };
+        uint64_t al[8], ar[8];
+        me_rows_e8<R, ME_LEAD>( rbase, (int)(rs / 4), F, al, ar, sink, std::make_integer_sequence<int, 2 * R + 8>{} );
+        if( live )
+#pragma unroll
+            for( int sl = 0; sl < 4; sl++ )
+                if( key[sl] < 0xF0000000u )
+                    atomicMin( &s_key[lmb * 8 + esa8_part( h, sl )], key[sl] );
+    }
+    __syncthreads();
+    // one lane per partition: the strict-< update (COPY3_IF_LT, me.h:87-93) when the window lies
+    // in the template, else pass 1's key and the partition's index for pass 2
+    for( int t = tid; t < MPW * 8 && wg0 + (uint32_t)(t >> 3) < nmb; t += 256 )
+    {
+        const int sm = t >> 3, p = t & 7;
+        const int64_t i = 8 * (int64_t)(wg0 + (uint32_t)sm) + p;
+        const int4 w = s_win[t];
+        const int2 org = s_org[sm];
+        const uint32_t k = s_key[t];
+        if( w.x >= org.x && w.x + w.w <= org.x + P && w.y >= org.y && w.z <= org.y + 2 * R )
+        {
+            const int16_t *q = par + 8 * i;
+            int32_t bc = init_cost[i], rx = q[0], ry = q[1];
+            if( k != 0xFFFFFFFFu && (int32_t)(k >> 12) < bc )
+            {
+                const int ki = (int)(k & 4095);
+                bc = (int32_t)(k >> 12);
+                ry = w.y + ki / w.w;
+                rx = w.x + ki % w.w;
+            }
+            out[3 * i] = bc;
+            out[3 * i + 1] = rx;
+            out[3 * i + 2] = ry;
+        }
+        else
+        {
+            out[3 * i] = (int32_t)k;
+            list[atomicAdd( count, 1u )] = (int32_t)i;
+        }
+    }
+}
+
+// direct SAD of an NDW-dword x PH block (fenc rows dword aligned, ref anywhere): every row's
+// loads issue before the first is summed
+template <int BD, int NDW, int PH>
+__device__ __forceinline__ uint32_t esa8_block_sad( const typename PT<BD>::pixel *fb, intptr_t fs,
+                                                    const typename PT<BD>::pixel *rb, intptr_t rs )
+{
+    uint32_t a[PH][NDW], b[PH][NDW];
+#pragma unroll
+    for( int y = 0; y < PH; y++ )
+    {
+        const uint32_t *fw = (const uint32_t *)(fb + y * fs);
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            a[y][k] = fw[k];
+        load_packed<NDW>( rb + y * rs, b[y] );
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for( int y = 0; y < PH; y++ )
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            s = sadp<BD>( a[y][k], b[y][k], s );
+    return s;
+}
+
+template <int BD>
+__global__ __launch_bounds__( 256 ) void me_esa8_rest_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                              intptr_t fs, intptr_t ffs,
+                                                              const typename PT<BD>::pixel *__restrict__ ref,
+                                                              intptr_t rs, intptr_t rfs, int mbw, int mbh, int me_range,
+                                                              const int16_t *__restrict__ centre,
+                                                              const int16_t *__restrict__ par,
+                                                              const int32_t *__restrict__ init_cost,
+                                                              const uint16_t *__restrict__ cost_mv,
+                                                              int32_t *__restrict__ out, const int32_t *__restrict__ list,
+                                                              const uint32_t *__restrict__ count, uint32_t n, int R,
+                                                              int G )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int PPD = PT<BD>::PPD;
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6), lane = threadIdx.x & 63;
+    const uint32_t total = count ? __builtin_amdgcn_readfirstlane( *count ) : n;
+    for( uint32_t e = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); e < total; e += nw )
+    {
+        const int64_t i = list ? list[e] : (int64_t)e;
+        const int64_t mb = i >> 3;
+        const int p = (int)(i & 7);
+        const int64_t t = mb / mbw;
+        const int mbx = (int)(mb - t * mbw), mby = (int)(t % mbh);
+        const int64_t f = t / mbh;
+        const int16_t *q = par + 8 * i;
+        const int bmx = q[0], bmy = q[1];
+        const int min_x = max( bmx - me_range, (int)q[4] ), min_y = max( bmy - me_range, (int)q[5] );
+        const int max_x = min( bmx + me_range, (int)q[6] ), max_y = min( bmy + me_range, (int)q[7] );
+        const int width = (max_x - min_x + 3) & ~3;
+        const uint16_t *cx = cost_mv - q[2], *cy = cost_mv - q[3];
+        // the template pass 1 covered (none without pass 1)
+        int tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
+        if( R > 0 )
+        {
+            int ox, oy;
+            esa8_window( R, 4 * G, centre ? centre[2 * mb] : 0, centre ? centre[2 * mb + 1] : 0, mbx, mby, mbw, mbh,
+                         ox, oy );
+            tx0 = ox, tx1 = ox + 4 * G - 1, ty0 = oy, ty1 = oy + 2 * R;
+        }
+        uint32_t key = R > 0 ? (uint32_t)out[3 * i] : 0xFFFFFFFFu;
+        // partition geometry: 0-1 16x8, 2-3 8x16, 4-7 8x8
+        const int px = p < 2 ? 0 : p < 4 ? 8 * (p - 2) : 8 * ((p - 4) & 1);
+        const int py = p < 2 ? 8 * p : p < 4 ? 0 : 8 * ((p - 4) >> 1);
+        const int pw = p < 2 ? 16 : 8, ph = p >= 2 && p < 4 ? 16 : 8;
+        const pixel *fb = fenc + f * ffs + (intptr_t)(16 * mby + py) * fs + 16 * mbx + px;
+        const pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + py) * rs + 16 * mbx + px;
+        // the window [x0, x1] x [y0, y1] minus its intersection with the template: a top band
+        // and a bottom band of whole rows, then the left and right parts of the rows between
+        // them; every lane takes candidates of that list (none of the window's covered ones)
+        const int x0 = min_x, x1 = min_x + width - 1, y0 = min_y, y1 = max_y;
+        int ix0 = max( x0, tx0 ), ix1 = min( x1, tx1 ), iy0 = max( y0, ty0 ), iy1 = min( y1, ty1 );
+        if( ix0 > ix1 || iy0 > iy1 )
+        {
+            iy0 = y1 + 1;           // no intersection: the whole window is the top band
+            iy1 = y1;
+            ix0 = x0;
+            ix1 = x0 - 1;
+        }
+        const int wd = width > 0 ? width : 1;
+        const int nt = width > 0 && y1 >= y0 ? (iy0 - y0) * width : 0, nb = (y1 - iy1) * width;
+        const int mh = iy1 - iy0 + 1, lw = ix0 - x0, rw = x1 - ix1;
+        const int nl = mh * lw, nr = mh * rw, nc = nt + nb + nl + nr;
+        for( int u = (int)lane; u < nc; u += 64 )
+        {
+            int mx, my, v = u;
+            if( v < nt )
+                my = y0 + v / wd, mx = x0 + v % wd;
+            else if( (v -= nt) < nb )
+                my = iy1 + 1 + v / wd, mx = x0 + v % wd;
+            else if( (v -= nb) < nl )
+                my = iy0 + v / lw, mx = x0 + v % lw;
+            else
+                v -= nl, my = iy0 + v / rw, mx = ix1 + 1 + v % rw;
+            const pixel *r = rb + (intptr_t)my * rs + mx;
+            const uint32_t sad = pw == 16 ? esa8_block_sad<BD, 16 / PPD, 8>( fb, fs, r, rs )
+                                 : ph == 16 ? esa8_block_sad<BD, 8 / PPD, 16>( fb, fs, r, rs )
+                                            : esa8_block_sad<BD, 8 / PPD, 8>( fb, fs, r, rs );
+            const uint32_t idx = (uint32_t)((my - min_y) * width + mx - min_x);
+            key = min( key, ((sad + cx[4 * mx] + cy[4 * my]) << 12) | idx );
+        }
+#pragma unroll
+        for( int off = 32; off >= 1; off >>= 1 )
+            key = min( key, (uint32_t)__shfl_xor( (int)key, off, 64 ) );
+        if( lane == 0 )
+        {
+            int32_t bc = init_cost[i], rx = bmx, ry = bmy;
+            if( key != 0xFFFFFFFFu && (int32_t)(key >> 12) < bc )
+            {
+                const int ki = (int)(key & 4095);
+                bc = (int32_t)(key >> 12);
+                ry = min_y + ki / width;
+                rx = min_x + ki % width;
+            }
+            out[3 * i] = bc;
+            out[3 * i + 1] = rx;
+            out[3 * i + 2] = ry;
+        }
+    }
+}
+
+template <int BD>
+hipError_t launch_me_search_esa8( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                  const typename PT<BD>::pixel *ref, intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                  int nframes, int range, int me_range, const int16_t *centre, const int16_t *par,
+                                  const int32_t *init_cost, const uint16_t *cost_mv, int32_t *out, hipStream_t stream )
+{
+    const int64_t nmb = (int64_t)nframes * mbw * mbh;
+    if( nmb <= 0 )
+        return hipSuccess;
+    if( nmb * 8 > 0x7fffffff ||
+        (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
+          (uintptr_t)(rs * sizeof( typename PT<BD>::pixel ))) & 3) )
+        return hipErrorInvalidValue;
+    const unsigned rest_wgs = (unsigned)std::min<int64_t>( (nmb * 8 + 3) / 4, 2048 );
+    if( BD == 8 && range > 0 )
+    {
+        void *buf = nullptr;
+        if( scratch_alloc( &buf, 256 + (size_t)nmb * 8 * sizeof( int32_t ), stream ) == hipSuccess )
+        {
+            uint32_t *cnt = (uint32_t *)buf;
+            int32_t *list = (int32_t *)((uint8_t *)buf + 256);
+            hipError_t e = hipMemsetAsync( cnt, 0, sizeof( uint32_t ), stream );
+            const int xcd = me_xcd();
+            if( e == hipSuccess )
+            {
+                if constexpr( BD == 8 )
+                {
+                    switch( range )
+                    {
+#define E8_CASE( RR )                                                                                             \
+                        case RR:                                                                                  \
+                            hipLaunchKernelGGL( ( me_esa8_kernel<RR> ),                                           \
+                                                dim3( (unsigned)((nmb + esa8_mbs<RR>() - 1) / esa8_mbs<RR>()) ),  \
+                                                dim3( 256 ), 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,    \
+                                                nframes, me_range, centre, par, init_cost, cost_mv, out, list,    \
+                                                cnt, xcd );                                                       \
+                            break;
+                        E8_CASE( 4 ) E8_CASE( 8 ) E8_CASE( 16 ) E8_CASE( 24 )
+#undef E8_CASE
+                    }
+                }
+                e = hipGetLastError();
+            }
+            if( e == hipSuccess )
+            {
+                hipLaunchKernelGGL( me_esa8_rest_kernel<BD>, dim3( rest_wgs ), dim3( 256 ), 0, stream, fenc, fs, ffs,
+                                    ref, rs, rfs, mbw, mbh, me_range, centre, par, init_cost, cost_mv, out, list, cnt,
+                                    0u, range, esa7_groups_rt( range ) );
+                e = hipGetLastError();
+            }
+            const hipError_t fr = hipFreeAsync( buf, stream );
+            return e != hipSuccess ? e : fr;
+        }
+        (void)hipGetLastError();                            // no scratch: every candidate in pass 2
+    }
+    hipLaunchKernelGGL( me_esa8_rest_kernel<BD>, dim3( rest_wgs ), dim3( 256 ), 0, stream, fenc, fs, ffs, ref, rs, rfs,
+                        mbw, mbh, me_range, centre, par, init_cost, cost_mv, out, nullptr, nullptr,
+                        (uint32_t)(nmb * 8), 0, 0 );
+    return hipGetLastError();
+}
+
+template hipError_t launch_me_search_esa8<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *, intptr_t, intptr_t,
+                                              int, int, int, int, int, const int16_t *, const int16_t *,
+                                              const int32_t *, const uint16_t *, int32_t *, hipStream_t );
+template hipError_t launch_me_search_esa8<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *, intptr_t,
+                                               intptr_t, int, int, int, int, int, const int16_t *, const int16_t *,
+                                               const int32_t *, const uint16_t *, int32_t *, hipStream_t );
 
 } // namespace x264hip
