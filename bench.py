@@ -1291,7 +1291,8 @@ def rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     16, template radius 16 around each MB's centre (mv 0).  Two contents: every partition's
     window centred on its MB's (the shared-absdiff pass decides all of them), and a quarter of
     the partitions starting from a predictor up to 3 pixels off it (x264 starts each partition
-    from its own best predictor; those windows' outside strips take the direct pass).  The
+    from its own best predictor; those windows' outside strips take the direct pass); and the
+    first with every centre at x = 1 (template rows off the dword grid).  The
     fraction is taken on the shared work, 256 byte absdiffs per 16x16 window candidate (the
     quadrant-table search's basis, full8_valu_frac); the first content is checked against the
     direct pass alone (range 0)."""
@@ -1309,14 +1310,17 @@ def rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     par_s[:, 0] += np.where(move, off[:, 0], 0).astype(np.int16)
     par_s[:, 1] += np.where(move, off[:, 1], 0).astype(np.int16)
     par_s[:, 2], par_s[:, 3] = 4 * par_s[:, 0], 4 * par_s[:, 1]
+    # a centre off the dword grid (x = 1): the template's row loads are misaligned
+    par_o = np.repeat(tesa_params(mbw, mbh, F, me_range, centre=(1, 0))[0], 8, axis=0)
+    cen_o = torch.tensor([1, 0], dtype=torch.int16, device="cuda").repeat(F * n1, 1)
     out = torch.empty((len(par), 3), dtype=torch.int32, device="cuda")
     init_d = torch.from_numpy(init).cuda()
     res = {}
-    for tag, pp in (("esa8", par), ("esa8_spread", par_s)):
+    for tag, pp, cc in (("esa8", par, cen_d), ("esa8_spread", par_s, cen_d), ("esa8_offgrid", par_o, cen_o)):
         par_d = torch.from_numpy(pp).cuda()
 
-        def step(par_d=par_d):
-            x.me_search_esa8(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, me_range, cen_d,
+        def step(par_d=par_d, cc=cc):
+            x.me_search_esa8(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, R, me_range, cc,
                              par_d, init_d, (cm_d, span), out=out, fenc_frame_stride=fstride,
                              ref_frame_stride=fstride)
         wall, ev_ms = timed(step, a.steps, a.warmup, world)
@@ -1330,7 +1334,7 @@ def rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
                                       ref_frame_stride=fstride)
             if not torch.equal(out, direct):
                 raise SystemExit("bench: me_search_esa8 template and direct passes disagree")
-        else:
+        elif tag == "esa8_spread":
             res[tag + "_moved_fraction"] = float(move.mean())
     return res
 

@@ -136,6 +136,8 @@ __global__ __launch_bounds__( 256 ) void me_full_sad16_kernel( const typename PT
 }
 
 typedef uint64_t u64x2a4 __attribute__( ( ext_vector_type( 2 ), aligned( 4 ) ) );
+typedef uint32_t u32x4a4 __attribute__( ( ext_vector_type( 4 ), aligned( 4 ) ) );
+typedef uint32_t u32x2a4 __attribute__( ( ext_vector_type( 2 ), aligned( 4 ) ) );
 
 // rows of ref-load lead in the grouped kernels: the loads of ref rows Y+1, Y+2 are issued
 // before row Y's SADs (16 1080p pairs, R 16: 8 bit 0.312 -> 0.300 ms from no lead to two
@@ -2012,9 +2014,11 @@ template hipError_t launch_me_tesa<10>( const uint16_t *, intptr_t, intptr_t, co
 // partition's SAD is the sum of the MB's 8x8 quadrant SADs at the same mv, so one pass of
 // absdiffs over a template serves all eight.
 //
-// Pass 1 (8 bit, me_esa8_kernel): the centred template of radius R around a per-MB centre --
-// 2R+1 rows, G = esa7_groups<R>() four-column groups (36 columns at R = 16) from the
-// dword-aligned origin me_window gives -- with each column group split over a lane PAIR: lane
+// Pass 1 (8 bit, me_esa8_kernel): the template of radius R around a per-MB centre -- 2R+1 rows
+// and 2R columns from (cx - R, cy - R) itself, which is an unclipped window's whole width-rounded
+// extent ((2R+3) & ~3 = 2R, me.c:626), so no alignment slack is computed (the origin is not
+// dword aligned then, and the row loads take the address path's misaligned form) -- in R/2
+// four-column groups, each split over a lane PAIR: lane
 // h = 0 folds fenc rows 0-7 and h = 1 rows 8-15 (2R+8 ref rows each, 8 candidate rows in flight,
 // left and right 8-column accumulators).  When a candidate row's sums finish, both lanes of the
 // pair hold their two quadrants and swap one of them over DPP, so each lane keys exactly four
@@ -2026,13 +2030,16 @@ template hipError_t launch_me_tesa<10>( const uint16_t *, intptr_t, intptr_t, co
 // saturating add (sat(min_k(x_k) + S) = min_k(sat(x_k + S))).  An MB's lanes meet in LDS; one
 // lane per partition then applies the strict-< update from the predictor cost when the
 // partition's whole window lies in the template.
-// Pass 2 (me_esa8_rest_kernel, any bit depth): one wave per listed partition evaluates the
-// window candidates outside the template with direct SADs and merges them into pass 1's key
-// -- partitions whose window is centred elsewhere than the MB's template (x264 starts each
-// partition from its own best predictor), or every partition at 10 bit / range 0.  So the
-// decisions are me.c's for any inputs; the template only decides how much is shared.
+// The direct pass (esa8_direct, any bit depth): the same workgroup then gives each partition
+// whose window leaves the template -- centred elsewhere than its MB (x264 starts each partition
+// from its own best predictor) or clipped past it -- one wave that scores the window's
+// candidates outside the template with direct SADs and merges them into the template key; at
+// 10 bit and range 0 me_esa8_direct_kernel scores every partition that way.  So the decisions
+// are me.c's for any inputs; the template only decides how much is shared.
 __host__ __device__ constexpr int esa8_part( int h, int s ) { return s == 0 ? 4 + 2 * h : s == 1 ? 5 + 2 * h : s == 2 ? h : 2 + h; }
-template <int R> constexpr int esa8_mbs() { return 256 / (2 * esa7_groups<R>()); }
+// 2R template columns: an unclipped window's (2R+3) & ~3 = 2R columns exactly
+template <int R> constexpr int esa8_groups() { return R / 2; }
+template <int R> constexpr int esa8_mbs() { return 256 / (2 * esa8_groups<R>()); }
 
 // me_window's template origin with run-time R and P (the same arithmetic)
 __device__ __forceinline__ void esa8_window( int R, int P, int cx, int cy, int mbx, int mby, int mbw, int mbh, int &ox,
@@ -2041,7 +2048,6 @@ __device__ __forceinline__ void esa8_window( int R, int P, int cx, int cy, int m
     int ax = 16 * mbx - R + cx, ay = 16 * mby - R + cy;
     ax = min( max( ax, -32 ), 16 * mbw + 12 - P );
     ay = min( max( ay, -32 ), 16 * mbh + 16 - 2 * R );
-    ax &= ~3;
     ox = ax - 16 * mbx;
     oy = ay - 16 * mby;
 }
@@ -2056,19 +2062,29 @@ __device__ __forceinline__ uint32_t esa8_mad( uint32_t v, uint32_t c, uint32_t s
     return d;
 }
 
+// rbase: the dword holding the lane's first window byte, sh: that byte's offset in it.  Each row
+// is six aligned dwords (the 20 bytes the lane's windows span, at any offset) realigned with
+// v_alignbyte: a misaligned 16-byte load costs the address path 4x an aligned one
+// (profiles/r01d_ta_probe.txt), which made the template pass address-bound off the dword grid.
 template <int R, int L, int Y, class Sink>
-__device__ __forceinline__ void me_row_e8( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
-                                           uint64_t (&al)[8], uint64_t (&ar)[8], Sink &sink, u64x2a4 (&e)[L],
-                                           u64x2a4 (&o)[L] )
+__device__ __forceinline__ void me_row_e8( const uint32_t *__restrict__ rbase, int rs_dw, uint32_t sh,
+                                           const uint32_t (&F)[8][4], uint64_t (&al)[8], uint64_t (&ar)[8],
+                                           Sink &sink, u32x4a4 (&wl)[L], u32x2a4 (&wh)[L] )
 {
     constexpr int C0 = Y - 7 > 0 ? Y - 7 : 0;
     constexpr int C1 = Y < 2 * R ? Y : 2 * R;
-    const uint64_t win[4] = { e[Y % L][0], o[Y % L][0], e[Y % L][1], o[Y % L][1] };
+    const u32x4a4 l4 = wl[Y % L];
+    const u32x2a4 h2 = wh[Y % L];
+    const uint32_t d0 = __builtin_amdgcn_alignbyte( l4.y, l4.x, sh ), d1 = __builtin_amdgcn_alignbyte( l4.z, l4.y, sh );
+    const uint32_t d2 = __builtin_amdgcn_alignbyte( l4.w, l4.z, sh ), d3 = __builtin_amdgcn_alignbyte( h2.x, l4.w, sh );
+    const uint32_t d4 = __builtin_amdgcn_alignbyte( h2.y, h2.x, sh );
+    const uint64_t win[4] = { (uint64_t)d1 << 32 | d0, (uint64_t)d2 << 32 | d1, (uint64_t)d3 << 32 | d2,
+                              (uint64_t)d4 << 32 | d3 };
     if constexpr( Y + L < 2 * R + 8 )
     {
         const uint32_t *row = rbase + (Y + L) * rs_dw;
-        e[Y % L] = *(const u64x2a4 *)row;
-        o[Y % L] = *(const u64x2a4 *)(row + 1);
+        wl[Y % L] = *(const u32x4a4 *)row;
+        wh[Y % L] = *(const u32x2a4 *)(row + 4);
     }
 #pragma unroll
     for( int c = C0; c <= C1; c++ )
@@ -2091,18 +2107,19 @@ __device__ __forceinline__ void me_row_e8( const uint32_t *__restrict__ rbase, i
 }
 
 template <int R, int L, class Sink, int... Ys>
-__device__ __forceinline__ void me_rows_e8( const uint32_t *__restrict__ rbase, int rs_dw, const uint32_t (&F)[8][4],
-                                            uint64_t (&al)[8], uint64_t (&ar)[8], Sink &sink,
-                                            std::integer_sequence<int, Ys...> )
+__device__ __forceinline__ void me_rows_e8( const uint32_t *__restrict__ rbase, int rs_dw, uint32_t sh,
+                                            const uint32_t (&F)[8][4], uint64_t (&al)[8], uint64_t (&ar)[8],
+                                            Sink &sink, std::integer_sequence<int, Ys...> )
 {
-    u64x2a4 e[L], o[L];
+    u32x4a4 wl[L];
+    u32x2a4 wh[L];
 #pragma unroll
     for( int k = 0; k < L; k++ )
     {
-        e[k] = *(const u64x2a4 *)(rbase + k * rs_dw);
-        o[k] = *(const u64x2a4 *)(rbase + k * rs_dw + 1);
+        wl[k] = *(const u32x4a4 *)(rbase + k * rs_dw);
+        wh[k] = *(const u32x2a4 *)(rbase + k * rs_dw + 4);
     }
-    ( me_row_e8<R, L, Ys>( rbase, rs_dw, F, al, ar, sink, e, o ), ... );
+    ( me_row_e8<R, L, Ys>( rbase, rs_dw, sh, F, al, ar, sink, wl, wh ), ... );
 }
 
 typedef uint16_t u16x2 __attribute__( ( ext_vector_type( 2 ) ) );
@@ -2113,6 +2130,129 @@ __device__ __forceinline__ uint64_t pk_add_u16x4( uint64_t a, uint64_t b )
     return ((uint64_t)__builtin_bit_cast( uint32_t, hi ) << 32) | __builtin_bit_cast( uint32_t, lo );
 }
 
+// The direct scan of one partition's uncovered candidates: the fenc block (NDW dwords x PH rows,
+// dword aligned) held in registers for the whole scan, each candidate's ref rows (anywhere) CH at
+// a time realigned from aligned loads.  Returns the lane's least key.
+template <int BD, int NDW, int PH, int CH>
+__device__ __forceinline__ uint32_t esa8_scan( const typename PT<BD>::pixel *fb, intptr_t fs,
+                                               const typename PT<BD>::pixel *rb, intptr_t rs, const uint16_t *cx,
+                                               const uint16_t *cy, int lane, int nt, int nb, int nl, int nr, int wd,
+                                               int lw, int rw, int x0, int y0, int iy0, int iy1, int ix1, int min_x,
+                                               int min_y, int width, uint32_t key )
+{
+    uint32_t a[PH][NDW];
+#pragma unroll
+    for( int y = 0; y < PH; y++ )
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            a[y][k] = ((const uint32_t *)(fb + y * fs))[k];
+    const int nc = nt + nb + nl + nr;
+    for( int u = lane; u < nc; u += 64 )
+    {
+        int mx, my, v = u;
+        if( v < nt )
+            my = y0 + v / wd, mx = x0 + v % wd;
+        else if( (v -= nt) < nb )
+            my = iy1 + 1 + v / wd, mx = x0 + v % wd;
+        else if( (v -= nb) < nl )
+            my = iy0 + v / lw, mx = x0 + v % lw;
+        else
+            v -= nl, my = iy0 + v / rw, mx = ix1 + 1 + v % rw;
+        const typename PT<BD>::pixel *r = rb + (intptr_t)my * rs + mx;
+        uint32_t sad = 0;
+#pragma unroll
+        for( int y0r = 0; y0r < PH; y0r += CH )
+        {
+            uint32_t b[CH][NDW];
+#pragma unroll
+            for( int y = 0; y < CH; y++ )
+                load_packed<NDW>( r + (y0r + y) * rs, b[y] );
+#pragma unroll
+            for( int y = 0; y < CH; y++ )
+#pragma unroll
+                for( int k = 0; k < NDW; k++ )
+                    sad = sadp<BD>( a[y0r + y][k], b[y][k], sad );
+        }
+        const uint32_t idx = (uint32_t)((my - min_y) * width + mx - min_x);
+        key = min( key, ((sad + cx[4 * mx] + cy[4 * my]) << 12) | idx );
+    }
+    return key;
+}
+
+// One wave finishes partition i = 8 mb + p: the candidates of its window outside the template
+// [tx0, tx1] x [ty0, ty1] (empty: all of them) by direct SADs, merged into `key` (the template
+// pass's, or all ones), then the strict-< update (COPY3_IF_LT, me.h:87-93) into out[3 i].
+template <int BD, int CH>
+__device__ __forceinline__ void esa8_direct( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
+                                             intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
+                                             intptr_t rs, intptr_t rfs, int mbw, int mbh, int me_range,
+                                             const int16_t *__restrict__ par, const int32_t *__restrict__ init_cost,
+                                             const uint16_t *__restrict__ cost_mv, int32_t *__restrict__ out,
+                                             int64_t i, uint32_t key, int tx0, int tx1, int ty0, int ty1, int lane )
+{
+    using pixel = typename PT<BD>::pixel;
+    constexpr int PPD = PT<BD>::PPD;
+    const int64_t mb = i >> 3;
+    const int p = (int)(i & 7);
+    const int64_t t = mb / mbw;
+    const int mbx = (int)(mb - t * mbw), mby = (int)(t % mbh);
+    const int64_t f = t / mbh;
+    const int16_t *q = par + 8 * i;
+    const int bmx = q[0], bmy = q[1];
+    const int min_x = max( bmx - me_range, (int)q[4] ), min_y = max( bmy - me_range, (int)q[5] );
+    const int max_x = min( bmx + me_range, (int)q[6] ), max_y = min( bmy + me_range, (int)q[7] );
+    const int width = (max_x - min_x + 3) & ~3;
+    const uint16_t *cx = cost_mv - q[2], *cy = cost_mv - q[3];
+    // partition geometry: 0-1 16x8, 2-3 8x16, 4-7 8x8
+    const int px = p < 2 ? 0 : p < 4 ? 8 * (p - 2) : 8 * ((p - 4) & 1);
+    const int py = p < 2 ? 8 * p : p < 4 ? 0 : 8 * ((p - 4) >> 1);
+    const int pw = p < 2 ? 16 : 8, ph = p >= 2 && p < 4 ? 16 : 8;
+    const pixel *fb = fenc + f * ffs + (intptr_t)(16 * mby + py) * fs + 16 * mbx + px;
+    const pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + py) * rs + 16 * mbx + px;
+    // the window [x0, x1] x [y0, y1] minus its intersection with the template: a top band
+    // and a bottom band of whole rows, then the left and right parts of the rows between
+    // them; every lane takes candidates of that list (none of the window's covered ones)
+    const int x0 = min_x, x1 = min_x + width - 1, y0 = min_y, y1 = max_y;
+    int ix0 = max( x0, tx0 ), ix1 = min( x1, tx1 ), iy0 = max( y0, ty0 ), iy1 = min( y1, ty1 );
+    if( ix0 > ix1 || iy0 > iy1 )
+    {
+        iy0 = y1 + 1;           // no intersection: the whole window is the top band
+        iy1 = y1;
+        ix0 = x0;
+        ix1 = x0 - 1;
+    }
+    const int wd = width > 0 ? width : 1;
+    const int nt = width > 0 && y1 >= y0 ? (iy0 - y0) * width : 0, nb = (y1 - iy1) * width;
+    const int mh = iy1 - iy0 + 1, lw = ix0 - x0, rw = x1 - ix1;
+    const int nl = mh * lw, nr = mh * rw;
+    if( pw == 16 )
+        key = esa8_scan<BD, 16 / PPD, 8, CH < 8 ? CH : 8>( fb, fs, rb, rs, cx, cy, lane, nt, nb, nl, nr, wd, lw, rw, x0,
+                                                          y0, iy0, iy1, ix1, min_x, min_y, width, key );
+    else if( ph == 16 )
+        key = esa8_scan<BD, 8 / PPD, 16, CH>( fb, fs, rb, rs, cx, cy, lane, nt, nb, nl, nr, wd, lw, rw, x0, y0, iy0,
+                                              iy1, ix1, min_x, min_y, width, key );
+    else
+        key = esa8_scan<BD, 8 / PPD, 8, CH < 8 ? CH : 8>( fb, fs, rb, rs, cx, cy, lane, nt, nb, nl, nr, wd, lw, rw, x0,
+                                                         y0, iy0, iy1, ix1, min_x, min_y, width, key );
+#pragma unroll
+    for( int off = 32; off >= 1; off >>= 1 )
+        key = min( key, (uint32_t)__shfl_xor( (int)key, off, 64 ) );
+    if( lane == 0 )
+    {
+        int32_t bc = init_cost[i], rx = bmx, ry = bmy;
+        if( key != 0xFFFFFFFFu && (int32_t)(key >> 12) < bc )
+        {
+            const int ki = (int)(key & 4095);
+            bc = (int32_t)(key >> 12);
+            ry = min_y + ki / width;
+            rx = min_x + ki % width;
+        }
+        out[3 * i] = bc;
+        out[3 * i + 1] = rx;
+        out[3 * i + 2] = ry;
+    }
+}
+
 template <int R>
 __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restrict__ fenc, intptr_t fs, intptr_t ffs,
                                                          const uint8_t *__restrict__ ref, intptr_t rs, intptr_t rfs,
@@ -2121,10 +2261,9 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
                                                          const int16_t *__restrict__ par,
                                                          const int32_t *__restrict__ init_cost,
                                                          const uint16_t *__restrict__ cost_mv,
-                                                         int32_t *__restrict__ out, int32_t *__restrict__ list,
-                                                         uint32_t *__restrict__ count, int xcd )
+                                                         int32_t *__restrict__ out, int xcd )
 {
-    constexpr int G = esa7_groups<R>();         // column groups per MB
+    constexpr int G = esa8_groups<R>();         // column groups per MB
     constexpr int P = 4 * G;                    // template columns
     constexpr int W = 2 * R + 1;                // template rows
     constexpr int MPW = esa8_mbs<R>();          // whole MBs per workgroup
@@ -2133,9 +2272,13 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
     __shared__ int2 s_mvp[MPW * 8];
     __shared__ int2 s_org[MPW];
     __shared__ uint32_t s_key[MPW * 8];
+    __shared__ uint16_t s_flag[MPW * 8];        // partitions left to the direct pass
+    __shared__ uint32_t s_nflag;
     const uint32_t nmb = (uint32_t)nframes * (uint32_t)mbh * (uint32_t)mbw;
     const int tid = (int)threadIdx.x;
     const bool spare = tid >= MPW * 2 * G;
+    if( tid == 0 )
+        s_nflag = 0;
     const uint32_t wg0 = (xcd ? xcd_block( blockIdx.x, gridDim.x ) : blockIdx.x) * MPW;
     const int lmb = spare ? 0 : tid / (2 * G), lane = tid - lmb * 2 * G, grp = lane >> 1, h = lane & 1;
     const uint32_t mbr = wg0 + (uint32_t)lmb;
@@ -2163,18 +2306,30 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
             s_org[lmb] = make_int2( ox, oy );
     }
     __syncthreads();
-    // row terms S = ycost << 12 | (my - min_y) * width inside [min_y, max_y], all ones outside
-    if( !spare )
+    // row terms S = ycost << 12 | (my - min_y) * width inside [min_y, max_y], all ones outside.
+    // Branch-free: the cost is read at the row clamped into the window (mvd 0 for an empty
+    // window) and discarded outside it.  NL = 8 k of the MB's lanes take one partition slot each
+    // and every (NL / 8)-th row (R >= 8); R = 4's six lanes take the entries in turn.
+    auto row_term = [&]( int c, int idx ) __attribute__( ( always_inline ) ) {
+        const int p = esa8_part( idx >> 2, idx & 3 ), my = oy + c;
+        const int4 w = s_win[lmb * 8 + p];
+        const bool in = my >= w.y && my <= w.z;
+        const int ci = w.z >= w.y && w.w > 0 ? 4 * min( max( my, w.y ), w.z ) - s_mvp[lmb * 8 + p].y : 0;
+        const uint32_t t = ((uint32_t)cost_mv[ci] << 12) + (uint32_t)((my - w.y) * w.w);
+        s_row[(lmb * W + c) * 8 + idx] = in ? t : 0xFFFFFFFFu;
+    };
+    constexpr int NL = (2 * G) / 8 * 8;
+    if constexpr( NL >= 8 )
+    {
+        if( !spare && lane < NL )
+            for( int c = lane >> 3; c < W; c += NL / 8 )
+                row_term( c, lane & 7 );
+    }
+    else if( !spare )
         for( int e = lane; e < W * 8; e += 2 * G )
-        {
-            const int c = e >> 3, idx = e & 7, p = esa8_part( idx >> 2, idx & 3 ), my = oy + c;
-            const int4 w = s_win[lmb * 8 + p];
-            s_row[(lmb * W + c) * 8 + idx] = my >= w.y && my <= w.z
-                                                 ? ((uint32_t)cost_mv[4 * my - s_mvp[lmb * 8 + p].y] << 12) +
-                                                       (uint32_t)((my - w.y) * w.w)
-                                                 : 0xFFFFFFFFu;
-        }
+            row_term( e >> 3, e & 7 );
     // column terms C = xcost << 12 | (mx - min_x) inside the window's columns, 0xF0000000 outside
+    // (the same clamped, branch-free read)
     uint32_t C[4][4];
 #pragma unroll
     for( int sl = 0; sl < 4; sl++ )
@@ -2186,8 +2341,10 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
         for( int k = 0; k < 4; k++ )
         {
             const int mx = ox + 4 * grp + k;
-            C[sl][k] = mx >= w.x && mx < w.x + w.w ? ((uint32_t)cost_mv[4 * mx - mvpx] << 12) + (uint32_t)(mx - w.x)
-                                                     : 0xF0000000u;
+            const bool in = mx >= w.x && mx < w.x + w.w;
+            const int ci = w.w > 0 ? 4 * min( max( mx, w.x ), w.x + w.w - 1 ) - mvpx : 0;
+            const uint32_t t = ((uint32_t)cost_mv[ci] << 12) + (uint32_t)(mx - w.x);
+            C[sl][k] = in ? t : 0xF0000000u;
         }
     }
     __syncthreads();
@@ -2202,13 +2359,17 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
 #pragma unroll
             for( int k = 0; k < 4; k++ )
                 F[r][k] = fe[r * fs_dw + k];
-        const uint32_t *rbase =
-            (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox) + grp;
+        // (the window's first byte: 16 mbx + ox + 4 grp; its dword and offset, 16 mbx being a multiple of 4)
+        const uint32_t *rbase = (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx +
+                                                   (ox & ~3)) + grp;
+        const uint32_t sh = (uint32_t)ox & 3;
         const uint32_t s4096 = 4096u;
         __attribute__( ( address_space( 3 ) ) ) uint32_t *srow =
             (__attribute__( ( address_space( 3 ) ) ) uint32_t *)(s_row + lmb * W * 8 + 4 * h);
         auto fold = [&]( uint64_t v, const uint32_t (&c)[4], uint32_t S, uint32_t &k ) __attribute__( ( always_inline ) ) {
             const uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+            // (v_mad_u32_u16 with op_sel picks the 16-bit half: one instruction per candidate;
+            // an extract + v_lshl_add_u32 ran 0.489 -> 0.515 ms, profiles/r06x_esa8_fold_ab.log)
             const uint32_t k0 = esa8_mad( lo, c[0], s4096, false ), k1 = esa8_mad( lo, c[1], s4096, true );
             const uint32_t k2 = esa8_mad( hi, c[2], s4096, false ), k3 = esa8_mad( hi, c[3], s4096, true );
             const uint32_t m = min( min( min( k0, k1 ), k2 ), k3 );
@@ -2233,7 +2394,7 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
             asm volatile( "" : "+v"( key[0] ), "+v"( key[1] ), "+v"( key[2] ), "+v"( key[3] ) );
         };
         uint64_t al[8], ar[8];
-        me_rows_e8<R, ME_LEAD>( rbase, (int)(rs / 4), F, al, ar, sink, std::make_integer_sequence<int, 2 * R + 8>{} );
+        me_rows_e8<R, ME_LEAD>( rbase, (int)(rs / 4), sh, F, al, ar, sink, std::make_integer_sequence<int, 2 * R + 8>{} );
         if( live )
 #pragma unroll
             for( int sl = 0; sl < 4; sl++ )
@@ -2242,11 +2403,11 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
     }
     __syncthreads();
     // one lane per partition: the strict-< update (COPY3_IF_LT, me.h:87-93) when the window lies
-    // in the template, else pass 1's key and the partition's index for pass 2
+    // in the template; the others are listed for the workgroup's direct pass below
     for( int t = tid; t < MPW * 8 && wg0 + (uint32_t)(t >> 3) < nmb; t += 256 )
     {
-        const int sm = t >> 3, p = t & 7;
-        const int64_t i = 8 * (int64_t)(wg0 + (uint32_t)sm) + p;
+        const int sm = t >> 3;
+        const int64_t i = 8 * (int64_t)(wg0 + (uint32_t)sm) + (t & 7);
         const int4 w = s_win[t];
         const int2 org = s_org[sm];
         const uint32_t k = s_key[t];
@@ -2266,137 +2427,39 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
             out[3 * i + 2] = ry;
         }
         else
-        {
-            out[3 * i] = (int32_t)k;
-            list[atomicAdd( count, 1u )] = (int32_t)i;
-        }
+            s_flag[atomicAdd( &s_nflag, 1u )] = (uint16_t)t;
     }
-}
-
-// direct SAD of an NDW-dword x PH block (fenc rows dword aligned, ref anywhere): every row's
-// loads issue before the first is summed
-template <int BD, int NDW, int PH>
-__device__ __forceinline__ uint32_t esa8_block_sad( const typename PT<BD>::pixel *fb, intptr_t fs,
-                                                    const typename PT<BD>::pixel *rb, intptr_t rs )
-{
-    uint32_t a[PH][NDW], b[PH][NDW];
-#pragma unroll
-    for( int y = 0; y < PH; y++ )
+    __syncthreads();
+    // the direct pass over the listed partitions' windows outside the template, one wave each
+    // (rows' loads four at a time: the main loop's registers are free by now, the full unroll's
+    // are not)
+    const uint32_t nflag = s_nflag;
+    for( uint32_t e = (uint32_t)(tid >> 6); e < nflag; e += 4 )
     {
-        const uint32_t *fw = (const uint32_t *)(fb + y * fs);
-#pragma unroll
-        for( int k = 0; k < NDW; k++ )
-            a[y][k] = fw[k];
-        load_packed<NDW>( rb + y * rs, b[y] );
+        const int t = s_flag[e], sm = t >> 3;
+        const int2 org = s_org[sm];
+        esa8_direct<8, 4>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, me_range, par, init_cost, cost_mv, out,
+                           8 * (int64_t)(wg0 + (uint32_t)sm) + (t & 7), s_key[t], org.x, org.x + P - 1, org.y,
+                           org.y + 2 * R, tid & 63 );
     }
-    uint32_t s = 0;
-#pragma unroll
-    for( int y = 0; y < PH; y++ )
-#pragma unroll
-        for( int k = 0; k < NDW; k++ )
-            s = sadp<BD>( a[y][k], b[y][k], s );
-    return s;
 }
 
+// every partition by direct SADs (10 bit, range 0, or no LDS for the template pass): one wave per
+// partition
 template <int BD>
-__global__ __launch_bounds__( 256 ) void me_esa8_rest_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
-                                                              intptr_t fs, intptr_t ffs,
-                                                              const typename PT<BD>::pixel *__restrict__ ref,
-                                                              intptr_t rs, intptr_t rfs, int mbw, int mbh, int me_range,
-                                                              const int16_t *__restrict__ centre,
-                                                              const int16_t *__restrict__ par,
-                                                              const int32_t *__restrict__ init_cost,
-                                                              const uint16_t *__restrict__ cost_mv,
-                                                              int32_t *__restrict__ out, const int32_t *__restrict__ list,
-                                                              const uint32_t *__restrict__ count, uint32_t n, int R,
-                                                              int G )
+__global__ __launch_bounds__( 256 ) void me_esa8_direct_kernel( const typename PT<BD>::pixel *__restrict__ fenc,
+                                                                intptr_t fs, intptr_t ffs,
+                                                                const typename PT<BD>::pixel *__restrict__ ref,
+                                                                intptr_t rs, intptr_t rfs, int mbw, int mbh,
+                                                                int me_range, const int16_t *__restrict__ par,
+                                                                const int32_t *__restrict__ init_cost,
+                                                                const uint16_t *__restrict__ cost_mv,
+                                                                int32_t *__restrict__ out, uint32_t n )
 {
-    using pixel = typename PT<BD>::pixel;
-    constexpr int PPD = PT<BD>::PPD;
-    const uint32_t nw = gridDim.x * (blockDim.x >> 6), lane = threadIdx.x & 63;
-    const uint32_t total = count ? __builtin_amdgcn_readfirstlane( *count ) : n;
-    for( uint32_t e = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); e < total; e += nw )
-    {
-        const int64_t i = list ? list[e] : (int64_t)e;
-        const int64_t mb = i >> 3;
-        const int p = (int)(i & 7);
-        const int64_t t = mb / mbw;
-        const int mbx = (int)(mb - t * mbw), mby = (int)(t % mbh);
-        const int64_t f = t / mbh;
-        const int16_t *q = par + 8 * i;
-        const int bmx = q[0], bmy = q[1];
-        const int min_x = max( bmx - me_range, (int)q[4] ), min_y = max( bmy - me_range, (int)q[5] );
-        const int max_x = min( bmx + me_range, (int)q[6] ), max_y = min( bmy + me_range, (int)q[7] );
-        const int width = (max_x - min_x + 3) & ~3;
-        const uint16_t *cx = cost_mv - q[2], *cy = cost_mv - q[3];
-        // the template pass 1 covered (none without pass 1)
-        int tx0 = 1, tx1 = 0, ty0 = 1, ty1 = 0;
-        if( R > 0 )
-        {
-            int ox, oy;
-            esa8_window( R, 4 * G, centre ? centre[2 * mb] : 0, centre ? centre[2 * mb + 1] : 0, mbx, mby, mbw, mbh,
-                         ox, oy );
-            tx0 = ox, tx1 = ox + 4 * G - 1, ty0 = oy, ty1 = oy + 2 * R;
-        }
-        uint32_t key = R > 0 ? (uint32_t)out[3 * i] : 0xFFFFFFFFu;
-        // partition geometry: 0-1 16x8, 2-3 8x16, 4-7 8x8
-        const int px = p < 2 ? 0 : p < 4 ? 8 * (p - 2) : 8 * ((p - 4) & 1);
-        const int py = p < 2 ? 8 * p : p < 4 ? 0 : 8 * ((p - 4) >> 1);
-        const int pw = p < 2 ? 16 : 8, ph = p >= 2 && p < 4 ? 16 : 8;
-        const pixel *fb = fenc + f * ffs + (intptr_t)(16 * mby + py) * fs + 16 * mbx + px;
-        const pixel *rb = ref + f * rfs + (intptr_t)(16 * mby + py) * rs + 16 * mbx + px;
-        // the window [x0, x1] x [y0, y1] minus its intersection with the template: a top band
-        // and a bottom band of whole rows, then the left and right parts of the rows between
-        // them; every lane takes candidates of that list (none of the window's covered ones)
-        const int x0 = min_x, x1 = min_x + width - 1, y0 = min_y, y1 = max_y;
-        int ix0 = max( x0, tx0 ), ix1 = min( x1, tx1 ), iy0 = max( y0, ty0 ), iy1 = min( y1, ty1 );
-        if( ix0 > ix1 || iy0 > iy1 )
-        {
-            iy0 = y1 + 1;           // no intersection: the whole window is the top band
-            iy1 = y1;
-            ix0 = x0;
-            ix1 = x0 - 1;
-        }
-        const int wd = width > 0 ? width : 1;
-        const int nt = width > 0 && y1 >= y0 ? (iy0 - y0) * width : 0, nb = (y1 - iy1) * width;
-        const int mh = iy1 - iy0 + 1, lw = ix0 - x0, rw = x1 - ix1;
-        const int nl = mh * lw, nr = mh * rw, nc = nt + nb + nl + nr;
-        for( int u = (int)lane; u < nc; u += 64 )
-        {
-            int mx, my, v = u;
-            if( v < nt )
-                my = y0 + v / wd, mx = x0 + v % wd;
-            else if( (v -= nt) < nb )
-                my = iy1 + 1 + v / wd, mx = x0 + v % wd;
-            else if( (v -= nb) < nl )
-                my = iy0 + v / lw, mx = x0 + v % lw;
-            else
-                v -= nl, my = iy0 + v / rw, mx = ix1 + 1 + v % rw;
-            const pixel *r = rb + (intptr_t)my * rs + mx;
-            const uint32_t sad = pw == 16 ? esa8_block_sad<BD, 16 / PPD, 8>( fb, fs, r, rs )
-                                 : ph == 16 ? esa8_block_sad<BD, 8 / PPD, 16>( fb, fs, r, rs )
-                                            : esa8_block_sad<BD, 8 / PPD, 8>( fb, fs, r, rs );
-            const uint32_t idx = (uint32_t)((my - min_y) * width + mx - min_x);
-            key = min( key, ((sad + cx[4 * mx] + cy[4 * my]) << 12) | idx );
-        }
-#pragma unroll
-        for( int off = 32; off >= 1; off >>= 1 )
-            key = min( key, (uint32_t)__shfl_xor( (int)key, off, 64 ) );
-        if( lane == 0 )
-        {
-            int32_t bc = init_cost[i], rx = bmx, ry = bmy;
-            if( key != 0xFFFFFFFFu && (int32_t)(key >> 12) < bc )
-            {
-                const int ki = (int)(key & 4095);
-                bc = (int32_t)(key >> 12);
-                ry = min_y + ki / width;
-                rx = min_x + ki % width;
-            }
-            out[3 * i] = bc;
-            out[3 * i + 1] = rx;
-            out[3 * i + 2] = ry;
-        }
-    }
+    const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+    for( uint32_t e = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); e < n; e += nw )
+        esa8_direct<BD, 16>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, me_range, par, init_cost, cost_mv, out,
+                             (int64_t)e, 0xFFFFFFFFu, 1, 0, 1, 0, (int)(threadIdx.x & 63) );
 }
 
 template <int BD>
@@ -2412,51 +2475,29 @@ hipError_t launch_me_search_esa8( const typename PT<BD>::pixel *fenc, intptr_t f
         (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
           (uintptr_t)(rs * sizeof( typename PT<BD>::pixel ))) & 3) )
         return hipErrorInvalidValue;
-    const unsigned rest_wgs = (unsigned)std::min<int64_t>( (nmb * 8 + 3) / 4, 2048 );
-    if( BD == 8 && range > 0 )
+    if constexpr( BD == 8 )
     {
-        void *buf = nullptr;
-        if( scratch_alloc( &buf, 256 + (size_t)nmb * 8 * sizeof( int32_t ), stream ) == hipSuccess )
+        if( range > 0 )
         {
-            uint32_t *cnt = (uint32_t *)buf;
-            int32_t *list = (int32_t *)((uint8_t *)buf + 256);
-            hipError_t e = hipMemsetAsync( cnt, 0, sizeof( uint32_t ), stream );
             const int xcd = me_xcd();
-            if( e == hipSuccess )
+            switch( range )
             {
-                if constexpr( BD == 8 )
-                {
-                    switch( range )
-                    {
 #define E8_CASE( RR )                                                                                             \
-                        case RR:                                                                                  \
-                            hipLaunchKernelGGL( ( me_esa8_kernel<RR> ),                                           \
-                                                dim3( (unsigned)((nmb + esa8_mbs<RR>() - 1) / esa8_mbs<RR>()) ),  \
-                                                dim3( 256 ), 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh,    \
-                                                nframes, me_range, centre, par, init_cost, cost_mv, out, list,    \
-                                                cnt, xcd );                                                       \
-                            break;
-                        E8_CASE( 4 ) E8_CASE( 8 ) E8_CASE( 16 ) E8_CASE( 24 )
+                case RR:                                                                                          \
+                    hipLaunchKernelGGL( ( me_esa8_kernel<RR> ),                                                   \
+                                        dim3( (unsigned)((nmb + esa8_mbs<RR>() - 1) / esa8_mbs<RR>()) ), dim3( 256 ), \
+                                        0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, me_range, centre, \
+                                        par, init_cost, cost_mv, out, xcd );                                      \
+                    break;
+                E8_CASE( 4 ) E8_CASE( 8 ) E8_CASE( 16 ) E8_CASE( 24 )
 #undef E8_CASE
-                    }
-                }
-                e = hipGetLastError();
             }
-            if( e == hipSuccess )
-            {
-                hipLaunchKernelGGL( me_esa8_rest_kernel<BD>, dim3( rest_wgs ), dim3( 256 ), 0, stream, fenc, fs, ffs,
-                                    ref, rs, rfs, mbw, mbh, me_range, centre, par, init_cost, cost_mv, out, list, cnt,
-                                    0u, range, esa7_groups_rt( range ) );
-                e = hipGetLastError();
-            }
-            const hipError_t fr = hipFreeAsync( buf, stream );
-            return e != hipSuccess ? e : fr;
+            return hipGetLastError();
         }
-        (void)hipGetLastError();                            // no scratch: every candidate in pass 2
     }
-    hipLaunchKernelGGL( me_esa8_rest_kernel<BD>, dim3( rest_wgs ), dim3( 256 ), 0, stream, fenc, fs, ffs, ref, rs, rfs,
-                        mbw, mbh, me_range, centre, par, init_cost, cost_mv, out, nullptr, nullptr,
-                        (uint32_t)(nmb * 8), 0, 0 );
+    hipLaunchKernelGGL( me_esa8_direct_kernel<BD>, dim3( (unsigned)std::min<int64_t>( (nmb * 8 + 3) / 4, 2048 ) ),
+                        dim3( 256 ), 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, me_range, par, init_cost,
+                        cost_mv, out, (uint32_t)(nmb * 8) );
     return hipGetLastError();
 }
 
