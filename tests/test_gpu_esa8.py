@@ -57,6 +57,13 @@ def test_esa8_moved_windows(hip, oracle, bd, R, me_range):
     _run(hip, oracle, bd, 96, 64, 2, R, me_range, seed=3 + R + bd, spread=5, frac=0.5, centre_amp=6)
 
 
+@pytest.mark.parametrize("R,me_range", [(16, 15), (16, 9), (24, 16), (8, 3)])
+def test_esa8_odd_ranges(hip, oracle, R, me_range):
+    """me_range below the template radius and odd (the width rounding then ends short of or at
+    the template's last column), with a quarter of the windows moved"""
+    _run(hip, oracle, 8, 96, 64, 2, R, me_range, seed=40 + R + me_range, spread=4, frac=0.25, centre_amp=5)
+
+
 @pytest.mark.parametrize("limit", [0, 12])
 def test_esa8_clipped(hip, oracle, limit):
     """mv_limit_fpel clips the windows at the frame edges (the width rounding then runs past
