@@ -1126,7 +1126,8 @@ def rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes,
     partition (search8_hex_*) of the F pairs of rates_refine's quarter-pel sequence, and UMH
     (--me umh, the slower presets) on 16x16 (search16_umh_*), every 4x4 partition (search4_hex_*:
     --partitions p4x4, analyse.c:1685-1760) and the exhaustive ESA window (search16_esa_*: --me
-    esa, me.c:618-631).  Rates in partitions/s; the
+    esa, me.c:618-631), and the 16x16 HEX search with x264's own predictors over each frame's MB
+    wavefront (search16_hex_wavefront_*, me_analyse_p16x16).  Rates in partitions/s; the
     candidates the reference evaluates (its fpelcmp / get_ref / refine calls, counted by the
     kernels) give the absdiff rate against the v_sad_u8 peak."""
     res = {"search_workload": "rates_refine's sequence, synthetic mvp / mvc (search_params), subme 7, me_range 16, "
@@ -1158,6 +1159,24 @@ def rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes,
                     leg + "_candidates_per_s": world * a.steps * cands / wall,
                     leg + "_absdiff_frac": cands * px / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF,
                     leg + "_mv_found_frac": ((out[:, 1] == 13) & (out[:, 2] == 10)).float().mean().item()})
+    # the same 16x16 HEX search with x264's own predictors (me_analyse_p16x16: mvp / mvc from the
+    # frame's decided neighbours, mvpred.c:129-157, 519-600, i_mv_range 512) -- the raster
+    # dependency as a wavefront of MB anti-diagonals, one predictor + one search launch each
+    n = F * mbw * mbh
+    out = torch.empty((F, mbw * mbh, 4), dtype=torch.int32, device="cuda")
+    ne = torch.empty((F, mbw * mbh, 2), dtype=torch.int32, device="cuda")
+
+    def wstep():
+        x.me_analyse_p16x16(dev[1:], origin, stride, dev[:-1], planes, origin, stride, mbw, mbh, F, 1, 7, 16,
+                            (cm_d, span), mv_range=512, out=out, nevals=ne, ext=ext, fenc_frame_stride=fstride,
+                            ref_frame_stride=fstride)
+    wall, ev_ms = timed(wstep, a.steps, a.warmup, world, graph=True)
+    nf = int((ne[..., 0] & 0xFFFF).sum().item())
+    res.update({"search16_hex_wavefront_mbs_per_s": world * a.steps * n / wall,
+                "search16_hex_wavefront_step_ms": ev_ms, "search16_hex_wavefront_diagonals": mbw + 2 * (mbh - 1),
+                "search16_hex_wavefront_fpel_calls_per_part": nf / n,
+                "search16_hex_wavefront_mv_found_frac":
+                    ((out[..., 1] == 13) & (out[..., 2] == 10)).float().mean().item()})
     return res
 
 

@@ -956,6 +956,31 @@ int x264hip_##BD##_me_search_ref( const pixel *fenc, intptr_t fenc_stride,      
                                   const uint16_t *cost_mv, int n, int32_t *out,                 \
                                   int32_t *nevals, const x264hip_refine_ext_t *ext,             \
                                   void *stream );                                               \
+/* x264's P16x16 reference-0 analysis of whole frames with the encoder's own predictors: for every \
+ * MB in raster order (analyse.c x264_mb_analyse_inter_p16x16), mvp = x264_mb_predict_mv_16x16      \
+ * (common/mvpred.c:129-157) and mvc = x264_mb_predict_mv_ref16x16 (mvpred.c:519-600, P slice,     \
+ * no MBAFF: lowres_mv[mb] doubled when lowres_mv (the lookahead's field of the pair, int16        \
+ * [n_frames][mb_width*mb_height][2]; 0x7fff in a frame's first entry = none) is given; the left,  \
+ * top, top-left and top-right MBs' 16x16 mvs, mv 0 off the frame; then, when ref_mv (the          \
+ * reference's mv16x16 field, same layout) is given, its colocated / right / below mvs scaled as   \
+ * clip3((mv * ref_mv_scale + 128) >> 8) with ref_mv_scale = (curpoc - refpoc) * inv_ref_poc), the \
+ * mv limits of analyse.c:330-349 (mv_range = i_mv_range in pixels), then x264_me_search_ref as   \
+ * x264hip_*_me_search_ref runs it (PIXEL_16x16).  Every MB is taken as P_L0 16x16 with its       \
+ * searched mv (the neighbours' mvs = their search results).  The raster dependency runs as a      \
+ * wavefront of MB anti-diagonals (x + 2y): one predictor launch and one search launch per       \
+ * diagonal, n_frames frames each.  out[4*(f*mb_width*mb_height + mb)] = { m->cost, mvx, mvy,       \
+ * cost_mv } (raster); nevals (or NULL) as me_search_ref's.  Other arguments as me_search_ref. */  \
+int x264hip_##BD##_me_analyse_p16x16( const pixel *fenc, intptr_t fenc_stride,                  \
+                                      intptr_t fenc_frame_stride, const pixel *fpel_w,          \
+                                      const pixel *fpel, const pixel *hpel_h,                   \
+                                      const pixel *hpel_v, const pixel *hpel_c,                 \
+                                      intptr_t ref_stride, intptr_t ref_frame_stride,           \
+                                      int mb_width, int mb_height, int n_frames, int me_method, \
+                                      int subme, int me_range, int mv_range,                    \
+                                      const int16_t *lowres_mv, const int16_t *ref_mv,          \
+                                      int ref_mv_scale, const uint16_t *cost_mv, int32_t *out,  \
+                                      int32_t *nevals, const x264hip_refine_ext_t *ext,         \
+                                      void *stream );                                           \
 /* x264_me_refine_bidir_satd (reference encoder/me.c:994-1183, rd = 0) for n bipred partitions   \
  * of size i_pixel (16x16 .. 8x8) -- the 4-D diamond over (mv0, mv1) that refine_bidir runs on   \
  * every B_BI_BI / D_BI_8x8 partition at subme >= 5 (analyse.c:2692-2730): up to 8 passes over   \

@@ -25,7 +25,7 @@ import numpy as np
 __all__ = [
     "LIB_PATH", "BackendUnavailable", "lib", "init", "pixel_init", "dct_init", "quant_init",
     "cqm_init", "pixel_cmp_batch", "me_search_full", "sub_dct_batch", "dc_batch", "quant_batch",
-    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "me_search_ref", "ssim_bands", "ssim_encoder_bands", "refine_ext", "RefineExt", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "me_search_esa8", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
+    "quant_dc_batch", "mb_dct_quant", "hpel_filter", "subpel_cmp_batch", "subpel_qpel9_batch", "me_table_pitch", "me_centred_pitch", "me_refine_subpel", "me_search_ref", "ssim_bands", "ssim_encoder_bands", "refine_ext", "RefineExt", "lowres_status", "trim", "me_esa_argmin", "me_tesa", "me_search_esa", "me_search_esa8", "me_analyse_p16x16", "ssd_plane_batch", "ssd_nv12_batch", "alloc_planes", "PIXEL_16x16", "PIXEL_16x8", "PIXEL_8x16",
     "PIXEL_8x8", "PIXEL_8x4", "PIXEL_4x8", "PIXEL_4x4", "PIXEL_4x16", "PIXEL_SIZES",
     "CMP_SAD", "CMP_SSD", "CMP_SATD", "CPU_HIP", "set_variant", "set_thread_device", "thread_device",
     "backend_banner", "forward_ref", "upload", "me_bind", "MeBinding", "weight_scale_plane", "stream_pair", "stream_pair_destroy", "me_search_full8",
@@ -1342,6 +1342,34 @@ def me_search_ref(fenc, fenc_origin, fenc_stride, fpel_w, planes, ref_origin, re
            ref_stride, rfs, i_pixel, me_method, subme, me_range, _ptr(pos), _ptr(par), _ptr(mvc), _ptr(cm, c0), n,
            _ptr(out), _ptr(nevals) if nevals is not None else None, *extra,
            _c.byref(ext) if ext is not None else None, _stream()), name)
+    return out
+
+
+def me_analyse_p16x16(fenc, fenc_origin, fenc_stride, fpel_w, planes, ref_origin, ref_stride, mb_width, mb_height,
+                      nframes, me_method, subme, me_range, cost_mv_center, mv_range=512, lowres_mv=None, ref_mv=None,
+                      ref_mv_scale=0, out=None, nevals=None, ext=None, fenc_frame_stride=None, ref_frame_stride=None):
+    """x264's P16x16 reference-0 analysis of whole frames with mvpred.c's predictors
+    (x264hip_*_me_analyse_p16x16): every MB searched in raster order's dependency (a wavefront of
+    MB anti-diagonals) with mvp = x264_mb_predict_mv_16x16 and mvc = x264_mb_predict_mv_ref16x16.
+    lowres_mv / ref_mv: int16 [nframes, mbs, 2] or None.  Returns int32 [nframes, mbs, 4] =
+    (m->cost, mvx, mvy, cost_mv) in raster order."""
+    import torch
+    bd = _pix_bd(fenc)
+    nmb = mb_width * mb_height
+    if out is None:
+        out = torch.empty((nframes, nmb, 4), dtype=torch.int32, device=fenc.device)
+    ffs = fenc_frame_stride if fenc_frame_stride is not None else (fenc[0].numel() if fenc.dim() == 3 else 0)
+    rfs = ref_frame_stride if ref_frame_stride is not None else _frame_stride(fpel_w, *planes)
+    cm, c0 = cost_mv_center
+    fn = getattr(lib(), f"x264hip_{bd}_me_analyse_p16x16")
+    fn.argtypes = [_P, _IP, _IP, _P, _P, _P, _P, _P, _IP, _IP] + [_c.c_int] * 7 + [_P, _P, _c.c_int, _P, _P, _P, _P,
+                                                                                   _P]
+    fn.restype = _c.c_int
+    _rc(fn(_ptr(fenc, fenc_origin), fenc_stride, ffs, _ptr(fpel_w, ref_origin), *[_ptr(p, ref_origin) for p in planes],
+           ref_stride, rfs, mb_width, mb_height, nframes, me_method, subme, me_range, mv_range,
+           _ptr(lowres_mv) if lowres_mv is not None else None, _ptr(ref_mv) if ref_mv is not None else None,
+           ref_mv_scale, _ptr(cm, c0), _ptr(out), _ptr(nevals) if nevals is not None else None,
+           _c.byref(ext) if ext is not None else None, _stream()), "me_analyse_p16x16")
     return out
 
 

@@ -1962,6 +1962,22 @@ extern "C" const char *x264hip_backend_banner( void )
                                                   me_range, pos, par, mvc, cost_mv, n, out, nevals, nullptr,         \
                                                   nullptr, ext, (hipStream_t)stream ), "me_search_ref" );            \
     }                                                                                                                \
+    extern "C" int x264hip_##BD##_me_analyse_p16x16(                                                              \
+        const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs, const PT<BD>::pixel *fw, const PT<BD>::pixel *p0,       \
+        const PT<BD>::pixel *p1, const PT<BD>::pixel *p2, const PT<BD>::pixel *p3, intptr_t rs, intptr_t rfs,         \
+        int mbw, int mbh, int nframes, int me_method, int subme, int me_range, int mv_range,                         \
+        const int16_t *lowres_mv, const int16_t *ref_mv, int ref_mv_scale, const uint16_t *cost_mv, int32_t *out,    \
+        int32_t *nevals, const x264hip_refine_ext_t *ext, void *stream )                                             \
+    {                                                                                                                \
+        if( mbw < 0 || mbh < 0 || nframes < 0 || mv_range < 1 || mv_range > 8192 ||                                  \
+            ( (int64_t)mbw * mbh * nframes > 0 && ( !fenc || !fw || !p0 || !p1 || !p2 || !p3 || !cost_mv || !out ) ) ) \
+            return X264HIP_EINVAL;                                                                                   \
+        const PT<BD>::pixel *planes[4] = { p0, p1, p2, p3 };                                                         \
+        return map_err( launch_me_analyse_p16x16<BD>( fenc, fs, ffs, fw, planes, rs, rfs, mbw, mbh, nframes,         \
+                                                      me_method, subme, me_range, mv_range, lowres_mv, ref_mv,       \
+                                                      ref_mv_scale, cost_mv, out, nevals, ext, (hipStream_t)stream ), \
+                        "me_analyse_p16x16" );                                                                       \
+    }                                                                                                                \
     extern "C" int x264hip_##BD##_me_refine_bidir_satd(                                                           \
         const PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs, const PT<BD>::pixel *l0f, const PT<BD>::pixel *l0h,     \
         const PT<BD>::pixel *l0v, const PT<BD>::pixel *l0c, const PT<BD>::pixel *l1f, const PT<BD>::pixel *l1h,       \

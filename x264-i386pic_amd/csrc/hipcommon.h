@@ -400,6 +400,14 @@ hipError_t launch_me_search_ref( const typename PT<BD>::pixel *fenc, intptr_t fs
                                  const int32_t *pos, const int16_t *par, const int16_t *mvc, const uint16_t *cost_mv,
                                  int n, int32_t *out, int32_t *nevals, int32_t *thr, const int32_t *rcost,
                                  const x264hip_refine_ext_t *ext, hipStream_t stream );
+// x264's P16x16 reference-0 analysis with mvpred.c's predictors, as an MB wavefront (refine.hip)
+template <int BD>
+hipError_t launch_me_analyse_p16x16( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                     const typename PT<BD>::pixel *fw, const typename PT<BD>::pixel *const planes[4],
+                                     intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, int me_method,
+                                     int subme, int me_range, int mv_range, const int16_t *lowres, const int16_t *tmv,
+                                     int tscale, const uint16_t *cost_mv, int32_t *out, int32_t *nevals,
+                                     const x264hip_refine_ext_t *ext, hipStream_t stream );
 template <int BD>
 hipError_t launch_me_refine_bidir( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
                                    const typename PT<BD>::pixel *const planes0[4],

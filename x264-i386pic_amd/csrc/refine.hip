@@ -1802,4 +1802,241 @@ template hipError_t launch_me_refine_subpel<10>( const uint16_t *, intptr_t, int
                                                  int32_t *, int32_t *, const int32_t *, const x264hip_refine_ext_t *,
                                                  hipStream_t );
 
+// ---------------------------------------------------------------------------
+// x264's P16x16 reference-0 analysis over whole frames with the encoder's own predictors
+// (x264hip_*_me_analyse_p16x16).  For every MB in raster order analyse.c's
+// x264_mb_analyse_inter_p16x16 takes mvp = x264_mb_predict_mv_16x16 (common/mvpred.c:129-157:
+// the median of the left, top and top-right -- or top-left -- neighbours' mvs, or the only one
+// with the reference) and mvc = x264_mb_predict_mv_ref16x16 (mvpred.c:519-600: the lookahead's
+// lowres mv doubled, the left / top / top-left / top-right MBs' 16x16 mvs -- mv 0 off the frame,
+// mvr[-1] -- and the reference's colocated / right / below mvs scaled by the POC distance), the
+// mv limits of analyse.c:330-349, then x264_me_search_ref.  The raster order's dependency (a MB
+// reads its left, top-left, top and top-right neighbours) is run as a wavefront: anti-diagonal d
+// = x + 2y only reads diagonals d-1 .. d-3, so each diagonal of every frame is one predictor
+// launch and one me_search_ref launch.  Every MB is taken as P_L0 16x16 with its searched mv (the
+// neighbours' cache mvs = their mvr), i.e. the analysis of a frame none of whose MBs ends as
+// intra, skip or a smaller partition.
+// Entries of diagonal d: frame-major, then y from ylo(d); global entry off(d) + f L(d) + y - ylo(d).
+__host__ __device__ inline int p16_ylo( int d, int mbw ) { return d - mbw + 1 > 0 ? (d - mbw + 2) / 2 : 0; }
+__host__ __device__ inline int p16_len( int d, int mbw, int mbh )
+{
+    const int hi = min( mbh - 1, d / 2 ), lo = p16_ylo( d, mbw );
+    return hi >= lo ? hi - lo + 1 : 0;
+}
+// MBs (of one frame) on diagonals below d
+__device__ inline int p16_before( int d, int mbw, int mbh )
+{
+    int n = 0;
+    for( int y = 0; y < mbh; y++ )
+        n += min( max( d - 2 * y, 0 ), mbw );
+    return n;
+}
+__device__ inline int p16_index( int f, int x, int y, int nf, int mbw, int mbh )
+{
+    const int d = x + 2 * y;
+    return nf * p16_before( d, mbw, mbh ) + f * p16_len( d, mbw, mbh ) + y - p16_ylo( d, mbw );
+}
+__device__ inline int p16_median( int a, int b, int c )
+{
+    return max( min( a, b ), min( max( a, b ), c ) );
+}
+
+__global__ __launch_bounds__( 256 ) void me_p16_predict_kernel( int d, int nf, int mbw, int mbh, int fmv,
+                                                                const int16_t *__restrict__ lowres,
+                                                                const int16_t *__restrict__ tmv, int tscale,
+                                                                const int32_t *__restrict__ outd,
+                                                                int32_t *__restrict__ pos, int16_t *__restrict__ par,
+                                                                int16_t *__restrict__ mvc )
+{
+    const int L = p16_len( d, mbw, mbh );
+    const int e = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if( e >= nf * L )
+        return;
+    const int f = e / L, y = p16_ylo( d, mbw ) + e % L, x = d - 2 * y;
+    const int nmb = mbw * mbh, mb = y * mbw + x;
+    const int g = nf * p16_before( d, mbw, mbh ) + e;
+    // a neighbour's 16x16 mv (the search result on an earlier diagonal), 0 off the frame
+    auto nb = [&]( int nx, int ny, int &mx, int &my ) -> bool {
+        if( nx < 0 || ny < 0 || nx >= mbw )
+        {
+            mx = my = 0;
+            return false;
+        }
+        const int i = p16_index( f, nx, ny, nf, mbw, mbh );
+        mx = outd[4 * i + 1];
+        my = outd[4 * i + 2];
+        return true;
+    };
+    int ax, ay, bx, by, cx, cy, dx, dy;
+    const bool va = nb( x - 1, y, ax, ay ), vb = nb( x, y - 1, bx, by );
+    const bool vd = nb( x - 1, y - 1, dx, dy );
+    bool vc = x + 1 < mbw && nb( x + 1, y - 1, cx, cy );
+    if( !vc )                               // mvpred.c:136-140: C unavailable -> D
+    {
+        cx = dx;
+        cy = dy;
+        vc = vd;
+    }
+    // x264_mb_predict_mv_16x16 with every available neighbour on reference 0 (mvpred.c:142-157)
+    int px, py;
+    const int cnt = va + vb + vc;
+    if( cnt == 1 )
+    {
+        px = va ? ax : vb ? bx : cx;
+        py = va ? ay : vb ? by : cy;
+    }
+    else if( cnt == 0 && !vb && !vc && va )
+    {
+        px = ax;
+        py = ay;
+    }
+    else
+    {
+        px = p16_median( ax, bx, cx );
+        py = p16_median( ay, by, cy );
+    }
+    // x264_mb_predict_mv_ref16x16 (mvpred.c:519-600), P slice, reference 0, no MBAFF
+    int16_t *m = mvc + 28 * (int64_t)g;
+    int i = 0;
+    auto put = [&]( int vx, int vy ) {
+        m[2 * i] = (int16_t)vx;
+        m[2 * i + 1] = (int16_t)vy;
+        i++;
+    };
+    if( lowres && lowres[2 * (int64_t)f * nmb] != 0x7fff )
+    {
+        // M32( lowres_mv ) * 2 & 0xfffeffff: each half doubled, wrapping in 16 bits
+        const uint32_t w = (uint32_t)(uint16_t)lowres[2 * ((int64_t)f * nmb + mb)] |
+                           ((uint32_t)(uint16_t)lowres[2 * ((int64_t)f * nmb + mb) + 1] << 16);
+        const uint32_t w2 = (w * 2u) & 0xfffeffffu;
+        put( (int16_t)(w2 & 0xffff), (int16_t)(w2 >> 16) );
+    }
+    int sx, sy;
+    nb( x - 1, y, sx, sy ), put( sx, sy );
+    nb( x, y - 1, sx, sy ), put( sx, sy );
+    nb( x - 1, y - 1, sx, sy ), put( sx, sy );
+    if( x + 1 < mbw )
+        nb( x + 1, y - 1, sx, sy );
+    else
+        sx = sy = 0;
+    put( sx, sy );
+    if( tmv )
+    {
+        auto tput = [&]( int k ) {
+            const int64_t t = (int64_t)f * nmb + k;
+            put( min( max( (tmv[2 * t] * tscale + 128) >> 8, -32768 ), 32767 ),
+                 min( max( (tmv[2 * t + 1] * tscale + 128) >> 8, -32768 ), 32767 ) );
+        };
+        tput( mb );
+        if( x < mbw - 1 )
+            tput( mb + 1 );
+        if( y < mbh - 1 )
+            tput( mb + mbw );
+    }
+    // the MB's limits (analyse.c:330-349)
+    const int min0 = 4 * (-16 * x - 24), max0 = 4 * (16 * (mbw - x - 1) + 24);
+    const int min1 = 4 * (-16 * y - 24), max1 = 4 * (16 * (mbh - y - 1) + 24);
+    const int smin0 = max( min0, -fmv ), smax0 = min( max0, fmv - 1 );
+    const int smin1 = max( min1, -fmv ), smax1 = min( max1, fmv - 1 );
+    int16_t *q = par + 12 * (int64_t)g;
+    q[0] = (int16_t)px;
+    q[1] = (int16_t)py;
+    q[2] = (int16_t)((smin0 >> 2) + 6);
+    q[3] = (int16_t)((smin1 >> 2) + 6);
+    q[4] = (int16_t)((smax0 >> 2) - 6);
+    q[5] = (int16_t)((smax1 >> 2) - 6);
+    q[6] = (int16_t)smin0;
+    q[7] = (int16_t)smin1;
+    q[8] = (int16_t)smax0;
+    q[9] = (int16_t)smax1;
+    q[10] = (int16_t)i;
+    q[11] = 0;
+    pos[3 * (int64_t)g] = f;
+    pos[3 * (int64_t)g + 1] = 16 * x;
+    pos[3 * (int64_t)g + 2] = 16 * y;
+}
+
+// diagonal-major results back to frame-major raster order
+__global__ __launch_bounds__( 256 ) void me_p16_unscramble_kernel( int nf, int mbw, int mbh,
+                                                                   const int32_t *__restrict__ outd,
+                                                                   const int32_t *__restrict__ nevd,
+                                                                   int32_t *__restrict__ out,
+                                                                   int32_t *__restrict__ nevals )
+{
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int nmb = mbw * mbh;
+    if( t >= (int64_t)nf * nmb )
+        return;
+    const int f = (int)(t / nmb), mb = (int)(t - (int64_t)f * nmb), y = mb / mbw, x = mb - y * mbw;
+    const int i = p16_index( f, x, y, nf, mbw, mbh );
+#pragma unroll
+    for( int k = 0; k < 4; k++ )
+        out[4 * t + k] = outd[4 * (int64_t)i + k];
+    if( nevals )
+    {
+        nevals[2 * t] = nevd[2 * (int64_t)i];
+        nevals[2 * t + 1] = nevd[2 * (int64_t)i + 1];
+    }
+}
+
+template <int BD>
+hipError_t launch_me_analyse_p16x16( const typename PT<BD>::pixel *fenc, intptr_t fs, intptr_t ffs,
+                                     const typename PT<BD>::pixel *fw, const typename PT<BD>::pixel *const planes[4],
+                                     intptr_t rs, intptr_t rfs, int mbw, int mbh, int nframes, int me_method,
+                                     int subme, int me_range, int mv_range, const int16_t *lowres, const int16_t *tmv,
+                                     int tscale, const uint16_t *cost_mv, int32_t *out, int32_t *nevals,
+                                     const x264hip_refine_ext_t *ext, hipStream_t stream )
+{
+    const int64_t n = (int64_t)nframes * mbw * mbh;
+    if( n <= 0 )
+        return hipSuccess;
+    if( n > (1 << 26) || mv_range < 1 || mv_range > 8192 )
+        return hipErrorInvalidValue;
+    // diagonal-major scratch: results, positions, call counts, par, mvc (each 256-byte aligned)
+    auto al = []( size_t v ) { return (v + 255) & ~(size_t)255; };
+    const size_t b_out = al( (size_t)n * 16 ), b_pos = al( (size_t)n * 12 ), b_nev = nevals ? al( (size_t)n * 8 ) : 0;
+    const size_t b_par = al( (size_t)n * 24 ), b_mvc = al( (size_t)n * 56 );
+    void *buf = nullptr;
+    hipError_t e = scratch_alloc( &buf, b_out + b_pos + b_nev + b_par + b_mvc, stream );
+    if( e != hipSuccess )
+        return e;
+    uint8_t *b = (uint8_t *)buf;
+    int32_t *outd = (int32_t *)b, *pos = (int32_t *)(b + b_out);
+    int32_t *nevd = nevals ? (int32_t *)(b + b_out + b_pos) : nullptr;
+    int16_t *par = (int16_t *)(b + b_out + b_pos + b_nev), *mvc = (int16_t *)(b + b_out + b_pos + b_nev + b_par);
+    const int nd = mbw + 2 * (mbh - 1);
+    int64_t off = 0;
+    for( int d = 0; d < nd && e == hipSuccess; d++ )
+    {
+        const int64_t nn = (int64_t)nframes * p16_len( d, mbw, mbh );
+        if( !nn )
+            continue;
+        hipLaunchKernelGGL( me_p16_predict_kernel, dim3( (unsigned)((nn + 255) / 256) ), dim3( 256 ), 0, stream, d,
+                            nframes, mbw, mbh, 4 * mv_range, lowres, tmv, tscale, outd, pos, par, mvc );
+        if( (e = hipGetLastError()) != hipSuccess )
+            break;
+        e = launch_me_search_ref<BD>( fenc, fs, ffs, fw, planes, rs, rfs, 0, me_method, subme, me_range, pos + 3 * off,
+                                      par + 12 * off, mvc + 28 * off, cost_mv, (int)nn, outd + 4 * off,
+                                      nevd ? nevd + 2 * off : nullptr, nullptr, nullptr, ext, stream );
+        off += nn;
+    }
+    if( e == hipSuccess )
+    {
+        hipLaunchKernelGGL( me_p16_unscramble_kernel, dim3( (unsigned)((n + 255) / 256) ), dim3( 256 ), 0, stream,
+                            nframes, mbw, mbh, outd, nevd, out, nevals );
+        e = hipGetLastError();
+    }
+    const hipError_t fr = hipFreeAsync( buf, stream );
+    return e != hipSuccess ? e : fr;
+}
+template hipError_t launch_me_analyse_p16x16<8>( const uint8_t *, intptr_t, intptr_t, const uint8_t *,
+                                                 const uint8_t *const[4], intptr_t, intptr_t, int, int, int, int, int,
+                                                 int, int, const int16_t *, const int16_t *, int, const uint16_t *,
+                                                 int32_t *, int32_t *, const x264hip_refine_ext_t *, hipStream_t );
+template hipError_t launch_me_analyse_p16x16<10>( const uint16_t *, intptr_t, intptr_t, const uint16_t *,
+                                                  const uint16_t *const[4], intptr_t, intptr_t, int, int, int, int,
+                                                  int, int, int, const int16_t *, const int16_t *, int,
+                                                  const uint16_t *, int32_t *, int32_t *, const x264hip_refine_ext_t *,
+                                                  hipStream_t );
+
 } // namespace x264hip
