@@ -1170,9 +1170,12 @@ def rates_search(x, a, world, mbw, mbh, F, dev, stride, origin, fstride, planes,
         x.me_analyse_p16x16(dev[1:], origin, stride, dev[:-1], planes, origin, stride, mbw, mbh, F, 1, 7, 16,
                             (cm_d, span), mv_range=512, out=out, nevals=ne, ext=ext, fenc_frame_stride=fstride,
                             ref_frame_stride=fstride)
-    wall, ev_ms = timed(wstep, a.steps, a.warmup, world, graph=True)
+    # (eager, fewer steps: ~510 launches a step would make a graph of tens of thousands of
+    # nodes, and the step is long enough to keep the queue fed)
+    ws = min(a.steps, 10)
+    wall, ev_ms = timed(wstep, ws, min(a.warmup, 2), world)
     nf = int((ne[..., 0] & 0xFFFF).sum().item())
-    res.update({"search16_hex_wavefront_mbs_per_s": world * a.steps * n / wall,
+    res.update({"search16_hex_wavefront_mbs_per_s": world * ws * n / wall,
                 "search16_hex_wavefront_step_ms": ev_ms, "search16_hex_wavefront_diagonals": mbw + 2 * (mbh - 1),
                 "search16_hex_wavefront_fpel_calls_per_part": nf / n,
                 "search16_hex_wavefront_mv_found_frac":
