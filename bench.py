@@ -1307,7 +1307,7 @@ def rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, bd=8):
     return res
 
 
-def rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
+def rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, pre="esa8"):
     """ESA decisions of every MB's eight sub-partitions (me_search_esa8: PIXEL_16x8 x2, 8x16 x2,
     8x8 x4, me.c:618-631 per partition, analyse.c:1425,1480,1546) over the F pairs at me_range
     16, template radius 16 around each MB's centre (mv 0).  Two contents: every partition's
@@ -1338,7 +1338,7 @@ def rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
     out = torch.empty((len(par), 3), dtype=torch.int32, device="cuda")
     init_d = torch.from_numpy(init).cuda()
     res = {}
-    for tag, pp, cc in (("esa8", par, cen_d), ("esa8_spread", par_s, cen_d), ("esa8_offgrid", par_o, cen_o)):
+    for tag, pp, cc in ((pre, par, cen_d), (pre + "_spread", par_s, cen_d), (pre + "_offgrid", par_o, cen_o)):
         par_d = torch.from_numpy(pp).cuda()
 
         def step(par_d=par_d, cc=cc):
@@ -1349,14 +1349,15 @@ def rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F):
         cands = esa_window_candidates(par1, me_range)        # 16x16 windows: the shared absdiffs
         res[tag + "_step_ms"] = ev_ms
         res[tag + "_partitions_per_s"] = world * a.steps * len(pp) / wall
-        res[tag + "_frac"] = cands * 256 / (ev_ms * 1e-3) / SAD_PEAK_ABSDIFF
-        if tag == "esa8":
+        # (10 bit: v_sad_u16 folds two absdiffs where v_sad_u8 folds four)
+        res[tag + "_frac"] = cands * 256 / (ev_ms * 1e-3) / (SAD_PEAK_ABSDIFF / (2 if pre == "esa8_10" else 1))
+        if tag == pre:
             direct = x.me_search_esa8(dev[1:], origin, stride, dev[:-1], origin, stride, mbw, mbh, F, 0, me_range,
                                       cen_d, par_d, init_d, (cm_d, span), fenc_frame_stride=fstride,
                                       ref_frame_stride=fstride)
             if not torch.equal(out, direct):
                 raise SystemExit("bench: me_search_esa8 template and direct passes disagree")
-        elif tag == "esa8_spread":
+        elif tag == pre + "_spread":
             res[tag + "_moved_fraction"] = float(move.mean())
     return res
 
@@ -1398,6 +1399,7 @@ def rates_10bit(x, a, world, mbw, mbh, F):
            "me10_absdiff_frac_of_v_sad_u16_peak": cands * 256 / (ev_ms * 1e-3) / VALU_LANE_OPS}
     del table
     res.update(rates_full8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, bd=10))
+    res.update(rates_esa8(x, a, world, dev, origin, stride, fstride, mbw, mbh, F, pre="esa8_10"))
     del dev
     flat = [16] * 64
     _, _, q8m, q8b = x.cqm_init(10, [flat] * 8)

@@ -40,11 +40,13 @@ def _run(hip, oracle, bd, W, H, nf, R, me_range, seed, **kw):
     return got, par, ic
 
 
+@pytest.mark.parametrize("bd", [8, 10])
 @pytest.mark.parametrize("R", [4, 8, 16, 24])
-def test_esa8_template_only(hip, oracle, R):
+def test_esa8_template_only(hip, oracle, bd, R):
     """every partition's window centred on its MB's template centre (range = me_range): the
-    shared-absdiff pass decides all of them"""
-    got, par, ic = _run(hip, oracle, 8, 96, 64, 2, R, R, seed=R, centre_amp=4)
+    shared-absdiff pass decides all of them (10 bit: column-pair lanes from the dword-aligned
+    origin)"""
+    got, par, ic = _run(hip, oracle, bd, 96, 64, 2, R, R, seed=R + bd, centre_amp=4)
     assert (got[:, 0] < ic).mean() > 0.3
 
 

@@ -2039,15 +2039,19 @@ template hipError_t launch_me_tesa<10>( const uint16_t *, intptr_t, intptr_t, co
 __host__ __device__ constexpr int esa8_part( int h, int s ) { return s == 0 ? 4 + 2 * h : s == 1 ? 5 + 2 * h : s == 2 ? h : 2 + h; }
 // 2R template columns: an unclipped window's (2R+3) & ~3 = 2R columns exactly
 template <int R> constexpr int esa8_groups() { return R / 2; }
-template <int R> constexpr int esa8_mbs() { return 256 / (2 * esa8_groups<R>()); }
+// 10 bit: column-PAIR groups (me_row5q's lane, two columns from 9 dwords a row), R + 1 of them
+// from the origin aligned down to a dword (2R + 2 columns)
+template <int BD, int R> constexpr int esa8_lgroups() { return BD == 8 ? esa8_groups<R>() : R + 1; }
+template <int BD, int R> constexpr int esa8_mbs() { return 256 / (2 * esa8_lgroups<BD, R>()); }
 
 // me_window's template origin with run-time R and P (the same arithmetic)
 __device__ __forceinline__ void esa8_window( int R, int P, int cx, int cy, int mbx, int mby, int mbw, int mbh, int &ox,
-                                             int &oy )
+                                             int &oy, int al = 0 )
 {
     int ax = 16 * mbx - R + cx, ay = 16 * mby - R + cy;
     ax = min( max( ax, -32 ), 16 * mbw + 12 - P );
     ay = min( max( ay, -32 ), 16 * mbh + 16 - 2 * R );
+    ax &= ~al;
     ox = ax - 16 * mbx;
     oy = ay - 16 * mby;
 }
@@ -2253,9 +2257,10 @@ __device__ __forceinline__ void esa8_direct( const typename PT<BD>::pixel *__res
     }
 }
 
-template <int R>
-__global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restrict__ fenc, intptr_t fs, intptr_t ffs,
-                                                         const uint8_t *__restrict__ ref, intptr_t rs, intptr_t rfs,
+template <int BD, int R>
+__global__ __launch_bounds__( 256 ) void me_esa8_kernel( const typename PT<BD>::pixel *__restrict__ fenc, intptr_t fs,
+                                                         intptr_t ffs, const typename PT<BD>::pixel *__restrict__ ref,
+                                                         intptr_t rs, intptr_t rfs,
                                                          int mbw, int mbh, int nframes, int me_range,
                                                          const int16_t *__restrict__ centre,
                                                          const int16_t *__restrict__ par,
@@ -2263,10 +2268,11 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
                                                          const uint16_t *__restrict__ cost_mv,
                                                          int32_t *__restrict__ out, int xcd )
 {
-    constexpr int G = esa8_groups<R>();         // column groups per MB
-    constexpr int P = 4 * G;                    // template columns
+    constexpr int CPG = BD == 8 ? 4 : 2;        // candidate columns per lane
+    constexpr int G = esa8_lgroups<BD, R>();    // column groups per MB
+    constexpr int P = CPG * G;                  // template columns
     constexpr int W = 2 * R + 1;                // template rows
-    constexpr int MPW = esa8_mbs<R>();          // whole MBs per workgroup
+    constexpr int MPW = esa8_mbs<BD, R>();      // whole MBs per workgroup
     __shared__ __attribute__( ( aligned( 16 ) ) ) uint32_t s_row[MPW * W * 8];   // row terms [mb][c][h*4 + slot]
     __shared__ int4 s_win[MPW * 8];             // { min_x, min_y, max_y, width } per partition
     __shared__ int2 s_mvp[MPW * 8];
@@ -2287,7 +2293,8 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
     const int mbx = (int)(mb32 - t32 * (uint32_t)mbw), mby = (int)(t32 - f32 * (uint32_t)mbh);
     const int64_t mb = mb32, f = f32;
     int ox, oy;
-    esa8_window( R, P, centre ? centre[2 * mb] : 0, centre ? centre[2 * mb + 1] : 0, mbx, mby, mbw, mbh, ox, oy );
+    esa8_window( R, P, centre ? centre[2 * mb] : 0, centre ? centre[2 * mb + 1] : 0, mbx, mby, mbw, mbh, ox, oy,
+                 BD == 8 ? 0 : 1 );
     // the partitions' windows (the MB's lanes, 2G of them: 6 at R = 4), the template origin,
     // the key slots
     if( !spare )
@@ -2330,7 +2337,7 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
             row_term( e >> 3, e & 7 );
     // column terms C = xcost << 12 | (mx - min_x) inside the window's columns, 0xF0000000 outside
     // (the same clamped, branch-free read)
-    uint32_t C[4][4];
+    uint32_t C[4][CPG];
 #pragma unroll
     for( int sl = 0; sl < 4; sl++ )
     {
@@ -2338,9 +2345,9 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
         const int4 w = s_win[lmb * 8 + p];
         const int mvpx = s_mvp[lmb * 8 + p].x;
 #pragma unroll
-        for( int k = 0; k < 4; k++ )
+        for( int k = 0; k < CPG; k++ )
         {
-            const int mx = ox + 4 * grp + k;
+            const int mx = ox + CPG * grp + k;
             const bool in = mx >= w.x && mx < w.x + w.w;
             const int ci = w.w > 0 ? 4 * min( max( mx, w.x ), w.x + w.w - 1 ) - mvpx : 0;
             const uint32_t t = ((uint32_t)cost_mv[ci] << 12) + (uint32_t)(mx - w.x);
@@ -2351,6 +2358,8 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
     uint32_t key[4] = { 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu };
     if( !spare )
     {
+      if constexpr( BD == 8 )
+      {
         uint32_t F[8][4];
         const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
         const int fs_dw = (int)(fs / 4);
@@ -2395,6 +2404,46 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
         };
         uint64_t al[8], ar[8];
         me_rows_e8<R, ME_LEAD>( rbase, (int)(rs / 4), sh, F, al, ar, sink, std::make_integer_sequence<int, 2 * R + 8>{} );
+      }
+      else
+      {
+        // 10 bit: me_row5q's lane (fenc row half h, columns 2 grp, 2 grp + 1 of the dword-aligned
+        // template), its candidate row's quadrants as two packed u16 pairs; 16x8 / 8x16 sums (up to
+        // 130944) and keys in 32-bit lanes
+        uint32_t F[8][8];
+        const uint32_t *fe = (const uint32_t *)(fenc + f * ffs + (intptr_t)(16 * mby + 8 * h) * fs + 16 * mbx);
+        const int fs_dw = (int)(fs / 2);
+#pragma unroll
+        for( int r = 0; r < 8; r++ )
+#pragma unroll
+            for( int k = 0; k < 8; k++ )
+                F[r][k] = fe[r * fs_dw + k];
+        const uint32_t *rbase =
+            (const uint32_t *)(ref + f * rfs + (intptr_t)(16 * mby + 8 * h + oy) * rs + 16 * mbx + ox + 2 * grp);
+        __attribute__( ( address_space( 3 ) ) ) uint32_t *srow =
+            (__attribute__( ( address_space( 3 ) ) ) uint32_t *)(s_row + lmb * W * 8 + 4 * h);
+        auto fold2 = [&]( uint32_t s0, uint32_t s1, const uint32_t (&c)[CPG], uint32_t S, uint32_t &k )
+            __attribute__( ( always_inline ) ) {
+            const uint32_t k0 = (s0 << 12) + c[0], k1 = (s1 << 12) + c[1], m = min( k0, k1 );
+            k = min( k, __builtin_elementwise_add_sat( m, S ) );
+        };
+        auto sink = [&]( int c, uint32_t l, uint32_t r ) {
+            __attribute__( ( address_space( 3 ) ) ) uint32_t *q = srow;
+            asm volatile( "" : "+v"( q ) );
+            typedef uint32_t u32x4 __attribute__( ( ext_vector_type( 4 ) ) );
+            const u32x4 S = *(__attribute__( ( address_space( 3 ) ) ) const u32x4 *)(q + c * 8);
+            const uint32_t send = h ? l : r, mine = h ? r : l;
+            const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp( (int)send, 0xB1, 0xF, 0xF, false );
+            const uint32_t l0 = l & 0xffff, l1 = l >> 16, r0 = r & 0xffff, r1 = r >> 16;
+            fold2( l0, l1, C[0], S.x, key[0] );
+            fold2( r0, r1, C[1], S.y, key[1] );
+            fold2( l0 + r0, l1 + r1, C[2], S.z, key[2] );
+            fold2( (mine & 0xffff) + (recv & 0xffff), (mine >> 16) + (recv >> 16), C[3], S.w, key[3] );
+            asm volatile( "" : "+v"( key[0] ), "+v"( key[1] ), "+v"( key[2] ), "+v"( key[3] ) );
+        };
+        uint32_t acc[8][4];
+        me_rows5q<R, ME_LEAD>( rbase, (int)(rs / 2), F, acc, sink, std::make_integer_sequence<int, 2 * R + 8>{} );
+      }
         if( live )
 #pragma unroll
             for( int sl = 0; sl < 4; sl++ )
@@ -2438,7 +2487,7 @@ __global__ __launch_bounds__( 256 ) void me_esa8_kernel( const uint8_t *__restri
     {
         const int t = s_flag[e], sm = t >> 3;
         const int2 org = s_org[sm];
-        esa8_direct<8, 4>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, me_range, par, init_cost, cost_mv, out,
+        esa8_direct<BD, 4>( fenc, fs, ffs, ref, rs, rfs, mbw, mbh, me_range, par, init_cost, cost_mv, out,
                            8 * (int64_t)(wg0 + (uint32_t)sm) + (t & 7), s_key[t], org.x, org.x + P - 1, org.y,
                            org.y + 2 * R, tid & 63 );
     }
@@ -2475,25 +2524,22 @@ hipError_t launch_me_search_esa8( const typename PT<BD>::pixel *fenc, intptr_t f
         (((uintptr_t)fenc | (uintptr_t)ref | (uintptr_t)(fs * sizeof( typename PT<BD>::pixel )) |
           (uintptr_t)(rs * sizeof( typename PT<BD>::pixel ))) & 3) )
         return hipErrorInvalidValue;
-    if constexpr( BD == 8 )
+    if( range > 0 )
     {
-        if( range > 0 )
+        const int xcd = me_xcd();
+        switch( range )
         {
-            const int xcd = me_xcd();
-            switch( range )
-            {
 #define E8_CASE( RR )                                                                                             \
-                case RR:                                                                                          \
-                    hipLaunchKernelGGL( ( me_esa8_kernel<RR> ),                                                   \
-                                        dim3( (unsigned)((nmb + esa8_mbs<RR>() - 1) / esa8_mbs<RR>()) ), dim3( 256 ), \
-                                        0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, me_range, centre, \
-                                        par, init_cost, cost_mv, out, xcd );                                      \
-                    break;
-                E8_CASE( 4 ) E8_CASE( 8 ) E8_CASE( 16 ) E8_CASE( 24 )
+            case RR:                                                                                              \
+                hipLaunchKernelGGL( ( me_esa8_kernel<BD, RR> ),                                                   \
+                                    dim3( (unsigned)((nmb + esa8_mbs<BD, RR>() - 1) / esa8_mbs<BD, RR>()) ), dim3( 256 ), \
+                                    0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, nframes, me_range, centre,  \
+                                    par, init_cost, cost_mv, out, xcd );                                          \
+                break;
+            E8_CASE( 4 ) E8_CASE( 8 ) E8_CASE( 16 ) E8_CASE( 24 )
 #undef E8_CASE
-            }
-            return hipGetLastError();
         }
+        return hipGetLastError();
     }
     hipLaunchKernelGGL( me_esa8_direct_kernel<BD>, dim3( (unsigned)std::min<int64_t>( (nmb * 8 + 3) / 4, 2048 ) ),
                         dim3( 256 ), 0, stream, fenc, fs, ffs, ref, rs, rfs, mbw, mbh, me_range, par, init_cost,
