@@ -786,8 +786,8 @@ int x264hip_##BD##_me_search_esa( const pixel *fenc, intptr_t fenc_stride, intpt
  * centre[2*mb..] (full-pel; NULL = mv 0) with me_search_centred's origin; a partition whose  \
  * window reaches outside it gets the rest of its window from direct SADs, so the decisions     \
  * are me.c's for any inputs, fastest when the partitions' windows are centred on the MB's      \
- * (centre = the 16x16 decision, range = me_range).  range 0 (and any range at 10 bit) takes   \
- * every candidate directly.  me_range <= 30; fenc / ref / strides dword aligned; every        \
+ * (centre = the 16x16 decision, range = me_range).  range 0 takes every candidate directly.    \
+ * me_range <= 30; fenc / ref / strides dword aligned; every                                   \
  * window (width-rounded) must lie inside the padded ref plane. */                              \
 int x264hip_##BD##_me_search_esa8( const pixel *fenc, intptr_t fenc_stride, intptr_t fenc_frame_stride, \
                                    const pixel *ref, intptr_t ref_stride, intptr_t ref_frame_stride,   \

@@ -2034,8 +2034,9 @@ template hipError_t launch_me_tesa<10>( const uint16_t *, intptr_t, intptr_t, co
 // whose window leaves the template -- centred elsewhere than its MB (x264 starts each partition
 // from its own best predictor) or clipped past it -- one wave that scores the window's
 // candidates outside the template with direct SADs and merges them into the template key; at
-// 10 bit and range 0 me_esa8_direct_kernel scores every partition that way.  So the decisions
-// are me.c's for any inputs; the template only decides how much is shared.
+// range 0 me_esa8_direct_kernel scores every partition that way.  So the decisions are me.c's
+// for any inputs; the template only decides how much is shared.  10 bit runs the same passes on
+// me_row5q's column-pair lanes (R + 1 pairs from the dword-aligned origin).
 __host__ __device__ constexpr int esa8_part( int h, int s ) { return s == 0 ? 4 + 2 * h : s == 1 ? 5 + 2 * h : s == 2 ? h : 2 + h; }
 // 2R template columns: an unclipped window's (2R+3) & ~3 = 2R columns exactly
 template <int R> constexpr int esa8_groups() { return R / 2; }
