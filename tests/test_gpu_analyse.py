@@ -85,3 +85,10 @@ def test_analyse_p16x16_predictor_sources(hip, oracle, lowres, temporal):
 def test_analyse_p16x16_mv_range(hip, oracle):
     """a small i_mv_range clamps the spel limits (analyse.c:336-339) on a wide frame"""
     _run(hip, oracle, 8, 160, 48, 1, 2, 7, 16, 0, seed=23, mv_range=40)
+
+
+@pytest.mark.parametrize("W,H", [(16, 64), (96, 16), (16, 16)])
+def test_analyse_p16x16_degenerate_shapes(hip, oracle, W, H):
+    """one MB column (every diagonal a single MB, C always off the frame), one MB row (A only),
+    a single MB"""
+    _run(hip, oracle, 8, W, H, 2, 1, 7, 16, 0, seed=29 + W + H)
