@@ -2184,6 +2184,72 @@ __device__ __forceinline__ uint32_t esa8_scan( const typename PT<BD>::pixel *fb,
     return key;
 }
 
+// 8 bit: the uncovered candidates in runs of four columns from min_x (the width-rounded window is
+// a whole number of runs): per fenc row one v_qsad_pk_u16_u8 per fenc dword scores the run's four
+// candidates from realigned ref dwords, against one v_sad_u8 chain per candidate above; a run that
+// also holds covered columns scores them again (the same keys: min is idempotent).  Top / bottom
+// bands are whole rows of runs, the rows between them the runs holding the left / right parts.
+template <int NDW, int PH>
+__device__ __forceinline__ uint32_t esa8_scan4( const uint8_t *fb, intptr_t fs, const uint8_t *rb, intptr_t rs,
+                                                const uint16_t *cx, const uint16_t *cy, int lane, int y0, int y1,
+                                                int iy0, int iy1, int ix0, int ix1, int x0, int width, int min_x,
+                                                int min_y, uint32_t key )
+{
+    uint32_t a[PH][NDW];
+#pragma unroll
+    for( int y = 0; y < PH; y++ )
+#pragma unroll
+        for( int k = 0; k < NDW; k++ )
+            a[y][k] = ((const uint32_t *)(fb + y * fs))[k];
+    if( width <= 0 || y1 < y0 )
+        return key;
+    const int x1 = x0 + width - 1, ng = width >> 2;
+    const int gl = (ix0 - x0 + 3) >> 2, gr0 = (ix1 + 1 - x0) >> 2, gr = ix1 + 1 <= x1 ? ng - gr0 : 0;
+    const int mh = iy1 - iy0 + 1;
+    const int nt = (iy0 - y0) * ng, nb = (y1 - iy1) * ng, nl = mh * gl, nr = mh * gr;
+    const int nu = nt + nb + nl + nr;
+    for( int u = lane; u < nu; u += 64 )
+    {
+        int my, g, v = u;
+        if( v < nt )
+            my = y0 + v / ng, g = v % ng;
+        else if( (v -= nt) < nb )
+            my = iy1 + 1 + v / ng, g = v % ng;
+        else if( (v -= nb) < nl )
+            my = iy0 + v / gl, g = v % gl;
+        else
+            v -= nl, my = iy0 + v / gr, g = gr0 + v % gr;
+        const int gx = x0 + 4 * g;
+        const uint8_t *r = rb + (intptr_t)my * rs + gx;
+        const uint32_t sh = (uint32_t)((uintptr_t)r & 3);
+        uint64_t acc = 0;
+#pragma unroll
+        for( int y = 0; y < PH; y++ )
+        {
+            const uint32_t *base = (const uint32_t *)(r + y * rs - sh);
+            uint32_t w[NDW + 2], d[NDW + 1];
+#pragma unroll
+            for( int k = 0; k <= NDW; k++ )
+                w[k] = base[k];
+            w[NDW + 1] = base[sh ? NDW + 1 : NDW];          // (aligned: no byte past the run is read)
+#pragma unroll
+            for( int k = 0; k <= NDW; k++ )
+                d[k] = __builtin_amdgcn_alignbyte( w[k + 1], w[k], sh );
+#pragma unroll
+            for( int k = 0; k < NDW; k++ )
+                acc = __builtin_amdgcn_qsad_pk_u16_u8( (uint64_t)d[k + 1] << 32 | d[k], a[y][k], acc );
+        }
+        const uint32_t rowc = cy[4 * my], rowi = (uint32_t)((my - min_y) * width + gx - min_x);
+#pragma unroll
+        for( int k = 0; k < 4; k++ )
+        {
+            const uint32_t sad = (uint32_t)(acc >> (16 * k)) & 0xffff;
+            key = min( key, ((sad + cx[4 * (gx + k)] + rowc) << 12) | (rowi + k) );
+        }
+    }
+    return key;
+}
+
 // One wave finishes partition i = 8 mb + p: the candidates of its window outside the template
 // [tx0, tx1] x [ty0, ty1] (empty: all of them) by direct SADs, merged into `key` (the template
 // pass's, or all ones), then the strict-< update (COPY3_IF_LT, me.h:87-93) into out[3 i].
@@ -2230,7 +2296,19 @@ __device__ __forceinline__ void esa8_direct( const typename PT<BD>::pixel *__res
     const int nt = width > 0 && y1 >= y0 ? (iy0 - y0) * width : 0, nb = (y1 - iy1) * width;
     const int mh = iy1 - iy0 + 1, lw = ix0 - x0, rw = x1 - ix1;
     const int nl = mh * lw, nr = mh * rw;
-    if( pw == 16 )
+    if constexpr( BD == 8 )
+    {
+        if( pw == 16 )
+            key = esa8_scan4<4, 8>( fb, fs, rb, rs, cx, cy, lane, y0, y1, iy0, iy1, ix0, ix1, x0, width, min_x, min_y,
+                                    key );
+        else if( ph == 16 )
+            key = esa8_scan4<2, 16>( fb, fs, rb, rs, cx, cy, lane, y0, y1, iy0, iy1, ix0, ix1, x0, width, min_x, min_y,
+                                     key );
+        else
+            key = esa8_scan4<2, 8>( fb, fs, rb, rs, cx, cy, lane, y0, y1, iy0, iy1, ix0, ix1, x0, width, min_x, min_y,
+                                    key );
+    }
+    else if( pw == 16 )
         key = esa8_scan<BD, 16 / PPD, 8, CH < 8 ? CH : 8>( fb, fs, rb, rs, cx, cy, lane, nt, nb, nl, nr, wd, lw, rw, x0,
                                                           y0, iy0, iy1, ix1, min_x, min_y, width, key );
     else if( ph == 16 )
