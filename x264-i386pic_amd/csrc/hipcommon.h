@@ -238,6 +238,41 @@ __device__ __forceinline__ uint32_t satd8x4_packed( const uint32_t (&a)[4][8 / P
     return had_sad_pairs( p, 0 );
 }
 
+// the biased Hadamard coefficients of one side of satd8x4_packed: b's paired columns with 0x8000
+// added to p[0][0] (so every coefficient carries it, mod 2^16), in had_sad_pairs' order (column
+// pass x, output k -> o[4x + k]).  SATD is linear in the difference, so with the fenc side's
+// coefficients precomputed, v_sad_u16( ref's, fenc's ) = |H(ref) - H(fenc)| per pair is
+// satd8x4_packed's sum without the fenc unpacking and the difference per candidate (both sides
+// lie within 0x8000 +- 16 * 1023: no wrap)
+template <int BD>
+__device__ __forceinline__ void had8x4_biased( const uint32_t (&b)[4][8 / PT<BD>::PPD], uint32_t (&o)[16] )
+{
+    x264hip_short2 p[4][4], d[4][4];
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+#pragma unroll
+        for( int x = 0; x < 4; x++ )
+            p[y][x] = pair_px<BD>( b[y], x );
+    p[0][0] = sat_bias( p[0][0] );
+#pragma unroll
+    for( int y = 0; y < 4; y++ )
+    {
+        const x264hip_short2 t0 = p[y][0] + p[y][1], t1 = p[y][0] - p[y][1];
+        const x264hip_short2 t2 = p[y][2] + p[y][3], t3 = p[y][2] - p[y][3];
+        d[y][0] = t0 + t2; d[y][2] = t0 - t2; d[y][1] = t1 + t3; d[y][3] = t1 - t3;
+    }
+#pragma unroll
+    for( int x = 0; x < 4; x++ )
+    {
+        const x264hip_short2 t0 = d[0][x] + d[1][x], t1 = d[0][x] - d[1][x];
+        const x264hip_short2 t2 = d[2][x] + d[3][x], t3 = d[2][x] - d[3][x];
+        o[4 * x + 0] = __builtin_bit_cast( uint32_t, t0 + t2 );
+        o[4 * x + 1] = __builtin_bit_cast( uint32_t, t0 - t2 );
+        o[4 * x + 2] = __builtin_bit_cast( uint32_t, t1 + t3 );
+        o[4 * x + 3] = __builtin_bit_cast( uint32_t, t1 - t3 );
+    }
+}
+
 // value stored to a dctcoef (int16 wrap at 8 bit), read back as int
 template <int BD> __device__ __forceinline__ int sto( int v ) { return (int)(typename PT<BD>::dctcoef)v; }
 

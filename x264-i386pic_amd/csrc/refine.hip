@@ -69,11 +69,16 @@ template <int BD> __device__ __forceinline__ uint32_t weigh_packed( uint32_t w, 
 // the lane's 8x4 tile of get_ref( mvx, mvy ) (weighted when WGT and wt.on) scored against its
 // fenc tile: SAD, or the sum of |coef| of the tile's two 4x4 Hadamards (even; halved by the
 // caller)
-template <int BD, bool SATD, bool WGT = false, int TW = 8>
+// LF: the lane's fenc side read from LDS (fl[256 w]: words 0-15 the tile's had8x4_biased
+// coefficients, 16 + HDW y + k its words; fa unused) -- the SATD then skips the fenc unpacking
+// and the difference per candidate, and the tile stays out of the kernel's registers
+typedef __attribute__( ( address_space( 3 ) ) ) const uint32_t lds_cu32;
+template <int BD, bool SATD, bool WGT = false, int TW = 8, bool LF = false>
 __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD>::PPD],
                                                const typename PT<BD>::pixel *q0, const typename PT<BD>::pixel *q1,
                                                const typename PT<BD>::pixel *q2, const typename PT<BD>::pixel *q3,
-                                               intptr_t rs, int mvx, int mvy, const RsWeight wt = {} )
+                                               intptr_t rs, int mvx, int mvy, const RsWeight wt = {},
+                                               lds_cu32 *fl = nullptr )
 {
     using pixel = typename PT<BD>::pixel;
     constexpr int HDW = 8 / PT<BD>::PPD, LW = HDW * TW / 8;   // words of a row; of the tile's row
@@ -118,8 +123,20 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
                 for( int k = 0; k < LW; k++ )
                     r1[y][k] = weigh_packed<BD>( r1[y][k], wt );
     // a 4-wide tile (TW 4) is the 8x4 SATD's left 4x4 with zero differences on the right
+    lds_cu32 *h = fl;
+    if constexpr( LF )
+        asm volatile( "" : "+v"( h ) );                 // read per candidate, not hoisted into registers
     if constexpr( SATD )
-        return satd8x4_packed<BD>( fa, r1 );
+    {
+        if constexpr( !LF )
+            return satd8x4_packed<BD>( fa, r1 );
+        uint32_t o[16], acc = 0;
+        had8x4_biased<BD>( r1, o );
+#pragma unroll
+        for( int k = 0; k < 16; k++ )
+            acc = __builtin_amdgcn_sad_u16( o[k], h[256 * k], acc );
+        return acc;
+    }
     else
     {
         uint32_t acc = 0;
@@ -127,7 +144,7 @@ __device__ __forceinline__ uint32_t tile_cost( const uint32_t (&fa)[4][8 / PT<BD
         for( int y = 0; y < 4; y++ )
 #pragma unroll
             for( int k = 0; k < LW; k++ )
-                acc = sadp<BD>( fa[y][k], r1[y][k], acc );
+                acc = sadp<BD>( LF ? h[256 * (16 + HDW * y + k)] : fa[y][k], r1[y][k], acc );
         return acc;
     }
 }
@@ -336,8 +353,31 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     const int ux = TW * (u % TX), uy = 4 * (u / TX);
     const int f = pos[3 * j], bx = pos[3 * j + 1], by = pos[3 * j + 2];
 
+    // the lane's fenc tile and its Hadamard coefficients in LDS, once (word-major: a word of
+    // every lane is one conflict-free row; tile_cost's LF form): luma-only 0.173 -> 0.163 ms per
+    // 130560 MBs.  Not with 4:2:0 / 4:2:2 chroma ME (EXT 1): 0.232 -> 0.237-0.239 ms with the
+    // coefficients in LDS or in registers (profiles/r06zt_ .. r06zw_refine_*_ab.log)
+    constexpr bool LF = EXT != 1;
     uint32_t fa[4][HDW];
+    __shared__ uint32_t s_fl[LF ? 16 + 4 * HDW : 1][LF ? 256 : 1];
     load_fenc_tile<BD, TW>( fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux, fs, fa );
+    if constexpr( LF )
+    {
+        uint32_t o[16];
+        had8x4_biased<BD>( fa, o );
+#pragma unroll
+        for( int k = 0; k < 16; k++ )
+            s_fl[k][threadIdx.x] = o[k];
+#pragma unroll
+        for( int y = 0; y < 4; y++ )
+#pragma unroll
+            for( int k = 0; k < HDW; k++ )
+            {
+                s_fl[16 + HDW * y + k][threadIdx.x] = fa[y][k];
+                fa[y][k] = 0u;                            // (unused by the LF form)
+            }
+    }
+    lds_cu32 *const hf = LF ? (lds_cu32 *)&s_fl[0][threadIdx.x] : nullptr;
     const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
     const pixel *const q0 = p0 + qo, *const q1 = p1 + qo, *const q2 = p2 + qo, *const q3 = p3 + qo;
 
@@ -425,8 +465,8 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         const int gy = g == 0 ? my[0] : g == 1 ? my[1] : g == 2 ? my[2] : my[3];
         uint32_t v = 0;
         if( tile )
-            v = satd ? tile_cost<BD, true, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 ) >> 1
-                     : tile_cost<BD, false, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 );
+            v = satd ? tile_cost<BD, true, EXT != 0, TW, LF>( fa, q0, q1, q2, q3, rs, gx, gy, wt0, hf ) >> 1
+                     : tile_cost<BD, false, EXT != 0, TW, LF>( fa, q0, q1, q2, q3, rs, gx, gy, wt0, hf );
         if( u == 0 )                                      // the group's mv cost, once
             v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
         v = group_sum<NT>( v );
@@ -440,8 +480,8 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
     auto eval4c = [&]( const int (&mx)[4], const int (&my)[4], int cx, int cy, int (&c)[4], int &cc ) __attribute__( ( always_inline ) ) {
         const int gx = g == 0 ? mx[0] : g == 1 ? mx[1] : g == 2 ? mx[2] : mx[3];
         const int gy = g == 0 ? my[0] : g == 1 ? my[1] : g == 2 ? my[2] : my[3];
-        uint32_t vc = tile_cost<BD, true, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, cx, cy, wt0 ) >> 1;
-        uint32_t v = tile_cost<BD, true, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, gx, gy, wt0 ) >> 1;
+        uint32_t vc = tile_cost<BD, true, EXT != 0, TW, LF>( fa, q0, q1, q2, q3, rs, cx, cy, wt0, hf ) >> 1;
+        uint32_t v = tile_cost<BD, true, EXT != 0, TW, LF>( fa, q0, q1, q2, q3, rs, gx, gy, wt0, hf ) >> 1;
         if( u == 0 )
         {
             v += (uint32_t)cmx[gx] + (uint32_t)cmy[gy];
@@ -459,8 +499,8 @@ __global__ __launch_bounds__( 256 ) void me_refine_subpel_kernel(
         uint32_t v = 0;
         if( g == 0 )
         {
-            v = satd ? tile_cost<BD, true, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, mx, my, wt0 ) >> 1
-                     : tile_cost<BD, false, EXT != 0, TW>( fa, q0, q1, q2, q3, rs, mx, my, wt0 );
+            v = satd ? tile_cost<BD, true, EXT != 0, TW, LF>( fa, q0, q1, q2, q3, rs, mx, my, wt0, hf ) >> 1
+                     : tile_cost<BD, false, EXT != 0, TW, LF>( fa, q0, q1, q2, q3, rs, mx, my, wt0, hf );
             if( u == 0 )
                 v += (uint32_t)cmx[mx] + (uint32_t)cmy[my];
         }
