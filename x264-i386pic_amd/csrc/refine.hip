@@ -1658,6 +1658,9 @@ __global__ __launch_bounds__( 256 ) void me_refine_bidir_kernel(
 
     uint32_t fa[4][HDW];
     load_fenc_tile<BD, TW>( fenc + f * ffs + (intptr_t)(by + uy) * fs + bx + ux, fs, fa );
+    uint32_t hr[16];                                      // SATD: the tile's biased Hadamards, once
+    if constexpr( SATD )
+        had8x4_biased<BD>( fa, hr );
     const intptr_t qo = (intptr_t)f * rfs + (intptr_t)(by + uy) * rs + bx + ux;
     const pixel *const p0 = a0 + qo, *const p1 = a1 + qo, *const p2 = a2 + qo, *const p3 = a3 + qo;
     const pixel *const r0 = b0 + qo, *const r1 = b1 + qo, *const r2 = b2 + qo, *const r3 = b3 + qo;
@@ -1720,7 +1723,14 @@ __global__ __launch_bounds__( 256 ) void me_refine_bidir_kernel(
                         }
                 }
                 if constexpr( SATD )
-                    v = satd8x4_packed<BD>( fa, t0 ) >> 1;
+                {
+                    uint32_t o[16];
+                    had8x4_biased<BD>( t0, o );
+#pragma unroll
+                    for( int k = 0; k < 16; k++ )
+                        v = __builtin_amdgcn_sad_u16( o[k], hr[k], v );
+                    v >>= 1;
+                }
                 else
                 {
 #pragma unroll
