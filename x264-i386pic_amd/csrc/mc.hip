@@ -897,6 +897,10 @@ __global__ __launch_bounds__( 256 ) void subpel_qpel9_kernel( const typename PT<
                 load_row_al<N8>( gcy + (ty + y) * rs + tx, cy[y] );
                 load_row_al<N8 + 1>( gxy + (ty + y) * rs + tx, xy[y] );
             }
+            // SATD: the fenc tile's biased Hadamards once for the nine candidates (had8x4_biased)
+            uint32_t hf[16];
+            if constexpr( OP != 0 )
+                had8x4_biased<BD>( f, hf );
 #pragma unroll
             for( int k = 0; k < 9; k++ )
             {
@@ -932,7 +936,13 @@ __global__ __launch_bounds__( 256 ) void subpel_qpel9_kernel( const typename PT<
                             acc[k] = sadp<BD>( f[r][d], pr[r][d], acc[k] );
                 }
                 else
-                    acc[k] += satd8x4_packed<BD>( f, pr );
+                {
+                    uint32_t o[16];
+                    had8x4_biased<BD>( pr, o );
+#pragma unroll
+                    for( int q = 0; q < 16; q++ )
+                        acc[k] = __builtin_amdgcn_sad_u16( o[q], hf[q], acc[k] );
+                }
             }
         }
 #pragma unroll
